@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""In-tree native build for minips_amd (no setuptools, no JIT cache).
+
+Targets
+  runtime   csrc/runtime/*.cc            -> build/obj/rt_*.o  (g++ -O2, C++17)
+  rt_py     csrc/bindings/runtime_py.cc  -> minips_amd/_runtime*.so   (pybind11)
+  tests     csrc/tests/runtime_test.cc   -> build/bin/runtime_test
+  apps      csrc/apps/*.cc               -> build/bin/<app>
+  kernels   csrc/kernels/*.hip           -> build/obj/k_*.o   (hipcc --offload-arch=gfx950)
+  ops_py    csrc/bindings/ops_py.cpp     -> minips_amd/_kernels*.so   (hipcc, torch headers)
+
+Rebuilds are mtime-driven: a target is rebuilt when any of its sources or any header in
+its source directories is newer than the output.  `python tools/build.py [targets...]`.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, "build")
+OBJ = os.path.join(BUILD, "obj")
+BIN = os.path.join(BUILD, "bin")
+PKG = os.path.join(ROOT, "minips_amd")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+JOBS = max(1, min(int(os.environ.get("MAX_JOBS", "8")), 16))
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+CXX = os.environ.get("CXX", "g++")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXXFLAGS = ["-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wno-unused-function", "-Wno-sign-compare"]
+HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {cmd[-1]}")
+
+
+def _mtime(p: str) -> float:
+    try:
+        return os.path.getmtime(p)
+    except OSError:
+        return -1.0
+
+
+def _stale(out: str, inputs: list[str]) -> bool:
+    t = _mtime(out)
+    return t < 0 or any(_mtime(i) > t for i in inputs)
+
+
+def _headers(*dirs: str) -> list[str]:
+    hs: list[str] = []
+    for d in dirs:
+        hs += glob.glob(os.path.join(ROOT, d, "*.h")) + glob.glob(os.path.join(ROOT, d, "*.cuh"))
+        hs += glob.glob(os.path.join(ROOT, d, "*.hpp"))
+    return hs
+
+
+def _compile_many(jobs: list[tuple[str, list[str], list[str]]]) -> None:
+    """jobs: (out, inputs, cmd)."""
+    todo = [j for j in jobs if _stale(j[0], j[1])]
+    if not todo:
+        return
+    with cf.ThreadPoolExecutor(JOBS) as ex:
+        futs = [ex.submit(_run, cmd) for _, _, cmd in todo]
+        for f in futs:
+            f.result()
+
+
+def _torch_flags() -> tuple[list[str], list[str]]:
+    import torch.utils.cpp_extension as ce  # noqa: WPS433
+
+    inc = []
+    for p in ce.include_paths("cuda") if "device_type" in ce.include_paths.__code__.co_varnames else ce.include_paths(True):
+        inc += ["-I", p]
+    libdir = ce.library_paths("cuda")[0] if "device_type" in ce.library_paths.__code__.co_varnames else ce.library_paths(True)[0]
+    py_inc = sysconfig.get_paths()["include"]
+    cflags = inc + ["-I", py_inc, "-DTORCH_EXTENSION_NAME=_kernels", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                    "-D_GLIBCXX_USE_CXX11_ABI=1", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1"]
+    ldflags = ["-L", libdir, "-Wl,-rpath," + libdir, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
+               "-lc10_hip", "-ltorch_hip"]
+    return cflags, ldflags
+
+
+def runtime_objs() -> list[str]:
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = _headers("csrc/runtime")
+    jobs, objs = [], []
+    for src in sorted(glob.glob(os.path.join(ROOT, "csrc/runtime/*.cc"))):
+        out = os.path.join(OBJ, "rt_" + os.path.basename(src)[:-3] + ".o")
+        objs.append(out)
+        jobs.append((out, [src] + hdrs, [CXX, *CXXFLAGS, "-c", src, "-o", out]))
+    _compile_many(jobs)
+    return objs
+
+
+def build_runtime_py(objs: list[str]) -> str:
+    import pybind11
+
+    src = os.path.join(ROOT, "csrc/bindings/runtime_py.cc")
+    out = os.path.join(PKG, "_runtime" + EXT)
+    inc = ["-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"]]
+    cmd = [CXX, *CXXFLAGS, "-shared", *inc, src, *objs, "-o", out]
+    _compile_many([(out, [src] + objs + _headers("csrc/runtime"), cmd)])
+    return out
+
+
+def build_tests(objs: list[str]) -> str:
+    os.makedirs(BIN, exist_ok=True)
+    src = os.path.join(ROOT, "csrc/tests/runtime_test.cc")
+    out = os.path.join(BIN, "runtime_test")
+    hdrs = _headers("csrc/runtime", "csrc/tests")
+    _compile_many([(out, [src] + objs + hdrs, [CXX, *CXXFLAGS, src, *objs, "-o", out])])
+    return out
+
+
+def build_apps(objs: list[str]) -> list[str]:
+    os.makedirs(BIN, exist_ok=True)
+    outs, jobs = [], []
+    hdrs = _headers("csrc/runtime", "csrc/apps")
+    for src in sorted(glob.glob(os.path.join(ROOT, "csrc/apps/*.cc"))):
+        out = os.path.join(BIN, os.path.basename(src)[:-3])
+        outs.append(out)
+        jobs.append((out, [src] + objs + hdrs, [CXX, *CXXFLAGS, src, *objs, "-o", out]))
+    _compile_many(jobs)
+    return outs
+
+
+def kernel_objs() -> list[str]:
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = _headers("csrc/kernels")
+    jobs, objs = [], []
+    for src in sorted(glob.glob(os.path.join(ROOT, "csrc/kernels/*.hip"))):
+        out = os.path.join(OBJ, "k_" + os.path.basename(src)[:-4] + ".o")
+        objs.append(out)
+        jobs.append((out, [src] + hdrs, [HIPCC, *HIPFLAGS, "-c", src, "-o", out]))
+    _compile_many(jobs)
+    return objs
+
+
+def build_ops_py(kobjs: list[str]) -> str:
+    src = os.path.join(ROOT, "csrc/bindings/ops_py.cpp")
+    out = os.path.join(PKG, "_kernels" + EXT)
+    bobj = os.path.join(OBJ, "ops_py.o")
+    cflags, ldflags = _torch_flags()
+    hdrs = _headers("csrc/kernels", "csrc/bindings")
+    _compile_many([(bobj, [src] + hdrs, [HIPCC, "-O2", "-std=c++17", "-fPIC", *cflags, "-c", src, "-o", bobj])])
+    _compile_many([(out, [bobj] + kobjs,
+                    [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", bobj, *kobjs, "-o", out, *ldflags])])
+    return out
+
+
+def main(argv: list[str]) -> int:
+    targets = set(argv) or {"runtime", "rt_py", "tests", "apps", "kernels", "ops_py"}
+    objs = runtime_objs()
+    if "rt_py" in targets:
+        print("built", build_runtime_py(objs))
+    if "tests" in targets:
+        print("built", build_tests(objs))
+    if "apps" in targets:
+        for o in build_apps(objs):
+            print("built", o)
+    if targets & {"kernels", "ops_py"}:
+        kobjs = kernel_objs()
+        if "ops_py" in targets:
+            print("built", build_ops_py(kobjs))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))
