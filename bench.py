@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Headline benchmark: samples/sec (whole node) of Criteo-shaped Wide&Deep under BSP on the
+MI355X parameter server (BASELINE.json metric), one process per GPU.
+
+    python bench.py --gpus 1 --steps 50 --warmup 10
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
+
+Per-GPU batch is fixed (weak scaling). Every timed step does the full PS superstep: synthetic
+batch generation on the GPU, sparse Get (dedupe + all-to-all), deep-tower forward/backward,
+sparse + dense Add, and the Clock (all-to-all of gradient rows + row-wise Adagrad on the
+owner shards, reduce-scatter + Adam + all-gather of the dense tower). Rank 0 prints one JSON
+line; `value` is the whole-job throughput and the time is the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "samples/sec (whole node) Criteo-shaped Wide&Deep BSP at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16384, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--consistency", default="bsp", choices=["bsp", "ssp", "asp"])
+    ap.add_argument("--staleness", type=int, default=0)
+    ap.add_argument("--profile-steps", type=int, default=0, help="print per-phase timings")
+    args = ap.parse_args()
+
+    from minips_amd.data.synthetic import CriteoSynth
+    from minips_amd.models.widedeep import WideDeep, WideDeepConfig
+    from minips_amd.ps.comm import init_distributed
+
+    comm = init_distributed()
+    n = comm.world
+    if n != args.gpus and comm.rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {n}", file=sys.stderr)
+    dev = comm.device
+    cfg = WideDeepConfig(consistency=args.consistency, staleness=args.staleness)
+    model = WideDeep(cfg, comm)
+    data = CriteoSynth(args.batch, cards=cfg.cards, device=dev, seed=1000 + comm.rank)
+
+    def step():
+        dense, keys, labels = data.next()
+        return model.train_step(dense, keys, labels)
+
+    loss0 = None
+    for i in range(args.warmup):
+        l = step()
+        if i == 0:
+            loss0 = float(l.item()) / args.batch
+    model.drain()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        l = step()
+    model.drain()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if n > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    loss_last = float(l.item()) / args.batch
+    samples = args.batch * n * args.steps
+    value = samples / elapsed
+    if comm.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (Criteo-Kaggle cardinalities, Zipf-like ids, 13 dense N(0,1)); random-init weights",
+            "config": {
+                "model": "Wide&Deep: 26 sparse (33.76M rows, emb 32 + wide 1, row-wise Adagrad) + 13 dense; "
+                         "deep MLP 848-1024-512-256-1 (Adam)",
+                "global_batch": args.batch * n,
+                "seq_len": None,
+                "parallelism": f"ps-dp{n} (BSP: a2a sparse rows, RS/AG dense)" if args.consistency == "bsp"
+                else f"ps-dp{n} ({args.consistency} s={args.staleness})",
+                "per_gpu_batch": args.batch,
+                "consistency": args.consistency,
+            },
+            "loss_first": round(loss0, 5) if loss0 is not None else None,
+            "loss_last": round(loss_last, 5),
+        }
+        print(json.dumps(out), flush=True)
+    if n > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

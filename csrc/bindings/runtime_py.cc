@@ -1,0 +1,280 @@
+// pybind11 bindings of the C++ PS runtime (module minips_amd._runtime).
+// Blocking calls (Get, CheckPoint, Barrier, Run, Stop) release the GIL; worker lambdas
+// passed to Engine.run are invoked on C++ threads that re-acquire it.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../runtime/checkpoint.h"
+#include "../runtime/comm.h"
+#include "../runtime/config.h"
+#include "../runtime/engine.h"
+
+namespace py = pybind11;
+using namespace minips;
+
+namespace {
+
+template <typename Val>
+void BindTable(py::module& m, const char* name) {
+  py::class_<KVClientTable<Val>>(m, name)
+      .def(
+          "get",
+          [](KVClientTable<Val>& t, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> keys) {
+            std::vector<Key> k(keys.data(), keys.data() + keys.size());
+            std::vector<Val> vals;
+            {
+              py::gil_scoped_release rel;
+              t.Get(k, &vals);
+            }
+            return py::array_t<Val>(vals.size(), vals.data());
+          },
+          "Blocking pull of sorted keys; returns values in key order.")
+      .def(
+          "add",
+          [](KVClientTable<Val>& t, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> keys,
+             py::array_t<Val, py::array::c_style | py::array::forcecast> vals) {
+            std::vector<Key> k(keys.data(), keys.data() + keys.size());
+            std::vector<Val> v(vals.data(), vals.data() + vals.size());
+            t.Add(k, v);
+          },
+          "Asynchronous push of (sorted keys, values).")
+      .def("clock", &KVClientTable<Val>::Clock)
+      .def("checkpoint", &KVClientTable<Val>::CheckPoint, py::call_guard<py::gil_scoped_release>())
+      .def("heartbeat", &KVClientTable<Val>::HeartBeat, py::arg("node_id"), py::arg("quit") = false);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_runtime, m) {
+  m.doc() = "minips_amd C++ parameter-server runtime";
+
+  py::enum_<Flag>(m, "Flag")
+      .value("kExit", Flag::kExit)
+      .value("kBarrier", Flag::kBarrier)
+      .value("kResetWorkerInModel", Flag::kResetWorkerInModel)
+      .value("kClock", Flag::kClock)
+      .value("kAdd", Flag::kAdd)
+      .value("kGet", Flag::kGet)
+      .value("kForceQuit", Flag::kForceQuit)
+      .value("kCheckpoint", Flag::kCheckpoint)
+      .value("kHeartBeat", Flag::kHeartBeat)
+      .value("kQuitHeartBeat", Flag::kQuitHeartBeat)
+      .value("kRollBack", Flag::kRollBack)
+      .value("kScale", Flag::kScale)
+      .value("kScaleRollback", Flag::kScaleRollback);
+  py::enum_<ModelType>(m, "ModelType").value("SSP", ModelType::SSP).value("BSP", ModelType::BSP).value("ASP", ModelType::ASP);
+  py::enum_<StorageType>(m, "StorageType").value("Map", StorageType::Map).value("Vector", StorageType::Vector);
+
+  py::class_<Node>(m, "Node")
+      .def(py::init([](uint32_t id, std::string host, int port, bool is_master, int gpu) {
+             Node n;
+             n.id = id;
+             n.hostname = host;
+             n.port = port;
+             n.is_master = is_master;
+             n.gpu = gpu;
+             return n;
+           }),
+           py::arg("id") = 0, py::arg("hostname") = "localhost", py::arg("port") = 0, py::arg("is_master") = false,
+           py::arg("gpu") = -1)
+      .def_readwrite("id", &Node::id)
+      .def_readwrite("hostname", &Node::hostname)
+      .def_readwrite("port", &Node::port)
+      .def_readwrite("is_master", &Node::is_master)
+      .def_readwrite("gpu", &Node::gpu)
+      .def("__repr__", &Node::DebugString);
+  m.def("parse_file", &ParseFile);
+  m.def("select_master", [](std::vector<Node> nodes, int hb) {
+    Node master = SelectMaster(nodes, hb);
+    return py::make_tuple(master, nodes);
+  });
+  m.def("check_valid_node_ids", &CheckValidNodeIds);
+  m.def("check_consecutive_ids", &CheckConsecutiveIds);
+
+  py::class_<Range>(m, "Range")
+      .def(py::init<uint64_t, uint64_t>())
+      .def("begin", &Range::begin)
+      .def("end", &Range::end)
+      .def("size", &Range::size)
+      .def("__repr__", [](const Range& r) { return "[" + std::to_string(r.begin()) + "," + std::to_string(r.end()) + ")"; });
+  m.def("even_ranges", &EvenRanges);
+
+  // --- Context (typed flag registry) --------------------------------------------------
+  py::class_<Context, std::unique_ptr<Context, py::nodelete>>(m, "Context")
+      .def_static("get", &Context::Get, py::return_value_policy::reference)
+      .def("define",
+           [](Context& c, const std::string& name, const std::string& type, const std::string& def,
+              const std::string& help) {
+             Context::Type t = type == "int" ? Context::Type::kInt
+                               : type == "bool" ? Context::Type::kBool
+                               : type == "double" ? Context::Type::kDouble
+                                                  : Context::Type::kString;
+             c.Define(name, t, def, help);
+           },
+           py::arg("name"), py::arg("type"), py::arg("default"), py::arg("help") = "")
+      .def("has", &Context::Has)
+      .def("get_string", &Context::get_string)
+      .def("get_int32", &Context::get_int32)
+      .def("get_int64", &Context::get_int64)
+      .def("get_bool", &Context::get_bool)
+      .def("get_double", &Context::get_double)
+      .def("set", [](Context& c, const std::string& n, const std::string& v) { c.set(n, v); })
+      .def("set_int", [](Context& c, const std::string& n, int64_t v) { c.set(n, v); })
+      .def("set_bool", [](Context& c, const std::string& n, bool v) { c.set(n, v); })
+      .def("parse_args", [](Context& c, const std::vector<std::string>& a, bool u) { return c.ParseArgs(a, u); },
+           py::arg("args"), py::arg("allow_unknown") = false)
+      .def("snapshot", &Context::Snapshot)
+      .def("help", &Context::Help)
+      .def("reset", &Context::ResetToDefaults)
+      .def("set_iteration", &Context::SetIteration)
+      .def("get_iteration", &Context::GetIteration)
+      .def("iteration_map", &Context::GetIterationMap)
+      .def("set_iteration_map", &Context::SetIterationMap);
+
+  // --- consistency building blocks -----------------------------------------------------
+  py::class_<ProgressTracker>(m, "ProgressTracker")
+      .def(py::init<>())
+      .def("init", &ProgressTracker::Init)
+      .def("advance_and_get_changed_min_clock", &ProgressTracker::AdvanceAndGetChangedMinClock)
+      .def("get_progress", &ProgressTracker::GetProgress)
+      .def("get_min_clock", &ProgressTracker::GetMinClock)
+      .def("get_num_threads", &ProgressTracker::GetNumThreads)
+      .def("is_unique_min", &ProgressTracker::IsUniqueMin)
+      .def("check_thread_valid", &ProgressTracker::CheckThreadValid)
+      .def("delete_node", &ProgressTracker::DeleteNode)
+      .def("dump", &ProgressTracker::Dump, py::arg("path"), py::arg("round_hundred") = false)
+      .def("restore", &ProgressTracker::Restore, py::arg("path"), py::arg("scale_node_id") = -1)
+      .def("progresses", &ProgressTracker::Progresses)
+      .def("__repr__", &ProgressTracker::DebugString);
+
+  py::class_<SimpleIdMapper>(m, "SimpleIdMapper")
+      .def(py::init<Node, std::vector<Node>>())
+      .def("init", &SimpleIdMapper::Init, py::arg("num_server_threads_per_node"), py::arg("skip_node_id") = -1)
+      .def("get_node_id_for_thread", &SimpleIdMapper::GetNodeIdForThread)
+      .def("allocate_worker_thread", &SimpleIdMapper::AllocateWorkerThread)
+      .def("deallocate_worker_thread", &SimpleIdMapper::DeallocateWorkerThread)
+      .def("get_server_threads_for_id", &SimpleIdMapper::GetServerThreadsForId)
+      .def("get_worker_helper_threads_for_id", &SimpleIdMapper::GetWorkerHelperThreadsForId)
+      .def("get_worker_threads_for_id", &SimpleIdMapper::GetWorkerThreadsForId)
+      .def("get_all_server_threads", &SimpleIdMapper::GetAllServerThreads);
+  m.attr("kMaxThreadsPerNode") = SimpleIdMapper::kMaxThreadsPerNode;
+  m.attr("kMaxBgThreadsPerNode") = SimpleIdMapper::kMaxBgThreadsPerNode;
+  m.attr("kWorkerHelperThreadId") = SimpleIdMapper::kWorkerHelperThreadId;
+
+  py::class_<WorkerAlloc>(m, "WorkerAlloc")
+      .def(py::init([](uint32_t node, uint32_t n) { return WorkerAlloc{node, n}; }))
+      .def_readwrite("node_id", &WorkerAlloc::node_id)
+      .def_readwrite("num_workers", &WorkerAlloc::num_workers);
+  py::class_<WorkerSpec>(m, "WorkerSpec")
+      .def(py::init<const std::vector<WorkerAlloc>&>())
+      .def("has_local_workers", &WorkerSpec::HasLocalWorkers)
+      .def("get_local_workers", &WorkerSpec::GetLocalWorkers)
+      .def("get_local_threads", &WorkerSpec::GetLocalThreads)
+      .def("get_all_thread_ids", &WorkerSpec::GetAllThreadIds)
+      .def("insert_worker_id_thread_id", &WorkerSpec::InsertWorkerIdThreadId)
+      .def("get_num_workers", &WorkerSpec::GetNumWorkers);
+
+  py::class_<RangePartitionManager>(m, "RangePartitionManager")
+      .def(py::init<const std::vector<uint32_t>&, const std::vector<Range>&, int>(), py::arg("server_thread_ids"),
+           py::arg("ranges"), py::arg("master_node_id") = -1)
+      .def("slice", [](const RangePartitionManager& pm, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> keys) {
+        SArray<Key> k(keys.data(), keys.size());
+        std::vector<std::pair<int, Keys>> sliced;
+        pm.Slice(k, &sliced);
+        py::list out;
+        for (auto& s : sliced) out.append(py::make_tuple(s.first, py::array_t<uint64_t>(s.second.size(), s.second.data())));
+        return out;
+      })
+      .def("get_ranges", &RangePartitionManager::GetRanges);
+
+  // --- engine / task / tables ----------------------------------------------------------
+  py::class_<Info>(m, "Info")
+      .def_readonly("thread_id", &Info::thread_id)
+      .def_readonly("worker_id", &Info::worker_id)
+      .def_readonly("node_id", &Info::node_id)
+      .def("create_kv_client_table",
+           [](const Info& info, uint32_t table_id, const std::string& dtype) -> py::object {
+             if (dtype == "float32") return py::cast(info.CreateKVClientTable<float>(table_id).release(), py::return_value_policy::take_ownership);
+             return py::cast(info.CreateKVClientTable<double>(table_id).release(), py::return_value_policy::take_ownership);
+           },
+           py::arg("table_id"), py::arg("dtype") = "float64");
+  BindTable<double>(m, "KVClientTableF64");
+  BindTable<float>(m, "KVClientTableF32");
+
+  py::class_<MLTask>(m, "MLTask")
+      .def(py::init<>())
+      .def("set_lambda", &MLTask::SetLambda)
+      .def("set_worker_alloc", &MLTask::SetWorkerAlloc)
+      .def("set_tables", &MLTask::SetTables)
+      .def("is_setup", &MLTask::IsSetup);
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<const Node&, const std::vector<Node>&, const Node&, const Node&>(), py::arg("node"),
+           py::arg("nodes"), py::arg("master") = Node(), py::arg("scale_node") = Node())
+      .def("start_everything", &Engine::StartEverything, py::arg("num_server_threads_per_node") = 1,
+           py::call_guard<py::gil_scoped_release>())
+      .def("stop_everything", &Engine::StopEverything, py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &Engine::Barrier, py::call_guard<py::gil_scoped_release>())
+      .def("force_quit", &Engine::ForceQuit)
+      .def("run", &Engine::Run, py::call_guard<py::gil_scoped_release>())
+      .def("get_ranges", &Engine::getRanges)
+      .def(
+          "create_table",
+          [](Engine& e, const std::vector<Range>& ranges, ModelType mt, StorageType st, int staleness,
+             const std::string& dtype) {
+            if (dtype == "float32") return e.CreateTable<float>(ranges, mt, st, staleness);
+            return e.CreateTable<double>(ranges, mt, st, staleness);
+          },
+          py::arg("ranges"), py::arg("model_type") = ModelType::BSP, py::arg("storage_type") = StorageType::Vector,
+          py::arg("staleness") = 0, py::arg("dtype") = "float64")
+      .def("set_dump_callback", &Engine::SetDumpCallback)
+      .def("is_need_rollback", &Engine::IsNeedRollBack)
+      .def("inc_rollback_count", &Engine::IncRollBackCount)
+      .def("recover_end", &Engine::RecoverEnd)
+      .def("wait_recover", &Engine::WaitRecover, py::call_guard<py::gil_scoped_release>())
+      .def("rollback_count", &Engine::RollBackCount)
+      .def("num_tables", &Engine::NumTables)
+      .def("get_node", &Engine::GetNode)
+      .def("get_nodes", &Engine::GetNodes)
+      .def("bytes_sent", [](Engine& e) { return e.GetMailbox() ? e.GetMailbox()->BytesSent() : 0; });
+
+  py::class_<Master>(m, "Master")
+      .def(py::init<const Node&, const std::vector<Node>&>(), py::call_guard<py::gil_scoped_release>())
+      .def("wait_all_quit", &Master::WaitAllQuit, py::arg("timeout_s") = 0.0, py::call_guard<py::gil_scoped_release>())
+      .def("stop_master", &Master::StopMaster, py::call_guard<py::gil_scoped_release>())
+      .def("rollback_count", &Master::RollBackCount)
+      .def("detected", [](Master& m) { return m.GetCheckThread()->Detected(); });
+
+  // --- checkpoint / data ---------------------------------------------------------------
+  m.def("dump_config_data", &DumpConfigData);
+  m.def("load_config_data", &LoadConfigData);
+  m.def("check_fault_tolerance", &CheckFaultTolerance, py::arg("phase"), py::arg("detail") = "");
+  m.def(
+      "load_libsvm",
+      [](const std::string& path, int shard, int num_shards, int threads, bool one_based) {
+        std::vector<SVMItem> items;
+        {
+          py::gil_scoped_release rel;
+          items = LoadLibsvmFile(path, shard, num_shards, threads, one_based);
+        }
+        // CSR arrays: rowptr, cols, vals, labels
+        std::vector<int64_t> rowptr{0}, cols;
+        std::vector<double> vals, labels;
+        for (auto& it : items) {
+          for (auto& f : it.x) {
+            cols.push_back(f.first);
+            vals.push_back(f.second);
+          }
+          rowptr.push_back((int64_t)cols.size());
+          labels.push_back(it.y);
+        }
+        return py::make_tuple(py::array_t<int64_t>(rowptr.size(), rowptr.data()),
+                              py::array_t<int64_t>(cols.size(), cols.data()),
+                              py::array_t<double>(vals.size(), vals.data()),
+                              py::array_t<double>(labels.size(), labels.data()));
+      },
+      py::arg("path"), py::arg("shard") = 0, py::arg("num_shards") = 1, py::arg("threads") = 4,
+      py::arg("one_based") = true);
+}

@@ -1,0 +1,56 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels.
+// Wave64 everywhere; bf16 handled as raw uint16 with round-to-nearest-even conversion.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MINIPS_HIP_CHECK(expr)                                                      \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess) {                                                         \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + \
+                               " at " __FILE__ ":" + std::to_string(__LINE__));     \
+    }                                                                               \
+  } while (0)
+
+namespace minips_k {
+
+constexpr int kWave = 64;
+
+typedef uint16_t bf16_t;
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// Grid size for grid-stride memory-bound kernels: ~8 blocks/CU on 256 CUs.
+inline int grid_for(int64_t work, int block, int cap = 2048) {
+  int64_t g = (work + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace minips_k

@@ -1,0 +1,259 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues (worker forward/backward of the MLP
+// towers: Wide&Deep deep tower, DLRM bottom/top MLPs, the 3-layer MLP, GPT-2 projections).
+//
+//   C[M,N] = A . B   (fp32 accumulate on v_mfma_f32_16x16x32_bf16)
+//   A stored MK ([M][K], k contiguous)  or KM ([K][M], m contiguous)
+//   B stored NK ([N][K], a Linear weight) or KN ([K][N], n contiguous)
+//   forward   Y = act(X W^T + b):        A=X  (MK), B=W  (NK)
+//   dgrad     dX = (dY W) * mask:        A=dY (MK), B=W  (KN)
+//   wgrad     dW += dY^T X  (split-K):   A=dY (KM), B=X  (KN)
+//
+// Tiling: 128x128x32 block tile, 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 MFMA
+// 16x16 tiles (64 accumulator VGPRs). Operands are staged global -> registers -> LDS with a
+// one-tile register prefetch (the next tile's loads are in flight during the MFMAs). MK/NK
+// tiles live in LDS as [row][k] and are read with ds_read_b128; KM/KN tiles live as
+// [k][row] and are read with the gfx950 transposing ds_read_b64_tr_b16, so no operand is
+// ever transposed in memory. When both operands are tr-read (wgrad) the k order inside a
+// 32-wide step is permuted identically on both sides so that each 32-lane half reads 8
+// consecutive LDS rows (bank-conflict free with the 288-B row pitch).
+// Block ids are remapped so that consecutive tiles of one row panel share an XCD (T1).
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace minips_k {
+
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int LDS_ROW = BK + 8;     // [row][k] pitch in bf16 (80 B)
+constexpr int LDS_TR = BM + 16;     // [k][row] pitch in bf16 (288 B)
+constexpr int TILE_ELEMS = (BM * LDS_ROW > BK * LDS_TR) ? BM * LDS_ROW : BK * LDS_TR;
+
+__device__ __forceinline__ v4s ds_read_tr16(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+// Loads one BMxBK (or BKxBM) tile chunk set into registers: 2 x 16 B per thread.
+template <bool KMAJOR>
+__device__ __forceinline__ void load_tile(const bf16_t* __restrict__ G, int ld, int row0, int k0, int rows, int K,
+                                          int tid, uint4 (&r)[2]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int c = tid + h * 256;
+    int row, k;
+    if (!KMAJOR) {
+      row = c >> 2;
+      k = (c & 3) * 8;
+    } else {
+      k = c >> 4;
+      row = (c & 15) * 8;
+    }
+    int gr = row0 + row, gk = k0 + k;
+    bool ok = (gr < rows) && (gk < K);
+    const bf16_t* src = !KMAJOR ? G + (int64_t)gr * ld + gk : G + (int64_t)gk * ld + gr;
+    r[h] = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <bool KMAJOR>
+__device__ __forceinline__ void store_tile(bf16_t* S, int tid, const uint4 (&r)[2]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int c = tid + h * 256;
+    if (!KMAJOR) {
+      *reinterpret_cast<uint4*>(S + (c >> 2) * LDS_ROW + (c & 3) * 8) = r[h];
+    } else {
+      *reinterpret_cast<uint4*>(S + (c >> 4) * LDS_TR + (c & 15) * 8) = r[h];
+    }
+  }
+}
+
+// Fragment of the 16x16x32 operand: 8 bf16 along k for row `row` (A) / column (B).
+template <bool KMAJOR, bool PERM>
+__device__ __forceinline__ v8s read_frag(const bf16_t* S, int row_base, int lane) {
+  int g = lane >> 4;
+  if (!KMAJOR) {
+    int row = row_base + (lane & 15);
+    if (!PERM) return *reinterpret_cast<const v8s*>(S + row * LDS_ROW + 8 * g);
+    v4s lo = *reinterpret_cast<const v4s*>(S + row * LDS_ROW + 4 * g);
+    v4s hi = *reinterpret_cast<const v4s*>(S + row * LDS_ROW + 16 + 4 * g);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  } else {
+    int i = lane & 15, q = i >> 2, p = i & 3;
+    int r0 = PERM ? 4 * g : 8 * g;
+    int r1 = PERM ? 16 + 4 * g : 8 * g + 4;
+    v4s lo = ds_read_tr16(S + (r0 + q) * LDS_TR + row_base + 4 * p);
+    v4s hi = ds_read_tr16(S + (r1 + q) * LDS_TR + row_base + 4 * p);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+struct EpiArgs {
+  void* C;
+  int ldc;
+  const bf16_t* bias;    // [N] bf16 (pulled params are bf16)
+  const bf16_t* mask;    // [M][ldmask] (relu mask source)
+  int ldmask;
+  float* colsum;         // [N] column sums of the (masked) output
+  float alpha;
+};
+
+template <bool A_KM, bool B_KN, int EPI>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                        int M, int N, int K, int lda, int ldb, int k_chunk,
+                                                        EpiArgs ep) {
+  constexpr bool PERM = A_KM && B_KN;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][TILE_ELEMS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware remap (T1): hardware deals blocks round-robin over 8 XCDs; give each XCD a
+  // contiguous run of tiles so neighbouring tiles (same A panel) share its L2.
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if (nwg >= 16) {
+    int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    bid = base + (bid >> 3);
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kb = blockIdx.z * k_chunk;
+  const int ke = min(K, kb + k_chunk);
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[2], rb[2];
+  int cur = 0;
+  if (kb < ke) {
+    load_tile<A_KM>(A, lda, m0, kb, M, ke, tid, ra);
+    load_tile<B_KN>(B, ldb, n0, kb, N, ke, tid, rb);
+    store_tile<A_KM>(smem[0][0], tid, ra);
+    store_tile<B_KN>(smem[0][1], tid, rb);
+  }
+  __syncthreads();
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool has_next = k0 + BK < ke;
+    if (has_next) {  // issue next tile's global loads before the MFMAs (T14 split)
+      load_tile<A_KM>(A, lda, m0, k0 + BK, M, ke, tid, ra);
+      load_tile<B_KN>(B, ldb, n0, k0 + BK, N, ke, tid, rb);
+    }
+    const bf16_t* SA = smem[cur][0];
+    const bf16_t* SB = smem[cur][1];
+    v8s af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = read_frag<A_KM, PERM>(SA, wm * 64 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = read_frag<B_KN, PERM>(SB, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i]),
+                                                            __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+    if (has_next) {
+      store_tile<A_KM>(smem[cur ^ 1][0], tid, ra);
+      store_tile<B_KN>(smem[cur ^ 1][1], tid, rb);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int col_l = lane & 15, row_q = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + col_l;
+    const bool col_ok = col < N;
+    float bias = 0.f;
+    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
+    float csum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + row_q + r;
+        if (!(col_ok && row < M)) continue;
+        float v = acc[i][j][r] * ep.alpha;
+        const int64_t off = (int64_t)row * ep.ldc + col;
+        if (EPI == kEpiStoreF32) {
+          ((float*)ep.C)[off] = v;
+        } else if (EPI == kEpiAtomicF32) {
+          atomicAdd(((float*)ep.C) + off, v);
+        } else if (EPI == kEpiBiasReluBf16) {
+          ((bf16_t*)ep.C)[off] = f2bf(fmaxf(v + bias, 0.f));
+        } else if (EPI == kEpiBiasBf16) {
+          ((bf16_t*)ep.C)[off] = f2bf(v + bias);
+        } else if (EPI == kEpiBiasGeluBf16) {
+          float x = v + bias;
+          float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
+          ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
+        } else if (EPI == kEpiStoreBf16) {
+          ((bf16_t*)ep.C)[off] = f2bf(v);
+        } else if (EPI == kEpiReluMaskBf16) {
+          float m = bf2f(ep.mask[(int64_t)row * ep.ldmask + col]);
+          float o = m > 0.f ? v : 0.f;
+          bf16_t ob = f2bf(o);
+          ((bf16_t*)ep.C)[off] = ob;
+          csum += bf2f(ob);
+        }
+      }
+    }
+    if (EPI == kEpiReluMaskBf16 && ep.colsum) {
+      csum += __shfl_xor(csum, 16, 64);
+      csum += __shfl_xor(csum, 32, 64);
+      if (lane < 16 && col_ok) atomicAdd(ep.colsum + col, csum);
+    }
+  }
+}
+
+template <bool A_KM, bool B_KN, int EPI>
+static void launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, int split_k,
+                   const EpiArgs& ep, hipStream_t s) {
+  int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int kc = ((K + split_k - 1) / split_k + BK - 1) / BK * BK;
+  int nsplit = (K + kc - 1) / kc;
+  dim3 grid(tiles, 1, nsplit);
+  hipLaunchKernelGGL((gemm_bf16_kernel<A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
+}
+
+#define MINIPS_GEMM_EPI_DISPATCH(AKM, BKN)                                                        \
+  switch (epi) {                                                                                 \
+    case kEpiStoreF32: launch<AKM, BKN, kEpiStoreF32>(A, B, M, N, K, lda, ldb, split_k, ep, s); break;  \
+    case kEpiAtomicF32: launch<AKM, BKN, kEpiAtomicF32>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
+    case kEpiBiasReluBf16: launch<AKM, BKN, kEpiBiasReluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
+    case kEpiBiasBf16: launch<AKM, BKN, kEpiBiasBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
+    case kEpiBiasGeluBf16: launch<AKM, BKN, kEpiBiasGeluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
+    case kEpiStoreBf16: launch<AKM, BKN, kEpiStoreBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
+    case kEpiReluMaskBf16: launch<AKM, BKN, kEpiReluMaskBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
+    default: throw std::runtime_error("gemm: unknown epilogue " + std::to_string(epi));           \
+  }
+
+void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+               bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
+               float alpha, int split_k, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  if (split_k < 1) split_k = 1;
+  if (split_k > 1 && epi != kEpiAtomicF32) throw std::runtime_error("gemm: split_k needs the atomic epilogue");
+  EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha};
+  if (!a_km && !b_kn) {
+    MINIPS_GEMM_EPI_DISPATCH(false, false)
+  } else if (!a_km && b_kn) {
+    MINIPS_GEMM_EPI_DISPATCH(false, true)
+  } else if (a_km && b_kn) {
+    MINIPS_GEMM_EPI_DISPATCH(true, true)
+  } else {
+    MINIPS_GEMM_EPI_DISPATCH(true, false)
+  }
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace minips_k

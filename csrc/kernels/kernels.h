@@ -1,0 +1,100 @@
+// Host-callable launchers of the gfx950 kernels (raw pointers + stream; no torch types).
+// The torch-facing validation layer is csrc/bindings/ops_py.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace minips_k {
+
+typedef uint16_t bf16_t;
+
+// ------------------------------------------------------------------ GEMM (gemm.hip)
+enum GemmEpilogue {
+  kEpiStoreF32 = 0,      // C fp32 = alpha*acc
+  kEpiAtomicF32 = 1,     // C fp32 += alpha*acc (split-K weight gradients)
+  kEpiBiasReluBf16 = 2,  // C bf16 = relu(acc + bias)
+  kEpiBiasBf16 = 3,      // C bf16 = acc + bias
+  kEpiStoreBf16 = 4,     // C bf16 = acc
+  kEpiReluMaskBf16 = 5,  // C bf16 = acc * (mask > 0); colsum[n] += sum_m C
+  kEpiBiasGeluBf16 = 6,  // C bf16 = gelu_tanh(acc + bias)
+};
+void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+               bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
+               float alpha, int split_k, hipStream_t s);
+
+// ------------------------------------------------------------------ sparse keys (sparse.hip)
+// Hash-based dedupe + owner bucketing of int64 keys in 3 launches (no sort):
+//   insert: open-addressing insert; first inserter of a key counts it for its owner shard
+//   assign: per unique key, position = offset[owner] + cursor (keys grouped by owner)
+//   inverse: inverse[i] = position of keys[i]
+// `bounds` [P+1] are the shard key ranges (owner = upper_bound(bounds, key) - 1); P=1 with
+// bounds {0, 2^63} makes it a plain unique. Work buffers are provided by the caller:
+// table_keys/table_pos [cap] (cap power of two >= 2n), slot [n], flags [n], counts [P],
+// cursor [P] (all state re-initialised inside).
+void unique_bucketize(const int64_t* keys, int64_t n, const int64_t* bounds, int P, int64_t* table_keys,
+                      int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
+                      int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s);
+
+// Row gather from a shard: out[i, :] = table[keys[i] - base, :] with dtype conversion.
+// table fp32 [R, D] row stride ld; out fp32 or bf16 [n, D].
+void gather_rows(const float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, void* out,
+                 bool out_bf16, hipStream_t s);
+// Scatter-add rows: acc[idx[i], :] += src[i, :] (fp32, float atomics, 2 rows per wave-instr).
+void scatter_add_rows(const float* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s);
+// Row-wise Adagrad on a shard (one accumulator per row, DLRM style):
+//   s[row] += mean(g^2); w[row,:] -= lr * g / (sqrt(s[row]) + eps)
+// Columns [D1, D) may use a second accumulator state2 (D1 = D: single group).
+void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
+                            int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s);
+// Plain SGD on rows: w[row,:] += scale * g  (the reference's "w += delta" server apply)
+void sparse_sgd(float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, const float* grads,
+                float scale, hipStream_t s);
+
+// EmbeddingBag (sum/mean) over an [R, D] table (fp32 or bf16 rows via gathered buffer):
+//   out[b, :] = pool_{j in bag b} rows[idx[j], :]   offsets [B+1]
+void embedding_bag_fwd(const float* rows, const int64_t* idx, const int64_t* offsets, int64_t B, int D, bool mean,
+                       float* out, hipStream_t s);
+void embedding_bag_bwd(const float* grad_out, const int64_t* idx, const int64_t* offsets, int64_t B, int D,
+                       bool mean, float* grad_rows, hipStream_t s);
+
+// ------------------------------------------------------------------ Wide&Deep (widedeep.hip)
+// Builds the deep-tower input X [B, ldx] bf16 = [F embeddings of width D | n_dense dense
+// features | zero pad]: columns [f*D, (f+1)*D) hold row inv[b*F+f] of the pulled rows
+// (bf16 [U, row_stride]), columns [F*D, F*D+n_dense) the dense features (fp32 [B, n_dense]).
+// wide_logit[b] = sum_f rows[inv[b*F+f], D] (the wide weight lives in column D of a row).
+void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B,
+                 int F, int D, bf16_t* X, int ldx, float* wide_logit, hipStream_t s);
+// Head (last Linear Hd->1 + BCE-with-logits, fwd and bwd fused):
+//   z = H[b,:].w + b0 + wide[b]; dz = (sigmoid(z) - y) * grad_scale
+//   dH = dz * w * (H > 0) (bf16), dw += dz*H, db += dz, dH_colsum += dH, dwide[b] = dz,
+//   loss_sum += BCE(z, y)
+void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
+             const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
+             float grad_scale, hipStream_t s);
+// Embedding backward: grad_rows[inv[b*F+f], 0:D] += dX[b, f*D : (f+1)*D] (fp32 dX, ld ldx),
+// grad_rows[inv[b*F+f], D] += dwide[b]   (grad_rows fp32 [U, row_stride], pre-zeroed).
+void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
+                     float* grad_rows, int row_stride, hipStream_t s);
+
+// ------------------------------------------------------------------ optimizers (optim.hip)
+// Fused Adam(W) on an fp32 master shard; optionally writes the bf16 copy for all-gather.
+void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2,
+                float eps, float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s);
+void sgd_apply(float* w, const float* g, int64_t n, float lr, float grad_scale, bf16_t* w_bf16, hipStream_t s);
+void adagrad_apply(float* w, float* acc, const float* g, int64_t n, float lr, float eps, float grad_scale,
+                   bf16_t* w_bf16, hipStream_t s);
+void cast_f32_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t s);
+void cast_bf16_f32(const bf16_t* x, float* y, int64_t n, hipStream_t s);
+
+// ------------------------------------------------------------------ LR / K-Means (ml.hip)
+// Sparse logistic regression over a CSR batch whose columns are positions into the pulled
+// weight vector w [U]: p_i = sigmoid(sum_j w[col_j] x_j); delta[col_j] += alpha*x_j*(y_i - p_i)
+// (labels < 0 treated as 0, lr_example.cpp:291-312). Optional correct-count for accuracy.
+void lr_sparse_step(const int64_t* rowptr, const int64_t* cols, const float* vals, const float* labels, int64_t B,
+                    const float* w, float alpha, float* delta, float* correct, hipStream_t s);
+// K-Means assignment: X [n, d] fp32, C [k, d] fp32 -> assign [n] (int32), min dist [n].
+void kmeans_assign(const float* X, int64_t n, int d, const float* C, int k, int32_t* assign, float* dist,
+                   hipStream_t s);
+
+}  // namespace minips_k

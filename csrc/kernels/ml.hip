@@ -1,0 +1,83 @@
+// Classic-ML worker kernels of the reference apps on the GPU data plane:
+//   lr_sparse_step  (K7/K8) sparse logistic regression gradient over a CSR mini-batch,
+//                   the math of apps/logistic_regression/lr_example.cpp:291-312
+//   kmeans_assign   (K9)    nearest-centre assignment, apps/kmeans/kmeans_helper.hpp:45-66
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace minips_k {
+
+// One wave per sample: lanes stride the sample's non-zeros.
+__global__ void lr_sparse_kernel(const int64_t* __restrict__ rowptr, const int64_t* __restrict__ cols,
+                                 const float* __restrict__ vals, const float* __restrict__ labels, int64_t B,
+                                 const float* __restrict__ w, float alpha, float* delta, float* correct) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  float hits = 0.f;
+  for (int64_t i = wave; i < B; i += nwaves) {
+    const int64_t s0 = rowptr[i], s1 = rowptr[i + 1];
+    float dot = 0.f;
+    for (int64_t j = s0 + lane; j < s1; j += 64) dot += w[cols[j]] * vals[j];
+    dot = warp_sum(dot);
+    const float p = sigmoidf_(dot);
+    const float y = labels[i] < 0.f ? 0.f : labels[i];
+    const float err = alpha * (y - p);
+    if (delta)
+      for (int64_t j = s0 + lane; j < s1; j += 64) atomicAdd(delta + cols[j], err * vals[j]);
+    if (lane == 0) hits += ((p > 0.5f) == (y > 0.5f)) ? 1.f : 0.f;
+  }
+  if (correct && lane == 0 && hits > 0.f) atomicAdd(correct, hits);
+}
+
+void lr_sparse_step(const int64_t* rowptr, const int64_t* cols, const float* vals, const float* labels, int64_t B,
+                    const float* w, float alpha, float* delta, float* correct, hipStream_t s) {
+  if (B <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(lr_sparse_kernel, grid_for(B * 64, block, 4096), block, 0, s, rowptr, cols, vals, labels, B, w,
+                     alpha, delta, correct);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// One wave per point, centres streamed k at a time; lanes split the dimension.
+__global__ void kmeans_assign_kernel(const float* __restrict__ X, int64_t n, int d, const float* __restrict__ C, int k,
+                                     int32_t* assign, float* dist) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nwaves) {
+    const float* x = X + i * d;
+    float best = 3.4e38f;
+    int besti = 0;
+    for (int c = 0; c < k; ++c) {
+      const float* cc = C + (int64_t)c * d;
+      float acc = 0.f;
+      for (int j = lane; j < d; j += 64) {
+        const float t = x[j] - cc[j];
+        acc += t * t;
+      }
+      acc = warp_sum(acc);
+      if (acc < best) {
+        best = acc;
+        besti = c;
+      }
+    }
+    if (lane == 0) {
+      assign[i] = besti;
+      if (dist) dist[i] = best;
+    }
+  }
+}
+
+void kmeans_assign(const float* X, int64_t n, int d, const float* C, int k, int32_t* assign, float* dist,
+                   hipStream_t s) {
+  if (n <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(kmeans_assign_kernel, grid_for(n * 64, block, 4096), block, 0, s, X, n, d, C, k, assign, dist);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace minips_k

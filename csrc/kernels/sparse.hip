@@ -1,0 +1,292 @@
+// Sparse-table kernels of the GPU parameter server:
+//   K5/K4  unique_bucketize   hash dedupe of a batch's keys + grouping by owner shard
+//   K2     gather_rows        server-side row gather (pull), fp32 -> fp32/bf16
+//   K1     scatter_add_rows   worker-side gradient dedupe (segment sum via float atomics)
+//   K1     sparse_rowwise_adagrad / sparse_sgd   server-side apply on the shard rows
+//          embedding_bag_fwd/bwd                 pooled lookups (DLRM-style bags)
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace minips_k {
+
+constexpr int64_t kEmpty = -1;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ int owner_of(const int64_t* bounds, int P, int64_t key) {
+  // upper_bound over P+1 sorted bounds (P <= a few dozen): linear scan is cheapest.
+  int o = 0;
+  for (int p = 1; p < P; ++p) o += (key >= bounds[p]) ? 1 : 0;
+  return o;
+}
+
+__global__ void ub_insert_kernel(const int64_t* __restrict__ keys, int64_t n, const int64_t* __restrict__ bounds,
+                                 int P, unsigned long long* table_keys, int64_t cap, int64_t* slot, int32_t* flags,
+                                 unsigned long long* counts) {
+  const int64_t mask = cap - 1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t key = keys[i];
+    int64_t h = (int64_t)(mix64((uint64_t)key) & (uint64_t)mask);
+    while (true) {
+      unsigned long long prev = atomicCAS(table_keys + h, (unsigned long long)kEmpty, (unsigned long long)key);
+      if (prev == (unsigned long long)kEmpty) {
+        flags[i] = 1;
+        slot[i] = h;
+        atomicAdd(counts + owner_of(bounds, P, key), 1ULL);
+        break;
+      }
+      if (prev == (unsigned long long)key) {
+        flags[i] = 0;
+        slot[i] = h;
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+}
+
+__global__ void ub_assign_kernel(const int64_t* __restrict__ keys, int64_t n, const int64_t* __restrict__ bounds,
+                                 int P, const int64_t* __restrict__ slot, const int32_t* __restrict__ flags,
+                                 const int64_t* __restrict__ counts, unsigned long long* cursor, int64_t* table_pos,
+                                 int64_t* out_keys) {
+  extern __shared__ int64_t offs[];  // exclusive prefix of counts
+  if (threadIdx.x == 0) {
+    int64_t acc = 0;
+    for (int p = 0; p < P; ++p) {
+      offs[p] = acc;
+      acc += counts[p];
+    }
+  }
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!flags[i]) continue;
+    const int64_t key = keys[i];
+    const int o = owner_of(bounds, P, key);
+    const int64_t pos = offs[o] + (int64_t)atomicAdd(cursor + o, 1ULL);
+    table_pos[slot[i]] = pos;
+    out_keys[pos] = key;
+  }
+}
+
+__global__ void ub_inverse_kernel(int64_t n, const int64_t* __restrict__ slot, const int64_t* __restrict__ table_pos,
+                                  int64_t* inverse) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    inverse[i] = table_pos[slot[i]];
+}
+
+void unique_bucketize(const int64_t* keys, int64_t n, const int64_t* bounds, int P, int64_t* table_keys,
+                      int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
+                      int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s) {
+  if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
+  if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
+  MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0xFF, cap * sizeof(int64_t), s));
+  MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, P * sizeof(int64_t), s));
+  MINIPS_HIP_CHECK(hipMemsetAsync(cursor, 0, P * sizeof(int64_t), s));
+  if (n == 0) return;
+  const int block = 256;
+  const int grid = grid_for(n, block, 4096);
+  hipLaunchKernelGGL(ub_insert_kernel, grid, block, 0, s, keys, n, bounds, P, (unsigned long long*)table_keys, cap,
+                     slot, flags, (unsigned long long*)counts);
+  hipLaunchKernelGGL(ub_assign_kernel, grid, block, P * sizeof(int64_t), s, keys, n, bounds, P, slot, flags, counts,
+                     (unsigned long long*)cursor, table_pos, out_keys);
+  hipLaunchKernelGGL(ub_inverse_kernel, grid, block, 0, s, n, slot, table_pos, inverse);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// --------------------------------------------------------------------------- gather
+template <bool BF16>
+__global__ void gather_rows_vec4(const float* __restrict__ table, int64_t ld, const int64_t* __restrict__ keys,
+                                 int64_t n, int64_t base, int D4, void* out) {
+  const int64_t total = n * D4;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = c / D4;
+    const int d4 = (int)(c - i * D4);
+    const float4 v = *reinterpret_cast<const float4*>(table + (keys[i] - base) * ld + d4 * 4);
+    if (BF16) {
+      uint2 o;
+      o.x = pack_bf2(v.x, v.y);
+      o.y = pack_bf2(v.z, v.w);
+      reinterpret_cast<uint2*>(out)[c] = o;
+    } else {
+      reinterpret_cast<float4*>(out)[c] = v;
+    }
+  }
+}
+
+template <bool BF16>
+__global__ void gather_rows_scalar(const float* __restrict__ table, int64_t ld, const int64_t* __restrict__ keys,
+                                   int64_t n, int64_t base, int D, void* out) {
+  const int64_t total = n * D;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = c / D;
+    const int d = (int)(c - i * D);
+    const float v = table[(keys[i] - base) * ld + d];
+    if (BF16)
+      reinterpret_cast<bf16_t*>(out)[c] = f2bf(v);
+    else
+      reinterpret_cast<float*>(out)[c] = v;
+  }
+}
+
+void gather_rows(const float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, void* out,
+                 bool out_bf16, hipStream_t s) {
+  if (n <= 0) return;
+  const int block = 256;
+  if (D % 4 == 0 && ld % 4 == 0) {
+    const int grid = grid_for(n * (D / 4), block);
+    if (out_bf16)
+      hipLaunchKernelGGL(gather_rows_vec4<true>, grid, block, 0, s, table, ld, keys, n, base, D / 4, out);
+    else
+      hipLaunchKernelGGL(gather_rows_vec4<false>, grid, block, 0, s, table, ld, keys, n, base, D / 4, out);
+  } else {
+    const int grid = grid_for(n * D, block);
+    if (out_bf16)
+      hipLaunchKernelGGL(gather_rows_scalar<true>, grid, block, 0, s, table, ld, keys, n, base, D, out);
+    else
+      hipLaunchKernelGGL(gather_rows_scalar<false>, grid, block, 0, s, table, ld, keys, n, base, D, out);
+  }
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// --------------------------------------------------------------------------- scatter-add
+__global__ void scatter_add_rows_kernel(const float* __restrict__ src, int64_t n, int D,
+                                        const int64_t* __restrict__ idx, float* acc) {
+  const int64_t total = n * D;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = c / D;
+    const int d = (int)(c - i * D);
+    atomicAdd(acc + idx[i] * D + d, src[c]);
+  }
+}
+
+void scatter_add_rows(const float* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s) {
+  if (n <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(scatter_add_rows_kernel, grid_for(n * D, block), block, 0, s, src, n, D, idx, acc);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// --------------------------------------------------------------------------- row-wise adagrad
+// One wave per row-group: lanes stride the row, a wave reduction gives mean(g^2).
+__global__ void sparse_rowwise_adagrad_kernel(float* table, int64_t ld, float* state, float* state2, int D1,
+                                              const int64_t* __restrict__ keys, int64_t n, int64_t base, int D,
+                                              const float* __restrict__ grads, float lr, float eps) {
+  // Columns [0, D1) share accumulator state[row]; columns [D1, D) share state2[row]
+  // (Wide&Deep keeps the deep embedding and the wide weight in one row, each with its own
+  // row-wise Adagrad state).
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nwaves) {
+    const int64_t row = keys[i] - base;
+    float sq1 = 0.f, sq2 = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      float g = grads[i * D + d];
+      if (d < D1) sq1 += g * g; else sq2 += g * g;
+    }
+    sq1 = warp_sum(sq1);
+    const float st1 = state[row] + sq1 / (float)D1;
+    float st2 = 0.f;
+    if (D1 < D) {
+      sq2 = warp_sum(sq2);
+      st2 = state2[row] + sq2 / (float)(D - D1);
+    }
+    if (lane == 0) {
+      state[row] = st1;
+      if (D1 < D) state2[row] = st2;
+    }
+    const float s1 = lr / (sqrtf(st1) + eps);
+    const float s2 = lr / (sqrtf(st2) + eps);
+    for (int d = lane; d < D; d += 64) table[row * ld + d] -= (d < D1 ? s1 : s2) * grads[i * D + d];
+  }
+}
+
+void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
+                            int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s) {
+  if (n <= 0) return;
+  if (D1 <= 0 || D1 > D) D1 = D;
+  if (D1 < D && !state2) throw std::runtime_error("sparse_rowwise_adagrad: split rows need state2");
+  const int block = 256;
+  const int grid = grid_for(n * 64, block, 4096);
+  hipLaunchKernelGGL(sparse_rowwise_adagrad_kernel, grid, block, 0, s, table, ld, state, state2, D1, keys, n, base, D,
+                     grads, lr, eps);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void sparse_sgd_kernel(float* table, int64_t ld, const int64_t* __restrict__ keys, int64_t n, int64_t base,
+                                  int D, const float* __restrict__ grads, float scale) {
+  const int64_t total = n * D;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = c / D;
+    const int d = (int)(c - i * D);
+    table[(keys[i] - base) * ld + d] += scale * grads[c];
+  }
+}
+
+void sparse_sgd(float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, const float* grads,
+                float scale, hipStream_t s) {
+  if (n <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(sparse_sgd_kernel, grid_for(n * D, block), block, 0, s, table, ld, keys, n, base, D, grads, scale);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// --------------------------------------------------------------------------- embedding bag
+__global__ void embedding_bag_fwd_kernel(const float* __restrict__ rows, const int64_t* __restrict__ idx,
+                                         const int64_t* __restrict__ offsets, int64_t B, int D, bool mean,
+                                         float* out) {
+  const int64_t total = B * D;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = c / D;
+    const int d = (int)(c - b * D);
+    const int64_t s0 = offsets[b], s1 = offsets[b + 1];
+    float acc = 0.f;
+    for (int64_t j = s0; j < s1; ++j) acc += rows[idx[j] * D + d];
+    if (mean && s1 > s0) acc /= (float)(s1 - s0);
+    out[c] = acc;
+  }
+}
+
+__global__ void embedding_bag_bwd_kernel(const float* __restrict__ grad_out, const int64_t* __restrict__ idx,
+                                         const int64_t* __restrict__ offsets, int64_t B, int D, bool mean,
+                                         float* grad_rows) {
+  const int64_t total = B * D;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = c / D;
+    const int d = (int)(c - b * D);
+    const int64_t s0 = offsets[b], s1 = offsets[b + 1];
+    float g = grad_out[c];
+    if (mean && s1 > s0) g /= (float)(s1 - s0);
+    for (int64_t j = s0; j < s1; ++j) atomicAdd(grad_rows + idx[j] * D + d, g);
+  }
+}
+
+void embedding_bag_fwd(const float* rows, const int64_t* idx, const int64_t* offsets, int64_t B, int D, bool mean,
+                       float* out, hipStream_t s) {
+  if (B <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(embedding_bag_fwd_kernel, grid_for(B * D, block), block, 0, s, rows, idx, offsets, B, D, mean,
+                     out);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void embedding_bag_bwd(const float* grad_out, const int64_t* idx, const int64_t* offsets, int64_t B, int D, bool mean,
+                       float* grad_rows, hipStream_t s) {
+  if (B <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(embedding_bag_bwd_kernel, grid_for(B * D, block), block, 0, s, grad_out, idx, offsets, B, D,
+                     mean, grad_rows);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace minips_k

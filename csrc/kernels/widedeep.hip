@@ -1,0 +1,172 @@
+// Wide&Deep worker kernels: input assembly (embedding lookup + dense concat + wide sum),
+// the fused output head (Linear Hd->1 + BCE-with-logits forward+backward), and the
+// embedding-gradient scatter into the per-unique-key gradient rows that are pushed to the
+// owning server shards.
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace minips_k {
+
+// One thread per (sample, 8-column chunk): a 16-byte store of 8 bf16.
+__global__ void wd_assemble_kernel(const float* __restrict__ dense, int n_dense, const bf16_t* __restrict__ rows,
+                                   int row_stride, const int64_t* __restrict__ inv, int64_t B, int F, int D,
+                                   bf16_t* __restrict__ X, int ldx, float* __restrict__ wide_logit) {
+  const int chunks = ldx >> 3;
+  const int emb_cols = F * D;
+  const int64_t total = B * chunks;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = c / chunks;
+    const int col0 = (int)(c - b * chunks) * 8;
+    uint32_t packed[4];
+    if (col0 + 8 <= emb_cols && (D & 7) == 0) {
+      // whole chunk inside one embedding: two 8-byte loads of the pulled bf16 row
+      const int f = col0 / D, d = col0 - f * D;
+      const bf16_t* src = rows + inv[b * F + f] * row_stride + d;
+      const uint2 lo = *reinterpret_cast<const uint2*>(src);
+      const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
+      packed[0] = lo.x;
+      packed[1] = lo.y;
+      packed[2] = hi.x;
+      packed[3] = hi.y;
+    } else {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = col0 + j;
+        if (col < emb_cols) {
+          const int f = col / D, d = col - f * D;
+          v[j] = bf2f(rows[inv[b * F + f] * row_stride + d]);
+        } else if (col < emb_cols + n_dense) {
+          v[j] = dense[b * n_dense + (col - emb_cols)];
+        } else {
+          v[j] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) packed[j] = pack_bf2(v[2 * j], v[2 * j + 1]);
+    }
+    *reinterpret_cast<uint4*>(X + b * ldx + col0) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+    if (col0 == 0) {
+      float w = 0.f;
+      for (int f = 0; f < F; ++f) w += bf2f(rows[inv[b * F + f] * row_stride + D]);
+      wide_logit[b] = w;
+    }
+  }
+}
+
+void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B,
+                 int F, int D, bf16_t* X, int ldx, float* wide_logit, hipStream_t s) {
+  if (ldx % 8) throw std::runtime_error("wd_assemble: ldx must be a multiple of 8");
+  if (F * D + n_dense > ldx) throw std::runtime_error("wd_assemble: ldx too small");
+  if (row_stride % 4) throw std::runtime_error("wd_assemble: row_stride must be a multiple of 4");
+  if (B <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(wd_assemble_kernel, grid_for(B * (ldx / 8), block, 8192), block, 0, s, dense, n_dense, rows,
+                     row_stride, inv, B, F, D, X, ldx, wide_logit);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// One wave per sample (grid-stride); each lane owns Hd/64 columns and keeps its dw / colsum
+// partials in registers across all samples it visits: one atomic per lane per column at the end.
+template <int PER_LANE>
+__global__ __launch_bounds__(256) void wd_head_kernel(const bf16_t* __restrict__ H, int64_t B, int Hd,
+                                                      const bf16_t* __restrict__ w, const bf16_t* __restrict__ b0,
+                                                      const float* __restrict__ wide, const float* __restrict__ y,
+                                                      bf16_t* __restrict__ dH, float* dw, float* db, float* dwide,
+                                                      float* loss_sum, float* colsum, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  float wl[PER_LANE], dwl[PER_LANE], csl[PER_LANE];
+#pragma unroll
+  for (int j = 0; j < PER_LANE; ++j) {
+    wl[j] = bf2f(w[lane * PER_LANE + j]);
+    dwl[j] = 0.f;
+    csl[j] = 0.f;
+  }
+  const float bias = bf2f(b0[0]);
+  float dbl = 0.f, lossl = 0.f;
+  for (int64_t b = wave; b < B; b += nwaves) {
+    float h[PER_LANE];
+    const bf16_t* hp = H + b * Hd + lane * PER_LANE;
+#pragma unroll
+    for (int j = 0; j < PER_LANE; ++j) h[j] = bf2f(hp[j]);
+    float z = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER_LANE; ++j) z += h[j] * wl[j];
+    z = warp_sum(z) + bias + wide[b];
+    const float label = y[b] > 0.5f ? 1.f : 0.f;
+    const float p = sigmoidf_(z);
+    const float dz = (p - label) * scale;
+    if (lane == 0) {
+      dwide[b] = dz;
+      dbl += dz;
+      lossl += fmaxf(z, 0.f) - z * label + log1pf(__expf(-fabsf(z)));
+    }
+    bf16_t* dp = dH + b * Hd + lane * PER_LANE;
+#pragma unroll
+    for (int j = 0; j < PER_LANE; ++j) {
+      dwl[j] += dz * h[j];
+      const bf16_t g = f2bf(h[j] > 0.f ? dz * wl[j] : 0.f);
+      dp[j] = g;
+      csl[j] += bf2f(g);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER_LANE; ++j) {
+    atomicAdd(dw + lane * PER_LANE + j, dwl[j]);
+    if (colsum) atomicAdd(colsum + lane * PER_LANE + j, csl[j]);
+  }
+  if (lane == 0) {
+    atomicAdd(db, dbl);
+    atomicAdd(loss_sum, lossl);
+  }
+}
+
+void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
+             const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
+             float grad_scale, hipStream_t s) {
+  if (B <= 0) return;
+  const int block = 256;
+  const int grid = (int)std::min<int64_t>(256, (B + 3) / 4);
+  switch (Hd) {
+    case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+    case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+    case 64 * 4: hipLaunchKernelGGL(wd_head_kernel<4>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+    case 64 * 8: hipLaunchKernelGGL(wd_head_kernel<8>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+    default: throw std::runtime_error("wd_head: Hd must be 64, 128, 256 or 512, got " + std::to_string(Hd));
+  }
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// One thread per (sample, feature, column): consecutive lanes add consecutive columns of a
+// row, so each wave-instruction is two contiguous 128-B row segments at D = 32 (the
+// full-rate float-atomic shape on gfx950).
+__global__ void wd_emb_backward_kernel(const float* __restrict__ dX, int ldx, const float* __restrict__ dwide,
+                                       const int64_t* __restrict__ inv, int64_t B, int F, int D,
+                                       float* __restrict__ grad_rows, int row_stride) {
+  const int64_t total = B * F * D;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bf = c / D;
+    const int d = (int)(c - bf * D);
+    const int64_t b = bf / F;
+    const int f = (int)(bf - b * F);
+    const int64_t row = inv[bf];
+    atomicAdd(grad_rows + row * row_stride + d, dX[b * ldx + f * D + d]);
+    if (d == 0) atomicAdd(grad_rows + row * row_stride + D, dwide[b]);
+  }
+}
+
+void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
+                     float* grad_rows, int row_stride, hipStream_t s) {
+  if (B <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(wd_emb_backward_kernel, grid_for(B * F * D, block, 8192), block, 0, s, dX, ldx, dwide, inv, B, F,
+                     D, grad_rows, row_stride);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace minips_k

@@ -1,0 +1,110 @@
+"""Synthetic data generators shaped like the BASELINE configs (no datasets are downloadable).
+
+* Criteo-shaped click logs (Wide&Deep / DLRM): 13 dense features ~ N(0,1), 26 categorical
+  features with the Criteo-Kaggle cardinalities; ids are drawn log-uniformly (a Zipf(1)-like
+  head: P(id <= k) = ln(k+1)/ln(card)) and scattered by a bijective multiplicative hash so the
+  hot ids spread over all server shards. Labels are a noisy function of the features, so the
+  loss decreases during training.
+* MNIST-shaped dense batches (784 -> 10 classes), GPT-2 token batches, webspam-shaped sparse
+  LR batches (16.6M feature ids, libsvm-like nnz per row).
+All generation happens on the target device with a torch.Generator (deterministic per rank).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+# Criteo Kaggle (display advertising challenge) per-feature cardinalities.
+CRITEO_KAGGLE_CARDS = [
+    1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194, 27, 14992,
+    5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572,
+]
+_HASH_PRIME = 2654435761  # prime: multiplication mod card is a bijection unless card % prime == 0
+
+
+class CriteoSynth:
+    def __init__(self, batch: int, cards=None, n_dense: int = 13, device="cpu", seed: int = 0,
+                 hot_alpha: float = 1.0):
+        self.batch = batch
+        self.cards = list(cards or CRITEO_KAGGLE_CARDS)
+        self.F = len(self.cards)
+        self.n_dense = n_dense
+        self.device = torch.device(device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self.offsets = torch.tensor([0] + list(_cumsum(self.cards))[:-1], dtype=torch.int64, device=self.device)
+        self.card_t = torch.tensor(self.cards, dtype=torch.int64, device=self.device)
+        self.log_card = torch.log(self.card_t.to(torch.float64) + 1.0)
+        self.num_rows = int(sum(self.cards))
+        self.hot_alpha = hot_alpha
+        self.w_dense = torch.randn(n_dense, generator=self.gen, device=self.device) / math.sqrt(n_dense)
+
+    def next(self):
+        B, F = self.batch, self.F
+        u = torch.rand(B, F, generator=self.gen, device=self.device, dtype=torch.float64)
+        raw = torch.floor(torch.exp(u * self.log_card) - 1.0).to(torch.int64)
+        raw = torch.minimum(raw, self.card_t - 1).clamp_min(0)
+        ids = (raw * _HASH_PRIME) % self.card_t
+        keys = ids + self.offsets
+        dense = torch.randn(B, self.n_dense, generator=self.gen, device=self.device)
+        logit = dense @ self.w_dense + 0.5 * ((raw[:, :4] % 2).sum(1).float() - 1.0)
+        noise = torch.rand(B, generator=self.gen, device=self.device)
+        labels = (torch.sigmoid(2.0 * logit) > noise).float()
+        return dense, keys, labels
+
+
+def _cumsum(xs):
+    s = 0
+    for x in xs:
+        s += x
+        yield s
+
+
+class MnistSynth:
+    """784-dim inputs in [0,1) and 10-class labels from a fixed random linear teacher."""
+
+    def __init__(self, batch: int, device="cpu", seed: int = 0, dim: int = 784, classes: int = 10):
+        self.batch, self.dim, self.classes = batch, dim, classes
+        self.device = torch.device(device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self.teacher = torch.randn(dim, classes, generator=self.gen, device=self.device)
+
+    def next(self):
+        x = torch.rand(self.batch, self.dim, generator=self.gen, device=self.device)
+        y = torch.argmax(x @ self.teacher, dim=1)
+        return x, y
+
+
+class TokenSynth:
+    """GPT-2 token batches: [B, T+1] uniform ids (inputs = [:, :-1], targets = [:, 1:])."""
+
+    def __init__(self, batch: int, seq: int, vocab: int = 50257, device="cpu", seed: int = 0):
+        self.batch, self.seq, self.vocab = batch, seq, vocab
+        self.device = torch.device(device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+
+    def next(self):
+        t = torch.randint(0, self.vocab, (self.batch, self.seq + 1), generator=self.gen, device=self.device)
+        return t[:, :-1].contiguous(), t[:, 1:].contiguous()
+
+
+class SparseLRSynth:
+    """webspam-shaped sparse LR: `num_dims` features, ~nnz ids per row, linear teacher labels."""
+
+    def __init__(self, batch: int, num_dims: int = 16_609_143, nnz: int = 64, device="cpu", seed: int = 0):
+        self.batch, self.num_dims, self.nnz = batch, num_dims, nnz
+        self.device = torch.device(device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+
+    def next(self):
+        B, k = self.batch, self.nnz
+        cols = torch.randint(0, self.num_dims, (B, k), generator=self.gen, device=self.device)
+        vals = torch.rand(B, k, generator=self.gen, device=self.device)
+        teacher = ((cols * _HASH_PRIME) % 7).float() - 3.0
+        y = ((teacher * vals).sum(1) > 0).float()
+        rowptr = torch.arange(0, (B + 1) * k, k, device=self.device, dtype=torch.int64)
+        return rowptr, cols.reshape(-1), vals.reshape(-1), y

@@ -1,0 +1,173 @@
+"""Wide&Deep on Criteo-shaped data over the GPU parameter server (BASELINE config 3 and the
+north-star benchmark).
+
+Parameters
+  sparse table  one row per categorical id (sum of the 26 cardinalities, 33.8M rows):
+                [32-dim deep embedding | 1 wide weight | 3 pad], row-wise Adagrad with a
+                separate accumulator for the deep part and for the wide weight.
+  dense table   deep tower Linear(848->1024)->ReLU->Linear(1024->512)->ReLU->
+                Linear(512->256)->ReLU->Linear(256->1), one flat fp32 master vector, Adam.
+Step (every kernel is a gfx950 HIP kernel; comm is RCCL):
+  sparse Get -> wd_assemble (lookup + dense concat + wide sum) -> 3 MFMA GEMMs (bias+ReLU
+  fused) -> wd_head (last layer + BCE fwd/bwd fused) -> per layer wgrad GEMM (split-K) +
+  dgrad GEMM (ReLU mask + bias-grad colsum fused) -> wd_emb_backward (segment sum into unique
+  rows) -> sparse Add + dense Add -> Clock (all-to-all / reduce-scatter, fused optimizers,
+  all-gather).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from ..ps.comm import Comm
+from ..ps.tables import DenseTable, SparseTable
+
+
+@dataclass
+class WideDeepConfig:
+    cards: list = field(default_factory=lambda: list(__import__(
+        "minips_amd.data.synthetic", fromlist=["CRITEO_KAGGLE_CARDS"]).CRITEO_KAGGLE_CARDS))
+    n_dense: int = 13
+    emb_dim: int = 32
+    row_width: int = 36          # 32 deep + 1 wide + 3 pad (16-byte rows)
+    hidden: tuple = (1024, 512, 256)
+    lr_dense: float = 1e-3
+    lr_sparse: float = 0.02
+    consistency: str = "bsp"
+    staleness: int = 0
+    seed: int = 0
+
+    @property
+    def F(self):
+        return len(self.cards)
+
+    @property
+    def in_dim(self):
+        k = self.F * self.emb_dim + self.n_dense
+        return (k + 7) // 8 * 8
+
+
+def _align(n, a=8):
+    return (n + a - 1) // a * a
+
+
+class WideDeep:
+    def __init__(self, cfg: WideDeepConfig, comm: Comm):
+        self.cfg = cfg
+        self.comm = comm
+        dev = comm.device
+        F, D = cfg.F, cfg.emb_dim
+        self.num_rows = int(sum(cfg.cards))
+        self.emb = SparseTable(comm, self.num_rows, cfg.row_width, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
+                               consistency=cfg.consistency, staleness=cfg.staleness, split=D, table_id=0,
+                               init_std=0.01, seed=cfg.seed)
+        # wide weights start at zero (columns >= D)
+        self.emb.shard[:, D:].zero_()
+        # dense layout: [W1 b1 W2 b2 W3 b3 w4 b4], every segment 8-element aligned
+        dims = [cfg.in_dim, *cfg.hidden]
+        self.layout = {}
+        off = 0
+        for i in range(len(cfg.hidden)):
+            n_out, n_in = dims[i + 1], dims[i]
+            self.layout[f"W{i + 1}"] = (off, (n_out, n_in))
+            off += _align(n_out * n_in)
+            self.layout[f"b{i + 1}"] = (off, (n_out,))
+            off += _align(n_out)
+        self.layout["w4"] = (off, (cfg.hidden[-1],))
+        off += _align(cfg.hidden[-1])
+        self.layout["b4"] = (off, (1,))
+        off += 8
+        self.n_params = off
+        self.dense = DenseTable(comm, self.n_params, optimizer="adam", lr=cfg.lr_dense,
+                                consistency=cfg.consistency, staleness=cfg.staleness, table_id=1)
+        self.dense.load_full(self._init_dense(dev))
+        self._bufs = {}
+
+    def _init_dense(self, dev):
+        g = torch.Generator(device="cpu")
+        g.manual_seed(self.cfg.seed + 17)
+        full = torch.zeros(self.n_params, dtype=torch.float32)
+        dims = [self.cfg.in_dim, *self.cfg.hidden]
+        for i in range(len(self.cfg.hidden)):
+            off, shape = self.layout[f"W{i + 1}"]
+            w = full[off: off + shape[0] * shape[1]].view(shape)
+            ops.kaiming_uniform_(w, dims[i], g)
+            if i == 0:  # padded input columns carry no signal
+                w[:, self.cfg.F * self.cfg.emb_dim + self.cfg.n_dense:] = 0
+        off, shape = self.layout["w4"]
+        ops.kaiming_uniform_(full[off: off + shape[0]], shape[0], g)
+        return full.to(dev)
+
+    def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        off, shape = self.layout[name]
+        n = 1
+        for s in shape:
+            n *= s
+        return buf[off: off + n].view(shape)
+
+    def _buffers(self, B):
+        if B not in self._bufs:
+            dev, cfg = self.comm.device, self.cfg
+            bf = dict(dtype=torch.bfloat16, device=dev)
+            h1, h2, h3 = cfg.hidden
+            self._bufs[B] = dict(
+                X=torch.empty(B, cfg.in_dim, **bf), H1=torch.empty(B, h1, **bf), H2=torch.empty(B, h2, **bf),
+                H3=torch.empty(B, h3, **bf), dH3=torch.empty(B, h3, **bf), dH2=torch.empty(B, h2, **bf),
+                dH1=torch.empty(B, h1, **bf),
+                dX=torch.empty(B, cfg.F * cfg.emb_dim, dtype=torch.float32, device=dev),
+                wide=torch.empty(B, dtype=torch.float32, device=dev),
+                dwide=torch.empty(B, dtype=torch.float32, device=dev),
+                loss=torch.zeros(1, dtype=torch.float32, device=dev),
+            )
+        return self._bufs[B]
+
+    def forward(self, dense, keys, rows, plan):
+        """Forward only (eval): returns logits [B] fp32."""
+        B = dense.shape[0]
+        b = self._buffers(B)
+        P = self.dense.get()
+        F, D = self.cfg.F, self.cfg.emb_dim
+        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"])
+        x = b["X"]
+        for i, h in enumerate(("H1", "H2", "H3")):
+            ops.linear_fwd(x, self.view(P, f"W{i + 1}"), self.view(P, f"b{i + 1}"), "relu", out=b[h])
+            x = b[h]
+        return x.float() @ self.view(P, "w4").float() + self.view(P, "b4").float() + b["wide"]
+
+    def train_step(self, dense, keys, labels) -> torch.Tensor:
+        """One BSP superstep: Get, forward, backward, Add, Clock. Returns the summed loss
+        (a device tensor; no host sync)."""
+        cfg = self.cfg
+        B = dense.shape[0]
+        F, D = cfg.F, cfg.emb_dim
+        b = self._buffers(B)
+        rows, plan = self.emb.get(keys)
+        P = self.dense.get()
+        G = self.dense.grad
+        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"])
+        ops.linear_fwd(b["X"], self.view(P, "W1"), self.view(P, "b1"), "relu", out=b["H1"])
+        ops.linear_fwd(b["H1"], self.view(P, "W2"), self.view(P, "b2"), "relu", out=b["H2"])
+        ops.linear_fwd(b["H2"], self.view(P, "W3"), self.view(P, "b3"), "relu", out=b["H3"])
+        b["loss"].zero_()
+        scale = 1.0 / (B * self.comm.world)
+        ops.wd_head(b["H3"], self.view(P, "w4"), self.view(P, "b4"), b["wide"], labels, b["dH3"],
+                    self.view(G, "w4"), self.view(G, "b4"), b["dwide"], b["loss"], self.view(G, "b3"), scale)
+        ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
+        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], colsum=self.view(G, "b2"), out=b["dH2"])
+        ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
+        ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], colsum=self.view(G, "b1"), out=b["dH1"])
+        ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
+        ops.linear_dgrad(b["dH1"], self.view(P, "W1"), out_f32=True, n_cols=F * D, out=b["dX"])
+        grad_rows = torch.zeros(max(plan.U, 1), cfg.row_width, dtype=torch.float32, device=self.comm.device)
+        ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows)
+        self.emb.add(plan, grad_rows)
+        self.dense.add()
+        self.emb.clock()
+        self.dense.clock()
+        return b["loss"]
+
+    def drain(self):
+        self.emb.drain()
+        self.dense.drain()

@@ -1,0 +1,305 @@
+"""Data-plane ops of minips_amd.
+
+Every op has ONE device implementation: GPU tensors go to the hand-written gfx950 HIP
+kernels in ``minips_amd._kernels`` (and raise if that extension is missing -- there is no
+silent eager fallback on a GPU). CPU tensors run a plain PyTorch reference of the same math;
+that path exists for the CPU/gloo plumbing configuration (BASELINE config 1) and as the fp32
+oracle the GPU numerics tests compare against.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .._native import kernels
+
+EPI_STORE_F32 = 0
+EPI_ATOMIC_F32 = 1
+EPI_BIAS_RELU_BF16 = 2
+EPI_BIAS_BF16 = 3
+EPI_STORE_BF16 = 4
+EPI_RELU_MASK_BF16 = 5
+EPI_BIAS_GELU_BF16 = 6
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None, mask=None, colsum=None,
+         alpha=1.0, split_k=1):
+    """C[M,N] (op)= A.B.  A is [M][K] (a_km=False) or [K][M]; B is [N][K] (b_kn=False) or [K][N]."""
+    if _gpu(A):
+        kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k))
+        return C
+    a = (A[:K, :M].t() if a_km else A[:M, :K]).float()
+    b = (B[:K, :N] if b_kn else B[:N, :K].t()).float()
+    acc = (a @ b) * alpha
+    if epi == EPI_STORE_F32:
+        C[:M, :N] = acc
+    elif epi == EPI_ATOMIC_F32:
+        C[:M, :N] += acc
+    elif epi in (EPI_BIAS_RELU_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU_BF16):
+        if bias is not None:
+            acc = acc + bias[:N].float()
+        if epi == EPI_BIAS_RELU_BF16:
+            acc = torch.relu(acc)
+        elif epi == EPI_BIAS_GELU_BF16:
+            acc = torch.nn.functional.gelu(acc, approximate="tanh")
+        C[:M, :N] = acc.to(torch.bfloat16)
+    elif epi == EPI_STORE_BF16:
+        C[:M, :N] = acc.to(torch.bfloat16)
+    elif epi == EPI_RELU_MASK_BF16:
+        out = torch.where(mask[:M, :N].float() > 0, acc, torch.zeros_like(acc)).to(torch.bfloat16)
+        C[:M, :N] = out
+        if colsum is not None:
+            colsum[:N] += out.float().sum(0)
+    else:
+        raise ValueError(f"unknown epilogue {epi}")
+    return C
+
+
+def linear_fwd(x, w, bias=None, act="relu", out=None):
+    """y = act(x w^T + b) in bf16 (x [M,K], w [N,K])."""
+    M, K = x.shape[0], w.shape[1]
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    epi = {"relu": EPI_BIAS_RELU_BF16, "none": EPI_BIAS_BF16, "gelu": EPI_BIAS_GELU_BF16}[act]
+    return gemm(x, w, out, M, N, K, False, False, epi, bias=bias)
+
+
+def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=None):
+    """dx = dy w (dy [M,N], w [N,K]) -> bf16 masked by (mask > 0) (+colsum), or fp32."""
+    M, N = dy.shape
+    K = w.shape[1] if n_cols is None else n_cols
+    if out is None:
+        out = torch.empty(M, K, dtype=torch.float32 if out_f32 else torch.bfloat16, device=dy.device)
+    epi = EPI_STORE_F32 if out_f32 else (EPI_RELU_MASK_BF16 if mask is not None else EPI_STORE_BF16)
+    return gemm(dy, w, out, M, K, N, False, True, epi, mask=mask, colsum=colsum)
+
+
+def linear_wgrad(dy, x, dw, split_k=None):
+    """dw[N,K] += dy^T x (dy [M,N], x [M,K]); fp32 accumulate."""
+    M, N = dy.shape
+    K = x.shape[1]
+    if split_k is None:
+        tiles = ((N + 127) // 128) * ((K + 127) // 128)
+        split_k = max(1, min(M // 256, (512 + tiles - 1) // tiles))
+    return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
+
+
+# ----------------------------------------------------------------------------- sparse keys
+def unique_bucketize(keys: torch.Tensor, bounds: torch.Tensor):
+    """Dedupe ``keys`` and group the unique keys by owner shard.
+
+    Returns (uniq [n] with the first sum(counts) valid, inverse [n], counts [P]) where
+    ``bounds`` [P+1] are the shard key boundaries and uniq[inverse[i]] == keys[i].
+    """
+    if _gpu(keys):
+        uniq, inv, counts = kernels().unique_bucketize(keys.contiguous(), bounds.contiguous())
+        return uniq, inv, counts
+    u, inv = torch.unique(keys, sorted=True, return_inverse=True)
+    owner = torch.bucketize(u, bounds[1:-1], right=True)
+    counts = torch.bincount(owner, minlength=bounds.numel() - 1)
+    # sorted unique keys are already grouped by owner (ranges are contiguous)
+    out = torch.empty_like(keys)
+    out[: u.numel()] = u
+    return out, inv, counts
+
+
+def gather_rows(table, keys, base, out):
+    if _gpu(keys):
+        kernels().gather_rows(table, keys, int(base), out)
+        return out
+    rows = table[(keys - base), : out.shape[1]]
+    out[: keys.numel()] = rows.to(out.dtype)
+    return out
+
+
+def scatter_add_rows(src, idx, acc):
+    if _gpu(src):
+        kernels().scatter_add_rows(src, idx, acc)
+        return acc
+    acc.index_add_(0, idx, src)
+    return acc
+
+
+def sparse_rowwise_adagrad(table, state, keys, base, grads, lr, eps=1e-8, state2=None, split=None):
+    D = grads.shape[1]
+    D1 = D if split is None else split
+    if _gpu(table):
+        kernels().sparse_rowwise_adagrad(table, state, state2, D1, keys, int(base), grads, float(lr), float(eps))
+        return
+    rows = keys - base
+    g1 = grads[:, :D1]
+    s1 = state[rows] + (g1 * g1).mean(1)
+    state[rows] = s1
+    table[rows, :D1] -= lr * g1 / (s1.sqrt() + eps).unsqueeze(1)
+    if D1 < D:
+        g2 = grads[:, D1:]
+        s2 = state2[rows] + (g2 * g2).mean(1)
+        state2[rows] = s2
+        table[rows, D1:D] -= lr * g2 / (s2.sqrt() + eps).unsqueeze(1)
+
+
+def sparse_sgd(table, keys, base, grads, scale):
+    if _gpu(table):
+        kernels().sparse_sgd(table, keys, int(base), grads, float(scale))
+        return
+    table.index_add_(0, keys - base, scale * grads, alpha=1.0) if grads.shape[1] == table.shape[1] else \
+        table[:, : grads.shape[1]].index_add_(0, keys - base, scale * grads)
+
+
+def embedding_bag_fwd(rows, idx, offsets, mean=False, out=None):
+    B = offsets.numel() - 1
+    if out is None:
+        out = torch.empty(B, rows.shape[1], dtype=torch.float32, device=rows.device)
+    if _gpu(rows):
+        kernels().embedding_bag_fwd(rows, idx, offsets, bool(mean), out)
+        return out
+    mode = "mean" if mean else "sum"
+    out.copy_(torch.nn.functional.embedding_bag(idx, rows, offsets[:-1], mode=mode, include_last_offset=False))
+    return out
+
+
+def embedding_bag_bwd(grad_out, idx, offsets, grad_rows, mean=False):
+    if _gpu(grad_out):
+        kernels().embedding_bag_bwd(grad_out, idx, offsets, bool(mean), grad_rows)
+        return grad_rows
+    lens = (offsets[1:] - offsets[:-1])
+    bag = torch.repeat_interleave(torch.arange(lens.numel(), device=idx.device), lens)
+    g = grad_out[bag]
+    if mean:
+        g = g / lens[bag].clamp_min(1).unsqueeze(1).to(g.dtype)
+    grad_rows.index_add_(0, idx, g)
+    return grad_rows
+
+
+# ----------------------------------------------------------------------------- Wide&Deep
+def wd_assemble(dense, rows, inv, F, D, X, wide_logit):
+    """X = [emb_0..emb_{F-1} | dense | 0-pad] (bf16); wide_logit[b] = sum_f rows[inv, D]."""
+    if _gpu(X):
+        kernels().wd_assemble(dense, rows, inv, int(F), int(D), X, wide_logit)
+        return X, wide_logit
+    B = X.shape[0]
+    r = rows[inv].view(B, F, rows.shape[1]).float()
+    X.zero_()
+    X[:, : F * D] = r[:, :, :D].reshape(B, F * D).to(torch.bfloat16)
+    X[:, F * D: F * D + dense.shape[1]] = dense.to(torch.bfloat16)
+    wide_logit.copy_(r[:, :, D].sum(1))
+    return X, wide_logit
+
+
+def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum=None, grad_scale=1.0):
+    if _gpu(H):
+        kernels().wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, float(grad_scale))
+        return
+    h = H.float()
+    z = h @ w.float() + b0.float() + wide_logit
+    y = (labels > 0.5).float()
+    p = torch.sigmoid(z)
+    dz = (p - y) * grad_scale
+    dwide.copy_(dz)
+    db += dz.sum()
+    loss_sum += (torch.clamp_min(z, 0) - z * y + torch.log1p(torch.exp(-z.abs()))).sum()
+    g = torch.where(h > 0, dz.unsqueeze(1) * w.float().unsqueeze(0), torch.zeros_like(h)).to(torch.bfloat16)
+    dH.copy_(g)
+    dw += (dz.unsqueeze(1) * h).sum(0)
+    if dH_colsum is not None:
+        dH_colsum += g.float().sum(0)
+
+
+def wd_emb_backward(dX, dwide, inv, F, D, grad_rows):
+    if _gpu(dX):
+        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows)
+        return grad_rows
+    B = dX.shape[0]
+    g = dX[:, : F * D].reshape(B * F, D)
+    grad_rows[:, :D].index_add_(0, inv, g)
+    grad_rows[:, D].index_add_(0, inv, dwide.repeat_interleave(F))
+    return grad_rows
+
+
+# ----------------------------------------------------------------------------- optimizers
+def adam_apply(w, m, v, g, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=1, grad_scale=1.0,
+               w_bf16=None):
+    if _gpu(w):
+        kernels().adam_apply(w, m, v, g, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+                             int(step), float(grad_scale), w_bf16)
+        return
+    gg = g * grad_scale
+    m.mul_(beta1).add_((1 - beta1) * gg)
+    v.mul_(beta2).add_((1 - beta2) * gg * gg)
+    bc1, bc2 = 1 - beta1 ** step, 1 - beta2 ** step
+    w.sub_(lr * ((m / bc1) / ((v / bc2).sqrt() + eps) + weight_decay * w))
+    if w_bf16 is not None:
+        w_bf16.copy_(w.to(torch.bfloat16))
+
+
+def sgd_apply(w, g, lr, grad_scale=1.0, w_bf16=None):
+    if _gpu(w):
+        kernels().sgd_apply(w, g, float(lr), float(grad_scale), w_bf16)
+        return
+    w.sub_(lr * grad_scale * g)
+    if w_bf16 is not None:
+        w_bf16.copy_(w.to(torch.bfloat16))
+
+
+def adagrad_apply(w, acc, g, lr, eps=1e-10, grad_scale=1.0, w_bf16=None):
+    if _gpu(w):
+        kernels().adagrad_apply(w, acc, g, float(lr), float(eps), float(grad_scale), w_bf16)
+        return
+    gg = g * grad_scale
+    acc.add_(gg * gg)
+    w.sub_(lr * gg / (acc.sqrt() + eps))
+    if w_bf16 is not None:
+        w_bf16.copy_(w.to(torch.bfloat16))
+
+
+def cast_f32_bf16(x, y):
+    if _gpu(x):
+        kernels().cast_f32_bf16(x, y)
+        return y
+    y.copy_(x.to(torch.bfloat16))
+    return y
+
+
+# ----------------------------------------------------------------------------- LR / K-Means
+def lr_sparse_step(rowptr, cols, vals, labels, w, alpha, delta=None, correct=None):
+    """Sparse LR gradient (lr_example.cpp:291-312): delta[col] += alpha*x*(y - sigmoid(w.x))."""
+    if _gpu(w):
+        kernels().lr_sparse_step(rowptr, cols, vals, labels, w, float(alpha), delta, correct)
+        return
+    B = labels.numel()
+    lens = rowptr[1:] - rowptr[:-1]
+    row = torch.repeat_interleave(torch.arange(B, device=w.device), lens)
+    dot = torch.zeros(B, dtype=w.dtype, device=w.device).index_add_(0, row, w[cols] * vals)
+    p = torch.sigmoid(dot)
+    y = labels.clamp_min(0)
+    err = alpha * (y - p)
+    if delta is not None:
+        delta.index_add_(0, cols, err[row] * vals)
+    if correct is not None:
+        correct += ((p > 0.5) == (y > 0.5)).float().sum()
+
+
+def kmeans_assign(X, C, assign=None, dist=None):
+    if assign is None:
+        assign = torch.empty(X.shape[0], dtype=torch.int32, device=X.device)
+    if _gpu(X):
+        kernels().kmeans_assign(X, C, assign, dist)
+        return assign
+    d = torch.cdist(X.double(), C.double()) ** 2
+    best, idx = d.min(1)
+    assign.copy_(idx.to(torch.int32))
+    if dist is not None:
+        dist.copy_(best.to(dist.dtype))
+    return assign
+
+
+def kaiming_uniform_(w: torch.Tensor, fan_in: int, gen=None):
+    bound = 1.0 / math.sqrt(fan_in)
+    return w.uniform_(-bound, bound, generator=gen)

@@ -1,0 +1,124 @@
+"""Collective helpers of the GPU data plane (RCCL over xGMI; gloo on CPU for tests).
+
+The PS message patterns map onto collectives:
+  C1/C2 sparse Get      -> all-to-all(counts) + all-to-all-v(keys) + all-to-all-v(rows)
+  C3    sparse Add      -> all-to-all-v(grad rows) into the owner shards
+  C1/C3 dense Get/Add   -> reduce-scatter(grads) / all-gather(params) of equal shards
+  C6    Barrier         -> 1-element all-reduce on the group
+With one rank every collective degenerates to a local copy (no RCCL launch at all).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class CommStats:
+    bytes_a2a: int = 0
+    bytes_rs: int = 0
+    bytes_ag: int = 0
+    calls: int = 0
+
+    def as_dict(self):
+        return dict(bytes_a2a=self.bytes_a2a, bytes_rs=self.bytes_rs, bytes_ag=self.bytes_ag, calls=self.calls)
+
+
+class Comm:
+    """Rank/world/device bookkeeping plus the collectives used by the tables."""
+
+    def __init__(self, group=None, device: torch.device | None = None):
+        self.initialized = dist.is_available() and dist.is_initialized()
+        self.group = group
+        self.rank = dist.get_rank(group) if self.initialized else 0
+        self.world = dist.get_world_size(group) if self.initialized else 1
+        self.backend = dist.get_backend(group) if self.initialized else "none"
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+        self.device = device
+        self.stats = CommStats()
+
+    # -- helpers ------------------------------------------------------------------------
+    def all_to_all_v(self, out: torch.Tensor, inp: torch.Tensor, recv_splits: list[int], send_splits: list[int]):
+        """Rows of ``inp`` split by ``send_splits`` go to ranks 0..P-1; ``out`` gets recv_splits."""
+        self.stats.calls += 1
+        if self.world == 1:
+            n = send_splits[0]
+            if n:
+                out[:n].copy_(inp[:n])
+            return out
+        self.stats.bytes_a2a += inp[: sum(send_splits)].numel() * inp.element_size()
+        o = out[: sum(recv_splits)]
+        i = inp[: sum(send_splits)]
+        dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
+        return out
+
+    def exchange_counts(self, counts: torch.Tensor) -> tuple[list[int], list[int]]:
+        """all-to-all of per-destination counts; returns (send, recv) as host lists (1 sync)."""
+        if self.world == 1:
+            c = counts.tolist()
+            return c, c
+        recv = torch.empty_like(counts)
+        dist.all_to_all_single(recv, counts, group=self.group)
+        both = torch.stack([counts, recv]).cpu()
+        return both[0].tolist(), both[1].tolist()
+
+    def reduce_scatter(self, out_shard: torch.Tensor, inp: torch.Tensor):
+        self.stats.calls += 1
+        if self.world == 1:
+            out_shard.copy_(inp)
+            return out_shard
+        self.stats.bytes_rs += inp.numel() * inp.element_size()
+        dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
+        return out_shard
+
+    def all_gather(self, out_full: torch.Tensor, shard: torch.Tensor):
+        self.stats.calls += 1
+        if self.world == 1:
+            if out_full.data_ptr() != shard.data_ptr():
+                out_full.copy_(shard)
+            return out_full
+        self.stats.bytes_ag += out_full.numel() * out_full.element_size()
+        if self.backend == "gloo" and shard.data_ptr() >= out_full.data_ptr() and \
+                shard.data_ptr() < out_full.data_ptr() + out_full.numel() * out_full.element_size():
+            shard = shard.clone()  # gloo does not support the in-place (aliased) form
+        dist.all_gather_into_tensor(out_full, shard, group=self.group)
+        return out_full
+
+    def all_reduce_(self, t: torch.Tensor, op=None):
+        if self.world == 1:
+            return t
+        dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def barrier(self):
+        if self.world == 1:
+            return
+        t = torch.zeros(1, device=self.device)
+        dist.all_reduce(t, group=self.group)
+        if t.is_cuda:
+            torch.cuda.synchronize(self.device)
+
+
+def init_distributed(backend: str | None = None) -> Comm:
+    """Initialise torch.distributed from the torchrun env (RANK/WORLD_SIZE/MASTER_*).
+
+    One process per GPU: the local rank selects the device; backend "nccl" is RCCL on ROCm.
+    """
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    return Comm()

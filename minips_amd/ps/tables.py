@@ -1,0 +1,325 @@
+"""GPU parameter-server tables: the KV Get/Add/Clock API over RCCL collectives.
+
+Each rank (one process per MI355X) is both a worker and the server of one equal key range
+of every table; shards live in that GPU's HBM.
+
+DenseTable  (flat fp32 master, equal shards)     reference: VectorStorage + BSPModel
+  get()    -> full parameter vector in the pull dtype (bf16 by default)
+  add(g)   -> gradients accumulate into the local fp32 buffer (BSP: invisible until Clock)
+  clock()  -> reduce-scatter(grad) -> fused optimizer on the owned shard -> all-gather
+              (the all-gather IS the next pull, so Gets after a Clock see the new values;
+              Gets before it see the start-of-superstep values: bsp_model.cpp:14-56)
+
+SparseTable (row table, equal key ranges)        reference: MapStorage/VectorStorage rows
+  get(keys)        -> hash dedupe + owner bucketing (HIP), all-to-all of counts and keys,
+                      owner row gather (HIP), all-to-all of rows back
+  add(plan, grads) -> buffered per-unique-key gradient rows
+  clock()          -> all-to-all of gradient rows to the owners, owner-side dedupe +
+                      segment sum (HIP) and row-wise Adagrad / SGD apply (HIP)
+
+Consistency: "bsp" applies at every Clock. "ssp" with staleness s (and "asp") issues the
+Clock's communication + apply on a dedicated HIP stream and only makes a later Get wait for
+the update of clock c-s-1 (bounded-staleness pipelining: the next steps' compute overlaps
+the collectives), which is exactly the SSP read guarantee (ssp_model.cpp:58-85).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from .comm import Comm
+
+
+def even_bounds(num_rows: int, parts: int) -> list[int]:
+    """Same split as the reference getRanges(): floor-sized ranges, the last takes the rest."""
+    step = num_rows // parts
+    b = [step * i for i in range(parts)] + [num_rows]
+    return b
+
+
+class _Pipeline:
+    """Tracks in-flight Clock work for SSP/ASP tables on a side stream."""
+
+    def __init__(self, comm: Comm, consistency: str, staleness: int):
+        self.consistency = consistency
+        self.staleness = staleness if consistency == "ssp" else (0 if consistency == "bsp" else 2)
+        self.async_ = consistency in ("ssp", "asp") and comm.device.type == "cuda" and self.staleness > 0
+        self.stream = torch.cuda.Stream(device=comm.device) if self.async_ else None
+        self.events: dict[int, torch.cuda.Event] = {}
+        self.clock = 0
+
+    def run(self, fn):
+        """Run ``fn`` (the clock's communication+apply) for the current clock."""
+        if not self.async_:
+            fn()
+        else:
+            cur = torch.cuda.current_stream(self.stream.device)
+            self.stream.wait_stream(cur)  # inputs produced on the compute stream
+            with torch.cuda.stream(self.stream):
+                fn()
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+            self.events[self.clock] = ev
+        self.clock += 1
+
+    def wait_clock(self, c: int):
+        """Make the compute stream wait until the Clock number ``c`` has been applied."""
+        if not self.async_ or c < 0:
+            return
+        cur = torch.cuda.current_stream(self.stream.device)
+        done = [k for k in self.events if k <= c]
+        if done:
+            cur.wait_event(self.events[max(done)])  # the side stream is in-order
+            for k in done:
+                del self.events[k]
+
+    def wait_for_read(self):
+        """Before a Get at clock c: updates of clocks <= c - s - 1 must be applied."""
+        self.wait_clock(self.clock - self.staleness - 1)
+
+    def keep_alive(self, *tensors):
+        """Tensors produced on the compute stream and consumed on the side stream."""
+        if self.async_:
+            for t in tensors:
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(self.stream)
+
+    def drain(self):
+        if self.async_:
+            cur = torch.cuda.current_stream(self.stream.device)
+            cur.wait_stream(self.stream)
+            self.events.clear()
+
+
+class DenseTable:
+    def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
+                 pull_dtype=torch.bfloat16, consistency: str = "bsp", staleness: int = 0, table_id: int = 0,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+        self.comm = comm
+        self.table_id = table_id
+        self.n_params = n_params
+        align = 64 * comm.world
+        self.n_pad = int(math.ceil(n_params / align) * align)
+        self.shard = self.n_pad // comm.world
+        self.base = comm.rank * self.shard
+        dev = comm.device
+        self.optimizer = optimizer
+        self.lr = lr
+        self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
+        self.pull_dtype = pull_dtype
+        self.master = torch.zeros(self.shard, dtype=torch.float32, device=dev)
+        self.m = torch.zeros_like(self.master) if optimizer in ("adam", "adagrad") else None
+        self.v = torch.zeros_like(self.master) if optimizer == "adam" else None
+        self.params = torch.zeros(self.n_pad, dtype=pull_dtype, device=dev)
+        self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
+        self.grad_shard = torch.zeros(self.shard, dtype=torch.float32, device=dev)
+        self.step = 0
+        self.pipe = _Pipeline(comm, consistency, staleness)
+        self._pending = False
+        # SSP/ASP: a ring of staleness+1 gradient buffers, so the side stream reduces clock t's
+        # gradients while the compute stream already writes clock t+1's.
+        self._ring = [self.grad] + [torch.zeros_like(self.grad) for _ in range(self.pipe.staleness)] \
+            if self.pipe.async_ else [self.grad]
+
+    # -- init / views -----------------------------------------------------------------------
+    def load_full(self, full: torch.Tensor):
+        """Initialise from the full fp32 vector (identical on every rank)."""
+        assert full.numel() == self.n_params
+        flat = torch.zeros(self.n_pad, dtype=torch.float32, device=self.comm.device)
+        flat[: self.n_params] = full.to(self.comm.device, torch.float32)
+        self.master.copy_(flat[self.base: self.base + self.shard])
+        self.params.copy_(flat.to(self.pull_dtype))
+
+    def full_master(self) -> torch.Tensor:
+        """All-gather of the fp32 master (checkpoint / tests)."""
+        out = torch.empty(self.n_pad, dtype=torch.float32, device=self.comm.device)
+        self.comm.all_gather(out, self.master)
+        return out[: self.n_params]
+
+    # -- KV API -----------------------------------------------------------------------------
+    def get(self) -> torch.Tensor:
+        self.pipe.wait_for_read()
+        return self.params
+
+    def add(self, grad: torch.Tensor | None = None):
+        """Accumulate a gradient (or mark the in-place-written self.grad as pushed)."""
+        if grad is not None:
+            self.grad[: grad.numel()] += grad.reshape(-1).to(torch.float32)
+        self._pending = True
+
+    def clock(self):
+        grad = self.grad
+        step = self.step + 1
+        self.step = step
+        pending = self._pending
+        self._pending = False
+
+        def work():
+            if pending:
+                self.comm.reduce_scatter(self.grad_shard, grad)
+                self._apply(self.grad_shard, step)
+                self.comm.all_gather(self.params, self.params[self.base: self.base + self.shard])
+            grad.zero_()
+
+        self.pipe.run(work)
+        if self.pipe.async_:
+            # next buffer of the ring: it was last used by clock step-len(ring); wait for it
+            self.grad = self._ring[step % len(self._ring)]
+            self.pipe.wait_clock(step - len(self._ring))
+
+    def _apply(self, g: torch.Tensor, step: int):
+        out = self.params[self.base: self.base + self.shard] if self.pull_dtype == torch.bfloat16 else None
+        if self.optimizer == "adam":
+            ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
+                           self.weight_decay, step, 1.0, out)
+        elif self.optimizer == "adagrad":
+            ops.adagrad_apply(self.master, self.m, g, self.lr, self.eps, 1.0, out)
+        elif self.optimizer == "sgd":
+            ops.sgd_apply(self.master, g, self.lr, 1.0, out)
+        elif self.optimizer == "add":  # the reference server apply: w += delta
+            self.master.add_(g)
+            if out is not None:
+                ops.cast_f32_bf16(self.master, out)
+        else:
+            raise ValueError(self.optimizer)
+        if out is None:
+            self.params[self.base: self.base + self.shard].copy_(self.master)
+
+    def drain(self):
+        self.pipe.drain()
+
+
+@dataclass
+class SparsePlan:
+    keys_n: int
+    inv: torch.Tensor          # [n] position of each requested key in the unique order
+    uniq: torch.Tensor         # [n] unique keys grouped by owner (first U valid)
+    U: int
+    send: list                 # keys requested from each owner
+    recv: list                 # keys each requester asked from me
+    recv_keys: torch.Tensor    # [M] keys I serve (grouped by requester)
+    own_uniq: torch.Tensor | None = None
+    own_inv: torch.Tensor | None = None
+    own_U: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+class SparseTable:
+    def __init__(self, comm: Comm, num_rows: int, width: int, optimizer: str = "rowwise_adagrad",
+                 lr: float = 0.01, eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "bsp",
+                 staleness: int = 0, split: int | None = None, table_id: int = 0, init_std: float = 0.01,
+                 seed: int = 1234):
+        self.comm = comm
+        self.table_id = table_id
+        self.num_rows = num_rows
+        self.width = width
+        self.optimizer, self.lr, self.eps = optimizer, lr, eps
+        self.pull_dtype = pull_dtype
+        self.split = split
+        dev = comm.device
+        b = even_bounds(num_rows, comm.world)
+        self.bounds_list = b
+        self.bounds = torch.tensor(b, dtype=torch.int64, device=dev)
+        self.base = b[comm.rank]
+        self.rows_local = b[comm.rank + 1] - b[comm.rank]
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + 7919 * comm.rank)
+        self.shard = torch.empty(self.rows_local, width, dtype=torch.float32, device=dev)
+        if init_std > 0:
+            self.shard.normal_(0.0, init_std, generator=g)
+        else:
+            self.shard.zero_()
+        self.state = torch.zeros(self.rows_local, dtype=torch.float32, device=dev) \
+            if optimizer == "rowwise_adagrad" else None
+        self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
+        self.pipe = _Pipeline(comm, consistency, staleness)
+        self._pending: list = []
+
+    # -- KV API -----------------------------------------------------------------------------
+    def plan(self, keys: torch.Tensor) -> SparsePlan:
+        keys = keys.reshape(-1).to(torch.int64)
+        uniq, inv, counts = ops.unique_bucketize(keys, self.bounds)
+        send, recv = self.comm.exchange_counts(counts)
+        U = int(sum(send))
+        M = int(sum(recv))
+        recv_keys = torch.empty(M, dtype=torch.int64, device=keys.device)
+        self.comm.all_to_all_v(recv_keys, uniq, recv, send)
+        p = SparsePlan(keys.numel(), inv, uniq, U, send, recv, recv_keys)
+        if self.comm.world > 1 and M > 0:
+            own_bounds = torch.tensor([0, 1 << 62], dtype=torch.int64, device=keys.device)
+            ou, oi, oc = ops.unique_bucketize(recv_keys, own_bounds)
+            p.own_uniq, p.own_inv = ou, oi
+            p.own_U = M if oc.numel() == 0 else int(oc.sum().item())
+        return p
+
+    def get(self, keys: torch.Tensor, plan: SparsePlan | None = None):
+        """Pull rows of ``keys``. Returns (rows [U, width] in unique order, plan); the row of
+        keys[i] is rows[plan.inv[i]]."""
+        self.pipe.wait_for_read()
+        if plan is None:
+            plan = self.plan(keys)
+        dev = self.comm.device
+        served = torch.empty(len(plan.recv_keys), self.width, dtype=self.pull_dtype, device=dev)
+        ops.gather_rows(self.shard, plan.recv_keys, self.base, served)
+        rows = torch.empty(plan.U, self.width, dtype=self.pull_dtype, device=dev)
+        self.comm.all_to_all_v(rows, served, plan.send, plan.recv)
+        return rows, plan
+
+    def get_rows(self, keys: torch.Tensor) -> torch.Tensor:
+        """Reference-style Get: the values of every requested key, in request order."""
+        rows, plan = self.get(keys)
+        return rows[plan.inv]
+
+    def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
+        """Push gradient rows (aligned with the plan's unique order)."""
+        assert grad_rows.shape[0] >= plan.U and grad_rows.dtype == torch.float32
+        self._pending.append((plan, grad_rows))
+
+    def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
+        """Reference-style Add(keys, vals) (duplicates are summed)."""
+        plan = self.plan(keys)
+        g = torch.zeros(max(plan.U, 1), self.width, dtype=torch.float32, device=self.comm.device)
+        ops.scatter_add_rows(vals.reshape(keys.numel(), -1).to(torch.float32).contiguous(), plan.inv, g)
+        self.add(plan, g)
+
+    def clock(self):
+        pending, self._pending = self._pending, []
+        for plan, g in pending:
+            self.pipe.keep_alive(g, plan.uniq, plan.recv_keys, plan.own_uniq, plan.own_inv)
+
+        def work():
+            for plan, grad_rows in pending:
+                self._push(plan, grad_rows)
+
+        self.pipe.run(work)
+
+    def _push(self, plan: SparsePlan, grad_rows: torch.Tensor):
+        dev = self.comm.device
+        if self.comm.world == 1:
+            keys, g, n = plan.uniq, grad_rows, plan.U
+        else:
+            M = len(plan.recv_keys)
+            recv = torch.empty(M, self.width, dtype=torch.float32, device=dev)
+            self.comm.all_to_all_v(recv, grad_rows, plan.recv, plan.send)
+            if M == 0:
+                return
+            g = torch.zeros(plan.own_U, self.width, dtype=torch.float32, device=dev)
+            ops.scatter_add_rows(recv, plan.own_inv, g)
+            keys, n = plan.own_uniq, plan.own_U
+        keys = keys[:n]
+        g = g[:n]
+        if self.optimizer == "rowwise_adagrad":
+            ops.sparse_rowwise_adagrad(self.shard, self.state, keys, self.base, g, self.lr, self.eps,
+                                       state2=self.state2, split=self.split)
+        elif self.optimizer == "sgd":
+            ops.sparse_sgd(self.shard, keys, self.base, g.contiguous(), -self.lr)
+        elif self.optimizer == "add":
+            ops.sparse_sgd(self.shard, keys, self.base, g.contiguous(), 1.0)
+        else:
+            raise ValueError(self.optimizer)
+
+    def drain(self):
+        self.pipe.drain()

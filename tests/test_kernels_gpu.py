@@ -1,0 +1,213 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op
+(the CPU implementations in minips_amd.ops are that reference)."""
+import pytest
+import torch
+
+from minips_amd import _native, ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.fixture(autouse=True)
+def _require_kernels(dev):
+    _native.kernels()  # a GPU run must load the native extension, never fall back
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 136, 96), (1024, 512, 848), (64, 1024, 32)])
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+def test_gemm_layouts_f32(dev, M, N, K, layout):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    a_km, b_kn = {"nt": (False, False), "nn": (False, True), "tn": (True, True)}[layout]
+    # asymmetric data catches transposed writes
+    A = torch.randn(K if a_km else M, M if a_km else K, generator=g)
+    B = torch.randn(K if b_kn else N, N if b_kn else K, generator=g)
+    if (a_km and M % 8) or (b_kn and N % 8):
+        pytest.skip("layout needs M/N % 8")
+    Ab, Bb = _bf(A), _bf(B)
+    ref = torch.empty(M, N)
+    ops.gemm(Ab, Bb, ref, M, N, K, a_km, b_kn, ops.EPI_STORE_F32)
+    C = torch.full((M, N), float("nan"), device=dev)
+    ops.gemm(Ab.to(dev), Bb.to(dev), C, M, N, K, a_km, b_kn, ops.EPI_STORE_F32)
+    torch.testing.assert_close(C.cpu(), ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
+
+
+def test_gemm_identity_asymmetric(dev):
+    # A = I with an asymmetric B: any row/col swap in the C write shows up exactly.
+    n = 128
+    A = torch.eye(n)
+    B = torch.arange(n * n, dtype=torch.float32).view(n, n) % 97
+    C = torch.zeros(n, n, device=dev)
+    ops.gemm(_bf(A).to(dev), _bf(B).to(dev), C, n, n, n, False, True, ops.EPI_STORE_F32)
+    torch.testing.assert_close(C.cpu(), _bf(B).float())
+
+
+def test_gemm_epilogues(dev):
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 384, 256, 160
+    X = _bf(torch.randn(M, K, generator=g))
+    W = _bf(torch.randn(N, K, generator=g) * 0.1)
+    b = _bf(torch.randn(N, generator=g))
+    for act in ("relu", "none", "gelu"):
+        ref = ops.linear_fwd(X, W, b, act)
+        out = ops.linear_fwd(X.to(dev), W.to(dev), b.to(dev), act)
+        torch.testing.assert_close(out.float().cpu(), ref.float(), rtol=2e-2, atol=2e-2)
+    # dgrad with relu mask + colsum
+    dY = _bf(torch.randn(M, N, generator=g))
+    mask = _bf(torch.randn(M, K, generator=g))
+    cs_ref = torch.zeros(K)
+    ref = ops.linear_dgrad(dY, W, mask=mask, colsum=cs_ref)
+    cs = torch.zeros(K, device=dev)
+    out = ops.linear_dgrad(dY.to(dev), W.to(dev), mask=mask.to(dev), colsum=cs)
+    torch.testing.assert_close(out.float().cpu(), ref.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(cs.cpu(), cs_ref, rtol=1e-3, atol=1e-2)
+    # wgrad split-K accumulate
+    dW_ref = torch.ones(N, K)
+    ops.linear_wgrad(dY, X, dW_ref)
+    dW = torch.ones(N, K, device=dev)
+    ops.linear_wgrad(dY.to(dev), X.to(dev), dW, split_k=3)
+    torch.testing.assert_close(dW.cpu(), dW_ref, rtol=2e-3, atol=2e-2)
+
+
+def test_unique_bucketize(dev):
+    g = torch.Generator().manual_seed(0)
+    keys = torch.randint(0, 5000, (20000,), generator=g)
+    bounds = torch.tensor([0, 1000, 2500, 4000, 5000])
+    uniq, inv, counts = ops.unique_bucketize(keys.to(dev), bounds.to(dev))
+    uniq, inv, counts = uniq.cpu(), inv.cpu(), counts.cpu()
+    U = int(counts.sum())
+    assert U == torch.unique(keys).numel()
+    torch.testing.assert_close(uniq[inv], keys)  # inverse is exact
+    u = uniq[:U]
+    assert torch.unique(u).numel() == U
+    start = 0
+    for p in range(4):  # grouped by owner
+        seg = u[start: start + int(counts[p])]
+        assert ((seg >= bounds[p]) & (seg < bounds[p + 1])).all()
+        start += int(counts[p])
+
+
+def test_gather_scatter_adagrad(dev):
+    g = torch.Generator().manual_seed(1)
+    R, W = 1000, 36
+    table = torch.randn(R, W, generator=g)
+    keys = torch.randint(100, 100 + R, (300,), generator=g).unique()
+    for dt in (torch.float32, torch.bfloat16):
+        out = torch.empty(keys.numel(), W, dtype=dt, device=dev)
+        ops.gather_rows(table.to(dev), keys.to(dev), 100, out)
+        torch.testing.assert_close(out.float().cpu(), table[keys - 100].to(dt).float())
+    src = torch.randn(500, W, generator=g)
+    idx = torch.randint(0, 50, (500,), generator=g)
+    acc = torch.zeros(50, W, device=dev)
+    ops.scatter_add_rows(src.to(dev), idx.to(dev), acc)
+    torch.testing.assert_close(acc.cpu(), torch.zeros(50, W).index_add_(0, idx, src), rtol=1e-5, atol=1e-5)
+    # row-wise adagrad with split state
+    grads = torch.randn(keys.numel(), 33, generator=g)
+    t_ref, s_ref, s2_ref = table.clone(), torch.rand(R, generator=g), torch.rand(R, generator=g)
+    t_gpu, s_gpu, s2_gpu = t_ref.to(dev), s_ref.to(dev), s2_ref.to(dev)
+    ops.sparse_rowwise_adagrad(t_ref, s_ref, keys, 100, grads, 0.1, 1e-8, state2=s2_ref, split=32)
+    ops.sparse_rowwise_adagrad(t_gpu, s_gpu, keys.to(dev), 100, grads.to(dev), 0.1, 1e-8, state2=s2_gpu, split=32)
+    torch.testing.assert_close(t_gpu.cpu(), t_ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(s_gpu.cpu(), s_ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-5, atol=1e-6)
+
+
+def test_dense_optimizers(dev):
+    g = torch.Generator().manual_seed(2)
+    n = 10003
+    w, m, v, gr = (torch.randn(n, generator=g) for _ in range(4))
+    v = v.abs()
+    cpu = [t.clone() for t in (w, m, v)]
+    gpu = [t.to(dev) for t in (w, m, v)]
+    wb = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    ops.adam_apply(*cpu, gr, 1e-2, step=3, weight_decay=0.01)
+    ops.adam_apply(*gpu, gr.to(dev), 1e-2, step=3, weight_decay=0.01, w_bf16=wb)
+    for a, b in zip(gpu, cpu):
+        torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(wb.float().cpu(), cpu[0].to(torch.bfloat16).float())
+    acc = torch.rand(n, generator=g)
+    w1, a1 = w.clone(), acc.clone()
+    w2, a2 = w.to(dev), acc.to(dev)
+    ops.adagrad_apply(w1, a1, gr, 0.1)
+    ops.adagrad_apply(w2, a2, gr.to(dev), 0.1)
+    torch.testing.assert_close(w2.cpu(), w1, rtol=1e-5, atol=1e-6)
+
+
+def test_widedeep_kernels(dev):
+    g = torch.Generator().manual_seed(4)
+    B, F, D, nd, U = 96, 5, 32, 13, 40
+    ldx = (F * D + nd + 7) // 8 * 8
+    rows = _bf(torch.randn(U, 36, generator=g))
+    inv = torch.randint(0, U, (B * F,), generator=g)
+    dense = torch.randn(B, nd, generator=g)
+    X_ref, w_ref = torch.empty(B, ldx, dtype=torch.bfloat16), torch.empty(B)
+    ops.wd_assemble(dense, rows, inv, F, D, X_ref, w_ref)
+    X, wl = torch.empty(B, ldx, dtype=torch.bfloat16, device=dev), torch.empty(B, device=dev)
+    ops.wd_assemble(dense.to(dev), rows.to(dev), inv.to(dev), F, D, X, wl)
+    torch.testing.assert_close(X.cpu(), X_ref)
+    torch.testing.assert_close(wl.cpu(), w_ref, rtol=1e-5, atol=1e-5)
+    # head
+    Hd = 256
+    H = _bf(torch.relu(torch.randn(B, Hd, generator=g)))
+    w = _bf(torch.randn(Hd, generator=g) * 0.1)
+    b0 = _bf(torch.tensor([0.1]))
+    y = (torch.rand(B, generator=g) > 0.5).float()
+
+    def run(d):
+        outs = dict(dH=torch.empty(B, Hd, dtype=torch.bfloat16, device=d), dw=torch.zeros(Hd, device=d),
+                    db=torch.zeros(1, device=d), dwide=torch.empty(B, device=d), loss=torch.zeros(1, device=d),
+                    cs=torch.zeros(Hd, device=d))
+        ops.wd_head(H.to(d), w.to(d), b0.to(d), w_ref.to(d), y.to(d), outs["dH"], outs["dw"], outs["db"],
+                    outs["dwide"], outs["loss"], outs["cs"], 1.0 / B)
+        return {k: v.cpu() for k, v in outs.items()}
+
+    r, o = run("cpu"), run(dev)
+    for k in r:
+        torch.testing.assert_close(o[k].float(), r[k].float(), rtol=2e-2, atol=1e-4)
+    # embedding backward
+    dX = torch.randn(B, F * D, generator=g)
+    dwide = torch.randn(B, generator=g)
+    gr_ref = torch.zeros(U, 36)
+    ops.wd_emb_backward(dX, dwide, inv, F, D, gr_ref)
+    gr = torch.zeros(U, 36, device=dev)
+    ops.wd_emb_backward(dX.to(dev), dwide.to(dev), inv.to(dev), F, D, gr)
+    torch.testing.assert_close(gr.cpu(), gr_ref, rtol=1e-4, atol=1e-4)
+
+
+def test_lr_and_kmeans(dev):
+    g = torch.Generator().manual_seed(5)
+    B, nnz, U = 64, 10, 200
+    rowptr = torch.arange(0, (B + 1) * nnz, nnz)
+    cols = torch.randint(0, U, (B * nnz,), generator=g)
+    vals = torch.rand(B * nnz, generator=g)
+    labels = torch.where(torch.rand(B, generator=g) > 0.5, 1.0, -1.0)
+    w = torch.randn(U, generator=g) * 0.1
+    d_ref, c_ref = torch.zeros(U), torch.zeros(1)
+    ops.lr_sparse_step(rowptr, cols, vals, labels, w, 0.5, d_ref, c_ref)
+    d, c = torch.zeros(U, device=dev), torch.zeros(1, device=dev)
+    ops.lr_sparse_step(rowptr.to(dev), cols.to(dev), vals.to(dev), labels.to(dev), w.to(dev), 0.5, d, c)
+    torch.testing.assert_close(d.cpu(), d_ref, rtol=1e-4, atol=1e-5)
+    assert float(c) == float(c_ref)
+    X = torch.randn(500, 24, generator=g)
+    C = torch.randn(5, 24, generator=g)
+    a_ref = ops.kmeans_assign(X, C)
+    a = ops.kmeans_assign(X.to(dev), C.to(dev))
+    assert (a.cpu() == a_ref).float().mean() > 0.995
+
+
+def test_embedding_bag(dev):
+    g = torch.Generator().manual_seed(6)
+    rows = torch.randn(100, 16, generator=g)
+    idx = torch.randint(0, 100, (50,), generator=g)
+    offsets = torch.tensor([0, 3, 3, 10, 25, 50])
+    for mean in (False, True):
+        ref = ops.embedding_bag_fwd(rows, idx, offsets, mean)
+        out = ops.embedding_bag_fwd(rows.to(dev), idx.to(dev), offsets.to(dev), mean)
+        torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=1e-5)
+        go = torch.randn(5, 16, generator=g)
+        gr_ref = ops.embedding_bag_bwd(go, idx, offsets, torch.zeros(100, 16), mean)
+        gr = ops.embedding_bag_bwd(go.to(dev), idx.to(dev), offsets.to(dev), torch.zeros(100, 16, device=dev), mean)
+        torch.testing.assert_close(gr.cpu(), gr_ref, rtol=1e-5, atol=1e-5)

@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box pass: smoke, GPU tests, short bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; any failure stops the script (set -e + &&).
+set -eo pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+STAGE=${1:-all}
+if [[ $STAGE == all || $STAGE == smoke ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+  tail -3 gpurun_out/smoke.log
+fi
+if [[ $STAGE == all || $STAGE == test ]]; then
+  timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -3 gpurun_out/pytest_gpu.log
+fi
+if [[ $STAGE == all || $STAGE == bench ]]; then
+  timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 ${BENCH_ARGS} > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
+  tail -2 gpurun_out/bench.log
+fi
+if [[ $STAGE == all || $STAGE == prof ]]; then
+  cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 3 ${BENCH_ARGS} > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
+  find gpurun_out/prof -name "*kernel_stats.csv" | head -3
+fi
