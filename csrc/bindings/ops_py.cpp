@@ -2,8 +2,8 @@
 // Every op validates device/dtype/shape/contiguity on the host BEFORE launching, so a bad
 // shape raises a Python exception instead of faulting the GPU, and launches on the current
 // HIP stream of the tensor's device (graph-capture safe: no allocation or sync in here).
-#include <c10/hip/HIPGuard.h>
-#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/extension.h>
 
 #include "../kernels/kernels.h"
@@ -12,7 +12,7 @@ namespace {
 
 using minips_k::bf16_t;
 
-hipStream_t stream_of(const at::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+hipStream_t stream_of(const at::Tensor& t) { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream(); }
 
 void check_gpu(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -65,14 +65,14 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   if (epi == minips_k::kEpiReluMaskBf16) TORCH_CHECK(mask_p, "relu-mask epilogue needs mask");
   float* colsum_p = opt_ptr<float>(colsum, at::kFloat, "colsum");
   if (colsum_p) TORCH_CHECK(colsum->numel() >= N, "colsum too short");
-  c10::hip::HIPGuard g(A.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
   minips_k::gemm_bf16(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)A.size(1),
                       (int)B.size(1), (int)C.size(1), a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p,
                       (float)alpha, (int)split_k, stream_of(A));
 }
 
 // Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P]).
-std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tensor& bounds) {
+std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tensor& bounds, int64_t F) {
   check_gpu(keys, "keys");
   check_gpu(bounds, "bounds");
   check_dtype(keys, at::kLong, "keys");
@@ -87,8 +87,9 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   auto slot = at::empty({n}, opts), flags = at::empty({n}, opts.dtype(at::kInt));
   auto counts = at::empty({P}, opts), cursor = at::empty({P}, opts);
   auto out_keys = at::empty({n}, opts), inverse = at::empty({n}, opts);
-  c10::hip::HIPGuard g(keys.device());
-  minips_k::unique_bucketize(ptr<int64_t>(keys), n, ptr<int64_t>(bounds), P, ptr<int64_t>(table_keys),
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  TORCH_CHECK(F >= 1 && n % F == 0, "unique_bucketize: numel must be a multiple of F");
+  minips_k::unique_bucketize(ptr<int64_t>(keys), n, (int)F, ptr<int64_t>(bounds), P, ptr<int64_t>(table_keys),
                              ptr<int64_t>(table_pos), cap, ptr<int64_t>(slot), ptr<int32_t>(flags),
                              ptr<int64_t>(counts), ptr<int64_t>(cursor), ptr<int64_t>(out_keys), ptr<int64_t>(inverse),
                              stream_of(keys));
@@ -106,7 +107,7 @@ void gather_rows(const at::Tensor& table, const at::Tensor& keys, int64_t base, 
   const int D = (int)out.size(1);
   TORCH_CHECK(D <= table.size(1), "out row wider than table row");
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "out must be fp32 or bf16");
-  c10::hip::HIPGuard g(keys.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::gather_rows(ptr<float>(table), table.stride(0), ptr<int64_t>(keys), n, base, D, out.data_ptr(),
                         out.scalar_type() == at::kBFloat16, stream_of(keys));
 }
@@ -120,7 +121,7 @@ void scatter_add_rows(const at::Tensor& src, const at::Tensor& idx, at::Tensor& 
   check_dtype(idx, at::kLong, "idx");
   TORCH_CHECK(src.dim() == 2 && acc.dim() == 2 && src.size(1) == acc.size(1), "row widths differ");
   TORCH_CHECK(idx.numel() == src.size(0), "idx/src length mismatch");
-  c10::hip::HIPGuard g(src.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
   minips_k::scatter_add_rows(ptr<float>(src), src.size(0), (int)src.size(1), ptr<int64_t>(idx), ptr<float>(acc),
                              stream_of(src));
 }
@@ -135,7 +136,7 @@ void sparse_rowwise_adagrad(at::Tensor& table, at::Tensor& state, const c10::opt
   check_dtype(grads, at::kFloat, "grads");
   TORCH_CHECK(grads.dim() == 2 && grads.size(0) == keys.numel() && grads.size(1) <= table.size(1), "grads shape");
   float* s2 = opt_ptr<float>(state2, at::kFloat, "state2");
-  c10::hip::HIPGuard g(table.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
   minips_k::sparse_rowwise_adagrad(ptr<float>(table), table.stride(0), ptr<float>(state), s2, (int)D1,
                                    ptr<int64_t>(keys), keys.numel(), base, (int)grads.size(1), ptr<float>(grads),
                                    (float)lr, (float)eps, stream_of(table));
@@ -146,7 +147,7 @@ void sparse_sgd(at::Tensor& table, const at::Tensor& keys, int64_t base, const a
   check_gpu(keys, "keys");
   check_gpu(grads, "grads");
   TORCH_CHECK(grads.dim() == 2 && grads.size(0) == keys.numel() && grads.size(1) <= table.size(1), "grads shape");
-  c10::hip::HIPGuard g(table.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
   minips_k::sparse_sgd(ptr<float>(table), table.stride(0), ptr<int64_t>(keys), keys.numel(), base,
                        (int)grads.size(1), ptr<float>(grads), (float)scale, stream_of(table));
 }
@@ -158,7 +159,7 @@ void embedding_bag_fwd(const at::Tensor& rows, const at::Tensor& idx, const at::
   check_gpu(offsets, "offsets");
   check_gpu(out, "out");
   TORCH_CHECK(out.size(0) == offsets.numel() - 1 && out.size(1) == rows.size(1), "out shape");
-  c10::hip::HIPGuard g(rows.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(rows.device());
   minips_k::embedding_bag_fwd(ptr<float>(rows), ptr<int64_t>(idx), ptr<int64_t>(offsets), out.size(0),
                               (int)rows.size(1), mean, ptr<float>(out), stream_of(rows));
 }
@@ -168,7 +169,7 @@ void embedding_bag_bwd(const at::Tensor& grad_out, const at::Tensor& idx, const 
   check_gpu(grad_out, "grad_out");
   check_gpu(grad_rows, "grad_rows");
   TORCH_CHECK(grad_out.size(1) == grad_rows.size(1), "width mismatch");
-  c10::hip::HIPGuard g(grad_out.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(grad_out.device());
   minips_k::embedding_bag_bwd(ptr<float>(grad_out), ptr<int64_t>(idx), ptr<int64_t>(offsets), grad_out.size(0),
                               (int)grad_out.size(1), mean, ptr<float>(grad_rows), stream_of(grad_out));
 }
@@ -187,7 +188,7 @@ void wd_assemble(const at::Tensor& dense, const at::Tensor& rows, const at::Tens
   TORCH_CHECK(inv.numel() == B * F, "inv must be [B*F]");
   TORCH_CHECK(dense.size(0) == B, "dense rows");
   TORCH_CHECK(rows.size(1) > D, "rows must hold D deep values + the wide weight");
-  c10::hip::HIPGuard g(X.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
   minips_k::wd_assemble(ptr<float>(dense), (int)dense.size(1), ptr<bf16_t>(rows), (int)rows.size(1),
                         ptr<int64_t>(inv), B, (int)F, (int)D, ptr<bf16_t>(X), (int)X.size(1), ptr<float>(wide_logit),
                         stream_of(X));
@@ -204,7 +205,7 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
   TORCH_CHECK(dH.sizes() == H.sizes(), "dH shape");
   TORCH_CHECK(w.numel() == H.size(1) && dw.numel() == H.size(1), "w/dw length");
   float* cs = opt_ptr<float>(dH_colsum, at::kFloat, "dH_colsum");
-  c10::hip::HIPGuard g(H.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(H.device());
   minips_k::wd_head(ptr<bf16_t>(H), H.size(0), (int)H.size(1), ptr<bf16_t>(w), ptr<bf16_t>(b0),
                     ptr<float>(wide_logit), ptr<float>(labels), ptr<bf16_t>(dH), ptr<float>(dw), ptr<float>(db),
                     ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H));
@@ -220,7 +221,7 @@ void wd_emb_backward(const at::Tensor& dX, const at::Tensor& dwide, const at::Te
   check_dtype(grad_rows, at::kFloat, "grad_rows");
   const int64_t B = dX.size(0);
   TORCH_CHECK(inv.numel() == B * F && dX.size(1) >= F * D && grad_rows.size(1) > D, "shapes");
-  c10::hip::HIPGuard g(dX.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
   minips_k::wd_emb_backward(ptr<float>(dX), (int)dX.size(1), ptr<float>(dwide), ptr<int64_t>(inv), B, (int)F, (int)D,
                             ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
 }
@@ -237,7 +238,7 @@ void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g
   TORCH_CHECK(w.numel() == m.numel() && w.numel() == v.numel() && w.numel() == g.numel(), "adam sizes differ");
   bf16_t* wb = opt_ptr<bf16_t>(w_bf16, at::kBFloat16, "w_bf16");
   if (wb) TORCH_CHECK(w_bf16->numel() == w.numel(), "w_bf16 size");
-  c10::hip::HIPGuard gd(w.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(w.device());
   minips_k::adam_apply(ptr<float>(w), ptr<float>(m), ptr<float>(v), ptr<float>(g), w.numel(), (float)lr, (float)beta1,
                        (float)beta2, (float)eps, (float)weight_decay, (int)step, (float)grad_scale, wb, stream_of(w));
 }
@@ -247,7 +248,7 @@ void sgd_apply(at::Tensor& w, const at::Tensor& g, double lr, double grad_scale,
   check_gpu(g, "g");
   TORCH_CHECK(w.numel() == g.numel(), "sizes differ");
   bf16_t* wb = opt_ptr<bf16_t>(w_bf16, at::kBFloat16, "w_bf16");
-  c10::hip::HIPGuard gd(w.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(w.device());
   minips_k::sgd_apply(ptr<float>(w), ptr<float>(g), w.numel(), (float)lr, (float)grad_scale, wb, stream_of(w));
 }
 
@@ -258,7 +259,7 @@ void adagrad_apply(at::Tensor& w, at::Tensor& acc, const at::Tensor& g, double l
   check_gpu(g, "g");
   TORCH_CHECK(w.numel() == g.numel() && w.numel() == acc.numel(), "sizes differ");
   bf16_t* wb = opt_ptr<bf16_t>(w_bf16, at::kBFloat16, "w_bf16");
-  c10::hip::HIPGuard gd(w.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(w.device());
   minips_k::adagrad_apply(ptr<float>(w), ptr<float>(acc), ptr<float>(g), w.numel(), (float)lr, (float)eps,
                           (float)grad_scale, wb, stream_of(w));
 }
@@ -269,7 +270,7 @@ void cast_f32_bf16(const at::Tensor& x, at::Tensor& y) {
   check_dtype(x, at::kFloat, "x");
   check_dtype(y, at::kBFloat16, "y");
   TORCH_CHECK(x.numel() == y.numel(), "sizes differ");
-  c10::hip::HIPGuard gd(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(x.device());
   minips_k::cast_f32_bf16(ptr<float>(x), ptr<bf16_t>(y), x.numel(), stream_of(x));
 }
 
@@ -283,7 +284,7 @@ void lr_sparse_step(const at::Tensor& rowptr, const at::Tensor& cols, const at::
   float* d = opt_ptr<float>(delta, at::kFloat, "delta");
   if (d) TORCH_CHECK(delta->numel() == w.numel(), "delta must match w");
   float* c = opt_ptr<float>(correct, at::kFloat, "correct");
-  c10::hip::HIPGuard gd(w.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(w.device());
   minips_k::lr_sparse_step(ptr<int64_t>(rowptr), ptr<int64_t>(cols), ptr<float>(vals), ptr<float>(labels),
                            labels.numel(), ptr<float>(w), (float)alpha, d, c, stream_of(w));
 }
@@ -297,9 +298,23 @@ void kmeans_assign(const at::Tensor& X, const at::Tensor& C, at::Tensor& assign,
   check_dtype(assign, at::kInt, "assign");
   TORCH_CHECK(X.size(1) == C.size(1) && assign.numel() == X.size(0), "kmeans shapes");
   float* dp = opt_ptr<float>(dist, at::kFloat, "dist");
-  c10::hip::HIPGuard gd(X.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(X.device());
   minips_k::kmeans_assign(ptr<float>(X), X.size(0), (int)X.size(1), ptr<float>(C), (int)C.size(0),
                           ptr<int32_t>(assign), dp, stream_of(X));
+}
+
+void criteo_synth(int64_t seed, int64_t step, const at::Tensor& cards, const at::Tensor& offsets, const at::Tensor& w,
+                  at::Tensor& dense, at::Tensor& keys, at::Tensor& labels) {
+  for (const at::Tensor* t : {&cards, &offsets, &w, (const at::Tensor*)&dense, (const at::Tensor*)&keys, (const at::Tensor*)&labels}) check_gpu(*t, "criteo_synth arg");
+  check_dtype(keys, at::kLong, "keys");
+  check_dtype(cards, at::kLong, "cards");
+  const int64_t B = labels.numel();
+  const int F = (int)cards.numel();
+  TORCH_CHECK(keys.numel() == B * F && dense.size(0) == B && w.numel() == dense.size(1), "criteo_synth shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  minips_k::criteo_synth((uint64_t)seed, (uint64_t)step, B, F, ptr<int64_t>(cards), ptr<int64_t>(offsets),
+                         (int)dense.size(1), ptr<float>(w), ptr<float>(dense), ptr<int64_t>(keys), ptr<float>(labels),
+                         stream_of(keys));
 }
 
 }  // namespace
@@ -314,7 +329,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("EPI_RELU_MASK_BF16") = (int)minips_k::kEpiReluMaskBf16;
   m.attr("EPI_BIAS_GELU_BF16") = (int)minips_k::kEpiBiasGeluBf16;
   m.def("gemm", &gemm);
-  m.def("unique_bucketize", &unique_bucketize);
+  m.def("unique_bucketize", &unique_bucketize, py::arg("keys"), py::arg("bounds"), py::arg("F") = 1);
   m.def("gather_rows", &gather_rows);
   m.def("scatter_add_rows", &scatter_add_rows);
   m.def("sparse_rowwise_adagrad", &sparse_rowwise_adagrad);
@@ -330,4 +345,5 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("lr_sparse_step", &lr_sparse_step);
   m.def("kmeans_assign", &kmeans_assign);
+  m.def("criteo_synth", &criteo_synth);
 }

@@ -1,0 +1,79 @@
+// Fused on-device synthetic batch generator for the Criteo-shaped benchmarks (one launch per
+// step instead of ~15 torch RNG/elementwise launches). Counter-based RNG (splitmix64 of
+// seed, step, element), so batches are reproducible and independent of the launch shape.
+//   dense  [B, n_dense] ~ N(0,1) (Box-Muller)
+//   keys   [B, F]  id = floor((card+1)^u) - 1 (log-uniform / Zipf(1) head), scattered by a
+//                  bijective multiplicative hash, plus the feature's row offset
+//   labels [B]     Bernoulli(sigmoid(2 * (dense.w + 0.5*(#odd of the first 4 raw ids - 1))))
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace minips_k {
+
+__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ULL;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ float u01f(uint64_t h) { return ((uint32_t)(h >> 40) + 0.5f) * (1.0f / 16777216.0f); }
+
+__device__ __forceinline__ int64_t raw_id(uint64_t sb, int f, int64_t card) {
+  const float u = u01f(splitmix(sb + 1000 + f));
+  int64_t raw = (int64_t)floorf(__expf(u * __logf((float)card + 1.f)) - 1.f);
+  return raw < 0 ? 0 : (raw >= card ? card - 1 : raw);
+}
+
+// Index space B*F (one key each) + B (dense features + label): no serial per-sample loop.
+__global__ void criteo_synth_kernel(uint64_t seed, uint64_t step, int64_t B, int F, const int64_t* __restrict__ cards,
+                                    const int64_t* __restrict__ offsets, int n_dense, const float* __restrict__ w,
+                                    float* __restrict__ dense, int64_t* __restrict__ keys, float* __restrict__ labels) {
+  const uint64_t base = splitmix(seed * 0x632be59bd9b4e019ULL + step);
+  const int64_t nk = B * F;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nk + B; e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < nk) {
+      const int64_t b = e / F;
+      const int f = (int)(e - b * F);
+      const uint64_t sb = splitmix(base ^ (uint64_t)b * 0xd1342543de82ef95ULL);
+      const int64_t card = cards[f];
+      const int64_t raw = raw_id(sb, f, card);
+      keys[e] = (int64_t)(((unsigned __int128)raw * 2654435761ULL) % (unsigned __int128)card) + offsets[f];
+    } else {
+      const int64_t b = e - nk;
+      const uint64_t sb = splitmix(base ^ (uint64_t)b * 0xd1342543de82ef95ULL);
+      float logit = 0.f;
+      for (int j = 0; j < n_dense; j += 2) {
+        const float u1 = u01f(splitmix(sb + 2 * j + 1)), u2 = u01f(splitmix(sb + 2 * j + 2));
+        const float r = sqrtf(-2.f * __logf(u1));
+        float sn, cs;
+        __sincosf(6.2831853f * u2, &sn, &cs);
+        dense[b * n_dense + j] = r * cs;
+        logit += r * cs * w[j];
+        if (j + 1 < n_dense) {
+          dense[b * n_dense + j + 1] = r * sn;
+          logit += r * sn * w[j + 1];
+        }
+      }
+      int odd = 0;
+      for (int f = 0; f < 4 && f < F; ++f) odd += (int)(raw_id(sb, f, cards[f]) & 1);
+      logit += 0.5f * ((float)odd - 1.f);
+      const float noise = u01f(splitmix(sb + 5000));
+      labels[b] = (1.f / (1.f + __expf(-2.f * logit)) > noise) ? 1.f : 0.f;
+    }
+  }
+}
+
+void criteo_synth(uint64_t seed, uint64_t step, int64_t B, int F, const int64_t* cards, const int64_t* offsets,
+                  int n_dense, const float* w, float* dense, int64_t* keys, float* labels, hipStream_t s) {
+  if (B <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(criteo_synth_kernel, grid_for(B * (F + 1), block, 4096), block, 0, s, seed, step, B, F, cards, offsets, n_dense, w,
+                     dense, keys, labels);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace minips_k

@@ -32,7 +32,8 @@ void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, i
 // bounds {0, 2^63} makes it a plain unique. Work buffers are provided by the caller:
 // table_keys/table_pos [cap] (cap power of two >= 2n), slot [n], flags [n], counts [P],
 // cursor [P] (all state re-initialised inside).
-void unique_bucketize(const int64_t* keys, int64_t n, const int64_t* bounds, int P, int64_t* table_keys,
+// keys may be a [B, F] batch (F > 1): tiles are then taken feature-major for better dedupe.
+void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s);
 
@@ -96,5 +97,9 @@ void lr_sparse_step(const int64_t* rowptr, const int64_t* cols, const float* val
 // K-Means assignment: X [n, d] fp32, C [k, d] fp32 -> assign [n] (int32), min dist [n].
 void kmeans_assign(const float* X, int64_t n, int d, const float* C, int k, int32_t* assign, float* dist,
                    hipStream_t s);
+
+// ------------------------------------------------------------------ synthetic data (data.hip)
+void criteo_synth(uint64_t seed, uint64_t step, int64_t B, int F, const int64_t* cards, const int64_t* offsets,
+                  int n_dense, const float* w, float* dense, int64_t* keys, float* labels, hipStream_t s);
 
 }  // namespace minips_k

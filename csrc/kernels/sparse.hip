@@ -30,28 +30,90 @@ __device__ __forceinline__ int owner_of(const int64_t* bounds, int P, int64_t ke
   return o;
 }
 
-__global__ void ub_insert_kernel(const int64_t* __restrict__ keys, int64_t n, const int64_t* __restrict__ bounds,
-                                 int P, unsigned long long* table_keys, int64_t cap, int64_t* slot, int32_t* flags,
-                                 unsigned long long* counts) {
-  const int64_t mask = cap - 1;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t key = keys[i];
-    int64_t h = (int64_t)(mix64((uint64_t)key) & (uint64_t)mask);
+// Wave-aggregated atomic add of 1 per active lane, grouped by `slot`: one atomic per
+// distinct slot per wave instead of one per lane (a single shared counter otherwise
+// serialises every unique key of the batch). Returns this lane's rank-ordered old value.
+__device__ __forceinline__ unsigned long long wave_agg_inc(unsigned long long* ctr, int slot, bool active) {
+  unsigned long long mine = 0;
+  unsigned long long pending = __ballot(active);
+  const int lane = threadIdx.x & 63;
+  while (pending) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const int s = __shfl(slot, leader);
+    const unsigned long long grp = __ballot(active && slot == s) & pending;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(ctr + s, (unsigned long long)__popcll(grp));
+    base = __shfl(base, leader);
+    if ((grp >> lane) & 1ULL) mine = base + (unsigned long long)__popcll(grp & ((1ULL << lane) - 1ULL));
+    pending &= ~grp;
+  }
+  return mine;
+}
+
+// Insert with block-local pre-dedupe: a block takes 256 keys of ONE feature (feature-major
+// tile over a [B, F] batch, F = 1 for a flat key list), dedupes them in an LDS hash, and only
+// the block-distinct keys probe the global table (read first, CAS only on an empty slot).
+// Zipf-hot ids (a 3-value feature hit by every sample) otherwise hammer one global slot with
+// thousands of CAS.
+constexpr int kUbTile = 256;
+constexpr int kUbLds = 512;
+
+__global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t rows_b,
+                                                            int F, const int64_t* __restrict__ bounds, int P,
+                                                            unsigned long long* table_keys, int64_t cap, int64_t* slot,
+                                                            int32_t* flags, unsigned long long* counts) {
+  __shared__ unsigned long long lkey[kUbLds];
+  __shared__ long long lgslot[kUbLds];
+  const int t = threadIdx.x;
+  for (int j = t; j < kUbLds; j += kUbTile) lkey[j] = (unsigned long long)kEmpty;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kUbTile + t;
+  const bool valid = i < n;
+  int64_t phys = i;
+  if (F > 1 && valid) phys = (i % rows_b) * F + i / rows_b;  // feature-major tile
+  const int64_t key = valid ? keys[phys] : 0;
+  int lslot = 0;
+  bool lead = false;
+  if (valid) {
+    int h = (int)(mix64((uint64_t)key) & (kUbLds - 1));
     while (true) {
-      unsigned long long prev = atomicCAS(table_keys + h, (unsigned long long)kEmpty, (unsigned long long)key);
+      unsigned long long prev = atomicCAS(lkey + h, (unsigned long long)kEmpty, (unsigned long long)key);
       if (prev == (unsigned long long)kEmpty) {
-        flags[i] = 1;
-        slot[i] = h;
-        atomicAdd(counts + owner_of(bounds, P, key), 1ULL);
+        lead = true;
         break;
       }
-      if (prev == (unsigned long long)key) {
-        flags[i] = 0;
-        slot[i] = h;
-        break;
+      if (prev == (unsigned long long)key) break;
+      h = (h + 1) & (kUbLds - 1);
+    }
+    lslot = h;
+  }
+  __syncthreads();
+  bool claimed = false;
+  int owner = 0;
+  if (lead) {
+    const int64_t mask = cap - 1;
+    int64_t h = (int64_t)(mix64((uint64_t)key * 0x9e3779b97f4a7c15ULL) & (uint64_t)mask);
+    while (true) {
+      unsigned long long cur = __hip_atomic_load(table_keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == (unsigned long long)key) break;
+      if (cur == (unsigned long long)kEmpty) {
+        unsigned long long prev = atomicCAS(table_keys + h, (unsigned long long)kEmpty, (unsigned long long)key);
+        if (prev == (unsigned long long)kEmpty) {
+          claimed = true;
+          break;
+        }
+        if (prev == (unsigned long long)key) break;
       }
       h = (h + 1) & mask;
     }
+    lgslot[lslot] = h;
+    if (claimed) owner = owner_of(bounds, P, key);
+  }
+  wave_agg_inc(counts, owner, claimed);
+  __syncthreads();
+  if (valid) {
+    slot[phys] = lgslot[lslot];
+    flags[phys] = claimed ? 1 : 0;
   }
 }
 
@@ -68,13 +130,23 @@ __global__ void ub_assign_kernel(const int64_t* __restrict__ keys, int64_t n, co
     }
   }
   __syncthreads();
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (!flags[i]) continue;
-    const int64_t key = keys[i];
-    const int o = owner_of(bounds, P, key);
-    const int64_t pos = offs[o] + (int64_t)atomicAdd(cursor + o, 1ULL);
-    table_pos[slot[i]] = pos;
-    out_keys[pos] = key;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t iters = (n + stride - 1) / stride;
+  for (int64_t it = 0; it < iters; ++it) {
+    const int64_t i = it * stride + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const bool claimer = i < n && flags[i];
+    int64_t key = 0;
+    int o = 0;
+    if (claimer) {
+      key = keys[i];
+      o = owner_of(bounds, P, key);
+    }
+    const unsigned long long r = wave_agg_inc(cursor, o, claimer);
+    if (claimer) {
+      const int64_t pos = offs[o] + (int64_t)r;
+      table_pos[slot[i]] = pos;
+      out_keys[pos] = key;
+    }
   }
 }
 
@@ -84,9 +156,10 @@ __global__ void ub_inverse_kernel(int64_t n, const int64_t* __restrict__ slot, c
     inverse[i] = table_pos[slot[i]];
 }
 
-void unique_bucketize(const int64_t* keys, int64_t n, const int64_t* bounds, int P, int64_t* table_keys,
+void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s) {
+  if (F < 1 || n % F) throw std::runtime_error("unique_bucketize: n must be a multiple of F");
   if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
   if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
   MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0xFF, cap * sizeof(int64_t), s));
@@ -95,8 +168,9 @@ void unique_bucketize(const int64_t* keys, int64_t n, const int64_t* bounds, int
   if (n == 0) return;
   const int block = 256;
   const int grid = grid_for(n, block, 4096);
-  hipLaunchKernelGGL(ub_insert_kernel, grid, block, 0, s, keys, n, bounds, P, (unsigned long long*)table_keys, cap,
-                     slot, flags, (unsigned long long*)counts);
+  const int64_t tiles = (n + kUbTile - 1) / kUbTile;
+  hipLaunchKernelGGL(ub_insert_kernel, dim3((unsigned)tiles), dim3(kUbTile), 0, s, keys, n, n / F, F, bounds, P,
+                     (unsigned long long*)table_keys, cap, slot, flags, (unsigned long long*)counts);
   hipLaunchKernelGGL(ub_assign_kernel, grid, block, P * sizeof(int64_t), s, keys, n, bounds, P, slot, flags, counts,
                      (unsigned long long*)cursor, table_pos, out_keys);
   hipLaunchKernelGGL(ub_inverse_kernel, grid, block, 0, s, n, slot, table_pos, inverse);

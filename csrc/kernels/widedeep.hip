@@ -89,40 +89,73 @@ __global__ __launch_bounds__(256) void wd_head_kernel(const bf16_t* __restrict__
   }
   const float bias = bf2f(b0[0]);
   float dbl = 0.f, lossl = 0.f;
-  for (int64_t b = wave; b < B; b += nwaves) {
-    float h[PER_LANE];
-    const bf16_t* hp = H + b * Hd + lane * PER_LANE;
+  // S samples per iteration: their loads and wave reductions are independent (ILP), so a wave
+  // pays one L2 round trip per S samples instead of per sample.
+  constexpr int S = 4;
+  for (int64_t b0s = wave * S; b0s < B; b0s += nwaves * S) {
+    float h[S][PER_LANE];
+    float z[S];
 #pragma unroll
-    for (int j = 0; j < PER_LANE; ++j) h[j] = bf2f(hp[j]);
-    float z = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const int64_t b = b0s + s;
 #pragma unroll
-    for (int j = 0; j < PER_LANE; ++j) z += h[j] * wl[j];
-    z = warp_sum(z) + bias + wide[b];
-    const float label = y[b] > 0.5f ? 1.f : 0.f;
-    const float p = sigmoidf_(z);
-    const float dz = (p - label) * scale;
-    if (lane == 0) {
-      dwide[b] = dz;
-      dbl += dz;
-      lossl += fmaxf(z, 0.f) - z * label + log1pf(__expf(-fabsf(z)));
+      for (int j = 0; j < PER_LANE; ++j) h[s][j] = 0.f;
+      if (b < B) {
+        const bf16_t* hp = H + b * Hd + lane * PER_LANE;
+#pragma unroll
+        for (int j = 0; j < PER_LANE; ++j) h[s][j] = bf2f(hp[j]);
+      }
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < PER_LANE; ++j) acc += h[s][j] * wl[j];
+      z[s] = acc;
     }
-    bf16_t* dp = dH + b * Hd + lane * PER_LANE;
 #pragma unroll
-    for (int j = 0; j < PER_LANE; ++j) {
-      dwl[j] += dz * h[j];
-      const bf16_t g = f2bf(h[j] > 0.f ? dz * wl[j] : 0.f);
-      dp[j] = g;
-      csl[j] += bf2f(g);
+    for (int s = 0; s < S; ++s) z[s] = warp_sum(z[s]);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int64_t b = b0s + s;
+      if (b >= B) break;
+      const float zz = z[s] + bias + wide[b];
+      const float label = y[b] > 0.5f ? 1.f : 0.f;
+      const float p = sigmoidf_(zz);
+      const float dz = (p - label) * scale;
+      if (lane == 0) {
+        dwide[b] = dz;
+        dbl += dz;
+        lossl += fmaxf(zz, 0.f) - zz * label + log1pf(__expf(-fabsf(zz)));
+      }
+      bf16_t* dp = dH + b * Hd + lane * PER_LANE;
+#pragma unroll
+      for (int j = 0; j < PER_LANE; ++j) {
+        dwl[j] += dz * h[s][j];
+        const bf16_t g = f2bf(h[s][j] > 0.f ? dz * wl[j] : 0.f);
+        dp[j] = g;
+        csl[j] += bf2f(g);
+      }
     }
   }
+  // reduce the 4 waves of the block in LDS, then one global atomic per column per block
+  __shared__ float red[2][4][64 * PER_LANE];
+  __shared__ float red_s[2][4];
+  const int wv = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < PER_LANE; ++j) {
-    atomicAdd(dw + lane * PER_LANE + j, dwl[j]);
-    if (colsum) atomicAdd(colsum + lane * PER_LANE + j, csl[j]);
+    red[0][wv][lane * PER_LANE + j] = dwl[j];
+    red[1][wv][lane * PER_LANE + j] = csl[j];
   }
   if (lane == 0) {
-    atomicAdd(db, dbl);
-    atomicAdd(loss_sum, lossl);
+    red_s[0][wv] = dbl;
+    red_s[1][wv] = lossl;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 64 * PER_LANE; c += blockDim.x) {
+    atomicAdd(dw + c, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
+    if (colsum) atomicAdd(colsum + c, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(db, red_s[0][0] + red_s[0][1] + red_s[0][2] + red_s[0][3]);
+    atomicAdd(loss_sum, red_s[1][0] + red_s[1][1] + red_s[1][2] + red_s[1][3]);
   }
 }
 
@@ -131,7 +164,7 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
              float grad_scale, hipStream_t s) {
   if (B <= 0) return;
   const int block = 256;
-  const int grid = (int)std::min<int64_t>(256, (B + 3) / 4);
+  const int grid = (int)std::min<int64_t>(128, (B + 15) / 16);  // per-block LDS reduction, then atomics
   switch (Hd) {
     case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
     case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
@@ -142,30 +175,84 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
-// One thread per (sample, feature, column): consecutive lanes add consecutive columns of a
-// row, so each wave-instruction is two contiguous 128-B row segments at D = 32 (the
-// full-rate float-atomic shape on gfx950).
-__global__ void wd_emb_backward_kernel(const float* __restrict__ dX, int ldx, const float* __restrict__ dwide,
-                                       const int64_t* __restrict__ inv, int64_t B, int F, int D,
-                                       float* __restrict__ grad_rows, int row_stride) {
-  const int64_t total = B * F * D;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t bf = c / D;
-    const int d = (int)(c - bf * D);
-    const int64_t b = bf / F;
-    const int f = (int)(bf - b * F);
-    const int64_t row = inv[bf];
-    atomicAdd(grad_rows + row * row_stride + d, dX[b * ldx + f * D + d]);
-    if (d == 0) atomicAdd(grad_rows + row * row_stride + D, dwide[b]);
+// Embedding backward with block-local dedupe: a block owns TB consecutive samples of ONE
+// feature, dedupes their unique-row ids in an LDS hash (compact ids by an LDS counter), sums
+// the gradient vectors of duplicates with LDS float atomics, and issues ONE global atomic per
+// distinct row per tile. Zipf-hot rows (e.g. a 3-value feature hit by every sample) would
+// otherwise serialise thousands of same-address global atomics. Work is linearised over
+// (lookup, column) so every wave-instruction touches contiguous row segments.
+constexpr int kEmbTB = 256;
+constexpr int kEmbHash = 512;
+
+__global__ __launch_bounds__(kEmbTB) void wd_emb_backward_kernel(const float* __restrict__ dX, int ldx,
+                                                                 const float* __restrict__ dwide,
+                                                                 const int64_t* __restrict__ inv, int64_t B, int F,
+                                                                 int D, float* __restrict__ grad_rows,
+                                                                 int row_stride) {
+  __shared__ int hkey[kEmbHash];
+  __shared__ int hidx[kEmbHash];
+  __shared__ int cidx[kEmbTB];
+  __shared__ int rowof[kEmbTB];
+  __shared__ int nd;
+  extern __shared__ float acc[];  // [distinct][W]
+  const int t = threadIdx.x;
+  const int f = blockIdx.y;
+  const int64_t b0 = (int64_t)blockIdx.x * kEmbTB;
+  const int W = D + 1;
+  const int nb = (int)min((int64_t)kEmbTB, B - b0);
+  for (int j = t; j < kEmbHash; j += kEmbTB) hkey[j] = -1;
+  if (t == 0) nd = 0;
+  __syncthreads();
+  int myslot = -1;
+  bool lead = false;
+  int r = -1;
+  if (t < nb) {
+    r = (int)inv[(b0 + t) * F + f];
+    int h = (int)((uint32_t)r * 2654435761u >> 23) & (kEmbHash - 1);
+    while (true) {
+      const int prev = atomicCAS(hkey + h, -1, r);
+      if (prev == -1) {
+        lead = true;
+        break;
+      }
+      if (prev == r) break;
+      h = (h + 1) & (kEmbHash - 1);
+    }
+    myslot = h;
+  }
+  __syncthreads();
+  if (lead) {
+    const int id = atomicAdd(&nd, 1);
+    hidx[myslot] = id;
+    rowof[id] = r;
+  }
+  __syncthreads();
+  if (t < nb) cidx[t] = hidx[myslot];
+  const int ndist = nd;
+  for (int i = t; i < ndist * W; i += kEmbTB) acc[i] = 0.f;
+  __syncthreads();
+  // deep part: element e = (lookup k, column d)
+  for (int e = t; e < nb * D; e += kEmbTB) {
+    const int k = e / D, d = e - k * D;
+    atomicAdd(acc + cidx[k] * W + d, dX[(b0 + k) * ldx + (int64_t)f * D + d]);
+  }
+  if (t < nb) atomicAdd(acc + cidx[t] * W + D, dwide[b0 + t]);
+  __syncthreads();
+  for (int e = t; e < ndist * W; e += kEmbTB) {
+    const int k = e / W, d = e - k * W;
+    atomicAdd(grad_rows + (int64_t)rowof[k] * row_stride + d, acc[e]);
   }
 }
 
 void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                      float* grad_rows, int row_stride, hipStream_t s) {
   if (B <= 0) return;
-  const int block = 256;
-  hipLaunchKernelGGL(wd_emb_backward_kernel, grid_for(B * F * D, block, 8192), block, 0, s, dX, ldx, dwide, inv, B, F,
-                     D, grad_rows, row_stride);
+  if (row_stride < D + 1) throw std::runtime_error("wd_emb_backward: row_stride < D + 1");
+  const size_t lds = (size_t)kEmbTB * (D + 1) * sizeof(float);
+  if (lds > 96 * 1024) throw std::runtime_error("wd_emb_backward: D too large");
+  dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);
+  hipLaunchKernelGGL(wd_emb_backward_kernel, grid, dim3(kEmbTB), lds, s, dX, ldx, dwide, inv, B, F, D, grad_rows,
+                     row_stride);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

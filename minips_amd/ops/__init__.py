@@ -92,14 +92,15 @@ def linear_wgrad(dy, x, dw, split_k=None):
 
 
 # ----------------------------------------------------------------------------- sparse keys
-def unique_bucketize(keys: torch.Tensor, bounds: torch.Tensor):
+def unique_bucketize(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1):
     """Dedupe ``keys`` and group the unique keys by owner shard.
 
     Returns (uniq [n] with the first sum(counts) valid, inverse [n], counts [P]) where
-    ``bounds`` [P+1] are the shard key boundaries and uniq[inverse[i]] == keys[i].
+    ``bounds`` [P+1] are the shard key boundaries and uniq[inverse[i]] == keys[i]. ``F`` > 1
+    declares the flat keys as a [B, F] batch (the GPU kernel then dedupes feature-major tiles).
     """
     if _gpu(keys):
-        uniq, inv, counts = kernels().unique_bucketize(keys.contiguous(), bounds.contiguous())
+        uniq, inv, counts = kernels().unique_bucketize(keys.contiguous(), bounds.contiguous(), int(F))
         return uniq, inv, counts
     u, inv = torch.unique(keys, sorted=True, return_inverse=True)
     owner = torch.bucketize(u, bounds[1:-1], right=True)

@@ -240,8 +240,9 @@ class SparseTable:
 
     # -- KV API -----------------------------------------------------------------------------
     def plan(self, keys: torch.Tensor) -> SparsePlan:
+        F = keys.shape[1] if keys.dim() == 2 else 1
         keys = keys.reshape(-1).to(torch.int64)
-        uniq, inv, counts = ops.unique_bucketize(keys, self.bounds)
+        uniq, inv, counts = ops.unique_bucketize(keys, self.bounds, F)
         send, recv = self.comm.exchange_counts(counts)
         U = int(sum(send))
         M = int(sum(recv))

@@ -151,7 +151,7 @@ def build_ops_py(kobjs: list[str]) -> str:
     bobj = os.path.join(OBJ, "ops_py.o")
     cflags, ldflags = _torch_flags()
     hdrs = _headers("csrc/kernels", "csrc/bindings")
-    _compile_many([(bobj, [src] + hdrs, [HIPCC, "-O2", "-std=c++17", "-fPIC", *cflags, "-c", src, "-o", bobj])])
+    _compile_many([(bobj, [src] + hdrs, [HIPCC, "-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", *cflags, "-c", src, "-o", bobj])])
     _compile_many([(out, [bobj] + kobjs,
                     [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", bobj, *kobjs, "-o", out, *ldflags])])
     return out
