@@ -17,6 +17,7 @@
 // 32-wide step is permuted identically on both sides so that each 32-lane half reads 8
 // consecutive LDS rows (bank-conflict free with the 288-B row pitch).
 // Block ids are remapped so that consecutive tiles of one row panel share an XCD (T1).
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -27,26 +28,31 @@ namespace minips_k {
 
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 
-constexpr int BM = 128, BN = 128, BK = 32;
-constexpr int LDS_ROW = BK + 8;     // [row][k] pitch in bf16 (80 B)
-constexpr int LDS_TR = BM + 16;     // [k][row] pitch in bf16 (288 B)
-constexpr int TILE_ELEMS = (BM * LDS_ROW > BK * LDS_TR) ? BM * LDS_ROW : BK * LDS_TR;
+constexpr int BM = 128, BN = 128;
+
+template <int BK>
+struct Lds {
+  static constexpr int ROW = BK + 8;   // [row][k] pitch in bf16 (80 B at BK=32, 144 B at BK=64)
+  static constexpr int TR = BM + 16;   // [k][row] pitch in bf16 (288 B)
+  static constexpr int TILE = (BM * ROW > BK * TR) ? BM * ROW : BK * TR;
+  static constexpr int CHUNKS = BM * BK / 8 / 256;  // 16-byte chunks per thread per operand tile
+};
 
 __device__ __forceinline__ v4s ds_read_tr16(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
-// Loads one BMxBK (or BKxBM) tile chunk set into registers: 2 x 16 B per thread.
-template <bool KMAJOR>
+// Loads one BMxBK (or BKxBM) tile into registers: CHUNKS x 16 B per thread.
+template <int BK, bool KMAJOR>
 __device__ __forceinline__ void load_tile(const bf16_t* __restrict__ G, int ld, int row0, int k0, int rows, int K,
-                                          int tid, uint4 (&r)[2]) {
+                                          int tid, uint4 (&r)[Lds<BK>::CHUNKS]) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < Lds<BK>::CHUNKS; ++h) {
     int c = tid + h * 256;
     int row, k;
     if (!KMAJOR) {
-      row = c >> 2;
-      k = (c & 3) * 8;
+      row = c / (BK / 8);
+      k = (c % (BK / 8)) * 8;
     } else {
       k = c >> 4;
       row = (c & 15) * 8;
@@ -58,35 +64,37 @@ __device__ __forceinline__ void load_tile(const bf16_t* __restrict__ G, int ld, 
   }
 }
 
-template <bool KMAJOR>
-__device__ __forceinline__ void store_tile(bf16_t* S, int tid, const uint4 (&r)[2]) {
+template <int BK, bool KMAJOR>
+__device__ __forceinline__ void store_tile(bf16_t* S, int tid, const uint4 (&r)[Lds<BK>::CHUNKS]) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < Lds<BK>::CHUNKS; ++h) {
     int c = tid + h * 256;
     if (!KMAJOR) {
-      *reinterpret_cast<uint4*>(S + (c >> 2) * LDS_ROW + (c & 3) * 8) = r[h];
+      *reinterpret_cast<uint4*>(S + (c / (BK / 8)) * Lds<BK>::ROW + (c % (BK / 8)) * 8) = r[h];
     } else {
-      *reinterpret_cast<uint4*>(S + (c >> 4) * LDS_TR + (c & 15) * 8) = r[h];
+      *reinterpret_cast<uint4*>(S + (c >> 4) * Lds<BK>::TR + (c & 15) * 8) = r[h];
     }
   }
 }
 
-// Fragment of the 16x16x32 operand: 8 bf16 along k for row `row` (A) / column (B).
-template <bool KMAJOR, bool PERM>
-__device__ __forceinline__ v8s read_frag(const bf16_t* S, int row_base, int lane) {
+// Fragment of the 16x16x32 operand for k sub-step `ks` (k in [32ks, 32ks+32)): 8 bf16 along
+// k for row `row_base + lane&15` (A) / column (B).
+template <int BK, bool KMAJOR, bool PERM>
+__device__ __forceinline__ v8s read_frag(const bf16_t* S, int row_base, int ks, int lane) {
   int g = lane >> 4;
   if (!KMAJOR) {
     int row = row_base + (lane & 15);
-    if (!PERM) return *reinterpret_cast<const v8s*>(S + row * LDS_ROW + 8 * g);
-    v4s lo = *reinterpret_cast<const v4s*>(S + row * LDS_ROW + 4 * g);
-    v4s hi = *reinterpret_cast<const v4s*>(S + row * LDS_ROW + 16 + 4 * g);
+    const bf16_t* p = S + row * Lds<BK>::ROW + 32 * ks;
+    if (!PERM) return *reinterpret_cast<const v8s*>(p + 8 * g);
+    v4s lo = *reinterpret_cast<const v4s*>(p + 4 * g);
+    v4s hi = *reinterpret_cast<const v4s*>(p + 16 + 4 * g);
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   } else {
     int i = lane & 15, q = i >> 2, p = i & 3;
-    int r0 = PERM ? 4 * g : 8 * g;
-    int r1 = PERM ? 16 + 4 * g : 8 * g + 4;
-    v4s lo = ds_read_tr16(S + (r0 + q) * LDS_TR + row_base + 4 * p);
-    v4s hi = ds_read_tr16(S + (r1 + q) * LDS_TR + row_base + 4 * p);
+    int r0 = 32 * ks + (PERM ? 4 * g : 8 * g);
+    int r1 = 32 * ks + (PERM ? 16 + 4 * g : 8 * g + 4);
+    v4s lo = ds_read_tr16(S + (r0 + q) * Lds<BK>::TR + row_base + 4 * p);
+    v4s hi = ds_read_tr16(S + (r1 + q) * Lds<BK>::TR + row_base + 4 * p);
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
@@ -101,12 +109,12 @@ struct EpiArgs {
   float alpha;
 };
 
-template <bool A_KM, bool B_KN, int EPI>
+template <int BK, bool A_KM, bool B_KN, int EPI>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         int M, int N, int K, int lda, int ldb, int k_chunk,
                                                         EpiArgs ep) {
   constexpr bool PERM = A_KM && B_KN;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][TILE_ELEMS];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][Lds<BK>::TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
@@ -131,37 +139,43 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[2], rb[2];
+  // One register set: tile t+1's global loads are issued before tile t's MFMAs and written
+  // to the other LDS buffer after them (T14 split). (A 2-deep register ring measured slower:
+  // the extra 32-64 VGPRs halve occupancy, which hides more latency than the ring.)
+  uint4 ra[Lds<BK>::CHUNKS], rb[Lds<BK>::CHUNKS];
   int cur = 0;
   if (kb < ke) {
-    load_tile<A_KM>(A, lda, m0, kb, M, ke, tid, ra);
-    load_tile<B_KN>(B, ldb, n0, kb, N, ke, tid, rb);
-    store_tile<A_KM>(smem[0][0], tid, ra);
-    store_tile<B_KN>(smem[0][1], tid, rb);
+    load_tile<BK, A_KM>(A, lda, m0, kb, M, ke, tid, ra);
+    load_tile<BK, B_KN>(B, ldb, n0, kb, N, ke, tid, rb);
+    store_tile<BK, A_KM>(smem[0][0], tid, ra);
+    store_tile<BK, B_KN>(smem[0][1], tid, rb);
   }
   __syncthreads();
   for (int k0 = kb; k0 < ke; k0 += BK) {
     const bool has_next = k0 + BK < ke;
-    if (has_next) {  // issue next tile's global loads before the MFMAs (T14 split)
-      load_tile<A_KM>(A, lda, m0, k0 + BK, M, ke, tid, ra);
-      load_tile<B_KN>(B, ldb, n0, k0 + BK, N, ke, tid, rb);
+    if (has_next) {
+      load_tile<BK, A_KM>(A, lda, m0, k0 + BK, M, ke, tid, ra);
+      load_tile<BK, B_KN>(B, ldb, n0, k0 + BK, N, ke, tid, rb);
     }
     const bf16_t* SA = smem[cur][0];
     const bf16_t* SB = smem[cur][1];
-    v8s af[4], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = read_frag<A_KM, PERM>(SA, wm * 64 + i * 16, lane);
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      v8s af[4], bfr[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = read_frag<B_KN, PERM>(SB, wn * 64 + j * 16, lane);
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<BK, A_KM, PERM>(SA, wm * 64 + i * 16, ks, lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BK, B_KN, PERM>(SB, wn * 64 + j * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i]),
-                                                            __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i]),
+                                                              __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+    }
     if (has_next) {
-      store_tile<A_KM>(smem[cur ^ 1][0], tid, ra);
-      store_tile<B_KN>(smem[cur ^ 1][1], tid, rb);
+      store_tile<BK, A_KM>(smem[cur ^ 1][0], tid, ra);
+      store_tile<BK, B_KN>(smem[cur ^ 1][1], tid, rb);
     }
     __syncthreads();
     cur ^= 1;
@@ -219,10 +233,22 @@ template <bool A_KM, bool B_KN, int EPI>
 static void launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, int split_k,
                    const EpiArgs& ep, hipStream_t s) {
   int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  int kc = ((K + split_k - 1) / split_k + BK - 1) / BK * BK;
+  // BK=64 halves the barriers per FLOP; short K chunks keep BK=32 (less tail waste).
+  const int kper = (K + split_k - 1) / split_k;
+  static const int forced = [] {
+    const char* e = std::getenv("MINIPS_GEMM_BK");
+    return e ? std::atoi(e) : 0;
+  }();
+  // measured: BK=64 wins on the forward/dgrad shapes, BK=32 on the split-K wgrad (tr-read) shapes
+  const bool bk64 = forced ? forced == 64 : (kper >= 256 && !(A_KM && B_KN));
+  const int BKs = bk64 ? 64 : 32;
+  int kc = (kper + BKs - 1) / BKs * BKs;
   int nsplit = (K + kc - 1) / kc;
   dim3 grid(tiles, 1, nsplit);
-  hipLaunchKernelGGL((gemm_bf16_kernel<A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
+  if (bk64)
+    hipLaunchKernelGGL((gemm_bf16_kernel<64, A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<32, A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
 }
 
 #define MINIPS_GEMM_EPI_DISPATCH(AKM, BKN)                                                        \

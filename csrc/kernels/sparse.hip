@@ -64,8 +64,10 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
                                                             int32_t* flags, unsigned long long* counts) {
   __shared__ unsigned long long lkey[kUbLds];
   __shared__ long long lgslot[kUbLds];
+  __shared__ unsigned int lcount[256];  // per-owner claims of this block (P <= 256)
   const int t = threadIdx.x;
   for (int j = t; j < kUbLds; j += kUbTile) lkey[j] = (unsigned long long)kEmpty;
+  for (int p = t; p < P; p += kUbTile) lcount[p] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kUbTile + t;
   const bool valid = i < n;
@@ -107,22 +109,37 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
       h = (h + 1) & mask;
     }
     lgslot[lslot] = h;
-    if (claimed) owner = owner_of(bounds, P, key);
+    if (claimed) {
+      owner = owner_of(bounds, P, key);
+      atomicAdd(lcount + owner, 1u);
+    }
   }
-  wave_agg_inc(counts, owner, claimed);
   __syncthreads();
+  for (int p = t; p < P; p += kUbTile)
+    if (lcount[p]) atomicAdd(counts + p, (unsigned long long)lcount[p]);
   if (valid) {
     slot[phys] = lgslot[lslot];
     flags[phys] = claimed ? 1 : 0;
   }
 }
 
-__global__ void ub_assign_kernel(const int64_t* __restrict__ keys, int64_t n, const int64_t* __restrict__ bounds,
-                                 int P, const int64_t* __restrict__ slot, const int32_t* __restrict__ flags,
-                                 const int64_t* __restrict__ counts, unsigned long long* cursor, int64_t* table_pos,
-                                 int64_t* out_keys) {
-  extern __shared__ int64_t offs[];  // exclusive prefix of counts
-  if (threadIdx.x == 0) {
+// Position assignment: one element per thread; ranks inside the block come from LDS
+// counters and each block takes ONE global atomic per owner shard for its base, so the
+// shared cursor sees (#blocks x P) atomics instead of one per unique key.
+constexpr int kUbMaxP = 256;
+
+__global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restrict__ keys, int64_t n,
+                                                        const int64_t* __restrict__ bounds, int P,
+                                                        const int64_t* __restrict__ slot,
+                                                        const int32_t* __restrict__ flags,
+                                                        const int64_t* __restrict__ counts, unsigned long long* cursor,
+                                                        int64_t* table_pos, int64_t* out_keys) {
+  __shared__ int64_t offs[kUbMaxP];
+  __shared__ unsigned int lcnt[kUbMaxP];
+  __shared__ unsigned long long lbase[kUbMaxP];
+  const int t = threadIdx.x;
+  for (int p = t; p < P; p += blockDim.x) lcnt[p] = 0;
+  if (t == 0) {
     int64_t acc = 0;
     for (int p = 0; p < P; ++p) {
       offs[p] = acc;
@@ -130,23 +147,24 @@ __global__ void ub_assign_kernel(const int64_t* __restrict__ keys, int64_t n, co
     }
   }
   __syncthreads();
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t iters = (n + stride - 1) / stride;
-  for (int64_t it = 0; it < iters; ++it) {
-    const int64_t i = it * stride + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const bool claimer = i < n && flags[i];
-    int64_t key = 0;
-    int o = 0;
-    if (claimer) {
-      key = keys[i];
-      o = owner_of(bounds, P, key);
-    }
-    const unsigned long long r = wave_agg_inc(cursor, o, claimer);
-    if (claimer) {
-      const int64_t pos = offs[o] + (int64_t)r;
-      table_pos[slot[i]] = pos;
-      out_keys[pos] = key;
-    }
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + t;
+  const bool claimer = i < n && flags[i];
+  int64_t key = 0;
+  int o = 0;
+  unsigned int r = 0;
+  if (claimer) {
+    key = keys[i];
+    o = owner_of(bounds, P, key);
+    r = atomicAdd(lcnt + o, 1u);
+  }
+  __syncthreads();
+  for (int p = t; p < P; p += blockDim.x)
+    lbase[p] = lcnt[p] ? atomicAdd(cursor + p, (unsigned long long)lcnt[p]) : 0ULL;
+  __syncthreads();
+  if (claimer) {
+    const int64_t pos = offs[o] + (int64_t)lbase[o] + (int64_t)r;
+    table_pos[slot[i]] = pos;
+    out_keys[pos] = key;
   }
 }
 
@@ -160,6 +178,7 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s) {
   if (F < 1 || n % F) throw std::runtime_error("unique_bucketize: n must be a multiple of F");
+  if (P < 1 || P > kUbMaxP) throw std::runtime_error("unique_bucketize: 1 <= P <= 256 owner shards");
   if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
   if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
   MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0xFF, cap * sizeof(int64_t), s));
@@ -171,8 +190,8 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
   const int64_t tiles = (n + kUbTile - 1) / kUbTile;
   hipLaunchKernelGGL(ub_insert_kernel, dim3((unsigned)tiles), dim3(kUbTile), 0, s, keys, n, n / F, F, bounds, P,
                      (unsigned long long*)table_keys, cap, slot, flags, (unsigned long long*)counts);
-  hipLaunchKernelGGL(ub_assign_kernel, grid, block, P * sizeof(int64_t), s, keys, n, bounds, P, slot, flags, counts,
-                     (unsigned long long*)cursor, table_pos, out_keys);
+  hipLaunchKernelGGL(ub_assign_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, keys, n, bounds, P, slot,
+                     flags, counts, (unsigned long long*)cursor, table_pos, out_keys);
   hipLaunchKernelGGL(ub_inverse_kernel, grid, block, 0, s, n, slot, table_pos, inverse);
   MINIPS_HIP_CHECK(hipGetLastError());
 }

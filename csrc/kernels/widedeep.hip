@@ -10,14 +10,24 @@
 
 namespace minips_k {
 
-// One thread per (sample, 8-column chunk): a 16-byte store of 8 bf16.
+// One thread per (sample, 8-column chunk): a 16-byte store of 8 bf16; threads past the
+// chunks compute the per-sample wide sums (one thread per sample) so no thread serialises.
 __global__ void wd_assemble_kernel(const float* __restrict__ dense, int n_dense, const bf16_t* __restrict__ rows,
                                    int row_stride, const int64_t* __restrict__ inv, int64_t B, int F, int D,
-                                   bf16_t* __restrict__ X, int ldx, float* __restrict__ wide_logit) {
+                                   bf16_t* __restrict__ X, int ldx, float* __restrict__ wide_logit, int ones_col) {
   const int chunks = ldx >> 3;
   const int emb_cols = F * D;
   const int64_t total = B * chunks;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total + B;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    if (c >= total) {
+      const int64_t b = c - total;
+      float w = 0.f;
+      const int64_t* iv = inv + b * F;
+      for (int f = 0; f < F; ++f) w += bf2f(rows[iv[f] * row_stride + D]);
+      wide_logit[b] = w;
+      continue;
+    }
     const int64_t b = c / chunks;
     const int col0 = (int)(c - b * chunks) * 8;
     uint32_t packed[4];
@@ -42,30 +52,26 @@ __global__ void wd_assemble_kernel(const float* __restrict__ dense, int n_dense,
         } else if (col < emb_cols + n_dense) {
           v[j] = dense[b * n_dense + (col - emb_cols)];
         } else {
-          v[j] = 0.f;
+          v[j] = col == ones_col ? 1.f : 0.f;
         }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) packed[j] = pack_bf2(v[2 * j], v[2 * j + 1]);
     }
     *reinterpret_cast<uint4*>(X + b * ldx + col0) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
-    if (col0 == 0) {
-      float w = 0.f;
-      for (int f = 0; f < F; ++f) w += bf2f(rows[inv[b * F + f] * row_stride + D]);
-      wide_logit[b] = w;
-    }
   }
 }
 
 void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B,
-                 int F, int D, bf16_t* X, int ldx, float* wide_logit, hipStream_t s) {
+                 int F, int D, bf16_t* X, int ldx, float* wide_logit, int ones_col, hipStream_t s) {
   if (ldx % 8) throw std::runtime_error("wd_assemble: ldx must be a multiple of 8");
   if (F * D + n_dense > ldx) throw std::runtime_error("wd_assemble: ldx too small");
+  if (ones_col >= ldx) throw std::runtime_error("wd_assemble: ones_col out of range");
   if (row_stride % 4) throw std::runtime_error("wd_assemble: row_stride must be a multiple of 4");
   if (B <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(wd_assemble_kernel, grid_for(B * (ldx / 8), block, 8192), block, 0, s, dense, n_dense, rows,
-                     row_stride, inv, B, F, D, X, ldx, wide_logit);
+  hipLaunchKernelGGL(wd_assemble_kernel, grid_for(B * (ldx / 8 + 1), block, 8192), block, 0, s, dense, n_dense, rows,
+                     row_stride, inv, B, F, D, X, ldx, wide_logit, ones_col);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -5,12 +5,13 @@ Parameters
   sparse table  one row per categorical id (sum of the 26 cardinalities, 33.8M rows):
                 [32-dim deep embedding | 1 wide weight | 3 pad], row-wise Adagrad with a
                 separate accumulator for the deep part and for the wide weight.
-  dense table   deep tower Linear(848->1024)->ReLU->Linear(1024->512)->ReLU->
-                Linear(512->256)->ReLU->Linear(256->1), one flat fp32 master vector, Adam.
+  dense table   deep tower Linear(845->1024)->ReLU->Linear(1024->512)->ReLU->
+                Linear(512->256)->ReLU->Linear(256->1), one flat fp32 master vector, Adam;
+                biases are folded into the weight matrices (constant-1 input column).
 Step (every kernel is a gfx950 HIP kernel; comm is RCCL):
   sparse Get -> wd_assemble (lookup + dense concat + wide sum) -> 3 MFMA GEMMs (bias+ReLU
-  fused) -> wd_head (last layer + BCE fwd/bwd fused) -> per layer wgrad GEMM (split-K) +
-  dgrad GEMM (ReLU mask + bias-grad colsum fused) -> wd_emb_backward (segment sum into unique
+  fused) -> wd_head (last layer + BCE fwd/bwd fused) -> per layer wgrad GEMM (split-K, the
+  bias gradient falls out of the ones column) + dgrad GEMM (ReLU mask fused) -> wd_emb_backward (segment sum into unique
   rows) -> sparse Add + dense Add -> Clock (all-to-all / reduce-scatter, fused optimizers,
   all-gather).
 """
@@ -45,7 +46,7 @@ class WideDeepConfig:
 
     @property
     def in_dim(self):
-        k = self.F * self.emb_dim + self.n_dense
+        k = self.F * self.emb_dim + self.n_dense + 1  # + constant-1 bias column
         return (k + 7) // 8 * 8
 
 
@@ -65,20 +66,19 @@ class WideDeep:
                                init_std=0.01, seed=cfg.seed)
         # wide weights start at zero (columns >= D)
         self.emb.shard[:, D:].zero_()
-        # dense layout: [W1 b1 W2 b2 W3 b3 w4 b4], every segment 8-element aligned
-        dims = [cfg.in_dim, *cfg.hidden]
+        # Dense layout: each Linear is stored as W_ext [n_out, k_pad] with the bias in column
+        # k_in (k_pad = align8(k_in + 1)); activations carry a constant-1 column at k_in. The
+        # forward GEMM then adds the bias for free and the weight-gradient GEMM produces the
+        # bias gradient in that column -- no bias epilogue, no column-sum atomics.
+        self.k_in = [cfg.F * cfg.emb_dim + cfg.n_dense, *cfg.hidden[:-1]]
+        self.k_pad = [_align(k + 1) for k in self.k_in]
         self.layout = {}
         off = 0
-        for i in range(len(cfg.hidden)):
-            n_out, n_in = dims[i + 1], dims[i]
-            self.layout[f"W{i + 1}"] = (off, (n_out, n_in))
-            off += _align(n_out * n_in)
-            self.layout[f"b{i + 1}"] = (off, (n_out,))
-            off += _align(n_out)
-        self.layout["w4"] = (off, (cfg.hidden[-1],))
-        off += _align(cfg.hidden[-1])
-        self.layout["b4"] = (off, (1,))
-        off += 8
+        for i, n_out in enumerate(cfg.hidden):
+            self.layout[f"W{i + 1}"] = (off, (n_out, self.k_pad[i]))
+            off += _align(n_out * self.k_pad[i])
+        self.layout["w4"] = (off, (cfg.hidden[-1] + 8,))  # [w4 | b4 | pad]
+        off += cfg.hidden[-1] + 8
         self.n_params = off
         self.dense = DenseTable(comm, self.n_params, optimizer="adam", lr=cfg.lr_dense,
                                 consistency=cfg.consistency, staleness=cfg.staleness, table_id=1)
@@ -89,15 +89,12 @@ class WideDeep:
         g = torch.Generator(device="cpu")
         g.manual_seed(self.cfg.seed + 17)
         full = torch.zeros(self.n_params, dtype=torch.float32)
-        dims = [self.cfg.in_dim, *self.cfg.hidden]
         for i in range(len(self.cfg.hidden)):
-            off, shape = self.layout[f"W{i + 1}"]
-            w = full[off: off + shape[0] * shape[1]].view(shape)
-            ops.kaiming_uniform_(w, dims[i], g)
-            if i == 0:  # padded input columns carry no signal
-                w[:, self.cfg.F * self.cfg.emb_dim + self.cfg.n_dense:] = 0
-        off, shape = self.layout["w4"]
-        ops.kaiming_uniform_(full[off: off + shape[0]], shape[0], g)
+            w = self.view(full, f"W{i + 1}")
+            ops.kaiming_uniform_(w[:, : self.k_in[i]], self.k_in[i], g)
+            w[:, self.k_in[i]:] = 0  # bias column and padding start at zero
+        h = self.cfg.hidden[-1]
+        ops.kaiming_uniform_(self.view(full, "w4")[:h], h, g)
         return full.to(dev)
 
     def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
@@ -112,8 +109,14 @@ class WideDeep:
             dev, cfg = self.comm.device, self.cfg
             bf = dict(dtype=torch.bfloat16, device=dev)
             h1, h2, h3 = cfg.hidden
+
+            def ext(n, k_in):  # activation with the constant-1 column at k_in, zero padding
+                t = torch.zeros(B, _align(k_in + 1), **bf)
+                t[:, k_in] = 1.0
+                return t
+
             self._bufs[B] = dict(
-                X=torch.empty(B, cfg.in_dim, **bf), H1=torch.empty(B, h1, **bf), H2=torch.empty(B, h2, **bf),
+                X=ext(self.k_in[0], self.k_in[0]), H1=ext(h1, h1), H2=ext(h2, h2),
                 H3=torch.empty(B, h3, **bf), dH3=torch.empty(B, h3, **bf), dH2=torch.empty(B, h2, **bf),
                 dH1=torch.empty(B, h1, **bf),
                 dX=torch.empty(B, cfg.F * cfg.emb_dim, dtype=torch.float32, device=dev),
@@ -123,18 +126,22 @@ class WideDeep:
             )
         return self._bufs[B]
 
+    def _forward(self, b, P):
+        ops.linear_fwd(b["X"], self.view(P, "W1"), None, "relu", out=b["H1"])
+        ops.linear_fwd(b["H1"], self.view(P, "W2"), None, "relu", out=b["H2"])
+        ops.linear_fwd(b["H2"], self.view(P, "W3"), None, "relu", out=b["H3"])
+
     def forward(self, dense, keys, rows, plan):
         """Forward only (eval): returns logits [B] fp32."""
         B = dense.shape[0]
         b = self._buffers(B)
         P = self.dense.get()
         F, D = self.cfg.F, self.cfg.emb_dim
-        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"])
-        x = b["X"]
-        for i, h in enumerate(("H1", "H2", "H3")):
-            ops.linear_fwd(x, self.view(P, f"W{i + 1}"), self.view(P, f"b{i + 1}"), "relu", out=b[h])
-            x = b[h]
-        return x.float() @ self.view(P, "w4").float() + self.view(P, "b4").float() + b["wide"]
+        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0])
+        self._forward(b, P)
+        h = self.cfg.hidden[-1]
+        w4 = self.view(P, "w4").float()
+        return b["H3"].float() @ w4[:h] + w4[h] + b["wide"]
 
     def train_step(self, dense, keys, labels) -> torch.Tensor:
         """One BSP superstep: Get, forward, backward, Add, Clock. Returns the summed loss
@@ -142,22 +149,22 @@ class WideDeep:
         cfg = self.cfg
         B = dense.shape[0]
         F, D = cfg.F, cfg.emb_dim
+        h = cfg.hidden[-1]
         b = self._buffers(B)
         rows, plan = self.emb.get(keys)
         P = self.dense.get()
         G = self.dense.grad
-        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"])
-        ops.linear_fwd(b["X"], self.view(P, "W1"), self.view(P, "b1"), "relu", out=b["H1"])
-        ops.linear_fwd(b["H1"], self.view(P, "W2"), self.view(P, "b2"), "relu", out=b["H2"])
-        ops.linear_fwd(b["H2"], self.view(P, "W3"), self.view(P, "b3"), "relu", out=b["H3"])
+        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0])
+        self._forward(b, P)
         b["loss"].zero_()
         scale = 1.0 / (B * self.comm.world)
-        ops.wd_head(b["H3"], self.view(P, "w4"), self.view(P, "b4"), b["wide"], labels, b["dH3"],
-                    self.view(G, "w4"), self.view(G, "b4"), b["dwide"], b["loss"], self.view(G, "b3"), scale)
+        w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
+        ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1], b["dwide"],
+                    b["loss"], None, scale)
         ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
-        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], colsum=self.view(G, "b2"), out=b["dH2"])
+        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=self.k_in[2], out=b["dH2"])
         ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
-        ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], colsum=self.view(G, "b1"), out=b["dH1"])
+        ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
         ops.linear_dgrad(b["dH1"], self.view(P, "W1"), out_f32=True, n_cols=F * D, out=b["dX"])
         grad_rows = torch.zeros(max(plan.U, 1), cfg.row_width, dtype=torch.float32, device=self.comm.device)

@@ -180,16 +180,19 @@ def embedding_bag_bwd(grad_out, idx, offsets, grad_rows, mean=False):
 
 
 # ----------------------------------------------------------------------------- Wide&Deep
-def wd_assemble(dense, rows, inv, F, D, X, wide_logit):
-    """X = [emb_0..emb_{F-1} | dense | 0-pad] (bf16); wide_logit[b] = sum_f rows[inv, D]."""
+def wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col=-1):
+    """X = [emb_0..emb_{F-1} | dense | 1 at ones_col | 0-pad] (bf16);
+    wide_logit[b] = sum_f rows[inv, D]."""
     if _gpu(X):
-        kernels().wd_assemble(dense, rows, inv, int(F), int(D), X, wide_logit)
+        kernels().wd_assemble(dense, rows, inv, int(F), int(D), X, wide_logit, int(ones_col))
         return X, wide_logit
     B = X.shape[0]
     r = rows[inv].view(B, F, rows.shape[1]).float()
     X.zero_()
     X[:, : F * D] = r[:, :, :D].reshape(B, F * D).to(torch.bfloat16)
     X[:, F * D: F * D + dense.shape[1]] = dense.to(torch.bfloat16)
+    if ones_col >= 0:
+        X[:, ones_col] = 1.0
     wide_logit.copy_(r[:, :, D].sum(1))
     return X, wide_logit
 
