@@ -1,0 +1,140 @@
+"""Launcher (parity with the reference scripts/launch_utils.py + scripts/<app>.py verbs).
+
+    python -m minips_amd.launch --app lr --hostfile config/localnodes local [--flag=value ...]
+    python -m minips_amd.launch --app lr --hostfile config/localnodes relaunch <node_id>
+    python -m minips_amd.launch --app lr --hostfile config/localnodes relocal <node_id>
+    python -m minips_amd.launch --app lr --hostfile config/localnodes scale <id> <host> <port>
+    python -m minips_amd.launch --app lr --hostfile config/localnodes kill
+
+`local` starts one process per hostfile line (locally, or over ssh for remote hosts) with
+`--my_id=<id> --config_file=<hostfile>` plus the pass-through flags. `relaunch` restarts one
+node with --use_weight_file (resume from the checkpoint) -- it is what the master's
+--relaunch_cmd calls. `kill` stops every process this launcher started (tracked by PID files,
+never by name pattern). Apps: lr, kmeans, basic (native C++ binaries in build/bin) or any
+executable path. For the GPU data plane use torchrun / bench.py (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shlex
+import signal
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+APPS = {"lr": "build/bin/lr_example", "kmeans": "build/bin/kmeans", "basic": "build/bin/basic_example"}
+PID_DIR = os.environ.get("MINIPS_PID_DIR", "/tmp/minips_pids")
+
+
+def parse_hostfile(path: str):
+    nodes = []
+    with open(path) as f:
+        for line in f:
+            line = line.split("#")[0].strip()
+            if not line:
+                continue
+            parts = line.split(":")
+            nodes.append({"id": int(parts[0]), "host": parts[1], "port": int(parts[2]),
+                          "gpu": int(parts[3]) if len(parts) > 3 else -1})
+    return nodes
+
+
+def _is_local(host: str) -> bool:
+    return host in ("localhost", "127.0.0.1", socket.gethostname())
+
+
+def _binary(app: str) -> str:
+    p = APPS.get(app, app)
+    return p if os.path.isabs(p) else os.path.join(ROOT, p)
+
+
+def _pidfile(app: str, node_id: int) -> str:
+    return os.path.join(PID_DIR, f"{os.path.basename(app)}_{node_id}.pid")
+
+
+def launch_node(app: str, hostfile: str, node: dict, flags: list[str], extra: list[str] = (), log_dir=None,
+                wait=False):
+    cmd = [_binary(app), f"--config_file={os.path.abspath(hostfile)}", f"--my_id={node['id']}", *flags, *extra]
+    env = dict(os.environ)
+    if node.get("gpu", -1) >= 0:
+        env["HIP_VISIBLE_DEVICES"] = str(node["gpu"])
+    os.makedirs(PID_DIR, exist_ok=True)
+    log = None
+    if log_dir:
+        os.makedirs(log_dir, exist_ok=True)
+        log = open(os.path.join(log_dir, f"node_{node['id']}.log"), "w")
+    if _is_local(node["host"]):
+        p = subprocess.Popen(cmd, env=env, stdout=log or None, stderr=subprocess.STDOUT if log else None,
+                             start_new_session=True)
+    else:
+        remote = " ".join(shlex.quote(c) for c in cmd)
+        p = subprocess.Popen(["ssh", "-o", "StrictHostKeyChecking=no", node["host"], remote],
+                             stdout=log or None, stderr=subprocess.STDOUT if log else None, start_new_session=True)
+    with open(_pidfile(app, node["id"]), "w") as f:
+        f.write(str(p.pid))
+    if wait:
+        return p.wait()
+    return p
+
+
+def launch_nodes(app: str, hostfile: str, flags: list[str], log_dir=None, wait=True, timeout=None):
+    procs = [launch_node(app, hostfile, n, flags, log_dir=log_dir) for n in parse_hostfile(hostfile)]
+    if not wait:
+        return procs
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=timeout))
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            rcs.append(-9)
+    return rcs
+
+
+def relaunch(app: str, hostfile: str, node_id: int, flags: list[str], log_dir=None):
+    node = next(n for n in parse_hostfile(hostfile) if n["id"] == node_id)
+    return launch_node(app, hostfile, node, flags, extra=["--use_weight_file=true"], log_dir=log_dir)
+
+
+def kill_nodes(app: str, hostfile: str):
+    for n in parse_hostfile(hostfile):
+        pf = _pidfile(app, n["id"])
+        if not os.path.exists(pf):
+            continue
+        with open(pf) as f:
+            pid = int(f.read().strip())
+        try:
+            os.killpg(pid, signal.SIGKILL)  # the process group this launcher created
+        except ProcessLookupError:
+            pass
+        os.remove(pf)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--app", default="lr")
+    ap.add_argument("--hostfile", default=os.path.join(ROOT, "config/localnodes"))
+    ap.add_argument("--log-dir", default=None)
+    ap.add_argument("verb", choices=["local", "relaunch", "relocal", "scale", "kill"])
+    ap.add_argument("args", nargs="*")
+    ns, flags = ap.parse_known_args(argv)
+    if ns.verb == "local":
+        rcs = launch_nodes(ns.app, ns.hostfile, flags, log_dir=ns.log_dir)
+        return max(abs(r) for r in rcs) if rcs else 0
+    if ns.verb in ("relaunch", "relocal"):
+        relaunch(ns.app, ns.hostfile, int(ns.args[0]), flags, log_dir=ns.log_dir)
+        return 0
+    if ns.verb == "scale":
+        nid, host, port = int(ns.args[0]), ns.args[1], int(ns.args[2])
+        node = {"id": nid, "host": host, "port": port, "gpu": -1}
+        launch_node(ns.app, ns.hostfile, node, flags, extra=["--scale=true", f"--scale_node_id={nid}"],
+                    log_dir=ns.log_dir)
+        return 0
+    kill_nodes(ns.app, ns.hostfile)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
