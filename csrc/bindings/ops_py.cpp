@@ -34,41 +34,79 @@ T* opt_ptr(const c10::optional<at::Tensor>& t, at::ScalarType dt, const char* na
 }
 
 // C = A . B with layout flags; see gemm.hip. Returns nothing (C preallocated).
+// Batched mode (batch > 1): operands are flat buffers addressed with 2-level strides; every
+// batch's extent is bounds-checked against the tensor sizes before launch.
 void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K, bool a_km,
           bool b_kn, int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& mask,
-          const c10::optional<at::Tensor>& colsum, double alpha, int64_t split_k) {
-  check_gpu(A, "A");
-  check_gpu(B, "B");
-  check_gpu(C, "C");
+          const c10::optional<at::Tensor>& colsum, double alpha, int64_t split_k, int64_t batch, int64_t inner,
+          int64_t lda_, int64_t ldb_, int64_t ldc_, std::vector<int64_t> strides) {
+  // 2-D operands may be column-sliced views: rows contiguous (stride(1) == 1), ld = stride(0).
+  auto check_mat = [](const at::Tensor& t, const char* n) {
+    TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
+    TORCH_CHECK(t.dim() == 2 ? t.stride(1) == 1 : t.is_contiguous(), n, " rows must be contiguous");
+  };
+  check_mat(A, "A");
+  check_mat(B, "B");
+  check_mat(C, "C");
   check_dtype(A, at::kBFloat16, "A");
   check_dtype(B, at::kBFloat16, "B");
-  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
-  const int64_t a_rows = a_km ? K : M, a_cols = a_km ? M : K;
-  const int64_t b_rows = b_kn ? K : N, b_cols = b_kn ? N : K;
-  TORCH_CHECK(A.size(0) == a_rows && A.size(1) >= a_cols, "A shape ", A.sizes(), " vs M,N,K=", M, ",", N, ",", K);
-  TORCH_CHECK(B.size(0) == b_rows && B.size(1) >= b_cols, "B shape ", B.sizes(), " vs M,N,K=", M, ",", N, ",", K);
-  TORCH_CHECK(C.size(0) == M && C.size(1) >= N, "C shape ", C.sizes(), " vs M,N=", M, ",", N);
-  TORCH_CHECK(A.size(1) % 8 == 0 && B.size(1) % 8 == 0, "leading dims must be multiples of 8 (16-byte rows)");
+  const bool f32_out = epi == minips_k::kEpiStoreF32 || epi == minips_k::kEpiAtomicF32;
+  check_dtype(C, f32_out ? at::kFloat : at::kBFloat16, "C");
   TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8");
   if (a_km) TORCH_CHECK(M % 8 == 0, "KM layout needs M % 8 == 0");
   if (b_kn) TORCH_CHECK(N % 8 == 0, "KN layout needs N % 8 == 0");
-  const bool f32_out = epi == minips_k::kEpiStoreF32 || epi == minips_k::kEpiAtomicF32;
-  check_dtype(C, f32_out ? at::kFloat : at::kBFloat16, "C");
+  const int64_t a_rows = a_km ? K : M, a_cols = a_km ? M : K;
+  const int64_t b_rows = b_kn ? K : N, b_cols = b_kn ? N : K;
+  int64_t lda, ldb, ldc;
+  std::vector<int64_t> st(6, 0);
+  if (batch <= 1) {
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
+    TORCH_CHECK(A.size(0) == a_rows && A.size(1) >= a_cols, "A shape ", A.sizes(), " vs M,N,K=", M, ",", N, ",", K);
+    TORCH_CHECK(B.size(0) == b_rows && B.size(1) >= b_cols, "B shape ", B.sizes(), " vs M,N,K=", M, ",", N, ",", K);
+    TORCH_CHECK(C.size(0) == M && C.size(1) >= N, "C shape ", C.sizes(), " vs M,N=", M, ",", N);
+    lda = A.stride(0);
+    ldb = B.stride(0);
+    ldc = C.stride(0);
+    batch = 1;
+    inner = 1;
+  } else {
+    TORCH_CHECK(strides.size() == 6, "batched gemm needs 6 strides");
+    st = strides;
+    lda = lda_;
+    ldb = ldb_;
+    ldc = ldc_;
+    TORCH_CHECK(inner >= 1 && batch % inner == 0, "batch must be a multiple of inner");
+    auto extent = [&](int64_t rows, int64_t cols, int64_t ld, int64_t so, int64_t si) {
+      return (batch / inner - 1) * so + (inner - 1) * si + (rows - 1) * ld + cols;
+    };
+    TORCH_CHECK(extent(a_rows, a_cols, lda, st[0], st[1]) <= A.numel(), "batched A out of bounds");
+    TORCH_CHECK(extent(b_rows, b_cols, ldb, st[2], st[3]) <= B.numel(), "batched B out of bounds");
+    TORCH_CHECK(extent(M, N, ldc, st[4], st[5]) <= C.numel(), "batched C out of bounds");
+    TORCH_CHECK(!mask.has_value() && !colsum.has_value(), "batched gemm has no mask/colsum");
+  }
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "leading dims must be multiples of 8 (16-byte rows)");
+  for (int i = 0; i < 4; ++i) TORCH_CHECK(st[i] % 8 == 0, "operand batch strides must be multiples of 8");
   const bf16_t* bias_p = opt_ptr<bf16_t>(bias, at::kBFloat16, "bias");
   if (bias_p) TORCH_CHECK(bias->numel() >= N, "bias too short");
-  const bf16_t* mask_p = opt_ptr<bf16_t>(mask, at::kBFloat16, "mask");
+  const bf16_t* mask_p = nullptr;
   int ldmask = 0;
-  if (mask_p) {
+  if (mask.has_value() && mask->defined()) {
+    check_mat(*mask, "mask");
+    check_dtype(*mask, at::kBFloat16, "mask");
+    mask_p = ptr<bf16_t>(*mask);
     TORCH_CHECK(mask->dim() == 2 && mask->size(0) == M && mask->size(1) >= N, "mask shape ", mask->sizes());
-    ldmask = (int)mask->size(1);
+    ldmask = (int)mask->stride(0);
   }
-  if (epi == minips_k::kEpiReluMaskBf16) TORCH_CHECK(mask_p, "relu-mask epilogue needs mask");
+  const bool needs_mask = epi == minips_k::kEpiReluMaskBf16 || epi == minips_k::kEpiBiasGeluAuxBf16 ||
+                          epi == minips_k::kEpiGeluGradBf16;
+  if (needs_mask) TORCH_CHECK(mask_p, "this epilogue needs mask/aux");
   float* colsum_p = opt_ptr<float>(colsum, at::kFloat, "colsum");
   if (colsum_p) TORCH_CHECK(colsum->numel() >= N, "colsum too short");
   c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
-  minips_k::gemm_bf16(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)A.size(1),
-                      (int)B.size(1), (int)C.size(1), a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p,
-                      (float)alpha, (int)split_k, stream_of(A));
+  minips_k::gemm_bf16_batched(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb,
+                              (int)ldc, a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p, (float)alpha,
+                              (int)split_k, (int)batch, (int)inner, st[0], st[1], st[2], st[3], st[4], st[5],
+                              stream_of(A));
 }
 
 // Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P]).
@@ -110,6 +148,19 @@ void gather_rows(const at::Tensor& table, const at::Tensor& keys, int64_t base, 
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::gather_rows(ptr<float>(table), table.stride(0), ptr<int64_t>(keys), n, base, D, out.data_ptr(),
                         out.scalar_type() == at::kBFloat16, stream_of(keys));
+}
+
+void lookup_rows(const at::Tensor& rows, const at::Tensor& inv, int64_t F, int64_t D, at::Tensor& out) {
+  check_gpu(rows, "rows");
+  check_gpu(inv, "inv");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1, "out must be a row-major GPU matrix");
+  check_dtype(rows, at::kBFloat16, "rows");
+  check_dtype(out, at::kBFloat16, "out");
+  const int64_t B = out.size(0);
+  TORCH_CHECK(inv.numel() == B * F && rows.size(1) >= D && out.size(1) >= F * D, "lookup_rows shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(rows.device());
+  minips_k::lookup_rows(ptr<bf16_t>(rows), (int)rows.size(1), ptr<int64_t>(inv), B, (int)F, (int)D, ptr<bf16_t>(out),
+                        (int)out.stride(0), stream_of(rows));
 }
 
 void scatter_add_rows(const at::Tensor& src, const at::Tensor& idx, at::Tensor& acc) {
@@ -211,18 +262,18 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
                     ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H));
 }
 
-void wd_emb_backward(const at::Tensor& dX, const at::Tensor& dwide, const at::Tensor& inv, int64_t F, int64_t D,
-                     at::Tensor& grad_rows) {
+void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, const at::Tensor& inv, int64_t F,
+                     int64_t D, at::Tensor& grad_rows, int64_t x_off) {
   check_gpu(dX, "dX");
-  check_gpu(dwide, "dwide");
+  const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
   check_gpu(inv, "inv");
   check_gpu(grad_rows, "grad_rows");
   check_dtype(dX, at::kFloat, "dX");
   check_dtype(grad_rows, at::kFloat, "grad_rows");
   const int64_t B = dX.size(0);
-  TORCH_CHECK(inv.numel() == B * F && dX.size(1) >= F * D && grad_rows.size(1) > D, "shapes");
+  TORCH_CHECK(inv.numel() == B * F && dX.size(1) >= x_off + F * D && grad_rows.size(1) >= D + (dw ? 1 : 0), "shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
-  minips_k::wd_emb_backward(ptr<float>(dX), (int)dX.size(1), ptr<float>(dwide), ptr<int64_t>(inv), B, (int)F, (int)D,
+  minips_k::wd_emb_backward(ptr<float>(dX) + x_off, (int)dX.size(1), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
                             ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
 }
 
@@ -317,6 +368,98 @@ void criteo_synth(int64_t seed, int64_t step, const at::Tensor& cards, const at:
                          stream_of(keys));
 }
 
+void layernorm_fwd(const at::Tensor& x, int64_t C, const at::Tensor& gamma, const at::Tensor& beta, double eps,
+                   at::Tensor& y, at::Tensor& mean, at::Tensor& rstd) {
+  for (const at::Tensor* t : {&x, &gamma, &beta, (const at::Tensor*)&y, (const at::Tensor*)&mean,
+                              (const at::Tensor*)&rstd})
+    check_gpu(*t, "layernorm arg");
+  TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.size(1) >= C && y.size(1) >= C && C <= 1024, "layernorm shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  minips_k::layernorm_fwd(ptr<bf16_t>(x), (int)x.size(1), x.size(0), (int)C, ptr<bf16_t>(gamma), ptr<bf16_t>(beta),
+                          (float)eps, ptr<bf16_t>(y), (int)y.size(1), ptr<float>(mean), ptr<float>(rstd), stream_of(x));
+}
+
+void layernorm_bwd(const at::Tensor& x, const at::Tensor& dy, int64_t C, const at::Tensor& gamma,
+                   const at::Tensor& mean, const at::Tensor& rstd, at::Tensor& dx, at::Tensor& dgamma,
+                   at::Tensor& dbeta, bool accumulate) {
+  TORCH_CHECK(x.is_cuda() && dy.is_cuda() && dx.is_cuda() && x.size(0) == dy.size(0) && dx.size(0) == x.size(0),
+              "layernorm_bwd shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  minips_k::layernorm_bwd(ptr<bf16_t>(x), (int)x.size(1), ptr<bf16_t>(dy), (int)dy.size(1), x.size(0), (int)C,
+                          ptr<bf16_t>(gamma), ptr<float>(mean), ptr<float>(rstd), ptr<bf16_t>(dx), (int)dx.size(1),
+                          ptr<float>(dgamma), ptr<float>(dbeta), accumulate, stream_of(x));
+}
+
+void softmax_xent(at::Tensor& logits, int64_t V, const at::Tensor& labels, double scale, at::Tensor& loss_sum,
+                  const c10::optional<at::Tensor>& correct) {
+  check_gpu(logits, "logits");
+  check_gpu(labels, "labels");
+  check_dtype(logits, at::kBFloat16, "logits");
+  check_dtype(labels, at::kLong, "labels");
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) >= V && labels.numel() == logits.size(0), "softmax_xent shapes");
+  float* c = opt_ptr<float>(correct, at::kFloat, "correct");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  minips_k::softmax_xent(ptr<bf16_t>(logits), (int)logits.size(1), logits.size(0), (int)V, ptr<int64_t>(labels),
+                         (float)scale, ptr<float>(loss_sum), c, stream_of(logits));
+}
+
+void causal_softmax_fwd(const at::Tensor& S, int64_t T, at::Tensor& P) {
+  check_gpu(S, "S");
+  check_gpu(P, "P");
+  TORCH_CHECK(S.numel() == P.numel() && S.numel() % (T * T) == 0, "causal_softmax shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(S.device());
+  minips_k::causal_softmax_fwd(ptr<float>(S), S.numel() / T, (int)T, ptr<bf16_t>(P), stream_of(S));
+}
+
+void causal_softmax_bwd(const at::Tensor& P, const at::Tensor& dP, int64_t T, double scale, at::Tensor& dS) {
+  check_gpu(P, "P");
+  check_gpu(dP, "dP");
+  check_gpu(dS, "dS");
+  TORCH_CHECK(P.numel() == dP.numel() && P.numel() == dS.numel() && P.numel() % (T * T) == 0, "shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(P.device());
+  minips_k::causal_softmax_bwd(ptr<bf16_t>(P), ptr<float>(dP), P.numel() / T, (int)T, (float)scale, ptr<bf16_t>(dS),
+                               stream_of(P));
+}
+
+void gelu_bwd(const at::Tensor& dh, const at::Tensor& u, at::Tensor& du) {
+  TORCH_CHECK(dh.numel() == u.numel() && du.numel() == u.numel(), "gelu_bwd sizes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(u.device());
+  minips_k::gelu_bwd(ptr<bf16_t>(dh), ptr<bf16_t>(u), u.numel(), ptr<bf16_t>(du), stream_of(u));
+}
+
+void add_bf16(const at::Tensor& a, const at::Tensor& b, at::Tensor& out) {
+  TORCH_CHECK(a.numel() == b.numel() && out.numel() == a.numel(), "add sizes");
+  check_gpu(a, "a");
+  check_gpu(b, "b");
+  check_gpu(out, "out");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  minips_k::add_bf16(ptr<bf16_t>(a), ptr<bf16_t>(b), a.numel(), ptr<bf16_t>(out), stream_of(a));
+}
+
+void dlrm_interact_fwd(const at::Tensor& V, int64_t NV, int64_t D, int64_t dense_idx, at::Tensor& out) {
+  check_gpu(V, "V");
+  check_gpu(out, "out");
+  const int64_t B = V.numel() / (NV * D);
+  TORCH_CHECK(out.size(0) == B && out.size(1) >= D + NV * (NV - 1) / 2, "interaction out shape");
+  TORCH_CHECK(dense_idx >= 0 && dense_idx < NV, "dense_idx");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(V.device());
+  minips_k::dlrm_interact_fwd(ptr<bf16_t>(V), B, (int)NV, (int)D, (int)dense_idx, ptr<bf16_t>(out), (int)out.size(1),
+                              stream_of(V));
+}
+
+void dlrm_interact_bwd(const at::Tensor& V, int64_t NV, int64_t D, int64_t dense_idx, const at::Tensor& dout,
+                       at::Tensor& dV, at::Tensor& d_dense) {
+  check_gpu(V, "V");
+  check_gpu(dout, "dout");
+  check_gpu(dV, "dV");
+  check_gpu(d_dense, "d_dense");
+  const int64_t B = V.numel() / (NV * D);
+  TORCH_CHECK(dV.numel() == V.numel() && dout.size(0) == B && d_dense.numel() == B * D, "interaction bwd shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(V.device());
+  minips_k::dlrm_interact_bwd(ptr<bf16_t>(V), B, (int)NV, (int)D, (int)dense_idx, ptr<bf16_t>(dout), (int)dout.size(1),
+                              ptr<float>(dV), ptr<bf16_t>(d_dense), stream_of(V));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_kernels, m) {
@@ -328,17 +471,32 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("EPI_STORE_BF16") = (int)minips_k::kEpiStoreBf16;
   m.attr("EPI_RELU_MASK_BF16") = (int)minips_k::kEpiReluMaskBf16;
   m.attr("EPI_BIAS_GELU_BF16") = (int)minips_k::kEpiBiasGeluBf16;
-  m.def("gemm", &gemm);
+  m.attr("EPI_BIAS_GELU_AUX_BF16") = (int)minips_k::kEpiBiasGeluAuxBf16;
+  m.attr("EPI_GELU_GRAD_BF16") = (int)minips_k::kEpiGeluGradBf16;
+  m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("a_km"), py::arg("b_kn"), py::arg("epi"), py::arg("bias"), py::arg("mask"), py::arg("colsum"),
+        py::arg("alpha") = 1.0, py::arg("split_k") = 1, py::arg("batch") = 1, py::arg("inner") = 1,
+        py::arg("lda") = 0, py::arg("ldb") = 0, py::arg("ldc") = 0, py::arg("strides") = std::vector<int64_t>());
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("causal_softmax_fwd", &causal_softmax_fwd);
+  m.def("causal_softmax_bwd", &causal_softmax_bwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("add_bf16", &add_bf16);
+  m.def("dlrm_interact_fwd", &dlrm_interact_fwd);
+  m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
   m.def("unique_bucketize", &unique_bucketize, py::arg("keys"), py::arg("bounds"), py::arg("F") = 1);
   m.def("gather_rows", &gather_rows);
   m.def("scatter_add_rows", &scatter_add_rows);
+  m.def("lookup_rows", &lookup_rows);
   m.def("sparse_rowwise_adagrad", &sparse_rowwise_adagrad);
   m.def("sparse_sgd", &sparse_sgd);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1);
   m.def("wd_head", &wd_head);
-  m.def("wd_emb_backward", &wd_emb_backward);
+  m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0);
   m.def("adam_apply", &adam_apply);
   m.def("sgd_apply", &sgd_apply);
   m.def("adagrad_apply", &adagrad_apply);

@@ -107,6 +107,9 @@ struct EpiArgs {
   int ldmask;
   float* colsum;         // [N] column sums of the (masked) output
   float alpha;
+  // batched GEMM: z = blockIdx.y, offsets (z / inner) * s_outer + (z % inner) * s_inner
+  int inner;
+  int64_t sa_o, sa_i, sb_o, sb_i, sc_o, sc_i;
 };
 
 template <int BK, bool A_KM, bool B_KN, int EPI>
@@ -131,6 +134,14 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kb = blockIdx.z * k_chunk;
+  {
+    const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
+    A += zo * ep.sa_o + zi * ep.sa_i;
+    B += zo * ep.sb_o + zi * ep.sb_i;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
+    ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
+  }
   const int ke = min(K, kb + k_chunk);
 
   v4f acc[4][4];
@@ -188,7 +199,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
     const int col = n0 + wn * 64 + j * 16 + col_l;
     const bool col_ok = col < N;
     float bias = 0.f;
-    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
+    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
     float csum = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -212,6 +223,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
           ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
         } else if (EPI == kEpiStoreBf16) {
           ((bf16_t*)ep.C)[off] = f2bf(v);
+        } else if (EPI == kEpiBiasGeluAuxBf16) {
+          const float x = v + bias;
+          const float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
+          ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
+          const_cast<bf16_t*>(ep.mask)[(int64_t)row * ep.ldmask + col] = f2bf(x);
+        } else if (EPI == kEpiGeluGradBf16) {
+          const float u = bf2f(ep.mask[(int64_t)row * ep.ldmask + col]);
+          const float k = 0.7978845608f, c3 = 0.044715f;
+          const float t = tanhf(k * (u + c3 * u * u * u));
+          const float gp = 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k * (1.f + 3.f * c3 * u * u);
+          ((bf16_t*)ep.C)[off] = f2bf(v * gp);
         } else if (EPI == kEpiReluMaskBf16) {
           float m = bf2f(ep.mask[(int64_t)row * ep.ldmask + col]);
           float o = m > 0.f ? v : 0.f;
@@ -231,7 +253,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
 
 template <bool A_KM, bool B_KN, int EPI>
 static void launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, int split_k,
-                   const EpiArgs& ep, hipStream_t s) {
+                   const EpiArgs& ep, int batch, hipStream_t s) {
   int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   // BK=64 halves the barriers per FLOP; short K chunks keep BK=32 (less tail waste).
   const int kper = (K + split_k - 1) / split_k;
@@ -244,7 +266,7 @@ static void launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int ld
   const int BKs = bk64 ? 64 : 32;
   int kc = (kper + BKs - 1) / BKs * BKs;
   int nsplit = (K + kc - 1) / kc;
-  dim3 grid(tiles, 1, nsplit);
+  dim3 grid(tiles, batch, nsplit);
   if (bk64)
     hipLaunchKernelGGL((gemm_bf16_kernel<64, A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
   else
@@ -253,23 +275,28 @@ static void launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int ld
 
 #define MINIPS_GEMM_EPI_DISPATCH(AKM, BKN)                                                        \
   switch (epi) {                                                                                 \
-    case kEpiStoreF32: launch<AKM, BKN, kEpiStoreF32>(A, B, M, N, K, lda, ldb, split_k, ep, s); break;  \
-    case kEpiAtomicF32: launch<AKM, BKN, kEpiAtomicF32>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
-    case kEpiBiasReluBf16: launch<AKM, BKN, kEpiBiasReluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
-    case kEpiBiasBf16: launch<AKM, BKN, kEpiBiasBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
-    case kEpiBiasGeluBf16: launch<AKM, BKN, kEpiBiasGeluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
-    case kEpiStoreBf16: launch<AKM, BKN, kEpiStoreBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
-    case kEpiReluMaskBf16: launch<AKM, BKN, kEpiReluMaskBf16>(A, B, M, N, K, lda, ldb, split_k, ep, s); break; \
+    case kEpiStoreF32: launch<AKM, BKN, kEpiStoreF32>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break;  \
+    case kEpiAtomicF32: launch<AKM, BKN, kEpiAtomicF32>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiBiasReluBf16: launch<AKM, BKN, kEpiBiasReluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiBiasBf16: launch<AKM, BKN, kEpiBiasBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiBiasGeluBf16: launch<AKM, BKN, kEpiBiasGeluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiStoreBf16: launch<AKM, BKN, kEpiStoreBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiReluMaskBf16: launch<AKM, BKN, kEpiReluMaskBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiBiasGeluAuxBf16: launch<AKM, BKN, kEpiBiasGeluAuxBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiGeluGradBf16: launch<AKM, BKN, kEpiGeluGradBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
     default: throw std::runtime_error("gemm: unknown epilogue " + std::to_string(epi));           \
   }
 
-void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-               bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
-               float alpha, int split_k, hipStream_t s) {
-  if (M <= 0 || N <= 0 || K <= 0) return;
+void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                       bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
+                       float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
+                       int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return;
   if (split_k < 1) split_k = 1;
   if (split_k > 1 && epi != kEpiAtomicF32) throw std::runtime_error("gemm: split_k needs the atomic epilogue");
-  EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha};
+  if (batch > 1 && (mask || colsum)) throw std::runtime_error("gemm: batched mode has no mask/colsum epilogue");
+  if (inner < 1) inner = 1;
+  EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i};
   if (!a_km && !b_kn) {
     MINIPS_GEMM_EPI_DISPATCH(false, false)
   } else if (!a_km && b_kn) {
@@ -280,6 +307,13 @@ void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, i
     MINIPS_GEMM_EPI_DISPATCH(true, false)
   }
   MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+               bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
+               float alpha, int split_k, hipStream_t s) {
+  gemm_bf16_batched(A, B, C, M, N, K, lda, ldb, ldc, a_km, b_kn, epi, bias, mask, ldmask, colsum, alpha, split_k, 1,
+                    1, 0, 0, 0, 0, 0, 0, s);
 }
 
 }  // namespace minips_k

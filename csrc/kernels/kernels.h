@@ -18,10 +18,18 @@ enum GemmEpilogue {
   kEpiStoreBf16 = 4,     // C bf16 = acc
   kEpiReluMaskBf16 = 5,  // C bf16 = acc * (mask > 0); colsum[n] += sum_m C
   kEpiBiasGeluBf16 = 6,  // C bf16 = gelu_tanh(acc + bias)
+  kEpiBiasGeluAuxBf16 = 7,  // C bf16 = gelu_tanh(u), mask(aux) bf16 = u = acc + bias (saved for bwd)
+  kEpiGeluGradBf16 = 8,     // C bf16 = acc * gelu'(mask)  (mask = saved pre-activation u)
 };
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
                float alpha, int split_k, hipStream_t s);
+// Batched form: `batch` GEMMs, z = blockIdx.y; operand offsets are (z / inner) * s_outer +
+// (z % inner) * s_inner elements (e.g. attention heads inside a [B*T, H*dh] activation).
+void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                       bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
+                       float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
+                       int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s);
 
 // ------------------------------------------------------------------ sparse keys (sparse.hip)
 // Hash-based dedupe + owner bucketing of int64 keys in 3 launches (no sort):
@@ -41,6 +49,9 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
 // table fp32 [R, D] row stride ld; out fp32 or bf16 [n, D].
 void gather_rows(const float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, void* out,
                  bool out_bf16, hipStream_t s);
+// Lookup: out[b, f*D:(f+1)*D] = rows[inv[b*F+f], 0:D]  (bf16; D % 8 == 0).
+void lookup_rows(const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B, int F, int D, bf16_t* out, int ldo,
+                 hipStream_t s);
 // Scatter-add rows: acc[idx[i], :] += src[i, :] (fp32, float atomics, 2 rows per wave-instr).
 void scatter_add_rows(const float* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s);
 // Row-wise Adagrad on a shard (one accumulator per row, DLRM style):
@@ -75,7 +86,8 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
              float grad_scale, hipStream_t s);
 // Embedding backward: grad_rows[inv[b*F+f], 0:D] += dX[b, f*D : (f+1)*D] (fp32 dX, ld ldx),
-// grad_rows[inv[b*F+f], D] += dwide[b]   (grad_rows fp32 [U, row_stride], pre-zeroed).
+// grad_rows[inv[b*F+f], D] += dwide[b] when dwide != null (grad_rows fp32 [U, row_stride],
+// pre-zeroed).
 void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                      float* grad_rows, int row_stride, hipStream_t s);
 
@@ -98,6 +110,27 @@ void lr_sparse_step(const int64_t* rowptr, const int64_t* cols, const float* val
 // K-Means assignment: X [n, d] fp32, C [k, d] fp32 -> assign [n] (int32), min dist [n].
 void kmeans_assign(const float* X, int64_t n, int d, const float* C, int k, int32_t* assign, float* dist,
                    hipStream_t s);
+
+// ------------------------------------------------------------------ dense-model kernels (nn.hip)
+void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gamma, const bf16_t* beta, float eps,
+                   bf16_t* y, int ldy, float* mean, float* rstd, hipStream_t s);
+void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t M, int C, const bf16_t* gamma,
+                   const float* mean, const float* rstd, bf16_t* dx, int lddx, float* dgamma, float* dbeta,
+                   bool accumulate_dx, hipStream_t s);
+// In place: logits [M, ld] bf16 become (softmax - onehot) * scale; loss_sum += sum CE.
+void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,
+                  float* correct, hipStream_t s);
+void causal_softmax_fwd(const float* S, int64_t rows, int T, bf16_t* P, hipStream_t s);
+void causal_softmax_bwd(const bf16_t* P, const float* dP, int64_t rows, int T, float scale, bf16_t* dS,
+                        hipStream_t s);
+void gelu_bwd(const bf16_t* dh, const bf16_t* u, int64_t n, bf16_t* du, hipStream_t s);
+void add_bf16(const bf16_t* a, const bf16_t* b, int64_t n, bf16_t* out, hipStream_t s);
+// DLRM dot interaction of NV vectors of width D per sample (V [B][NV][D] bf16): out[b] =
+// [V[b][dense_idx] | V_i.V_j for i > j]. Backward: dV fp32 for all vectors, and the dense
+// vector's gradient ReLU-masked by its value as bf16 (feeds the bottom MLP's backward).
+void dlrm_interact_fwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, bf16_t* out, int ldo, hipStream_t s);
+void dlrm_interact_bwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, const bf16_t* dout, int ldo,
+                       float* dV, bf16_t* d_dense, hipStream_t s);
 
 // ------------------------------------------------------------------ synthetic data (data.hip)
 void criteo_synth(uint64_t seed, uint64_t step, int64_t B, int F, const int64_t* cards, const int64_t* offsets,

@@ -1,0 +1,337 @@
+// Dense-model worker kernels (MLP, GPT-2-small, DLRM) for gfx950:
+//   layernorm_fwd/bwd      row LayerNorm, bf16 activations, fp32 statistics, fp32 param grads
+//   softmax_xent           fused softmax + cross-entropy forward/backward over [M, V] logits
+//                          (MLP classes, GPT-2 vocab 50257): one block per row, 3 L2-resident passes
+//   causal_softmax_fwd/bwd attention probabilities with the causal mask, one wave per row
+//   gelu_bwd               dU = dH * gelu'(U)
+//   add_bf16               residual adds
+//   dlrm_interact_fwd/bwd  DLRM pairwise dot-product interaction (27 vectors x 64) per sample
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace minips_k {
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = warp_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  return t;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = warp_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = -3.4e38f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// ---------------------------------------------------------------------------- LayerNorm
+// One wave per row, C <= 64*16.
+__global__ void layernorm_fwd_kernel(const bf16_t* __restrict__ x, int ldx, int64_t M, int C,
+                                     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta, float eps,
+                                     bf16_t* __restrict__ y, int ldy, float* __restrict__ mean_out,
+                                     float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wave; r < M; r += nw) {
+    const bf16_t* xr = x + r * ldx;
+    float s = 0.f, ss = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float v = bf2f(xr[c]);
+      s += v;
+      ss += v * v;
+    }
+    s = warp_sum(s);
+    ss = warp_sum(ss);
+    const float mu = s / C;
+    const float var = fmaxf(ss / C - mu * mu, 0.f);
+    const float rs = rsqrtf(var + eps);
+    for (int c = lane; c < C; c += 64) {
+      const float v = (bf2f(xr[c]) - mu) * rs;
+      y[r * ldy + c] = f2bf(v * bf2f(gamma[c]) + bf2f(beta[c]));
+    }
+    if (lane == 0) {
+      mean_out[r] = mu;
+      rstd_out[r] = rs;
+    }
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma; param grads reduced per
+// block in LDS (C <= 1024) then one atomic per column per block.
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                            const bf16_t* __restrict__ dy, int lddy, int64_t M, int C,
+                                                            const bf16_t* __restrict__ gamma,
+                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                            bf16_t* __restrict__ dx, int lddx, float* dgamma,
+                                                            float* dbeta, bool accumulate_dx) {
+  __shared__ float sg[1024], sb[1024];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    sg[c] = 0.f;
+    sb[c] = 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wave; r < M; r += nw) {
+    const float mu = mean[r], rs = rstd[r];
+    float a = 0.f, b = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float xh = (bf2f(x[r * ldx + c]) - mu) * rs;
+      const float d = bf2f(dy[r * lddy + c]);
+      const float g = d * bf2f(gamma[c]);
+      a += g;
+      b += g * xh;
+      atomicAdd(sg + c, d * xh);
+      atomicAdd(sb + c, d);
+    }
+    a = warp_sum(a) / C;
+    b = warp_sum(b) / C;
+    for (int c = lane; c < C; c += 64) {
+      const float xh = (bf2f(x[r * ldx + c]) - mu) * rs;
+      const float g = bf2f(dy[r * lddy + c]) * bf2f(gamma[c]);
+      float v = rs * (g - a - xh * b);
+      if (accumulate_dx) v += bf2f(dx[r * lddx + c]);
+      dx[r * lddx + c] = f2bf(v);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    atomicAdd(dgamma + c, sg[c]);
+    atomicAdd(dbeta + c, sb[c]);
+  }
+}
+
+void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gamma, const bf16_t* beta, float eps,
+                   bf16_t* y, int ldy, float* mean, float* rstd, hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(layernorm_fwd_kernel, grid_for(M * 64, 256, 4096), 256, 0, s, x, ldx, M, C, gamma, beta, eps, y,
+                     ldy, mean, rstd);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t M, int C, const bf16_t* gamma,
+                   const float* mean, const float* rstd, bf16_t* dx, int lddx, float* dgamma, float* dbeta,
+                   bool accumulate_dx, hipStream_t s) {
+  if (M <= 0) return;
+  if (C > 1024) throw std::runtime_error("layernorm_bwd: C <= 1024");
+  hipLaunchKernelGGL(layernorm_bwd_kernel, grid_for(M * 64, 256, 512), 256, 0, s, x, ldx, dy, lddy, M, C, gamma, mean,
+                     rstd, dx, lddx, dgamma, dbeta, accumulate_dx);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------- softmax-xent
+// logits may be updated in place with the gradient ((softmax - onehot) * scale).
+__global__ __launch_bounds__(256) void softmax_xent_kernel(bf16_t* __restrict__ logits, int ld, int64_t M, int V,
+                                                           const int64_t* __restrict__ labels, float scale,
+                                                           float* loss_sum, float* correct) {
+  __shared__ float red[8];
+  for (int64_t r = blockIdx.x; r < M; r += gridDim.x) {
+    bf16_t* row = logits + r * ld;
+    float mx = -3.4e38f;
+    for (int c = threadIdx.x; c < V; c += blockDim.x) mx = fmaxf(mx, bf2f(row[c]));
+    mx = block_max(mx, red);
+    float se = 0.f;
+    for (int c = threadIdx.x; c < V; c += blockDim.x) se += __expf(bf2f(row[c]) - mx);
+    se = block_sum(se, red);
+    const int64_t lab = labels[r];
+    const float lse = mx + __logf(se);
+    if (threadIdx.x == 0) {
+      const float zl = (lab >= 0 && lab < V) ? bf2f(row[lab]) : lse;
+      atomicAdd(loss_sum, lse - zl);
+      if (correct && lab >= 0 && lab < V && zl >= mx) atomicAdd(correct, 1.f);
+    }
+    __syncthreads();
+    const float inv = 1.f / se;
+    for (int c = threadIdx.x; c < V; c += blockDim.x) {
+      const float p = __expf(bf2f(row[c]) - mx) * inv;
+      row[c] = f2bf((p - (c == lab ? 1.f : 0.f)) * scale);
+    }
+    __syncthreads();
+  }
+}
+
+void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,
+                  float* correct, hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(softmax_xent_kernel, (int)std::min<int64_t>(M, 8192), 256, 0, s, logits, ld, M, V, labels, scale,
+                     loss_sum, correct);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------- attention softmax
+// S [Z][T][T] fp32 scores (already scaled) -> P bf16 with causal mask (col > row -> 0).
+__global__ void causal_softmax_fwd_kernel(const float* __restrict__ S, int64_t rows, int T, bf16_t* __restrict__ P) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wave; r < rows; r += nw) {
+    const int i = (int)(r % T);
+    const float* s = S + r * T;
+    float mx = -3.4e38f;
+    for (int c = lane; c <= i; c += 64) mx = fmaxf(mx, s[c]);
+    mx = warp_max(mx);
+    float se = 0.f;
+    for (int c = lane; c <= i; c += 64) se += __expf(s[c] - mx);
+    se = warp_sum(se);
+    const float inv = 1.f / se;
+    bf16_t* p = P + r * T;
+    for (int c = lane; c < T; c += 64) p[c] = c <= i ? f2bf(__expf(s[c] - mx) * inv) : (bf16_t)0;
+  }
+}
+
+// dS = P * (dP - rowsum(P * dP)) * scale  (dP fp32 [Z][T][T]) -> bf16
+__global__ void causal_softmax_bwd_kernel(const bf16_t* __restrict__ P, const float* __restrict__ dP, int64_t rows,
+                                          int T, float scale, bf16_t* __restrict__ dS) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wave; r < rows; r += nw) {
+    const int i = (int)(r % T);
+    const bf16_t* p = P + r * T;
+    const float* dp = dP + r * T;
+    float dot = 0.f;
+    for (int c = lane; c <= i; c += 64) dot += bf2f(p[c]) * dp[c];
+    dot = warp_sum(dot);
+    bf16_t* ds = dS + r * T;
+    for (int c = lane; c < T; c += 64) ds[c] = c <= i ? f2bf(bf2f(p[c]) * (dp[c] - dot) * scale) : (bf16_t)0;
+  }
+}
+
+void causal_softmax_fwd(const float* S, int64_t rows, int T, bf16_t* P, hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(causal_softmax_fwd_kernel, grid_for(rows * 64, 256, 8192), 256, 0, s, S, rows, T, P);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+void causal_softmax_bwd(const bf16_t* P, const float* dP, int64_t rows, int T, float scale, bf16_t* dS,
+                        hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(causal_softmax_bwd_kernel, grid_for(rows * 64, 256, 8192), 256, 0, s, P, dP, rows, T, scale, dS);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------- elementwise
+__device__ __forceinline__ float gelu_grad(float u) {
+  const float k = 0.7978845608f, c = 0.044715f;
+  const float t = tanhf(k * (u + c * u * u * u));
+  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k * (1.f + 3.f * c * u * u);
+}
+
+__global__ void gelu_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* __restrict__ u, int64_t n,
+                                bf16_t* __restrict__ du) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    du[i] = f2bf(bf2f(dh[i]) * gelu_grad(bf2f(u[i])));
+}
+void gelu_bwd(const bf16_t* dh, const bf16_t* u, int64_t n, bf16_t* du, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gelu_bwd_kernel, grid_for(n, 256), 256, 0, s, dh, u, n, du);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, int64_t n,
+                                bf16_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = f2bf(bf2f(a[i]) + bf2f(b[i]));
+}
+void add_bf16(const bf16_t* a, const bf16_t* b, int64_t n, bf16_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(add_bf16_kernel, grid_for(n, 256), 256, 0, s, a, b, n, out);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------- DLRM interaction
+// V [B][NV][D] bf16 -> out[b] = [V[b][dense_idx] (D) | V_i.V_j for i > j] at out + b*ldo.
+// One block per sample (grid-stride); the sample's vectors are staged in LDS.
+__device__ __forceinline__ void pair_of(int p, int* i, int* j) {
+  int a = (int)((1.f + sqrtf(1.f + 8.f * p)) * 0.5f);
+  while (a * (a - 1) / 2 > p) --a;
+  while ((a + 1) * a / 2 <= p) ++a;
+  *i = a;
+  *j = p - a * (a - 1) / 2;
+}
+
+__global__ __launch_bounds__(256) void dlrm_interact_fwd_kernel(const bf16_t* __restrict__ V, int64_t B, int NV, int D,
+                                                                int dense_idx, bf16_t* __restrict__ out, int ldo) {
+  extern __shared__ float sv[];  // NV rows of D+1 floats (odd stride: lanes on different rows hit different banks)
+  const int npairs = NV * (NV - 1) / 2;
+  const int Dp = D + 1;
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    const bf16_t* vb = V + b * NV * D;
+    for (int e = threadIdx.x; e < NV * D; e += blockDim.x) sv[(e / D) * Dp + e % D] = bf2f(vb[e]);
+    __syncthreads();
+    bf16_t* ob = out + b * ldo;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) ob[d] = vb[dense_idx * D + d];
+    for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
+      int i, j;
+      pair_of(p, &i, &j);
+      float acc = 0.f;
+      for (int d = 0; d < D; ++d) acc += sv[i * Dp + d] * sv[j * Dp + d];
+      ob[D + p] = f2bf(acc);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void dlrm_interact_bwd_kernel(const bf16_t* __restrict__ V, int64_t B, int NV, int D,
+                                                                int dense_idx, const bf16_t* __restrict__ dout, int ldo,
+                                                                float* __restrict__ dV, bf16_t* __restrict__ d_dense) {
+  extern __shared__ float sm[];  // V: NV*D, dZ: NV*NV
+  float* sv = sm;
+  float* dz = sm + NV * D;
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    const bf16_t* vb = V + b * NV * D;
+    const bf16_t* ob = dout + b * ldo;
+    for (int i = threadIdx.x; i < NV * D; i += blockDim.x) sv[i] = bf2f(vb[i]);
+    for (int q = threadIdx.x; q < NV * NV; q += blockDim.x) {
+      const int i = q / NV, j = q % NV;
+      float g = 0.f;
+      if (i != j) {
+        const int hi = i > j ? i : j, lo = i > j ? j : i;
+        g = bf2f(ob[D + hi * (hi - 1) / 2 + lo]);
+      }
+      dz[q] = g;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < NV * D; e += blockDim.x) {
+      const int i = e / D, d = e % D;
+      float acc = (i == dense_idx) ? bf2f(ob[d]) : 0.f;
+      for (int j = 0; j < NV; ++j) acc += dz[i * NV + j] * sv[j * D + d];
+      dV[b * NV * D + e] = acc;
+      if (i == dense_idx) d_dense[b * D + d] = f2bf(sv[e] > 0.f ? acc : 0.f);
+    }
+    __syncthreads();
+  }
+}
+
+void dlrm_interact_fwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, bf16_t* out, int ldo, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(dlrm_interact_fwd_kernel, (int)std::min<int64_t>(B, 8192), 256, NV * (D + 1) * sizeof(float), s, V, B,
+                     NV, D, dense_idx, out, ldo);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+void dlrm_interact_bwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, const bf16_t* dout, int ldo,
+                       float* dV, bf16_t* d_dense, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(dlrm_interact_bwd_kernel, (int)std::min<int64_t>(B, 8192), 256,
+                     (NV * D + NV * NV) * sizeof(float), s, V, B, NV, D, dense_idx, dout, ldo, dV, d_dense);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace minips_k

@@ -383,3 +383,32 @@ void embedding_bag_bwd(const float* grad_out, const int64_t* idx, const int64_t*
 }
 
 }  // namespace minips_k
+
+namespace minips_k {
+
+// out[b, f*D : (f+1)*D] = rows[inv[b*F+f], 0:D] (bf16, 16-byte chunks; D % 8 == 0).
+__global__ void lookup_rows_kernel(const bf16_t* __restrict__ rows, int row_stride, const int64_t* __restrict__ inv,
+                                   int64_t B, int F, int D, bf16_t* __restrict__ out, int ldo) {
+  const int chunks = D >> 3;
+  const int64_t total = B * F * chunks;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bf = c / chunks;
+    const int ch = (int)(c - bf * chunks);
+    const int64_t b = bf / F;
+    const int f = (int)(bf - b * F);
+    const bf16_t* src = rows + inv[bf] * row_stride + ch * 8;
+    const uint2 lo = *reinterpret_cast<const uint2*>(src), hi = *reinterpret_cast<const uint2*>(src + 4);
+    *reinterpret_cast<uint4*>(out + b * ldo + f * D + ch * 8) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
+
+void lookup_rows(const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B, int F, int D, bf16_t* out, int ldo,
+                 hipStream_t s) {
+  if (D % 8 || row_stride % 4 || ldo % 8) throw std::runtime_error("lookup_rows: D%8, row_stride%4, ldo%8 required");
+  if (B <= 0) return;
+  hipLaunchKernelGGL(lookup_rows_kernel, grid_for(B * F * (D / 8), 256, 8192), 256, 0, s, rows, row_stride, inv, B, F,
+                     D, out, ldo);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace minips_k

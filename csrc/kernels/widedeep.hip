@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kEmbTB) void wd_emb_backward_kernel(const float* __
   const int t = threadIdx.x;
   const int f = blockIdx.y;
   const int64_t b0 = (int64_t)blockIdx.x * kEmbTB;
-  const int W = D + 1;
+  const int W = dwide ? D + 1 : D;
   const int nb = (int)min((int64_t)kEmbTB, B - b0);
   for (int j = t; j < kEmbHash; j += kEmbTB) hkey[j] = -1;
   if (t == 0) nd = 0;
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(kEmbTB) void wd_emb_backward_kernel(const float* __
     const int k = e / D, d = e - k * D;
     atomicAdd(acc + cidx[k] * W + d, dX[(b0 + k) * ldx + (int64_t)f * D + d]);
   }
-  if (t < nb) atomicAdd(acc + cidx[t] * W + D, dwide[b0 + t]);
+  if (dwide && t < nb) atomicAdd(acc + cidx[t] * W + D, dwide[b0 + t]);
   __syncthreads();
   for (int e = t; e < ndist * W; e += kEmbTB) {
     const int k = e / W, d = e - k * W;
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(kEmbTB) void wd_emb_backward_kernel(const float* __
 void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                      float* grad_rows, int row_stride, hipStream_t s) {
   if (B <= 0) return;
-  if (row_stride < D + 1) throw std::runtime_error("wd_emb_backward: row_stride < D + 1");
+  if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("wd_emb_backward: row_stride too small");
   const size_t lds = (size_t)kEmbTB * (D + 1) * sizeof(float);
   if (lds > 96 * 1024) throw std::runtime_error("wd_emb_backward: D too large");
   dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);

@@ -1,0 +1,144 @@
+"""DLRM-style model with a (up to) 10B-row embedding table sharded over the PS ranks
+(BASELINE config 5), asynchronous SGD by default.
+
+  sparse: one SparseTable row per categorical id, width D (default 64), 64-bit keys, row-wise
+          Adagrad (1 float of optimizer state per row: 10B rows x 64 fp32 = 2.56 TB of weights
+          + 40 GB of state over 8 x 288 GB -- sized per rank by `rows`).
+  dense:  bottom MLP 13 -> 512 -> 256 -> D, dot interaction of the D-vector with the 26
+          embeddings (351 pairs + D), top MLP 416 -> 512 -> 256 -> 1, BCE. One DenseTable.
+Consistency "asp" runs every Clock's exchange (all-to-all-v over RCCL point-to-point
+send/recv + apply) on a side stream without gating the next Gets beyond a 2-clock bound;
+"bsp"/"ssp" are available as for the other models.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from ..ps.comm import Comm
+from ..ps.tables import DenseTable, SparseTable
+from .layers import Linear, ParamLayout, align, ext_activation
+
+
+@dataclass
+class DLRMConfig:
+    num_rows: int = 10_000_000_000
+    F: int = 26
+    n_dense: int = 13
+    D: int = 64
+    bottom: tuple = (512, 256)
+    top: tuple = (512, 256)
+    lr_dense: float = 1e-3
+    lr_sparse: float = 0.02
+    consistency: str = "asp"
+    staleness: int = 0
+    p2p: bool = True
+    seed: int = 0
+    cards: list = field(default_factory=list)  # optional per-feature cardinalities (sum <= num_rows)
+
+
+class DLRM:
+    def __init__(self, cfg: DLRMConfig, comm: Comm):
+        self.cfg, self.comm = cfg, comm
+        D, F = cfg.D, cfg.F
+        self.NV = F + 1
+        self.emb = SparseTable(comm, cfg.num_rows, D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
+                               consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01, seed=cfg.seed,
+                               p2p=cfg.p2p)
+        self.layout = ParamLayout()
+        dims = [cfg.n_dense, *cfg.bottom, D]
+        self.bottom = [Linear(self.layout, f"bot{i}", dims[i], dims[i + 1]) for i in range(len(dims) - 1)]
+        self.n_int = D + self.NV * (self.NV - 1) // 2
+        tdims = [self.n_int, *cfg.top]
+        self.top = [Linear(self.layout, f"top{i}", tdims[i], tdims[i + 1]) for i in range(len(tdims) - 1)]
+        self.layout.add("head", (cfg.top[-1] + 8,))
+        self.dense = DenseTable(comm, self.layout.size, optimizer="adam", lr=cfg.lr_dense,
+                                consistency=cfg.consistency, staleness=cfg.staleness, p2p=False)
+        g = torch.Generator().manual_seed(cfg.seed + 3)
+        full = torch.zeros(self.layout.size)
+        for l in self.bottom + self.top:
+            l.init(full, g)
+        h = self.layout.view(full, "head")
+        h[: cfg.top[-1]].uniform_(-cfg.top[-1] ** -0.5, cfg.top[-1] ** -0.5, generator=g)
+        self.dense.load_full(full)
+        self._bufs = {}
+
+    def _buffers(self, B):
+        if B not in self._bufs:
+            dev, cfg = self.comm.device, self.cfg
+            bf = dict(dtype=torch.bfloat16, device=dev)
+            bdims = [cfg.n_dense, *cfg.bottom]
+            self._bufs[B] = dict(
+                bacts=[ext_activation(B, d, dev) for d in bdims],
+                bgrads=[torch.empty(B, d, **bf) for d in cfg.bottom],
+                V=torch.zeros(B, self.NV * cfg.D, **bf),
+                tacts=[ext_activation(B, self.n_int, dev)] + [ext_activation(B, d, dev) for d in cfg.top[:-1]],
+                H=torch.empty(B, cfg.top[-1], **bf), dH=torch.empty(B, cfg.top[-1], **bf),
+                tgrads=[torch.empty(B, d, **bf) for d in cfg.top[:-1]],
+                dI=torch.zeros(B, align(self.n_int), **bf),
+                dV=torch.empty(B, self.NV * cfg.D, dtype=torch.float32, device=dev),
+                dbot=torch.empty(B, cfg.D, **bf),
+                zero=torch.zeros(B, dtype=torch.float32, device=dev),
+                dwide=torch.empty(B, dtype=torch.float32, device=dev),
+                loss=torch.zeros(1, device=dev),
+            )
+        return self._bufs[B]
+
+    def train_step(self, dense, keys, labels):
+        cfg = self.cfg
+        B, F, D = dense.shape[0], cfg.F, cfg.D
+        b = self._buffers(B)
+        rows, plan = self.emb.get(keys)
+        P = self.dense.get()
+        G = self.dense.grad
+        # V = [emb_0 .. emb_{F-1} | bottom(dense)]  (the dense vector is the last one)
+        ops.lookup_rows(rows, plan.inv, F, D, b["V"])
+        ba = b["bacts"]
+        ba[0][:, : cfg.n_dense].copy_(dense)
+        for i, l in enumerate(self.bottom):
+            out = ba[i + 1] if i + 1 < len(self.bottom) else b["V"][:, F * D:]
+            l.forward(P, ba[i], out, "relu")
+        ta = b["tacts"]
+        ops.dlrm_interact_fwd(b["V"], self.NV, D, ta[0], dense_idx=F)
+        for i, l in enumerate(self.top):
+            out = ta[i + 1] if i + 1 < len(self.top) else b["H"]
+            l.forward(P, ta[i], out, "relu")
+        hw = self.layout.view(P, "head")
+        hg = self.layout.view(G, "head")
+        h = cfg.top[-1]
+        b["loss"].zero_()
+        ops.wd_head(b["H"], hw[:h], hw[h:h + 1], b["zero"], labels, b["dH"], hg[:h], hg[h:h + 1], b["dwide"],
+                    b["loss"], None, 1.0 / (B * self.comm.world))
+        dy = b["dH"]
+        for i in range(len(self.top) - 1, -1, -1):
+            l = self.top[i]
+            l.wgrad(G, dy, ta[i])
+            if i > 0:
+                dx = b["tgrads"][i - 1]
+                l.dgrad(P, dy, dx, mask=ta[i])
+            else:
+                dx = b["dI"]
+                l.dgrad(P, dy, dx)
+            dy = dx
+        ops.dlrm_interact_bwd(b["V"], self.NV, D, b["dI"], b["dV"], b["dbot"], dense_idx=F)
+        dy = b["dbot"]
+        for i in range(len(self.bottom) - 1, -1, -1):
+            l = self.bottom[i]
+            l.wgrad(G, dy, ba[i])
+            if i > 0:
+                dx = b["bgrads"][i - 1]
+                l.dgrad(P, dy, dx, mask=ba[i])
+                dy = dx
+        grad_rows = torch.zeros(max(plan.U, 1), D, dtype=torch.float32, device=self.comm.device)
+        ops.wd_emb_backward(b["dV"], None, plan.inv, F, D, grad_rows, x_off=0)
+        self.emb.add(plan, grad_rows)
+        self.dense.add()
+        self.emb.clock()
+        self.dense.clock()
+        return b["loss"]
+
+    def drain(self):
+        self.emb.drain()
+        self.dense.drain()

@@ -1,0 +1,97 @@
+"""Building blocks shared by the dense-tower models on the GPU parameter server.
+
+ParamLayout   names -> (offset, shape) views into one flat parameter vector (the DenseTable
+              master / pulled copy / gradient buffer all share the layout).
+Linear        bias folded into the weight: W_ext [n_out, k_pad] with the bias in column k_in;
+              activations carry a constant-1 column at k_in (see ext_activation), so the
+              forward GEMM adds the bias and the weight-gradient GEMM yields the bias gradient.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+
+
+def align(n: int, a: int = 8) -> int:
+    return (n + a - 1) // a * a
+
+
+class ParamLayout:
+    def __init__(self):
+        self.entries: dict[str, tuple[int, tuple]] = {}
+        self.size = 0
+
+    def add(self, name: str, shape: tuple) -> str:
+        n = 1
+        for s in shape:
+            n *= s
+        self.entries[name] = (self.size, tuple(shape))
+        self.size += align(n, 64)  # 128-byte aligned segments (bf16 and fp32 views stay 16-B aligned)
+        return name
+
+    def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        off, shape = self.entries[name]
+        n = 1
+        for s in shape:
+            n *= s
+        return buf[off: off + n].view(shape)
+
+
+def ext_activation(rows: int, k_in: int, device, dtype=torch.bfloat16) -> torch.Tensor:
+    """[rows, align8(k_in + 1)] activation buffer whose column k_in is the constant 1."""
+    t = torch.zeros(rows, align(k_in + 1), dtype=dtype, device=device)
+    t[:, k_in] = 1.0
+    return t
+
+
+class Linear:
+    """A bias-folded Linear(k_in -> n_out) living in a ParamLayout."""
+
+    def __init__(self, layout: ParamLayout, name: str, k_in: int, n_out: int, n_pad: int | None = None):
+        self.name, self.k_in, self.n_out = name, k_in, n_out
+        self.k_pad = align(k_in + 1)
+        self.n_rows = n_pad or n_out  # rows beyond n_out stay zero (K-padding of the next dgrad)
+        layout.add(name, (self.n_rows, self.k_pad))
+        self.layout = layout
+
+    def init(self, full: torch.Tensor, gen, std: float | None = None):
+        w = self.layout.view(full, self.name)
+        w.zero_()
+        if std is None:
+            bound = 1.0 / math.sqrt(self.k_in)
+            w[: self.n_out, : self.k_in].uniform_(-bound, bound, generator=gen)
+        else:
+            w[: self.n_out, : self.k_in].normal_(0.0, std, generator=gen)
+
+    def W(self, P):
+        return self.layout.view(P, self.name)
+
+    def forward(self, P, x_ext, out, act="relu", aux=None):
+        """out[:, :n_out] = act(x_ext W_ext^T); x_ext carries the ones column."""
+        W = self.W(P)
+        M = x_ext.shape[0]
+        if act == "gelu_aux":
+            return ops.gemm(x_ext, W, out, M, self.n_out, self.k_pad, False, False, ops.EPI_BIAS_GELU_AUX_BF16,
+                            mask=aux)
+        epi = {"relu": ops.EPI_BIAS_RELU_BF16, "none": ops.EPI_BIAS_BF16}[act]
+        return ops.gemm(x_ext, W, out, M, self.n_out, self.k_pad, False, False, epi)
+
+    def wgrad(self, G, dy, x_ext):
+        """G_W += dy^T x_ext (split-K; the bias gradient lands in column k_in)."""
+        return ops.linear_wgrad(dy, x_ext, self.W(G))
+
+    def dgrad(self, P, dy, out, mask=None, gelu_u=None, out_f32=False, k_rows=None):
+        """out = dy W[:, :k_in] (ReLU-masked by `mask`, or times gelu'(gelu_u))."""
+        W = self.W(P)
+        M = dy.shape[0]
+        K = k_rows or self.n_rows
+        if out_f32:
+            return ops.gemm(dy, W, out, M, self.k_in, K, False, True, ops.EPI_STORE_F32)
+        if gelu_u is not None:
+            return ops.gemm(dy, W, out, M, self.k_in, K, False, True, ops.EPI_GELU_GRAD_BF16, mask=gelu_u)
+        if mask is not None:
+            return ops.gemm(dy, W, out, M, self.k_in, K, False, True, ops.EPI_RELU_MASK_BF16, mask=mask)
+        return ops.gemm(dy, W, out, M, self.k_in, K, False, True, ops.EPI_STORE_BF16)

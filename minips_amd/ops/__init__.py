@@ -21,6 +21,14 @@ EPI_BIAS_BF16 = 3
 EPI_STORE_BF16 = 4
 EPI_RELU_MASK_BF16 = 5
 EPI_BIAS_GELU_BF16 = 6
+EPI_BIAS_GELU_AUX_BF16 = 7  # C = gelu(u), mask(aux) = u  (pre-activation saved for backward)
+EPI_GELU_GRAD_BF16 = 8      # C = acc * gelu'(mask)
+
+
+def _gelu_grad(u):
+    k, c = 0.7978845608, 0.044715
+    t = torch.tanh(k * (u + c * u ** 3))
+    return 0.5 * (1 + t) + 0.5 * u * (1 - t * t) * k * (1 + 3 * c * u * u)
 
 
 def _gpu(t: torch.Tensor) -> bool:
@@ -41,6 +49,13 @@ def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None,
         C[:M, :N] = acc
     elif epi == EPI_ATOMIC_F32:
         C[:M, :N] += acc
+    elif epi == EPI_BIAS_GELU_AUX_BF16:
+        if bias is not None:
+            acc = acc + bias[:N].float()
+        mask[:M, :N] = acc.to(torch.bfloat16)
+        C[:M, :N] = torch.nn.functional.gelu(acc, approximate="tanh").to(torch.bfloat16)
+    elif epi == EPI_GELU_GRAD_BF16:
+        C[:M, :N] = (acc * _gelu_grad(mask[:M, :N].float())).to(torch.bfloat16)
     elif epi in (EPI_BIAS_RELU_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU_BF16):
         if bias is not None:
             acc = acc + bias[:N].float()
@@ -58,6 +73,27 @@ def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None,
             colsum[:N] += out.float().sum(0)
     else:
         raise ValueError(f"unknown epilogue {epi}")
+    return C
+
+
+def gemm_batched(A, B, C, M, N, K, a_km, b_kn, epi, batch, inner, lda, ldb, ldc, strides, alpha=1.0, bias=None):
+    """``batch`` GEMMs over flat buffers; operand z starts at (z//inner)*s_outer + (z%inner)*s_inner
+    (strides = [sa_o, sa_i, sb_o, sb_i, sc_o, sc_i] in elements), leading dims lda/ldb/ldc."""
+    if _gpu(A):
+        kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, None, None, float(alpha), 1, int(batch), int(inner),
+                       int(lda), int(ldb), int(ldc), [int(x) for x in strides])
+        return C
+    Af, Bf, Cf = A.reshape(-1), B.reshape(-1), C.reshape(-1)
+    for z in range(batch):
+        zo, zi = divmod(z, inner)
+        oa, ob, oc = (zo * strides[0] + zi * strides[1], zo * strides[2] + zi * strides[3],
+                      zo * strides[4] + zi * strides[5])
+        ar, ac = (K, M) if a_km else (M, K)
+        br, bc = (K, N) if b_kn else (N, K)
+        a = Af[oa: oa + (ar - 1) * lda + ac].as_strided((ar, ac), (lda, 1))
+        b = Bf[ob: ob + (br - 1) * ldb + bc].as_strided((br, bc), (ldb, 1))
+        c = Cf[oc: oc + (M - 1) * ldc + N].as_strided((M, N), (ldc, 1))
+        gemm(a, b, c, M, N, K, a_km, b_kn, epi, bias=bias, alpha=alpha)
     return C
 
 
@@ -117,6 +153,16 @@ def gather_rows(table, keys, base, out):
         return out
     rows = table[(keys - base), : out.shape[1]]
     out[: keys.numel()] = rows.to(out.dtype)
+    return out
+
+
+def lookup_rows(rows, inv, F, D, out):
+    """out[b, f*D:(f+1)*D] = rows[inv[b*F+f], :D] (bf16; out may be a row-major column slice)."""
+    if _gpu(rows):
+        kernels().lookup_rows(rows, inv, int(F), int(D), out)
+        return out
+    B = out.shape[0]
+    out[:, : F * D] = rows[inv, :D].reshape(B, F * D).to(out.dtype)
     return out
 
 
@@ -216,14 +262,16 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
         dH_colsum += g.float().sum(0)
 
 
-def wd_emb_backward(dX, dwide, inv, F, D, grad_rows):
+def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0):
+    """grad_rows[inv[b*F+f], :D] += dX[b, x_off + f*D : ...]; column D += dwide[b] if given."""
     if _gpu(dX):
-        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows)
+        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off))
         return grad_rows
     B = dX.shape[0]
-    g = dX[:, : F * D].reshape(B * F, D)
+    g = dX[:, x_off: x_off + F * D].reshape(B * F, D)
     grad_rows[:, :D].index_add_(0, inv, g)
-    grad_rows[:, D].index_add_(0, inv, dwide.repeat_interleave(F))
+    if dwide is not None:
+        grad_rows[:, D].index_add_(0, inv, dwide.repeat_interleave(F))
     return grad_rows
 
 
@@ -302,6 +350,126 @@ def kmeans_assign(X, C, assign=None, dist=None):
     if dist is not None:
         dist.copy_(best.to(dist.dtype))
     return assign
+
+
+# ----------------------------------------------------------------------------- dense models
+def layernorm_fwd(x, C, gamma, beta, eps, y, mean, rstd):
+    if _gpu(x):
+        kernels().layernorm_fwd(x, int(C), gamma, beta, float(eps), y, mean, rstd)
+        return y
+    xf = x[:, :C].float()
+    mu = xf.mean(1)
+    var = (xf * xf).mean(1) - mu * mu
+    rs = torch.rsqrt(var.clamp_min(0) + eps)
+    y[:, :C] = ((xf - mu[:, None]) * rs[:, None] * gamma.float() + beta.float()).to(torch.bfloat16)
+    mean.copy_(mu)
+    rstd.copy_(rs)
+    return y
+
+
+def layernorm_bwd(x, dy, C, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=False):
+    if _gpu(x):
+        kernels().layernorm_bwd(x, dy, int(C), gamma, mean, rstd, dx, dgamma, dbeta, bool(accumulate))
+        return dx
+    xh = (x[:, :C].float() - mean[:, None]) * rstd[:, None]
+    d = dy[:, :C].float()
+    g = d * gamma.float()
+    a = g.mean(1, keepdim=True)
+    b = (g * xh).mean(1, keepdim=True)
+    v = rstd[:, None] * (g - a - xh * b)
+    if accumulate:
+        v = v + dx[:, :C].float()
+    dx[:, :C] = v.to(torch.bfloat16)
+    dgamma += (d * xh).sum(0)
+    dbeta += d.sum(0)
+    return dx
+
+
+def softmax_xent(logits, V, labels, scale, loss_sum, correct=None):
+    """In place: logits[:, :V] <- (softmax - onehot) * scale (bf16); loss_sum += sum CE."""
+    if _gpu(logits):
+        kernels().softmax_xent(logits, int(V), labels, float(scale), loss_sum, correct)
+        return logits
+    z = logits[:, :V].float()
+    lse = torch.logsumexp(z, 1)
+    loss_sum += (lse - z.gather(1, labels[:, None]).squeeze(1)).sum()
+    if correct is not None:
+        correct += (z.argmax(1) == labels).float().sum()
+    p = torch.softmax(z, 1)
+    p[torch.arange(z.shape[0]), labels] -= 1.0
+    logits[:, :V] = (p * scale).to(torch.bfloat16)
+    return logits
+
+
+def causal_softmax_fwd(S, T, P):
+    if _gpu(S):
+        kernels().causal_softmax_fwd(S, int(T), P)
+        return P
+    s = S.reshape(-1, T, T).float()
+    mask = torch.ones(T, T, dtype=torch.bool).triu(1)
+    P.view(-1, T, T).copy_(torch.softmax(s.masked_fill(mask, float("-inf")), -1).to(P.dtype))
+    return P
+
+
+def causal_softmax_bwd(P, dP, T, scale, dS):
+    if _gpu(P):
+        kernels().causal_softmax_bwd(P, dP, int(T), float(scale), dS)
+        return dS
+    p = P.reshape(-1, T, T).float()
+    dp = dP.reshape(-1, T, T).float()
+    mask = torch.ones(T, T, dtype=torch.bool).triu(1)
+    dp = dp.masked_fill(mask, 0.0)
+    ds = p * (dp - (p * dp).sum(-1, keepdim=True)) * scale
+    dS.view(-1, T, T).copy_(ds.to(dS.dtype))
+    return dS
+
+
+def gelu_bwd(dh, u, du):
+    if _gpu(u):
+        kernels().gelu_bwd(dh, u, du)
+        return du
+    du.copy_((dh.float() * _gelu_grad(u.float())).to(du.dtype))
+    return du
+
+
+def add_bf16(a, b, out):
+    if _gpu(a):
+        kernels().add_bf16(a, b, out)
+        return out
+    out.copy_((a.float() + b.float()).to(out.dtype))
+    return out
+
+
+def dlrm_interact_fwd(V, NV, D, out, dense_idx=0):
+    """V [B, NV, D] bf16 -> out[b] = [V[b,dense_idx] | V_i . V_j for i > j (lower triangle, row-major)]."""
+    if _gpu(V):
+        kernels().dlrm_interact_fwd(V, int(NV), int(D), int(dense_idx), out)
+        return out
+    v = V.reshape(-1, NV, D).float()
+    z = v @ v.transpose(1, 2)
+    ii, jj = torch.tril_indices(NV, NV, -1)
+    out[:, :D] = V.reshape(-1, NV, D)[:, dense_idx]
+    out[:, D: D + ii.numel()] = z[:, ii, jj].to(out.dtype)
+    return out
+
+
+def dlrm_interact_bwd(V, NV, D, dout, dV, d_dense, dense_idx=0):
+    """dV fp32 [B, NV*D]; d_dense bf16 [B, D] = dV[:, dense_idx] * (V[:, dense_idx] > 0)."""
+    if _gpu(V):
+        kernels().dlrm_interact_bwd(V, int(NV), int(D), int(dense_idx), dout, dV, d_dense)
+        return dV
+    v = V.reshape(-1, NV, D).float()
+    B = v.shape[0]
+    ii, jj = torch.tril_indices(NV, NV, -1)
+    dz = torch.zeros(B, NV, NV)
+    g = dout[:, D: D + ii.numel()].float()
+    dz[:, ii, jj] = g
+    dz[:, jj, ii] = g
+    d = dz @ v
+    d[:, dense_idx] += dout[:, :D].float()
+    dV.view(B, NV, D).copy_(d)
+    d_dense.copy_(torch.where(v[:, dense_idx] > 0, d[:, dense_idx], torch.zeros_like(d[:, dense_idx])).to(d_dense.dtype))
+    return dV
 
 
 def kaiming_uniform_(w: torch.Tensor, fan_in: int, gen=None):

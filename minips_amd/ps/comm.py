@@ -42,8 +42,13 @@ class Comm:
         self.stats = CommStats()
 
     # -- helpers ------------------------------------------------------------------------
-    def all_to_all_v(self, out: torch.Tensor, inp: torch.Tensor, recv_splits: list[int], send_splits: list[int]):
-        """Rows of ``inp`` split by ``send_splits`` go to ranks 0..P-1; ``out`` gets recv_splits."""
+    def all_to_all_v(self, out: torch.Tensor, inp: torch.Tensor, recv_splits: list[int], send_splits: list[int],
+                     p2p: bool = False):
+        """Rows of ``inp`` split by ``send_splits`` go to ranks 0..P-1; ``out`` gets recv_splits.
+
+        p2p=True issues the exchange as grouped point-to-point send/recv pairs (one per peer
+        with a non-empty message, the own segment copied locally) -- the SSP/ASP data path;
+        otherwise one RCCL all-to-all-v."""
         self.stats.calls += 1
         if self.world == 1:
             n = send_splits[0]
@@ -51,9 +56,30 @@ class Comm:
                 out[:n].copy_(inp[:n])
             return out
         self.stats.bytes_a2a += inp[: sum(send_splits)].numel() * inp.element_size()
-        o = out[: sum(recv_splits)]
-        i = inp[: sum(send_splits)]
-        dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
+        if not p2p:
+            o = out[: sum(recv_splits)]
+            i = inp[: sum(send_splits)]
+            dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
+            return out
+        so = [0]
+        for c in send_splits:
+            so.append(so[-1] + c)
+        ro = [0]
+        for c in recv_splits:
+            ro.append(ro[-1] + c)
+        ops_ = []
+        for peer in range(self.world):
+            if peer == self.rank:
+                if send_splits[peer]:
+                    out[ro[peer]: ro[peer + 1]].copy_(inp[so[peer]: so[peer + 1]])
+                continue
+            if send_splits[peer]:
+                ops_.append(dist.P2POp(dist.isend, inp[so[peer]: so[peer + 1]].contiguous(), peer, group=self.group))
+            if recv_splits[peer]:
+                ops_.append(dist.P2POp(dist.irecv, out[ro[peer]: ro[peer + 1]], peer, group=self.group))
+        if ops_:
+            for r in dist.batch_isend_irecv(ops_):
+                r.wait()
         return out
 
     def exchange_counts(self, counts: torch.Tensor) -> tuple[list[int], list[int]]:

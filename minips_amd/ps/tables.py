@@ -97,7 +97,7 @@ class _Pipeline:
 class DenseTable:
     def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
                  pull_dtype=torch.bfloat16, consistency: str = "bsp", staleness: int = 0, table_id: int = 0,
-                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, p2p: bool = False):
         self.comm = comm
         self.table_id = table_id
         self.n_params = n_params
@@ -211,7 +211,7 @@ class SparseTable:
     def __init__(self, comm: Comm, num_rows: int, width: int, optimizer: str = "rowwise_adagrad",
                  lr: float = 0.01, eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "bsp",
                  staleness: int = 0, split: int | None = None, table_id: int = 0, init_std: float = 0.01,
-                 seed: int = 1234):
+                 seed: int = 1234, p2p: bool | None = None):
         self.comm = comm
         self.table_id = table_id
         self.num_rows = num_rows
@@ -236,6 +236,8 @@ class SparseTable:
             if optimizer == "rowwise_adagrad" else None
         self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
         self.pipe = _Pipeline(comm, consistency, staleness)
+        # SSP/ASP move rows with point-to-point send/recv by default, BSP with all-to-all-v
+        self.p2p = (consistency != "bsp") if p2p is None else p2p
         self._pending: list = []
 
     # -- KV API -----------------------------------------------------------------------------
@@ -247,7 +249,7 @@ class SparseTable:
         U = int(sum(send))
         M = int(sum(recv))
         recv_keys = torch.empty(M, dtype=torch.int64, device=keys.device)
-        self.comm.all_to_all_v(recv_keys, uniq, recv, send)
+        self.comm.all_to_all_v(recv_keys, uniq, recv, send, p2p=self.p2p)
         p = SparsePlan(keys.numel(), inv, uniq, U, send, recv, recv_keys)
         if self.comm.world > 1 and M > 0:
             own_bounds = torch.tensor([0, 1 << 62], dtype=torch.int64, device=keys.device)
@@ -266,7 +268,7 @@ class SparseTable:
         served = torch.empty(len(plan.recv_keys), self.width, dtype=self.pull_dtype, device=dev)
         ops.gather_rows(self.shard, plan.recv_keys, self.base, served)
         rows = torch.empty(plan.U, self.width, dtype=self.pull_dtype, device=dev)
-        self.comm.all_to_all_v(rows, served, plan.send, plan.recv)
+        self.comm.all_to_all_v(rows, served, plan.send, plan.recv, p2p=self.p2p)
         return rows, plan
 
     def get_rows(self, keys: torch.Tensor) -> torch.Tensor:
@@ -304,7 +306,7 @@ class SparseTable:
         else:
             M = len(plan.recv_keys)
             recv = torch.empty(M, self.width, dtype=torch.float32, device=dev)
-            self.comm.all_to_all_v(recv, grad_rows, plan.recv, plan.send)
+            self.comm.all_to_all_v(recv, grad_rows, plan.recv, plan.send, p2p=self.p2p)
             if M == 0:
                 return
             g = torch.zeros(plan.own_U, self.width, dtype=torch.float32, device=dev)

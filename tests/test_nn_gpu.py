@@ -1,0 +1,195 @@
+"""Numerics of the dense-model gfx950 kernels (LayerNorm, softmax-xent, causal softmax,
+GELU, residual add, DLRM interaction, lookup, batched/strided GEMM, GELU epilogues) against
+the plain-PyTorch fp32 reference of the same op, plus GPU-vs-CPU model steps (MLP, DLRM)."""
+import pytest
+import torch
+
+from minips_amd import _native, ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _require_kernels(dev):
+    _native.kernels()
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def _close(a, b, tol):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), rtol=tol, atol=tol)
+
+
+def test_layernorm(dev):
+    g = torch.Generator().manual_seed(1)
+    M, C, ld = 300, 768, 776
+    x = _bf(torch.randn(M, ld, generator=g) * 2 + 0.5)
+    gamma, beta = _bf(torch.randn(C, generator=g)), _bf(torch.randn(C, generator=g))
+    outs = {}
+    for d in ("cpu", dev):
+        y = torch.zeros(M, ld, dtype=torch.bfloat16, device=d)
+        mean, rstd = torch.empty(M, device=d), torch.empty(M, device=d)
+        ops.layernorm_fwd(x.to(d), C, gamma.to(d), beta.to(d), 1e-5, y, mean, rstd)
+        dy = _bf(torch.randn(M, ld, generator=torch.Generator().manual_seed(2))).to(d)
+        dx = torch.zeros(M, ld, dtype=torch.bfloat16, device=d)
+        dg, db = torch.zeros(C, device=d), torch.zeros(C, device=d)
+        ops.layernorm_bwd(x.to(d), dy, C, gamma.to(d), mean, rstd, dx, dg, db)
+        outs[str(d)] = (y, mean, rstd, dx, dg, db)
+    c, gp = outs["cpu"], outs[str(dev)]
+    _close(gp[0][:, :C], c[0][:, :C], 3e-2)
+    _close(gp[1], c[1], 1e-4)
+    _close(gp[2], c[2], 1e-3)
+    _close(gp[3][:, :C], c[3][:, :C], 5e-2)
+    _close(gp[4], c[4], 0.3)
+    _close(gp[5], c[5], 0.3)
+
+
+@pytest.mark.parametrize("V,ld", [(10, 16), (1000, 1000), (50257, 50264)])
+def test_softmax_xent(dev, V, ld):
+    g = torch.Generator().manual_seed(V)
+    M = 64
+    z = _bf(torch.randn(M, ld, generator=g) * 3)
+    y = torch.randint(0, V, (M,), generator=g)
+    res = {}
+    for d in ("cpu", dev):
+        lg = z.clone().to(d)
+        loss, corr = torch.zeros(1, device=d), torch.zeros(1, device=d)
+        ops.softmax_xent(lg, V, y.to(d), 0.5, loss, corr)
+        res[str(d)] = (lg[:, :V], loss, corr)
+    c, gp = res["cpu"], res[str(dev)]
+    _close(gp[0], c[0], 1e-2)
+    _close(gp[1], c[1], 1e-3 * M)
+    assert abs(float(gp[2]) - float(c[2])) <= 1
+
+
+@pytest.mark.parametrize("T", [64, 128, 1024])
+def test_causal_softmax(dev, T):
+    g = torch.Generator().manual_seed(T)
+    BH = 3
+    S = torch.randn(BH, T, T, generator=g) * 4
+    dP = torch.randn(BH, T, T, generator=g)
+    res = {}
+    for d in ("cpu", dev):
+        P = torch.empty(BH, T, T, dtype=torch.bfloat16, device=d)
+        ops.causal_softmax_fwd(S.to(d), T, P)
+        dS = torch.empty(BH, T, T, dtype=torch.bfloat16, device=d)
+        ops.causal_softmax_bwd(P, dP.to(d), T, 0.125, dS)
+        res[str(d)] = (P, dS)
+    _close(res[str(dev)][0], res["cpu"][0], 1e-2)
+    _close(res[str(dev)][1], res["cpu"][1], 2e-2)
+
+
+def test_gelu_add(dev):
+    g = torch.Generator().manual_seed(5)
+    u, dh, b = (_bf(torch.randn(4097, generator=g) * 2) for _ in range(3))
+    res = {}
+    for d in ("cpu", dev):
+        du = torch.empty(4097, dtype=torch.bfloat16, device=d)
+        ops.gelu_bwd(dh.to(d), u.to(d), du)
+        s = torch.empty_like(du)
+        ops.add_bf16(u.to(d), b.to(d), s)
+        res[str(d)] = (du, s)
+    _close(res[str(dev)][0], res["cpu"][0], 2e-2)
+    _close(res[str(dev)][1], res["cpu"][1], 1e-2)
+
+
+def test_dlrm_interaction_and_lookup(dev):
+    g = torch.Generator().manual_seed(8)
+    B, NV, D, F = 96, 27, 64, 26
+    U = 500
+    rows = _bf(torch.randn(U, D, generator=g))
+    inv = torch.randint(0, U, (B * F,), generator=g)
+    bottom = _bf(torch.relu(torch.randn(B, D, generator=g)) - 0.2)
+    dout = _bf(torch.randn(B, 416, generator=g))
+    res = {}
+    for d in ("cpu", dev):
+        V = torch.zeros(B, NV * D, dtype=torch.bfloat16, device=d)
+        ops.lookup_rows(rows.to(d), inv.to(d), F, D, V)
+        V[:, F * D:] = bottom.to(d)
+        out = torch.zeros(B, 416, dtype=torch.bfloat16, device=d)
+        ops.dlrm_interact_fwd(V, NV, D, out, dense_idx=F)
+        dV = torch.empty(B, NV * D, device=d)
+        dd = torch.empty(B, D, dtype=torch.bfloat16, device=d)
+        ops.dlrm_interact_bwd(V, NV, D, dout.to(d), dV, dd, dense_idx=F)
+        res[str(d)] = (V, out, dV, dd)
+    for a, b, tol in zip(res[str(dev)], res["cpu"], (0, 3e-2, 2e-2, 3e-2)):
+        _close(a, b, max(tol, 1e-6))
+
+
+def test_gemm_strided_batched_and_gelu(dev):
+    g = torch.Generator().manual_seed(11)
+    # batched: 2 outer x 3 inner "heads" of [T, hd] blocks interleaved inside [*, 3*hd] rows
+    Bo, H, T, hd = 2, 3, 128, 64
+    Q = _bf(torch.randn(Bo * T, H * hd, generator=g))
+    Kt = _bf(torch.randn(Bo * T, H * hd, generator=g))
+    strides = [T * H * hd, hd, T * H * hd, hd, H * T * T, T * T]
+    res = {}
+    for d in ("cpu", dev):
+        S = torch.zeros(Bo * H, T, T, device=d)
+        ops.gemm_batched(Q.to(d), Kt.to(d), S, T, T, hd, False, False, ops.EPI_STORE_F32, Bo * H, H, H * hd, H * hd,
+                         T, strides, alpha=0.125)
+        res[str(d)] = S
+    _close(res[str(dev)], res["cpu"], 2e-2)
+    # GELU aux epilogue and its gradient epilogue
+    M, N, K = 256, 384, 136
+    X, W = _bf(torch.randn(M, K, generator=g)), _bf(torch.randn(N, K, generator=g) * 0.1)
+    dY = _bf(torch.randn(M, N, generator=g))
+    out = {}
+    for d in ("cpu", dev):
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=d)
+        U = torch.empty(M, N, dtype=torch.bfloat16, device=d)
+        ops.gemm(X.to(d), W.to(d), C, M, N, K, False, False, ops.EPI_BIAS_GELU_AUX_BF16, mask=U)
+        dX = torch.empty(M, N, dtype=torch.bfloat16, device=d)
+        ops.gemm(dY.to(d), torch.eye(N, dtype=torch.bfloat16, device=d), dX, M, N, N, False, True,
+                 ops.EPI_GELU_GRAD_BF16, mask=U)
+        out[str(d)] = (C, U, dX)
+    for a, b in zip(out[str(dev)], out["cpu"]):
+        _close(a, b, 3e-2)
+
+
+# ------------------------------------------------------------------------------ models
+def test_mlp_gpu_matches_cpu(dev):
+    from minips_amd.data.synthetic import MnistSynth
+    from minips_amd.models.mlp import MLP, MLPConfig
+    from minips_amd.ps.comm import Comm
+
+    data = MnistSynth(256, device="cpu", seed=3)
+    batches = [data.next() for _ in range(4)]
+    losses = {}
+    for d in ("cpu", dev):
+        m = MLP(MLPConfig(), Comm(device=torch.device(d)))
+        ls = []
+        for x, y in batches:
+            loss, _ = m.train_step(x.to(d), y.to(d))
+            ls.append(float(loss) / 256)
+        m.drain()
+        losses[str(d)] = ls
+    for a, b in zip(losses[str(dev)], losses["cpu"]):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(b)), losses
+
+
+def test_dlrm_gpu_matches_cpu(dev):
+    from minips_amd.models.dlrm import DLRM, DLRMConfig
+    from minips_amd.ps.comm import Comm
+
+    g = torch.Generator().manual_seed(4)
+    batches = []
+    for _ in range(4):
+        dense = torch.randn(256, 13, generator=g)
+        keys = torch.randint(0, 20000, (256, 26), generator=g)
+        y = (dense[:, 0] > 0).float()
+        batches.append((dense, keys, y))
+    emb = torch.randn(20000, 64, generator=g) * 0.05
+    losses = {}
+    for d in ("cpu", dev):
+        m = DLRM(DLRMConfig(num_rows=20000, consistency="bsp"), Comm(device=torch.device(d)))
+        m.emb.shard.copy_(emb.to(d))
+        ls = []
+        for dense, keys, y in batches:
+            ls.append(float(m.train_step(dense.to(d), keys.to(d), y.to(d))) / 256)
+        m.drain()
+        losses[str(d)] = ls
+    for a, b in zip(losses[str(dev)], losses["cpu"]):
+        assert abs(a - b) < 2e-2, losses
