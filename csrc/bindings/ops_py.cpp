@@ -61,9 +61,9 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   std::vector<int64_t> st(6, 0);
   if (batch <= 1) {
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
-    TORCH_CHECK(A.size(0) == a_rows && A.size(1) >= a_cols, "A shape ", A.sizes(), " vs M,N,K=", M, ",", N, ",", K);
-    TORCH_CHECK(B.size(0) == b_rows && B.size(1) >= b_cols, "B shape ", B.sizes(), " vs M,N,K=", M, ",", N, ",", K);
-    TORCH_CHECK(C.size(0) == M && C.size(1) >= N, "C shape ", C.sizes(), " vs M,N=", M, ",", N);
+    TORCH_CHECK(A.size(0) >= a_rows && A.size(1) >= a_cols, "A shape ", A.sizes(), " vs M,N,K=", M, ",", N, ",", K);
+    TORCH_CHECK(B.size(0) >= b_rows && B.size(1) >= b_cols, "B shape ", B.sizes(), " vs M,N,K=", M, ",", N, ",", K);
+    TORCH_CHECK(C.size(0) >= M && C.size(1) >= N, "C shape ", C.sizes(), " vs M,N=", M, ",", N);
     lda = A.stride(0);
     ldb = B.stride(0);
     ldc = C.stride(0);
@@ -436,6 +436,36 @@ void add_bf16(const at::Tensor& a, const at::Tensor& b, at::Tensor& out) {
   minips_k::add_bf16(ptr<bf16_t>(a), ptr<bf16_t>(b), a.numel(), ptr<bf16_t>(out), stream_of(a));
 }
 
+void embed_fwd(const at::Tensor& wte, const at::Tensor& wpe, const at::Tensor& tok, int64_t T, at::Tensor& out) {
+  for (const at::Tensor* t : {&wte, &wpe, &tok, (const at::Tensor*)&out}) check_gpu(*t, "embed arg");
+  check_dtype(wte, at::kBFloat16, "wte");
+  check_dtype(wpe, at::kBFloat16, "wpe");
+  check_dtype(tok, at::kLong, "tok");
+  check_dtype(out, at::kBFloat16, "out");
+  const int64_t C = wte.size(1), M = tok.numel();
+  TORCH_CHECK(C % 8 == 0 && wpe.size(1) == C && wpe.size(0) >= T && out.dim() == 2 && out.stride(1) == 1 &&
+                  out.size(0) == M && out.size(1) >= C && out.stride(0) % 8 == 0,
+              "embed_fwd shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(wte.device());
+  minips_k::embed_fwd(ptr<bf16_t>(wte), ptr<bf16_t>(wpe), ptr<int64_t>(tok), M, (int)T, (int)C, ptr<bf16_t>(out),
+                      (int)out.stride(0), stream_of(wte));
+}
+
+void embed_bwd(const at::Tensor& dx, const at::Tensor& tok, int64_t T, at::Tensor& dwte, at::Tensor& dwpe) {
+  for (const at::Tensor* t : {&dx, &tok, (const at::Tensor*)&dwte, (const at::Tensor*)&dwpe}) check_gpu(*t, "embed arg");
+  check_dtype(dx, at::kBFloat16, "dx");
+  check_dtype(tok, at::kLong, "tok");
+  check_dtype(dwte, at::kFloat, "dwte");
+  check_dtype(dwpe, at::kFloat, "dwpe");
+  const int64_t C = dwte.size(1), M = tok.numel();
+  TORCH_CHECK(C % 2 == 0 && dwpe.size(1) == C && dwpe.size(0) >= T && dx.dim() == 2 && dx.stride(1) == 1 &&
+                  dx.size(0) == M && dx.size(1) >= C && dx.stride(0) % 2 == 0,
+              "embed_bwd shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dx.device());
+  minips_k::embed_bwd(ptr<bf16_t>(dx), (int)dx.stride(0), ptr<int64_t>(tok), M, (int)T, (int)C, ptr<float>(dwte),
+                      ptr<float>(dwpe), stream_of(dx));
+}
+
 void dlrm_interact_fwd(const at::Tensor& V, int64_t NV, int64_t D, int64_t dense_idx, at::Tensor& out) {
   check_gpu(V, "V");
   check_gpu(out, "out");
@@ -490,6 +520,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("gather_rows", &gather_rows);
   m.def("scatter_add_rows", &scatter_add_rows);
   m.def("lookup_rows", &lookup_rows);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
   m.def("sparse_rowwise_adagrad", &sparse_rowwise_adagrad);
   m.def("sparse_sgd", &sparse_sgd);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);

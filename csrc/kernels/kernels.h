@@ -125,6 +125,10 @@ void causal_softmax_bwd(const bf16_t* P, const float* dP, int64_t rows, int T, f
                         hipStream_t s);
 void gelu_bwd(const bf16_t* dh, const bf16_t* u, int64_t n, bf16_t* du, hipStream_t s);
 void add_bf16(const bf16_t* a, const bf16_t* b, int64_t n, bf16_t* out, hipStream_t s);
+void embed_fwd(const bf16_t* wte, const bf16_t* wpe, const int64_t* tok, int64_t M, int T, int C, bf16_t* out, int ldo,
+               hipStream_t s);
+void embed_bwd(const bf16_t* dx, int ldx, const int64_t* tok, int64_t M, int T, int C, float* dwte, float* dwpe,
+               hipStream_t s);
 // DLRM dot interaction of NV vectors of width D per sample (V [B][NV][D] bf16): out[b] =
 // [V[b][dense_idx] | V_i.V_j for i > j]. Backward: dV fp32 for all vectors, and the dense
 // vector's gradient ReLU-masked by its value as bf16 (feeds the bottom MLP's backward).

@@ -256,6 +256,62 @@ void add_bf16(const bf16_t* a, const bf16_t* b, int64_t n, bf16_t* out, hipStrea
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------- token + position embedding
+// out[m, :C] = wte[tok[m], :C] + wpe[m % T, :C]; 8 bf16 (16 B) per thread, C % 8 == 0.
+__global__ void embed_fwd_kernel(const bf16_t* __restrict__ wte, const bf16_t* __restrict__ wpe,
+                                 const int64_t* __restrict__ tok, int64_t M, int T, int C, bf16_t* __restrict__ out,
+                                 int ldo) {
+  const int cv = C >> 3;
+  const int64_t n = M * cv;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / cv;
+    const int c = (int)(i - m * cv) << 3;
+    const uint4 a = *(const uint4*)(wte + tok[m] * C + c);
+    const uint4 b = *(const uint4*)(wpe + (m % T) * C + c);
+    const uint32_t* pa = (const uint32_t*)&a;
+    const uint32_t* pb = (const uint32_t*)&b;
+    uint4 o;
+    uint32_t* po = (uint32_t*)&o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float lo = __uint_as_float(pa[q] << 16) + __uint_as_float(pb[q] << 16);
+      const float hi = __uint_as_float(pa[q] & 0xffff0000u) + __uint_as_float(pb[q] & 0xffff0000u);
+      po[q] = pack_bf2(lo, hi);
+    }
+    *(uint4*)(out + m * ldo + c) = o;
+  }
+}
+// dwte[tok[m]] += dx[m]; dwpe[m % T] += dx[m]   (fp32 atomics; token ids spread the wte rows)
+__global__ void embed_bwd_kernel(const bf16_t* __restrict__ dx, int ldx, const int64_t* __restrict__ tok, int64_t M,
+                                 int T, int C, float* __restrict__ dwte, float* __restrict__ dwpe) {
+  const int cv = C >> 1;
+  const int64_t n = M * cv;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / cv;
+    const int c = (int)(i - m * cv) << 1;
+    const uint32_t v = *(const uint32_t*)(dx + m * ldx + c);
+    const float lo = __uint_as_float(v << 16), hi = __uint_as_float(v & 0xffff0000u);
+    float* w = dwte + tok[m] * C + c;
+    atomicAdd(w, lo);
+    atomicAdd(w + 1, hi);
+    float* p = dwpe + (m % T) * C + c;
+    atomicAdd(p, lo);
+    atomicAdd(p + 1, hi);
+  }
+}
+void embed_fwd(const bf16_t* wte, const bf16_t* wpe, const int64_t* tok, int64_t M, int T, int C, bf16_t* out, int ldo,
+               hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(embed_fwd_kernel, grid_for(M * (C / 8), 256, 8192), 256, 0, s, wte, wpe, tok, M, T, C, out, ldo);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+void embed_bwd(const bf16_t* dx, int ldx, const int64_t* tok, int64_t M, int T, int C, float* dwte, float* dwpe,
+               hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(embed_bwd_kernel, grid_for(M * (C / 2), 256, 8192), 256, 0, s, dx, ldx, tok, M, T, C, dwte, dwpe);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 // ---------------------------------------------------------------------------- DLRM interaction
 // V [B][NV][D] bf16 -> out[b] = [V[b][dense_idx] (D) | V_i.V_j for i > j] at out + b*ldo.
 // One block per sample (grid-stride); the sample's vectors are staged in LDS.

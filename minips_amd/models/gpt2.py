@@ -1,0 +1,234 @@
+"""GPT-2-small trained through the GPU parameter server (BASELINE config 4): every dense
+parameter lives in ONE DenseTable whose fp32 master + Adam state are sharded over the PS ranks
+(reduce-scatter of gradients, fused Adam on the owned shard, all-gather of the bf16 pull).
+
+Architecture (GPT-2 small): vocab 50257 (padded to 50304 rows), context 1024, d_model 768,
+12 layers x 12 heads, pre-LayerNorm blocks, GELU(tanh) MLP 768 -> 3072 -> 768, tied LM head.
+
+Compute path (all gfx950 kernels from minips_amd.ops, no autograd):
+  embed_fwd                   x0 = wte[tok] + wpe[pos]
+  layernorm_fwd               into a bias-folded activation (ones column at 768)
+  gemm (bias epilogue)        qkv = ln1 W_qkv^T
+  batched gemm  (alpha=1/8)   S = Q K^T        per (sample, head), Q/K read in place from qkv
+  causal_softmax_fwd          P = softmax(mask(S)) (bf16, kept for backward)
+  batched gemm                O = P V          written into the proj input (bias-folded)
+  gemm + add_bf16             x_mid = x + O W_o^T
+  gemm (GELU-aux epilogue)    g = gelu(ln2 W_fc^T), pre-activation u saved
+  gemm + add_bf16             x_next = x_mid + g W_proj^T
+  gemm + softmax_xent         logits = ln_f(x) wte^T, fused softmax-CE forward/backward in place
+The backward mirrors it with dgrad/wgrad GEMMs (ReLU/GELU-grad epilogues), causal_softmax_bwd,
+layernorm_bwd (accumulating into the residual gradient) and embed_bwd.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from .. import ops
+from ..ps.comm import Comm
+from ..ps.tables import DenseTable
+from .layers import Linear, ParamLayout, align, ext_activation
+
+
+@dataclass
+class GPT2Config:
+    vocab: int = 50257
+    n_ctx: int = 1024
+    d: int = 768
+    n_layer: int = 12
+    n_head: int = 12
+    lr: float = 3e-4
+    weight_decay: float = 0.0
+    consistency: str = "bsp"
+    staleness: int = 0
+    seed: int = 0
+
+    @property
+    def vocab_pad(self):
+        return align(self.vocab, 64)
+
+
+class GPT2:
+    def __init__(self, cfg: GPT2Config, comm: Comm):
+        assert cfg.d % cfg.n_head == 0 and (cfg.d // cfg.n_head) % 8 == 0
+        self.cfg, self.comm = cfg, comm
+        d = cfg.d
+        L = ParamLayout()
+        self.layout = L
+        L.add("wte", (cfg.vocab_pad, d))
+        L.add("wpe", (cfg.n_ctx, d))
+        self.blocks = []
+        for i in range(cfg.n_layer):
+            blk = dict(
+                ln1_g=L.add(f"h{i}.ln1_g", (d,)), ln1_b=L.add(f"h{i}.ln1_b", (d,)),
+                qkv=Linear(L, f"h{i}.qkv", d, 3 * d),
+                proj=Linear(L, f"h{i}.proj", d, d),
+                ln2_g=L.add(f"h{i}.ln2_g", (d,)), ln2_b=L.add(f"h{i}.ln2_b", (d,)),
+                fc=Linear(L, f"h{i}.fc", d, 4 * d),
+                fc2=Linear(L, f"h{i}.fc2", 4 * d, d),
+            )
+            self.blocks.append(blk)
+        L.add("lnf_g", (d,))
+        L.add("lnf_b", (d,))
+        self.table = DenseTable(comm, L.size, optimizer="adam", lr=cfg.lr, consistency=cfg.consistency,
+                                staleness=cfg.staleness, weight_decay=cfg.weight_decay, betas=(0.9, 0.95))
+        g = torch.Generator().manual_seed(cfg.seed)
+        full = torch.zeros(L.size)
+        L.view(full, "wte")[: cfg.vocab].normal_(0.0, 0.02, generator=g)
+        L.view(full, "wpe").normal_(0.0, 0.01, generator=g)
+        proj_std = 0.02 / math.sqrt(2 * cfg.n_layer)
+        for blk in self.blocks:
+            for name in ("ln1_g", "ln2_g"):
+                L.view(full, blk[name]).fill_(1.0)
+            blk["qkv"].init(full, g, std=0.02)
+            blk["fc"].init(full, g, std=0.02)
+            blk["proj"].init(full, g, std=proj_std)
+            blk["fc2"].init(full, g, std=proj_std)
+        L.view(full, "lnf_g").fill_(1.0)
+        self.table.load_full(full)
+        self._bufs = {}
+
+    @property
+    def n_params(self):
+        c = self.cfg
+        return c.vocab * c.d + c.n_ctx * c.d + c.n_layer * (12 * c.d * c.d + 13 * c.d) + 2 * c.d
+
+    # ------------------------------------------------------------------------------ buffers
+    def _buffers(self, B, T):
+        key = (B, T)
+        if key not in self._bufs:
+            c, dev = self.cfg, self.comm.device
+            M, d, H = B * T, c.d, c.n_head
+            bf = dict(dtype=torch.bfloat16, device=dev)
+            f32 = dict(dtype=torch.float32, device=dev)
+            nl = c.n_layer
+            self._bufs[key] = dict(
+                x=[torch.empty(M, d, **bf) for _ in range(nl + 1)],       # residual stream per layer input
+                xm=[torch.empty(M, d, **bf) for _ in range(nl)],          # after attention
+                h1=[ext_activation(M, d, dev) for _ in range(nl)],        # ln1 out (+ ones column)
+                h2=[ext_activation(M, d, dev) for _ in range(nl)],
+                st1=[(torch.empty(M, **f32), torch.empty(M, **f32)) for _ in range(nl)],
+                st2=[(torch.empty(M, **f32), torch.empty(M, **f32)) for _ in range(nl)],
+                qkv=[torch.empty(M, 3 * d, **bf) for _ in range(nl)],
+                P=[torch.empty(B * H, T, T, **bf) for _ in range(nl)],
+                ao=[ext_activation(M, d, dev) for _ in range(nl)],        # attention out (+ ones)
+                u=[torch.empty(M, 4 * d, **bf) for _ in range(nl)],       # pre-GELU
+                g=[ext_activation(M, 4 * d, dev) for _ in range(nl)],     # GELU out (+ ones)
+                hf=ext_activation(M, d, dev), stf=(torch.empty(M, **f32), torch.empty(M, **f32)),
+                logits=torch.empty(M, c.vocab_pad, **bf),
+                S=torch.empty(B * H, T, T, **f32), dP=torch.empty(B * H, T, T, **f32),
+                dS=torch.empty(B * H, T, T, **bf),
+                tmp=torch.empty(M, d, **bf), dx=torch.empty(M, d, **bf), dh=torch.empty(M, d, **bf),
+                dqkv=torch.empty(M, 3 * d, **bf), dao=torch.empty(M, d, **bf), du=torch.empty(M, 4 * d, **bf),
+                loss=torch.zeros(1, **f32),
+            )
+        return self._bufs[key]
+
+    # ------------------------------------------------------------------------------ attention
+    def _attn_fwd(self, qkv, P, S, out, B, T):
+        c = self.cfg
+        d, H = c.d, c.n_head
+        hd = d // H
+        flat = qkv.reshape(-1)
+        ld = 3 * d
+        scale = 1.0 / math.sqrt(hd)
+        # S[b,h] = Q K^T (both [T, hd] row-major slices of qkv)
+        ops.gemm_batched(flat, flat[d:], S, T, T, hd, False, False, ops.EPI_STORE_F32, B * H, H, ld, ld, T,
+                         [T * ld, hd, T * ld, hd, H * T * T, T * T], alpha=scale)
+        ops.causal_softmax_fwd(S, T, P)
+        # O[b,h] = P V  -> out columns h*hd.. of the bias-folded proj input
+        ldo = out.stride(0)
+        ops.gemm_batched(P.reshape(-1), flat[2 * d:], out.reshape(-1), T, hd, T, False, True, ops.EPI_STORE_BF16,
+                         B * H, H, T, ld, ldo, [H * T * T, T * T, T * ld, hd, T * ldo, hd])
+
+    def _attn_bwd(self, qkv, P, dO, dqkv, b, B, T):
+        c = self.cfg
+        d, H = c.d, c.n_head
+        hd = d // H
+        flat = qkv.reshape(-1)
+        dflat = dqkv.reshape(-1)
+        ld = 3 * d
+        scale = 1.0 / math.sqrt(hd)
+        dOf = dO.reshape(-1)
+        # dP = dO V^T
+        ops.gemm_batched(dOf, flat[2 * d:], b["dP"], T, T, hd, False, False, ops.EPI_STORE_F32, B * H, H, d, ld, T,
+                         [T * d, hd, T * ld, hd, H * T * T, T * T])
+        # dV = P^T dO
+        ops.gemm_batched(P.reshape(-1), dOf, dflat[2 * d:], T, hd, T, True, True, ops.EPI_STORE_BF16, B * H, H, T, d,
+                         ld, [H * T * T, T * T, T * d, hd, T * ld, hd])
+        ops.causal_softmax_bwd(P, b["dP"], T, scale, b["dS"])
+        dS = b["dS"].reshape(-1)
+        # dQ = dS K ; dK = dS^T Q
+        ops.gemm_batched(dS, flat[d:], dflat, T, hd, T, False, True, ops.EPI_STORE_BF16, B * H, H, T, ld, ld,
+                         [H * T * T, T * T, T * ld, hd, T * ld, hd])
+        ops.gemm_batched(dS, flat, dflat[d:], T, hd, T, True, True, ops.EPI_STORE_BF16, B * H, H, T, ld, ld,
+                         [H * T * T, T * T, T * ld, hd, T * ld, hd])
+
+    # ------------------------------------------------------------------------------ step
+    def train_step(self, tokens, targets):
+        """tokens/targets [B, T] int64. Returns the summed token cross-entropy (device scalar)."""
+        c = self.cfg
+        B, T = tokens.shape
+        assert T <= c.n_ctx and T % 8 == 0
+        M, d = B * T, c.d
+        b = self._buffers(B, T)
+        L = self.layout
+        P = self.table.get()
+        G = self.table.grad
+        v = lambda buf, name: L.view(buf, name)  # noqa: E731
+        x = b["x"]
+        ops.embed_fwd(v(P, "wte"), v(P, "wpe"), tokens, T, x[0])
+        for i, blk in enumerate(self.blocks):
+            m1, r1 = b["st1"][i]
+            ops.layernorm_fwd(x[i], d, v(P, blk["ln1_g"]), v(P, blk["ln1_b"]), 1e-5, b["h1"][i], m1, r1)
+            blk["qkv"].forward(P, b["h1"][i], b["qkv"][i], "none")
+            self._attn_fwd(b["qkv"][i], b["P"][i], b["S"], b["ao"][i], B, T)
+            blk["proj"].forward(P, b["ao"][i], b["tmp"], "none")
+            ops.add_bf16(x[i], b["tmp"], b["xm"][i])
+            m2, r2 = b["st2"][i]
+            ops.layernorm_fwd(b["xm"][i], d, v(P, blk["ln2_g"]), v(P, blk["ln2_b"]), 1e-5, b["h2"][i], m2, r2)
+            blk["fc"].forward(P, b["h2"][i], b["g"][i], "gelu_aux", aux=b["u"][i])
+            blk["fc2"].forward(P, b["g"][i], b["tmp"], "none")
+            ops.add_bf16(b["xm"][i], b["tmp"], x[i + 1])
+        mf, rf = b["stf"]
+        hf = b["hf"]
+        ops.layernorm_fwd(x[-1], d, v(P, "lnf_g"), v(P, "lnf_b"), 1e-5, hf, mf, rf)
+        wte = v(P, "wte")
+        logits = b["logits"]
+        ops.gemm(hf[:, :d], wte, logits, M, c.vocab_pad, d, False, False, ops.EPI_STORE_BF16)
+        b["loss"].zero_()
+        ops.softmax_xent(logits, c.vocab, targets.reshape(-1), 1.0 / (M * self.comm.world), b["loss"])
+        # ---- backward
+        ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"))
+        dh = b["dh"]
+        ops.gemm(logits, wte, dh, M, d, c.vocab_pad, False, True, ops.EPI_STORE_BF16)
+        dx = b["dx"]
+        ops.layernorm_bwd(x[-1], dh, d, v(P, "lnf_g"), mf, rf, dx, v(G, "lnf_g"), v(G, "lnf_b"))
+        for i in range(c.n_layer - 1, -1, -1):
+            blk = self.blocks[i]
+            # MLP branch
+            blk["fc2"].wgrad(G, dx, b["g"][i])
+            blk["fc2"].dgrad(P, dx, b["du"], gelu_u=b["u"][i])
+            blk["fc"].wgrad(G, b["du"], b["h2"][i])
+            blk["fc"].dgrad(P, b["du"], dh)
+            m2, r2 = b["st2"][i]
+            ops.layernorm_bwd(b["xm"][i], dh, d, v(P, blk["ln2_g"]), m2, r2, dx, v(G, blk["ln2_g"]),
+                              v(G, blk["ln2_b"]), accumulate=True)
+            # attention branch
+            blk["proj"].wgrad(G, dx, b["ao"][i])
+            blk["proj"].dgrad(P, dx, b["dao"])
+            self._attn_bwd(b["qkv"][i], b["P"][i], b["dao"], b["dqkv"], b, B, T)
+            blk["qkv"].wgrad(G, b["dqkv"], b["h1"][i])
+            blk["qkv"].dgrad(P, b["dqkv"], dh)
+            m1, r1 = b["st1"][i]
+            ops.layernorm_bwd(x[i], dh, d, v(P, blk["ln1_g"]), m1, r1, dx, v(G, blk["ln1_g"]), v(G, blk["ln1_b"]),
+                              accumulate=True)
+        ops.embed_bwd(dx, tokens, T, v(G, "wte"), v(G, "wpe"))
+        self.table.add()
+        self.table.clock()
+        return b["loss"]
+
+    def drain(self):
+        self.table.drain()

@@ -440,6 +440,30 @@ def add_bf16(a, b, out):
     return out
 
 
+def embed_fwd(wte, wpe, tok, T, out):
+    """out[m, :C] = wte[tok[m]] + wpe[m % T] (bf16)."""
+    if _gpu(wte):
+        kernels().embed_fwd(wte, wpe, tok.reshape(-1), int(T), out)
+        return out
+    t = tok.reshape(-1)
+    C = wte.shape[1]
+    pos = torch.arange(t.numel()) % T
+    out[:, :C] = (wte[t].float() + wpe[pos].float()).to(out.dtype)
+    return out
+
+
+def embed_bwd(dx, tok, T, dwte, dwpe):
+    """dwte[tok[m]] += dx[m, :C]; dwpe[m % T] += dx[m, :C] (fp32 accumulators)."""
+    if _gpu(dx):
+        kernels().embed_bwd(dx, tok.reshape(-1), int(T), dwte, dwpe)
+        return
+    t = tok.reshape(-1)
+    C = dwte.shape[1]
+    d = dx[:, :C].float()
+    dwte.index_add_(0, t, d)
+    dwpe.index_add_(0, torch.arange(t.numel()) % T, d)
+
+
 def dlrm_interact_fwd(V, NV, D, out, dense_idx=0):
     """V [B, NV, D] bf16 -> out[b] = [V[b,dense_idx] | V_i . V_j for i > j (lower triangle, row-major)]."""
     if _gpu(V):

@@ -95,3 +95,60 @@ def test_dlrm_asp_two_ranks_runs():
     for r in (0, 1):
         losses = out[r][0]
         assert all(l == l for l in losses) and losses[-1] < 1.0
+
+
+# ------------------------------------------------------------------------------ LR / K-Means
+def _lr_run(rank, world, steps=25):
+    from minips_amd.data.synthetic import SparseLRSynth
+    from minips_amd.models.lr import SparseLR, SparseLRConfig
+    from minips_amd.ps.comm import Comm
+
+    comm = Comm(device=torch.device("cpu"))
+    m = SparseLR(SparseLRConfig(num_dims=4000, alpha=0.05), comm)
+    data = SparseLRSynth(256, num_dims=4000, nnz=16, seed=7 + rank)
+    accs = []
+    for _ in range(steps):
+        accs.append(float(m.train_step(*data.next())) / 256)
+    return accs, m.table.shard[:50].reshape(-1).tolist()
+
+
+def _lr_fn(rank, world):
+    return _lr_run(rank, world)
+
+
+def test_sparse_lr_learns_cpu():
+    accs, _ = _lr_run(0, 1)
+    assert sum(accs[-5:]) / 5 > 0.7, accs
+
+
+def test_sparse_lr_two_ranks():
+    out = run_world(_lr_fn)
+    for r in (0, 1):
+        assert sum(out[r][0][-5:]) / 5 > 0.7, out[r][0]
+
+
+def _km_run(rank, world, steps=8):
+    from minips_amd.models.kmeans import KMeans, KMeansConfig
+    from minips_amd.ps.comm import Comm
+
+    comm = Comm(device=torch.device("cpu"))
+    g = torch.Generator().manual_seed(0)
+    true = torch.randn(6, 12, generator=g) * 5
+    km = KMeans(KMeansConfig(K=6, dims=12), comm, init_centres=true + torch.randn(6, 12, generator=g))
+    dg = torch.Generator().manual_seed(100 + rank)
+    sse = []
+    for _ in range(steps):
+        X = true[torch.randint(0, 6, (512,), generator=dg)] + torch.randn(512, 12, generator=dg) * 0.5
+        sse.append(float(km.train_step(X)) / 512)
+    return sse, km.centres().reshape(-1).tolist()
+
+
+def _km_fn(rank, world):
+    return _km_run(rank, world)
+
+
+def test_kmeans_converges_two_ranks():
+    out = run_world(_km_fn)
+    assert out[0][1] == out[1][1]  # both ranks pull the same centres
+    for r in (0, 1):
+        assert out[r][0][-1] < 12 * 0.25 * 1.3, out[r][0]

@@ -193,3 +193,33 @@ def test_dlrm_gpu_matches_cpu(dev):
         losses[str(d)] = ls
     for a, b in zip(losses[str(dev)], losses["cpu"]):
         assert abs(a - b) < 2e-2, losses
+
+
+def test_lr_kmeans_gpu_matches_cpu(dev):
+    from minips_amd.data.synthetic import SparseLRSynth
+    from minips_amd.models.kmeans import KMeans, KMeansConfig
+    from minips_amd.models.lr import SparseLR, SparseLRConfig
+    from minips_amd.ps.comm import Comm
+
+    data = SparseLRSynth(256, num_dims=4000, nnz=16, seed=7)
+    batches = [data.next() for _ in range(6)]
+    g = torch.Generator().manual_seed(0)
+    true = torch.randn(6, 12, generator=g) * 5
+    init = true + torch.randn(6, 12, generator=g)
+    Xs = [true[torch.randint(0, 6, (512,), generator=g)] + torch.randn(512, 12, generator=g) * 0.5 for _ in range(4)]
+    res = {}
+    for d in ("cpu", dev):
+        comm = Comm(device=torch.device(d))
+        m = SparseLR(SparseLRConfig(num_dims=4000, alpha=0.05), comm)
+        acc = [float(m.train_step(*(t.to(d) for t in b))) for b in batches]
+        m.drain()
+        km = KMeans(KMeansConfig(K=6, dims=12), comm, init_centres=init)
+        sse = [float(km.train_step(X.to(d))) for X in Xs]
+        km.drain()
+        res[str(d)] = (acc, m.table.shard.cpu(), sse, km.centres().cpu())
+    c, gp = res["cpu"], res[str(dev)]
+    assert max(abs(a - b) for a, b in zip(gp[0], c[0])) <= 2
+    torch.testing.assert_close(gp[1], c[1], rtol=1e-4, atol=1e-5)
+    for a, b in zip(gp[2], c[2]):
+        assert abs(a - b) < 1e-3 * b
+    torch.testing.assert_close(gp[3], c[3], rtol=1e-4, atol=1e-4)

@@ -1,0 +1,146 @@
+#!/usr/bin/env python3
+"""Throughput of the other BASELINE configurations on the GPU parameter server, with the same
+timing discipline as bench.py (W untimed warmup steps, exactly K timed steps bracketed by
+barrier + synchronize, max over ranks, whole-job value, one JSON line on rank 0).
+
+    python tools/bench_models.py --model gpt2 --steps 10 --warmup 3
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_models.py --model dlrm
+
+models: mlp (config 2, samples/s), gpt2 (config 4, tokens/s), dlrm (config 5, samples/s),
+        lr (config 1 on GPUs, samples/s), kmeans (samples/s), widedeep-ssp (config 3).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def build(args, comm):
+    dev = comm.device
+    r = comm.rank
+    if args.model == "mlp":
+        from minips_amd.data.synthetic import MnistSynth
+        from minips_amd.models.mlp import MLP, MLPConfig
+
+        B = args.batch or 8192
+        m = MLP(MLPConfig(consistency=args.consistency, staleness=args.staleness), comm)
+        data = MnistSynth(B, device=dev, seed=r)
+        return m, (lambda: m.train_step(*data.next())[0]), B, "samples/s", \
+            dict(model="MLP 784-512-512-10 (Adam, dense PS table)", seq_len=None)
+    if args.model == "gpt2":
+        from minips_amd.data.synthetic import TokenSynth
+        from minips_amd.models.gpt2 import GPT2, GPT2Config
+
+        B, T = args.batch or 8, args.seq
+        m = GPT2(GPT2Config(consistency=args.consistency, staleness=args.staleness), comm)
+        data = TokenSynth(B, T, device=dev, seed=r)
+        return m, (lambda: m.train_step(*data.next())), B * T, "tokens/s", \
+            dict(model="GPT-2 small 124M (12L/768d/12H, vocab 50257), dense params sharded over PS ranks",
+                 seq_len=T, batch_per_gpu=B)
+    if args.model == "dlrm":
+        from minips_amd.models.dlrm import DLRM, DLRMConfig
+
+        B = args.batch or 16384
+        cfg = DLRMConfig(num_rows=args.rows, consistency=args.consistency, staleness=args.staleness)
+        m = DLRM(cfg, comm)
+        g = torch.Generator(device=dev)
+        g.manual_seed(r)
+
+        def step():
+            dense = torch.randn(B, cfg.n_dense, generator=g, device=dev)
+            keys = torch.randint(0, cfg.num_rows, (B, cfg.F), generator=g, device=dev)
+            y = (dense[:, 0] > 0).float()
+            return m.train_step(dense, keys, y)
+
+        return m, step, B, "samples/s", dict(model=f"DLRM {cfg.num_rows} rows x {cfg.D} (26 sparse + 13 dense), "
+                                                   f"{cfg.consistency}", seq_len=None)
+    if args.model == "lr":
+        from minips_amd.data.synthetic import SparseLRSynth
+        from minips_amd.models.lr import SparseLR, SparseLRConfig
+
+        B = args.batch or 65536
+        m = SparseLR(SparseLRConfig(consistency=args.consistency, staleness=args.staleness), comm)
+        data = SparseLRSynth(B, nnz=64, device=dev, seed=r)
+        return m, (lambda: m.train_step(*data.next())), B, "samples/s", \
+            dict(model="sparse LR, 16.6M features, 64 nnz/row", seq_len=None)
+    if args.model == "kmeans":
+        from minips_amd.models.kmeans import KMeans, KMeansConfig
+
+        B = args.batch or 65536
+        cfg = KMeansConfig(K=1000, dims=128, consistency=args.consistency, staleness=args.staleness)
+        m = KMeans(cfg, comm)
+        g = torch.Generator(device=dev)
+        g.manual_seed(r)
+        return m, (lambda: m.train_step(torch.randn(B, cfg.dims, generator=g, device=dev))), B, "samples/s", \
+            dict(model="mini-batch K-Means K=1000 D=128", seq_len=None)
+    if args.model == "widedeep-ssp":
+        from minips_amd.data.synthetic import CriteoSynth
+        from minips_amd.models.widedeep import WideDeep, WideDeepConfig
+
+        B = args.batch or 16384
+        cfg = WideDeepConfig(consistency="ssp", staleness=max(1, args.staleness))
+        m = WideDeep(cfg, comm)
+        data = CriteoSynth(B, cards=cfg.cards, device=dev, seed=1000 + r)
+        return m, (lambda: m.train_step(*data.next())), B, "samples/s", \
+            dict(model="Wide&Deep Criteo SSP", seq_len=None)
+    raise SystemExit(f"unknown model {args.model}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (samples or sequences)")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--rows", type=int, default=100_000_000, help="DLRM embedding rows (whole table)")
+    ap.add_argument("--consistency", default="bsp")
+    ap.add_argument("--staleness", type=int, default=0)
+    args = ap.parse_args()
+    from minips_amd.ps.comm import init_distributed
+
+    comm = init_distributed()
+    dev = comm.device
+    model, step, per_step, unit, cfg = build(args, comm)
+    for _ in range(args.warmup):
+        step()
+    model.drain()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    model.drain()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if comm.world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t)
+    if comm.rank == 0:
+        print(json.dumps({
+            "metric": f"{unit.split('/')[0]}/sec (whole job) {args.model} {args.consistency}",
+            "value": round(per_step * comm.world * args.steps / el, 1), "unit": unit, "n_gpus": comm.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "dtype": "bf16" if args.model in ("mlp", "gpt2", "dlrm",
+                                                                                            "widedeep-ssp") else "fp32",
+            "data": "synthetic", "last": float(out.float().sum()) if torch.is_tensor(out) else None,
+            "config": dict(cfg, parallelism=f"ps-dp{comm.world}"),
+        }), flush=True)
+    if comm.world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
