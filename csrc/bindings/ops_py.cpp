@@ -368,26 +368,48 @@ void criteo_synth(int64_t seed, int64_t step, const at::Tensor& cards, const at:
                          stream_of(keys));
 }
 
+void check_ln(const at::Tensor& t, int64_t C, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(1) >= C && t.stride(0) % 4 == 0, n,
+              " must be a row-major GPU matrix with >= C columns and a leading dim % 4 == 0");
+  check_dtype(t, at::kBFloat16, n);
+}
+
 void layernorm_fwd(const at::Tensor& x, int64_t C, const at::Tensor& gamma, const at::Tensor& beta, double eps,
                    at::Tensor& y, at::Tensor& mean, at::Tensor& rstd) {
-  for (const at::Tensor* t : {&x, &gamma, &beta, (const at::Tensor*)&y, (const at::Tensor*)&mean,
-                              (const at::Tensor*)&rstd})
-    check_gpu(*t, "layernorm arg");
-  TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.size(1) >= C && y.size(1) >= C && C <= 1024, "layernorm shapes");
+  TORCH_CHECK(C % 4 == 0 && C <= 1024, "layernorm: C % 4 == 0 and C <= 1024");
+  check_ln(x, C, "x");
+  check_ln(y, C, "y");
+  TORCH_CHECK(y.size(0) == x.size(0) && mean.numel() == x.size(0) && rstd.numel() == x.size(0), "layernorm rows");
+  check_gpu(gamma, "gamma");
+  check_gpu(beta, "beta");
+  check_dtype(gamma, at::kBFloat16, "gamma");
+  check_dtype(beta, at::kBFloat16, "beta");
+  check_dtype(mean, at::kFloat, "mean");
+  check_dtype(rstd, at::kFloat, "rstd");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  minips_k::layernorm_fwd(ptr<bf16_t>(x), (int)x.size(1), x.size(0), (int)C, ptr<bf16_t>(gamma), ptr<bf16_t>(beta),
-                          (float)eps, ptr<bf16_t>(y), (int)y.size(1), ptr<float>(mean), ptr<float>(rstd), stream_of(x));
+  minips_k::layernorm_fwd(ptr<bf16_t>(x), (int)x.stride(0), x.size(0), (int)C, ptr<bf16_t>(gamma), ptr<bf16_t>(beta),
+                          (float)eps, ptr<bf16_t>(y), (int)y.stride(0), ptr<float>(mean), ptr<float>(rstd),
+                          stream_of(x));
 }
 
 void layernorm_bwd(const at::Tensor& x, const at::Tensor& dy, int64_t C, const at::Tensor& gamma,
                    const at::Tensor& mean, const at::Tensor& rstd, at::Tensor& dx, at::Tensor& dgamma,
                    at::Tensor& dbeta, bool accumulate) {
-  TORCH_CHECK(x.is_cuda() && dy.is_cuda() && dx.is_cuda() && x.size(0) == dy.size(0) && dx.size(0) == x.size(0),
-              "layernorm_bwd shapes");
+  TORCH_CHECK(C % 4 == 0 && C <= 1024, "layernorm: C % 4 == 0 and C <= 1024");
+  check_ln(x, C, "x");
+  check_ln(dy, C, "dy");
+  check_ln(dx, C, "dx");
+  const int64_t M = x.size(0);
+  TORCH_CHECK(dy.size(0) == M && dx.size(0) == M && mean.numel() == M && rstd.numel() == M, "layernorm_bwd rows");
+  check_dtype(gamma, at::kBFloat16, "gamma");
+  check_dtype(dgamma, at::kFloat, "dgamma");
+  check_dtype(dbeta, at::kFloat, "dbeta");
+  TORCH_CHECK(gamma.numel() >= C && dgamma.numel() >= C && dbeta.numel() >= C, "layernorm_bwd params");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  minips_k::layernorm_bwd(ptr<bf16_t>(x), (int)x.size(1), ptr<bf16_t>(dy), (int)dy.size(1), x.size(0), (int)C,
-                          ptr<bf16_t>(gamma), ptr<float>(mean), ptr<float>(rstd), ptr<bf16_t>(dx), (int)dx.size(1),
-                          ptr<float>(dgamma), ptr<float>(dbeta), accumulate, stream_of(x));
+  at::Tensor partial = at::empty({(int64_t)minips_k::layernorm_bwd_blocks(M) * 2 * C}, x.options().dtype(at::kFloat));
+  minips_k::layernorm_bwd(ptr<bf16_t>(x), (int)x.stride(0), ptr<bf16_t>(dy), (int)dy.stride(0), M, (int)C,
+                          ptr<bf16_t>(gamma), ptr<float>(mean), ptr<float>(rstd), ptr<bf16_t>(dx), (int)dx.stride(0),
+                          ptr<float>(dgamma), ptr<float>(dbeta), ptr<float>(partial), accumulate, stream_of(x));
 }
 
 void softmax_xent(at::Tensor& logits, int64_t V, const at::Tensor& labels, double scale, at::Tensor& loss_sum,
@@ -434,6 +456,42 @@ void add_bf16(const at::Tensor& a, const at::Tensor& b, at::Tensor& out) {
   check_gpu(out, "out");
   c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   minips_k::add_bf16(ptr<bf16_t>(a), ptr<bf16_t>(b), a.numel(), ptr<bf16_t>(out), stream_of(a));
+}
+
+void check_rows(const at::Tensor& t, int64_t rows, int64_t cols, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) == rows && t.size(1) >= cols &&
+                  t.stride(0) % 8 == 0,
+              n, " must be a [", rows, ", >=", cols, "] row-major GPU matrix with a leading dim % 8 == 0");
+  check_dtype(t, at::kBFloat16, n);
+}
+
+void attn_fwd(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H, double scale, at::Tensor& O, at::Tensor& lse) {
+  const int64_t d = H * 64;
+  check_rows(qkv, B * T, 3 * d, "qkv");
+  check_rows(O, B * T, d, "O");
+  check_gpu(lse, "lse");
+  check_dtype(lse, at::kFloat, "lse");
+  TORCH_CHECK(lse.numel() >= B * H * T, "lse too small");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  minips_k::attn_fwd(ptr<bf16_t>(qkv), (int)qkv.stride(0), (int)B, (int)T, (int)H, (int)d, (float)scale,
+                     ptr<bf16_t>(O), (int)O.stride(0), ptr<float>(lse), stream_of(qkv));
+}
+
+void attn_bwd(const at::Tensor& qkv, const at::Tensor& O, const at::Tensor& dO, const at::Tensor& lse, at::Tensor& delta,
+              int64_t B, int64_t T, int64_t H, double scale, at::Tensor& dqkv) {
+  const int64_t d = H * 64;
+  check_rows(qkv, B * T, 3 * d, "qkv");
+  check_rows(O, B * T, d, "O");
+  check_rows(dO, B * T, d, "dO");
+  check_rows(dqkv, B * T, 3 * d, "dqkv");
+  check_dtype(lse, at::kFloat, "lse");
+  check_dtype(delta, at::kFloat, "delta");
+  TORCH_CHECK(lse.is_cuda() && delta.is_cuda() && lse.numel() >= B * H * T && delta.numel() >= B * H * T,
+              "lse/delta too small");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  minips_k::attn_bwd(ptr<bf16_t>(qkv), (int)qkv.stride(0), ptr<bf16_t>(O), (int)O.stride(0), ptr<bf16_t>(dO),
+                     (int)dO.stride(0), ptr<float>(lse), ptr<float>(delta), (int)B, (int)T, (int)H, (int)d,
+                     (float)scale, ptr<bf16_t>(dqkv), (int)dqkv.stride(0), stream_of(qkv));
 }
 
 void embed_fwd(const at::Tensor& wte, const at::Tensor& wpe, const at::Tensor& tok, int64_t T, at::Tensor& out) {
@@ -521,6 +579,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("scatter_add_rows", &scatter_add_rows);
   m.def("lookup_rows", &lookup_rows);
   m.def("embed_fwd", &embed_fwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("sparse_rowwise_adagrad", &sparse_rowwise_adagrad);
   m.def("sparse_sgd", &sparse_sgd);

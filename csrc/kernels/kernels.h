@@ -114,9 +114,11 @@ void kmeans_assign(const float* X, int64_t n, int d, const float* C, int k, int3
 // ------------------------------------------------------------------ dense-model kernels (nn.hip)
 void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gamma, const bf16_t* beta, float eps,
                    bf16_t* y, int ldy, float* mean, float* rstd, hipStream_t s);
+// partial: scratch of layernorm_bwd_blocks(M) * 2 * C floats (per-block dgamma/dbeta partials).
+int layernorm_bwd_blocks(int64_t M);
 void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t M, int C, const bf16_t* gamma,
                    const float* mean, const float* rstd, bf16_t* dx, int lddx, float* dgamma, float* dbeta,
-                   bool accumulate_dx, hipStream_t s);
+                   float* partial, bool accumulate_dx, hipStream_t s);
 // In place: logits [M, ld] bf16 become (softmax - onehot) * scale; loss_sum += sum CE.
 void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,
                   float* correct, hipStream_t s);
@@ -125,6 +127,12 @@ void causal_softmax_bwd(const bf16_t* P, const float* dP, int64_t rows, int T, f
                         hipStream_t s);
 void gelu_bwd(const bf16_t* dh, const bf16_t* u, int64_t n, bf16_t* du, hipStream_t s);
 void add_bf16(const bf16_t* a, const bf16_t* b, int64_t n, bf16_t* out, hipStream_t s);
+// Fused causal attention, head dim 64 (attention.hip). qkv [B*T][ldq] holds Q|K|V (each dmodel
+// = H*64 columns); O/dO/dqkv row-major with head h at column h*64; lse/delta [B*H*T] fp32.
+void attn_fwd(const bf16_t* qkv, int ldq, int B, int T, int H, int dmodel, float scale, bf16_t* O, int ldo, float* lse,
+              hipStream_t s);
+void attn_bwd(const bf16_t* qkv, int ldq, const bf16_t* O, int ldo, const bf16_t* dO, int lddo, const float* lse,
+              float* delta, int B, int T, int H, int dmodel, float scale, bf16_t* dqkv, int lddq, hipStream_t s);
 void embed_fwd(const bf16_t* wte, const bf16_t* wpe, const int64_t* tok, int64_t M, int T, int C, bf16_t* out, int ldo,
                hipStream_t s);
 void embed_bwd(const bf16_t* dx, int ldx, const int64_t* tok, int64_t M, int T, int C, float* dwte, float* dwpe,

@@ -41,30 +41,69 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }
 
 // ---------------------------------------------------------------------------- LayerNorm
-// One wave per row, C <= 64*16.
-__global__ void layernorm_fwd_kernel(const bf16_t* __restrict__ x, int ldx, int64_t M, int C,
-                                     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta, float eps,
-                                     bf16_t* __restrict__ y, int ldy, float* __restrict__ mean_out,
-                                     float* __restrict__ rstd_out) {
+// One wave per row; lane l owns columns k*256 + 4l .. +3 (k < 4), so C <= 1024, C % 4 == 0 and the
+// row lives in registers between the statistics and the output pass (8-byte vector loads).
+constexpr int kLnK = 4;
+
+__device__ __forceinline__ void ld4(const bf16_t* p, float v[4]) {
+  const uint2 u = *(const uint2*)p;
+  v[0] = __uint_as_float(u.x << 16);
+  v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16);
+  v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ void st4(bf16_t* p, const float v[4]) {
+  uint2 u;
+  u.x = pack_bf2(v[0], v[1]);
+  u.y = pack_bf2(v[2], v[3]);
+  *(uint2*)p = u;
+}
+
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16_t* __restrict__ x, int ldx, int64_t M, int C,
+                                                            const bf16_t* __restrict__ gamma,
+                                                            const bf16_t* __restrict__ beta, float eps,
+                                                            bf16_t* __restrict__ y, int ldy, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  float gm[kLnK][4], bt[kLnK][4];
+#pragma unroll
+  for (int k = 0; k < kLnK; ++k) {
+    const int c = k * 256 + lane * 4;
+    if (c < C) {
+      ld4(gamma + c, gm[k]);
+      ld4(beta + c, bt[k]);
+    }
+  }
   for (int64_t r = wave; r < M; r += nw) {
-    const bf16_t* xr = x + r * ldx;
+    float v[kLnK][4];
     float s = 0.f, ss = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float v = bf2f(xr[c]);
-      s += v;
-      ss += v * v;
+#pragma unroll
+    for (int k = 0; k < kLnK; ++k) {
+      const int c = k * 256 + lane * 4;
+      if (c < C) {
+        ld4(x + r * ldx + c, v[k]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          s += v[k][q];
+          ss += v[k][q] * v[k][q];
+        }
+      }
     }
     s = warp_sum(s);
     ss = warp_sum(ss);
     const float mu = s / C;
-    const float var = fmaxf(ss / C - mu * mu, 0.f);
-    const float rs = rsqrtf(var + eps);
-    for (int c = lane; c < C; c += 64) {
-      const float v = (bf2f(xr[c]) - mu) * rs;
-      y[r * ldy + c] = f2bf(v * bf2f(gamma[c]) + bf2f(beta[c]));
+    const float rs = rsqrtf(fmaxf(ss / C - mu * mu, 0.f) + eps);
+#pragma unroll
+    for (int k = 0; k < kLnK; ++k) {
+      const int c = k * 256 + lane * 4;
+      if (c < C) {
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (v[k][q] - mu) * rs * gm[k][q] + bt[k][q];
+        st4(y + r * ldy + c, o);
+      }
     }
     if (lane == 0) {
       mean_out[r] = mu;
@@ -73,55 +112,102 @@ __global__ void layernorm_fwd_kernel(const bf16_t* __restrict__ x, int ldx, int6
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma; param grads reduced per
-// block in LDS (C <= 1024) then one atomic per column per block.
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma. dgamma/dbeta: every lane
+// accumulates its own columns in registers over the wave's rows, the 4 waves of a block combine
+// in LDS and the block writes one partial row [2C] (no atomics); layernorm_colsum adds the
+// partials into dgamma/dbeta.
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __restrict__ x, int ldx,
                                                             const bf16_t* __restrict__ dy, int lddy, int64_t M, int C,
                                                             const bf16_t* __restrict__ gamma,
                                                             const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                            bf16_t* __restrict__ dx, int lddx, float* dgamma,
-                                                            float* dbeta, bool accumulate_dx) {
-  __shared__ float sg[1024], sb[1024];
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    sg[c] = 0.f;
-    sb[c] = 0.f;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
+                                                            bf16_t* __restrict__ dx, int lddx,
+                                                            float* __restrict__ partial, bool accumulate_dx) {
+  __shared__ float red[4][2][1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  float gm[kLnK][4], ag[kLnK][4], ab[kLnK][4];
+#pragma unroll
+  for (int k = 0; k < kLnK; ++k) {
+    const int c = k * 256 + lane * 4;
+    if (c < C) ld4(gamma + c, gm[k]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ag[k][q] = ab[k][q] = 0.f;
+  }
   for (int64_t r = wave; r < M; r += nw) {
     const float mu = mean[r], rs = rstd[r];
+    float xh[kLnK][4], g[kLnK][4];
     float a = 0.f, b = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float xh = (bf2f(x[r * ldx + c]) - mu) * rs;
-      const float d = bf2f(dy[r * lddy + c]);
-      const float g = d * bf2f(gamma[c]);
-      a += g;
-      b += g * xh;
-      atomicAdd(sg + c, d * xh);
-      atomicAdd(sb + c, d);
+#pragma unroll
+    for (int k = 0; k < kLnK; ++k) {
+      const int c = k * 256 + lane * 4;
+      if (c < C) {
+        float d[4];
+        ld4(x + r * ldx + c, xh[k]);
+        ld4(dy + r * lddy + c, d);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          xh[k][q] = (xh[k][q] - mu) * rs;
+          g[k][q] = d[q] * gm[k][q];
+          a += g[k][q];
+          b += g[k][q] * xh[k][q];
+          ag[k][q] += d[q] * xh[k][q];
+          ab[k][q] += d[q];
+        }
+      }
     }
     a = warp_sum(a) / C;
     b = warp_sum(b) / C;
-    for (int c = lane; c < C; c += 64) {
-      const float xh = (bf2f(x[r * ldx + c]) - mu) * rs;
-      const float g = bf2f(dy[r * lddy + c]) * bf2f(gamma[c]);
-      float v = rs * (g - a - xh * b);
-      if (accumulate_dx) v += bf2f(dx[r * lddx + c]);
-      dx[r * lddx + c] = f2bf(v);
+#pragma unroll
+    for (int k = 0; k < kLnK; ++k) {
+      const int c = k * 256 + lane * 4;
+      if (c < C) {
+        float o[4], prev[4];
+        if (accumulate_dx) ld4(dx + r * lddx + c, prev);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = rs * (g[k][q] - a - xh[k][q] * b) + (accumulate_dx ? prev[q] : 0.f);
+        st4(dx + r * lddx + c, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kLnK; ++k) {
+    const int c = k * 256 + lane * 4;
+    if (c < C) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        red[w][0][c + q] = ag[k][q];
+        red[w][1][c + q] = ab[k][q];
+      }
     }
   }
   __syncthreads();
+  float* out = partial + (int64_t)blockIdx.x * 2 * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    atomicAdd(dgamma + c, sg[c]);
-    atomicAdd(dbeta + c, sb[c]);
+    out[c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    out[C + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
   }
 }
+
+// dst[j] += sum_g partial[g][j] for j < 2C  (dst = [dgamma | dbeta] as two pointers)
+__global__ void layernorm_colsum_kernel(const float* __restrict__ partial, int G, int C, float* __restrict__ dgamma,
+                                        float* __restrict__ dbeta) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * C) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += partial[(int64_t)g * 2 * C + j];
+  if (j < C)
+    dgamma[j] += s;
+  else
+    dbeta[j - C] += s;
+}
+
+int layernorm_bwd_blocks(int64_t M) { return (int)std::min<int64_t>(std::max<int64_t>((M + 31) / 32, 1), 512); }
 
 void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gamma, const bf16_t* beta, float eps,
                    bf16_t* y, int ldy, float* mean, float* rstd, hipStream_t s) {
   if (M <= 0) return;
+  if (C > 1024 || C % 4) throw std::runtime_error("layernorm: C <= 1024 and C % 4 == 0");
   hipLaunchKernelGGL(layernorm_fwd_kernel, grid_for(M * 64, 256, 4096), 256, 0, s, x, ldx, M, C, gamma, beta, eps, y,
                      ldy, mean, rstd);
   MINIPS_HIP_CHECK(hipGetLastError());
@@ -129,11 +215,14 @@ void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gam
 
 void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t M, int C, const bf16_t* gamma,
                    const float* mean, const float* rstd, bf16_t* dx, int lddx, float* dgamma, float* dbeta,
-                   bool accumulate_dx, hipStream_t s) {
+                   float* partial, bool accumulate_dx, hipStream_t s) {
   if (M <= 0) return;
-  if (C > 1024) throw std::runtime_error("layernorm_bwd: C <= 1024");
-  hipLaunchKernelGGL(layernorm_bwd_kernel, grid_for(M * 64, 256, 512), 256, 0, s, x, ldx, dy, lddy, M, C, gamma, mean,
-                     rstd, dx, lddx, dgamma, dbeta, accumulate_dx);
+  if (C > 1024 || C % 4) throw std::runtime_error("layernorm: C <= 1024 and C % 4 == 0");
+  const int G = layernorm_bwd_blocks(M);
+  hipLaunchKernelGGL(layernorm_bwd_kernel, G, 256, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx, partial,
+                     accumulate_dx);
+  MINIPS_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(layernorm_colsum_kernel, (2 * C + 255) / 256, 256, 0, s, partial, G, C, dgamma, dbeta);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

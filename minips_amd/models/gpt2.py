@@ -9,15 +9,15 @@ Compute path (all gfx950 kernels from minips_amd.ops, no autograd):
   embed_fwd                   x0 = wte[tok] + wpe[pos]
   layernorm_fwd               into a bias-folded activation (ones column at 768)
   gemm (bias epilogue)        qkv = ln1 W_qkv^T
-  batched gemm  (alpha=1/8)   S = Q K^T        per (sample, head), Q/K read in place from qkv
-  causal_softmax_fwd          P = softmax(mask(S)) (bf16, kept for backward)
-  batched gemm                O = P V          written into the proj input (bias-folded)
+  attn_fwd                    fused causal flash attention (MFMA, online softmax; Q/K/V read in
+                              place from qkv, O written into the bias-folded proj input, only
+                              the per-query log-sum-exp kept for the backward)
   gemm + add_bf16             x_mid = x + O W_o^T
   gemm (GELU-aux epilogue)    g = gelu(ln2 W_fc^T), pre-activation u saved
   gemm + add_bf16             x_next = x_mid + g W_proj^T
   gemm + softmax_xent         logits = ln_f(x) wte^T, fused softmax-CE forward/backward in place
-The backward mirrors it with dgrad/wgrad GEMMs (ReLU/GELU-grad epilogues), causal_softmax_bwd,
-layernorm_bwd (accumulating into the residual gradient) and embed_bwd.
+The backward mirrors it with dgrad/wgrad GEMMs (GELU-grad epilogue), attn_bwd (recomputes P per
+tile; dQ and dK/dV sweeps), layernorm_bwd (accumulating into the residual gradient) and embed_bwd.
 """
 from __future__ import annotations
 
@@ -112,59 +112,18 @@ class GPT2:
                 st1=[(torch.empty(M, **f32), torch.empty(M, **f32)) for _ in range(nl)],
                 st2=[(torch.empty(M, **f32), torch.empty(M, **f32)) for _ in range(nl)],
                 qkv=[torch.empty(M, 3 * d, **bf) for _ in range(nl)],
-                P=[torch.empty(B * H, T, T, **bf) for _ in range(nl)],
+                lse=[torch.empty(B * H * T, **f32) for _ in range(nl)],  # attention log-sum-exp
                 ao=[ext_activation(M, d, dev) for _ in range(nl)],        # attention out (+ ones)
                 u=[torch.empty(M, 4 * d, **bf) for _ in range(nl)],       # pre-GELU
                 g=[ext_activation(M, 4 * d, dev) for _ in range(nl)],     # GELU out (+ ones)
                 hf=ext_activation(M, d, dev), stf=(torch.empty(M, **f32), torch.empty(M, **f32)),
                 logits=torch.empty(M, c.vocab_pad, **bf),
-                S=torch.empty(B * H, T, T, **f32), dP=torch.empty(B * H, T, T, **f32),
-                dS=torch.empty(B * H, T, T, **bf),
+                delta=torch.empty(B * H * T, **f32),
                 tmp=torch.empty(M, d, **bf), dx=torch.empty(M, d, **bf), dh=torch.empty(M, d, **bf),
                 dqkv=torch.empty(M, 3 * d, **bf), dao=torch.empty(M, d, **bf), du=torch.empty(M, 4 * d, **bf),
                 loss=torch.zeros(1, **f32),
             )
         return self._bufs[key]
-
-    # ------------------------------------------------------------------------------ attention
-    def _attn_fwd(self, qkv, P, S, out, B, T):
-        c = self.cfg
-        d, H = c.d, c.n_head
-        hd = d // H
-        flat = qkv.reshape(-1)
-        ld = 3 * d
-        scale = 1.0 / math.sqrt(hd)
-        # S[b,h] = Q K^T (both [T, hd] row-major slices of qkv)
-        ops.gemm_batched(flat, flat[d:], S, T, T, hd, False, False, ops.EPI_STORE_F32, B * H, H, ld, ld, T,
-                         [T * ld, hd, T * ld, hd, H * T * T, T * T], alpha=scale)
-        ops.causal_softmax_fwd(S, T, P)
-        # O[b,h] = P V  -> out columns h*hd.. of the bias-folded proj input
-        ldo = out.stride(0)
-        ops.gemm_batched(P.reshape(-1), flat[2 * d:], out.reshape(-1), T, hd, T, False, True, ops.EPI_STORE_BF16,
-                         B * H, H, T, ld, ldo, [H * T * T, T * T, T * ld, hd, T * ldo, hd])
-
-    def _attn_bwd(self, qkv, P, dO, dqkv, b, B, T):
-        c = self.cfg
-        d, H = c.d, c.n_head
-        hd = d // H
-        flat = qkv.reshape(-1)
-        dflat = dqkv.reshape(-1)
-        ld = 3 * d
-        scale = 1.0 / math.sqrt(hd)
-        dOf = dO.reshape(-1)
-        # dP = dO V^T
-        ops.gemm_batched(dOf, flat[2 * d:], b["dP"], T, T, hd, False, False, ops.EPI_STORE_F32, B * H, H, d, ld, T,
-                         [T * d, hd, T * ld, hd, H * T * T, T * T])
-        # dV = P^T dO
-        ops.gemm_batched(P.reshape(-1), dOf, dflat[2 * d:], T, hd, T, True, True, ops.EPI_STORE_BF16, B * H, H, T, d,
-                         ld, [H * T * T, T * T, T * d, hd, T * ld, hd])
-        ops.causal_softmax_bwd(P, b["dP"], T, scale, b["dS"])
-        dS = b["dS"].reshape(-1)
-        # dQ = dS K ; dK = dS^T Q
-        ops.gemm_batched(dS, flat[d:], dflat, T, hd, T, False, True, ops.EPI_STORE_BF16, B * H, H, T, ld, ld,
-                         [H * T * T, T * T, T * ld, hd, T * ld, hd])
-        ops.gemm_batched(dS, flat, dflat[d:], T, hd, T, True, True, ops.EPI_STORE_BF16, B * H, H, T, ld, ld,
-                         [H * T * T, T * T, T * ld, hd, T * ld, hd])
 
     # ------------------------------------------------------------------------------ step
     def train_step(self, tokens, targets):
@@ -173,6 +132,7 @@ class GPT2:
         B, T = tokens.shape
         assert T <= c.n_ctx and T % 8 == 0
         M, d = B * T, c.d
+        scale = 1.0 / math.sqrt(d // c.n_head)
         b = self._buffers(B, T)
         L = self.layout
         P = self.table.get()
@@ -184,7 +144,7 @@ class GPT2:
             m1, r1 = b["st1"][i]
             ops.layernorm_fwd(x[i], d, v(P, blk["ln1_g"]), v(P, blk["ln1_b"]), 1e-5, b["h1"][i], m1, r1)
             blk["qkv"].forward(P, b["h1"][i], b["qkv"][i], "none")
-            self._attn_fwd(b["qkv"][i], b["P"][i], b["S"], b["ao"][i], B, T)
+            ops.attn_fwd(b["qkv"][i], B, T, c.n_head, scale, b["ao"][i], b["lse"][i])
             blk["proj"].forward(P, b["ao"][i], b["tmp"], "none")
             ops.add_bf16(x[i], b["tmp"], b["xm"][i])
             m2, r2 = b["st2"][i]
@@ -219,7 +179,7 @@ class GPT2:
             # attention branch
             blk["proj"].wgrad(G, dx, b["ao"][i])
             blk["proj"].dgrad(P, dx, b["dao"])
-            self._attn_bwd(b["qkv"][i], b["P"][i], b["dao"], b["dqkv"], b, B, T)
+            ops.attn_bwd(b["qkv"][i], b["ao"][i], b["dao"], b["lse"][i], b["delta"], B, T, c.n_head, scale, b["dqkv"])
             blk["qkv"].wgrad(G, b["dqkv"], b["h1"][i])
             blk["qkv"].dgrad(P, b["dqkv"], dh)
             m1, r1 = b["st1"][i]

@@ -84,14 +84,19 @@ class Linear:
         return ops.linear_wgrad(dy, x_ext, self.W(G))
 
     def dgrad(self, P, dy, out, mask=None, gelu_u=None, out_f32=False, k_rows=None):
-        """out = dy W[:, :k_in] (ReLU-masked by `mask`, or times gelu'(gelu_u))."""
+        """out = dy W[:, :k_in] (ReLU-masked by `mask`, or times gelu'(gelu_u)).
+
+        The [K][N] weight layout is read 8 columns at a time, so an unaligned k_in computes
+        align8(k_in) columns: the extra ones (bias column, zero padding) land in out's padding."""
         W = self.W(P)
         M = dy.shape[0]
         K = k_rows or self.n_rows
+        N = align(self.k_in)
+        assert out.shape[1] >= N, f"dgrad output needs {N} columns"
         if out_f32:
-            return ops.gemm(dy, W, out, M, self.k_in, K, False, True, ops.EPI_STORE_F32)
+            return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_STORE_F32)
         if gelu_u is not None:
-            return ops.gemm(dy, W, out, M, self.k_in, K, False, True, ops.EPI_GELU_GRAD_BF16, mask=gelu_u)
+            return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_GELU_GRAD_BF16, mask=gelu_u)
         if mask is not None:
-            return ops.gemm(dy, W, out, M, self.k_in, K, False, True, ops.EPI_RELU_MASK_BF16, mask=mask)
-        return ops.gemm(dy, W, out, M, self.k_in, K, False, True, ops.EPI_STORE_BF16)
+            return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_RELU_MASK_BF16, mask=mask)
+        return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_STORE_BF16)

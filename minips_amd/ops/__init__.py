@@ -440,6 +440,50 @@ def add_bf16(a, b, out):
     return out
 
 
+def _attn_heads(x, B, T, H, col0):
+    hd = 64
+    return x[:, col0: col0 + H * hd].float().reshape(B, T, H, hd).transpose(1, 2)
+
+
+def attn_fwd(qkv, B, T, H, scale, O, lse):
+    """Fused causal attention (head dim 64): O[:, h*64:] = softmax(mask(Q K^T scale)) V per head,
+    lse [B*H*T] = log2-sum-exp2 of the scaled scores (log2 units, for the backward)."""
+    if _gpu(qkv):
+        kernels().attn_fwd(qkv, int(B), int(T), int(H), float(scale), O, lse)
+        return O
+    d = H * 64
+    q, k, v = (_attn_heads(qkv, B, T, H, c) for c in (0, d, 2 * d))
+    s = (q @ k.transpose(-1, -2)) * scale
+    s = s.masked_fill(torch.ones(T, T, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    lse.view(B, H, T).copy_(torch.logsumexp(s, -1) * (1.0 / math.log(2.0)))
+    o = torch.softmax(s, -1) @ v
+    O[:, :d] = o.transpose(1, 2).reshape(B * T, d).to(O.dtype)
+    return O
+
+
+def attn_bwd(qkv, O, dO, lse, delta, B, T, H, scale, dqkv):
+    """Backward of attn_fwd: writes dQ|dK|dV into dqkv [B*T, 3*H*64]; delta is [B*H*T] scratch."""
+    if _gpu(qkv):
+        kernels().attn_bwd(qkv, O, dO, lse, delta, int(B), int(T), int(H), float(scale), dqkv)
+        return dqkv
+    d = H * 64
+    q, k, v = (_attn_heads(qkv, B, T, H, c) for c in (0, d, 2 * d))
+    o = _attn_heads(O, B, T, H, 0)
+    do = _attn_heads(dO, B, T, H, 0)
+    s = (q @ k.transpose(-1, -2)) * scale
+    mask = torch.ones(T, T, dtype=torch.bool, device=s.device).triu(1)
+    p = torch.exp2(s * (1.0 / math.log(2.0)) - lse.view(B, H, T, 1)).masked_fill(mask, 0.0)
+    dl = (do * o).sum(-1, keepdim=True)
+    delta.view(B, H, T).copy_(dl.squeeze(-1))
+    dv = p.transpose(-1, -2) @ do
+    ds = p * (do @ v.transpose(-1, -2) - dl)
+    dq = ds @ k * scale
+    dk = ds.transpose(-1, -2) @ q * scale
+    for i, t in enumerate((dq, dk, dv)):
+        dqkv[:, i * d: (i + 1) * d] = t.transpose(1, 2).reshape(B * T, d).to(dqkv.dtype)
+    return dqkv
+
+
 def embed_fwd(wte, wpe, tok, T, out):
     """out[m, :C] = wte[tok[m]] + wpe[m % T] (bf16)."""
     if _gpu(wte):

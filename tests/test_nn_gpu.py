@@ -223,3 +223,28 @@ def test_lr_kmeans_gpu_matches_cpu(dev):
     for a, b in zip(gp[2], c[2]):
         assert abs(a - b) < 1e-3 * b
     torch.testing.assert_close(gp[3], c[3], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 64, 2), (1, 256, 3), (2, 200, 2), (1, 1024, 1)])
+def test_flash_attention(dev, B, T, H):
+    g = torch.Generator().manual_seed(T + H)
+    d = H * 64
+    qkv = _bf(torch.randn(B * T, 3 * d, generator=g))
+    dO = _bf(torch.randn(B * T, d, generator=g))
+    scale = 0.125
+    res = {}
+    for dv in ("cpu", dev):
+        O = torch.zeros(B * T, d + 8, dtype=torch.bfloat16, device=dv)
+        lse = torch.empty(B * H * T, device=dv)
+        ops.attn_fwd(qkv.to(dv), B, T, H, scale, O, lse)
+        dq = torch.zeros(B * T, 3 * d, dtype=torch.bfloat16, device=dv)
+        delta = torch.empty(B * H * T, device=dv)
+        # backward from the CPU forward output so both sides see the same O
+        Oc = res["cpu"][0].to(dv) if "cpu" in res else O
+        ops.attn_bwd(qkv.to(dv), Oc, dO.to(dv), lse, delta, B, T, H, scale, dq)
+        res[str(dv)] = (O, lse, dq)
+    c, gp = res["cpu"], res[str(dev)]
+    _close(gp[0][:, :d], c[0][:, :d], 2e-2)
+    _close(gp[1], c[1], 2e-3)
+    err = (gp[2].float().cpu() - c[2].float()).abs().max() / c[2].float().abs().max()
+    assert err < 2e-2, float(err)
