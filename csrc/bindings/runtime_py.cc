@@ -10,11 +10,64 @@
 #include "../runtime/comm.h"
 #include "../runtime/config.h"
 #include "../runtime/engine.h"
+#include "../runtime/shard_io.h"
 
 namespace py = pybind11;
 using namespace minips;
 
 namespace {
+
+DType ParseDType(const std::string& s) {
+  if (s == "float32") return DType::kF32;
+  if (s == "bfloat16") return DType::kBF16;
+  if (s == "float64") return DType::kF64;
+  if (s == "int64") return DType::kI64;
+  if (s == "int32") return DType::kI32;
+  throw std::invalid_argument("unsupported dtype " + s);
+}
+const char* DTypeName(DType t) {
+  switch (t) {
+    case DType::kF32:
+      return "float32";
+    case DType::kBF16:
+      return "bfloat16";
+    case DType::kF64:
+      return "float64";
+    case DType::kI64:
+      return "int64";
+    case DType::kI32:
+      return "int32";
+  }
+  return "?";
+}
+ShardMeta MetaFromDict(const py::dict& d) {
+  ShardMeta m;
+  m.global_rows = d["global_rows"].cast<uint64_t>();
+  m.base = d["base"].cast<uint64_t>();
+  m.rows = d["rows"].cast<uint64_t>();
+  m.cols = d["cols"].cast<uint64_t>();
+  m.clock = d["clock"].cast<int64_t>();
+  m.table_id = d["table_id"].cast<int32_t>();
+  m.rank = d["rank"].cast<int32_t>();
+  m.world = d["world"].cast<int32_t>();
+  m.kind = d["kind"].cast<std::string>();
+  return m;
+}
+// arrays: [(name, data_ptr, dtype, rows, cols)] -- host memory kept alive by the caller
+std::vector<ArrayRef> ArraysFromList(const py::list& l) {
+  std::vector<ArrayRef> out;
+  for (auto item : l) {
+    auto t = item.cast<py::tuple>();
+    ArrayRef a;
+    a.name = t[0].cast<std::string>();
+    a.data = reinterpret_cast<const void*>(t[1].cast<uintptr_t>());
+    a.dtype = ParseDType(t[2].cast<std::string>());
+    a.rows = t[3].cast<uint64_t>();
+    a.cols = t[4].cast<uint64_t>();
+    out.push_back(a);
+  }
+  return out;
+}
 
 template <typename Val>
 void BindTable(py::module& m, const char* name) {
@@ -277,4 +330,63 @@ PYBIND11_MODULE(_runtime, m) {
       },
       py::arg("path"), py::arg("shard") = 0, py::arg("num_shards") = 1, py::arg("threads") = 4,
       py::arg("one_based") = true);
+
+  // --- GPU shard checkpoint files (binary sidecar + reference text format) ---------------
+  py::class_<AsyncShardWriter>(m, "ShardWriter")
+      .def(py::init<>())
+      .def(
+          "submit",
+          [](AsyncShardWriter& w, const std::string& path, const py::dict& meta, const py::list& arrays,
+             const std::string& text_path) {
+            ShardMeta mm = MetaFromDict(meta);
+            std::vector<ArrayRef> aa = ArraysFromList(arrays);
+            return w.Submit([path, mm, aa, text_path] {
+              WriteShard(path, mm, aa);
+              if (!text_path.empty() && !aa.empty()) WriteTextParams(text_path, aa[0]);
+            });
+          },
+          py::arg("path"), py::arg("meta"), py::arg("arrays"), py::arg("text_path") = "")
+      .def("wait", &AsyncShardWriter::Wait, py::call_guard<py::gil_scoped_release>())
+      .def("wait_all", &AsyncShardWriter::WaitAll, py::call_guard<py::gil_scoped_release>())
+      .def("take_error", &AsyncShardWriter::TakeError);
+  m.def(
+      "read_shard",
+      [](const std::string& path) {
+        LoadedShard s;
+        {
+          py::gil_scoped_release rel;
+          s = ReadShard(path);
+        }
+        py::dict meta;
+        meta["global_rows"] = s.meta.global_rows;
+        meta["base"] = s.meta.base;
+        meta["rows"] = s.meta.rows;
+        meta["cols"] = s.meta.cols;
+        meta["clock"] = s.meta.clock;
+        meta["table_id"] = s.meta.table_id;
+        meta["rank"] = s.meta.rank;
+        meta["world"] = s.meta.world;
+        meta["kind"] = s.meta.kind;
+        py::list arrays;
+        for (auto& a : s.arrays) {
+          auto* holder = new std::vector<char>(std::move(a.bytes));
+          py::capsule own(holder, [](void* p) { delete static_cast<std::vector<char>*>(p); });
+          py::array_t<uint8_t> buf({(py::ssize_t)holder->size()}, {(py::ssize_t)1},
+                                   reinterpret_cast<uint8_t*>(holder->data()), own);
+          arrays.append(py::make_tuple(a.name, DTypeName(a.dtype), a.rows, a.cols, buf));
+        }
+        return py::make_tuple(meta, arrays);
+      },
+      py::arg("path"));
+  m.def(
+      "read_text_params",
+      [](const std::string& path, uint64_t n) {
+        std::vector<double> v;
+        {
+          py::gil_scoped_release rel;
+          v = ReadTextParams(path, n);
+        }
+        return py::array_t<double>(v.size(), v.data());
+      },
+      py::arg("path"), py::arg("n"));
 }

@@ -189,17 +189,25 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __rest
   }
 }
 
-// dst[j] += sum_g partial[g][j] for j < 2C  (dst = [dgamma | dbeta] as two pointers)
-__global__ void layernorm_colsum_kernel(const float* __restrict__ partial, int G, int C, float* __restrict__ dgamma,
-                                        float* __restrict__ dbeta) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 2 * C) return;
+// dgamma/dbeta[j] += sum_g partial[g][j], j < 2C: 64 columns per block (coalesced rows), the
+// block's 4 waves split the G partial rows and combine in LDS.
+__global__ __launch_bounds__(256) void layernorm_colsum_kernel(const float* __restrict__ partial, int G, int C,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int g = 0; g < G; ++g) s += partial[(int64_t)g * 2 * C + j];
-  if (j < C)
-    dgamma[j] += s;
-  else
-    dbeta[j - C] += s;
+  if (j < 2 * C)
+    for (int g = w; g < G; g += 4) s += partial[(int64_t)g * 2 * C + j];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && j < 2 * C) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (j < C)
+      dgamma[j] += t;
+    else
+      dbeta[j - C] += t;
+  }
 }
 
 int layernorm_bwd_blocks(int64_t M) { return (int)std::min<int64_t>(std::max<int64_t>((M + 31) / 32, 1), 512); }
@@ -222,46 +230,122 @@ void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t
   hipLaunchKernelGGL(layernorm_bwd_kernel, G, 256, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx, partial,
                      accumulate_dx);
   MINIPS_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(layernorm_colsum_kernel, (2 * C + 255) / 256, 256, 0, s, partial, G, C, dgamma, dbeta);
+  hipLaunchKernelGGL(layernorm_colsum_kernel, (2 * C + 63) / 64, 256, 0, s, partial, G, C, dgamma, dbeta);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------- softmax-xent
-// logits may be updated in place with the gradient ((softmax - onehot) * scale).
-__global__ __launch_bounds__(256) void softmax_xent_kernel(bf16_t* __restrict__ logits, int ld, int64_t M, int V,
-                                                           const int64_t* __restrict__ labels, float scale,
-                                                           float* loss_sum, float* correct) {
-  __shared__ float red[8];
+// logits are updated in place with the gradient ((softmax - onehot) * scale); columns [V, ld)
+// inside the last 8-wide chunk are zeroed. One 512-thread block per row; the row (up to
+// 512 * 8 * 13 = 53248 columns, GPT-2's 50304 included) stays in registers as packed 16-byte
+// chunks, so HBM sees exactly one read and one write of the logits.
+constexpr int kXentThreads = 512, kXentChunks = 13;
+
+// Component q of a uint4 without taking its address (keeps the chunk array in registers).
+__device__ __forceinline__ uint32_t u4get(const uint4& v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w; }
+__device__ __forceinline__ float u4elem(const uint4& v, int q) {
+  const uint32_t w = u4get(v, q >> 1);
+  return (q & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+}
+
+__device__ __forceinline__ float xent_block_max(float v, float* red) {
+  v = warp_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = -3.4e38f;
+#pragma unroll
+  for (int i = 0; i < kXentThreads / 64; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+__device__ __forceinline__ float xent_block_sum(float v, float* red) {
+  v = warp_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < kXentThreads / 64; ++i) t += red[i];
+  return t;
+}
+
+__global__ __launch_bounds__(kXentThreads) void softmax_xent_kernel(bf16_t* __restrict__ logits, int ld, int64_t M,
+                                                                    int V, const int64_t* __restrict__ labels,
+                                                                    float scale, float* loss_sum, float* correct) {
+  __shared__ float red[kXentThreads / 64];
+  const int nfull = V >> 3;          // chunks with 8 valid columns
+  const int tail = V & 7;            // valid columns of chunk nfull (0: none)
+  const float L2E = 1.4426950408889634f;
   for (int64_t r = blockIdx.x; r < M; r += gridDim.x) {
     bf16_t* row = logits + r * ld;
+    uint4 v[kXentChunks];
     float mx = -3.4e38f;
-    for (int c = threadIdx.x; c < V; c += blockDim.x) mx = fmaxf(mx, bf2f(row[c]));
-    mx = block_max(mx, red);
+#pragma unroll
+    for (int k = 0; k < kXentChunks; ++k) {
+      const int ch = threadIdx.x + k * kXentThreads;
+      if (ch < nfull) {
+        v[k] = *reinterpret_cast<const uint4*>(row + ch * 8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) mx = fmaxf(mx, u4elem(v[k], q));
+      } else if (ch == nfull && tail) {
+        v[k] = *reinterpret_cast<const uint4*>(row + ch * 8);
+#pragma unroll 1
+        for (int q = 0; q < tail; ++q) mx = fmaxf(mx, bf2f(row[ch * 8 + q]));
+      }
+    }
+    mx = xent_block_max(mx, red);
+    const float ml2 = mx * L2E;
     float se = 0.f;
-    for (int c = threadIdx.x; c < V; c += blockDim.x) se += __expf(bf2f(row[c]) - mx);
-    se = block_sum(se, red);
+#pragma unroll
+    for (int k = 0; k < kXentChunks; ++k) {
+      const int ch = threadIdx.x + k * kXentThreads;
+      if (ch < nfull) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) se += __builtin_amdgcn_exp2f(u4elem(v[k], q) * L2E - ml2);
+      } else if (ch == nfull && tail) {
+#pragma unroll 1
+        for (int q = 0; q < tail; ++q) se += __builtin_amdgcn_exp2f(bf2f(row[ch * 8 + q]) * L2E - ml2);
+      }
+    }
+    se = xent_block_sum(se, red);
     const int64_t lab = labels[r];
     const float lse = mx + __logf(se);
-    if (threadIdx.x == 0) {
-      const float zl = (lab >= 0 && lab < V) ? bf2f(row[lab]) : lse;
+    if (threadIdx.x == 0 && lab >= 0 && lab < V) {  // (row[lab] is rewritten only after the block syncs)
+      const float zl = bf2f(row[lab]);
       atomicAdd(loss_sum, lse - zl);
-      if (correct && lab >= 0 && lab < V && zl >= mx) atomicAdd(correct, 1.f);
+      if (correct && zl >= mx) atomicAdd(correct, 1.f);
     }
     __syncthreads();
-    const float inv = 1.f / se;
-    for (int c = threadIdx.x; c < V; c += blockDim.x) {
-      const float p = __expf(bf2f(row[c]) - mx) * inv;
-      row[c] = f2bf((p - (c == lab ? 1.f : 0.f)) * scale);
+    const float sinv = scale / se;
+#pragma unroll
+    for (int k = 0; k < kXentChunks; ++k) {
+      const int ch = threadIdx.x + k * kXentThreads;
+      if (ch < nfull || (ch == nfull && tail)) {
+        const int nv = ch < nfull ? 8 : tail;
+        uint32_t o[4];
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+          const float g0 = __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2) * L2E - ml2) * sinv;
+          const float g1 = __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2 + 1) * L2E - ml2) * sinv;
+          o[q2] = pack_bf2(2 * q2 < nv ? g0 : 0.f, 2 * q2 + 1 < nv ? g1 : 0.f);
+        }
+        *reinterpret_cast<uint4*>(row + ch * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
     }
     __syncthreads();
+    if (threadIdx.x == 0 && lab >= 0 && lab < V) row[lab] = f2bf(bf2f(row[lab]) - scale);  // the -onehot term
   }
 }
 
 void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,
                   float* correct, hipStream_t s) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(softmax_xent_kernel, (int)std::min<int64_t>(M, 8192), 256, 0, s, logits, ld, M, V, labels, scale,
-                     loss_sum, correct);
+  if ((V + 7) / 8 > kXentThreads * kXentChunks || ld % 8 || ld < (V + 7) / 8 * 8)
+    throw std::runtime_error("softmax_xent: V <= 53248 and ld % 8 == 0, ld >= align8(V)");
+  hipLaunchKernelGGL(softmax_xent_kernel, (int)std::min<int64_t>(M, 4096), kXentThreads, 0, s, logits, ld, M, V,
+                     labels, scale, loss_sum, correct);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -191,6 +191,42 @@ class DenseTable:
     def drain(self):
         self.pipe.drain()
 
+    # -- checkpoint hooks (minips_amd.ps.checkpoint) -------------------------------------------
+    def shard_state(self):
+        """(meta, {name: tensor}) of the owned shard: fp32 master + optimizer state, padding
+        beyond n_params excluded."""
+        rows = max(0, min(self.shard, self.n_params - self.base))
+        arrays = {"master": self.master[:rows]}
+        if self.m is not None:
+            arrays["m"] = self.m[:rows]
+        if self.v is not None:
+            arrays["v"] = self.v[:rows]
+        meta = dict(global_rows=self.n_params, base=self.base, rows=rows, cols=1, clock=self.step,
+                    table_id=self.table_id, rank=self.comm.rank, world=self.comm.world, kind="dense")
+        return meta, arrays
+
+    def load_shard_pieces(self, pieces, clock: int):
+        """pieces: [(meta, {name: cpu tensor})] from any world size; copies every overlap of a
+        piece's global range with the owned shard, then re-pulls (all-gather) the parameters."""
+        lo, hi = self.base, min(self.base + self.shard, self.n_params)
+        dst = {"master": self.master, "m": self.m, "v": self.v}
+        for meta, arrays in pieces:
+            a, b = max(lo, meta["base"]), min(hi, meta["base"] + meta["rows"])
+            if a >= b:
+                continue
+            for name, t in arrays.items():
+                d = dst.get(name)
+                if d is not None:
+                    d[a - lo: b - lo].copy_(t.reshape(-1)[a - meta["base"]: b - meta["base"]])
+        self.step = int(clock)
+        self.pipe.clock = int(clock)
+        own = self.params[self.base: self.base + self.shard]
+        if self.pull_dtype == torch.bfloat16:
+            ops.cast_f32_bf16(self.master, own)
+        else:
+            own.copy_(self.master)
+        self.comm.all_gather(self.params, own)
+
 
 @dataclass
 class SparsePlan:
@@ -326,3 +362,28 @@ class SparseTable:
 
     def drain(self):
         self.pipe.drain()
+
+    # -- checkpoint hooks (minips_amd.ps.checkpoint) -------------------------------------------
+    def shard_state(self):
+        arrays = {"params": self.shard}
+        if self.state is not None:
+            arrays["state"] = self.state
+        if self.state2 is not None:
+            arrays["state2"] = self.state2
+        meta = dict(global_rows=self.num_rows, base=self.base, rows=self.rows_local, cols=self.width,
+                    clock=self.pipe.clock, table_id=self.table_id, rank=self.comm.rank, world=self.comm.world,
+                    kind="sparse")
+        return meta, arrays
+
+    def load_shard_pieces(self, pieces, clock: int):
+        lo, hi = self.base, self.base + self.rows_local
+        dst = {"params": self.shard, "state": self.state, "state2": self.state2}
+        for meta, arrays in pieces:
+            a, b = max(lo, meta["base"]), min(hi, meta["base"] + meta["rows"])
+            if a >= b:
+                continue
+            for name, t in arrays.items():
+                d = dst.get(name)
+                if d is not None:
+                    d[a - lo: b - lo].copy_(t[a - meta["base"]: b - meta["base"]].reshape(d[a - lo: b - lo].shape))
+        self.pipe.clock = int(clock)

@@ -1,0 +1,139 @@
+"""Observability of a PS rank.
+
+MetricsLogger   structured JSONL per rank (``$MINIPS_METRICS_DIR/rank<r>.jsonl`` when set):
+                step records (step time, samples/s, bytes pushed/pulled per collective and the
+                achieved GB/s, staleness histogram, pending-buffer depth) and events (checkpoint,
+                restore, fault-tolerance phases). Without the env var it only keeps counters.
+range(name)     roctx range (libroctx64) around Get / Add / Clock / apply / collectives, so the
+                phases show up in rocprofv3 --marker-trace timelines; a no-op when roctx is absent.
+fault_tolerance_phase(n, detail)
+                the reference's "[Fault Tolerance][PhaseN][ts] ..." line (base/utils.hpp:24-53).
+"""
+from __future__ import annotations
+
+import collections
+import contextlib
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+_ROCTX = None
+_ROCTX_TRIED = False
+
+
+def _roctx():
+    global _ROCTX, _ROCTX_TRIED
+    if not _ROCTX_TRIED:
+        _ROCTX_TRIED = True
+        if os.environ.get("MINIPS_ROCTX", "1") != "0":
+            for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+                try:
+                    lib = ctypes.CDLL(name)
+                    lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                    lib.roctxRangePushA.restype = ctypes.c_int
+                    lib.roctxRangePop.restype = ctypes.c_int
+                    _ROCTX = lib
+                    break
+                except OSError:
+                    continue
+    return _ROCTX
+
+
+@contextlib.contextmanager
+def range(name: str):  # noqa: A001 - mirrors the roctx naming
+    lib = _roctx()
+    if lib is not None:
+        lib.roctxRangePushA(name.encode())
+    try:
+        yield
+    finally:
+        if lib is not None:
+            lib.roctxRangePop()
+
+
+class MetricsLogger:
+    def __init__(self, rank: int = 0, path: str | None = None):
+        self.rank = rank
+        self.path = path
+        self._f = None
+        self._lock = threading.Lock()
+        self.staleness_hist: collections.Counter = collections.Counter()
+        self.pending_depth_max = 0
+        self.steps = 0
+        self._last = None
+
+    def _write(self, rec: dict):
+        if self.path is None:
+            return
+        with self._lock:
+            if self._f is None:
+                os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+                self._f = open(self.path, "a", buffering=1)
+            self._f.write(json.dumps(rec) + "\n")
+
+    def event(self, kind: str, **fields):
+        self._write(dict(ts=time.time(), rank=self.rank, event=kind, **fields))
+
+    def observe_staleness(self, s: int):
+        self.staleness_hist[int(s)] += 1
+
+    def observe_pending(self, depth: int):
+        self.pending_depth_max = max(self.pending_depth_max, int(depth))
+
+    def step(self, step: int, samples: int, seconds: float, comm_stats=None, **extra):
+        """One training-step record; comm_stats is a CommStats (bytes since the last call)."""
+        self.steps += 1
+        rec = dict(ts=time.time(), rank=self.rank, step=step, step_ms=round(seconds * 1e3, 4),
+                   samples_per_s=round(samples / seconds, 1) if seconds > 0 else None)
+        if comm_stats is not None:
+            d = comm_stats.as_dict()
+            prev = self._last or {k: 0 for k in d}
+            delta = {k: d[k] - prev.get(k, 0) for k in d}
+            self._last = d
+            moved = delta["bytes_a2a"] + delta["bytes_rs"] + delta["bytes_ag"]
+            rec.update(bytes_pushed=delta["bytes_a2a"] // 2 + delta["bytes_rs"],
+                       bytes_pulled=delta["bytes_a2a"] - delta["bytes_a2a"] // 2 + delta["bytes_ag"],
+                       collectives=delta["calls"],
+                       xgmi_gbps=round(moved / seconds / 1e9, 3) if seconds > 0 else None)
+        if self.staleness_hist:
+            rec["staleness_hist"] = dict(self.staleness_hist)
+        if self.pending_depth_max:
+            rec["pending_depth_max"] = self.pending_depth_max
+        rec.update(extra)
+        self._write(rec)
+        return rec
+
+    def close(self):
+        with self._lock:
+            if self._f is not None:
+                self._f.close()
+                self._f = None
+
+
+_LOGGER: MetricsLogger | None = None
+
+
+def get_logger() -> MetricsLogger:
+    global _LOGGER
+    if _LOGGER is None:
+        rank = int(os.environ.get("RANK", "0"))
+        d = os.environ.get("MINIPS_METRICS_DIR")
+        _LOGGER = MetricsLogger(rank, os.path.join(d, f"rank{rank}.jsonl") if d else None)
+    return _LOGGER
+
+
+_PHASES = {1: "Phase1", 2: "Phase2 detect failure", 3: "Phase3 restart", 4: "Phase4 recover",
+           5: "Phase5 others recovered"}
+
+
+def fault_tolerance_phase(phase: int, detail: str = "", stream=None):
+    """Reference log line "[Fault Tolerance][Phase<n>][<unix ms>] <name>: <detail>" (base/utils.hpp:24-53),
+    same text as the native runtime's CheckFaultTolerance."""
+    ts = int(time.time() * 1000)
+    line = f"[Fault Tolerance][Phase{phase}][{ts}] {_PHASES.get(phase, 'Phase?')}" + (f": {detail}" if detail else "")
+    print(line, file=stream or sys.stderr, flush=True)
+    get_logger().event("fault_tolerance", phase=phase, detail=detail, ts_ms=ts)
+    return line
