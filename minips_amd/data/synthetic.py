@@ -66,6 +66,16 @@ class CriteoSynth:
         labels = (torch.sigmoid(2.0 * logit) > noise).float()
         return dense, keys, labels
 
+    def skip(self, n: int):
+        """Advance past ``n`` batches (resume from a checkpoint at the same data position)."""
+        if self.device.type == "cuda":
+            if not hasattr(self, "_seed"):
+                self._seed = int(torch.randint(0, 2**62, (1,), generator=self.gen, device=self.device).item())
+            self._step = getattr(self, "_step", 0) + n
+        else:
+            for _ in range(n):
+                self.next()
+
 
 def _cumsum(xs):
     s = 0

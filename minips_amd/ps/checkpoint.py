@@ -1,7 +1,11 @@
 """Checkpoint / resume of the GPU parameter-server tables.
 
-Files under ``prefix`` (local FS), one set per rank ``my_id``, reference names and text formats
-kept for compatibility:
+Every checkpoint goes to ``<prefix>iter_<k>/`` and becomes the restore point only when it is
+committed: after every rank finished writing, a barrier, then rank 0 atomically rewrites
+``<prefix>latest`` (= k) and drops older iteration directories. A failure while a checkpoint is
+still being written therefore restores the previous complete one, never a mix of iterations.
+Files inside an iteration directory, one set per rank ``my_id``, keep the reference names and
+text formats:
 
   server_params_<id>_t<table>.bin  binary sidecar: header + fp32 shard + optimizer state
                                    (native writer, csrc/runtime/shard_io.cc)
@@ -51,7 +55,9 @@ class Checkpointer:
         self._host: dict = {}
         self._thread: threading.Thread | None = None
         self._error: BaseException | None = None
+        self._pending_iter: int | None = None
         self.last_seconds = 0.0
+        self.keep = 2
 
     # ------------------------------------------------------------------------------ save
     def _staging(self, key, t: torch.Tensor) -> torch.Tensor:
@@ -61,10 +67,15 @@ class Checkpointer:
             self._host[key] = h
         return h
 
+    def iter_dir(self, iteration: int) -> str:
+        return f"{self.prefix}iter_{int(iteration)}/"
+
     def save(self, tables: dict, iteration: int, blocking: bool = False):
-        """Checkpoint every table ({table_id: table}) at ``iteration`` (collective: all ranks)."""
-        self.wait()
+        """Checkpoint every table ({table_id: table}) at ``iteration`` (collective: all ranks).
+        The write drains in the background; ``commit()`` (collective) publishes it."""
+        self.commit()
         t0 = time.perf_counter()
+        out = self.iter_dir(iteration)
         for t in tables.values():
             t.drain()
         # every rank's clock of every table -> the progress files carry the whole tracker view
@@ -104,10 +115,10 @@ class Checkpointer:
                     arrays = [(n, h.data_ptr(), _DT[h.dtype], h.shape[0] if h.dim() else 1,
                                h.shape[1] if h.dim() > 1 else 1) for n, h in host.items()]
                     n_vals = sum(h.numel() for h in host.values()) // max(1, len(host))
-                    text = _prefix_path(self.prefix, base) if n_vals <= self.text_limit else ""
-                    self._writer.submit(_prefix_path(self.prefix, base + ".bin"), meta, arrays, text)
-                    self._write_progress(tid, clk)
-                self._write_worker_config(iteration)
+                    text = _prefix_path(out, base) if n_vals <= self.text_limit else ""
+                    self._writer.submit(_prefix_path(out, base + ".bin"), meta, arrays, text)
+                    self._write_progress(out, tid, clk)
+                self._write_worker_config(out, iteration)
                 self._writer.wait_all()
                 err = self._writer.take_error()
                 if err:
@@ -120,8 +131,30 @@ class Checkpointer:
 
         self._thread = threading.Thread(target=work, name="minips-ckpt", daemon=True)
         self._thread.start()
+        self._pending_iter = int(iteration)
         if blocking:
-            self.wait()
+            self.commit()
+
+    def commit(self):
+        """Finish the in-flight checkpoint on every rank and publish it (collective)."""
+        if self._pending_iter is None:
+            return
+        self.wait()
+        self.comm.barrier()
+        it, self._pending_iter = self._pending_iter, None
+        if self.comm.rank == 0:
+            tmp = self.prefix + "latest.tmp"
+            with open(tmp, "w") as f:
+                f.write(str(it))
+            os.replace(tmp, self.prefix + "latest")
+            done = sorted(int(d[len("iter_"):]) for d in os.listdir(self.prefix or ".")
+                          if d.startswith("iter_") and d[len("iter_"):].isdigit())
+            for old in done[:-self.keep]:
+                if old != it:
+                    import shutil
+
+                    shutil.rmtree(self.iter_dir(old), ignore_errors=True)
+        self.comm.barrier()
 
     def wait(self):
         if self._thread is not None:
@@ -131,29 +164,40 @@ class Checkpointer:
             e, self._error = self._error, None
             raise e
 
-    def _write_progress(self, tid: int, clocks: list):
-        path = _prefix_path(self.prefix, f"server_progress_{self.my_id}_t{tid}")
+    def _write_progress(self, out: str, tid: int, clocks: list):
+        path = _prefix_path(out, f"server_progress_{self.my_id}_t{tid}")
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         parts = [f"min_clock:{int(min(clocks))}"]
         parts += [f"{r * 1000 + WORKER_TID_OFFSET}:{int(c)}" for r, c in enumerate(clocks)]
         with open(path, "w") as f:
             f.write(" ".join(parts) + " ")
 
-    def _write_worker_config(self, iteration: int):
-        path = _prefix_path(self.prefix, f"worker_config_{self.my_id}")
+    def _write_worker_config(self, out: str, iteration: int):
+        path = _prefix_path(out, f"worker_config_{self.my_id}")
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         runtime().dump_config_data(path, {int(self.comm.rank): int(iteration)})
 
     # ------------------------------------------------------------------------------ load
-    def exists(self) -> bool:
-        return os.path.exists(_prefix_path(self.prefix, f"worker_config_{self.my_id}"))
+    def latest(self) -> int | None:
+        try:
+            return int(open(self.prefix + "latest").read().strip())
+        except (OSError, ValueError):
+            return None
 
-    def load(self, tables: dict) -> int:
-        """Restore every table from the sidecars of all ranks; returns the saved iteration."""
+    def exists(self) -> bool:
+        return self.latest() is not None
+
+    def load(self, tables: dict, iteration: int | None = None) -> int:
+        """Restore every table from the sidecars of all ranks of the latest committed checkpoint
+        (or ``iteration``); returns the saved iteration."""
+        it = self.latest() if iteration is None else int(iteration)
+        if it is None:
+            raise FileNotFoundError(f"no committed checkpoint under {self.prefix!r} (missing 'latest')")
+        src = self.iter_dir(it)
         for tid, table in sorted(tables.items()):
-            files = sorted(glob.glob(glob.escape(self.prefix) + f"server_params_*_t{tid}.bin"))
+            files = sorted(glob.glob(glob.escape(src) + f"server_params_*_t{tid}.bin"))
             if not files:
-                raise FileNotFoundError(f"no checkpoint shards for table {tid} under {self.prefix!r}")
+                raise FileNotFoundError(f"no checkpoint shards for table {tid} under {src!r}")
             pieces, clock = [], None
             my_meta = table.shard_state()[0]
             for path in files:
@@ -174,8 +218,10 @@ class Checkpointer:
                 if meta["rank"] == self.my_id or clock is None:
                     clock = meta["clock"]
             table.load_shard_pieces(pieces, clock or 0)
-        cfg = runtime().load_config_data(_prefix_path(self.prefix, f"worker_config_{self.my_id}"))
-        it = int(cfg.get(int(self.comm.rank), max(cfg.values()) if cfg else 0))
+        cfg_path = _prefix_path(src, f"worker_config_{self.my_id}")
+        if os.path.exists(cfg_path):
+            cfg = runtime().load_config_data(cfg_path)
+            it = int(cfg.get(int(self.comm.rank), it))
         get_logger().event("restore", iteration=it, prefix=self.prefix, tables=len(tables))
         return it
 
