@@ -1,5 +1,9 @@
 #include "checkpoint.h"
 
+#include <memory>
+
+#include "io.h"
+
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -106,38 +110,52 @@ bool ParseLibsvm(const char* line, size_t len, SVMItem* out, bool one_based) {
 
 std::vector<SVMItem> LoadLibsvmFile(const std::string& path, int shard, int num_shards, int num_threads,
                                     bool one_based) {
-  std::ifstream in(path, std::ios::binary);
-  MINIPS_CHECK(in.good(), "cannot read " << path);
-  std::string buf((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-  size_t n = buf.size();
-  auto align_line = [&](size_t pos) {
-    if (pos == 0 || pos >= n) return std::min(pos, n);
-    while (pos < n && buf[pos - 1] != '\n') ++pos;
-    return pos;
-  };
-  size_t sb = align_line(n * (size_t)shard / (size_t)num_shards);
-  size_t se = align_line(n * (size_t)(shard + 1) / (size_t)num_shards);
-  num_threads = std::max(1, num_threads);
-  std::vector<std::vector<SVMItem>> parts(num_threads);
+  // Blocks of every input file (a path, a directory or a comma list) are handed to this rank by
+  // the BlockAssigner and read by `num_threads` loader threads through the mmap'd
+  // LineInputFormat (io.h); results are kept per block so the order is deterministic.
+  const auto files = ListInputFiles(path);
+  uint64_t total = 0;
+  for (auto& f : files) {
+    std::ifstream in(f, std::ios::binary | std::ios::ate);
+    total += (uint64_t)in.tellg();
+  }
+  // ~4 blocks per loader thread and rank, at least 64 KiB (hdfs_block_size analogue)
+  const uint64_t block = std::max<uint64_t>(64 << 10, total / std::max(1, 4 * num_threads * num_shards) + 1);
+  auto blocks = SplitFiles(files, block);
+  std::vector<std::vector<SVMItem>> per_block(blocks.size());
+  BlockAssigner assigner(blocks, shard, num_shards);
   std::vector<std::thread> th;
-  for (int t = 0; t < num_threads; ++t) {
-    size_t b = align_line(sb + (se - sb) * (size_t)t / (size_t)num_threads);
-    size_t e = align_line(sb + (se - sb) * (size_t)(t + 1) / (size_t)num_threads);
-    if (t == num_threads - 1) e = se;
-    th.emplace_back([&, t, b, e] {
-      size_t p = b;
-      while (p < e) {
-        size_t nl = buf.find('\n', p);
-        if (nl == std::string::npos || nl > e) nl = e;
-        SVMItem item;
-        if (ParseLibsvm(buf.data() + p, nl - p, &item, one_based)) parts[t].push_back(std::move(item));
-        p = nl + 1;
+  std::mutex err_mu;
+  std::string err;
+  for (int t = 0; t < std::max(1, num_threads); ++t) {
+    th.emplace_back([&] {
+      try {
+        std::string cur;
+        std::unique_ptr<MappedFile> mf;
+        while (auto blk = assigner.Next()) {
+          if (blk->path != cur) {
+            mf.reset(new MappedFile(blk->path));
+            cur = blk->path;
+          }
+          LineInputFormat in(*mf, *blk);
+          const char* l;
+          size_t n;
+          auto& out = per_block[blk->id];
+          while (in.Next(&l, &n)) {
+            SVMItem item;
+            if (ParseLibsvm(l, n, &item, one_based)) out.push_back(std::move(item));
+          }
+        }
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> lk(err_mu);
+        err = e.what();
       }
     });
   }
   for (auto& t : th) t.join();
+  MINIPS_CHECK(err.empty(), "libsvm load failed: " << err);
   std::vector<SVMItem> all;
-  for (auto& p : parts)
+  for (auto& p : per_block)
     for (auto& it : p) all.push_back(std::move(it));
   return all;
 }

@@ -17,6 +17,9 @@
 #include "../runtime/comm.h"
 #include "../runtime/config.h"
 #include "../runtime/engine.h"
+#include "../runtime/io.h"
+#include "../runtime/serialization.h"
+#include "../runtime/shard_io.h"
 #include "../runtime/server.h"
 #include "../runtime/worker.h"
 #include "minitest.h"
@@ -813,6 +816,147 @@ TEST(Master, HeartbeatDetectsSilentNode) {
   e0.StopEverything();
   m.StopMaster();
   Context::Get().ResetToDefaults();
+}
+
+// ----------------------------------------------------------------------------- BinStream
+struct Custom {
+  int a = 0;
+  std::string s;
+  void serialize(minips::BinStream& b) const { b << a << s; }
+  void deserialize(minips::BinStream& b) { b >> a >> s; }
+};
+
+TEST(BinStream, RoundTrip) {
+  using namespace minips;
+  BinStream b;
+  std::vector<double> v{1.5, -2.0};
+  std::map<int, std::string> m{{1, "x"}, {7, "yz"}};
+  std::unordered_map<std::string, int> um{{"k", 3}};
+  std::vector<std::string> vs{"a", "", "bcd"};
+  SArray<Key> keys{3, 9, 27};
+  auto sp = std::make_shared<int>(42);
+  std::shared_ptr<int> nul;
+  Custom c;
+  c.a = 5;
+  c.s = "hi";
+  std::vector<Custom> vc{c, c};
+  b << 7 << std::string("hello") << v << m << um << vs << keys << std::make_pair(1, 2.5) << sp << nul << c << vc;
+  int i;
+  std::string str;
+  std::vector<double> v2;
+  std::map<int, std::string> m2;
+  std::unordered_map<std::string, int> um2;
+  std::vector<std::string> vs2;
+  SArray<Key> k2;
+  std::pair<int, double> pr;
+  std::shared_ptr<int> sp2, nul2 = std::make_shared<int>(1);
+  Custom c2;
+  std::vector<Custom> vc2;
+  BinStream r = BinStream::FromSArray(b.ToSArray());
+  r >> i >> str >> v2 >> m2 >> um2 >> vs2 >> k2 >> pr >> sp2 >> nul2 >> c2 >> vc2;
+  EXPECT_EQ(i, 7);
+  EXPECT_EQ(str, std::string("hello"));
+  EXPECT_TRUE(v2 == v);
+  EXPECT_TRUE(m2 == m);
+  EXPECT_TRUE(um2 == um);
+  EXPECT_TRUE(vs2 == vs);
+  EXPECT_EQ(k2.size(), 3u);
+  EXPECT_EQ(k2[2], (Key)27);
+  EXPECT_EQ(pr.second, 2.5);
+  EXPECT_EQ(*sp2, 42);
+  EXPECT_TRUE(nul2 == nullptr);
+  EXPECT_EQ(c2.s, std::string("hi"));
+  EXPECT_EQ(vc2.size(), 2u);
+  EXPECT_EQ(r.size(), 0u);
+  EXPECT_THROW(r >> i);
+}
+
+// ----------------------------------------------------------------------------- shard files
+TEST(ShardIO, BinaryAndTextRoundTrip) {
+  using namespace minips;
+  std::vector<float> params{0.f, 1.5f, 0.f, -2.25f, 3.f, 0.f};
+  std::vector<float> state{0.1f, 0.2f, 0.3f};
+  ShardMeta m;
+  m.global_rows = 10;
+  m.base = 4;
+  m.rows = 3;
+  m.cols = 2;
+  m.clock = 17;
+  m.table_id = 1;
+  m.rank = 2;
+  m.world = 3;
+  m.kind = "sparse";
+  const std::string dir = "/tmp/minips_shard_test_" + std::to_string(::getpid()) + "/";
+  AsyncShardWriter w;
+  auto t = w.Submit([&] {
+    WriteShard(dir + "a.bin", m, {{"params", params.data(), DType::kF32, 3, 2}, {"state", state.data(), DType::kF32, 3, 1}});
+    WriteTextParams(dir + "a.txt", {"params", params.data(), DType::kF32, 3, 2});
+  });
+  w.Wait(t);
+  EXPECT_EQ(w.TakeError(), std::string());
+  LoadedShard s = ReadShard(dir + "a.bin");
+  EXPECT_EQ(s.meta.clock, 17);
+  EXPECT_EQ(s.meta.kind, std::string("sparse"));
+  ASSERT_EQ(s.arrays.size(), 2u);
+  EXPECT_EQ(std::memcmp(s.arrays[0].bytes.data(), params.data(), 24), 0);
+  EXPECT_EQ(s.arrays[1].rows, 3u);
+  auto txt = ReadTextParams(dir + "a.txt", 6);
+  for (int i = 0; i < 6; ++i) EXPECT_EQ((float)txt[i], params[i]);
+  std::ifstream raw(dir + "a.txt");
+  std::string line;
+  std::getline(raw, line);
+  EXPECT_EQ(line, std::string("1:1.5 3:-2.25 4:3 "));
+  EXPECT_THROW(ReadShard(dir + "a.txt"));
+  auto t2 = w.Submit([] { throw std::runtime_error("disk full"); });
+  w.Wait(t2);
+  EXPECT_EQ(w.TakeError(), std::string("disk full"));
+}
+
+// ----------------------------------------------------------------------------- io
+TEST(IO, LinesReadExactlyOnceAcrossBlocks) {
+  using namespace minips;
+  const std::string dir = "/tmp/minips_io_test_" + std::to_string(::getpid()) + "/";
+  EnsureParentDir(dir + "x");
+  uint64_t expect_sum = 0, expect_lines = 0;
+  for (int f = 0; f < 3; ++f) {
+    std::ofstream o(dir + "part-" + std::to_string(f));
+    for (int i = 0; i < 257 + 31 * f; ++i) {
+      const int v = f * 100000 + i;
+      o << v << std::string((size_t)(i * 7 % 23), ' ') << "\n";
+      expect_sum += (uint64_t)v;
+      expect_lines++;
+    }
+    if (f == 2) o << 999999;  // last line without a trailing newline
+  }
+  expect_sum += 999999;
+  expect_lines++;
+  auto files = ListInputFiles(dir);
+  ASSERT_EQ(files.size(), 3u);
+  for (uint64_t bs : {1ull, 7ull, 64ull, 1000ull, 1ull << 20}) {
+    for (int ranks : {1, 3}) {
+      std::atomic<uint64_t> sum{0}, lines{0};
+      for (int r = 0; r < ranks; ++r) {
+        lines += LoadLines(files, bs, r, ranks, 4, [&](const char* l, size_t n, int) {
+          sum += std::stoull(std::string(l, n));
+        });
+      }
+      EXPECT_EQ(lines.load(), expect_lines);
+      EXPECT_EQ(sum.load(), expect_sum);
+    }
+  }
+}
+
+TEST(IO, AsyncReadBufferKeepsOrder) {
+  using namespace minips;
+  int next = 0;
+  AsyncReadBuffer<int> buf([&](int* out) {
+    if (next >= 100) return false;
+    *out = next++;
+    return true;
+  }, 4);
+  int v, expect = 0;
+  while (buf.Get(&v)) EXPECT_EQ(v, expect++);
+  EXPECT_EQ(expect, 100);
 }
 
 int main(int argc, char** argv) { return minitest::RunAll(argc, argv); }
