@@ -494,6 +494,41 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& O, const at::Tensor& dO, 
                      (float)scale, ptr<bf16_t>(dqkv), (int)dqkv.stride(0), stream_of(qkv));
 }
 
+void hash_slots(at::Tensor& tab_keys, const at::Tensor& q, at::Tensor& slots, at::Tensor& vals, double init_scale,
+                int64_t seed, at::Tensor& counters) {
+  for (const at::Tensor* t : {(const at::Tensor*)&tab_keys, &q, (const at::Tensor*)&slots, (const at::Tensor*)&vals,
+                              (const at::Tensor*)&counters})
+    check_gpu(*t, "hash arg");
+  check_dtype(tab_keys, at::kLong, "tab_keys");
+  check_dtype(q, at::kLong, "q");
+  check_dtype(slots, at::kLong, "slots");
+  check_dtype(vals, at::kFloat, "vals");
+  check_dtype(counters, at::kInt, "counters");
+  TORCH_CHECK(vals.dim() == 2 && vals.size(0) == tab_keys.numel() && vals.is_contiguous(), "vals [cap, W]");
+  TORCH_CHECK(slots.numel() >= q.numel() && counters.numel() >= 2, "hash_slots sizes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  minips_k::hash_slots(reinterpret_cast<unsigned long long*>(tab_keys.data_ptr()), tab_keys.numel(), ptr<int64_t>(q),
+                       q.numel(), ptr<int64_t>(slots), ptr<float>(vals), (int)vals.size(1), (float)init_scale,
+                       (uint64_t)seed, ptr<int>(counters), stream_of(q));
+}
+
+void hash_rehash(const at::Tensor& old_keys, const at::Tensor& old_vals, const c10::optional<at::Tensor>& old_state,
+                 at::Tensor& new_keys, at::Tensor& new_vals, const c10::optional<at::Tensor>& new_state,
+                 at::Tensor& counters) {
+  check_dtype(old_keys, at::kLong, "old_keys");
+  check_dtype(new_keys, at::kLong, "new_keys");
+  TORCH_CHECK(old_vals.size(0) == old_keys.numel() && new_vals.size(0) == new_keys.numel() &&
+                  old_vals.size(1) == new_vals.size(1),
+              "rehash shapes");
+  TORCH_CHECK(old_state.has_value() == new_state.has_value(), "state on both sides or neither");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(old_keys.device());
+  minips_k::hash_rehash(reinterpret_cast<const unsigned long long*>(old_keys.data_ptr()), ptr<float>(old_vals),
+                        old_state.has_value() ? ptr<float>(*old_state) : nullptr, old_keys.numel(),
+                        reinterpret_cast<unsigned long long*>(new_keys.data_ptr()), ptr<float>(new_vals),
+                        new_state.has_value() ? ptr<float>(*new_state) : nullptr, new_keys.numel(),
+                        (int)new_vals.size(1), ptr<int>(counters), stream_of(old_keys));
+}
+
 void embed_fwd(const at::Tensor& wte, const at::Tensor& wpe, const at::Tensor& tok, int64_t T, at::Tensor& out) {
   for (const at::Tensor* t : {&wte, &wpe, &tok, (const at::Tensor*)&out}) check_gpu(*t, "embed arg");
   check_dtype(wte, at::kBFloat16, "wte");
@@ -579,6 +614,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("scatter_add_rows", &scatter_add_rows);
   m.def("lookup_rows", &lookup_rows);
   m.def("embed_fwd", &embed_fwd);
+  m.def("hash_slots", &hash_slots);
+  m.def("hash_rehash", &hash_rehash);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("embed_bwd", &embed_bwd);

@@ -127,6 +127,13 @@ void causal_softmax_bwd(const bf16_t* P, const float* dP, int64_t rows, int T, f
                         hipStream_t s);
 void gelu_bwd(const bf16_t* dh, const bf16_t* u, int64_t n, bf16_t* du, hipStream_t s);
 void add_bf16(const bf16_t* a, const bf16_t* b, int64_t n, bf16_t* out, hipStream_t s);
+// GPU hash-table shard (hashtable.hip): tab_keys EMPTY = ~0; counters[0] += inserts,
+// counters[1] += failed lookups (table full); slot -1 for those.
+void hash_slots(unsigned long long* tab_keys, int64_t cap, const int64_t* q, int64_t n, int64_t* slots, float* vals,
+                int W, float init_scale, uint64_t seed, int* counters, hipStream_t s);
+void hash_rehash(const unsigned long long* old_keys, const float* old_vals, const float* old_state, int64_t old_cap,
+                 unsigned long long* new_keys, float* new_vals, float* new_state, int64_t new_cap, int W, int* counters,
+                 hipStream_t s);
 // Fused causal attention, head dim 64 (attention.hip). qkv [B*T][ldq] holds Q|K|V (each dmodel
 // = H*64 columns); O/dO/dqkv row-major with head h at column h*64; lse/delta [B*H*T] fp32.
 void attn_fwd(const bf16_t* qkv, int ldq, int B, int T, int H, int dmodel, float scale, bf16_t* O, int ldo, float* lse,

@@ -484,6 +484,69 @@ def attn_bwd(qkv, O, dO, lse, delta, B, T, H, scale, dqkv):
     return dqkv
 
 
+_U64 = (1 << 64) - 1
+
+
+def _mix64_int(x: int) -> int:
+    x ^= x >> 33
+    x = (x * 0xFF51AFD7ED558CCD) & _U64
+    x ^= x >> 33
+    x = (x * 0xC4CEB9FE1A85EC53) & _U64
+    x ^= x >> 33
+    return x
+
+
+def hash_slots(tab_keys, q, slots, vals, init_scale, seed, counters):
+    """Lookup-or-insert of q in the open-addressing table (EMPTY = -1), linear probing from
+    mix64(key); new rows are zero or uniform[-a, a) from mix64(key*golden + seed + c)."""
+    if _gpu(q):
+        kernels().hash_slots(tab_keys, q, slots, vals, float(init_scale), int(seed), counters)
+        return slots
+    cap = tab_keys.numel()
+    W = vals.shape[1]
+    tk = tab_keys.tolist()
+    out = []
+    for k in q.tolist():
+        s = _mix64_int(k & _U64) & (cap - 1)
+        found = -1
+        for _ in range(cap):
+            if tk[s] == k:
+                found = s
+                break
+            if tk[s] == -1:
+                tk[s] = k
+                tab_keys[s] = k
+                if init_scale != 0.0:
+                    row = []
+                    for c in range(W):
+                        h = _mix64_int(((k & _U64) * 0x9E3779B97F4A7C15 + seed + c) & _U64)
+                        row.append(init_scale * (2.0 * float(h >> 40) / 16777216.0 - 1.0))
+                    vals[s] = torch.tensor(row, dtype=vals.dtype)
+                else:
+                    vals[s] = 0
+                counters[0] += 1
+                found = s
+                break
+            s = (s + 1) & (cap - 1)
+        if found < 0:
+            counters[1] += 1
+        out.append(found)
+    slots[: len(out)] = torch.tensor(out, dtype=torch.int64)
+    return slots
+
+
+def hash_rehash(old_keys, old_vals, old_state, new_keys, new_vals, new_state, counters):
+    if _gpu(old_keys):
+        kernels().hash_rehash(old_keys, old_vals, old_state, new_keys, new_vals, new_state, counters)
+        return
+    occ = (old_keys != -1).nonzero().reshape(-1)
+    slots = torch.empty(occ.numel(), dtype=torch.int64)
+    hash_slots(new_keys, old_keys[occ], slots, new_vals, 0.0, 0, counters)
+    new_vals[slots] = old_vals[occ]
+    if old_state is not None:
+        new_state[slots] = old_state[occ]
+
+
 def embed_fwd(wte, wpe, tok, T, out):
     """out[m, :C] = wte[tok[m]] + wpe[m % T] (bf16)."""
     if _gpu(wte):

@@ -115,7 +115,7 @@ class Checkpointer:
                     arrays = [(n, h.data_ptr(), _DT[h.dtype], h.shape[0] if h.dim() else 1,
                                h.shape[1] if h.dim() > 1 else 1) for n, h in host.items()]
                     n_vals = sum(h.numel() for h in host.values()) // max(1, len(host))
-                    text = _prefix_path(out, base) if n_vals <= self.text_limit else ""
+                    text = _prefix_path(out, base) if n_vals <= self.text_limit and meta["kind"] != "hash" else ""
                     self._writer.submit(_prefix_path(out, base + ".bin"), meta, arrays, text)
                     self._write_progress(out, tid, clk)
                 self._write_worker_config(out, iteration)
@@ -206,7 +206,7 @@ class Checkpointer:
                     raise ValueError(f"{path}: table shape {meta['global_rows']}x{meta['cols']} does not match "
                                      f"{my_meta['global_rows']}x{my_meta['cols']}")
                 lo, hi = meta["base"], meta["base"] + meta["rows"]
-                if hi <= my_meta["base"] or lo >= my_meta["base"] + my_meta["rows"]:
+                if meta["kind"] != "hash" and (hi <= my_meta["base"] or lo >= my_meta["base"] + my_meta["rows"]):
                     if meta["rank"] == self.my_id:
                         clock = meta["clock"]
                     continue

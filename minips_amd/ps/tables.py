@@ -277,9 +277,21 @@ class SparseTable:
         self._pending: list = []
 
     # -- KV API -----------------------------------------------------------------------------
+    def _route_keys(self, keys: torch.Tensor) -> torch.Tensor:
+        """Keys as exchanged between ranks (identity for range-partitioned tables)."""
+        return keys
+
+    def _serve_index(self, plan: SparsePlan):
+        """(row table, row index tensor, base) for the rows this rank serves in ``plan``."""
+        return self.shard, plan.recv_keys, self.base
+
+    def _owner_rows(self, keys: torch.Tensor):
+        """(row index tensor, base) of owned unique keys being updated."""
+        return keys, self.base
+
     def plan(self, keys: torch.Tensor) -> SparsePlan:
         F = keys.shape[1] if keys.dim() == 2 else 1
-        keys = keys.reshape(-1).to(torch.int64)
+        keys = self._route_keys(keys.reshape(-1).to(torch.int64))
         uniq, inv, counts = ops.unique_bucketize(keys, self.bounds, F)
         send, recv = self.comm.exchange_counts(counts)
         U = int(sum(send))
@@ -288,7 +300,7 @@ class SparseTable:
         self.comm.all_to_all_v(recv_keys, uniq, recv, send, p2p=self.p2p)
         p = SparsePlan(keys.numel(), inv, uniq, U, send, recv, recv_keys)
         if self.comm.world > 1 and M > 0:
-            own_bounds = torch.tensor([0, 1 << 62], dtype=torch.int64, device=keys.device)
+            own_bounds = torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=keys.device)
             ou, oi, oc = ops.unique_bucketize(recv_keys, own_bounds)
             p.own_uniq, p.own_inv = ou, oi
             p.own_U = M if oc.numel() == 0 else int(oc.sum().item())
@@ -302,7 +314,8 @@ class SparseTable:
             plan = self.plan(keys)
         dev = self.comm.device
         served = torch.empty(len(plan.recv_keys), self.width, dtype=self.pull_dtype, device=dev)
-        ops.gather_rows(self.shard, plan.recv_keys, self.base, served)
+        table, index, base = self._serve_index(plan)
+        ops.gather_rows(table, index, base, served)
         rows = torch.empty(plan.U, self.width, dtype=self.pull_dtype, device=dev)
         self.comm.all_to_all_v(rows, served, plan.send, plan.recv, p2p=self.p2p)
         return rows, plan
@@ -348,15 +361,18 @@ class SparseTable:
             g = torch.zeros(plan.own_U, self.width, dtype=torch.float32, device=dev)
             ops.scatter_add_rows(recv, plan.own_inv, g)
             keys, n = plan.own_uniq, plan.own_U
-        keys = keys[:n]
+        keys, base = self._owner_rows(keys[:n])
         g = g[:n]
+        self._apply_rows(keys, base, g)
+
+    def _apply_rows(self, keys, base, g):
         if self.optimizer == "rowwise_adagrad":
-            ops.sparse_rowwise_adagrad(self.shard, self.state, keys, self.base, g, self.lr, self.eps,
+            ops.sparse_rowwise_adagrad(self.shard, self.state, keys, base, g, self.lr, self.eps,
                                        state2=self.state2, split=self.split)
         elif self.optimizer == "sgd":
-            ops.sparse_sgd(self.shard, keys, self.base, g.contiguous(), -self.lr)
+            ops.sparse_sgd(self.shard, keys, base, g.contiguous(), -self.lr)
         elif self.optimizer == "add":
-            ops.sparse_sgd(self.shard, keys, self.base, g.contiguous(), 1.0)
+            ops.sparse_sgd(self.shard, keys, base, g.contiguous(), 1.0)
         else:
             raise ValueError(self.optimizer)
 
@@ -386,4 +402,122 @@ class SparseTable:
                 d = dst.get(name)
                 if d is not None:
                     d[a - lo: b - lo].copy_(t[a - meta["base"]: b - meta["base"]].reshape(d[a - lo: b - lo].shape))
+        self.pipe.clock = int(clock)
+
+
+# ------------------------------------------------------------------------------------------------
+MASK63 = (1 << 63) - 1
+_M1, _M2 = 0x5BD1E9955BD1E995 & MASK63 | 1, 0x1B873593C2B2AE35 & MASK63 | 1
+
+
+def mix63(k: torch.Tensor) -> torch.Tensor:
+    """Bijection of [0, 2^63): xor-shifts and odd multiplies mod 2^63 (int64 arithmetic wraps mod
+    2^64; the mask keeps 63 bits). Spreads arbitrary user keys evenly over the rank ranges."""
+    x = k & MASK63
+    x = x ^ (x >> 31)
+    x = (x * _M1) & MASK63
+    x = x ^ (x >> 29)
+    x = (x * _M2) & MASK63
+    x = x ^ (x >> 32)
+    return x
+
+
+class HashSparseTable(SparseTable):
+    """Unbounded key space (reference MapStorage, server/map_storage.hpp): keys in [0, 2^63) are
+    mixed by a bijection and range-partitioned over the ranks; each rank stores its keys in a GPU
+    open-addressing hash table (csrc/kernels/hashtable.hip) whose rows are created on first
+    touch -- zero (MapStorage's default-insert) or a deterministic per-key uniform init -- and
+    grows (rehash, doubling) past 70% load. The Get/Add/Clock protocol is SparseTable's."""
+
+    def __init__(self, comm: Comm, width: int, capacity: int = 1 << 16, optimizer: str = "add", lr: float = 0.01,
+                 eps: float = 1e-8, pull_dtype=torch.float32, consistency: str = "bsp", staleness: int = 0,
+                 table_id: int = 0, init_std: float = 0.0, seed: int = 1234, p2p: bool | None = None):
+        self.comm = comm
+        self.table_id = table_id
+        self.num_rows = MASK63
+        self.width = width
+        self.optimizer, self.lr, self.eps = optimizer, lr, eps
+        self.pull_dtype = pull_dtype
+        self.split = None
+        dev = comm.device
+        b = even_bounds(MASK63, comm.world)
+        self.bounds_list = b
+        self.bounds = torch.tensor(b, dtype=torch.int64, device=dev)
+        self.base = b[comm.rank]
+        self.rows_local = 0
+        self.init_scale = float(init_std) * math.sqrt(3.0)
+        self.seed = int(seed)
+        cap = 1 << max(4, int(capacity - 1).bit_length())
+        self._alloc(cap)
+        self.counters = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.pipe = _Pipeline(comm, consistency, staleness)
+        self.p2p = (consistency != "bsp") if p2p is None else p2p
+        self._pending: list = []
+
+    def _alloc(self, cap: int):
+        dev = self.comm.device
+        self.capacity = cap
+        self.tab_keys = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+        self.shard = torch.zeros(cap, self.width, dtype=torch.float32, device=dev)
+        self.state = torch.zeros(cap, dtype=torch.float32, device=dev) if self.optimizer == "rowwise_adagrad" \
+            else None
+        self.state2 = None
+
+    def _route_keys(self, keys):
+        if bool((keys < 0).any()):
+            raise ValueError("HashSparseTable keys must be in [0, 2^63)")
+        return mix63(keys)
+
+    def size(self) -> int:
+        return int(self.counters[0].item())
+
+    def _slots(self, keys: torch.Tensor) -> torch.Tensor:
+        need = keys.numel()
+        if need == 0:
+            return torch.empty(0, dtype=torch.int64, device=keys.device)
+        if (self.size() + need) > 0.7 * self.capacity:
+            self._grow(max(self.capacity * 2, 1 << int(math.ceil(math.log2((self.size() + need) / 0.5)))))
+        slots = torch.empty(need, dtype=torch.int64, device=keys.device)
+        ops.hash_slots(self.tab_keys, keys, slots, self.shard, self.init_scale, self.seed, self.counters)
+        if int(self.counters[1].item()):
+            raise RuntimeError("hash table full")
+        return slots
+
+    def _grow(self, new_cap: int):
+        old = (self.tab_keys, self.shard, self.state)
+        self._alloc(new_cap)
+        cnt = torch.zeros(2, dtype=torch.int32, device=self.comm.device)
+        ops.hash_rehash(old[0], old[1], old[2], self.tab_keys, self.shard, self.state, cnt)
+        self.counters[0] = cnt[0]
+
+    def _serve_index(self, plan):
+        slots = self._slots(plan.recv_keys)  # insert-on-miss: unseen keys get their initial row
+        plan.extra["served_slots"] = slots
+        return self.shard, slots, 0
+
+    def _owner_rows(self, keys):
+        return self._slots(keys), 0
+
+    # -- checkpoint hooks: (key, row, state) triples of the occupied slots --------------------
+    def shard_state(self):
+        occ = self.tab_keys >= 0
+        arrays = {"keys": self.tab_keys[occ].view(-1, 1), "params": self.shard[occ]}
+        if self.state is not None:
+            arrays["state"] = self.state[occ].view(-1, 1)
+        n = int(occ.sum())
+        meta = dict(global_rows=MASK63, base=0, rows=n, cols=self.width, clock=self.pipe.clock,
+                    table_id=self.table_id, rank=self.comm.rank, world=self.comm.world, kind="hash")
+        return meta, arrays
+
+    def load_shard_pieces(self, pieces, clock: int):
+        lo, hi = self.bounds_list[self.comm.rank], self.bounds_list[self.comm.rank + 1]
+        for meta, arrays in pieces:
+            keys = arrays["keys"].reshape(-1).to(self.comm.device)
+            mine = (keys >= lo) & (keys < hi)
+            if not bool(mine.any()):
+                continue
+            slots = self._slots(keys[mine])
+            self.shard[slots] = arrays["params"].to(self.comm.device)[mine]
+            if self.state is not None and "state" in arrays:
+                self.state[slots] = arrays["state"].reshape(-1).to(self.comm.device)[mine]
         self.pipe.clock = int(clock)
