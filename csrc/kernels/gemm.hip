@@ -112,6 +112,68 @@ struct EpiArgs {
   int64_t sa_o, sa_i, sb_o, sb_i, sc_o, sc_i;
 };
 
+// Fused epilogue of one wave's 64x64 accumulator block (rows m0 + 64*wm.., cols n0 + 64*wn..).
+template <int EPI>
+__device__ __forceinline__ void epilogue(const v4f (&acc)[4][4], const EpiArgs& ep, int M, int N, int m0, int n0,
+                                         int wm, int wn, int lane) {
+  const int col_l = lane & 15, row_q = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + col_l;
+    const bool col_ok = col < N;
+    float bias = 0.f;
+    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
+    float csum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + row_q + r;
+        if (!(col_ok && row < M)) continue;
+        float v = acc[i][j][r] * ep.alpha;
+        const int64_t off = (int64_t)row * ep.ldc + col;
+        if (EPI == kEpiStoreF32) {
+          ((float*)ep.C)[off] = v;
+        } else if (EPI == kEpiAtomicF32) {
+          atomicAdd(((float*)ep.C) + off, v);
+        } else if (EPI == kEpiBiasReluBf16) {
+          ((bf16_t*)ep.C)[off] = f2bf(fmaxf(v + bias, 0.f));
+        } else if (EPI == kEpiBiasBf16) {
+          ((bf16_t*)ep.C)[off] = f2bf(v + bias);
+        } else if (EPI == kEpiBiasGeluBf16) {
+          float x = v + bias;
+          float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
+          ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
+        } else if (EPI == kEpiStoreBf16) {
+          ((bf16_t*)ep.C)[off] = f2bf(v);
+        } else if (EPI == kEpiBiasGeluAuxBf16) {
+          const float x = v + bias;
+          const float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
+          ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
+          const_cast<bf16_t*>(ep.mask)[(int64_t)row * ep.ldmask + col] = f2bf(x);
+        } else if (EPI == kEpiGeluGradBf16) {
+          const float u = bf2f(ep.mask[(int64_t)row * ep.ldmask + col]);
+          const float k = 0.7978845608f, c3 = 0.044715f;
+          const float t = tanhf(k * (u + c3 * u * u * u));
+          const float gp = 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k * (1.f + 3.f * c3 * u * u);
+          ((bf16_t*)ep.C)[off] = f2bf(v * gp);
+        } else if (EPI == kEpiReluMaskBf16) {
+          float m = bf2f(ep.mask[(int64_t)row * ep.ldmask + col]);
+          float o = m > 0.f ? v : 0.f;
+          bf16_t ob = f2bf(o);
+          ((bf16_t*)ep.C)[off] = ob;
+          csum += bf2f(ob);
+        }
+      }
+    }
+    if (EPI == kEpiReluMaskBf16 && ep.colsum) {
+      csum += __shfl_xor(csum, 16, 64);
+      csum += __shfl_xor(csum, 32, 64);
+      if (lane < 16 && col_ok) atomicAdd(ep.colsum + col, csum);
+    }
+  }
+}
+
 template <int BK, bool A_KM, bool B_KN, int EPI>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         int M, int N, int K, int lda, int ldb, int k_chunk,
@@ -192,69 +254,174 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
     cur ^= 1;
   }
 
-  // ---------------------------------------------------------------- epilogue
-  const int col_l = lane & 15, row_q = (lane >> 4) * 4;
+  epilogue<EPI>(acc, ep, M, N, m0, n0, wm, wn, lane);
+}
+
+
+// ================================================================ v2: LDS-DMA staging
+// Same 128x128 tile / 2x2 waves / fragment math as above, but operands go global -> LDS with
+// buffer_load_dwordx4 ... lds (no register staging, no VGPRs for the tile in flight), BK = 64
+// always, 2 LDS stages (64 KiB -> 2 workgroups per CU). Lane-linear LDS images (a DMA wave
+// instruction writes 1 KiB contiguously) are made bank-conflict-free by XOR-swizzling the
+// 16-byte chunk index on the SOURCE address side:
+//   [row][64 k] images (MK / NK operands, ds_read_b128): chunk' = chunk ^ ((row >> 1) & 7)
+//     -> the 16 rows of a 16-lane read group cover all 64 banks
+//   [k][128 m] images (KM / KN operands, ds_read_b64_tr_b16): chunk' = chunk ^ swz(k),
+//     swz(k) = 2 * ((k & 3) | (((k >> 2) ^ (k >> 3)) & 1) << 2)
+//     -> the 8 k-rows read by a 32-lane half land on 8 distinct 32-byte bank groups, for both
+//        the plain and the permuted (wgrad) k order
+// Out-of-range chunks (M/N/K tails) get an offset past the buffer's num_records, so the DMA
+// writes zeros. One barrier after the stage's DMA retires (counted vmcnt, raw s_barrier: the
+// next stage stays in flight), one before its buffer is refilled.
+constexpr int BK2 = 64;
+constexpr uint32_t kOobOffset = 0x80000000u;
+
+__device__ __forceinline__ int swz_k(int k) { return 2 * ((k & 3) | ((((k >> 2) ^ (k >> 3)) & 1) << 2)); }
+
+template <bool KMAJOR>
+__device__ __forceinline__ void dma_tile(__amdgpu_buffer_rsrc_t rsrc, int ld, int row0, int k0, int rows, int kend,
+                                         bf16_t* S, int wave, int lane) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + col_l;
-    const bool col_ok = col < N;
-    float bias = 0.f;
-    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
-    float csum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + row_q + r;
-        if (!(col_ok && row < M)) continue;
-        float v = acc[i][j][r] * ep.alpha;
-        const int64_t off = (int64_t)row * ep.ldc + col;
-        if (EPI == kEpiStoreF32) {
-          ((float*)ep.C)[off] = v;
-        } else if (EPI == kEpiAtomicF32) {
-          atomicAdd(((float*)ep.C) + off, v);
-        } else if (EPI == kEpiBiasReluBf16) {
-          ((bf16_t*)ep.C)[off] = f2bf(fmaxf(v + bias, 0.f));
-        } else if (EPI == kEpiBiasBf16) {
-          ((bf16_t*)ep.C)[off] = f2bf(v + bias);
-        } else if (EPI == kEpiBiasGeluBf16) {
-          float x = v + bias;
-          float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
-          ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
-        } else if (EPI == kEpiStoreBf16) {
-          ((bf16_t*)ep.C)[off] = f2bf(v);
-        } else if (EPI == kEpiBiasGeluAuxBf16) {
-          const float x = v + bias;
-          const float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
-          ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
-          const_cast<bf16_t*>(ep.mask)[(int64_t)row * ep.ldmask + col] = f2bf(x);
-        } else if (EPI == kEpiGeluGradBf16) {
-          const float u = bf2f(ep.mask[(int64_t)row * ep.ldmask + col]);
-          const float k = 0.7978845608f, c3 = 0.044715f;
-          const float t = tanhf(k * (u + c3 * u * u * u));
-          const float gp = 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k * (1.f + 3.f * c3 * u * u);
-          ((bf16_t*)ep.C)[off] = f2bf(v * gp);
-        } else if (EPI == kEpiReluMaskBf16) {
-          float m = bf2f(ep.mask[(int64_t)row * ep.ldmask + col]);
-          float o = m > 0.f ? v : 0.f;
-          bf16_t ob = f2bf(o);
-          ((bf16_t*)ep.C)[off] = ob;
-          csum += bf2f(ob);
-        }
-      }
+    uint32_t voff;
+    bf16_t* dst;
+    if (!KMAJOR) {
+      const int R = 32 * wave + 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((R >> 1) & 7);
+      const int gr = row0 + R, gk = k0 + 8 * c;
+      voff = (gr < rows && gk < kend) ? (uint32_t)(((int64_t)gr * ld + gk) * 2) : kOobOffset;
+      dst = S + (32 * wave + 8 * j) * BK2;
+    } else {
+      const int kr = 16 * wave + 4 * j + (lane >> 4);
+      const int c = (lane & 15) ^ swz_k(kr);
+      const int gk = k0 + kr, gm = row0 + 8 * c;
+      voff = (gk < kend && gm < rows) ? (uint32_t)(((int64_t)gk * ld + gm) * 2) : kOobOffset;
+      dst = S + (16 * wave + 4 * j) * BM;
     }
-    if (EPI == kEpiReluMaskBf16 && ep.colsum) {
-      csum += __shfl_xor(csum, 16, 64);
-      csum += __shfl_xor(csum, 32, 64);
-      if (lane < 16 && col_ok) atomicAdd(ep.colsum + col, csum);
-    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
   }
+}
+
+template <bool KMAJOR, bool PERM>
+__device__ __forceinline__ v8s frag2(const bf16_t* S, int row_base, int ks, int lane) {
+  const int g = lane >> 4;
+  if (!KMAJOR) {
+    const int R = row_base + (lane & 15);
+    const int c = (4 * ks + g) ^ ((R >> 1) & 7);
+    return *reinterpret_cast<const v8s*>(S + R * BK2 + 8 * c);
+  } else {
+    const int i = lane & 15, q = i >> 2, p = i & 3;
+    const int r0 = 32 * ks + (PERM ? 4 * g : 8 * g) + q;
+    const int r1 = 32 * ks + (PERM ? 16 + 4 * g : 8 * g + 4) + q;
+    const int ch = (row_base >> 3) + (p >> 1), sub = 4 * (p & 1);
+    const v4s lo = ds_read_tr16(S + r0 * BM + 8 * (ch ^ swz_k(r0)) + sub);
+    const v4s hi = ds_read_tr16(S + r1 * BM + 8 * (ch ^ swz_k(r1)) + sub);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+template <bool A_KM, bool B_KN, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_v2_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                         int M, int N, int K, int lda, int ldb, int k_chunk,
+                                                         EpiArgs ep) {
+  constexpr bool PERM = A_KM && B_KN;
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2][2][BM * BK2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if (nwg >= 16) {
+    int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    bid = base + (bid >> 3);
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  {
+    const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
+    A += zo * ep.sa_o + zi * ep.sa_i;
+    B += zo * ep.sb_o + zi * ep.sb_i;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
+    ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
+  }
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7ffffff0, 0x00020000);
+  const int kb = blockIdx.z * k_chunk;
+  const int ke = min(K, kb + k_chunk);
+  const int nt = ke > kb ? (ke - kb + BK2 - 1) / BK2 : 0;
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+    dma_tile<A_KM>(ra, lda, m0, kb, M, ke, smem[0][0], wave, lane);
+    dma_tile<B_KN>(rb, ldb, n0, kb, N, ke, smem[0][1], wave, lane);
+  }
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) {
+      const int k1 = kb + (t + 1) * BK2;
+      dma_tile<A_KM>(ra, lda, m0, k1, M, ke, smem[cur ^ 1][0], wave, lane);
+      dma_tile<B_KN>(rb, ldb, n0, k1, N, ke, smem[cur ^ 1][1], wave, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this stage retired, the next one in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bf16_t* SA = smem[cur][0];
+    const bf16_t* SB = smem[cur][1];
+#pragma unroll
+    for (int ks = 0; ks < BK2 / 32; ++ks) {
+      v8s af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag2<A_KM, PERM>(SA, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag2<B_KN, PERM>(SB, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i]),
+                                                              __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is refilled
+    asm volatile("" ::: "memory");
+  }
+  epilogue<EPI>(acc, ep, M, N, m0, n0, wm, wn, lane);
+}
+
+static int gemm_impl() {
+  static const int v = [] {
+    const char* e = std::getenv("MINIPS_GEMM_IMPL");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
 }
 
 template <bool A_KM, bool B_KN, int EPI>
 static void launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, int split_k,
                    const EpiArgs& ep, int batch, hipStream_t s) {
   int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  // v2 (LDS-DMA) needs every byte offset within one batch element below 2 GiB (32-bit voffset)
+  const int64_t a_ext = (int64_t)((A_KM ? K : M) - 1) * lda + (A_KM ? M : K);
+  const int64_t b_ext = (int64_t)((B_KN ? K : N) - 1) * ldb + (B_KN ? N : K);
+  // measured (tools/bench_gemm.py): v2 wins on forward / dgrad; the split-K wgrad (both operands
+  // tr-read) stays on the register-staged BK=32 kernel, which is faster there
+  if (gemm_impl() == 2 && !(A_KM && B_KN) && a_ext * 2 < 0x7ff00000ll && b_ext * 2 < 0x7ff00000ll) {
+    const int kper = (K + split_k - 1) / split_k;
+    const int kc = (kper + BK2 - 1) / BK2 * BK2;
+    const int nsplit = (K + kc - 1) / kc;
+    dim3 grid(tiles, batch, nsplit);
+    hipLaunchKernelGGL((gemm_v2_kernel<A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
+    return;
+  }
   // BK=64 halves the barriers per FLOP; short K chunks keep BK=32 (less tail waste).
   const int kper = (K + split_k - 1) / split_k;
   static const int forced = [] {
