@@ -103,10 +103,17 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   float* colsum_p = opt_ptr<float>(colsum, at::kFloat, "colsum");
   if (colsum_p) TORCH_CHECK(colsum->numel() >= N, "colsum too short");
   c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
+  static const bool use_slab = [] {
+    const char* e = std::getenv("MINIPS_SPLITK_SLAB");
+    return !e || std::atoi(e) != 0;
+  }();
+  at::Tensor slab;
+  if (use_slab && split_k > 1 && batch <= 1 && epi == minips_k::kEpiAtomicF32 && N % 4 == 0)
+    slab = at::empty({split_k * M * N}, A.options().dtype(at::kFloat));  // caching allocator, stream-ordered
   minips_k::gemm_bf16_batched(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb,
                               (int)ldc, a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p, (float)alpha,
                               (int)split_k, (int)batch, (int)inner, st[0], st[1], st[2], st[3], st[4], st[5],
-                              stream_of(A));
+                              stream_of(A), slab.defined() ? ptr<float>(slab) : nullptr);
 }
 
 // Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P]).
@@ -268,13 +275,18 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
   const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
   check_gpu(inv, "inv");
   check_gpu(grad_rows, "grad_rows");
-  check_dtype(dX, at::kFloat, "dX");
+  TORCH_CHECK(dX.scalar_type() == at::kFloat || dX.scalar_type() == at::kBFloat16, "dX must be fp32 or bf16");
   check_dtype(grad_rows, at::kFloat, "grad_rows");
   const int64_t B = dX.size(0);
+  TORCH_CHECK(dX.dim() == 2 && dX.stride(1) == 1, "dX must be a row-major matrix");
   TORCH_CHECK(inv.numel() == B * F && dX.size(1) >= x_off + F * D && grad_rows.size(1) >= D + (dw ? 1 : 0), "shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
-  minips_k::wd_emb_backward(ptr<float>(dX) + x_off, (int)dX.size(1), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
-                            ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
+  if (dX.scalar_type() == at::kFloat)
+    minips_k::wd_emb_backward(ptr<float>(dX) + x_off, (int)dX.stride(0), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
+                              ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
+  else
+    minips_k::wd_emb_backward_bf16(ptr<bf16_t>(dX) + x_off, (int)dX.stride(0), dw, ptr<int64_t>(inv), B, (int)F,
+                                   (int)D, ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
 }
 
 void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g, double lr, double beta1,

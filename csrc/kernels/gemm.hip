@@ -110,6 +110,7 @@ struct EpiArgs {
   // batched GEMM: z = blockIdx.y, offsets (z / inner) * s_outer + (z % inner) * s_inner
   int inner;
   int64_t sa_o, sa_i, sb_o, sb_i, sc_o, sc_i;
+  int64_t sc_split;  // split-K slab mode: C += blockIdx.z * sc_split (0 = all splits share C)
 };
 
 // Fused epilogue of one wave's 64x64 accumulator block (rows m0 + 64*wm.., cols n0 + 64*wn..).
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
     const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
-    const int64_t co = zo * ep.sc_o + zi * ep.sc_i;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
     const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void gemm_v2_kernel(const bf16_t* __restric
     const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
-    const int64_t co = zo * ep.sc_o + zi * ep.sc_i;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
     const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
@@ -406,21 +407,25 @@ static int gemm_impl() {
 }
 
 template <bool A_KM, bool B_KN, int EPI>
-static void launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, int split_k,
-                   const EpiArgs& ep, int batch, hipStream_t s) {
+static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, int split_k,
+                  const EpiArgs& ep, int batch, hipStream_t s) {
   int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   // v2 (LDS-DMA) needs every byte offset within one batch element below 2 GiB (32-bit voffset)
   const int64_t a_ext = (int64_t)((A_KM ? K : M) - 1) * lda + (A_KM ? M : K);
   const int64_t b_ext = (int64_t)((B_KN ? K : N) - 1) * ldb + (B_KN ? N : K);
   // measured (tools/bench_gemm.py): v2 wins on forward / dgrad; the split-K wgrad (both operands
   // tr-read) stays on the register-staged BK=32 kernel, which is faster there
-  if (gemm_impl() == 2 && !(A_KM && B_KN) && a_ext * 2 < 0x7ff00000ll && b_ext * 2 < 0x7ff00000ll) {
+  static const bool wgrad_v2 = [] {
+    const char* e = std::getenv("MINIPS_GEMM_WGRAD_V2");
+    return e && std::atoi(e) == 1;
+  }();
+  if (gemm_impl() == 2 && (!(A_KM && B_KN) || wgrad_v2) && a_ext * 2 < 0x7ff00000ll && b_ext * 2 < 0x7ff00000ll) {
     const int kper = (K + split_k - 1) / split_k;
     const int kc = (kper + BK2 - 1) / BK2 * BK2;
     const int nsplit = (K + kc - 1) / kc;
     dim3 grid(tiles, batch, nsplit);
     hipLaunchKernelGGL((gemm_v2_kernel<A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
-    return;
+    return nsplit;
   }
   // BK=64 halves the barriers per FLOP; short K chunks keep BK=32 (less tail waste).
   const int kper = (K + split_k - 1) / split_k;
@@ -438,32 +443,79 @@ static void launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int ld
     hipLaunchKernelGGL((gemm_bf16_kernel<64, A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
   else
     hipLaunchKernelGGL((gemm_bf16_kernel<32, A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
+  return nsplit;
 }
 
 #define MINIPS_GEMM_EPI_DISPATCH(AKM, BKN)                                                        \
   switch (epi) {                                                                                 \
-    case kEpiStoreF32: launch<AKM, BKN, kEpiStoreF32>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break;  \
-    case kEpiAtomicF32: launch<AKM, BKN, kEpiAtomicF32>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiBiasReluBf16: launch<AKM, BKN, kEpiBiasReluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiBiasBf16: launch<AKM, BKN, kEpiBiasBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiBiasGeluBf16: launch<AKM, BKN, kEpiBiasGeluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiStoreBf16: launch<AKM, BKN, kEpiStoreBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiReluMaskBf16: launch<AKM, BKN, kEpiReluMaskBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiBiasGeluAuxBf16: launch<AKM, BKN, kEpiBiasGeluAuxBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiGeluGradBf16: launch<AKM, BKN, kEpiGeluGradBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiStoreF32: nsplit = launch<AKM, BKN, kEpiStoreF32>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break;  \
+    case kEpiAtomicF32: nsplit = launch<AKM, BKN, kEpiAtomicF32>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiBiasReluBf16: nsplit = launch<AKM, BKN, kEpiBiasReluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiBiasBf16: nsplit = launch<AKM, BKN, kEpiBiasBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiBiasGeluBf16: nsplit = launch<AKM, BKN, kEpiBiasGeluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiStoreBf16: nsplit = launch<AKM, BKN, kEpiStoreBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiReluMaskBf16: nsplit = launch<AKM, BKN, kEpiReluMaskBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiBiasGeluAuxBf16: nsplit = launch<AKM, BKN, kEpiBiasGeluAuxBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
+    case kEpiGeluGradBf16: nsplit = launch<AKM, BKN, kEpiGeluGradBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
     default: throw std::runtime_error("gemm: unknown epilogue " + std::to_string(epi));           \
   }
+
+// out[r][c] (ldc) += sum_s slab[s][r][c]   (slab [nsplit][M][N] fp32, float4 over columns)
+__global__ void splitk_reduce_kernel(const float* __restrict__ slab, int nsplit, int M, int N, float* __restrict__ out,
+                                     int ldc) {
+  const int n4 = N >> 2;
+  const int64_t total = (int64_t)M * n4, plane = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / n4;
+    const int c = (int)(i - r * n4) * 4;
+    float4 a = *reinterpret_cast<const float4*>(slab + r * N + c);
+    for (int z = 1; z < nsplit; ++z) {
+      const float4 b = *reinterpret_cast<const float4*>(slab + z * plane + r * N + c);
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    float* o = out + r * ldc + c;
+    o[0] += a.x;
+    o[1] += a.y;
+    o[2] += a.z;
+    o[3] += a.w;
+  }
+}
 
 void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                        bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
                        float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
-                       int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s) {
+                       int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s, float* slab) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return;
   if (split_k < 1) split_k = 1;
   if (split_k > 1 && epi != kEpiAtomicF32) throw std::runtime_error("gemm: split_k needs the atomic epilogue");
   if (batch > 1 && (mask || colsum)) throw std::runtime_error("gemm: batched mode has no mask/colsum epilogue");
   if (inner < 1) inner = 1;
-  EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i};
+  int nsplit = 1;
+  if (slab && split_k > 1 && batch == 1 && N % 4 == 0) {
+    // split-K without atomics: every K slice stores its partial tile into its own slab plane,
+    // one streaming kernel adds the planes into C (measured faster than fp32 atomics)
+    EpiArgs sp{slab, N, nullptr, nullptr, 0, nullptr, alpha, 1, 0, 0, 0, 0, 0, 0, (int64_t)M * N};
+    EpiArgs& ep = sp;
+    epi = kEpiStoreF32;
+    if (!a_km && !b_kn) {
+      MINIPS_GEMM_EPI_DISPATCH(false, false)
+    } else if (!a_km && b_kn) {
+      MINIPS_GEMM_EPI_DISPATCH(false, true)
+    } else if (a_km && b_kn) {
+      MINIPS_GEMM_EPI_DISPATCH(true, true)
+    } else {
+      MINIPS_GEMM_EPI_DISPATCH(true, false)
+    }
+    MINIPS_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(splitk_reduce_kernel, grid_for((int64_t)M * (N / 4), 256, 4096), 256, 0, s, slab, nsplit, M, N,
+                       (float*)C, ldc);
+    MINIPS_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i, 0};
   if (!a_km && !b_kn) {
     MINIPS_GEMM_EPI_DISPATCH(false, false)
   } else if (!a_km && b_kn) {
@@ -480,7 +532,7 @@ void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, i
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
                float alpha, int split_k, hipStream_t s) {
   gemm_bf16_batched(A, B, C, M, N, K, lda, ldb, ldc, a_km, b_kn, epi, bias, mask, ldmask, colsum, alpha, split_k, 1,
-                    1, 0, 0, 0, 0, 0, 0, s);
+                    1, 0, 0, 0, 0, 0, 0, s, nullptr);
 }
 
 }  // namespace minips_k

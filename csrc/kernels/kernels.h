@@ -29,7 +29,8 @@ void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, i
 void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                        bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
                        float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
-                       int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s);
+                       int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s,
+                       float* slab = nullptr);  // split-K workspace [split_k][M][N] (atomic epilogue only)
 
 // ------------------------------------------------------------------ sparse keys (sparse.hip)
 // Hash-based dedupe + owner bucketing of int64 keys in 3 launches (no sort):
@@ -90,6 +91,8 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
 // pre-zeroed).
 void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                      float* grad_rows, int row_stride, hipStream_t s);
+void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
+                          float* grad_rows, int row_stride, hipStream_t s);
 
 // ------------------------------------------------------------------ optimizers (optim.hip)
 // Fused Adam(W) on an fp32 master shard; optionally writes the bf16 copy for all-gather.

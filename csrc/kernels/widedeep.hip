@@ -190,7 +190,11 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
 constexpr int kEmbTB = 256;
 constexpr int kEmbHash = 512;
 
-__global__ __launch_bounds__(kEmbTB) void wd_emb_backward_kernel(const float* __restrict__ dX, int ldx,
+__device__ __forceinline__ float ld_grad(const float* p) { return *p; }
+__device__ __forceinline__ float ld_grad(const bf16_t* p) { return bf2f(*p); }
+
+template <typename TX>
+__global__ __launch_bounds__(kEmbTB) void wd_emb_backward_kernel(const TX* __restrict__ dX, int ldx,
                                                                  const float* __restrict__ dwide,
                                                                  const int64_t* __restrict__ inv, int64_t B, int F,
                                                                  int D, float* __restrict__ grad_rows,
@@ -240,7 +244,7 @@ __global__ __launch_bounds__(kEmbTB) void wd_emb_backward_kernel(const float* __
   // deep part: element e = (lookup k, column d)
   for (int e = t; e < nb * D; e += kEmbTB) {
     const int k = e / D, d = e - k * D;
-    atomicAdd(acc + cidx[k] * W + d, dX[(b0 + k) * ldx + (int64_t)f * D + d]);
+    atomicAdd(acc + cidx[k] * W + d, ld_grad(dX + (b0 + k) * ldx + (int64_t)f * D + d));
   }
   if (dwide && t < nb) atomicAdd(acc + cidx[t] * W + D, dwide[b0 + t]);
   __syncthreads();
@@ -250,16 +254,26 @@ __global__ __launch_bounds__(kEmbTB) void wd_emb_backward_kernel(const float* __
   }
 }
 
-void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
-                     float* grad_rows, int row_stride, hipStream_t s) {
+template <typename TX>
+static void emb_backward(const TX* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
+                         float* grad_rows, int row_stride, hipStream_t s) {
   if (B <= 0) return;
   if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("wd_emb_backward: row_stride too small");
   const size_t lds = (size_t)kEmbTB * (D + 1) * sizeof(float);
   if (lds > 96 * 1024) throw std::runtime_error("wd_emb_backward: D too large");
   dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);
-  hipLaunchKernelGGL(wd_emb_backward_kernel, grid, dim3(kEmbTB), lds, s, dX, ldx, dwide, inv, B, F, D, grad_rows,
+  hipLaunchKernelGGL(wd_emb_backward_kernel<TX>, grid, dim3(kEmbTB), lds, s, dX, ldx, dwide, inv, B, F, D, grad_rows,
                      row_stride);
   MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
+                     float* grad_rows, int row_stride, hipStream_t s) {
+  emb_backward(dX, ldx, dwide, inv, B, F, D, grad_rows, row_stride, s);
+}
+void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
+                          float* grad_rows, int row_stride, hipStream_t s) {
+  emb_backward(dX, ldx, dwide, inv, B, F, D, grad_rows, row_stride, s);
 }
 
 }  // namespace minips_k

@@ -119,7 +119,7 @@ class WideDeep:
                 X=ext(self.k_in[0], self.k_in[0]), H1=ext(h1, h1), H2=ext(h2, h2),
                 H3=torch.empty(B, h3, **bf), dH3=torch.empty(B, h3, **bf), dH2=torch.empty(B, h2, **bf),
                 dH1=torch.empty(B, h1, **bf),
-                dX=torch.empty(B, cfg.F * cfg.emb_dim, dtype=torch.float32, device=dev),
+                dX=torch.empty(B, cfg.F * cfg.emb_dim, **bf),  # bf16: half the bytes of the emb backward
                 wide=torch.empty(B, dtype=torch.float32, device=dev),
                 dwide=torch.empty(B, dtype=torch.float32, device=dev),
                 loss=torch.zeros(1, dtype=torch.float32, device=dev),
@@ -166,7 +166,7 @@ class WideDeep:
         ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
-        ops.linear_dgrad(b["dH1"], self.view(P, "W1"), out_f32=True, n_cols=F * D, out=b["dX"])
+        ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
         grad_rows = torch.zeros(max(plan.U, 1), cfg.row_width, dtype=torch.float32, device=self.comm.device)
         ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows)
         self.emb.add(plan, grad_rows)

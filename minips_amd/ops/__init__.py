@@ -117,13 +117,18 @@ def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=
     return gemm(dy, w, out, M, K, N, False, True, epi, mask=mask, colsum=colsum)
 
 
+_WGRAD_BLOCKS = int(__import__("os").environ.get("MINIPS_WGRAD_BLOCKS", "512"))
+
+
 def linear_wgrad(dy, x, dw, split_k=None):
     """dw[N,K] += dy^T x (dy [M,N], x [M,K]); fp32 accumulate."""
     M, N = dy.shape
     K = x.shape[1]
     if split_k is None:
         tiles = ((N + 127) // 128) * ((K + 127) // 128)
-        split_k = max(1, min(M // 256, (512 + tiles - 1) // tiles))
+        # ~512 blocks, but >= 640 reduction rows per split (tools/bench_gemm.py sweep: shorter
+        # slices lose to their fixed prologue/epilogue cost; the slab reduce makes splits cheap)
+        split_k = max(1, min(M // 640, (_WGRAD_BLOCKS + tiles - 1) // tiles))
     return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
 
 
@@ -268,7 +273,7 @@ def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0):
         kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off))
         return grad_rows
     B = dX.shape[0]
-    g = dX[:, x_off: x_off + F * D].reshape(B * F, D)
+    g = dX[:, x_off: x_off + F * D].float().reshape(B * F, D)
     grad_rows[:, :D].index_add_(0, inv, g)
     if dwide is not None:
         grad_rows[:, D].index_add_(0, inv, dwide.repeat_interleave(F))

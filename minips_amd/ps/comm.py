@@ -40,6 +40,20 @@ class Comm:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
         self.device = device
         self.stats = CommStats()
+        self._bg: Comm | None = None
+
+    def background(self) -> "Comm":
+        """A second communicator over the same ranks for collectives issued on a side HIP stream
+        (SSP/ASP clock work): RCCL kernels of ONE communicator running concurrently from two
+        streams may wait on each other, two communicators progress independently. Creating it
+        is collective (first call on every rank, in the same order)."""
+        if self.world == 1:
+            return self
+        if self._bg is None:
+            ranks = list(range(self.world)) if self.group is None else dist.get_process_group_ranks(self.group)
+            self._bg = Comm(group=dist.new_group(ranks), device=self.device)
+            self._bg.stats = self.stats  # one byte account per rank
+        return self._bg
 
     # -- helpers ------------------------------------------------------------------------
     def all_to_all_v(self, out: torch.Tensor, inp: torch.Tensor, recv_splits: list[int], send_splits: list[int],

@@ -118,6 +118,8 @@ class DenseTable:
         self.grad_shard = torch.zeros(self.shard, dtype=torch.float32, device=dev)
         self.step = 0
         self.pipe = _Pipeline(comm, consistency, staleness)
+        if self.pipe.async_:
+            comm.background()  # collective: create the side-stream communicator up front
         self._pending = False
         # SSP/ASP: a ring of staleness+1 gradient buffers, so the side stream reduces clock t's
         # gradients while the compute stream already writes clock t+1's.
@@ -157,11 +159,13 @@ class DenseTable:
         pending = self._pending
         self._pending = False
 
+        comm = self.comm.background() if self.pipe.async_ else self.comm
+
         def work():
             if pending:
-                self.comm.reduce_scatter(self.grad_shard, grad)
+                comm.reduce_scatter(self.grad_shard, grad)
                 self._apply(self.grad_shard, step)
-                self.comm.all_gather(self.params, self.params[self.base: self.base + self.shard])
+                comm.all_gather(self.params, self.params[self.base: self.base + self.shard])
             grad.zero_()
 
         self.pipe.run(work)
@@ -272,6 +276,8 @@ class SparseTable:
             if optimizer == "rowwise_adagrad" else None
         self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
         self.pipe = _Pipeline(comm, consistency, staleness)
+        if self.pipe.async_:
+            comm.background()  # collective: create the side-stream communicator up front
         # SSP/ASP move rows with point-to-point send/recv by default, BSP with all-to-all-v
         self.p2p = (consistency != "bsp") if p2p is None else p2p
         self._pending: list = []
@@ -355,7 +361,8 @@ class SparseTable:
         else:
             M = len(plan.recv_keys)
             recv = torch.empty(M, self.width, dtype=torch.float32, device=dev)
-            self.comm.all_to_all_v(recv, grad_rows, plan.recv, plan.send, p2p=self.p2p)
+            comm = self.comm.background() if self.pipe.async_ else self.comm
+            comm.all_to_all_v(recv, grad_rows, plan.recv, plan.send, p2p=self.p2p)
             if M == 0:
                 return
             g = torch.zeros(plan.own_U, self.width, dtype=torch.float32, device=dev)
@@ -451,6 +458,8 @@ class HashSparseTable(SparseTable):
         self._alloc(cap)
         self.counters = torch.zeros(2, dtype=torch.int32, device=dev)
         self.pipe = _Pipeline(comm, consistency, staleness)
+        if self.pipe.async_:
+            comm.background()  # collective: create the side-stream communicator up front
         self.p2p = (consistency != "bsp") if p2p is None else p2p
         self._pending: list = []
 

@@ -31,7 +31,7 @@ def run(rounds=20):
         split = 1
         if lay == "tn":
             tiles = ((M + 127) // 128) * ((N + 127) // 128)
-            split = max(1, min(K // 256, (512 + tiles - 1) // tiles))
+            split = max(1, min(K // 640, (int(os.environ.get("MINIPS_WGRAD_BLOCKS", "512")) + tiles - 1) // tiles))
         At = A.t() if a_km else A
         Bt = B if b_kn else B.t()
 
