@@ -281,6 +281,23 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
   TORCH_CHECK(dX.dim() == 2 && dX.stride(1) == 1, "dX must be a row-major matrix");
   TORCH_CHECK(inv.numel() == B * F && dX.size(1) >= x_off + F * D && grad_rows.size(1) >= D + (dw ? 1 : 0), "shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
+  static const bool tile_mode = [] {
+    const char* e = std::getenv("MINIPS_EMB_BWD");
+    return e && std::string(e) == "tile";
+  }();
+  if (!tile_mode && (D == 16 || D == 32 || D == 64) && grad_rows.size(0) < (1ll << 31) && B * F < (1ll << 31) &&
+      x_off % 4 == 0 && dX.stride(0) % 4 == 0) {
+    // segment-sum path: overwrites rows [0, U) of grad_rows
+    const int64_t U = grad_rows.size(0);
+    TORCH_CHECK(grad_rows.stride(1) == 1, "grad_rows must be row-major");
+    at::Tensor ws = at::empty({3 * U + 1 + 2 * B * F + U / 1024 + 1}, inv.options().dtype(at::kInt));
+    const bool bf = dX.scalar_type() == at::kBFloat16;
+    const void* base = bf ? (const void*)(ptr<bf16_t>(dX) + x_off) : (const void*)(ptr<float>(dX) + x_off);
+    minips_k::emb_backward_segment(base, bf, (int)dX.stride(0), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
+                                   ptr<float>(grad_rows), (int)grad_rows.stride(0), (int)U, ws.data_ptr<int>(),
+                                   stream_of(dX));
+    return;
+  }
   if (dX.scalar_type() == at::kFloat)
     minips_k::wd_emb_backward(ptr<float>(dX) + x_off, (int)dX.stride(0), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
                               ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));

@@ -91,6 +91,12 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
 // pre-zeroed).
 void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                      float* grad_rows, int row_stride, hipStream_t s);
+// Segment-sum form of the embedding backward: grad_rows[u] = sum over lookups j with
+// inv[j] == u for every row u < U (zero-filled first, padding included); lookups are grouped
+// by row (count / scan / fill) and summed piecewise, float atomics only where a piece boundary
+// cuts a row. ws: (3U + 2 + 2*B*F + U/1024) int32 workspace.
+void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,
+                          int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                           float* grad_rows, int row_stride, hipStream_t s);
 

@@ -2,6 +2,7 @@
 // the fused output head (Linear Hd->1 + BCE-with-logits forward+backward), and the
 // embedding-gradient scatter into the per-unique-key gradient rows that are pushed to the
 // owning server shards.
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -274,6 +275,327 @@ void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                           float* grad_rows, int row_stride, hipStream_t s) {
   emb_backward(dX, ldx, dwide, inv, B, F, D, grad_rows, row_stride, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Segment-sum embedding backward (no float atomics): the lookups are grouped by unique row in a
+// CSR built from `inv`, then every unique row sums its members in registers and is written once.
+//   seg_count  per (feature, 256-sample tile): LDS-hash dedupe of the tile's rows, one integer
+//              atomic per distinct row per tile (hot rows see <= B/256 atomics, not B)
+//   scan       exclusive prefix sum of the U counts (three coalesced passes)
+//   seg_fill   same traversal; a tile reserves a contiguous range per distinct row with one
+//              atomic on its cursor and drops its lookups in by their LDS rank
+//   seg_sum    fixed-size pieces of the row-sorted lookups per wave (below): loads are batched so
+//              a Zipf-hot row with thousands of lookups is spread over many waves instead of
+//              serialising one, and only rows cut by a piece boundary need an fp32 atomic
+
+struct TileDedupe {
+  int hkey[kEmbHash];
+  int hidx[kEmbHash];
+  int cnt[kEmbTB];
+  int rowof[kEmbTB];
+  int base[kEmbTB];
+  int nd;
+};
+
+// Fills the LDS dedupe of the tile; returns (via refs) this thread's row and its distinct index.
+__device__ __forceinline__ void tile_dedupe(TileDedupe& T, const int64_t* __restrict__ inv, int64_t b0, int nb, int F,
+                                            int f, int t, int& r, int& di, int& rank) {
+  for (int j = t; j < kEmbHash; j += kEmbTB) T.hkey[j] = -1;
+  if (t < kEmbTB) T.cnt[t] = 0;
+  if (t == 0) T.nd = 0;
+  __syncthreads();
+  int slot = -1;
+  bool lead = false;
+  r = -1;
+  if (t < nb) {
+    r = (int)inv[(b0 + t) * F + f];
+    int h = (int)((uint32_t)r * 2654435761u >> 23) & (kEmbHash - 1);
+    while (true) {
+      const int prev = atomicCAS(T.hkey + h, -1, r);
+      if (prev == -1) {
+        lead = true;
+        break;
+      }
+      if (prev == r) break;
+      h = (h + 1) & (kEmbHash - 1);
+    }
+    slot = h;
+  }
+  __syncthreads();
+  if (lead) {
+    const int id = atomicAdd(&T.nd, 1);
+    T.hidx[slot] = id;
+    T.rowof[id] = r;
+  }
+  __syncthreads();
+  di = -1;
+  rank = 0;
+  if (t < nb) {
+    di = T.hidx[slot];
+    rank = atomicAdd(T.cnt + di, 1);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kEmbTB) void emb_seg_count_kernel(const int64_t* __restrict__ inv, int64_t B, int F,
+                                                               int* __restrict__ counts) {
+  __shared__ TileDedupe T;
+  const int t = threadIdx.x, f = blockIdx.y;
+  const int64_t b0 = (int64_t)blockIdx.x * kEmbTB;
+  const int nb = (int)min((int64_t)kEmbTB, B - b0);
+  int r, di, rank;
+  tile_dedupe(T, inv, b0, nb, F, f, t, r, di, rank);
+  if (t < T.nd) atomicAdd(counts + T.rowof[t], T.cnt[t]);
+}
+
+// Exclusive prefix sum offsets[i] = sum(counts[0..i)), offsets[U] = total, in three coalesced
+// passes over 1024-element tiles (tile sums -> scan of the tile sums -> per-tile scan + prefix).
+constexpr int kScanTile = 1024;
+
+__device__ __forceinline__ int block_excl_scan256(int v, int* sh, int* total) {
+  // 256 threads: wave-level inclusive scan with shuffles, then the 4 wave totals
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  int base = 0;
+  for (int i = 0; i < w; ++i) base += sh[i];
+  *total = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(256) void emb_scan_reduce_kernel(const int* __restrict__ counts, int U,
+                                                              int* __restrict__ tile_sums) {
+  __shared__ int sh[4];
+  const int i0 = blockIdx.x * kScanTile + threadIdx.x * 4;
+  int v = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v += (i0 + q < U) ? counts[i0 + q] : 0;
+  int tot;
+  block_excl_scan256(v, sh, &tot);
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void emb_scan_top_kernel(int* __restrict__ tile_sums, int ntiles) {
+  __shared__ int sh[4];
+  int carry = 0;
+  for (int base = 0; base < ntiles; base += 256) {
+    const int i = base + threadIdx.x;
+    const int v = i < ntiles ? tile_sums[i] : 0;
+    int tot;
+    const int ex = block_excl_scan256(v, sh, &tot);
+    if (i < ntiles) tile_sums[i] = carry + ex;
+    carry += tot;
+  }
+}
+
+__global__ __launch_bounds__(256) void emb_scan_final_kernel(const int* __restrict__ counts, int U,
+                                                             const int* __restrict__ tile_prefix,
+                                                             int* __restrict__ offsets) {
+  __shared__ int sh[4];
+  const int i0 = blockIdx.x * kScanTile + threadIdx.x * 4;
+  int c[4], v = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    c[q] = (i0 + q < U) ? counts[i0 + q] : 0;
+    v += c[q];
+  }
+  int tot;
+  int run = tile_prefix[blockIdx.x] + block_excl_scan256(v, sh, &tot);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (i0 + q < U) offsets[i0 + q] = run;
+    run += c[q];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) offsets[U] = tile_prefix[blockIdx.x] + tot;
+}
+
+__global__ __launch_bounds__(kEmbTB) void emb_seg_fill_kernel(const int64_t* __restrict__ inv, int64_t B, int F,
+                                                              const int* __restrict__ offsets,
+                                                              int* __restrict__ cursor, int* __restrict__ members,
+                                                              int* __restrict__ memrow) {
+  __shared__ TileDedupe T;
+  const int t = threadIdx.x, f = blockIdx.y;
+  const int64_t b0 = (int64_t)blockIdx.x * kEmbTB;
+  const int nb = (int)min((int64_t)kEmbTB, B - b0);
+  int r, di, rank;
+  tile_dedupe(T, inv, b0, nb, F, f, t, r, di, rank);
+  if (t < T.nd) T.base[t] = offsets[T.rowof[t]] + atomicAdd(cursor + T.rowof[t], T.cnt[t]);
+  __syncthreads();
+  if (t < nb) {
+    const int pos = T.base[di] + rank;
+    members[pos] = (int)((b0 + t) * F + f);  // lookup id j = b*F + f
+    memrow[pos] = r;
+  }
+}
+
+// Piecewise segmented sum over the row-sorted lookups: a wave owns a piece of 64/D x kSegG
+// consecutive members, each D-lane group a contiguous kSegG of them, read kSegBatch at a time
+// (independent loads in flight). A group flushes its running sum at every row change: a plain
+// store when the row lies entirely inside the group's range, an fp32 atomic otherwise (only
+// rows cut by a range boundary -- grad_rows is zero-filled first).
+constexpr int kSegG = 16, kSegBatch = 8;
+
+// 4 consecutive gradient values of one lookup row segment.
+__device__ __forceinline__ float4 ld_grad4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld_grad4(const bf16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+template <int D>
+__device__ __forceinline__ void seg_flush(float* __restrict__ grad_rows, int row_stride, int row, float4 acc,
+                                          float accw, bool wide, int prev_row, int next_row, int l) {
+  float* out = grad_rows + (int64_t)row * row_stride + 4 * l;
+  if (row != prev_row && row != next_row) {  // the whole row lies inside this group's range
+    out[0] = acc.x;
+    out[1] = acc.y;
+    out[2] = acc.z;
+    out[3] = acc.w;
+    if (wide && l == 0) out[D] = accw;
+  } else {
+    atomicAdd(out + 0, acc.x);
+    atomicAdd(out + 1, acc.y);
+    atomicAdd(out + 2, acc.z);
+    atomicAdd(out + 3, acc.w);
+    if (wide && l == 0) atomicAdd(out + D, accw);
+  }
+}
+
+// Piecewise segmented sum over the row-sorted lookups. A group of D/4 lanes reads one lookup's
+// D values as 4-wide vectors (64/(D/4) lookups per wave-instruction); each group owns kSegG
+// consecutive lookups, loaded kSegBatch at a time (independent loads in flight), and flushes its
+// running sum at every row change: a plain store when the row lies entirely inside the group's
+// range, fp32 atomics when the row continues across the range boundary (grad_rows is zero-filled
+// first).
+template <typename TX, int D>
+__global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__ dX, int ldx,
+                                                          const float* __restrict__ dwide, int F,
+                                                          const int* __restrict__ members,
+                                                          const int* __restrict__ memrow, int total,
+                                                          float* __restrict__ grad_rows, int row_stride) {
+  constexpr int L = D / 4, PER = 64 / L;
+  const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
+  const bool wide = dwide != nullptr;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t piece = wave; piece * (PER * kSegG) < total; piece += nw) {
+    const int a = (int)(piece * (PER * kSegG)) + sub * kSegG;
+    const int b = min(total, a + kSegG);
+    const int prev_row = (a > 0 && a <= total) ? memrow[a - 1] : -1;
+    const int next_row = b < total ? memrow[b] : -1;
+    int cur = -1;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float accw = 0.f;
+    for (int m0 = a; m0 < b; m0 += kSegBatch) {
+      int u[kSegBatch], bb[kSegBatch];
+      float4 v[kSegBatch];
+      float vw[kSegBatch];
+#pragma unroll
+      for (int q = 0; q < kSegBatch; ++q) {
+        const int m = m0 + q;
+        u[q] = m < b ? memrow[m] : -1;
+        const int j = m < b ? members[m] : 0;
+        bb[q] = j / F;
+        const int ff = j - bb[q] * F;
+        v[q] = m < b ? ld_grad4(dX + (int64_t)bb[q] * ldx + ff * D + 4 * l) : make_float4(0.f, 0.f, 0.f, 0.f);
+        vw[q] = (wide && l == 0 && m < b) ? dwide[bb[q]] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < kSegBatch; ++q) {
+        if (u[q] < 0) break;
+        if (u[q] != cur) {
+          if (cur >= 0) seg_flush<D>(grad_rows, row_stride, cur, acc, accw, wide, prev_row, next_row, l);
+          cur = u[q];
+          acc = make_float4(0.f, 0.f, 0.f, 0.f);
+          accw = 0.f;
+        }
+        acc.x += v[q].x;
+        acc.y += v[q].y;
+        acc.z += v[q].z;
+        acc.w += v[q].w;
+        accw += vw[q];
+      }
+    }
+    // A Zipf-hot row covers whole waves: combine the groups' partials in registers first, so a
+    // hot row takes one atomic per wave instead of one per group (same-address atomics serialise
+    // at the memory side).
+    const int c0 = __shfl(cur, 0, 64);
+    if (__all(cur == c0) && c0 >= 0) {
+#pragma unroll
+      for (int o = L; o < 64; o <<= 1) {
+        acc.x += __shfl_xor(acc.x, o, 64);
+        acc.y += __shfl_xor(acc.y, o, 64);
+        acc.z += __shfl_xor(acc.z, o, 64);
+        acc.w += __shfl_xor(acc.w, o, 64);
+        accw += __shfl_xor(accw, o, 64);
+      }
+      const int p0 = __shfl(prev_row, 0, 64), n1 = __shfl(next_row, 63, 64);
+      if (sub == 0) seg_flush<D>(grad_rows, row_stride, c0, acc, accw, wide, p0, n1, l);
+    } else if (cur >= 0) {
+      seg_flush<D>(grad_rows, row_stride, cur, acc, accw, wide, prev_row, next_row, l);
+    }
+  }
+}
+
+template <typename TX>
+static void emb_backward_seg(const TX* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
+                             float* grad_rows, int row_stride, int U, int* ws, hipStream_t s) {
+  // ws: counts[U] | cursor[U] | offsets[U+1] | members[B*F] | memrow[B*F] | tiles[U/1024+1]
+  const int total = (int)(B * F);
+  int* counts = ws;
+  int* cursor = counts + U;
+  int* offsets = cursor + U;
+  int* members = offsets + U + 1;
+  int* memrow = members + total;
+  int* tiles = memrow + total;
+  const int ntiles = (U + kScanTile - 1) / kScanTile;
+  MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int) * 2 * (size_t)U, s));  // counts, cursor
+  MINIPS_HIP_CHECK(hipMemsetAsync(grad_rows, 0, sizeof(float) * (size_t)U * row_stride, s));
+  dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);
+  hipLaunchKernelGGL(emb_seg_count_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, counts);
+  hipLaunchKernelGGL(emb_scan_reduce_kernel, ntiles, 256, 0, s, counts, U, tiles);
+  hipLaunchKernelGGL(emb_scan_top_kernel, 1, 256, 0, s, tiles, ntiles);
+  hipLaunchKernelGGL(emb_scan_final_kernel, ntiles, 256, 0, s, counts, U, tiles, offsets);
+  hipLaunchKernelGGL(emb_seg_fill_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, offsets, cursor, members, memrow);
+  const int pieces = (total + (256 / D) * kSegG - 1) / ((256 / D) * kSegG);
+  const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
+#define MINIPS_SEG_LAUNCH(DD)                                                                                      \
+  hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD>), blocks, 256, 0, s, dX, ldx, dwide, F, members, memrow, total,  \
+                     grad_rows, row_stride);
+  switch (D) {
+    case 16:
+      MINIPS_SEG_LAUNCH(16)
+      break;
+    case 32:
+      MINIPS_SEG_LAUNCH(32)
+      break;
+    case 64:
+      MINIPS_SEG_LAUNCH(64)
+      break;
+    default:
+      throw std::runtime_error("emb_backward_seg: D must be 16, 32 or 64");
+  }
+#undef MINIPS_SEG_LAUNCH
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,
+                          int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s) {
+  if (B <= 0 || U <= 0) return;
+  if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("emb_backward_segment: row_stride too small");
+  if (bf16)
+    emb_backward_seg(static_cast<const bf16_t*>(dX), ldx, dwide, inv, B, F, D, grad_rows, row_stride, U, ws, s);
+  else
+    emb_backward_seg(static_cast<const float*>(dX), ldx, dwide, inv, B, F, D, grad_rows, row_stride, U, ws, s);
 }
 
 }  // namespace minips_k

@@ -167,7 +167,9 @@ class WideDeep:
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
         ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
-        grad_rows = torch.zeros(max(plan.U, 1), cfg.row_width, dtype=torch.float32, device=self.comm.device)
+        dev = self.comm.device
+        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.U, 1), cfg.row_width,
+                                                                         dtype=torch.float32, device=dev)
         ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows)
         self.emb.add(plan, grad_rows)
         self.dense.add()

@@ -268,7 +268,10 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
 
 
 def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0):
-    """grad_rows[inv[b*F+f], :D] += dX[b, x_off + f*D : ...]; column D += dwide[b] if given."""
+    """grad_rows[u, :D] = sum of dX[b, x_off + f*D : ...] over the lookups (b, f) with
+    inv[b*F+f] == u; column D likewise sums dwide[b] when given. On the GPU every row of
+    grad_rows is written (rows without lookups become 0); the CPU reference adds into grad_rows,
+    so callers pass a zeroed buffer."""
     if _gpu(dX):
         kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off))
         return grad_rows

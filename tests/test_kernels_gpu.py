@@ -229,3 +229,22 @@ def test_criteo_synth_kernel(dev):
     assert torch.unique(col).numel() < 4096
     d2 = CriteoSynth(4096, device=dev, seed=3)
     torch.testing.assert_close(d2.next()[1], keys)  # reproducible
+
+
+@pytest.mark.parametrize("D,dtype", [(32, torch.bfloat16), (64, torch.float32), (16, torch.bfloat16)])
+def test_embedding_backward_segment_hot_rows(dev, D, dtype):
+    """Segment-sum embedding backward incl. Zipf-hot rows (> 2048 lookups, split over waves) and
+    rows without lookups (written as zero)."""
+    g = torch.Generator().manual_seed(D)
+    B, F, U = 8192, 3, 5000
+    inv = torch.randint(0, U - 100, (B * F,), generator=g)  # the last 100 rows get no lookups
+    inv[: 6000] = 7                                         # a hot row: 6000 lookups
+    inv[6000: 8500] = 11                                    # and one just above the split size
+    dX = torch.randn(B, F * D + 8, generator=g).to(dtype)
+    dwide = torch.randn(B, generator=g)
+    ref = torch.zeros(U, D + 1)
+    ops.wd_emb_backward(dX.float(), dwide, inv, F, D, ref)
+    gr = torch.full((U, D + 1), float("nan"), device=dev)  # every row must be overwritten
+    ops.wd_emb_backward(dX.to(dev), dwide.to(dev), inv.to(dev), F, D, gr)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(gr.cpu(), ref, rtol=1e-4, atol=tol * 8)
