@@ -270,13 +270,51 @@ void scatter_add_rows(const float* src, int64_t n, int D, const int64_t* idx, fl
 }
 
 // --------------------------------------------------------------------------- row-wise adagrad
-// One wave per row-group: lanes stride the row, a wave reduction gives mean(g^2).
+// Half a wave per row (two rows per wave-instruction) for rows of <= 64 values: every lane holds
+// its <= 2 gradient values in registers (one read), the two mean(g^2) reductions are xor
+// shuffles inside the 32-lane half. Wider rows take a whole wave and stride.
+// Columns [0, D1) share accumulator state[row]; columns [D1, D) share state2[row] (Wide&Deep
+// keeps the deep embedding and the wide weight in one row, each with its own Adagrad state).
+__global__ void sparse_rowwise_adagrad_half_kernel(float* table, int64_t ld, float* state, float* state2, int D1,
+                                                   const int64_t* __restrict__ keys, int64_t n, int64_t base, int D,
+                                                   const float* __restrict__ grads, float lr, float eps) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i0 = wave * 2; i0 < n; i0 += nwaves * 2) {
+    const int64_t i = i0 + half;
+    const bool ok = i < n;
+    float g0 = 0.f, g1 = 0.f;
+    int64_t row = 0;
+    if (ok) {
+      row = keys[i] - base;
+      if (l < D) g0 = grads[i * D + l];
+      if (l + 32 < D) g1 = grads[i * D + l + 32];
+    }
+    float sq1 = (l < D1 ? g0 * g0 : 0.f) + (l + 32 < D1 ? g1 * g1 : 0.f);
+    float sq2 = (l >= D1 && l < D ? g0 * g0 : 0.f) + (l + 32 >= D1 && l + 32 < D ? g1 * g1 : 0.f);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      sq1 += __shfl_xor(sq1, o, 64);
+      sq2 += __shfl_xor(sq2, o, 64);
+    }
+    if (!ok) continue;
+    const float st1 = state[row] + sq1 / (float)D1;
+    const float st2 = D1 < D ? state2[row] + sq2 / (float)(D - D1) : 0.f;
+    if (l == 0) {
+      state[row] = st1;
+      if (D1 < D) state2[row] = st2;
+    }
+    const float s1 = lr / (sqrtf(st1) + eps), s2 = lr / (sqrtf(st2) + eps);
+    float* tr = table + row * ld;
+    if (l < D) tr[l] -= (l < D1 ? s1 : s2) * g0;
+    if (l + 32 < D) tr[l + 32] -= (l + 32 < D1 ? s1 : s2) * g1;
+  }
+}
+
 __global__ void sparse_rowwise_adagrad_kernel(float* table, int64_t ld, float* state, float* state2, int D1,
                                               const int64_t* __restrict__ keys, int64_t n, int64_t base, int D,
                                               const float* __restrict__ grads, float lr, float eps) {
-  // Columns [0, D1) share accumulator state[row]; columns [D1, D) share state2[row]
-  // (Wide&Deep keeps the deep embedding and the wide weight in one row, each with its own
-  // row-wise Adagrad state).
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -310,9 +348,13 @@ void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state
   if (D1 <= 0 || D1 > D) D1 = D;
   if (D1 < D && !state2) throw std::runtime_error("sparse_rowwise_adagrad: split rows need state2");
   const int block = 256;
-  const int grid = grid_for(n * 64, block, 4096);
-  hipLaunchKernelGGL(sparse_rowwise_adagrad_kernel, grid, block, 0, s, table, ld, state, state2, D1, keys, n, base, D,
-                     grads, lr, eps);
+  if (D <= 64) {
+    hipLaunchKernelGGL(sparse_rowwise_adagrad_half_kernel, grid_for(n * 32, block, 8192), block, 0, s, table, ld,
+                       state, state2, D1, keys, n, base, D, grads, lr, eps);
+  } else {
+    hipLaunchKernelGGL(sparse_rowwise_adagrad_kernel, grid_for(n * 64, block, 4096), block, 0, s, table, ld, state,
+                       state2, D1, keys, n, base, D, grads, lr, eps);
+  }
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -19,16 +19,23 @@ __global__ void wd_assemble_kernel(const float* __restrict__ dense, int n_dense,
   const int chunks = ldx >> 3;
   const int emb_cols = F * D;
   const int64_t total = B * chunks;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total + B;
+  // items [0, total): 8-column chunks of X; items [total, total + 32B): (sample, feature lane)
+  // pairs of the wide sum -- 32 lanes per sample load their features' wide weights in parallel
+  // and reduce with shuffles (a serial per-sample loop is 26 dependent loads). total is rounded
+  // up to a multiple of 64 so a wave never mixes the two kinds of items.
+  const int64_t total_r = (total + 63) & ~63ll;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total_r + 32 * B;
        c += (int64_t)gridDim.x * blockDim.x) {
-    if (c >= total) {
-      const int64_t b = c - total;
-      float w = 0.f;
-      const int64_t* iv = inv + b * F;
-      for (int f = 0; f < F; ++f) w += bf2f(rows[iv[f] * row_stride + D]);
-      wide_logit[b] = w;
+    if (c >= total_r) {
+      const int64_t k = c - total_r, b = k >> 5;
+      const int f = (int)(k & 31);
+      float w = f < F ? bf2f(rows[inv[b * F + f] * row_stride + D]) : 0.f;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+      if (f == 0) wide_logit[b] = w;
       continue;
     }
+    if (c >= total) continue;
     const int64_t b = c / chunks;
     const int col0 = (int)(c - b * chunks) * 8;
     uint32_t packed[4];
@@ -71,15 +78,21 @@ void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_st
   if (row_stride % 4) throw std::runtime_error("wd_assemble: row_stride must be a multiple of 4");
   if (B <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(wd_assemble_kernel, grid_for(B * (ldx / 8 + 1), block, 8192), block, 0, s, dense, n_dense, rows,
+  if (F > 32) throw std::runtime_error("wd_assemble: at most 32 features");
+  // every thread must take the same number of grid-stride steps through the wide-sum items (their
+  // shuffles need all 32 lanes of a sample): size the grid so the loop runs exactly once
+  const int64_t items = ((B * (ldx / 8) + 63) & ~63ll) + 32 * B;
+  hipLaunchKernelGGL(wd_assemble_kernel, (int)((items + block - 1) / block), block, 0, s, dense, n_dense, rows,
                      row_stride, inv, B, F, D, X, ldx, wide_logit, ones_col);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 // One wave per sample (grid-stride); each lane owns Hd/64 columns and keeps its dw / colsum
 // partials in registers across all samples it visits: one atomic per lane per column at the end.
+constexpr int kHeadWaves = 16;  // 1024-thread blocks: 4x the waves in flight, same atomic count
+
 template <int PER_LANE>
-__global__ __launch_bounds__(256) void wd_head_kernel(const bf16_t* __restrict__ H, int64_t B, int Hd,
+__global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* __restrict__ H, int64_t B, int Hd,
                                                       const bf16_t* __restrict__ w, const bf16_t* __restrict__ b0,
                                                       const float* __restrict__ wide, const float* __restrict__ y,
                                                       bf16_t* __restrict__ dH, float* dw, float* db, float* dwide,
@@ -143,8 +156,8 @@ __global__ __launch_bounds__(256) void wd_head_kernel(const bf16_t* __restrict__
     }
   }
   // reduce the 4 waves of the block in LDS, then one global atomic per column per block
-  __shared__ float red[2][4][64 * PER_LANE];
-  __shared__ float red_s[2][4];
+  __shared__ float red[2][kHeadWaves][64 * PER_LANE];
+  __shared__ float red_s[2][kHeadWaves];
   const int wv = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < PER_LANE; ++j) {
@@ -157,12 +170,24 @@ __global__ __launch_bounds__(256) void wd_head_kernel(const bf16_t* __restrict__
   }
   __syncthreads();
   for (int c = threadIdx.x; c < 64 * PER_LANE; c += blockDim.x) {
-    atomicAdd(dw + c, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
-    if (colsum) atomicAdd(colsum + c, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < kHeadWaves; ++w) {
+      a += red[0][w][c];
+      b += red[1][w][c];
+    }
+    atomicAdd(dw + c, a);
+    if (colsum) atomicAdd(colsum + c, b);
   }
   if (threadIdx.x == 0) {
-    atomicAdd(db, red_s[0][0] + red_s[0][1] + red_s[0][2] + red_s[0][3]);
-    atomicAdd(loss_sum, red_s[1][0] + red_s[1][1] + red_s[1][2] + red_s[1][3]);
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < kHeadWaves; ++w) {
+      a += red_s[0][w];
+      b += red_s[1][w];
+    }
+    atomicAdd(db, a);
+    atomicAdd(loss_sum, b);
   }
 }
 
@@ -170,8 +195,8 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
              float grad_scale, hipStream_t s) {
   if (B <= 0) return;
-  const int block = 256;
-  const int grid = (int)std::min<int64_t>(128, (B + 15) / 16);  // per-block LDS reduction, then atomics
+  const int block = 64 * kHeadWaves;
+  const int grid = (int)std::min<int64_t>(128, (B + 63) / 64);  // per-block LDS reduction, then atomics
   switch (Hd) {
     case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
     case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;

@@ -163,8 +163,11 @@ class DenseTable:
 
         def work():
             if pending:
-                comm.reduce_scatter(self.grad_shard, grad)
-                self._apply(self.grad_shard, step)
+                if comm.world == 1:  # the whole gradient is the owned shard
+                    self._apply(grad, step)
+                else:
+                    comm.reduce_scatter(self.grad_shard, grad)
+                    self._apply(self.grad_shard, step)
                 comm.all_gather(self.params, self.params[self.base: self.base + self.shard])
             grad.zero_()
 
@@ -302,8 +305,11 @@ class SparseTable:
         send, recv = self.comm.exchange_counts(counts)
         U = int(sum(send))
         M = int(sum(recv))
-        recv_keys = torch.empty(M, dtype=torch.int64, device=keys.device)
-        self.comm.all_to_all_v(recv_keys, uniq, recv, send, p2p=self.p2p)
+        if self.comm.world == 1:
+            recv_keys = uniq[:M]
+        else:
+            recv_keys = torch.empty(M, dtype=torch.int64, device=keys.device)
+            self.comm.all_to_all_v(recv_keys, uniq, recv, send, p2p=self.p2p)
         p = SparsePlan(keys.numel(), inv, uniq, U, send, recv, recv_keys)
         if self.comm.world > 1 and M > 0:
             own_bounds = torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=keys.device)
@@ -322,6 +328,8 @@ class SparseTable:
         served = torch.empty(len(plan.recv_keys), self.width, dtype=self.pull_dtype, device=dev)
         table, index, base = self._serve_index(plan)
         ops.gather_rows(table, index, base, served)
+        if self.comm.world == 1:  # the served rows ARE the requested rows: no exchange, no copy
+            return served, plan
         rows = torch.empty(plan.U, self.width, dtype=self.pull_dtype, device=dev)
         self.comm.all_to_all_v(rows, served, plan.send, plan.recv, p2p=self.p2p)
         return rows, plan
