@@ -279,31 +279,36 @@ constexpr uint32_t kOobOffset = 0x80000000u;
 
 __device__ __forceinline__ int swz_k(int k) { return 2 * ((k & 3) | ((((k >> 2) ^ (k >> 3)) & 1) << 2)); }
 
-template <bool KMAJOR>
+// One operand tile of ROWS x 64 k (MK/NK image [ROWS][64]) or 64 k x ROWS (KM/KN image
+// [64][ROWS]) = ROWS/8 DMA wave-instructions of 1 KiB, split over the workgroup's waves.
+template <bool KMAJOR, int ROWS, int NWAVES>
 __device__ __forceinline__ void dma_tile(__amdgpu_buffer_rsrc_t rsrc, int ld, int row0, int k0, int rows, int kend,
                                          bf16_t* S, int wave, int lane) {
+  constexpr int INSTR = ROWS / 8, PER = INSTR / NWAVES;
+  static_assert(INSTR % NWAVES == 0, "tile must split evenly over the waves");
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < PER; ++j) {
+    const int gi = wave * PER + j;  // 1-KiB piece index
     uint32_t voff;
-    bf16_t* dst;
     if (!KMAJOR) {
-      const int R = 32 * wave + 8 * j + (lane >> 3);
+      const int R = 8 * gi + (lane >> 3);
       const int c = (lane & 7) ^ ((R >> 1) & 7);
       const int gr = row0 + R, gk = k0 + 8 * c;
       voff = (gr < rows && gk < kend) ? (uint32_t)(((int64_t)gr * ld + gk) * 2) : kOobOffset;
-      dst = S + (32 * wave + 8 * j) * BK2;
     } else {
-      const int kr = 16 * wave + 4 * j + (lane >> 4);
-      const int c = (lane & 15) ^ swz_k(kr);
+      constexpr int CH = ROWS / 8;           // 16-byte chunks per k-row
+      constexpr int RPI = 64 / CH;           // k-rows per 1-KiB piece
+      const int kr = RPI * gi + lane / CH;
+      const int c = (lane % CH) ^ swz_k(kr);  // flips chunk bits 1..3 only: stays in its 256-B half
       const int gk = k0 + kr, gm = row0 + 8 * c;
       voff = (gk < kend && gm < rows) ? (uint32_t)(((int64_t)gk * ld + gm) * 2) : kOobOffset;
-      dst = S + (16 * wave + 4 * j) * BM;
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(S + gi * 512), 16, voff,
+                                             0, 0, 0);
   }
 }
 
-template <bool KMAJOR, bool PERM>
+template <bool KMAJOR, bool PERM, int ROWS>
 __device__ __forceinline__ v8s frag2(const bf16_t* S, int row_base, int ks, int lane) {
   const int g = lane >> 4;
   if (!KMAJOR) {
@@ -315,21 +320,26 @@ __device__ __forceinline__ v8s frag2(const bf16_t* S, int row_base, int ks, int 
     const int r0 = 32 * ks + (PERM ? 4 * g : 8 * g) + q;
     const int r1 = 32 * ks + (PERM ? 16 + 4 * g : 8 * g + 4) + q;
     const int ch = (row_base >> 3) + (p >> 1), sub = 4 * (p & 1);
-    const v4s lo = ds_read_tr16(S + r0 * BM + 8 * (ch ^ swz_k(r0)) + sub);
-    const v4s hi = ds_read_tr16(S + r1 * BM + 8 * (ch ^ swz_k(r1)) + sub);
+    const v4s lo = ds_read_tr16(S + r0 * ROWS + 8 * (ch ^ swz_k(r0)) + sub);
+    const v4s hi = ds_read_tr16(S + r1 * ROWS + 8 * (ch ^ swz_k(r1)) + sub);
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
 
-template <bool A_KM, bool B_KN, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_v2_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                         int M, int N, int K, int lda, int ldb, int k_chunk,
-                                                         EpiArgs ep) {
+// TM x TN output tile, (TM/64) x (TN/64) waves of 64x64 each (4, 8 or 16 waves). 128x128
+// keeps 2 workgroups per CU; the 256-wide tiles halve the L2->LDS bytes per MFMA (the loads,
+// not the MFMAs, bound this kernel at these sizes) and run one 16- or 8-wave workgroup per CU.
+template <int TM, int TN, bool A_KM, bool B_KN, int EPI>
+__global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __restrict__ A,
+                                                               const bf16_t* __restrict__ B, int M, int N, int K,
+                                                               int lda, int ldb, int k_chunk, EpiArgs ep) {
   constexpr bool PERM = A_KM && B_KN;
-  __shared__ __attribute__((aligned(1024))) bf16_t smem[2][2][BM * BK2];
+  constexpr int WN = TN / 64, NWAVES = (TM / 64) * (TN / 64);
+  constexpr int VM_STAGE = (TM / 8 + TN / 8) / NWAVES;  // DMA instructions per thread per stage
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2][(TM + TN) * BK2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (N + TN - 1) / TN, tiles_m = (M + TM - 1) / TM;
   const int nwg = tiles_m * tiles_n;
   int bid = blockIdx.x;
   if (nwg >= 16) {
@@ -338,7 +348,7 @@ __global__ __launch_bounds__(256, 2) void gemm_v2_kernel(const bf16_t* __restric
     bid = base + (bid >> 3);
   }
   const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * TM, n0 = tn * TN;
   {
     const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
     A += zo * ep.sa_o + zi * ep.sa_i;
@@ -360,30 +370,30 @@ __global__ __launch_bounds__(256, 2) void gemm_v2_kernel(const bf16_t* __restric
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   if (nt > 0) {
-    dma_tile<A_KM>(ra, lda, m0, kb, M, ke, smem[0][0], wave, lane);
-    dma_tile<B_KN>(rb, ldb, n0, kb, N, ke, smem[0][1], wave, lane);
+    dma_tile<A_KM, TM, NWAVES>(ra, lda, m0, kb, M, ke, smem[0], wave, lane);
+    dma_tile<B_KN, TN, NWAVES>(rb, ldb, n0, kb, N, ke, smem[0] + TM * BK2, wave, lane);
   }
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
     if (t + 1 < nt) {
       const int k1 = kb + (t + 1) * BK2;
-      dma_tile<A_KM>(ra, lda, m0, k1, M, ke, smem[cur ^ 1][0], wave, lane);
-      dma_tile<B_KN>(rb, ldb, n0, k1, N, ke, smem[cur ^ 1][1], wave, lane);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this stage retired, the next one in flight
+      dma_tile<A_KM, TM, NWAVES>(ra, lda, m0, k1, M, ke, smem[cur ^ 1], wave, lane);
+      dma_tile<B_KN, TN, NWAVES>(rb, ldb, n0, k1, N, ke, smem[cur ^ 1] + TM * BK2, wave, lane);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_STAGE) : "memory");  // this stage retired, the next in flight
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const bf16_t* SA = smem[cur][0];
-    const bf16_t* SB = smem[cur][1];
+    const bf16_t* SA = smem[cur];
+    const bf16_t* SB = smem[cur] + TM * BK2;
 #pragma unroll
     for (int ks = 0; ks < BK2 / 32; ++ks) {
       v8s af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag2<A_KM, PERM>(SA, wm * 64 + i * 16, ks, lane);
+      for (int i = 0; i < 4; ++i) af[i] = frag2<A_KM, PERM, TM>(SA, wm * 64 + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag2<B_KN, PERM>(SB, wn * 64 + j * 16, ks, lane);
+      for (int j = 0; j < 4; ++j) bfr[j] = frag2<B_KN, PERM, TN>(SB, wn * 64 + j * 16, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -423,8 +433,33 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
     const int kper = (K + split_k - 1) / split_k;
     const int kc = (kper + BK2 - 1) / BK2 * BK2;
     const int nsplit = (K + kc - 1) / kc;
-    dim3 grid(tiles, batch, nsplit);
-    hipLaunchKernelGGL((gemm_v2_kernel<A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
+    // Tile choice by wave quantisation: a 256x256 workgroup fills a CU alone (128 KiB LDS), two
+    // 128x128 ones share it; take the 256 tile when its last round of workgroups is at least as
+    // full as the 128 tile's (it moves half the L2->LDS bytes per MFMA), else 128x128
+    // (tools/bench_gemm.py: gpt.fc 1536 vs 384 tiles -> 128 wins; W&D dgrad0 256 tiles -> 256 wins).
+    static const int force_tile = [] {
+      const char* e = std::getenv("MINIPS_GEMM_TILE");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int64_t work = (int64_t)batch * nsplit;
+    const int64_t t256 = work * ((M + 255) / 256) * ((N + 255) / 256);
+    const int64_t t128 = work * (int64_t)tiles;
+    const double eff256 = (double)t256 / (double)(((t256 + 255) / 256) * 256);
+    const double eff128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
+    const int pick = force_tile ? force_tile : (eff256 >= eff128 ? 256 : 128);
+    if (pick == 256) {
+      dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
+      hipLaunchKernelGGL((gemm_v2_kernel<256, 256, A_KM, B_KN, EPI>), grid, dim3(1024), 0, s, A, B, M, N, K, lda, ldb,
+                         kc, ep);
+    } else if (pick == 200) {  // 256 x 128
+      dim3 grid(((M + 255) / 256) * ((N + 127) / 128), batch, nsplit);
+      hipLaunchKernelGGL((gemm_v2_kernel<256, 128, A_KM, B_KN, EPI>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb,
+                         kc, ep);
+    } else {
+      dim3 grid(tiles, batch, nsplit);
+      hipLaunchKernelGGL((gemm_v2_kernel<128, 128, A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb,
+                         kc, ep);
+    }
     return nsplit;
   }
   // BK=64 halves the barriers per FLOP; short K chunks keep BK=32 (less tail waste).
