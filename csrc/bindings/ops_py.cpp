@@ -174,14 +174,19 @@ void scatter_add_rows(const at::Tensor& src, const at::Tensor& idx, at::Tensor& 
   check_gpu(src, "src");
   check_gpu(idx, "idx");
   check_gpu(acc, "acc");
-  check_dtype(src, at::kFloat, "src");
+  TORCH_CHECK(src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16, "src must be fp32 or bf16");
   check_dtype(acc, at::kFloat, "acc");
   check_dtype(idx, at::kLong, "idx");
-  TORCH_CHECK(src.dim() == 2 && acc.dim() == 2 && src.size(1) == acc.size(1), "row widths differ");
+  TORCH_CHECK(src.dim() == 2 && acc.dim() == 2 && src.size(1) == acc.size(1) && src.is_contiguous(),
+              "row widths differ");
   TORCH_CHECK(idx.numel() == src.size(0), "idx/src length mismatch");
   c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
-  minips_k::scatter_add_rows(ptr<float>(src), src.size(0), (int)src.size(1), ptr<int64_t>(idx), ptr<float>(acc),
-                             stream_of(src));
+  if (src.scalar_type() == at::kFloat)
+    minips_k::scatter_add_rows(ptr<float>(src), src.size(0), (int)src.size(1), ptr<int64_t>(idx), ptr<float>(acc),
+                               stream_of(src));
+  else
+    minips_k::scatter_add_rows_bf16(ptr<bf16_t>(src), src.size(0), (int)src.size(1), ptr<int64_t>(idx),
+                                    ptr<float>(acc), stream_of(src));
 }
 
 void sparse_rowwise_adagrad(at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,

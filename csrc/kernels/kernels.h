@@ -55,6 +55,7 @@ void lookup_rows(const bf16_t* rows, int row_stride, const int64_t* inv, int64_t
                  hipStream_t s);
 // Scatter-add rows: acc[idx[i], :] += src[i, :] (fp32, float atomics, 2 rows per wave-instr).
 void scatter_add_rows(const float* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s);
+void scatter_add_rows_bf16(const bf16_t* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s);
 // Row-wise Adagrad on a shard (one accumulator per row, DLRM style):
 //   s[row] += mean(g^2); w[row,:] -= lr * g / (sqrt(s[row]) + eps)
 // Columns [D1, D) may use a second accumulator state2 (D1 = D: single group).

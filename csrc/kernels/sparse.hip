@@ -252,20 +252,32 @@ void gather_rows(const float* table, int64_t ld, const int64_t* keys, int64_t n,
 }
 
 // --------------------------------------------------------------------------- scatter-add
-__global__ void scatter_add_rows_kernel(const float* __restrict__ src, int64_t n, int D,
-                                        const int64_t* __restrict__ idx, float* acc) {
+__device__ __forceinline__ float ld_f(const float* p) { return *p; }
+__device__ __forceinline__ float ld_f(const bf16_t* p) { return bf2f(*p); }
+
+template <typename T>
+__global__ void scatter_add_rows_kernel(const T* __restrict__ src, int64_t n, int D, const int64_t* __restrict__ idx,
+                                        float* acc) {
   const int64_t total = n * D;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = c / D;
     const int d = (int)(c - i * D);
-    atomicAdd(acc + idx[i] * D + d, src[c]);
+    atomicAdd(acc + idx[i] * D + d, ld_f(src + c));
   }
 }
 
 void scatter_add_rows(const float* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s) {
   if (n <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(scatter_add_rows_kernel, grid_for(n * D, block), block, 0, s, src, n, D, idx, acc);
+  hipLaunchKernelGGL(scatter_add_rows_kernel<float>, grid_for(n * D, block), block, 0, s, src, n, D, idx, acc);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// bf16 gradient rows (the compressed push payload) accumulated into fp32
+void scatter_add_rows_bf16(const bf16_t* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s) {
+  if (n <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(scatter_add_rows_kernel<bf16_t>, grid_for(n * D, block), block, 0, s, src, n, D, idx, acc);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -172,10 +172,11 @@ def lookup_rows(rows, inv, F, D, out):
 
 
 def scatter_add_rows(src, idx, acc):
+    """acc[idx[i]] += src[i] (src fp32 or bf16, acc fp32)."""
     if _gpu(src):
         kernels().scatter_add_rows(src, idx, acc)
         return acc
-    acc.index_add_(0, idx, src)
+    acc.index_add_(0, idx, src.float())
     return acc
 
 

@@ -254,8 +254,12 @@ class SparseTable:
     def __init__(self, comm: Comm, num_rows: int, width: int, optimizer: str = "rowwise_adagrad",
                  lr: float = 0.01, eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "bsp",
                  staleness: int = 0, split: int | None = None, table_id: int = 0, init_std: float = 0.01,
-                 seed: int = 1234, p2p: bool | None = None):
+                 seed: int = 1234, p2p: bool | None = None, push_dtype=None):
         self.comm = comm
+        # gradient rows cross xGMI in bf16 on multi-GPU runs (half the push bytes; the owner
+        # accumulates in fp32), fp32 otherwise
+        self.push_dtype = push_dtype or (torch.bfloat16 if comm.device.type == "cuda" and comm.world > 1
+                                         else torch.float32)
         self.table_id = table_id
         self.num_rows = num_rows
         self.width = width
@@ -368,9 +372,12 @@ class SparseTable:
             keys, g, n = plan.uniq, grad_rows, plan.U
         else:
             M = len(plan.recv_keys)
-            recv = torch.empty(M, self.width, dtype=torch.float32, device=dev)
+            recv = torch.empty(M, self.width, dtype=self.push_dtype, device=dev)
             comm = self.comm.background() if self.pipe.async_ else self.comm
-            comm.all_to_all_v(recv, grad_rows, plan.recv, plan.send, p2p=self.p2p)
+            send = grad_rows[: plan.U]
+            if send.dtype != self.push_dtype:
+                send = send.to(self.push_dtype)
+            comm.all_to_all_v(recv, send, plan.recv, plan.send, p2p=self.p2p)
             if M == 0:
                 return
             g = torch.zeros(plan.own_U, self.width, dtype=torch.float32, device=dev)
@@ -446,9 +453,11 @@ class HashSparseTable(SparseTable):
 
     def __init__(self, comm: Comm, width: int, capacity: int = 1 << 16, optimizer: str = "add", lr: float = 0.01,
                  eps: float = 1e-8, pull_dtype=torch.float32, consistency: str = "bsp", staleness: int = 0,
-                 table_id: int = 0, init_std: float = 0.0, seed: int = 1234, p2p: bool | None = None):
+                 table_id: int = 0, init_std: float = 0.0, seed: int = 1234, p2p: bool | None = None,
+                 push_dtype=None):
         self.comm = comm
         self.table_id = table_id
+        self.push_dtype = push_dtype or torch.float32  # MapStorage values are exact sums: keep fp32
         self.num_rows = MASK63
         self.width = width
         self.optimizer, self.lr, self.eps = optimizer, lr, eps

@@ -143,3 +143,25 @@ def test_widedeep_two_ranks_match_one():
         assert abs(a - b) < 2e-3, (l0, one_losses)
     diff = max(abs(a - b) for a, b in zip(m0, one_master))
     assert diff < 2e-3
+
+
+def _sparse_bf16_push_fn(rank, world):
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.tables import SparseTable
+
+    comm = Comm(device=torch.device("cpu"))
+    t = SparseTable(comm, num_rows=100, width=4, optimizer="add", pull_dtype=torch.float32, init_std=0.0,
+                    push_dtype=torch.bfloat16)
+    keys = torch.tensor([3, 50, 97, 3, rank])
+    t.add_keys(keys, torch.full((5, 4), 0.5 * (rank + 1)))
+    t.clock()
+    return t.get_rows(keys).tolist()
+
+
+def test_sparse_push_in_bf16():
+    """The multi-GPU push sends gradient rows as bf16 (owner accumulates fp32)."""
+    out = run_world(_sparse_bf16_push_fn)
+    for rank, rows in out.items():
+        expect = {3: 3.0, 50: 1.5, 97: 1.5, 0: 0.5, 1: 1.0}
+        for k, row in zip([3, 50, 97, 3, rank], rows):
+            assert row == [expect[k]] * 4, (rank, k, row)
