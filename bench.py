@@ -52,9 +52,15 @@ def main():
     model = WideDeep(cfg, comm)
     data = CriteoSynth(args.batch, cards=cfg.cards, device=dev, seed=1000 + comm.rank)
 
+    # the next batch is generated one step ahead so its key routing (dedupe + count all-to-all)
+    # runs on the planning stream during the current step (lookahead; no table state is read)
+    state = {"cur": data.next()}
+
     def step():
-        dense, keys, labels = data.next()
-        return model.train_step(dense, keys, labels)
+        nxt = data.next()
+        dense, keys, labels = state["cur"]
+        state["cur"] = nxt
+        return model.train_step(dense, keys, labels, next_keys=nxt[1])
 
     loss0 = None
     for i in range(args.warmup):

@@ -116,7 +116,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
                               stream_of(A), slab.defined() ? ptr<float>(slab) : nullptr);
 }
 
-// Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P]).
+// Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P], U [1]).
 std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tensor& bounds, int64_t F) {
   check_gpu(keys, "keys");
   check_gpu(bounds, "bounds");
@@ -130,7 +130,7 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   auto opts = keys.options();
   auto table_keys = at::empty({cap}, opts), table_pos = at::empty({cap}, opts);
   auto slot = at::empty({n}, opts), flags = at::empty({n}, opts.dtype(at::kInt));
-  auto counts = at::empty({P}, opts), cursor = at::empty({P}, opts);
+  auto counts = at::empty({P + 1}, opts), cursor = at::empty({P}, opts);  // counts[P] = total unique
   auto out_keys = at::empty({n}, opts), inverse = at::empty({n}, opts);
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   TORCH_CHECK(F >= 1 && n % F == 0, "unique_bucketize: numel must be a multiple of F");
@@ -138,10 +138,17 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
                              ptr<int64_t>(table_pos), cap, ptr<int64_t>(slot), ptr<int32_t>(flags),
                              ptr<int64_t>(counts), ptr<int64_t>(cursor), ptr<int64_t>(out_keys), ptr<int64_t>(inverse),
                              stream_of(keys));
-  return {out_keys, inverse, counts};
+  return {out_keys, inverse, counts.narrow(0, 0, P), counts.narrow(0, P, 1)};
 }
 
-void gather_rows(const at::Tensor& table, const at::Tensor& keys, int64_t base, at::Tensor& out) {
+static const int64_t* count_ptr(const c10::optional<at::Tensor>& n_dev) {
+  if (!n_dev.has_value() || !n_dev->defined()) return nullptr;
+  TORCH_CHECK(n_dev->is_cuda() && n_dev->scalar_type() == at::kLong && n_dev->numel() >= 1, "n_dev: int64 GPU scalar");
+  return n_dev->data_ptr<int64_t>();
+}
+
+void gather_rows(const at::Tensor& table, const at::Tensor& keys, int64_t base, at::Tensor& out,
+                 const c10::optional<at::Tensor>& n_dev) {
   check_gpu(keys, "keys");
   check_gpu(out, "out");
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.stride(1) == 1, "table must be a row-major GPU matrix");
@@ -154,7 +161,7 @@ void gather_rows(const at::Tensor& table, const at::Tensor& keys, int64_t base, 
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "out must be fp32 or bf16");
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::gather_rows(ptr<float>(table), table.stride(0), ptr<int64_t>(keys), n, base, D, out.data_ptr(),
-                        out.scalar_type() == at::kBFloat16, stream_of(keys));
+                        out.scalar_type() == at::kBFloat16, stream_of(keys), count_ptr(n_dev));
 }
 
 void lookup_rows(const at::Tensor& rows, const at::Tensor& inv, int64_t F, int64_t D, at::Tensor& out) {
@@ -190,7 +197,8 @@ void scatter_add_rows(const at::Tensor& src, const at::Tensor& idx, at::Tensor& 
 }
 
 void sparse_rowwise_adagrad(at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
-                            const at::Tensor& keys, int64_t base, const at::Tensor& grads, double lr, double eps) {
+                            const at::Tensor& keys, int64_t base, const at::Tensor& grads, double lr, double eps,
+                            const c10::optional<at::Tensor>& n_dev) {
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.stride(1) == 1, "table must be a row-major GPU matrix");
   check_gpu(state, "state");
   check_gpu(keys, "keys");
@@ -202,17 +210,18 @@ void sparse_rowwise_adagrad(at::Tensor& table, at::Tensor& state, const c10::opt
   c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
   minips_k::sparse_rowwise_adagrad(ptr<float>(table), table.stride(0), ptr<float>(state), s2, (int)D1,
                                    ptr<int64_t>(keys), keys.numel(), base, (int)grads.size(1), ptr<float>(grads),
-                                   (float)lr, (float)eps, stream_of(table));
+                                   (float)lr, (float)eps, stream_of(table), count_ptr(n_dev));
 }
 
-void sparse_sgd(at::Tensor& table, const at::Tensor& keys, int64_t base, const at::Tensor& grads, double scale) {
+void sparse_sgd(at::Tensor& table, const at::Tensor& keys, int64_t base, const at::Tensor& grads, double scale,
+                const c10::optional<at::Tensor>& n_dev) {
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.stride(1) == 1, "table must be a row-major GPU matrix");
   check_gpu(keys, "keys");
   check_gpu(grads, "grads");
   TORCH_CHECK(grads.dim() == 2 && grads.size(0) == keys.numel() && grads.size(1) <= table.size(1), "grads shape");
   c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
   minips_k::sparse_sgd(ptr<float>(table), table.stride(0), ptr<int64_t>(keys), keys.numel(), base,
-                       (int)grads.size(1), ptr<float>(grads), (float)scale, stream_of(table));
+                       (int)grads.size(1), ptr<float>(grads), (float)scale, stream_of(table), count_ptr(n_dev));
 }
 
 void embedding_bag_fwd(const at::Tensor& rows, const at::Tensor& idx, const at::Tensor& offsets, bool mean,
@@ -275,7 +284,7 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
 }
 
 void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, const at::Tensor& inv, int64_t F,
-                     int64_t D, at::Tensor& grad_rows, int64_t x_off) {
+                     int64_t D, at::Tensor& grad_rows, int64_t x_off, const c10::optional<at::Tensor>& U_dev) {
   check_gpu(dX, "dX");
   const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
   check_gpu(inv, "inv");
@@ -300,7 +309,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
     const void* base = bf ? (const void*)(ptr<bf16_t>(dX) + x_off) : (const void*)(ptr<float>(dX) + x_off);
     minips_k::emb_backward_segment(base, bf, (int)dX.stride(0), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
                                    ptr<float>(grad_rows), (int)grad_rows.stride(0), (int)U, ws.data_ptr<int>(),
-                                   stream_of(dX));
+                                   stream_of(dX), count_ptr(U_dev));
     return;
   }
   if (dX.scalar_type() == at::kFloat)
@@ -644,7 +653,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dlrm_interact_fwd", &dlrm_interact_fwd);
   m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
   m.def("unique_bucketize", &unique_bucketize, py::arg("keys"), py::arg("bounds"), py::arg("F") = 1);
-  m.def("gather_rows", &gather_rows);
+  m.def("gather_rows", &gather_rows, py::arg("table"), py::arg("keys"), py::arg("base"), py::arg("out"),
+        py::arg("n_dev") = py::none());
   m.def("scatter_add_rows", &scatter_add_rows);
   m.def("lookup_rows", &lookup_rows);
   m.def("embed_fwd", &embed_fwd);
@@ -653,13 +663,16 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("embed_bwd", &embed_bwd);
-  m.def("sparse_rowwise_adagrad", &sparse_rowwise_adagrad);
-  m.def("sparse_sgd", &sparse_sgd);
+  m.def("sparse_rowwise_adagrad", &sparse_rowwise_adagrad, py::arg("table"), py::arg("state"), py::arg("state2"),
+        py::arg("D1"), py::arg("keys"), py::arg("base"), py::arg("grads"), py::arg("lr"), py::arg("eps"),
+        py::arg("n_dev") = py::none());
+  m.def("sparse_sgd", &sparse_sgd, py::arg("table"), py::arg("keys"), py::arg("base"), py::arg("grads"),
+        py::arg("scale"), py::arg("n_dev") = py::none());
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1);
   m.def("wd_head", &wd_head);
-  m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0);
+  m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none());
   m.def("adam_apply", &adam_apply);
   m.def("sgd_apply", &sgd_apply);
   m.def("adagrad_apply", &adagrad_apply);

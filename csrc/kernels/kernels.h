@@ -39,7 +39,8 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
 //   inverse: inverse[i] = position of keys[i]
 // `bounds` [P+1] are the shard key ranges (owner = upper_bound(bounds, key) - 1); P=1 with
 // bounds {0, 2^63} makes it a plain unique. Work buffers are provided by the caller:
-// table_keys/table_pos [cap] (cap power of two >= 2n), slot [n], flags [n], counts [P],
+// table_keys/table_pos [cap] (cap power of two >= 2n), slot [n], flags [n], counts [P+1]
+// (counts[P] = total unique on return),
 // cursor [P] (all state re-initialised inside).
 // keys may be a [B, F] batch (F > 1): tiles are then taken feature-major for better dedupe.
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
@@ -48,8 +49,10 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
 
 // Row gather from a shard: out[i, :] = table[keys[i] - base, :] with dtype conversion.
 // table fp32 [R, D] row stride ld; out fp32 or bf16 [n, D].
+// n_dev (nullable, here and below): device-side row count <= n (n then only sizes the grid),
+// so a table op can consume a count produced on the GPU without a host round trip.
 void gather_rows(const float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, void* out,
-                 bool out_bf16, hipStream_t s);
+                 bool out_bf16, hipStream_t s, const int64_t* n_dev = nullptr);
 // Lookup: out[b, f*D:(f+1)*D] = rows[inv[b*F+f], 0:D]  (bf16; D % 8 == 0).
 void lookup_rows(const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B, int F, int D, bf16_t* out, int ldo,
                  hipStream_t s);
@@ -60,10 +63,11 @@ void scatter_add_rows_bf16(const bf16_t* src, int64_t n, int D, const int64_t* i
 //   s[row] += mean(g^2); w[row,:] -= lr * g / (sqrt(s[row]) + eps)
 // Columns [D1, D) may use a second accumulator state2 (D1 = D: single group).
 void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
-                            int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s);
+                            int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s,
+                            const int64_t* n_dev = nullptr);
 // Plain SGD on rows: w[row,:] += scale * g  (the reference's "w += delta" server apply)
 void sparse_sgd(float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, const float* grads,
-                float scale, hipStream_t s);
+                float scale, hipStream_t s, const int64_t* n_dev = nullptr);
 
 // EmbeddingBag (sum/mean) over an [R, D] table (fp32 or bf16 rows via gathered buffer):
 //   out[b, :] = pool_{j in bag b} rows[idx[j], :]   offsets [B+1]
@@ -95,9 +99,11 @@ void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t
 // Segment-sum form of the embedding backward: grad_rows[u] = sum over lookups j with
 // inv[j] == u for every row u < U (zero-filled first, padding included); lookups are grouped
 // by row (count / scan / fill) and summed piecewise, float atomics only where a piece boundary
-// cuts a row. ws: (3U + 2 + 2*B*F + U/1024) int32 workspace.
+// cuts a row. ws: (3U + 2 + 2*B*F + U/1024) int32 workspace. U_dev (nullable): the device-side
+// unique count (U is then its upper bound; only rows < *U_dev are zero-filled).
 void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,
-                          int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s);
+                          int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s,
+                          const int64_t* U_dev = nullptr);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                           float* grad_rows, int row_stride, hipStream_t s);
 

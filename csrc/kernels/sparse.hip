@@ -117,6 +117,12 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
   __syncthreads();
   for (int p = t; p < P; p += kUbTile)
     if (lcount[p]) atomicAdd(counts + p, (unsigned long long)lcount[p]);
+  if (t == 0) {
+    // counts[P] = total unique: the device-side U that consumers bound their loops by (no host sync)
+    unsigned long long blk = 0;
+    for (int p = 0; p < P; ++p) blk += lcount[p];
+    if (blk) atomicAdd(counts + P, blk);
+  }
   if (valid) {
     slot[phys] = lgslot[lslot];
     flags[phys] = claimed ? 1 : 0;
@@ -182,7 +188,7 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
   if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
   if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
   MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0xFF, cap * sizeof(int64_t), s));
-  MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, P * sizeof(int64_t), s));
+  MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, (P + 1) * sizeof(int64_t), s));  // counts[P] = total
   MINIPS_HIP_CHECK(hipMemsetAsync(cursor, 0, P * sizeof(int64_t), s));
   if (n == 0) return;
   const int block = 256;
@@ -197,10 +203,13 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
 }
 
 // --------------------------------------------------------------------------- gather
+// n_dev (nullable): device-side row count (<= n, the grid's upper bound)
+__device__ __forceinline__ int64_t dev_count(int64_t n, const int64_t* n_dev) { return n_dev ? min(n, *n_dev) : n; }
+
 template <bool BF16>
 __global__ void gather_rows_vec4(const float* __restrict__ table, int64_t ld, const int64_t* __restrict__ keys,
-                                 int64_t n, int64_t base, int D4, void* out) {
-  const int64_t total = n * D4;
+                                 int64_t n, int64_t base, int D4, void* out, const int64_t* n_dev) {
+  const int64_t total = dev_count(n, n_dev) * D4;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = c / D4;
     const int d4 = (int)(c - i * D4);
@@ -218,8 +227,8 @@ __global__ void gather_rows_vec4(const float* __restrict__ table, int64_t ld, co
 
 template <bool BF16>
 __global__ void gather_rows_scalar(const float* __restrict__ table, int64_t ld, const int64_t* __restrict__ keys,
-                                   int64_t n, int64_t base, int D, void* out) {
-  const int64_t total = n * D;
+                                   int64_t n, int64_t base, int D, void* out, const int64_t* n_dev) {
+  const int64_t total = dev_count(n, n_dev) * D;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = c / D;
     const int d = (int)(c - i * D);
@@ -232,21 +241,21 @@ __global__ void gather_rows_scalar(const float* __restrict__ table, int64_t ld, 
 }
 
 void gather_rows(const float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, void* out,
-                 bool out_bf16, hipStream_t s) {
+                 bool out_bf16, hipStream_t s, const int64_t* n_dev) {
   if (n <= 0) return;
   const int block = 256;
   if (D % 4 == 0 && ld % 4 == 0) {
     const int grid = grid_for(n * (D / 4), block);
     if (out_bf16)
-      hipLaunchKernelGGL(gather_rows_vec4<true>, grid, block, 0, s, table, ld, keys, n, base, D / 4, out);
+      hipLaunchKernelGGL(gather_rows_vec4<true>, grid, block, 0, s, table, ld, keys, n, base, D / 4, out, n_dev);
     else
-      hipLaunchKernelGGL(gather_rows_vec4<false>, grid, block, 0, s, table, ld, keys, n, base, D / 4, out);
+      hipLaunchKernelGGL(gather_rows_vec4<false>, grid, block, 0, s, table, ld, keys, n, base, D / 4, out, n_dev);
   } else {
     const int grid = grid_for(n * D, block);
     if (out_bf16)
-      hipLaunchKernelGGL(gather_rows_scalar<true>, grid, block, 0, s, table, ld, keys, n, base, D, out);
+      hipLaunchKernelGGL(gather_rows_scalar<true>, grid, block, 0, s, table, ld, keys, n, base, D, out, n_dev);
     else
-      hipLaunchKernelGGL(gather_rows_scalar<false>, grid, block, 0, s, table, ld, keys, n, base, D, out);
+      hipLaunchKernelGGL(gather_rows_scalar<false>, grid, block, 0, s, table, ld, keys, n, base, D, out, n_dev);
   }
   MINIPS_HIP_CHECK(hipGetLastError());
 }
@@ -289,7 +298,9 @@ void scatter_add_rows_bf16(const bf16_t* src, int64_t n, int D, const int64_t* i
 // keeps the deep embedding and the wide weight in one row, each with its own Adagrad state).
 __global__ void sparse_rowwise_adagrad_half_kernel(float* table, int64_t ld, float* state, float* state2, int D1,
                                                    const int64_t* __restrict__ keys, int64_t n, int64_t base, int D,
-                                                   const float* __restrict__ grads, float lr, float eps) {
+                                                   const float* __restrict__ grads, float lr, float eps,
+                                                   const int64_t* n_dev) {
+  n = dev_count(n, n_dev);
   const int lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -326,7 +337,9 @@ __global__ void sparse_rowwise_adagrad_half_kernel(float* table, int64_t ld, flo
 
 __global__ void sparse_rowwise_adagrad_kernel(float* table, int64_t ld, float* state, float* state2, int D1,
                                               const int64_t* __restrict__ keys, int64_t n, int64_t base, int D,
-                                              const float* __restrict__ grads, float lr, float eps) {
+                                              const float* __restrict__ grads, float lr, float eps,
+                                              const int64_t* n_dev) {
+  n = dev_count(n, n_dev);
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -355,24 +368,25 @@ __global__ void sparse_rowwise_adagrad_kernel(float* table, int64_t ld, float* s
 }
 
 void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
-                            int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s) {
+                            int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s,
+                            const int64_t* n_dev) {
   if (n <= 0) return;
   if (D1 <= 0 || D1 > D) D1 = D;
   if (D1 < D && !state2) throw std::runtime_error("sparse_rowwise_adagrad: split rows need state2");
   const int block = 256;
   if (D <= 64) {
     hipLaunchKernelGGL(sparse_rowwise_adagrad_half_kernel, grid_for(n * 32, block, 8192), block, 0, s, table, ld,
-                       state, state2, D1, keys, n, base, D, grads, lr, eps);
+                       state, state2, D1, keys, n, base, D, grads, lr, eps, n_dev);
   } else {
     hipLaunchKernelGGL(sparse_rowwise_adagrad_kernel, grid_for(n * 64, block, 4096), block, 0, s, table, ld, state,
-                       state2, D1, keys, n, base, D, grads, lr, eps);
+                       state2, D1, keys, n, base, D, grads, lr, eps, n_dev);
   }
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 __global__ void sparse_sgd_kernel(float* table, int64_t ld, const int64_t* __restrict__ keys, int64_t n, int64_t base,
-                                  int D, const float* __restrict__ grads, float scale) {
-  const int64_t total = n * D;
+                                  int D, const float* __restrict__ grads, float scale, const int64_t* n_dev) {
+  const int64_t total = dev_count(n, n_dev) * D;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = c / D;
     const int d = (int)(c - i * D);
@@ -381,10 +395,10 @@ __global__ void sparse_sgd_kernel(float* table, int64_t ld, const int64_t* __res
 }
 
 void sparse_sgd(float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, const float* grads,
-                float scale, hipStream_t s) {
+                float scale, hipStream_t s, const int64_t* n_dev) {
   if (n <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(sparse_sgd_kernel, grid_for(n * D, block), block, 0, s, table, ld, keys, n, base, D, grads, scale);
+  hipLaunchKernelGGL(sparse_sgd_kernel, grid_for(n * D, block), block, 0, s, table, ld, keys, n, base, D, grads, scale, n_dev);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

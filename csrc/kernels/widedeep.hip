@@ -571,9 +571,16 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
   }
 }
 
+// Zero rows [0, min(U, *U_dev)) of an fp32 [*, stride] matrix (float4 stores; stride % 4 == 0).
+__global__ void zero_rows_dev_kernel(float* __restrict__ rows, int stride, int64_t U, const int64_t* __restrict__ U_dev) {
+  const int64_t n = min(U, *U_dev) * (stride >> 2);
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<float4*>(rows)[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 template <typename TX>
 static void emb_backward_seg(const TX* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
-                             float* grad_rows, int row_stride, int U, int* ws, hipStream_t s) {
+                             float* grad_rows, int row_stride, int U, int* ws, hipStream_t s, const int64_t* U_dev) {
   // ws: counts[U] | cursor[U] | offsets[U+1] | members[B*F] | memrow[B*F] | tiles[U/1024+1]
   const int total = (int)(B * F);
   int* counts = ws;
@@ -584,7 +591,11 @@ static void emb_backward_seg(const TX* dX, int ldx, const float* dwide, const in
   int* tiles = memrow + total;
   const int ntiles = (U + kScanTile - 1) / kScanTile;
   MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int) * 2 * (size_t)U, s));  // counts, cursor
-  MINIPS_HIP_CHECK(hipMemsetAsync(grad_rows, 0, sizeof(float) * (size_t)U * row_stride, s));
+  if (U_dev && row_stride % 4 == 0)
+    hipLaunchKernelGGL(zero_rows_dev_kernel, grid_for((int64_t)U * (row_stride / 4), 256, 4096), 256, 0, s, grad_rows,
+                       row_stride, (int64_t)U, U_dev);
+  else
+    MINIPS_HIP_CHECK(hipMemsetAsync(grad_rows, 0, sizeof(float) * (size_t)U * row_stride, s));
   dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);
   hipLaunchKernelGGL(emb_seg_count_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, counts);
   hipLaunchKernelGGL(emb_scan_reduce_kernel, ntiles, 256, 0, s, counts, U, tiles);
@@ -614,13 +625,14 @@ static void emb_backward_seg(const TX* dX, int ldx, const float* dwide, const in
 }
 
 void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,
-                          int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s) {
+                          int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s,
+                          const int64_t* U_dev) {
   if (B <= 0 || U <= 0) return;
   if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("emb_backward_segment: row_stride too small");
   if (bf16)
-    emb_backward_seg(static_cast<const bf16_t*>(dX), ldx, dwide, inv, B, F, D, grad_rows, row_stride, U, ws, s);
+    emb_backward_seg(static_cast<const bf16_t*>(dX), ldx, dwide, inv, B, F, D, grad_rows, row_stride, U, ws, s, U_dev);
   else
-    emb_backward_seg(static_cast<const float*>(dX), ldx, dwide, inv, B, F, D, grad_rows, row_stride, U, ws, s);
+    emb_backward_seg(static_cast<const float*>(dX), ldx, dwide, inv, B, F, D, grad_rows, row_stride, U, ws, s, U_dev);
 }
 
 }  // namespace minips_k

@@ -86,15 +86,24 @@ class DLRM:
             )
         return self._bufs[B]
 
-    def train_step(self, dense, keys, labels):
+    def prefetch(self, keys):
+        """Lookahead key planning of the next batch (see WideDeep.prefetch)."""
+        self._next_plan = (keys, self.emb.plan_async(keys))
+
+    def train_step(self, dense, keys, labels, next_keys=None):
         cfg = self.cfg
         B, F, D = dense.shape[0], cfg.F, cfg.D
         b = self._buffers(B)
-        rows, plan = self.emb.get(keys)
-        P = self.dense.get()
+        pre = getattr(self, "_next_plan", None)
+        plan = pre[1] if pre is not None and pre[0] is keys else None
+        self._next_plan = None
+        if next_keys is not None:
+            self.prefetch(next_keys)
+        rows, plan = self.emb.get(keys, plan=plan)
         G = self.dense.grad
         # V = [emb_0 .. emb_{F-1} | bottom(dense)]  (the dense vector is the last one)
         ops.lookup_rows(rows, plan.inv, F, D, b["V"])
+        P = self.dense.get()
         ba = b["bacts"]
         ba[0][:, : cfg.n_dense].copy_(dense)
         for i, l in enumerate(self.bottom):
@@ -111,10 +120,13 @@ class DLRM:
         b["loss"].zero_()
         ops.wd_head(b["H"], hw[:h], hw[h:h + 1], b["zero"], labels, b["dH"], hg[:h], hg[h:h + 1], b["dwide"],
                     b["loss"], None, 1.0 / (B * self.comm.world))
+        # dgrad chain first (top MLP -> interaction), then the embedding gradient goes out on the
+        # sparse push lane while the weight-gradient GEMMs run on the compute stream
         dy = b["dH"]
+        dys = []
         for i in range(len(self.top) - 1, -1, -1):
             l = self.top[i]
-            l.wgrad(G, dy, ta[i])
+            dys.append((l, dy, ta[i]))
             if i > 0:
                 dx = b["tgrads"][i - 1]
                 l.dgrad(P, dy, dx, mask=ta[i])
@@ -123,6 +135,14 @@ class DLRM:
                 l.dgrad(P, dy, dx)
             dy = dx
         ops.dlrm_interact_bwd(b["V"], self.NV, D, b["dI"], b["dV"], b["dbot"], dense_idx=F)
+        dev = self.comm.device
+        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), D, dtype=torch.float32,
+                                                                         device=dev)
+        ops.wd_emb_backward(b["dV"], None, plan.inv, F, D, grad_rows, x_off=0, U_dev=plan.U_dev)
+        self.emb.add(plan, grad_rows)
+        self.emb.clock()
+        for l, g_out, x_in in dys:
+            l.wgrad(G, g_out, x_in)
         dy = b["dbot"]
         for i in range(len(self.bottom) - 1, -1, -1):
             l = self.bottom[i]
@@ -131,11 +151,7 @@ class DLRM:
                 dx = b["bgrads"][i - 1]
                 l.dgrad(P, dy, dx, mask=ba[i])
                 dy = dx
-        grad_rows = torch.zeros(max(plan.U, 1), D, dtype=torch.float32, device=self.comm.device)
-        ops.wd_emb_backward(b["dV"], None, plan.inv, F, D, grad_rows, x_off=0)
-        self.emb.add(plan, grad_rows)
         self.dense.add()
-        self.emb.clock()
         self.dense.clock()
         return b["loss"]
 

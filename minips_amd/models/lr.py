@@ -34,10 +34,11 @@ class SparseLR:
         Returns the number of correctly classified rows (before the update)."""
         dev = self.comm.device
         rows, plan = self.table.get(cols)
-        delta = torch.zeros(plan.U, dtype=torch.float32, device=dev)
+        delta = torch.zeros(max(plan.cap, 1), dtype=torch.float32, device=dev)
         correct = torch.zeros(1, dtype=torch.float32, device=dev)
-        if plan.U:
-            ops.lr_sparse_step(rowptr, plan.inv, vals, labels, rows.view(-1), self.cfg.alpha, delta, correct)
+        if plan.cap:
+            ops.lr_sparse_step(rowptr, plan.inv, vals, labels, rows.view(-1)[: plan.cap], self.cfg.alpha,
+                               delta[: plan.cap], correct)
             self.table.add(plan, delta.view(-1, 1))
         self.table.clock()
         return correct

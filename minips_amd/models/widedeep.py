@@ -143,37 +143,55 @@ class WideDeep:
         w4 = self.view(P, "w4").float()
         return b["H3"].float() @ w4[:h] + w4[h] + b["wide"]
 
-    def train_step(self, dense, keys, labels) -> torch.Tensor:
+    def prefetch(self, keys):
+        """Lookahead: start routing the NEXT batch's keys (dedupe + count all-to-all on the
+        planning stream) so it overlaps the current step; train_step picks the plan up."""
+        self._next_plan = (keys, self.emb.plan_async(keys))
+
+    def train_step(self, dense, keys, labels, next_keys=None) -> torch.Tensor:
         """One BSP superstep: Get, forward, backward, Add, Clock. Returns the summed loss
-        (a device tensor; no host sync)."""
+        (a device tensor; no host sync).
+
+        Ordering for overlap (MI355X: RCCL on side streams, one communicator lane each):
+          sparse Get (gather + rows all-to-all) -> assemble -> dense Get (waits for the previous
+          dense Clock only here) -> forward -> head -> dgrad chain -> embedding backward ->
+          sparse Add+Clock (all-to-all of gradient rows + row-wise Adagrad on the push lane,
+          overlapping the weight-gradient GEMMs) -> wgrad GEMMs -> dense Add+Clock
+          (reduce-scatter + Adam + all-gather on the dense lane, overlapping the next step's
+          sparse Get). ``next_keys`` starts the next batch's key planning right away."""
         cfg = self.cfg
         B = dense.shape[0]
         F, D = cfg.F, cfg.emb_dim
         h = cfg.hidden[-1]
         b = self._buffers(B)
-        rows, plan = self.emb.get(keys)
-        P = self.dense.get()
+        pre = getattr(self, "_next_plan", None)
+        plan = pre[1] if pre is not None and pre[0] is keys else None
+        self._next_plan = None
+        if next_keys is not None:
+            self.prefetch(next_keys)
+        rows, plan = self.emb.get(keys, plan=plan)
         G = self.dense.grad
         ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0])
+        P = self.dense.get()
         self._forward(b, P)
         b["loss"].zero_()
         scale = 1.0 / (B * self.comm.world)
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1], b["dwide"],
                     b["loss"], None, scale)
-        ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=self.k_in[2], out=b["dH2"])
-        ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
-        ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
         ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
         dev = self.comm.device
-        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.U, 1), cfg.row_width,
+        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), cfg.row_width,
                                                                          dtype=torch.float32, device=dev)
-        ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows)
+        ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows, U_dev=plan.U_dev)
         self.emb.add(plan, grad_rows)
-        self.dense.add()
         self.emb.clock()
+        ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
+        ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
+        ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
+        self.dense.add()
         self.dense.clock()
         return b["loss"]
 

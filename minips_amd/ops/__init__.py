@@ -140,22 +140,32 @@ def unique_bucketize(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1):
     ``bounds`` [P+1] are the shard key boundaries and uniq[inverse[i]] == keys[i]. ``F`` > 1
     declares the flat keys as a [B, F] batch (the GPU kernel then dedupes feature-major tiles).
     """
+    uniq, inv, counts, _ = unique_bucketize_n(keys, bounds, F)
+    return uniq, inv, counts
+
+
+def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1):
+    """unique_bucketize plus the total unique count U as a 1-element device tensor, so that
+    consumers (gather_rows / sparse_* with ``n_dev``, wd_emb_backward with ``U_dev``) bound
+    their work on the GPU without a host round trip."""
     if _gpu(keys):
-        uniq, inv, counts = kernels().unique_bucketize(keys.contiguous(), bounds.contiguous(), int(F))
-        return uniq, inv, counts
+        return tuple(kernels().unique_bucketize(keys.contiguous(), bounds.contiguous(), int(F)))
     u, inv = torch.unique(keys, sorted=True, return_inverse=True)
     owner = torch.bucketize(u, bounds[1:-1], right=True)
     counts = torch.bincount(owner, minlength=bounds.numel() - 1)
     # sorted unique keys are already grouped by owner (ranges are contiguous)
     out = torch.empty_like(keys)
     out[: u.numel()] = u
-    return out, inv, counts
+    return out, inv, counts, torch.tensor([u.numel()], dtype=torch.int64)
 
 
-def gather_rows(table, keys, base, out):
+def gather_rows(table, keys, base, out, n_dev=None):
+    """out[i] = table[keys[i] - base] for i < n (n = keys.numel(), or the device count n_dev)."""
     if _gpu(keys):
-        kernels().gather_rows(table, keys, int(base), out)
+        kernels().gather_rows(table, keys, int(base), out, n_dev)
         return out
+    if n_dev is not None:
+        keys = keys[: int(n_dev.reshape(-1)[0])]
     rows = table[(keys - base), : out.shape[1]]
     out[: keys.numel()] = rows.to(out.dtype)
     return out
@@ -180,12 +190,16 @@ def scatter_add_rows(src, idx, acc):
     return acc
 
 
-def sparse_rowwise_adagrad(table, state, keys, base, grads, lr, eps=1e-8, state2=None, split=None):
+def sparse_rowwise_adagrad(table, state, keys, base, grads, lr, eps=1e-8, state2=None, split=None, n_dev=None):
     D = grads.shape[1]
     D1 = D if split is None else split
     if _gpu(table):
-        kernels().sparse_rowwise_adagrad(table, state, state2, D1, keys, int(base), grads, float(lr), float(eps))
+        kernels().sparse_rowwise_adagrad(table, state, state2, D1, keys, int(base), grads, float(lr), float(eps),
+                                         n_dev)
         return
+    if n_dev is not None:
+        n = int(n_dev.reshape(-1)[0])
+        keys, grads = keys[:n], grads[:n]
     rows = keys - base
     g1 = grads[:, :D1]
     s1 = state[rows] + (g1 * g1).mean(1)
@@ -198,10 +212,13 @@ def sparse_rowwise_adagrad(table, state, keys, base, grads, lr, eps=1e-8, state2
         table[rows, D1:D] -= lr * g2 / (s2.sqrt() + eps).unsqueeze(1)
 
 
-def sparse_sgd(table, keys, base, grads, scale):
+def sparse_sgd(table, keys, base, grads, scale, n_dev=None):
     if _gpu(table):
-        kernels().sparse_sgd(table, keys, int(base), grads, float(scale))
+        kernels().sparse_sgd(table, keys, int(base), grads, float(scale), n_dev)
         return
+    if n_dev is not None:
+        n = int(n_dev.reshape(-1)[0])
+        keys, grads = keys[:n], grads[:n]
     table.index_add_(0, keys - base, scale * grads, alpha=1.0) if grads.shape[1] == table.shape[1] else \
         table[:, : grads.shape[1]].index_add_(0, keys - base, scale * grads)
 
@@ -268,13 +285,13 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
         dH_colsum += g.float().sum(0)
 
 
-def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0):
+def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None):
     """grad_rows[u, :D] = sum of dX[b, x_off + f*D : ...] over the lookups (b, f) with
     inv[b*F+f] == u; column D likewise sums dwide[b] when given. On the GPU every row of
     grad_rows is written (rows without lookups become 0); the CPU reference adds into grad_rows,
     so callers pass a zeroed buffer."""
     if _gpu(dX):
-        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off))
+        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), U_dev)
         return grad_rows
     B = dX.shape[0]
     g = dX[:, x_off: x_off + F * D].float().reshape(B * F, D)

@@ -40,22 +40,52 @@ class Comm:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
         self.device = device
         self.stats = CommStats()
-        self._bg: Comm | None = None
+        self._lanes: dict[str, Comm] = {}
+        self._plan_stream = None
 
-    def background(self) -> "Comm":
-        """A second communicator over the same ranks for collectives issued on a side HIP stream
-        (SSP/ASP clock work): RCCL kernels of ONE communicator running concurrently from two
-        streams may wait on each other, two communicators progress independently. Creating it
-        is collective (first call on every rank, in the same order)."""
+    def lane(self, name: str) -> "Comm":
+        """A named extra communicator over the same ranks, for collectives issued on their own HIP
+        stream (key planning, sparse push, dense clock): ops of ONE communicator are serialised
+        in issue order, so work that must overlap needs separate communicators, which progress
+        independently. Creating one is collective (first call on every rank, in the same order
+        -- the tables do it in their constructors)."""
         if self.world == 1:
             return self
-        if self._bg is None:
+        if name not in self._lanes:
             ranks = list(range(self.world)) if self.group is None else dist.get_process_group_ranks(self.group)
-            self._bg = Comm(group=dist.new_group(ranks), device=self.device)
-            self._bg.stats = self.stats  # one byte account per rank
-        return self._bg
+            c = Comm(group=dist.new_group(ranks), device=self.device)
+            c.stats = self.stats  # one byte account per rank
+            self._lanes[name] = c
+        return self._lanes[name]
+
+    def background(self) -> "Comm":
+        """The side-stream communicator of SSP/ASP clock work (see lane())."""
+        return self.lane("bg")
+
+    def plan_stream(self):
+        """The HIP stream on which lookahead key planning runs (one per rank, shared by tables)."""
+        if self._plan_stream is None and self.device.type == "cuda":
+            self._plan_stream = torch.cuda.Stream(device=self.device)
+        return self._plan_stream
 
     # -- helpers ------------------------------------------------------------------------
+    def _staged(self, *ts) -> bool:
+        """GPU tensors over a gloo group: the multi-rank GPU TEST harness (several ranks sharing
+        one card, where RCCL refuses duplicate devices) stages them through host memory, so the
+        streams / lanes / lookahead logic runs on the GPU at world > 1. Never a production path:
+        init_distributed() picks RCCL whenever GPUs are present."""
+        return self.backend == "gloo" and any(t.is_cuda for t in ts)
+
+    @staticmethod
+    def _host(t: torch.Tensor) -> torch.Tensor:
+        # gloo moves raw 16-bit payloads as fp16 bit patterns (it has no bf16 / int16 path)
+        t = t.detach().cpu()
+        return t.view(torch.float16) if t.dtype == torch.bfloat16 else t
+
+    @staticmethod
+    def _back(dst: torch.Tensor, host: torch.Tensor):
+        dst.copy_(host.view(dst.dtype) if dst.dtype == torch.bfloat16 else host)
+
     def all_to_all_v(self, out: torch.Tensor, inp: torch.Tensor, recv_splits: list[int], send_splits: list[int],
                      p2p: bool = False):
         """Rows of ``inp`` split by ``send_splits`` go to ranks 0..P-1; ``out`` gets recv_splits.
@@ -63,6 +93,11 @@ class Comm:
         p2p=True issues the exchange as grouped point-to-point send/recv pairs (one per peer
         with a non-empty message, the own segment copied locally) -- the SSP/ASP data path;
         otherwise one RCCL all-to-all-v."""
+        if self.world > 1 and self._staged(out, inp):
+            o = self._host(out[: sum(recv_splits)])
+            self.all_to_all_v(o, self._host(inp[: sum(send_splits)]), recv_splits, send_splits, p2p)
+            self._back(out[: sum(recv_splits)], o)
+            return out
         self.stats.calls += 1
         if self.world == 1:
             n = send_splits[0]
@@ -96,17 +131,34 @@ class Comm:
                 r.wait()
         return out
 
+    def all_to_all_counts(self, recv: torch.Tensor, counts: torch.Tensor):
+        """Device-side all-to-all of per-destination counts (no host sync)."""
+        if self.world == 1:
+            recv.copy_(counts)
+        elif self._staged(recv, counts):
+            r = torch.empty(recv.shape, dtype=recv.dtype)
+            dist.all_to_all_single(r, counts.cpu(), group=self.group)
+            recv.copy_(r)
+        else:
+            dist.all_to_all_single(recv, counts, group=self.group)
+        return recv
+
     def exchange_counts(self, counts: torch.Tensor) -> tuple[list[int], list[int]]:
         """all-to-all of per-destination counts; returns (send, recv) as host lists (1 sync)."""
         if self.world == 1:
             c = counts.tolist()
             return c, c
         recv = torch.empty_like(counts)
-        dist.all_to_all_single(recv, counts, group=self.group)
+        self.all_to_all_counts(recv, counts)
         both = torch.stack([counts, recv]).cpu()
         return both[0].tolist(), both[1].tolist()
 
     def reduce_scatter(self, out_shard: torch.Tensor, inp: torch.Tensor):
+        if self.world > 1 and self._staged(out_shard, inp):
+            o = torch.empty(out_shard.shape, dtype=out_shard.dtype)
+            self.reduce_scatter(o, inp.cpu())
+            out_shard.copy_(o)
+            return out_shard
         self.stats.calls += 1
         if self.world == 1:
             out_shard.copy_(inp)
@@ -116,6 +168,11 @@ class Comm:
         return out_shard
 
     def all_gather(self, out_full: torch.Tensor, shard: torch.Tensor):
+        if self.world > 1 and self._staged(out_full, shard):
+            o = self._host(out_full)
+            self.all_gather(o, self._host(shard).clone())
+            self._back(out_full, o)
+            return out_full
         self.stats.calls += 1
         if self.world == 1:
             if out_full.data_ptr() != shard.data_ptr():
@@ -131,6 +188,11 @@ class Comm:
     def all_reduce_(self, t: torch.Tensor, op=None):
         if self.world == 1:
             return t
+        if self._staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=op or dist.ReduceOp.SUM, group=self.group)
+            t.copy_(h)
+            return t
         dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
         return t
 
@@ -138,7 +200,7 @@ class Comm:
         if self.world == 1:
             return
         t = torch.zeros(1, device=self.device)
-        dist.all_reduce(t, group=self.group)
+        self.all_reduce_(t)
         if t.is_cuda:
             torch.cuda.synchronize(self.device)
 

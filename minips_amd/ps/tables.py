@@ -25,6 +25,7 @@ the collectives), which is exactly the SSP read guarantee (ssp_model.cpp:58-85).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -40,13 +41,31 @@ def even_bounds(num_rows: int, parts: int) -> list[int]:
     return b
 
 
-class _Pipeline:
-    """Tracks in-flight Clock work for SSP/ASP tables on a side stream."""
+def _overlap_default() -> bool:
+    return os.environ.get("MINIPS_OVERLAP", "1") != "0"
 
-    def __init__(self, comm: Comm, consistency: str, staleness: int):
+
+class _Pipeline:
+    """Tracks in-flight Clock work issued on a side HIP stream.
+
+    On the GPU every consistency model runs the Clock's communication + apply on the table's
+    own stream (and its own communicator lane) and gates READS instead of the issue: a Get at
+    clock c waits only for the update of clock c - s - 1. BSP is s = 0 (the Get waits for the
+    previous Clock -- the reference rule that Gets after a Clock see the new values), but the
+    Clock itself now overlaps with whatever the worker does before its next Get (the rest of
+    the backward pass, the next batch's key planning and dense assembly). SSP(s) relaxes the
+    gate to s clocks, ASP to a fixed pipelining depth. On CPU (gloo tests) the work runs inline.
+    """
+
+    def __init__(self, comm: Comm, consistency: str, staleness: int, overlap: bool | None = None):
         self.consistency = consistency
         self.staleness = staleness if consistency == "ssp" else (0 if consistency == "bsp" else 2)
-        self.async_ = consistency in ("ssp", "asp") and comm.device.type == "cuda" and self.staleness > 0
+        overlap = _overlap_default() if overlap is None else overlap
+        if consistency == "bsp":
+            # one rank has no communication to hide: the extra stream hops only cost (measured)
+            self.async_ = comm.device.type == "cuda" and overlap and comm.world > 1
+        else:
+            self.async_ = comm.device.type == "cuda" and self.staleness > 0
         self.stream = torch.cuda.Stream(device=comm.device) if self.async_ else None
         self.events: dict[int, torch.cuda.Event] = {}
         self.clock = 0
@@ -118,12 +137,12 @@ class DenseTable:
         self.grad_shard = torch.zeros(self.shard, dtype=torch.float32, device=dev)
         self.step = 0
         self.pipe = _Pipeline(comm, consistency, staleness)
-        if self.pipe.async_:
-            comm.background()  # collective: create the side-stream communicator up front
+        # collective: this table's clock communicator is created up front, in constructor order
+        self.lane = comm.lane(f"dense{table_id}") if self.pipe.async_ else comm
         self._pending = False
-        # SSP/ASP: a ring of staleness+1 gradient buffers, so the side stream reduces clock t's
-        # gradients while the compute stream already writes clock t+1's.
-        self._ring = [self.grad] + [torch.zeros_like(self.grad) for _ in range(self.pipe.staleness)] \
+        # async clocks: a ring of staleness+2 gradient buffers, so the side stream reduces clock
+        # t's gradients while the compute stream already writes clock t+1's.
+        self._ring = [self.grad] + [torch.zeros_like(self.grad) for _ in range(self.pipe.staleness + 1)] \
             if self.pipe.async_ else [self.grad]
 
     # -- init / views -----------------------------------------------------------------------
@@ -137,6 +156,7 @@ class DenseTable:
 
     def full_master(self) -> torch.Tensor:
         """All-gather of the fp32 master (checkpoint / tests)."""
+        self.drain()
         out = torch.empty(self.n_pad, dtype=torch.float32, device=self.comm.device)
         self.comm.all_gather(out, self.master)
         return out[: self.n_params]
@@ -159,7 +179,7 @@ class DenseTable:
         pending = self._pending
         self._pending = False
 
-        comm = self.comm.background() if self.pipe.async_ else self.comm
+        comm = self.lane
 
         def work():
             if pending:
@@ -202,6 +222,7 @@ class DenseTable:
     def shard_state(self):
         """(meta, {name: tensor}) of the owned shard: fp32 master + optimizer state, padding
         beyond n_params excluded."""
+        self.drain()
         rows = max(0, min(self.shard, self.n_params - self.base))
         arrays = {"master": self.master[:rows]}
         if self.m is not None:
@@ -237,20 +258,40 @@ class DenseTable:
 
 @dataclass
 class SparsePlan:
+    """Routing of one batch's keys. Row counts are host ints on multi-rank runs (the all-to-all
+    splits need them anyway); on one rank the unique count stays on the GPU (``U_dev``) and
+    buffers are sized by the upper bound ``cap`` -- no host round trip per step."""
     keys_n: int
     inv: torch.Tensor          # [n] position of each requested key in the unique order
     uniq: torch.Tensor         # [n] unique keys grouped by owner (first U valid)
-    U: int
-    send: list                 # keys requested from each owner
-    recv: list                 # keys each requester asked from me
+    cap: int                   # rows to allocate for per-unique-key buffers (>= U)
+    send: list | None          # keys requested from each owner
+    recv: list | None          # keys each requester asked from me
     recv_keys: torch.Tensor    # [M] keys I serve (grouped by requester)
+    U_dev: torch.Tensor | None = None   # [1] device-side U (None: cap == U exactly)
     own_uniq: torch.Tensor | None = None
     own_inv: torch.Tensor | None = None
-    own_U: int = 0
+    own_U_dev: torch.Tensor | None = None
     extra: dict = field(default_factory=dict)
+    _U: int | None = None
+
+    @property
+    def U(self) -> int:
+        """Exact unique-key count (host; syncs once when only the device count exists)."""
+        if self._U is None:
+            self._U = self.cap if self.U_dev is None else int(self.U_dev.item())
+        return self._U
+
+
+class _PendingPlan:
+    """A plan whose dedupe + count exchange was issued on the planning stream (lookahead)."""
+    __slots__ = ("keys", "F", "flat", "uniq", "inv", "counts", "U_dev", "host", "event")
 
 
 class SparseTable:
+    # hash tables need exact host counts (insert-on-miss must not see padding keys)
+    _exact_counts = False
+
     def __init__(self, comm: Comm, num_rows: int, width: int, optimizer: str = "rowwise_adagrad",
                  lr: float = 0.01, eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "bsp",
                  staleness: int = 0, split: int | None = None, table_id: int = 0, init_std: float = 0.01,
@@ -282,12 +323,19 @@ class SparseTable:
         self.state = torch.zeros(self.rows_local, dtype=torch.float32, device=dev) \
             if optimizer == "rowwise_adagrad" else None
         self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
+        self._init_comm(consistency, staleness, p2p)
+
+    def _init_comm(self, consistency, staleness, p2p):
+        comm = self.comm
         self.pipe = _Pipeline(comm, consistency, staleness)
-        if self.pipe.async_:
-            comm.background()  # collective: create the side-stream communicator up front
+        # collective, in constructor order on every rank: the push lane (side-stream clock work)
+        # and the planning lane (lookahead dedupe + count exchange)
+        self.lane = comm.lane(f"sparse{self.table_id}") if self.pipe.async_ else comm
+        self.plan_lane = comm.lane("plan") if comm.device.type == "cuda" else comm
         # SSP/ASP move rows with point-to-point send/recv by default, BSP with all-to-all-v
         self.p2p = (consistency != "bsp") if p2p is None else p2p
         self._pending: list = []
+        self._own_bounds = torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=comm.device)
 
     # -- KV API -----------------------------------------------------------------------------
     def _route_keys(self, keys: torch.Tensor) -> torch.Tensor:
@@ -302,39 +350,90 @@ class SparseTable:
         """(row index tensor, base) of owned unique keys being updated."""
         return keys, self.base
 
-    def plan(self, keys: torch.Tensor) -> SparsePlan:
-        F = keys.shape[1] if keys.dim() == 2 else 1
-        keys = self._route_keys(keys.reshape(-1).to(torch.int64))
-        uniq, inv, counts = ops.unique_bucketize(keys, self.bounds, F)
-        send, recv = self.comm.exchange_counts(counts)
-        U = int(sum(send))
-        M = int(sum(recv))
+    def _start_plan(self, keys: torch.Tensor) -> _PendingPlan:
+        """Dedupe + owner bucketing + all-to-all of the per-owner counts, issued on the current
+        stream; the counts land in pinned host memory behind an event."""
+        pp = _PendingPlan()
+        pp.keys = keys
+        pp.F = keys.shape[1] if keys.dim() == 2 else 1
+        pp.flat = self._route_keys(keys.reshape(-1).to(torch.int64))
+        pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.unique_bucketize_n(pp.flat, self.bounds, pp.F)
+        pp.host = pp.event = None
+        if self.comm.world > 1:
+            recv = torch.empty_like(pp.counts)
+            self.plan_lane.all_to_all_counts(recv, pp.counts)
+            both = torch.stack([pp.counts, recv])
+            if both.is_cuda:
+                pp.host = torch.empty(both.shape, dtype=both.dtype, pin_memory=True)
+                pp.host.copy_(both, non_blocking=True)
+                pp.event = torch.cuda.Event()
+                pp.event.record()
+            else:
+                pp.host = both
+        return pp
+
+    def plan_async(self, keys: torch.Tensor):
+        """Lookahead: start planning ``keys`` (a LATER batch) on the planning stream, so its
+        dedupe and count exchange overlap the current step; pass the result to get(plan=...).
+        Planning reads no table state, so issuing it early changes no consistency semantics."""
+        if self.comm.device.type != "cuda" or self._exact_counts:
+            return self.plan(keys)
+        ps = self.comm.plan_stream()
+        cur = torch.cuda.current_stream(self.comm.device)
+        ps.wait_stream(cur)  # the keys are produced on the compute stream
+        with torch.cuda.stream(ps):
+            pp = self._start_plan(keys)
+        keys.record_stream(ps)
+        for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev):
+            t.record_stream(cur)  # produced on the planning stream, consumed on the compute stream
+        if pp.event is None:
+            pp.event = torch.cuda.Event()
+            pp.event.record(ps)
+        return pp
+
+    def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
+        dev = self.comm.device
+        n = pp.flat.numel()
+        if pp.event is not None:
+            torch.cuda.current_stream(dev).wait_event(pp.event)
         if self.comm.world == 1:
-            recv_keys = uniq[:M]
-        else:
-            recv_keys = torch.empty(M, dtype=torch.int64, device=keys.device)
-            self.comm.all_to_all_v(recv_keys, uniq, recv, send, p2p=self.p2p)
-        p = SparsePlan(keys.numel(), inv, uniq, U, send, recv, recv_keys)
-        if self.comm.world > 1 and M > 0:
-            own_bounds = torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=keys.device)
-            ou, oi, oc = ops.unique_bucketize(recv_keys, own_bounds)
-            p.own_uniq, p.own_inv = ou, oi
-            p.own_U = M if oc.numel() == 0 else int(oc.sum().item())
+            if self._exact_counts or dev.type != "cuda":
+                U = int(pp.U_dev.item())
+                return SparsePlan(n, pp.inv, pp.uniq, U, [U], [U], pp.uniq[:U], _U=U)
+            return SparsePlan(n, pp.inv, pp.uniq, n, None, None, pp.uniq, U_dev=pp.U_dev)
+        if pp.event is not None:
+            pp.event.synchronize()  # the only host wait of a step: the all-to-all splits
+        send, recv = pp.host[0].tolist(), pp.host[1].tolist()
+        U, M = int(sum(send)), int(sum(recv))
+        recv_keys = torch.empty(M, dtype=torch.int64, device=dev)
+        self.comm.all_to_all_v(recv_keys, pp.uniq, recv, send, p2p=self.p2p)
+        p = SparsePlan(n, pp.inv, pp.uniq, U, send, recv, recv_keys, _U=U)
+        if M > 0:
+            # owner-side dedupe of the keys requested by all ranks (the push sums their rows)
+            ou, oi, _, oU = ops.unique_bucketize_n(recv_keys, self._own_bounds)
+            p.own_uniq, p.own_inv, p.own_U_dev = ou, oi, oU
+            if self._exact_counts:
+                p.extra["own_U"] = int(oU.item())
         return p
 
-    def get(self, keys: torch.Tensor, plan: SparsePlan | None = None):
-        """Pull rows of ``keys``. Returns (rows [U, width] in unique order, plan); the row of
-        keys[i] is rows[plan.inv[i]]."""
-        self.pipe.wait_for_read()
+    def plan(self, keys: torch.Tensor) -> SparsePlan:
+        return self._finish_plan(self._start_plan(keys))
+
+    def get(self, keys: torch.Tensor, plan=None):
+        """Pull rows of ``keys``. Returns (rows [cap, width] in unique order, plan); the row of
+        keys[i] is rows[plan.inv[i]]. ``plan`` may be a plan_async() handle for these keys."""
         if plan is None:
             plan = self.plan(keys)
+        elif isinstance(plan, _PendingPlan):
+            plan = self._finish_plan(plan)
+        self.pipe.wait_for_read()  # BSP: the previous Clock's apply; SSP: clock c-s-1
         dev = self.comm.device
         served = torch.empty(len(plan.recv_keys), self.width, dtype=self.pull_dtype, device=dev)
         table, index, base = self._serve_index(plan)
-        ops.gather_rows(table, index, base, served)
+        ops.gather_rows(table, index, base, served, n_dev=plan.U_dev if self.comm.world == 1 else None)
         if self.comm.world == 1:  # the served rows ARE the requested rows: no exchange, no copy
             return served, plan
-        rows = torch.empty(plan.U, self.width, dtype=self.pull_dtype, device=dev)
+        rows = torch.empty(plan.cap, self.width, dtype=self.pull_dtype, device=dev)
         self.comm.all_to_all_v(rows, served, plan.send, plan.recv, p2p=self.p2p)
         return rows, plan
 
@@ -344,21 +443,22 @@ class SparseTable:
         return rows[plan.inv]
 
     def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
-        """Push gradient rows (aligned with the plan's unique order)."""
-        assert grad_rows.shape[0] >= plan.U and grad_rows.dtype == torch.float32
+        """Push gradient rows (aligned with the plan's unique order; rows >= U are ignored)."""
+        assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == torch.float32
         self._pending.append((plan, grad_rows))
 
     def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
         """Reference-style Add(keys, vals) (duplicates are summed)."""
         plan = self.plan(keys)
-        g = torch.zeros(max(plan.U, 1), self.width, dtype=torch.float32, device=self.comm.device)
+        g = torch.zeros(max(plan.cap, 1), self.width, dtype=torch.float32, device=self.comm.device)
         ops.scatter_add_rows(vals.reshape(keys.numel(), -1).to(torch.float32).contiguous(), plan.inv, g)
         self.add(plan, g)
 
     def clock(self):
         pending, self._pending = self._pending, []
         for plan, g in pending:
-            self.pipe.keep_alive(g, plan.uniq, plan.recv_keys, plan.own_uniq, plan.own_inv)
+            self.pipe.keep_alive(g, plan.uniq, plan.recv_keys, plan.own_uniq, plan.own_inv, plan.U_dev,
+                                 plan.own_U_dev)
 
         def work():
             for plan, grad_rows in pending:
@@ -369,32 +469,31 @@ class SparseTable:
     def _push(self, plan: SparsePlan, grad_rows: torch.Tensor):
         dev = self.comm.device
         if self.comm.world == 1:
-            keys, g, n = plan.uniq, grad_rows, plan.U
+            keys, g, n_dev, n = plan.uniq, grad_rows, plan.U_dev, plan.cap
         else:
             M = len(plan.recv_keys)
             recv = torch.empty(M, self.width, dtype=self.push_dtype, device=dev)
-            comm = self.comm.background() if self.pipe.async_ else self.comm
             send = grad_rows[: plan.U]
             if send.dtype != self.push_dtype:
                 send = send.to(self.push_dtype)
-            comm.all_to_all_v(recv, send, plan.recv, plan.send, p2p=self.p2p)
+            self.lane.all_to_all_v(recv, send, plan.recv, plan.send, p2p=self.p2p)
             if M == 0:
                 return
-            g = torch.zeros(plan.own_U, self.width, dtype=torch.float32, device=dev)
+            n = plan.extra.get("own_U", M)
+            g = torch.zeros(n, self.width, dtype=torch.float32, device=dev)
             ops.scatter_add_rows(recv, plan.own_inv, g)
-            keys, n = plan.own_uniq, plan.own_U
+            keys, n_dev = plan.own_uniq, (None if "own_U" in plan.extra else plan.own_U_dev)
         keys, base = self._owner_rows(keys[:n])
-        g = g[:n]
-        self._apply_rows(keys, base, g)
+        self._apply_rows(keys, base, g[:n], n_dev)
 
-    def _apply_rows(self, keys, base, g):
+    def _apply_rows(self, keys, base, g, n_dev=None):
         if self.optimizer == "rowwise_adagrad":
             ops.sparse_rowwise_adagrad(self.shard, self.state, keys, base, g, self.lr, self.eps,
-                                       state2=self.state2, split=self.split)
+                                       state2=self.state2, split=self.split, n_dev=n_dev)
         elif self.optimizer == "sgd":
-            ops.sparse_sgd(self.shard, keys, base, g.contiguous(), -self.lr)
+            ops.sparse_sgd(self.shard, keys, base, g.contiguous(), -self.lr, n_dev=n_dev)
         elif self.optimizer == "add":
-            ops.sparse_sgd(self.shard, keys, base, g.contiguous(), 1.0)
+            ops.sparse_sgd(self.shard, keys, base, g.contiguous(), 1.0, n_dev=n_dev)
         else:
             raise ValueError(self.optimizer)
 
@@ -403,6 +502,7 @@ class SparseTable:
 
     # -- checkpoint hooks (minips_amd.ps.checkpoint) -------------------------------------------
     def shard_state(self):
+        self.drain()
         arrays = {"params": self.shard}
         if self.state is not None:
             arrays["state"] = self.state
@@ -451,6 +551,8 @@ class HashSparseTable(SparseTable):
     touch -- zero (MapStorage's default-insert) or a deterministic per-key uniform init -- and
     grows (rehash, doubling) past 70% load. The Get/Add/Clock protocol is SparseTable's."""
 
+    _exact_counts = True
+
     def __init__(self, comm: Comm, width: int, capacity: int = 1 << 16, optimizer: str = "add", lr: float = 0.01,
                  eps: float = 1e-8, pull_dtype=torch.float32, consistency: str = "bsp", staleness: int = 0,
                  table_id: int = 0, init_std: float = 0.0, seed: int = 1234, p2p: bool | None = None,
@@ -474,11 +576,7 @@ class HashSparseTable(SparseTable):
         cap = 1 << max(4, int(capacity - 1).bit_length())
         self._alloc(cap)
         self.counters = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.pipe = _Pipeline(comm, consistency, staleness)
-        if self.pipe.async_:
-            comm.background()  # collective: create the side-stream communicator up front
-        self.p2p = (consistency != "bsp") if p2p is None else p2p
-        self._pending: list = []
+        self._init_comm(consistency, staleness, p2p)
 
     def _alloc(self, cap: int):
         dev = self.comm.device
@@ -526,6 +624,7 @@ class HashSparseTable(SparseTable):
 
     # -- checkpoint hooks: (key, row, state) triples of the occupied slots --------------------
     def shard_state(self):
+        self.drain()
         occ = self.tab_keys >= 0
         arrays = {"keys": self.tab_keys[occ].view(-1, 1), "params": self.shard[occ]}
         if self.state is not None:
