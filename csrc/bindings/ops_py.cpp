@@ -130,7 +130,8 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   auto opts = keys.options();
   auto table_keys = at::empty({cap}, opts), table_pos = at::empty({cap}, opts);
   auto slot = at::empty({n}, opts), flags = at::empty({n}, opts.dtype(at::kInt));
-  auto counts = at::empty({P + 1}, opts), cursor = at::empty({P}, opts);  // counts[P] = total unique
+  auto cbuf = at::empty({2 * P + 1}, opts);  // counts[P] | total | cursor[P] (one memset)
+  auto counts = cbuf.narrow(0, 0, P + 1), cursor = cbuf.narrow(0, P + 1, P);
   auto out_keys = at::empty({n}, opts), inverse = at::empty({n}, opts);
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   TORCH_CHECK(F >= 1 && n % F == 0, "unique_bucketize: numel must be a multiple of F");
@@ -283,8 +284,24 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
                     ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H));
 }
 
+// Lookup CSR grouped by unique row (members/memrow int32 [B*F]) for U (upper-bound) rows.
+std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t U) {
+  check_gpu(inv, "inv");
+  check_dtype(inv, at::kLong, "inv");
+  const int64_t n = inv.numel();
+  TORCH_CHECK(F >= 1 && n % F == 0 && U >= 1 && U < (1ll << 31) && n < (1ll << 31), "emb_build_csr shapes");
+  auto io = inv.options().dtype(at::kInt);
+  at::Tensor ws = at::empty({3 * U + 1 + U / 1024 + 1}, io);
+  at::Tensor members = at::empty({n}, io), memrow = at::empty({n}, io);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(inv.device());
+  minips_k::emb_build_csr(ptr<int64_t>(inv), n / F, (int)F, (int)U, ws.data_ptr<int>(), members.data_ptr<int>(),
+                          memrow.data_ptr<int>(), stream_of(inv));
+  return {members, memrow};
+}
+
 void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, const at::Tensor& inv, int64_t F,
-                     int64_t D, at::Tensor& grad_rows, int64_t x_off, const c10::optional<at::Tensor>& U_dev) {
+                     int64_t D, at::Tensor& grad_rows, int64_t x_off, const c10::optional<at::Tensor>& U_dev,
+                     const c10::optional<at::Tensor>& members, const c10::optional<at::Tensor>& memrow) {
   check_gpu(dX, "dX");
   const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
   check_gpu(inv, "inv");
@@ -304,6 +321,17 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
     // segment-sum path: overwrites rows [0, U) of grad_rows
     const int64_t U = grad_rows.size(0);
     TORCH_CHECK(grad_rows.stride(1) == 1, "grad_rows must be row-major");
+    const bool bf0 = dX.scalar_type() == at::kBFloat16;
+    const void* base0 = bf0 ? (const void*)(ptr<bf16_t>(dX) + x_off) : (const void*)(ptr<float>(dX) + x_off);
+    if (members.has_value() && members->defined()) {  // CSR prebuilt at planning time
+      TORCH_CHECK(memrow.has_value() && members->numel() == B * F && memrow->numel() == B * F &&
+                      members->scalar_type() == at::kInt && memrow->scalar_type() == at::kInt,
+                  "members/memrow: int32 [B*F]");
+      minips_k::emb_backward_csr(base0, bf0, (int)dX.stride(0), dw, B, (int)F, (int)D, members->data_ptr<int>(),
+                                 memrow->data_ptr<int>(), ptr<float>(grad_rows), (int)grad_rows.stride(0), (int)U,
+                                 stream_of(dX), count_ptr(U_dev));
+      return;
+    }
     at::Tensor ws = at::empty({3 * U + 1 + 2 * B * F + U / 1024 + 1}, inv.options().dtype(at::kInt));
     const bool bf = dX.scalar_type() == at::kBFloat16;
     const void* base = bf ? (const void*)(ptr<bf16_t>(dX) + x_off) : (const void*)(ptr<float>(dX) + x_off);
@@ -672,7 +700,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1);
   m.def("wd_head", &wd_head);
-  m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none());
+  m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
+        py::arg("members") = py::none(), py::arg("memrow") = py::none());
+  m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"));
   m.def("adam_apply", &adam_apply);
   m.def("sgd_apply", &sgd_apply);
   m.def("adagrad_apply", &adagrad_apply);

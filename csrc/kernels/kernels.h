@@ -104,6 +104,12 @@ void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t
 void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,
                           int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s,
                           const int64_t* U_dev = nullptr);
+// The two halves of emb_backward_segment: the lookup CSR (depends on inv only; ws: counts[U] |
+// cursor[U] | offsets[U+1] | tiles[U/1024+1]; members/memrow [B*F]) and the segmented sum.
+void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s);
+void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
+                      const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
+                      const int64_t* U_dev = nullptr);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                           float* grad_rows, int row_stride, hipStream_t s);
 

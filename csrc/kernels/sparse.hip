@@ -188,8 +188,12 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
   if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
   if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
   MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0xFF, cap * sizeof(int64_t), s));
-  MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, (P + 1) * sizeof(int64_t), s));  // counts[P] = total
-  MINIPS_HIP_CHECK(hipMemsetAsync(cursor, 0, P * sizeof(int64_t), s));
+  if (cursor == counts + P + 1) {  // one buffer: counts[P] (+ total) | cursor[P]
+    MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, (2 * P + 1) * sizeof(int64_t), s));
+  } else {
+    MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, (P + 1) * sizeof(int64_t), s));  // counts[P] = total
+    MINIPS_HIP_CHECK(hipMemsetAsync(cursor, 0, P * sizeof(int64_t), s));
+  }
   if (n == 0) return;
   const int block = 256;
   const int grid = grid_for(n, block, 4096);

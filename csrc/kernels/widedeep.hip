@@ -578,30 +578,36 @@ __global__ void zero_rows_dev_kernel(float* __restrict__ rows, int stride, int64
     reinterpret_cast<float4*>(rows)[c] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-template <typename TX>
-static void emb_backward_seg(const TX* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
-                             float* grad_rows, int row_stride, int U, int* ws, hipStream_t s, const int64_t* U_dev) {
-  // ws: counts[U] | cursor[U] | offsets[U+1] | members[B*F] | memrow[B*F] | tiles[U/1024+1]
-  const int total = (int)(B * F);
+// CSR of the lookups grouped by unique row (depends on `inv` only, so the PS builds it at
+// planning time, off the critical path). ws: counts[U] | cursor[U] | offsets[U+1] | tiles;
+// members/memrow: [B*F] lookup ids and their rows, sorted by row.
+void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s) {
+  if (B <= 0 || U <= 0) return;
   int* counts = ws;
   int* cursor = counts + U;
   int* offsets = cursor + U;
-  int* members = offsets + U + 1;
-  int* memrow = members + total;
-  int* tiles = memrow + total;
+  int* tiles = offsets + U + 1;
   const int ntiles = (U + kScanTile - 1) / kScanTile;
   MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int) * 2 * (size_t)U, s));  // counts, cursor
-  if (U_dev && row_stride % 4 == 0)
-    hipLaunchKernelGGL(zero_rows_dev_kernel, grid_for((int64_t)U * (row_stride / 4), 256, 4096), 256, 0, s, grad_rows,
-                       row_stride, (int64_t)U, U_dev);
-  else
-    MINIPS_HIP_CHECK(hipMemsetAsync(grad_rows, 0, sizeof(float) * (size_t)U * row_stride, s));
   dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);
   hipLaunchKernelGGL(emb_seg_count_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, counts);
   hipLaunchKernelGGL(emb_scan_reduce_kernel, ntiles, 256, 0, s, counts, U, tiles);
   hipLaunchKernelGGL(emb_scan_top_kernel, 1, 256, 0, s, tiles, ntiles);
   hipLaunchKernelGGL(emb_scan_final_kernel, ntiles, 256, 0, s, counts, U, tiles, offsets);
   hipLaunchKernelGGL(emb_seg_fill_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, offsets, cursor, members, memrow);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+template <typename TX>
+static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, int F, int D, const int* members,
+                        const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
+                        const int64_t* U_dev) {
+  const int total = (int)(B * F);
+  if (U_dev && row_stride % 4 == 0)
+    hipLaunchKernelGGL(zero_rows_dev_kernel, grid_for((int64_t)U * (row_stride / 4), 256, 4096), 256, 0, s, grad_rows,
+                       row_stride, (int64_t)U, U_dev);
+  else
+    MINIPS_HIP_CHECK(hipMemsetAsync(grad_rows, 0, sizeof(float) * (size_t)U * row_stride, s));
   const int pieces = (total + (256 / D) * kSegG - 1) / ((256 / D) * kSegG);
   const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
 #define MINIPS_SEG_LAUNCH(DD)                                                                                      \
@@ -624,15 +630,28 @@ static void emb_backward_seg(const TX* dX, int ldx, const float* dwide, const in
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
+                      const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
+                      const int64_t* U_dev) {
+  if (B <= 0 || U <= 0) return;
+  if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("emb_backward_csr: row_stride too small");
+  if (bf16)
+    emb_seg_sum(static_cast<const bf16_t*>(dX), ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s,
+                U_dev);
+  else
+    emb_seg_sum(static_cast<const float*>(dX), ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s,
+                U_dev);
+}
+
 void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,
                           int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s,
                           const int64_t* U_dev) {
   if (B <= 0 || U <= 0) return;
-  if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("emb_backward_segment: row_stride too small");
-  if (bf16)
-    emb_backward_seg(static_cast<const bf16_t*>(dX), ldx, dwide, inv, B, F, D, grad_rows, row_stride, U, ws, s, U_dev);
-  else
-    emb_backward_seg(static_cast<const float*>(dX), ldx, dwide, inv, B, F, D, grad_rows, row_stride, U, ws, s, U_dev);
+  // ws: counts[U] | cursor[U] | offsets[U+1] | tiles[U/1024+1] | members[B*F] | memrow[B*F]
+  int* members = ws + 3 * U + 1 + (U / 1024 + 1);
+  int* memrow = members + B * F;
+  emb_build_csr(inv, B, F, U, ws, members, memrow, s);
+  emb_backward_csr(dX, bf16, ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s, U_dev);
 }
 
 }  // namespace minips_k

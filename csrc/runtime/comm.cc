@@ -124,6 +124,7 @@ int Mailbox::ConnectWithRetry(const Node& n, double timeout_s) {
       if (fd >= 0) ::close(fd);
       freeaddrinfo(res);
     }
+    if (stopping_) return -1;
     if (std::chrono::steady_clock::now() > deadline) {
       MINIPS_CHECK(false, "node " << node_.id << " cannot connect to " << n.DebugString());
     }
@@ -166,8 +167,10 @@ void Mailbox::Start(const Node* master, const Node* scale_node) {
 void Mailbox::ConnectTo(const Node& n) {
   std::lock_guard<std::mutex> lk(send_mu_);
   peers_[n.id] = n;
-  if (n.id != node_.id && !out_fds_.count(n.id))
-    out_fds_[n.id] = ConnectWithRetry(n, Context::Get().get_double("barrier_timeout_s"));
+  if (n.id != node_.id && !out_fds_.count(n.id)) {
+    const int fd = ConnectWithRetry(n, Context::Get().get_double("barrier_timeout_s"));
+    if (fd >= 0) out_fds_[n.id] = fd;
+  }
 }
 
 void Mailbox::SetScaleNode(const Node& n) {
@@ -179,6 +182,7 @@ void Mailbox::SetScaleNode(const Node& n) {
 void Mailbox::Stop(bool barrier) {
   if (!running_) return;
   if (barrier) Barrier();
+  stopping_ = true;
   running_ = false;
   char c = 'x';
   if (wake_pipe_[1] >= 0) (void)!::write(wake_pipe_[1], &c, 1);
@@ -251,6 +255,8 @@ void Mailbox::Dispatch(Message&& msg) {
       {
         std::lock_guard<std::mutex> lk(barrier_mu_);
         barrier_count_ += 1;
+        MINIPS_VLOG(2, "mailbox " << node_.id << " barrier msg from " << msg.meta.sender << " count "
+                                  << barrier_count_);
       }
       barrier_cond_.notify_all();
       return;
@@ -321,9 +327,16 @@ int Mailbox::SendToNode(uint32_t node_id, const Message& msg) {
   std::lock_guard<std::mutex> lk(send_mu_);
   auto it = out_fds_.find(node_id);
   if (it == out_fds_.end()) {
+    if (stopping_) {
+      MINIPS_VLOG(1, "mailbox " << node_.id << ": stopping, dropped " << FlagName(msg.meta.flag) << " to node "
+                                << node_id);
+      return -1;
+    }
     auto pit = peers_.find(node_id);
     MINIPS_CHECK(pit != peers_.end(), "node " << node_.id << ": unknown destination node " << node_id);
-    out_fds_[node_id] = ConnectWithRetry(pit->second, Context::Get().get_double("barrier_timeout_s"));
+    const int nfd = ConnectWithRetry(pit->second, Context::Get().get_double("barrier_timeout_s"));
+    if (nfd < 0) return -1;
+    out_fds_[node_id] = nfd;
     it = out_fds_.find(node_id);
   }
   int fd = it->second;
@@ -332,7 +345,8 @@ int Mailbox::SendToNode(uint32_t node_id, const Message& msg) {
   for (size_t i = 0; ok && i < msg.data.size(); ++i)
     if (msg.data[i].size()) ok = WriteAll(fd, msg.data[i].data(), msg.data[i].size());
   if (!ok) {
-    MINIPS_LOG(1, "mailbox " << node_.id << ": send to node " << node_id << " failed");
+    MINIPS_LOG(1, "mailbox " << node_.id << ": send of " << FlagName(msg.meta.flag) << " (" << msg.meta.sender
+                             << " -> " << msg.meta.recver << ") to node " << node_id << " failed");
     ::close(fd);
     out_fds_.erase(node_id);
     return -1;
@@ -391,6 +405,7 @@ void Mailbox::Barrier() {
   bool ok = barrier_cond_.wait_for(lk, std::chrono::duration<double>(timeout),
                                    [&] { return barrier_count_ >= target(); });
   MINIPS_CHECK(ok, "node " << node_.id << " barrier timed out (" << barrier_count_ << "/" << target() << ")");
+  MINIPS_VLOG(2, "mailbox " << node_.id << " barrier passed (" << barrier_count_ << "/" << target() << ")");
   barrier_count_ -= target();
 }
 
@@ -420,10 +435,36 @@ void Sender::Stop() {
   if (thread_.joinable()) thread_.join();
 }
 
+// Flush marker: a kExit addressed to recver -2 (never a real thread id).
+constexpr int32_t kFlushMarker = -2;
+
+void Sender::Flush() {
+  if (!thread_.joinable()) return;
+  uint64_t ticket;
+  {
+    std::lock_guard<std::mutex> lk(flush_mu_);
+    ticket = ++flush_asked_;
+  }
+  Message m;
+  m.meta.flag = Flag::kExit;
+  m.meta.recver = kFlushMarker;
+  send_message_queue_.Push(m);
+  std::unique_lock<std::mutex> lk(flush_mu_);
+  flush_cv_.wait(lk, [&] { return flush_done_ >= ticket; });
+}
+
 void Sender::Main() {
   while (true) {
     Message msg;
     send_message_queue_.WaitAndPop(&msg);
+    if (msg.meta.flag == Flag::kExit && msg.meta.recver == kFlushMarker) {
+      {
+        std::lock_guard<std::mutex> lk(flush_mu_);
+        ++flush_done_;
+      }
+      flush_cv_.notify_all();
+      continue;
+    }
     if (msg.meta.flag == Flag::kExit && msg.meta.recver < 0) break;
     try {
       mailbox_->Send(msg);

@@ -14,7 +14,9 @@
 // (minips_amd/ps).
 #pragma once
 
+#include <condition_variable>
 #include <map>
+#include <mutex>
 #include <set>
 
 #include "base.h"
@@ -103,6 +105,9 @@ class Mailbox : public AbstractMailbox {
   int wake_pipe_[2] = {-1, -1};
   std::thread receiver_;
   std::atomic<bool> running_{false};
+  // set once the shutdown barrier has passed: remote sends are dropped instead of reconnecting
+  // (a peer that already exited would otherwise stall Stop() for the whole connect timeout)
+  std::atomic<bool> stopping_{false};
   std::atomic<uint64_t> bytes_sent_{0}, msgs_sent_{0};
 };
 
@@ -111,6 +116,10 @@ class Sender : public AbstractSender {
   explicit Sender(AbstractMailbox* mailbox) : mailbox_(mailbox) {}
   void Start() override;
   void Stop() override;
+  // Blocks until every message queued before the call has been handed to the mailbox. A
+  // barrier goes out on the mailbox directly, so without this it can overtake a worker's last
+  // Add/Clock still waiting in the queue (the peer may then pass the barrier and stop first).
+  void Flush();
   ThreadsafeQueue<Message>* GetMessageQueue() override { return &send_message_queue_; }
 
  private:
@@ -118,6 +127,9 @@ class Sender : public AbstractSender {
   AbstractMailbox* mailbox_;
   ThreadsafeQueue<Message> send_message_queue_;
   std::thread thread_;
+  std::mutex flush_mu_;
+  std::condition_variable flush_cv_;
+  uint64_t flush_asked_ = 0, flush_done_ = 0;
 };
 
 }  // namespace minips

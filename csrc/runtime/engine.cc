@@ -150,6 +150,7 @@ void Engine::ScaleRollBack(int scale_node_id) {
 
 void Engine::StopEverything() {
   StopHeartbeatThread();
+  if (sender_) sender_->Flush();
   StopMailbox(true);
   StopSender();
   StopServerThreads();
@@ -278,6 +279,7 @@ void Engine::Run(const MLTask& task) {
     for (auto& t : group) t.join();
     for (auto tid : threads) mailbox_->DeregisterQueue(tid);
   }
+  if (sender_) sender_->Flush();  // the workers' last Adds/Clocks leave before the barrier
   mailbox_->Barrier();
   for (auto& kv : spec.GetNodeToWorkers()) {
     (void)kv;

@@ -88,7 +88,7 @@ class DLRM:
 
     def prefetch(self, keys):
         """Lookahead key planning of the next batch (see WideDeep.prefetch)."""
-        self._next_plan = (keys, self.emb.plan_async(keys))
+        self._next_plan = (keys, self.emb.plan_async(keys, csr=True))
 
     def train_step(self, dense, keys, labels, next_keys=None):
         cfg = self.cfg
@@ -97,6 +97,8 @@ class DLRM:
         pre = getattr(self, "_next_plan", None)
         plan = pre[1] if pre is not None and pre[0] is keys else None
         self._next_plan = None
+        if plan is None:
+            plan = self.emb.plan(keys, csr=True)
         if next_keys is not None:
             self.prefetch(next_keys)
         rows, plan = self.emb.get(keys, plan=plan)
@@ -138,7 +140,7 @@ class DLRM:
         dev = self.comm.device
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), D, dtype=torch.float32,
                                                                          device=dev)
-        ops.wd_emb_backward(b["dV"], None, plan.inv, F, D, grad_rows, x_off=0, U_dev=plan.U_dev)
+        ops.wd_emb_backward(b["dV"], None, plan.inv, F, D, grad_rows, x_off=0, U_dev=plan.U_dev, csr=plan.csr)
         self.emb.add(plan, grad_rows)
         self.emb.clock()
         for l, g_out, x_in in dys:

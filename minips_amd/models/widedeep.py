@@ -146,7 +146,7 @@ class WideDeep:
     def prefetch(self, keys):
         """Lookahead: start routing the NEXT batch's keys (dedupe + count all-to-all on the
         planning stream) so it overlaps the current step; train_step picks the plan up."""
-        self._next_plan = (keys, self.emb.plan_async(keys))
+        self._next_plan = (keys, self.emb.plan_async(keys, csr=True))
 
     def train_step(self, dense, keys, labels, next_keys=None) -> torch.Tensor:
         """One BSP superstep: Get, forward, backward, Add, Clock. Returns the summed loss
@@ -167,6 +167,8 @@ class WideDeep:
         pre = getattr(self, "_next_plan", None)
         plan = pre[1] if pre is not None and pre[0] is keys else None
         self._next_plan = None
+        if plan is None:
+            plan = self.emb.plan(keys, csr=True)
         if next_keys is not None:
             self.prefetch(next_keys)
         rows, plan = self.emb.get(keys, plan=plan)
@@ -185,7 +187,7 @@ class WideDeep:
         dev = self.comm.device
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), cfg.row_width,
                                                                          dtype=torch.float32, device=dev)
-        ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows, U_dev=plan.U_dev)
+        ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows, U_dev=plan.U_dev, csr=plan.csr)
         self.emb.add(plan, grad_rows)
         self.emb.clock()
         ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))

@@ -285,13 +285,24 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
         dH_colsum += g.float().sum(0)
 
 
-def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None):
+def emb_build_csr(inv, F, U):
+    """Lookups grouped by unique row: (members, memrow) int32 [n] with memrow sorted and
+    members[i] the lookup id (b*F + f) of the i-th entry. Depends on ``inv`` only, so the PS
+    builds it while planning a batch (off the critical path)."""
+    if _gpu(inv):
+        return tuple(kernels().emb_build_csr(inv, int(F), int(max(U, 1))))
+    order = torch.sort(inv, stable=True).indices
+    return order.to(torch.int32), inv[order].to(torch.int32)
+
+
+def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=None):
     """grad_rows[u, :D] = sum of dX[b, x_off + f*D : ...] over the lookups (b, f) with
     inv[b*F+f] == u; column D likewise sums dwide[b] when given. On the GPU every row of
     grad_rows is written (rows without lookups become 0); the CPU reference adds into grad_rows,
     so callers pass a zeroed buffer."""
     if _gpu(dX):
-        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), U_dev)
+        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), U_dev,
+                                  *(csr if csr is not None else (None, None)))
         return grad_rows
     B = dX.shape[0]
     g = dX[:, x_off: x_off + F * D].float().reshape(B * F, D)

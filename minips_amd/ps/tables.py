@@ -272,6 +272,7 @@ class SparsePlan:
     own_uniq: torch.Tensor | None = None
     own_inv: torch.Tensor | None = None
     own_U_dev: torch.Tensor | None = None
+    csr: tuple | None = None   # (members, memrow) lookups grouped by unique row (emb backward)
     extra: dict = field(default_factory=dict)
     _U: int | None = None
 
@@ -285,7 +286,7 @@ class SparsePlan:
 
 class _PendingPlan:
     """A plan whose dedupe + count exchange was issued on the planning stream (lookahead)."""
-    __slots__ = ("keys", "F", "flat", "uniq", "inv", "counts", "U_dev", "host", "event")
+    __slots__ = ("keys", "F", "flat", "uniq", "inv", "counts", "U_dev", "host", "event", "csr")
 
 
 class SparseTable:
@@ -350,14 +351,16 @@ class SparseTable:
         """(row index tensor, base) of owned unique keys being updated."""
         return keys, self.base
 
-    def _start_plan(self, keys: torch.Tensor) -> _PendingPlan:
+    def _start_plan(self, keys: torch.Tensor, csr: bool = False) -> _PendingPlan:
         """Dedupe + owner bucketing + all-to-all of the per-owner counts, issued on the current
-        stream; the counts land in pinned host memory behind an event."""
+        stream; the counts land in pinned host memory behind an event. ``csr`` also groups the
+        lookups by unique row for the embedding backward (it depends on the keys only)."""
         pp = _PendingPlan()
         pp.keys = keys
         pp.F = keys.shape[1] if keys.dim() == 2 else 1
         pp.flat = self._route_keys(keys.reshape(-1).to(torch.int64))
         pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.unique_bucketize_n(pp.flat, self.bounds, pp.F)
+        pp.csr = ops.emb_build_csr(pp.inv, pp.F, pp.flat.numel()) if csr and pp.inv.is_cuda else None
         pp.host = pp.event = None
         if self.comm.world > 1:
             recv = torch.empty_like(pp.counts)
@@ -372,19 +375,20 @@ class SparseTable:
                 pp.host = both
         return pp
 
-    def plan_async(self, keys: torch.Tensor):
+    def plan_async(self, keys: torch.Tensor, csr: bool = False):
         """Lookahead: start planning ``keys`` (a LATER batch) on the planning stream, so its
-        dedupe and count exchange overlap the current step; pass the result to get(plan=...).
-        Planning reads no table state, so issuing it early changes no consistency semantics."""
+        dedupe, count exchange (and lookup CSR) overlap the current step; pass the result to
+        get(plan=...). Planning reads no table state, so issuing it early changes no
+        consistency semantics."""
         if self.comm.device.type != "cuda" or self._exact_counts:
-            return self.plan(keys)
+            return self.plan(keys, csr)
         ps = self.comm.plan_stream()
         cur = torch.cuda.current_stream(self.comm.device)
         ps.wait_stream(cur)  # the keys are produced on the compute stream
         with torch.cuda.stream(ps):
-            pp = self._start_plan(keys)
+            pp = self._start_plan(keys, csr)
         keys.record_stream(ps)
-        for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev):
+        for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev, *(pp.csr or ())):
             t.record_stream(cur)  # produced on the planning stream, consumed on the compute stream
         if pp.event is None:
             pp.event = torch.cuda.Event()
@@ -399,15 +403,15 @@ class SparseTable:
         if self.comm.world == 1:
             if self._exact_counts or dev.type != "cuda":
                 U = int(pp.U_dev.item())
-                return SparsePlan(n, pp.inv, pp.uniq, U, [U], [U], pp.uniq[:U], _U=U)
-            return SparsePlan(n, pp.inv, pp.uniq, n, None, None, pp.uniq, U_dev=pp.U_dev)
+                return SparsePlan(n, pp.inv, pp.uniq, U, [U], [U], pp.uniq[:U], csr=pp.csr, _U=U)
+            return SparsePlan(n, pp.inv, pp.uniq, n, None, None, pp.uniq, U_dev=pp.U_dev, csr=pp.csr)
         if pp.event is not None:
             pp.event.synchronize()  # the only host wait of a step: the all-to-all splits
         send, recv = pp.host[0].tolist(), pp.host[1].tolist()
         U, M = int(sum(send)), int(sum(recv))
         recv_keys = torch.empty(M, dtype=torch.int64, device=dev)
         self.comm.all_to_all_v(recv_keys, pp.uniq, recv, send, p2p=self.p2p)
-        p = SparsePlan(n, pp.inv, pp.uniq, U, send, recv, recv_keys, _U=U)
+        p = SparsePlan(n, pp.inv, pp.uniq, U, send, recv, recv_keys, csr=pp.csr, _U=U)
         if M > 0:
             # owner-side dedupe of the keys requested by all ranks (the push sums their rows)
             ou, oi, _, oU = ops.unique_bucketize_n(recv_keys, self._own_bounds)
@@ -416,8 +420,8 @@ class SparseTable:
                 p.extra["own_U"] = int(oU.item())
         return p
 
-    def plan(self, keys: torch.Tensor) -> SparsePlan:
-        return self._finish_plan(self._start_plan(keys))
+    def plan(self, keys: torch.Tensor, csr: bool = False) -> SparsePlan:
+        return self._finish_plan(self._start_plan(keys, csr))
 
     def get(self, keys: torch.Tensor, plan=None):
         """Pull rows of ``keys``. Returns (rows [cap, width] in unique order, plan); the row of

@@ -248,3 +248,39 @@ def test_embedding_backward_segment_hot_rows(dev, D, dtype):
     ops.wd_emb_backward(dX.to(dev), dwide.to(dev), inv.to(dev), F, D, gr)
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-3
     torch.testing.assert_close(gr.cpu(), ref, rtol=1e-4, atol=tol * 8)
+
+
+def test_device_counts_and_prebuilt_csr(dev):
+    """unique_bucketize_n's device-side U bounds gather / row-wise Adagrad / the embedding
+    backward without a host sync; the CSR prebuilt at planning time gives the same gradient."""
+    g = torch.Generator().manual_seed(5)
+    B, F, D = 4096, 4, 32
+    keys = torch.randint(0, 3000, (B, F), generator=g)
+    bounds = torch.tensor([0, 3000])
+    uniq, inv, counts, U_dev = ops.unique_bucketize_n(keys.to(dev), bounds.to(dev), F)
+    U = int(U_dev.item())
+    assert U == int(counts.sum()) == torch.unique(keys).numel()
+    n = keys.numel()
+    table = torch.randn(3000, 36, generator=g)
+    # gather bounded by the device count: rows past U untouched
+    out = torch.full((n, 36), 7.0, device=dev)
+    ops.gather_rows(table.to(dev), uniq, 0, out, n_dev=U_dev)
+    torch.testing.assert_close(out[:U].cpu(), table[uniq[:U].cpu()])
+    assert bool((out[U:] == 7.0).all())
+    # embedding backward with the prebuilt CSR vs the reference
+    dX = torch.randn(B, F * D, generator=g).to(torch.bfloat16)
+    dwide = torch.randn(B, generator=g)
+    ref = torch.zeros(U, D + 1)
+    ops.wd_emb_backward(dX.float(), dwide, inv.cpu(), F, D, ref)
+    csr = ops.emb_build_csr(inv, F, n)
+    gr = torch.full((n, D + 1), float("nan"), device=dev)
+    ops.wd_emb_backward(dX.to(dev), dwide.to(dev), inv, F, D, gr, U_dev=U_dev, csr=csr)
+    torch.testing.assert_close(gr[:U].cpu(), ref, rtol=1e-4, atol=0.16)
+    # row-wise Adagrad bounded by the device count: keys past U (garbage) never applied
+    t_gpu = table.to(dev)
+    st = torch.zeros(3000, device=dev)
+    grads = torch.randn(n, 36, generator=g)
+    ops.sparse_rowwise_adagrad(t_gpu, st, uniq, 0, grads.to(dev), 0.1, n_dev=U_dev)
+    t_ref, s_ref = table.clone(), torch.zeros(3000)
+    ops.sparse_rowwise_adagrad(t_ref, s_ref, uniq[:U].cpu(), 0, grads[:U], 0.1)
+    torch.testing.assert_close(t_gpu.cpu(), t_ref, rtol=1e-5, atol=1e-5)
