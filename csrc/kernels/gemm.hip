@@ -113,23 +113,23 @@ struct EpiArgs {
   int64_t sc_split;  // split-K slab mode: C += blockIdx.z * sc_split (0 = all splits share C)
 };
 
-// Fused epilogue of one wave's 64x64 accumulator block (rows m0 + 64*wm.., cols n0 + 64*wn..).
-template <int EPI>
-__device__ __forceinline__ void epilogue(const v4f (&acc)[4][4], const EpiArgs& ep, int M, int N, int m0, int n0,
-                                         int wm, int wn, int lane) {
+// Fused epilogue of one wave's (16 MR) x 64 accumulator block at rows mb.., cols nb...
+template <int EPI, int MR>
+__device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiArgs& ep, int M, int N, int mb, int nb,
+                                            int lane) {
   const int col_l = lane & 15, row_q = (lane >> 4) * 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + col_l;
+    const int col = nb + j * 16 + col_l;
     const bool col_ok = col < N;
     float bias = 0.f;
     if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
     float csum = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MR; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + row_q + r;
+        const int row = mb + i * 16 + row_q + r;
         if (!(col_ok && row < M)) continue;
         float v = acc[i][j][r] * ep.alpha;
         const int64_t off = (int64_t)row * ep.ldc + col;
@@ -173,6 +173,13 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[4][4], const EpiArgs& 
       if (lane < 16 && col_ok) atomicAdd(ep.colsum + col, csum);
     }
   }
+}
+
+// One wave's 64x64 accumulator block (rows m0 + 64*wm.., cols n0 + 64*wn..).
+template <int EPI>
+__device__ __forceinline__ void epilogue(const v4f (&acc)[4][4], const EpiArgs& ep, int M, int N, int m0, int n0,
+                                         int wm, int wn, int lane) {
+  epilogue_at<EPI, 4>(acc, ep, M, N, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
 template <int BK, bool A_KM, bool B_KN, int EPI>
@@ -408,6 +415,137 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
   epilogue<EPI>(acc, ep, M, N, m0, n0, wm, wn, lane);
 }
 
+// ================================================================ v3: 256x256, 8 waves, phase-split K-step
+// 256x256 output tile, 8 waves as 2 (M) x 4 (N), each wave 128x64 = 8x4 MFMA 16x16 tiles (128
+// accumulator registers), BK = 64, operands staged by LDS-DMA (same swizzled images as v2) as
+// 128-row HALF tiles: [buf][A0 | A1 | B0 | B1], 16 KiB each, 2 buffers = 128 KiB (1 WG / CU).
+// A K-step is split so that halves free up early and the DMA runs two K-steps ahead:
+//   phase 0: read ALL of this wave's A fragments (16 x ds_read_b128: 8 m-tiles x 2 k) and the
+//            B fragments of n-tile 0, 16 MFMAs; barrier -> the A halves of this buffer are free
+//   phase 1: stage A of K-step t+2 into this buffer; B n-tile 1, 16 MFMAs
+//   phase 2, 3: B n-tiles 2, 3, 16 MFMAs each
+//   end:     counted vmcnt (A(t+2) stays in flight) + barrier -> B halves free, buffer t+1 landed
+// and B of K-step t+1 is staged at phase 0 of t (into the other buffer, last read in t-1). So A
+// has ~7 phases and B ~4 phases (~1.5 / 0.9 us) of load latency budget instead of one K-step.
+// Raw s_barrier + explicit waits only: __syncthreads() would drain the DMA (vmcnt(0)).
+constexpr int kV3Half = 128 * BK2;
+
+template <bool A_KM, bool B_KN, int EPI, bool EARLY_A = true>
+__global__ __launch_bounds__(512) void gemm_v3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                      int M, int N, int K, int lda, int ldb, int k_chunk,
+                                                      EpiArgs ep) {
+  constexpr bool PERM = A_KM && B_KN;
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2][4 * kV3Half];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = (N + 255) / 256, tiles_m = (M + 255) / 256;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if (nwg >= 16) {
+    int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    bid = base + (bid >> 3);
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  {
+    const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
+    A += zo * ep.sa_o + zi * ep.sa_i;
+    B += zo * ep.sb_o + zi * ep.sb_i;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
+    ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
+  }
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7ffffff0, 0x00020000);
+  const int kb = blockIdx.z * k_chunk;
+  const int ke = min(K, kb + k_chunk);
+  const int nt = ke > kb ? (ke - kb + BK2 - 1) / BK2 : 0;
+
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // 2 DMA instructions per thread per half tile -> 4 per operand per K-step
+  auto stage_a = [&](int t, int buf) {
+    const int k = kb + t * BK2;
+    dma_tile<A_KM, 128, 8>(ra, lda, m0, k, M, ke, smem[buf], wave, lane);
+    dma_tile<A_KM, 128, 8>(ra, lda, m0 + 128, k, M, ke, smem[buf] + kV3Half, wave, lane);
+  };
+  auto stage_b = [&](int t, int buf) {
+    const int k = kb + t * BK2;
+    dma_tile<B_KN, 128, 8>(rb, ldb, n0, k, N, ke, smem[buf] + 2 * kV3Half, wave, lane);
+    dma_tile<B_KN, 128, 8>(rb, ldb, n0 + 128, k, N, ke, smem[buf] + 3 * kV3Half, wave, lane);
+  };
+
+  if (nt > 0) {
+    stage_a(0, 0);
+    stage_b(0, 0);
+  }
+  if (EARLY_A && nt > 1) {
+    stage_a(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A(0), B(0) landed; A(1) in flight
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    const bf16_t* SA = smem[buf] + wr * kV3Half;
+    const bf16_t* SB = smem[buf] + (2 + (wc >> 1)) * kV3Half;
+    const int bcol = (wc & 1) * 64;
+    // ---- phase 0: every A fragment of the K-step + B n-tile 0
+    if (t + 1 < nt) {
+      if (!EARLY_A) stage_a(t + 1, buf ^ 1);  // plain double buffering: both operands one K-step ahead
+      stage_b(t + 1, buf ^ 1);
+    }
+    v8s af[8][2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag2<A_KM, PERM, 128>(SA, i * 16, ks, lane);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) bfr[ks] = frag2<B_KN, PERM, 128>(SB, bcol, ks, lane);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i][ks]),
+                                                            __builtin_bit_cast(v8bf, bfr[ks]), acc[i][0], 0, 0, 0);
+    if (EARLY_A) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's A reads of this buffer retired
+      asm volatile("" ::: "memory");
+      // ---- phases 1..3: B n-tiles 1..3 (A from registers); A of K-step t+2 streams in
+      if (t + 2 < nt) stage_a(t + 2, buf);
+    }
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[ks] = frag2<B_KN, PERM, 128>(SB, bcol + j * 16, ks, lane);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i][ks]),
+                                                              __builtin_bit_cast(v8bf, bfr[ks]), acc[i][j], 0, 0, 0);
+    }
+    // ---- end of K-step: operands of t+1 landed (A(t+2) may stay in flight), B halves free
+    if (EARLY_A && t + 2 < nt) {
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  epilogue_at<EPI, 8>(acc, ep, M, N, m0 + wr * 128, n0 + wc * 64, lane);
+}
+
 static int gemm_impl() {
   static const int v = [] {
     const char* e = std::getenv("MINIPS_GEMM_IMPL");
@@ -425,11 +563,16 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
   const int64_t b_ext = (int64_t)((B_KN ? K : N) - 1) * ldb + (B_KN ? N : K);
   // measured (tools/bench_gemm.py): v2 wins on forward / dgrad; the split-K wgrad (both operands
   // tr-read) stays on the register-staged BK=32 kernel, which is faster there
-  static const bool wgrad_v2 = [] {
-    const char* e = std::getenv("MINIPS_GEMM_WGRAD_V2");
-    return e && std::atoi(e) == 1;
+  // wgrad kernel (MINIPS_GEMM_WGRAD): v1 (default; register-staged BK=32, the fastest measured on
+  // the split-K wgrad shapes: tools/sweep_wgrad.py), v2, or v3 (256x256 phase-split tiles, split-K
+  // chosen by ops.linear_wgrad for ~one workgroup per CU)
+  static const int wgrad_mode = [] {
+    const char* e = std::getenv("MINIPS_GEMM_WGRAD");
+    if (!e) return 1;
+    return std::string(e) == "v3" ? 3 : (std::string(e) == "v2" ? 2 : 1);
   }();
-  if (gemm_impl() == 2 && (!(A_KM && B_KN) || wgrad_v2) && a_ext * 2 < 0x7ff00000ll && b_ext * 2 < 0x7ff00000ll) {
+  const bool wgrad = A_KM && B_KN;
+  if (gemm_impl() == 2 && (!wgrad || wgrad_mode >= 2) && a_ext * 2 < 0x7ff00000ll && b_ext * 2 < 0x7ff00000ll) {
     const int kper = (K + split_k - 1) / split_k;
     const int kc = (kper + BK2 - 1) / BK2 * BK2;
     const int nsplit = (K + kc - 1) / kc;
@@ -446,8 +589,27 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
     const int64_t t128 = work * (int64_t)tiles;
     const double eff256 = (double)t256 / (double)(((t256 + 255) / 256) * 256);
     const double eff128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
-    const int pick = force_tile ? force_tile : (eff256 >= eff128 ? 256 : 128);
-    if (pick == 256) {
+    const int pick = force_tile ? force_tile : ((wgrad && wgrad_mode == 3) || eff256 >= eff128 ? 256 : 128);
+    // v3 (experimental, MINIPS_GEMM_V3=1): measured within +-3 % of v2 on the forward shapes and
+    // 10-25 % slower on the tr-read (dgrad/wgrad) shapes (tools/gpu_v3.sh), so v2 stays the default
+    static const bool v3 = [] {
+      const char* e = std::getenv("MINIPS_GEMM_V3");
+      return e && std::atoi(e) != 0;
+    }();
+    static const bool v3_early = [] {
+      const char* e = std::getenv("MINIPS_GEMM_V3_EARLY");
+      return !e || std::atoi(e) != 0;
+    }();
+    const bool use_v3 = v3 || (wgrad && wgrad_mode == 3);
+    if (pick == 256 && use_v3) {
+      dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
+      if (v3_early)
+        hipLaunchKernelGGL((gemm_v3_kernel<A_KM, B_KN, EPI, true>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb, kc,
+                           ep);
+      else
+        hipLaunchKernelGGL((gemm_v3_kernel<A_KM, B_KN, EPI, false>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb,
+                           kc, ep);
+    } else if (pick == 256) {
       dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
       hipLaunchKernelGGL((gemm_v2_kernel<256, 256, A_KM, B_KN, EPI>), grid, dim3(1024), 0, s, A, B, M, N, K, lda, ldb,
                          kc, ep);

@@ -117,7 +117,9 @@ def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=
     return gemm(dy, w, out, M, K, N, False, True, epi, mask=mask, colsum=colsum)
 
 
-_WGRAD_BLOCKS = int(__import__("os").environ.get("MINIPS_WGRAD_BLOCKS", "512"))
+_WGRAD_MODE = __import__("os").environ.get("MINIPS_GEMM_WGRAD", "v1")
+_WGRAD_BLOCKS = int(__import__("os").environ.get("MINIPS_WGRAD_BLOCKS", "256" if _WGRAD_MODE == "v3" else "512"))
+_WGRAD_MIN_ROWS = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS", "512" if _WGRAD_MODE == "v3" else "640"))
 
 
 def linear_wgrad(dy, x, dw, split_k=None):
@@ -125,10 +127,12 @@ def linear_wgrad(dy, x, dw, split_k=None):
     M, N = dy.shape
     K = x.shape[1]
     if split_k is None:
-        tiles = ((N + 127) // 128) * ((K + 127) // 128)
-        # ~512 blocks, but >= 640 reduction rows per split (tools/bench_gemm.py sweep: shorter
-        # slices lose to their fixed prologue/epilogue cost; the slab reduce makes splits cheap)
-        split_k = max(1, min(M // 640, (_WGRAD_BLOCKS + tiles - 1) // tiles))
+        t = 256 if _WGRAD_MODE == "v3" else 128
+        tiles = ((N + t - 1) // t) * ((K + t - 1) // t)
+        # about one workgroup per CU (v3: 256x256 tiles, 1 WG/CU; v1/v2: ~512 128x128 blocks), but
+        # a minimum number of reduction rows per split (tools/sweep_wgrad.py: shorter slices lose
+        # to their fixed prologue/epilogue cost; the slab reduce makes splits cheap)
+        split_k = max(1, min(M // _WGRAD_MIN_ROWS, (_WGRAD_BLOCKS + tiles - 1) // tiles))
     return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
 
 

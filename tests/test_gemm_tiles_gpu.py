@@ -1,0 +1,66 @@
+"""Every GEMM kernel variant against the fp32 reference, incl. M/N/K tails, split-K and batched
+mode. The tile/kernel choice is read from the environment once per process, so each variant runs
+in its own subprocess (one at a time): v3 (256x256 phase-split, 8 waves), v2 256x256 (16 waves),
+v2 128x128, and the v1 / v2 / v3 weight-gradient paths."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHECK = r'''
+import torch
+from minips_amd import ops
+dev = torch.device("cuda", 0)
+bf = lambda x: x.to(torch.bfloat16)
+worst = 0.0
+for (M, N, K) in [(256, 256, 64), (520, 264, 200), (1000, 776, 848), (64, 1024, 1032), (300, 2048, 72)]:
+    for layout in ("nt", "nn", "tn"):
+        a_km, b_kn = {"nt": (False, False), "nn": (False, True), "tn": (True, True)}[layout]
+        if (a_km and M % 8) or (b_kn and N % 8):
+            continue
+        g = torch.Generator().manual_seed(M + N + K)
+        A = bf(torch.randn(K if a_km else M, M if a_km else K, generator=g))
+        B = bf(torch.randn(K if b_kn else N, N if b_kn else K, generator=g))
+        ref = (A.float().t() if a_km else A.float()) @ (B.float() if b_kn else B.float().t())
+        for split in ((1, 3) if layout == "tn" else (1,)):
+            C = torch.zeros(M, N, device=dev) if split > 1 else torch.full((M, N), float("nan"), device=dev)
+            epi = ops.EPI_ATOMIC_F32 if split > 1 else ops.EPI_STORE_F32
+            ops.gemm(A.to(dev), B.to(dev), C, M, N, K, a_km, b_kn, epi, split_k=split)
+            err = float((C.cpu() - ref).abs().max()) / (K ** 0.5)
+            assert err < 3e-3, (M, N, K, layout, split, err)
+            worst = max(worst, err)
+# wgrad through linear_wgrad (default split choice), accumulating into a non-zero dW
+dy = bf(torch.randn(4096, 520))
+x = bf(torch.randn(4096, 264))
+dW = torch.ones(520, 264, device=dev)
+ops.linear_wgrad(dy.to(dev), x.to(dev), dW)
+ref = 1.0 + dy.float().t() @ x.float()
+assert float((dW.cpu() - ref).abs().max()) < 0.2, float((dW.cpu() - ref).abs().max())
+# batched (attention-style strided) GEMM
+Bt, Mb, Nb, Kb = 3, 200, 136, 64
+A = bf(torch.randn(Bt, Mb, Kb)); B = bf(torch.randn(Bt, Nb, Kb))
+C = torch.empty(Bt, Mb, Nb, device=dev)
+ops.gemm_batched(A.to(dev), B.to(dev), C, Mb, Nb, Kb, False, False, ops.EPI_STORE_F32, Bt, 1, Kb, Kb, Nb,
+                 (Mb * Kb, 0, Nb * Kb, 0, Mb * Nb, 0))
+ref = A.float() @ B.float().transpose(1, 2)
+assert float((C.cpu() - ref).abs().max()) < 0.05
+print("ok", worst)
+'''
+
+
+@pytest.mark.parametrize("env", [
+    {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "1"},         # v3
+    {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "1", "MINIPS_GEMM_V3_EARLY": "0", "MINIPS_GEMM_WGRAD": "v3"},
+    {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "0"},         # v2 256x256
+    {"MINIPS_GEMM_TILE": "128", "MINIPS_GEMM_WGRAD": "v2"},     # v2 128x128 incl. wgrad
+    {},                                                         # defaults (v1 wgrad)
+])
+def test_gemm_variant(env):
+    e = dict(os.environ, **env)
+    r = subprocess.run([sys.executable, "-c", CHECK], cwd=ROOT, env=e, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, (env, r.stdout[-2000:], r.stderr[-3000:])

@@ -169,8 +169,7 @@ def main(argv: list[str]) -> int:
             print("built", o)
     if targets & {"kernels", "ops_py"}:
         kobjs = kernel_objs()
-        if "ops_py" in targets:
-            print("built", build_ops_py(kobjs))
+        print("built", build_ops_py(kobjs))  # always relink: a stale .so would silently run old kernels
     return 0
 
 
