@@ -425,6 +425,35 @@ void kmeans_assign(const at::Tensor& X, const at::Tensor& C, at::Tensor& assign,
                           ptr<int32_t>(assign), dp, stream_of(X));
 }
 
+void kmeans_split3(const at::Tensor& src, at::Tensor& out, int64_t order, at::Tensor& norms) {
+  check_gpu(src, "src");
+  check_gpu(out, "out");
+  check_gpu(norms, "norms");
+  check_dtype(src, at::kFloat, "src");
+  check_dtype(out, at::kBFloat16, "out");
+  check_dtype(norms, at::kFloat, "norms");
+  TORCH_CHECK(src.is_contiguous() && out.is_contiguous() && out.size(0) == src.size(0) &&
+                  out.size(1) >= 3 * src.size(1) && norms.numel() >= src.size(0), "kmeans_split3 shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
+  minips_k::kmeans_split3(ptr<float>(src), src.size(0), (int)src.size(1), ptr<bf16_t>(out), (int)out.size(1),
+                          (int)order, ptr<float>(norms), stream_of(src));
+}
+
+void kmeans_argmin(const at::Tensor& S, const at::Tensor& cn, const at::Tensor& xn, at::Tensor& assign,
+                   const c10::optional<at::Tensor>& dist) {
+  for (const at::Tensor* t : {&S, &cn, &xn}) {
+    check_gpu(*t, "kmeans_argmin arg");
+    check_dtype(*t, at::kFloat, "kmeans_argmin arg");
+  }
+  check_dtype(assign, at::kInt, "assign");
+  TORCH_CHECK(S.dim() == 2 && S.is_contiguous() && cn.numel() >= S.size(1) && xn.numel() >= S.size(0) &&
+                  assign.numel() >= S.size(0), "kmeans_argmin shapes");
+  float* dp = opt_ptr<float>(dist, at::kFloat, "dist");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(S.device());
+  minips_k::kmeans_argmin(ptr<float>(S), S.size(0), (int)S.size(1), ptr<float>(cn), ptr<float>(xn),
+                          ptr<int32_t>(assign), dp, stream_of(S));
+}
+
 void criteo_synth(int64_t seed, int64_t step, const at::Tensor& cards, const at::Tensor& offsets, const at::Tensor& w,
                   at::Tensor& dense, at::Tensor& keys, at::Tensor& labels) {
   for (const at::Tensor* t : {&cards, &offsets, &w, (const at::Tensor*)&dense, (const at::Tensor*)&keys, (const at::Tensor*)&labels}) check_gpu(*t, "criteo_synth arg");
@@ -709,5 +738,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("lr_sparse_step", &lr_sparse_step);
   m.def("kmeans_assign", &kmeans_assign);
+  m.def("kmeans_split3", &kmeans_split3);
+  m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
 }

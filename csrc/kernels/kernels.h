@@ -130,6 +130,11 @@ void cast_bf16_f32(const bf16_t* x, float* y, int64_t n, hipStream_t s);
 void lr_sparse_step(const int64_t* rowptr, const int64_t* cols, const float* vals, const float* labels, int64_t B,
                     const float* w, float alpha, float* delta, float* correct, hipStream_t s);
 // K-Means assignment: X [n, d] fp32, C [k, d] fp32 -> assign [n] (int32), min dist [n].
+// MFMA assignment pieces (ops.kmeans_assign): hi/lo bf16 split (+ squared row norms) and the
+// argmin over a GEMM-produced S = X.C^T (fp32 [n, k]).
+void kmeans_split3(const float* src, int64_t r, int d, bf16_t* out, int ld, int order, float* norms, hipStream_t s);
+void kmeans_argmin(const float* S, int64_t n, int k, const float* cn, const float* xn, int32_t* assign, float* dist,
+                   hipStream_t s);
 void kmeans_assign(const float* X, int64_t n, int d, const float* C, int k, int32_t* assign, float* dist,
                    hipStream_t s);
 

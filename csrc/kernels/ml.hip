@@ -80,4 +80,81 @@ void kmeans_assign(const float* X, int64_t n, int d, const float* C, int k, int3
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------------------------
+// MFMA form of the assignment: d(x, c) = |x|^2 + |c|^2 - 2 x.c with x.c from the bf16
+// MFMA GEMM at ~fp32 accuracy via a hi/lo split: x = xh + xl (xh = bf16(x), xl = bf16(x - xh)),
+// x.c ~= xh.ch + xh.cl + xl.ch, i.e. ONE GEMM over 3d-long rows A = [xh | xh | xl],
+// B = [ch | cl | ch] (the dropped xl.cl term is ~2^-16 relative).
+//   split3_kernel  fp32 [r, d] -> bf16 [r, ld] (ld >= 3d, zero pad) + row squared norms
+//   argmin_kernel  one wave per row of S = A.B^T (fp32 [n, k]): argmin_c |c|^2 - 2 S[i, c]
+__global__ void split3_kernel(const float* __restrict__ src, int64_t r, int d, bf16_t* __restrict__ out, int ld,
+                              int order, float* __restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < r; i += nw) {
+    const float* x = src + i * d;
+    bf16_t* o = out + i * ld;
+    float sq = 0.f;
+    for (int j = lane; j < d; j += 64) {
+      const float v = x[j];
+      sq += v * v;
+      const bf16_t h = f2bf(v);
+      const bf16_t l = f2bf(v - bf2f(h));
+      o[j] = h;                             // segment 0: hi
+      o[d + j] = order == 0 ? h : l;        // A: [h | h | l]   B: [h | l | h]
+      o[2 * d + j] = order == 0 ? l : h;
+    }
+    for (int j = 3 * d + lane; j < ld; j += 64) o[j] = f2bf(0.f);
+    sq = warp_sum(sq);
+    if (lane == 0) norms[i] = sq;
+  }
+}
+
+__global__ void kmeans_argmin_kernel(const float* __restrict__ S, int64_t n, int k, const float* __restrict__ cn,
+                                     const float* __restrict__ xn, int32_t* assign, float* dist) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nw) {
+    const float* row = S + i * k;
+    float best = 3.4e38f;
+    int bi = 0x7fffffff;
+    for (int c = lane; c < k; c += 64) {
+      const float v = cn[c] - 2.f * row[c];
+      if (v < best) {  // lanes walk c upward: the first minimum per lane wins
+        best = v;
+        bi = c;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob < best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      assign[i] = bi;
+      if (dist) dist[i] = fmaxf(best + xn[i], 0.f);
+    }
+  }
+}
+
+void kmeans_split3(const float* src, int64_t r, int d, bf16_t* out, int ld, int order, float* norms, hipStream_t s) {
+  if (r <= 0) return;
+  if (ld < 3 * d) throw std::runtime_error("kmeans_split3: ld < 3d");
+  hipLaunchKernelGGL(split3_kernel, grid_for(r * 64, 256, 8192), 256, 0, s, src, r, d, out, ld, order, norms);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void kmeans_argmin(const float* S, int64_t n, int k, const float* cn, const float* xn, int32_t* assign, float* dist,
+                   hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(kmeans_argmin_kernel, grid_for(n * 64, 256, 8192), 256, 0, s, S, n, k, cn, xn, assign, dist);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace minips_k

@@ -379,11 +379,36 @@ def lr_sparse_step(rowptr, cols, vals, labels, w, alpha, delta=None, correct=Non
         correct += ((p > 0.5) == (y > 0.5)).float().sum()
 
 
-def kmeans_assign(X, C, assign=None, dist=None):
+_KMEANS_CHUNK = 16384  # rows of S = X.C^T per GEMM (keeps the fp32 score block L2/MALL-sized)
+
+
+def kmeans_assign(X, C, assign=None, dist=None, mfma=None):
+    """Nearest centre of every row of X (fp32 [n, d]) among C (fp32 [k, d]); optional squared
+    distance. GPU: the MFMA form (hi/lo-split bf16 GEMM for x.c, argmin kernel) unless the
+    problem is tiny (or mfma=False: the one-wave-per-point fp32 kernel)."""
     if assign is None:
         assign = torch.empty(X.shape[0], dtype=torch.int32, device=X.device)
     if _gpu(X):
-        kernels().kmeans_assign(X, C, assign, dist)
+        n, d = X.shape
+        k = C.shape[0]
+        if mfma is None:
+            mfma = n * k >= 1 << 16 and k >= 16
+        if not mfma:
+            kernels().kmeans_assign(X, C, assign, dist)
+            return assign
+        ld = (3 * d + 7) // 8 * 8
+        Xc, Cc = X.contiguous(), C.contiguous()
+        Cs = torch.empty(k, ld, dtype=torch.bfloat16, device=X.device)
+        cn = torch.empty(k, dtype=torch.float32, device=X.device)
+        kernels().kmeans_split3(Cc, Cs, 1, cn)
+        xn = torch.empty(n, dtype=torch.float32, device=X.device)
+        for r0 in range(0, n, _KMEANS_CHUNK):
+            r1 = min(n, r0 + _KMEANS_CHUNK)
+            Xs = torch.empty(r1 - r0, ld, dtype=torch.bfloat16, device=X.device)
+            kernels().kmeans_split3(Xc[r0:r1], Xs, 0, xn[r0:r1])
+            S = torch.empty(r1 - r0, k, dtype=torch.float32, device=X.device)
+            gemm(Xs, Cs, S, r1 - r0, k, ld, False, False, EPI_STORE_F32)
+            kernels().kmeans_argmin(S, cn, xn[r0:r1], assign[r0:r1], None if dist is None else dist[r0:r1])
         return assign
     d = torch.cdist(X.double(), C.double()) ** 2
     best, idx = d.min(1)

@@ -284,3 +284,19 @@ def test_device_counts_and_prebuilt_csr(dev):
     t_ref, s_ref = table.clone(), torch.zeros(3000)
     ops.sparse_rowwise_adagrad(t_ref, s_ref, uniq[:U].cpu(), 0, grads[:U], 0.1)
     torch.testing.assert_close(t_gpu.cpu(), t_ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,k,d", [(20000, 1000, 128), (3000, 37, 20)])
+def test_kmeans_assign_mfma(dev, n, k, d):
+    """MFMA (hi/lo-split bf16 GEMM + argmin) assignment vs the fp64 reference: the chosen centre
+    is optimal up to fp32 rounding of the distance, and the distances match."""
+    g = torch.Generator().manual_seed(k)
+    X = torch.randn(n, d, generator=g)
+    C = torch.randn(k, d, generator=g)
+    dist_ref = torch.cdist(X.double(), C.double()) ** 2
+    best_ref = dist_ref.min(1).values
+    dist = torch.empty(n, device=dev)
+    a = ops.kmeans_assign(X.to(dev), C.to(dev), dist=dist, mfma=True).cpu().long()
+    chosen = dist_ref.gather(1, a.view(-1, 1)).view(-1)
+    assert bool(((chosen - best_ref) <= 1e-4 * best_ref.abs() + 1e-4).all())
+    torch.testing.assert_close(dist.cpu().double(), best_ref, rtol=1e-4, atol=1e-3)

@@ -7,7 +7,8 @@ barrier + synchronize, max over ranks, whole-job value, one JSON line on rank 0)
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_models.py --model dlrm
 
 models: mlp (config 2, samples/s), gpt2 (config 4, tokens/s), dlrm (config 5, samples/s),
-        lr (config 1 on GPUs, samples/s), kmeans (samples/s), widedeep-ssp (config 3).
+        dlrm-10b (config 5 at its per-GPU shard: 1.25B rows x 16 per GPU, ASP), lr (config 1 on GPUs,
+        samples/s), kmeans (samples/s), widedeep-ssp (config 3).
 """
 from __future__ import annotations
 
@@ -45,23 +46,37 @@ def build(args, comm):
         return m, (lambda: m.train_step(*data.next())), B * T, "tokens/s", \
             dict(model="GPT-2 small 124M (12L/768d/12H, vocab 50257), dense params sharded over PS ranks",
                  seq_len=T, batch_per_gpu=B)
-    if args.model == "dlrm":
+    if args.model in ("dlrm", "dlrm-10b"):
         from minips_amd.models.dlrm import DLRM, DLRMConfig
 
         B = args.batch or 16384
-        cfg = DLRMConfig(num_rows=args.rows, consistency=args.consistency, staleness=args.staleness)
+        if args.model == "dlrm-10b":
+            # BASELINE config 5: a 10B-row table over 8 GPUs = 1.25B rows (x 16 fp32 + row-wise
+            # Adagrad state = 85 GB) per GPU; weak scaling keeps the per-GPU shard fixed
+            rows = args.rows_per_gpu * comm.world
+            cfg = DLRMConfig(num_rows=rows, D=16, consistency=args.consistency if args.consistency != "bsp"
+                             else "asp", staleness=args.staleness)
+        else:
+            cfg = DLRMConfig(num_rows=args.rows, consistency=args.consistency, staleness=args.staleness)
         m = DLRM(cfg, comm)
         g = torch.Generator(device=dev)
         g.manual_seed(r)
 
-        def step():
+        def batch():
             dense = torch.randn(B, cfg.n_dense, generator=g, device=dev)
             keys = torch.randint(0, cfg.num_rows, (B, cfg.F), generator=g, device=dev)
-            y = (dense[:, 0] > 0).float()
-            return m.train_step(dense, keys, y)
+            return dense, keys, (dense[:, 0] > 0).float()
+
+        state = {"cur": batch()}
+
+        def step():  # next batch generated one step ahead: lookahead key planning
+            nxt = batch()
+            cur, state["cur"] = state["cur"], nxt
+            return m.train_step(*cur, next_keys=nxt[1])
 
         return m, step, B, "samples/s", dict(model=f"DLRM {cfg.num_rows} rows x {cfg.D} (26 sparse + 13 dense), "
-                                                   f"{cfg.consistency}", seq_len=None)
+                                                   f"{cfg.consistency}", seq_len=None,
+                                             rows_per_gpu=cfg.num_rows // comm.world, consistency=cfg.consistency)
     if args.model == "lr":
         from minips_amd.data.synthetic import SparseLRSynth
         from minips_amd.models.lr import SparseLR, SparseLRConfig
@@ -89,8 +104,15 @@ def build(args, comm):
         cfg = WideDeepConfig(consistency="ssp", staleness=max(1, args.staleness))
         m = WideDeep(cfg, comm)
         data = CriteoSynth(B, cards=cfg.cards, device=dev, seed=1000 + r)
-        return m, (lambda: m.train_step(*data.next())), B, "samples/s", \
-            dict(model="Wide&Deep Criteo SSP", seq_len=None)
+        state = {"cur": data.next()}
+
+        def step():
+            nxt = data.next()
+            cur, state["cur"] = state["cur"], nxt
+            return m.train_step(*cur, next_keys=nxt[1])
+
+        return m, step, B, "samples/s", dict(model="Wide&Deep Criteo SSP", seq_len=None,
+                                             consistency=f"ssp{cfg.staleness}")
     raise SystemExit(f"unknown model {args.model}")
 
 
@@ -102,6 +124,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (samples or sequences)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--rows", type=int, default=100_000_000, help="DLRM embedding rows (whole table)")
+    ap.add_argument("--rows-per-gpu", type=int, default=1_250_000_000, help="dlrm-10b: rows per GPU shard")
     ap.add_argument("--consistency", default="bsp")
     ap.add_argument("--staleness", type=int, default=0)
     args = ap.parse_args()
@@ -129,10 +152,10 @@ def main():
     el = float(t)
     if comm.rank == 0:
         print(json.dumps({
-            "metric": f"{unit.split('/')[0]}/sec (whole job) {args.model} {args.consistency}",
+            "metric": f"{unit.split('/')[0]}/sec (whole job) {args.model} {cfg.pop('consistency', args.consistency)}",
             "value": round(per_step * comm.world * args.steps / el, 1), "unit": unit, "n_gpus": comm.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "dtype": "bf16" if args.model in ("mlp", "gpt2", "dlrm",
+            "higher_is_better": True, "scaling": "weak", "dtype": "bf16" if args.model in ("mlp", "gpt2", "dlrm", "dlrm-10b",
                                                                                             "widedeep-ssp") else "fp32",
             "data": "synthetic", "last": float(out.float().sum()) if torch.is_tensor(out) else None,
             "config": dict(cfg, parallelism=f"ps-dp{comm.world}"),
