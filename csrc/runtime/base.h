@@ -31,6 +31,22 @@
 
 namespace minips {
 
+// Timed condition wait. libstdc++ maps a steady_clock wait_for to pthread_cond_clockwait, which
+// the gcc-11 ThreadSanitizer does not intercept (the unlock/relock inside the wait is invisible ->
+// false "double lock" and race reports), so sanitizer builds wait on the system clock instead.
+template <class Pred>
+inline bool CondWaitFor(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, double seconds, Pred pred) {
+#if defined(__SANITIZE_THREAD__)
+  const auto deadline = std::chrono::system_clock::now() +
+                        std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                            std::chrono::duration<double>(seconds));
+  return cv.wait_until(lk, deadline, pred);
+#else
+  return cv.wait_for(lk, std::chrono::duration<double>(seconds), pred);
+#endif
+}
+
+
 using Key = uint64_t;
 
 // ---------------------------------------------------------------------------------------
@@ -176,11 +192,11 @@ struct Range {
 template <typename T>
 class ThreadsafeQueue {
  public:
+  // Notifies while holding the lock: a waiter that pops the element and then destroys the queue
+  // (a call-scoped reply queue, Engine::InitTable) cannot do so while Push still touches it.
   void Push(T elem) {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      queue_.push_back(std::move(elem));
-    }
+    std::lock_guard<std::mutex> lk(mu_);
+    queue_.push_back(std::move(elem));
     cond_.notify_all();
   }
   void WaitAndPop(T* elem) {
@@ -192,7 +208,7 @@ class ThreadsafeQueue {
   // Returns false on timeout (the reference has no timeouts: a hung barrier hangs forever).
   bool WaitAndPopFor(T* elem, double seconds) {
     std::unique_lock<std::mutex> lk(mu_);
-    if (!cond_.wait_for(lk, std::chrono::duration<double>(seconds), [this] { return !queue_.empty(); }))
+    if (!CondWaitFor(cond_, lk, seconds, [this] { return !queue_.empty(); }))
       return false;
     *elem = std::move(queue_.front());
     queue_.pop_front();

@@ -290,15 +290,18 @@ void Mailbox::Dispatch(Message&& msg) {
     default:
       break;
   }
-  ThreadsafeQueue<Message>* q = nullptr;
+  // Push under queue_mu_: DeregisterQueue (same lock) then guarantees no push is in flight, so a
+  // queue can be destroyed right after it is deregistered (TSan-found use-after-free otherwise).
+  bool delivered = false;
   {
     std::lock_guard<std::mutex> lk(queue_mu_);
     auto it = queue_map_.find((uint32_t)msg.meta.recver);
-    if (it != queue_map_.end()) q = it->second;
+    if (it != queue_map_.end()) {
+      it->second->Push(std::move(msg));
+      delivered = true;
+    }
   }
-  if (q) {
-    q->Push(std::move(msg));
-  } else {
+  if (!delivered) {
     MINIPS_LOG(1, "mailbox " << node_.id << ": no queue for recver " << msg.meta.recver << " ("
                              << FlagName(msg.meta.flag) << "), dropped");
   }
@@ -402,8 +405,7 @@ void Mailbox::Barrier() {
     std::lock_guard<std::mutex> nl(nodes_mu_);
     return (int)nodes_.size() + ((has_scale_ && !HasNode(nodes_, scale_node_.id)) ? 1 : 0);
   };
-  bool ok = barrier_cond_.wait_for(lk, std::chrono::duration<double>(timeout),
-                                   [&] { return barrier_count_ >= target(); });
+  bool ok = CondWaitFor(barrier_cond_, lk, timeout, [&] { return barrier_count_ >= target(); });
   MINIPS_CHECK(ok, "node " << node_.id << " barrier timed out (" << barrier_count_ << "/" << target() << ")");
   MINIPS_VLOG(2, "mailbox " << node_.id << " barrier passed (" << barrier_count_ << "/" << target() << ")");
   barrier_count_ -= target();

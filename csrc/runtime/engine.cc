@@ -90,7 +90,7 @@ void Engine::StartHeartbeatThread() {
     SendHeartBeat(false);  // announce immediately (recovering nodes trigger rollback on it)
     while (heartbeat_running_) {
       std::unique_lock<std::mutex> lk(hb_mu_);
-      hb_cond_.wait_for(lk, std::chrono::milliseconds(period), [this] { return !heartbeat_running_; });
+      CondWaitFor(hb_cond_, lk, period / 1000.0, [this] { return !heartbeat_running_; });
       if (!heartbeat_running_) break;
       lk.unlock();
       SendHeartBeat(false);
@@ -479,7 +479,7 @@ void HeartBeatCheckThread::Main() {
   while (true) {
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cond_.wait_for(lk, std::chrono::milliseconds(period), [this] { return !running_; });
+      CondWaitFor(cond_, lk, period / 1000.0, [this] { return !running_; });
       if (!running_) return;
     }
     if (mt_->AllQuit()) return;

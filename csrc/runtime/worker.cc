@@ -24,7 +24,7 @@ void CallbackRunner::WaitRequest(uint32_t app_tid, uint32_t model_id) {
     return t.first <= t.second;
   };
   if (timeout_s_ > 0) {
-    MINIPS_CHECK(cond_.wait_for(lk, std::chrono::duration<double>(timeout_s_), done),
+    MINIPS_CHECK(CondWaitFor(cond_, lk, timeout_s_, done),
                  "request of thread " << app_tid << " table " << model_id << " timed out");
   } else {
     cond_.wait(lk, done);
@@ -65,7 +65,7 @@ void CallbackRunner::WaitCheckPoint() {
   std::unique_lock<std::mutex> lk(mu_);
   auto done = [&] { return checkpoint_expected_ <= checkpoint_current_; };
   if (timeout_s_ > 0) {
-    MINIPS_CHECK(cond_.wait_for(lk, std::chrono::duration<double>(timeout_s_), done), "checkpoint timed out");
+    MINIPS_CHECK(CondWaitFor(cond_, lk, timeout_s_, done), "checkpoint timed out");
   } else {
     cond_.wait(lk, done);
   }

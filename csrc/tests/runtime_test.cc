@@ -275,7 +275,8 @@ TEST(BSPModel, CheckGetAndAdd) {
   std::unique_ptr<AbstractStorage> st(new MapStorage<int>());
   BSPModel model(0, std::move(st), &q, CheckpointConfig());
   ResetWorkers(&model, &q, {2, 3});
-  model.Get(*new Message(KV<int>(Flag::kGet, 2, {1})));
+  Message g0 = KV<int>(Flag::kGet, 2, {1});
+  model.Get(g0);
   ASSERT_EQ(q.Size(), 1u);
   Message useless;
   q.WaitAndPop(&useless);

@@ -47,6 +47,10 @@ def _is_local(host: str) -> bool:
 
 def _binary(app: str) -> str:
     p = APPS.get(app, app)
+    # MINIPS_BIN_DIR swaps the build (e.g. build/san_thread/bin for sanitizer runs of the apps)
+    bdir = os.environ.get("MINIPS_BIN_DIR")
+    if bdir and app in APPS:
+        p = os.path.join(bdir, os.path.basename(p))
     return p if os.path.isabs(p) else os.path.join(ROOT, p)
 
 

@@ -8,6 +8,8 @@ Targets
   apps      csrc/apps/*.cc               -> build/bin/<app>
   kernels   csrc/kernels/*.hip           -> build/obj/k_*.o   (hipcc --offload-arch=gfx950)
   ops_py    csrc/bindings/ops_py.cpp     -> minips_amd/_kernels*.so   (hipcc, torch headers)
+  san_thread / san_address   runtime + runtime_test + apps built with -fsanitize=thread|address
+            (host code only) -> build/san_<kind>/bin/ (race detection on the runtime)
 
 Rebuilds are mtime-driven: a target is rebuilt when any of its sources or any header in
 its source directories is newer than the output.  `python tools/build.py [targets...]`.
@@ -157,8 +159,40 @@ def build_ops_py(kobjs: list[str]) -> str:
     return out
 
 
+def build_sanitized(kind: str) -> list[str]:
+    """The CPU runtime, its unit/integration tests and the apps under a sanitizer."""
+    d = os.path.join(BUILD, f"san_{kind}")
+    obj, bin_ = os.path.join(d, "obj"), os.path.join(d, "bin")
+    os.makedirs(obj, exist_ok=True)
+    os.makedirs(bin_, exist_ok=True)
+    flags = [f for f in CXXFLAGS if f != "-O2"] + ["-O1", "-g", f"-fsanitize={kind}", "-fno-omit-frame-pointer"]
+    hdrs = _headers("csrc/runtime")
+    jobs, objs = [], []
+    for src in sorted(glob.glob(os.path.join(ROOT, "csrc/runtime/*.cc"))):
+        out = os.path.join(obj, os.path.basename(src)[:-3] + ".o")
+        objs.append(out)
+        jobs.append((out, [src] + hdrs, [CXX, *flags, "-c", src, "-o", out]))
+    _compile_many(jobs)
+    outs, jobs = [], []
+    srcs = [os.path.join(ROOT, "csrc/tests/runtime_test.cc")] + sorted(glob.glob(os.path.join(ROOT, "csrc/apps/*.cc")))
+    for src in srcs:
+        out = os.path.join(bin_, os.path.basename(src)[:-3])
+        outs.append(out)
+        jobs.append((out, [src] + objs + _headers("csrc/runtime", "csrc/tests", "csrc/apps"),
+                     [CXX, *flags, src, *objs, "-o", out]))
+    _compile_many(jobs)
+    return outs
+
+
 def main(argv: list[str]) -> int:
     targets = set(argv) or {"runtime", "rt_py", "tests", "apps", "kernels", "ops_py"}
+    for kind in ("thread", "address"):
+        if f"san_{kind}" in targets:
+            for o in build_sanitized(kind):
+                print("built", o)
+            targets.discard(f"san_{kind}")
+            if not targets:
+                return 0
     objs = runtime_objs()
     if "rt_py" in targets:
         print("built", build_runtime_py(objs))
