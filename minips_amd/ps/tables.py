@@ -98,6 +98,14 @@ class _Pipeline:
     def wait_for_read(self):
         """Before a Get at clock c: updates of clocks <= c - s - 1 must be applied."""
         self.wait_clock(self.clock - self.staleness - 1)
+        if self.async_ and self.events:
+            # observed staleness of this read: earlier clocks whose update is still in flight
+            # (non-blocking event queries; the metrics JSONL reports the histogram per step)
+            from ..utils.metrics import get_logger
+
+            log = get_logger()
+            log.observe_pending(len(self.events))
+            log.observe_staleness(sum(1 for ev in self.events.values() if not ev.query()))
 
     def keep_alive(self, *tensors):
         """Tensors produced on the compute stream and consumed on the side stream."""
@@ -256,6 +264,17 @@ class DenseTable:
         self.comm.all_gather(self.params, own)
 
 
+_ROUTE_PRIMES = (402653189, 201326611, 100663319, 50331653, 25165843, 12582917, 6291469, 3145739, 1572869)
+
+
+def _route_multiplier(num_rows: int) -> int:
+    """A prime multiplier coprime to num_rows with key * A < 2^63 (0: no mixing possible)."""
+    for p in _ROUTE_PRIMES:
+        if num_rows % p and num_rows * p < (1 << 63) and p < num_rows:
+            return p
+    return 0
+
+
 @dataclass
 class SparsePlan:
     """Routing of one batch's keys. Row counts are host ints on multi-rank runs (the all-to-all
@@ -296,8 +315,16 @@ class SparseTable:
     def __init__(self, comm: Comm, num_rows: int, width: int, optimizer: str = "rowwise_adagrad",
                  lr: float = 0.01, eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "bsp",
                  staleness: int = 0, split: int | None = None, table_id: int = 0, init_std: float = 0.01,
-                 seed: int = 1234, p2p: bool | None = None, push_dtype=None):
+                 seed: int = 1234, p2p: bool | None = None, push_dtype=None, route: str = "mix"):
         self.comm = comm
+        # Key -> row placement. "range": row = key (the reference's contiguous range partition).
+        # "mix" (default): row = key * A mod num_rows, a bijection (A prime, coprime to num_rows),
+        # then the same equal ranges: contiguous key blocks (a big feature of a concatenated
+        # table, or a hot id range) spread over every shard instead of overloading one owner --
+        # on Criteo-shaped batches the busiest of 8 range owners serves 6x the rows of the
+        # quietest. Rows, checkpoints and re-sharding live in the routed space (it depends on
+        # num_rows only, so any world size agrees).
+        self.route_mult = _route_multiplier(num_rows) if route == "mix" else 0
         # gradient rows cross xGMI in bf16 on multi-GPU runs (half the push bytes; the owner
         # accumulates in fp32), fp32 otherwise
         self.push_dtype = push_dtype or (torch.bfloat16 if comm.device.type == "cuda" and comm.world > 1
@@ -340,7 +367,9 @@ class SparseTable:
 
     # -- KV API -----------------------------------------------------------------------------
     def _route_keys(self, keys: torch.Tensor) -> torch.Tensor:
-        """Keys as exchanged between ranks (identity for range-partitioned tables)."""
+        """Keys as exchanged between ranks and stored: the global row of each key."""
+        if self.route_mult:
+            return (keys * self.route_mult) % self.num_rows
         return keys
 
     def _serve_index(self, plan: SparsePlan):
