@@ -117,7 +117,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
 }
 
 // Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P], U [1]).
-std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tensor& bounds, int64_t F) {
+std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tensor& bounds, int64_t F,
+                                         int64_t route_mult, int64_t route_n) {
   check_gpu(keys, "keys");
   check_gpu(bounds, "bounds");
   check_dtype(keys, at::kLong, "keys");
@@ -138,7 +139,7 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   minips_k::unique_bucketize(ptr<int64_t>(keys), n, (int)F, ptr<int64_t>(bounds), P, ptr<int64_t>(table_keys),
                              ptr<int64_t>(table_pos), cap, ptr<int64_t>(slot), ptr<int32_t>(flags),
                              ptr<int64_t>(counts), ptr<int64_t>(cursor), ptr<int64_t>(out_keys), ptr<int64_t>(inverse),
-                             stream_of(keys));
+                             stream_of(keys), (uint64_t)route_mult, (uint64_t)route_n);
   return {out_keys, inverse, counts.narrow(0, 0, P), counts.narrow(0, P, 1)};
 }
 
@@ -709,7 +710,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("add_bf16", &add_bf16);
   m.def("dlrm_interact_fwd", &dlrm_interact_fwd);
   m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
-  m.def("unique_bucketize", &unique_bucketize, py::arg("keys"), py::arg("bounds"), py::arg("F") = 1);
+  m.def("unique_bucketize", &unique_bucketize, py::arg("keys"), py::arg("bounds"), py::arg("F") = 1,
+        py::arg("route_mult") = 0, py::arg("route_n") = 0);
   m.def("gather_rows", &gather_rows, py::arg("table"), py::arg("keys"), py::arg("base"), py::arg("out"),
         py::arg("n_dev") = py::none());
   m.def("scatter_add_rows", &scatter_add_rows);

@@ -43,9 +43,11 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
 // (counts[P] = total unique on return),
 // cursor [P] (all state re-initialised inside).
 // keys may be a [B, F] batch (F > 1): tiles are then taken feature-major for better dedupe.
+// route_mult != 0 dedupes the ROUTED keys key * route_mult mod route_n (uniq holds routed keys).
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
-                      int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s);
+                      int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult = 0,
+                      uint64_t route_n = 0);
 
 // Row gather from a shard: out[i, :] = table[keys[i] - base, :] with dtype conversion.
 // table fp32 [R, D] row stride ld; out fp32 or bf16 [n, D].

@@ -58,10 +58,17 @@ __device__ __forceinline__ unsigned long long wave_agg_inc(unsigned long long* c
 constexpr int kUbTile = 256;
 constexpr int kUbLds = 512;
 
+// Optional key routing fused into the dedupe: key -> key * mult mod rn (a bijection of [0, rn) when
+// mult is coprime to rn; the caller guarantees key * mult < 2^63). mult == 0: identity.
+__device__ __forceinline__ int64_t route_key(int64_t key, uint64_t mult, uint64_t rn) {
+  return mult ? (int64_t)(((uint64_t)key * mult) % rn) : key;
+}
+
 __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t rows_b,
                                                             int F, const int64_t* __restrict__ bounds, int P,
                                                             unsigned long long* table_keys, int64_t cap, int64_t* slot,
-                                                            int32_t* flags, unsigned long long* counts) {
+                                                            int32_t* flags, unsigned long long* counts, uint64_t rmult,
+                                                            uint64_t rn) {
   __shared__ unsigned long long lkey[kUbLds];
   __shared__ long long lgslot[kUbLds];
   __shared__ unsigned int lcount[256];  // per-owner claims of this block (P <= 256)
@@ -73,7 +80,7 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
   const bool valid = i < n;
   int64_t phys = i;
   if (F > 1 && valid) phys = (i % rows_b) * F + i / rows_b;  // feature-major tile
-  const int64_t key = valid ? keys[phys] : 0;
+  const int64_t key = valid ? route_key(keys[phys], rmult, rn) : 0;
   int lslot = 0;
   bool lead = false;
   if (valid) {
@@ -139,7 +146,8 @@ __global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restric
                                                         const int64_t* __restrict__ slot,
                                                         const int32_t* __restrict__ flags,
                                                         const int64_t* __restrict__ counts, unsigned long long* cursor,
-                                                        int64_t* table_pos, int64_t* out_keys) {
+                                                        int64_t* table_pos, int64_t* out_keys, uint64_t rmult,
+                                                        uint64_t rn) {
   __shared__ int64_t offs[kUbMaxP];
   __shared__ unsigned int lcnt[kUbMaxP];
   __shared__ unsigned long long lbase[kUbMaxP];
@@ -159,7 +167,7 @@ __global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restric
   int o = 0;
   unsigned int r = 0;
   if (claimer) {
-    key = keys[i];
+    key = route_key(keys[i], rmult, rn);
     o = owner_of(bounds, P, key);
     r = atomicAdd(lcnt + o, 1u);
   }
@@ -182,8 +190,10 @@ __global__ void ub_inverse_kernel(int64_t n, const int64_t* __restrict__ slot, c
 
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
-                      int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s) {
+                      int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult,
+                      uint64_t route_n) {
   if (F < 1 || n % F) throw std::runtime_error("unique_bucketize: n must be a multiple of F");
+  if (route_mult && !route_n) throw std::runtime_error("unique_bucketize: routing needs the row count");
   if (P < 1 || P > kUbMaxP) throw std::runtime_error("unique_bucketize: 1 <= P <= 256 owner shards");
   if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
   if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
@@ -199,9 +209,10 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
   const int grid = grid_for(n, block, 4096);
   const int64_t tiles = (n + kUbTile - 1) / kUbTile;
   hipLaunchKernelGGL(ub_insert_kernel, dim3((unsigned)tiles), dim3(kUbTile), 0, s, keys, n, n / F, F, bounds, P,
-                     (unsigned long long*)table_keys, cap, slot, flags, (unsigned long long*)counts);
+                     (unsigned long long*)table_keys, cap, slot, flags, (unsigned long long*)counts, route_mult,
+                     route_n);
   hipLaunchKernelGGL(ub_assign_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, keys, n, bounds, P, slot,
-                     flags, counts, (unsigned long long*)cursor, table_pos, out_keys);
+                     flags, counts, (unsigned long long*)cursor, table_pos, out_keys, route_mult, route_n);
   hipLaunchKernelGGL(ub_inverse_kernel, grid, block, 0, s, n, slot, table_pos, inverse);
   MINIPS_HIP_CHECK(hipGetLastError());
 }

@@ -148,12 +148,18 @@ def unique_bucketize(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1):
     return uniq, inv, counts
 
 
-def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1):
+def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1, route_mult: int = 0,
+                       route_n: int = 0):
     """unique_bucketize plus the total unique count U as a 1-element device tensor, so that
     consumers (gather_rows / sparse_* with ``n_dev``, wd_emb_backward with ``U_dev``) bound
-    their work on the GPU without a host round trip."""
+    their work on the GPU without a host round trip. ``route_mult`` != 0 first maps every key to
+    key * route_mult mod route_n (fused into the GPU kernel)."""
     if _gpu(keys):
-        return tuple(kernels().unique_bucketize(keys.contiguous(), bounds.contiguous(), int(F)))
+        return tuple(kernels().unique_bucketize(keys.contiguous(), bounds.contiguous(), int(F), int(route_mult),
+                                                int(route_n)))
+    keys = keys.reshape(-1)
+    if route_mult:
+        keys = (keys * route_mult) % route_n
     u, inv = torch.unique(keys, sorted=True, return_inverse=True)
     owner = torch.bucketize(u, bounds[1:-1], right=True)
     counts = torch.bincount(owner, minlength=bounds.numel() - 1)

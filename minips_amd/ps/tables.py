@@ -387,8 +387,15 @@ class SparseTable:
         pp = _PendingPlan()
         pp.keys = keys
         pp.F = keys.shape[1] if keys.dim() == 2 else 1
-        pp.flat = self._route_keys(keys.reshape(-1).to(torch.int64))
-        pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.unique_bucketize_n(pp.flat, self.bounds, pp.F)
+        flat = keys.reshape(-1).to(torch.int64)
+        rmult = getattr(self, "route_mult", 0)
+        if rmult:  # range tables: the routing is fused into the dedupe kernel
+            pp.flat = flat
+            pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.unique_bucketize_n(flat, self.bounds, pp.F, rmult,
+                                                                          self.num_rows)
+        else:
+            pp.flat = self._route_keys(flat)
+            pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.unique_bucketize_n(pp.flat, self.bounds, pp.F)
         pp.csr = ops.emb_build_csr(pp.inv, pp.F, pp.flat.numel()) if csr and pp.inv.is_cuda else None
         pp.host = pp.event = None
         if self.comm.world > 1:

@@ -300,3 +300,19 @@ def test_kmeans_assign_mfma(dev, n, k, d):
     chosen = dist_ref.gather(1, a.view(-1, 1)).view(-1)
     assert bool(((chosen - best_ref) <= 1e-4 * best_ref.abs() + 1e-4).all())
     torch.testing.assert_close(dist.cpu().double(), best_ref, rtol=1e-4, atol=1e-3)
+
+
+def test_unique_bucketize_fused_routing(dev):
+    """key -> key*A mod N routing fused into the dedupe kernel matches routing first on the CPU."""
+    from minips_amd.ps.tables import _route_multiplier
+
+    g = torch.Generator().manual_seed(8)
+    N = 33_762_577
+    A = _route_multiplier(N)
+    keys = torch.randint(0, N, (4096, 26), generator=g)
+    keys[:, 3] = keys[0, 3]  # a hot id
+    bounds = torch.tensor([0, N // 4, N // 2, 3 * (N // 4), N])
+    u, inv, c, U = ops.unique_bucketize_n(keys.to(dev), bounds.to(dev), 26, A, N)
+    ur, invr, cr, Ur = ops.unique_bucketize_n(keys, bounds, 26, A, N)
+    assert int(U) == int(Ur) and c.cpu().tolist() == cr.tolist()
+    assert torch.equal(u.cpu()[inv.cpu()], (keys.reshape(-1) * A) % N)

