@@ -57,13 +57,16 @@ class _Pipeline:
     gate to s clocks, ASP to a fixed pipelining depth. On CPU (gloo tests) the work runs inline.
     """
 
-    def __init__(self, comm: Comm, consistency: str, staleness: int, overlap: bool | None = None):
+    def __init__(self, comm: Comm, consistency: str, staleness: int, overlap: bool | None = None,
+                 kind: str = ""):
         self.consistency = consistency
         self.staleness = staleness if consistency == "ssp" else (0 if consistency == "bsp" else 2)
         overlap = _overlap_default() if overlap is None else overlap
         if consistency == "bsp":
-            # one rank has no communication to hide: the extra stream hops only cost (measured)
-            self.async_ = comm.device.type == "cuda" and overlap and comm.world > 1
+            # one rank has no communication to hide; MINIPS_OVERLAP_W1 lists the table kinds that
+            # still run their clock on a side stream there (the apply overlapping other compute)
+            w1 = os.environ.get("MINIPS_OVERLAP_W1", "").split(",")
+            self.async_ = comm.device.type == "cuda" and overlap and (comm.world > 1 or kind in w1)
         else:
             self.async_ = comm.device.type == "cuda" and self.staleness > 0
         self.stream = torch.cuda.Stream(device=comm.device) if self.async_ else None
@@ -144,7 +147,7 @@ class DenseTable:
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self.grad_shard = torch.zeros(self.shard, dtype=torch.float32, device=dev)
         self.step = 0
-        self.pipe = _Pipeline(comm, consistency, staleness)
+        self.pipe = _Pipeline(comm, consistency, staleness, kind="dense")
         # collective: this table's clock communicator is created up front, in constructor order
         self.lane = comm.lane(f"dense{table_id}") if self.pipe.async_ else comm
         self._pending = False
@@ -355,7 +358,7 @@ class SparseTable:
 
     def _init_comm(self, consistency, staleness, p2p):
         comm = self.comm
-        self.pipe = _Pipeline(comm, consistency, staleness)
+        self.pipe = _Pipeline(comm, consistency, staleness, kind="sparse")
         # collective, in constructor order on every rank: the push lane (side-stream clock work)
         # and the planning lane (lookahead dedupe + count exchange)
         self.lane = comm.lane(f"sparse{self.table_id}") if self.pipe.async_ else comm
