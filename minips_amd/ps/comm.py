@@ -214,13 +214,20 @@ def init_distributed(backend: str | None = None) -> Comm:
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # MINIPS_DIST_BACKEND=gloo (+ MINIPS_SHARE_DEVICE=1): the multi-rank test harness on one
+            # card (RCCL refuses two ranks on one device); production picks RCCL whenever GPUs exist
+            backend = os.environ.get("MINIPS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        # test harness only: several ranks on one card (MINIPS_SHARE_DEVICE=1 -> all on device 0)
+        if os.environ.get("MINIPS_SHARE_DEVICE") == "1":
+            local = 0
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group(backend, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+            if torch.cuda.is_available():
+                torch.cuda.set_device(local)
     elif torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     return Comm()

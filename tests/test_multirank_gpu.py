@@ -96,3 +96,24 @@ def test_widedeep_overlap_matches_sync():
         assert dd <= 6 * 2e-3 and dmean <= 2e-5, (rank, dd, dmean)
         # row-wise Adagrad (lr 0.02) normalises the same way
         assert de <= 6 * 2 * 0.02 and emean <= 1e-5, (rank, de, emean)
+
+
+def test_bench_two_ranks_end_to_end():
+    """bench.py under torchrun with 2 ranks (gloo staging on one card): the driver's multi-GPU
+    control flow -- lanes, lookahead planning, barriers, max-over-ranks timing, one JSON line."""
+    import json
+    import subprocess
+    import sys
+
+    from _util import ROOT, free_ports
+
+    env = dict(os.environ, MINIPS_SHARE_DEVICE="1", MINIPS_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_ports(1)[0]), "bench.py", "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--batch", "2048"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["value"] > 0 and out["config"]["global_batch"] == 4096
