@@ -283,6 +283,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
 // next stage stays in flight), one before its buffer is refilled.
 constexpr int BK2 = 64;
 constexpr uint32_t kOobOffset = 0x80000000u;
+#ifndef MINIPS_GEMM_SETPRIO
+#define MINIPS_GEMM_SETPRIO 0  // T5 setprio pair: measured -1..-4 % here (tools/gpu_gemm_ab.sh)
+#endif
+constexpr bool kSetPrio = MINIPS_GEMM_SETPRIO != 0;
 
 __device__ __forceinline__ int swz_k(int k) { return 2 * ((k & 3) | ((((k >> 2) ^ (k >> 3)) & 1) << 2)); }
 
@@ -401,12 +405,14 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
       for (int i = 0; i < 4; ++i) af[i] = frag2<A_KM, PERM, TM>(SA, wm * 64 + i * 16, ks, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = frag2<B_KN, PERM, TN>(SB, wn * 64 + j * 16, ks, lane);
+      if (kSetPrio) __builtin_amdgcn_s_setprio(1);  // T5: keeps the cluster between the barriers
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i]),
                                                               __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+      if (kSetPrio) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is refilled
@@ -510,12 +516,14 @@ __global__ __launch_bounds__(512) void gemm_v3_kernel(const bf16_t* __restrict__
       for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag2<A_KM, PERM, 128>(SA, i * 16, ks, lane);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) bfr[ks] = frag2<B_KN, PERM, 128>(SB, bcol, ks, lane);
+    if (kSetPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i][ks]),
                                                             __builtin_bit_cast(v8bf, bfr[ks]), acc[i][0], 0, 0, 0);
+    if (kSetPrio) __builtin_amdgcn_s_setprio(0);
     if (EARLY_A) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's A reads of this buffer retired
@@ -527,12 +535,14 @@ __global__ __launch_bounds__(512) void gemm_v3_kernel(const bf16_t* __restrict__
     for (int j = 1; j < 4; ++j) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) bfr[ks] = frag2<B_KN, PERM, 128>(SB, bcol + j * 16, ks, lane);
+      if (kSetPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 8; ++i)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i][ks]),
                                                               __builtin_bit_cast(v8bf, bfr[ks]), acc[i][j], 0, 0, 0);
+      if (kSetPrio) __builtin_amdgcn_s_setprio(0);
     }
     // ---- end of K-step: operands of t+1 landed (A(t+2) may stay in flight), B halves free
     if (EARLY_A && t + 2 < nt) {
