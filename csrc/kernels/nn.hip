@@ -191,26 +191,38 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __rest
 
 // dgamma/dbeta[j] += sum_g partial[g][j], j < 2C: 64 columns per block (coalesced rows), the
 // block's 4 waves split the G partial rows and combine in LDS.
+// blockIdx.y takes a slice of the G partial rows (kColsumSlices slices, fp32 atomics into the
+// parameter gradients) so the reduction spreads over ~24 x 16 blocks instead of 24 serial ones.
+constexpr int kColsumSlices = 16;
+
 __global__ __launch_bounds__(256) void layernorm_colsum_kernel(const float* __restrict__ partial, int G, int C,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
+  const int per = (G + gridDim.y - 1) / gridDim.y;
+  const int g0 = blockIdx.y * per, g1 = min(G, g0 + per);
   float s = 0.f;
   if (j < 2 * C)
-    for (int g = w; g < G; g += 4) s += partial[(int64_t)g * 2 * C + j];
+    for (int g = g0 + w; g < g1; g += 4) s += partial[(int64_t)g * 2 * C + j];
   red[w][lane] = s;
   __syncthreads();
   if (w == 0 && j < 2 * C) {
     const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    if (j < C)
-      dgamma[j] += t;
-    else
-      dbeta[j - C] += t;
+    if (gridDim.y == 1) {
+      if (j < C)
+        dgamma[j] += t;
+      else
+        dbeta[j - C] += t;
+    } else {
+      atomicAdd(j < C ? dgamma + j : dbeta + (j - C), t);
+    }
   }
 }
 
-int layernorm_bwd_blocks(int64_t M) { return (int)std::min<int64_t>(std::max<int64_t>((M + 31) / 32, 1), 512); }
+// ~8 rows per 4-wave block: 4x the waves of a 32-rows-per-block split, so the row loop's
+// dependent load -> reduce -> store chain is hidden by occupancy instead of serialised.
+int layernorm_bwd_blocks(int64_t M) { return (int)std::min<int64_t>(std::max<int64_t>((M + 7) / 8, 1), 1024); }
 
 void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gamma, const bf16_t* beta, float eps,
                    bf16_t* y, int ldy, float* mean, float* rstd, hipStream_t s) {
@@ -230,7 +242,8 @@ void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t
   hipLaunchKernelGGL(layernorm_bwd_kernel, G, 256, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx, partial,
                      accumulate_dx);
   MINIPS_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(layernorm_colsum_kernel, (2 * C + 63) / 64, 256, 0, s, partial, G, C, dgamma, dbeta);
+  hipLaunchKernelGGL(layernorm_colsum_kernel, dim3((2 * C + 63) / 64, G >= 64 ? kColsumSlices : 1), 256, 0, s,
+                     partial, G, C, dgamma, dbeta);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
