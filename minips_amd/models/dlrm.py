@@ -155,7 +155,15 @@ class DLRM:
                 dy = dx
         self.dense.add()
         self.dense.clock()
+        self._advance_next_plan()
         return b["loss"]
+
+    def _advance_next_plan(self):
+        """The step is issued: exchange the prefetched plan's keys now (planning stream), off
+        the next step's critical path (SparseTable.advance_plan)."""
+        pre = getattr(self, "_next_plan", None)
+        if pre is not None:
+            self._next_plan = (pre[0], self.emb.advance_plan(pre[1]))
 
     def drain(self):
         self.emb.drain()

@@ -434,8 +434,9 @@ class SparseTable:
             pp.event.record(ps)
         return pp
 
-    def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
+    def _finish_plan(self, pp: _PendingPlan, comm: Comm | None = None) -> SparsePlan:
         dev = self.comm.device
+        comm = comm or self.comm
         n = pp.flat.numel()
         if pp.event is not None:
             torch.cuda.current_stream(dev).wait_event(pp.event)
@@ -449,7 +450,7 @@ class SparseTable:
         send, recv = pp.host[0].tolist(), pp.host[1].tolist()
         U, M = int(sum(send)), int(sum(recv))
         recv_keys = torch.empty(M, dtype=torch.int64, device=dev)
-        self.comm.all_to_all_v(recv_keys, pp.uniq, recv, send, p2p=self.p2p)
+        comm.all_to_all_v(recv_keys, pp.uniq, recv, send, p2p=self.p2p)
         p = SparsePlan(n, pp.inv, pp.uniq, U, send, recv, recv_keys, csr=pp.csr, _U=U)
         if M > 0:
             # owner-side dedupe of the keys requested by all ranks (the push sums their rows)
@@ -462,6 +463,25 @@ class SparseTable:
     def plan(self, keys: torch.Tensor, csr: bool = False) -> SparsePlan:
         return self._finish_plan(self._start_plan(keys, csr))
 
+    def advance_plan(self, pending):
+        """Second half of lookahead planning, called once the current step is issued: wait (host)
+        for the pending plan's counts, then issue the all-to-all of its keys and the owner-side
+        dedupe on the planning stream / lane, so that only the row gather and the row exchange
+        remain on the critical path of the step that uses the plan."""
+        if not isinstance(pending, _PendingPlan) or self.comm.world == 1 or self.comm.device.type != "cuda":
+            return pending
+        ps = self.comm.plan_stream()
+        cur = torch.cuda.current_stream(self.comm.device)
+        with torch.cuda.stream(ps):
+            plan = self._finish_plan(pending, comm=self.plan_lane)
+            ev = torch.cuda.Event()
+            ev.record(ps)
+        for t in (plan.recv_keys, plan.own_uniq, plan.own_inv, plan.own_U_dev):
+            if t is not None:
+                t.record_stream(cur)
+        plan.extra["ready"] = ev
+        return plan
+
     def get(self, keys: torch.Tensor, plan=None):
         """Pull rows of ``keys``. Returns (rows [cap, width] in unique order, plan); the row of
         keys[i] is rows[plan.inv[i]]. ``plan`` may be a plan_async() handle for these keys."""
@@ -469,6 +489,9 @@ class SparseTable:
             plan = self.plan(keys)
         elif isinstance(plan, _PendingPlan):
             plan = self._finish_plan(plan)
+        ready = plan.extra.pop("ready", None)
+        if ready is not None:  # keys exchanged on the planning stream (advance_plan)
+            torch.cuda.current_stream(self.comm.device).wait_event(ready)
         self.pipe.wait_for_read()  # BSP: the previous Clock's apply; SSP: clock c-s-1
         dev = self.comm.device
         served = torch.empty(len(plan.recv_keys), self.width, dtype=self.pull_dtype, device=dev)
