@@ -135,6 +135,20 @@ class Checkpointer:
         if blocking:
             self.commit()
 
+    def try_commit(self) -> bool:
+        """Publish the in-flight checkpoint if every rank's background writer has finished
+        (collective: one tiny MIN all-reduce while a checkpoint is pending, nothing otherwise);
+        training never blocks on the disk. Returns whether it was published."""
+        if self._pending_iter is None:
+            return False
+        done = torch.tensor([0.0 if (self._thread is not None and self._thread.is_alive()) else 1.0],
+                            device=self.comm.device)
+        self.comm.all_reduce_(done, op=__import__("torch.distributed", fromlist=["ReduceOp"]).ReduceOp.MIN)
+        if float(done.item()) < 1.0:
+            return False
+        self.commit()
+        return True
+
     def commit(self):
         """Finish the in-flight checkpoint on every rank and publish it (collective)."""
         if self._pending_iter is None:

@@ -45,10 +45,16 @@ def parse(argv=None):
     ap.add_argument("--heartbeat_dir", default="")
     ap.add_argument("--fail_rank", type=int, default=-1)
     ap.add_argument("--fail_step", type=int, default=-1)
+    ap.add_argument("--fail_mode", default="exit", choices=["exit", "hang"])
+    ap.add_argument("--checkpoint_commit", default="eager", choices=["eager", "async"],
+                    help="eager: publish a checkpoint at the next step (waits for its files); async: "
+                         "publish once every rank's writer finished (training never waits for the disk)")
     ap.add_argument("--with_injected_straggler", type=_flag_bool, default=False)
     ap.add_argument("--report_prefix", default="")
     ap.add_argument("--report_interval", type=int, default=10)
     ap.add_argument("--metrics_dir", default="")
+    ap.add_argument("--timing_skip", type=int, default=0,
+                    help="iterations excluded from steady_ms_per_iter (first-launch / warm-up costs)")
     ap.add_argument("--alpha", type=float, default=0.05)
     return ap.parse_args(argv)
 
@@ -176,13 +182,22 @@ def main(argv=None):
         data.skip(start)
         failed = int(os.environ.get("MINIPS_FAILED_RANK", "-1"))
         metrics.fault_tolerance_phase(4 if rank == failed else 5, f"rank {rank} restored iteration {start}")
-    inj = FaultInjector(rank, args.fail_rank, args.fail_step, args.with_injected_straggler, args.seed)
+    inj = FaultInjector(rank, args.fail_rank, args.fail_step, args.with_injected_straggler, args.seed,
+                        mode=args.fail_mode, heartbeat=hb)
     log = metrics.get_logger()
     losses = []
     report = open(args.report_prefix + f"report_{rank}", "a") if args.report_prefix else None
     t_start = time.perf_counter()
+    t_steady, n_steady = None, 0
     for it in range(start, args.steps):
-        ck.commit()  # publishes the checkpoint issued after the previous step (no-op otherwise)
+        if it == start + args.timing_skip:
+            if comm.device.type == "cuda":
+                torch.cuda.synchronize(comm.device)
+            t_steady, n_steady = time.perf_counter(), args.steps - it
+        if args.checkpoint_commit == "async":
+            ck.try_commit()  # publishes an in-flight checkpoint once every rank's files are written
+        else:
+            ck.commit()  # publishes the checkpoint issued after the previous step (no-op otherwise)
         inj.step(it)
         t0 = time.perf_counter()
         with metrics.range(f"step {it}"):
@@ -200,6 +215,9 @@ def main(argv=None):
                 and it + 1 < args.steps:
             ck.save(tables, iteration=it + 1)
     model.drain()
+    if comm.device.type == "cuda":
+        torch.cuda.synchronize(comm.device)
+    steady_ms = (time.perf_counter() - t_steady) * 1e3 / n_steady if t_steady is not None and n_steady else None
     ck.commit()
     # parameter checksum over every table (identical on all ranks)
     sums = torch.tensor([float(t.shard_state()[1][next(iter(t.shard_state()[1]))].double().sum())
@@ -212,7 +230,9 @@ def main(argv=None):
     if rank == 0:
         print(json.dumps(dict(model=args.model, steps=args.steps, start=start, losses=losses,
                               checksum=[round(float(x), 6) for x in sums.cpu()],
-                              total_ms=round((time.perf_counter() - t_start) * 1e3, 1))), flush=True)
+                              total_ms=round((time.perf_counter() - t_start) * 1e3, 1),
+                              steady_ms_per_iter=round(steady_ms, 4) if steady_ms is not None else None)),
+              flush=True)
     if comm.world > 1:
         dist.barrier()
         dist.destroy_process_group()

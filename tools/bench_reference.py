@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""Head-to-head measurements for the reference's own published numbers (BASELINE.md "Target for this
+repo"): the reference reports LR iteration times, checkpoint overhead and fault-recovery phase
+times (report.pdf Fig. 13/15/16, report.md), all on a 15-machine 1 GbE CPU cluster.
+
+    python tools/bench_reference.py [--quick] > profiles/reference_comparison.md
+
+1. LR on webspam-shaped data (16,609,143 features, 64 nnz/row, BASELINE P2/P9/D1): per-iteration
+   latency and samples/s at the reference's per-iteration size (8 workers x batch 1 = 8 samples)
+   and at a GPU-sized batch, under BSP, SSP s=0 and SSP s=1 (python -m minips_amd.train).
+2. Checkpoint overhead (P3 vs P4): the same LR run with a checkpoint every 100 iterations
+   (binary sidecar; the reference text files are written for shards of <= 4M values) vs none.
+3. Recovery phases (P6-P8): 2 ranks under the elastic supervisor (heartbeat 1 s), rank 1 stops
+   answering (--fail_mode=hang) at iteration 30; phase times from the [Fault Tolerance] log
+   lines: detect (hang -> Phase2), restart (Phase2 -> Phase3), failed rank recovered (Phase3 ->
+   Phase4), others recovered (Phase3 -> Phase5). On a one-GPU box both ranks share the card over
+   gloo (MINIPS_SHARE_DEVICE / MINIPS_DIST_BACKEND); with several GPUs they use RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _train(args: list[str], timeout: int = 900) -> dict:
+    cmd = [sys.executable, "-m", "minips_amd.train", "--model", "lr", *args]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    if r.returncode != 0:
+        raise RuntimeError(f"{cmd}\n{r.stderr[-3000:]}")
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def lr_table(quick: bool):
+    rows = []
+    for batch, steps in ((8, 400 if quick else 2000), (65536, 60 if quick else 300)):
+        for cons, st in (("bsp", 0), ("ssp", 0), ("ssp", 1)):
+            out = _train(["--batch", str(batch), "--steps", str(steps), "--consistency", cons, "--staleness", str(st),
+                          "--timing_skip", "20"])
+            ms = out["steady_ms_per_iter"]
+            rows.append((batch, f"{cons.upper()}" + (f" s={st}" if cons == "ssp" else ""), ms, batch / ms * 1e3))
+    print("## 1. Sparse LR, webspam-shaped (16.6M features, 64 nnz/row), one MI355X\n")
+    print("| samples / iteration | consistency | ms / iteration | samples/s |")
+    print("|---|---|---|---|")
+    for b, c, ms, sps in rows:
+        print(f"| {b} | {c} | {ms:.3f} | {sps:,.0f} |")
+    print("\nReference (15 CPU machines, 1 GbE): webspam LR with checkpointing ~62 ms/iteration "
+          "(P9, ~130 samples/s cluster-wide, D1); kdd12 ~165 ms/iteration (P10).\n")
+
+
+def ckpt_table(quick: bool):
+    steps = 300 if quick else 1000
+    d = tempfile.mkdtemp(prefix="minips_ck_")
+    base = ["--batch", "65536", "--steps", str(steps), "--timing_skip", "20"]
+    off = _train(base)["steady_ms_per_iter"]
+    on = _train(base + ["--checkpoint_toggle=1", "--checkpoint_every", "100", f"--checkpoint_file_prefix={d}/",
+                        "--checkpoint_commit", "async"])["steady_ms_per_iter"]
+    files = sorted(glob.glob(f"{d}/iter_*/*"))
+    size = sum(os.path.getsize(f) for f in files if os.path.isfile(f))
+    print("## 2. Checkpoint overhead (LR, 16.6M-row table, checkpoint every 100 iterations)\n")
+    print("| checkpointing | ms / iteration | overhead |")
+    print("|---|---|---|")
+    print(f"| off | {off:.3f} | |")
+    print(f"| every 100 iterations (binary sidecar, async writer) | {on:.3f} | "
+          f"{(on / off - 1) * 100:+.1f}% |")
+    print(f"\nLast checkpoint directory: {len(files)} files, {size / 1e6:.1f} MB. Reference: 55.7 vs 35.3 s "
+          "per iteration with / without checkpointing (+58%, P3 vs P4).\n")
+
+
+def _ts(pattern: str, text: str):
+    m = re.search(pattern, text)
+    return int(m.group(1)) if m else None
+
+
+def recovery_table():
+    import torch
+
+    tmp = tempfile.mkdtemp(prefix="minips_ft_")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    if torch.cuda.is_available() and torch.cuda.device_count() < 2:
+        env.update(MINIPS_SHARE_DEVICE="1", MINIPS_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "minips_amd.elastic", "--nproc", "2", "--heartbeat_interval", "1.0",
+           "--max_restarts", "1", "--run_dir", f"{tmp}/run", "--log_dir", f"{tmp}/log", "--",
+           sys.executable, "-m", "minips_amd.train", "--model", "lr", "--batch", "8192", "--steps", "60",
+           "--checkpoint_toggle=1", "--checkpoint_every", "10", f"--checkpoint_file_prefix={tmp}/ck/",
+           "--fail_rank=1", "--fail_step=30", "--fail_mode=hang"]
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    wall = time.time() - t0
+    logs = {os.path.basename(f): open(f).read() for f in glob.glob(f"{tmp}/log/*.log")}
+    sup = r.stderr
+    inj = _ts(r"\[fault injection\]\[(\d+)\]", logs.get("rank1_attempt0.log", ""))
+    p2 = _ts(r"\[Fault Tolerance\]\[Phase2\]\[(\d+)\]", sup)
+    p3 = _ts(r"\[Fault Tolerance\]\[Phase3\]\[(\d+)\]", sup)
+    p4 = _ts(r"\[Fault Tolerance\]\[Phase4\]\[(\d+)\]", logs.get("rank1_attempt1.log", ""))
+    p5 = _ts(r"\[Fault Tolerance\]\[Phase5\]\[(\d+)\]", logs.get("rank0_attempt1.log", ""))
+    print("## 3. Fault recovery (2 ranks, heartbeat 1 s, rank 1 stops answering at iteration 30)\n")
+    if r.returncode != 0 or None in (inj, p2, p3, p4, p5):
+        print(f"run failed (rc {r.returncode}); supervisor stderr tail:\n```\n{sup[-2000:]}\n```\n")
+        return
+    print("| phase | here (ms) | reference 5 machines (s, P6) | reference 15 machines (s, P7) |")
+    print("|---|---|---|---|")
+    print(f"| Phase2 detect failure (hang -> detected; 3 x heartbeat) | {p2 - inj} | 8 | 7 |")
+    print(f"| Phase3 restart (stop rank set, relaunch) | {p3 - p2} | 10 | 9 |")
+    print(f"| Phase4 failed rank recovered (start + restore) | {p4 - p3} | 58 | 46 |")
+    print(f"| Phase5 other ranks recovered | {p5 - p3} | 42 | 31 |")
+    print(f"\nWhole run (60 iterations incl. the failure, restart and resumed tail): {wall:.1f} s; the "
+          "reference's webspam timeline (P8): detect 50,023 ms with a 15 s heartbeat, failed node "
+          "recovers 122,318 ms.\n")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", default="lr,ckpt,recovery")
+    a = ap.parse_args()
+    print("# Reference head-to-head (tools/bench_reference.py)\n")
+    parts = a.only.split(",")
+    if "lr" in parts:
+        lr_table(a.quick)
+    if "ckpt" in parts:
+        ckpt_table(a.quick)
+    if "recovery" in parts:
+        recovery_table()
+
+
+if __name__ == "__main__":
+    main()
