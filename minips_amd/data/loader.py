@@ -30,15 +30,46 @@ class LibsvmData:
     def __len__(self):
         return self.n
 
+    def to(self, device) -> "LibsvmData":
+        """Keep the whole shard resident in device memory (288 GB of HBM holds webspam/kdd12-sized
+        shards many times over): batches are then cut on the GPU with no host work per step."""
+        self._rp_host = self.rowptr.cpu()
+        self.rowptr, self.cols, self.vals, self.labels = (t.to(device) for t in
+                                                          (self.rowptr, self.cols, self.vals, self.labels))
+        return self
+
+    def _span(self, a: int, b: int):
+        """Rows [a, b) (no wrap) as a contiguous CSR slice: no per-row work; the bounds come from a
+        host copy of rowptr, so cutting a batch of HBM-resident data needs no device sync."""
+        if not hasattr(self, "_rp_host"):
+            self._rp_host = self.rowptr.cpu()
+        lo, hi = int(self._rp_host[a]), int(self._rp_host[b])
+        return self.rowptr[a: b + 1] - lo, lo, hi
+
     def batch(self, start: int, size: int):
-        """CSR batch of rows start .. start+size (wrapping)."""
-        idx = (torch.arange(size) + start) % max(self.n, 1)
-        lens = self.rowptr[idx + 1] - self.rowptr[idx]
-        rp = torch.zeros(size + 1, dtype=torch.int64)
-        rp[1:] = torch.cumsum(lens, 0)
-        gather = torch.cat([torch.arange(int(self.rowptr[i]), int(self.rowptr[i + 1])) for i in idx.tolist()]) \
-            if size else torch.empty(0, dtype=torch.int64)
-        return rp, self.cols[gather], self.vals[gather], self.labels[idx]
+        """CSR batch of rows start .. start+size (wrapping): consecutive samples from a start point as
+        the reference sampler takes them (lib/batch_data_sampler.cpp:50-71), cut as at most two
+        contiguous CSR slices (vectorised; runs where the data lives, host or HBM)."""
+        n = max(self.n, 1)
+        start %= n
+        parts, rows_left, pos = [], size, start
+        while rows_left > 0:
+            take = min(rows_left, n - pos)
+            parts.append((pos, pos + take))
+            rows_left -= take
+            pos = 0
+        rps, cols, vals, labels, off = [], [], [], [], 0
+        for a, b in parts:
+            rp, lo, hi = self._span(a, b)
+            rps.append((rp[1:] if rps else rp) + off)
+            off = off + (hi - lo)
+            cols.append(self.cols[lo:hi])
+            vals.append(self.vals[lo:hi])
+            labels.append(self.labels[a:b])
+        if not parts:
+            z = self.rowptr[:1] * 0
+            return z, self.cols[:0], self.vals[:0], self.labels[:0]
+        return torch.cat(rps), torch.cat(cols), torch.cat(vals), torch.cat(labels)
 
     def batches(self, size: int, seed: int = 0):
         g = torch.Generator().manual_seed(seed)

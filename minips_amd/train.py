@@ -56,6 +56,8 @@ def parse(argv=None):
     ap.add_argument("--timing_skip", type=int, default=0,
                     help="iterations excluded from steady_ms_per_iter (first-launch / warm-up costs)")
     ap.add_argument("--alpha", type=float, default=0.05)
+    ap.add_argument("--input", default="", help="libsvm file / directory / comma list (LR; reference --input)")
+    ap.add_argument("--num_dims", type=int, default=0, help="feature count (reference flag; 0: infer / default)")
     return ap.parse_args(argv)
 
 
@@ -105,11 +107,28 @@ def build(args, comm):
         B = args.batch or (2 if args.small else 8)
         data = _Skippable(TokenSynth(B, cfg.n_ctx, vocab=cfg.vocab, device=dev, seed=seed))
         return m, {0: m.table}, data, (lambda b: m.train_step(*b)), B * cfg.n_ctx
+    if args.model == "lr" and args.input:
+        # reference LR on a libsvm file (lr_example.cpp --input): this rank's shard is loaded by the
+        # native block assigner / mmap reader and kept resident in HBM; batches are consecutive
+        # rows from a random start (lib/batch_data_sampler.cpp), cut on the device
+        from .data.loader import LibsvmData
+        from .models.lr import SparseLR, SparseLRConfig
+
+        shard = LibsvmData(args.input, r, comm.world).to(dev)
+        nd = args.num_dims
+        if not nd:  # every rank must size the table alike: max feature id over all shards
+            t = torch.tensor([float(shard.cols.max()) + 1 if shard.cols.numel() else 1.0], device=dev)
+            comm.all_reduce_(t, op=dist.ReduceOp.MAX)
+            nd = int(t.item())
+        m = SparseLR(SparseLRConfig(num_dims=nd, alpha=args.alpha, consistency=args.consistency,
+                                    staleness=args.staleness), comm)
+        B = args.batch or 1024
+        return m, {0: m.table}, _Skippable(_Batches(shard, B, seed)), (lambda b: -m.train_step(*b)), B
     if args.model == "lr":
         from .data.synthetic import SparseLRSynth
         from .models.lr import SparseLR, SparseLRConfig
 
-        nd = 5000 if args.small else 16_609_143
+        nd = args.num_dims or (5000 if args.small else 16_609_143)
         m = SparseLR(SparseLRConfig(num_dims=nd, alpha=args.alpha, consistency=args.consistency,
                                     staleness=args.staleness), comm)
         B = args.batch or (128 if args.small else 65536)
@@ -137,6 +156,14 @@ class _Skippable:
     def skip(self, n):
         for _ in range(n):
             self.inner.next()
+
+
+class _Batches:
+    def __init__(self, shard, B, seed):
+        self.it = shard.batches(B, seed=seed)
+
+    def next(self):
+        return next(self.it)
 
 
 class _DLRMData:
