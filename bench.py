@@ -52,15 +52,30 @@ def main():
     model = WideDeep(cfg, comm)
     data = CriteoSynth(args.batch, cards=cfg.cards, device=dev, seed=1000 + comm.rank)
 
-    # the next batch is generated one step ahead so its key routing (dedupe + count all-to-all)
-    # runs on the planning stream during the current step (lookahead; no table state is read)
-    state = {"cur": data.next()}
+    # The next batch is generated one step ahead, like a data loader prefetching, and ON the
+    # planning stream, so generation and its key routing (dedupe + count all-to-all) both run
+    # beside the current step (lookahead; no table state is read). The compute stream waits for
+    # a batch's event before using it.
+    ps = comm.plan_stream()
+    main_stream = torch.cuda.current_stream(dev)
+
+    def produce():
+        with torch.cuda.stream(ps):
+            b = data.next()
+            ev = torch.cuda.Event()
+            ev.record(ps)
+        for t in b:
+            t.record_stream(main_stream)
+        return b, ev
+
+    state = {"cur": produce()}
 
     def step():
-        nxt = data.next()
-        dense, keys, labels = state["cur"]
+        nxt = produce()
+        (dense, keys, labels), ev = state["cur"]
         state["cur"] = nxt
-        return model.train_step(dense, keys, labels, next_keys=nxt[1])
+        main_stream.wait_event(ev)
+        return model.train_step(dense, keys, labels, next_keys=nxt[0][1], next_on_plan_stream=True)
 
     loss0 = None
     for i in range(args.warmup):

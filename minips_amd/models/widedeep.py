@@ -143,12 +143,12 @@ class WideDeep:
         w4 = self.view(P, "w4").float()
         return b["H3"].float() @ w4[:h] + w4[h] + b["wide"]
 
-    def prefetch(self, keys):
+    def prefetch(self, keys, keys_on_plan_stream: bool = False):
         """Lookahead: start routing the NEXT batch's keys (dedupe + count all-to-all on the
         planning stream) so it overlaps the current step; train_step picks the plan up."""
-        self._next_plan = (keys, self.emb.plan_async(keys, csr=True))
+        self._next_plan = (keys, self.emb.plan_async(keys, csr=True, keys_on_plan_stream=keys_on_plan_stream))
 
-    def train_step(self, dense, keys, labels, next_keys=None) -> torch.Tensor:
+    def train_step(self, dense, keys, labels, next_keys=None, next_on_plan_stream: bool = False) -> torch.Tensor:
         """One BSP superstep: Get, forward, backward, Add, Clock. Returns the summed loss
         (a device tensor; no host sync).
 
@@ -158,7 +158,8 @@ class WideDeep:
           sparse Add+Clock (all-to-all of gradient rows + row-wise Adagrad on the push lane,
           overlapping the weight-gradient GEMMs) -> wgrad GEMMs -> dense Add+Clock
           (reduce-scatter + Adam + all-gather on the dense lane, overlapping the next step's
-          sparse Get). ``next_keys`` starts the next batch's key planning right away."""
+          sparse Get). ``next_keys`` starts the next batch's key planning right away
+          (``next_on_plan_stream``: that batch was generated on the planning stream itself)."""
         cfg = self.cfg
         B = dense.shape[0]
         F, D = cfg.F, cfg.emb_dim
@@ -170,7 +171,7 @@ class WideDeep:
         if plan is None:
             plan = self.emb.plan(keys, csr=True)
         if next_keys is not None:
-            self.prefetch(next_keys)
+            self.prefetch(next_keys, keys_on_plan_stream=next_on_plan_stream)
         rows, plan = self.emb.get(keys, plan=plan)
         G = self.dense.grad
         ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0])

@@ -414,16 +414,19 @@ class SparseTable:
                 pp.host = both
         return pp
 
-    def plan_async(self, keys: torch.Tensor, csr: bool = False):
+    def plan_async(self, keys: torch.Tensor, csr: bool = False, keys_on_plan_stream: bool = False):
         """Lookahead: start planning ``keys`` (a LATER batch) on the planning stream, so its
         dedupe, count exchange (and lookup CSR) overlap the current step; pass the result to
         get(plan=...). Planning reads no table state, so issuing it early changes no
-        consistency semantics."""
+        consistency semantics. ``keys_on_plan_stream``: the keys were produced on the planning
+        stream itself (a data producer running there), so planning need not wait for the
+        compute stream at all."""
         if self.comm.device.type != "cuda" or self._exact_counts:
             return self.plan(keys, csr)
         ps = self.comm.plan_stream()
         cur = torch.cuda.current_stream(self.comm.device)
-        ps.wait_stream(cur)  # the keys are produced on the compute stream
+        if not keys_on_plan_stream:
+            ps.wait_stream(cur)  # the keys are produced on the compute stream
         with torch.cuda.stream(ps):
             pp = self._start_plan(keys, csr)
         keys.record_stream(ps)
