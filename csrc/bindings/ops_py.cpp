@@ -118,7 +118,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
 
 // Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P], U [1]).
 std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tensor& bounds, int64_t F,
-                                         int64_t route_mult, int64_t route_n) {
+                                         int64_t route_mult, int64_t route_n, int64_t extra_zero_ints) {
   check_gpu(keys, "keys");
   check_gpu(bounds, "bounds");
   check_dtype(keys, at::kLong, "keys");
@@ -129,18 +129,22 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   int64_t cap = 1024;
   while (cap < 2 * n) cap <<= 1;
   auto opts = keys.options();
-  auto table_keys = at::empty({cap}, opts), table_pos = at::empty({cap}, opts);
+  // table_keys | counts[P] | total | cursor[P] in one allocation: one zero memset clears them all
+  const int64_t extra64 = (std::max<int64_t>(extra_zero_ints, 0) + 1) / 2;  // int32 count -> int64 words
+  auto zbuf = at::empty({cap + 2 * P + 1 + extra64}, opts);
+  auto table_keys = zbuf.narrow(0, 0, cap), table_pos = at::empty({cap}, opts);
   auto slot = at::empty({n}, opts), flags = at::empty({n}, opts.dtype(at::kInt));
-  auto cbuf = at::empty({2 * P + 1}, opts);  // counts[P] | total | cursor[P] (one memset)
-  auto counts = cbuf.narrow(0, 0, P + 1), cursor = cbuf.narrow(0, P + 1, P);
+  auto counts = zbuf.narrow(0, cap, P + 1), cursor = zbuf.narrow(0, cap + P + 1, P);
   auto out_keys = at::empty({n}, opts), inverse = at::empty({n}, opts);
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   TORCH_CHECK(F >= 1 && n % F == 0, "unique_bucketize: numel must be a multiple of F");
   minips_k::unique_bucketize(ptr<int64_t>(keys), n, (int)F, ptr<int64_t>(bounds), P, ptr<int64_t>(table_keys),
                              ptr<int64_t>(table_pos), cap, ptr<int64_t>(slot), ptr<int32_t>(flags),
                              ptr<int64_t>(counts), ptr<int64_t>(cursor), ptr<int64_t>(out_keys), ptr<int64_t>(inverse),
-                             stream_of(keys), (uint64_t)route_mult, (uint64_t)route_n);
-  return {out_keys, inverse, counts.narrow(0, 0, P), counts.narrow(0, P, 1)};
+                             stream_of(keys), (uint64_t)route_mult, (uint64_t)route_n, extra64 * 8);
+  std::vector<at::Tensor> out{out_keys, inverse, counts.narrow(0, 0, P), counts.narrow(0, P, 1)};
+  if (extra64) out.push_back(zbuf.narrow(0, cap + 2 * P + 1, extra64).view(at::kInt));  // zeroed workspace
+  return out;
 }
 
 static const int64_t* count_ptr(const c10::optional<at::Tensor>& n_dev) {
@@ -286,17 +290,24 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
 }
 
 // Lookup CSR grouped by unique row (members/memrow int32 [B*F]) for U (upper-bound) rows.
-std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t U) {
+std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t U,
+                                      const c10::optional<at::Tensor>& zeroed) {
   check_gpu(inv, "inv");
   check_dtype(inv, at::kLong, "inv");
   const int64_t n = inv.numel();
   TORCH_CHECK(F >= 1 && n % F == 0 && U >= 1 && U < (1ll << 31) && n < (1ll << 31), "emb_build_csr shapes");
   auto io = inv.options().dtype(at::kInt);
-  at::Tensor ws = at::empty({3 * U + 1 + U / 1024 + 1}, io);
+  int* zc = nullptr;
+  if (zeroed.has_value() && zeroed->defined()) {
+    TORCH_CHECK(zeroed->is_cuda() && zeroed->scalar_type() == at::kInt && zeroed->numel() >= 2 * U,
+                "zeroed: int32 GPU block of >= 2U (already zero)");
+    zc = zeroed->data_ptr<int>();
+  }
+  at::Tensor ws = at::empty({(zc ? 0 : 2 * U) + U + 1 + U / 1024 + 1}, io);
   at::Tensor members = at::empty({n}, io), memrow = at::empty({n}, io);
   c10::hip::HIPGuardMasqueradingAsCUDA g(inv.device());
   minips_k::emb_build_csr(ptr<int64_t>(inv), n / F, (int)F, (int)U, ws.data_ptr<int>(), members.data_ptr<int>(),
-                          memrow.data_ptr<int>(), stream_of(inv));
+                          memrow.data_ptr<int>(), stream_of(inv), zc);
   return {members, memrow};
 }
 
@@ -711,7 +722,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dlrm_interact_fwd", &dlrm_interact_fwd);
   m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
   m.def("unique_bucketize", &unique_bucketize, py::arg("keys"), py::arg("bounds"), py::arg("F") = 1,
-        py::arg("route_mult") = 0, py::arg("route_n") = 0);
+        py::arg("route_mult") = 0, py::arg("route_n") = 0, py::arg("extra_zero_ints") = 0);
   m.def("gather_rows", &gather_rows, py::arg("table"), py::arg("keys"), py::arg("base"), py::arg("out"),
         py::arg("n_dev") = py::none());
   m.def("scatter_add_rows", &scatter_add_rows);
@@ -733,7 +744,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_head", &wd_head);
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none());
-  m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"));
+  m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none());
   m.def("adam_apply", &adam_apply);
   m.def("sgd_apply", &sgd_apply);
   m.def("adagrad_apply", &adagrad_apply);

@@ -44,10 +44,12 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
 // cursor [P] (all state re-initialised inside).
 // keys may be a [B, F] batch (F > 1): tiles are then taken feature-major for better dedupe.
 // route_mult != 0 dedupes the ROUTED keys key * route_mult mod route_n (uniq holds routed keys).
+// extra_zero_bytes: when table_keys | counts | cursor are one buffer, that many more bytes after
+// cursor are zeroed by the same memset (a workspace for a following op, e.g. emb_build_csr).
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult = 0,
-                      uint64_t route_n = 0);
+                      uint64_t route_n = 0, int64_t extra_zero_bytes = 0);
 
 // Row gather from a shard: out[i, :] = table[keys[i] - base, :] with dtype conversion.
 // table fp32 [R, D] row stride ld; out fp32 or bf16 [n, D].
@@ -108,7 +110,9 @@ void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide
                           const int64_t* U_dev = nullptr);
 // The two halves of emb_backward_segment: the lookup CSR (depends on inv only; ws: counts[U] |
 // cursor[U] | offsets[U+1] | tiles[U/1024+1]; members/memrow [B*F]) and the segmented sum.
-void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s);
+// zeroed_cc (nullable): a pre-zeroed 2U-int block used for counts|cursor (ws then starts at offsets).
+void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s,
+                   int* zeroed_cc = nullptr);
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
                       const int64_t* U_dev = nullptr);

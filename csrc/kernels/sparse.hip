@@ -102,16 +102,19 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
   if (lead) {
     const int64_t mask = cap - 1;
     int64_t h = (int64_t)(mix64((uint64_t)key * 0x9e3779b97f4a7c15ULL) & (uint64_t)mask);
+    // global slots hold key + 1 (keys are < 2^63), so 0 marks an empty slot and the table is
+    // cleared by the same zero memset as the per-owner counters (one memset per call)
+    const unsigned long long tag = (unsigned long long)key + 1ULL;
     while (true) {
       unsigned long long cur = __hip_atomic_load(table_keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cur == (unsigned long long)key) break;
-      if (cur == (unsigned long long)kEmpty) {
-        unsigned long long prev = atomicCAS(table_keys + h, (unsigned long long)kEmpty, (unsigned long long)key);
-        if (prev == (unsigned long long)kEmpty) {
+      if (cur == tag) break;
+      if (cur == 0ULL) {
+        unsigned long long prev = atomicCAS(table_keys + h, 0ULL, tag);
+        if (prev == 0ULL) {
           claimed = true;
           break;
         }
-        if (prev == (unsigned long long)key) break;
+        if (prev == tag) break;
       }
       h = (h + 1) & mask;
     }
@@ -191,16 +194,20 @@ __global__ void ub_inverse_kernel(int64_t n, const int64_t* __restrict__ slot, c
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult,
-                      uint64_t route_n) {
+                      uint64_t route_n, int64_t extra_zero_bytes) {
   if (F < 1 || n % F) throw std::runtime_error("unique_bucketize: n must be a multiple of F");
   if (route_mult && !route_n) throw std::runtime_error("unique_bucketize: routing needs the row count");
   if (P < 1 || P > kUbMaxP) throw std::runtime_error("unique_bucketize: 1 <= P <= 256 owner shards");
   if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
   if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
-  MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0xFF, cap * sizeof(int64_t), s));
-  if (cursor == counts + P + 1) {  // one buffer: counts[P] (+ total) | cursor[P]
+  if (counts == table_keys + cap && cursor == counts + P + 1) {
+    // one buffer: table [cap] | counts [P] | total | cursor [P] -> a single zero memset
+    MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, (cap + 2 * P + 1) * sizeof(int64_t) + extra_zero_bytes, s));
+  } else if (cursor == counts + P + 1) {
+    MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, cap * sizeof(int64_t), s));
     MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, (2 * P + 1) * sizeof(int64_t), s));
   } else {
+    MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, cap * sizeof(int64_t), s));
     MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, (P + 1) * sizeof(int64_t), s));  // counts[P] = total
     MINIPS_HIP_CHECK(hipMemsetAsync(cursor, 0, P * sizeof(int64_t), s));
   }

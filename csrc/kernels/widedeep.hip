@@ -581,14 +581,17 @@ __global__ void zero_rows_dev_kernel(float* __restrict__ rows, int stride, int64
 // CSR of the lookups grouped by unique row (depends on `inv` only, so the PS builds it at
 // planning time, off the critical path). ws: counts[U] | cursor[U] | offsets[U+1] | tiles;
 // members/memrow: [B*F] lookup ids and their rows, sorted by row.
-void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s) {
+void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s,
+                   int* zeroed_cc) {
   if (B <= 0 || U <= 0) return;
-  int* counts = ws;
+  // counts | cursor: 2U ints that must start at zero -- a caller-provided, already-zeroed block
+  // (cleared by the dedupe's memset) or the head of ws
+  int* counts = zeroed_cc ? zeroed_cc : ws;
   int* cursor = counts + U;
-  int* offsets = cursor + U;
+  int* offsets = zeroed_cc ? ws : cursor + U;
   int* tiles = offsets + U + 1;
   const int ntiles = (U + kScanTile - 1) / kScanTile;
-  MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int) * 2 * (size_t)U, s));  // counts, cursor
+  if (!zeroed_cc) MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int) * 2 * (size_t)U, s));
   dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);
   hipLaunchKernelGGL(emb_seg_count_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, counts);
   hipLaunchKernelGGL(emb_scan_reduce_kernel, ntiles, 256, 0, s, counts, U, tiles);

@@ -392,14 +392,20 @@ class SparseTable:
         pp.F = keys.shape[1] if keys.dim() == 2 else 1
         flat = keys.reshape(-1).to(torch.int64)
         rmult = getattr(self, "route_mult", 0)
+        want_csr = csr and flat.is_cuda
+        n = flat.numel()
+        zeroed = None
         if rmult:  # range tables: the routing is fused into the dedupe kernel
             pp.flat = flat
-            pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.unique_bucketize_n(flat, self.bounds, pp.F, rmult,
-                                                                          self.num_rows)
+            res = ops.unique_bucketize_n(flat, self.bounds, pp.F, rmult, self.num_rows,
+                                         extra_zero_ints=2 * n if want_csr else 0)
         else:
             pp.flat = self._route_keys(flat)
-            pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.unique_bucketize_n(pp.flat, self.bounds, pp.F)
-        pp.csr = ops.emb_build_csr(pp.inv, pp.F, pp.flat.numel()) if csr and pp.inv.is_cuda else None
+            res = ops.unique_bucketize_n(pp.flat, self.bounds, pp.F, extra_zero_ints=2 * n if want_csr else 0)
+        if want_csr:  # the CSR's counters were cleared by the dedupe's single memset
+            res, zeroed = res
+        pp.uniq, pp.inv, pp.counts, pp.U_dev = res
+        pp.csr = ops.emb_build_csr(pp.inv, pp.F, n, zeroed=zeroed) if want_csr else None
         pp.host = pp.event = None
         if self.comm.world > 1:
             recv = torch.empty_like(pp.counts)
