@@ -8,6 +8,8 @@ Linear        bias folded into the weight: W_ext [n_out, k_pad] with the bias in
 """
 from __future__ import annotations
 
+import contextlib
+
 import math
 
 import torch
@@ -100,3 +102,28 @@ class Linear:
         if mask is not None:
             return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_RELU_MASK_BF16, mask=mask)
         return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_STORE_BF16)
+
+
+class SideStream:
+    """Fork-join helper: independent work (weight gradients) issued on a second HIP stream.
+
+    ``with side.fork():`` makes the side stream wait for everything issued so far on the current
+    stream, then runs the block on the side stream; ``join()`` makes the current stream wait for
+    all forked work. Disabled (or on CPU) it is a no-op and the block runs inline."""
+
+    def __init__(self, device, enabled: bool = True):
+        self.stream = torch.cuda.Stream(device=device) if enabled and torch.device(device).type == "cuda" else None
+
+    @contextlib.contextmanager
+    def fork(self):
+        if self.stream is None:
+            yield
+            return
+        cur = torch.cuda.current_stream(self.stream.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            yield
+
+    def join(self):
+        if self.stream is not None:
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)

@@ -17,12 +17,14 @@ Step (every kernel is a gfx950 HIP kernel; comm is RCCL):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
 
 from .. import ops
 from ..ps.comm import Comm
+from .layers import SideStream
 from ..ps.tables import DenseTable, SparseTable
 
 
@@ -84,6 +86,7 @@ class WideDeep:
                                 consistency=cfg.consistency, staleness=cfg.staleness, table_id=1)
         self.dense.load_full(self._init_dense(dev))
         self._bufs = {}
+        self._side = SideStream(dev, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
 
     def _init_dense(self, dev):
         g = torch.Generator(device="cpu")
@@ -182,8 +185,17 @@ class WideDeep:
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1], b["dwide"],
                     b["loss"], None, scale)
+        side = self._side
+        # weight gradients fork onto a second stream as soon as their inputs exist, beside the
+        # dgrad chain (their split-K tails and reduces fill the gaps of the dependent chain)
+        with side.fork():
+            ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=self.k_in[2], out=b["dH2"])
+        with side.fork():
+            ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
+        with side.fork():
+            ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
         ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
         dev = self.comm.device
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), cfg.row_width,
@@ -191,9 +203,7 @@ class WideDeep:
         ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows, U_dev=plan.U_dev, csr=plan.csr)
         self.emb.add(plan, grad_rows)
         self.emb.clock()
-        ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
-        ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
-        ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
+        side.join()
         self.dense.add()
         self.dense.clock()
         self._advance_next_plan()
