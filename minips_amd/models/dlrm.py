@@ -12,6 +12,7 @@ send/recv + apply) on a side stream without gating the next Gets beyond a 2-cloc
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -19,7 +20,7 @@ import torch
 from .. import ops
 from ..ps.comm import Comm
 from ..ps.tables import DenseTable, SparseTable
-from .layers import Linear, ParamLayout, align, ext_activation
+from .layers import SideStream, Linear, ParamLayout, align, ext_activation
 
 
 @dataclass
@@ -64,6 +65,7 @@ class DLRM:
         h[: cfg.top[-1]].uniform_(-cfg.top[-1] ** -0.5, cfg.top[-1] ** -0.5, generator=g)
         self.dense.load_full(full)
         self._bufs = {}
+        self._side = SideStream(comm.device, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
 
     def _buffers(self, B):
         if B not in self._bufs:
@@ -125,10 +127,11 @@ class DLRM:
         # dgrad chain first (top MLP -> interaction), then the embedding gradient goes out on the
         # sparse push lane while the weight-gradient GEMMs run on the compute stream
         dy = b["dH"]
-        dys = []
+        side = self._side
         for i in range(len(self.top) - 1, -1, -1):
             l = self.top[i]
-            dys.append((l, dy, ta[i]))
+            with side.fork():  # weight gradients beside the dgrad chain (per-layer buffers: no reuse)
+                l.wgrad(G, dy, ta[i])
             if i > 0:
                 dx = b["tgrads"][i - 1]
                 l.dgrad(P, dy, dx, mask=ta[i])
@@ -143,16 +146,16 @@ class DLRM:
         ops.wd_emb_backward(b["dV"], None, plan.inv, F, D, grad_rows, x_off=0, U_dev=plan.U_dev, csr=plan.csr)
         self.emb.add(plan, grad_rows)
         self.emb.clock()
-        for l, g_out, x_in in dys:
-            l.wgrad(G, g_out, x_in)
         dy = b["dbot"]
         for i in range(len(self.bottom) - 1, -1, -1):
             l = self.bottom[i]
-            l.wgrad(G, dy, ba[i])
+            with side.fork():
+                l.wgrad(G, dy, ba[i])
             if i > 0:
                 dx = b["bgrads"][i - 1]
                 l.dgrad(P, dy, dx, mask=ba[i])
                 dy = dx
+        side.join()
         self.dense.add()
         self.dense.clock()
         self._advance_next_plan()

@@ -22,6 +22,7 @@ tile; dQ and dK/dV sweeps), layernorm_bwd (accumulating into the residual gradie
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -29,7 +30,7 @@ import torch
 from .. import ops
 from ..ps.comm import Comm
 from ..ps.tables import DenseTable
-from .layers import Linear, ParamLayout, align, ext_activation
+from .layers import SideStream, Linear, ParamLayout, align, ext_activation
 
 
 @dataclass
@@ -89,6 +90,7 @@ class GPT2:
         L.view(full, "lnf_g").fill_(1.0)
         self.table.load_full(full)
         self._bufs = {}
+        self._side = SideStream(comm.device, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
 
     @property
     def n_params(self):
@@ -160,31 +162,48 @@ class GPT2:
         ops.gemm(hf[:, :d], wte, logits, M, c.vocab_pad, d, False, False, ops.EPI_STORE_BF16)
         b["loss"].zero_()
         ops.softmax_xent(logits, c.vocab, targets.reshape(-1), 1.0 / (M * self.comm.world), b["loss"])
-        # ---- backward
-        ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"))
+        # ---- backward. Weight gradients fork onto a side stream beside the dgrad chain; before the
+        # chain overwrites a buffer a forked wgrad reads (dx, du, dqkv), it waits for that wgrad.
+        side = self._side
+        with side.fork():
+            ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"))
         dh = b["dh"]
         ops.gemm(logits, wte, dh, M, d, c.vocab_pad, False, True, ops.EPI_STORE_BF16)
         dx = b["dx"]
         ops.layernorm_bwd(x[-1], dh, d, v(P, "lnf_g"), mf, rf, dx, v(G, "lnf_g"), v(G, "lnf_b"))
+        ev_du = ev_dqkv = None
         for i in range(c.n_layer - 1, -1, -1):
             blk = self.blocks[i]
             # MLP branch
-            blk["fc2"].wgrad(G, dx, b["g"][i])
+            with side.fork():
+                blk["fc2"].wgrad(G, dx, b["g"][i])
+            ev_dx = side.mark()
+            side.wait(ev_du)  # du: read by the previous layer's fc wgrad
             blk["fc2"].dgrad(P, dx, b["du"], gelu_u=b["u"][i])
-            blk["fc"].wgrad(G, b["du"], b["h2"][i])
+            with side.fork():
+                blk["fc"].wgrad(G, b["du"], b["h2"][i])
+            ev_du = side.mark()
             blk["fc"].dgrad(P, b["du"], dh)
             m2, r2 = b["st2"][i]
+            side.wait(ev_dx)  # dx accumulates next
             ops.layernorm_bwd(b["xm"][i], dh, d, v(P, blk["ln2_g"]), m2, r2, dx, v(G, blk["ln2_g"]),
                               v(G, blk["ln2_b"]), accumulate=True)
             # attention branch
-            blk["proj"].wgrad(G, dx, b["ao"][i])
+            with side.fork():
+                blk["proj"].wgrad(G, dx, b["ao"][i])
+            ev_dx = side.mark()
             blk["proj"].dgrad(P, dx, b["dao"])
+            side.wait(ev_dqkv)  # dqkv: read by the previous layer's qkv wgrad
             ops.attn_bwd(b["qkv"][i], b["ao"][i], b["dao"], b["lse"][i], b["delta"], B, T, c.n_head, scale, b["dqkv"])
-            blk["qkv"].wgrad(G, b["dqkv"], b["h1"][i])
+            with side.fork():
+                blk["qkv"].wgrad(G, b["dqkv"], b["h1"][i])
+            ev_dqkv = side.mark()
             blk["qkv"].dgrad(P, b["dqkv"], dh)
             m1, r1 = b["st1"][i]
+            side.wait(ev_dx)
             ops.layernorm_bwd(x[i], dh, d, v(P, blk["ln1_g"]), m1, r1, dx, v(G, blk["ln1_g"]), v(G, blk["ln1_b"]),
                               accumulate=True)
+        side.join()  # embed_bwd accumulates into the wte gradient the LM-head wgrad wrote
         ops.embed_bwd(dx, tokens, T, v(G, "wte"), v(G, "wpe"))
         self.table.add()
         self.table.clock()

@@ -127,3 +127,16 @@ class SideStream:
     def join(self):
         if self.stream is not None:
             torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+
+    def mark(self):
+        """Event after the work forked so far (None when disabled)."""
+        if self.stream is None:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+    def wait(self, ev):
+        """The current stream waits for ``ev`` (before it overwrites a buffer forked work reads)."""
+        if ev is not None:
+            torch.cuda.current_stream(self.stream.device).wait_event(ev)
