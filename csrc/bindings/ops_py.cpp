@@ -362,7 +362,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
 
 void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g, double lr, double beta1,
                 double beta2, double eps, double weight_decay, int64_t step, double grad_scale,
-                const c10::optional<at::Tensor>& w_bf16) {
+                const c10::optional<at::Tensor>& w_bf16, const c10::optional<at::Tensor>& step_dev) {
   for (auto* t : {&w, &m, &v}) {
     check_gpu(*t, "adam state");
     check_dtype(*t, at::kFloat, "adam state");
@@ -374,7 +374,8 @@ void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g
   if (wb) TORCH_CHECK(w_bf16->numel() == w.numel(), "w_bf16 size");
   c10::hip::HIPGuardMasqueradingAsCUDA gd(w.device());
   minips_k::adam_apply(ptr<float>(w), ptr<float>(m), ptr<float>(v), ptr<float>(g), w.numel(), (float)lr, (float)beta1,
-                       (float)beta2, (float)eps, (float)weight_decay, (int)step, (float)grad_scale, wb, stream_of(w));
+                       (float)beta2, (float)eps, (float)weight_decay, (int)step, (float)grad_scale, wb, stream_of(w),
+                       step_dev.has_value() && step_dev->defined() ? step_dev->data_ptr<int>() : nullptr);
 }
 
 void sgd_apply(at::Tensor& w, const at::Tensor& g, double lr, double grad_scale, const c10::optional<at::Tensor>& w_bf16) {
@@ -745,7 +746,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none());
   m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none());
-  m.def("adam_apply", &adam_apply);
+  m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),
+        py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"),
+        py::arg("grad_scale"), py::arg("w_bf16"), py::arg("step_dev") = py::none());
   m.def("sgd_apply", &sgd_apply);
   m.def("adagrad_apply", &adagrad_apply);
   m.def("cast_f32_bf16", &cast_f32_bf16);

@@ -11,7 +11,13 @@ namespace minips_k {
 
 __global__ void adam_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                             const float* __restrict__ g, int64_t n, float lr, float b1, float b2, float eps, float wd,
-                            float bc1, float bc2, float gscale, bf16_t* __restrict__ wb) {
+                            float bc1, float bc2, float gscale, bf16_t* __restrict__ wb,
+                            const int* __restrict__ step_dev) {
+  if (step_dev) {  // device-side step (graph-replayable clocks): bias corrections from *step_dev
+    const float t = (float)*step_dev;
+    bc1 = 1.f - powf(b1, t);
+    bc2 = 1.f - powf(b2, t);
+  }
   const int64_t n4 = n >> 2;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 W = reinterpret_cast<float4*>(w)[i], M = reinterpret_cast<float4*>(m)[i];
@@ -50,7 +56,7 @@ static void check_align(const void* p, const char* what) {
 }
 
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2, float eps,
-                float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s) {
+                float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s, const int* step_dev) {
   if (n <= 0) return;
   check_align(w, "adam w");
   check_align(m, "adam m");
@@ -60,7 +66,7 @@ void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float l
   const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
   const int block = 256;
   hipLaunchKernelGGL(adam_kernel, grid_for((n + 3) / 4, block), block, 0, s, w, m, v, g, n, lr, beta1, beta2, eps,
-                     weight_decay, bc1, bc2, grad_scale, w_bf16);
+                     weight_decay, bc1, bc2, grad_scale, w_bf16, step_dev);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -328,11 +328,15 @@ def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=No
 
 # ----------------------------------------------------------------------------- optimizers
 def adam_apply(w, m, v, g, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=1, grad_scale=1.0,
-               w_bf16=None):
+               w_bf16=None, step_dev=None):
+    """Fused Adam(W). ``step_dev`` (int32 [1] device tensor): the bias-correction step is read on the
+    device, so a captured (HIP graph) clock stays correct on replay."""
     if _gpu(w):
         kernels().adam_apply(w, m, v, g, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
-                             int(step), float(grad_scale), w_bf16)
+                             int(step), float(grad_scale), w_bf16, step_dev)
         return
+    if step_dev is not None:
+        step = int(step_dev.reshape(-1)[0])
     gg = g * grad_scale
     m.mul_(beta1).add_((1 - beta1) * gg)
     v.mul_(beta2).add_((1 - beta2) * gg * gg)

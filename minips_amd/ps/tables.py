@@ -147,6 +147,9 @@ class DenseTable:
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self.grad_shard = torch.zeros(self.shard, dtype=torch.float32, device=dev)
         self.step = 0
+        # the Adam step also lives on the device (advanced inside the clock) so that a clock
+        # captured in a HIP graph replays with the right bias correction
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.pipe = _Pipeline(comm, consistency, staleness, kind="dense")
         # collective: this table's clock communicator is created up front, in constructor order
         self.lane = comm.lane(f"dense{table_id}") if self.pipe.async_ else comm
@@ -193,6 +196,7 @@ class DenseTable:
         comm = self.lane
 
         def work():
+            self.step_dev.add_(1)  # device twin of self.step (one per clock)
             if pending:
                 if comm.world == 1:  # the whole gradient is the owned shard
                     self._apply(grad, step)
@@ -212,7 +216,7 @@ class DenseTable:
         out = self.params[self.base: self.base + self.shard] if self.pull_dtype == torch.bfloat16 else None
         if self.optimizer == "adam":
             ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
-                           self.weight_decay, step, 1.0, out)
+                           self.weight_decay, step, 1.0, out, step_dev=self.step_dev)
         elif self.optimizer == "adagrad":
             ops.adagrad_apply(self.master, self.m, g, self.lr, self.eps, 1.0, out)
         elif self.optimizer == "sgd":
@@ -258,6 +262,7 @@ class DenseTable:
                 if d is not None:
                     d[a - lo: b - lo].copy_(t.reshape(-1)[a - meta["base"]: b - meta["base"]])
         self.step = int(clock)
+        self.step_dev.fill_(int(clock))
         self.pipe.clock = int(clock)
         own = self.params[self.base: self.base + self.shard]
         if self.pull_dtype == torch.bfloat16:
