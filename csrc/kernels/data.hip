@@ -36,12 +36,17 @@ __global__ void criteo_synth_kernel(uint64_t seed, uint64_t step, int64_t B, int
   const int64_t nk = B * F;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nk + B; e += (int64_t)gridDim.x * blockDim.x) {
     if (e < nk) {
-      const int64_t b = e / F;
+      // 32-bit index math and a 64-bit modulo when the product fits (every Criteo card is < 2^32):
+      // the 128-bit remainder is a long software routine, and it dominated this kernel
+      const int64_t b = nk < (1LL << 31) ? (int64_t)((uint32_t)e / (uint32_t)F) : e / F;
       const int f = (int)(e - b * F);
       const uint64_t sb = splitmix(base ^ (uint64_t)b * 0xd1342543de82ef95ULL);
       const int64_t card = cards[f];
       const int64_t raw = raw_id(sb, f, card);
-      keys[e] = (int64_t)(((unsigned __int128)raw * 2654435761ULL) % (unsigned __int128)card) + offsets[f];
+      const uint64_t h = card < (1LL << 32)
+                             ? ((uint64_t)raw * 2654435761ULL) % (uint64_t)card
+                             : (uint64_t)(((unsigned __int128)raw * 2654435761ULL) % (unsigned __int128)card);
+      keys[e] = (int64_t)h + offsets[f];
     } else {
       const int64_t b = e - nk;
       const uint64_t sb = splitmix(base ^ (uint64_t)b * 0xd1342543de82ef95ULL);

@@ -4,6 +4,7 @@
 //   K1     scatter_add_rows   worker-side gradient dedupe (segment sum via float atomics)
 //   K1     sparse_rowwise_adagrad / sparse_sgd   server-side apply on the shard rows
 //          embedding_bag_fwd/bwd                 pooled lookups (DLRM-style bags)
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -357,6 +358,71 @@ __global__ void sparse_rowwise_adagrad_half_kernel(float* table, int64_t ld, flo
   }
 }
 
+// Rows of 16 < D <= 64 floats with D % 4 == 0 (16-byte rows): 8 lanes per row, one float4 per
+// lane for columns [0, 32) and a second float4 for [32, D) on the first (D - 32) / 4 lanes, so a
+// wave keeps 8 rows' loads in flight at once (the 32-lane variant above is latency-bound: key ->
+// row -> read-modify-write, two rows per wave).
+__global__ __launch_bounds__(256) void sparse_rowwise_adagrad_v4_kernel(float* table, int64_t ld, float* state,
+                                                                        float* state2, int D1,
+                                                                        const int64_t* __restrict__ keys, int64_t n,
+                                                                        int64_t base, int D,
+                                                                        const float* __restrict__ grads, float lr,
+                                                                        float eps, const int64_t* n_dev) {
+  n = dev_count(n, n_dev);
+  const int lane = threadIdx.x & 63, sub = lane >> 3, l = lane & 7;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int c0 = 4 * l, c1 = 32 + 4 * l;
+  const bool has0 = c0 < D, has1 = c1 < D;  // D % 4 == 0: a float4 is all in or all out
+  for (int64_t i0 = wave * 8; i0 < n; i0 += nwaves * 8) {
+    const int64_t i = i0 + sub;
+    const bool ok = i < n;
+    const int64_t row = ok ? keys[i] - base : 0;
+    float4 g0 = make_float4(0.f, 0.f, 0.f, 0.f), g1 = g0, t0 = g0, t1 = g0;
+    float* tr = table + row * ld;
+    if (ok && has0) {
+      g0 = *reinterpret_cast<const float4*>(grads + i * D + c0);
+      t0 = *reinterpret_cast<const float4*>(tr + c0);
+      if (has1) {
+        g1 = *reinterpret_cast<const float4*>(grads + i * D + c1);
+        t1 = *reinterpret_cast<const float4*>(tr + c1);
+      }
+    }
+    const float st_old1 = ok ? state[row] : 0.f;
+    const float st_old2 = ok && D1 < D ? state2[row] : 0.f;
+    float sq1 = 0.f, sq2 = 0.f;
+    const float a[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (q < 4 ? c0 : c1) + (q & 3);
+      const float sq = a[q] * a[q];
+      if (c < D1) sq1 += sq;
+      else sq2 += sq;  // zero beyond D: g1 stays 0 when !has1
+    }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+      sq1 += __shfl_xor(sq1, o, 64);
+      sq2 += __shfl_xor(sq2, o, 64);
+    }
+    if (!ok) continue;
+    const float st1 = st_old1 + sq1 / (float)D1;
+    const float st2 = D1 < D ? st_old2 + sq2 / (float)(D - D1) : 0.f;
+    if (l == 0) {
+      state[row] = st1;
+      if (D1 < D) state2[row] = st2;
+    }
+    const float s1 = lr / (sqrtf(st1) + eps), s2 = lr / (sqrtf(st2) + eps);
+    float o[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (q < 4 ? c0 : c1) + (q & 3);
+      o[q] -= (c < D1 ? s1 : s2) * a[q];
+    }
+    if (has0) *reinterpret_cast<float4*>(tr + c0) = make_float4(o[0], o[1], o[2], o[3]);
+    if (has1) *reinterpret_cast<float4*>(tr + c1) = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
 __global__ void sparse_rowwise_adagrad_kernel(float* table, int64_t ld, float* state, float* state2, int D1,
                                               const int64_t* __restrict__ keys, int64_t n, int64_t base, int D,
                                               const float* __restrict__ grads, float lr, float eps,
@@ -389,6 +455,14 @@ __global__ void sparse_rowwise_adagrad_kernel(float* table, int64_t ld, float* s
   }
 }
 
+static bool adagrad_v4_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MINIPS_ADAGRAD_V4");
+    return !(e && std::string(e) == "0");
+  }();
+  return on;
+}
+
 void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
                             int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s,
                             const int64_t* n_dev) {
@@ -396,7 +470,12 @@ void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state
   if (D1 <= 0 || D1 > D) D1 = D;
   if (D1 < D && !state2) throw std::runtime_error("sparse_rowwise_adagrad: split rows need state2");
   const int block = 256;
-  if (D <= 64) {
+  const bool vec4 = D > 16 && D <= 64 && D % 4 == 0 && ld % 4 == 0 && reinterpret_cast<uintptr_t>(table) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(grads) % 16 == 0 && adagrad_v4_enabled();
+  if (vec4) {
+    hipLaunchKernelGGL(sparse_rowwise_adagrad_v4_kernel, grid_for(n * 8, block, 16384), block, 0, s, table, ld, state,
+                       state2, D1, keys, n, base, D, grads, lr, eps, n_dev);
+  } else if (D <= 64) {
     hipLaunchKernelGGL(sparse_rowwise_adagrad_half_kernel, grid_for(n * 32, block, 8192), block, 0, s, table, ld,
                        state, state2, D1, keys, n, base, D, grads, lr, eps, n_dev);
   } else {

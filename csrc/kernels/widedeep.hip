@@ -466,7 +466,7 @@ __global__ __launch_bounds__(kEmbTB) void emb_seg_fill_kernel(const int64_t* __r
 // (independent loads in flight). A group flushes its running sum at every row change: a plain
 // store when the row lies entirely inside the group's range, an fp32 atomic otherwise (only
 // rows cut by a range boundary -- grad_rows is zero-filled first).
-constexpr int kSegG = 16, kSegBatch = 8;
+constexpr int kSegG = 16, kSegBatch = 8;  // defaults; MINIPS_SEG_CFG picks other (G, batch) pairs
 
 // 4 consecutive gradient values of one lookup row segment.
 __device__ __forceinline__ float4 ld_grad4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -501,7 +501,7 @@ __device__ __forceinline__ void seg_flush(float* __restrict__ grad_rows, int row
 // running sum at every row change: a plain store when the row lies entirely inside the group's
 // range, fp32 atomics when the row continues across the range boundary (grad_rows is zero-filled
 // first).
-template <typename TX, int D>
+template <typename TX, int D, int kSegG, int kSegBatch>
 __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__ dX, int ldx,
                                                           const float* __restrict__ dwide, int F,
                                                           const int* __restrict__ members,
@@ -611,11 +611,28 @@ static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, in
                        row_stride, (int64_t)U, U_dev);
   else
     MINIPS_HIP_CHECK(hipMemsetAsync(grad_rows, 0, sizeof(float) * (size_t)U * row_stride, s));
-  const int pieces = (total + (256 / D) * kSegG - 1) / ((256 / D) * kSegG);
+  static const int cfg = [] {
+    const char* e = std::getenv("MINIPS_SEG_CFG");
+    return e ? std::atoi(e) : 0;
+  }();
+  // cfg 0: G=16 lookups per group loaded 8 at a time; 1: G=16 in one batch of 16; 2: G=8 x 8;
+  // 3: G=32 x 16
+  const int G = cfg == 2 ? 8 : cfg == 3 ? 32 : 16;
+  const int pieces = (total + (256 / D) * G - 1) / ((256 / D) * G);
   const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
-#define MINIPS_SEG_LAUNCH(DD)                                                                                      \
-  hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD>), blocks, 256, 0, s, dX, ldx, dwide, F, members, memrow, total,  \
-                     grad_rows, row_stride);
+#define MINIPS_SEG_LAUNCH2(DD, GG, BB)                                                                              \
+  hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB>), blocks, 256, 0, s, dX, ldx, dwide, F, members, memrow,   \
+                     total, grad_rows, row_stride);
+#define MINIPS_SEG_LAUNCH(DD)                  \
+  if (cfg == 1) {                              \
+    MINIPS_SEG_LAUNCH2(DD, 16, 16)             \
+  } else if (cfg == 2) {                       \
+    MINIPS_SEG_LAUNCH2(DD, 8, 8)               \
+  } else if (cfg == 3) {                       \
+    MINIPS_SEG_LAUNCH2(DD, 32, 16)             \
+  } else {                                     \
+    MINIPS_SEG_LAUNCH2(DD, kSegG, kSegBatch)   \
+  }
   switch (D) {
     case 16:
       MINIPS_SEG_LAUNCH(16)
@@ -629,6 +646,7 @@ static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, in
     default:
       throw std::runtime_error("emb_backward_seg: D must be 16, 32 or 64");
   }
+#undef MINIPS_SEG_LAUNCH2
 #undef MINIPS_SEG_LAUNCH
   MINIPS_HIP_CHECK(hipGetLastError());
 }

@@ -115,6 +115,28 @@ def test_gather_scatter_adagrad(dev):
     torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("D,split", [(36, 32), (64, 64), (20, 20), (48, 40)])
+def test_rowwise_adagrad_vec4(dev, D, split):
+    """16-byte rows take the 8-lanes-per-row float4 kernel: same result as the CPU reference,
+    including the split (deep | wide) state and rows past 32 columns."""
+    g = torch.Generator().manual_seed(D)
+    R = 5000
+    table = torch.randn(R, D, generator=g)
+    keys = torch.randperm(R, generator=g)[:3001] + 7
+    grads = torch.randn(keys.numel(), D, generator=g)
+    s_ref, s2_ref = torch.rand(R, generator=g), torch.rand(R, generator=g)
+    t_ref = table.clone()
+    t_gpu, s_gpu, s2_gpu = table.to(dev), s_ref.to(dev), s2_ref.to(dev)
+    kw = dict(state2=s2_ref, split=split) if split < D else {}
+    ops.sparse_rowwise_adagrad(t_ref, s_ref, keys, 7, grads, 0.05, 1e-8, **kw)
+    kw = dict(state2=s2_gpu, split=split) if split < D else {}
+    ops.sparse_rowwise_adagrad(t_gpu, s_gpu, keys.to(dev), 7, grads.to(dev), 0.05, 1e-8, **kw)
+    torch.testing.assert_close(t_gpu.cpu(), t_ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(s_gpu.cpu(), s_ref, rtol=1e-5, atol=1e-6)
+    if split < D:
+        torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-5, atol=1e-6)
+
+
 def test_dense_optimizers(dev):
     g = torch.Generator().manual_seed(2)
     n = 10003

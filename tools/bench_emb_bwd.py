@@ -20,18 +20,26 @@ def main(B=16384):
     U = int(counts.sum())
     dX = torch.randn(B, 26 * 32, device=dev).to(torch.bfloat16)
     dw = torch.randn(B, device=dev)
-    g = torch.zeros(U, 33, device=dev)
-    for _ in range(3):
-        ops.wd_emb_backward(dX, dw, inv, 26, 32, g)
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(20):
-        ops.wd_emb_backward(dX, dw, inv, 26, 32, g)
-    e.record()
-    torch.cuda.synchronize()
-    print(f"U={U} lookups={B * 26} emb_backward {s.elapsed_time(e) / 20 * 1e3:.1f} us "
-          f"(MINIPS_EMB_BWD={os.environ.get('MINIPS_EMB_BWD', 'segment')})")
+    g = torch.zeros(U, 36, device=dev)
+
+    def timed(fn, n=20):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(n):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / n * 1e3
+
+    full = timed(lambda: ops.wd_emb_backward(dX, dw, inv, 26, 32, g))
+    csr = ops.emb_build_csr(inv, 26, U)
+    build = timed(lambda: ops.emb_build_csr(inv, 26, U))
+    seg = timed(lambda: ops.wd_emb_backward(dX, dw, inv, 26, 32, g, csr=csr))
+    print(f"U={U} lookups={B * 26} MINIPS_SEG_CFG={os.environ.get('MINIPS_SEG_CFG', '0')}: build+sum {full:.1f} us, "
+          f"csr build {build:.1f} us, zero+segment sum {seg:.1f} us")
 
 
 if __name__ == "__main__":
