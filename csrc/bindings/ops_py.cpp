@@ -129,12 +129,13 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   int64_t cap = 1024;
   while (cap < 2 * n) cap <<= 1;
   auto opts = keys.options();
-  // table_keys | counts[P] | total | cursor[P] in one allocation: one zero memset clears them all
+  // table_keys | counts[P] | total | shard counters [2*S*P] in one allocation: one zero memset
   const int64_t extra64 = (std::max<int64_t>(extra_zero_ints, 0) + 1) / 2;  // int32 count -> int64 words
-  auto zbuf = at::empty({cap + 2 * P + 1 + extra64}, opts);
+  const int64_t shw = 2 * (int64_t)minips_k::ub_shards(P) * P;
+  auto zbuf = at::empty({cap + P + 1 + shw + extra64}, opts);
   auto table_keys = zbuf.narrow(0, 0, cap), table_pos = at::empty({cap}, opts);
   auto slot = at::empty({n}, opts), flags = at::empty({n}, opts.dtype(at::kInt));
-  auto counts = zbuf.narrow(0, cap, P + 1), cursor = zbuf.narrow(0, cap + P + 1, P);
+  auto counts = zbuf.narrow(0, cap, P + 1), cursor = zbuf.narrow(0, cap + P + 1, shw);
   auto out_keys = at::empty({n}, opts), inverse = at::empty({n}, opts);
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   TORCH_CHECK(F >= 1 && n % F == 0, "unique_bucketize: numel must be a multiple of F");
@@ -143,7 +144,7 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
                              ptr<int64_t>(counts), ptr<int64_t>(cursor), ptr<int64_t>(out_keys), ptr<int64_t>(inverse),
                              stream_of(keys), (uint64_t)route_mult, (uint64_t)route_n, extra64 * 8);
   std::vector<at::Tensor> out{out_keys, inverse, counts.narrow(0, 0, P), counts.narrow(0, P, 1)};
-  if (extra64) out.push_back(zbuf.narrow(0, cap + 2 * P + 1, extra64).view(at::kInt));  // zeroed workspace
+  if (extra64) out.push_back(zbuf.narrow(0, cap + P + 1 + shw, extra64).view(at::kInt));  // zeroed workspace
   return out;
 }
 

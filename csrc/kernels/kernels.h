@@ -46,6 +46,8 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
 // route_mult != 0 dedupes the ROUTED keys key * route_mult mod route_n (uniq holds routed keys).
 // extra_zero_bytes: when table_keys | counts | cursor are one buffer, that many more bytes after
 // cursor are zeroed by the same memset (a workspace for a following op, e.g. emb_build_csr).
+// counter shards of unique_bucketize's zero buffer for P owners (table | counts | total | 2*S*P | extra)
+int ub_shards(int P);
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult = 0,

@@ -4,6 +4,7 @@
 //   K1     scatter_add_rows   worker-side gradient dedupe (segment sum via float atomics)
 //   K1     sparse_rowwise_adagrad / sparse_sgd   server-side apply on the shard rows
 //          embedding_bag_fwd/bwd                 pooled lookups (DLRM-style bags)
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -59,6 +60,16 @@ __device__ __forceinline__ unsigned long long wave_agg_inc(unsigned long long* c
 constexpr int kUbTile = 256;
 constexpr int kUbLds = 512;
 
+// element i of the feature-major order over a [rows_b, F] batch -> its index in the batch
+__device__ __forceinline__ int64_t tile_phys(int64_t i, int64_t rows_b, int F) {
+  if (rows_b * F < (1LL << 31)) {  // 32-bit division: the 64-bit one is a long software routine
+    const uint32_t ui = (uint32_t)i, rb = (uint32_t)rows_b;
+    const uint32_t f = ui / rb;
+    return (int64_t)(ui - f * rb) * F + f;
+  }
+  return (i % rows_b) * F + i / rows_b;
+}
+
 // Optional key routing fused into the dedupe: key -> key * mult mod rn (a bijection of [0, rn) when
 // mult is coprime to rn; the caller guarantees key * mult < 2^63). mult == 0: identity.
 __device__ __forceinline__ int64_t route_key(int64_t key, uint64_t mult, uint64_t rn) {
@@ -68,8 +79,8 @@ __device__ __forceinline__ int64_t route_key(int64_t key, uint64_t mult, uint64_
 __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t rows_b,
                                                             int F, const int64_t* __restrict__ bounds, int P,
                                                             unsigned long long* table_keys, int64_t cap, int64_t* slot,
-                                                            int32_t* flags, unsigned long long* counts, uint64_t rmult,
-                                                            uint64_t rn) {
+                                                            int32_t* flags, unsigned long long* sh_counts, int S,
+                                                            uint64_t rmult, uint64_t rn) {
   __shared__ unsigned long long lkey[kUbLds];
   __shared__ long long lgslot[kUbLds];
   __shared__ unsigned int lcount[256];  // per-owner claims of this block (P <= 256)
@@ -80,7 +91,7 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
   const int64_t i = (int64_t)blockIdx.x * kUbTile + t;
   const bool valid = i < n;
   int64_t phys = i;
-  if (F > 1 && valid) phys = (i % rows_b) * F + i / rows_b;  // feature-major tile
+  if (F > 1 && valid) phys = tile_phys(i, rows_b, F);  // feature-major tile
   const int64_t key = valid ? route_key(keys[phys], rmult, rn) : 0;
   int lslot = 0;
   bool lead = false;
@@ -126,17 +137,14 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
     }
   }
   __syncthreads();
+  // per-owner claim counts into counter shard blockIdx % S: every block adding to ONE counter
+  // serialises ~n/256 memory-side atomics on one address (~12 ns each: tens of microseconds)
+  unsigned long long* sh = sh_counts + (size_t)(blockIdx.x % S) * P;
   for (int p = t; p < P; p += kUbTile)
-    if (lcount[p]) atomicAdd(counts + p, (unsigned long long)lcount[p]);
-  if (t == 0) {
-    // counts[P] = total unique: the device-side U that consumers bound their loops by (no host sync)
-    unsigned long long blk = 0;
-    for (int p = 0; p < P; ++p) blk += lcount[p];
-    if (blk) atomicAdd(counts + P, blk);
-  }
-  if (valid) {
-    slot[phys] = lgslot[lslot];
-    flags[phys] = claimed ? 1 : 0;
+    if (lcount[p]) atomicAdd(sh + p, (unsigned long long)lcount[p]);
+  if (valid) {  // tile order: ub_assign's block b sees exactly the elements of this block b
+    slot[i] = lgslot[lslot];
+    flags[i] = claimed ? 1 : 0;
   }
 }
 
@@ -145,25 +153,44 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
 // shared cursor sees (#blocks x P) atomics instead of one per unique key.
 constexpr int kUbMaxP = 256;
 
-__global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restrict__ keys, int64_t n,
-                                                        const int64_t* __restrict__ bounds, int P,
+__global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t rows_b,
+                                                        int F, const int64_t* __restrict__ bounds, int P,
                                                         const int64_t* __restrict__ slot,
                                                         const int32_t* __restrict__ flags,
-                                                        const int64_t* __restrict__ counts, unsigned long long* cursor,
+                                                        const int64_t* __restrict__ sh_counts, int S,
+                                                        unsigned long long* sh_cursor, int64_t* counts,
                                                         int64_t* table_pos, int64_t* out_keys, uint64_t rmult,
                                                         uint64_t rn) {
   __shared__ int64_t offs[kUbMaxP];
+  __shared__ int64_t tot[kUbMaxP];
   __shared__ unsigned int lcnt[kUbMaxP];
   __shared__ unsigned long long lbase[kUbMaxP];
   const int t = threadIdx.x;
-  for (int p = t; p < P; p += blockDim.x) lcnt[p] = 0;
+  const int sh = (int)(blockIdx.x % S);
+  // owner p's unique keys occupy [sum_{q<p} tot[q], +tot[p]); inside that range the shards follow
+  // each other, so this block's shard starts pre[p] further (all from the insert's shard counts)
+  for (int p = t; p < P; p += blockDim.x) {
+    int64_t total = 0, pre = 0;
+    for (int q = 0; q < S; ++q) {
+      const int64_t c = sh_counts[(size_t)q * P + p];
+      total += c;
+      pre += q < sh ? c : 0;
+    }
+    tot[p] = total;
+    offs[p] = pre;
+    lcnt[p] = 0;
+  }
+  __syncthreads();
   if (t == 0) {
     int64_t acc = 0;
     for (int p = 0; p < P; ++p) {
-      offs[p] = acc;
-      acc += counts[p];
+      offs[p] += acc;
+      acc += tot[p];
     }
+    if (blockIdx.x == 0) counts[P] = acc;  // total unique: the device-side U (no host sync)
   }
+  if (blockIdx.x == 0)
+    for (int p = t; p < P; p += blockDim.x) counts[p] = tot[p];
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + t;
   const bool claimer = i < n && flags[i];
@@ -171,13 +198,13 @@ __global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restric
   int o = 0;
   unsigned int r = 0;
   if (claimer) {
-    key = route_key(keys[i], rmult, rn);
+    key = route_key(keys[F > 1 ? tile_phys(i, rows_b, F) : i], rmult, rn);
     o = owner_of(bounds, P, key);
     r = atomicAdd(lcnt + o, 1u);
   }
   __syncthreads();
-  for (int p = t; p < P; p += blockDim.x)
-    lbase[p] = lcnt[p] ? atomicAdd(cursor + p, (unsigned long long)lcnt[p]) : 0ULL;
+  unsigned long long* cur = sh_cursor + (size_t)sh * P;
+  for (int p = t; p < P; p += blockDim.x) lbase[p] = lcnt[p] ? atomicAdd(cur + p, (unsigned long long)lcnt[p]) : 0ULL;
   __syncthreads();
   if (claimer) {
     const int64_t pos = offs[o] + (int64_t)lbase[o] + (int64_t)r;
@@ -186,11 +213,13 @@ __global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restric
   }
 }
 
-__global__ void ub_inverse_kernel(int64_t n, const int64_t* __restrict__ slot, const int64_t* __restrict__ table_pos,
-                                  int64_t* inverse) {
+__global__ void ub_inverse_kernel(int64_t n, int64_t rows_b, int F, const int64_t* __restrict__ slot,
+                                  const int64_t* __restrict__ table_pos, int64_t* inverse) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    inverse[i] = table_pos[slot[i]];
+    inverse[F > 1 ? tile_phys(i, rows_b, F) : i] = table_pos[slot[i]];
 }
+
+int ub_shards(int P) { return std::max(1, std::min(32, 256 / std::max(P, 1))); }
 
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
@@ -201,27 +230,25 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
   if (P < 1 || P > kUbMaxP) throw std::runtime_error("unique_bucketize: 1 <= P <= 256 owner shards");
   if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
   if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
-  if (counts == table_keys + cap && cursor == counts + P + 1) {
-    // one buffer: table [cap] | counts [P] | total | cursor [P] -> a single zero memset
-    MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, (cap + 2 * P + 1) * sizeof(int64_t) + extra_zero_bytes, s));
-  } else if (cursor == counts + P + 1) {
-    MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, cap * sizeof(int64_t), s));
-    MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, (2 * P + 1) * sizeof(int64_t), s));
-  } else {
-    MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, cap * sizeof(int64_t), s));
-    MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, (P + 1) * sizeof(int64_t), s));  // counts[P] = total
-    MINIPS_HIP_CHECK(hipMemsetAsync(cursor, 0, P * sizeof(int64_t), s));
-  }
+  if (counts != table_keys + cap || cursor != counts + P + 1)
+    throw std::runtime_error("unique_bucketize: expects one buffer table | counts | total | shard counters");
+  // one buffer: table [cap] | counts [P] | total | shard counts [S*P] | shard cursors [S*P] | extra
+  // (`cursor` points at the shard counts; the caller sizes it with ub_shards) -> one zero memset
+  const int S = ub_shards(P);
+  int64_t* sh_counts = cursor;
+  int64_t* sh_cursor = cursor + (size_t)S * P;
+  MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, (cap + P + 1 + 2 * (int64_t)S * P) * sizeof(int64_t) + extra_zero_bytes, s));
   if (n == 0) return;
   const int block = 256;
   const int grid = grid_for(n, block, 4096);
   const int64_t tiles = (n + kUbTile - 1) / kUbTile;
   hipLaunchKernelGGL(ub_insert_kernel, dim3((unsigned)tiles), dim3(kUbTile), 0, s, keys, n, n / F, F, bounds, P,
-                     (unsigned long long*)table_keys, cap, slot, flags, (unsigned long long*)counts, route_mult,
+                     (unsigned long long*)table_keys, cap, slot, flags, (unsigned long long*)sh_counts, S, route_mult,
                      route_n);
-  hipLaunchKernelGGL(ub_assign_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, keys, n, bounds, P, slot,
-                     flags, counts, (unsigned long long*)cursor, table_pos, out_keys, route_mult, route_n);
-  hipLaunchKernelGGL(ub_inverse_kernel, grid, block, 0, s, n, slot, table_pos, inverse);
+  hipLaunchKernelGGL(ub_assign_kernel, dim3((unsigned)tiles), dim3(kUbTile), 0, s, keys, n, n / F, F, bounds, P, slot,
+                     flags, sh_counts, S, (unsigned long long*)sh_cursor, counts, table_pos, out_keys, route_mult,
+                     route_n);
+  hipLaunchKernelGGL(ub_inverse_kernel, grid, block, 0, s, n, n / F, F, slot, table_pos, inverse);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
