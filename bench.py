@@ -63,7 +63,14 @@ def main():
     # beside the current step (lookahead; no table state is read). The compute stream waits for
     # a batch's event before using it.
     ps = comm.plan_stream()
-    main_stream = torch.cuda.current_stream(dev)
+    # the step runs on a high-priority stream (the planning stream keeps normal priority)
+    from minips_amd.models.layers import compute_priority
+
+    main_stream = torch.cuda.Stream(device=dev, priority=compute_priority()) if dev.type == "cuda" \
+        else torch.cuda.current_stream(dev)
+    if dev.type == "cuda":
+        main_stream.wait_stream(torch.cuda.default_stream(dev))  # model init ran on the default stream
+    torch.cuda.set_stream(main_stream)
 
     def produce():
         with torch.cuda.stream(ps):

@@ -169,10 +169,15 @@ __global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restric
   const int sh = (int)(blockIdx.x % S);
   // owner p's unique keys occupy [sum_{q<p} tot[q], +tot[p]); inside that range the shards follow
   // each other, so this block's shard starts pre[p] further (all from the insert's shard counts)
+  // S * P <= 256 (ub_shards): one load per thread, all in flight at once (a per-owner loop over
+  // the shards would chain S memory-side latencies -- the counters were just written by atomics)
+  __shared__ int64_t shc[256];
+  if (t < S * P) shc[t] = sh_counts[t];
+  __syncthreads();
   for (int p = t; p < P; p += blockDim.x) {
     int64_t total = 0, pre = 0;
     for (int q = 0; q < S; ++q) {
-      const int64_t c = sh_counts[(size_t)q * P + p];
+      const int64_t c = shc[q * P + p];
       total += c;
       pre += q < sh ? c : 0;
     }
@@ -219,7 +224,7 @@ __global__ void ub_inverse_kernel(int64_t n, int64_t rows_b, int F, const int64_
     inverse[F > 1 ? tile_phys(i, rows_b, F) : i] = table_pos[slot[i]];
 }
 
-int ub_shards(int P) { return std::max(1, std::min(32, 256 / std::max(P, 1))); }
+int ub_shards(int P) { return std::max(1, std::min(32, 256 / std::max(P, 1))); }  // S * P <= 256
 
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,

@@ -104,6 +104,16 @@ class Linear:
         return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_STORE_BF16)
 
 
+def compute_priority() -> int:
+    """HIP stream priority for the training step's compute streams (main and weight-gradient side
+    stream). MINIPS_COMPUTE_PRIORITY=1 makes them high priority (-1), so the dispatcher favours
+    their workgroups over the planning / data stream's; measured neutral on the W&D step
+    (0.520-0.524 vs 0.519-0.521 ms), so normal priority is the default."""
+    import os
+
+    return -1 if os.environ.get("MINIPS_COMPUTE_PRIORITY", "0") == "1" else 0
+
+
 class SideStream:
     """Fork-join helper: independent work (weight gradients) issued on a second HIP stream.
 
@@ -112,7 +122,8 @@ class SideStream:
     all forked work. Disabled (or on CPU) it is a no-op and the block runs inline."""
 
     def __init__(self, device, enabled: bool = True):
-        self.stream = torch.cuda.Stream(device=device) if enabled and torch.device(device).type == "cuda" else None
+        self.stream = torch.cuda.Stream(device=device, priority=compute_priority()) \
+            if enabled and torch.device(device).type == "cuda" else None
 
     @contextlib.contextmanager
     def fork(self):
