@@ -84,11 +84,14 @@ def main():
     state = {"cur": produce()}
 
     def step():
-        nxt = produce()
         (dense, keys, labels), ev = state["cur"]
-        state["cur"] = nxt
         main_stream.wait_event(ev)
-        return model.train_step(dense, keys, labels, next_keys=nxt[0][1], next_on_plan_stream=True)
+
+        def next_keys():  # called by train_step where it issues the look-ahead planning
+            state["cur"] = produce()
+            return state["cur"][0][1]
+
+        return model.train_step(dense, keys, labels, next_keys=next_keys, next_on_plan_stream=True)
 
     loss0 = None
     for i in range(args.warmup):

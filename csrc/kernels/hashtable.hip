@@ -34,6 +34,7 @@ __global__ void hash_slots_kernel(unsigned long long* __restrict__ tab_keys, int
     const unsigned long long k = (unsigned long long)q[i];
     int64_t s = (int64_t)(mix64(k) & (uint64_t)mask);
     int64_t found = -1;
+    bool inserted = false;
     for (int64_t probe = 0; probe < cap; ++probe) {
       const unsigned long long cur = tab_keys[s];
       if (cur == k) {
@@ -52,7 +53,7 @@ __global__ void hash_slots_kernel(unsigned long long* __restrict__ tab_keys, int
             }
             row[c] = v;
           }
-          atomicAdd(counters, 1);
+          inserted = true;
           found = s;
           break;
         }
@@ -63,7 +64,14 @@ __global__ void hash_slots_kernel(unsigned long long* __restrict__ tab_keys, int
       }
       s = (s + 1) & mask;
     }
-    if (found < 0) atomicAdd(counters + 1, 1);  // table full
+    // wave-aggregated counters: one atomic per wave, not one per inserted key (same-address
+    // atomics serialise at the memory side)
+    const unsigned long long ins = __ballot(inserted), full = __ballot(found < 0);
+    const int leader = __ffsll((long long)__ballot(1)) - 1;
+    if ((threadIdx.x & 63) == leader) {
+      if (ins) atomicAdd(counters, __popcll(ins));
+      if (full) atomicAdd(counters + 1, __popcll(full));  // table full
+    }
     slots[i] = found;
   }
 }

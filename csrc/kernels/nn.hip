@@ -291,6 +291,9 @@ __global__ __launch_bounds__(kXentThreads) void softmax_xent_kernel(bf16_t* __re
   const int nfull = V >> 3;          // chunks with 8 valid columns
   const int tail = V & 7;            // valid columns of chunk nfull (0: none)
   const float L2E = 1.4426950408889634f;
+  // loss / hit sums accumulate in thread 0 over the block's rows: one atomic per block at the
+  // end (one per row would serialise M same-address atomics at the memory side, ~12 ns each)
+  float loss_acc = 0.f, hit_acc = 0.f;
   for (int64_t r = blockIdx.x; r < M; r += gridDim.x) {
     bf16_t* row = logits + r * ld;
     uint4 v[kXentChunks];
@@ -327,8 +330,8 @@ __global__ __launch_bounds__(kXentThreads) void softmax_xent_kernel(bf16_t* __re
     const float lse = mx + __logf(se);
     if (threadIdx.x == 0 && lab >= 0 && lab < V) {  // (row[lab] is rewritten only after the block syncs)
       const float zl = bf2f(row[lab]);
-      atomicAdd(loss_sum, lse - zl);
-      if (correct && zl >= mx) atomicAdd(correct, 1.f);
+      loss_acc += lse - zl;
+      hit_acc += zl >= mx ? 1.f : 0.f;
     }
     __syncthreads();
     const float sinv = scale / se;
@@ -349,6 +352,10 @@ __global__ __launch_bounds__(kXentThreads) void softmax_xent_kernel(bf16_t* __re
     }
     __syncthreads();
     if (threadIdx.x == 0 && lab >= 0 && lab < V) row[lab] = f2bf(bf2f(row[lab]) - scale);  // the -onehot term
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(loss_sum, loss_acc);
+    if (correct) atomicAdd(correct, hit_acc);
   }
 }
 

@@ -132,8 +132,12 @@ class SideStream:
             return
         cur = torch.cuda.current_stream(self.stream.device)
         self.stream.wait_stream(cur)
-        with torch.cuda.stream(self.stream):
-            yield
+        prev = ops.overlap_mode(True)  # forked work: GEMM splits chosen for throughput, not latency
+        try:
+            with torch.cuda.stream(self.stream):
+                yield
+        finally:
+            ops.overlap_mode(prev)
 
     def join(self):
         if self.stream is not None:

@@ -52,6 +52,12 @@ class WideDeepConfig:
         return (k + 7) // 8 * 8
 
 
+# where train_step issues the next batch's planning (dedupe, CSR, count exchange) and, with a
+# callable next_keys, its generation: "start" | "head" (after the forward) | "dgrad" (after the
+# dgrad chain, beside the memory-bound embedding backward)
+_PLAN_AT = os.environ.get("MINIPS_PLAN_AT", "start")
+
+
 def _align(n, a=8):
     return (n + a - 1) // a * a
 
@@ -173,8 +179,15 @@ class WideDeep:
         self._next_plan = None
         if plan is None:
             plan = self.emb.plan(keys, csr=True)
-        if next_keys is not None:
-            self.prefetch(next_keys, keys_on_plan_stream=next_on_plan_stream)
+
+        def issue_next(point):
+            # next_keys may be a callable that produces the next batch (on the planning stream)
+            # when called: the planning work then starts at _PLAN_AT, not at the step start
+            if next_keys is not None and point == _PLAN_AT:
+                nk = next_keys() if callable(next_keys) else next_keys
+                self.prefetch(nk, keys_on_plan_stream=next_on_plan_stream)
+
+        issue_next("start")
         rows, plan = self.emb.get(keys, plan=plan)
         G = self.dense.grad
         ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0])
@@ -185,6 +198,7 @@ class WideDeep:
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1], b["dwide"],
                     b["loss"], None, scale)
+        issue_next("head")
         side = self._side
         # weight gradients fork onto a second stream as soon as their inputs exist, beside the
         # dgrad chain (their split-K tails and reduces fill the gaps of the dependent chain)
@@ -197,6 +211,7 @@ class WideDeep:
         with side.fork():
             ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
         ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
+        issue_next("dgrad")
         dev = self.comm.device
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), cfg.row_width,
                                                                          dtype=torch.float32, device=dev)

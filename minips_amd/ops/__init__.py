@@ -119,9 +119,21 @@ def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=
 
 _WGRAD_MODE = __import__("os").environ.get("MINIPS_GEMM_WGRAD", "v1")
 _WGRAD_BLOCKS = int(__import__("os").environ.get("MINIPS_WGRAD_BLOCKS", "256" if _WGRAD_MODE == "v3" else "512"))
-# 2048 rows per split: the wgrads run on a side stream beside the dgrad chain, where fewer, longer
-# splits (less slab traffic) beat the isolated-kernel optimum of 640 (W&D step 0.560 -> 0.550 ms)
-_WGRAD_MIN_ROWS = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS", "512" if _WGRAD_MODE == "v3" else "2048"))
+# Reduction rows per split: 640 is the isolated-kernel optimum (a wgrad on the critical path, e.g.
+# the MLP); a wgrad forked onto a side stream beside the dgrad chain (SideStream, which sets
+# overlap_mode) favours throughput: fewer, longer splits with less slab traffic (W&D step 0.560 ->
+# 0.550 ms at 2048; the MLP step loses 15 % at 2048 when its wgrads are on the critical path).
+_WGRAD_MIN_ROWS = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS", "512" if _WGRAD_MODE == "v3" else "640"))
+_WGRAD_MIN_ROWS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS_OVERLAP",
+                                                           "512" if _WGRAD_MODE == "v3" else "2048"))
+_overlap_state = __import__("threading").local()
+
+
+def overlap_mode(on: bool) -> bool:
+    """Mark GEMMs issued from now on as overlapped side-stream work (returns the previous mode)."""
+    prev = getattr(_overlap_state, "on", False)
+    _overlap_state.on = on
+    return prev
 
 
 def linear_wgrad(dy, x, dw, split_k=None):
@@ -134,7 +146,8 @@ def linear_wgrad(dy, x, dw, split_k=None):
         # about one workgroup per CU (v3: 256x256 tiles, 1 WG/CU; v1/v2: ~512 128x128 blocks), but
         # a minimum number of reduction rows per split (tools/sweep_wgrad.py: shorter slices lose
         # to their fixed prologue/epilogue cost; the slab reduce makes splits cheap)
-        split_k = max(1, min(M // _WGRAD_MIN_ROWS, (_WGRAD_BLOCKS + tiles - 1) // tiles))
+        min_rows = _WGRAD_MIN_ROWS_OVERLAP if getattr(_overlap_state, "on", False) else _WGRAD_MIN_ROWS
+        split_k = max(1, min(M // min_rows, (_WGRAD_BLOCKS + tiles - 1) // tiles))
     return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
 
 
