@@ -118,7 +118,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
 
 // Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P], U [1]).
 std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tensor& bounds, int64_t F,
-                                         int64_t route_mult, int64_t route_n, int64_t extra_zero_ints) {
+                                         int64_t route_mult, int64_t route_n, int64_t extra_zero_ints,
+                                         bool csr_counts) {
   check_gpu(keys, "keys");
   check_gpu(bounds, "bounds");
   check_dtype(keys, at::kLong, "keys");
@@ -126,13 +127,20 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   TORCH_CHECK(bounds.dim() == 1 && bounds.numel() >= 2, "bounds must be [P+1]");
   const int64_t n = keys.numel();
   const int P = (int)bounds.numel() - 1;
+  // capacity: the next power of two above n (every key fits: U <= n < cap). Batches repeat ids
+  // heavily (Criteo-shaped: U ~ n/5), so the load factor stays low while the table (and its
+  // per-call zero fill) is half the size of a 2n table and stays closer to L2
   int64_t cap = 1024;
-  while (cap < 2 * n) cap <<= 1;
+  while (cap <= n) cap <<= 1;
   auto opts = keys.options();
   // table_keys | counts[P] | total | shard counters [2*S*P] in one allocation: one zero memset
   const int64_t extra64 = (std::max<int64_t>(extra_zero_ints, 0) + 1) / 2;  // int32 count -> int64 words
   const int64_t shw = 2 * (int64_t)minips_k::ub_shards(P) * P;
-  auto zbuf = at::empty({cap + P + 1 + shw + extra64}, opts);
+  // csr_counts: the first n ints of the extra block receive the per-unique-key lookup counts (the
+  // embedding-backward CSR's row sizes), from per-slot counters (cap int32) cleared by the memset
+  TORCH_CHECK(!csr_counts || extra_zero_ints >= n, "csr_counts needs extra_zero_ints >= n");
+  const int64_t scw = csr_counts ? cap / 2 : 0;
+  auto zbuf = at::empty({cap + P + 1 + shw + scw + extra64}, opts);
   auto table_keys = zbuf.narrow(0, 0, cap), table_pos = at::empty({cap}, opts);
   auto slot = at::empty({n}, opts), flags = at::empty({n}, opts.dtype(at::kInt));
   auto counts = zbuf.narrow(0, cap, P + 1), cursor = zbuf.narrow(0, cap + P + 1, shw);
@@ -142,9 +150,11 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   minips_k::unique_bucketize(ptr<int64_t>(keys), n, (int)F, ptr<int64_t>(bounds), P, ptr<int64_t>(table_keys),
                              ptr<int64_t>(table_pos), cap, ptr<int64_t>(slot), ptr<int32_t>(flags),
                              ptr<int64_t>(counts), ptr<int64_t>(cursor), ptr<int64_t>(out_keys), ptr<int64_t>(inverse),
-                             stream_of(keys), (uint64_t)route_mult, (uint64_t)route_n, extra64 * 8);
+                             stream_of(keys), (uint64_t)route_mult, (uint64_t)route_n, extra64 * 8,
+                             csr_counts ? reinterpret_cast<int*>(zbuf.data_ptr<int64_t>() + cap + P + 1 + shw + scw)
+                                        : nullptr);
   std::vector<at::Tensor> out{out_keys, inverse, counts.narrow(0, 0, P), counts.narrow(0, P, 1)};
-  if (extra64) out.push_back(zbuf.narrow(0, cap + P + 1 + shw, extra64).view(at::kInt));  // zeroed workspace
+  if (extra64) out.push_back(zbuf.narrow(0, cap + P + 1 + shw + scw, extra64).view(at::kInt));  // zeroed workspace
   return out;
 }
 
@@ -292,7 +302,7 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
 
 // Lookup CSR grouped by unique row (members/memrow int32 [B*F]) for U (upper-bound) rows.
 std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t U,
-                                      const c10::optional<at::Tensor>& zeroed) {
+                                      const c10::optional<at::Tensor>& zeroed, bool counts_ready) {
   check_gpu(inv, "inv");
   check_dtype(inv, at::kLong, "inv");
   const int64_t n = inv.numel();
@@ -308,7 +318,7 @@ std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t 
   at::Tensor members = at::empty({n}, io), memrow = at::empty({n}, io);
   c10::hip::HIPGuardMasqueradingAsCUDA g(inv.device());
   minips_k::emb_build_csr(ptr<int64_t>(inv), n / F, (int)F, (int)U, ws.data_ptr<int>(), members.data_ptr<int>(),
-                          memrow.data_ptr<int>(), stream_of(inv), zc);
+                          memrow.data_ptr<int>(), stream_of(inv), zc, counts_ready && zc);
   return {members, memrow};
 }
 
@@ -724,7 +734,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dlrm_interact_fwd", &dlrm_interact_fwd);
   m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
   m.def("unique_bucketize", &unique_bucketize, py::arg("keys"), py::arg("bounds"), py::arg("F") = 1,
-        py::arg("route_mult") = 0, py::arg("route_n") = 0, py::arg("extra_zero_ints") = 0);
+        py::arg("route_mult") = 0, py::arg("route_n") = 0, py::arg("extra_zero_ints") = 0,
+        py::arg("csr_counts") = false);
   m.def("gather_rows", &gather_rows, py::arg("table"), py::arg("keys"), py::arg("base"), py::arg("out"),
         py::arg("n_dev") = py::none());
   m.def("scatter_add_rows", &scatter_add_rows);
@@ -746,7 +757,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_head", &wd_head);
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none());
-  m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none());
+  m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none(),
+        py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),
         py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"),
         py::arg("grad_scale"), py::arg("w_bf16"), py::arg("step_dev") = py::none());

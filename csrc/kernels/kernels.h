@@ -51,7 +51,7 @@ int ub_shards(int P);
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult = 0,
-                      uint64_t route_n = 0, int64_t extra_zero_bytes = 0);
+                      uint64_t route_n = 0, int64_t extra_zero_bytes = 0, int* csr_counts = nullptr);
 
 // Row gather from a shard: out[i, :] = table[keys[i] - base, :] with dtype conversion.
 // table fp32 [R, D] row stride ld; out fp32 or bf16 [n, D].
@@ -114,7 +114,7 @@ void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide
 // cursor[U] | offsets[U+1] | tiles[U/1024+1]; members/memrow [B*F]) and the segmented sum.
 // zeroed_cc (nullable): a pre-zeroed 2U-int block used for counts|cursor (ws then starts at offsets).
 void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s,
-                   int* zeroed_cc = nullptr);
+                   int* zeroed_cc = nullptr, bool counts_ready = false);
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
                       const int64_t* U_dev = nullptr);

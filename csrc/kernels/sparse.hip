@@ -80,12 +80,16 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
                                                             int F, const int64_t* __restrict__ bounds, int P,
                                                             unsigned long long* table_keys, int64_t cap, int64_t* slot,
                                                             int32_t* flags, unsigned long long* sh_counts, int S,
-                                                            uint64_t rmult, uint64_t rn) {
+                                                            uint64_t rmult, uint64_t rn, int* slot_cnt) {
   __shared__ unsigned long long lkey[kUbLds];
   __shared__ long long lgslot[kUbLds];
+  __shared__ unsigned int lkcnt[kUbLds];  // occurrences of each block-distinct key (slot_cnt)
   __shared__ unsigned int lcount[256];  // per-owner claims of this block (P <= 256)
   const int t = threadIdx.x;
-  for (int j = t; j < kUbLds; j += kUbTile) lkey[j] = (unsigned long long)kEmpty;
+  for (int j = t; j < kUbLds; j += kUbTile) {
+    lkey[j] = (unsigned long long)kEmpty;
+    lkcnt[j] = 0;
+  }
   for (int p = t; p < P; p += kUbTile) lcount[p] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kUbTile + t;
@@ -107,6 +111,7 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
       h = (h + 1) & (kUbLds - 1);
     }
     lslot = h;
+    if (slot_cnt) atomicAdd(lkcnt + h, 1u);
   }
   __syncthreads();
   bool claimed = false;
@@ -131,6 +136,9 @@ __global__ __launch_bounds__(kUbTile) void ub_insert_kernel(const int64_t* __res
       h = (h + 1) & mask;
     }
     lgslot[lslot] = h;
+    // per-key lookup counts (the embedding-backward CSR's row sizes): one global atomic per
+    // block-distinct key, not per lookup (Zipf-hot keys would serialise thousands)
+    if (slot_cnt) atomicAdd(slot_cnt + h, (int)lkcnt[lslot]);
     if (claimed) {
       owner = owner_of(bounds, P, key);
       atomicAdd(lcount + owner, 1u);
@@ -160,7 +168,8 @@ __global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restric
                                                         const int64_t* __restrict__ sh_counts, int S,
                                                         unsigned long long* sh_cursor, int64_t* counts,
                                                         int64_t* table_pos, int64_t* out_keys, uint64_t rmult,
-                                                        uint64_t rn) {
+                                                        uint64_t rn, const int* __restrict__ slot_cnt,
+                                                        int* __restrict__ csr_counts) {
   __shared__ int64_t offs[kUbMaxP];
   __shared__ int64_t tot[kUbMaxP];
   __shared__ unsigned int lcnt[kUbMaxP];
@@ -213,8 +222,10 @@ __global__ __launch_bounds__(256) void ub_assign_kernel(const int64_t* __restric
   __syncthreads();
   if (claimer) {
     const int64_t pos = offs[o] + (int64_t)lbase[o] + (int64_t)r;
-    table_pos[slot[i]] = pos;
+    const int64_t sl = slot[i];
+    table_pos[sl] = pos;
     out_keys[pos] = key;
+    if (csr_counts) csr_counts[pos] = slot_cnt[sl];
   }
 }
 
@@ -229,19 +240,22 @@ int ub_shards(int P) { return std::max(1, std::min(32, 256 / std::max(P, 1))); }
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult,
-                      uint64_t route_n, int64_t extra_zero_bytes) {
+                      uint64_t route_n, int64_t extra_zero_bytes, int* csr_counts) {
   if (F < 1 || n % F) throw std::runtime_error("unique_bucketize: n must be a multiple of F");
   if (route_mult && !route_n) throw std::runtime_error("unique_bucketize: routing needs the row count");
   if (P < 1 || P > kUbMaxP) throw std::runtime_error("unique_bucketize: 1 <= P <= 256 owner shards");
   if (cap & (cap - 1)) throw std::runtime_error("unique_bucketize: capacity must be a power of two");
-  if (n > 0 && cap < 2 * n) throw std::runtime_error("unique_bucketize: capacity < 2n");
+  if (n > 0 && cap <= n) throw std::runtime_error("unique_bucketize: capacity must exceed n");
   if (counts != table_keys + cap || cursor != counts + P + 1)
     throw std::runtime_error("unique_bucketize: expects one buffer table | counts | total | shard counters");
-  // one buffer: table [cap] | counts [P] | total | shard counts [S*P] | shard cursors [S*P] | extra
-  // (`cursor` points at the shard counts; the caller sizes it with ub_shards) -> one zero memset
+  // one buffer: table [cap] | counts [P] | total | shard counts [S*P] | shard cursors [S*P] |
+  // (csr_counts: per-slot lookup counts, cap int32) | extra; `cursor` points at the shard counts
+  // (the caller sizes it with ub_shards) -> one zero memset
   const int S = ub_shards(P);
   int64_t* sh_counts = cursor;
   int64_t* sh_cursor = cursor + (size_t)S * P;
+  int* slot_cnt = csr_counts ? reinterpret_cast<int*>(sh_cursor + (size_t)S * P) : nullptr;
+  if (csr_counts) extra_zero_bytes += cap * (int64_t)sizeof(int);
   MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, (cap + P + 1 + 2 * (int64_t)S * P) * sizeof(int64_t) + extra_zero_bytes, s));
   if (n == 0) return;
   const int block = 256;
@@ -249,10 +263,10 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
   const int64_t tiles = (n + kUbTile - 1) / kUbTile;
   hipLaunchKernelGGL(ub_insert_kernel, dim3((unsigned)tiles), dim3(kUbTile), 0, s, keys, n, n / F, F, bounds, P,
                      (unsigned long long*)table_keys, cap, slot, flags, (unsigned long long*)sh_counts, S, route_mult,
-                     route_n);
+                     route_n, slot_cnt);
   hipLaunchKernelGGL(ub_assign_kernel, dim3((unsigned)tiles), dim3(kUbTile), 0, s, keys, n, n / F, F, bounds, P, slot,
                      flags, sh_counts, S, (unsigned long long*)sh_cursor, counts, table_pos, out_keys, route_mult,
-                     route_n);
+                     route_n, slot_cnt, csr_counts);
   hipLaunchKernelGGL(ub_inverse_kernel, grid, block, 0, s, n, n / F, F, slot, table_pos, inverse);
   MINIPS_HIP_CHECK(hipGetLastError());
 }

@@ -91,6 +91,44 @@ void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_st
 // partials in registers across all samples it visits: one atomic per lane per column at the end.
 constexpr int kHeadWaves = 16;  // 1024-thread blocks: 4x the waves in flight, same atomic count
 
+// PER_LANE consecutive bf16 of a row as one vector access (8 B for 4, 16 B for 8): the
+// element-wise 2-byte loads / stores cost 4-8 memory instructions per lane instead of one
+template <int PER_LANE>
+__device__ __forceinline__ void head_load(const bf16_t* p, float (&h)[PER_LANE]) {
+  if constexpr (PER_LANE == 4) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    h[0] = __uint_as_float(u.x << 16);
+    h[1] = __uint_as_float(u.x & 0xffff0000u);
+    h[2] = __uint_as_float(u.y << 16);
+    h[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else if constexpr (PER_LANE == 8) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      h[2 * q] = __uint_as_float(w[q] << 16);
+      h[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < PER_LANE; ++j) h[j] = bf2f(p[j]);
+  }
+}
+
+// v holds bf16-exact values (already rounded): their top 16 bits are the bf16 encoding
+template <int PER_LANE>
+__device__ __forceinline__ void head_store(bf16_t* p, const float (&v)[PER_LANE]) {
+  auto pk = [](float lo, float hi) { return (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u); };
+  if constexpr (PER_LANE == 4) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+  } else if constexpr (PER_LANE == 8) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(pk(v[0], v[1]), pk(v[2], v[3]), pk(v[4], v[5]), pk(v[6], v[7]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < PER_LANE; ++j) p[j] = f2bf(v[j]);
+  }
+}
+
 template <int PER_LANE>
 __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* __restrict__ H, int64_t B, int Hd,
                                                       const bf16_t* __restrict__ w, const bf16_t* __restrict__ b0,
@@ -120,11 +158,7 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
       const int64_t b = b0s + s;
 #pragma unroll
       for (int j = 0; j < PER_LANE; ++j) h[s][j] = 0.f;
-      if (b < B) {
-        const bf16_t* hp = H + b * Hd + lane * PER_LANE;
-#pragma unroll
-        for (int j = 0; j < PER_LANE; ++j) h[s][j] = bf2f(hp[j]);
-      }
+      if (b < B) head_load<PER_LANE>(H + b * Hd + lane * PER_LANE, h[s]);
       float acc = 0.f;
 #pragma unroll
       for (int j = 0; j < PER_LANE; ++j) acc += h[s][j] * wl[j];
@@ -145,14 +179,14 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
         dbl += dz;
         lossl += fmaxf(zz, 0.f) - zz * label + log1pf(__expf(-fabsf(zz)));
       }
-      bf16_t* dp = dH + b * Hd + lane * PER_LANE;
+      float gv[PER_LANE];
 #pragma unroll
       for (int j = 0; j < PER_LANE; ++j) {
         dwl[j] += dz * h[s][j];
-        const bf16_t g = f2bf(h[s][j] > 0.f ? dz * wl[j] : 0.f);
-        dp[j] = g;
-        csl[j] += bf2f(g);
+        gv[j] = bf2f(f2bf(h[s][j] > 0.f ? dz * wl[j] : 0.f));
+        csl[j] += gv[j];
       }
+      head_store<PER_LANE>(dH + b * Hd + lane * PER_LANE, gv);
     }
   }
   // reduce the 4 waves of the block in LDS, then one global atomic per column per block
@@ -481,10 +515,14 @@ __device__ __forceinline__ void seg_flush(float* __restrict__ grad_rows, int row
                                           float accw, bool wide, int prev_row, int next_row, int l) {
   float* out = grad_rows + (int64_t)row * row_stride + 4 * l;
   if (row != prev_row && row != next_row) {  // the whole row lies inside this group's range
-    out[0] = acc.x;
-    out[1] = acc.y;
-    out[2] = acc.z;
-    out[3] = acc.w;
+    if ((row_stride & 3) == 0)
+      *reinterpret_cast<float4*>(out) = acc;  // 16-byte rows: one vector store
+    else {
+      out[0] = acc.x;
+      out[1] = acc.y;
+      out[2] = acc.z;
+      out[3] = acc.w;
+    }
     if (wide && l == 0) out[D] = accw;
   } else {
     atomicAdd(out + 0, acc.x);
@@ -582,7 +620,7 @@ __global__ void zero_rows_dev_kernel(float* __restrict__ rows, int stride, int64
 // planning time, off the critical path). ws: counts[U] | cursor[U] | offsets[U+1] | tiles;
 // members/memrow: [B*F] lookup ids and their rows, sorted by row.
 void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s,
-                   int* zeroed_cc) {
+                   int* zeroed_cc, bool counts_ready) {
   if (B <= 0 || U <= 0) return;
   // counts | cursor: 2U ints that must start at zero -- a caller-provided, already-zeroed block
   // (cleared by the dedupe's memset) or the head of ws
@@ -593,7 +631,8 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
   const int ntiles = (U + kScanTile - 1) / kScanTile;
   if (!zeroed_cc) MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int) * 2 * (size_t)U, s));
   dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);
-  hipLaunchKernelGGL(emb_seg_count_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, counts);
+  // counts_ready: the dedupe already wrote the per-row lookup counts into zeroed_cc[0, U)
+  if (!(counts_ready && zeroed_cc)) hipLaunchKernelGGL(emb_seg_count_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, counts);
   hipLaunchKernelGGL(emb_scan_reduce_kernel, ntiles, 256, 0, s, counts, U, tiles);
   hipLaunchKernelGGL(emb_scan_top_kernel, 1, 256, 0, s, tiles, ntiles);
   hipLaunchKernelGGL(emb_scan_final_kernel, ntiles, 256, 0, s, counts, U, tiles, offsets);

@@ -164,14 +164,16 @@ def unique_bucketize(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1):
 
 
 def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1, route_mult: int = 0,
-                       route_n: int = 0, extra_zero_ints: int = 0):
+                       route_n: int = 0, extra_zero_ints: int = 0, csr_counts: bool = False):
     """unique_bucketize plus the total unique count U as a 1-element device tensor, so that
     consumers (gather_rows / sparse_* with ``n_dev``, wd_emb_backward with ``U_dev``) bound
     their work on the GPU without a host round trip. ``route_mult`` != 0 first maps every key to
-    key * route_mult mod route_n (fused into the GPU kernel)."""
+    key * route_mult mod route_n (fused into the GPU kernel). ``csr_counts`` (GPU, with
+    extra_zero_ints >= n): the first n ints of the zeroed block receive each unique key's lookup
+    count, for emb_build_csr(..., counts_ready=True)."""
     if _gpu(keys):
         out = kernels().unique_bucketize(keys.contiguous(), bounds.contiguous(), int(F), int(route_mult),
-                                         int(route_n), int(extra_zero_ints))
+                                         int(route_n), int(extra_zero_ints), bool(csr_counts))
         if extra_zero_ints:  # (..., zeroed int32 workspace cleared by the same memset)
             return tuple(out[:4]), out[4]
         return tuple(out)
@@ -313,13 +315,13 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
         dH_colsum += g.float().sum(0)
 
 
-def emb_build_csr(inv, F, U, zeroed=None):
+def emb_build_csr(inv, F, U, zeroed=None, counts_ready=False):
     """Lookups grouped by unique row: (members, memrow) int32 [n] with memrow sorted and
     members[i] the lookup id (b*F + f) of the i-th entry. Depends on ``inv`` only, so the PS
     builds it while planning a batch (off the critical path). ``zeroed``: an already-zero int32
     block of >= 2U (from unique_bucketize_n's extra_zero_ints) saves the counter memset."""
     if _gpu(inv):
-        return tuple(kernels().emb_build_csr(inv, int(F), int(max(U, 1)), zeroed))
+        return tuple(kernels().emb_build_csr(inv, int(F), int(max(U, 1)), zeroed, bool(counts_ready)))
     order = torch.sort(inv, stable=True).indices
     return order.to(torch.int32), inv[order].to(torch.int32)
 

@@ -283,6 +283,11 @@ def _route_multiplier(num_rows: int) -> int:
     return 0
 
 
+# the dedupe counts each unique key's lookups for the embedding-backward CSR (one pass less);
+# MINIPS_CSR_FUSED=0 counts in emb_build_csr instead
+_CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
+
+
 @dataclass
 class SparsePlan:
     """Routing of one batch's keys. Row counts are host ints on multi-rank runs (the all-to-all
@@ -398,19 +403,21 @@ class SparseTable:
         flat = keys.reshape(-1).to(torch.int64)
         rmult = getattr(self, "route_mult", 0)
         want_csr = csr and flat.is_cuda
+        fused = want_csr and _CSR_FUSED
         n = flat.numel()
         zeroed = None
         if rmult:  # range tables: the routing is fused into the dedupe kernel
             pp.flat = flat
             res = ops.unique_bucketize_n(flat, self.bounds, pp.F, rmult, self.num_rows,
-                                         extra_zero_ints=2 * n if want_csr else 0)
+                                         extra_zero_ints=2 * n if want_csr else 0, csr_counts=fused)
         else:
             pp.flat = self._route_keys(flat)
-            res = ops.unique_bucketize_n(pp.flat, self.bounds, pp.F, extra_zero_ints=2 * n if want_csr else 0)
-        if want_csr:  # the CSR's counters were cleared by the dedupe's single memset
-            res, zeroed = res
+            res = ops.unique_bucketize_n(pp.flat, self.bounds, pp.F, extra_zero_ints=2 * n if want_csr else 0,
+                                         csr_counts=fused)
+        if want_csr:  # the CSR's counters were cleared by the dedupe's single memset, and the
+            res, zeroed = res  # dedupe already counted each unique key's lookups into them
         pp.uniq, pp.inv, pp.counts, pp.U_dev = res
-        pp.csr = ops.emb_build_csr(pp.inv, pp.F, n, zeroed=zeroed) if want_csr else None
+        pp.csr = ops.emb_build_csr(pp.inv, pp.F, n, zeroed=zeroed, counts_ready=fused) if want_csr else None
         pp.host = pp.event = None
         if self.comm.world > 1:
             recv = torch.empty_like(pp.counts)

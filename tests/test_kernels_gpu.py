@@ -338,3 +338,28 @@ def test_unique_bucketize_fused_routing(dev):
     ur, invr, cr, Ur = ops.unique_bucketize_n(keys, bounds, 26, A, N)
     assert int(U) == int(Ur) and c.cpu().tolist() == cr.tolist()
     assert torch.equal(u.cpu()[inv.cpu()], (keys.reshape(-1) * A) % N)
+
+
+@pytest.mark.parametrize("P", [1, 8])
+def test_dedupe_fused_csr_counts(dev, P):
+    """The dedupe's fused per-key lookup counts equal bincount(inverse), and the CSR built from
+    them (counts_ready) groups exactly the lookups of each unique row."""
+    g = torch.Generator().manual_seed(P)
+    B, F = 4096, 26
+    hot = torch.randint(0, 4, (B, F), generator=g)            # Zipf-like head: tiny cardinalities
+    cold = torch.randint(0, 1 << 20, (B, F), generator=g)
+    keys = torch.where(torch.rand(B, F, generator=g) < 0.5, hot, cold).to(dev)
+    n = B * F
+    bounds = torch.linspace(0, 1 << 20, P + 1).long().to(dev)
+    bounds[-1] = 1 << 62
+    (uniq, inv, counts, U_dev), zeroed = ops.unique_bucketize_n(keys, bounds, F, extra_zero_ints=2 * n,
+                                                                csr_counts=True)
+    U = int(U_dev.item())
+    ref = torch.bincount(inv.cpu(), minlength=U)
+    torch.testing.assert_close(zeroed[:U].cpu(), ref.to(torch.int32))
+    assert int(zeroed[U:n].abs().sum()) == 0
+    members, memrow = ops.emb_build_csr(inv, F, n, zeroed=zeroed, counts_ready=True)
+    memrow_c, members_c = memrow.cpu().long(), members.cpu().long()
+    assert bool((memrow_c[1:] >= memrow_c[:-1]).all())
+    torch.testing.assert_close(inv.cpu()[members_c], memrow_c)
+    assert sorted(members_c.tolist()) == list(range(n))
