@@ -11,7 +11,7 @@ if [[ $STAGE == all || $STAGE == smoke ]]; then
   tail -3 gpurun_out/smoke.log
 fi
 if [[ $STAGE == all || $STAGE == test ]]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
   tail -3 gpurun_out/pytest_gpu.log
 fi
 if [[ $STAGE == all || $STAGE == bench ]]; then
