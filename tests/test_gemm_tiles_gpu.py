@@ -41,6 +41,16 @@ dW = torch.ones(520, 264, device=dev)
 ops.linear_wgrad(dy.to(dev), x.to(dev), dW)
 ref = 1.0 + dy.float().t() @ x.float()
 assert float((dW.cpu() - ref).abs().max()) < 0.2, float((dW.cpu() - ref).abs().max())
+# back-to-back split-K wgrads on one stream (slab workspace reuse), many splits, M/N tails
+for it, (Mw, Nw, Kw, sp) in enumerate([(8192, 1024, 848, 8), (8192, 520, 264, 16), (2048, 264, 136, 5),
+                                       (8192, 1024, 848, 8), (4096, 256, 1032, 2)]):
+    g = torch.Generator().manual_seed(it)
+    dy = bf(torch.randn(Mw, Nw, generator=g)); x = bf(torch.randn(Mw, Kw, generator=g))
+    dW = torch.full((Nw, Kw), 0.5, device=dev)
+    ops.linear_wgrad(dy.to(dev), x.to(dev), dW, split_k=sp)
+    ref = 0.5 + dy.float().t() @ x.float()
+    e = float((dW.cpu() - ref).abs().max()) / (Mw ** 0.5)
+    assert e < 3e-3, (it, Mw, Nw, Kw, sp, e)
 # batched (attention-style strided) GEMM
 Bt, Mb, Nb, Kb = 3, 200, 136, 64
 A = bf(torch.randn(Bt, Mb, Kb)); B = bf(torch.randn(Bt, Nb, Kb))
@@ -58,7 +68,7 @@ print("ok", worst)
     {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "1", "MINIPS_GEMM_V3_EARLY": "0", "MINIPS_GEMM_WGRAD": "v3"},
     {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "0"},         # v2 256x256
     {"MINIPS_GEMM_TILE": "128", "MINIPS_GEMM_WGRAD": "v2"},     # v2 128x128 incl. wgrad
-    {},                                                         # defaults (v1 wgrad)
+    {},                                                         # defaults (v1 wgrad, slab reduce)
 ])
 def test_gemm_variant(env):
     e = dict(os.environ, **env)
