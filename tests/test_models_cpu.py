@@ -1,6 +1,7 @@
 """CPU (torch reference ops) tests of the dense-tower models: each learns on synthetic data,
 and a 2-rank gloo run of the same global batch matches the 1-rank run (BSP) -- SURVEY.md §4
 items 3/5 (multi-worker semantics, end-to-end convergence)."""
+import pytest
 import torch
 
 from test_ps_gloo import run_world
@@ -152,3 +153,44 @@ def test_kmeans_converges_two_ranks():
     assert out[0][1] == out[1][1]  # both ranks pull the same centres
     for r in (0, 1):
         assert out[r][0][-1] < 12 * 0.25 * 1.3, out[r][0]
+
+
+def _blobs(K=8, D=16, n=4000, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    true = torch.randn(K, D, generator=g) * 6
+    X = true[torch.randint(0, K, (n,), generator=g)] + torch.randn(n, D, generator=g) * 0.3
+    return true, X
+
+
+@pytest.mark.parametrize("mode", ["random", "kmeans++", "kmeans_parallel"])
+def test_kmeans_init_modes(mode):
+    """Seeding modes of the reference's init_task (kmeans_helper.hpp:68-207): D^2 seeding
+    covers every well-separated blob; all modes return K rows drawn from the data."""
+    from minips_amd.models.kmeans import init_centres, sampled_sse
+
+    true, X = _blobs()
+    C = init_centres(X, 8, mode, seed=3)
+    assert C.shape == (8, 16)
+    # every centre is a data point (k-means|| candidates are data points too)
+    assert (torch.cdist(C, X, compute_mode="donot_use_mm_for_euclid_dist").min(1).values < 1e-4).all()
+    if mode != "random":
+        hit = torch.cdist(true, C).argmin(0).unique().numel()
+        assert hit == 8, hit
+        assert sampled_sse(X, C, n=200) < 16 * 0.3 ** 2 * 4
+    with pytest.raises(ValueError):
+        init_centres(X, 8, "bogus")
+
+
+def _km_init_fn(rank, world):
+    from minips_amd.models.kmeans import KMeans, KMeansConfig
+    from minips_amd.ps.comm import Comm
+
+    _, X = _blobs(seed=10 + rank)  # different local data per rank
+    km = KMeans(KMeansConfig(K=8, dims=16, init_mode="kmeans++", seed=1), Comm(device=torch.device("cpu")),
+                init_data=X)
+    return km.centres().reshape(-1).tolist()
+
+
+def test_kmeans_init_broadcast_two_ranks():
+    out = run_world(_km_init_fn)
+    assert out[0] == out[1]  # rank 0 seeds, every rank loads the same centres

@@ -248,3 +248,22 @@ def test_flash_attention(dev, B, T, H):
     _close(gp[1], c[1], 2e-3)
     err = (gp[2].float().cpu() - c[2].float()).abs().max() / c[2].float().abs().max()
     assert err < 2e-2, float(err)
+
+
+@pytest.mark.parametrize("mode", ["kmeans++", "kmeans_parallel"])
+def test_kmeans_init_gpu(dev, mode):
+    """GPU seeding: every D^2 pass runs the kmeans_assign kernels (MFMA form for the k-means||
+    candidate assignment); every well-separated blob receives a centre."""
+    from minips_amd.models.kmeans import init_centres, sampled_sse
+
+    g = torch.Generator().manual_seed(0)
+    K, D = 64, 32
+    true = torch.randn(K, D, generator=g) * 8
+    X = true[torch.randint(0, K, (20000,), generator=g)] + torch.randn(20000, D, generator=g) * 0.2
+    C = init_centres(X.to(dev), K, mode, seed=5)
+    torch.cuda.synchronize()
+    C = C.cpu()
+    assert C.shape == (K, D) and torch.isfinite(C).all()
+    hit = torch.cdist(true, C).argmin(0).unique().numel()
+    assert hit >= K - 2, hit  # D^2 seeding leaves at most a couple of blobs doubled up
+    assert sampled_sse(X.to(dev), C.to(dev), n=500) < 50.0
