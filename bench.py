@@ -15,6 +15,7 @@ line; `value` is the whole-job throughput and the time is the max over ranks.
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import sys
@@ -42,7 +43,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16384, help="per-GPU batch (weak scaling)")
     ap.add_argument("--consistency", default="bsp", choices=["bsp", "ssp", "asp"])
     ap.add_argument("--staleness", type=int, default=0)
-    ap.add_argument("--profile-steps", type=int, default=0, help="print per-phase timings")
+    ap.add_argument("--profile-steps", type=int, default=0, help="after the timed run: host issue time per step and a cProfile of N more steps (stderr)")
     args = ap.parse_args()
 
     from minips_amd.data.synthetic import CriteoSynth
@@ -81,15 +82,22 @@ def main():
             t.record_stream(main_stream)
         return b, ev
 
-    state = {"cur": produce()}
+    # Batches (and their key plans) run LOOKAHEAD steps ahead: the planning stream works on batch
+    # n+LOOKAHEAD while step n computes, so a plan is long finished when its step starts even
+    # though the host issues only about one step ahead of the GPU. Measured neutral on one MI355X
+    # (depth 1/2/3: 0.522-0.530 ms/step, tools/gpu_lookahead.sh), so the default stays 1.
+    lookahead = max(1, int(os.environ.get("MINIPS_LOOKAHEAD", "1")))
+    queue = collections.deque(produce() for _ in range(lookahead))
+    for (_, k, _), _ev in list(queue)[1:]:
+        model.prefetch(k, keys_on_plan_stream=True)
 
     def step():
-        (dense, keys, labels), ev = state["cur"]
+        (dense, keys, labels), ev = queue.popleft()
         main_stream.wait_event(ev)
 
         def next_keys():  # called by train_step where it issues the look-ahead planning
-            state["cur"] = produce()
-            return state["cur"][0][1]
+            queue.append(produce())
+            return queue[-1][0][1]
 
         return model.train_step(dense, keys, labels, next_keys=next_keys, next_on_plan_stream=True)
 
@@ -145,6 +153,27 @@ def main():
             "loss_last": round(loss_last, 5),
         }
         print(json.dumps(out), flush=True)
+    if args.profile_steps > 0:  # after the timed region: host issue time per step + host hot spots
+        import cProfile
+        import pstats
+
+        issue = []
+        pr = cProfile.Profile()
+        t1 = time.perf_counter()
+        for _ in range(args.profile_steps):
+            a = time.perf_counter()
+            pr.enable()
+            step()
+            pr.disable()
+            issue.append(time.perf_counter() - a)
+        model.drain()
+        torch.cuda.synchronize(dev)
+        wall = (time.perf_counter() - t1) / args.profile_steps
+        issue.sort()
+        print(f"[profile] wall {wall * 1e3:.3f} ms/step (cProfile on), host issue median "
+              f"{issue[len(issue) // 2] * 1e3:.3f} ms, min {issue[0] * 1e3:.3f}, max {issue[-1] * 1e3:.3f}",
+              file=sys.stderr, flush=True)
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(18)
     if n > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -155,7 +155,8 @@ class WideDeep:
     def prefetch(self, keys, keys_on_plan_stream: bool = False):
         """Lookahead: start routing the NEXT batch's keys (dedupe + count all-to-all on the
         planning stream) so it overlaps the current step; train_step picks the plan up."""
-        self._next_plan = (keys, self.emb.plan_async(keys, csr=True, keys_on_plan_stream=keys_on_plan_stream))
+        pend = self.__dict__.setdefault("_pending_plans", [])
+        pend.append([keys, self.emb.plan_async(keys, csr=True, keys_on_plan_stream=keys_on_plan_stream)])
 
     def train_step(self, dense, keys, labels, next_keys=None, next_on_plan_stream: bool = False) -> torch.Tensor:
         """One BSP superstep: Get, forward, backward, Add, Clock. Returns the summed loss
@@ -174,9 +175,14 @@ class WideDeep:
         F, D = cfg.F, cfg.emb_dim
         h = cfg.hidden[-1]
         b = self._buffers(B)
-        pre = getattr(self, "_next_plan", None)
-        plan = pre[1] if pre is not None and pre[0] is keys else None
-        self._next_plan = None
+        # plans issued ahead (prefetch); a batch may be several steps ahead (data-loader depth)
+        pend = self.__dict__.setdefault("_pending_plans", [])
+        plan = None
+        for i, (k, pp) in enumerate(pend):
+            if k is keys:
+                plan = pp
+                del pend[: i + 1]  # older entries were never consumed: drop them
+                break
         if plan is None:
             plan = self.emb.plan(keys, csr=True)
 
@@ -225,11 +231,13 @@ class WideDeep:
         return b["loss"]
 
     def _advance_next_plan(self):
-        """The step is issued: exchange the prefetched plan's keys now (planning stream), off
-        the next step's critical path (SparseTable.advance_plan)."""
-        pre = getattr(self, "_next_plan", None)
-        if pre is not None:
-            self._next_plan = (pre[0], self.emb.advance_plan(pre[1]))
+        """The step is issued: exchange the prefetched plans' keys now (planning stream), off
+        the next step's critical path (SparseTable.advance_plan). With several plans in flight
+        the newest one (issued by this very step) waits for the next step, so the host never
+        blocks on counts that were just launched."""
+        pend = self.__dict__.get("_pending_plans") or []
+        for e in (pend[:-1] if len(pend) > 1 else pend):
+            e[1] = self.emb.advance_plan(e[1])
 
     def drain(self):
         self.emb.drain()
