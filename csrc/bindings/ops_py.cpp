@@ -373,7 +373,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
 
 void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g, double lr, double beta1,
                 double beta2, double eps, double weight_decay, int64_t step, double grad_scale,
-                const c10::optional<at::Tensor>& w_bf16, const c10::optional<at::Tensor>& step_dev) {
+                const c10::optional<at::Tensor>& w_bf16, const c10::optional<at::Tensor>& step_dev, bool zero_g) {
   for (auto* t : {&w, &m, &v}) {
     check_gpu(*t, "adam state");
     check_dtype(*t, at::kFloat, "adam state");
@@ -386,7 +386,7 @@ void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g
   c10::hip::HIPGuardMasqueradingAsCUDA gd(w.device());
   minips_k::adam_apply(ptr<float>(w), ptr<float>(m), ptr<float>(v), ptr<float>(g), w.numel(), (float)lr, (float)beta1,
                        (float)beta2, (float)eps, (float)weight_decay, (int)step, (float)grad_scale, wb, stream_of(w),
-                       step_dev.has_value() && step_dev->defined() ? step_dev->data_ptr<int>() : nullptr);
+                       step_dev.has_value() && step_dev->defined() ? step_dev->data_ptr<int>() : nullptr, zero_g);
 }
 
 void sgd_apply(at::Tensor& w, const at::Tensor& g, double lr, double grad_scale, const c10::optional<at::Tensor>& w_bf16) {
@@ -761,7 +761,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),
         py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"),
-        py::arg("grad_scale"), py::arg("w_bf16"), py::arg("step_dev") = py::none());
+        py::arg("grad_scale"), py::arg("w_bf16"), py::arg("step_dev") = py::none(), py::arg("zero_g") = false);
   m.def("sgd_apply", &sgd_apply);
   m.def("adagrad_apply", &adagrad_apply);
   m.def("cast_f32_bf16", &cast_f32_bf16);

@@ -10,9 +10,9 @@
 namespace minips_k {
 
 __global__ void adam_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
-                            const float* __restrict__ g, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                            float* __restrict__ g, int64_t n, float lr, float b1, float b2, float eps, float wd,
                             float bc1, float bc2, float gscale, bf16_t* __restrict__ wb,
-                            const int* __restrict__ step_dev) {
+                            const int* __restrict__ step_dev, bool zero_g) {
   if (step_dev) {  // device-side step (graph-replayable clocks): bias corrections from *step_dev
     const float t = (float)*step_dev;
     bc1 = 1.f - powf(b1, t);
@@ -39,6 +39,7 @@ __global__ void adam_kernel(float* __restrict__ w, float* __restrict__ m, float*
     reinterpret_cast<float4*>(m)[i] = M;
     reinterpret_cast<float4*>(v)[i] = V;
     if (wb) reinterpret_cast<uint2*>(wb)[i] = make_uint2(pack_bf2(W.x, W.y), pack_bf2(W.z, W.w));
+    if (zero_g) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // next clock's accumulator
   }
   // tail
   for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -48,6 +49,7 @@ __global__ void adam_kernel(float* __restrict__ w, float* __restrict__ m, float*
     v[i] = b2 * v[i] + (1.f - b2) * gg * gg;
     w[i] -= lr * ((m[i] / bc1) / (sqrtf(v[i] / bc2) + eps) + wd * w[i]);
     if (wb) wb[i] = f2bf(w[i]);
+    if (zero_g) g[i] = 0.f;
   }
 }
 
@@ -56,7 +58,8 @@ static void check_align(const void* p, const char* what) {
 }
 
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2, float eps,
-                float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s, const int* step_dev) {
+                float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s, const int* step_dev,
+                bool zero_g) {
   if (n <= 0) return;
   check_align(w, "adam w");
   check_align(m, "adam m");
@@ -65,8 +68,8 @@ void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float l
   if (w_bf16 && (reinterpret_cast<uintptr_t>(w_bf16) & 7)) throw std::runtime_error("adam w_bf16 must be 8B aligned");
   const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
   const int block = 256;
-  hipLaunchKernelGGL(adam_kernel, grid_for((n + 3) / 4, block), block, 0, s, w, m, v, g, n, lr, beta1, beta2, eps,
-                     weight_decay, bc1, bc2, grad_scale, w_bf16, step_dev);
+  hipLaunchKernelGGL(adam_kernel, grid_for((n + 3) / 4, block), block, 0, s, w, m, v, const_cast<float*>(g), n, lr, beta1, beta2, eps,
+                     weight_decay, bc1, bc2, grad_scale, w_bf16, step_dev, zero_g);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -345,12 +345,13 @@ def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=No
 
 # ----------------------------------------------------------------------------- optimizers
 def adam_apply(w, m, v, g, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=1, grad_scale=1.0,
-               w_bf16=None, step_dev=None):
+               w_bf16=None, step_dev=None, zero_g=False):
     """Fused Adam(W). ``step_dev`` (int32 [1] device tensor): the bias-correction step is read on the
-    device, so a captured (HIP graph) clock stays correct on replay."""
+    device, so a captured (HIP graph) clock stays correct on replay. ``zero_g``: the kernel also
+    clears ``g`` after reading it (the gradient accumulator of the next clock; no fill kernel)."""
     if _gpu(w):
         kernels().adam_apply(w, m, v, g, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
-                             int(step), float(grad_scale), w_bf16, step_dev)
+                             int(step), float(grad_scale), w_bf16, step_dev, bool(zero_g))
         return
     if step_dev is not None:
         step = int(step_dev.reshape(-1)[0])
@@ -361,6 +362,8 @@ def adam_apply(w, m, v, g, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.
     w.sub_(lr * ((m / bc1) / ((v / bc2).sqrt() + eps) + weight_decay * w))
     if w_bf16 is not None:
         w_bf16.copy_(w.to(torch.bfloat16))
+    if zero_g:
+        g.zero_()
 
 
 def sgd_apply(w, g, lr, grad_scale=1.0, w_bf16=None):

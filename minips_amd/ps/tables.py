@@ -199,12 +199,17 @@ class DenseTable:
             self.step_dev.add_(1)  # device twin of self.step (one per clock)
             if pending:
                 if comm.world == 1:  # the whole gradient is the owned shard
-                    self._apply(grad, step)
+                    # Adam clears it in the same pass (one fewer full-size kernel per clock)
+                    cleared = self._apply(grad, step, zero_g=grad.numel() == self.shard)
                 else:
                     comm.reduce_scatter(self.grad_shard, grad)
                     self._apply(self.grad_shard, step)
+                    cleared = False
                 comm.all_gather(self.params, self.params[self.base: self.base + self.shard])
-            grad.zero_()
+            else:
+                cleared = False
+            if not cleared:
+                grad.zero_()
 
         self.pipe.run(work)
         if self.pipe.async_:
@@ -212,11 +217,15 @@ class DenseTable:
             self.grad = self._ring[step % len(self._ring)]
             self.pipe.wait_clock(step - len(self._ring))
 
-    def _apply(self, g: torch.Tensor, step: int):
+    def _apply(self, g: torch.Tensor, step: int, zero_g: bool = False) -> bool:
+        """Apply the optimizer to the owned shard; True if ``g`` was cleared on the way."""
         out = self.params[self.base: self.base + self.shard] if self.pull_dtype == torch.bfloat16 else None
         if self.optimizer == "adam":
             ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
-                           self.weight_decay, step, 1.0, out, step_dev=self.step_dev)
+                           self.weight_decay, step, 1.0, out, step_dev=self.step_dev, zero_g=zero_g)
+            if out is None:
+                self.params[self.base: self.base + self.shard].copy_(self.master)
+            return zero_g
         elif self.optimizer == "adagrad":
             ops.adagrad_apply(self.master, self.m, g, self.lr, self.eps, 1.0, out)
         elif self.optimizer == "sgd":
@@ -229,6 +238,7 @@ class DenseTable:
             raise ValueError(self.optimizer)
         if out is None:
             self.params[self.base: self.base + self.shard].copy_(self.master)
+        return False
 
     def drain(self):
         self.pipe.drain()

@@ -150,6 +150,12 @@ def test_dense_optimizers(dev):
     for a, b in zip(gpu, cpu):
         torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(wb.float().cpu(), cpu[0].to(torch.bfloat16).float())
+    # zero_g: same update, and the gradient (odd length: float4 body + tail) comes back cleared
+    gz, gpu2 = gr.to(dev), [t.to(dev) for t in (w, m, v)]
+    ops.adam_apply(*gpu2, gz, 1e-2, step=3, weight_decay=0.01, zero_g=True)
+    for a, b in zip(gpu2, cpu):
+        torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=1e-6)
+    assert int((gz != 0).sum()) == 0
     acc = torch.rand(n, generator=g)
     w1, a1 = w.clone(), acc.clone()
     w2, a2 = w.to(dev), acc.to(dev)

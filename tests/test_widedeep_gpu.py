@@ -49,3 +49,27 @@ def test_widedeep_gpu_matches_cpu(dev):
 def test_widedeep_ssp_runs(dev):
     losses, _ = _run(dev, steps=10, consistency="ssp", staleness=1)
     assert all(l == l for l in losses) and losses[-1] < losses[0] + 0.05
+
+
+def test_widedeep_lookahead_depth_matches(dev):
+    """Key plans issued 1 or 2 batches ahead on the planning stream (bench.py's data-loader
+    depth) give the same training as planning each batch in its own step: planning reads no
+    table state, so the lookahead changes no semantics."""
+    data = CriteoSynth(512, cards=CARDS, device="cpu", seed=4)
+    batches = [tuple(t.to(dev) for t in data.next()) for _ in range(8)]
+    res = {}
+    for depth in (0, 1, 2):
+        torch.manual_seed(0)
+        m = WideDeep(WideDeepConfig(cards=CARDS), Comm(device=torch.device(dev)))
+        m.emb.shard.copy_(_init_rows(m))
+        for k in range(1, depth):  # batches 1..depth-1 planned before the first step
+            m.prefetch(batches[k][1])
+        losses = []
+        for i, (dense, keys, y) in enumerate(batches):
+            nk = batches[i + depth][1] if depth and i + depth < len(batches) else None
+            losses.append(float(m.train_step(dense, keys, y, next_keys=nk).item()) / 512)
+        m.drain()
+        res[depth] = losses
+    for depth in (1, 2):
+        for a, b in zip(res[depth], res[0]):
+            assert abs(a - b) < 1e-4, (depth, res)
