@@ -6,6 +6,7 @@
 // comm/{sender,mailbox}_test) with identical expected values, plus the tests the reference
 // lacked: checkpoint round trips in all three models, BSP/ASP CheckPoint not hanging,
 // libsvm/dumper round trip, heartbeat failure detection. Ports are ephemeral (no races).
+#include <atomic>
 #include <netinet/in.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -671,6 +672,65 @@ TEST(Mailbox, BarrierFourNodes) {
 }
 
 // ------------------------------------------------------------------------------ engine
+TEST(Mailbox, BarrierTwoNodes) {
+  // reference comm/mailbox_test.cpp:201-226 (ephemeral ports here, not fixed ones)
+  std::vector<Node> nodes;
+  for (uint32_t i = 0; i < 2; ++i) nodes.push_back(Node{i, "localhost", FreePort()});
+  FakeIdMapper idm;
+  std::atomic<int> passed{0};
+  std::vector<std::unique_ptr<Mailbox>> mbs;
+  for (auto& n : nodes) mbs.emplace_back(new Mailbox(n, nodes, &idm));
+  std::vector<std::thread> th;
+  for (auto& mb : mbs)
+    th.emplace_back([&mb, &passed] {
+      mb->Start();
+      mb->Barrier();
+      passed.fetch_add(1);
+      mb->Barrier();
+      // both nodes passed the first barrier before either leaves the second
+      if (passed.load() != 2) throw std::runtime_error("barrier let a node through early");
+      mb->Stop();
+    });
+  for (auto& t : th) t.join();
+  EXPECT_EQ(passed.load(), 2);
+}
+
+TEST(Engine, SingleNodeMapStorageTask) {
+  // reference driver/engine_test.cpp:51-92 (StartEverything on one node + SimpleTaskMapStorage)
+  Context::Get().ResetToDefaults();
+  Node me{0, "localhost", FreePort()};
+  Engine engine(me, {me});
+  engine.StartEverything(1);
+  auto t = engine.CreateTable<double>(EvenRanges(100, 1), ModelType::ASP, StorageType::Map, 0);
+  engine.Barrier();
+  MLTask task;
+  task.SetWorkerAlloc({{0, 4}});
+  task.SetTables({t});
+  std::atomic<int> ran{0};
+  task.SetLambda([&](const Info& info) {
+    auto table = info.CreateKVClientTable<double>(t);
+    table->Add(std::vector<Key>{3, 97}, std::vector<double>{1.0, 2.0});
+    table->Clock();
+    ran.fetch_add(1);
+  });
+  engine.Run(task);
+  std::vector<double> v;
+  MLTask check;
+  check.SetWorkerAlloc({{0, 1}});
+  check.SetTables({t});
+  check.SetLambda([&](const Info& info) {
+    auto table = info.CreateKVClientTable<double>(t);
+    table->Get(std::vector<Key>{3, 50, 97}, &v);
+  });
+  engine.Run(check);
+  engine.StopEverything();
+  EXPECT_EQ(ran.load(), 4);
+  ASSERT_EQ(v.size(), 3u);
+  EXPECT_DOUBLE_EQ(v[0], 4.0);
+  EXPECT_DOUBLE_EQ(v[1], 0.0);  // MapStorage default for a never-added key
+  EXPECT_DOUBLE_EQ(v[2], 8.0);
+}
+
 TEST(Engine, MultipleEnginesKVRoundTrip) {
   Context::Get().ResetToDefaults();
   std::vector<Node> nodes;
