@@ -161,8 +161,12 @@ class Checkpointer:
             with open(tmp, "w") as f:
                 f.write(str(it))
             os.replace(tmp, self.prefix + "latest")
-            done = sorted(int(d[len("iter_"):]) for d in os.listdir(self.prefix or ".")
-                          if d.startswith("iter_") and d[len("iter_"):].isdigit())
+            # the prefix is a path prefix (reference style, e.g. "/ckpt/lr_"), not necessarily a
+            # directory: list its directory and match "<basename>iter_<n>"
+            pdir, stem = os.path.split(self.prefix)
+            tag = stem + "iter_"
+            done = sorted(int(d[len(tag):]) for d in os.listdir(pdir or ".")
+                          if d.startswith(tag) and d[len(tag):].isdigit())
             for old in done[:-self.keep]:
                 if old != it:
                     import shutil

@@ -127,7 +127,18 @@ class _Pipeline:
 class DenseTable:
     def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
                  pull_dtype=torch.bfloat16, consistency: str = "bsp", staleness: int = 0, table_id: int = 0,
-                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, p2p: bool = False):
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, p2p: bool = False,
+                 value_dtype=torch.float32):
+        """``value_dtype`` float64 gives the reference's ``double`` tables (KVClientTable<double>
+        with VectorStorage::SubAdd, server/vector_storage.hpp:28-38): optimizer "add" only, pulled
+        in fp64, so BSP sums are exact for exactly representable deltas."""
+        if value_dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"value_dtype {value_dtype}")
+        if value_dtype == torch.float64:
+            if optimizer != "add":
+                raise ValueError("fp64 dense tables support the reference's plain add apply only")
+            pull_dtype = torch.float64
+        self.value_dtype = value_dtype
         self.comm = comm
         self.table_id = table_id
         self.n_params = n_params
@@ -140,12 +151,12 @@ class DenseTable:
         self.lr = lr
         self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
         self.pull_dtype = pull_dtype
-        self.master = torch.zeros(self.shard, dtype=torch.float32, device=dev)
+        self.master = torch.zeros(self.shard, dtype=value_dtype, device=dev)
         self.m = torch.zeros_like(self.master) if optimizer in ("adam", "adagrad") else None
         self.v = torch.zeros_like(self.master) if optimizer == "adam" else None
         self.params = torch.zeros(self.n_pad, dtype=pull_dtype, device=dev)
-        self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
-        self.grad_shard = torch.zeros(self.shard, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.n_pad, dtype=value_dtype, device=dev)
+        self.grad_shard = torch.zeros(self.shard, dtype=value_dtype, device=dev)
         self.step = 0
         # the Adam step also lives on the device (advanced inside the clock) so that a clock
         # captured in a HIP graph replays with the right bias correction
@@ -161,17 +172,17 @@ class DenseTable:
 
     # -- init / views -----------------------------------------------------------------------
     def load_full(self, full: torch.Tensor):
-        """Initialise from the full fp32 vector (identical on every rank)."""
+        """Initialise from the full vector (identical on every rank)."""
         assert full.numel() == self.n_params
-        flat = torch.zeros(self.n_pad, dtype=torch.float32, device=self.comm.device)
-        flat[: self.n_params] = full.to(self.comm.device, torch.float32)
+        flat = torch.zeros(self.n_pad, dtype=self.value_dtype, device=self.comm.device)
+        flat[: self.n_params] = full.to(self.comm.device, self.value_dtype)
         self.master.copy_(flat[self.base: self.base + self.shard])
         self.params.copy_(flat.to(self.pull_dtype))
 
     def full_master(self) -> torch.Tensor:
-        """All-gather of the fp32 master (checkpoint / tests)."""
+        """All-gather of the master values (checkpoint / tests)."""
         self.drain()
-        out = torch.empty(self.n_pad, dtype=torch.float32, device=self.comm.device)
+        out = torch.empty(self.n_pad, dtype=self.value_dtype, device=self.comm.device)
         self.comm.all_gather(out, self.master)
         return out[: self.n_params]
 
@@ -183,7 +194,7 @@ class DenseTable:
     def add(self, grad: torch.Tensor | None = None):
         """Accumulate a gradient (or mark the in-place-written self.grad as pushed)."""
         if grad is not None:
-            self.grad[: grad.numel()] += grad.reshape(-1).to(torch.float32)
+            self.grad[: grad.numel()] += grad.reshape(-1).to(self.value_dtype)
         self._pending = True
 
     def clock(self):

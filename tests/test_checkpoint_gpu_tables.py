@@ -162,3 +162,43 @@ def test_checkpoint_resume_on_gpu(dev, tmp_path):
     # (float atomics in split-K GEMMs / scatter-adds: bitwise equality is not guaranteed on GPU)
     torch.testing.assert_close(m2.dense.master, m.dense.master, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(m2.emb.shard, m.emb.shard, rtol=1e-3, atol=1e-4)
+
+
+
+def _fp64_table_roundtrip(device):
+    from minips_amd.ps.checkpoint import Checkpointer
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.tables import DenseTable
+
+    import tempfile
+
+    n = 4099
+    comm = Comm(device=torch.device(device))
+    t = DenseTable(comm, n, optimizer="add", value_dtype=torch.float64)
+    base = torch.arange(n, dtype=torch.float64)
+    expect = torch.zeros(n, dtype=torch.float64)
+    for s in range(5):
+        assert torch.equal(t.get()[:n].cpu(), expect)
+        d = 0.1 * base + 1e-9 * s
+        t.add(d.to(device))
+        t.clock()
+        expect = expect + d
+    t.drain()
+    assert t.params.dtype == torch.float64 and torch.equal(t.full_master().cpu(), expect)
+    with tempfile.TemporaryDirectory() as dname:
+        Checkpointer(comm, os.path.join(dname, "ck")).save({"w": t}, iteration=5, blocking=True)
+        t2 = DenseTable(comm, n, optimizer="add", value_dtype=torch.float64)
+        assert Checkpointer(comm, os.path.join(dname, "ck")).load({"w": t2}) == 5
+        assert torch.equal(t2.full_master().cpu(), expect)
+        assert torch.equal(t2.get()[:n].cpu(), expect)
+
+
+def test_dense_fp64_table_exact_cpu():
+    """fp64 dense table (reference KVClientTable<double>): BSP adds are exact and a checkpoint
+    round trip keeps every fp64 bit."""
+    _fp64_table_roundtrip("cpu")
+
+
+@pytest.mark.gpu
+def test_dense_fp64_table_gpu_exact(dev):
+    _fp64_table_roundtrip(dev)

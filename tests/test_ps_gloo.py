@@ -165,3 +165,45 @@ def test_sparse_push_in_bf16():
         expect = {3: 3.0, 50: 1.5, 97: 1.5, 0: 0.5, 1: 1.0}
         for k, row in zip([3, 50, 97, 3, rank], rows):
             assert row == [expect[k]] * 4, (rank, k, row)
+
+
+# ------------------------------------------------------------------------------ fp64 dense table
+def _fp64_bsp_fn(rank, world, steps=4, n=1000):
+    """The reference's double tables (BSP): after clock t every rank pulls exactly the fp64 sum
+    of t supersteps of every rank's deltas -- bit-for-bit, no fp32 rounding anywhere."""
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.tables import DenseTable
+
+    comm = Comm(device=torch.device("cpu"))
+    t = DenseTable(comm, n, optimizer="add", value_dtype=torch.float64)
+    base = torch.arange(n, dtype=torch.float64)
+    expect = torch.zeros(n, dtype=torch.float64)
+    ok = True
+    for s in range(steps):
+        got = t.get()[:n].clone()
+        ok = ok and bool(torch.equal(got, expect))
+        t.add(0.1 * (rank + 1) * base + 1e-9 * s)
+        t.clock()
+        tot = torch.zeros(n, dtype=torch.float64)
+        for r in range(world):
+            tot = tot + (0.1 * (r + 1) * base + 1e-9 * s)
+        expect = expect + tot
+    t.drain()
+    final = t.get()[:n]
+    return ok, bool(torch.equal(final, expect)), str(final.dtype), float((final.float().double() - expect).abs().max())
+
+
+def test_dense_fp64_bsp_exact_two_ranks():
+    out = run_world(_fp64_bsp_fn)
+    for r in (0, 1):
+        ok, final_ok, dtype, f32_err = out[r]
+        assert ok and final_ok and dtype == "torch.float64", out[r]
+        assert f32_err > 0  # the values are not fp32-representable: fp64 was really kept
+
+
+def test_dense_fp64_rejects_optimizers():
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.tables import DenseTable
+
+    with pytest.raises(ValueError):
+        DenseTable(Comm(device=torch.device("cpu")), 10, optimizer="adam", value_dtype=torch.float64)
