@@ -85,8 +85,10 @@ def main():
     # Batches (and their key plans) run LOOKAHEAD steps ahead: the planning stream works on batch
     # n+LOOKAHEAD while step n computes, so a plan is long finished when its step starts even
     # though the host issues only about one step ahead of the GPU. Measured neutral on one MI355X
-    # (depth 1/2/3: 0.522-0.530 ms/step, tools/gpu_lookahead.sh), so the default stays 1.
-    lookahead = max(1, int(os.environ.get("MINIPS_LOOKAHEAD", "1")))
+    # (depth 1/2/3: 0.522-0.530 ms/step, tools/gpu_lookahead.sh), so one rank keeps depth 1. With
+    # several ranks depth 2 is the default: the one host wait of a step (a plan's all-to-all
+    # split sizes, SparseTable.advance_plan) then lands on counts issued a whole step earlier.
+    lookahead = max(1, int(os.environ.get("MINIPS_LOOKAHEAD", "2" if n > 1 else "1")))
     queue = collections.deque(produce() for _ in range(lookahead))
     for (_, k, _), _ev in list(queue)[1:]:
         model.prefetch(k, keys_on_plan_stream=True)
