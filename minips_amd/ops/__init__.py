@@ -126,6 +126,12 @@ _WGRAD_BLOCKS = int(__import__("os").environ.get("MINIPS_WGRAD_BLOCKS", "256" if
 _WGRAD_MIN_ROWS = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS", "512" if _WGRAD_MODE == "v3" else "640"))
 _WGRAD_MIN_ROWS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS_OVERLAP",
                                                            "512" if _WGRAD_MODE == "v3" else "2048"))
+# Overlapped wgrads with few output tiles (W&D's 256x512 W3 grad: 8 tiles) would get only ~64
+# workgroups at 2048 rows per split; this floor on the block count (0: off) lets them split finer
+# (never below _WGRAD_MIN_ROWS rows per split). Measured worse on one MI355X (W&D 0.528 ->
+# 0.539 ms/step at 128 blocks, 0.548 at 256: the finer splits steal CUs from the dgrad chain and
+# add slab traffic; tools/gpu_wgrad_blocks.sh), so it stays off.
+_WGRAD_MIN_BLOCKS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_BLOCKS_OVERLAP", "0"))
 _overlap_state = __import__("threading").local()
 
 
@@ -146,8 +152,11 @@ def linear_wgrad(dy, x, dw, split_k=None):
         # about one workgroup per CU (v3: 256x256 tiles, 1 WG/CU; v1/v2: ~512 128x128 blocks), but
         # a minimum number of reduction rows per split (tools/sweep_wgrad.py: shorter slices lose
         # to their fixed prologue/epilogue cost; the slab reduce makes splits cheap)
-        min_rows = _WGRAD_MIN_ROWS_OVERLAP if getattr(_overlap_state, "on", False) else _WGRAD_MIN_ROWS
+        overlapped = getattr(_overlap_state, "on", False)
+        min_rows = _WGRAD_MIN_ROWS_OVERLAP if overlapped else _WGRAD_MIN_ROWS
         split_k = max(1, min(M // min_rows, (_WGRAD_BLOCKS + tiles - 1) // tiles))
+        if overlapped and _WGRAD_MIN_BLOCKS_OVERLAP and split_k * tiles < _WGRAD_MIN_BLOCKS_OVERLAP:
+            split_k = max(split_k, min(M // _WGRAD_MIN_ROWS, -(-_WGRAD_MIN_BLOCKS_OVERLAP // tiles)))
     return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
 
 
