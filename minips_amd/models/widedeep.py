@@ -56,6 +56,10 @@ class WideDeepConfig:
 # callable next_keys, its generation: "start" | "head" (after the forward) | "dgrad" (after the
 # dgrad chain, beside the memory-bound embedding backward)
 _PLAN_AT = os.environ.get("MINIPS_PLAN_AT", "start")
+# issue an async dense clock from the weight-gradient side stream (see train_step). Measured
+# slower on one MI355X (MINIPS_OVERLAP_W1=dense: 0.525-0.529 -> 0.544-0.549 ms/step: Adam then
+# competes with the memory-bound embedding backward; tools/gpu_dense_side.sh), so off by default.
+_DENSE_CLOCK_ON_SIDE = os.environ.get("MINIPS_DENSE_CLOCK_ON_SIDE", "0") == "1"
 
 
 def _align(n, a=8):
@@ -217,6 +221,14 @@ class WideDeep:
         with side.fork():
             ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
         ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
+        # an async dense clock (its own stream) needs only the weight gradients: issued from the
+        # side stream it starts as soon as the last wgrad ends, beside the embedding backward and
+        # the sparse push, instead of behind them
+        dense_early = _DENSE_CLOCK_ON_SIDE and self.dense.pipe.async_ and side.stream is not None
+        if dense_early:
+            with torch.cuda.stream(side.stream):
+                self.dense.add()
+                self.dense.clock()
         issue_next("dgrad")
         dev = self.comm.device
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), cfg.row_width,
@@ -225,8 +237,9 @@ class WideDeep:
         self.emb.add(plan, grad_rows)
         self.emb.clock()
         side.join()
-        self.dense.add()
-        self.dense.clock()
+        if not dense_early:
+            self.dense.add()
+            self.dense.clock()
         self._advance_next_plan()
         return b["loss"]
 
