@@ -52,6 +52,10 @@ def parse(argv=None):
                     help="eager: publish a checkpoint at the next step (waits for its files); async: "
                          "publish once every rank's writer finished (training never waits for the disk)")
     ap.add_argument("--with_injected_straggler", type=_flag_bool, default=False)
+    ap.add_argument("--K", type=int, default=0, help="K-Means centres (0: model default)")
+    ap.add_argument("--kmeans_init_mode", default="", choices=["", "random", "kmeans++", "kmeans_parallel"],
+                    help="K-Means seeding from a batch of local data (reference kmeans.cpp:154-192); "
+                         "empty: N(0,1) centres")
     ap.add_argument("--report_prefix", default="")
     ap.add_argument("--report_interval", type=int, default=10)
     ap.add_argument("--metrics_dir", default="")
@@ -139,10 +143,13 @@ def build(args, comm):
     if args.model == "kmeans":
         from .models.kmeans import KMeans, KMeansConfig
 
-        cfg = KMeansConfig(K=8 if args.small else 1000, dims=16 if args.small else 128,
-                           consistency=args.consistency, staleness=args.staleness)
-        m = KMeans(cfg, comm)
+        cfg = KMeansConfig(K=args.K or (8 if args.small else 1000), dims=16 if args.small else 128,
+                           consistency=args.consistency, staleness=args.staleness,
+                           init_mode=args.kmeans_init_mode or "random", seed=seed)
         B = args.batch or (256 if args.small else 65536)
+        # seeding reads its own batch of local data (rank 0's seeds are broadcast)
+        init = _GaussData(max(B, cfg.K), cfg.dims, dev, seed + 7919).next() if args.kmeans_init_mode else None
+        m = KMeans(cfg, comm, init_data=init)
         data = _Skippable(_GaussData(B, cfg.dims, dev, seed))
         return m, {0: m.table}, data, (lambda b: m.train_step(b)), B
     raise ValueError(args.model)

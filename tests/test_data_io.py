@@ -1,6 +1,7 @@
 """File ingest (SURVEY.md §2.6 io/, §2.7 lib/): libsvm shards through the native block assigner +
 mmap line reader cover every line exactly once across ranks, and a file-fed sparse LR learns
 through the prefetching loader."""
+import pytest
 import random
 
 import torch
@@ -74,3 +75,20 @@ def test_train_driver_file_input(tmp_path):
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     accs = [-v for _, v in out["losses"]]
     assert sum(accs[-5:]) / 5 > 0.85, accs
+
+
+@pytest.mark.parametrize("mode", ["kmeans++", "kmeans_parallel"])
+def test_train_driver_kmeans_init_flags(mode):
+    """--K / --kmeans_init_mode (the reference K-Means app's flags, kmeans.cpp:18-52)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "minips_amd.train", "--model", "kmeans", "--small=1", "--steps", "4",
+                        "--K", "6", "--kmeans_init_mode", mode], cwd=root, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["model"] == "kmeans" and all(v == v for _, v in out["losses"])
