@@ -12,7 +12,7 @@ import torch
 
 from .. import ops
 from ..ps.comm import Comm
-from ..ps.tables import SparseTable
+from ..ps.tables import HashSparseTable, SparseTable
 
 
 @dataclass
@@ -21,13 +21,20 @@ class SparseLRConfig:
     alpha: float = 0.1
     consistency: str = "bsp"
     staleness: int = 0
+    storage: str = "vector"  # reference kStorageType: "vector" (dense key range) or "map" (hash)
 
 
 class SparseLR:
     def __init__(self, cfg: SparseLRConfig, comm: Comm):
         self.cfg, self.comm = cfg, comm
-        self.table = SparseTable(comm, cfg.num_dims, 1, optimizer="add", pull_dtype=torch.float32, init_std=0.0,
-                                 consistency=cfg.consistency, staleness=cfg.staleness)
+        if cfg.storage.lower() == "map":  # MapStorage: rows created on first touch, zero-initialised
+            self.table = HashSparseTable(comm, 1, optimizer="add", pull_dtype=torch.float32, init_std=0.0,
+                                         consistency=cfg.consistency, staleness=cfg.staleness)
+        elif cfg.storage.lower() == "vector":
+            self.table = SparseTable(comm, cfg.num_dims, 1, optimizer="add", pull_dtype=torch.float32, init_std=0.0,
+                                     consistency=cfg.consistency, staleness=cfg.staleness)
+        else:
+            raise ValueError(f"kStorageType {cfg.storage!r}: Map or Vector")
 
     def train_step(self, rowptr, cols, vals, labels):
         """CSR batch (rowptr [B+1], cols/vals [nnz], labels [B] in {0,1} or {-1,1}).

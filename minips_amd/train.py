@@ -52,6 +52,8 @@ def parse(argv=None):
                     help="eager: publish a checkpoint at the next step (waits for its files); async: "
                          "publish once every rank's writer finished (training never waits for the disk)")
     ap.add_argument("--with_injected_straggler", type=_flag_bool, default=False)
+    ap.add_argument("--kStorageType", default="Vector", type=str.lower, choices=["vector", "map"],
+                    help="LR parameter storage: Vector (key range) or Map (GPU hash table, MapStorage)")
     ap.add_argument("--K", type=int, default=0, help="K-Means centres (0: model default)")
     ap.add_argument("--kmeans_init_mode", default="", choices=["", "random", "kmeans++", "kmeans_parallel"],
                     help="K-Means seeding from a batch of local data (reference kmeans.cpp:154-192); "
@@ -127,7 +129,7 @@ def build(args, comm):
             comm.all_reduce_(t, op=dist.ReduceOp.MAX)
             nd = int(t.item())
         m = SparseLR(SparseLRConfig(num_dims=nd, alpha=args.alpha, consistency=args.consistency,
-                                    staleness=args.staleness), comm)
+                                    staleness=args.staleness, storage=args.kStorageType), comm)
         B = args.batch or 1024
         return m, {0: m.table}, _Skippable(_Batches(shard, B, seed)), (lambda b: -m.train_step(*b)), B
     if args.model == "lr":
@@ -136,7 +138,7 @@ def build(args, comm):
 
         nd = args.num_dims or (5000 if args.small else 16_609_143)
         m = SparseLR(SparseLRConfig(num_dims=nd, alpha=args.alpha, consistency=args.consistency,
-                                    staleness=args.staleness), comm)
+                                    staleness=args.staleness, storage=args.kStorageType), comm)
         B = args.batch or (128 if args.small else 65536)
         data = _Skippable(SparseLRSynth(B, num_dims=nd, nnz=16 if args.small else 64, device=dev, seed=seed))
         return m, {0: m.table}, data, (lambda b: -m.train_step(*b)), B

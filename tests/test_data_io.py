@@ -92,3 +92,21 @@ def test_train_driver_kmeans_init_flags(mode):
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["model"] == "kmeans" and all(v == v for _, v in out["losses"])
+
+
+def test_train_driver_lr_map_storage_matches_vector():
+    """--kStorageType Map (GPU hash-table MapStorage) trains exactly like Vector storage (the
+    reference LR app's kStorageType flag; both start from zero rows)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for st in ("Vector", "Map"):
+        r = subprocess.run([sys.executable, "-m", "minips_amd.train", "--model", "lr", "--small=1", "--steps", "20",
+                            "--kStorageType", st], cwd=root, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[st] = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["losses"]
+    assert res["Map"] == res["Vector"], res
