@@ -257,9 +257,16 @@ def main(argv=None):
         torch.cuda.synchronize(comm.device)
     steady_ms = (time.perf_counter() - t_steady) * 1e3 / n_steady if t_steady is not None and n_steady else None
     ck.commit()
-    # parameter checksum over every table (identical on all ranks)
-    sums = torch.tensor([float(t.shard_state()[1][next(iter(t.shard_state()[1]))].double().sum())
-                         for t in tables.values()], dtype=torch.float64, device=comm.device)
+    # parameter checksum over every table (identical on all ranks): the parameter values only
+    # (hash tables also export their keys, which are not parameters)
+    def _param_sum(t):
+        arrays = t.shard_state()[1]
+        a = arrays.get("params", arrays.get("master", arrays.get("rows")))
+        if a is None:
+            a = next(iter(arrays.values()))
+        return float(a.double().sum())
+
+    sums = torch.tensor([_param_sum(t) for t in tables.values()], dtype=torch.float64, device=comm.device)
     comm.all_reduce_(sums)
     if comm.device.type == "cuda":
         torch.cuda.synchronize(comm.device)

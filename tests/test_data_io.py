@@ -108,5 +108,6 @@ def test_train_driver_lr_map_storage_matches_vector():
         r = subprocess.run([sys.executable, "-m", "minips_amd.train", "--model", "lr", "--small=1", "--steps", "20",
                             "--kStorageType", st], cwd=root, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
-        res[st] = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["losses"]
-    assert res["Map"] == res["Vector"], res
+        out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        res[st] = (out["losses"], out["checksum"])
+    assert res["Map"] == res["Vector"], res  # same training and the same parameter sum
