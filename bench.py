@@ -15,17 +15,10 @@ line; `value` is the whole-job throughput and the time is the max over ranks.
 from __future__ import annotations
 
 import argparse
-import collections
 import json
 import os
 import sys
 import time
-
-# One HW queue per HIP stream up to 8 (HIP's default is 4): a rank drives ~9 streams (compute,
-# planning, weight-gradient side stream, two clock lanes, and the RCCL streams of four process
-# groups); streams sharing a HW queue serialise behind each other's event waits, which with
-# collectives in flight can stall ranks on one another. Set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import torch
 import torch.distributed as dist
@@ -43,6 +36,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16384, help="per-GPU batch (weak scaling)")
     ap.add_argument("--consistency", default="bsp", choices=["bsp", "ssp", "asp"])
     ap.add_argument("--staleness", type=int, default=0)
+    ap.add_argument("--test-cards", default="", help=argparse.SUPPRESS)
     ap.add_argument("--profile-steps", type=int, default=0, help="after the timed run: host issue time per step and a cProfile of N more steps (stderr)")
     args = ap.parse_args()
 
@@ -55,53 +49,28 @@ def main():
     if n != args.gpus and comm.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {n}", file=sys.stderr)
     dev = comm.device
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
     cfg = WideDeepConfig(consistency=args.consistency, staleness=args.staleness)
+    if args.test_cards:  # CPU/gloo plumbing tests only: a small table, NOT the benchmark config
+        cfg.cards = [int(c) for c in args.test_cards.split(",")]
     model = WideDeep(cfg, comm)
     data = CriteoSynth(args.batch, cards=cfg.cards, device=dev, seed=1000 + comm.rank)
 
-    # The next batch is generated one step ahead, like a data loader prefetching, and ON the
-    # planning stream, so generation and its key routing (dedupe + count all-to-all) both run
-    # beside the current step (lookahead; no table state is read). The compute stream waits for
-    # a batch's event before using it.
-    ps = comm.plan_stream()
-    # the step runs on a high-priority stream (the planning stream keeps normal priority)
+    # the step runs on its own stream; batches are generated (and their keys routed) on the
+    # planning stream, LOOKAHEAD steps ahead (minips_amd/models/feeder.py)
+    from minips_amd.models.feeder import LookaheadFeeder
     from minips_amd.models.layers import compute_priority
 
-    main_stream = torch.cuda.Stream(device=dev, priority=compute_priority()) if dev.type == "cuda" \
-        else torch.cuda.current_stream(dev)
     if dev.type == "cuda":
+        main_stream = torch.cuda.Stream(device=dev, priority=compute_priority())
         main_stream.wait_stream(torch.cuda.default_stream(dev))  # model init ran on the default stream
-    torch.cuda.set_stream(main_stream)
-
-    def produce():
-        with torch.cuda.stream(ps):
-            b = data.next()
-            ev = torch.cuda.Event()
-            ev.record(ps)
-        for t in b:
-            t.record_stream(main_stream)
-        return b, ev
-
-    # Batches (and their key plans) run LOOKAHEAD steps ahead: the planning stream works on batch
-    # n+LOOKAHEAD while step n computes, so a plan is long finished when its step starts even
-    # though the host issues only about one step ahead of the GPU. Measured neutral on one MI355X
-    # (depth 1/2/3: 0.522-0.530 ms/step, tools/gpu_lookahead.sh), so one rank keeps depth 1. With
-    # several ranks depth 2 is the default: the one host wait of a step (a plan's all-to-all
-    # split sizes, SparseTable.advance_plan) then lands on counts issued a whole step earlier.
-    lookahead = max(1, int(os.environ.get("MINIPS_LOOKAHEAD", "2" if n > 1 else "1")))
-    queue = collections.deque(produce() for _ in range(lookahead))
-    for (_, k, _), _ev in list(queue)[1:]:
-        model.prefetch(k, keys_on_plan_stream=True)
-
-    def step():
-        (dense, keys, labels), ev = queue.popleft()
-        main_stream.wait_event(ev)
-
-        def next_keys():  # called by train_step where it issues the look-ahead planning
-            queue.append(produce())
-            return queue[-1][0][1]
-
-        return model.train_step(dense, keys, labels, next_keys=next_keys, next_on_plan_stream=True)
+        torch.cuda.set_stream(main_stream)
+    feeder = LookaheadFeeder(model, data, comm)
+    step = feeder.step
 
     loss0 = None
     for i in range(args.warmup):
@@ -109,16 +78,16 @@ def main():
         if i == 0:
             loss0 = float(l.item()) / args.batch
     model.drain()
-    torch.cuda.synchronize(dev)
+    sync()
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         l = step()
     model.drain()
-    torch.cuda.synchronize(dev)
+    sync()
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if n > 1:
@@ -127,6 +96,12 @@ def main():
     loss_last = float(l.item()) / args.batch
     samples = args.batch * n * args.steps
     value = samples / elapsed
+    if n == 1:
+        # one rank owns every shard: Get/Add/Clock are local gathers/applies, no collective runs
+        parallelism = f"ps-dp1 ({args.consistency}; single rank: local shards, no collectives)"
+    else:
+        parallelism = (f"ps-dp{n} ({args.consistency}" + (f" s={args.staleness}" if args.consistency != "bsp" else "")
+                       + f" over {comm.backend}: a2a sparse rows, RS/AG dense)")
     if comm.rank == 0:
         out = {
             "metric": METRIC,
@@ -142,14 +117,16 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (Criteo-Kaggle cardinalities, Zipf-like ids, 13 dense N(0,1)); random-init weights",
             "config": {
-                "model": "Wide&Deep: 26 sparse (33.76M rows, emb 32 + wide 1, row-wise Adagrad) + 13 dense; "
-                         "deep MLP 848-1024-512-256-1 (Adam)",
+                "model": ("PLUMBING TEST (small tables, not the benchmark) " if args.test_cards else "")
+                + "Wide&Deep: 26 sparse (33.76M rows, emb 32 + wide 1, row-wise Adagrad) + 13 dense; "
+                "deep MLP 848-1024-512-256-1 (Adam)",
                 "global_batch": args.batch * n,
                 "seq_len": None,
-                "parallelism": f"ps-dp{n} (BSP: a2a sparse rows, RS/AG dense)" if args.consistency == "bsp"
-                else f"ps-dp{n} ({args.consistency} s={args.staleness})",
+                "parallelism": parallelism,
                 "per_gpu_batch": args.batch,
                 "consistency": args.consistency,
+                "world_size": comm.world,
+                "backend": comm.backend,
             },
             "loss_first": round(loss0, 5) if loss0 is not None else None,
             "loss_last": round(loss_last, 5),
@@ -169,7 +146,7 @@ def main():
             pr.disable()
             issue.append(time.perf_counter() - a)
         model.drain()
-        torch.cuda.synchronize(dev)
+        sync()
         wall = (time.perf_counter() - t1) / args.profile_steps
         issue.sort()
         print(f"[profile] wall {wall * 1e3:.3f} ms/step (cProfile on), host issue median "

@@ -53,7 +53,7 @@ class GPT2Config:
 
 class GPT2:
     def __init__(self, cfg: GPT2Config, comm: Comm):
-        assert cfg.d % cfg.n_head == 0 and (cfg.d // cfg.n_head) % 8 == 0
+        assert cfg.d == 64 * cfg.n_head, "the attention kernels are specialised for head dim 64"
         self.cfg, self.comm = cfg, comm
         d = cfg.d
         L = ParamLayout()

@@ -6,9 +6,30 @@ The PS message patterns map onto collectives:
   C1/C3 dense Get/Add   -> reduce-scatter(grads) / all-gather(params) of equal shards
   C6    Barrier         -> 1-element all-reduce on the group
 With one rank every collective degenerates to a local copy (no RCCL launch at all).
+
+Ordering contract (why the data plane cannot deadlock, whatever the HW-queue count)
+-----------------------------------------------------------------------------------
+The reference keeps one FIFO sender per process (comm/sender.cpp:7-30 feeding
+comm/mailbox.cpp:231-308), so a worker's messages leave in program order. The GPU data plane
+keeps the same contract with ONE communicator per rank:
+
+1. Every collective of a rank goes through this Comm's single process group, whichever HIP
+   stream issues it (compute, planning, a table's clock stream). RCCL runs a communicator's
+   ops on one internal stream in issue order, so the n-th collective of every rank is the
+   same op (same kind, dtype and row width; all-to-all-v splits agree pairwise).
+2. Every rank issues the same program: the tables' issue points (plan, get, clock, advance)
+   are identical on all ranks and never depend on timing or on a non-blocking query.
+3. A host wait (an event of the count exchange) and a stream wait (wait_event) only target
+   work issued EARLIER in that rank's program.
+By induction over the issue order, collective n completes on every rank once collectives
+< n have: nothing it waits for was issued after it, on any rank. Streams multiplexed onto
+fewer hardware queues (GPU_MAX_HW_QUEUES, 4 by default) only delay, never reorder, packets
+issued earlier, so the argument survives queue sharing. ``trace`` records the issue order;
+tests/test_comm_schedule.py checks that 4- and 8-rank runs issue identical sequences.
 """
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 
@@ -28,7 +49,8 @@ class CommStats:
 
 
 class Comm:
-    """Rank/world/device bookkeeping plus the collectives used by the tables."""
+    """Rank/world/device bookkeeping plus the collectives used by the tables (one ordered
+    communicator per rank: see the module docstring)."""
 
     def __init__(self, group=None, device: torch.device | None = None):
         self.initialized = dist.is_available() and dist.is_initialized()
@@ -40,27 +62,14 @@ class Comm:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
         self.device = device
         self.stats = CommStats()
-        self._lanes: dict[str, Comm] = {}
         self._plan_stream = None
+        # issue-order record of the collectives [(op, dtype, shape-invariant size)], enabled by
+        # MINIPS_COMM_TRACE=1 or by assigning a list (tests)
+        self.trace: list | None = [] if os.environ.get("MINIPS_COMM_TRACE") == "1" else None
 
-    def lane(self, name: str) -> "Comm":
-        """A named extra communicator over the same ranks, for collectives issued on their own HIP
-        stream (key planning, sparse push, dense clock): ops of ONE communicator are serialised
-        in issue order, so work that must overlap needs separate communicators, which progress
-        independently. Creating one is collective (first call on every rank, in the same order
-        -- the tables do it in their constructors)."""
-        if self.world == 1:
-            return self
-        if name not in self._lanes:
-            ranks = list(range(self.world)) if self.group is None else dist.get_process_group_ranks(self.group)
-            c = Comm(group=dist.new_group(ranks), device=self.device)
-            c.stats = self.stats  # one byte account per rank
-            self._lanes[name] = c
-        return self._lanes[name]
-
-    def background(self) -> "Comm":
-        """The side-stream communicator of SSP/ASP clock work (see lane())."""
-        return self.lane("bg")
+    def _record(self, op: str, t: torch.Tensor | None = None, size=None):
+        if self.trace is not None:
+            self.trace.append((op, str(t.dtype).replace("torch.", "") if t is not None else "", size))
 
     def plan_stream(self):
         """The HIP stream on which lookahead key planning runs (one per rank, shared by tables)."""
@@ -99,6 +108,8 @@ class Comm:
             self._back(out[: sum(recv_splits)], o)
             return out
         self.stats.calls += 1
+        if self.world > 1:
+            self._record("a2av_p2p" if p2p else "a2av", inp, tuple(inp.shape[1:]))
         if self.world == 1:
             n = send_splits[0]
             if n:
@@ -135,7 +146,9 @@ class Comm:
         """Device-side all-to-all of per-destination counts (no host sync)."""
         if self.world == 1:
             recv.copy_(counts)
-        elif self._staged(recv, counts):
+            return recv
+        self._record("a2a_counts", counts, counts.numel())
+        if self._staged(recv, counts):
             r = torch.empty(recv.shape, dtype=recv.dtype)
             dist.all_to_all_single(r, counts.cpu(), group=self.group)
             recv.copy_(r)
@@ -160,6 +173,8 @@ class Comm:
             out_shard.copy_(o)
             return out_shard
         self.stats.calls += 1
+        if self.world > 1:
+            self._record("reduce_scatter", inp, inp.numel())
         if self.world == 1:
             out_shard.copy_(inp)
             return out_shard
@@ -174,6 +189,8 @@ class Comm:
             self._back(out_full, o)
             return out_full
         self.stats.calls += 1
+        if self.world > 1:
+            self._record("all_gather", out_full, out_full.numel())
         if self.world == 1:
             if out_full.data_ptr() != shard.data_ptr():
                 out_full.copy_(shard)
@@ -188,6 +205,7 @@ class Comm:
     def all_reduce_(self, t: torch.Tensor, op=None):
         if self.world == 1:
             return t
+        self._record("all_reduce", t, t.numel())
         if self._staged(t):
             h = t.cpu()
             dist.all_reduce(h, op=op or dist.ReduceOp.SUM, group=self.group)
@@ -209,7 +227,12 @@ def init_distributed(backend: str | None = None) -> Comm:
     """Initialise torch.distributed from the torchrun env (RANK/WORLD_SIZE/MASTER_*).
 
     One process per GPU: the local rank selects the device; backend "nccl" is RCCL on ROCm.
+    A collective that does not complete within MINIPS_PG_TIMEOUT seconds (default 60) aborts
+    the communicator and ends the process with an error (RCCL async error handling), so a
+    stuck peer turns into a non-zero exit the elastic supervisor restarts from, not a hang.
     """
+    timeout = datetime.timedelta(seconds=float(os.environ.get("MINIPS_PG_TIMEOUT", "60")))
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -223,9 +246,9 @@ def init_distributed(backend: str | None = None) -> Comm:
             local = 0
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            dist.init_process_group(backend, device_id=torch.device("cuda", local), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
             if torch.cuda.is_available():
                 torch.cuda.set_device(local)
     elif torch.cuda.is_available():

@@ -49,7 +49,7 @@ class _Pipeline:
     """Tracks in-flight Clock work issued on a side HIP stream.
 
     On the GPU every consistency model runs the Clock's communication + apply on the table's
-    own stream (and its own communicator lane) and gates READS instead of the issue: a Get at
+    own stream (its collectives join the rank's single ordered communicator, ps/comm.py) and gates READS instead of the issue: a Get at
     clock c waits only for the update of clock c - s - 1. BSP is s = 0 (the Get waits for the
     previous Clock -- the reference rule that Gets after a Clock see the new values), but the
     Clock itself now overlaps with whatever the worker does before its next Get (the rest of
@@ -162,8 +162,6 @@ class DenseTable:
         # captured in a HIP graph replays with the right bias correction
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.pipe = _Pipeline(comm, consistency, staleness, kind="dense")
-        # collective: this table's clock communicator is created up front, in constructor order
-        self.lane = comm.lane(f"dense{table_id}") if self.pipe.async_ else comm
         self._pending = False
         # async clocks: a ring of staleness+2 gradient buffers, so the side stream reduces clock
         # t's gradients while the compute stream already writes clock t+1's.
@@ -204,7 +202,7 @@ class DenseTable:
         pending = self._pending
         self._pending = False
 
-        comm = self.lane
+        comm = self.comm
 
         def work():
             self.step_dev.add_(1)  # device twin of self.step (one per clock)
@@ -390,10 +388,6 @@ class SparseTable:
     def _init_comm(self, consistency, staleness, p2p):
         comm = self.comm
         self.pipe = _Pipeline(comm, consistency, staleness, kind="sparse")
-        # collective, in constructor order on every rank: the push lane (side-stream clock work)
-        # and the planning lane (lookahead dedupe + count exchange)
-        self.lane = comm.lane(f"sparse{self.table_id}") if self.pipe.async_ else comm
-        self.plan_lane = comm.lane("plan") if comm.device.type == "cuda" else comm
         # SSP/ASP move rows with point-to-point send/recv by default, BSP with all-to-all-v
         self.p2p = (consistency != "bsp") if p2p is None else p2p
         self._pending: list = []
@@ -442,7 +436,7 @@ class SparseTable:
         pp.host = pp.event = None
         if self.comm.world > 1:
             recv = torch.empty_like(pp.counts)
-            self.plan_lane.all_to_all_counts(recv, pp.counts)
+            self.comm.all_to_all_counts(recv, pp.counts)
             both = torch.stack([pp.counts, recv])
             if both.is_cuda:
                 pp.host = torch.empty(both.shape, dtype=both.dtype, pin_memory=True)
@@ -459,9 +453,12 @@ class SparseTable:
         get(plan=...). Planning reads no table state, so issuing it early changes no
         consistency semantics. ``keys_on_plan_stream``: the keys were produced on the planning
         stream itself (a data producer running there), so planning need not wait for the
-        compute stream at all."""
-        if self.comm.device.type != "cuda" or self._exact_counts:
+        compute stream at all. On the CPU the same two halves run at the same issue points
+        (inline), so a gloo run issues exactly the collective sequence of an RCCL run."""
+        if self._exact_counts:
             return self.plan(keys, csr)
+        if self.comm.device.type != "cuda":
+            return self._start_plan(keys, csr)
         ps = self.comm.plan_stream()
         cur = torch.cuda.current_stream(self.comm.device)
         if not keys_on_plan_stream:
@@ -476,9 +473,9 @@ class SparseTable:
             pp.event.record(ps)
         return pp
 
-    def _finish_plan(self, pp: _PendingPlan, comm: Comm | None = None) -> SparsePlan:
+    def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
         dev = self.comm.device
-        comm = comm or self.comm
+        comm = self.comm
         n = pp.flat.numel()
         if pp.event is not None:
             torch.cuda.current_stream(dev).wait_event(pp.event)
@@ -508,14 +505,16 @@ class SparseTable:
     def advance_plan(self, pending):
         """Second half of lookahead planning, called once the current step is issued: wait (host)
         for the pending plan's counts, then issue the all-to-all of its keys and the owner-side
-        dedupe on the planning stream / lane, so that only the row gather and the row exchange
+        dedupe on the planning stream, so that only the row gather and the row exchange
         remain on the critical path of the step that uses the plan."""
-        if not isinstance(pending, _PendingPlan) or self.comm.world == 1 or self.comm.device.type != "cuda":
+        if not isinstance(pending, _PendingPlan) or self.comm.world == 1:
             return pending
+        if self.comm.device.type != "cuda":
+            return self._finish_plan(pending)
         ps = self.comm.plan_stream()
         cur = torch.cuda.current_stream(self.comm.device)
         with torch.cuda.stream(ps):
-            plan = self._finish_plan(pending, comm=self.plan_lane)
+            plan = self._finish_plan(pending)
             ev = torch.cuda.Event()
             ev.record(ps)
         for t in (plan.recv_keys, plan.own_uniq, plan.own_inv, plan.own_U_dev):
@@ -559,7 +558,7 @@ class SparseTable:
         """Reference-style Add(keys, vals) (duplicates are summed)."""
         plan = self.plan(keys)
         g = torch.zeros(max(plan.cap, 1), self.width, dtype=torch.float32, device=self.comm.device)
-        ops.scatter_add_rows(vals.reshape(keys.numel(), -1).to(torch.float32).contiguous(), plan.inv, g)
+        ops.scatter_add_rows(vals.reshape(keys.numel(), self.width).to(torch.float32).contiguous(), plan.inv, g)
         self.add(plan, g)
 
     def clock(self):
@@ -584,7 +583,7 @@ class SparseTable:
             send = grad_rows[: plan.U]
             if send.dtype != self.push_dtype:
                 send = send.to(self.push_dtype)
-            self.lane.all_to_all_v(recv, send, plan.recv, plan.send, p2p=self.p2p)
+            self.comm.all_to_all_v(recv, send, plan.recv, plan.send, p2p=self.p2p)
             if M == 0:
                 return
             n = plan.extra.get("own_U", M)

@@ -20,7 +20,6 @@ import os
 import sys
 import time
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")  # see bench.py: one HW queue per HIP stream of a rank
 
 import torch
 import torch.distributed as dist

@@ -1,7 +1,7 @@
 """Multi-rank tests of the GPU data plane on ONE MI355X: two ranks share cuda:0 and talk over gloo
 (the Comm stages GPU tensors through host memory, since RCCL refuses two ranks on one device).
 This runs the real world>1 GPU code paths -- lookahead key planning on the planning stream,
-BSP clocks overlapped on per-table side streams with their own communicator lanes, device-side
+BSP clocks overlapped on per-table side streams (one ordered communicator per rank), device-side
 counts -- which the 8-GPU driver bench relies on."""
 import os
 
@@ -100,7 +100,7 @@ def test_widedeep_overlap_matches_sync():
 
 def test_bench_two_ranks_end_to_end():
     """bench.py under torchrun with 2 ranks (gloo staging on one card): the driver's multi-GPU
-    control flow -- lanes, lookahead planning, barriers, max-over-ranks timing, one JSON line."""
+    control flow -- lookahead planning, barriers, max-over-ranks timing, one JSON line."""
     import json
     import subprocess
     import sys

@@ -31,13 +31,21 @@ def run_world(fn, world=2):
     for p in procs:
         p.start()
     out = {}
-    for _ in range(world):
-        r, v = q.get(timeout=240)
-        out[r] = v
-    for p in procs:
-        p.join(timeout=60)
-    for r, v in out.items():
-        assert not (isinstance(v, str) and v.startswith("ERROR")), v
+    try:
+        for _ in range(world):
+            r, v = q.get(timeout=240)
+            out[r] = v
+            if isinstance(v, str) and v.startswith("ERROR"):
+                break  # peers may be blocked in a collective with the failed rank
+    finally:
+        for p in procs:
+            p.join(timeout=60 if len(out) == world else 1)
+            if p.is_alive():
+                p.kill()
+    errs = [v for v in out.values() if isinstance(v, str) and v.startswith("ERROR")]
+    # a failing rank closes its connections: show the root cause, not a peer's echo of it
+    errs.sort(key=lambda e: "Connection closed" in e or "Connection reset" in e)
+    assert not errs, errs[0]
     return out
 
 

@@ -18,12 +18,6 @@ import os
 import sys
 import time
 
-# One HW queue per HIP stream up to 8 (HIP's default is 4): a rank drives ~9 streams (compute,
-# planning, weight-gradient side stream, two clock lanes, and the RCCL streams of four process
-# groups); streams sharing a HW queue serialise behind each other's event waits, which with
-# collectives in flight can stall ranks on one another. Set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 import torch
 import torch.distributed as dist
 
