@@ -478,16 +478,23 @@ void kmeans_argmin(const at::Tensor& S, const at::Tensor& cn, const at::Tensor& 
                           ptr<int32_t>(assign), dp, stream_of(S));
 }
 
-void criteo_synth(int64_t seed, int64_t step, const at::Tensor& cards, const at::Tensor& offsets, const at::Tensor& w,
-                  at::Tensor& dense, at::Tensor& keys, at::Tensor& labels) {
+void criteo_synth(int64_t seed, int64_t step, const c10::optional<at::Tensor>& step_dev, const at::Tensor& cards,
+                  const at::Tensor& offsets, const at::Tensor& w, at::Tensor& dense, at::Tensor& keys,
+                  at::Tensor& labels) {
   for (const at::Tensor* t : {&cards, &offsets, &w, (const at::Tensor*)&dense, (const at::Tensor*)&keys, (const at::Tensor*)&labels}) check_gpu(*t, "criteo_synth arg");
   check_dtype(keys, at::kLong, "keys");
   check_dtype(cards, at::kLong, "cards");
   const int64_t B = labels.numel();
   const int F = (int)cards.numel();
   TORCH_CHECK(keys.numel() == B * F && dense.size(0) == B && w.numel() == dense.size(1), "criteo_synth shapes");
+  const int64_t* sd = nullptr;
+  if (step_dev && step_dev->defined()) {
+    check_gpu(*step_dev, "step_dev");
+    check_dtype(*step_dev, at::kLong, "step_dev");
+    sd = ptr<int64_t>(*step_dev);
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
-  minips_k::criteo_synth((uint64_t)seed, (uint64_t)step, B, F, ptr<int64_t>(cards), ptr<int64_t>(offsets),
+  minips_k::criteo_synth((uint64_t)seed, (uint64_t)step, sd, B, F, ptr<int64_t>(cards), ptr<int64_t>(offsets),
                          (int)dense.size(1), ptr<float>(w), ptr<float>(dense), ptr<int64_t>(keys), ptr<float>(labels),
                          stream_of(keys));
 }

@@ -29,9 +29,13 @@ __device__ __forceinline__ int64_t raw_id(uint64_t sb, int f, int64_t card) {
 }
 
 // Index space B*F (one key each) + B (dense features + label): no serial per-sample loop.
-__global__ void criteo_synth_kernel(uint64_t seed, uint64_t step, int64_t B, int F, const int64_t* __restrict__ cards,
+__global__ void criteo_synth_kernel(uint64_t seed, uint64_t step, const int64_t* __restrict__ step_dev, int64_t B, int F,
+                                    const int64_t* __restrict__ cards,
                                     const int64_t* __restrict__ offsets, int n_dense, const float* __restrict__ w,
                                     float* __restrict__ dense, int64_t* __restrict__ keys, float* __restrict__ labels) {
+  // step_dev: the step counter lives on the device (advanced by the caller's stream), so a step
+  // captured in a HIP graph draws a new batch on every replay
+  if (step_dev) step += (uint64_t)*step_dev;
   const uint64_t base = splitmix(seed * 0x632be59bd9b4e019ULL + step);
   const int64_t nk = B * F;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nk + B; e += (int64_t)gridDim.x * blockDim.x) {
@@ -72,11 +76,13 @@ __global__ void criteo_synth_kernel(uint64_t seed, uint64_t step, int64_t B, int
   }
 }
 
-void criteo_synth(uint64_t seed, uint64_t step, int64_t B, int F, const int64_t* cards, const int64_t* offsets,
-                  int n_dense, const float* w, float* dense, int64_t* keys, float* labels, hipStream_t s) {
+void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t B, int F, const int64_t* cards,
+                  const int64_t* offsets, int n_dense, const float* w, float* dense, int64_t* keys, float* labels,
+                  hipStream_t s) {
   if (B <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(criteo_synth_kernel, grid_for(B * (F + 1), block, 4096), block, 0, s, seed, step, B, F, cards, offsets, n_dense, w,
+  hipLaunchKernelGGL(criteo_synth_kernel, grid_for(B * (F + 1), block, 4096), block, 0, s, seed, step, step_dev, B, F, cards, offsets,
+                     n_dense, w,
                      dense, keys, labels);
   MINIPS_HIP_CHECK(hipGetLastError());
 }

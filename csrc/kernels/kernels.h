@@ -188,7 +188,8 @@ void dlrm_interact_bwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx,
                        float* dV, bf16_t* d_dense, hipStream_t s);
 
 // ------------------------------------------------------------------ synthetic data (data.hip)
-void criteo_synth(uint64_t seed, uint64_t step, int64_t B, int F, const int64_t* cards, const int64_t* offsets,
-                  int n_dense, const float* w, float* dense, int64_t* keys, float* labels, hipStream_t s);
+void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t B, int F, const int64_t* cards,
+                  const int64_t* offsets, int n_dense, const float* w, float* dense, int64_t* keys, float* labels,
+                  hipStream_t s);
 
 }  // namespace minips_k

@@ -46,14 +46,17 @@ class CriteoSynth:
             # one fused gfx950 launch (csrc/kernels/data.hip) instead of ~15 torch kernels
             from .._native import kernels
 
-            self._step = getattr(self, "_step", 0) + 1
             if not hasattr(self, "_seed"):
                 self._seed = int(torch.randint(0, 2**62, (1,), generator=self.gen, device=self.device).item())
+                # the step counter lives on the device: a step captured in a HIP graph draws a
+                # fresh batch on every replay
+                self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._step_dev.add_(1)
             dense = torch.empty(B, self.n_dense, device=self.device)
             keys = torch.empty(B, F, dtype=torch.int64, device=self.device)
             labels = torch.empty(B, device=self.device)
-            kernels().criteo_synth(self._seed, self._step, self.card_t, self.offsets, self.w_dense, dense, keys,
-                                   labels)
+            kernels().criteo_synth(self._seed, 0, self._step_dev, self.card_t, self.offsets, self.w_dense, dense,
+                                   keys, labels)
             return dense, keys, labels
         u = torch.rand(B, F, generator=self.gen, device=self.device, dtype=torch.float64)
         raw = torch.floor(torch.exp(u * self.log_card) - 1.0).to(torch.int64)
