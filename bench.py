@@ -73,7 +73,7 @@ def main():
     step = feeder.step
     # one rank: after eager warm-up steps the whole step is captured into one HIP graph
     # (GraphedFeeder) and the remaining warm-up and all timed steps are graph replays
-    use_graph = dev.type == "cuda" and n == 1 and args.consistency == "bsp" and os.environ.get("MINIPS_GRAPH", "1") != "0"
+    use_graph = dev.type == "cuda" and n == 1 and args.consistency == "bsp" and os.environ.get("MINIPS_GRAPH", "0") == "1"
     eager_warm = max(1, args.warmup - 1) if use_graph else args.warmup
 
     loss0 = None

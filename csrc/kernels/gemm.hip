@@ -175,6 +175,166 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
   }
 }
 
+// LDS-staged epilogue of one wave's (16 MR) x 64 accumulator block at rows mb.., cols nb.. (v2/v3).
+// The accumulator fragments hold 4 rows x 1 column per lane (16 lanes per row), so storing them
+// directly writes 2-byte (bf16) / 4-byte values in 32-64 B pieces: ~64 store instructions per
+// wave per 64x64 block and partial cache lines. Instead each 16-row slice goes through a private
+// per-wave LDS scratch [16][68] fp32 (row pitch 272 B: the ds_write_b32 fragment pattern is
+// conflict-free), is read back row-contiguous and leaves as whole 128-B (bf16) / 256-B (fp32)
+// row segments: 16-byte stores (8 bf16 or 4 fp32 per lane), 16-byte mask/aux accesses, one
+// 256-B atomic wave-instruction per row for the split-K fp32 epilogue. Scalar tail path when a
+// row segment is not 16-byte aligned or runs past N. `scr` = this wave's 16*68 floats of LDS,
+// free once every wave has left the main loop (its final barrier).
+constexpr int kScrPitch = 68;
+constexpr int kScrFloats = 16 * kScrPitch;
+
+template <int EPI>
+__device__ __forceinline__ float epi_apply(float v, float bias, float m, bf16_t* aux_out) {
+  if (EPI == kEpiBiasReluBf16) return fmaxf(v + bias, 0.f);
+  if (EPI == kEpiBiasBf16) return v + bias;
+  if (EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16) {
+    const float x = v + bias;
+    if (EPI == kEpiBiasGeluAuxBf16) *aux_out = f2bf(x);
+    const float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
+    return 0.5f * x * (1.f + t);
+  }
+  if (EPI == kEpiGeluGradBf16) {
+    const float k = 0.7978845608f, c3 = 0.044715f;
+    const float t = tanhf(k * (m + c3 * m * m * m));
+    const float gp = 0.5f * (1.f + t) + 0.5f * m * (1.f - t * t) * k * (1.f + 3.f * c3 * m * m);
+    return v * gp;
+  }
+  if (EPI == kEpiReluMaskBf16) return m > 0.f ? v : 0.f;
+  return v;  // kEpiStoreBf16 / kEpiStoreF32
+}
+
+template <int EPI, int MR>
+__device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiArgs& ep, int M, int N, int mb, int nb,
+                                             int lane, float* __restrict__ scr) {
+  constexpr bool F32OUT = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
+  constexpr bool HAS_BIAS = EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 ||
+                            EPI == kEpiBiasGeluAuxBf16;
+  constexpr bool READ_MASK = EPI == kEpiReluMaskBf16 || EPI == kEpiGeluGradBf16;
+  const int col_l = lane & 15, row_q = (lane >> 4) * 4;
+  // vector paths need 16-byte aligned row segments
+  const bool c_vec = ((ep.ldc & (F32OUT ? 3 : 7)) == 0) && ((reinterpret_cast<uintptr_t>(ep.C) & 15) == 0);
+  const bool m_vec = ((ep.ldmask & 7) == 0) && ((reinterpret_cast<uintptr_t>(ep.mask) & 15) == 0);
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scr[(row_q + r) * kScrPitch + j * 16 + col_l] = acc[i][j][r] * ep.alpha;
+    __builtin_amdgcn_wave_barrier();
+    const int row0 = mb + i * 16;
+    if (EPI == kEpiAtomicF32) {
+      // one row per wave-instruction: 64 lanes x 4 B = 256 contiguous bytes
+      const int col = nb + lane;
+#pragma unroll 4
+      for (int rr = 0; rr < 16; ++rr) {
+        const int row = row0 + rr;
+        if (row < M && col < N) atomicAdd(((float*)ep.C) + (int64_t)row * ep.ldc + col, scr[rr * kScrPitch + lane]);
+      }
+    } else if (F32OUT) {
+#pragma unroll
+      for (int ro = 0; ro < 4; ++ro) {
+        const int rr = ro * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+        const int row = row0 + rr, col = nb + c4;
+        if (row >= M) continue;
+        const float4 v = *reinterpret_cast<const float4*>(scr + rr * kScrPitch + c4);
+        float* dst = ((float*)ep.C) + (int64_t)row * ep.ldc + col;
+        if (c_vec && col + 4 <= N) {
+          *reinterpret_cast<float4*>(dst) = v;
+        } else {
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+          for (int e = 0; e < 4; ++e)
+            if (col + e < N) dst[e] = vv[e];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int ro = 0; ro < 2; ++ro) {
+        const int rr = ro * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+        const int row = row0 + rr, col = nb + c8;
+        const bool row_ok = row < M;
+        const float4 lo = *reinterpret_cast<const float4*>(scr + rr * kScrPitch + c8);
+        const float4 hi = *reinterpret_cast<const float4*>(scr + rr * kScrPitch + c8 + 4);
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const bool full = col + 8 <= N;
+        float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (HAS_BIAS && ep.bias) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bias[e] = (col + e < N) ? bf2f(ep.bias[col + e]) : 0.f;
+        }
+        float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const int64_t moff = (int64_t)row * ep.ldmask + col;
+        if (READ_MASK && row_ok) {
+          if (m_vec && full) {
+            const uint4 mu = *reinterpret_cast<const uint4*>(ep.mask + moff);
+            const uint32_t w[4] = {mu.x, mu.y, mu.z, mu.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              m[2 * e] = __uint_as_float(w[e] << 16);
+              m[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+            }
+          } else {
+            for (int e = 0; e < 8; ++e)
+              if (col + e < N) m[e] = bf2f(ep.mask[moff + e]);
+          }
+        }
+        bf16_t aux[8];
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = epi_apply<EPI>(v[e], bias[e], m[e], &aux[e]);
+        uint32_t pk[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = pack_bf2(o[2 * e], o[2 * e + 1]);
+        if (EPI == kEpiReluMaskBf16 && ep.colsum && row_ok) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            csum[2 * e] += __uint_as_float(pk[e] << 16);
+            csum[2 * e + 1] += __uint_as_float(pk[e] & 0xffff0000u);
+          }
+        }
+        if (!row_ok) continue;
+        bf16_t* dst = ((bf16_t*)ep.C) + (int64_t)row * ep.ldc + col;
+        if (c_vec && full) {
+          *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        } else {
+          for (int e = 0; e < 8; ++e)
+            if (col + e < N) dst[e] = (bf16_t)((e & 1) ? (pk[e >> 1] >> 16) : (pk[e >> 1] & 0xffffu));
+        }
+        if (EPI == kEpiBiasGeluAuxBf16) {
+          bf16_t* adst = const_cast<bf16_t*>(ep.mask) + moff;
+          if (m_vec && full) {
+            uint32_t a[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[e] = (uint32_t)aux[2 * e] | ((uint32_t)aux[2 * e + 1] << 16);
+            *reinterpret_cast<uint4*>(adst) = make_uint4(a[0], a[1], a[2], a[3]);
+          } else {
+            for (int e = 0; e < 8; ++e)
+              if (col + e < N) adst[e] = aux[e];
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // this slice's reads retire before the next slice's writes
+  }
+  if (EPI == kEpiReluMaskBf16 && ep.colsum) {
+    // lanes with equal (lane & 7) hold the same 8 columns: fold rows over lane bits 3..5
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float c = csum[e];
+      c += __shfl_xor(c, 8, 64);
+      c += __shfl_xor(c, 16, 64);
+      c += __shfl_xor(c, 32, 64);
+      const int col = nb + (lane & 7) * 8 + e;
+      if (lane < 8 && col < N) atomicAdd(ep.colsum + col, c);
+    }
+  }
+}
+
 // One wave's 64x64 accumulator block (rows m0 + 64*wm.., cols n0 + 64*wn..).
 template <int EPI>
 __device__ __forceinline__ void epilogue(const v4f (&acc)[4][4], const EpiArgs& ep, int M, int N, int m0, int n0,
@@ -287,6 +447,10 @@ constexpr uint32_t kOobOffset = 0x80000000u;
 #define MINIPS_GEMM_SETPRIO 0  // T5 setprio pair: measured -1..-4 % here (tools/gpu_gemm_ab.sh)
 #endif
 constexpr bool kSetPrio = MINIPS_GEMM_SETPRIO != 0;
+#ifndef MINIPS_GEMM_LDS_EPILOGUE
+#define MINIPS_GEMM_LDS_EPILOGUE 1  // staged epilogue (epilogue_lds); 0: direct fragment stores
+#endif
+constexpr bool kLdsEpilogue = MINIPS_GEMM_LDS_EPILOGUE != 0;
 
 __device__ __forceinline__ int swz_k(int k) { return 2 * ((k & 3) | ((((k >> 2) ^ (k >> 3)) & 1) << 2)); }
 
@@ -348,6 +512,7 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
   constexpr int WN = TN / 64, NWAVES = (TM / 64) * (TN / 64);
   constexpr int VM_STAGE = (TM / 8 + TN / 8) / NWAVES;  // DMA instructions per thread per stage
   __shared__ __attribute__((aligned(1024))) bf16_t smem[2][(TM + TN) * BK2];
+  static_assert(sizeof(smem) >= sizeof(float) * NWAVES * kScrFloats, "epilogue scratch must fit the staging LDS");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_n = (N + TN - 1) / TN, tiles_m = (M + TM - 1) / TM;
@@ -418,7 +583,11 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
     __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is refilled
     asm volatile("" ::: "memory");
   }
-  epilogue<EPI>(acc, ep, M, N, m0, n0, wm, wn, lane);
+  if (kLdsEpilogue)
+    epilogue_lds<EPI, 4>(acc, ep, M, N, m0 + wm * 64, n0 + wn * 64, lane,
+                         reinterpret_cast<float*>(&smem[0][0]) + wave * kScrFloats);
+  else
+    epilogue<EPI>(acc, ep, M, N, m0, n0, wm, wn, lane);
 }
 
 // ================================================================ v3: 256x256, 8 waves, phase-split K-step
@@ -442,6 +611,7 @@ __global__ __launch_bounds__(512) void gemm_v3_kernel(const bf16_t* __restrict__
                                                       EpiArgs ep) {
   constexpr bool PERM = A_KM && B_KN;
   __shared__ __attribute__((aligned(1024))) bf16_t smem[2][4 * kV3Half];
+  static_assert(sizeof(smem) >= sizeof(float) * 8 * kScrFloats, "epilogue scratch must fit the staging LDS");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = (N + 255) / 256, tiles_m = (M + 255) / 256;
@@ -553,7 +723,11 @@ __global__ __launch_bounds__(512) void gemm_v3_kernel(const bf16_t* __restrict__
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
-  epilogue_at<EPI, 8>(acc, ep, M, N, m0 + wr * 128, n0 + wc * 64, lane);
+  if (kLdsEpilogue)
+    epilogue_lds<EPI, 8>(acc, ep, M, N, m0 + wr * 128, n0 + wc * 64, lane,
+                         reinterpret_cast<float*>(&smem[0][0]) + wave * kScrFloats);
+  else
+    epilogue_at<EPI, 8>(acc, ep, M, N, m0 + wr * 128, n0 + wc * 64, lane);
 }
 
 static int gemm_impl() {
