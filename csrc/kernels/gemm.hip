@@ -747,12 +747,12 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
   const int64_t b_ext = (int64_t)((B_KN ? K : N) - 1) * ldb + (B_KN ? N : K);
   // measured (tools/bench_gemm.py): v2 wins on forward / dgrad; the split-K wgrad (both operands
   // tr-read) stays on the register-staged BK=32 kernel, which is faster there
-  // wgrad kernel (MINIPS_GEMM_WGRAD): v1 (default; register-staged BK=32, the fastest measured on
-  // the split-K wgrad shapes: tools/sweep_wgrad.py), v2, or v3 (256x256 phase-split tiles, split-K
-  // chosen by ops.linear_wgrad for ~one workgroup per CU)
+  // wgrad kernel (MINIPS_GEMM_WGRAD): v2 (default: LDS-DMA, tr-read operands, staged epilogue), v1
+  // (register-staged BK=32, round-1 default), or v3 (256x256 phase-split tiles, split-K chosen by
+  // ops.linear_wgrad for ~one workgroup per CU)
   static const int wgrad_mode = [] {
     const char* e = std::getenv("MINIPS_GEMM_WGRAD");
-    if (!e) return 1;
+    if (!e) return 2;  // v2 + LDS-staged epilogue measured best in the W&D step (tools/gpu_wgrad_ab2.sh)
     return std::string(e) == "v3" ? 3 : (std::string(e) == "v2" ? 2 : 1);
   }();
   const bool wgrad = A_KM && B_KN;

@@ -117,15 +117,17 @@ def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=
     return gemm(dy, w, out, M, K, N, False, True, epi, mask=mask, colsum=colsum)
 
 
-_WGRAD_MODE = __import__("os").environ.get("MINIPS_GEMM_WGRAD", "v1")
+_WGRAD_MODE = __import__("os").environ.get("MINIPS_GEMM_WGRAD", "v2")
 _WGRAD_BLOCKS = int(__import__("os").environ.get("MINIPS_WGRAD_BLOCKS", "256" if _WGRAD_MODE == "v3" else "512"))
 # Reduction rows per split: 640 is the isolated-kernel optimum (a wgrad on the critical path, e.g.
 # the MLP); a wgrad forked onto a side stream beside the dgrad chain (SideStream, which sets
 # overlap_mode) favours throughput: fewer, longer splits with less slab traffic (W&D step 0.560 ->
 # 0.550 ms at 2048; the MLP step loses 15 % at 2048 when its wgrads are on the critical path).
 _WGRAD_MIN_ROWS = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS", "512" if _WGRAD_MODE == "v3" else "640"))
+# round 2 (LDS-staged epilogue, v2 wgrad): 1024 rows per overlapped split measured best
+# (W&D 0.461 ms vs 0.490 at 2048; tools/gpu_wgrad_ab2.sh)
 _WGRAD_MIN_ROWS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS_OVERLAP",
-                                                           "512" if _WGRAD_MODE == "v3" else "2048"))
+                                                           "512" if _WGRAD_MODE == "v3" else "1024"))
 # Overlapped wgrads with few output tiles (W&D's 256x512 W3 grad: 8 tiles) would get only ~64
 # workgroups at 2048 rows per split; this floor on the block count (0: off) lets them split finer
 # (never below _WGRAD_MIN_ROWS rows per split). Measured worse on one MI355X (W&D 0.528 ->
