@@ -6,6 +6,9 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/extension.h>
 
+#include <cstring>
+#include <tuple>
+
 #include "../kernels/kernels.h"
 
 namespace {
@@ -714,7 +717,85 @@ void dlrm_interact_bwd(const at::Tensor& V, int64_t NV, int64_t D, int64_t dense
                               ptr<float>(dV), ptr<bf16_t>(d_dense), stream_of(V));
 }
 
+// --- one-sided shards over xGMI (minips_amd/ps/onesided.py) -------------------------------------
+// A hipMalloc'd, zero-filled buffer exported for IPC: (uint8 tensor owning it, 64-byte handle).
+std::tuple<at::Tensor, py::bytes> ipc_alloc(int64_t nbytes, int64_t device) {
+  TORCH_CHECK(nbytes > 0, "ipc_alloc: nbytes must be > 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(at::Device(at::kCUDA, (c10::DeviceIndex)device));
+  void* p = nullptr;
+  TORCH_CHECK(hipMalloc(&p, (size_t)nbytes) == hipSuccess, "ipc_alloc: hipMalloc of ", nbytes, " bytes failed");
+  TORCH_CHECK(hipMemset(p, 0, (size_t)nbytes) == hipSuccess, "ipc_alloc: hipMemset failed");
+  hipIpcMemHandle_t h;
+  TORCH_CHECK(hipIpcGetMemHandle(&h, p) == hipSuccess, "ipc_alloc: hipIpcGetMemHandle failed");
+  auto t = torch::from_blob(p, {nbytes}, [](void* q) { (void)hipFree(q); },
+                            at::TensorOptions().dtype(at::kByte).device(at::kCUDA, (c10::DeviceIndex)device));
+  return {t, py::bytes(reinterpret_cast<const char*>(&h), sizeof(h))};
+}
+
+// Maps a peer's exported buffer into this process (peer access enabled lazily); the tensor owns
+// the mapping (closed when it is freed).
+at::Tensor ipc_open(py::bytes handle, int64_t nbytes, int64_t device) {
+  const std::string hs = handle;
+  TORCH_CHECK(hs.size() == sizeof(hipIpcMemHandle_t), "ipc_open: bad handle size ", hs.size());
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, hs.data(), sizeof(h));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(at::Device(at::kCUDA, (c10::DeviceIndex)device));
+  void* p = nullptr;
+  TORCH_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess,
+              "ipc_open: hipIpcOpenMemHandle failed");
+  return torch::from_blob(p, {nbytes}, [](void* q) { (void)hipIpcCloseMemHandle(q); },
+                          at::TensorOptions().dtype(at::kByte).device(at::kCUDA, (c10::DeviceIndex)device));
+}
+
+void check_remote(const at::Tensor& bases, const at::Tensor& bounds, const at::Tensor& keys) {
+  check_gpu(bases, "bases");
+  check_gpu(bounds, "bounds");
+  check_gpu(keys, "keys");
+  check_dtype(bases, at::kLong, "bases");
+  check_dtype(bounds, at::kLong, "bounds");
+  check_dtype(keys, at::kLong, "keys");
+  TORCH_CHECK(bounds.numel() == bases.numel() + 1, "bounds must have P+1 entries");
+}
+
+void remote_gather(const at::Tensor& bases, const at::Tensor& bounds, const at::Tensor& keys,
+                   const c10::optional<at::Tensor>& n_dev, int64_t W, at::Tensor& out) {
+  check_remote(bases, bounds, keys);
+  check_gpu(out, "out");
+  const int64_t n = keys.numel();
+  TORCH_CHECK(out.dim() == 2 && out.size(0) >= n && out.size(1) == W, "out must be [>= n, W]");
+  const bool bf = out.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || out.scalar_type() == at::kFloat, "out must be fp32 or bf16");
+  const int64_t* nd = nullptr;
+  if (n_dev && n_dev->defined()) {
+    check_gpu(*n_dev, "n_dev");
+    check_dtype(*n_dev, at::kLong, "n_dev");
+    nd = ptr<int64_t>(*n_dev);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  minips_k::remote_gather(ptr<int64_t>(bases), ptr<int64_t>(bounds), (int)bases.numel(), ptr<int64_t>(keys), n, nd,
+                          (int)W, out.data_ptr(), bf, stream_of(keys));
+}
+
+void remote_scatter_add(const at::Tensor& bases, const at::Tensor& bounds, const at::Tensor& keys,
+                        const at::Tensor& vals, double scale, const c10::optional<at::Tensor>& n_dev) {
+  check_remote(bases, bounds, keys);
+  check_gpu(vals, "vals");
+  check_dtype(vals, at::kFloat, "vals");
+  const int64_t n = keys.numel();
+  TORCH_CHECK(vals.dim() == 2 && vals.size(0) >= n, "vals must be [>= n, W]");
+  const int64_t* nd = nullptr;
+  if (n_dev && n_dev->defined()) {
+    check_gpu(*n_dev, "n_dev");
+    check_dtype(*n_dev, at::kLong, "n_dev");
+    nd = ptr<int64_t>(*n_dev);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  minips_k::remote_scatter_add(ptr<int64_t>(bases), ptr<int64_t>(bounds), (int)bases.numel(), ptr<int64_t>(keys), n,
+                               nd, ptr<float>(vals), (int)vals.size(1), (float)scale, stream_of(keys));
+}
+
 }  // namespace
+
 
 PYBIND11_MODULE(_kernels, m) {
   m.doc() = "minips_amd gfx950 HIP kernels";
@@ -777,4 +858,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_split3", &kmeans_split3);
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
+  m.def("ipc_alloc", &ipc_alloc);
+  m.def("ipc_open", &ipc_open);
+  m.def("remote_gather", &remote_gather);
+  m.def("remote_scatter_add", &remote_scatter_add);
 }

@@ -349,6 +349,74 @@ PYBIND11_MODULE(_runtime, m) {
       .def("wait", &AsyncShardWriter::Wait, py::call_guard<py::gil_scoped_release>())
       .def("wait_all", &AsyncShardWriter::WaitAll, py::call_guard<py::gil_scoped_release>())
       .def("take_error", &AsyncShardWriter::TakeError);
+  py::class_<ShardFileWriter>(m, "ShardFileWriter")
+      .def(py::init([](const std::string& path, const py::dict& meta, const py::list& arrays) {
+             std::vector<ArrayDesc> desc;
+             for (auto item : arrays) {
+               auto t = item.cast<py::tuple>();
+               ArrayDesc d;
+               d.name = t[0].cast<std::string>();
+               d.dtype = ParseDType(t[1].cast<std::string>());
+               d.rows = t[2].cast<uint64_t>();
+               d.cols = t[3].cast<uint64_t>();
+               desc.push_back(d);
+             }
+             return new ShardFileWriter(path, MetaFromDict(meta), desc);
+           }),
+           py::arg("path"), py::arg("meta"), py::arg("arrays"))
+      .def(
+          "write_rows",
+          [](ShardFileWriter& w, int array, uint64_t row0, uintptr_t src, uint64_t nrows) {
+            py::gil_scoped_release rel;
+            w.WriteRows(array, row0, reinterpret_cast<const void*>(src), nrows);
+          },
+          py::arg("array"), py::arg("row0"), py::arg("src"), py::arg("nrows"))
+      .def("close", &ShardFileWriter::Close, py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "read_shard_header",
+      [](const std::string& path) {
+        ShardHeader h;
+        {
+          py::gil_scoped_release rel;
+          h = ReadShardHeader(path);
+        }
+        py::dict meta;
+        meta["global_rows"] = h.meta.global_rows;
+        meta["base"] = h.meta.base;
+        meta["rows"] = h.meta.rows;
+        meta["cols"] = h.meta.cols;
+        meta["clock"] = h.meta.clock;
+        meta["table_id"] = h.meta.table_id;
+        meta["rank"] = h.meta.rank;
+        meta["world"] = h.meta.world;
+        meta["kind"] = h.meta.kind;
+        py::list arrays;
+        for (const auto& a : h.arrays) arrays.append(py::make_tuple(a.name, DTypeName(a.dtype), a.rows, a.cols, a.offset));
+        return py::make_tuple(meta, arrays);
+      },
+      py::arg("path"));
+  m.def(
+      "read_rows",
+      [](const std::string& path, uint64_t offset, uint64_t row_bytes, uint64_t row0, uint64_t nrows, uintptr_t dst) {
+        py::gil_scoped_release rel;
+        ReadRows(path, offset, row_bytes, row0, nrows, reinterpret_cast<void*>(dst));
+      },
+      py::arg("path"), py::arg("offset"), py::arg("row_bytes"), py::arg("row0"), py::arg("nrows"), py::arg("dst"));
+  m.def(
+      "write_text_params",
+      [](const std::string& path, uintptr_t data, const std::string& dtype, uint64_t rows, uint64_t cols) {
+        ArrayRef a;
+        a.name = "params";
+        a.data = reinterpret_cast<const void*>(data);
+        a.dtype = ParseDType(dtype);
+        a.rows = rows;
+        a.cols = cols;
+        py::gil_scoped_release rel;
+        WriteTextParams(path, a);
+      },
+      py::arg("path"), py::arg("data"), py::arg("dtype"), py::arg("rows"), py::arg("cols"));
+  m.def("shard_bytes_read", &ShardBytesRead);
+  m.def("reset_shard_bytes_read", &ResetShardBytesRead);
   m.def(
       "read_shard",
       [](const std::string& path) {

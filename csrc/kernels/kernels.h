@@ -192,4 +192,11 @@ void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t
                   const int64_t* offsets, int n_dense, const float* w, float* dense, int64_t* keys, float* labels,
                   hipStream_t s);
 
+// ------------------------------------------------------------------ one-sided xGMI path (onesided.hip)
+// bases [P] int64 device pointers of the per-rank fp32 shards [rows_o, W]; bounds [P+1] key ranges
+void remote_gather(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,
+                   const int64_t* n_dev, int W, void* out, bool out_bf16, hipStream_t s);
+void remote_scatter_add(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,
+                        const int64_t* n_dev, const float* vals, int W, float scale, hipStream_t s);
+
 }  // namespace minips_k

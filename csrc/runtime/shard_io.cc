@@ -1,5 +1,11 @@
 #include "shard_io.h"
 
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -12,22 +18,84 @@ namespace minips {
 
 namespace {
 constexpr char kMagic[8] = {'M', 'P', 'S', 'S', 'H', 'R', 'D', '1'};
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;
+constexpr uint64_t kAlign = 4096;
+std::atomic<uint64_t> g_bytes_read{0};
 
-template <typename T>
-void put(std::ofstream& o, const T& v) {
-  o.write(reinterpret_cast<const char*>(&v), sizeof(T));
+uint64_t AlignUp(uint64_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
+
+void PWriteAll(int fd, const void* src, uint64_t n, uint64_t off, const std::string& what) {
+  const char* p = static_cast<const char*>(src);
+  while (n > 0) {
+    const ssize_t w = ::pwrite(fd, p, (size_t)std::min<uint64_t>(n, 1ull << 30), (off_t)off);
+    if (w < 0 && errno == EINTR) continue;
+    MINIPS_CHECK(w > 0, "pwrite failed on " << what << ": " << std::strerror(errno));
+    p += w;
+    off += (uint64_t)w;
+    n -= (uint64_t)w;
+  }
 }
+
+void PReadAll(int fd, void* dst, uint64_t n, uint64_t off, const std::string& what) {
+  char* p = static_cast<char*>(dst);
+  while (n > 0) {
+    const ssize_t r = ::pread(fd, p, (size_t)std::min<uint64_t>(n, 1ull << 30), (off_t)off);
+    if (r < 0 && errno == EINTR) continue;
+    MINIPS_CHECK(r > 0, "pread failed / truncated " << what << ": " << (r < 0 ? std::strerror(errno) : "eof"));
+    p += r;
+    off += (uint64_t)r;
+    n -= (uint64_t)r;
+    g_bytes_read += (uint64_t)r;
+  }
+}
+
+// Header image: magic, version, meta, n, [name, dtype, rows, cols, bytes, offset]...
+std::string HeaderImage(const ShardMeta& m, const std::vector<ArrayDesc>& arrays) {
+  std::ostringstream o(std::ios::binary);
+  auto put = [&](const auto& v) { o.write(reinterpret_cast<const char*>(&v), sizeof(v)); };
+  auto put_s = [&](const std::string& s) {
+    put((uint32_t)s.size());
+    o.write(s.data(), (std::streamsize)s.size());
+  };
+  o.write(kMagic, 8);
+  put(kVersion);
+  put(m.global_rows);
+  put(m.base);
+  put(m.rows);
+  put(m.cols);
+  put(m.clock);
+  put(m.table_id);
+  put(m.rank);
+  put(m.world);
+  put_s(m.kind);
+  put((uint32_t)arrays.size());
+  for (const auto& a : arrays) {
+    put_s(a.name);
+    put((uint32_t)a.dtype);
+    put(a.rows);
+    put(a.cols);
+    put(a.bytes);
+    put(a.offset);
+  }
+  return o.str();
+}
+
+// Assigns 4 KiB aligned offsets after a header of the final size.
+void LayoutArrays(const ShardMeta& m, std::vector<ArrayDesc>& arrays) {
+  for (auto& a : arrays) a.bytes = a.rows * a.cols * DTypeSize(a.dtype);
+  uint64_t off = AlignUp(HeaderImage(m, arrays).size());
+  for (auto& a : arrays) {
+    a.offset = off;
+    off = AlignUp(off + a.bytes);
+  }
+}
+
 template <typename T>
 T get(std::ifstream& i) {
   T v;
   i.read(reinterpret_cast<char*>(&v), sizeof(T));
   MINIPS_CHECK(i.good(), "truncated shard file");
   return v;
-}
-void put_str(std::ofstream& o, const std::string& s) {
-  put<uint32_t>(o, (uint32_t)s.size());
-  o.write(s.data(), (std::streamsize)s.size());
 }
 std::string get_str(std::ifstream& i) {
   const uint32_t n = get<uint32_t>(i);
@@ -74,72 +142,123 @@ size_t DTypeSize(DType t) {
 }
 
 void WriteShard(const std::string& path, const ShardMeta& m, const std::vector<ArrayRef>& arrays) {
-  EnsureParentDir(path);
-  const std::string tmp = path + ".tmp";
-  {
-    std::ofstream o(tmp, std::ios::binary | std::ios::trunc);
-    MINIPS_CHECK(o.good(), "cannot write " << tmp);
-    o.write(kMagic, 8);
-    put<uint32_t>(o, kVersion);
-    put<uint64_t>(o, m.global_rows);
-    put<uint64_t>(o, m.base);
-    put<uint64_t>(o, m.rows);
-    put<uint64_t>(o, m.cols);
-    put<int64_t>(o, m.clock);
-    put<int32_t>(o, m.table_id);
-    put<int32_t>(o, m.rank);
-    put<int32_t>(o, m.world);
-    put_str(o, m.kind);
-    put<uint32_t>(o, (uint32_t)arrays.size());
-    for (const auto& a : arrays) {
-      put_str(o, a.name);
-      put<uint32_t>(o, (uint32_t)a.dtype);
-      put<uint64_t>(o, a.rows);
-      put<uint64_t>(o, a.cols);
-      const uint64_t bytes = a.rows * a.cols * DTypeSize(a.dtype);
-      put<uint64_t>(o, bytes);
-      if (bytes) o.write(static_cast<const char*>(a.data), (std::streamsize)bytes);
-    }
-    MINIPS_CHECK(o.good(), "write failed: " << tmp);
+  std::vector<ArrayDesc> desc;
+  for (const auto& a : arrays) {
+    ArrayDesc d;
+    d.name = a.name;
+    d.dtype = a.dtype;
+    d.rows = a.rows;
+    d.cols = a.cols;
+    desc.push_back(d);
   }
-  // atomic publish: a crash mid-write never leaves a truncated checkpoint under the real name
-  MINIPS_CHECK(std::rename(tmp.c_str(), path.c_str()) == 0, "rename " << tmp << " -> " << path);
+  ShardFileWriter w(path, m, desc);
+  for (size_t k = 0; k < arrays.size(); ++k)
+    if (arrays[k].rows) w.WriteRows((int)k, 0, arrays[k].data, arrays[k].rows);
+  w.Close();
 }
 
-LoadedShard ReadShard(const std::string& path) {
+ShardHeader ReadShardHeader(const std::string& path) {
   std::ifstream i(path, std::ios::binary);
   MINIPS_CHECK(i.good(), "cannot read " << path);
   char magic[8];
   i.read(magic, 8);
   MINIPS_CHECK(i.good() && std::memcmp(magic, kMagic, 8) == 0, "not a minips shard file: " << path);
   const uint32_t ver = get<uint32_t>(i);
-  MINIPS_CHECK(ver == kVersion, "unsupported shard version " << ver);
-  LoadedShard s;
-  s.meta.global_rows = get<uint64_t>(i);
-  s.meta.base = get<uint64_t>(i);
-  s.meta.rows = get<uint64_t>(i);
-  s.meta.cols = get<uint64_t>(i);
-  s.meta.clock = get<int64_t>(i);
-  s.meta.table_id = get<int32_t>(i);
-  s.meta.rank = get<int32_t>(i);
-  s.meta.world = get<int32_t>(i);
-  s.meta.kind = get_str(i);
+  MINIPS_CHECK(ver == kVersion, "unsupported shard version " << ver << " in " << path);
+  ShardHeader h;
+  h.meta.global_rows = get<uint64_t>(i);
+  h.meta.base = get<uint64_t>(i);
+  h.meta.rows = get<uint64_t>(i);
+  h.meta.cols = get<uint64_t>(i);
+  h.meta.clock = get<int64_t>(i);
+  h.meta.table_id = get<int32_t>(i);
+  h.meta.rank = get<int32_t>(i);
+  h.meta.world = get<int32_t>(i);
+  h.meta.kind = get_str(i);
   const uint32_t n = get<uint32_t>(i);
-  MINIPS_CHECK(n < 64, "corrupt array count");
+  MINIPS_CHECK(n < 64, "corrupt array count in " << path);
   for (uint32_t k = 0; k < n; ++k) {
-    LoadedArray a;
+    ArrayDesc a;
     a.name = get_str(i);
     a.dtype = (DType)get<uint32_t>(i);
     a.rows = get<uint64_t>(i);
     a.cols = get<uint64_t>(i);
-    const uint64_t bytes = get<uint64_t>(i);
-    MINIPS_CHECK(bytes == a.rows * a.cols * DTypeSize(a.dtype), "array size mismatch in " << path);
-    a.bytes.resize(bytes);
-    if (bytes) i.read(a.bytes.data(), (std::streamsize)bytes);
-    MINIPS_CHECK(i.good() || bytes == 0, "truncated array " << a.name << " in " << path);
+    a.bytes = get<uint64_t>(i);
+    a.offset = get<uint64_t>(i);
+    MINIPS_CHECK(a.bytes == a.rows * a.cols * DTypeSize(a.dtype), "array size mismatch in " << path);
+    h.arrays.push_back(a);
+  }
+  return h;
+}
+
+void ReadRows(const std::string& path, uint64_t offset, uint64_t row_bytes, uint64_t row0, uint64_t nrows, void* dst) {
+  if (nrows == 0) return;
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  MINIPS_CHECK(fd >= 0, "cannot open " << path << ": " << std::strerror(errno));
+  try {
+    PReadAll(fd, dst, nrows * row_bytes, offset + row0 * row_bytes, path);
+  } catch (...) {
+    ::close(fd);
+    throw;
+  }
+  ::close(fd);
+}
+
+uint64_t ShardBytesRead() { return g_bytes_read.load(); }
+void ResetShardBytesRead() { g_bytes_read = 0; }
+
+LoadedShard ReadShard(const std::string& path) {
+  const ShardHeader h = ReadShardHeader(path);
+  LoadedShard s;
+  s.meta = h.meta;
+  for (const auto& d : h.arrays) {
+    LoadedArray a;
+    a.name = d.name;
+    a.dtype = d.dtype;
+    a.rows = d.rows;
+    a.cols = d.cols;
+    a.bytes.resize(d.bytes);
+    if (d.bytes) ReadRows(path, d.offset, d.cols * DTypeSize(d.dtype), 0, d.rows, a.bytes.data());
     s.arrays.push_back(std::move(a));
   }
   return s;
+}
+
+ShardFileWriter::ShardFileWriter(const std::string& path, const ShardMeta& meta, const std::vector<ArrayDesc>& arrays)
+    : path_(path), tmp_(path + ".tmp"), arrays_(arrays) {
+  EnsureParentDir(path);
+  LayoutArrays(meta, arrays_);
+  fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  MINIPS_CHECK(fd_ >= 0, "cannot write " << tmp_ << ": " << std::strerror(errno));
+  const std::string hdr = HeaderImage(meta, arrays_);
+  PWriteAll(fd_, hdr.data(), hdr.size(), 0, tmp_);
+  uint64_t end = AlignUp(hdr.size());
+  for (const auto& a : arrays_) end = std::max(end, a.offset + a.bytes);
+  MINIPS_CHECK(::ftruncate(fd_, (off_t)end) == 0, "ftruncate " << tmp_);
+}
+
+ShardFileWriter::~ShardFileWriter() {
+  if (fd_ >= 0) {
+    ::close(fd_);
+    std::remove(tmp_.c_str());  // never closed: an abandoned checkpoint leaves no file behind
+  }
+}
+
+void ShardFileWriter::WriteRows(int array, uint64_t row0, const void* src, uint64_t nrows) {
+  MINIPS_CHECK(fd_ >= 0, "ShardFileWriter already closed");
+  MINIPS_CHECK(array >= 0 && array < (int)arrays_.size(), "bad array index " << array);
+  const ArrayDesc& a = arrays_[array];
+  MINIPS_CHECK(row0 + nrows <= a.rows, "rows [" << row0 << ", " << row0 + nrows << ") out of range " << a.rows);
+  const uint64_t rb = a.cols * DTypeSize(a.dtype);
+  PWriteAll(fd_, src, nrows * rb, a.offset + row0 * rb, tmp_);
+}
+
+void ShardFileWriter::Close() {
+  MINIPS_CHECK(fd_ >= 0, "ShardFileWriter already closed");
+  MINIPS_CHECK(::close(fd_) == 0, "close " << tmp_);
+  fd_ = -1;
+  // atomic publish: a crash mid-write never leaves a truncated checkpoint under the real name
+  MINIPS_CHECK(std::rename(tmp_.c_str(), path_.c_str()) == 0, "rename " << tmp_ << " -> " << path_);
 }
 
 void WriteTextParams(const std::string& path, const ArrayRef& a) {

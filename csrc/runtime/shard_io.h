@@ -8,6 +8,16 @@
 // the reference Restore mis-parses that format -- ReadTextParams parses it correctly).
 // Writes run on a background thread from host memory the caller keeps alive (pinned staging
 // buffers the D2H copies landed in), so a checkpoint overlaps the next training steps.
+//
+// Format v2 (scales to multi-hundred-GB shards, e.g. a 10B-row embedding table over 8 GPUs):
+// the header lists every array with its file offset (4 KiB aligned), so
+//   * a writer streams an array in row chunks (ShardFileWriter::WriteRows -> pwrite) from a
+//     bounded pinned ring, never holding a whole shard in host memory;
+//   * a reader parses the header only (ReadShardHeader) and preads exactly the rows of the
+//     global range it owns (ReadRows), so an N -> M reshard reads each byte once in total
+//     instead of every rank reading every file.
+// ShardBytesRead() counts the payload bytes read by this process (tests assert read
+// amplification with it).
 #pragma once
 
 #include <condition_variable>
@@ -51,6 +61,17 @@ struct LoadedArray {
   std::vector<char> bytes;
 };
 
+struct ArrayDesc {  // header entry of one array in a v2 shard file
+  std::string name;
+  DType dtype = DType::kF32;
+  uint64_t rows = 0, cols = 1, bytes = 0, offset = 0;
+};
+
+struct ShardHeader {
+  ShardMeta meta;
+  std::vector<ArrayDesc> arrays;
+};
+
 struct LoadedShard {
   ShardMeta meta;
   std::vector<LoadedArray> arrays;
@@ -58,7 +79,29 @@ struct LoadedShard {
 
 // Synchronous writers / readers.
 void WriteShard(const std::string& path, const ShardMeta& meta, const std::vector<ArrayRef>& arrays);
-LoadedShard ReadShard(const std::string& path);
+LoadedShard ReadShard(const std::string& path);  // whole file (small shards, tools)
+ShardHeader ReadShardHeader(const std::string& path);
+// Reads rows [row0, row0 + nrows) of the array at `offset` (row_bytes each) into dst.
+void ReadRows(const std::string& path, uint64_t offset, uint64_t row_bytes, uint64_t row0, uint64_t nrows, void* dst);
+uint64_t ShardBytesRead();
+void ResetShardBytesRead();
+
+// Streaming writer of one v2 shard file: the header (with every array's offset) is written on
+// construction into "<path>.tmp", rows arrive in any order by pwrite, Close() renames the file
+// into place (a crash never leaves a truncated file under the real name).
+class ShardFileWriter {
+ public:
+  ShardFileWriter(const std::string& path, const ShardMeta& meta, const std::vector<ArrayDesc>& arrays);
+  ~ShardFileWriter();
+  void WriteRows(int array, uint64_t row0, const void* src, uint64_t nrows);
+  void Close();
+  const std::vector<ArrayDesc>& arrays() const { return arrays_; }
+
+ private:
+  std::string path_, tmp_;
+  std::vector<ArrayDesc> arrays_;
+  int fd_ = -1;
+};
 // Reference text format of one array: "<local_idx>:<val> " for non-zero entries, one line.
 void WriteTextParams(const std::string& path, const ArrayRef& a);
 // Parses the text format back into a dense vector of `n` values (missing entries = 0).

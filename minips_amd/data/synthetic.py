@@ -46,11 +46,7 @@ class CriteoSynth:
             # one fused gfx950 launch (csrc/kernels/data.hip) instead of ~15 torch kernels
             from .._native import kernels
 
-            if not hasattr(self, "_seed"):
-                self._seed = int(torch.randint(0, 2**62, (1,), generator=self.gen, device=self.device).item())
-                # the step counter lives on the device: a step captured in a HIP graph draws a
-                # fresh batch on every replay
-                self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._init_gpu()
             self._step_dev.add_(1)
             dense = torch.empty(B, self.n_dense, device=self.device)
             keys = torch.empty(B, F, dtype=torch.int64, device=self.device)
@@ -69,12 +65,18 @@ class CriteoSynth:
         labels = (torch.sigmoid(2.0 * logit) > noise).float()
         return dense, keys, labels
 
+    def _init_gpu(self):
+        if not hasattr(self, "_seed"):
+            self._seed = int(torch.randint(0, 2**62, (1,), generator=self.gen, device=self.device).item())
+            # the step counter lives on the device: a step captured in a HIP graph draws a fresh
+            # batch on every replay
+            self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+
     def skip(self, n: int):
         """Advance past ``n`` batches (resume from a checkpoint at the same data position)."""
         if self.device.type == "cuda":
-            if not hasattr(self, "_seed"):
-                self._seed = int(torch.randint(0, 2**62, (1,), generator=self.gen, device=self.device).item())
-            self._step = getattr(self, "_step", 0) + n
+            self._init_gpu()
+            self._step_dev.add_(n)
         else:
             for _ in range(n):
                 self.next()

@@ -7,20 +7,32 @@ still being written therefore restores the previous complete one, never a mix of
 Files inside an iteration directory, one set per rank ``my_id``, keep the reference names and
 text formats:
 
-  server_params_<id>_t<table>.bin  binary sidecar: header + fp32 shard + optimizer state
-                                   (native writer, csrc/runtime/shard_io.cc)
+  server_params_<id>_t<table>.bin  binary sidecar (format v2, csrc/runtime/shard_io.h): header
+                                   with per-array file offsets + fp32 shard + optimizer state
   server_params_<id>_t<table>      reference text format "<local_idx>:<val> " of the non-zero
-                                   parameters (vector_storage.hpp:54-73), small tables only
+                                   parameters (vector_storage.hpp:54-73), shards up to text_limit
   server_progress_<id>_t<table>    "min_clock:<c> <tid>:<c> ..." (progress_tracker.hpp:68-85),
                                    exact clocks (no RoundHundred), tids in SimpleIdMapper layout
   worker_config_<id>               "<worker_id>:<iteration> " (svm_dumper.hpp:51-66)
 
-Saving is asynchronous: the shards are copied device -> pinned host on a side HIP stream, and a
-background thread writes the files (the C++ writer releases the GIL), so training continues
-while the checkpoint drains. ``wait()`` joins it. Loading reads every rank's sidecar of a table
-and copies the overlap of each piece's global row range with the local shard, so a checkpoint
-taken at one world size restores at another (elastic restart). The reference defects are fixed:
-text restore parses its own format, BSP/ASP tables checkpoint (no hang), one file per table.
+Consistent snapshot, bounded host memory (sized for a 10B-row table: ~85 GB of shard per rank)
+---------------------------------------------------------------------------------------------
+The reference dumps from the server thread, so no Add races the dump (ssp_model.cpp:112-125).
+Here the shard must not change between the start and the end of its device -> host copy:
+  * shard <= ``ring_bytes`` (default 1 GiB): D2H into pinned staging on the checkpoint stream;
+    the compute stream waits for that copy (only), then the files are written in the background.
+  * larger, and HBM has room for a copy: a device-side snapshot (D2D clone, ~3 TB/s); the
+    compute stream waits for the clone only; the background writer streams the snapshot through
+    a pinned ring of ``ring_bytes`` (two slots, D2H of chunk i+1 overlapping pwrite of chunk i).
+  * larger, no HBM headroom: the same ring streaming from the live shard, in the foreground
+    (training waits, like the reference's synchronous dump).
+Host staging never exceeds ``ring_bytes`` (``peak_staging_bytes`` records it).
+
+Restore reads the header of every file of a table (a few hundred bytes) and preads exactly the
+rows of the global range this rank owns (hash tables: keys are stored sorted, the owned key
+range is found by binary search), so an N -> M reshard reads every payload byte once in total.
+The reference defects are fixed: text restore parses its own format, BSP/ASP tables checkpoint
+(no hang), one file per table.
 """
 from __future__ import annotations
 
@@ -29,6 +41,7 @@ import os
 import threading
 import time
 
+import numpy as np
 import torch
 
 from .._native import runtime
@@ -38,35 +51,63 @@ _DT = {torch.float32: "float32", torch.bfloat16: "bfloat16", torch.float64: "flo
        torch.int32: "int32"}
 _TD = {v: k for k, v in _DT.items()}
 WORKER_TID_OFFSET = 100  # SimpleIdMapper: workers of node n are n*1000 + [100, 1000)
+_RING_DEFAULT = int(os.environ.get("MINIPS_CKPT_RING_MB", "1024")) << 20
 
 
 def _prefix_path(prefix: str, name: str) -> str:
     return prefix + name
 
 
+def _as2d(t: torch.Tensor) -> torch.Tensor:
+    if t.dim() == 0:
+        return t.reshape(1, 1)
+    if t.dim() == 1:
+        return t.reshape(-1, 1)
+    return t.reshape(t.shape[0], -1) if t.numel() else t.reshape(t.shape[0], max(1, int(np.prod(t.shape[1:]))))
+
+
 class Checkpointer:
-    def __init__(self, comm, prefix: str, my_id: int | None = None, text_limit: int = 1 << 22):
+    def __init__(self, comm, prefix: str, my_id: int | None = None, text_limit: int = 1 << 22,
+                 ring_bytes: int | None = None):
         self.comm = comm
         self.prefix = prefix
         self.my_id = comm.rank if my_id is None else my_id
         self.text_limit = text_limit  # write the reference text file when a shard has <= this many values
-        self._writer = runtime().ShardWriter()
-        self._stream = torch.cuda.Stream(device=comm.device) if comm.device.type == "cuda" else None
+        self.ring_bytes = int(ring_bytes or _RING_DEFAULT)
+        self.cuda = comm.device.type == "cuda"
+        self._stream = torch.cuda.Stream(device=comm.device) if self.cuda else None
         self._host: dict = {}
+        self._ring: list = []
+        self._staging_now = 0
+        self.peak_staging_bytes = 0
+        self.last_mode = None
         self._thread: threading.Thread | None = None
         self._error: BaseException | None = None
         self._pending_iter: int | None = None
         self.last_seconds = 0.0
         self.keep = 2
 
-    # ------------------------------------------------------------------------------ save
-    def _staging(self, key, t: torch.Tensor) -> torch.Tensor:
-        h = self._host.get(key)
-        if h is None or h.shape != t.shape or h.dtype != t.dtype:
-            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=t.is_cuda)
-            self._host[key] = h
-        return h
+    # ------------------------------------------------------------------------------ staging
+    def _alloc_host(self, nbytes: int) -> torch.Tensor:
+        t = torch.empty(nbytes, dtype=torch.uint8, pin_memory=self.cuda)
+        self._staging_now += nbytes
+        self.peak_staging_bytes = max(self.peak_staging_bytes, self._staging_now)
+        return t
 
+    def _release_staging(self):
+        self._host.clear()
+        self._ring = []
+        self._staging_now = 0
+
+    def _ring_slots(self, max_row_bytes: int):
+        """Two pinned slots of ring_bytes / 2 each (at least one row of the widest array)."""
+        slot = max(self.ring_bytes // 2, max_row_bytes)
+        if not self._ring or self._ring[0].numel() < slot:
+            self._ring = []
+            self._ring = [self._alloc_host(slot) for _ in range(2)]
+        return self._ring
+
+    # ------------------------------------------------------------------------------ save
     def iter_dir(self, iteration: int) -> str:
         return f"{self.prefix}iter_{int(iteration)}/"
 
@@ -85,55 +126,142 @@ class Checkpointer:
         self.comm.all_gather(allc, clocks)
         allc = allc.view(self.comm.world, -1).cpu()
         jobs = []
-        cur = torch.cuda.current_stream(self.comm.device) if self._stream is not None else None
-        if self._stream is not None:
-            self._stream.wait_stream(cur)
         for k, (tid, table) in enumerate(sorted(tables.items())):
             meta, arrays = table.shard_state()
-            host = {}
-            for name, dev in arrays.items():
-                h = self._staging((tid, name), dev)
-                if self._stream is not None:
-                    with torch.cuda.stream(self._stream):
-                        h.copy_(dev, non_blocking=True)
-                        dev.record_stream(self._stream)
-                else:
-                    h.copy_(dev)
-                host[name] = h
-            jobs.append((tid, meta, host, allc[:, k].tolist()))
-        ev = None
-        if self._stream is not None:
-            ev = torch.cuda.Event()
-            ev.record(self._stream)
+            jobs.append((tid, meta, {n: _as2d(a) for n, a in arrays.items()}, allc[:, k].tolist()))
+        total = sum(a.numel() * a.element_size() for _, _, arrs, _ in jobs for a in arrs.values())
+        self._release_staging()
+        mode = self._snapshot_mode(total)
+        self.last_mode = mode
+        cur = torch.cuda.current_stream(self.comm.device) if self.cuda else None
+        if mode == "pinned":
+            # whole shards fit the staging budget: one D2H per array on the checkpoint stream; the
+            # compute stream waits for these copies before it can touch the shards again
+            if self.cuda:
+                self._stream.wait_stream(cur)
+            staged = []
+            for tid, meta, arrs, clk in jobs:
+                host = {}
+                for name, a in arrs.items():
+                    h = self._alloc_host(a.numel() * a.element_size()).view(a.dtype).view(a.shape)
+                    if self.cuda:
+                        with torch.cuda.stream(self._stream):
+                            h.copy_(a, non_blocking=True)
+                    else:
+                        h.copy_(a)
+                    host[name] = h
+                staged.append((tid, meta, host, clk))
+            ev = None
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+                cur.wait_event(ev)  # no Add/apply may run before the D2H copies finished
+            jobs = staged
+        elif mode == "device":
+            self._stream.wait_stream(cur)
+            snap = []
+            with torch.cuda.stream(self._stream):
+                for tid, meta, arrs, clk in jobs:
+                    snap.append((tid, meta, {n: a.clone() for n, a in arrs.items()}, clk))
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+            cur.wait_event(ev)  # the clone is the consistent image; training continues after it
+            jobs = snap
+        else:
+            ev = None
+            if self.cuda:
+                self._stream.wait_stream(cur)
 
         def work():
             try:
                 if ev is not None:
                     ev.synchronize()
-                for tid, meta, host, clk in jobs:
-                    base = f"server_params_{self.my_id}_t{tid}"
-                    arrays = [(n, h.data_ptr(), _DT[h.dtype], h.shape[0] if h.dim() else 1,
-                               h.shape[1] if h.dim() > 1 else 1) for n, h in host.items()]
-                    n_vals = sum(h.numel() for h in host.values()) // max(1, len(host))
-                    text = _prefix_path(out, base) if n_vals <= self.text_limit and meta["kind"] != "hash" else ""
-                    self._writer.submit(_prefix_path(out, base + ".bin"), meta, arrays, text)
+                for tid, meta, arrs, clk in jobs:
+                    self._write_table(out, tid, meta, arrs, host_ready=(mode == "pinned"))
                     self._write_progress(out, tid, clk)
                 self._write_worker_config(out, iteration)
-                self._writer.wait_all()
-                err = self._writer.take_error()
-                if err:
-                    raise RuntimeError(err)
                 self.last_seconds = time.perf_counter() - t0
                 get_logger().event("checkpoint", iteration=iteration, seconds=round(self.last_seconds, 4),
-                                   tables=len(jobs), prefix=self.prefix)
+                                   tables=len(jobs), prefix=self.prefix, mode=mode, bytes=int(total),
+                                   peak_staging=int(self.peak_staging_bytes))
             except BaseException as e:  # surfaced by wait()
                 self._error = e
 
-        self._thread = threading.Thread(target=work, name="minips-ckpt", daemon=True)
-        self._thread.start()
         self._pending_iter = int(iteration)
+        if mode == "stream":  # no room for a snapshot: write from the live shards, training waits
+            work()
+            self._thread = None
+            if self._error is not None:
+                e, self._error = self._error, None
+                raise e
+        else:
+            self._thread = threading.Thread(target=work, name="minips-ckpt", daemon=True)
+            self._thread.start()
         if blocking:
             self.commit()
+
+    def _snapshot_mode(self, total: int) -> str:
+        if total <= self.ring_bytes:
+            return "pinned"
+        if self.cuda:
+            free, _ = torch.cuda.mem_get_info(self.comm.device)
+            if free > total + (2 << 30):
+                return "device"
+        return "stream"
+
+    def _write_table(self, out: str, tid: int, meta: dict, arrs: dict, host_ready: bool):
+        base = f"server_params_{self.my_id}_t{tid}"
+        desc = [(n, _DT[a.dtype], a.shape[0], a.shape[1]) for n, a in arrs.items()]
+        w = runtime().ShardFileWriter(_prefix_path(out, base + ".bin"), meta, desc)
+        for k, (name, a) in enumerate(arrs.items()):
+            if host_ready or not a.is_cuda:
+                self._write_host_array(w, k, a)
+            else:
+                self._stream_array(w, k, a)
+        w.close()
+        first = next(iter(arrs.values()), None)
+        n_vals = first.numel() if first is not None else 0
+        if host_ready and first is not None and n_vals <= self.text_limit and meta["kind"] != "hash":
+            runtime().write_text_params(_prefix_path(out, base), first.data_ptr(), _DT[first.dtype],
+                                        first.shape[0], first.shape[1])
+
+    def _write_host_array(self, w, k: int, a: torch.Tensor):
+        """Host-resident array: written in ring-sized pieces (a CPU table streams through the ring
+        so it never needs a second whole-shard host copy)."""
+        if a.shape[0] == 0:
+            return
+        a = a.contiguous()
+        rb = a.shape[1] * a.element_size()
+        step = max(1, (self.ring_bytes // 2) // rb)
+        for r0 in range(0, a.shape[0], step):
+            n = min(step, a.shape[0] - r0)
+            w.write_rows(k, r0, a[r0:].data_ptr(), n)
+
+    def _stream_array(self, w, k: int, a: torch.Tensor):
+        """Device array -> file through the two-slot pinned ring: the D2H of chunk i+1 runs on
+        the checkpoint stream while chunk i is written."""
+        rows = a.shape[0]
+        if rows == 0:
+            return
+        rb = a.shape[1] * a.element_size()
+        slots = self._ring_slots(rb)
+        step = max(1, slots[0].numel() // rb)
+        prev = None
+        for i, r0 in enumerate(range(0, rows, step)):
+            n = min(step, rows - r0)
+            dst = slots[i % 2][: n * rb].view(a.dtype).view(n, a.shape[1])
+            with torch.cuda.stream(self._stream):
+                dst.copy_(a[r0: r0 + n], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+            if prev is not None:
+                p_ev, p_r0, p_n, p_dst = prev
+                p_ev.synchronize()
+                w.write_rows(k, p_r0, p_dst.data_ptr(), p_n)
+            prev = (ev, r0, n, dst)
+        p_ev, p_r0, p_n, p_dst = prev
+        p_ev.synchronize()
+        w.write_rows(k, p_r0, p_dst.data_ptr(), p_n)
 
     def try_commit(self) -> bool:
         """Publish the in-flight checkpoint if every rank's background writer has finished
@@ -174,10 +302,21 @@ class Checkpointer:
                     shutil.rmtree(self.iter_dir(old), ignore_errors=True)
         self.comm.barrier()
 
+    def abandon(self):
+        """In-place rollback: finish the local writer, drop the uncommitted checkpoint (its commit
+        would be a collective on the broken group)."""
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        self._error = None
+        self._pending_iter = None
+        self._release_staging()
+
     def wait(self):
         if self._thread is not None:
             self._thread.join()
             self._thread = None
+        self._release_staging()
         if self._error is not None:
             e, self._error = self._error, None
             raise e
@@ -206,42 +345,96 @@ class Checkpointer:
         return self.latest() is not None
 
     def load(self, tables: dict, iteration: int | None = None) -> int:
-        """Restore every table from the sidecars of all ranks of the latest committed checkpoint
-        (or ``iteration``); returns the saved iteration."""
+        """Restore every table from the latest committed checkpoint (or ``iteration``), reading
+        only the rows this rank owns; returns the saved iteration."""
         it = self.latest() if iteration is None else int(iteration)
         if it is None:
             raise FileNotFoundError(f"no committed checkpoint under {self.prefix!r} (missing 'latest')")
         src = self.iter_dir(it)
+        self._release_staging()
         for tid, table in sorted(tables.items()):
             files = sorted(glob.glob(glob.escape(src) + f"server_params_*_t{tid}.bin"))
             if not files:
                 raise FileNotFoundError(f"no checkpoint shards for table {tid} under {src!r}")
-            pieces, clock = [], None
             my_meta = table.shard_state()[0]
-            for path in files:
-                meta, arrays = runtime().read_shard(path)
+            heads = [runtime().read_shard_header(p) for p in files]
+            clock = None
+            for path, (meta, _) in zip(files, heads):
                 if meta["global_rows"] != my_meta["global_rows"] or meta["cols"] != my_meta["cols"]:
                     raise ValueError(f"{path}: table shape {meta['global_rows']}x{meta['cols']} does not match "
                                      f"{my_meta['global_rows']}x{my_meta['cols']}")
-                lo, hi = meta["base"], meta["base"] + meta["rows"]
-                if meta["kind"] != "hash" and (hi <= my_meta["base"] or lo >= my_meta["base"] + my_meta["rows"]):
-                    if meta["rank"] == self.my_id:
-                        clock = meta["clock"]
-                    continue
-                tens = {}
-                for name, dt, rows, cols, buf in arrays:
-                    t = torch.frombuffer(buf, dtype=_TD[dt]) if len(buf) else torch.empty(0, dtype=_TD[dt])
-                    tens[name] = t.view(int(rows), int(cols)).to(self.comm.device)
-                pieces.append((meta, tens))
                 if meta["rank"] == self.my_id or clock is None:
                     clock = meta["clock"]
-            table.load_shard_pieces(pieces, clock or 0)
+            lo, hi = table.restore_range()
+            if my_meta["kind"] == "hash":
+                for path, (meta, arrays) in zip(files, heads):
+                    self._load_hash_file(table, path, meta, arrays, lo, hi)
+            else:
+                dst = table.restore_dst()
+                for path, (meta, arrays) in zip(files, heads):
+                    a, b = max(lo, meta["base"]), min(hi, meta["base"] + meta["rows"])
+                    if a >= b:
+                        continue  # nothing of this file is ours: not a byte read
+                    for name, dt, rows, cols, off in arrays:
+                        d = dst.get(name)
+                        if d is not None:
+                            self._read_rows_into(path, off, _TD[dt], int(cols), a - meta["base"], b - a,
+                                                 d[a - lo: b - lo])
+            table.finish_restore(clock or 0)
+        self._release_staging()
         cfg_path = _prefix_path(src, f"worker_config_{self.my_id}")
         if os.path.exists(cfg_path):
             cfg = runtime().load_config_data(cfg_path)
             it = int(cfg.get(int(self.comm.rank), it))
-        get_logger().event("restore", iteration=it, prefix=self.prefix, tables=len(tables))
+        get_logger().event("restore", iteration=it, prefix=self.prefix, tables=len(tables),
+                           bytes_read=int(runtime().shard_bytes_read()))
         return it
+
+    def _read_rows_into(self, path, off, dtype, cols, r0, n, dst: torch.Tensor):
+        """pread rows [r0, r0+n) into dst ([n, cols] view on the table's device) through the ring."""
+        esz = torch.empty(0, dtype=dtype).element_size()
+        rb = cols * esz
+        slots = self._ring_slots(rb)
+        step = max(1, slots[0].numel() // rb)
+        for i, s in enumerate(range(0, n, step)):
+            m = min(step, n - s)
+            host = slots[i % 2][: m * rb]
+            runtime().read_rows(path, int(off), rb, int(r0 + s), m, host.data_ptr())
+            src = host.view(dtype).view(m, cols)
+            d = dst[s: s + m]
+            d.copy_(src.reshape(d.shape).to(d.dtype))  # synchronous: the slot is reused next round
+
+    def _load_hash_file(self, table, path, meta, arrays, lo, hi):
+        """Hash shards store their (mixed) keys sorted: binary-search the owned key range [lo, hi)
+        and stream only those rows."""
+        desc = {name: (dt, int(rows), int(cols), int(off)) for name, dt, rows, cols, off in arrays}
+        kdt, nrows, _, koff = desc["keys"]
+        probe = np.empty(1, dtype=np.int64)
+
+        def lower_bound(key):
+            a, b = 0, nrows
+            while a < b:
+                mid = (a + b) // 2
+                runtime().read_rows(path, koff, 8, mid, 1, probe.ctypes.data)
+                if int(probe[0]) < key:
+                    a = mid + 1
+                else:
+                    b = mid
+            return a
+
+        i0, i1 = lower_bound(lo), lower_bound(hi)
+        if i0 >= i1:
+            return
+        width = max(desc[n][2] for n in desc) * 8
+        step = max(1, (self.ring_bytes // 4) // width)
+        for s in range(i0, i1, step):
+            m = min(step, i1 - s)
+            chunk = {}
+            for name, (dt, _, cols, off) in desc.items():
+                t = torch.empty(m, cols, dtype=_TD[dt], device=self.comm.device)
+                self._read_rows_into(path, off, _TD[dt], cols, s, m, t)
+                chunk[name] = t
+            table.restore_insert(chunk)
 
 
 def load_text_params(path: str, n: int) -> torch.Tensor:
@@ -255,4 +448,3 @@ def parse_progress(path: str) -> dict:
         k, v = tok.split(":")
         out[k if k == "min_clock" else int(k)] = int(v)
     return out
-

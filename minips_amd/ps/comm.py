@@ -29,8 +29,10 @@ tests/test_comm_schedule.py checks that 4- and 8-rank runs issue identical seque
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
+import threading
 from dataclasses import dataclass
 
 import torch
@@ -66,6 +68,32 @@ class Comm:
         # issue-order record of the collectives [(op, dtype, shape-invariant size)], enabled by
         # MINIPS_COMM_TRACE=1 or by assigning a list (tests)
         self.trace: list | None = [] if os.environ.get("MINIPS_COMM_TRACE") == "1" else None
+        self._waiting = 0
+        self._wlock = threading.Lock()
+
+    def refresh(self):
+        """Re-read rank / world / backend after the default process group was re-created (in-place
+        rollback, minips_amd.train): every table keeps this same Comm object."""
+        self.initialized = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank(self.group) if self.initialized else 0
+        self.world = dist.get_world_size(self.group) if self.initialized else 1
+        self.backend = dist.get_backend(self.group) if self.initialized else "none"
+
+    @contextlib.contextmanager
+    def waiting(self):
+        """Marks a host wait on peers (a blocking collective, a collective's result): the
+        heartbeat reports state "comm", so the supervisor can tell a rank that waits for a stuck
+        peer from the stuck rank itself."""
+        with self._wlock:
+            self._waiting += 1
+        try:
+            yield
+        finally:
+            with self._wlock:
+                self._waiting -= 1
+
+    def state(self) -> str:
+        return "comm" if self._waiting > 0 else "run"
 
     def _record(self, op: str, t: torch.Tensor | None = None, size=None):
         if self.trace is not None:
@@ -119,7 +147,8 @@ class Comm:
         if not p2p:
             o = out[: sum(recv_splits)]
             i = inp[: sum(send_splits)]
-            dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
+            with self.waiting():
+                dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
             return out
         so = [0]
         for c in send_splits:
@@ -138,8 +167,9 @@ class Comm:
             if recv_splits[peer]:
                 ops_.append(dist.P2POp(dist.irecv, out[ro[peer]: ro[peer + 1]], peer, group=self.group))
         if ops_:
-            for r in dist.batch_isend_irecv(ops_):
-                r.wait()
+            with self.waiting():
+                for r in dist.batch_isend_irecv(ops_):
+                    r.wait()
         return out
 
     def all_to_all_counts(self, recv: torch.Tensor, counts: torch.Tensor):
@@ -150,10 +180,12 @@ class Comm:
         self._record("a2a_counts", counts, counts.numel())
         if self._staged(recv, counts):
             r = torch.empty(recv.shape, dtype=recv.dtype)
-            dist.all_to_all_single(r, counts.cpu(), group=self.group)
+            with self.waiting():
+                dist.all_to_all_single(r, counts.cpu(), group=self.group)
             recv.copy_(r)
         else:
-            dist.all_to_all_single(recv, counts, group=self.group)
+            with self.waiting():
+                dist.all_to_all_single(recv, counts, group=self.group)
         return recv
 
     def exchange_counts(self, counts: torch.Tensor) -> tuple[list[int], list[int]]:
@@ -179,7 +211,8 @@ class Comm:
             out_shard.copy_(inp)
             return out_shard
         self.stats.bytes_rs += inp.numel() * inp.element_size()
-        dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
+        with self.waiting():
+            dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
         return out_shard
 
     def all_gather(self, out_full: torch.Tensor, shard: torch.Tensor):
@@ -199,7 +232,8 @@ class Comm:
         if self.backend == "gloo" and shard.data_ptr() >= out_full.data_ptr() and \
                 shard.data_ptr() < out_full.data_ptr() + out_full.numel() * out_full.element_size():
             shard = shard.clone()  # gloo does not support the in-place (aliased) form
-        dist.all_gather_into_tensor(out_full, shard, group=self.group)
+        with self.waiting():
+            dist.all_gather_into_tensor(out_full, shard, group=self.group)
         return out_full
 
     def all_reduce_(self, t: torch.Tensor, op=None):
@@ -208,10 +242,12 @@ class Comm:
         self._record("all_reduce", t, t.numel())
         if self._staged(t):
             h = t.cpu()
-            dist.all_reduce(h, op=op or dist.ReduceOp.SUM, group=self.group)
+            with self.waiting():
+                dist.all_reduce(h, op=op or dist.ReduceOp.SUM, group=self.group)
             t.copy_(h)
             return t
-        dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
+        with self.waiting():
+            dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
         return t
 
     def barrier(self):
@@ -220,7 +256,8 @@ class Comm:
         t = torch.zeros(1, device=self.device)
         self.all_reduce_(t)
         if t.is_cuda:
-            torch.cuda.synchronize(self.device)
+            with self.waiting():
+                torch.cuda.synchronize(self.device)
 
 
 def init_distributed(backend: str | None = None) -> Comm:

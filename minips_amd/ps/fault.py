@@ -1,17 +1,25 @@
 """Rank-side fault-tolerance helpers.
 
-Heartbeat          daemon thread that stamps <dir>/hb_<rank> every `interval` s; the supervisor
-                   (minips_amd.elastic) declares a rank failed when its stamp is older than
-                   3 x interval (master/heartbeat_check_thread.cpp:29) or the process exited.
+Heartbeat          daemon thread that stamps <dir>/hb_<rank> every `interval` s with JSON
+                   {t, step, state}: ``step`` is the last iteration the TRAINING LOOP completed
+                   (``progress()``), ``state`` is "run", "comm" (blocked in a collective / on a
+                   collective's result, see ps.comm.Comm.waiting) or "recover" (rolling back).
+                   The supervisor (minips_amd.elastic) declares a rank failed when the stamp is
+                   older than 3 x interval (master/heartbeat_check_thread.cpp:29: the process is
+                   gone or frozen) OR when its step has not advanced for the progress timeout
+                   while it is not waiting on a peer (it is stuck inside a step: a hung kernel,
+                   a deadlock, a sleep), so a live thread can no longer mask a hung rank.
 FaultInjector      --fail_rank/--fail_step: that rank fails when it reaches the step, on the first
                    attempt only -- --fail_mode=exit: the process dies (os._exit; detected from the
-                   exit status); --fail_mode=hang: it stops heartbeating and stalls, like a machine
-                   that stops answering (detected only by the 3 x interval heartbeat timeout, the
-                   reference's only detector); --with_injected_straggler: a 5% chance per step of
-                   sleeping U(0, 100) ms (lr_example.cpp:347-353).
+                   exit status); --fail_mode=hang: it stops heartbeating and stalls (a machine that
+                   stops answering); --fail_mode=hang_in_step: it blocks INSIDE the step with the
+                   heartbeat thread untouched (detected by the progress check only);
+                   --with_injected_straggler: a 5% chance per step of sleeping U(0, 100) ms
+                   (lr_example.cpp:347-353).
 """
 from __future__ import annotations
 
+import json
 import os
 import random
 import threading
@@ -19,19 +27,30 @@ import time
 
 
 class Heartbeat:
-    def __init__(self, directory: str, rank: int, interval: float):
+    def __init__(self, directory: str, rank: int, interval: float, state_fn=None):
         self.path = os.path.join(directory, f"hb_{rank}")
         self.interval = interval
+        self.step = -1
+        self.state = "run"
+        self.state_fn = state_fn  # optional: returns "comm" while the rank waits on its peers
         os.makedirs(directory, exist_ok=True)
         self._stop = threading.Event()
         self._beat()
         self._th = threading.Thread(target=self._loop, name="minips-heartbeat", daemon=True)
         self._th.start()
 
+    def progress(self, step: int):
+        """Called by the training loop after each completed iteration (and at long phases:
+        start-up, restore, checkpoint), so the stamp carries real progress."""
+        self.step = int(step)
+
     def _beat(self):
+        state = self.state
+        if state == "run" and self.state_fn is not None:
+            state = self.state_fn() or "run"
         tmp = self.path + ".tmp"
         with open(tmp, "w") as f:
-            f.write(f"{time.time():.3f}")
+            f.write(json.dumps({"t": round(time.time(), 3), "step": self.step, "state": state}))
         os.replace(tmp, self.path)
 
     def _loop(self):
@@ -47,6 +66,15 @@ class Heartbeat:
                 f.write(f"{time.time():.3f}")
 
 
+def read_heartbeat(path: str):
+    """-> (mtime-free stamp time, step, state) of a heartbeat file, or None."""
+    try:
+        d = json.loads(open(path).read())
+        return float(d["t"]), int(d.get("step", -1)), str(d.get("state", "run"))
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 class FaultInjector:
     def __init__(self, rank: int, fail_rank: int = -1, fail_step: int = -1, straggler: bool = False,
                  seed: int = 0, mode: str = "exit", heartbeat: Heartbeat | None = None):
@@ -54,11 +82,16 @@ class FaultInjector:
         self.mode, self.heartbeat = mode, heartbeat
         self.fail_rank, self.fail_step = fail_rank, fail_step
         self.straggler = straggler
-        self.first_attempt = int(os.environ.get("MINIPS_RESTART_COUNT", "0")) == 0
+        self.first_attempt = int(os.environ.get("MINIPS_RESTART_COUNT", "0")) == 0 and \
+            int(os.environ.get("MINIPS_GENERATION", "0")) == 0
         self.rng = random.Random(seed * 7919 + rank)
 
+    def _hit(self, step: int) -> bool:
+        return self.first_attempt and self.rank == self.fail_rank and step == self.fail_step
+
     def step(self, step: int):
-        if self.first_attempt and self.rank == self.fail_rank and step == self.fail_step:
+        """Called at the top of an iteration (exit / hang / straggler)."""
+        if self._hit(step) and self.mode in ("exit", "hang"):
             print(f"[fault injection][{int(time.time() * 1000)}] rank {self.rank} {self.mode} at step {step}",
                   flush=True)
             if self.mode == "hang":
@@ -69,3 +102,12 @@ class FaultInjector:
             os._exit(17)
         if self.straggler and self.rng.random() < 0.05:
             time.sleep(self.rng.uniform(0.0, 0.1))
+
+    def in_step(self, step: int):
+        """Called INSIDE the step (between the Get and the Clock): hang_in_step blocks here while
+        the heartbeat thread keeps stamping."""
+        if self._hit(step) and self.mode == "hang_in_step":
+            print(f"[fault injection][{int(time.time() * 1000)}] rank {self.rank} hangs inside step {step}",
+                  flush=True)
+            while True:
+                time.sleep(3600)

@@ -123,6 +123,10 @@ class _Pipeline:
             cur.wait_stream(self.stream)
             self.events.clear()
 
+    def reset(self):
+        """In-place rollback: forget in-flight clocks (issued on the broken communicator)."""
+        self.events.clear()
+
 
 class DenseTable:
     def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
@@ -252,6 +256,12 @@ class DenseTable:
     def drain(self):
         self.pipe.drain()
 
+    def reset_after_rollback(self):
+        self.pipe.reset()
+        self._pending = False
+        for g in self._ring:
+            g.zero_()
+
     # -- checkpoint hooks (minips_amd.ps.checkpoint) -------------------------------------------
     def shard_state(self):
         """(meta, {name: tensor}) of the owned shard: fp32 master + optimizer state, padding
@@ -267,19 +277,17 @@ class DenseTable:
                     table_id=self.table_id, rank=self.comm.rank, world=self.comm.world, kind="dense")
         return meta, arrays
 
-    def load_shard_pieces(self, pieces, clock: int):
-        """pieces: [(meta, {name: cpu tensor})] from any world size; copies every overlap of a
-        piece's global range with the owned shard, then re-pulls (all-gather) the parameters."""
-        lo, hi = self.base, min(self.base + self.shard, self.n_params)
-        dst = {"master": self.master, "m": self.m, "v": self.v}
-        for meta, arrays in pieces:
-            a, b = max(lo, meta["base"]), min(hi, meta["base"] + meta["rows"])
-            if a >= b:
-                continue
-            for name, t in arrays.items():
-                d = dst.get(name)
-                if d is not None:
-                    d[a - lo: b - lo].copy_(t.reshape(-1)[a - meta["base"]: b - meta["base"]])
+    def restore_range(self):
+        """Global element range [lo, hi) this rank restores (checkpoint.Checkpointer.load)."""
+        return self.base, max(self.base, min(self.base + self.shard, self.n_params))
+
+    def restore_dst(self):
+        """Device destinations of the checkpointed arrays, [rows, 1] in restore_range order."""
+        return {n: t.view(-1, 1) for n, t in (("master", self.master), ("m", self.m), ("v", self.v))
+                if t is not None}
+
+    def finish_restore(self, clock: int):
+        """After the rows landed: clocks, then re-pull (all-gather) the parameters."""
         self.step = int(clock)
         self.step_dev.fill_(int(clock))
         self.pipe.clock = int(clock)
@@ -404,9 +412,17 @@ class SparseTable:
         """(row table, row index tensor, base) for the rows this rank serves in ``plan``."""
         return self.shard, plan.recv_keys, self.base
 
-    def _owner_rows(self, keys: torch.Tensor):
+    def _owner_rows(self, keys: torch.Tensor, plan=None):
         """(row index tensor, base) of owned unique keys being updated."""
         return keys, self.base
+
+    def _owner_keys(self, plan: SparsePlan):
+        """The owned unique keys a push of ``plan`` updates (exact-count plans only)."""
+        if self.comm.world == 1:
+            return plan.uniq[: plan.cap]
+        if plan.own_uniq is None:
+            return None
+        return plan.own_uniq[: plan.extra.get("own_U", len(plan.recv_keys))]
 
     def _start_plan(self, keys: torch.Tensor, csr: bool = False) -> _PendingPlan:
         """Dedupe + owner bucketing + all-to-all of the per-owner counts, issued on the current
@@ -485,7 +501,8 @@ class SparseTable:
                 return SparsePlan(n, pp.inv, pp.uniq, U, [U], [U], pp.uniq[:U], csr=pp.csr, _U=U)
             return SparsePlan(n, pp.inv, pp.uniq, n, None, None, pp.uniq, U_dev=pp.U_dev, csr=pp.csr)
         if pp.event is not None:
-            pp.event.synchronize()  # the only host wait of a step: the all-to-all splits
+            with self.comm.waiting():
+                pp.event.synchronize()  # the only host wait of a step: the all-to-all splits
         send, recv = pp.host[0].tolist(), pp.host[1].tolist()
         U, M = int(sum(send)), int(sum(recv))
         recv_keys = torch.empty(M, dtype=torch.int64, device=dev)
@@ -590,7 +607,7 @@ class SparseTable:
             g = torch.zeros(n, self.width, dtype=torch.float32, device=dev)
             ops.scatter_add_rows(recv, plan.own_inv, g)
             keys, n_dev = plan.own_uniq, (None if "own_U" in plan.extra else plan.own_U_dev)
-        keys, base = self._owner_rows(keys[:n])
+        keys, base = self._owner_rows(keys[:n], plan)
         self._apply_rows(keys, base, g[:n], n_dev)
 
     def _apply_rows(self, keys, base, g, n_dev=None):
@@ -607,6 +624,10 @@ class SparseTable:
     def drain(self):
         self.pipe.drain()
 
+    def reset_after_rollback(self):
+        self.pipe.reset()
+        self._pending = []
+
     # -- checkpoint hooks (minips_amd.ps.checkpoint) -------------------------------------------
     def shard_state(self):
         self.drain()
@@ -620,17 +641,18 @@ class SparseTable:
                     kind="sparse")
         return meta, arrays
 
-    def load_shard_pieces(self, pieces, clock: int):
-        lo, hi = self.base, self.base + self.rows_local
-        dst = {"params": self.shard, "state": self.state, "state2": self.state2}
-        for meta, arrays in pieces:
-            a, b = max(lo, meta["base"]), min(hi, meta["base"] + meta["rows"])
-            if a >= b:
-                continue
-            for name, t in arrays.items():
-                d = dst.get(name)
-                if d is not None:
-                    d[a - lo: b - lo].copy_(t[a - meta["base"]: b - meta["base"]].reshape(d[a - lo: b - lo].shape))
+    def restore_range(self):
+        return self.base, self.base + self.rows_local
+
+    def restore_dst(self):
+        out = {"params": self.shard}
+        if self.state is not None:
+            out["state"] = self.state.view(-1, 1)
+        if self.state2 is not None:
+            out["state2"] = self.state2.view(-1, 1)
+        return out
+
+    def finish_restore(self, clock: int):
         self.pipe.clock = int(clock)
 
 
@@ -702,54 +724,82 @@ class HashSparseTable(SparseTable):
     def size(self) -> int:
         return int(self.counters[0].item())
 
-    def _slots(self, keys: torch.Tensor) -> torch.Tensor:
+    def _slots(self, keys: torch.Tensor, grow: bool = True) -> torch.Tensor:
+        """Lookup-or-insert. ``grow=False``: the keys are known to be present (no insert, no
+        growth check, no host sync) -- safe inside side-stream clock work."""
         need = keys.numel()
         if need == 0:
             return torch.empty(0, dtype=torch.int64, device=keys.device)
-        if (self.size() + need) > 0.7 * self.capacity:
+        if grow and (self.size() + need) > 0.7 * self.capacity:
             self._grow(max(self.capacity * 2, 1 << int(math.ceil(math.log2((self.size() + need) / 0.5)))))
         slots = torch.empty(need, dtype=torch.int64, device=keys.device)
         ops.hash_slots(self.tab_keys, keys, slots, self.shard, self.init_scale, self.seed, self.counters)
-        if int(self.counters[1].item()):
+        if grow and int(self.counters[1].item()):
             raise RuntimeError("hash table full")
         return slots
 
     def _grow(self, new_cap: int):
+        # The rehash copies the rows on the current stream: every clock issued so far (SSP/ASP
+        # applies on the pipe stream write into the current rows) must land first, and the old
+        # buffers stay reserved for the streams that used them (ADVICE r1: lost updates / reuse).
+        self.pipe.drain()
         old = (self.tab_keys, self.shard, self.state)
         self._alloc(new_cap)
         cnt = torch.zeros(2, dtype=torch.int32, device=self.comm.device)
         ops.hash_rehash(old[0], old[1], old[2], self.tab_keys, self.shard, self.state, cnt)
         self.counters[0] = cnt[0]
+        if self.pipe.stream is not None:
+            for t in old:
+                if t is not None:
+                    t.record_stream(self.pipe.stream)
 
     def _serve_index(self, plan):
         slots = self._slots(plan.recv_keys)  # insert-on-miss: unseen keys get their initial row
         plan.extra["served_slots"] = slots
         return self.shard, slots, 0
 
-    def _owner_rows(self, keys):
-        return self._slots(keys), 0
+    def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
+        """Resolve (insert-on-miss) the owner slots NOW, on the issuing stream: the clock's apply
+        may run on the pipe stream, where a table growth must never happen."""
+        keys = self._owner_keys(plan)
+        if keys is not None and "own_slots" not in plan.extra:
+            plan.extra["own_slots"] = self._slots(keys)
+            plan.extra["own_cap"] = self.capacity
+        super().add(plan, grad_rows)
 
-    # -- checkpoint hooks: (key, row, state) triples of the occupied slots --------------------
+    def _owner_rows(self, keys, plan=None):
+        slots = plan.extra.get("own_slots") if plan is not None else None
+        if slots is None or self.capacity != plan.extra.get("own_cap"):
+            # the table grew after add() (a rehash moves rows): the keys are present, so a
+            # lookup-only probe re-resolves them without any growth on this stream
+            slots = self._slots(keys, grow=False)
+        return slots, 0
+
+    # -- checkpoint hooks: (key, row, state) triples of the occupied slots, sorted by key ------
     def shard_state(self):
+        """Sorted by (mixed) key, so a restore at any world size finds its key range by binary
+        search in the file instead of reading every rank's whole table."""
         self.drain()
-        occ = self.tab_keys >= 0
-        arrays = {"keys": self.tab_keys[occ].view(-1, 1), "params": self.shard[occ]}
+        occ = (self.tab_keys >= 0).nonzero().squeeze(1)
+        keys, order = torch.sort(self.tab_keys[occ])
+        slots = occ[order]
+        arrays = {"keys": keys.view(-1, 1), "params": self.shard[slots]}
         if self.state is not None:
-            arrays["state"] = self.state[occ].view(-1, 1)
-        n = int(occ.sum())
-        meta = dict(global_rows=MASK63, base=0, rows=n, cols=self.width, clock=self.pipe.clock,
+            arrays["state"] = self.state[slots].view(-1, 1)
+        meta = dict(global_rows=MASK63, base=0, rows=int(keys.numel()), cols=self.width, clock=self.pipe.clock,
                     table_id=self.table_id, rank=self.comm.rank, world=self.comm.world, kind="hash")
         return meta, arrays
 
-    def load_shard_pieces(self, pieces, clock: int):
-        lo, hi = self.bounds_list[self.comm.rank], self.bounds_list[self.comm.rank + 1]
-        for meta, arrays in pieces:
-            keys = arrays["keys"].reshape(-1).to(self.comm.device)
-            mine = (keys >= lo) & (keys < hi)
-            if not bool(mine.any()):
-                continue
-            slots = self._slots(keys[mine])
-            self.shard[slots] = arrays["params"].to(self.comm.device)[mine]
-            if self.state is not None and "state" in arrays:
-                self.state[slots] = arrays["state"].reshape(-1).to(self.comm.device)[mine]
+    def restore_range(self):
+        return self.bounds_list[self.comm.rank], self.bounds_list[self.comm.rank + 1]
+
+    def restore_insert(self, chunk: dict):
+        """Insert checkpointed (key, params, state) rows of this rank's key range."""
+        keys = chunk["keys"].reshape(-1)
+        slots = self._slots(keys)
+        self.shard[slots] = chunk["params"].to(self.shard.dtype)
+        if self.state is not None and "state" in chunk:
+            self.state[slots] = chunk["state"].reshape(-1).to(self.state.dtype)
+
+    def finish_restore(self, clock: int):
         self.pipe.clock = int(clock)

@@ -46,7 +46,12 @@ def parse(argv=None):
     ap.add_argument("--heartbeat_dir", default="")
     ap.add_argument("--fail_rank", type=int, default=-1)
     ap.add_argument("--fail_step", type=int, default=-1)
-    ap.add_argument("--fail_mode", default="exit", choices=["exit", "hang"])
+    ap.add_argument("--fail_mode", default="exit", choices=["exit", "hang", "hang_in_step"])
+    ap.add_argument("--recovery", default="inplace", choices=["inplace", "restart"],
+                    help="inplace: after a peer failure the survivors roll back in their processes and "
+                         "the supervisor relaunches only the failed rank; restart: the whole rank set")
+    ap.add_argument("--force_quit_rank", type=int, default=-1,
+                    help="(LR --input) treat this rank's shard as empty: it ForceQuits, the others continue")
     ap.add_argument("--checkpoint_commit", default="eager", choices=["eager", "async"],
                     help="eager: publish a checkpoint at the next step (waits for its files); async: "
                          "publish once every rank's writer finished (training never waits for the disk)")
@@ -73,7 +78,9 @@ SMALL_CARDS = [50, 7, 300, 20, 5, 60, 90, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19
 
 
 def build(args, comm):
-    """-> (model, tables {id: table}, data stream with next()/skip(), step fn(batch) -> loss, samples/step)."""
+    """-> (model, tables {id: table}, make_data() -> a fresh data stream with next()/skip(), step
+    fn(batch) -> loss, samples/step). A fresh stream + skip(k) repositions the data at iteration k
+    (restart and in-place rollback)."""
     dev = comm.device
     r = comm.rank
     seed = args.seed * 1000 + r
@@ -85,16 +92,16 @@ def build(args, comm):
                              **({"cards": SMALL_CARDS} if args.small else {}))
         m = WideDeep(cfg, comm)
         B = args.batch or (64 if args.small else 16384)
-        data = CriteoSynth(B, cards=cfg.cards, device=dev, seed=seed)
-        return m, {0: m.emb, 1: m.dense}, data, (lambda b: m.train_step(*b)), B
+        return m, {0: m.emb, 1: m.dense}, (lambda: CriteoSynth(B, cards=cfg.cards, device=dev, seed=seed)), \
+            (lambda b: m.train_step(*b)), B
     if args.model == "mlp":
         from .data.synthetic import MnistSynth
         from .models.mlp import MLP, MLPConfig
 
         m = MLP(MLPConfig(consistency=args.consistency, staleness=args.staleness), comm)
         B = args.batch or (64 if args.small else 8192)
-        data = _Skippable(MnistSynth(B, device=dev, seed=seed))
-        return m, {0: m.table}, data, (lambda b: m.train_step(*b)[0]), B
+        return m, {0: m.table}, (lambda: _Skippable(MnistSynth(B, device=dev, seed=seed))), \
+            (lambda b: m.train_step(*b)[0]), B
     if args.model == "dlrm":
         from .models.dlrm import DLRM, DLRMConfig
 
@@ -102,8 +109,8 @@ def build(args, comm):
                          staleness=args.staleness)
         m = DLRM(cfg, comm)
         B = args.batch or (64 if args.small else 16384)
-        data = _Skippable(_DLRMData(B, cfg, dev, seed))
-        return m, {0: m.emb, 1: m.dense}, data, (lambda b: m.train_step(*b)), B
+        return m, {0: m.emb, 1: m.dense}, (lambda: _Skippable(_DLRMData(B, cfg, dev, seed))), \
+            (lambda b: m.train_step(*b)), B
     if args.model == "gpt2":
         from .data.synthetic import TokenSynth
         from .models.gpt2 import GPT2, GPT2Config
@@ -112,16 +119,15 @@ def build(args, comm):
         cfg = GPT2Config(consistency=args.consistency, staleness=args.staleness, **kw)
         m = GPT2(cfg, comm)
         B = args.batch or (2 if args.small else 8)
-        data = _Skippable(TokenSynth(B, cfg.n_ctx, vocab=cfg.vocab, device=dev, seed=seed))
-        return m, {0: m.table}, data, (lambda b: m.train_step(*b)), B * cfg.n_ctx
+        return m, {0: m.table}, (lambda: _Skippable(TokenSynth(B, cfg.n_ctx, vocab=cfg.vocab, device=dev, seed=seed))), \
+            (lambda b: m.train_step(*b)), B * cfg.n_ctx
     if args.model == "lr" and args.input:
         # reference LR on a libsvm file (lr_example.cpp --input): this rank's shard is loaded by the
         # native block assigner / mmap reader and kept resident in HBM; batches are consecutive
         # rows from a random start (lib/batch_data_sampler.cpp), cut on the device
-        from .data.loader import LibsvmData
         from .models.lr import SparseLR, SparseLRConfig
 
-        shard = LibsvmData(args.input, r, comm.world).to(dev)
+        shard = args._shard.to(dev)
         nd = args.num_dims
         if not nd:  # every rank must size the table alike: max feature id over all shards
             t = torch.tensor([float(shard.cols.max()) + 1 if shard.cols.numel() else 1.0], device=dev)
@@ -130,7 +136,7 @@ def build(args, comm):
         m = SparseLR(SparseLRConfig(num_dims=nd, alpha=args.alpha, consistency=args.consistency,
                                     staleness=args.staleness, storage=args.kStorageType), comm)
         B = args.batch or 1024
-        return m, {0: m.table}, _Skippable(_Batches(shard, B, seed)), (lambda b: -m.train_step(*b)), B
+        return m, {0: m.table}, (lambda: _Skippable(_Batches(shard, B, seed))), (lambda b: -m.train_step(*b)), B
     if args.model == "lr":
         from .data.synthetic import SparseLRSynth
         from .models.lr import SparseLR, SparseLRConfig
@@ -139,8 +145,9 @@ def build(args, comm):
         m = SparseLR(SparseLRConfig(num_dims=nd, alpha=args.alpha, consistency=args.consistency,
                                     staleness=args.staleness, storage=args.kStorageType), comm)
         B = args.batch or (128 if args.small else 65536)
-        data = _Skippable(SparseLRSynth(B, num_dims=nd, nnz=16 if args.small else 64, device=dev, seed=seed))
-        return m, {0: m.table}, data, (lambda b: -m.train_step(*b)), B
+        return m, {0: m.table}, \
+            (lambda: _Skippable(SparseLRSynth(B, num_dims=nd, nnz=16 if args.small else 64, device=dev, seed=seed))), \
+            (lambda b: -m.train_step(*b)), B
     if args.model == "kmeans":
         from .models.kmeans import KMeans, KMeansConfig
 
@@ -151,8 +158,7 @@ def build(args, comm):
         # seeding reads its own batch of local data (rank 0's seeds are broadcast)
         init = _GaussData(max(B, cfg.K), cfg.dims, dev, seed + 7919).next() if args.kmeans_init_mode else None
         m = KMeans(cfg, comm, init_data=init)
-        data = _Skippable(_GaussData(B, cfg.dims, dev, seed))
-        return m, {0: m.table}, data, (lambda b: m.train_step(b)), B
+        return m, {0: m.table}, (lambda: _Skippable(_GaussData(B, cfg.dims, dev, seed))), (lambda b: m.train_step(b)), B
     raise ValueError(args.model)
 
 
@@ -198,6 +204,58 @@ class _GaussData:
         return torch.randn(self.B, self.D, generator=self.g, device=self.dev)
 
 
+def _is_comm_failure(e: BaseException) -> bool:
+    """A collective failed because a peer died / the communicator was aborted (gloo: connection
+    closed or reset; RCCL with TORCH_NCCL_ASYNC_ERROR_HANDLING=2: aborted / timed out)."""
+    msg = f"{type(e).__name__}: {e}"
+    return any(k in msg for k in ("Connection closed", "Connection reset", "Broken pipe", "DistBackendError",
+                                  "NCCL", "aborted", "timed out", "Timed out", "Gloo", "peer"))
+
+
+def _force_quit(comm, has_data: bool, rank: int):
+    """Graceful degradation (reference lr_example.cpp:145-152, mailbox.cpp:159-171): a rank with
+    no data leaves and the others continue among themselves. Every rank learns every rank's flag
+    (one all-gather), the survivors form a sub-group (collective over the full group); a quitting
+    rank returns None. Survivors get a Comm over their group: the tables are built on it, so
+    they are sharded over the survivors only."""
+    from .ps.comm import Comm
+    from .utils import metrics
+
+    if comm.world == 1:
+        return comm
+    flags = torch.empty(comm.world, dtype=torch.float32, device=comm.device)
+    comm.all_gather(flags, torch.tensor([1.0 if has_data else 0.0], device=comm.device))
+    survivors = [r for r, f in enumerate(flags.tolist()) if f > 0]
+    if len(survivors) == comm.world:
+        return comm
+    if not survivors:
+        raise RuntimeError("no rank has any data")
+    quitters = sorted(set(range(comm.world)) - set(survivors))
+    if rank == survivors[0]:
+        metrics.fault_tolerance_phase(2, f"kForceQuit from ranks {quitters} (no data); {len(survivors)} ranks continue")
+    group = dist.new_group(survivors)
+    if not has_data:
+        print(f"[rank {rank}] kForceQuit: no data, leaving the job", file=sys.stderr, flush=True)
+        return None
+    return Comm(group=group, device=comm.device)
+
+
+def _wait_directive(hb_dir: str, generation: int, timeout: float = 300.0) -> dict:
+    """Rollback directive of the supervisor (minips_amd.elastic): a newer generation with the
+    rendezvous port of the re-formed group (the reference's kRollBack, mailbox.cpp:172-191)."""
+    path = os.path.join(hb_dir, "rollback.json")
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            d = json.loads(open(path).read())
+            if int(d["generation"]) > generation:
+                return d
+        except (OSError, ValueError, KeyError):
+            pass
+        time.sleep(0.05)
+    raise TimeoutError("no rollback directive from the supervisor")
+
+
 def main(argv=None):
     args = parse(argv)
     from .ps.checkpoint import Checkpointer
@@ -207,18 +265,43 @@ def main(argv=None):
 
     if args.metrics_dir:
         os.environ["MINIPS_METRICS_DIR"] = args.metrics_dir
+    inplace = args.recovery == "inplace" and bool(args.heartbeat_dir)
+    if inplace:  # RCCL: a dead peer aborts the communicator and raises, instead of killing us
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
     comm = init_distributed()
     rank = comm.rank
-    hb = Heartbeat(args.heartbeat_dir, rank, args.heartbeat_interval) \
+    generation = int(os.environ.get("MINIPS_GENERATION", "0"))
+    hb = Heartbeat(args.heartbeat_dir, rank, args.heartbeat_interval, state_fn=lambda: comm.state()) \
         if args.heartbeat_interval > 0 and args.heartbeat_dir else None
-    model, tables, data, step_fn, per_step = build(args, comm)
+    if args.model == "lr" and args.input:
+        from .data.loader import LibsvmData
+
+        args._shard = LibsvmData(args.input, comm.rank, comm.world)
+        sub = _force_quit(comm, args._shard.n > 0 and args.force_quit_rank != rank, rank)
+        if sub is None:
+            if hb:
+                hb.stop()
+            dist.destroy_process_group()
+            return 0
+        if sub is not comm:
+            comm = sub
+            inplace = False  # a sub-group job restarts as a whole (its ranks are a subset)
+    model, tables, make_data, step_fn, per_step = build(args, comm)
+    data = make_data()
     ck = Checkpointer(comm, args.checkpoint_file_prefix)
     start = 0
-    if args.use_weight_file:
+    if args.use_weight_file and not ck.exists():
+        # a restart before the first committed checkpoint (or with checkpoint_toggle off): there
+        # is nothing to roll back to, so the relaunched job starts over
+        print(f"[rank {rank}] --use_weight_file but no committed checkpoint under "
+              f"{args.checkpoint_file_prefix!r}: starting from iteration 0", file=sys.stderr, flush=True)
+    elif args.use_weight_file:
         start = ck.load(tables)
         data.skip(start)
         failed = int(os.environ.get("MINIPS_FAILED_RANK", "-1"))
         metrics.fault_tolerance_phase(4 if rank == failed else 5, f"rank {rank} restored iteration {start}")
+    if hb:
+        hb.progress(start - 1)
     inj = FaultInjector(rank, args.fail_rank, args.fail_step, args.with_injected_straggler, args.seed,
                         mode=args.fail_mode, heartbeat=hb)
     log = metrics.get_logger()
@@ -226,31 +309,82 @@ def main(argv=None):
     report = open(args.report_prefix + f"report_{rank}", "a") if args.report_prefix else None
     t_start = time.perf_counter()
     t_steady, n_steady = None, 0
-    for it in range(start, args.steps):
-        if it == start + args.timing_skip:
-            if comm.device.type == "cuda":
-                torch.cuda.synchronize(comm.device)
-            t_steady, n_steady = time.perf_counter(), args.steps - it
-        if args.checkpoint_commit == "async":
-            ck.try_commit()  # publishes an in-flight checkpoint once every rank's files are written
-        else:
-            ck.commit()  # publishes the checkpoint issued after the previous step (no-op otherwise)
-        inj.step(it)
-        t0 = time.perf_counter()
-        with metrics.range(f"step {it}"):
-            loss = step_fn(data.next())
-        if (it + 1) % 10 == 0 or it + 1 == args.steps:
-            lv = float(loss.float().sum()) / per_step
-            losses.append((it, lv))
-            log.step(it, per_step, time.perf_counter() - t0, comm.stats, loss=lv)
-            if rank == 0:
-                print(f"Current iteration={it + 1} on node={rank} loss={lv:.5f}", flush=True)
-        if report and (it + 1) % args.report_interval == 0:
-            report.write(f"{it + 1}\t{(time.perf_counter() - t_start) * 1e3:.1f}\n")
-            report.flush()
-        if args.checkpoint_toggle and args.checkpoint_every > 0 and (it + 1) % args.checkpoint_every == 0 \
-                and it + 1 < args.steps:
-            ck.save(tables, iteration=it + 1)
+
+    def rollback():
+        """Survivor side of an in-place recovery (reference: mailbox.cpp:172-191 kRollBack ->
+        RollBackServer / RollBackWorker): drop the broken communicator, join the re-formed group
+        on the supervisor's new rendezvous, restore every table from the last committed
+        checkpoint and reposition the data; the relaunched rank restores the same iteration."""
+        nonlocal generation, data, losses
+        hb.state = "recover"
+        ck.abandon()
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001 - the group is already broken
+            pass
+        d = _wait_directive(args.heartbeat_dir, generation)
+        generation = int(d["generation"])
+        os.environ["MASTER_PORT"] = str(d["port"])
+        os.environ["MINIPS_GENERATION"] = str(generation)
+        dist.destroy_process_group() if dist.is_initialized() else None
+        init_distributed()
+        comm.refresh()
+        for t in tables.values():
+            t.reset_after_rollback()
+        if hasattr(model, "_pending_plans"):
+            model._pending_plans = []  # planned on the broken communicator
+        if not ck.exists():
+            raise RuntimeError("in-place rollback needs a committed checkpoint")
+        it0 = ck.load(tables)
+        data = make_data()
+        data.skip(it0)
+        losses = [x for x in losses if x[0] < it0]
+        metrics.fault_tolerance_phase(5, f"rank {rank} rolled back in place to iteration {it0} "
+                                         f"(failed rank {d.get('failed_rank')}, generation {generation})")
+        hb.state = "run"
+        hb.progress(it0 - 1)
+        return it0
+
+    it = start
+    while it < args.steps:
+        try:
+            if it == start + args.timing_skip and t_steady is None:
+                if comm.device.type == "cuda":
+                    torch.cuda.synchronize(comm.device)
+                t_steady, n_steady = time.perf_counter(), args.steps - it
+            if args.checkpoint_commit == "async":
+                ck.try_commit()  # publishes an in-flight checkpoint once every rank's files are written
+            else:
+                ck.commit()  # publishes the checkpoint issued after the previous step (no-op otherwise)
+            inj.step(it)
+            t0 = time.perf_counter()
+            with metrics.range(f"step {it}"):
+                batch = data.next()
+                inj.in_step(it)
+                loss = step_fn(batch)
+            if (it + 1) % 10 == 0 or it + 1 == args.steps:
+                with comm.waiting():
+                    lv = float(loss.float().sum()) / per_step
+                losses.append((it, lv))
+                log.step(it, per_step, time.perf_counter() - t0, comm.stats, loss=lv)
+                if rank == 0:
+                    print(f"Current iteration={it + 1} on node={rank} loss={lv:.5f}", flush=True)
+            if report and (it + 1) % args.report_interval == 0:
+                report.write(f"{it + 1}\t{(time.perf_counter() - t_start) * 1e3:.1f}\n")
+                report.flush()
+            if args.checkpoint_toggle and args.checkpoint_every > 0 and (it + 1) % args.checkpoint_every == 0 \
+                    and it + 1 < args.steps:
+                ck.save(tables, iteration=it + 1)
+            if hb:
+                hb.progress(it)
+            it += 1
+        except Exception as e:  # noqa: BLE001
+            if not (inplace and hb is not None and comm.world > 1 and _is_comm_failure(e)):
+                raise
+            print(f"[rank {rank}] collective failed at iteration {it} ({type(e).__name__}): rolling back in place",
+                  file=sys.stderr, flush=True)
+            it = rollback()
+            t_steady = None
     model.drain()
     if comm.device.type == "cuda":
         torch.cuda.synchronize(comm.device)
@@ -271,14 +405,15 @@ def main(argv=None):
         torch.cuda.synchronize(comm.device)
     if hb:
         hb.stop()
-    if rank == 0:
+    if comm.rank == 0:
         print(json.dumps(dict(model=args.model, steps=args.steps, start=start, losses=losses,
                               checksum=[round(float(x), 6) for x in sums.cpu()],
                               total_ms=round((time.perf_counter() - t_start) * 1e3, 1),
-                              steady_ms_per_iter=round(steady_ms, 4) if steady_ms is not None else None)),
+                              steady_ms_per_iter=round(steady_ms, 4) if steady_ms is not None else None,
+                              world=comm.world, generation=generation)),
               flush=True)
     if comm.world > 1:
-        dist.barrier()
+        comm.barrier()
         dist.destroy_process_group()
     return 0
 

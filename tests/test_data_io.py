@@ -110,4 +110,11 @@ def test_train_driver_lr_map_storage_matches_vector():
         assert r.returncode == 0, r.stderr[-2000:]
         out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
         res[st] = (out["losses"], out["checksum"])
-    assert res["Map"] == res["Vector"], res  # same training and the same parameter sum
+    # same training and the same parameter sum; on a GPU the delta sums use fp32 atomics and the
+    # two storages order their unique keys differently, so compare with a float tolerance
+    (lm, cm), (lv, cv) = res["Map"], res["Vector"]
+    assert [i for i, _ in lm] == [i for i, _ in lv]
+    for (_, a), (_, b) in zip(lm, lv):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(b)), res
+    for a, b in zip(cm, cv):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), res

@@ -1,24 +1,32 @@
-"""Fault injection end to end: 2 gloo ranks train under the elastic
-supervisor with periodic checkpoints; rank 1 is killed mid-run (--fail_rank/--fail_step), the
-supervisor detects it (Phase2), relaunches the rank set from the last committed checkpoint (Phase3),
-the ranks restore (Phase4/5) and finish; the final parameters equal an uninterrupted run's."""
+"""Fault injection end to end under the elastic supervisor, gloo ranks:
+
+* restart: rank 1 dies, the whole rank set is relaunched from the last committed checkpoint;
+* in-place (the reference's rollback, comm/mailbox.cpp:172-191): at 4 ranks rank 1 dies, only it
+  is relaunched, the 3 survivors roll back inside their processes;
+* a rank stuck INSIDE a step (heartbeat thread untouched) is detected by the progress check
+  within 3 x interval and recovered in place;
+* kForceQuit: ranks with no data leave, the others finish among themselves.
+Every recovered run ends with exactly the parameters of an uninterrupted run (BSP)."""
 import json
 import os
+import re
 import subprocess
 import sys
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HB = 0.5
 
 
-def _run(tmp, extra, name):
-    cmd = [sys.executable, "-m", "minips_amd.elastic", "--nproc", "2", "--heartbeat_interval", "0.5",
-           "--max_restarts", "2", "--run_dir", str(tmp / f"run_{name}"), "--log_dir", str(tmp / f"log_{name}"), "--",
-           sys.executable, "-m", "minips_amd.train", "--small=1", "--steps", "12", "--checkpoint_toggle=1",
-           "--checkpoint_every", "4", f"--checkpoint_file_prefix={tmp}/ck_{name}/", *extra]
-    env = dict(os.environ, PYTHONPATH=ROOT)
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+def _run(tmp, extra, name, nproc=2, recovery="restart", train_extra=()):
+    cmd = [sys.executable, "-m", "minips_amd.elastic", "--nproc", str(nproc), "--heartbeat_interval", str(HB),
+           "--max_restarts", "2", "--recovery", recovery, "--run_dir", str(tmp / f"run_{name}"), "--log_dir",
+           str(tmp / f"log_{name}"), "--", sys.executable, "-m", "minips_amd.train", "--small=1", "--steps", "12",
+           "--checkpoint_toggle=1", "--checkpoint_every", "4", f"--checkpoint_file_prefix={tmp}/ck_{name}/",
+           *extra, *train_extra]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     logs = {}
     for f in sorted(os.listdir(tmp / f"log_{name}")):
         logs[f] = open(tmp / f"log_{name}" / f).read()
@@ -26,7 +34,7 @@ def _run(tmp, extra, name):
 
 
 def _summary(logs):
-    last = [l for l in logs[max(k for k in logs if k.startswith("rank0_"))].splitlines() if l.startswith("{")]
+    last = [l for k in sorted(logs) if k.startswith("rank0_") for l in logs[k].splitlines() if l.startswith("{")]
     return json.loads(last[-1])
 
 
@@ -45,3 +53,62 @@ def test_kill_rank_restart_restore(tmp_path, model):
     assert b["start"] == 8  # resumed from the checkpoint committed after iteration 8
     assert a["checksum"] == b["checksum"], (a, b)
     assert a["losses"][-1] == b["losses"][-1]
+
+
+def test_kill_rank_inplace_rollback_four_ranks(tmp_path):
+    """4 ranks: rank 1 exits at step 9; only it is relaunched, ranks 0, 2, 3 roll back in place
+    (same processes: rank 0 writes a single log file) to the committed iteration 8."""
+    ref, ref_logs = _run(tmp_path, ["--model=widedeep"], "ref4", nproc=4, recovery="inplace")
+    assert ref.returncode == 0, ref.stderr[-3000:]
+    got, logs = _run(tmp_path, ["--model=widedeep", "--fail_rank=1", "--fail_step=9"], "ip4", nproc=4,
+                     recovery="inplace")
+    assert got.returncode == 0, (got.stderr[-3000:], logs)
+    assert "rank 1 failed" in got.stderr and "survivors roll back in place" in got.stderr
+    assert sorted(k for k in logs if k.startswith("rank0_")) == ["rank0_attempt0.log"]  # never relaunched
+    for r in (0, 2, 3):
+        assert "rolled back in place to iteration 8" in logs[f"rank{r}_attempt0.log"], logs[f"rank{r}_attempt0.log"]
+    assert "[Fault Tolerance][Phase4]" in logs["rank1_attempt1.log"]
+    a, b = _summary(ref_logs), _summary(logs)
+    assert b["generation"] == 1 and b["world"] == 4
+    assert a["checksum"] == b["checksum"], (a, b)
+    assert a["losses"][-1] == b["losses"][-1]
+
+
+def test_hang_inside_step_detected_by_progress(tmp_path):
+    """Rank 1 blocks inside step 6 while its heartbeat thread keeps stamping: the progress check
+    (not the stamp age) detects it within 3 x interval (+ one poll), and the job recovers."""
+    ref, ref_logs = _run(tmp_path, ["--model=widedeep"], "refh", nproc=2, recovery="inplace")
+    assert ref.returncode == 0, ref.stderr[-3000:]
+    got, logs = _run(tmp_path, ["--model=widedeep", "--fail_rank=1", "--fail_step=6", "--fail_mode=hang_in_step"],
+                     "hang", nproc=2, recovery="inplace")
+    assert got.returncode == 0, (got.stderr[-3000:], logs)
+    m = re.search(r"\[fault injection\]\[(\d+)\] rank 1 hangs inside step 6", logs["rank1_attempt0.log"])
+    d = re.search(r"\[Fault Tolerance\]\[Phase2\]\[(\d+)\].*rank 1 failed.*stuck inside a step", got.stderr)
+    assert m and d, (got.stderr[-2000:], logs["rank1_attempt0.log"][-2000:])
+    delay = (int(d.group(1)) - int(m.group(1))) / 1000.0
+    assert delay <= 3 * HB + 1.0, delay
+    assert _summary(ref_logs)["checksum"] == _summary(logs)["checksum"]
+
+
+def test_force_quit_rank_without_data(tmp_path):
+    """kForceQuit (lr_example.cpp:145-152): LR over libsvm files; ranks 2 and 3 get no data, leave,
+    and ranks 0 and 1 train to the end as a 2-rank group (tables sharded over the survivors)."""
+    d = tmp_path / "svm"
+    d.mkdir()
+    import random
+
+    rng = random.Random(0)
+    for name in ("a.txt", "b.txt"):
+        with open(d / name, "w") as f:
+            for _ in range(200):
+                feats = sorted(rng.sample(range(1, 300), 8))
+                f.write(("+1" if rng.random() < 0.5 else "-1") + "".join(f" {j}:{rng.random():.3f}" for j in feats) +
+                        "\n")
+    got, logs = _run(tmp_path, ["--model=lr", f"--input={d}", "--num_dims=300", "--batch_size=32"], "fq", nproc=4,
+                     recovery="inplace")
+    assert got.returncode == 0, (got.stderr[-3000:], logs)
+    out = _summary(logs)
+    assert out["world"] == 2, out
+    quit_logs = logs["rank2_attempt0.log"] + logs["rank3_attempt0.log"]
+    assert quit_logs.count("kForceQuit: no data") == 2
+    assert "kForceQuit from ranks [2, 3]" in logs["rank0_attempt0.log"]

@@ -98,3 +98,29 @@ def test_hash_kernel_matches_cpu(dev):
         rb = b[1][b[2]]
         torch.testing.assert_close(ra, rb, rtol=1e-6, atol=1e-7)
         assert torch.equal(a[0][a[2]], q) and torch.equal(b[0][b[2]], q)
+
+
+@pytest.mark.gpu
+def test_hash_table_ssp_growth_matches_bsp(dev):
+    """Map storage under SSP (clock applies on the side stream, staleness 1) with key sets that
+    force several rehashes: no update is lost, the final rows equal the BSP table's."""
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.tables import HashSparseTable
+
+    comm = Comm(device=dev)
+    res = {}
+    for mode, s in (("bsp", 0), ("ssp", 1)):
+        t = HashSparseTable(comm, width=4, capacity=16, consistency=mode, staleness=s)
+        assert t.pipe.async_ == (mode == "ssp")
+        caps = []
+        for step in range(12):
+            keys = torch.arange(step * 40, step * 40 + 60, device=dev) * 7919  # 40 new keys a step: growth
+            t.get_rows(keys)
+            t.add_keys(keys, torch.full((keys.numel(), 4), float(step + 1), device=dev))
+            t.clock()
+            caps.append(t.capacity)
+        t.drain()
+        allk = torch.arange(0, 11 * 40 + 60, device=dev) * 7919
+        res[mode] = (t.get_rows(allk).cpu(), caps)
+    assert len(set(res["ssp"][1])) >= 3  # the SSP table really grew several times
+    assert torch.equal(res["bsp"][0], res["ssp"][0])
