@@ -36,6 +36,10 @@ class DLRMConfig:
     consistency: str = "asp"
     staleness: int = 0
     p2p: bool = True
+    # "collective": SparseTable / DenseTable over RCCL (all-to-all-v / RS+AG, gated per consistency);
+    # "onesided": SSP / ASP async SGD with NO collective on the data path -- rows gathered from and
+    # atomically added into the owners' IPC-mapped HBM over xGMI (ps/onesided.py)
+    transport: str = "collective"
     seed: int = 0
     cards: list = field(default_factory=list)  # optional per-feature cardinalities (sum <= num_rows)
 
@@ -45,9 +49,16 @@ class DLRM:
         self.cfg, self.comm = cfg, comm
         D, F = cfg.D, cfg.F
         self.NV = F + 1
-        self.emb = SparseTable(comm, cfg.num_rows, D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
-                               consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01, seed=cfg.seed,
-                               p2p=cfg.p2p)
+        if cfg.transport == "onesided":
+            from ..ps.onesided import OneSidedSparseTable
+
+            self.emb = OneSidedSparseTable(comm, cfg.num_rows, D, optimizer="sgd", lr=cfg.lr_sparse,
+                                           consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
+                                           seed=cfg.seed)
+        else:
+            self.emb = SparseTable(comm, cfg.num_rows, D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
+                                   consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
+                                   seed=cfg.seed, p2p=cfg.p2p)
         self.layout = ParamLayout()
         dims = [cfg.n_dense, *cfg.bottom, D]
         self.bottom = [Linear(self.layout, f"bot{i}", dims[i], dims[i + 1]) for i in range(len(dims) - 1)]
@@ -55,8 +66,14 @@ class DLRM:
         tdims = [self.n_int, *cfg.top]
         self.top = [Linear(self.layout, f"top{i}", tdims[i], tdims[i + 1]) for i in range(len(tdims) - 1)]
         self.layout.add("head", (cfg.top[-1] + 8,))
-        self.dense = DenseTable(comm, self.layout.size, optimizer="adam", lr=cfg.lr_dense,
-                                consistency=cfg.consistency, staleness=cfg.staleness, p2p=False)
+        if cfg.transport == "onesided":
+            from ..ps.onesided import OneSidedDenseTable
+
+            self.dense = OneSidedDenseTable(comm, self.layout.size, lr=cfg.lr_dense * 10,
+                                            consistency=cfg.consistency, staleness=cfg.staleness)
+        else:
+            self.dense = DenseTable(comm, self.layout.size, optimizer="adam", lr=cfg.lr_dense,
+                                    consistency=cfg.consistency, staleness=cfg.staleness, p2p=False)
         g = torch.Generator().manual_seed(cfg.seed + 3)
         full = torch.zeros(self.layout.size)
         for l in self.bottom + self.top:

@@ -50,6 +50,8 @@ def parse(argv=None):
     ap.add_argument("--recovery", default="inplace", choices=["inplace", "restart"],
                     help="inplace: after a peer failure the survivors roll back in their processes and "
                          "the supervisor relaunches only the failed rank; restart: the whole rank set")
+    ap.add_argument("--transport", default="collective", choices=["collective", "onesided"],
+                    help="DLRM SSP/ASP data path: RCCL collectives, or one-sided IPC row access (ps/onesided.py)")
     ap.add_argument("--force_quit_rank", type=int, default=-1,
                     help="(LR --input) treat this rank's shard as empty: it ForceQuits, the others continue")
     ap.add_argument("--checkpoint_commit", default="eager", choices=["eager", "async"],
@@ -106,7 +108,7 @@ def build(args, comm):
         from .models.dlrm import DLRM, DLRMConfig
 
         cfg = DLRMConfig(num_rows=20000 if args.small else 100_000_000, consistency=args.consistency,
-                         staleness=args.staleness)
+                         staleness=args.staleness, transport=args.transport)
         m = DLRM(cfg, comm)
         B = args.batch or (64 if args.small else 16384)
         return m, {0: m.emb, 1: m.dense}, (lambda: _Skippable(_DLRMData(B, cfg, dev, seed))), \
