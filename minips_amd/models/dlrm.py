@@ -54,7 +54,7 @@ class DLRM:
 
             self.emb = OneSidedSparseTable(comm, cfg.num_rows, D, optimizer="sgd", lr=cfg.lr_sparse,
                                            consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
-                                           seed=cfg.seed)
+                                           seed=cfg.seed, pull_dtype=torch.bfloat16)
         else:
             self.emb = SparseTable(comm, cfg.num_rows, D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
                                    consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
