@@ -45,6 +45,9 @@ class GPT2Config:
     consistency: str = "bsp"
     staleness: int = 0
     seed: int = 0
+    # multi-rank: per-layer gradient buckets (~28 MB each at GPT-2 small) reduced + applied +
+    # re-gathered as soon as the layer's backward finished (DenseTable bucket_ready)
+    bucketed: bool = True
 
     @property
     def vocab_pad(self):
@@ -73,8 +76,11 @@ class GPT2:
             self.blocks.append(blk)
         L.add("lnf_g", (d,))
         L.add("lnf_b", (d,))
+        starts = [L.entries[f"h{i}.ln1_g"][0] for i in range(cfg.n_layer)] if cfg.bucketed else None
         self.table = DenseTable(comm, L.size, optimizer="adam", lr=cfg.lr, consistency=cfg.consistency,
-                                staleness=cfg.staleness, weight_decay=cfg.weight_decay, betas=(0.9, 0.95))
+                                staleness=cfg.staleness, weight_decay=cfg.weight_decay, betas=(0.9, 0.95),
+                                buckets=starts)
+        self._layer_bucket = [self.table.bucket_for_layer(x) for x in starts] if starts else None
         g = torch.Generator().manual_seed(cfg.seed)
         full = torch.zeros(L.size)
         L.view(full, "wte")[: cfg.vocab].normal_(0.0, 0.02, generator=g)
@@ -203,6 +209,8 @@ class GPT2:
             side.wait(ev_dx)
             ops.layernorm_bwd(x[i], dh, d, v(P, blk["ln1_g"]), m1, r1, dx, v(G, blk["ln1_g"]), v(G, blk["ln1_b"]),
                               accumulate=True)
+            if self._layer_bucket is not None:  # layer i's gradients are final: send its bucket
+                self.table.bucket_ready(self._layer_bucket[i], events=(side.mark(),))
         side.join()  # embed_bwd accumulates into the wte gradient the LM-head wgrad wrote
         ops.embed_bwd(dx, tokens, T, v(G, "wte"), v(G, "wpe"))
         self.table.add()

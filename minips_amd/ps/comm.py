@@ -33,7 +33,7 @@ import contextlib
 import datetime
 import os
 import threading
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
@@ -45,9 +45,11 @@ class CommStats:
     bytes_rs: int = 0
     bytes_ag: int = 0
     calls: int = 0
+    bucket_bytes: dict = field(default_factory=dict)  # "t<table>b<k>" -> RS + AG bytes (bucketed clocks)
 
     def as_dict(self):
-        return dict(bytes_a2a=self.bytes_a2a, bytes_rs=self.bytes_rs, bytes_ag=self.bytes_ag, calls=self.calls)
+        return dict(bytes_a2a=self.bytes_a2a, bytes_rs=self.bytes_rs, bytes_ag=self.bytes_ag, calls=self.calls,
+                    bucket_bytes=dict(self.bucket_bytes))
 
 
 class Comm:

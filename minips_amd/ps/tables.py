@@ -132,10 +132,19 @@ class DenseTable:
     def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
                  pull_dtype=torch.bfloat16, consistency: str = "bsp", staleness: int = 0, table_id: int = 0,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, p2p: bool = False,
-                 value_dtype=torch.float32):
+                 value_dtype=torch.float32, buckets=None):
         """``value_dtype`` float64 gives the reference's ``double`` tables (KVClientTable<double>
         with VectorStorage::SubAdd, server/vector_storage.hpp:28-38): optimizer "add" only, pulled
-        in fp64, so BSP sums are exact for exactly representable deltas."""
+        in fp64, so BSP sums are exact for exactly representable deltas.
+
+        ``buckets`` (multi-rank): element offsets where the model's layers start. The clock then
+        runs per bucket -- reduce-scatter of the bucket's gradient, the optimizer on the owned
+        slice, all-gather of the bucket's parameters -- and a bucket is issued as soon as the
+        model calls ``bucket_ready(k)`` during its backward, so the communication of the late
+        layers overlaps the backward of the early ones (SURVEY §5.8 bucket sizing: per-layer
+        buckets of 8-64 MB). Ownership is then bucket-major: rank r owns the r-th slice of every
+        bucket (the shard buffers are those slices in bucket order); checkpoints keep the
+        canonical contiguous layout (shard_state / finish_restore convert)."""
         if value_dtype not in (torch.float32, torch.float64):
             raise ValueError(f"value_dtype {value_dtype}")
         if value_dtype == torch.float64:
@@ -171,6 +180,111 @@ class DenseTable:
         # t's gradients while the compute stream already writes clock t+1's.
         self._ring = [self.grad] + [torch.zeros_like(self.grad) for _ in range(self.pipe.staleness + 1)] \
             if self.pipe.async_ else [self.grad]
+        self.buckets = None
+        if buckets is not None and comm.world > 1:
+            self._init_buckets(buckets)
+
+    # -- bucketed clocks ----------------------------------------------------------------------
+    def _init_buckets(self, starts):
+        W = self.comm.world
+        unit = 64 * W
+        # a bucket starts at the first aligned offset at or after a layer start: it then holds the
+        # tail of its layer plus at most `unit` elements of the NEXT layer, whose backward finished
+        # earlier -- so a bucket is complete when its own layer's backward is
+        edges = sorted({0, self.n_pad} | {min(self.n_pad, -(-int(x) // unit) * unit) for x in starts})
+        self.buckets = [(a, b) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+        self._boff, off = [], 0
+        for lo, hi in self.buckets:
+            self._boff.append((off, (hi - lo) // W))
+            off += (hi - lo) // W
+        assert off == self.shard
+        self._issued: set = set()
+
+    def bucket_of(self, offset: int) -> int:
+        """Index of the bucket holding element ``offset``."""
+        for k, (lo, hi) in enumerate(self.buckets):
+            if lo <= offset < hi:
+                return k
+        raise IndexError(offset)
+
+    def bucket_for_layer(self, start: int) -> int | None:
+        """The bucket a layer starting at element ``start`` completes (None: not bucketed)."""
+        if self.buckets is None:
+            return None
+        unit = 64 * self.comm.world
+        return self.bucket_of(min(self.n_pad - 1, -(-int(start) // unit) * unit))
+
+    def _own_piece(self, k: int):
+        lo, _ = self.buckets[k]
+        off, sz = self._boff[k]
+        g0 = lo + self.comm.rank * sz
+        return off, sz, g0
+
+    def _bucket_work(self, k: int, grad: torch.Tensor, step: int):
+        lo, hi = self.buckets[k]
+        off, sz, g0 = self._own_piece(k)
+        comm = self.comm
+        if not self._issued:  # first bucket of this clock: the device Adam step advances once
+            self.step_dev.add_(1)
+        self._issued.add(k)
+        comm.reduce_scatter(self.grad_shard[off: off + sz], grad[lo:hi])
+        sl = slice(off, off + sz)
+        out = self.params[g0: g0 + sz] if self.pull_dtype == torch.bfloat16 else None
+        if self.optimizer == "adam":
+            ops.adam_apply(self.master[sl], self.m[sl], self.v[sl], self.grad_shard[sl], self.lr, self.betas[0],
+                           self.betas[1], self.eps, self.weight_decay, step, 1.0, out, step_dev=self.step_dev)
+        elif self.optimizer == "adagrad":
+            ops.adagrad_apply(self.master[sl], self.m[sl], self.grad_shard[sl], self.lr, self.eps, 1.0, out)
+        elif self.optimizer == "sgd":
+            ops.sgd_apply(self.master[sl], self.grad_shard[sl], self.lr, 1.0, out)
+        elif self.optimizer == "add":
+            self.master[sl].add_(self.grad_shard[sl])
+            if out is not None:
+                ops.cast_f32_bf16(self.master[sl], out)
+        else:
+            raise ValueError(self.optimizer)
+        if out is None:
+            self.params[g0: g0 + sz].copy_(self.master[sl])
+        comm.all_gather(self.params[lo:hi], self.params[g0: g0 + sz])
+        grad[lo:hi].zero_()
+        comm.stats.bucket_bytes[f"t{self.table_id}b{k}"] = comm.stats.bucket_bytes.get(f"t{self.table_id}b{k}", 0) + \
+            (hi - lo) * grad.element_size() + (hi - lo) * self.params.element_size()
+
+    def bucket_ready(self, k: int, events=()):
+        """The gradients of bucket ``k`` are complete (every writer is on the current stream or
+        behind ``events``): issue its reduce-scatter + apply + all-gather now (on the clock
+        stream when clocks are asynchronous, so it overlaps the rest of the backward)."""
+        if self.buckets is None or k in self._issued:
+            return
+        self._pending = True  # the gradients were written in place into self.grad
+        grad, step = self.grad, self.step + 1
+        if self.pipe.async_:
+            st = self.pipe.stream
+            st.wait_stream(torch.cuda.current_stream(st.device))
+            for ev in events:
+                if ev is not None:
+                    st.wait_event(ev)
+            self.pipe.keep_alive(grad)
+            with torch.cuda.stream(st):
+                self._bucket_work(k, grad, step)
+        else:
+            self._bucket_work(k, grad, step)
+
+    def _full_from_pieces(self, t: torch.Tensor) -> torch.Tensor:
+        """All-gather a bucket-major shard buffer into the full vector in canonical order."""
+        W = self.comm.world
+        gathered = torch.empty(W * self.shard, dtype=t.dtype, device=t.device)
+        self.comm.all_gather(gathered, t)
+        gathered = gathered.view(W, self.shard)
+        full = torch.empty(self.n_pad, dtype=t.dtype, device=t.device)
+        for (lo, _), (off, sz) in zip(self.buckets, self._boff):
+            full[lo: lo + W * sz].view(W, sz).copy_(gathered[:, off: off + sz])
+        return full
+
+    def _pieces_from_full(self, full: torch.Tensor, dst: torch.Tensor):
+        for k in range(len(self.buckets)):
+            off, sz, g0 = self._own_piece(k)
+            dst[off: off + sz].copy_(full[g0: g0 + sz])
 
     # -- init / views -----------------------------------------------------------------------
     def load_full(self, full: torch.Tensor):
@@ -178,12 +292,17 @@ class DenseTable:
         assert full.numel() == self.n_params
         flat = torch.zeros(self.n_pad, dtype=self.value_dtype, device=self.comm.device)
         flat[: self.n_params] = full.to(self.comm.device, self.value_dtype)
-        self.master.copy_(flat[self.base: self.base + self.shard])
+        if self.buckets is not None:
+            self._pieces_from_full(flat, self.master)
+        else:
+            self.master.copy_(flat[self.base: self.base + self.shard])
         self.params.copy_(flat.to(self.pull_dtype))
 
     def full_master(self) -> torch.Tensor:
         """All-gather of the master values (checkpoint / tests)."""
         self.drain()
+        if self.buckets is not None:
+            return self._full_from_pieces(self.master)[: self.n_params]
         out = torch.empty(self.n_pad, dtype=self.value_dtype, device=self.comm.device)
         self.comm.all_gather(out, self.master)
         return out[: self.n_params]
@@ -207,6 +326,22 @@ class DenseTable:
         self._pending = False
 
         comm = self.comm
+
+        if self.buckets is not None:
+            def work():  # the buckets the backward did not issue yet, in order
+                if pending:
+                    for k in range(len(self.buckets)):
+                        if k not in self._issued:
+                            self._bucket_work(k, grad, step)
+                else:
+                    self.step_dev.add_(1)
+                self._issued = set()
+
+            self.pipe.run(work)
+            if self.pipe.async_:
+                self.grad = self._ring[step % len(self._ring)]
+                self.pipe.wait_clock(step - len(self._ring))
+            return
 
         def work():
             self.step_dev.add_(1)  # device twin of self.step (one per clock)
@@ -268,11 +403,15 @@ class DenseTable:
         beyond n_params excluded."""
         self.drain()
         rows = max(0, min(self.shard, self.n_params - self.base))
-        arrays = {"master": self.master[:rows]}
-        if self.m is not None:
-            arrays["m"] = self.m[:rows]
-        if self.v is not None:
-            arrays["v"] = self.v[:rows]
+        if self.buckets is not None:  # canonical contiguous layout: the same files as unbucketed
+            arrays = {n: self._full_from_pieces(t)[self.base: self.base + rows]
+                      for n, t in (("master", self.master), ("m", self.m), ("v", self.v)) if t is not None}
+        else:
+            arrays = {"master": self.master[:rows]}
+            if self.m is not None:
+                arrays["m"] = self.m[:rows]
+            if self.v is not None:
+                arrays["v"] = self.v[:rows]
         meta = dict(global_rows=self.n_params, base=self.base, rows=rows, cols=1, clock=self.step,
                     table_id=self.table_id, rank=self.comm.rank, world=self.comm.world, kind="dense")
         return meta, arrays
@@ -283,14 +422,28 @@ class DenseTable:
 
     def restore_dst(self):
         """Device destinations of the checkpointed arrays, [rows, 1] in restore_range order."""
-        return {n: t.view(-1, 1) for n, t in (("master", self.master), ("m", self.m), ("v", self.v))
-                if t is not None}
+        tabs = (("master", self.master), ("m", self.m), ("v", self.v))
+        if self.buckets is not None:  # land in the canonical layout, redistribute in finish_restore
+            self._canon = {n: torch.zeros_like(t) for n, t in tabs if t is not None}
+            return {n: t.view(-1, 1) for n, t in self._canon.items()}
+        return {n: t.view(-1, 1) for n, t in tabs if t is not None}
 
     def finish_restore(self, clock: int):
         """After the rows landed: clocks, then re-pull (all-gather) the parameters."""
         self.step = int(clock)
         self.step_dev.fill_(int(clock))
         self.pipe.clock = int(clock)
+        if self.buckets is not None:
+            full = None
+            for n, c in self._canon.items():
+                g = torch.empty(self.n_pad, dtype=c.dtype, device=c.device)
+                self.comm.all_gather(g, c)
+                self._pieces_from_full(g, getattr(self, n))
+                if n == "master":
+                    full = g
+            self._canon = None
+            self.params.copy_(full.to(self.pull_dtype))
+            return
         own = self.params[self.base: self.base + self.shard]
         if self.pull_dtype == torch.bfloat16:
             ops.cast_f32_bf16(self.master, own)

@@ -90,9 +90,13 @@ class MetricsLogger:
                    samples_per_s=round(samples / seconds, 1) if seconds > 0 else None)
         if comm_stats is not None:
             d = comm_stats.as_dict()
+            buckets = d.pop("bucket_bytes", {})
             prev = self._last or {k: 0 for k in d}
             delta = {k: d[k] - prev.get(k, 0) for k in d}
-            self._last = d
+            prev_b = prev.get("bucket_bytes", {})
+            self._last = dict(d, bucket_bytes=buckets)
+            if buckets:  # per-bucket RS + AG bytes of bucketed dense clocks (this step)
+                rec["bucket_bytes"] = {k: v - prev_b.get(k, 0) for k, v in buckets.items()}
             moved = delta["bytes_a2a"] + delta["bytes_rs"] + delta["bytes_ag"]
             rec.update(bytes_pushed=delta["bytes_a2a"] // 2 + delta["bytes_rs"],
                        bytes_pulled=delta["bytes_a2a"] - delta["bytes_a2a"] // 2 + delta["bytes_ag"],

@@ -147,3 +147,51 @@ def test_large_shard_streams_through_ring_gpu_policy():
         t2 = _tables(comm)
         assert Checkpointer(comm, os.path.join(d, "a_"), ring_bytes=RING).load(t2) == 1
         assert torch.equal(t2[1].shard, t[1].shard) and torch.equal(t2[0].v, t[0].v)
+
+
+class _GptSave:
+    def __init__(self, prefix):
+        self.prefix = prefix
+
+    def __call__(self, rank, world):
+        from minips_amd.models.gpt2 import GPT2, GPT2Config
+        from minips_amd.ps.checkpoint import Checkpointer
+        from minips_amd.ps.comm import Comm
+
+        comm = Comm(device=torch.device("cpu"))
+        m = GPT2(GPT2Config(vocab=300, n_ctx=32, d=128, n_layer=2, n_head=2, lr=1e-3), comm)
+        g = torch.Generator().manual_seed(2)
+        tokens = torch.randint(0, 300, (8, 32), generator=g)
+        per = 8 // world
+        for _ in range(2):
+            m.train_step(tokens[rank * per:(rank + 1) * per], torch.roll(tokens, -1, 1)[rank * per:(rank + 1) * per])
+        Checkpointer(comm, self.prefix).save({0: m.table}, iteration=2, blocking=True)
+        return m.table.full_master().tolist(), m.table.buckets is not None
+
+
+class _GptLoad:
+    def __init__(self, prefix, bucketed):
+        self.prefix, self.bucketed = prefix, bucketed
+
+    def __call__(self, rank, world):
+        from minips_amd.models.gpt2 import GPT2, GPT2Config
+        from minips_amd.ps.checkpoint import Checkpointer
+        from minips_amd.ps.comm import Comm
+
+        comm = Comm(device=torch.device("cpu"))
+        m = GPT2(GPT2Config(vocab=300, n_ctx=32, d=128, n_layer=2, n_head=2, lr=1e-3, bucketed=self.bucketed), comm)
+        assert Checkpointer(comm, self.prefix).load({0: m.table}) == 2
+        return m.table.full_master().tolist(), m.table.step, m.table.m.abs().sum().item() > 0
+
+
+@pytest.mark.parametrize("restore_world,bucketed", [(2, True), (3, False)])
+def test_bucketed_dense_checkpoint_is_canonical(tmp_path, restore_world, bucketed):
+    """A bucketed (bucket-major ownership) dense table checkpoints in the canonical contiguous
+    layout: it restores at another world size, bucketed or not, to the same parameters."""
+    prefix = str(tmp_path / "g_")
+    saved = run_world(_GptSave(prefix), world=4)
+    full0, was_bucketed = saved[0]
+    assert was_bucketed
+    out = run_world(_GptLoad(prefix, bucketed), world=restore_world)
+    for r, (full, step, has_m) in out.items():
+        assert full == full0 and step == 2 and has_m

@@ -117,3 +117,38 @@ def test_bench_two_ranks_end_to_end():
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["value"] > 0 and out["config"]["global_batch"] == 4096
+
+
+def _gpt2_buckets_gpu(rank, world):
+    """GPT-2 (tiny) at 2 ranks on one card: per-layer bucket clocks issued from the backward on
+    the clock stream (waiting on the weight-gradient side stream) vs one whole-table clock."""
+    from minips_amd.models.gpt2 import GPT2, GPT2Config
+    from minips_amd.ps.comm import Comm
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    res = {}
+    for bucketed in (False, True):
+        m = GPT2(GPT2Config(vocab=500, n_ctx=64, d=128, n_layer=2, n_head=2, lr=1e-3, bucketed=bucketed),
+                 Comm(device=dev))
+        assert (m.table.buckets is not None) == bucketed and m.table.pipe.async_
+        g = torch.Generator().manual_seed(2)
+        tokens = torch.randint(0, 500, (4, 64), generator=g)
+        targets = torch.roll(tokens, -1, 1)
+        losses = []
+        for _ in range(4):
+            l = m.train_step(tokens[rank * 2:(rank + 1) * 2].to(dev), targets[rank * 2:(rank + 1) * 2].to(dev))
+            losses.append(float(l.item()))
+        m.drain()
+        res[bucketed] = (losses, m.table.full_master().cpu())
+    torch.cuda.synchronize()
+    (l0, p0), (l1, p1) = res[False], res[True]
+    return l0, l1, float((p0 - p1).abs().max())
+
+
+def test_gpt2_bucketed_clocks_gpu_streams():
+    out = run_world(_gpt2_buckets_gpu)
+    for rank, (l0, l1, dmax) in out.items():
+        for a, b in zip(l0, l1):
+            assert abs(a - b) <= 1e-3 * abs(a) + 1e-3, (rank, l0, l1)
+        assert dmax < 4 * 2e-3, (rank, dmax)  # float-atomic wgrad order; Adam lr 1e-3 per step

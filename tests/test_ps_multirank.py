@@ -275,3 +275,51 @@ def test_model_losses_match_one_rank(world, run):
         assert many[r] == many[0]  # the all-reduced loss is identical on every rank
     for a, b in zip(many[0], one):
         assert abs(a - b) <= 3e-3 * max(1.0, abs(b)), (many[0], one)
+
+
+# ------------------------------------------------------------------------------ bucketed dense clocks
+def _gpt2_bucket_run(rank, world, bucketed=True, steps=3):
+    import json
+    import os
+    import tempfile
+
+    from minips_amd.models.gpt2 import GPT2, GPT2Config
+    from minips_amd.ps.comm import Comm
+    from minips_amd.utils.metrics import MetricsLogger
+
+    torch.set_num_threads(1)
+    comm = Comm(device=torch.device("cpu"))
+    m = GPT2(GPT2Config(vocab=300, n_ctx=32, d=128, n_layer=3, n_head=2, lr=1e-3, bucketed=bucketed), comm)
+    g = torch.Generator().manual_seed(2)
+    tokens = torch.randint(0, 300, (8, 32), generator=g)
+    targets = torch.roll(tokens, -1, 1)
+    per = 8 // world
+    path = os.path.join(tempfile.mkdtemp(), f"m{rank}.jsonl")
+    log = MetricsLogger(rank, path)
+    for it in range(steps):
+        m.train_step(tokens[rank * per:(rank + 1) * per], targets[rank * per:(rank + 1) * per])
+        log.step(it, per * 32, 1.0, comm.stats)
+    recs = [json.loads(l) for l in open(path)]
+    n_buckets = len(m.table.buckets) if m.table.buckets else 0
+    return m.table.full_master().tolist(), recs[-1].get("bucket_bytes"), n_buckets
+
+
+def _gpt2_b(rank, world):
+    return _gpt2_bucket_run(rank, world, True)
+
+
+def _gpt2_nb(rank, world):
+    return _gpt2_bucket_run(rank, world, False)
+
+
+def test_gpt2_bucketed_clock_equals_unbucketed():
+    """4 ranks: per-layer buckets (RS + Adam + AG issued during the backward) give the same
+    parameters as one whole-table clock; the metrics JSONL carries per-bucket bytes."""
+    b = run_world(_gpt2_b, world=4)
+    nb = run_world(_gpt2_nb, world=4)
+    for r in range(4):
+        pb, bytes_b, nbk = b[r]
+        pn, bytes_n, _ = nb[r]
+        assert nbk == 4 and bytes_n is None  # embedding bucket + one per layer
+        assert torch.allclose(torch.tensor(pb), torch.tensor(pn), rtol=0, atol=1e-6)
+        assert len(bytes_b) == 4 and all(v > 0 for v in bytes_b.values()), bytes_b
