@@ -172,12 +172,20 @@ void gather_rows(const at::Tensor& table, const at::Tensor& keys, int64_t base, 
   check_gpu(keys, "keys");
   check_gpu(out, "out");
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.stride(1) == 1, "table must be a row-major GPU matrix");
-  check_dtype(table, at::kFloat, "table");
   check_dtype(keys, at::kLong, "keys");
   const int64_t n = keys.numel();
   TORCH_CHECK(out.dim() == 2 && out.size(0) >= n, "out shape ", out.sizes());
   const int D = (int)out.size(1);
   TORCH_CHECK(D <= table.size(1), "out row wider than table row");
+  if (table.scalar_type() == at::kDouble) {  // reference-precision tables (f64.hip)
+    check_dtype(out, at::kDouble, "out");
+    TORCH_CHECK(D == table.size(1) && table.is_contiguous() && out.is_contiguous(), "fp64 gather: whole rows");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+    minips_k::gather_rows_f64(ptr<double>(table), D, ptr<int64_t>(keys), base, n, count_ptr(n_dev), ptr<double>(out),
+                              stream_of(keys));
+    return;
+  }
+  check_dtype(table, at::kFloat, "table");
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "out must be fp32 or bf16");
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::gather_rows(ptr<float>(table), table.stride(0), ptr<int64_t>(keys), n, base, D, out.data_ptr(),
@@ -201,13 +209,19 @@ void scatter_add_rows(const at::Tensor& src, const at::Tensor& idx, at::Tensor& 
   check_gpu(src, "src");
   check_gpu(idx, "idx");
   check_gpu(acc, "acc");
-  TORCH_CHECK(src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16, "src must be fp32 or bf16");
-  check_dtype(acc, at::kFloat, "acc");
   check_dtype(idx, at::kLong, "idx");
   TORCH_CHECK(src.dim() == 2 && acc.dim() == 2 && src.size(1) == acc.size(1) && src.is_contiguous(),
               "row widths differ");
   TORCH_CHECK(idx.numel() == src.size(0), "idx/src length mismatch");
   c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
+  if (src.scalar_type() == at::kDouble) {
+    check_dtype(acc, at::kDouble, "acc");
+    minips_k::scatter_add_rows_f64(ptr<double>(src), ptr<int64_t>(idx), src.size(0), (int)src.size(1),
+                                   ptr<double>(acc), stream_of(src));
+    return;
+  }
+  TORCH_CHECK(src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16, "src must be fp32 or bf16");
+  check_dtype(acc, at::kFloat, "acc");
   if (src.scalar_type() == at::kFloat)
     minips_k::scatter_add_rows(ptr<float>(src), src.size(0), (int)src.size(1), ptr<int64_t>(idx), ptr<float>(acc),
                                stream_of(src));
@@ -239,7 +253,17 @@ void sparse_sgd(at::Tensor& table, const at::Tensor& keys, int64_t base, const a
   check_gpu(keys, "keys");
   check_gpu(grads, "grads");
   TORCH_CHECK(grads.dim() == 2 && grads.size(0) == keys.numel() && grads.size(1) <= table.size(1), "grads shape");
+  check_dtype(keys, at::kLong, "keys");
   c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  if (table.scalar_type() == at::kDouble) {
+    check_dtype(grads, at::kDouble, "grads");
+    TORCH_CHECK(grads.size(1) == table.size(1) && table.is_contiguous(), "fp64 apply: whole rows");
+    minips_k::sparse_add_f64(ptr<double>(table), (int)table.size(1), ptr<int64_t>(keys), base, ptr<double>(grads),
+                             keys.numel(), scale, count_ptr(n_dev), stream_of(table));
+    return;
+  }
+  check_dtype(table, at::kFloat, "table");
+  check_dtype(grads, at::kFloat, "grads");
   minips_k::sparse_sgd(ptr<float>(table), table.stride(0), ptr<int64_t>(keys), keys.numel(), base,
                        (int)grads.size(1), ptr<float>(grads), (float)scale, stream_of(table), count_ptr(n_dev));
 }
@@ -427,9 +451,18 @@ void lr_sparse_step(const at::Tensor& rowptr, const at::Tensor& cols, const at::
                     const at::Tensor& labels, const at::Tensor& w, double alpha,
                     const c10::optional<at::Tensor>& delta, const c10::optional<at::Tensor>& correct) {
   for (auto* t : {&rowptr, &cols, &vals, &labels, &w}) check_gpu(*t, "lr input");
-  check_dtype(w, at::kFloat, "w");
   check_dtype(vals, at::kFloat, "vals");
   TORCH_CHECK(rowptr.numel() == labels.numel() + 1, "rowptr must be [B+1]");
+  if (w.scalar_type() == at::kDouble) {  // reference-precision LR (double tables)
+    double* d = opt_ptr<double>(delta, at::kDouble, "delta");
+    if (d) TORCH_CHECK(delta->numel() == w.numel(), "delta must match w");
+    float* c = opt_ptr<float>(correct, at::kFloat, "correct");
+    c10::hip::HIPGuardMasqueradingAsCUDA gd(w.device());
+    minips_k::lr_sparse_step_f64(ptr<int64_t>(rowptr), ptr<int64_t>(cols), ptr<float>(vals), ptr<float>(labels),
+                                 labels.numel(), ptr<double>(w), alpha, d, c, stream_of(w));
+    return;
+  }
+  check_dtype(w, at::kFloat, "w");
   float* d = opt_ptr<float>(delta, at::kFloat, "delta");
   if (d) TORCH_CHECK(delta->numel() == w.numel(), "delta must match w");
   float* c = opt_ptr<float>(correct, at::kFloat, "correct");

@@ -199,4 +199,13 @@ void remote_gather(const int64_t* bases, const int64_t* bounds, int P, const int
 void remote_scatter_add(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,
                         const int64_t* n_dev, const float* vals, int W, float scale, hipStream_t s);
 
+// ------------------------------------------------------------------ fp64 parity tables (f64.hip, ml.hip)
+void gather_rows_f64(const double* table, int W, const int64_t* keys, int64_t base, int64_t n, const int64_t* n_dev,
+                     double* out, hipStream_t s);
+void scatter_add_rows_f64(const double* src, const int64_t* idx, int64_t n, int W, double* acc, hipStream_t s);
+void sparse_add_f64(double* table, int W, const int64_t* keys, int64_t base, const double* grads, int64_t n,
+                    double scale, const int64_t* n_dev, hipStream_t s);
+void lr_sparse_step_f64(const int64_t* rowptr, const int64_t* cols, const float* vals, const float* labels, int64_t B,
+                        const double* w, double alpha, double* delta, float* correct, hipStream_t s);
+
 }  // namespace minips_k

@@ -10,25 +10,34 @@
 
 namespace minips_k {
 
-// One wave per sample: lanes stride the sample's non-zeros.
+template <typename T>
+__device__ __forceinline__ T wave_sum_t(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// One wave per sample: lanes stride the sample's non-zeros. T = float (the performance path) or
+// double (the reference's double tables, lr_example.cpp:182: parity runs).
+template <typename T>
 __global__ void lr_sparse_kernel(const int64_t* __restrict__ rowptr, const int64_t* __restrict__ cols,
                                  const float* __restrict__ vals, const float* __restrict__ labels, int64_t B,
-                                 const float* __restrict__ w, float alpha, float* delta, float* correct) {
+                                 const T* __restrict__ w, T alpha, T* delta, float* correct) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   float hits = 0.f;
   for (int64_t i = wave; i < B; i += nwaves) {
     const int64_t s0 = rowptr[i], s1 = rowptr[i + 1];
-    float dot = 0.f;
-    for (int64_t j = s0 + lane; j < s1; j += 64) dot += w[cols[j]] * vals[j];
-    dot = warp_sum(dot);
-    const float p = sigmoidf_(dot);
-    const float y = labels[i] < 0.f ? 0.f : labels[i];
-    const float err = alpha * (y - p);
+    T dot = 0;
+    for (int64_t j = s0 + lane; j < s1; j += 64) dot += w[cols[j]] * (T)vals[j];
+    dot = wave_sum_t(dot);
+    const T p = (T)1 / ((T)1 + exp(-dot));
+    const T y = labels[i] < 0.f ? (T)0 : (T)labels[i];
+    const T err = alpha * (y - p);
     if (delta)
-      for (int64_t j = s0 + lane; j < s1; j += 64) atomicAdd(delta + cols[j], err * vals[j]);
-    if (lane == 0) hits += ((p > 0.5f) == (y > 0.5f)) ? 1.f : 0.f;
+      for (int64_t j = s0 + lane; j < s1; j += 64) atomicAdd(delta + cols[j], err * (T)vals[j]);
+    if (lane == 0) hits += ((p > (T)0.5) == (y > (T)0.5)) ? 1.f : 0.f;
   }
   if (correct && lane == 0 && hits > 0.f) atomicAdd(correct, hits);
 }
@@ -37,8 +46,17 @@ void lr_sparse_step(const int64_t* rowptr, const int64_t* cols, const float* val
                     const float* w, float alpha, float* delta, float* correct, hipStream_t s) {
   if (B <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(lr_sparse_kernel, grid_for(B * 64, block, 4096), block, 0, s, rowptr, cols, vals, labels, B, w,
-                     alpha, delta, correct);
+  hipLaunchKernelGGL(lr_sparse_kernel<float>, grid_for(B * 64, block, 4096), block, 0, s, rowptr, cols, vals, labels,
+                     B, w, alpha, delta, correct);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void lr_sparse_step_f64(const int64_t* rowptr, const int64_t* cols, const float* vals, const float* labels, int64_t B,
+                        const double* w, double alpha, double* delta, float* correct, hipStream_t s) {
+  if (B <= 0) return;
+  const int block = 256;
+  hipLaunchKernelGGL(lr_sparse_kernel<double>, grid_for(B * 64, block, 4096), block, 0, s, rowptr, cols, vals,
+                     labels, B, w, alpha, delta, correct);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

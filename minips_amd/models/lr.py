@@ -22,6 +22,7 @@ class SparseLRConfig:
     consistency: str = "bsp"
     staleness: int = 0
     storage: str = "vector"  # reference kStorageType: "vector" (dense key range) or "map" (hash)
+    value_dtype: torch.dtype = torch.float32  # float64: the reference's CreateTable<double>
 
 
 class SparseLR:
@@ -32,7 +33,8 @@ class SparseLR:
                                          consistency=cfg.consistency, staleness=cfg.staleness)
         elif cfg.storage.lower() == "vector":
             self.table = SparseTable(comm, cfg.num_dims, 1, optimizer="add", pull_dtype=torch.float32, init_std=0.0,
-                                     consistency=cfg.consistency, staleness=cfg.staleness)
+                                     consistency=cfg.consistency, staleness=cfg.staleness,
+                                     value_dtype=cfg.value_dtype)
         else:
             raise ValueError(f"kStorageType {cfg.storage!r}: Map or Vector")
 
@@ -41,7 +43,7 @@ class SparseLR:
         Returns the number of correctly classified rows (before the update)."""
         dev = self.comm.device
         rows, plan = self.table.get(cols)
-        delta = torch.zeros(max(plan.cap, 1), dtype=torch.float32, device=dev)
+        delta = torch.zeros(max(plan.cap, 1), dtype=rows.dtype, device=dev)
         correct = torch.zeros(1, dtype=torch.float32, device=dev)
         if plan.cap:
             ops.lr_sparse_step(rowptr, plan.inv, vals, labels, rows.view(-1)[: plan.cap], self.cfg.alpha,

@@ -223,11 +223,11 @@ def lookup_rows(rows, inv, F, D, out):
 
 
 def scatter_add_rows(src, idx, acc):
-    """acc[idx[i]] += src[i] (src fp32 or bf16, acc fp32)."""
+    """acc[idx[i]] += src[i] (src fp32 or bf16, acc fp32; or both fp64)."""
     if _gpu(src):
         kernels().scatter_add_rows(src, idx, acc)
         return acc
-    acc.index_add_(0, idx, src.float())
+    acc.index_add_(0, idx, src.to(acc.dtype))
     return acc
 
 

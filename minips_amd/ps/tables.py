@@ -508,7 +508,18 @@ class SparseTable:
     def __init__(self, comm: Comm, num_rows: int, width: int, optimizer: str = "rowwise_adagrad",
                  lr: float = 0.01, eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "bsp",
                  staleness: int = 0, split: int | None = None, table_id: int = 0, init_std: float = 0.01,
-                 seed: int = 1234, p2p: bool | None = None, push_dtype=None, route: str = "mix"):
+                 seed: int = 1234, p2p: bool | None = None, push_dtype=None, route: str = "mix",
+                 value_dtype=torch.float32):
+        """``value_dtype`` float64: the reference's double tables (CreateTable<double>,
+        lr_example.cpp:182; values read as double, kv_client_table.hpp:96-101) -- optimizer "add"
+        (VectorStorage::SubAdd), rows pulled and pushed in fp64 (f64.hip kernels)."""
+        if value_dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"value_dtype {value_dtype}")
+        if value_dtype == torch.float64:
+            if optimizer != "add":
+                raise ValueError("fp64 sparse tables support the reference's plain add apply only")
+            pull_dtype = push_dtype = torch.float64
+        self.value_dtype = value_dtype
         self.comm = comm
         # Key -> row placement. "range": row = key (the reference's contiguous range partition).
         # "mix" (default): row = key * A mod num_rows, a bijection (A prime, coprime to num_rows),
@@ -536,7 +547,7 @@ class SparseTable:
         self.rows_local = b[comm.rank + 1] - b[comm.rank]
         g = torch.Generator(device=dev)
         g.manual_seed(seed + 7919 * comm.rank)
-        self.shard = torch.empty(self.rows_local, width, dtype=torch.float32, device=dev)
+        self.shard = torch.empty(self.rows_local, width, dtype=value_dtype, device=dev)
         if init_std > 0:
             self.shard.normal_(0.0, init_std, generator=g)
         else:
@@ -721,14 +732,15 @@ class SparseTable:
 
     def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
         """Push gradient rows (aligned with the plan's unique order; rows >= U are ignored)."""
-        assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == torch.float32
+        assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == getattr(self, "value_dtype", torch.float32)
         self._pending.append((plan, grad_rows))
 
     def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
         """Reference-style Add(keys, vals) (duplicates are summed)."""
         plan = self.plan(keys)
-        g = torch.zeros(max(plan.cap, 1), self.width, dtype=torch.float32, device=self.comm.device)
-        ops.scatter_add_rows(vals.reshape(keys.numel(), self.width).to(torch.float32).contiguous(), plan.inv, g)
+        vdt = getattr(self, "value_dtype", torch.float32)
+        g = torch.zeros(max(plan.cap, 1), self.width, dtype=vdt, device=self.comm.device)
+        ops.scatter_add_rows(vals.reshape(keys.numel(), self.width).to(vdt).contiguous(), plan.inv, g)
         self.add(plan, g)
 
     def clock(self):
@@ -757,7 +769,7 @@ class SparseTable:
             if M == 0:
                 return
             n = plan.extra.get("own_U", M)
-            g = torch.zeros(n, self.width, dtype=torch.float32, device=dev)
+            g = torch.zeros(n, self.width, dtype=getattr(self, "value_dtype", torch.float32), device=dev)
             ops.scatter_add_rows(recv, plan.own_inv, g)
             keys, n_dev = plan.own_uniq, (None if "own_U" in plan.extra else plan.own_U_dev)
         keys, base = self._owner_rows(keys[:n], plan)

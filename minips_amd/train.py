@@ -50,6 +50,8 @@ def parse(argv=None):
     ap.add_argument("--recovery", default="inplace", choices=["inplace", "restart"],
                     help="inplace: after a peer failure the survivors roll back in their processes and "
                          "the supervisor relaunches only the failed rank; restart: the whole rank set")
+    ap.add_argument("--value_dtype", default="float32", choices=["float32", "float64"],
+                    help="LR table precision; float64 = the reference's CreateTable<double> (lr_example.cpp:182)")
     ap.add_argument("--transport", default="collective", choices=["collective", "onesided"],
                     help="DLRM SSP/ASP data path: RCCL collectives, or one-sided IPC row access (ps/onesided.py)")
     ap.add_argument("--force_quit_rank", type=int, default=-1,
@@ -136,7 +138,8 @@ def build(args, comm):
             comm.all_reduce_(t, op=dist.ReduceOp.MAX)
             nd = int(t.item())
         m = SparseLR(SparseLRConfig(num_dims=nd, alpha=args.alpha, consistency=args.consistency,
-                                    staleness=args.staleness, storage=args.kStorageType), comm)
+                                    staleness=args.staleness, storage=args.kStorageType,
+                                    value_dtype=getattr(torch, args.value_dtype)), comm)
         B = args.batch or 1024
         return m, {0: m.table}, (lambda: _Skippable(_Batches(shard, B, seed))), (lambda b: -m.train_step(*b)), B
     if args.model == "lr":
@@ -145,7 +148,8 @@ def build(args, comm):
 
         nd = args.num_dims or (5000 if args.small else 16_609_143)
         m = SparseLR(SparseLRConfig(num_dims=nd, alpha=args.alpha, consistency=args.consistency,
-                                    staleness=args.staleness, storage=args.kStorageType), comm)
+                                    staleness=args.staleness, storage=args.kStorageType,
+                                    value_dtype=getattr(torch, args.value_dtype)), comm)
         B = args.batch or (128 if args.small else 65536)
         return m, {0: m.table}, \
             (lambda: _Skippable(SparseLRSynth(B, num_dims=nd, nnz=16 if args.small else 64, device=dev, seed=seed))), \

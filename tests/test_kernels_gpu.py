@@ -369,3 +369,23 @@ def test_dedupe_fused_csr_counts(dev, P):
     assert bool((memrow_c[1:] >= memrow_c[:-1]).all())
     torch.testing.assert_close(inv.cpu()[members_c], memrow_c)
     assert sorted(members_c.tolist()) == list(range(n))
+
+
+def test_sparse_lr_fp64_matches_cpu(dev):
+    """Reference-precision LR (double tables, lr_example.cpp:182): the fp64 HIP path (f64 row
+    kernels + lr_sparse_step<double>) matches the CPU fp64 oracle to fp64 rounding."""
+    from minips_amd.data.synthetic import SparseLRSynth
+    from minips_amd.models.lr import SparseLR, SparseLRConfig
+    from minips_amd.ps.comm import Comm
+
+    res = {}
+    for d in (torch.device("cpu"), dev):
+        m = SparseLR(SparseLRConfig(num_dims=3000, alpha=0.05, value_dtype=torch.float64), Comm(device=d))
+        data = SparseLRSynth(256, num_dims=3000, nnz=16, device="cpu", seed=7)
+        for _ in range(5):
+            rp, c, v, y = data.next()
+            m.train_step(rp.to(d), c.to(d), v.to(d), y.to(d))
+        res[d.type] = m.table.shard.cpu()
+    assert res["cuda"].dtype == torch.float64
+    assert torch.allclose(res["cuda"], res["cpu"], rtol=1e-12, atol=1e-14)
+    assert res["cpu"].abs().sum() > 0

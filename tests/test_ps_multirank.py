@@ -323,3 +323,34 @@ def test_gpt2_bucketed_clock_equals_unbucketed():
         assert nbk == 4 and bytes_n is None  # embedding bucket + one per layer
         assert torch.allclose(torch.tensor(pb), torch.tensor(pn), rtol=0, atol=1e-6)
         assert len(bytes_b) == 4 and all(v > 0 for v in bytes_b.values()), bytes_b
+
+
+def _sparse_f64(rank, world):
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.tables import SparseTable
+
+    torch.set_num_threads(1)
+    comm = Comm(device=torch.device("cpu"))
+    t = SparseTable(comm, num_rows=1003, width=2, optimizer="add", init_std=0.0, value_dtype=torch.float64)
+    keys = _rank_keys(rank)
+    for step in range(3):
+        t.add_keys(keys, torch.full((keys.numel(), 2), 0.1 * (rank + 1) + 1e-12 * step, dtype=torch.float64))
+        t.clock()
+    got = t.get_rows(torch.arange(1003))
+    return str(got.dtype), got.tolist()
+
+
+@pytest.mark.parametrize("world", WORLDS)
+def test_sparse_table_fp64_exact(world):
+    """The reference's double tables: sums exact in fp64 (not fp32-representable deltas)."""
+    out = run_world(_sparse_f64, world=world)
+    exp = torch.zeros(1003, dtype=torch.float64)
+    for step in range(3):
+        for r in range(world):
+            for k in _rank_keys(r).tolist():
+                exp[k] += 0.1 * (r + 1) + 1e-12 * step
+    for rank, (dt, got) in out.items():
+        assert dt == "torch.float64"
+        g = torch.tensor(got, dtype=torch.float64)
+        assert torch.allclose(g[:, 0], exp, rtol=1e-15, atol=1e-15), rank
+        assert not torch.equal(g[:, 0].float().double(), g[:, 0])  # really fp64 values

@@ -11,9 +11,10 @@ times (report.pdf Fig. 13/15/16, report.md), all on a 15-machine 1 GbE CPU clust
 2. Checkpoint overhead (P3 vs P4): the same LR run with a checkpoint every 100 iterations
    (binary sidecar; the reference text files are written for shards of <= 4M values) vs none.
 3. Recovery phases (P6-P8): 2 ranks under the elastic supervisor (heartbeat 1 s), rank 1 stops
-   answering (--fail_mode=hang) at iteration 30; phase times from the [Fault Tolerance] log
-   lines: detect (hang -> Phase2), restart (Phase2 -> Phase3), failed rank recovered (Phase3 ->
-   Phase4), others recovered (Phase3 -> Phase5). On a one-GPU box both ranks share the card over
+   answering (--fail_mode=hang) at iteration 30, once with a whole rank-set restart and once
+   with in-place survivor rollback; phase times from the [Fault Tolerance] log lines: detect
+   (hang -> Phase2), restart (Phase2 -> Phase3), failed rank recovered (Phase3 -> Phase4),
+   others recovered (Phase3 -> Phase5). On a one-GPU box both ranks share the card over
    gloo (MINIPS_SHARE_DEVICE / MINIPS_DIST_BACKEND); with several GPUs they use RCCL.
 """
 from __future__ import annotations
@@ -42,17 +43,19 @@ def _train(args: list[str], timeout: int = 900) -> dict:
 
 def lr_table(quick: bool):
     rows = []
-    for batch, steps in ((8, 400 if quick else 2000), (65536, 60 if quick else 300)):
-        for cons, st in (("bsp", 0), ("ssp", 0), ("ssp", 1)):
-            out = _train(["--batch", str(batch), "--steps", str(steps), "--consistency", cons, "--staleness", str(st),
-                          "--timing_skip", "20"])
-            ms = out["steady_ms_per_iter"]
-            rows.append((batch, f"{cons.upper()}" + (f" s={st}" if cons == "ssp" else ""), ms, batch / ms * 1e3))
+    for dt in ("float64", "float32"):  # float64 = the reference's double tables (lr_example.cpp:182)
+        for batch, steps in ((8, 400 if quick else 2000), (65536, 60 if quick else 300)):
+            for cons, st in (("bsp", 0), ("ssp", 0), ("ssp", 1)):
+                out = _train(["--batch", str(batch), "--steps", str(steps), "--consistency", cons, "--staleness",
+                              str(st), "--timing_skip", "20", "--value_dtype", dt])
+                ms = out["steady_ms_per_iter"]
+                rows.append((dt, batch, f"{cons.upper()}" + (f" s={st}" if cons == "ssp" else ""), ms,
+                             batch / ms * 1e3))
     print("## 1. Sparse LR, webspam-shaped (16.6M features, 64 nnz/row), one MI355X\n")
-    print("| samples / iteration | consistency | ms / iteration | samples/s |")
-    print("|---|---|---|---|")
-    for b, c, ms, sps in rows:
-        print(f"| {b} | {c} | {ms:.3f} | {sps:,.0f} |")
+    print("| table precision | samples / iteration | consistency | ms / iteration | samples/s |")
+    print("|---|---|---|---|---|")
+    for dt, b, c, ms, sps in rows:
+        print(f"| {dt}{' (reference precision)' if dt == 'float64' else ''} | {b} | {c} | {ms:.3f} | {sps:,.0f} |")
     print("\nReference (15 CPU machines, 1 GbE): webspam LR with checkpointing ~62 ms/iteration "
           "(P9, ~130 samples/s cluster-wide, D1); kdd12 ~165 ms/iteration (P10).\n")
 
@@ -81,7 +84,7 @@ def _ts(pattern: str, text: str):
     return int(m.group(1)) if m else None
 
 
-def recovery_table():
+def _recovery_run(mode: str):
     import torch
 
     tmp = tempfile.mkdtemp(prefix="minips_ft_")
@@ -89,7 +92,7 @@ def recovery_table():
     if torch.cuda.is_available() and torch.cuda.device_count() < 2:
         env.update(MINIPS_SHARE_DEVICE="1", MINIPS_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "minips_amd.elastic", "--nproc", "2", "--heartbeat_interval", "1.0",
-           "--max_restarts", "1", "--run_dir", f"{tmp}/run", "--log_dir", f"{tmp}/log", "--",
+           "--max_restarts", "1", "--recovery", mode, "--run_dir", f"{tmp}/run", "--log_dir", f"{tmp}/log", "--",
            sys.executable, "-m", "minips_amd.train", "--model", "lr", "--batch", "8192", "--steps", "60",
            "--checkpoint_toggle=1", "--checkpoint_every", "10", f"--checkpoint_file_prefix={tmp}/ck/",
            "--fail_rank=1", "--fail_step=30", "--fail_mode=hang"]
@@ -102,20 +105,33 @@ def recovery_table():
     p2 = _ts(r"\[Fault Tolerance\]\[Phase2\]\[(\d+)\]", sup)
     p3 = _ts(r"\[Fault Tolerance\]\[Phase3\]\[(\d+)\]", sup)
     p4 = _ts(r"\[Fault Tolerance\]\[Phase4\]\[(\d+)\]", logs.get("rank1_attempt1.log", ""))
-    p5 = _ts(r"\[Fault Tolerance\]\[Phase5\]\[(\d+)\]", logs.get("rank0_attempt1.log", ""))
+    # in place, rank 0 keeps its process (and its first log file) and rolls back inside it
+    p5 = _ts(r"\[Fault Tolerance\]\[Phase5\]\[(\d+)\]",
+             logs.get("rank0_attempt1.log" if mode == "restart" else "rank0_attempt0.log", ""))
+    return r.returncode, sup, wall, (inj, p2, p3, p4, p5)
+
+
+def recovery_table():
     print("## 3. Fault recovery (2 ranks, heartbeat 1 s, rank 1 stops answering at iteration 30)\n")
-    if r.returncode != 0 or None in (inj, p2, p3, p4, p5):
-        print(f"run failed (rc {r.returncode}); supervisor stderr tail:\n```\n{sup[-2000:]}\n```\n")
-        return
-    print("| phase | here (ms) | reference 5 machines (s, P6) | reference 15 machines (s, P7) |")
-    print("|---|---|---|---|")
-    print(f"| Phase2 detect failure (hang -> detected; 3 x heartbeat) | {p2 - inj} | 8 | 7 |")
-    print(f"| Phase3 restart (stop rank set, relaunch) | {p3 - p2} | 10 | 9 |")
-    print(f"| Phase4 failed rank recovered (start + restore) | {p4 - p3} | 58 | 46 |")
-    print(f"| Phase5 other ranks recovered | {p5 - p3} | 42 | 31 |")
-    print(f"\nWhole run (60 iterations incl. the failure, restart and resumed tail): {wall:.1f} s; the "
-          "reference's webspam timeline (P8): detect 50,023 ms with a 15 s heartbeat, failed node "
-          "recovers 122,318 ms.\n")
+    res = {}
+    for mode in ("restart", "inplace"):
+        rc, sup, wall, ts = _recovery_run(mode)
+        if rc != 0 or None in ts:
+            print(f"{mode}: run failed (rc {rc}); supervisor stderr tail:\n```\n{sup[-2000:]}\n```\n")
+            return
+        res[mode] = (wall, ts)
+    print("| phase | restart mode (ms) | in-place mode (ms) | reference 5 machines (s, P6) | reference 15 machines (s, P7) |")
+    print("|---|---|---|---|---|")
+    (wr, (i1, a2, a3, a4, a5)), (wi, (j1, b2, b3, b4, b5)) = res["restart"], res["inplace"]
+    print(f"| Phase2 detect failure (hang -> detected; 3 x heartbeat) | {a2 - i1} | {b2 - j1} | 8 | 7 |")
+    print(f"| Phase3 restart (restart: stop + relaunch the rank set; in place: relaunch the failed rank) "
+          f"| {a3 - a2} | {b3 - b2} | 10 | 9 |")
+    print(f"| Phase4 failed rank recovered (start + restore) | {a4 - a3} | {b4 - b3} | 58 | 46 |")
+    print(f"| Phase5 other ranks recovered (restart: new processes; in place: rollback in their process) "
+          f"| {a5 - a3} | {b5 - b3} | 42 | 31 |")
+    print(f"\nWhole run (60 iterations incl. the failure and the resumed tail): restart {wr:.1f} s, in place "
+          f"{wi:.1f} s; the reference's webspam timeline (P8): detect 50,023 ms with a 15 s heartbeat, failed "
+          "node recovers 122,318 ms.\n")
 
 
 def main():
