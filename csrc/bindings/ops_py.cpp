@@ -827,6 +827,38 @@ void remote_scatter_add(const at::Tensor& bases, const at::Tensor& bounds, const
                                nd, ptr<float>(vals), (int)vals.size(1), (float)scale, stream_of(keys));
 }
 
+void kmeans_assign_csr(const at::Tensor& rowptr, const at::Tensor& cols, const at::Tensor& vals, const at::Tensor& C,
+                       at::Tensor& cnorm, at::Tensor& assign, const c10::optional<at::Tensor>& dist) {
+  for (const at::Tensor* t : {&rowptr, &cols, &vals, &C, (const at::Tensor*)&cnorm, (const at::Tensor*)&assign})
+    check_gpu(*t, "kmeans_csr arg");
+  check_dtype(rowptr, at::kLong, "rowptr");
+  check_dtype(cols, at::kLong, "cols");
+  check_dtype(vals, at::kFloat, "vals");
+  check_dtype(C, at::kFloat, "C");
+  check_dtype(cnorm, at::kFloat, "cnorm");
+  check_dtype(assign, at::kInt, "assign");
+  const int64_t n = rowptr.numel() - 1;
+  TORCH_CHECK(C.dim() == 2 && cnorm.numel() == C.size(0) && assign.numel() == n && cols.numel() == vals.numel(),
+              "kmeans_csr shapes");
+  float* dp = opt_ptr<float>(dist, at::kFloat, "dist");
+  if (dp) TORCH_CHECK(dist->numel() == n, "dist must be [n]");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(C.device());
+  minips_k::kmeans_assign_csr(ptr<int64_t>(rowptr), ptr<int64_t>(cols), ptr<float>(vals), n, ptr<float>(C),
+                              (int)C.size(0), C.size(1), ptr<float>(cnorm), ptr<int32_t>(assign), dp, stream_of(C));
+}
+
+void kmeans_csr_accum(const at::Tensor& rowptr, const at::Tensor& cols, const at::Tensor& vals,
+                      const at::Tensor& assign, at::Tensor& sums) {
+  for (const at::Tensor* t : {&rowptr, &cols, &vals, &assign, (const at::Tensor*)&sums}) check_gpu(*t, "kmeans_csr arg");
+  check_dtype(vals, at::kFloat, "vals");
+  check_dtype(sums, at::kFloat, "sums");
+  check_dtype(assign, at::kInt, "assign");
+  TORCH_CHECK(sums.dim() == 2 && assign.numel() == rowptr.numel() - 1, "kmeans_csr_accum shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(sums.device());
+  minips_k::kmeans_csr_accum(ptr<int64_t>(rowptr), ptr<int64_t>(cols), ptr<float>(vals), rowptr.numel() - 1,
+                             ptr<int32_t>(assign), sums.size(1), ptr<float>(sums), stream_of(sums));
+}
+
 }  // namespace
 
 
@@ -892,6 +924,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
   m.def("ipc_alloc", &ipc_alloc);
+  m.def("kmeans_assign_csr", &kmeans_assign_csr);
+  m.def("kmeans_csr_accum", &kmeans_csr_accum);
   m.def("ipc_open", &ipc_open);
   m.def("remote_gather", &remote_gather);
   m.def("remote_scatter_add", &remote_scatter_add);

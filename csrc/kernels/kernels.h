@@ -208,4 +208,10 @@ void sparse_add_f64(double* table, int W, const int64_t* keys, int64_t base, con
 void lr_sparse_step_f64(const int64_t* rowptr, const int64_t* cols, const float* vals, const float* labels, int64_t B,
                         const double* w, double alpha, double* delta, float* correct, hipStream_t s);
 
+// ------------------------------------------------------------------ sparse K-Means (ml.hip)
+void kmeans_assign_csr(const int64_t* rowptr, const int64_t* cols, const float* vals, int64_t n, const float* C,
+                       int k, int64_t d, float* cnorm, int32_t* assign, float* dist, hipStream_t s);
+void kmeans_csr_accum(const int64_t* rowptr, const int64_t* cols, const float* vals, int64_t n, const int32_t* assign,
+                      int64_t d, float* sums, hipStream_t s);
+
 }  // namespace minips_k

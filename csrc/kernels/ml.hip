@@ -175,4 +175,98 @@ void kmeans_argmin(const float* S, int64_t n, int k, const float* cn, const floa
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------- sparse (CSR) K-Means
+// The reference K-Means clusters sparse libsvm points (webspam: 16.6M features) against dense
+// centres: nearest centre over sparse x (kmeans_helper.hpp:45-66) and the centre update
+// (kmeans.cpp:238-267). One wave per point, lanes over its non-zeros:
+//   d_k = |x|^2 - 2 x.c_k + |c_k|^2   (|c_k|^2 precomputed per step: kmeans_cnorm)
+__global__ void kmeans_cnorm_kernel(const float* __restrict__ C, int k, int64_t d, float* __restrict__ out) {
+  // one block per centre
+  const int c = blockIdx.x;
+  float acc = 0.f;
+  for (int64_t j = threadIdx.x; j < d; j += blockDim.x) {
+    const float t = C[(int64_t)c * d + j];
+    acc += t * t;
+  }
+  acc = warp_sum(acc);
+  __shared__ float part[16];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) part[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += part[i];
+    out[c] = t;
+  }
+}
+
+__global__ void kmeans_assign_csr_kernel(const int64_t* __restrict__ rowptr, const int64_t* __restrict__ cols,
+                                         const float* __restrict__ vals, int64_t n, const float* __restrict__ C,
+                                         int k, int64_t d, const float* __restrict__ cnorm, int32_t* assign,
+                                         float* dist) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nwaves) {
+    const int64_t s0 = rowptr[i], s1 = rowptr[i + 1];
+    float xn = 0.f;
+    for (int64_t j = s0 + lane; j < s1; j += 64) xn += vals[j] * vals[j];
+    xn = warp_sum(xn);
+    float best = 3.4e38f;
+    int besti = 0;
+    for (int c = 0; c < k; ++c) {
+      const float* cc = C + (int64_t)c * d;
+      float dot = 0.f;
+      for (int64_t j = s0 + lane; j < s1; j += 64) {
+        const int64_t col = cols[j];
+        if (col < d) dot += vals[j] * cc[col];
+      }
+      dot = warp_sum(dot);
+      const float dd = xn - 2.f * dot + cnorm[c];
+      if (dd < best) {
+        best = dd;
+        besti = c;
+      }
+    }
+    if (lane == 0) {
+      assign[i] = besti;
+      if (dist) dist[i] = fmaxf(best, 0.f);
+    }
+  }
+}
+
+// sums[assign[i], col] += val over every non-zero of every point (the batch's centre sums)
+__global__ void kmeans_csr_accum_kernel(const int64_t* __restrict__ rowptr, const int64_t* __restrict__ cols,
+                                        const float* __restrict__ vals, int64_t n, const int32_t* __restrict__ assign,
+                                        int64_t d, float* __restrict__ sums) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nwaves) {
+    float* row = sums + (int64_t)assign[i] * d;
+    for (int64_t j = rowptr[i] + lane; j < rowptr[i + 1]; j += 64) {
+      const int64_t col = cols[j];
+      if (col < d) atomicAdd(row + col, vals[j]);
+    }
+  }
+}
+
+void kmeans_assign_csr(const int64_t* rowptr, const int64_t* cols, const float* vals, int64_t n, const float* C,
+                       int k, int64_t d, float* cnorm, int32_t* assign, float* dist, hipStream_t s) {
+  if (n <= 0 || k <= 0) return;
+  hipLaunchKernelGGL(kmeans_cnorm_kernel, k, 256, 0, s, C, k, d, cnorm);
+  MINIPS_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(kmeans_assign_csr_kernel, grid_for(n * 64, 256, 4096), 256, 0, s, rowptr, cols, vals, n, C, k, d,
+                     cnorm, assign, dist);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void kmeans_csr_accum(const int64_t* rowptr, const int64_t* cols, const float* vals, int64_t n, const int32_t* assign,
+                      int64_t d, float* sums, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(kmeans_csr_accum_kernel, grid_for(n * 64, 256, 4096), 256, 0, s, rowptr, cols, vals, n, assign,
+                     d, sums);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace minips_k

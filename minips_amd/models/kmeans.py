@@ -1,4 +1,5 @@
-"""Mini-batch K-Means on the GPU parameter server (reference examples/kmeans_example.cpp):
+"""Mini-batch K-Means on the GPU parameter server (reference apps/kmeans/kmeans.cpp), on dense
+points (train_step) or sparse libsvm/CSR points (train_step_csr, the reference's input):
 the K x D centres and the K member counts live in one DenseTable with the plain ``add`` apply.
 Each Clock a worker assigns its batch to the nearest centres (fused ``kmeans_assign`` kernel),
 accumulates per-centre sums/counts (scatter-add), and pushes
@@ -150,6 +151,30 @@ class KMeans:
         sums = torch.zeros(K, D, dtype=torch.float32, device=dev)
         ops.scatter_add_rows(X.contiguous(), idx, sums)
         n = torch.bincount(idx, minlength=K).to(torch.float32)
+        n_glob = self.comm.all_reduce_(n.clone())
+        denom = (N + n_glob).clamp_min(1.0)
+        G = self.table.grad
+        G[: K * D].view(K, D).copy_((sums - n[:, None] * C) / denom[:, None])
+        G[K * D: K * D + K].copy_(n)
+        self.table.add()
+        self.table.clock()
+        return dist.sum()
+
+    def train_step_csr(self, rowptr, cols, vals):
+        """Sparse points (CSR batch; the reference clusters libsvm rows, kmeans_helper.hpp:45-66,
+        kmeans.cpp:238-267) against the dense centres: the same batched 1/count update as
+        train_step. Returns the batch's summed squared distance (before the update)."""
+        K, D = self.cfg.K, self.cfg.dims
+        dev = self.comm.device
+        P = self.table.get()
+        C = P[: K * D].view(K, D)
+        N = P[K * D: K * D + K]
+        n_pts = rowptr.numel() - 1
+        dist = torch.empty(n_pts, dtype=torch.float32, device=dev)
+        assign = ops.kmeans_assign_csr(rowptr, cols, vals, C, dist=dist)
+        sums = torch.zeros(K, D, dtype=torch.float32, device=dev)
+        ops.kmeans_csr_accum(rowptr, cols, vals, assign, sums)
+        n = torch.bincount(assign.to(torch.int64), minlength=K).to(torch.float32)
         n_glob = self.comm.all_reduce_(n.clone())
         denom = (N + n_glob).clamp_min(1.0)
         G = self.table.grad

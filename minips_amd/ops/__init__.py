@@ -424,6 +424,42 @@ def lr_sparse_step(rowptr, cols, vals, labels, w, alpha, delta=None, correct=Non
         correct += ((p > 0.5) == (y > 0.5)).float().sum()
 
 
+def kmeans_assign_csr(rowptr, cols, vals, C, assign=None, dist=None):
+    """Nearest centre of every sparse point (CSR rowptr [n+1], cols / vals [nnz]) among the dense
+    centres C [k, d] fp32 (kmeans_helper.hpp:45-66); optional squared distances. int32 assign."""
+    n = rowptr.numel() - 1
+    if assign is None:
+        assign = torch.empty(n, dtype=torch.int32, device=C.device)
+    if _gpu(C):
+        cnorm = torch.empty(C.shape[0], dtype=torch.float32, device=C.device)
+        kernels().kmeans_assign_csr(rowptr, cols, vals, C, cnorm, assign, dist)
+        return assign
+    lens = rowptr[1:] - rowptr[:-1]
+    row = torch.repeat_interleave(torch.arange(n, device=C.device), lens)
+    ok = cols < C.shape[1]
+    xn = torch.zeros(n, dtype=torch.float32).index_add_(0, row, vals * vals)
+    dots = torch.zeros(n, C.shape[0], dtype=torch.float32)
+    dots.index_add_(0, row[ok], vals[ok, None] * C[:, cols[ok]].t())
+    d2 = xn[:, None] - 2 * dots + (C * C).sum(1)[None]
+    best, idx = d2.min(1)
+    assign.copy_(idx.to(torch.int32))
+    if dist is not None:
+        dist.copy_(best.clamp_min(0))
+    return assign
+
+
+def kmeans_csr_accum(rowptr, cols, vals, assign, sums):
+    """sums[assign[i], col] += val for every non-zero of every point."""
+    if _gpu(sums):
+        kernels().kmeans_csr_accum(rowptr, cols, vals, assign, sums)
+        return sums
+    n = rowptr.numel() - 1
+    row = torch.repeat_interleave(torch.arange(n, device=sums.device), rowptr[1:] - rowptr[:-1])
+    ok = cols < sums.shape[1]
+    sums.index_put_((assign.to(torch.int64)[row[ok]], cols[ok]), vals[ok], accumulate=True)
+    return sums
+
+
 _KMEANS_CHUNK = 16384  # rows of S = X.C^T per GEMM (keeps the fp32 score block L2/MALL-sized)
 
 

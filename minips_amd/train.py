@@ -154,6 +154,30 @@ def build(args, comm):
         return m, {0: m.table}, \
             (lambda: _Skippable(SparseLRSynth(B, num_dims=nd, nnz=16 if args.small else 64, device=dev, seed=seed))), \
             (lambda b: -m.train_step(*b)), B
+    if args.model == "kmeans" and args.input:
+        # the reference K-Means input: sparse libsvm points (kmeans.cpp reads --input); the
+        # shard stays resident in HBM and batches are consecutive rows, cut on the device
+        from .models.kmeans import KMeans, KMeansConfig
+
+        shard = args._shard.to(dev)
+        nd = args.num_dims
+        if not nd:  # every rank must size the table alike: max feature id over all shards
+            t = torch.tensor([float(shard.cols.max()) + 1 if shard.cols.numel() else 1.0], device=dev)
+            comm.all_reduce_(t, op=dist.ReduceOp.MAX)
+            nd = int(t.item())
+        cfg = KMeansConfig(K=args.K or 8, dims=nd, consistency=args.consistency, staleness=args.staleness,
+                           init_mode=args.kmeans_init_mode or "random", seed=seed)
+        B = args.batch or 256
+        init = None
+        if args.kmeans_init_mode:
+            rp, c, v, _ = shard.batch(0, max(B, cfg.K))
+            init = torch.zeros(rp.numel() - 1, nd, dtype=torch.float32, device=dev)
+            row = torch.repeat_interleave(torch.arange(rp.numel() - 1, device=dev), rp[1:] - rp[:-1])
+            ok = c < nd
+            init.index_put_((row[ok], c[ok]), v[ok], accumulate=True)  # densify the seeding batch only
+        m = KMeans(cfg, comm, init_data=init)
+        return m, {0: m.table}, (lambda: _Skippable(_Batches(shard, B, seed))), \
+            (lambda b: m.train_step_csr(b[0], b[1], b[2])), B
     if args.model == "kmeans":
         from .models.kmeans import KMeans, KMeansConfig
 
@@ -279,7 +303,7 @@ def main(argv=None):
     generation = int(os.environ.get("MINIPS_GENERATION", "0"))
     hb = Heartbeat(args.heartbeat_dir, rank, args.heartbeat_interval, state_fn=lambda: comm.state()) \
         if args.heartbeat_interval > 0 and args.heartbeat_dir else None
-    if args.model == "lr" and args.input:
+    if args.model in ("lr", "kmeans") and args.input:
         from .data.loader import LibsvmData
 
         args._shard = LibsvmData(args.input, comm.rank, comm.world)

@@ -118,3 +118,66 @@ def test_train_driver_lr_map_storage_matches_vector():
         assert abs(a - b) <= 1e-4 * max(1.0, abs(b)), res
     for a, b in zip(cm, cv):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), res
+
+
+def _clustered_libsvm(path, n=800, seed=0):
+    """4 sparse clusters in 32 features: a point of cluster c has 6 of the 8 features
+    [8c, 8c+8) set to ~1 (libsvm, 1-based). Best SSE/point ~1.5; one centre ~4.9."""
+    import random
+
+    rng = random.Random(seed)
+    with open(path, "w") as f:
+        for _ in range(n):
+            c = rng.randrange(4)
+            feats = sorted(rng.sample(range(8 * c, 8 * c + 8), 6))
+            f.write("1" + "".join(f" {j + 1}:{1.0 + 0.05 * rng.uniform(-1, 1):.4f}" for j in feats) + "\n")
+
+
+def _kmeans_parity(tmp_path, device_env):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from _util import ensure_built, write_hostfile
+    from minips_amd import launch
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    data = str(tmp_path / "pts.svm")
+    _clustered_libsvm(data)
+    ensure_built("runtime", "apps")
+    hf = write_hostfile(str(tmp_path / "hosts"), 1)
+    rcs = launch.launch_nodes("kmeans", hf, [f"--input={data}", "--K=4", "--num_dims=32", "--num_iters=60",
+                                             "--batch_size=40", "--kmeans_init_mode=kmeans++",
+                                             "--num_workers_per_node=2", "--report_interval=10"],
+                              log_dir=str(tmp_path / "logs"), timeout=120)
+    assert rcs == [0], rcs
+    native = json.loads([l for l in open(tmp_path / "logs" / "node_0.log") if l.startswith("{")][-1])
+    native_pp = native["sampled_sse"] / 50.0
+    r = subprocess.run([sys.executable, "-m", "minips_amd.train", "--model", "kmeans", "--input", data, "--K", "4",
+                        "--num_dims", "32", "--kmeans_init_mode", "kmeans++", "--steps", "60", "--batch", "128"],
+                       cwd=root, capture_output=True, text=True, timeout=300, env=dict(os.environ, **device_env))
+    assert r.returncode == 0, r.stderr[-3000:]
+    ours = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    ours_pp = ours["losses"][-1][1]
+    return native_pp, ours_pp
+
+
+def test_kmeans_csr_matches_native_app(tmp_path):
+    """Sparse (libsvm) K-Means: the PS K-Means on CSR batches reaches the clustering quality of
+    the native C++ app (per-point updates, reference kmeans.cpp) on the same file (SSE/point
+    near the 1.5 optimum, far below the 4.9 of one centre). Parity unpinned beyond that:
+    batched vs per-point updates and different sampling."""
+    native_pp, ours_pp = _kmeans_parity(tmp_path, {"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+    # both well below one centre's 4.9; ours (batched 1/count steps) at least as good as the
+    # native per-point updates, which may leave two clusters under one centre (~3)
+    assert native_pp < 4.0 and ours_pp < 2.5, (native_pp, ours_pp)
+    assert ours_pp <= native_pp + 0.5, (native_pp, ours_pp)
+
+
+@pytest.mark.gpu
+def test_kmeans_csr_gpu_matches_native_app(dev, tmp_path):
+    """The same with the gfx950 CSR kernels (kmeans_assign_csr / kmeans_csr_accum)."""
+    native_pp, ours_pp = _kmeans_parity(tmp_path, {})
+    assert native_pp < 4.0 and ours_pp < 2.5, (native_pp, ours_pp)
+    assert ours_pp <= native_pp + 0.5, (native_pp, ours_pp)
