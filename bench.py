@@ -37,7 +37,8 @@ def main():
     ap.add_argument("--consistency", default="bsp", choices=["bsp", "ssp", "asp"])
     ap.add_argument("--staleness", type=int, default=0)
     ap.add_argument("--test-cards", default="", help=argparse.SUPPRESS)
-    ap.add_argument("--profile-steps", type=int, default=0, help="after the timed run: host issue time per step and a cProfile of N more steps (stderr)")
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="after the timed run: host issue time per step and a cProfile of N more steps (stderr)")
     args = ap.parse_args()
 
     from minips_amd.data.synthetic import CriteoSynth
@@ -73,7 +74,8 @@ def main():
     step = feeder.step
     # one rank: after eager warm-up steps the whole step is captured into one HIP graph
     # (GraphedFeeder) and the remaining warm-up and all timed steps are graph replays
-    use_graph = dev.type == "cuda" and n == 1 and args.consistency == "bsp" and os.environ.get("MINIPS_GRAPH", "0") == "1"
+    use_graph = dev.type == "cuda" and n == 1 and args.consistency == "bsp" and os.environ.get("MINIPS_GRAPH",
+                                                                                               "0") == "1"
     eager_warm = max(1, args.warmup - 1) if use_graph else args.warmup
 
     loss0 = None

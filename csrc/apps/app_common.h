@@ -14,7 +14,14 @@
 
 namespace minips_app {
 
-using namespace minips;
+using minips::Context;
+using minips::Master;
+using minips::ModelType;
+using minips::Node;
+using minips::ParseFile;
+using minips::StorageType;
+using minips::SVMItem;
+
 
 inline void DefineCommonFlags() {
   auto& c = Context::Get();
@@ -40,7 +47,8 @@ inline ModelType ParseModelType(const std::string& s) {
   if (s == "ASP") return ModelType::ASP;
   return ModelType::SSP;
 }
-inline StorageType ParseStorageType(const std::string& s) { return s == "Map" ? StorageType::Map : StorageType::Vector; }
+inline StorageType ParseStorageType(const std::string& s) { return s == "Map" ? StorageType::Map
+                                                           : StorageType::Vector; }
 
 // Webspam-shaped synthetic samples with a sparse linear teacher (labels +1/-1).
 inline std::vector<SVMItem> SyntheticData(int rows, int64_t dims, int nnz, uint64_t seed) {

@@ -71,7 +71,8 @@ int main(int argc, char** argv) {
   auto table_id = engine.CreateTable<double>(engine.getRanges(), ParseModelType(ctx.get_string("kModelType")),
                                              ParseStorageType(ctx.get_string("kStorageType")),
                                              ctx.get_int32("kStaleness"));
-  if (ctx.get_bool("init_dump") && ctx.get_bool("checkpoint_toggle")) DumpSVMData(ck.prefix + "worker_" + std::to_string(me.id), data);
+  if (ctx.get_bool("init_dump") && ctx.get_bool("checkpoint_toggle")) DumpSVMData(ck.prefix + "worker_"
+                                                                                  + std::to_string(me.id), data);
   if (recovering) CheckFaultTolerance(4, "node " + std::to_string(me.id) + " restored its shard");
 
   MLTask task;

@@ -15,7 +15,9 @@ namespace {
 
 using minips_k::bf16_t;
 
-hipStream_t stream_of(const at::Tensor& t) { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream(); }
+hipStream_t stream_of(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
 
 void check_gpu(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -416,7 +418,8 @@ void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g
                        step_dev.has_value() && step_dev->defined() ? step_dev->data_ptr<int>() : nullptr, zero_g);
 }
 
-void sgd_apply(at::Tensor& w, const at::Tensor& g, double lr, double grad_scale, const c10::optional<at::Tensor>& w_bf16) {
+void sgd_apply(at::Tensor& w, const at::Tensor& g, double lr, double grad_scale,
+               const c10::optional<at::Tensor>& w_bf16) {
   check_gpu(w, "w");
   check_gpu(g, "g");
   TORCH_CHECK(w.numel() == g.numel(), "sizes differ");
@@ -471,7 +474,8 @@ void lr_sparse_step(const at::Tensor& rowptr, const at::Tensor& cols, const at::
                            labels.numel(), ptr<float>(w), (float)alpha, d, c, stream_of(w));
 }
 
-void kmeans_assign(const at::Tensor& X, const at::Tensor& C, at::Tensor& assign, const c10::optional<at::Tensor>& dist) {
+void kmeans_assign(const at::Tensor& X, const at::Tensor& C, at::Tensor& assign,
+                   const c10::optional<at::Tensor>& dist) {
   check_gpu(X, "X");
   check_gpu(C, "C");
   check_gpu(assign, "assign");
@@ -517,7 +521,8 @@ void kmeans_argmin(const at::Tensor& S, const at::Tensor& cn, const at::Tensor& 
 void criteo_synth(int64_t seed, int64_t step, const c10::optional<at::Tensor>& step_dev, const at::Tensor& cards,
                   const at::Tensor& offsets, const at::Tensor& w, at::Tensor& dense, at::Tensor& keys,
                   at::Tensor& labels) {
-  for (const at::Tensor* t : {&cards, &offsets, &w, (const at::Tensor*)&dense, (const at::Tensor*)&keys, (const at::Tensor*)&labels}) check_gpu(*t, "criteo_synth arg");
+  for (const at::Tensor* t : {&cards, &offsets, &w, (const at::Tensor*)&dense, (const at::Tensor*)&keys,
+                              (const at::Tensor*)&labels}) check_gpu(*t, "criteo_synth arg");
   check_dtype(keys, at::kLong, "keys");
   check_dtype(cards, at::kLong, "cards");
   const int64_t B = labels.numel();
@@ -644,7 +649,8 @@ void attn_fwd(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H, double sca
                      ptr<bf16_t>(O), (int)O.stride(0), ptr<float>(lse), stream_of(qkv));
 }
 
-void attn_bwd(const at::Tensor& qkv, const at::Tensor& O, const at::Tensor& dO, const at::Tensor& lse, at::Tensor& delta,
+void attn_bwd(const at::Tensor& qkv, const at::Tensor& O, const at::Tensor& dO, const at::Tensor& lse,
+              at::Tensor& delta,
               int64_t B, int64_t T, int64_t H, double scale, at::Tensor& dqkv) {
   const int64_t d = H * 64;
   check_rows(qkv, B * T, 3 * d, "qkv");
@@ -712,7 +718,8 @@ void embed_fwd(const at::Tensor& wte, const at::Tensor& wpe, const at::Tensor& t
 }
 
 void embed_bwd(const at::Tensor& dx, const at::Tensor& tok, int64_t T, at::Tensor& dwte, at::Tensor& dwpe) {
-  for (const at::Tensor* t : {&dx, &tok, (const at::Tensor*)&dwte, (const at::Tensor*)&dwpe}) check_gpu(*t, "embed arg");
+  for (const at::Tensor* t : {&dx, &tok, (const at::Tensor*)&dwte, (const at::Tensor*)&dwpe}) check_gpu(*t,
+                                                                                                        "embed arg");
   check_dtype(dx, at::kBFloat16, "dx");
   check_dtype(tok, at::kLong, "tok");
   check_dtype(dwte, at::kFloat, "dwte");
@@ -849,7 +856,8 @@ void kmeans_assign_csr(const at::Tensor& rowptr, const at::Tensor& cols, const a
 
 void kmeans_csr_accum(const at::Tensor& rowptr, const at::Tensor& cols, const at::Tensor& vals,
                       const at::Tensor& assign, at::Tensor& sums) {
-  for (const at::Tensor* t : {&rowptr, &cols, &vals, &assign, (const at::Tensor*)&sums}) check_gpu(*t, "kmeans_csr arg");
+  for (const at::Tensor* t : {&rowptr, &cols, &vals, &assign, (const at::Tensor*)&sums}) check_gpu(*t,
+                                                                                                   "kmeans_csr arg");
   check_dtype(vals, at::kFloat, "vals");
   check_dtype(sums, at::kFloat, "sums");
   check_dtype(assign, at::kInt, "assign");
@@ -906,9 +914,11 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("scale"), py::arg("n_dev") = py::none());
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
-  m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1);
+  m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"),
+        py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1);
   m.def("wd_head", &wd_head);
-  m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"), py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
+  m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
+        py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none());
   m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none(),
         py::arg("counts_ready") = false);

@@ -117,7 +117,8 @@ PYBIND11_MODULE(_runtime, m) {
       .value("kRollBack", Flag::kRollBack)
       .value("kScale", Flag::kScale)
       .value("kScaleRollback", Flag::kScaleRollback);
-  py::enum_<ModelType>(m, "ModelType").value("SSP", ModelType::SSP).value("BSP", ModelType::BSP).value("ASP", ModelType::ASP);
+  py::enum_<ModelType>(m, "ModelType").value("SSP", ModelType::SSP).value("BSP", ModelType::BSP).value("ASP",
+      ModelType::ASP);
   py::enum_<StorageType>(m, "StorageType").value("Map", StorageType::Map).value("Vector", StorageType::Vector);
 
   py::class_<Node>(m, "Node")
@@ -151,7 +152,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def("begin", &Range::begin)
       .def("end", &Range::end)
       .def("size", &Range::size)
-      .def("__repr__", [](const Range& r) { return "[" + std::to_string(r.begin()) + "," + std::to_string(r.end()) + ")"; });
+      .def("__repr__", [](const Range& r) { return "[" + std::to_string(r.begin()) + ","
+                                                     + std::to_string(r.end()) + ")"; });
   m.def("even_ranges", &EvenRanges);
 
   // --- Context (typed flag registry) --------------------------------------------------
@@ -232,12 +234,14 @@ PYBIND11_MODULE(_runtime, m) {
   py::class_<RangePartitionManager>(m, "RangePartitionManager")
       .def(py::init<const std::vector<uint32_t>&, const std::vector<Range>&, int>(), py::arg("server_thread_ids"),
            py::arg("ranges"), py::arg("master_node_id") = -1)
-      .def("slice", [](const RangePartitionManager& pm, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> keys) {
+      .def("slice", [](const RangePartitionManager& pm, py::array_t<uint64_t,
+                       py::array::c_style | py::array::forcecast> keys) {
         SArray<Key> k(keys.data(), keys.size());
         std::vector<std::pair<int, Keys>> sliced;
         pm.Slice(k, &sliced);
         py::list out;
-        for (auto& s : sliced) out.append(py::make_tuple(s.first, py::array_t<uint64_t>(s.second.size(), s.second.data())));
+        for (auto& s : sliced) out.append(py::make_tuple(s.first, py::array_t<uint64_t>(s.second.size(),
+                                                                                        s.second.data())));
         return out;
       })
       .def("get_ranges", &RangePartitionManager::GetRanges);
@@ -249,8 +253,10 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readonly("node_id", &Info::node_id)
       .def("create_kv_client_table",
            [](const Info& info, uint32_t table_id, const std::string& dtype) -> py::object {
-             if (dtype == "float32") return py::cast(info.CreateKVClientTable<float>(table_id).release(), py::return_value_policy::take_ownership);
-             return py::cast(info.CreateKVClientTable<double>(table_id).release(), py::return_value_policy::take_ownership);
+             if (dtype == "float32") return py::cast(info.CreateKVClientTable<float>(table_id).release(),
+                                                     py::return_value_policy::take_ownership);
+             return py::cast(info.CreateKVClientTable<double>(table_id).release(),
+                             py::return_value_policy::take_ownership);
            },
            py::arg("table_id"), py::arg("dtype") = "float64");
   BindTable<double>(m, "KVClientTableF64");
@@ -391,7 +397,8 @@ PYBIND11_MODULE(_runtime, m) {
         meta["world"] = h.meta.world;
         meta["kind"] = h.meta.kind;
         py::list arrays;
-        for (const auto& a : h.arrays) arrays.append(py::make_tuple(a.name, DTypeName(a.dtype), a.rows, a.cols, a.offset));
+        for (const auto& a : h.arrays) arrays.append(py::make_tuple(a.name, DTypeName(a.dtype), a.rows,
+                                                                    a.cols, a.offset));
         return py::make_tuple(meta, arrays);
       },
       py::arg("path"));

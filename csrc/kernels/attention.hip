@@ -88,7 +88,8 @@ __device__ __forceinline__ void tile_load(const bf16_t* G, int64_t ld, int r0, i
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int c = tid + h * 256, r = c >> 3, col = (c & 7) * 8;
-    t.v[h] = (r0 + r < rows) ? *reinterpret_cast<const uint4*>(G + (int64_t)(r0 + r) * ld + col) : make_uint4(0, 0, 0, 0);
+    t.v[h] = (r0 + r < rows) ? *reinterpret_cast<const uint4*>(G + (int64_t)(r0 + r) * ld + col)
+        : make_uint4(0, 0, 0, 0);
   }
 }
 __device__ __forceinline__ void tile_store(bf16_t* S, int tid, const TileRegs& t) {
@@ -277,7 +278,8 @@ __global__ void attn_prep_kernel(const bf16_t* __restrict__ O, int ldo, const bf
 }
 
 // ------------------------------------------------------------------------------ dQ
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, int ldq, const bf16_t* __restrict__ dO,
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, int ldq,
+                                                          const bf16_t* __restrict__ dO,
                                                           int lddo, const float* __restrict__ lse,
                                                           const float* __restrict__ delta, int T, int H, int dmodel,
                                                           float sl2, float scale, bf16_t* __restrict__ dqkv, int lddq) {
@@ -385,7 +387,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16_t* __restr
                                                            const bf16_t* __restrict__ dO, int lddo,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta, int T, int H, int dmodel,
-                                                           float sl2, float scale, bf16_t* __restrict__ dqkv, int lddq) {
+                                                           float sl2, float scale, bf16_t* __restrict__ dqkv,
+                                                               int lddq) {
   __shared__ __attribute__((aligned(16))) bf16_t sm[2][2][TILE * LP];  // [buf][Q|dO]
   __shared__ float srow[2][2][TILE];                                    // [buf][lse|delta]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;

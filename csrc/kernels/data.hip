@@ -29,7 +29,8 @@ __device__ __forceinline__ int64_t raw_id(uint64_t sb, int f, int64_t card) {
 }
 
 // Index space B*F (one key each) + B (dense features + label): no serial per-sample loop.
-__global__ void criteo_synth_kernel(uint64_t seed, uint64_t step, const int64_t* __restrict__ step_dev, int64_t B, int F,
+__global__ void criteo_synth_kernel(uint64_t seed, uint64_t step, const int64_t* __restrict__ step_dev,
+                                    int64_t B, int F,
                                     const int64_t* __restrict__ cards,
                                     const int64_t* __restrict__ offsets, int n_dense, const float* __restrict__ w,
                                     float* __restrict__ dense, int64_t* __restrict__ keys, float* __restrict__ labels) {
@@ -81,7 +82,8 @@ void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t
                   hipStream_t s) {
   if (B <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(criteo_synth_kernel, grid_for(B * (F + 1), block, 4096), block, 0, s, seed, step, step_dev, B, F, cards, offsets,
+  hipLaunchKernelGGL(criteo_synth_kernel, grid_for(B * (F + 1), block, 4096), block, 0, s, seed, step,
+                     step_dev, B, F, cards, offsets,
                      n_dense, w,
                      dense, keys, labels);
   MINIPS_HIP_CHECK(hipGetLastError());

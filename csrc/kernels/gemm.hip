@@ -123,7 +123,8 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
     const int col = nb + j * 16 + col_l;
     const bool col_ok = col < N;
     float bias = 0.f;
-    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
+    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16
+        || EPI == kEpiBiasGeluAuxBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
     float csum = 0.f;
 #pragma unroll
     for (int i = 0; i < MR; ++i) {
@@ -827,18 +828,23 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
   return nsplit;
 }
 
-#define MINIPS_GEMM_EPI_DISPATCH(AKM, BKN)                                                        \
-  switch (epi) {                                                                                 \
-    case kEpiStoreF32: nsplit = launch<AKM, BKN, kEpiStoreF32>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break;  \
-    case kEpiAtomicF32: nsplit = launch<AKM, BKN, kEpiAtomicF32>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiBiasReluBf16: nsplit = launch<AKM, BKN, kEpiBiasReluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiBiasBf16: nsplit = launch<AKM, BKN, kEpiBiasBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiBiasGeluBf16: nsplit = launch<AKM, BKN, kEpiBiasGeluBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiStoreBf16: nsplit = launch<AKM, BKN, kEpiStoreBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiReluMaskBf16: nsplit = launch<AKM, BKN, kEpiReluMaskBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiBiasGeluAuxBf16: nsplit = launch<AKM, BKN, kEpiBiasGeluAuxBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    case kEpiGeluGradBf16: nsplit = launch<AKM, BKN, kEpiGeluGradBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); break; \
-    default: throw std::runtime_error("gemm: unknown epilogue " + std::to_string(epi));           \
+#define MINIPS_EPI_CASE(AKM, BKN, E)                                          \
+  case E:                                                                     \
+    nsplit = launch<AKM, BKN, E>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); \
+    break;
+#define MINIPS_GEMM_EPI_DISPATCH(AKM, BKN)                                        \
+  switch (epi) {                                                                 \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiStoreF32)                                      \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiAtomicF32)                                     \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiBiasReluBf16)                                  \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiBiasBf16)                                      \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiBiasGeluBf16)                                  \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiStoreBf16)                                     \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiReluMaskBf16)                                  \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiBiasGeluAuxBf16)                               \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiGeluGradBf16)                                  \
+    default:                                                                     \
+      throw std::runtime_error("gemm: unknown epilogue " + std::to_string(epi)); \
   }
 
 // out[r][c] (ldc) += sum_s slab[s][r][c]   (slab [nsplit][M][N] fp32, float4 over columns)

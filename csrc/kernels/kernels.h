@@ -124,7 +124,8 @@ void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const i
 // ------------------------------------------------------------------ optimizers (optim.hip)
 // Fused Adam(W) on an fp32 master shard; optionally writes the bf16 copy for all-gather.
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2,
-                float eps, float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s, const int* step_dev = nullptr,
+                float eps, float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s,
+                    const int* step_dev = nullptr,
                 bool zero_g = false);
 void sgd_apply(float* w, const float* g, int64_t n, float lr, float grad_scale, bf16_t* w_bf16, hipStream_t s);
 void adagrad_apply(float* w, float* acc, const float* g, int64_t n, float lr, float eps, float grad_scale,

@@ -62,7 +62,8 @@ __device__ __forceinline__ void st4(bf16_t* p, const float v[4]) {
 __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16_t* __restrict__ x, int ldx, int64_t M, int C,
                                                             const bf16_t* __restrict__ gamma,
                                                             const bf16_t* __restrict__ beta, float eps,
-                                                            bf16_t* __restrict__ y, int ldy, float* __restrict__ mean_out,
+                                                            bf16_t* __restrict__ y, int ldy,
+                                                                float* __restrict__ mean_out,
                                                             float* __restrict__ rstd_out) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -119,7 +120,8 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16_t* __rest
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __restrict__ x, int ldx,
                                                             const bf16_t* __restrict__ dy, int lddy, int64_t M, int C,
                                                             const bf16_t* __restrict__ gamma,
-                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                            const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
                                                             bf16_t* __restrict__ dx, int lddx,
                                                             float* __restrict__ partial, bool accumulate_dx) {
   __shared__ float red[4][2][1024];
@@ -255,7 +257,8 @@ void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t
 constexpr int kXentThreads = 512, kXentChunks = 13;
 
 // Component q of a uint4 without taking its address (keeps the chunk array in registers).
-__device__ __forceinline__ uint32_t u4get(const uint4& v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w; }
+__device__ __forceinline__ uint32_t u4get(const uint4& v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2
+                                                                  ? v.z : v.w; }
 __device__ __forceinline__ float u4elem(const uint4& v, int q) {
   const uint32_t w = u4get(v, q >> 1);
   return (q & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
@@ -571,7 +574,8 @@ __global__ __launch_bounds__(256) void dlrm_interact_bwd_kernel(const bf16_t* __
 
 void dlrm_interact_fwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, bf16_t* out, int ldo, hipStream_t s) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(dlrm_interact_fwd_kernel, (int)std::min<int64_t>(B, 8192), 256, NV * (D + 1) * sizeof(float), s, V, B,
+  hipLaunchKernelGGL(dlrm_interact_fwd_kernel, (int)std::min<int64_t>(B, 8192), 256, NV * (D + 1)
+                     * sizeof(float), s, V, B,
                      NV, D, dense_idx, out, ldo);
   MINIPS_HIP_CHECK(hipGetLastError());
 }

@@ -68,7 +68,8 @@ void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float l
   if (w_bf16 && (reinterpret_cast<uintptr_t>(w_bf16) & 7)) throw std::runtime_error("adam w_bf16 must be 8B aligned");
   const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
   const int block = 256;
-  hipLaunchKernelGGL(adam_kernel, grid_for((n + 3) / 4, block), block, 0, s, w, m, v, const_cast<float*>(g), n, lr, beta1, beta2, eps,
+  hipLaunchKernelGGL(adam_kernel, grid_for((n + 3) / 4, block), block, 0, s, w, m, v, const_cast<float*>(g),
+                     n, lr, beta1, beta2, eps,
                      weight_decay, bc1, bc2, grad_scale, w_bf16, step_dev, zero_g);
   MINIPS_HIP_CHECK(hipGetLastError());
 }

@@ -256,7 +256,8 @@ void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* boun
   int64_t* sh_cursor = cursor + (size_t)S * P;
   int* slot_cnt = csr_counts ? reinterpret_cast<int*>(sh_cursor + (size_t)S * P) : nullptr;
   if (csr_counts) extra_zero_bytes += cap * (int64_t)sizeof(int);
-  MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, (cap + P + 1 + 2 * (int64_t)S * P) * sizeof(int64_t) + extra_zero_bytes, s));
+  MINIPS_HIP_CHECK(hipMemsetAsync(table_keys, 0, (cap + P + 1 + 2 * (int64_t)S * P) * sizeof(int64_t)
+                                  + extra_zero_bytes, s));
   if (n == 0) return;
   const int block = 256;
   const int grid = grid_for(n, block, 4096);
@@ -545,7 +546,8 @@ void sparse_sgd(float* table, int64_t ld, const int64_t* keys, int64_t n, int64_
                 float scale, hipStream_t s, const int64_t* n_dev) {
   if (n <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(sparse_sgd_kernel, grid_for(n * D, block), block, 0, s, table, ld, keys, n, base, D, grads, scale, n_dev);
+  hipLaunchKernelGGL(sparse_sgd_kernel, grid_for(n * D, block), block, 0, s, table, ld, keys, n, base, D,
+                     grads, scale, n_dev);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -232,10 +232,14 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
   const int block = 64 * kHeadWaves;
   const int grid = (int)std::min<int64_t>(128, (B + 63) / 64);  // per-block LDS reduction, then atomics
   switch (Hd) {
-    case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
-    case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
-    case 64 * 4: hipLaunchKernelGGL(wd_head_kernel<4>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
-    case 64 * 8: hipLaunchKernelGGL(wd_head_kernel<8>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+    case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+    case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+    case 64 * 4: hipLaunchKernelGGL(wd_head_kernel<4>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+    case 64 * 8: hipLaunchKernelGGL(wd_head_kernel<8>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
     default: throw std::runtime_error("wd_head: Hd must be 64, 128, 256 or 512, got " + std::to_string(Hd));
   }
   MINIPS_HIP_CHECK(hipGetLastError());
@@ -610,7 +614,8 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
 }
 
 // Zero rows [0, min(U, *U_dev)) of an fp32 [*, stride] matrix (float4 stores; stride % 4 == 0).
-__global__ void zero_rows_dev_kernel(float* __restrict__ rows, int stride, int64_t U, const int64_t* __restrict__ U_dev) {
+__global__ void zero_rows_dev_kernel(float* __restrict__ rows, int stride, int64_t U,
+                                     const int64_t* __restrict__ U_dev) {
   const int64_t n = min(U, *U_dev) * (stride >> 2);
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
     reinterpret_cast<float4*>(rows)[c] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -632,7 +637,8 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
   if (!zeroed_cc) MINIPS_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int) * 2 * (size_t)U, s));
   dim3 grid((unsigned)((B + kEmbTB - 1) / kEmbTB), (unsigned)F);
   // counts_ready: the dedupe already wrote the per-row lookup counts into zeroed_cc[0, U)
-  if (!(counts_ready && zeroed_cc)) hipLaunchKernelGGL(emb_seg_count_kernel, grid, dim3(kEmbTB), 0, s, inv, B, F, counts);
+  if (!(counts_ready && zeroed_cc)) hipLaunchKernelGGL(emb_seg_count_kernel, grid, dim3(kEmbTB), 0, s, inv, B,
+                                                       F, counts);
   hipLaunchKernelGGL(emb_scan_reduce_kernel, ntiles, 256, 0, s, counts, U, tiles);
   hipLaunchKernelGGL(emb_scan_top_kernel, 1, 256, 0, s, tiles, ntiles);
   hipLaunchKernelGGL(emb_scan_final_kernel, ntiles, 256, 0, s, counts, U, tiles, offsets);

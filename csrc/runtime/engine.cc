@@ -360,7 +360,8 @@ void Engine::OnScaleRollBack(const Node& n) {
 void Engine::UpdateAndRestart(int failed_node_id) {
   {
     std::lock_guard<std::mutex> lk(nodes_mu_);
-    nodes_.erase(std::remove_if(nodes_.begin(), nodes_.end(), [&](const Node& n) { return (int)n.id == failed_node_id; }),
+    nodes_.erase(std::remove_if(nodes_.begin(), nodes_.end(),
+                                [&](const Node& n) { return (int)n.id == failed_node_id; }),
                  nodes_.end());
   }
   auto nodes = GetNodes();

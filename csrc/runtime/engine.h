@@ -62,7 +62,8 @@ class MLTask {
 class Engine : public MailboxHooks {
  public:
   // `master` with is_master=false means "no master". `scale_node` with port<=0 = none.
-  Engine(const Node& node, const std::vector<Node>& nodes, const Node& master = Node(), const Node& scale_node = Node());
+  Engine(const Node& node, const std::vector<Node>& nodes, const Node& master = Node(),
+         const Node& scale_node = Node());
   ~Engine() override;
 
   void StartEverything(int num_server_threads_per_node = 1);

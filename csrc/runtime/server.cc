@@ -96,7 +96,8 @@ void ProgressTracker::Restore(const std::string& path, int scale_node_id) {
       int tid = std::stoi(k);
       progresses_[tid] = v;
       if (scale_node_id >= 0) {
-        int mid = scale_node_id * (int)SimpleIdMapper::kMaxThreadsPerNode + tid % (int)SimpleIdMapper::kMaxThreadsPerNode;
+        int mid = scale_node_id * (int)SimpleIdMapper::kMaxThreadsPerNode
+            + tid % (int)SimpleIdMapper::kMaxThreadsPerNode;
         progresses_[mid] = v;
       }
     }
@@ -324,7 +325,8 @@ void BSPModel::Get(Message& msg) {
     ReplyGet(msg);
   } else {
     MINIPS_CHECK(false, "progress error in BSPModel::Get { get progress: " << progress
-                                                                          << ", min clock: " << tracker_.GetMinClock() << " }");
+                                                                          << ", min clock: "
+                                                                          << tracker_.GetMinClock() << " }");
   }
 }
 

@@ -116,7 +116,8 @@ inline int RunAll(int argc, char** argv) {
 #define EXPECT_TRUE(a) MT_CHECK_OP((bool)(a), true, ==, false)
 #define EXPECT_FALSE(a) MT_CHECK_OP((bool)(a), false, ==, false)
 #define ASSERT_TRUE(a) MT_CHECK_OP((bool)(a), true, ==, true)
-#define EXPECT_DOUBLE_EQ(a, b) MT_CHECK_OP(std::fabs((double)(a) - (double)(b)) <= 1e-12 * (1 + std::fabs((double)(b))), true, ==, false)
+#define EXPECT_DOUBLE_EQ(a, b) \
+  MT_CHECK_OP(std::fabs((double)(a) - (double)(b)) <= 1e-12 * (1 + std::fabs((double)(b))), true, ==, false)
 #define EXPECT_NEAR(a, b, tol) MT_CHECK_OP(std::fabs((double)(a) - (double)(b)) <= (tol), true, ==, false)
 #define EXPECT_THROW(stmt)                                                     \
   do {                                                                         \

@@ -950,7 +950,8 @@ TEST(ShardIO, BinaryAndTextRoundTrip) {
   const std::string dir = "/tmp/minips_shard_test_" + std::to_string(::getpid()) + "/";
   AsyncShardWriter w;
   auto t = w.Submit([&] {
-    WriteShard(dir + "a.bin", m, {{"params", params.data(), DType::kF32, 3, 2}, {"state", state.data(), DType::kF32, 3, 1}});
+    WriteShard(dir + "a.bin", m, {{"params", params.data(), DType::kF32, 3, 2}, {"state", state.data(),
+                                                                                 DType::kF32, 3, 1}});
     WriteTextParams(dir + "a.txt", {"params", params.data(), DType::kF32, 3, 2});
   });
   w.Wait(t);

@@ -58,7 +58,7 @@ class WideDeepConfig:
 _PLAN_AT = os.environ.get("MINIPS_PLAN_AT", "start")
 # issue an async dense clock from the weight-gradient side stream (see train_step). Measured
 # slower on one MI355X (MINIPS_OVERLAP_W1=dense: 0.525-0.529 -> 0.544-0.549 ms/step: Adam then
-# competes with the memory-bound embedding backward; tools/gpu_dense_side.sh), so off by default.
+# competes with the memory-bound embedding backward; tools/gpu_ab.sh), so off by default.
 _DENSE_CLOCK_ON_SIDE = os.environ.get("MINIPS_DENSE_CLOCK_ON_SIDE", "0") == "1"
 
 

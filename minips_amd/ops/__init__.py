@@ -125,14 +125,14 @@ _WGRAD_BLOCKS = int(__import__("os").environ.get("MINIPS_WGRAD_BLOCKS", "256" if
 # 0.550 ms at 2048; the MLP step loses 15 % at 2048 when its wgrads are on the critical path).
 _WGRAD_MIN_ROWS = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS", "512" if _WGRAD_MODE == "v3" else "640"))
 # round 2 (LDS-staged epilogue, v2 wgrad): 1024 rows per overlapped split measured best
-# (W&D 0.461 ms vs 0.490 at 2048; tools/gpu_wgrad_ab2.sh)
+# (W&D 0.461 ms vs 0.490 at 2048; tools/gpu_ab.sh, profiles/r2/gemm_round2.txt)
 _WGRAD_MIN_ROWS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS_OVERLAP",
                                                            "512" if _WGRAD_MODE == "v3" else "1024"))
 # Overlapped wgrads with few output tiles (W&D's 256x512 W3 grad: 8 tiles) would get only ~64
 # workgroups at 2048 rows per split; this floor on the block count (0: off) lets them split finer
 # (never below _WGRAD_MIN_ROWS rows per split). Measured worse on one MI355X (W&D 0.528 ->
 # 0.539 ms/step at 128 blocks, 0.548 at 256: the finer splits steal CUs from the dgrad chain and
-# add slab traffic; tools/gpu_wgrad_blocks.sh), so it stays off.
+# add slab traffic; tools/gpu_ab.sh), so it stays off.
 _WGRAD_MIN_BLOCKS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_BLOCKS_OVERLAP", "0"))
 _overlap_state = __import__("threading").local()
 
@@ -746,7 +746,8 @@ def dlrm_interact_bwd(V, NV, D, dout, dV, d_dense, dense_idx=0):
     d = dz @ v
     d[:, dense_idx] += dout[:, :D].float()
     dV.view(B, NV, D).copy_(d)
-    d_dense.copy_(torch.where(v[:, dense_idx] > 0, d[:, dense_idx], torch.zeros_like(d[:, dense_idx])).to(d_dense.dtype))
+    d_dense.copy_(torch.where(v[:, dense_idx] > 0, d[:, dense_idx], torch.zeros_like(d[:,
+                                                                                       dense_idx])).to(d_dense.dtype))
     return dV
 
 

@@ -63,7 +63,8 @@ class Comm:
         self.world = dist.get_world_size(group) if self.initialized else 1
         self.backend = dist.get_backend(group) if self.initialized else "none"
         if device is None:
-            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+            device = torch.device("cuda",
+                                  torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
         self.device = device
         self.stats = CommStats()
         self._plan_stream = None

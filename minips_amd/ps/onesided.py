@@ -152,7 +152,8 @@ class OneSidedSparseTable:
                 dist.broadcast_object_list(box, src=0, group=comm.group)
                 name = box[0]
             self._paths = [os.path.join("/dev/shm", f"{name}_{r}") for r in range(comm.world)]
-            mine = np.memmap(self._paths[comm.rank], dtype=np.float32, mode="w+", shape=(max(1, self.rows_local), width))
+            mine = np.memmap(self._paths[comm.rank], dtype=np.float32, mode="w+", shape=(max(1,
+                                                                                             self.rows_local), width))
             mine[:] = 0
             mine.flush()
             if comm.world > 1:

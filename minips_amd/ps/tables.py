@@ -49,12 +49,13 @@ class _Pipeline:
     """Tracks in-flight Clock work issued on a side HIP stream.
 
     On the GPU every consistency model runs the Clock's communication + apply on the table's
-    own stream (its collectives join the rank's single ordered communicator, ps/comm.py) and gates READS instead of the issue: a Get at
-    clock c waits only for the update of clock c - s - 1. BSP is s = 0 (the Get waits for the
-    previous Clock -- the reference rule that Gets after a Clock see the new values), but the
-    Clock itself now overlaps with whatever the worker does before its next Get (the rest of
-    the backward pass, the next batch's key planning and dense assembly). SSP(s) relaxes the
-    gate to s clocks, ASP to a fixed pipelining depth. On CPU (gloo tests) the work runs inline.
+    own stream (its collectives join the rank's single ordered communicator, ps/comm.py) and
+    gates READS instead of the issue: a Get at clock c waits only for the update of clock
+    c - s - 1. BSP is s = 0 (the Get waits for the previous Clock -- the reference rule that
+    Gets after a Clock see the new values), but the Clock itself now overlaps with whatever the
+    worker does before its next Get (the rest of the backward pass, the next batch's key
+    planning and dense assembly). SSP(s) relaxes the gate to s clocks, ASP to a fixed
+    pipelining depth. On CPU (gloo tests) the work runs inline.
     """
 
     def __init__(self, comm: Comm, consistency: str, staleness: int, overlap: bool | None = None,

@@ -123,7 +123,8 @@ def build(args, comm):
         cfg = GPT2Config(consistency=args.consistency, staleness=args.staleness, **kw)
         m = GPT2(cfg, comm)
         B = args.batch or (2 if args.small else 8)
-        return m, {0: m.table}, (lambda: _Skippable(TokenSynth(B, cfg.n_ctx, vocab=cfg.vocab, device=dev, seed=seed))), \
+        return m, {0: m.table}, (lambda: _Skippable(TokenSynth(B, cfg.n_ctx, vocab=cfg.vocab, device=dev,             \
+                                                               seed=seed))),                                          \
             (lambda b: m.train_step(*b)), B * cfg.n_ctx
     if args.model == "lr" and args.input:
         # reference LR on a libsvm file (lr_example.cpp --input): this rank's shard is loaded by the

@@ -42,7 +42,8 @@ def main():
     fl = 4.0 * B * H * T * T / 2 * 64
     tf = timeit(lambda: ops.attn_fwd(qkv, B, T, H, 0.125, O, lse))
     tb = timeit(lambda: ops.attn_bwd(qkv, O, dO, lse, delta, B, T, H, 0.125, dqkv))
-    print(f"ours  fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF/s   bwd {tb * 1e3:8.1f} us {2.5 * fl / tb / 1e9:7.1f} TF/s")
+    print(f"ours  fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF/s   "
+          f"bwd {tb * 1e3:8.1f} us {2.5 * fl / tb / 1e9:7.1f} TF/s")
     q, k, v = (qkv[:, i * d:(i + 1) * d].reshape(B, T, H, 64).transpose(1, 2).contiguous() for i in range(3))
     q.requires_grad_(True), k.requires_grad_(True), v.requires_grad_(True)
     go = dO.reshape(B, T, H, 64).transpose(1, 2).contiguous()

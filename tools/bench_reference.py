@@ -120,7 +120,8 @@ def recovery_table():
             print(f"{mode}: run failed (rc {rc}); supervisor stderr tail:\n```\n{sup[-2000:]}\n```\n")
             return
         res[mode] = (wall, ts)
-    print("| phase | restart mode (ms) | in-place mode (ms) | reference 5 machines (s, P6) | reference 15 machines (s, P7) |")
+    print("| phase | restart mode (ms) | in-place mode (ms) | reference 5 machines (s, P6) "
+          "| reference 15 machines (s, P7) |")
     print("|---|---|---|---|---|")
     (wr, (i1, a2, a3, a4, a5)), (wi, (j1, b2, b3, b4, b5)) = res["restart"], res["inplace"]
     print(f"| Phase2 detect failure (hang -> detected; 3 x heartbeat) | {a2 - i1} | {b2 - j1} | 8 | 7 |")

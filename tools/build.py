@@ -80,9 +80,11 @@ def _torch_flags() -> tuple[list[str], list[str]]:
     import torch.utils.cpp_extension as ce  # noqa: WPS433
 
     inc = []
-    for p in ce.include_paths("cuda") if "device_type" in ce.include_paths.__code__.co_varnames else ce.include_paths(True):
+    new_api = "device_type" in ce.include_paths.__code__.co_varnames
+    for p in ce.include_paths("cuda") if new_api else ce.include_paths(True):
         inc += ["-I", p]
-    libdir = ce.library_paths("cuda")[0] if "device_type" in ce.library_paths.__code__.co_varnames else ce.library_paths(True)[0]
+    new_api = "device_type" in ce.library_paths.__code__.co_varnames
+    libdir = ce.library_paths("cuda")[0] if new_api else ce.library_paths(True)[0]
     py_inc = sysconfig.get_paths()["include"]
     cflags = inc + ["-I", py_inc, "-DTORCH_EXTENSION_NAME=_kernels", "-DTORCH_API_INCLUDE_EXTENSION_H",
                     "-D_GLIBCXX_USE_CXX11_ABI=1", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1"]
@@ -153,7 +155,8 @@ def build_ops_py(kobjs: list[str]) -> str:
     bobj = os.path.join(OBJ, "ops_py.o")
     cflags, ldflags = _torch_flags()
     hdrs = _headers("csrc/kernels", "csrc/bindings")
-    _compile_many([(bobj, [src] + hdrs, [HIPCC, "-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", *cflags, "-c", src, "-o", bobj])])
+    _compile_many([(bobj, [src] + hdrs, [HIPCC, "-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+                                         *cflags, "-c", src, "-o", bobj])])
     _compile_many([(out, [bobj] + kobjs,
                     [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", bobj, *kobjs, "-o", out, *ldflags])])
     return out

@@ -9,6 +9,7 @@ cd "$(dirname "$0")/.."
 case "${1:-cpu}" in
   cpu)
     python tools/build.py
+    python tools/lint.py
     cmake -S . -B build/cmake -G Ninja -DMINIPS_BUILD_KERNELS=OFF > /dev/null
     cmake --build build/cmake -j "${MAX_JOBS:-8}" > /dev/null
     ctest --test-dir build/cmake --output-on-failure

@@ -45,7 +45,8 @@ def main():
             e.synchronize()
             ts.append(s.elapsed_time(e) / 5 * 1e3)
         t = sorted(ts)[len(ts) // 2]
-        print(f"{a.tag:10s} M={M} N={N} K={K:5d} {a.layout} split={a.split} {t:8.1f} us {2.0 * M * N * K / t / 1e6:7.1f} TF/s",
+        print(f"{a.tag:10s} M={M} N={N} K={K:5d} {a.layout} split={a.split} {t:8.1f} us "
+              f"{2.0 * M * N * K / t / 1e6:7.1f} TF/s",
               flush=True)
 
 
