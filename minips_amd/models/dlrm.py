@@ -21,6 +21,7 @@ from .. import ops
 from ..ps.comm import Comm
 from ..ps.tables import DenseTable, SparseTable
 from .layers import SideStream, Linear, ParamLayout, align, ext_activation
+from .feeder import LookaheadPlans
 
 
 @dataclass
@@ -44,7 +45,7 @@ class DLRMConfig:
     cards: list = field(default_factory=list)  # optional per-feature cardinalities (sum <= num_rows)
 
 
-class DLRM:
+class DLRM(LookaheadPlans):
     def __init__(self, cfg: DLRMConfig, comm: Comm):
         self.cfg, self.comm = cfg, comm
         D, F = cfg.D, cfg.F
@@ -105,21 +106,14 @@ class DLRM:
             )
         return self._bufs[B]
 
-    def prefetch(self, keys):
-        """Lookahead key planning of the next batch (see WideDeep.prefetch)."""
-        self._next_plan = (keys, self.emb.plan_async(keys, csr=True))
-
-    def train_step(self, dense, keys, labels, next_keys=None):
+    def train_step(self, dense, keys, labels, next_keys=None, next_on_plan_stream: bool = False):
         cfg = self.cfg
         B, F, D = dense.shape[0], cfg.F, cfg.D
         b = self._buffers(B)
-        pre = getattr(self, "_next_plan", None)
-        plan = pre[1] if pre is not None and pre[0] is keys else None
-        self._next_plan = None
-        if plan is None:
-            plan = self.emb.plan(keys, csr=True)
+        plan = self._take_plan(keys)
         if next_keys is not None:
-            self.prefetch(next_keys)
+            nk = next_keys() if callable(next_keys) else next_keys
+            self.prefetch(nk, keys_on_plan_stream=next_on_plan_stream)
         rows, plan = self.emb.get(keys, plan=plan)
         G = self.dense.grad
         # V = [emb_0 .. emb_{F-1} | bottom(dense)]  (the dense vector is the last one)
@@ -177,13 +171,6 @@ class DLRM:
         self.dense.clock()
         self._advance_next_plan()
         return b["loss"]
-
-    def _advance_next_plan(self):
-        """The step is issued: exchange the prefetched plan's keys now (planning stream), off
-        the next step's critical path (SparseTable.advance_plan)."""
-        pre = getattr(self, "_next_plan", None)
-        if pre is not None:
-            self._next_plan = (pre[0], self.emb.advance_plan(pre[1]))
 
     def drain(self):
         self.emb.drain()

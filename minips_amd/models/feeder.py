@@ -57,6 +57,46 @@ class LookaheadFeeder:
         return self.model.train_step(dense, keys, labels, next_keys=next_keys, next_on_plan_stream=self.cuda)
 
 
+class LookaheadPlans:
+    """Mixin of the recommendation models (WideDeep, DLRM): key plans issued ahead of the step
+    that uses them (``self.emb`` is the SparseTable). A plan goes through three issue points,
+    each placed so that the rank's single ordered communicator (ps/comm.py) never holds a
+    look-ahead collective in front of the current step's own exchanges:
+
+      prefetch (step n-d, planning stream)   dedupe + owner bucketing, no collective
+      end of step n-d                        all-to-all of the per-owner counts
+      end of step n-d+1 (d >= 2)             host reads the counts (issued a step earlier: no
+                                             wait on the current step), all-to-all of the keys
+                                             + owner-side dedupe
+      step n                                 row gather + row exchange only
+
+    With depth 1 the last two halves run at the start of step n (SparseTable._finish_plan)."""
+
+    def prefetch(self, keys, keys_on_plan_stream: bool = False):
+        """Start routing a future batch's keys on the planning stream; train_step picks the
+        plan up when that batch comes (a batch may be several steps ahead: data-loader depth)."""
+        pend = self.__dict__.setdefault("_pending_plans", [])
+        pend.append([keys, self.emb.plan_async(keys, csr=True, keys_on_plan_stream=keys_on_plan_stream)])
+
+    def _take_plan(self, keys):
+        pend = self.__dict__.setdefault("_pending_plans", [])
+        for i, (k, pp) in enumerate(pend):
+            if k is keys:
+                del pend[: i + 1]  # older entries were never consumed: drop them
+                return pp
+        return self.emb.plan(keys, csr=True)
+
+    def _advance_next_plan(self):
+        """The step is issued: run the prefetched plans' collectives now, after this step's own
+        row exchanges and clocks (SparseTable.advance_plan): the older plans exchange their keys,
+        the newest one (planned by this very step) only its counts."""
+        pend = self.__dict__.get("_pending_plans") or []
+        for e in pend[:-1]:
+            e[1] = self.emb.advance_plan(e[1], finish=True)
+        if pend:
+            pend[-1][1] = self.emb.advance_plan(pend[-1][1], finish=False)
+
+
 def _batch_plan_tensors(batch, pp) -> list:
     """The device tensors one step hands to the next: the look-ahead batch and its pending key
     plan (deduplicated by storage: the flat key view aliases the batch keys)."""

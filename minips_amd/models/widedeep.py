@@ -25,6 +25,7 @@ import torch
 from .. import ops
 from ..ps.comm import Comm
 from .layers import SideStream
+from .feeder import LookaheadPlans
 from ..ps.tables import DenseTable, SparseTable
 
 
@@ -66,7 +67,7 @@ def _align(n, a=8):
     return (n + a - 1) // a * a
 
 
-class WideDeep:
+class WideDeep(LookaheadPlans):
     def __init__(self, cfg: WideDeepConfig, comm: Comm):
         self.cfg = cfg
         self.comm = comm
@@ -156,12 +157,6 @@ class WideDeep:
         w4 = self.view(P, "w4").float()
         return b["H3"].float() @ w4[:h] + w4[h] + b["wide"]
 
-    def prefetch(self, keys, keys_on_plan_stream: bool = False):
-        """Lookahead: start routing the NEXT batch's keys (dedupe + count all-to-all on the
-        planning stream) so it overlaps the current step; train_step picks the plan up."""
-        pend = self.__dict__.setdefault("_pending_plans", [])
-        pend.append([keys, self.emb.plan_async(keys, csr=True, keys_on_plan_stream=keys_on_plan_stream)])
-
     def train_step(self, dense, keys, labels, next_keys=None, next_on_plan_stream: bool = False) -> torch.Tensor:
         """One BSP superstep: Get, forward, backward, Add, Clock. Returns the summed loss
         (a device tensor; no host sync).
@@ -179,16 +174,7 @@ class WideDeep:
         F, D = cfg.F, cfg.emb_dim
         h = cfg.hidden[-1]
         b = self._buffers(B)
-        # plans issued ahead (prefetch); a batch may be several steps ahead (data-loader depth)
-        pend = self.__dict__.setdefault("_pending_plans", [])
-        plan = None
-        for i, (k, pp) in enumerate(pend):
-            if k is keys:
-                plan = pp
-                del pend[: i + 1]  # older entries were never consumed: drop them
-                break
-        if plan is None:
-            plan = self.emb.plan(keys, csr=True)
+        plan = self._take_plan(keys)  # issued ahead (LookaheadPlans.prefetch) or planned now
 
         def issue_next(point):
             # next_keys may be a callable that produces the next batch (on the planning stream)
@@ -242,15 +228,6 @@ class WideDeep:
             self.dense.clock()
         self._advance_next_plan()
         return b["loss"]
-
-    def _advance_next_plan(self):
-        """The step is issued: exchange the prefetched plans' keys now (planning stream), off
-        the next step's critical path (SparseTable.advance_plan). With several plans in flight
-        the newest one (issued by this very step) waits for the next step, so the host never
-        blocks on counts that were just launched."""
-        pend = self.__dict__.get("_pending_plans") or []
-        for e in (pend[:-1] if len(pend) > 1 else pend):
-            e[1] = self.emb.advance_plan(e[1])
 
     def drain(self):
         self.emb.drain()

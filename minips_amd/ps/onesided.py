@@ -242,7 +242,7 @@ class OneSidedSparseTable:
     def plan_async(self, keys: torch.Tensor, csr: bool = False, keys_on_plan_stream: bool = False):
         return self._plan(keys)
 
-    def advance_plan(self, pending):
+    def advance_plan(self, pending, finish: bool = True):
         return pending
 
     def add(self, plan: OneSidedPlan, grad_rows: torch.Tensor):

@@ -499,7 +499,7 @@ class SparsePlan:
 
 class _PendingPlan:
     """A plan whose dedupe + count exchange was issued on the planning stream (lookahead)."""
-    __slots__ = ("keys", "F", "flat", "uniq", "inv", "counts", "U_dev", "host", "event", "csr")
+    __slots__ = ("keys", "F", "flat", "uniq", "inv", "counts", "U_dev", "host", "event", "csr", "cev", "exchanged")
 
 
 class SparseTable:
@@ -589,10 +589,11 @@ class SparseTable:
             return None
         return plan.own_uniq[: plan.extra.get("own_U", len(plan.recv_keys))]
 
-    def _start_plan(self, keys: torch.Tensor, csr: bool = False) -> _PendingPlan:
-        """Dedupe + owner bucketing + all-to-all of the per-owner counts, issued on the current
-        stream; the counts land in pinned host memory behind an event. ``csr`` also groups the
-        lookups by unique row for the embedding backward (it depends on the keys only)."""
+    def _start_plan(self, keys: torch.Tensor, csr: bool = False, exchange: bool = True) -> _PendingPlan:
+        """Dedupe + owner bucketing (+ the all-to-all of the per-owner counts unless
+        ``exchange`` is False: _exchange_counts does it later), issued on the current stream;
+        the counts land in pinned host memory behind an event. ``csr`` also groups the lookups
+        by unique row for the embedding backward (it depends on the keys only)."""
         pp = _PendingPlan()
         pp.keys = keys
         pp.F = keys.shape[1] if keys.dim() == 2 else 1
@@ -614,19 +615,28 @@ class SparseTable:
             res, zeroed = res  # dedupe already counted each unique key's lookups into them
         pp.uniq, pp.inv, pp.counts, pp.U_dev = res
         pp.csr = ops.emb_build_csr(pp.inv, pp.F, n, zeroed=zeroed, counts_ready=fused) if want_csr else None
-        pp.host = pp.event = None
-        if self.comm.world > 1:
-            recv = torch.empty_like(pp.counts)
-            self.comm.all_to_all_counts(recv, pp.counts)
-            both = torch.stack([pp.counts, recv])
-            if both.is_cuda:
-                pp.host = torch.empty(both.shape, dtype=both.dtype, pin_memory=True)
-                pp.host.copy_(both, non_blocking=True)
-                pp.event = torch.cuda.Event()
-                pp.event.record()
-            else:
-                pp.host = both
+        pp.host = pp.event = pp.cev = None
+        pp.exchanged = self.comm.world == 1
+        if exchange:
+            self._exchange_counts(pp)
         return pp
+
+    def _exchange_counts(self, pp: _PendingPlan):
+        """All-to-all of the plan's per-owner counts on the current stream; the counts land in
+        pinned host memory behind ``pp.cev`` (the host reads them to size the key exchange)."""
+        if pp.exchanged:
+            return
+        pp.exchanged = True
+        recv = torch.empty_like(pp.counts)
+        self.comm.all_to_all_counts(recv, pp.counts)
+        both = torch.stack([pp.counts, recv])
+        if both.is_cuda:
+            pp.host = torch.empty(both.shape, dtype=both.dtype, pin_memory=True)
+            pp.host.copy_(both, non_blocking=True)
+            pp.cev = torch.cuda.Event()
+            pp.cev.record()
+        else:
+            pp.host = both
 
     def plan_async(self, keys: torch.Tensor, csr: bool = False, keys_on_plan_stream: bool = False):
         """Lookahead: start planning ``keys`` (a LATER batch) on the planning stream, so its
@@ -639,19 +649,18 @@ class SparseTable:
         if self._exact_counts:
             return self.plan(keys, csr)
         if self.comm.device.type != "cuda":
-            return self._start_plan(keys, csr)
+            return self._start_plan(keys, csr, exchange=False)
         ps = self.comm.plan_stream()
         cur = torch.cuda.current_stream(self.comm.device)
         if not keys_on_plan_stream:
             ps.wait_stream(cur)  # the keys are produced on the compute stream
         with torch.cuda.stream(ps):
-            pp = self._start_plan(keys, csr)
+            pp = self._start_plan(keys, csr, exchange=False)
+            pp.event = torch.cuda.Event()
+            pp.event.record(ps)
         keys.record_stream(ps)
         for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev, *(pp.csr or ())):
             t.record_stream(cur)  # produced on the planning stream, consumed on the compute stream
-        if pp.event is None:
-            pp.event = torch.cuda.Event()
-            pp.event.record(ps)
         return pp
 
     def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
@@ -660,14 +669,16 @@ class SparseTable:
         n = pp.flat.numel()
         if pp.event is not None:
             torch.cuda.current_stream(dev).wait_event(pp.event)
+        if not pp.exchanged:  # nobody issued the count exchange yet: do it here
+            self._exchange_counts(pp)
         if self.comm.world == 1:
             if self._exact_counts or dev.type != "cuda":
                 U = int(pp.U_dev.item())
                 return SparsePlan(n, pp.inv, pp.uniq, U, [U], [U], pp.uniq[:U], csr=pp.csr, _U=U)
             return SparsePlan(n, pp.inv, pp.uniq, n, None, None, pp.uniq, U_dev=pp.U_dev, csr=pp.csr)
-        if pp.event is not None:
+        if pp.cev is not None:
             with self.comm.waiting():
-                pp.event.synchronize()  # the only host wait of a step: the all-to-all splits
+                pp.cev.synchronize()  # the only host wait of a step: the all-to-all splits
         send, recv = pp.host[0].tolist(), pp.host[1].tolist()
         U, M = int(sum(send)), int(sum(recv))
         recv_keys = torch.empty(M, dtype=torch.int64, device=dev)
@@ -684,17 +695,25 @@ class SparseTable:
     def plan(self, keys: torch.Tensor, csr: bool = False) -> SparsePlan:
         return self._finish_plan(self._start_plan(keys, csr))
 
-    def advance_plan(self, pending):
-        """Second half of lookahead planning, called once the current step is issued: wait (host)
-        for the pending plan's counts, then issue the all-to-all of its keys and the owner-side
-        dedupe on the planning stream, so that only the row gather and the row exchange
-        remain on the critical path of the step that uses the plan."""
+    def advance_plan(self, pending, finish: bool = True):
+        """Later halves of lookahead planning, called once the current step is issued (so these
+        collectives follow the step's own row exchanges and clocks in the rank's single ordered
+        communicator, ps/comm.py): issue the count exchange of a pending plan if it is not done
+        yet; with ``finish``, then wait (host) for the counts and issue the all-to-all of its
+        keys and the owner-side dedupe on the planning stream, so that only the row gather and
+        the row exchange remain on the critical path of the step that uses the plan."""
         if not isinstance(pending, _PendingPlan) or self.comm.world == 1:
             return pending
         if self.comm.device.type != "cuda":
-            return self._finish_plan(pending)
+            self._exchange_counts(pending)
+            return self._finish_plan(pending) if finish else pending
         ps = self.comm.plan_stream()
         cur = torch.cuda.current_stream(self.comm.device)
+        if not pending.exchanged:
+            with torch.cuda.stream(ps):
+                self._exchange_counts(pending)
+        if not finish:
+            return pending
         with torch.cuda.stream(ps):
             plan = self._finish_plan(pending)
             ev = torch.cuda.Event()

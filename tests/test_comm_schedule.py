@@ -59,6 +59,16 @@ def test_collective_sequence_identical_across_ranks(world, fn):
     for r in range(1, world):
         assert out[r] == ref, (r, next(i for i, (a, b) in enumerate(zip(out[r], ref)) if a != b)
                                if len(out[r]) == len(ref) else (len(out[r]), len(ref)))
+    # look-ahead planning never sits in front of a step's own exchanges in the FIFO: within a
+    # step (up to its dense all-gather) every key-routing collective (int64) precedes the row
+    # exchanges, i.e. the planning of step n+1 / n+2 was issued at the end of step n
+    seg = []
+    for op, dt, size in ref:
+        seg.append(dt)
+        if op == "all_gather":
+            first = next(i for i, d in enumerate(seg) if d != "int64")
+            assert "int64" not in seg[first:], seg
+            seg = []
 
 
 def test_no_extra_communicators():
