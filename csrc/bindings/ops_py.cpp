@@ -400,6 +400,46 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
                                    (int)D, ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
 }
 
+// Embedding backward fused with the row-wise Adagrad apply (see kernels.h). members/memrow: the
+// plan's lookup CSR; uniq: the plan's unique keys (memrow indexes it); scr: zeroed scratch.
+void emb_seg_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, int64_t F, int64_t D,
+                     const at::Tensor& members, const at::Tensor& memrow, const at::Tensor& uniq, int64_t base,
+                     at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
+                     double lr, double eps, at::Tensor& scr) {
+  TORCH_CHECK(dX.is_cuda() && dX.dim() == 2 && dX.stride(1) == 1, "dX: row-major GPU matrix");
+  TORCH_CHECK(dX.scalar_type() == at::kFloat || dX.scalar_type() == at::kBFloat16, "dX must be fp32 or bf16");
+  const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
+  const int64_t B = dX.size(0);
+  TORCH_CHECK(D == 16 || D == 32 || D == 64, "D must be 16, 32 or 64");
+  TORCH_CHECK(dX.size(1) >= F * D && dX.stride(0) % 4 == 0, "dX shape / row stride");
+  for (auto* t : {&members, &memrow}) {
+    check_gpu(*t, "csr");
+    check_dtype(*t, at::kInt, "csr");
+    TORCH_CHECK(t->numel() == B * F, "members/memrow: int32 [B*F]");
+  }
+  check_gpu(uniq, "uniq");
+  check_dtype(uniq, at::kLong, "uniq");
+  check_gpu(table, "table");
+  check_dtype(table, at::kFloat, "table");
+  check_gpu(state, "state");
+  check_dtype(state, at::kFloat, "state");
+  check_gpu(scr, "scr");
+  check_dtype(scr, at::kFloat, "scr");
+  const int64_t W = table.size(1);
+  TORCH_CHECK(table.dim() == 2 && W % 4 == 0 && W >= D + (dw ? 1 : 0), "table: [rows, W], W % 4 == 0, W > D");
+  TORCH_CHECK(state.numel() == table.size(0), "state: one value per table row");
+  float* s2 = opt_ptr<float>(state2, at::kFloat, "state2");
+  TORCH_CHECK(D1 == W || (D1 == D && s2 && state2->numel() == table.size(0)), "split: D1 == W, or D1 == D with state2");
+  // memrow < U <= uniq.numel() <= scr rows; uniq holds this rank's routed keys (its shard = all rows)
+  TORCH_CHECK(uniq.numel() <= B * F && scr.dim() == 2 && scr.size(0) >= uniq.numel() && scr.size(1) >= D + 1 &&
+                  scr.size(1) % 4 == 0, "scr: [>= U, >= D+1] fp32, row stride % 4 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
+  minips_k::emb_seg_adagrad(dX.data_ptr(), dX.scalar_type() == at::kBFloat16, (int)dX.stride(0), dw, B, (int)F,
+                            (int)D, members.data_ptr<int>(), memrow.data_ptr<int>(), ptr<int64_t>(uniq), base,
+                            ptr<float>(table), (int)W, (int)W, ptr<float>(state), s2, (int)D1, (float)lr, (float)eps,
+                            ptr<float>(scr), (int)scr.size(1), stream_of(dX));
+}
+
 void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g, double lr, double beta1,
                 double beta2, double eps, double weight_decay, int64_t step, double grad_scale,
                 const c10::optional<at::Tensor>& w_bf16, const c10::optional<at::Tensor>& step_dev, bool zero_g) {
@@ -920,6 +960,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none());
+  m.def("emb_seg_adagrad", &emb_seg_adagrad);
   m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none(),
         py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),

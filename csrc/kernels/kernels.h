@@ -120,6 +120,13 @@ void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, in
                       const int64_t* U_dev = nullptr);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                           float* grad_rows, int row_stride, hipStream_t s);
+// Embedding backward fused with the row-wise Adagrad apply (one rank, local shard): the rows of
+// uniq[memrow] get Adagrad with the segment sums of their lookups' dX rows (+ dwide at column D)
+// without a grad_rows buffer. scr: [U, scr_ld >= D+1] fp32, all zero before and after the call.
+void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
+                     const int* members, const int* memrow, const int64_t* uniq, int64_t base, float* table, int ld,
+                     int W, float* state, float* state2, int D1, float lr, float eps, float* scr, int scr_ld,
+                     hipStream_t s);
 
 // ------------------------------------------------------------------ optimizers (optim.hip)
 // Fused Adam(W) on an fp32 master shard; optionally writes the bf16 copy for all-gather.

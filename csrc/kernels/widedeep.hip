@@ -696,6 +696,255 @@ static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, in
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------- fused backward + row-wise Adagrad
+// One rank (the PS shard is local): the segmented sum above feeds the row-wise Adagrad apply
+// directly instead of writing grad_rows [U, W] fp32 and reading it back in a second kernel
+// (sparse_rowwise_adagrad), and no zero-fill of grad_rows. Same piecewise traversal (a D/4-lane
+// group owns G consecutive row-sorted lookups); when a group reaches a row's first lookup it
+// also loads that row's table values and Adagrad state in the same batch as the gradient loads
+// (no dependent load at the flush). A row that lies entirely inside one group's range is
+// updated in place at its flush; a row cut by a group boundary (Zipf-hot rows, range edges)
+// is accumulated with fp32 atomics into a persistent zeroed scratch [U, scr_ld], and a second
+// kernel applies it -- one thread group per group boundary that is the row's FIRST cut -- and
+// clears the scratch row again. Semantics of ops.sparse_rowwise_adagrad with state2 for
+// columns [D1, W): sq1 = mean over [0, D1), sq2 = mean over [D1, W) (zero pad columns count).
+struct SegAdagradArgs {
+  const int64_t* uniq;  // [U] unique keys (table row = key - base)
+  int64_t base;
+  float* table;         // [rows, ld] fp32
+  int ld, W, D1;
+  float* state;         // [rows]
+  float* state2;        // [rows] or null (D1 == W)
+  float lr, eps;
+  float* scr;           // [U, scr_ld] fp32, zero outside a call
+  int scr_ld;
+};
+
+// sum over the L lanes of one row group (xor partners stay inside the group: all active)
+template <int L>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < L; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Row-wise Adagrad of one row held by the L lanes of a group: acc = emb gradient columns
+// [4l, 4l+4), accw = wide gradient at column D (lane 0). t/tw = the row's current values,
+// st1_old/st2_old its Adagrad state (on every lane of the group).
+template <int D>
+__device__ __forceinline__ void seg_adagrad_apply(const SegAdagradArgs& a, int64_t row, float4 acc, float accw,
+                                                  bool wide, float4 t, float tw, float st1_old, float st2_old, int l) {
+  constexpr int L = D / 4;
+  const float sq_e = group_sum<L>(acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w);
+  const float sq_w = group_sum<L>(l == 0 ? accw * accw : 0.f);
+  const bool split = a.D1 < a.W;  // D1 == D: the wide column (and the pad) has its own state
+  const float st1 = st1_old + (split ? sq_e : sq_e + sq_w) / (float)a.D1;
+  const float st2 = split ? st2_old + sq_w / (float)(a.W - a.D1) : 0.f;
+  const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
+  float* tr = a.table + row * (int64_t)a.ld;
+  *reinterpret_cast<float4*>(tr + 4 * l) =
+      make_float4(t.x - s1 * acc.x, t.y - s1 * acc.y, t.z - s1 * acc.z, t.w - s1 * acc.w);
+  if (l == 0) {
+    if (wide) tr[D] = tw - s2 * accw;
+    a.state[row] = st1;
+    if (split) a.state2[row] = st2;
+  }
+}
+
+template <typename TX, int D, int G, int NB>
+__global__ __launch_bounds__(256) void emb_seg_adagrad_kernel(const TX* __restrict__ dX, int ldx,
+                                                              const float* __restrict__ dwide, int F,
+                                                              const int* __restrict__ members,
+                                                              const int* __restrict__ memrow, int total,
+                                                              SegAdagradArgs a) {
+  constexpr int L = D / 4, PER = 64 / L;
+  const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
+  const bool wide = dwide != nullptr;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t piece = wave; piece * (PER * G) < total; piece += nw) {
+    const int ga = (int)(piece * (PER * G)) + sub * G;
+    const int gb = min(total, ga + G);
+    const int prev_row = (ga > 0 && ga <= total) ? memrow[ga - 1] : -1;
+    const int next_row = gb < total ? memrow[gb] : -1;
+    int cur = -1, last = prev_row;
+    bool cur_has = false;
+    int64_t cur_trow = 0;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), ct = acc;
+    float accw = 0.f, ctw = 0.f, cs1 = 0.f, cs2 = 0.f;
+    auto flush = [&]() {
+      if (cur != prev_row && cur != next_row) {  // whole row inside this group: apply now
+        if (cur_has) seg_adagrad_apply<D>(a, cur_trow, acc, accw, wide, ct, ctw, cs1, cs2, l);
+      } else {
+        float* out = a.scr + (int64_t)cur * a.scr_ld + 4 * l;
+        atomicAdd(out + 0, acc.x);
+        atomicAdd(out + 1, acc.y);
+        atomicAdd(out + 2, acc.z);
+        atomicAdd(out + 3, acc.w);
+        if (wide && l == 0) atomicAdd(a.scr + (int64_t)cur * a.scr_ld + D, accw);
+      }
+    };
+    for (int m0 = ga; m0 < gb; m0 += NB) {
+      int u[NB];
+      bool st[NB];
+      int64_t trow[NB];
+      float4 v[NB], t[NB];
+      float vw[NB], tw[NB], s1[NB], s2[NB];
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int m = m0 + q;
+        const bool ok = m < gb;
+        u[q] = ok ? memrow[m] : -1;
+        const int j = ok ? members[m] : 0;
+        const int bb = j / F, ff = j - bb * F;
+        v[q] = ok ? ld_grad4(dX + (int64_t)bb * ldx + ff * D + 4 * l) : make_float4(0.f, 0.f, 0.f, 0.f);
+        vw[q] = (wide && l == 0 && ok) ? dwide[bb] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {  // the first lookup of a row in this range: its table row too
+        st[q] = u[q] >= 0 && u[q] != (q == 0 ? last : u[q - 1]);
+        trow[q] = st[q] ? a.uniq[u[q]] - a.base : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        t[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        tw[q] = s1[q] = s2[q] = 0.f;
+        if (st[q]) {
+          const float* tr = a.table + trow[q] * (int64_t)a.ld;
+          t[q] = *reinterpret_cast<const float4*>(tr + 4 * l);
+          if (wide && l == 0) tw[q] = tr[D];
+          s1[q] = a.state[trow[q]];  // every lane: each scales its own columns
+          if (a.state2) s2[q] = a.state2[trow[q]];
+        }
+      }
+      last = u[NB - 1] >= 0 ? u[NB - 1] : last;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        if (u[q] < 0) break;
+        if (u[q] != cur) {
+          if (cur >= 0) flush();
+          cur = u[q];
+          cur_has = st[q];
+          cur_trow = trow[q];
+          ct = t[q];
+          ctw = tw[q];
+          cs1 = s1[q];
+          cs2 = s2[q];
+          acc = make_float4(0.f, 0.f, 0.f, 0.f);
+          accw = 0.f;
+        }
+        acc.x += v[q].x;
+        acc.y += v[q].y;
+        acc.z += v[q].z;
+        acc.w += v[q].w;
+        accw += vw[q];
+      }
+    }
+    // A Zipf-hot row spanning the whole wave: combine the groups' partials in registers first
+    // (one atomic per wave instead of one per group: same-address atomics serialise at the
+    // memory side). Such a row is cut by group boundaries, so the cut-row kernel applies it.
+    const int c0 = __shfl(cur, 0, 64);
+    if (__all(cur == c0) && c0 >= 0) {
+#pragma unroll
+      for (int o = L; o < 64; o <<= 1) {
+        acc.x += __shfl_xor(acc.x, o, 64);
+        acc.y += __shfl_xor(acc.y, o, 64);
+        acc.z += __shfl_xor(acc.z, o, 64);
+        acc.w += __shfl_xor(acc.w, o, 64);
+        accw += __shfl_xor(accw, o, 64);
+      }
+      if (sub == 0) {
+        float* out = a.scr + (int64_t)c0 * a.scr_ld + 4 * l;
+        atomicAdd(out + 0, acc.x);
+        atomicAdd(out + 1, acc.y);
+        atomicAdd(out + 2, acc.z);
+        atomicAdd(out + 3, acc.w);
+        if (wide && l == 0) atomicAdd(a.scr + (int64_t)c0 * a.scr_ld + D, accw);
+      }
+    } else if (cur >= 0) {
+      flush();
+    }
+  }
+}
+
+// Rows cut by a group boundary: boundary b = k*G handles the row iff the row continues across
+// b and b is its first cut (the previous boundary does not cut the same row).
+template <int D>
+__global__ __launch_bounds__(256) void emb_cut_adagrad_kernel(const int* __restrict__ memrow, int total, int G,
+                                                              bool wide, SegAdagradArgs a) {
+  constexpr int L = D / 4, PER = 64 / L;
+  const int lane = threadIdx.x & 63, l = lane % L;
+  const int64_t nb = (total - 1) / G;  // boundaries 1..nb
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t k = 1 + wave * PER + lane / L; k <= nb; k += nw * PER) {
+    const int b = (int)(k * G);
+    const int u = memrow[b];
+    if (memrow[b - 1] != u) continue;
+    if (b - G > 0 && memrow[b - G - 1] == u) continue;
+    float* sr = a.scr + (int64_t)u * a.scr_ld;
+    const float4 g = *reinterpret_cast<const float4*>(sr + 4 * l);
+    const float gw = (wide && l == 0) ? sr[D] : 0.f;
+    *reinterpret_cast<float4*>(sr + 4 * l) = make_float4(0.f, 0.f, 0.f, 0.f);  // scratch clean for the next call
+    if (wide && l == 0) sr[D] = 0.f;
+    const int64_t row = a.uniq[u] - a.base;
+    const float* tr = a.table + row * (int64_t)a.ld;
+    const float4 t = *reinterpret_cast<const float4*>(tr + 4 * l);
+    const float tw = (wide && l == 0) ? tr[D] : 0.f;
+    const float s1 = a.state[row];
+    const float s2 = a.state2 ? a.state2[row] : 0.f;
+    seg_adagrad_apply<D>(a, row, g, gw, wide, t, tw, s1, s2, l);
+  }
+}
+
+void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
+                     const int* members, const int* memrow, const int64_t* uniq, int64_t base, float* table, int ld,
+                     int W, float* state, float* state2, int D1, float lr, float eps, float* scr, int scr_ld,
+                     hipStream_t s) {
+  const int total = (int)(B * F);
+  if (total <= 0) return;
+  const SegAdagradArgs a{uniq, base, table, ld, W, D1, state, state2, lr, eps, scr, scr_ld};
+  static const int nb_cfg = [] {
+    const char* e = std::getenv("MINIPS_SEGADA_NB");
+    return e ? std::atoi(e) : 4;  // W&D step: NB 4 0.473, 8 0.487, 16 0.515 ms (unfused 0.465)
+  }();
+  constexpr int G = 16;
+  const int pieces = (total + (256 / D) * G - 1) / ((256 / D) * G);
+  const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
+  const int64_t nbound = (total - 1) / G;
+  const int cut_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((nbound * (D / 4) + 255) / 256, 65535));
+#define MINIPS_SEGADA(DD)                                                                                       \
+  if (bf16 && nb_cfg == 16)                                                                                     \
+    hipLaunchKernelGGL((emb_seg_adagrad_kernel<bf16_t, DD, G, 16>), blocks, 256, 0, s,                          \
+                       static_cast<const bf16_t*>(dX), ldx, dwide, F, members, memrow, total, a);              \
+  else if (bf16 && nb_cfg == 4)                                                                                 \
+    hipLaunchKernelGGL((emb_seg_adagrad_kernel<bf16_t, DD, G, 4>), blocks, 256, 0, s,                           \
+                       static_cast<const bf16_t*>(dX), ldx, dwide, F, members, memrow, total, a);              \
+  else if (bf16)                                                                                                \
+    hipLaunchKernelGGL((emb_seg_adagrad_kernel<bf16_t, DD, G, 8>), blocks, 256, 0, s,                           \
+                       static_cast<const bf16_t*>(dX), ldx, dwide, F, members, memrow, total, a);              \
+  else                                                                                                          \
+    hipLaunchKernelGGL((emb_seg_adagrad_kernel<float, DD, G, 8>), blocks, 256, 0, s,                           \
+                       static_cast<const float*>(dX), ldx, dwide, F, members, memrow, total, a);               \
+  if (nbound > 0)                                                                                               \
+    hipLaunchKernelGGL((emb_cut_adagrad_kernel<DD>), cut_blocks, 256, 0, s, memrow, total, G, dwide != nullptr, a);
+  switch (D) {
+    case 16:
+      MINIPS_SEGADA(16)
+      break;
+    case 32:
+      MINIPS_SEGADA(32)
+      break;
+    case 64:
+      MINIPS_SEGADA(64)
+      break;
+    default:
+      throw std::runtime_error("emb_seg_adagrad: D must be 16, 32 or 64");
+  }
+#undef MINIPS_SEGADA
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
                       const int64_t* U_dev) {

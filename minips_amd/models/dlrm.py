@@ -151,11 +151,7 @@ class DLRM(LookaheadPlans):
                 l.dgrad(P, dy, dx)
             dy = dx
         ops.dlrm_interact_bwd(b["V"], self.NV, D, b["dI"], b["dV"], b["dbot"], dense_idx=F)
-        dev = self.comm.device
-        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), D, dtype=torch.float32,
-                                                                         device=dev)
-        ops.wd_emb_backward(b["dV"], None, plan.inv, F, D, grad_rows, x_off=0, U_dev=plan.U_dev, csr=plan.csr)
-        self.emb.add(plan, grad_rows)
+        self.emb.add_lookup_grads(plan, b["dV"], None, F, D)
         self.emb.clock()
         dy = b["dbot"]
         for i in range(len(self.bottom) - 1, -1, -1):

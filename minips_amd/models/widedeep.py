@@ -216,11 +216,7 @@ class WideDeep(LookaheadPlans):
                 self.dense.add()
                 self.dense.clock()
         issue_next("dgrad")
-        dev = self.comm.device
-        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), cfg.row_width,
-                                                                         dtype=torch.float32, device=dev)
-        ops.wd_emb_backward(b["dX"], b["dwide"], plan.inv, F, D, grad_rows, U_dev=plan.U_dev, csr=plan.csr)
-        self.emb.add(plan, grad_rows)
+        self.emb.add_lookup_grads(plan, b["dX"], b["dwide"], F, D)  # per-lookup gradients; the table reduces
         self.emb.clock()
         side.join()
         if not dense_early:

@@ -354,6 +354,28 @@ def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=No
     return grad_rows
 
 
+def emb_seg_adagrad(dX, dwide, F, D, csr, uniq, U, base, table, state, state2, split, lr, eps, scratch):
+    """Embedding backward fused with the row-wise Adagrad apply of one rank's local shard: the
+    rows uniq[:U] get sparse_rowwise_adagrad with the gradient wd_emb_backward would produce
+    (segment sums of the lookups' dX rows, dwide at column D), without the grad_rows buffer.
+    ``csr`` = the plan's (members, memrow); ``scratch`` [>= len(uniq), W] fp32, zero before and
+    after (the GPU kernel accumulates rows cut by its piece boundaries there). ``U`` is used on
+    the CPU only (the GPU reads the rows off memrow)."""
+    W = table.shape[1]
+    D1 = W if split is None else split
+    if _gpu(dX):
+        kernels().emb_seg_adagrad(dX, dwide, int(F), int(D), csr[0], csr[1], uniq, int(base), table, state,
+                                  state2, int(D1), float(lr), float(eps), scratch)
+        return
+    B = dX.shape[0]
+    inv = torch.empty(B * F, dtype=torch.int64)
+    inv[csr[0].long()] = csr[1].long()
+    grad_rows = torch.zeros(max(U, 1), W, dtype=torch.float32)
+    wd_emb_backward(dX.float(), dwide, inv, F, D, grad_rows)
+    sparse_rowwise_adagrad(table, state, uniq[:U], base, grad_rows[:U], lr, eps, state2=state2,
+                           split=None if D1 == W else D1)
+
+
 # ----------------------------------------------------------------------------- optimizers
 def adam_apply(w, m, v, g, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=1, grad_scale=1.0,
                w_bf16=None, step_dev=None, zero_g=False):

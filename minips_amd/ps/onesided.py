@@ -249,6 +249,16 @@ class OneSidedSparseTable:
         assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == torch.float32
         self._pending.append((plan, grad_rows))
 
+    def add_lookup_grads(self, plan: OneSidedPlan, dX: torch.Tensor, dwide, F: int, D: int, x_off: int = 0):
+        """Per-lookup gradients (SparseTable.add_lookup_grads): segment-summed per unique row here,
+        then atomically added into the owners' rows at the clock."""
+        dev = self.comm.device
+        g = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width, dtype=torch.float32,
+                                                                 device=dev)
+        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, g, x_off=x_off, U_dev=getattr(plan, "U_dev", None),
+                            csr=getattr(plan, "csr", None))
+        self.add(plan, g)
+
     def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
         plan = self._plan(keys)
         g = torch.zeros(max(plan.cap, 1), self.width, dtype=torch.float32, device=self.comm.device)

@@ -497,6 +497,22 @@ class SparsePlan:
         return self._U
 
 
+# one rank + row-wise Adagrad: MINIPS_FUSED_EMB_ADAGRAD=1 feeds the embedding backward's segment
+# sums to the apply directly (ops.emb_seg_adagrad, no grad_rows buffer). Measured slower in the
+# Wide&Deep step on one MI355X (0.473-0.477 vs 0.465 ms/step: the fused kernel's key -> row ->
+# table load chain costs more than the 2 x U x 144 B it saves; tools/gpu_ab.sh), so off by default.
+_FUSED_EMB_ADAGRAD = os.environ.get("MINIPS_FUSED_EMB_ADAGRAD", "0") == "1"
+
+
+class _LookupGrads:
+    """A push in lookup form (SparseTable.add_lookup_grads): dX [B, >= F*D] holds one gradient
+    row per lookup (b, f) at columns f*D.., dwide [B] the sample's wide-column gradient."""
+    __slots__ = ("dX", "dwide", "F", "D")
+
+    def __init__(self, dX, dwide, F, D):
+        self.dX, self.dwide, self.F, self.D = dX, dwide, F, D
+
+
 class _PendingPlan:
     """A plan whose dedupe + count exchange was issued on the planning stream (lookahead)."""
     __slots__ = ("keys", "F", "flat", "uniq", "inv", "counts", "U_dev", "host", "event", "csr", "cev", "exchanged")
@@ -755,6 +771,35 @@ class SparseTable:
         assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == getattr(self, "value_dtype", torch.float32)
         self._pending.append((plan, grad_rows))
 
+    def add_lookup_grads(self, plan: SparsePlan, dX: torch.Tensor, dwide, F: int, D: int, x_off: int = 0):
+        """Push the gradient of every lookup of ``plan``'s batch: dX[b, x_off + f*D : +D] for
+        lookup (b, f) (+ dwide[b] into column D of the row). The table reduces them per unique
+        row -- the Add of the reference's worker, which sends one summed row per key. One rank
+        with row-wise Adagrad fuses that reduction into the apply (no gradient-row buffer,
+        ops.emb_seg_adagrad); otherwise the rows are segment-summed here and pushed by add()."""
+        if self._fused_lookup_ok(plan, dX, dwide, D, x_off):
+            self._pending.append((plan, _LookupGrads(dX[:, x_off:] if x_off else dX, dwide, F, D)))
+            return
+        dev = self.comm.device
+        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width,
+                                                                         dtype=torch.float32, device=dev)
+        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, grad_rows, x_off=x_off, U_dev=plan.U_dev, csr=plan.csr)
+        self.add(plan, grad_rows)
+
+    def _fused_lookup_ok(self, plan, dX, dwide, D, x_off) -> bool:
+        return (_FUSED_EMB_ADAGRAD and self.comm.world == 1 and dX.is_cuda and self.optimizer == "rowwise_adagrad"
+                and self.value_dtype == torch.float32 and type(self)._owner_rows is SparseTable._owner_rows
+                and plan.csr is not None and D in (16, 32, 64) and x_off % 4 == 0 and dX.stride(0) % 4 == 0
+                and self.width % 4 == 0 and self.width >= D + (dwide is not None)
+                and (self.split is None or self.split == D))
+
+    def _seg_scratch(self, n: int) -> torch.Tensor:
+        """Zeroed fp32 [>= n, width] accumulator of the fused apply (the kernel leaves it zero)."""
+        s = getattr(self, "_scr", None)
+        if s is None or s.shape[0] < n:
+            s = self._scr = torch.zeros(n, self.width, dtype=torch.float32, device=self.comm.device)
+        return s
+
     def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
         """Reference-style Add(keys, vals) (duplicates are summed)."""
         plan = self.plan(keys)
@@ -766,7 +811,8 @@ class SparseTable:
     def clock(self):
         pending, self._pending = self._pending, []
         for plan, g in pending:
-            self.pipe.keep_alive(g, plan.uniq, plan.recv_keys, plan.own_uniq, plan.own_inv, plan.U_dev,
+            held = (g.dX, g.dwide, *plan.csr) if isinstance(g, _LookupGrads) else (g,)
+            self.pipe.keep_alive(*held, plan.uniq, plan.recv_keys, plan.own_uniq, plan.own_inv, plan.U_dev,
                                  plan.own_U_dev)
 
         def work():
@@ -775,8 +821,14 @@ class SparseTable:
 
         self.pipe.run(work)
 
-    def _push(self, plan: SparsePlan, grad_rows: torch.Tensor):
+    def _push(self, plan: SparsePlan, grad_rows):
         dev = self.comm.device
+        if isinstance(grad_rows, _LookupGrads):  # one rank, fused reduction + apply
+            lg = grad_rows
+            ops.emb_seg_adagrad(lg.dX, lg.dwide, lg.F, lg.D, plan.csr, plan.uniq, plan.cap, self.base, self.shard,
+                                self.state, self.state2, self.split, self.lr, self.eps,
+                                self._seg_scratch(plan.uniq.numel()))
+            return
         if self.comm.world == 1:
             keys, g, n_dev, n = plan.uniq, grad_rows, plan.U_dev, plan.cap
         else:

@@ -389,3 +389,41 @@ def test_sparse_lr_fp64_matches_cpu(dev):
     assert res["cuda"].dtype == torch.float64
     assert torch.allclose(res["cuda"], res["cpu"], rtol=1e-12, atol=1e-14)
     assert res["cpu"].abs().sum() > 0
+
+
+@pytest.mark.parametrize("D,wide,split,dtype", [(32, True, True, torch.bfloat16), (32, True, False, torch.float32),
+                                                (16, False, False, torch.bfloat16), (64, True, True, torch.bfloat16)])
+def test_fused_emb_backward_adagrad(dev, D, wide, split, dtype):
+    """ops.emb_seg_adagrad (one-rank fused embedding backward + row-wise Adagrad) against the
+    fp32 reference of the two separate ops, over two steps (the scratch must come back zero):
+    Zipf-hot rows covering whole waves, rows cut by piece boundaries, single-lookup rows."""
+    g = torch.Generator().manual_seed(D + 3 * wide + 5 * split)
+    B, F, R = 4096, 5, 20000
+    W = D + 4
+    table = torch.randn(R, W, generator=g)
+    state = torch.rand(R, generator=g)
+    state2 = torch.rand(R, generator=g) if split else None
+    t_gpu, s_gpu = table.to(dev), state.to(dev)
+    s2_gpu = state2.to(dev) if split else None
+    t_ref, s_ref = table.clone(), state.clone()
+    s2_ref = state2.clone() if split else None
+    scr = torch.zeros(B * F, W, device=dev)
+    bounds = torch.tensor([0, R], device=dev)
+    for step in range(2):
+        keys = torch.randint(0, R, (B, F), generator=g)
+        keys.view(-1)[:6000] = 7 + step        # hot rows: thousands of lookups, cut by many boundaries
+        keys.view(-1)[6000:6040] = 11           # a row just over two pieces
+        uniq, inv, _, U_dev = ops.unique_bucketize_n(keys.to(dev), bounds, F)
+        U = int(U_dev.item())
+        csr = ops.emb_build_csr(inv, F, keys.numel())
+        dX = torch.randn(B, F * D + 8, generator=g).to(dtype)
+        dwide = torch.randn(B, generator=g) if wide else None
+        ops.emb_seg_adagrad(dX.to(dev), dwide.to(dev) if wide else None, F, D, csr, uniq, U, 0, t_gpu, s_gpu,
+                            s2_gpu, D if split else None, 0.05, 1e-8, scr)
+        ops.emb_seg_adagrad(dX.float(), dwide, F, D, (csr[0].cpu(), csr[1].cpu()), uniq.cpu(), U, 0, t_ref, s_ref,
+                            s2_ref, D if split else None, 0.05, 1e-8, None)
+        torch.testing.assert_close(t_gpu.cpu(), t_ref, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(s_gpu.cpu(), s_ref, rtol=1e-4, atol=1e-5)
+        if split:
+            torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-4, atol=1e-5)
+        assert int(scr.count_nonzero()) == 0
