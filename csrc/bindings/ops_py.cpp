@@ -293,7 +293,9 @@ void embedding_bag_bwd(const at::Tensor& grad_out, const at::Tensor& idx, const 
 }
 
 void wd_assemble(const at::Tensor& dense, const at::Tensor& rows, const at::Tensor& inv, int64_t F, int64_t D,
-                 at::Tensor& X, at::Tensor& wide_logit, int64_t ones_col) {
+                 at::Tensor& X, at::Tensor& wide_logit, int64_t ones_col, const c10::optional<at::Tensor>& zero) {
+  float* z = opt_ptr<float>(zero, at::kFloat, "zero");
+  if (z) TORCH_CHECK(zero->numel() >= 1, "zero: at least one element");
   check_gpu(dense, "dense");
   check_gpu(rows, "rows");
   check_gpu(inv, "inv");
@@ -309,7 +311,7 @@ void wd_assemble(const at::Tensor& dense, const at::Tensor& rows, const at::Tens
   c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
   minips_k::wd_assemble(ptr<float>(dense), (int)dense.size(1), ptr<bf16_t>(rows), (int)rows.size(1),
                         ptr<int64_t>(inv), B, (int)F, (int)D, ptr<bf16_t>(X), (int)X.size(1), ptr<float>(wide_logit),
-                        (int)ones_col, stream_of(X));
+                        (int)ones_col, stream_of(X), z);
 }
 
 void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& wide_logit,
@@ -955,7 +957,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"),
-        py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1);
+        py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1, py::arg("zero") = py::none());
   m.def("wd_head", &wd_head);
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),

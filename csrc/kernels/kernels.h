@@ -88,8 +88,11 @@ void embedding_bag_bwd(const float* grad_out, const int64_t* idx, const int64_t*
 // (bf16 [U, row_stride]), columns [F*D, F*D+n_dense) the dense features (fp32 [B, n_dense]).
 // wide_logit[b] = sum_f rows[inv[b*F+f], D] (the wide weight lives in column D of a row).
 // Column ones_col (>= 0) is set to 1.0: the bias input of a bias-folded first layer.
+// zero_out (nullable): one float the kernel sets to 0 (the step's loss accumulator, so the step
+// needs no separate fill kernel before the head's atomics)
 void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B,
-                 int F, int D, bf16_t* X, int ldx, float* wide_logit, int ones_col, hipStream_t s);
+                 int F, int D, bf16_t* X, int ldx, float* wide_logit, int ones_col, hipStream_t s,
+                 float* zero_out = nullptr);
 // Head (last Linear Hd->1 + BCE-with-logits, fwd and bwd fused):
 //   z = H[b,:].w + b0 + wide[b]; dz = (sigmoid(z) - y) * grad_scale
 //   dH = dz * w * (H > 0) (bf16), dw += dz*H, db += dz, dH_colsum += dH, dwide[b] = dz,

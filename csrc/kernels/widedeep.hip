@@ -15,7 +15,9 @@ namespace minips_k {
 // chunks compute the per-sample wide sums (one thread per sample) so no thread serialises.
 __global__ void wd_assemble_kernel(const float* __restrict__ dense, int n_dense, const bf16_t* __restrict__ rows,
                                    int row_stride, const int64_t* __restrict__ inv, int64_t B, int F, int D,
-                                   bf16_t* __restrict__ X, int ldx, float* __restrict__ wide_logit, int ones_col) {
+                                   bf16_t* __restrict__ X, int ldx, float* __restrict__ wide_logit, int ones_col,
+                                   float* __restrict__ zero_out) {
+  if (zero_out && blockIdx.x == 0 && threadIdx.x == 0) *zero_out = 0.f;
   const int chunks = ldx >> 3;
   const int emb_cols = F * D;
   const int64_t total = B * chunks;
@@ -71,7 +73,7 @@ __global__ void wd_assemble_kernel(const float* __restrict__ dense, int n_dense,
 }
 
 void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B,
-                 int F, int D, bf16_t* X, int ldx, float* wide_logit, int ones_col, hipStream_t s) {
+                 int F, int D, bf16_t* X, int ldx, float* wide_logit, int ones_col, hipStream_t s, float* zero_out) {
   if (ldx % 8) throw std::runtime_error("wd_assemble: ldx must be a multiple of 8");
   if (F * D + n_dense > ldx) throw std::runtime_error("wd_assemble: ldx too small");
   if (ones_col >= ldx) throw std::runtime_error("wd_assemble: ones_col out of range");
@@ -83,7 +85,7 @@ void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_st
   // shuffles need all 32 lanes of a sample): size the grid so the loop runs exactly once
   const int64_t items = ((B * (ldx / 8) + 63) & ~63ll) + 32 * B;
   hipLaunchKernelGGL(wd_assemble_kernel, (int)((items + block - 1) / block), block, 0, s, dense, n_dense, rows,
-                     row_stride, inv, B, F, D, X, ldx, wide_logit, ones_col);
+                     row_stride, inv, B, F, D, X, ldx, wide_logit, ones_col, zero_out);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

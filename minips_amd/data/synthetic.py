@@ -47,12 +47,19 @@ class CriteoSynth:
             from .._native import kernels
 
             self._init_gpu()
-            self._step_dev.add_(1)
+            self._host_step += 1
             dense = torch.empty(B, self.n_dense, device=self.device)
             keys = torch.empty(B, F, dtype=torch.int64, device=self.device)
             labels = torch.empty(B, device=self.device)
-            kernels().criteo_synth(self._seed, 0, self._step_dev, self.card_t, self.offsets, self.w_dense, dense,
-                                   keys, labels)
+            if torch.cuda.is_current_stream_capturing():
+                # a captured step draws a fresh batch on every replay: the counter advances on the
+                # device (graph_prepare set it from the host count before the capture)
+                self._step_dev.add_(1)
+                kernels().criteo_synth(self._seed, 0, self._step_dev, self.card_t, self.offsets, self.w_dense,
+                                       dense, keys, labels)
+            else:
+                kernels().criteo_synth(self._seed, self._host_step, None, self.card_t, self.offsets, self.w_dense,
+                                       dense, keys, labels)
             return dense, keys, labels
         u = torch.rand(B, F, generator=self.gen, device=self.device, dtype=torch.float64)
         raw = torch.floor(torch.exp(u * self.log_card) - 1.0).to(torch.int64)
@@ -68,15 +75,25 @@ class CriteoSynth:
     def _init_gpu(self):
         if not hasattr(self, "_seed"):
             self._seed = int(torch.randint(0, 2**62, (1,), generator=self.gen, device=self.device).item())
-            # the step counter lives on the device: a step captured in a HIP graph draws a fresh
-            # batch on every replay
+            self._host_step = 0
+            # device twin of the step counter, used inside HIP-graph captures only
             self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+    def graph_prepare(self):
+        """Before capturing a step that draws batches: the device counter = the host count."""
+        if self.device.type == "cuda":
+            self._init_gpu()
+            self._step_dev.fill_(self._host_step)
+
+    def graph_replayed(self, n: int = 1):
+        """A captured step was replayed ``n`` times: the host count follows the device's."""
+        self._host_step += n
 
     def skip(self, n: int):
         """Advance past ``n`` batches (resume from a checkpoint at the same data position)."""
         if self.device.type == "cuda":
             self._init_gpu()
-            self._step_dev.add_(n)
+            self._host_step += n
         else:
             for _ in range(n):
                 self.next()

@@ -140,6 +140,14 @@ class GraphedFeeder:
         f.queue[0] = (batch, None)
         static = _batch_plan_tensors(batch, pp)
         saved = [(getattr(t, "step", None), t.pipe.clock) for t in self.tables]
+        # device twins of the host counters (Adam step, data draw): eager steps leave them alone,
+        # the captured step advances them on the device
+        for t in self.tables:
+            if hasattr(t, "sync_step_dev"):
+                t.sync_step_dev()
+        if hasattr(f.data, "graph_prepare"):
+            f.data.graph_prepare()
+        saved_draws = getattr(f.data, "_host_step", None)
         self.graph = torch.cuda.CUDAGraph()
         main, ps = f.main, f.plan_stream
         with torch.cuda.graph(self.graph, stream=main):
@@ -161,6 +169,8 @@ class GraphedFeeder:
             if st is not None:
                 t.step = st
             t.pipe.clock = ck
+        if saved_draws is not None:
+            f.data._host_step = saved_draws
 
     def step(self):
         self.graph.replay()
@@ -168,4 +178,6 @@ class GraphedFeeder:
             if hasattr(t, "step"):
                 t.step += 1
             t.pipe.clock += 1
+        if hasattr(self.f.data, "graph_replayed"):
+            self.f.data.graph_replayed(1)
         return self.loss

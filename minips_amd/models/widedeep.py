@@ -186,10 +186,9 @@ class WideDeep(LookaheadPlans):
         issue_next("start")
         rows, plan = self.emb.get(keys, plan=plan)
         G = self.dense.grad
-        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0])
+        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
         P = self.dense.get()
         self._forward(b, P)
-        b["loss"].zero_()
         scale = 1.0 / (B * self.comm.world)
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1], b["dwide"],

@@ -290,12 +290,15 @@ def embedding_bag_bwd(grad_out, idx, offsets, grad_rows, mean=False):
 
 
 # ----------------------------------------------------------------------------- Wide&Deep
-def wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col=-1):
+def wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col=-1, zero=None):
     """X = [emb_0..emb_{F-1} | dense | 1 at ones_col | 0-pad] (bf16);
-    wide_logit[b] = sum_f rows[inv, D]."""
+    wide_logit[b] = sum_f rows[inv, D]. ``zero`` (fp32 [1], optional) is set to 0 on the way
+    (the step's loss accumulator: no separate fill kernel)."""
     if _gpu(X):
-        kernels().wd_assemble(dense, rows, inv, int(F), int(D), X, wide_logit, int(ones_col))
+        kernels().wd_assemble(dense, rows, inv, int(F), int(D), X, wide_logit, int(ones_col), zero)
         return X, wide_logit
+    if zero is not None:
+        zero.zero_()
     B = X.shape[0]
     r = rows[inv].view(B, F, rows.shape[1]).float()
     X.zero_()

@@ -221,19 +221,33 @@ class DenseTable:
         g0 = lo + self.comm.rank * sz
         return off, sz, g0
 
+    def _step_dev_for_clock(self, first: bool = True):
+        """The Adam step's device twin ``step_dev`` advances only inside a HIP-graph capture (a
+        replayed step must read a fresh step on the device; GraphedStep / GraphedFeeder set it
+        from the host step before capturing). Eager clocks pass the host step: no extra kernel
+        on the clock's stream. Returns the step_dev argument for adam_apply."""
+        if not (self.master.is_cuda and torch.cuda.is_current_stream_capturing()):
+            return None
+        if first:
+            self.step_dev.add_(1)
+        return self.step_dev
+
+    def sync_step_dev(self):
+        """Before a HIP-graph capture: the device step twin = the host step."""
+        self.step_dev.fill_(int(self.step))
+
     def _bucket_work(self, k: int, grad: torch.Tensor, step: int):
         lo, hi = self.buckets[k]
         off, sz, g0 = self._own_piece(k)
         comm = self.comm
-        if not self._issued:  # first bucket of this clock: the device Adam step advances once
-            self.step_dev.add_(1)
+        sd = self._step_dev_for_clock(first=not self._issued)
         self._issued.add(k)
         comm.reduce_scatter(self.grad_shard[off: off + sz], grad[lo:hi])
         sl = slice(off, off + sz)
         out = self.params[g0: g0 + sz] if self.pull_dtype == torch.bfloat16 else None
         if self.optimizer == "adam":
             ops.adam_apply(self.master[sl], self.m[sl], self.v[sl], self.grad_shard[sl], self.lr, self.betas[0],
-                           self.betas[1], self.eps, self.weight_decay, step, 1.0, out, step_dev=self.step_dev)
+                           self.betas[1], self.eps, self.weight_decay, step, 1.0, out, step_dev=sd)
         elif self.optimizer == "adagrad":
             ops.adagrad_apply(self.master[sl], self.m[sl], self.grad_shard[sl], self.lr, self.eps, 1.0, out)
         elif self.optimizer == "sgd":
@@ -335,7 +349,7 @@ class DenseTable:
                         if k not in self._issued:
                             self._bucket_work(k, grad, step)
                 else:
-                    self.step_dev.add_(1)
+                    self._step_dev_for_clock()
                 self._issued = set()
 
             self.pipe.run(work)
@@ -345,14 +359,14 @@ class DenseTable:
             return
 
         def work():
-            self.step_dev.add_(1)  # device twin of self.step (one per clock)
+            sd = self._step_dev_for_clock()
             if pending:
                 if comm.world == 1:  # the whole gradient is the owned shard
                     # Adam clears it in the same pass (one fewer full-size kernel per clock)
-                    cleared = self._apply(grad, step, zero_g=grad.numel() == self.shard)
+                    cleared = self._apply(grad, step, zero_g=grad.numel() == self.shard, step_dev=sd)
                 else:
                     comm.reduce_scatter(self.grad_shard, grad)
-                    self._apply(self.grad_shard, step)
+                    self._apply(self.grad_shard, step, step_dev=sd)
                     cleared = False
                 comm.all_gather(self.params, self.params[self.base: self.base + self.shard])
             else:
@@ -366,12 +380,12 @@ class DenseTable:
             self.grad = self._ring[step % len(self._ring)]
             self.pipe.wait_clock(step - len(self._ring))
 
-    def _apply(self, g: torch.Tensor, step: int, zero_g: bool = False) -> bool:
+    def _apply(self, g: torch.Tensor, step: int, zero_g: bool = False, step_dev=None) -> bool:
         """Apply the optimizer to the owned shard; True if ``g`` was cleared on the way."""
         out = self.params[self.base: self.base + self.shard] if self.pull_dtype == torch.bfloat16 else None
         if self.optimizer == "adam":
             ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
-                           self.weight_decay, step, 1.0, out, step_dev=self.step_dev, zero_g=zero_g)
+                           self.weight_decay, step, 1.0, out, step_dev=step_dev, zero_g=zero_g)
             if out is None:
                 self.params[self.base: self.base + self.shard].copy_(self.master)
             return zero_g

@@ -4,8 +4,9 @@ A step of a small model issues ~20 kernels of a few microseconds each, so the ho
 launch) is the bottleneck, not the GPU. ``GraphedStep`` captures one step into a HIP graph (via
 ``torch.cuda.CUDAGraph``, HIP graphs on ROCm) and replays it: one launch per step. Requirements,
 met by the dense models on one rank: static shapes, inputs copied into fixed buffers, no host
-syncs inside, and optimizer state that advances on the device (DenseTable keeps the Adam step in
-``step_dev``). Host-side bookkeeping that Python would have done per step (``DenseTable.step``,
+syncs inside, and optimizer state that advances on the device (DenseTable keeps a device twin of
+the Adam step, ``step_dev``, which a captured clock advances; it is set from the host step here).
+Host-side bookkeeping that Python would have done per step (``DenseTable.step``,
 the clock counter) is advanced by ``replay`` so checkpoints stay consistent.
 """
 from __future__ import annotations
@@ -35,6 +36,9 @@ class GraphedStep:
         # capture records the step without running it: the host counters the Python step
         # advanced during capture are rolled back, so only the ``warmup`` steps count
         saved = [(t.step, t.pipe.clock) for t in self.tables]
+        for t in self.tables:  # the captured clock advances the Adam step on the device
+            if hasattr(t, "sync_step_dev"):
+                t.sync_step_dev()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = fn(*self.static)
