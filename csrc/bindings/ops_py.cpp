@@ -402,6 +402,18 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
                                    (int)D, ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
 }
 
+void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x: row-major GPU matrix");
+  check_dtype(x, at::kBFloat16, "x");
+  check_gpu(out, "out");
+  check_dtype(out, at::kFloat, "out");
+  TORCH_CHECK(out.numel() >= x.size(1) && x.size(1) % 8 == 0 && x.stride(0) % 8 == 0,
+              "colsum: out >= N floats, N and the row stride multiples of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "colsum: x must be 16-byte aligned");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  minips_k::colsum_bf16(ptr<bf16_t>(x), x.size(0), (int)x.size(1), (int)x.stride(0), ptr<float>(out), stream_of(x));
+}
+
 // Embedding backward fused with the row-wise Adagrad apply (see kernels.h). members/memrow: the
 // plan's lookup CSR; uniq: the plan's unique keys (memrow indexes it); scr: zeroed scratch.
 void emb_seg_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, int64_t F, int64_t D,
@@ -963,6 +975,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none());
   m.def("emb_seg_adagrad", &emb_seg_adagrad);
+  m.def("colsum_bf16", &colsum_bf16);
   m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none(),
         py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),

@@ -221,6 +221,24 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
   const bool c_vec = ((ep.ldc & (F32OUT ? 3 : 7)) == 0) && ((reinterpret_cast<uintptr_t>(ep.C) & 15) == 0);
   const bool m_vec = ((ep.ldmask & 7) == 0) && ((reinterpret_cast<uintptr_t>(ep.mask) & 15) == 0);
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // the bias depends on the column only: this lane's 8 columns are loaded once (one 16-byte
+  // load when aligned), not per 16-row slice
+  float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (HAS_BIAS && ep.bias) {
+    const int col = nb + (lane & 7) * 8;
+    if (col + 8 <= N && (reinterpret_cast<uintptr_t>(ep.bias + col) & 15) == 0) {
+      const uint4 bu = *reinterpret_cast<const uint4*>(ep.bias + col);
+      const uint32_t w[4] = {bu.x, bu.y, bu.z, bu.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bias[2 * e] = __uint_as_float(w[e] << 16);
+        bias[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bias[e] = (col + e < N) ? bf2f(ep.bias[col + e]) : 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MR; ++i) {
 #pragma unroll
@@ -263,11 +281,6 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
         const float4 hi = *reinterpret_cast<const float4*>(scr + rr * kScrPitch + c8 + 4);
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         const bool full = col + 8 <= N;
-        float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (HAS_BIAS && ep.bias) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bias[e] = (col + e < N) ? bf2f(ep.bias[col + e]) : 0.f;
-        }
         float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         const int64_t moff = (int64_t)row * ep.ldmask + col;
         if (READ_MASK && row_ok) {

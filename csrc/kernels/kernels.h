@@ -123,6 +123,8 @@ void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, in
                       const int64_t* U_dev = nullptr);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                           float* grad_rows, int row_stride, hipStream_t s);
+// out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
+void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s);
 // Embedding backward fused with the row-wise Adagrad apply (one rank, local shard): the rows of
 // uniq[memrow] get Adagrad with the segment sums of their lookups' dX rows (+ dwide at column D)
 // without a grad_rows buffer. scr: [U, scr_ld >= D+1] fp32, all zero before and after the call.

@@ -232,7 +232,12 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
              float grad_scale, hipStream_t s) {
   if (B <= 0) return;
   const int block = 64 * kHeadWaves;
-  const int grid = (int)std::min<int64_t>(128, (B + 63) / 64);  // per-block LDS reduction, then atomics
+  // per-block LDS reduction, then atomics; one block per CU (128 blocks left half the chip idle)
+  static const int max_blocks = [] {
+    const char* e = std::getenv("MINIPS_HEAD_BLOCKS");
+    return e ? std::atoi(e) : 256;
+  }();
+  const int grid = (int)std::min<int64_t>(max_blocks, (B + 63) / 64);
   switch (Hd) {
     case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
                                     dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
@@ -244,6 +249,54 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
                                     dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
     default: throw std::runtime_error("wd_head: Hd must be 64, 128, 256 or 512, got " + std::to_string(Hd));
   }
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+// out[c] += sum_r x[r, c] (x bf16 [M, N] row-major, ld; N % 8 == 0): the bias gradient of a
+// Linear from its output gradient. A block owns a 64-column strip and a chunk of rows; each
+// thread sums 8 columns (one 16-byte load per row) over every 32nd row of the chunk, the
+// block folds its 32 row-lanes in LDS and issues one atomic per column. Chunks are sized for
+// ~2 blocks per CU, so a column takes only M / rows_per_block same-address atomics (fp32
+// atomics from every XCD meet at the memory side: a per-wave atomic in a GEMM epilogue --
+// 256 per column -- cost the W&D dgrad 44 us).
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restrict__ x, int64_t M, int N, int ld,
+                                                          int rows_per_block, float* __restrict__ out) {
+  __shared__ float red[32][65];
+  const int t = threadIdx.x, c8 = (t & 7) * 8, rl = t >> 3;
+  const int col0 = blockIdx.x * 64 + c8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col0 < N) {
+    for (int64_t r = r0 + rl; r < r1; r += 32) {
+      const uint4 u = *reinterpret_cast<const uint4*>(x + r * ld + col0);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[2 * q] += __uint_as_float(w[q] << 16);
+        acc[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][c8 + e] = acc[e];
+  __syncthreads();
+  if (t < 64) {
+    float v = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) v += red[i][t];
+    const int col = blockIdx.x * 64 + t;
+    if (col < N) atomicAdd(out + col, v);
+  }
+}
+
+void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s) {
+  if (M <= 0 || N <= 0) return;
+  if (N % 8 || ld % 8) throw std::runtime_error("colsum_bf16: N and ld must be multiples of 8");
+  const int strips = (N + 63) / 64;
+  const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(512 / strips, (M + 255) / 256));
+  const int rpb = (int)((M + chunks - 1) / chunks);
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(strips, (unsigned)chunks), 256, 0, s, x, M, N, ld, rpb, out);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -63,6 +63,16 @@ _PLAN_AT = os.environ.get("MINIPS_PLAN_AT", "start")
 _DENSE_CLOCK_ON_SIDE = os.environ.get("MINIPS_DENSE_CLOCK_ON_SIDE", "0") == "1"
 
 
+# Dense-layout knobs (see WideDeep.__init__): layer-1 K padding, and bias handling of layers 2/3:
+# "ext" (folded, K = 1032 / 520) or "vec" (bias vectors, K = 1024 / 512, colsum bias gradients).
+# In the whole W&D step on one MI355X (tools/gpu_ab.sh, ms/step): ext/8 0.453, ext/64 0.451,
+# vec/8 0.460, vec/64 0.457 -- the isolated GEMM gains of "vec" (fwd2 -7 us, W2 wgrad -10 us)
+# do not survive the 3-stream overlap (its W2 weight gradient switches to 512 128x128 blocks,
+# which crowd the dgrad chain), so "ext" with a 64-aligned layer-1 K is the default.
+_K1_ALIGN = int(os.environ.get("MINIPS_WD_K1_ALIGN", "64"))
+_BIAS_VEC = os.environ.get("MINIPS_WD_BIAS", "ext") == "vec"
+
+
 def _align(n, a=8):
     return (n + a - 1) // a * a
 
@@ -79,17 +89,24 @@ class WideDeep(LookaheadPlans):
                                init_std=0.01, seed=cfg.seed)
         # wide weights start at zero (columns >= D)
         self.emb.shard[:, D:].zero_()
-        # Dense layout: each Linear is stored as W_ext [n_out, k_pad] with the bias in column
-        # k_in (k_pad = align8(k_in + 1)); activations carry a constant-1 column at k_in. The
-        # forward GEMM then adds the bias for free and the weight-gradient GEMM produces the
-        # bias gradient in that column -- no bias epilogue, no column-sum atomics.
+        # Dense layout: each Linear is stored as W_ext [n_out, k_pad] with the bias in column k_in;
+        # activations carry a constant-1 column at k_in, so the forward GEMM adds the bias and the
+        # weight-gradient GEMM yields its gradient (no bias epilogue, no column-sum atomics).
+        # Layer 1's k_pad is a multiple of 64: whole 64-deep K-steps and 128-byte rows for the
+        # LDS-DMA (K = 896: the 16384x1024 forward takes 30.7 us vs 38.8 us at align8's 848;
+        # tools/bench_gemm.py). MINIPS_WD_BIAS=vec gives layers 2/3 bias vectors instead (see
+        # _BIAS_VEC): dH3's column sums from wd_head, dH2's from a column-sum kernel.
         self.k_in = [cfg.F * cfg.emb_dim + cfg.n_dense, *cfg.hidden[:-1]]
-        self.k_pad = [_align(k + 1) for k in self.k_in]
+        self.k_pad = [_align(self.k_in[0] + 1, _K1_ALIGN),
+                      *(self.k_in[1:] if _BIAS_VEC else [_align(k + 1) for k in self.k_in[1:]])]
         self.layout = {}
         off = 0
         for i, n_out in enumerate(cfg.hidden):
             self.layout[f"W{i + 1}"] = (off, (n_out, self.k_pad[i]))
-            off += _align(n_out * self.k_pad[i])
+            off += _align(n_out * self.k_pad[i], 64)
+            if i > 0 and _BIAS_VEC:
+                self.layout[f"b{i + 1}"] = (off, (n_out,))
+                off += _align(n_out, 64)
         self.layout["w4"] = (off, (cfg.hidden[-1] + 8,))  # [w4 | b4 | pad]
         off += cfg.hidden[-1] + 8
         self.n_params = off
@@ -124,13 +141,18 @@ class WideDeep(LookaheadPlans):
             bf = dict(dtype=torch.bfloat16, device=dev)
             h1, h2, h3 = cfg.hidden
 
-            def ext(n, k_in):  # activation with the constant-1 column at k_in, zero padding
-                t = torch.zeros(B, _align(k_in + 1), **bf)
-                t[:, k_in] = 1.0
+            X = torch.zeros(B, self.k_pad[0], **bf)  # constant-1 column at k_in (layer-1 bias), zero pad
+            X[:, self.k_in[0]] = 1.0
+
+            def act(n):  # bias folded (MINIPS_WD_BIAS=ext): constant-1 column at n, zero padding
+                if _BIAS_VEC:
+                    return torch.empty(B, n, **bf)
+                t = torch.zeros(B, _align(n + 1), **bf)
+                t[:, n] = 1.0
                 return t
 
             self._bufs[B] = dict(
-                X=ext(self.k_in[0], self.k_in[0]), H1=ext(h1, h1), H2=ext(h2, h2),
+                X=X, H1=act(h1), H2=act(h2),
                 H3=torch.empty(B, h3, **bf), dH3=torch.empty(B, h3, **bf), dH2=torch.empty(B, h2, **bf),
                 dH1=torch.empty(B, h1, **bf),
                 dX=torch.empty(B, cfg.F * cfg.emb_dim, **bf),  # bf16: half the bytes of the emb backward
@@ -142,8 +164,8 @@ class WideDeep(LookaheadPlans):
 
     def _forward(self, b, P):
         ops.linear_fwd(b["X"], self.view(P, "W1"), None, "relu", out=b["H1"])
-        ops.linear_fwd(b["H1"], self.view(P, "W2"), None, "relu", out=b["H2"])
-        ops.linear_fwd(b["H2"], self.view(P, "W3"), None, "relu", out=b["H3"])
+        ops.linear_fwd(b["H1"], self.view(P, "W2"), self.view(P, "b2") if _BIAS_VEC else None, "relu", out=b["H2"])
+        ops.linear_fwd(b["H2"], self.view(P, "W3"), self.view(P, "b3") if _BIAS_VEC else None, "relu", out=b["H3"])
 
     def forward(self, dense, keys, rows, plan):
         """Forward only (eval): returns logits [B] fp32."""
@@ -191,8 +213,9 @@ class WideDeep(LookaheadPlans):
         self._forward(b, P)
         scale = 1.0 / (B * self.comm.world)
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
+        # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1], b["dwide"],
-                    b["loss"], None, scale)
+                    b["loss"], self.view(G, "b3") if _BIAS_VEC else None, scale)
         issue_next("head")
         side = self._side
         # weight gradients fork onto a second stream as soon as their inputs exist, beside the
@@ -201,6 +224,8 @@ class WideDeep(LookaheadPlans):
             ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=self.k_in[2], out=b["dH2"])
         with side.fork():
+            if _BIAS_VEC:
+                ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
             ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         with side.fork():

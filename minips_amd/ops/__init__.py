@@ -107,6 +107,15 @@ def linear_fwd(x, w, bias=None, act="relu", out=None):
     return gemm(x, w, out, M, N, K, False, False, epi, bias=bias)
 
 
+def colsum_add(x, out):
+    """out[:N] += x.sum(0) in fp32 (x bf16 [M, N]): a Linear's bias gradient from its dy."""
+    if _gpu(x):
+        kernels().colsum_bf16(x, out)
+        return out
+    out[: x.shape[1]] += x.float().sum(0)
+    return out
+
+
 def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=None):
     """dx = dy w (dy [M,N], w [N,K]) -> bf16 masked by (mask > 0) (+colsum), or fp32."""
     M, N = dy.shape

@@ -427,3 +427,14 @@ def test_fused_emb_backward_adagrad(dev, D, wide, split, dtype):
         if split:
             torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-4, atol=1e-5)
         assert int(scr.count_nonzero()) == 0
+
+
+def test_colsum_bf16(dev):
+    """ops.colsum_add (bias gradient of a Linear) against the fp32 column sums."""
+    g = torch.Generator().manual_seed(11)
+    for M, N in ((16384, 512), (1000, 72), (3, 8)):
+        x = torch.randn(M, N, generator=g).to(torch.bfloat16)
+        out = torch.full((N,), 0.5)
+        ref = out + x.float().sum(0)
+        got = ops.colsum_add(x.to(dev), out.to(dev))
+        torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-3)

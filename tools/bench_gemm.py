@@ -20,9 +20,21 @@ SHAPES = [  # (name, M, N, K, layout)
 ]
 
 
+def _shapes():
+    """SHAPES, or GEMM_SHAPES='name:M:N:K:layout,...' from the environment."""
+    env = os.environ.get("GEMM_SHAPES")
+    if not env:
+        return SHAPES
+    out = []
+    for item in env.split(","):
+        name, M, N, K, lay = item.split(":")
+        out.append((name, int(M), int(N), int(K), lay))
+    return out
+
+
 def run(rounds=20):
     dev = torch.device("cuda")
-    for name, M, N, K, lay in SHAPES:
+    for name, M, N, K, lay in _shapes():
         a_km, b_kn = {"nt": (False, False), "nn": (False, True), "tn": (True, True)}[lay]
         A = torch.randn((K, M) if a_km else (M, K), device=dev).to(torch.bfloat16)
         B = torch.randn((K, N) if b_kn else (N, K), device=dev).to(torch.bfloat16)
