@@ -871,9 +871,21 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, int nsplit,
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / n4;
     const int c = (int)(i - r * n4) * 4;
-    float4 a = *reinterpret_cast<const float4*>(slab + r * N + c);
-    for (int z = 1; z < nsplit; ++z) {
-      const float4 b = *reinterpret_cast<const float4*>(slab + z * plane + r * N + c);
+    const float* p = slab + r * N + c;
+    float4 a = *reinterpret_cast<const float4*>(p);
+    int z = 1;
+    for (; z + 3 < nsplit; z += 4) {  // 4 independent plane loads in flight per thread
+      const float4 b0 = *reinterpret_cast<const float4*>(p + z * plane);
+      const float4 b1 = *reinterpret_cast<const float4*>(p + (z + 1) * plane);
+      const float4 b2 = *reinterpret_cast<const float4*>(p + (z + 2) * plane);
+      const float4 b3 = *reinterpret_cast<const float4*>(p + (z + 3) * plane);
+      a.x += (b0.x + b1.x) + (b2.x + b3.x);
+      a.y += (b0.y + b1.y) + (b2.y + b3.y);
+      a.z += (b0.z + b1.z) + (b2.z + b3.z);
+      a.w += (b0.w + b1.w) + (b2.w + b3.w);
+    }
+    for (; z < nsplit; ++z) {
+      const float4 b = *reinterpret_cast<const float4*>(p + z * plane);
       a.x += b.x;
       a.y += b.y;
       a.z += b.z;

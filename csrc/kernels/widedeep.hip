@@ -603,7 +603,8 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
                                                           const float* __restrict__ dwide, int F,
                                                           const int* __restrict__ members,
                                                           const int* __restrict__ memrow, int total,
-                                                          float* __restrict__ grad_rows, int row_stride) {
+                                                          float* __restrict__ grad_rows, int row_stride,
+                                                          int diag) {
   constexpr int L = D / 4, PER = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
   const bool wide = dwide != nullptr;
@@ -612,8 +613,9 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
   for (int64_t piece = wave; piece * (PER * kSegG) < total; piece += nw) {
     const int a = (int)(piece * (PER * kSegG)) + sub * kSegG;
     const int b = min(total, a + kSegG);
-    const int prev_row = (a > 0 && a <= total) ? memrow[a - 1] : -1;
-    const int next_row = b < total ? memrow[b] : -1;
+    // diag (MINIPS_SEG_DIAG=1, timing only, wrong sums): every flush is a plain store
+    const int prev_row = diag ? -2 : ((a > 0 && a <= total) ? memrow[a - 1] : -1);
+    const int next_row = diag ? -2 : (b < total ? memrow[b] : -1);
     int cur = -1;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     float accw = 0.f;
@@ -651,7 +653,7 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
     // hot row takes one atomic per wave instead of one per group (same-address atomics serialise
     // at the memory side).
     const int c0 = __shfl(cur, 0, 64);
-    if (__all(cur == c0) && c0 >= 0) {
+    if (!diag && __all(cur == c0) && c0 >= 0) {
 #pragma unroll
       for (int o = L; o < 64; o <<= 1) {
         acc.x += __shfl_xor(acc.x, o, 64);
@@ -715,6 +717,10 @@ static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, in
     const char* e = std::getenv("MINIPS_SEG_CFG");
     return e ? std::atoi(e) : 0;
   }();
+  static const int diag = [] {
+    const char* e = std::getenv("MINIPS_SEG_DIAG");
+    return e ? std::atoi(e) : 0;
+  }();
   // cfg 0: G=16 lookups per group loaded 8 at a time; 1: G=16 in one batch of 16; 2: G=8 x 8;
   // 3: G=32 x 16
   const int G = cfg == 2 ? 8 : cfg == 3 ? 32 : 16;
@@ -722,7 +728,7 @@ static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, in
   const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
 #define MINIPS_SEG_LAUNCH2(DD, GG, BB)                                                                              \
   hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB>), blocks, 256, 0, s, dX, ldx, dwide, F, members, memrow,   \
-                     total, grad_rows, row_stride);
+                     total, grad_rows, row_stride, diag);
 #define MINIPS_SEG_LAUNCH(DD)                  \
   if (cfg == 1) {                              \
     MINIPS_SEG_LAUNCH2(DD, 16, 16)             \

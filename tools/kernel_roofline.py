@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Per-kernel achieved TFLOP/s and TB/s of the 1-GPU Wide&Deep step against MI355X peaks, from a
+rocprofv3 kernel trace (``--kernel-trace --output-format csv``) of bench.py:
+
+    python tools/kernel_roofline.py gpurun_out/prof/run_kernel_trace.csv --U 212000 > profiles/...
+
+Kernels are identified by name + grid size and given the FLOPs / bytes of their W&D call (batch
+16384, 26 x 32-d embeddings + 13 dense, MLP 896(ext)-1024-512-256-1, bias-folded K of 1032 / 520,
+weight-gradient split-K slabs); ``U`` = unique keys per batch (tools/wd_unique.py). Durations
+are medians over the steady steps (the first 3 steps are skipped). Bytes are the compulsory
+traffic (each operand read once, outputs written once), so TB/s is a lower bound on what the
+kernel moved. Peaks: 2.5 PFLOP/s dense bf16 MFMA, 8 TB/s HBM3E."""
+import argparse
+import csv
+import re
+import statistics
+
+PEAK_TF, PEAK_TB = 2500.0, 8.0
+B, F, D, ND = 16384, 26, 32, 13
+K1, H1, H2, H3 = 896, 1024, 512, 256
+K2, K3 = 1032, 520            # bias-folded K of layers 2 / 3 (ext layout)
+W = 36                        # sparse row: 32 emb + wide + pad (fp32 in the table)
+
+
+def gemm(M, N, K, out_bytes, split=1):
+    flops = 2.0 * M * N * K
+    byts = (M * K + N * K) * 2 + M * N * out_bytes * split
+    return flops, byts
+
+
+def spec(U):
+    """(name regex, grid X or None, label, flops, bytes)"""
+    n = B * F
+    return [
+        (r"gemm_v2_kernel<256, 256, false, false", 262144, "fwd1 X.W1^T 16384x1024x896 +bias/ReLU", *gemm(B, H1, K1, 2)),
+        (r"gemm_v2_kernel<128, 128, false, false", 131072, "fwd2 16384x512x1032 +ReLU", *gemm(B, H2, K2, 2)),
+        (r"gemm_v2_kernel<128, 128, false, false", 65536, "fwd3 16384x256x520 +ReLU", *gemm(B, H3, K3, 2)),
+        (r"gemm_v2_kernel<128, 128, false, true", 131072, "dgrad dH2 16384x512x256 (ReLU mask)",
+         gemm(B, H2, H3, 2)[0], gemm(B, H2, H3, 2)[1] + B * H2 * 2),
+        (r"gemm_v2_kernel<256, 256, false, true, 5", 262144, "dgrad dH1 16384x1024x512 (ReLU mask)",
+         gemm(B, H1, H2, 2)[0], gemm(B, H1, H2, 2)[1] + B * H1 * 2),
+        (r"gemm_v2_kernel<256, 256, false, true, 4", 262144, "dgrad dX 16384x832x1024", *gemm(B, F * D, H1, 2)),
+        (r"gemm_v2_kernel<128, 128, true, true", None, "wgrad W3 256x520x16384 (split-K slabs)",
+         *gemm(H3, K3, B, 4, 16)),
+        (r"gemm_v2_kernel<256, 256, true, true", 10240, "wgrad W2 512x1032x16384 (split-K slabs)",
+         *gemm(H2, K2, B, 4, 15)),
+        (r"gemm_v2_kernel<256, 256, true, true", 16384, "wgrad W1 1024x896x16384 (split-K slabs)",
+         *gemm(H1, K1, B, 4, 10)),
+        (r"splitk_reduce_kernel", 33280, "split-K reduce W3 (16 planes)", 0, 16 * H3 * K3 * 4 + 2 * H3 * K3 * 4),
+        (r"splitk_reduce_kernel", 132096, "split-K reduce W2 (15 planes)", 0, 15 * H2 * K2 * 4 + 2 * H2 * K2 * 4),
+        (r"splitk_reduce_kernel", 229376, "split-K reduce W1 (10 planes)", 0, 10 * H1 * K1 * 4 + 2 * H1 * K1 * 4),
+        (r"gather_rows_vec4", None, "sparse Get: gather U rows -> bf16", 0, U * (W * 4 + W * 2 + 8)),
+        (r"wd_assemble_kernel", None, "assemble X (lookup + dense + wide sum)", 0,
+         B * K1 * 2 + n * (D * 2 + 8 + 2) + B * ND * 4 + B * 4),
+        (r"wd_head_kernel", None, "head Linear 256->1 + BCE fwd/bwd", 0, B * H3 * 2 * 2 + B * 12),
+        (r"zero_rows_dev_kernel", None, "zero grad rows", 0, U * W * 4),
+        (r"emb_seg_sum_kernel", None, "embedding backward (segment sums)", 0, n * (D * 2 + 8 + 4) + U * W * 4),
+        (r"sparse_rowwise_adagrad_v4", None, "row-wise Adagrad apply (U rows)", 0, U * (W * 4 * 3 + 8 + 8 + 8)),
+        (r"adam_kernel", None, "Adam (dense 1.58M params)", 0, 1582080 * (16 + 18)),
+        (r"criteo_synth_kernel", None, "synthetic batch (planning stream)", 0, B * (F * 8 + ND * 4 + 4)),
+        (r"ub_insert_kernel", None, "dedupe: hash insert (planning)", 0, n * 8 * 2),
+        (r"ub_assign_kernel", None, "dedupe: assign (planning)", 0, n * 8 * 2 + U * 8),
+        (r"ub_inverse_kernel", None, "dedupe: inverse (planning)", 0, n * 8 * 2),
+        (r"emb_seg_fill_kernel", None, "lookup CSR fill (planning)", 0, n * (8 + 8)),
+    ]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--U", type=float, required=True, help="unique keys per batch (tools/wd_unique.py)")
+    ap.add_argument("--skip", type=int, default=3, help="steps to skip")
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "gather_rows" in r["Kernel_Name"]]
+    steps = [rows[starts[i]: starts[i + 1]] for i in range(a.skip, len(starts) - 1)]
+    specs = spec(a.U)
+    per = {}
+    for st in steps:
+        for r in st:
+            name, gx = r["Kernel_Name"], int(r["Grid_Size_X"])
+            for pat, g, label, fl, by in specs:
+                if re.search(pat, name) and (g is None or g == gx):
+                    per.setdefault(label, (fl, by, []))[2].append((int(r["End_Timestamp"]) -
+                                                                  int(r["Start_Timestamp"])) / 1e3)
+                    break
+    print(f"# W&D 1-GPU step: per-kernel achieved rates ({len(steps)} steady steps, U = {a.U:.0f})\n")
+    print("| kernel | us (median) | GFLOP | MB | TFLOP/s | % bf16 peak | TB/s | % HBM peak |")
+    print("|---|---|---|---|---|---|---|---|")
+    tot = 0.0
+    for _, _, label, _, _ in specs:
+        if label not in per:
+            continue
+        fl, by, ds = per[label]
+        us = statistics.median(ds)
+        tot += us
+        tf = fl / us / 1e6
+        tb = by / us / 1e6
+        print(f"| {label} | {us:.1f} | {fl / 1e9:.1f} | {by / 1e6:.1f} | {tf:.0f} | {100 * tf / PEAK_TF:.0f}% | "
+              f"{tb:.2f} | {100 * tb / PEAK_TB:.0f}% |")
+    print(f"\nSum of the listed kernels: {tot:.0f} us per step (the streams overlap: compute, weight-gradient "
+          "side stream, planning stream).")
+
+
+if __name__ == "__main__":
+    main()
