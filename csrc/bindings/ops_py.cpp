@@ -402,6 +402,46 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
                                    (int)D, ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
 }
 
+// Sort-based planning of a [B, F] batch with disjoint column key ranges (see kernels.h).
+// Returns (uniq, inv, counts [1], U_dev [1], members, memrow).
+std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& col_base, int64_t col_bits,
+                                    int64_t route_mult, int64_t route_n) {
+  check_gpu(keys, "keys");
+  check_dtype(keys, at::kLong, "keys");
+  check_gpu(col_base, "col_base");
+  check_dtype(col_base, at::kLong, "col_base");
+  TORCH_CHECK(keys.dim() == 2, "keys: [B, F]");
+  const int64_t B = keys.size(0), F = keys.size(1);
+  TORCH_CHECK(B >= 1 && B <= 16384 && F >= 1 && F <= 64, "plan_sorted: 1 <= B <= 16384, 1 <= F <= 64");
+  TORCH_CHECK(col_base.numel() == F, "col_base: one base per column");
+  TORCH_CHECK(col_bits >= 1 && col_bits <= 32, "col_bits: 1..32");
+  const int64_t n = B * F;
+  auto o64 = keys.options();
+  auto ws = at::empty({2 * n + F}, o64.dtype(at::kInt));
+  auto ukey = at::empty({n}, o64), uniq = at::empty({n}, o64), inv = at::empty({n}, o64);
+  auto members = at::empty({n}, o64.dtype(at::kInt)), memrow = at::empty({n}, o64.dtype(at::kInt));
+  auto counts = at::empty({2}, o64);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), (int)col_bits,
+                        (uint64_t)route_mult, (uint64_t)route_n, ws.data_ptr<int32_t>(), ptr<int64_t>(ukey),
+                        ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
+                        ptr<int64_t>(counts), stream_of(keys));
+  return {uniq, inv, counts.narrow(0, 0, 1), counts.narrow(0, 1, 1), members, memrow};
+}
+
+// A HIP stream whose kernels may only use the CUs set in `mask` (hipExtStreamCreateWithCUMask;
+// 32-bit words, bit i = CU i). Returned as an integer handle for torch.cuda.ExternalStream; the
+// stream lives for the process (the planning stream of a rank).
+int64_t cu_masked_stream(int64_t device, std::vector<int64_t> mask) {
+  TORCH_CHECK(!mask.empty(), "cu_masked_stream: empty mask");
+  std::vector<uint32_t> m(mask.begin(), mask.end());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  hipStream_t st = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data());
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+  return reinterpret_cast<int64_t>(st);
+}
+
 void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x: row-major GPU matrix");
   check_dtype(x, at::kBFloat16, "x");
@@ -976,6 +1016,8 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("members") = py::none(), py::arg("memrow") = py::none());
   m.def("emb_seg_adagrad", &emb_seg_adagrad);
   m.def("colsum_bf16", &colsum_bf16);
+  m.def("cu_masked_stream", &cu_masked_stream);
+  m.def("plan_sorted", &plan_sorted);
   m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none(),
         py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),

@@ -1,0 +1,216 @@
+// Sort-based key planning of a [B, F] lookup batch whose F columns hold disjoint key ranges
+// (Wide&Deep / DLRM: feature f's ids live in [base_f, base_f + card_f)).
+//
+// The hash dedupe (sparse.hip, unique_bucketize) resolves duplicates across workgroups with
+// device-scope atomics (CAS probes, per-key counts, shard cursors). Those execute at the memory
+// side on the multi-XCD part and slow every concurrently running kernel: the W&D step measured
+// 0.450 ms with per-step planning vs 0.360 ms stepping through pre-planned batches
+// (tools/step_ablation.py) even with the planning stream confined to 16 CUs. This planner uses
+// no atomics at all:
+//
+//   plan_sort_col  one 1024-thread workgroup per column: the column's <= 16384 (key - base_f, b)
+//                  pairs sit in registers (16 per thread) and are LSD radix-sorted in LDS, 4 bits
+//                  per pass (ceil(col_bits / 4) passes): per-thread packed 8-bit digit counters ->
+//                  [digit][thread] LDS histogram -> block exclusive scan -> stable scatter ->
+//                  reload. Run heads of the sorted keys give the column's unique keys in ascending
+//                  order and each lookup's column-local unique index.
+//   plan_emit      global unique index u = (sum of the unique counts of columns < f) + local:
+//                  uniq[u] (routed key), inv[b*F + f] = u, and the embedding backward's CSR for
+//                  free -- members (lookup ids grouped by u, ascending) and memrow (their u).
+//
+// Deterministic (no atomics, stable sort); unique keys come out column-major, ascending inside a
+// column; one owner (a one-rank table: counts[0] = U).
+#include <stdexcept>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace minips_k {
+
+constexpr int kPsThreads = 1024, kPsItems = 16, kPsMax = kPsThreads * kPsItems;
+
+// Exclusive scan of one value per thread over a 1024-thread block; *total = the sum. ws: >= 17
+// uint32 of LDS; ends with a barrier (ws reusable).
+__device__ __forceinline__ uint32_t ps_block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) ws[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t w = lane < 16 ? ws[lane] : 0u;
+    uint32_t s = w;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const uint32_t y = __shfl_up(s, o, 64);
+      if (lane >= o) s += y;
+    }
+    if (lane < 16) ws[lane] = s - w;
+    if (lane == 15) ws[16] = s;
+  }
+  __syncthreads();
+  const uint32_t res = ws[wave] + x - v;
+  *total = ws[16];
+  __syncthreads();
+  return res;
+}
+
+__device__ __forceinline__ uint32_t ps_count(uint64_t lo, uint64_t hi, int d) {
+  return (uint32_t)((d < 8 ? (lo >> (8 * d)) : (hi >> (8 * (d - 8)))) & 0xffu);
+}
+
+__global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const int64_t* __restrict__ keys, int B, int F,
+                                                                   const int64_t* __restrict__ col_base, int nbits,
+                                                                   int32_t* __restrict__ sorted_b,
+                                                                   int32_t* __restrict__ local_u,
+                                                                   int64_t* __restrict__ ukey,
+                                                                   int32_t* __restrict__ ucount) {
+  __shared__ uint16_t cnt[16 * kPsThreads];  // [digit][thread] counts, then their scanned offsets
+  __shared__ uint32_t skey[kPsMax];
+  __shared__ uint16_t sval[kPsMax];
+  __shared__ uint32_t ws[20];
+  const int t = threadIdx.x, f = blockIdx.x;
+  const int64_t base = col_base[f];
+  uint32_t k[kPsItems];
+  uint32_t v[kPsItems];
+#pragma unroll
+  for (int q = 0; q < kPsItems; ++q) {
+    const int i = t * kPsItems + q;
+    // padding items (i >= B) get the largest key: with the stable sort they land behind every
+    // real item even when a real key ties with their truncated value
+    k[q] = i < B ? (uint32_t)(keys[(int64_t)i * F + f] - base) : 0xffffffffu;
+    v[q] = (uint32_t)i;
+  }
+  for (int shift = 0; shift < nbits; shift += 4) {
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int q = 0; q < kPsItems; ++q) {
+      const int d = (int)((k[q] >> shift) & 15u);
+      if (d < 8) lo += 1ull << (8 * d);
+      else hi += 1ull << (8 * (d - 8));
+    }
+#pragma unroll
+    for (int d = 0; d < 16; ++d) cnt[d * kPsThreads + t] = (uint16_t)ps_count(lo, hi, d);
+    __syncthreads();
+    // exclusive scan in [digit][thread] order: thread t owns entries [16t, 16t + 16)
+    uint32_t loc[16];
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      loc[q] = s;
+      s += cnt[16 * t + q];
+    }
+    uint32_t tot;
+    const uint32_t pre = ps_block_scan(s, ws, &tot);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) cnt[16 * t + q] = (uint16_t)(pre + loc[q]);
+    __syncthreads();
+    uint64_t slo = 0, shi = 0;
+#pragma unroll
+    for (int q = 0; q < kPsItems; ++q) {
+      const int d = (int)((k[q] >> shift) & 15u);
+      const uint32_t r = ps_count(slo, shi, d);
+      if (d < 8) slo += 1ull << (8 * d);
+      else shi += 1ull << (8 * (d - 8));
+      const uint32_t pos = (uint32_t)cnt[d * kPsThreads + t] + r;
+      skey[pos] = k[q];
+      sval[pos] = (uint16_t)v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPsItems; ++q) {
+      k[q] = skey[t * kPsItems + q];
+      v[q] = sval[t * kPsItems + q];
+    }
+    __syncthreads();
+  }
+  // run heads of the sorted keys (skey still holds them: nbits >= 1 ran at least one pass)
+  uint32_t heads = 0;
+#pragma unroll
+  for (int q = 0; q < kPsItems; ++q) {
+    const int pos = t * kPsItems + q;
+    const bool h = pos < B && (pos == 0 || k[q] != skey[pos - 1]);
+    heads += h ? 1u : 0u;
+  }
+  uint32_t total;
+  uint32_t run = ps_block_scan(heads, ws, &total);
+  const int64_t col0 = (int64_t)f * B;
+#pragma unroll
+  for (int q = 0; q < kPsItems; ++q) {
+    const int pos = t * kPsItems + q;
+    if (pos >= B) break;
+    const bool h = pos == 0 || k[q] != skey[pos - 1];
+    if (h) ++run;
+    const uint32_t lu = run - 1;
+    sorted_b[col0 + pos] = (int32_t)v[q];
+    local_u[col0 + pos] = (int32_t)lu;
+    if (h) ukey[col0 + lu] = base + (int64_t)k[q];
+  }
+  if (t == 0) ucount[f] = (int32_t)total;
+}
+
+__device__ __forceinline__ int64_t ps_route(int64_t key, uint64_t mult, uint64_t rn) {
+  return mult ? (int64_t)(((uint64_t)key * mult) % rn) : key;
+}
+
+__global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int32_t* __restrict__ sorted_b,
+                                                        const int32_t* __restrict__ local_u,
+                                                        const int64_t* __restrict__ ukey,
+                                                        const int32_t* __restrict__ ucount, uint64_t rmult,
+                                                        uint64_t rn, int64_t* __restrict__ uniq,
+                                                        int64_t* __restrict__ inv, int32_t* __restrict__ members,
+                                                        int32_t* __restrict__ memrow, int64_t* __restrict__ counts) {
+  __shared__ int64_t basef[65];
+  __shared__ int32_t ucf[64];
+  const int t = threadIdx.x;
+  if (t < F) ucf[t] = ucount[t];
+  __syncthreads();
+  if (t == 0) {
+    int64_t acc = 0;
+    for (int c = 0; c < F; ++c) {
+      basef[c] = acc;
+      acc += ucf[c];
+    }
+    basef[F] = acc;
+    if (blockIdx.x == 0) {
+      counts[0] = acc;  // one owner: counts[0] = U
+      counts[1] = acc;  // the device-side U
+    }
+  }
+  __syncthreads();
+  const int64_t n = (int64_t)B * F;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + t; idx < n; idx += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(idx / B);
+    const int pos = (int)(idx - (int64_t)c * B);
+    const int64_t u = basef[c] + local_u[idx];
+    const int64_t j = (int64_t)sorted_b[idx] * F + c;
+    inv[j] = u;
+    members[idx] = (int32_t)j;
+    memrow[idx] = (int32_t)u;
+    if (pos < ucf[c]) uniq[basef[c] + pos] = ps_route(ukey[idx], rmult, rn);
+  }
+}
+
+void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, int col_bits, uint64_t route_mult,
+                 uint64_t route_n, int32_t* ws, int64_t* ukey, int64_t* uniq, int64_t* inv, int32_t* members,
+                 int32_t* memrow, int64_t* counts, hipStream_t s) {
+  if (B < 1 || B > kPsMax) throw std::runtime_error("plan_sorted: 1 <= B <= 16384 rows per column");
+  if (F < 1 || F > 64) throw std::runtime_error("plan_sorted: 1 <= F <= 64 columns");
+  if (col_bits < 1 || col_bits > 32) throw std::runtime_error("plan_sorted: column key range must be 1..32 bits");
+  if (route_mult && !route_n) throw std::runtime_error("plan_sorted: routing needs the row count");
+  const int64_t n = (int64_t)B * F;
+  int32_t* sorted_b = ws;
+  int32_t* local_u = ws + n;
+  int32_t* ucount = ws + 2 * n;
+  hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, keys, B, F, col_base, col_bits, sorted_b, local_u,
+                     ukey, ucount);
+  hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
+                     route_mult, route_n, uniq, inv, members, memrow, counts);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace minips_k

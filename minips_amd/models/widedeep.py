@@ -84,9 +84,10 @@ class WideDeep(LookaheadPlans):
         dev = comm.device
         F, D = cfg.F, cfg.emb_dim
         self.num_rows = int(sum(cfg.cards))
+        bases = [sum(cfg.cards[:f]) for f in range(F)]  # feature f's ids start at its offset
         self.emb = SparseTable(comm, self.num_rows, cfg.row_width, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
                                consistency=cfg.consistency, staleness=cfg.staleness, split=D, table_id=0,
-                               init_std=0.01, seed=cfg.seed)
+                               init_std=0.01, seed=cfg.seed, columns=(bases, cfg.cards))
         # wide weights start at zero (columns >= D)
         self.emb.shard[:, D:].zero_()
         # Dense layout: each Linear is stored as W_ext [n_out, k_pad] with the bias in column k_in;

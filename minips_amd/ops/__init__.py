@@ -209,6 +209,35 @@ def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1, rou
     return out, inv, counts, torch.tensor([u.numel()], dtype=torch.int64)
 
 
+def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0):
+    """Key planning of a [B, F] batch whose columns hold disjoint key ranges (column f's keys in
+    [col_base[f], col_base[f] + 2**col_bits)): per-column radix sort, no atomics (plan.hip).
+    Returns (uniq [n] (first U valid, routed, column-major then ascending), inv [n], counts [1],
+    U_dev [1], members [n] int32, memrow [n] int32) -- the unique_bucketize_n outputs for one owner
+    plus the lookup CSR of emb_build_csr."""
+    if _gpu(keys):
+        return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), int(col_bits), int(route_mult),
+                                           int(route_n)))
+    B, F = keys.shape
+    uniq_l, inv_l = [], []
+    base = 0
+    for f in range(F):
+        u, i = torch.unique(keys[:, f], sorted=True, return_inverse=True)
+        uniq_l.append(u)
+        inv_l.append(i + base)
+        base += u.numel()
+    U = base
+    uniq = torch.cat(uniq_l)
+    if route_mult:
+        uniq = (uniq * route_mult) % route_n
+    out = torch.empty(B * F, dtype=torch.int64)
+    out[:U] = uniq
+    inv = torch.stack(inv_l, 1).reshape(-1)
+    order = torch.sort(inv, stable=True).indices
+    cnt = torch.tensor([U], dtype=torch.int64)
+    return out, inv, cnt, cnt.clone(), order.to(torch.int32), inv[order].to(torch.int32)
+
+
 def gather_rows(table, keys, base, out, n_dev=None):
     """out[i] = table[keys[i] - base] for i < n (n = keys.numel(), or the device count n_dev)."""
     if _gpu(keys):

@@ -511,6 +511,11 @@ class SparsePlan:
         return self._U
 
 
+# Key planning of [B, F] batches with disjoint column key ranges (SparseTable ``columns``) on one
+# rank: per-column radix sort without atomics (ops.plan_sorted) instead of the hash dedupe, whose
+# memory-side atomics slow the concurrently running step; MINIPS_SORT_PLAN=0 keeps the hash path
+_SORT_PLAN = os.environ.get("MINIPS_SORT_PLAN", "1") != "0"
+
 # one rank + row-wise Adagrad: MINIPS_FUSED_EMB_ADAGRAD=1 feeds the embedding backward's segment
 # sums to the apply directly (ops.emb_seg_adagrad, no grad_rows buffer). Measured slower in the
 # Wide&Deep step on one MI355X (0.473-0.477 vs 0.465 ms/step: the fused kernel's key -> row ->
@@ -540,10 +545,14 @@ class SparseTable:
                  lr: float = 0.01, eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "bsp",
                  staleness: int = 0, split: int | None = None, table_id: int = 0, init_std: float = 0.01,
                  seed: int = 1234, p2p: bool | None = None, push_dtype=None, route: str = "mix",
-                 value_dtype=torch.float32):
+                 value_dtype=torch.float32, columns=None):
         """``value_dtype`` float64: the reference's double tables (CreateTable<double>,
         lr_example.cpp:182; values read as double, kv_client_table.hpp:96-101) -- optimizer "add"
-        (VectorStorage::SubAdd), rows pulled and pushed in fp64 (f64.hip kernels)."""
+        (VectorStorage::SubAdd), rows pulled and pushed in fp64 (f64.hip kernels).
+
+        ``columns`` = (bases, cards): a caller whose [B, F] key batches hold disjoint ranges per
+        column (column f's keys in [bases[f], bases[f] + cards[f]), e.g. concatenated feature
+        tables) lets one-rank planning use the atomic-free per-column sort (ops.plan_sorted)."""
         if value_dtype not in (torch.float32, torch.float64):
             raise ValueError(f"value_dtype {value_dtype}")
         if value_dtype == torch.float64:
@@ -552,6 +561,12 @@ class SparseTable:
             pull_dtype = push_dtype = torch.float64
         self.value_dtype = value_dtype
         self.comm = comm
+        self.columns = None
+        if columns is not None:
+            bases, cards = columns
+            bits = max(1, max(int(c) - 1 for c in cards).bit_length())
+            if bits <= 32:
+                self.columns = (torch.as_tensor(list(bases), dtype=torch.int64, device=comm.device), bits)
         # Key -> row placement. "range": row = key (the reference's contiguous range partition).
         # "mix" (default): row = key * A mod num_rows, a bijection (A prime, coprime to num_rows),
         # then the same equal ranges: contiguous key blocks (a big feature of a concatenated
@@ -633,6 +648,20 @@ class SparseTable:
         fused = want_csr and _CSR_FUSED
         n = flat.numel()
         zeroed = None
+        cols = self.columns
+        if (cols is not None and _SORT_PLAN and flat.is_cuda and self.comm.world == 1 and keys.dim() == 2
+                and keys.shape[0] <= 16384 and keys.shape[1] == cols[0].numel()):
+            # disjoint column key ranges on one rank: atomic-free per-column sort (ops.plan_sorted),
+            # which also yields the embedding backward's lookup CSR
+            pp.flat = flat
+            uniq, inv, counts, U_dev, members, memrow = ops.plan_sorted(
+                keys if keys.dtype == torch.int64 else keys.to(torch.int64), cols[0], cols[1], rmult,
+                self.num_rows if rmult else 0)
+            pp.uniq, pp.inv, pp.counts, pp.U_dev = uniq, inv, counts, U_dev
+            pp.csr = (members, memrow) if want_csr else None
+            pp.host = pp.event = pp.cev = None
+            pp.exchanged = True
+            return pp
         if rmult:  # range tables: the routing is fused into the dedupe kernel
             pp.flat = flat
             res = ops.unique_bucketize_n(flat, self.bounds, pp.F, rmult, self.num_rows,

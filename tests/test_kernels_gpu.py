@@ -1,5 +1,7 @@
 """Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op
 (the CPU implementations in minips_amd.ops are that reference)."""
+import math
+
 import pytest
 import torch
 
@@ -438,3 +440,30 @@ def test_colsum_bf16(dev):
         ref = out + x.float().sum(0)
         got = ops.colsum_add(x.to(dev), out.to(dev))
         torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,cards", [(16384, [3, 1460, 10131227, 583, 24, 2202608]), (1000, [5, 70000]),
+                                     (16384, [1 << 24])])
+def test_plan_sorted_matches_reference(dev, B, cards):
+    """Atomic-free sort-based planning (plan.hip) vs the fp32-free CPU reference: same unique keys
+    (column-major, ascending), uniq[inv] == routed keys, and the lookup CSR grouped by row."""
+    g = torch.Generator().manual_seed(B + len(cards))
+    bases = [sum(cards[:f]) for f in range(len(cards))]
+    cols = []
+    for c, base in zip(cards, bases):
+        zipf = torch.floor(torch.exp(torch.rand(B, generator=g, dtype=torch.float64) * math.log(c + 1)) - 1)
+        cols.append(zipf.clamp(0, c - 1).to(torch.int64) + base)
+    keys = torch.stack(cols, 1)
+    R = sum(cards)
+    mult = 402653189 if R % 402653189 else 201326611
+    bits = max(1, max(c - 1 for c in cards).bit_length())
+    ref = ops.plan_sorted(keys, torch.tensor(bases), bits, mult, R)
+    got = [t.cpu() for t in ops.plan_sorted(keys.to(dev), torch.tensor(bases, device=dev), bits, mult, R)]
+    U = int(ref[3])
+    assert int(got[3]) == U == int(got[2])
+    torch.testing.assert_close(got[0][:U], ref[0][:U])
+    torch.testing.assert_close(got[1], ref[1])
+    torch.testing.assert_close(got[0][got[1]], (keys.reshape(-1) * mult) % R)
+    torch.testing.assert_close(got[5], ref[5])                      # memrow: rows ascending
+    assert bool((got[1][got[4].long()] == got[5].long()).all())      # members belong to their row
+    assert sorted(got[4].tolist()) == list(range(B * len(cards)))

@@ -32,7 +32,8 @@ def spec(U):
     """(name regex, grid X or None, label, flops, bytes)"""
     n = B * F
     return [
-        (r"gemm_v2_kernel<256, 256, false, false", 262144, "fwd1 X.W1^T 16384x1024x896 +bias/ReLU", *gemm(B, H1, K1, 2)),
+        (r"gemm_v2_kernel<256, 256, false, false", 262144, "fwd1 X.W1^T 16384x1024x896 +bias/ReLU",
+         *gemm(B, H1, K1, 2)),
         (r"gemm_v2_kernel<128, 128, false, false", 131072, "fwd2 16384x512x1032 +ReLU", *gemm(B, H2, K2, 2)),
         (r"gemm_v2_kernel<128, 128, false, false", 65536, "fwd3 16384x256x520 +ReLU", *gemm(B, H3, K3, 2)),
         (r"gemm_v2_kernel<128, 128, false, true", 131072, "dgrad dH2 16384x512x256 (ReLU mask)",

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""What the 1-GPU Wide&Deep step pays for its data + key planning: times bench.py's loop
+(LookaheadFeeder: next batch generated and planned on the planning stream every step) against
+the same model stepping through a ring of pre-generated batches whose plans were computed up
+front (no generation, no dedupe / CSR per step; distinct batches keep the row traffic real).
+Diagnostic only -- the second number is not a valid benchmark."""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _time(fn, n):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e3
+
+
+def main(n=int(os.environ.get("STEPS", "300"))):
+    from minips_amd.data.synthetic import CriteoSynth
+    from minips_amd.models.feeder import LookaheadFeeder
+    from minips_amd.models.widedeep import WideDeep, WideDeepConfig
+    from minips_amd.ps.comm import Comm
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    comm = Comm(device=dev)
+    cfg = WideDeepConfig()
+    model = WideDeep(cfg, comm)
+    data = CriteoSynth(16384, cards=cfg.cards, device=dev, seed=1)
+    feeder = LookaheadFeeder(model, data, comm)
+    full = _time(feeder.step, n)
+    torch.cuda.synchronize()
+    # a ring of pre-generated batches with their plans: realistic cache behaviour for the rows
+    ring = []
+    for _ in range(int(os.environ.get("RING", "48"))):
+        dense, keys, labels = data.next()
+        ring.append((dense, keys, labels, model.emb.plan(keys, csr=True)))
+    torch.cuda.synchronize()
+    plans = {id(b[1]): b[3] for b in ring}
+    model._take_plan = lambda k: plans[id(k)]
+    pos = [0]
+
+    def step():
+        d, k, y, _ = ring[pos[0] % len(ring)]
+        pos[0] += 1
+        model.train_step(d, k, y)
+
+    fixed = _time(step, n)
+    print(f"feeder step {full:.4f} ms | pre-planned ring of {len(ring)} batches {fixed:.4f} ms | data + planning "
+          f"cost {full - fixed:.4f} ms/step")
+
+
+if __name__ == "__main__":
+    main()
