@@ -404,25 +404,29 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
 
 // Sort-based planning of a [B, F] batch with disjoint column key ranges (see kernels.h).
 // Returns (uniq, inv, counts [1], U_dev [1], members, memrow).
-std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& col_base, int64_t col_bits,
-                                    int64_t route_mult, int64_t route_n) {
+std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& col_base, const at::Tensor& col_bits,
+                                    std::vector<int64_t> col_bits_host, int64_t route_mult, int64_t route_n) {
   check_gpu(keys, "keys");
   check_dtype(keys, at::kLong, "keys");
   check_gpu(col_base, "col_base");
   check_dtype(col_base, at::kLong, "col_base");
+  check_gpu(col_bits, "col_bits");
+  check_dtype(col_bits, at::kInt, "col_bits");
   TORCH_CHECK(keys.dim() == 2, "keys: [B, F]");
   const int64_t B = keys.size(0), F = keys.size(1);
   TORCH_CHECK(B >= 1 && B <= 16384 && F >= 1 && F <= 64, "plan_sorted: 1 <= B <= 16384, 1 <= F <= 64");
-  TORCH_CHECK(col_base.numel() == F, "col_base: one base per column");
-  TORCH_CHECK(col_bits >= 1 && col_bits <= 32, "col_bits: 1..32");
+  TORCH_CHECK(col_base.numel() == F && col_bits.numel() == F && (int64_t)col_bits_host.size() == F,
+              "one base / bit count per column");
+  // the host copy of the device bit counts is what is validated (the kernel trusts the device one)
+  for (int64_t b : col_bits_host) TORCH_CHECK(b >= 1 && b <= 32, "col_bits: 1..32");
   const int64_t n = B * F;
   auto o64 = keys.options();
-  auto ws = at::empty({2 * n + F}, o64.dtype(at::kInt));
+  auto ws = at::empty({3 * n + F + 4}, o64.dtype(at::kInt));  // sorted_b | local_u | ucount | column-major keys
   auto ukey = at::empty({n}, o64), uniq = at::empty({n}, o64), inv = at::empty({n}, o64);
   auto members = at::empty({n}, o64.dtype(at::kInt)), memrow = at::empty({n}, o64.dtype(at::kInt));
   auto counts = at::empty({2}, o64);
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
-  minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), (int)col_bits,
+  minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), col_bits.data_ptr<int32_t>(),
                         (uint64_t)route_mult, (uint64_t)route_n, ws.data_ptr<int32_t>(), ptr<int64_t>(ukey),
                         ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
                         ptr<int64_t>(counts), stream_of(keys));

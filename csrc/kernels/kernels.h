@@ -124,12 +124,12 @@ void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, in
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                           float* grad_rows, int row_stride, hipStream_t s);
 // Sort-based key planning of a [B, F] batch with disjoint column key ranges (plan.hip): keys of
-// column f lie in [col_base[f], col_base[f] + 2^col_bits). One owner. ws: int32 [2*B*F + F],
-// ukey: int64 [B*F]. Outputs: uniq [B*F] (first U valid, routed), inv [B*F], the lookup CSR
-// members/memrow [B*F] int32, counts [2] = {U (owner 0), U}.
-void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, int col_bits, uint64_t route_mult,
-                 uint64_t route_n, int32_t* ws, int64_t* ukey, int64_t* uniq, int64_t* inv, int32_t* members,
-                 int32_t* memrow, int64_t* counts, hipStream_t s);
+// column f lie in [col_base[f], col_base[f] + 2^col_bits[f]), 1 <= col_bits[f] <= 32 (device
+// arrays). One owner. ws: int32 [3*B*F + F], ukey: int64 [B*F]. Outputs: uniq [B*F] (first U
+// valid, routed), inv [B*F], the lookup CSR members/memrow [B*F] int32, counts [2] = {U, U}.
+void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
+                 uint64_t route_mult, uint64_t route_n, int32_t* ws, int64_t* ukey, int64_t* uniq, int64_t* inv,
+                 int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s);
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
 void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s);
 // Embedding backward fused with the row-wise Adagrad apply (one rank, local shard): the rows of

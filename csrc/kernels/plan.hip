@@ -10,7 +10,7 @@
 //
 //   plan_sort_col  one 1024-thread workgroup per column: the column's <= 16384 (key - base_f, b)
 //                  pairs sit in registers (16 per thread) and are LSD radix-sorted in LDS, 4 bits
-//                  per pass (ceil(col_bits / 4) passes): per-thread packed 8-bit digit counters ->
+//                  per pass (ceil(col_bits[f] / 4) passes): per-thread packed 8-bit digit counters ->
 //                  [digit][thread] LDS histogram -> block exclusive scan -> stable scatter ->
 //                  reload. Run heads of the sorted keys give the column's unique keys in ascending
 //                  order and each lookup's column-local unique index.
@@ -63,28 +63,70 @@ __device__ __forceinline__ uint32_t ps_count(uint64_t lo, uint64_t hi, int d) {
   return (uint32_t)((d < 8 ? (lo >> (8 * d)) : (hi >> (8 * (d - 8)))) & 0xffu);
 }
 
-__global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const int64_t* __restrict__ keys, int B, int F,
-                                                                   const int64_t* __restrict__ col_base, int nbits,
+// [B, F] int64 keys -> column-major [F, B] uint32 (key - base_f) through a 64 x F LDS tile: the
+// sort reads its column as contiguous 16-byte vectors instead of one 8-byte key per 208-byte row
+// (that strided column gather pulled the whole batch through each sorting CU: ~70 us fixed cost)
+__global__ __launch_bounds__(256) void plan_transpose_kernel(const int64_t* __restrict__ keys, int B, int F,
+                                                             const int64_t* __restrict__ col_base,
+                                                             uint32_t* __restrict__ krel) {
+  __shared__ uint32_t tile[64][65];
+  __shared__ int64_t basef[64];
+  const int t = threadIdx.x;
+  if (t < F) basef[t] = col_base[t];
+  const int b0 = blockIdx.x * 64;
+  __syncthreads();
+  for (int e = t; e < 64 * F; e += 256) {  // coalesced row-major reads
+    const int r = e / F, c = e - r * F;
+    const int b = b0 + r;
+    if (b < B) tile[c][r] = (uint32_t)(keys[(int64_t)b * F + c] - basef[c]);
+  }
+  __syncthreads();
+  for (int e = t; e < 64 * F; e += 256) {  // coalesced column-major writes
+    const int c = e >> 6, r = e & 63;
+    const int b = b0 + r;
+    if (b < B) krel[(int64_t)c * B + b] = tile[c][r];
+  }
+}
+
+__global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const uint32_t* __restrict__ krel, int B,
+                                                                   const int64_t* __restrict__ col_base,
+                                                                   const int32_t* __restrict__ col_bits,
                                                                    int32_t* __restrict__ sorted_b,
                                                                    int32_t* __restrict__ local_u,
                                                                    int64_t* __restrict__ ukey,
                                                                    int32_t* __restrict__ ucount) {
-  __shared__ uint16_t cnt[16 * kPsThreads];  // [digit][thread] counts, then their scanned offsets
-  __shared__ uint32_t skey[kPsMax];
-  __shared__ uint16_t sval[kPsMax];
+  __shared__ __attribute__((aligned(16))) uint16_t cnt[16 * kPsThreads];  // [digit][thread] counts -> offsets
+  __shared__ __attribute__((aligned(16))) uint32_t skey[kPsMax];
+  __shared__ __attribute__((aligned(16))) uint16_t sval[kPsMax];
   __shared__ uint32_t ws[20];
   const int t = threadIdx.x, f = blockIdx.x;
   const int64_t base = col_base[f];
+  const int nbits = col_bits[f];  // a small-cardinality column sorts in fewer passes
   uint32_t k[kPsItems];
   uint32_t v[kPsItems];
+  const uint32_t* col = krel + (int64_t)f * B;
+  if ((B & 3) == 0 && (reinterpret_cast<uintptr_t>(krel) & 15) == 0 && t * kPsItems + kPsItems <= B) {
+    // 4 x 16-byte loads of this thread's 16 keys
+    const uint4* p = reinterpret_cast<const uint4*>(col + t * kPsItems);
 #pragma unroll
-  for (int q = 0; q < kPsItems; ++q) {
-    const int i = t * kPsItems + q;
-    // padding items (i >= B) get the largest key: with the stable sort they land behind every
-    // real item even when a real key ties with their truncated value
-    k[q] = i < B ? (uint32_t)(keys[(int64_t)i * F + f] - base) : 0xffffffffu;
-    v[q] = (uint32_t)i;
+    for (int e = 0; e < 4; ++e) {
+      const uint4 u = p[e];
+      k[4 * e] = u.x;
+      k[4 * e + 1] = u.y;
+      k[4 * e + 2] = u.z;
+      k[4 * e + 3] = u.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kPsItems; ++q) {
+      const int i = t * kPsItems + q;
+      // padding items (i >= B) get the largest key: with the stable sort they land behind every
+      // real item even when a real key ties with their truncated value
+      k[q] = i < B ? col[i] : 0xffffffffu;
+    }
   }
+#pragma unroll
+  for (int q = 0; q < kPsItems; ++q) v[q] = (uint32_t)(t * kPsItems + q);
   for (int shift = 0; shift < nbits; shift += 4) {
     uint64_t lo = 0, hi = 0;
 #pragma unroll
@@ -96,18 +138,26 @@ __global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const int64_t
 #pragma unroll
     for (int d = 0; d < 16; ++d) cnt[d * kPsThreads + t] = (uint16_t)ps_count(lo, hi, d);
     __syncthreads();
-    // exclusive scan in [digit][thread] order: thread t owns entries [16t, 16t + 16)
-    uint32_t loc[16];
+    // exclusive scan in [digit][thread] order: thread t owns entries [16t, 16t + 16), read and
+    // written as two 16-byte vectors (scalar 2-byte accesses at a 32-byte lane stride conflict)
+    uint4* cv = reinterpret_cast<uint4*>(cnt) + 2 * t;
+    const uint4 c0 = cv[0], c1 = cv[1];
+    const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    uint32_t o[8];
     uint32_t s = 0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      loc[q] = s;
-      s += cnt[16 * t + q];
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t a = w[e] & 0xffffu, b = w[e] >> 16;
+      o[e] = s | ((s + a) << 16);
+      s += a + b;
     }
     uint32_t tot;
     const uint32_t pre = ps_block_scan(s, ws, &tot);
+    const uint32_t pre2 = pre | (pre << 16);  // offsets < 2^14 + 2^14: the halves never carry
 #pragma unroll
-    for (int q = 0; q < 16; ++q) cnt[16 * t + q] = (uint16_t)(pre + loc[q]);
+    for (int e = 0; e < 8; ++e) o[e] += pre2;
+    cv[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    cv[1] = make_uint4(o[4], o[5], o[6], o[7]);
     __syncthreads();
     uint64_t slo = 0, shi = 0;
 #pragma unroll
@@ -121,10 +171,28 @@ __global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const int64_t
       sval[pos] = (uint16_t)v[q];
     }
     __syncthreads();
+    {  // reload this thread's 16 consecutive items as 16-byte vectors (a scalar reload at a 64-byte
+       // lane stride is a 16-way bank conflict per item)
+      const uint4* kp = reinterpret_cast<const uint4*>(skey + t * kPsItems);
+      const uint4* vp = reinterpret_cast<const uint4*>(sval + t * kPsItems);
 #pragma unroll
-    for (int q = 0; q < kPsItems; ++q) {
-      k[q] = skey[t * kPsItems + q];
-      v[q] = sval[t * kPsItems + q];
+      for (int e = 0; e < 4; ++e) {
+        const uint4 u = kp[e];
+        k[4 * e] = u.x;
+        k[4 * e + 1] = u.y;
+        k[4 * e + 2] = u.z;
+        k[4 * e + 3] = u.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const uint4 u = vp[e];
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          v[8 * e + 2 * h] = w[h] & 0xffffu;
+          v[8 * e + 2 * h + 1] = w[h] >> 16;
+        }
+      }
     }
     __syncthreads();
   }
@@ -195,18 +263,19 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
   }
 }
 
-void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, int col_bits, uint64_t route_mult,
-                 uint64_t route_n, int32_t* ws, int64_t* ukey, int64_t* uniq, int64_t* inv, int32_t* members,
-                 int32_t* memrow, int64_t* counts, hipStream_t s) {
+void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
+                 uint64_t route_mult, uint64_t route_n, int32_t* ws, int64_t* ukey, int64_t* uniq, int64_t* inv,
+                 int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s) {
   if (B < 1 || B > kPsMax) throw std::runtime_error("plan_sorted: 1 <= B <= 16384 rows per column");
   if (F < 1 || F > 64) throw std::runtime_error("plan_sorted: 1 <= F <= 64 columns");
-  if (col_bits < 1 || col_bits > 32) throw std::runtime_error("plan_sorted: column key range must be 1..32 bits");
   if (route_mult && !route_n) throw std::runtime_error("plan_sorted: routing needs the row count");
   const int64_t n = (int64_t)B * F;
   int32_t* sorted_b = ws;
   int32_t* local_u = ws + n;
   int32_t* ucount = ws + 2 * n;
-  hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, keys, B, F, col_base, col_bits, sorted_b, local_u,
+  uint32_t* krel = reinterpret_cast<uint32_t*>(ws + ((2 * n + F + 3) & ~int64_t(3)));  // 16-byte aligned
+  hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, krel);
+  hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u,
                      ukey, ucount);
   hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
                      route_mult, route_n, uniq, inv, members, memrow, counts);

@@ -209,15 +209,19 @@ def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1, rou
     return out, inv, counts, torch.tensor([u.numel()], dtype=torch.int64)
 
 
-def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0):
+def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None):
     """Key planning of a [B, F] batch whose columns hold disjoint key ranges (column f's keys in
-    [col_base[f], col_base[f] + 2**col_bits)): per-column radix sort, no atomics (plan.hip).
+    [col_base[f], col_base[f] + 2**col_bits[f])): per-column radix sort, no atomics (plan.hip).
+    ``col_bits``: a list of ints (or one int for every column).
     Returns (uniq [n] (first U valid, routed, column-major then ascending), inv [n], counts [1],
     U_dev [1], members [n] int32, memrow [n] int32) -- the unique_bucketize_n outputs for one owner
     plus the lookup CSR of emb_build_csr."""
     if _gpu(keys):
-        return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), int(col_bits), int(route_mult),
-                                           int(route_n)))
+        bits = [int(col_bits)] * keys.shape[1] if isinstance(col_bits, int) else [int(b) for b in col_bits]
+        if bits_dev is None:  # (tables pass their cached device copy: no H2D copy per plan)
+            bits_dev = torch.tensor(bits, dtype=torch.int32, device=keys.device)
+        return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), bits_dev, bits,
+                                           int(route_mult), int(route_n)))
     B, F = keys.shape
     uniq_l, inv_l = [], []
     base = 0

@@ -564,9 +564,10 @@ class SparseTable:
         self.columns = None
         if columns is not None:
             bases, cards = columns
-            bits = max(1, max(int(c) - 1 for c in cards).bit_length())
-            if bits <= 32:
-                self.columns = (torch.as_tensor(list(bases), dtype=torch.int64, device=comm.device), bits)
+            bits = [max(1, (int(c) - 1).bit_length()) for c in cards]
+            if max(bits) <= 32:
+                self.columns = (torch.as_tensor(list(bases), dtype=torch.int64, device=comm.device), bits,
+                                torch.tensor(bits, dtype=torch.int32, device=comm.device))
         # Key -> row placement. "range": row = key (the reference's contiguous range partition).
         # "mix" (default): row = key * A mod num_rows, a bijection (A prime, coprime to num_rows),
         # then the same equal ranges: contiguous key blocks (a big feature of a concatenated
@@ -648,7 +649,7 @@ class SparseTable:
         fused = want_csr and _CSR_FUSED
         n = flat.numel()
         zeroed = None
-        cols = self.columns
+        cols = getattr(self, "columns", None)  # (HashSparseTable has no column ranges)
         if (cols is not None and _SORT_PLAN and flat.is_cuda and self.comm.world == 1 and keys.dim() == 2
                 and keys.shape[0] <= 16384 and keys.shape[1] == cols[0].numel()):
             # disjoint column key ranges on one rank: atomic-free per-column sort (ops.plan_sorted),
@@ -656,7 +657,7 @@ class SparseTable:
             pp.flat = flat
             uniq, inv, counts, U_dev, members, memrow = ops.plan_sorted(
                 keys if keys.dtype == torch.int64 else keys.to(torch.int64), cols[0], cols[1], rmult,
-                self.num_rows if rmult else 0)
+                self.num_rows if rmult else 0, bits_dev=cols[2])
             pp.uniq, pp.inv, pp.counts, pp.U_dev = uniq, inv, counts, U_dev
             pp.csr = (members, memrow) if want_csr else None
             pp.host = pp.event = pp.cev = None
