@@ -55,8 +55,19 @@ def main(n=int(os.environ.get("STEPS", "300"))):
         model.train_step(d, k, y)
 
     fixed = _time(step, n)
+    # the same ring, plus the planning stream's work of a real step (next batch generated and
+    # planned, result discarded): isolates its interference from the feeder's hand-over
+    ps = comm.plan_stream()
+
+    def step_plus_planning():
+        with torch.cuda.stream(ps):
+            k = data.next()[1]
+        model.emb.plan_async(k, csr=True, keys_on_plan_stream=True)
+        step()
+
+    both = _time(step_plus_planning, n)
     print(f"feeder step {full:.4f} ms | pre-planned ring of {len(ring)} batches {fixed:.4f} ms | data + planning "
-          f"cost {full - fixed:.4f} ms/step")
+          f"cost {full - fixed:.4f} ms/step | ring + discarded planning {both:.4f} ms")
 
 
 if __name__ == "__main__":
