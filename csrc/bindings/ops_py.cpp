@@ -405,7 +405,12 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
 // Sort-based planning of a [B, F] batch with disjoint column key ranges (see kernels.h).
 // Returns (uniq, inv, counts [1], U_dev [1], members, memrow).
 std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& col_base, const at::Tensor& col_bits,
-                                    std::vector<int64_t> col_bits_host, int64_t route_mult, int64_t route_n) {
+                                    std::vector<int64_t> col_bits_host, int64_t route_mult, int64_t route_n,
+                                    const at::Tensor& bounds) {
+  check_gpu(bounds, "bounds");
+  check_dtype(bounds, at::kLong, "bounds");
+  const int64_t P = bounds.numel() - 1;
+  TORCH_CHECK(P >= 1 && P <= 16, "plan_sorted: 1..16 owners");
   check_gpu(keys, "keys");
   check_dtype(keys, at::kLong, "keys");
   check_gpu(col_base, "col_base");
@@ -421,16 +426,18 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
   for (int64_t b : col_bits_host) TORCH_CHECK(b >= 1 && b <= 32, "col_bits: 1..32");
   const int64_t n = B * F;
   auto o64 = keys.options();
-  auto ws = at::empty({3 * n + F + 4}, o64.dtype(at::kInt));  // sorted_b | local_u | ucount | column-major keys
+  const int64_t nchunks = (n + 1023) / 1024;
+  auto ws = at::empty({4 * n + F + 4 + 2 * nchunks * P}, o64.dtype(at::kInt));  // see kernels.h
   auto ukey = at::empty({n}, o64), uniq = at::empty({n}, o64), inv = at::empty({n}, o64);
   auto members = at::empty({n}, o64.dtype(at::kInt)), memrow = at::empty({n}, o64.dtype(at::kInt));
-  auto counts = at::empty({2}, o64);
+  auto counts = at::empty({P + 1}, o64);
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), col_bits.data_ptr<int32_t>(),
-                        (uint64_t)route_mult, (uint64_t)route_n, ws.data_ptr<int32_t>(), ptr<int64_t>(ukey),
+                        (uint64_t)route_mult, (uint64_t)route_n, ptr<int64_t>(bounds), (int)P, ws.data_ptr<int32_t>(),
+                        ptr<int64_t>(ukey),
                         ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
                         ptr<int64_t>(counts), stream_of(keys));
-  return {uniq, inv, counts.narrow(0, 0, 1), counts.narrow(0, 1, 1), members, memrow};
+  return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow};
 }
 
 // A HIP stream whose kernels may only use the CUs set in `mask` (hipExtStreamCreateWithCUMask;

@@ -125,11 +125,12 @@ void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const i
                           float* grad_rows, int row_stride, hipStream_t s);
 // Sort-based key planning of a [B, F] batch with disjoint column key ranges (plan.hip): keys of
 // column f lie in [col_base[f], col_base[f] + 2^col_bits[f]), 1 <= col_bits[f] <= 32 (device
-// arrays). One owner. ws: int32 [3*B*F + F], ukey: int64 [B*F]. Outputs: uniq [B*F] (first U
-// valid, routed), inv [B*F], the lookup CSR members/memrow [B*F] int32, counts [2] = {U, U}.
+// arrays); P owners with routed-key bounds [P+1] (1 <= P <= 16). ws: int32 [4*B*F + F + 4 +
+// 2*ceil(B*F/1024)*P], ukey: int64 [B*F]. Outputs: uniq [B*F] (first U valid, routed, grouped
+// by owner), inv [B*F], the lookup CSR members/memrow [B*F] int32, counts [P+1] = {per owner, U}.
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
-                 uint64_t route_mult, uint64_t route_n, int32_t* ws, int64_t* ukey, int64_t* uniq, int64_t* inv,
-                 int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s);
+                 uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
+                 int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s);
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
 void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s);
 // Embedding backward fused with the row-wise Adagrad apply (one rank, local shard): the rows of

@@ -18,8 +18,10 @@
 //                  uniq[u] (routed key), inv[b*F + f] = u, and the embedding backward's CSR for
 //                  free -- members (lookup ids grouped by u, ascending) and memrow (their u).
 //
-// Deterministic (no atomics, stable sort); unique keys come out column-major, ascending inside a
-// column; one owner (a one-rank table: counts[0] = U).
+// Deterministic (no global atomics, stable sort); unique keys come out column-major, ascending
+// inside a column; with several owners (P > 1, a multi-rank table) they are then regrouped by
+// owner shard (plan_owner_*: stable counting sort over chunks), inv/memrow pointing at the
+// regrouped positions.
 #include <stdexcept>
 
 #include "common.h"
@@ -225,15 +227,9 @@ __device__ __forceinline__ int64_t ps_route(int64_t key, uint64_t mult, uint64_t
   return mult ? (int64_t)(((uint64_t)key * mult) % rn) : key;
 }
 
-__global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int32_t* __restrict__ sorted_b,
-                                                        const int32_t* __restrict__ local_u,
-                                                        const int64_t* __restrict__ ukey,
-                                                        const int32_t* __restrict__ ucount, uint64_t rmult,
-                                                        uint64_t rn, int64_t* __restrict__ uniq,
-                                                        int64_t* __restrict__ inv, int32_t* __restrict__ members,
-                                                        int32_t* __restrict__ memrow, int64_t* __restrict__ counts) {
-  __shared__ int64_t basef[65];
-  __shared__ int32_t ucf[64];
+// column prefix of the unique counts (F <= 64), computed per block; returns U
+__device__ __forceinline__ int64_t ps_col_prefix(const int32_t* __restrict__ ucount, int F, int64_t* basef,
+                                                 int32_t* ucf) {
   const int t = threadIdx.x;
   if (t < F) ucf[t] = ucount[t];
   __syncthreads();
@@ -244,41 +240,240 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
       acc += ucf[c];
     }
     basef[F] = acc;
-    if (blockIdx.x == 0) {
-      counts[0] = acc;  // one owner: counts[0] = U
-      counts[1] = acc;  // the device-side U
-    }
   }
   __syncthreads();
+  return basef[F];
+}
+
+__device__ __forceinline__ int ps_owner(const int64_t* bounds, int P, int64_t k) {
+  int lo = 0, hi = P;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (bounds[mid] <= k) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// routed key of global unique index u (column-major: column c holds [basef[c], basef[c+1]))
+__device__ __forceinline__ int64_t ps_ukey_routed(int64_t u, int F, int B, const int64_t* basef,
+                                                  const int64_t* __restrict__ ukey, uint64_t rmult, uint64_t rn) {
+  int c = 0;
+  while (c + 1 < F && basef[c + 1] <= u) ++c;
+  return ps_route(ukey[(int64_t)c * B + (u - basef[c])], rmult, rn);
+}
+
+// ---- several owners (multi-rank tables): the unique keys are regrouped by owner shard with a
+// stable counting sort over chunks of kPoChunk unique indices -- per-chunk owner counts, one
+// scan per owner over the chunks, then each chunk places its keys (no atomics anywhere).
+constexpr int kPoChunk = 1024, kPoMaxP = 16;
+
+__global__ __launch_bounds__(256) void plan_owner_count_kernel(int B, int F, const int64_t* __restrict__ ukey,
+                                                               const int32_t* __restrict__ ucount,
+                                                               const int64_t* __restrict__ bounds, int P,
+                                                               uint64_t rmult, uint64_t rn, int32_t* __restrict__ ocnt) {
+  __shared__ int64_t basef[65];
+  __shared__ int32_t ucf[64];
+  __shared__ int64_t sb[kPoMaxP + 1];
+  __shared__ uint32_t lc[kPoMaxP];
+  const int t = threadIdx.x;
+  if (t <= P) sb[t] = bounds[t];
+  if (t < P) lc[t] = 0;
+  const int64_t U = ps_col_prefix(ucount, F, basef, ucf);
+  const int64_t u0 = (int64_t)blockIdx.x * kPoChunk;
+  for (int e = t; e < kPoChunk; e += 256) {
+    const int64_t u = u0 + e;
+    if (u < U) atomicAdd(&lc[ps_owner(sb, P, ps_ukey_routed(u, F, B, basef, ukey, rmult, rn))], 1u);
+  }
+  __syncthreads();
+  if (t < P) ocnt[(int64_t)blockIdx.x * P + t] = (int32_t)lc[t];
+}
+
+// one block: ooff[chunk][p] = (keys of owners < p) + (keys of owner p in earlier chunks);
+// counts[p] = keys of owner p, counts[P] = U
+__global__ __launch_bounds__(256) void plan_owner_scan_kernel(int nchunks, int P, const int32_t* __restrict__ ocnt,
+                                                              int32_t* __restrict__ ooff, int64_t* __restrict__ counts) {
+  __shared__ uint32_t ws[20];
+  __shared__ int64_t tot[kPoMaxP + 1];
+  const int t = threadIdx.x;
+  const int per = (nchunks + 255) / 256;
+  // pass 1: totals per owner
+  for (int p = 0; p < P; ++p) {
+    uint32_t s = 0;
+    for (int i = 0; i < per; ++i) {
+      const int c = t * per + i;
+      if (c < nchunks) s += (uint32_t)ocnt[(int64_t)c * P + p];
+    }
+    // block reduce through the scan helper of a 256-thread block: reuse warp shuffles
+    uint32_t x = s;
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if ((t & 63) == 0) ws[t >> 6] = x;
+    __syncthreads();
+    if (t == 0) tot[p] = (int64_t)ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
+  }
+  if (t == 0) {
+    int64_t acc = 0;
+    for (int p = 0; p < P; ++p) {
+      counts[p] = tot[p];
+      const int64_t c = tot[p];
+      tot[p] = acc;  // owner base
+      acc += c;
+    }
+    counts[P] = acc;
+  }
+  __syncthreads();
+  // pass 2: exclusive scan of each owner's chunk counts
+  for (int p = 0; p < P; ++p) {
+    uint32_t loc[8];
+    uint32_t s = 0;
+    for (int i = 0; i < per && i < 8; ++i) {
+      const int c = t * per + i;
+      loc[i] = s;
+      s += c < nchunks ? (uint32_t)ocnt[(int64_t)c * P + p] : 0u;
+    }
+    const int lane = t & 63, wave = t >> 6;
+    uint32_t x = s;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    uint32_t wpre = 0;
+    for (int w = 0; w < wave; ++w) wpre += ws[w];
+    const uint32_t pre = wpre + x - s;
+    for (int i = 0; i < per && i < 8; ++i) {
+      const int c = t * per + i;
+      if (c < nchunks) ooff[(int64_t)c * P + p] = (int32_t)(tot[p] + pre + loc[i]);
+    }
+    __syncthreads();
+  }
+}
+
+// place the chunk's unique keys: stable rank among the chunk's keys of the same owner
+__global__ __launch_bounds__(256) void plan_owner_perm_kernel(int B, int F, const int64_t* __restrict__ ukey,
+                                                              const int32_t* __restrict__ ucount,
+                                                              const int64_t* __restrict__ bounds, int P,
+                                                              uint64_t rmult, uint64_t rn,
+                                                              const int32_t* __restrict__ ooff,
+                                                              int32_t* __restrict__ perm, int64_t* __restrict__ uniq) {
+  __shared__ int64_t basef[65];
+  __shared__ int32_t ucf[64];
+  __shared__ int64_t sb[kPoMaxP + 1];
+  __shared__ uint32_t cnt[kPoMaxP][256];  // [owner][thread] -> exclusive offsets inside the chunk
+  __shared__ uint32_t ws[20];
+  const int t = threadIdx.x;
+  if (t <= P) sb[t] = bounds[t];
+  const int64_t U = ps_col_prefix(ucount, F, basef, ucf);
+  const int64_t u0 = (int64_t)blockIdx.x * kPoChunk + 4 * t;  // 4 consecutive unique indices per thread
+  int own[4];
+  int64_t rk[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    own[e] = -1;
+    if (u0 + e < U) {
+      rk[e] = ps_ukey_routed(u0 + e, F, B, basef, ukey, rmult, rn);
+      own[e] = ps_owner(sb, P, rk[e]);
+    }
+  }
+  for (int p = 0; p < P; ++p) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) c += own[e] == p ? 1u : 0u;
+    cnt[p][t] = c;
+  }
+  __syncthreads();
+  // exclusive scan over [owner][thread]: owner by owner (P <= 16 block scans of 256 values)
+  for (int p = 0; p < P; ++p) {
+    const uint32_t v = cnt[p][t];
+    const int lane = t & 63, wave = t >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    uint32_t wpre = 0;
+    for (int w = 0; w < wave; ++w) wpre += ws[w];
+    cnt[p][t] = wpre + x - v;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (own[e] < 0) continue;
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < e && own[q] == own[e]) ++r;
+    const int64_t pos = (int64_t)ooff[(int64_t)blockIdx.x * P + own[e]] + cnt[own[e]][t] + r;
+    perm[u0 + e] = (int32_t)pos;
+    uniq[pos] = rk[e];
+  }
+}
+
+__global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int32_t* __restrict__ sorted_b,
+                                                        const int32_t* __restrict__ local_u,
+                                                        const int64_t* __restrict__ ukey,
+                                                        const int32_t* __restrict__ ucount, uint64_t rmult,
+                                                        uint64_t rn, const int32_t* __restrict__ perm,
+                                                        int64_t* __restrict__ uniq, int64_t* __restrict__ inv,
+                                                        int32_t* __restrict__ members, int32_t* __restrict__ memrow,
+                                                        int64_t* __restrict__ counts) {
+  __shared__ int64_t basef[65];
+  __shared__ int32_t ucf[64];
+  const int t = threadIdx.x;
+  const int64_t U = ps_col_prefix(ucount, F, basef, ucf);
+  if (!perm && blockIdx.x == 0 && t == 0) {
+    counts[0] = U;  // one owner: counts[0] = U
+    counts[1] = U;  // the device-side U
+  }
   const int64_t n = (int64_t)B * F;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + t; idx < n; idx += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(idx / B);
     const int pos = (int)(idx - (int64_t)c * B);
-    const int64_t u = basef[c] + local_u[idx];
+    int64_t u = basef[c] + local_u[idx];
+    if (perm) u = perm[u];  // owner-grouped position
     const int64_t j = (int64_t)sorted_b[idx] * F + c;
     inv[j] = u;
     members[idx] = (int32_t)j;
     memrow[idx] = (int32_t)u;
-    if (pos < ucf[c]) uniq[basef[c] + pos] = ps_route(ukey[idx], rmult, rn);
+    if (!perm && pos < ucf[c]) uniq[basef[c] + pos] = ps_route(ukey[idx], rmult, rn);
   }
 }
 
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
-                 uint64_t route_mult, uint64_t route_n, int32_t* ws, int64_t* ukey, int64_t* uniq, int64_t* inv,
-                 int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s) {
+                 uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
+                 int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s) {
   if (B < 1 || B > kPsMax) throw std::runtime_error("plan_sorted: 1 <= B <= 16384 rows per column");
   if (F < 1 || F > 64) throw std::runtime_error("plan_sorted: 1 <= F <= 64 columns");
+  if (P < 1 || P > kPoMaxP) throw std::runtime_error("plan_sorted: 1 <= P <= 16 owners");
   if (route_mult && !route_n) throw std::runtime_error("plan_sorted: routing needs the row count");
   const int64_t n = (int64_t)B * F;
+  // ws: sorted_b [n] | local_u [n] | ucount [F] | (16-byte aligned) column-major keys [n] | perm [n] |
+  //     owner counts / offsets [2 * nchunks * P]
   int32_t* sorted_b = ws;
   int32_t* local_u = ws + n;
   int32_t* ucount = ws + 2 * n;
-  uint32_t* krel = reinterpret_cast<uint32_t*>(ws + ((2 * n + F + 3) & ~int64_t(3)));  // 16-byte aligned
+  const int64_t kofs = (2 * n + F + 3) & ~int64_t(3);
+  uint32_t* krel = reinterpret_cast<uint32_t*>(ws + kofs);  // 16-byte aligned
+  int32_t* perm = ws + kofs + n;
+  const int nchunks = (int)((n + kPoChunk - 1) / kPoChunk);
+  int32_t* ocnt = perm + n;
+  int32_t* ooff = ocnt + (int64_t)nchunks * P;
   hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, krel);
   hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u,
                      ukey, ucount);
+  if (P > 1) {
+    hipLaunchKernelGGL(plan_owner_count_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
+                       route_n, ocnt);
+    hipLaunchKernelGGL(plan_owner_scan_kernel, 1, 256, 0, s, nchunks, P, ocnt, ooff, counts);
+    hipLaunchKernelGGL(plan_owner_perm_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
+                       route_n, ooff, perm, uniq);
+  }
   hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
-                     route_mult, route_n, uniq, inv, members, memrow, counts);
+                     route_mult, route_n, P > 1 ? perm : nullptr, uniq, inv, members, memrow, counts);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -209,19 +209,22 @@ def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1, rou
     return out, inv, counts, torch.tensor([u.numel()], dtype=torch.int64)
 
 
-def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None):
+def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None, bounds=None):
     """Key planning of a [B, F] batch whose columns hold disjoint key ranges (column f's keys in
-    [col_base[f], col_base[f] + 2**col_bits[f])): per-column radix sort, no atomics (plan.hip).
-    ``col_bits``: a list of ints (or one int for every column).
-    Returns (uniq [n] (first U valid, routed, column-major then ascending), inv [n], counts [1],
-    U_dev [1], members [n] int32, memrow [n] int32) -- the unique_bucketize_n outputs for one owner
-    plus the lookup CSR of emb_build_csr."""
+    [col_base[f], col_base[f] + 2**col_bits[f])): per-column radix sort, no global atomics
+    (plan.hip). ``col_bits``: a list of ints (or one int for every column); ``bounds`` [P+1]: the
+    owners' routed-key ranges (None: one owner). Returns (uniq [n] (first U valid, routed; column-
+    major, ascending inside a column, then stably grouped by owner), inv [n], counts [P], U_dev [1],
+    members [n] int32, memrow [n] int32) -- the unique_bucketize_n outputs plus the lookup CSR of
+    emb_build_csr (rows contiguous, in column-major key order)."""
+    if bounds is None:
+        bounds = torch.tensor([0, (1 << 62)], dtype=torch.int64, device=keys.device)
     if _gpu(keys):
         bits = [int(col_bits)] * keys.shape[1] if isinstance(col_bits, int) else [int(b) for b in col_bits]
         if bits_dev is None:  # (tables pass their cached device copy: no H2D copy per plan)
             bits_dev = torch.tensor(bits, dtype=torch.int32, device=keys.device)
         return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), bits_dev, bits,
-                                           int(route_mult), int(route_n)))
+                                           int(route_mult), int(route_n), bounds.contiguous()))
     B, F = keys.shape
     uniq_l, inv_l = [], []
     base = 0
@@ -234,12 +237,18 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
     uniq = torch.cat(uniq_l)
     if route_mult:
         uniq = (uniq * route_mult) % route_n
+    P = bounds.numel() - 1
+    owner = torch.bucketize(uniq, bounds[1:-1], right=True)
+    perm_order = torch.sort(owner, stable=True).indices      # regrouped position -> u
+    perm = torch.empty(U, dtype=torch.int64)
+    perm[perm_order] = torch.arange(U)                         # u -> regrouped position
     out = torch.empty(B * F, dtype=torch.int64)
-    out[:U] = uniq
-    inv = torch.stack(inv_l, 1).reshape(-1)
-    order = torch.sort(inv, stable=True).indices
-    cnt = torch.tensor([U], dtype=torch.int64)
-    return out, inv, cnt, cnt.clone(), order.to(torch.int32), inv[order].to(torch.int32)
+    out[:U] = uniq[perm_order]
+    inv_u = torch.stack(inv_l, 1).reshape(-1)                  # column-major u of each lookup
+    order = torch.sort(inv_u, stable=True).indices             # lookups grouped by u (ascending)
+    counts = torch.bincount(owner, minlength=P).to(torch.int64)
+    return (out, perm[inv_u], counts, torch.tensor([U], dtype=torch.int64), order.to(torch.int32),
+            perm[inv_u[order]].to(torch.int32))
 
 
 def gather_rows(table, keys, base, out, n_dev=None):

@@ -650,18 +650,20 @@ class SparseTable:
         n = flat.numel()
         zeroed = None
         cols = getattr(self, "columns", None)  # (HashSparseTable has no column ranges)
-        if (cols is not None and _SORT_PLAN and flat.is_cuda and self.comm.world == 1 and keys.dim() == 2
+        if (cols is not None and _SORT_PLAN and flat.is_cuda and self.comm.world <= 16 and keys.dim() == 2
                 and keys.shape[0] <= 16384 and keys.shape[1] == cols[0].numel()):
-            # disjoint column key ranges on one rank: atomic-free per-column sort (ops.plan_sorted),
-            # which also yields the embedding backward's lookup CSR
+            # disjoint column key ranges: atomic-free per-column sort (ops.plan_sorted), unique keys
+            # regrouped by owner, and the embedding backward's lookup CSR on the way
             pp.flat = flat
             uniq, inv, counts, U_dev, members, memrow = ops.plan_sorted(
                 keys if keys.dtype == torch.int64 else keys.to(torch.int64), cols[0], cols[1], rmult,
-                self.num_rows if rmult else 0, bits_dev=cols[2])
+                self.num_rows if rmult else 0, bits_dev=cols[2], bounds=self.bounds)
             pp.uniq, pp.inv, pp.counts, pp.U_dev = uniq, inv, counts, U_dev
             pp.csr = (members, memrow) if want_csr else None
             pp.host = pp.event = pp.cev = None
-            pp.exchanged = True
+            pp.exchanged = self.comm.world == 1
+            if exchange:
+                self._exchange_counts(pp)
             return pp
         if rmult:  # range tables: the routing is fused into the dedupe kernel
             pp.flat = flat

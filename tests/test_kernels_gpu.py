@@ -442,12 +442,14 @@ def test_colsum_bf16(dev):
         torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("B,cards", [(16384, [3, 1460, 10131227, 583, 24, 2202608]), (1000, [5, 70000]),
-                                     (16384, [1 << 24])])
-def test_plan_sorted_matches_reference(dev, B, cards):
-    """Atomic-free sort-based planning (plan.hip) vs the fp32-free CPU reference: same unique keys
-    (column-major, ascending), uniq[inv] == routed keys, and the lookup CSR grouped by row."""
-    g = torch.Generator().manual_seed(B + len(cards))
+@pytest.mark.parametrize("B,cards,P", [(16384, [3, 1460, 10131227, 583, 24, 2202608], 1),
+                                       (16384, [3, 1460, 10131227, 583, 24, 2202608], 8), (1000, [5, 70000], 3),
+                                       (16384, [1 << 24], 1)])
+def test_plan_sorted_matches_reference(dev, B, cards, P):
+    """Atomic-free sort-based planning (plan.hip) vs the CPU reference of the same op: unique keys
+    column-major / ascending, stably regrouped by owner for P > 1 owners; uniq[inv] == routed
+    keys; the lookup CSR with contiguous rows; per-owner counts."""
+    g = torch.Generator().manual_seed(B + len(cards) + P)
     bases = [sum(cards[:f]) for f in range(len(cards))]
     cols = []
     for c, base in zip(cards, bases):
@@ -456,14 +458,17 @@ def test_plan_sorted_matches_reference(dev, B, cards):
     keys = torch.stack(cols, 1)
     R = sum(cards)
     mult = 402653189 if R % 402653189 else 201326611
-    bits = max(1, max(c - 1 for c in cards).bit_length())
-    ref = ops.plan_sorted(keys, torch.tensor(bases), bits, mult, R)
-    got = [t.cpu() for t in ops.plan_sorted(keys.to(dev), torch.tensor(bases, device=dev), bits, mult, R)]
+    bits = [max(1, (c - 1).bit_length()) for c in cards]
+    bounds = torch.tensor([R * p // P for p in range(P + 1)], dtype=torch.int64)
+    ref = ops.plan_sorted(keys, torch.tensor(bases), bits, mult, R, bounds=bounds)
+    got = [t.cpu() for t in ops.plan_sorted(keys.to(dev), torch.tensor(bases, device=dev), bits, mult, R,
+                                            bounds=bounds.to(dev))]
     U = int(ref[3])
-    assert int(got[3]) == U == int(got[2])
-    torch.testing.assert_close(got[0][:U], ref[0][:U])
+    assert int(got[3]) == U and int(got[2].sum()) == U
+    torch.testing.assert_close(got[2], ref[2])                      # per-owner counts
+    torch.testing.assert_close(got[0][:U], ref[0][:U])              # grouped by owner
     torch.testing.assert_close(got[1], ref[1])
     torch.testing.assert_close(got[0][got[1]], (keys.reshape(-1) * mult) % R)
-    torch.testing.assert_close(got[5], ref[5])                      # memrow: rows ascending
+    torch.testing.assert_close(got[4], ref[4])
+    torch.testing.assert_close(got[5], ref[5])
     assert bool((got[1][got[4].long()] == got[5].long()).all())      # members belong to their row
-    assert sorted(got[4].tolist()) == list(range(B * len(cards)))
