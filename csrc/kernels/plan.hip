@@ -271,7 +271,8 @@ constexpr int kPoChunk = 1024, kPoMaxP = 16;
 __global__ __launch_bounds__(256) void plan_owner_count_kernel(int B, int F, const int64_t* __restrict__ ukey,
                                                                const int32_t* __restrict__ ucount,
                                                                const int64_t* __restrict__ bounds, int P,
-                                                               uint64_t rmult, uint64_t rn, int32_t* __restrict__ ocnt) {
+                                                               uint64_t rmult, uint64_t rn,
+                                                               int32_t* __restrict__ ocnt) {
   __shared__ int64_t basef[65];
   __shared__ int32_t ucf[64];
   __shared__ int64_t sb[kPoMaxP + 1];
@@ -292,7 +293,8 @@ __global__ __launch_bounds__(256) void plan_owner_count_kernel(int B, int F, con
 // one block: ooff[chunk][p] = (keys of owners < p) + (keys of owner p in earlier chunks);
 // counts[p] = keys of owner p, counts[P] = U
 __global__ __launch_bounds__(256) void plan_owner_scan_kernel(int nchunks, int P, const int32_t* __restrict__ ocnt,
-                                                              int32_t* __restrict__ ooff, int64_t* __restrict__ counts) {
+                                                              int32_t* __restrict__ ooff,
+                                                              int64_t* __restrict__ counts) {
   __shared__ uint32_t ws[20];
   __shared__ int64_t tot[kPoMaxP + 1];
   const int t = threadIdx.x;
