@@ -66,8 +66,16 @@ def main(n=int(os.environ.get("STEPS", "300"))):
         step()
 
     both = _time(step_plus_planning, n)
+
+    def step_plus_data():
+        with torch.cuda.stream(ps):
+            data.next()
+        step()
+
+    data_only = _time(step_plus_data, n)
     print(f"feeder step {full:.4f} ms | pre-planned ring of {len(ring)} batches {fixed:.4f} ms | data + planning "
-          f"cost {full - fixed:.4f} ms/step | ring + discarded planning {both:.4f} ms")
+          f"cost {full - fixed:.4f} ms/step | ring + discarded planning {both:.4f} ms | ring + discarded batch "
+          f"generation only {data_only:.4f} ms")
 
 
 if __name__ == "__main__":
