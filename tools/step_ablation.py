@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def _time(fn, n):
-    for _ in range(10):
+    for _ in range(40):
         fn()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
