@@ -22,6 +22,8 @@
 // inside a column; with several owners (P > 1, a multi-rank table) they are then regrouped by
 // owner shard (plan_owner_*: stable counting sort over chunks), inv/memrow pointing at the
 // regrouped positions.
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "common.h"
@@ -445,6 +447,20 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
   }
 }
 
+// timing experiments (idempotent re-runs): MINIPS_PLAN_REPEAT=k repeats the kernels selected by
+// MINIPS_PLAN_REPEAT_WHICH (bit 0 transpose, 1 sort, 2 emit) k times
+static int plan_reps(int bit) {
+  static const int reps = [] {
+    const char* e = std::getenv("MINIPS_PLAN_REPEAT");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  static const int which = [] {
+    const char* e = std::getenv("MINIPS_PLAN_REPEAT_WHICH");
+    return e ? std::atoi(e) : 7;
+  }();
+  return (which & bit) ? reps : 1;
+}
+
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s) {
@@ -464,9 +480,11 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
   const int nchunks = (int)((n + kPoChunk - 1) / kPoChunk);
   int32_t* ocnt = perm + n;
   int32_t* ooff = ocnt + (int64_t)nchunks * P;
-  hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, krel);
-  hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u,
-                     ukey, ucount);
+  for (int r = 0; r < plan_reps(1); ++r)
+    hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, krel);
+  for (int r = 0; r < plan_reps(2); ++r)
+    hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u,
+                       ukey, ucount);
   if (P > 1) {
     hipLaunchKernelGGL(plan_owner_count_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
                        route_n, ocnt);
@@ -474,8 +492,9 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
     hipLaunchKernelGGL(plan_owner_perm_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
                        route_n, ooff, perm, uniq);
   }
-  hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
-                     route_mult, route_n, P > 1 ? perm : nullptr, uniq, inv, members, memrow, counts);
+  for (int r = 0; r < plan_reps(4); ++r)
+    hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
+                       route_mult, route_n, P > 1 ? perm : nullptr, uniq, inv, members, memrow, counts);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

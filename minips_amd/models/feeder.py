@@ -24,12 +24,24 @@ def default_depth(world: int) -> int:
 
 
 class LookaheadFeeder:
-    def __init__(self, model, data, comm, depth: int | None = None):
+    """``fence`` (default: MINIPS_FEED_FENCE, on): after each step the planning stream waits for
+    the compute stream (one event per step). Everything the planning stream hands to a step --
+    the batch and its key plan -- is then safe to recycle from the planning stream once the step
+    is issued, so neither needs ``record_stream`` (an allocator event per tensor on the compute
+    stream when it is freed: ~30 us per W&D step for the ~10 tensors). The planning work of later
+    batches is issued after the fence anyway, so no overlap is lost."""
+
+    def __init__(self, model, data, comm, depth: int | None = None, fence: bool | None = None):
         self.model, self.data, self.comm = model, data, comm
         self.cuda = comm.device.type == "cuda"
         self.plan_stream = comm.plan_stream() if self.cuda else None
         self.main = torch.cuda.current_stream(comm.device) if self.cuda else None
         self.depth = depth or default_depth(comm.world)
+        if fence is None:
+            fence = os.environ.get("MINIPS_FEED_FENCE", "1") != "0"
+        self.fence = bool(fence and self.cuda)
+        if self.fence:
+            model._fenced = True
         self.queue = collections.deque(self._produce() for _ in range(self.depth))
         for (_, k, _), _ev in list(self.queue)[1:]:
             model.prefetch(k, keys_on_plan_stream=self.cuda)
@@ -41,8 +53,9 @@ class LookaheadFeeder:
             b = self.data.next()
             ev = torch.cuda.Event()
             ev.record(self.plan_stream)
-        for t in b:
-            t.record_stream(self.main)
+        if not self.fence:
+            for t in b:
+                t.record_stream(self.main)
         return b, ev
 
     def step(self):
@@ -54,7 +67,12 @@ class LookaheadFeeder:
             self.queue.append(self._produce())
             return self.queue[-1][0][1]
 
-        return self.model.train_step(dense, keys, labels, next_keys=next_keys, next_on_plan_stream=self.cuda)
+        loss = self.model.train_step(dense, keys, labels, next_keys=next_keys, next_on_plan_stream=self.cuda)
+        if self.fence:  # the planning stream's later work (and buffer reuse) follows this step
+            ev = torch.cuda.Event()
+            ev.record(self.main)
+            self.plan_stream.wait_event(ev)
+        return loss
 
 
 class LookaheadPlans:
@@ -74,9 +92,12 @@ class LookaheadPlans:
 
     def prefetch(self, keys, keys_on_plan_stream: bool = False):
         """Start routing a future batch's keys on the planning stream; train_step picks the
-        plan up when that batch comes (a batch may be several steps ahead: data-loader depth)."""
+        plan up when that batch comes (a batch may be several steps ahead: data-loader depth).
+        A model driven by a fencing LookaheadFeeder (``_fenced``) skips the per-tensor stream
+        bookkeeping of the plan (SparseTable.plan_async ``fenced``)."""
         pend = self.__dict__.setdefault("_pending_plans", [])
-        pend.append([keys, self.emb.plan_async(keys, csr=True, keys_on_plan_stream=keys_on_plan_stream)])
+        pend.append([keys, self.emb.plan_async(keys, csr=True, keys_on_plan_stream=keys_on_plan_stream,
+                                               fenced=self.__dict__.get("_fenced", False))])
 
     def _take_plan(self, keys):
         pend = self.__dict__.setdefault("_pending_plans", [])

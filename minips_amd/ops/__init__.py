@@ -209,6 +209,9 @@ def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1, rou
     return out, inv, counts, torch.tensor([u.numel()], dtype=torch.int64)
 
 
+_PLAN_BITS_CAP = int(__import__("os").environ.get("MINIPS_PLAN_BITS_CAP", "0"))
+
+
 def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None, bounds=None):
     """Key planning of a [B, F] batch whose columns hold disjoint key ranges (column f's keys in
     [col_base[f], col_base[f] + 2**col_bits[f])): per-column radix sort, no global atomics
@@ -221,6 +224,9 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
         bounds = torch.tensor([0, (1 << 62)], dtype=torch.int64, device=keys.device)
     if _gpu(keys):
         bits = [int(col_bits)] * keys.shape[1] if isinstance(col_bits, int) else [int(b) for b in col_bits]
+        if _PLAN_BITS_CAP:  # timing experiment only: fewer radix passes, WRONG dedupe (in-range keys)
+            bits = [min(b, _PLAN_BITS_CAP) for b in bits]
+            bits_dev = None
         if bits_dev is None:  # (tables pass their cached device copy: no H2D copy per plan)
             bits_dev = torch.tensor(bits, dtype=torch.int32, device=keys.device)
         return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), bits_dev, bits,

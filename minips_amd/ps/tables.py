@@ -700,14 +700,22 @@ class SparseTable:
         else:
             pp.host = both
 
-    def plan_async(self, keys: torch.Tensor, csr: bool = False, keys_on_plan_stream: bool = False):
+    def plan_async(self, keys: torch.Tensor, csr: bool = False, keys_on_plan_stream: bool = False,
+                   fenced: bool = False):
         """Lookahead: start planning ``keys`` (a LATER batch) on the planning stream, so its
         dedupe, count exchange (and lookup CSR) overlap the current step; pass the result to
         get(plan=...). Planning reads no table state, so issuing it early changes no
         consistency semantics. ``keys_on_plan_stream``: the keys were produced on the planning
         stream itself (a data producer running there), so planning need not wait for the
         compute stream at all. On the CPU the same two halves run at the same issue points
-        (inline), so a gloo run issues exactly the collective sequence of an RCCL run."""
+        (inline), so a gloo run issues exactly the collective sequence of an RCCL run.
+
+        ``fenced``: the caller orders the planning stream after each step's compute-stream work
+        (LookaheadFeeder's end-of-step fence), so the plan's buffers -- allocated on the planning
+        stream and read on the compute stream -- need no per-tensor ``record_stream``: each
+        record_stream costs an allocator event on the compute stream when the tensor is freed,
+        and those events cost the W&D step ~30 us (tools/step_ablation.py). Only valid while the
+        plan is consumed inside the fenced step (one rank, synchronous clocks)."""
         if self._exact_counts:
             return self.plan(keys, csr)
         if self.comm.device.type != "cuda":
@@ -720,6 +728,8 @@ class SparseTable:
             pp = self._start_plan(keys, csr, exchange=False)
             pp.event = torch.cuda.Event()
             pp.event.record(ps)
+        if fenced and self.comm.world == 1 and not self.pipe.async_:
+            return pp
         keys.record_stream(ps)
         for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev, *(pp.csr or ())):
             t.record_stream(cur)  # produced on the planning stream, consumed on the compute stream

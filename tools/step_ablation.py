@@ -73,9 +73,41 @@ def main(n=int(os.environ.get("STEPS", "300"))):
         step()
 
     data_only = _time(step_plus_data, n)
+
+    def step_then_planning():
+        step()
+        with torch.cuda.stream(ps):
+            k = data.next()[1]
+        model.emb.plan_async(k, csr=True, keys_on_plan_stream=True)
+
+    after = _time(step_then_planning, n)
+    import time as _t
+
+    def host_plan_cost():  # host time of issuing one batch generation + plan (GPU idle-ish)
+        torch.cuda.synchronize()
+        t0 = _t.perf_counter()
+        for _ in range(50):
+            with torch.cuda.stream(ps):
+                k = data.next()[1]
+            model.emb.plan_async(k, csr=True, keys_on_plan_stream=True)
+        t1 = _t.perf_counter()
+        torch.cuda.synchronize()
+        return (t1 - t0) / 50 * 1e3
+
+    host_ms = host_plan_cost()
+
+    def step_plus_bare_planning():  # the same kernels without plan_async's stream bookkeeping
+        with torch.cuda.stream(ps):
+            k = data.next()[1]
+            model.emb._start_plan(k, csr=True, exchange=False)
+        step()
+
+    bare = _time(step_plus_bare_planning, n)
     print(f"feeder step {full:.4f} ms | pre-planned ring of {len(ring)} batches {fixed:.4f} ms | data + planning "
           f"cost {full - fixed:.4f} ms/step | ring + discarded planning {both:.4f} ms | ring + discarded batch "
-          f"generation only {data_only:.4f} ms")
+          f"generation only {data_only:.4f} ms | planning issued after the step {after:.4f} ms | host issue of "
+          f"one batch + plan {host_ms:.4f} ms | ring + planning kernels without record_stream/events "
+          f"{bare:.4f} ms")
 
 
 if __name__ == "__main__":
