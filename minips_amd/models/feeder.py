@@ -60,7 +60,11 @@ class LookaheadFeeder:
 
     def step(self):
         (dense, keys, labels), ev = self.queue.popleft()
-        if ev is not None:
+        # the batch was generated on the planning stream before its key plan: a step whose plan
+        # was prefetched waits on the plan's event before it touches the batch (SparseTable.get),
+        # so the batch event is only needed when the step plans the keys itself
+        planned = self.fence and any(k is keys for k, _ in getattr(self.model, "_pending_plans", ()))
+        if ev is not None and not planned:
             self.main.wait_event(ev)
 
         def next_keys():  # called by train_step where it issues the look-ahead planning
