@@ -124,6 +124,15 @@ class SideStream:
     def __init__(self, device, enabled: bool = True):
         self.stream = torch.cuda.Stream(device=device, priority=compute_priority()) \
             if enabled and torch.device(device).type == "cuda" else None
+        # fork / join events are re-recorded every step (a wait binds to the record issued before
+        # it): no event objects created and destroyed per fork
+        self._evs = [torch.cuda.Event() for _ in range(8)] if self.stream is not None else []
+        self._ev_i = 0
+
+    def _event(self):
+        ev = self._evs[self._ev_i % len(self._evs)]
+        self._ev_i += 1
+        return ev
 
     @contextlib.contextmanager
     def fork(self):
@@ -131,7 +140,9 @@ class SideStream:
             yield
             return
         cur = torch.cuda.current_stream(self.stream.device)
-        self.stream.wait_stream(cur)
+        ev = self._event()
+        ev.record(cur)
+        self.stream.wait_event(ev)
         prev = ops.overlap_mode(True)  # forked work: GEMM splits chosen for throughput, not latency
         try:
             with torch.cuda.stream(self.stream):
@@ -141,7 +152,9 @@ class SideStream:
 
     def join(self):
         if self.stream is not None:
-            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+            ev = self._event()
+            ev.record(self.stream)
+            torch.cuda.current_stream(self.stream.device).wait_event(ev)
 
     def mark(self):
         """Event after the work forked so far (None when disabled)."""
