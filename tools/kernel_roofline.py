@@ -59,9 +59,13 @@ def spec(U):
         (r"sparse_rowwise_adagrad_v4", None, "row-wise Adagrad apply (U rows)", 0, U * (W * 4 * 3 + 8 + 8 + 8)),
         (r"adam_kernel", None, "Adam (dense 1.58M params)", 0, 1582080 * (16 + 18)),
         (r"criteo_synth_kernel", None, "synthetic batch (planning stream)", 0, B * (F * 8 + ND * 4 + 4)),
-        (r"ub_insert_kernel", None, "dedupe: hash insert (planning)", 0, n * 8 * 2),
-        (r"ub_assign_kernel", None, "dedupe: assign (planning)", 0, n * 8 * 2 + U * 8),
-        (r"ub_inverse_kernel", None, "dedupe: inverse (planning)", 0, n * 8 * 2),
+        (r"plan_transpose_kernel", None, "plan: keys -> column-major (planning)", 0, n * (8 + 4)),
+        (r"plan_sort_col_kernel", None, "plan: per-column LDS radix sort, 26 WGs (planning)", 0,
+         n * (4 + 4 + 4) + U * 8),
+        (r"plan_emit_kernel", None, "plan: uniq / inv / lookup CSR (planning)", 0, n * (4 + 4 + 8 + 4 + 4) + U * 16),
+        (r"ub_insert_kernel", None, "hash dedupe: insert (planning, non-column tables)", 0, n * 8 * 2),
+        (r"ub_assign_kernel", None, "hash dedupe: assign (planning)", 0, n * 8 * 2 + U * 8),
+        (r"ub_inverse_kernel", None, "hash dedupe: inverse (planning)", 0, n * 8 * 2),
         (r"emb_seg_fill_kernel", None, "lookup CSR fill (planning)", 0, n * (8 + 8)),
     ]
 
