@@ -25,7 +25,14 @@ using minips::SVMItem;
 
 inline void DefineCommonFlags() {
   auto& c = Context::Get();
-  c.Define("input", Context::Type::kString, "", "libsvm input (local path); empty = synthetic");
+  c.Define("input", Context::Type::kString, "", "libsvm input: path/dir/comma list, file://, webhdfs:// or hdfs:// "
+           "URL (a bare path is read from HDFS when --hdfs_namenode is set); empty = synthetic");
+  c.Define("hdfs_namenode", Context::Type::kString, "", "HDFS namenode host for bare --input paths");
+  c.Define("hdfs_namenode_port", Context::Type::kInt, "9000", "namenode RPC port (libhdfs3)");
+  c.Define("hdfs_http_port", Context::Type::kInt, "0", "namenode HTTP port: > 0 reads through WebHDFS");
+  c.Define("assigner_master_port", Context::Type::kInt, "0",
+           "> 0: node 0 serves locality-aware block assignment on this port (HDFSBlockAssigner); "
+           "0: static byte-range shards");
   c.Define("kModelType", Context::Type::kString, "SSP", "ASP/SSP/BSP");
   c.Define("kStorageType", Context::Type::kString, "Vector", "Map/Vector");
   c.Define("batch_size", Context::Type::kInt, "100", "samples per iteration per worker");
@@ -40,6 +47,42 @@ inline void DefineCommonFlags() {
   c.Define("report_interval", Context::Type::kInt, "0", "report every N iterations");
   c.Define("synthetic_rows", Context::Type::kInt, "2000", "synthetic samples per node");
   c.Define("synthetic_nnz", Context::Type::kInt, "20", "synthetic non-zeros per sample");
+}
+
+// The app's libsvm input (lib/abstract_data_loader.hpp): static shards, or blocks handed out by
+// the locality-aware assigner that node 0 serves on --assigner_master_port.
+inline std::vector<SVMItem> LoadAppData(const std::vector<Node>& nodes, int my_index) {
+  auto& c = Context::Get();
+  std::string input = c.get_string("input");
+  const std::string nn = c.get_string("hdfs_namenode");
+  if (!nn.empty() && input.find("://") == std::string::npos) {
+    const int http = c.get_int32("hdfs_http_port");
+    input = (http > 0 ? "webhdfs://" + nn + ":" + std::to_string(http)
+                      : "hdfs://" + nn + ":" + std::to_string(c.get_int32("hdfs_namenode_port"))) +
+            (input.empty() || input[0] != '/' ? "/" : "") + input;
+  }
+  minips::LoadOptions opt;
+  opt.rank = my_index;
+  opt.num_ranks = (int)nodes.size();
+  opt.num_threads = c.get_int32("num_local_load_thread");
+  const int port = c.get_int32("assigner_master_port");
+  std::unique_ptr<minips::BlockAssignerServer> server;
+  if (port > 0) {
+    if (my_index == 0) {
+      server.reset(new minips::BlockAssignerServer(port));
+      server->Start();
+    }
+    opt.assigner = nodes[0].hostname + ":" + std::to_string(port);
+    opt.host = nodes[my_index].hostname;  // the hostfile names hosts as HDFS reports datanodes
+  }
+  auto data = minips::LoadLibsvmFile(input, opt, true);
+  if (server) {  // serve until every loader thread of every node has exited (kExit)
+    if (!server->WaitDone(600)) MINIPS_LOG(1, "block assigner: not every loader exited");
+    MINIPS_LOG(0, "block assigner: " << server->LocalServed() << " local / " << server->RemoteServed()
+                                     << " remote blocks");
+    server->Stop();
+  }
+  return data;
 }
 
 inline ModelType ParseModelType(const std::string& s) {

@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
   MINIPS_CHECK(K > 0 && dims > 0, "K and num_dims must be positive");
   const int my_index = (int)(std::find(nodes.begin(), nodes.end(), me) - nodes.begin());
   std::vector<SVMItem> data = !ctx.get_string("input").empty()
-                                  ? LoadLibsvmFile(ctx.get_string("input"), my_index, (int)nodes.size(), 4)
+                                  ? LoadAppData(nodes, my_index)
                                   : SyntheticData(ctx.get_int32("synthetic_rows"), dims, ctx.get_int32("synthetic_nnz"),
                                                   31 + me.id);
   Engine engine(me, nodes, master);

@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
     CheckFaultTolerance(3, "node " + std::to_string(me.id) + " restarting");
     data = LoadSVMData(ck.prefix + "worker_" + std::to_string(me.id));
   } else if (!ctx.get_string("input").empty()) {
-    data = LoadLibsvmFile(ctx.get_string("input"), my_index, (int)nodes.size(), ctx.get_int32("num_local_load_thread"));
+    data = LoadAppData(nodes, my_index);
   } else {
     data = SyntheticData(ctx.get_int32("synthetic_rows"), num_dims, ctx.get_int32("synthetic_nnz"), 17 + me.id);
   }

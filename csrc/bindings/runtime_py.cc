@@ -7,6 +7,8 @@
 #include <pybind11/stl.h>
 
 #include "../runtime/checkpoint.h"
+#include "../runtime/fs.h"
+#include "../runtime/io.h"
 #include "../runtime/comm.h"
 #include "../runtime/config.h"
 #include "../runtime/engine.h"
@@ -312,11 +314,20 @@ PYBIND11_MODULE(_runtime, m) {
   m.def("check_fault_tolerance", &CheckFaultTolerance, py::arg("phase"), py::arg("detail") = "");
   m.def(
       "load_libsvm",
-      [](const std::string& path, int shard, int num_shards, int threads, bool one_based) {
+      [](const std::string& path, int shard, int num_shards, int threads, bool one_based, const std::string& assigner,
+         const std::string& host, uint64_t block_size, int job_id) {
         std::vector<SVMItem> items;
         {
           py::gil_scoped_release rel;
-          items = LoadLibsvmFile(path, shard, num_shards, threads, one_based);
+          LoadOptions opt;
+          opt.rank = shard;
+          opt.num_ranks = num_shards;
+          opt.num_threads = threads;
+          opt.assigner = assigner;
+          opt.host = host;
+          opt.block_size = block_size;
+          opt.job_id = job_id;
+          items = LoadLibsvmFile(path, opt, one_based);
         }
         // CSR arrays: rowptr, cols, vals, labels
         std::vector<int64_t> rowptr{0}, cols;
@@ -335,7 +346,63 @@ PYBIND11_MODULE(_runtime, m) {
                               py::array_t<double>(labels.size(), labels.data()));
       },
       py::arg("path"), py::arg("shard") = 0, py::arg("num_shards") = 1, py::arg("threads") = 4,
-      py::arg("one_based") = true);
+      py::arg("one_based") = true, py::arg("assigner") = "", py::arg("host") = "", py::arg("block_size") = 0,
+      py::arg("job_id") = 0);
+
+  // --- file systems (general_fstream: local / webhdfs:// / hdfs://) and block assignment ----
+  // every call that may wait on a remote file system releases the GIL (a WebHDFS peer in the
+  // same process -- the tests' stand-in -- needs it to answer)
+  m.def("fs_list", [](const std::string& url) {
+    std::vector<FileStat> files;
+    {
+      py::gil_scoped_release rel;
+      files = ListInputs(url);
+    }
+    std::vector<py::tuple> out;
+    for (auto& f : files) out.push_back(py::make_tuple(f.url, f.size, f.block_size));
+    return out;
+  });
+  m.def("fs_locations", [](const std::string& url) {
+    std::vector<BlockLocation> locs;
+    {
+      py::gil_scoped_release rel;
+      FileStat f = FileSystem::For(url).Stat(url);
+      locs = FileSystem::For(url).Locations(f);
+    }
+    std::vector<py::tuple> out;
+    for (auto& l : locs) out.push_back(py::make_tuple(l.offset, l.length, l.hosts));
+    return out;
+  });
+  m.def("fs_read", [](const std::string& url) {
+    std::string s;
+    {
+      py::gil_scoped_release rel;
+      s = ReadFileToString(url);
+    }
+    return py::bytes(s);
+  });
+  m.def("fs_write", [](const std::string& url, const std::string& data) {
+    py::gil_scoped_release rel;
+    EnsureParentDir(url);
+    WriteStringToFile(url, data);
+  });
+  m.def("fs_exists", [](const std::string& url) { return FileSystem::For(url).Exists(url); },
+        py::call_guard<py::gil_scoped_release>());
+  m.def("libhdfs3_available", []() {
+    std::string why;
+    const bool ok = LibHdfs3Available(&why);
+    return py::make_tuple(ok, why);
+  });
+  m.def("remote_bytes_read", &RemoteBytesRead);
+  m.def("local_host_name", &LocalHostName);
+  py::class_<BlockAssignerServer>(m, "BlockAssignerServer")
+      .def(py::init<int>(), py::arg("port") = 0)
+      .def("start", &BlockAssignerServer::Start)
+      .def("stop", &BlockAssignerServer::Stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &BlockAssignerServer::Port)
+      .def("wait_done", &BlockAssignerServer::WaitDone, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("local_served", &BlockAssignerServer::LocalServed)
+      .def_property_readonly("remote_served", &BlockAssignerServer::RemoteServed);
 
   // --- GPU shard checkpoint files (binary sidecar + reference text format) ---------------
   py::class_<AsyncShardWriter>(m, "ShardWriter")

@@ -4,6 +4,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+
+#include "fs.h"
 #include <iomanip>
 
 #include "config.h"
@@ -73,7 +75,7 @@ std::string Node::DebugString() const {
 }
 
 std::vector<Node> ParseFile(const std::string& path) {
-  std::ifstream in(path);
+  GeneralIfstream in(path);
   MINIPS_CHECK(in.good(), "cannot open hostfile " << path);
   std::vector<Node> nodes;
   std::string line;

@@ -10,6 +10,8 @@
 #include <cerrno>
 #include <cstdlib>
 #include <fstream>
+
+#include "fs.h"
 #include <iomanip>
 #include <set>
 #include <thread>
@@ -17,6 +19,16 @@
 namespace minips {
 
 void EnsureParentDir(const std::string& path) {
+  if (!IsLocalUrl(path)) {  // remote file systems: mkdir -p of the parent through the FileSystem
+    const Url u = ParseUrl(path);
+    const auto s = u.path.rfind('/');
+    if (s != std::string::npos && s > 0) {
+      Url parent = u;
+      parent.path = u.path.substr(0, s);
+      FileSystem::For(path).MakeDirs(parent.ToString());
+    }
+    return;
+  }
   auto slash = path.rfind('/');
   if (slash == std::string::npos || slash == 0) return;
   std::string dir = path.substr(0, slash);
@@ -34,7 +46,7 @@ void EnsureParentDir(const std::string& path) {
 
 void DumpSVMData(const std::string& path, const std::vector<SVMItem>& data) {
   EnsureParentDir(path);
-  std::ofstream out(path, std::ios::trunc);
+  GeneralOfstream out(path);
   MINIPS_CHECK(out.good(), "cannot write " << path);
   out << std::setprecision(17);
   for (auto& it : data) {
@@ -42,19 +54,23 @@ void DumpSVMData(const std::string& path, const std::vector<SVMItem>& data) {
     for (auto& f : it.x) out << " " << f.first << ":" << f.second;
     out << "\n";
   }
+  out.close();
+  MINIPS_CHECK(out.good(), "write failed " << path);
 }
 
 std::vector<SVMItem> LoadSVMData(const std::string& path) { return LoadLibsvmFile(path, 0, 1, 4, false); }
 
 void DumpConfigData(const std::string& path, const std::map<int, int>& iteration_map) {
   EnsureParentDir(path);
-  std::ofstream out(path, std::ios::trunc);
+  GeneralOfstream out(path);
   MINIPS_CHECK(out.good(), "cannot write " << path);
   for (auto& kv : iteration_map) out << kv.first << ":" << kv.second << " ";
+  out.close();
+  MINIPS_CHECK(out.good(), "write failed " << path);
 }
 
 std::map<int, int> LoadConfigData(const std::string& path) {
-  std::ifstream in(path);
+  GeneralIfstream in(path);
   MINIPS_CHECK(in.good(), "cannot read " << path);
   std::map<int, int> m;
   std::string tok;
@@ -68,11 +84,13 @@ std::map<int, int> LoadConfigData(const std::string& path) {
 
 void DumpScaleFile(const std::string& path, const Node& node) {
   EnsureParentDir(path);
-  std::ofstream out(path, std::ios::trunc);
+  GeneralOfstream out(path);
   MINIPS_CHECK(out.good(), "cannot write " << path);
   out << node.id << ":" << node.hostname << ":" << node.port;
   if (node.gpu >= 0) out << ":" << node.gpu;
   out << "\n";
+  out.close();
+  MINIPS_CHECK(out.good(), "write failed " << path);
 }
 
 Node LoadScaleFile(const std::string& path) {
@@ -108,56 +126,33 @@ bool ParseLibsvm(const char* line, size_t len, SVMItem* out, bool one_based) {
   return true;
 }
 
+std::vector<SVMItem> LoadLibsvmFile(const std::string& path, const LoadOptions& opt, bool one_based) {
+  // Blocks of every input (a path, a directory or a comma list; local, webhdfs:// or hdfs://)
+  // are handed out statically (rank r of n) or by the locality-aware block assigner, and parsed
+  // by `opt.num_threads` loader threads (io.h ForEachLine); results are kept per block and
+  // concatenated in block order, so the order is deterministic for a given assignment.
+  const int threads = std::max(1, opt.num_threads);
+  std::vector<std::map<int, std::vector<SVMItem>>> per_thread(threads);
+  ForEachLine(path, opt, [&](const FileBlock& b, const char* l, size_t n, int t) {
+    SVMItem item;
+    if (ParseLibsvm(l, n, &item, one_based)) per_thread[t][b.id].push_back(std::move(item));
+  });
+  std::map<int, std::vector<SVMItem>*> order;
+  for (auto& m : per_thread)
+    for (auto& kv : m) order[kv.first] = &kv.second;
+  std::vector<SVMItem> all;
+  for (auto& kv : order)
+    for (auto& it : *kv.second) all.push_back(std::move(it));
+  return all;
+}
+
 std::vector<SVMItem> LoadLibsvmFile(const std::string& path, int shard, int num_shards, int num_threads,
                                     bool one_based) {
-  // Blocks of every input file (a path, a directory or a comma list) are handed to this rank by
-  // the BlockAssigner and read by `num_threads` loader threads through the mmap'd
-  // LineInputFormat (io.h); results are kept per block so the order is deterministic.
-  const auto files = ListInputFiles(path);
-  uint64_t total = 0;
-  for (auto& f : files) {
-    std::ifstream in(f, std::ios::binary | std::ios::ate);
-    total += (uint64_t)in.tellg();
-  }
-  // ~4 blocks per loader thread and rank, at least 64 KiB (hdfs_block_size analogue)
-  const uint64_t block = std::max<uint64_t>(64 << 10, total / std::max(1, 4 * num_threads * num_shards) + 1);
-  auto blocks = SplitFiles(files, block);
-  std::vector<std::vector<SVMItem>> per_block(blocks.size());
-  BlockAssigner assigner(blocks, shard, num_shards);
-  std::vector<std::thread> th;
-  std::mutex err_mu;
-  std::string err;
-  for (int t = 0; t < std::max(1, num_threads); ++t) {
-    th.emplace_back([&] {
-      try {
-        std::string cur;
-        std::unique_ptr<MappedFile> mf;
-        while (auto blk = assigner.Next()) {
-          if (blk->path != cur) {
-            mf.reset(new MappedFile(blk->path));
-            cur = blk->path;
-          }
-          LineInputFormat in(*mf, *blk);
-          const char* l;
-          size_t n;
-          auto& out = per_block[blk->id];
-          while (in.Next(&l, &n)) {
-            SVMItem item;
-            if (ParseLibsvm(l, n, &item, one_based)) out.push_back(std::move(item));
-          }
-        }
-      } catch (const std::exception& e) {
-        std::lock_guard<std::mutex> lk(err_mu);
-        err = e.what();
-      }
-    });
-  }
-  for (auto& t : th) t.join();
-  MINIPS_CHECK(err.empty(), "libsvm load failed: " << err);
-  std::vector<SVMItem> all;
-  for (auto& p : per_block)
-    for (auto& it : p) all.push_back(std::move(it));
-  return all;
+  LoadOptions opt;
+  opt.rank = shard;
+  opt.num_ranks = num_shards;
+  opt.num_threads = num_threads;
+  return LoadLibsvmFile(path, opt, one_based);
 }
 
 BatchDataSampler::BatchDataSampler(const std::vector<SVMItem>* data, int batch_size, uint64_t seed)

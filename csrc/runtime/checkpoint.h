@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "base.h"
+#include "io.h"
 #include "node.h"
 
 namespace minips {
@@ -44,6 +45,8 @@ bool ParseLibsvm(const char* line, size_t len, SVMItem* out, bool one_based = tr
 // `num_threads` parser threads.
 std::vector<SVMItem> LoadLibsvmFile(const std::string& path, int shard = 0, int num_shards = 1,
                                     int num_threads = 4, bool one_based = true);
+// Same, with the full loader options (block assigner service, locality host, block size).
+std::vector<SVMItem> LoadLibsvmFile(const std::string& path, const LoadOptions& opt, bool one_based = true);
 
 class BatchDataSampler {
  public:

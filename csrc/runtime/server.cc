@@ -3,6 +3,8 @@
 #include <algorithm>
 #include <cmath>
 #include <fstream>
+
+#include "fs.h"
 #include <iomanip>
 
 #include "checkpoint.h"
@@ -73,16 +75,17 @@ int ProgressTracker::Update(int failed_node_id, const std::vector<Node>&) {
 int32_t ProgressTracker::RoundHundred(int32_t input) { return 100 * (int32_t)std::round(input / 100.0); }
 
 void ProgressTracker::Dump(const std::string& path, bool round_hundred) const {
-  std::ofstream out(path, std::ios::trunc);
+  GeneralOfstream out(path);
   MINIPS_CHECK(out.good(), "cannot write " << path);
   auto f = [&](int v) { return round_hundred ? RoundHundred(v) : v; };
   out << "min_clock" << ":" << f(min_clock_) << " ";
   for (auto& kv : progresses_) out << kv.first << ":" << f(kv.second) << " ";
+  out.close();
   MINIPS_CHECK(out.good(), "write failed " << path);
 }
 
 void ProgressTracker::Restore(const std::string& path, int scale_node_id) {
-  std::ifstream in(path);
+  GeneralIfstream in(path);
   MINIPS_CHECK(in.good(), "cannot read " << path);
   std::string tok;
   while (in >> tok) {
@@ -195,7 +198,7 @@ template <typename Val>
 void MapStorage<Val>::Dump(const CheckpointConfig& cfg) {
   if (!cfg.toggle) return;
   EnsureParentDir(cfg.ParamsFile());
-  std::ofstream out(cfg.ParamsFile(), std::ios::trunc);
+  GeneralOfstream out(cfg.ParamsFile());
   MINIPS_CHECK(out.good(), "cannot write " << cfg.ParamsFile());
   std::vector<Key> keys;
   for (auto& kv : storage_) keys.push_back(kv.first);
@@ -205,10 +208,12 @@ void MapStorage<Val>::Dump(const CheckpointConfig& cfg) {
     WriteVal(out, storage_[k]);
     out << " ";
   }
+  out.close();
+  MINIPS_CHECK(out.good(), "write failed " << cfg.ParamsFile());
 }
 template <typename Val>
 void MapStorage<Val>::Restore(const CheckpointConfig& cfg) {
-  std::ifstream in(cfg.ParamsFile());
+  GeneralIfstream in(cfg.ParamsFile());
   MINIPS_CHECK(in.good(), "cannot read " << cfg.ParamsFile());
   storage_.clear();
   std::string tok;
@@ -223,7 +228,7 @@ template <typename Val>
 void VectorStorage<Val>::Dump(const CheckpointConfig& cfg) {
   if (!cfg.toggle) return;
   EnsureParentDir(cfg.ParamsFile());
-  std::ofstream out(cfg.ParamsFile(), std::ios::trunc);
+  GeneralOfstream out(cfg.ParamsFile());
   MINIPS_CHECK(out.good(), "cannot write " << cfg.ParamsFile());
   // Reference format (server/vector_storage.hpp:54-73): one line, "<local_idx>:<val> " for
   // every non-zero entry.
@@ -234,10 +239,12 @@ void VectorStorage<Val>::Dump(const CheckpointConfig& cfg) {
       out << " ";
     }
   }
+  out.close();
+  MINIPS_CHECK(out.good(), "write failed " << cfg.ParamsFile());
 }
 template <typename Val>
 void VectorStorage<Val>::Restore(const CheckpointConfig& cfg) {
-  std::ifstream in(cfg.ParamsFile());
+  GeneralIfstream in(cfg.ParamsFile());
   MINIPS_CHECK(in.good(), "cannot read " << cfg.ParamsFile());
   std::fill(storage_.begin(), storage_.end(), Val());
   std::string tok;

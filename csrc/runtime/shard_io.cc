@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+
+#include "fs.h"
 #include <sstream>
 #include <stdexcept>
 
@@ -263,7 +265,7 @@ void ShardFileWriter::Close() {
 
 void WriteTextParams(const std::string& path, const ArrayRef& a) {
   EnsureParentDir(path);
-  std::ofstream o(path, std::ios::trunc);
+  GeneralOfstream o(path);
   MINIPS_CHECK(o.good(), "cannot write " << path);
   o.precision(9);
   const uint64_t n = a.rows * a.cols;
@@ -281,11 +283,12 @@ void WriteTextParams(const std::string& path, const ArrayRef& a) {
     }
   }
   o << buf;
+  o.close();
   MINIPS_CHECK(o.good(), "write failed: " << path);
 }
 
 std::vector<double> ReadTextParams(const std::string& path, uint64_t n) {
-  std::ifstream in(path);
+  GeneralIfstream in(path);
   MINIPS_CHECK(in.good(), "cannot read " << path);
   std::vector<double> out(n, 0.0);
   std::string tok;

@@ -18,6 +18,7 @@
 #include "../runtime/comm.h"
 #include "../runtime/config.h"
 #include "../runtime/engine.h"
+#include "../runtime/fs.h"
 #include "../runtime/io.h"
 #include "../runtime/serialization.h"
 #include "../runtime/shard_io.h"
@@ -1019,6 +1020,141 @@ TEST(IO, AsyncReadBufferKeepsOrder) {
   int v, expect = 0;
   while (buf.Get(&v)) EXPECT_EQ(v, expect++);
   EXPECT_EQ(expect, 100);
+}
+
+TEST(IO, RemoteWindowReaderMatchesMmap) {
+  // The buffered block window (remote file systems) yields exactly the lines of the mmap path.
+  using namespace minips;
+  const std::string path = "/tmp/minips_io_win_" + std::to_string(::getpid());
+  {
+    std::ofstream o(path);
+    for (int i = 0; i < 3000; ++i) o << i << std::string((size_t)(i * 13 % 97), 'x') << "\n";
+    o << "tail-without-newline";
+  }
+  MappedFile mf(path);
+  auto rf = FileSystem::For(path).OpenRead(path);
+  for (uint64_t bs : {1ull, 5ull, 333ull, 4096ull, 1ull << 22}) {
+    std::vector<std::string> a, b;
+    std::string win;
+    for (auto& blk : SplitFiles({path}, bs)) {
+      LineInputFormat x(mf, blk);
+      LineInputFormat y = ReadBlockWindow(rf.get(), blk, &win);
+      const char* l;
+      size_t n;
+      while (x.Next(&l, &n)) a.emplace_back(l, n);
+      while (y.Next(&l, &n)) b.emplace_back(l, n);
+    }
+    EXPECT_EQ(a.size(), 3001u);
+    EXPECT_TRUE(a == b);
+  }
+  ::unlink(path.c_str());
+}
+
+TEST(IO, LocalityAssignerPrefersLocalAndDropsReplicas) {
+  using namespace minips;
+  std::vector<FileBlock> blocks;
+  // 6 blocks: 0-2 on {a,b}, 3-4 on {b,c}, 5 on {c}
+  const std::vector<std::vector<std::string>> hosts = {{"a", "b"}, {"a", "b"}, {"a", "b"},
+                                                       {"b", "c"}, {"b", "c"}, {"c"}};
+  for (int i = 0; i < 6; ++i) blocks.push_back(FileBlock{"f", (uint64_t)i * 10, 10, 60, i, hosts[i]});
+  LocalityAssigner a(blocks);
+  std::vector<int> seen(6, 0);
+  for (int i = 0; i < 3; ++i) {  // a gets its three local blocks
+    auto b = a.Next("a");
+    ASSERT_TRUE(b.has_value());
+    EXPECT_TRUE(b->id <= 2);
+    seen[b->id]++;
+  }
+  auto b = a.Next("b");  // a's blocks are gone from b's list too: b gets 3 or 4
+  ASSERT_TRUE(b.has_value());
+  EXPECT_TRUE(b->id == 3 || b->id == 4);
+  seen[b->id]++;
+  auto r = a.Next("a");  // nothing local left for a: a remote block (from c, which has the most)
+  ASSERT_TRUE(r.has_value());
+  EXPECT_TRUE(r->id >= 3);
+  seen[r->id]++;
+  while (auto x = a.Next("zz")) seen[x->id]++;
+  for (int i = 0; i < 6; ++i) EXPECT_EQ(seen[i], 1);
+  EXPECT_EQ(a.LocalServed(), 4u);
+  EXPECT_EQ(a.RemoteServed(), 2u);
+  EXPECT_FALSE(a.Next("a").has_value());
+}
+
+TEST(IO, AssignerServiceHandsEveryBlockOnce) {
+  // node 0's assigner service + coordinated loaders of 3 "nodes" x 2 threads: every line is read
+  // exactly once and the service halts after all 6 loader threads sent kExit.
+  using namespace minips;
+  const std::string dir = "/tmp/minips_io_asg_" + std::to_string(::getpid()) + "/";
+  EnsureParentDir(dir + "x");
+  uint64_t expect = 0;
+  for (int f = 0; f < 4; ++f) {
+    std::ofstream o(dir + "part-" + std::to_string(f));
+    for (int i = 0; i < 500; ++i) {
+      o << (f * 1000 + i) << "\n";
+      expect += (uint64_t)(f * 1000 + i);
+    }
+  }
+  BlockAssignerServer srv(0);
+  srv.Start();
+  std::atomic<uint64_t> sum{0}, lines{0};
+  std::vector<std::thread> nodes;
+  for (int r = 0; r < 3; ++r) {
+    nodes.emplace_back([&, r] {
+      LoadOptions opt;
+      opt.rank = r;
+      opt.num_ranks = 3;
+      opt.num_threads = 2;
+      opt.block_size = 512;
+      opt.assigner = "127.0.0.1:" + std::to_string(srv.Port());
+      opt.host = "host" + std::to_string(r);
+      lines += ForEachLine(dir, opt, [&](const FileBlock&, const char* l, size_t n, int) {
+        sum += std::stoull(std::string(l, n));
+      });
+    });
+  }
+  for (auto& t : nodes) t.join();
+  EXPECT_TRUE(srv.WaitDone(10));
+  srv.Stop();
+  EXPECT_EQ(lines.load(), 2000u);
+  EXPECT_EQ(sum.load(), expect);
+  // local files: every block is "on" this host, which none of the fake hosts is -> all remote
+  EXPECT_EQ(srv.LocalServed(), 0u);
+  EXPECT_TRUE(srv.RemoteServed() > 0);
+}
+
+TEST(FS, UrlsAndGeneralStreams) {
+  using namespace minips;
+  Url u = ParseUrl("hdfs://nn.example:9000/data/a.txt");
+  EXPECT_EQ(u.scheme, std::string("hdfs"));
+  EXPECT_EQ(u.host, std::string("nn.example"));
+  EXPECT_EQ(u.port, 9000);
+  EXPECT_EQ(u.path, std::string("/data/a.txt"));
+  Url w = ParseUrl("http://dn1:9864/webhdfs/v1/x?op=OPEN&offset=3");
+  EXPECT_EQ(w.query, std::string("op=OPEN&offset=3"));
+  EXPECT_EQ(ParseUrl("/tmp/x").scheme, std::string(""));
+  EXPECT_EQ(ParseUrl("file:///tmp/x").path, std::string("/tmp/x"));
+  EXPECT_TRUE(IsLocalUrl("file:///tmp/x"));
+  EXPECT_FALSE(IsLocalUrl("webhdfs://nn:9870/x"));
+  const std::string p = "file:///tmp/minips_fs_" + std::to_string(::getpid());
+  {
+    GeneralOfstream o(p);
+    for (int i = 0; i < 200000; ++i) o << i << " ";
+    o.close();
+    EXPECT_TRUE(o.good());
+  }
+  GeneralIfstream in(p);
+  int v, expect = 0;
+  while (in >> v) EXPECT_EQ(v, expect++);
+  EXPECT_EQ(expect, 200000);
+  GeneralIfstream s(p);
+  s.seekg(6);  // "0 1 2 3 " -> token at byte 6 is "3"
+  s >> v;
+  EXPECT_EQ(v, 3);
+  GeneralIfstream missing("/nonexistent/minips/file");
+  EXPECT_FALSE(missing.good());
+  std::string why;
+  if (!LibHdfs3Available(&why)) EXPECT_TRUE(why.find("webhdfs://") != std::string::npos);
+  ::unlink(ParseUrl(p).path.c_str());
 }
 
 int main(int argc, char** argv) { return minitest::RunAll(argc, argv); }
