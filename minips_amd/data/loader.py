@@ -19,8 +19,12 @@ from .._native import runtime
 
 
 class LibsvmData:
-    def __init__(self, path: str, rank: int = 0, world: int = 1, threads: int = 4, one_based: bool = True):
-        rowptr, cols, vals, labels = runtime().load_libsvm(path, rank, world, threads, one_based)
+    def __init__(self, path: str, rank: int = 0, world: int = 1, threads: int = 4, one_based: bool = True,
+                 assigner: str = "", host: str = ""):
+        # path: local / webhdfs:// / hdfs:// (csrc/runtime/fs.h); assigner "host:port": blocks come
+        # from the locality-aware BlockAssignerServer instead of the static rank partition
+        rowptr, cols, vals, labels = runtime().load_libsvm(path, rank, world, threads, one_based, assigner=assigner,
+                                                           host=host)
         self.rowptr = torch.from_numpy(rowptr)
         self.cols = torch.from_numpy(cols)
         self.vals = torch.from_numpy(vals).float()

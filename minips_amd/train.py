@@ -72,9 +72,42 @@ def parse(argv=None):
     ap.add_argument("--timing_skip", type=int, default=0,
                     help="iterations excluded from steady_ms_per_iter (first-launch / warm-up costs)")
     ap.add_argument("--alpha", type=float, default=0.05)
-    ap.add_argument("--input", default="", help="libsvm file / directory / comma list (LR; reference --input)")
+    ap.add_argument("--input", default="", help="libsvm file / directory / comma list (LR; reference --input); "
+                    "local, webhdfs://nn:port/path or hdfs://nn:port/path")
+    ap.add_argument("--hdfs_namenode", default="", help="read a bare --input path from this HDFS namenode")
+    ap.add_argument("--hdfs_namenode_port", type=int, default=9000)
+    ap.add_argument("--hdfs_http_port", type=int, default=0, help="> 0: read HDFS through WebHDFS on this port")
+    ap.add_argument("--assigner_master_port", type=int, default=0,
+                    help="> 0: rank 0 serves locality-aware block assignment (HDFSBlockAssigner) on this port")
     ap.add_argument("--num_dims", type=int, default=0, help="feature count (reference flag; 0: infer / default)")
     return ap.parse_args(argv)
+
+
+def _load_input(args, comm):
+    """This rank's libsvm shard: static byte-range blocks, or blocks handed out by the locality-aware
+    assigner that rank 0 serves (reference HDFSManager: node 0 runs the HDFSBlockAssigner)."""
+    from ._native import runtime
+    from .data.loader import LibsvmData
+
+    url = args.input
+    if args.hdfs_namenode and "://" not in url:
+        auth = (f"webhdfs://{args.hdfs_namenode}:{args.hdfs_http_port}" if args.hdfs_http_port > 0
+                else f"hdfs://{args.hdfs_namenode}:{args.hdfs_namenode_port}")
+        url = auth + ("" if url.startswith("/") else "/") + url
+    if args.assigner_master_port <= 0:
+        return LibsvmData(url, comm.rank, comm.world)
+    srv = None
+    if comm.rank == 0:
+        srv = runtime().BlockAssignerServer(args.assigner_master_port)
+        srv.start()
+    master = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    data = LibsvmData(url, comm.rank, comm.world, assigner=f"{master}:{args.assigner_master_port}",
+                      host=runtime().local_host_name())
+    if srv is not None:  # serve until every loader thread of every rank has exited (kExit)
+        srv.wait_done(600.0)
+        print(f"[rank 0] block assigner: {srv.local_served} local / {srv.remote_served} remote blocks", flush=True)
+        srv.stop()
+    return data
 
 
 SMALL_CARDS = [50, 7, 300, 20, 5, 60, 90, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27,
@@ -307,7 +340,7 @@ def main(argv=None):
     if args.model in ("lr", "kmeans") and args.input:
         from .data.loader import LibsvmData
 
-        args._shard = LibsvmData(args.input, comm.rank, comm.world)
+        args._shard = _load_input(args, comm)
         sub = _force_quit(comm, args._shard.n > 0 and args.force_quit_rank != rank, rank)
         if sub is None:
             if hb:

@@ -159,3 +159,36 @@ def test_lr_app_webhdfs_input_assigner_and_checkpoints(tmp_path):
     params = (root / "ck" / "server_params_0").read_text().split()
     assert params and all(":" in p for p in params)
     assert (root / "ck" / "server_progress_0").read_text().startswith("min_clock:")
+
+
+def test_train_driver_two_ranks_webhdfs_assigner(tmp_path):
+    """python -m minips_amd.train (2 gloo ranks) --model lr with the input on (mock) HDFS and rank 0
+    serving block assignment: every sample lands on exactly one rank and training converges."""
+    import subprocess
+    import sys
+
+    from _util import free_ports
+
+    root = tmp_path / "hdfs"
+    (root / "d").mkdir(parents=True)
+    rng = random.Random(5)
+    teacher = [rng.gauss(0, 1) for _ in range(300)]
+    with open(root / "d" / "part-0", "w") as f:
+        for _ in range(4000):
+            feats = sorted(rng.sample(range(300), 10))
+            f.write(("1" if sum(teacher[k] for k in feats) > 0 else "0") + "".join(f" {k + 1}:1" for k in feats) + "\n")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mport, aport = free_ports(2)
+    with MockWebHdfs(str(root), block_size=16384) as fs:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+               "127.0.0.1", "--master-port", str(mport), "-m", "minips_amd.train", "--model", "lr",
+               "--input", "/d", "--hdfs_namenode", "127.0.0.1", "--hdfs_http_port", str(fs.port),
+               "--assigner_master_port", str(aport), "--num_dims", "300", "--batch", "100", "--steps", "120",
+               "--alpha", "0.1"]
+        r = subprocess.run(cmd, cwd=repo, capture_output=True, text=True, timeout=300,
+                           env={**os.environ, "CUDA_VISIBLE_DEVICES": ""})
+        assert r.returncode == 0, r.stderr[-3000:]
+    assert "block assigner:" in r.stdout
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    accs = [-v for _, v in out["losses"]]
+    assert sum(accs[-5:]) / 5 > 0.8, accs
