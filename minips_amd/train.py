@@ -72,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--timing_skip", type=int, default=0,
                     help="iterations excluded from steady_ms_per_iter (first-launch / warm-up costs)")
     ap.add_argument("--alpha", type=float, default=0.05)
+    ap.add_argument("--num_workers_per_node", type=int, default=1,
+                    help="LR: logical workers per rank, each with its own sampler and batch_size (reference flag); "
+                    "their batches of a clock go out as one fused Get/Add")
     ap.add_argument("--input", default="", help="libsvm file / directory / comma list (LR; reference --input); "
                     "local, webhdfs://nn:port/path or hdfs://nn:port/path")
     ap.add_argument("--hdfs_namenode", default="", help="read a bare --input path from this HDFS namenode")
@@ -175,7 +178,10 @@ def build(args, comm):
                                     staleness=args.staleness, storage=args.kStorageType,
                                     value_dtype=getattr(torch, args.value_dtype)), comm)
         B = args.batch or 1024
-        return m, {0: m.table}, (lambda: _Skippable(_Batches(shard, B, seed))), (lambda b: -m.train_step(*b)), B
+        W = max(1, args.num_workers_per_node)
+        return m, {0: m.table}, (lambda: _Skippable(_WorkerGroup([_Batches(shard, B, seed + _WSEED * w)
+                                                                  for w in range(W)]))), \
+            (lambda b: -m.train_step(*b)), B * W
     if args.model == "lr":
         from .data.synthetic import SparseLRSynth
         from .models.lr import SparseLR, SparseLRConfig
@@ -185,9 +191,11 @@ def build(args, comm):
                                     staleness=args.staleness, storage=args.kStorageType,
                                     value_dtype=getattr(torch, args.value_dtype)), comm)
         B = args.batch or (128 if args.small else 65536)
+        W = max(1, args.num_workers_per_node)
         return m, {0: m.table}, \
-            (lambda: _Skippable(SparseLRSynth(B, num_dims=nd, nnz=16 if args.small else 64, device=dev, seed=seed))), \
-            (lambda b: -m.train_step(*b)), B
+            (lambda: _Skippable(_WorkerGroup([SparseLRSynth(B, num_dims=nd, nnz=16 if args.small else 64, device=dev,
+                                                            seed=seed + _WSEED * w) for w in range(W)]))), \
+            (lambda b: -m.train_step(*b)), B * W
     if args.model == "kmeans" and args.input:
         # the reference K-Means input: sparse libsvm points (kmeans.cpp reads --input); the
         # shard stays resident in HBM and batches are consecutive rows, cut on the device
@@ -224,6 +232,33 @@ def build(args, comm):
         m = KMeans(cfg, comm, init_data=init)
         return m, {0: m.table}, (lambda: _Skippable(_GaussData(B, cfg.dims, dev, seed))), (lambda b: m.train_step(b)), B
     raise ValueError(args.model)
+
+
+_WSEED = 104729
+
+
+class _WorkerGroup:
+    """``--num_workers_per_node`` logical workers on one GPU rank (the reference runs that many
+    worker threads per process over the node's data, driver/engine.cpp:266-288, lr_example.cpp:
+    203-207): each worker keeps its own sampler (own start point / seed, its own batch_size), and
+    the W CSR batches of a clock are concatenated into ONE Get / Add / Clock -- one set of launches
+    instead of W. Under BSP this is exactly the reference's result: all W workers read the clock-c
+    parameters and the server sums their pushes (VectorStorage::SubAdd is additive); under SSP/ASP
+    the workers of a rank advance together, a schedule both models admit."""
+
+    def __init__(self, its):
+        self.its = its
+
+    def next(self):
+        parts = [it.next() for it in self.its]
+        if len(parts) == 1:
+            return parts[0]
+        rps, off = [], 0
+        for i, (rp, c, _, _) in enumerate(parts):
+            rps.append((rp if i == 0 else rp[1:]) + off)
+            off += c.numel()
+        return (torch.cat(rps), torch.cat([p[1] for p in parts]), torch.cat([p[2] for p in parts]),
+                torch.cat([p[3] for p in parts]))
 
 
 class _Skippable:

@@ -128,6 +128,35 @@ def test_sparse_lr_two_ranks():
         assert sum(out[r][0][-5:]) / 5 > 0.7, out[r][0]
 
 
+def test_lr_worker_group_equals_separate_worker_pushes():
+    """--num_workers_per_node W on one rank: the fused Get/Add of the W workers' batches gives the
+    same table as W reference workers that each Get the clock-c rows, push their own deltas, and
+    share one Clock (server sums the pushes, vector_storage.hpp:28-38)."""
+    from minips_amd import ops
+    from minips_amd.data.synthetic import SparseLRSynth
+    from minips_amd.models.lr import SparseLR, SparseLRConfig
+    from minips_amd.ps.comm import Comm
+    from minips_amd.train import _WorkerGroup
+
+    cfg = SparseLRConfig(num_dims=3000, alpha=0.05, value_dtype=torch.float64)
+    fused = SparseLR(cfg, Comm(device=torch.device("cpu")))
+    sep = SparseLR(cfg, Comm(device=torch.device("cpu")))
+    mk = lambda: [SparseLRSynth(64, num_dims=3000, nnz=12, seed=s) for s in (5, 6, 7)]  # noqa: E731
+    group, solo = _WorkerGroup(mk()), mk()
+    for _ in range(6):
+        fused.train_step(*group.next())
+        batches = [w.next() for w in solo]
+        pulled = [sep.table.get(b[1]) for b in batches]  # every worker reads clock-c parameters
+        for (rp, cols, vals, y), (rows, plan) in zip(batches, pulled):
+            delta = torch.zeros(max(plan.cap, 1), dtype=rows.dtype)
+            ops.lr_sparse_step(rp, plan.inv, vals, y, rows.view(-1)[: plan.cap], cfg.alpha, delta[: plan.cap],
+                               torch.zeros(1))
+            sep.table.add(plan, delta.view(-1, 1))
+        sep.table.clock()
+    torch.testing.assert_close(fused.table.shard, sep.table.shard, rtol=0, atol=1e-12)
+    assert float(fused.table.shard.abs().sum()) > 0
+
+
 def _km_run(rank, world, steps=8):
     from minips_amd.models.kmeans import KMeans, KMeansConfig
     from minips_amd.ps.comm import Comm
