@@ -489,6 +489,23 @@ PYBIND11_MODULE(_runtime, m) {
         WriteTextParams(path, a);
       },
       py::arg("path"), py::arg("data"), py::arg("dtype"), py::arg("rows"), py::arg("cols"));
+  py::class_<TextParamsWriter>(m, "TextParamsWriter")
+      .def(py::init<const std::string&>(), py::call_guard<py::gil_scoped_release>())
+      .def(
+          "append",
+          [](TextParamsWriter& w, uintptr_t data, const std::string& dtype, uint64_t rows, uint64_t cols) {
+            ArrayRef a;
+            a.name = "params";
+            a.data = reinterpret_cast<const void*>(data);
+            a.dtype = ParseDType(dtype);
+            a.rows = rows;
+            a.cols = cols;
+            py::gil_scoped_release rel;
+            w.Append(a);
+          },
+          py::arg("data"), py::arg("dtype"), py::arg("rows"), py::arg("cols"))
+      .def("close", &TextParamsWriter::Close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("elements", &TextParamsWriter::Elements);
   m.def("shard_bytes_read", &ShardBytesRead);
   m.def("reset_shard_bytes_read", &ResetShardBytesRead);
   m.def(

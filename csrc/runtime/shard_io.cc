@@ -263,28 +263,53 @@ void ShardFileWriter::Close() {
   MINIPS_CHECK(std::rename(tmp_.c_str(), path_.c_str()) == 0, "rename " << tmp_ << " -> " << path_);
 }
 
-void WriteTextParams(const std::string& path, const ArrayRef& a) {
+TextParamsWriter::TextParamsWriter(const std::string& path) : path_(path) {
   EnsureParentDir(path);
-  GeneralOfstream o(path);
-  MINIPS_CHECK(o.good(), "cannot write " << path);
-  o.precision(9);
+  out_.reset(new GeneralOfstream(path));
+  MINIPS_CHECK(out_->good(), "cannot write " << path);
+  buf_.reserve(1 << 20);
+}
+
+TextParamsWriter::~TextParamsWriter() {
+  try {
+    Close();
+  } catch (const std::exception&) {
+  }
+}
+
+void TextParamsWriter::Append(const ArrayRef& a) {
+  MINIPS_CHECK(out_, "TextParamsWriter already closed");
   const uint64_t n = a.rows * a.cols;
-  std::string buf;
-  buf.reserve(1 << 20);
+  // shortest round-trip precision of the stored type (fp64 tables need 17 digits)
+  const char* fmt = a.dtype == DType::kF64 ? "%llu:%.17g " : "%llu:%.9g ";
   char tmp[64];
   for (uint64_t i = 0; i < n; ++i) {
     const double v = elem(a, i);
     if (v == 0.0) continue;
-    const int len = std::snprintf(tmp, sizeof(tmp), "%llu:%.9g ", (unsigned long long)i, v);
-    buf.append(tmp, len);
-    if (buf.size() > (1u << 20) - 64) {
-      o << buf;
-      buf.clear();
+    const int len = std::snprintf(tmp, sizeof(tmp), fmt, (unsigned long long)(next_ + i), v);
+    buf_.append(tmp, len);
+    if (buf_.size() > (1u << 20) - 64) {
+      *out_ << buf_;
+      buf_.clear();
     }
   }
-  o << buf;
-  o.close();
-  MINIPS_CHECK(o.good(), "write failed: " << path);
+  next_ += n;
+}
+
+void TextParamsWriter::Close() {
+  if (!out_) return;
+  *out_ << buf_;
+  buf_.clear();
+  out_->close();
+  const bool ok = out_->good();
+  out_.reset();
+  MINIPS_CHECK(ok, "write failed: " << path_);
+}
+
+void WriteTextParams(const std::string& path, const ArrayRef& a) {
+  TextParamsWriter w(path);
+  w.Append(a);
+  w.Close();
 }
 
 std::vector<double> ReadTextParams(const std::string& path, uint64_t n) {

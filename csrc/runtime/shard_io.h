@@ -20,6 +20,10 @@
 // amplification with it).
 #pragma once
 
+#include <memory>
+
+#include "fs.h"
+
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -104,6 +108,22 @@ class ShardFileWriter {
 };
 // Reference text format of one array: "<local_idx>:<val> " for non-zero entries, one line.
 void WriteTextParams(const std::string& path, const ArrayRef& a);
+// The same format written in pieces (a shard streamed through the checkpoint ring): every
+// Append continues the running element index; any FileSystem URL (local, webhdfs://, hdfs://).
+class TextParamsWriter {
+ public:
+  explicit TextParamsWriter(const std::string& path);
+  ~TextParamsWriter();
+  void Append(const ArrayRef& a);
+  void Close();
+  uint64_t Elements() const { return next_; }
+
+ private:
+  std::string path_;
+  std::unique_ptr<GeneralOfstream> out_;
+  std::string buf_;
+  uint64_t next_ = 0;
+};
 // Parses the text format back into a dense vector of `n` values (missing entries = 0).
 std::vector<double> ReadTextParams(const std::string& path, uint64_t n);
 

@@ -11,6 +11,10 @@ text formats:
                                    with per-array file offsets + fp32 shard + optimizer state
   server_params_<id>_t<table>      reference text format "<local_idx>:<val> " of the non-zero
                                    parameters (vector_storage.hpp:54-73), shards up to text_limit
+                                   values (text_limit < 0: every shard; streamed from the same
+                                   ring chunks as the binary file, so any size)
+After a commit, ``<prefix>server_params_<id>`` / ``server_progress_<id>`` / ``worker_config_<id>``
+(the reference's flat names; table k > 0 as ``..._t<k>``) link into the committed iteration.
   server_progress_<id>_t<table>    "min_clock:<c> <tid>:<c> ..." (progress_tracker.hpp:68-85),
                                    exact clocks (no RoundHundred), tids in SimpleIdMapper layout
   worker_config_<id>               "<worker_id>:<iteration> " (svm_dumper.hpp:51-66)
@@ -213,19 +217,24 @@ class Checkpointer:
         base = f"server_params_{self.my_id}_t{tid}"
         desc = [(n, _DT[a.dtype], a.shape[0], a.shape[1]) for n, a in arrs.items()]
         w = runtime().ShardFileWriter(_prefix_path(out, base + ".bin"), meta, desc)
-        for k, (name, a) in enumerate(arrs.items()):
-            if host_ready or not a.is_cuda:
-                self._write_host_array(w, k, a)
-            else:
-                self._stream_array(w, k, a)
-        w.close()
         first = next(iter(arrs.values()), None)
         n_vals = first.numel() if first is not None else 0
-        if host_ready and first is not None and n_vals <= self.text_limit and meta["kind"] != "hash":
-            runtime().write_text_params(_prefix_path(out, base), first.data_ptr(), _DT[first.dtype],
-                                        first.shape[0], first.shape[1])
+        # the reference text file of the parameters, fed from the same chunks as the binary file
+        # (no extra host copy, any shard size); text_limit < 0 writes it for every shard
+        want_text = first is not None and meta["kind"] != "hash" and (self.text_limit < 0 or
+                                                                       n_vals <= self.text_limit)
+        text = runtime().TextParamsWriter(_prefix_path(out, base)) if want_text else None
+        for k, (name, a) in enumerate(arrs.items()):
+            tw = text if k == 0 else None
+            if host_ready or not a.is_cuda:
+                self._write_host_array(w, k, a, tw)
+            else:
+                self._stream_array(w, k, a, tw)
+        w.close()
+        if text is not None:
+            text.close()
 
-    def _write_host_array(self, w, k: int, a: torch.Tensor):
+    def _write_host_array(self, w, k: int, a: torch.Tensor, text=None):
         """Host-resident array: written in ring-sized pieces (a CPU table streams through the ring
         so it never needs a second whole-shard host copy)."""
         if a.shape[0] == 0:
@@ -236,8 +245,10 @@ class Checkpointer:
         for r0 in range(0, a.shape[0], step):
             n = min(step, a.shape[0] - r0)
             w.write_rows(k, r0, a[r0:].data_ptr(), n)
+            if text is not None:
+                text.append(a[r0:].data_ptr(), _DT[a.dtype], n, a.shape[1])
 
-    def _stream_array(self, w, k: int, a: torch.Tensor):
+    def _stream_array(self, w, k: int, a: torch.Tensor, text=None):
         """Device array -> file through the two-slot pinned ring: the D2H of chunk i+1 runs on
         the checkpoint stream while chunk i is written."""
         rows = a.shape[0]
@@ -247,6 +258,12 @@ class Checkpointer:
         slots = self._ring_slots(rb)
         step = max(1, slots[0].numel() // rb)
         prev = None
+
+        def put(p_r0, p_n, p_dst):
+            w.write_rows(k, p_r0, p_dst.data_ptr(), p_n)
+            if text is not None:
+                text.append(p_dst.data_ptr(), _DT[a.dtype], p_n, a.shape[1])
+
         for i, r0 in enumerate(range(0, rows, step)):
             n = min(step, rows - r0)
             dst = slots[i % 2][: n * rb].view(a.dtype).view(n, a.shape[1])
@@ -257,11 +274,11 @@ class Checkpointer:
             if prev is not None:
                 p_ev, p_r0, p_n, p_dst = prev
                 p_ev.synchronize()
-                w.write_rows(k, p_r0, p_dst.data_ptr(), p_n)
+                put(p_r0, p_n, p_dst)
             prev = (ev, r0, n, dst)
         p_ev, p_r0, p_n, p_dst = prev
         p_ev.synchronize()
-        w.write_rows(k, p_r0, p_dst.data_ptr(), p_n)
+        put(p_r0, p_n, p_dst)
 
     def try_commit(self) -> bool:
         """Publish the in-flight checkpoint if every rank's background writer has finished
@@ -301,6 +318,36 @@ class Checkpointer:
 
                     shutil.rmtree(self.iter_dir(old), ignore_errors=True)
         self.comm.barrier()
+        self._link_reference_names(it)
+
+    def _link_reference_names(self, it: int):
+        """The reference's flat names (<prefix>server_params_<my_id>, server_progress_<my_id>,
+        worker_config_<my_id>; vector_storage.hpp:54-73, progress_tracker.hpp:68-85,
+        svm_dumper.hpp:51-66) as symlinks into the committed iteration: table 0 keeps the plain
+        name, table k > 0 gets "_t<k>". Swapped atomically (symlink + rename), local prefixes only."""
+        src = self.iter_dir(it)
+        pdir = os.path.dirname(self.prefix) or "."
+        names = [(f"worker_config_{self.my_id}", f"worker_config_{self.my_id}")]
+        for f in sorted(glob.glob(glob.escape(src) + f"server_p*_{self.my_id}_t*")):
+            name = os.path.basename(f)
+            if name.endswith(".bin"):
+                continue
+            stem, tid = name.rsplit("_t", 1)
+            names.append((name, stem if tid == "0" else name))
+        for have, ref in names:
+            target = os.path.join(src, have)
+            if not os.path.exists(target):
+                continue
+            link = self.prefix + ref
+            tmp = link + f".lnk{os.getpid()}"
+            try:
+                os.symlink(os.path.relpath(target, pdir), tmp)
+                os.replace(tmp, link)
+            except OSError:
+                try:
+                    os.unlink(tmp)
+                except OSError:
+                    pass
 
     def abandon(self):
         """In-place rollback: finish the local writer, drop the uncommitted checkpoint (its commit

@@ -40,6 +40,9 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--checkpoint_toggle", type=_flag_bool, default=False)
     ap.add_argument("--checkpoint_file_prefix", default="/tmp/minips_ckpt/")
+    ap.add_argument("--checkpoint_text_limit", type=int, default=1 << 22,
+                    help="write the reference text file (<idx>:<val>) for shards of up to this many values "
+                    "(-1: every shard, streamed); the binary sidecar is always written")
     ap.add_argument("--checkpoint_every", type=int, default=100)
     ap.add_argument("--use_weight_file", type=_flag_bool, default=False)
     ap.add_argument("--heartbeat_interval", type=float, default=0.0)
@@ -387,7 +390,7 @@ def main(argv=None):
             inplace = False  # a sub-group job restarts as a whole (its ranks are a subset)
     model, tables, make_data, step_fn, per_step = build(args, comm)
     data = make_data()
-    ck = Checkpointer(comm, args.checkpoint_file_prefix)
+    ck = Checkpointer(comm, args.checkpoint_file_prefix, text_limit=args.checkpoint_text_limit)
     start = 0
     if args.use_weight_file and not ck.exists():
         # a restart before the first committed checkpoint (or with checkpoint_toggle off): there

@@ -195,3 +195,49 @@ def test_bucketed_dense_checkpoint_is_canonical(tmp_path, restore_world, buckete
     out = run_world(_GptLoad(prefix, bucketed), world=restore_world)
     for r, (full, step, has_m) in out.items():
         assert full == full0 and step == 2 and has_m
+
+
+def _save_text(rank, world, prefix):
+    from minips_amd.ps.checkpoint import Checkpointer
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.tables import DenseTable, SparseTable
+
+    comm = Comm(device=torch.device("cpu"))
+    dense = DenseTable(comm, 1001, optimizer="add", value_dtype=torch.float64)
+    dense.load_full(torch.arange(1001, dtype=torch.float64) / 3.0)  # needs 17 digits to round-trip
+    sparse = SparseTable(comm, num_rows=N_ROWS, width=W, optimizer="rowwise_adagrad", pull_dtype=torch.float32,
+                         init_std=0.0, route="range")
+    rows = torch.arange(sparse.base, sparse.base + sparse.rows_local, dtype=torch.float32)
+    sparse.shard.copy_(rows[:, None] * 10 + torch.arange(W, dtype=torch.float32) + 1)
+    ck = Checkpointer(comm, prefix, ring_bytes=RING, text_limit=-1)  # text for every shard, streamed
+    ck.save({0: dense, 1: sparse}, iteration=3, blocking=True)
+    return dense.master.clone(), sparse.shard.reshape(-1).clone()
+
+
+class _SaveText:
+    def __init__(self, prefix):
+        self.prefix = prefix
+
+    def __call__(self, rank, world):
+        return _save_text(rank, world, self.prefix)
+
+
+def test_streamed_text_checkpoint_and_reference_names(tmp_path):
+    """text_limit=-1: the reference text file is written for every shard from the ring chunks
+    (RING forces many chunks; indices continue across them, fp64 keeps 17 digits), and the
+    reference's flat names <prefix>server_params_<id> / server_progress_<id> / worker_config_<id>
+    point into the committed iteration."""
+    from minips_amd.ps.checkpoint import load_text_params
+
+    prefix = str(tmp_path / "ck_")
+    out = run_world(_SaveText(prefix), world=2)
+    for r in range(2):
+        dense_master, sparse_flat = out[r]
+        got = load_text_params(f"{prefix}server_params_{r}", dense_master.numel()).to(torch.float64)
+        assert torch.equal(got, dense_master)  # exact fp64 round trip through the text
+        got1 = load_text_params(f"{prefix}server_params_{r}_t1", sparse_flat.numel()).float()
+        assert torch.equal(got1, sparse_flat)
+        assert os.path.islink(f"{prefix}server_params_{r}")
+        assert os.path.realpath(f"{prefix}server_params_{r}").endswith(f"iter_3/server_params_{r}_t0")
+        assert open(f"{prefix}server_progress_{r}").read().startswith("min_clock:")
+        assert open(f"{prefix}worker_config_{r}").read().strip()
