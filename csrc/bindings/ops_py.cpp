@@ -773,7 +773,7 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& O, const at::Tensor& dO, 
 }
 
 void hash_slots(at::Tensor& tab_keys, const at::Tensor& q, at::Tensor& slots, at::Tensor& vals, double init_scale,
-                int64_t seed, at::Tensor& counters) {
+                int64_t seed, at::Tensor& counters, const c10::optional<at::Tensor>& n_dev) {
   for (const at::Tensor* t : {(const at::Tensor*)&tab_keys, &q, (const at::Tensor*)&slots, (const at::Tensor*)&vals,
                               (const at::Tensor*)&counters})
     check_gpu(*t, "hash arg");
@@ -787,7 +787,7 @@ void hash_slots(at::Tensor& tab_keys, const at::Tensor& q, at::Tensor& slots, at
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   minips_k::hash_slots(reinterpret_cast<unsigned long long*>(tab_keys.data_ptr()), tab_keys.numel(), ptr<int64_t>(q),
                        q.numel(), ptr<int64_t>(slots), ptr<float>(vals), (int)vals.size(1), (float)init_scale,
-                       (uint64_t)seed, ptr<int>(counters), stream_of(q));
+                       (uint64_t)seed, ptr<int>(counters), stream_of(q), count_ptr(n_dev));
 }
 
 void hash_rehash(const at::Tensor& old_keys, const at::Tensor& old_vals, const c10::optional<at::Tensor>& old_state,
@@ -1007,7 +1007,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("scatter_add_rows", &scatter_add_rows);
   m.def("lookup_rows", &lookup_rows);
   m.def("embed_fwd", &embed_fwd);
-  m.def("hash_slots", &hash_slots);
+  m.def("hash_slots", &hash_slots, py::arg("tab_keys"), py::arg("q"), py::arg("slots"), py::arg("vals"),
+        py::arg("init_scale"), py::arg("seed"), py::arg("counters"), py::arg("n_dev") = py::none());
   m.def("hash_rehash", &hash_rehash);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

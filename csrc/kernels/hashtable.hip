@@ -27,15 +27,19 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 }
 
 __global__ void hash_slots_kernel(unsigned long long* __restrict__ tab_keys, int64_t cap, const int64_t* __restrict__ q,
-                                  int64_t n, int64_t* __restrict__ slots, float* __restrict__ vals, int W,
-                                  float init_scale, uint64_t seed, int* __restrict__ counters) {
+                                  int64_t n, const int64_t* __restrict__ n_dev, int64_t* __restrict__ slots,
+                                  float* __restrict__ vals, int W, float init_scale, uint64_t seed,
+                                  int* __restrict__ counters) {
   const int64_t mask = cap - 1;
+  // n_dev: the valid prefix of q is known only on the device (a dedupe's unique count): the
+  // entries past it are left alone (slot -1) -- no host sync to trim q
+  const int64_t n_valid = n_dev ? min(n, *n_dev) : n;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long k = (unsigned long long)q[i];
     int64_t s = (int64_t)(mix64(k) & (uint64_t)mask);
-    int64_t found = -1;
+    int64_t found = i < n_valid ? -1 : -2;
     bool inserted = false;
-    for (int64_t probe = 0; probe < cap; ++probe) {
+    for (int64_t probe = 0; found == -1 && probe < cap; ++probe) {
       const unsigned long long cur = tab_keys[s];
       if (cur == k) {
         found = s;
@@ -66,13 +70,13 @@ __global__ void hash_slots_kernel(unsigned long long* __restrict__ tab_keys, int
     }
     // wave-aggregated counters: one atomic per wave, not one per inserted key (same-address
     // atomics serialise at the memory side)
-    const unsigned long long ins = __ballot(inserted), full = __ballot(found < 0);
+    const unsigned long long ins = __ballot(inserted), full = __ballot(found == -1);
     const int leader = __ffsll((long long)__ballot(1)) - 1;
     if ((threadIdx.x & 63) == leader) {
       if (ins) atomicAdd(counters, __popcll(ins));
       if (full) atomicAdd(counters + 1, __popcll(full));  // table full
     }
-    slots[i] = found;
+    slots[i] = found < 0 ? -1 : found;
   }
 }
 
@@ -98,11 +102,11 @@ __global__ void hash_rehash_kernel(const unsigned long long* __restrict__ old_ke
 }
 
 void hash_slots(unsigned long long* tab_keys, int64_t cap, const int64_t* q, int64_t n, int64_t* slots, float* vals,
-                int W, float init_scale, uint64_t seed, int* counters, hipStream_t s) {
+                int W, float init_scale, uint64_t seed, int* counters, hipStream_t s, const int64_t* n_dev) {
   if (n <= 0) return;
   if (cap <= 0 || (cap & (cap - 1))) throw std::runtime_error("hash table capacity must be a power of two");
-  hipLaunchKernelGGL(hash_slots_kernel, grid_for(n, 256, 4096), 256, 0, s, tab_keys, cap, q, n, slots, vals, W,
-                     init_scale, seed, counters);
+  hipLaunchKernelGGL(hash_slots_kernel, grid_for(n, 256, 4096), 256, 0, s, tab_keys, cap, q, n, n_dev, slots, vals,
+                     W, init_scale, seed, counters);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -186,8 +186,9 @@ void gelu_bwd(const bf16_t* dh, const bf16_t* u, int64_t n, bf16_t* du, hipStrea
 void add_bf16(const bf16_t* a, const bf16_t* b, int64_t n, bf16_t* out, hipStream_t s);
 // GPU hash-table shard (hashtable.hip): tab_keys EMPTY = ~0; counters[0] += inserts,
 // counters[1] += failed lookups (table full); slot -1 for those.
+// n_dev (optional, device int64): only q[0, *n_dev) are looked up / inserted; the rest get slot -1.
 void hash_slots(unsigned long long* tab_keys, int64_t cap, const int64_t* q, int64_t n, int64_t* slots, float* vals,
-                int W, float init_scale, uint64_t seed, int* counters, hipStream_t s);
+                int W, float init_scale, uint64_t seed, int* counters, hipStream_t s, const int64_t* n_dev = nullptr);
 void hash_rehash(const unsigned long long* old_keys, const float* old_vals, const float* old_state, int64_t old_cap,
                  unsigned long long* new_keys, float* new_vals, float* new_state, int64_t new_cap, int W, int* counters,
                  hipStream_t s);

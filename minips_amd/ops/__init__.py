@@ -725,12 +725,17 @@ def _mix64_int(x: int) -> int:
     return x
 
 
-def hash_slots(tab_keys, q, slots, vals, init_scale, seed, counters):
+def hash_slots(tab_keys, q, slots, vals, init_scale, seed, counters, n_dev=None):
     """Lookup-or-insert of q in the open-addressing table (EMPTY = -1), linear probing from
-    mix64(key); new rows are zero or uniform[-a, a) from mix64(key*golden + seed + c)."""
+    mix64(key); new rows are zero or uniform[-a, a) from mix64(key*golden + seed + c). With
+    ``n_dev`` (device int64 count) only q[:n_dev] is resolved; the rest get slot -1."""
     if _gpu(q):
-        kernels().hash_slots(tab_keys, q, slots, vals, float(init_scale), int(seed), counters)
+        kernels().hash_slots(tab_keys, q, slots, vals, float(init_scale), int(seed), counters, n_dev)
         return slots
+    if n_dev is not None:
+        n = int(n_dev.reshape(-1)[0])
+        slots[n:] = -1
+        q, slots = q[:n], slots[:n]
     cap = tab_keys.numel()
     W = vals.shape[1]
     tk = tab_keys.tolist()

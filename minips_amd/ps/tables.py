@@ -971,9 +971,15 @@ class HashSparseTable(SparseTable):
     mixed by a bijection and range-partitioned over the ranks; each rank stores its keys in a GPU
     open-addressing hash table (csrc/kernels/hashtable.hip) whose rows are created on first
     touch -- zero (MapStorage's default-insert) or a deterministic per-key uniform init -- and
-    grows (rehash, doubling) past 70% load. The Get/Add/Clock protocol is SparseTable's."""
+    grows (rehash, doubling) past 70% load. The Get/Add/Clock protocol is SparseTable's.
 
-    _exact_counts = True
+    No host sync on the hot path: the lookups take the dedupe's device-side unique count (the
+    kernel resolves only that prefix), the growth check runs against a host-side upper bound of
+    the size (inserts so far <= keys submitted) and reads the device counters only when that
+    bound crosses the load limit, and the key-range check (keys < 2^63) and the table-full flag
+    are read at those same sync points (or drain / size())."""
+
+    _exact_counts = False
 
     def __init__(self, comm: Comm, width: int, capacity: int = 1 << 16, optimizer: str = "add", lr: float = 0.01,
                  eps: float = 1e-8, pull_dtype=torch.float32, consistency: str = "bsp", staleness: int = 0,
@@ -998,6 +1004,8 @@ class HashSparseTable(SparseTable):
         cap = 1 << max(4, int(capacity - 1).bit_length())
         self._alloc(cap)
         self.counters = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._size_ub = 0  # host-side upper bound of the occupied slots
+        self._neg = None   # device flag: a negative (>= 2^63 unsigned) key was seen
         self._init_comm(consistency, staleness, p2p)
 
     def _alloc(self, cap: int):
@@ -1010,25 +1018,41 @@ class HashSparseTable(SparseTable):
         self.state2 = None
 
     def _route_keys(self, keys):
-        if bool((keys < 0).any()):
+        if keys.is_cuda:  # checked at the next sync point (no host round trip per batch)
+            neg = (keys < 0).any()
+            self._neg = neg if self._neg is None else (self._neg | neg)
+        elif bool((keys < 0).any()):
             raise ValueError("HashSparseTable keys must be in [0, 2^63)")
         return mix63(keys)
 
-    def size(self) -> int:
-        return int(self.counters[0].item())
+    def _sync_counters(self) -> int:
+        """One host read of the device counters (+ the deferred checks); returns the size."""
+        size, full = (int(v) for v in self.counters.tolist())
+        if self._neg is not None:
+            neg, self._neg = bool(self._neg), None
+            if neg:
+                raise ValueError("HashSparseTable keys must be in [0, 2^63)")
+        if full:
+            raise RuntimeError("hash table full")
+        self._size_ub = size
+        return size
 
-    def _slots(self, keys: torch.Tensor, grow: bool = True) -> torch.Tensor:
-        """Lookup-or-insert. ``grow=False``: the keys are known to be present (no insert, no
-        growth check, no host sync) -- safe inside side-stream clock work."""
+    def size(self) -> int:
+        return self._sync_counters()
+
+    def _slots(self, keys: torch.Tensor, grow: bool = True, n_dev=None) -> torch.Tensor:
+        """Lookup-or-insert of keys[:n_dev] (n_dev: device count, None = all). ``grow=False``:
+        the keys are known to be present (no insert, no growth check) -- safe inside side-stream
+        clock work."""
         need = keys.numel()
         if need == 0:
             return torch.empty(0, dtype=torch.int64, device=keys.device)
-        if grow and (self.size() + need) > 0.7 * self.capacity:
-            self._grow(max(self.capacity * 2, 1 << int(math.ceil(math.log2((self.size() + need) / 0.5)))))
+        if grow:
+            if self._size_ub + need > 0.7 * self.capacity and self._sync_counters() + need > 0.7 * self.capacity:
+                self._grow(max(self.capacity * 2, 1 << int(math.ceil(math.log2((self._size_ub + need) / 0.5)))))
+            self._size_ub += need
         slots = torch.empty(need, dtype=torch.int64, device=keys.device)
-        ops.hash_slots(self.tab_keys, keys, slots, self.shard, self.init_scale, self.seed, self.counters)
-        if grow and int(self.counters[1].item()):
-            raise RuntimeError("hash table full")
+        ops.hash_slots(self.tab_keys, keys, slots, self.shard, self.init_scale, self.seed, self.counters, n_dev=n_dev)
         return slots
 
     def _grow(self, new_cap: int):
@@ -1041,14 +1065,25 @@ class HashSparseTable(SparseTable):
         cnt = torch.zeros(2, dtype=torch.int32, device=self.comm.device)
         ops.hash_rehash(old[0], old[1], old[2], self.tab_keys, self.shard, self.state, cnt)
         self.counters[0] = cnt[0]
+        self.counters[1] = 0
         if self.pipe.stream is not None:
             for t in old:
                 if t is not None:
                     t.record_stream(self.pipe.stream)
 
+    def _own_n_dev(self, plan):
+        """Device count of the valid owned unique keys of ``plan`` (None: all are valid)."""
+        if plan is None:
+            return None
+        if self.comm.world == 1:
+            return plan.U_dev
+        return None if "own_U" in plan.extra else plan.own_U_dev
+
     def _serve_index(self, plan):
-        slots = self._slots(plan.recv_keys)  # insert-on-miss: unseen keys get their initial row
+        # insert-on-miss: unseen keys get their initial row (one rank: the unique prefix only)
+        slots = self._slots(plan.recv_keys, n_dev=plan.U_dev if self.comm.world == 1 else None)
         plan.extra["served_slots"] = slots
+        plan.extra["served_cap"] = self.capacity
         return self.shard, slots, 0
 
     def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
@@ -1056,7 +1091,12 @@ class HashSparseTable(SparseTable):
         may run on the pipe stream, where a table growth must never happen."""
         keys = self._owner_keys(plan)
         if keys is not None and "own_slots" not in plan.extra:
-            plan.extra["own_slots"] = self._slots(keys)
+            served = plan.extra.get("served_slots")
+            if served is not None and self.comm.world == 1 and plan.extra.get("served_cap") == self.capacity:
+                plan.extra["own_slots"] = served  # one rank: the pushed keys ARE the served keys
+            else:
+                # keys served by this plan's Get are present already: a lookup, no growth check
+                plan.extra["own_slots"] = self._slots(keys, grow=served is None, n_dev=self._own_n_dev(plan))
             plan.extra["own_cap"] = self.capacity
         super().add(plan, grad_rows)
 
@@ -1065,8 +1105,13 @@ class HashSparseTable(SparseTable):
         if slots is None or self.capacity != plan.extra.get("own_cap"):
             # the table grew after add() (a rehash moves rows): the keys are present, so a
             # lookup-only probe re-resolves them without any growth on this stream
-            slots = self._slots(keys, grow=False)
+            slots = self._slots(keys, grow=False, n_dev=self._own_n_dev(plan))
         return slots, 0
+
+    def drain(self):
+        super().drain()
+        if self.counters.is_cuda:
+            self._sync_counters()  # surface a deferred key-range / table-full error
 
     # -- checkpoint hooks: (key, row, state) triples of the occupied slots, sorted by key ------
     def shard_state(self):
