@@ -61,3 +61,42 @@ def test_lr_checkpoint_files(tmp_path):
     prog = open(ck + "server_progress_0").read()
     assert prog.startswith("min_clock:")
     assert open(ck + "worker_config_0").read().strip()
+
+
+def test_cluster_layout_parsing():
+    from minips_amd.launch import cluster_layout, expand_nodelist, expand_tasks_per_node
+
+    assert expand_nodelist("gpu[01-03,07],login1") == ["gpu01", "gpu02", "gpu03", "gpu07", "login1"]
+    assert expand_tasks_per_node("2(x3),1", 4) == [2, 2, 2, 1]
+    me, nodes = cluster_layout({"SLURM_PROCID": "3", "SLURM_JOB_NODELIST": "n[1-2]", "SLURM_TASKS_PER_NODE": "2(x2)"},
+                               100)
+    assert me == 3 and nodes == [(0, "n1", 100), (1, "n1", 101), (2, "n2", 100), (3, "n2", 101)]
+    me, nodes = cluster_layout({"JOB_COMPLETION_INDEX": "2", "MINIPS_HOSTS": "p-0.svc,p-1.svc,p-2.svc"}, 7)
+    assert me == 2 and nodes[2] == (2, "p-2.svc", 7)
+
+
+def test_lr_via_simulated_slurm_steps(tmp_path):
+    """The cluster verb (YARN-client/AM analogue) inside two simulated Slurm tasks on this host:
+    each task derives its id and the same hostfile from SLURM_* and runs its node of the LR app."""
+    import subprocess
+    import sys
+
+    from _util import ROOT, free_ports
+
+    port = free_ports(1)[0]
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, SLURM_PROCID=str(rank), SLURM_JOB_NODELIST="localhost", SLURM_TASKS_PER_NODE="2",
+                   SLURM_JOB_ID="t1")
+        cmd = [sys.executable, "-m", "minips_amd.launch", "--app", "lr", "--start-port", str(port),
+               "--hostfile-out", str(tmp_path / f"hosts_{rank}"), "--log-dir", str(tmp_path / "logs"), "cluster",
+               "--num_workers_per_node=2", "--num_iters=150", "--batch_size=20", "--num_dims=3000",
+               "--kModelType=BSP", "--alpha=0.5"]
+        procs.append(subprocess.Popen(cmd, cwd=ROOT, env=env))
+    rcs = [p.wait(timeout=180) for p in procs]
+    assert rcs == [0, 0]
+    assert open(tmp_path / "hosts_0").read() == open(tmp_path / "hosts_1").read() == \
+        f"0:localhost:{port}\n1:localhost:{port + 1}\n"
+    for i in range(2):
+        with open(tmp_path / "logs" / f"node_{i}.log") as f:
+            assert json.loads([l for l in f if l.startswith("{")][-1])["accuracy"] > 0.8
