@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "../runtime/checkpoint.h"
+#include "../runtime/clock_board.h"
 #include "../runtime/fs.h"
 #include "../runtime/io.h"
 #include "../runtime/comm.h"
@@ -395,6 +396,17 @@ PYBIND11_MODULE(_runtime, m) {
   });
   m.def("remote_bytes_read", &RemoteBytesRead);
   m.def("local_host_name", &LocalHostName);
+  py::class_<ClockBoard>(m, "ClockBoard")
+      .def(py::init<const std::string&, int, int, bool, double>(), py::arg("name"), py::arg("world"), py::arg("rank"),
+           py::arg("create"), py::arg("attach_timeout_s") = 30.0)
+      .def("publish", &ClockBoard::Publish)
+      .def("get", &ClockBoard::Get)
+      .def("min_clock", &ClockBoard::MinClock)
+      .def("snapshot", &ClockBoard::Snapshot)
+      .def("wait_min_at_least", &ClockBoard::WaitMinAtLeast, py::arg("target"), py::arg("timeout_s") = 0.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("wakeups", &ClockBoard::Wakeups)
+      .def("unlink", &ClockBoard::Unlink);
   py::class_<BlockAssignerServer>(m, "BlockAssignerServer")
       .def(py::init<int>(), py::arg("port") = 0)
       .def("start", &BlockAssignerServer::Start)

@@ -15,6 +15,7 @@
 #include <fstream>
 
 #include "../runtime/checkpoint.h"
+#include "../runtime/clock_board.h"
 #include "../runtime/comm.h"
 #include "../runtime/config.h"
 #include "../runtime/engine.h"
@@ -1155,6 +1156,42 @@ TEST(FS, UrlsAndGeneralStreams) {
   std::string why;
   if (!LibHdfs3Available(&why)) EXPECT_TRUE(why.find("webhdfs://") != std::string::npos);
   ::unlink(ParseUrl(p).path.c_str());
+}
+
+TEST(ClockBoard, SspGateWakesOnPublishAndTimesOut) {
+  // Two ranks' views of one segment (as two processes map it): rank 0 waits for min clock >= 3
+  // while rank 1 publishes 1, 2, 3; the wait returns only after the last publish. A stuck clock
+  // makes the gate throw after its timeout instead of hanging.
+  using namespace minips;
+  const std::string name = "minips_cb_test_" + std::to_string(::getpid());
+  ClockBoard r0(name, 2, 0, true), r1(name, 2, 1, false);
+  r0.Publish(5);
+  EXPECT_EQ(r1.Get(0), 5);
+  EXPECT_EQ(r0.MinClock(), 0);
+  std::atomic<int> published{0};
+  std::thread pub([&] {
+    for (int c = 1; c <= 3; ++c) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      published = c;
+      r1.Publish(c);
+    }
+  });
+  const double waited = r0.WaitMinAtLeast(3, 10.0);
+  EXPECT_EQ(published.load(), 3);
+  EXPECT_TRUE(waited > 0.03);
+  EXPECT_EQ(r0.MinClock(), 3);
+  pub.join();
+  bool threw = false;
+  try {
+    r0.WaitMinAtLeast(9, 0.05);
+  } catch (const CheckError&) {
+    threw = true;
+  }
+  EXPECT_TRUE(threw);
+  std::vector<int64_t> snap = r1.Snapshot();
+  EXPECT_EQ(snap[0], 5);
+  EXPECT_EQ(snap[1], 3);
+  r0.Unlink();
 }
 
 int main(int argc, char** argv) { return minitest::RunAll(argc, argv); }

@@ -13,7 +13,8 @@ This table gets the same semantics with NO collective on the data path:
 * Get = direct gather of the requested rows from their owners' HBM; Add + Clock = atomic
   scatter-add into the owners' rows (``add``: w += delta, the reference SubAdd; ``sgd``:
   w -= lr * g, the ASP async SGD of the DLRM config) -- the owner does nothing;
-* progress: a clock vector in host shared memory (/dev/shm, one slot per rank). A rank
+* progress: a clock vector in host shared memory (/dev/shm, one slot per rank; the native
+  csrc/runtime/clock_board.h, futex wake-ups). A rank
   publishes clock c+1 only after its clock-c adds completed on the GPU (a publisher thread
   waits on the event recorded after them), so a reader that sees clock c+1 sees those adds.
 * SSP gate (a Get at own clock c): wait until min over ranks >= c - staleness -- the
@@ -25,7 +26,6 @@ a per-owner file lock around the scatter-add in place of the GPU atomics.
 from __future__ import annotations
 
 import fcntl
-import mmap
 import os
 import queue
 import threading
@@ -43,9 +43,13 @@ from .tables import even_bounds
 
 
 class ClockBoard:
-    """Per-rank clocks in a /dev/shm segment shared by the ranks of one node."""
+    """Per-rank clocks in a /dev/shm segment shared by the ranks of one node: the native board
+    (csrc/runtime/clock_board.h -- one cache line per rank, release stores, a futex the SSP gate
+    sleeps on instead of polling from Python)."""
 
     def __init__(self, comm: Comm, name: str | None = None):
+        from .._native import runtime
+
         self.comm = comm
         self.world, self.rank = comm.world, comm.rank
         if name is None:
@@ -55,36 +59,28 @@ class ClockBoard:
                 dist.broadcast_object_list(box, src=0, group=comm.group)
                 name = box[0]
         self.path = os.path.join("/dev/shm", name)
-        nbytes = 8 * max(1, self.world)
-        fd = os.open(self.path, os.O_RDWR | os.O_CREAT, 0o600)
-        try:
-            if os.fstat(fd).st_size < nbytes:
-                os.ftruncate(fd, nbytes)
-            self._mm = mmap.mmap(fd, nbytes)
-        finally:
-            os.close(fd)
-        self.clocks = np.frombuffer(self._mm, dtype=np.int64, count=self.world)
         self.owner = comm.rank == 0
+        self._b = runtime().ClockBoard(name, max(1, self.world), self.rank, self.owner)
 
     def publish(self, clock: int):
-        self.clocks[self.rank] = clock  # an aligned 8-byte store: readers see old or new, never torn
+        self._b.publish(int(clock))
+
+    def get(self, rank: int) -> int:
+        return self._b.get(rank)
 
     def min_clock(self) -> int:
-        return int(self.clocks.min())
+        return self._b.min_clock()
+
+    def wait_min(self, target: int, timeout_s: float = 0.0) -> float:
+        """Block (GIL released, futex sleep) until min clock >= target; returns seconds waited."""
+        return self._b.wait_min_at_least(int(target), float(timeout_s))
 
     def snapshot(self) -> list:
-        return [int(c) for c in self.clocks]
+        return list(self._b.snapshot())
 
     def close(self):
-        try:
-            self._mm.close()
-        except (BufferError, ValueError):
-            pass
         if self.owner:
-            try:
-                os.unlink(self.path)
-            except FileNotFoundError:
-                pass
+            self._b.unlink()
 
 
 @dataclass
@@ -168,6 +164,9 @@ class OneSidedSparseTable:
             g.manual_seed(seed + 7919 * comm.rank)
             self.shard.normal_(0.0, init_std, generator=g)
         self.board = ClockBoard(comm)
+        # a straggler that never publishes again is a failure (the supervisor restarts the set),
+        # not an infinite hang of every other rank
+        self.gate_timeout_s = float(os.environ.get("MINIPS_SSP_GATE_TIMEOUT", "600"))
         self.clock_n = 0
         self._pending: list = []
         self.waited_s = 0.0
@@ -193,13 +192,7 @@ class OneSidedSparseTable:
         """SSP: a Get at own clock c waits while c > min_clock + staleness (ssp_model.cpp:58-85)."""
         c = self.clock_n
         if self.consistency == "ssp":
-            t0 = None
-            while c > self.board.min_clock() + self.staleness:
-                if t0 is None:
-                    t0 = time.perf_counter()
-                time.sleep(0.0002)
-            if t0 is not None:
-                self.waited_s += time.perf_counter() - t0
+            self.waited_s += self.board.wait_min(c - self.staleness, self.gate_timeout_s)
         self.staleness_seen.append(c - self.board.min_clock())
 
     # ------------------------------------------------------------------------------ KV API
@@ -297,7 +290,7 @@ class OneSidedSparseTable:
         """Wait until this rank's clocks are applied and published."""
         if self.cuda:
             torch.cuda.current_stream(self.comm.device).synchronize()
-            while not self._pub_q.empty() or self.board.clocks[self.comm.rank] < self.clock_n:
+            while not self._pub_q.empty() or self.board.get(self.comm.rank) < self.clock_n:
                 time.sleep(0.0005)
 
     def close(self):
