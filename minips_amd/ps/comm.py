@@ -56,7 +56,11 @@ class Comm:
     """Rank/world/device bookkeeping plus the collectives used by the tables (one ordered
     communicator per rank: see the module docstring)."""
 
-    def __init__(self, group=None, device: torch.device | None = None):
+    def __init__(self, group=None, device: torch.device | None = None, force_collectives: bool = False):
+        """``force_collectives``: run every collective through the process group even at world 1
+        (tests: the RCCL calls of the multi-rank data plane, with the tables' dtypes and layouts,
+        executed on a one-GPU box)."""
+        self.force = force_collectives
         self.initialized = dist.is_available() and dist.is_initialized()
         self.group = group
         self.rank = dist.get_rank(group) if self.initialized else 0
@@ -155,7 +159,7 @@ class Comm:
         self.stats.calls += 1
         if self.world > 1:
             self._record("a2av_p2p" if p2p else "a2av", inp, tuple(inp.shape[1:]))
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             n = send_splits[0]
             if n:
                 out[:n].copy_(inp[:n])
@@ -191,7 +195,7 @@ class Comm:
 
     def all_to_all_counts(self, recv: torch.Tensor, counts: torch.Tensor):
         """Device-side all-to-all of per-destination counts (no host sync)."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             recv.copy_(counts)
             return recv
         self._record("a2a_counts", counts, counts.numel())
@@ -207,7 +211,7 @@ class Comm:
 
     def exchange_counts(self, counts: torch.Tensor) -> tuple[list[int], list[int]]:
         """all-to-all of per-destination counts; returns (send, recv) as host lists (1 sync)."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             c = counts.tolist()
             return c, c
         recv = torch.empty_like(counts)
@@ -224,7 +228,7 @@ class Comm:
         self.stats.calls += 1
         if self.world > 1:
             self._record("reduce_scatter", inp, inp.numel())
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             out_shard.copy_(inp)
             return out_shard
         self.stats.bytes_rs += inp.numel() * inp.element_size()
@@ -241,7 +245,7 @@ class Comm:
         self.stats.calls += 1
         if self.world > 1:
             self._record("all_gather", out_full, out_full.numel())
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             if out_full.data_ptr() != shard.data_ptr():
                 out_full.copy_(shard)
             return out_full
@@ -254,7 +258,7 @@ class Comm:
         return out_full
 
     def all_reduce_(self, t: torch.Tensor, op=None):
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return t
         self._record("all_reduce", t, t.numel())
         if self._staged(t):
@@ -268,7 +272,7 @@ class Comm:
         return t
 
     def barrier(self):
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return
         t = torch.zeros(1, device=self.device)
         self.all_reduce_(t)

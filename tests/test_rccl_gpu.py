@@ -1,0 +1,92 @@
+"""The data plane's RCCL calls on real hardware. RCCL refuses two ranks on one device, so a
+one-GPU box can only run a one-rank communicator; with ``Comm(force_collectives=True)`` every
+Comm collective still goes through ProcessGroupNCCL (= RCCL) with exactly the dtypes, layouts
+and split lists the tables use at N > 1 (bf16 row all-to-all-v with uneven splits, int64 count
+exchange, fp32/fp64 reduce-scatter, in-place bf16/fp64 all-gather, MAX all-reduce of the bench's
+timer, the barrier), so a layout or dtype RCCL rejects fails here instead of in the driver's
+8-GPU scaling run."""
+import datetime
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def nccl_comm():
+    from _util import free_ports
+    from minips_amd.ps.comm import Comm
+
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_ports(1)[0]}", rank=0, world_size=1,
+                            device_id=dev, timeout=datetime.timedelta(seconds=60))
+    try:
+        assert dist.get_backend() == "nccl"
+        yield Comm(device=dev, force_collectives=True)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_table_collectives(nccl_comm):
+    comm = nccl_comm
+    dev = comm.device
+    # sparse Get / Add: rows of width 33 (32 emb + 1 wide) in bf16, and fp32 gradient rows
+    for dt in (torch.bfloat16, torch.float32):
+        inp = torch.randn(1000, 33, device=dev).to(dt)
+        out = torch.empty(1200, 33, dtype=dt, device=dev)
+        comm.all_to_all_v(out, inp, [937], [937])
+        torch.testing.assert_close(out[:937], inp[:937], rtol=0, atol=0)
+        out.zero_()
+        comm.all_to_all_v(out, inp, [937], [937], p2p=True)  # the SSP/ASP send/recv form
+        torch.testing.assert_close(out[:937], inp[:937], rtol=0, atol=0)
+    keys = torch.randint(0, 1 << 40, (500,), device=dev)
+    kout = torch.empty(500, dtype=torch.int64, device=dev)
+    comm.all_to_all_v(kout, keys, [500], [500])
+    assert torch.equal(kout, keys)
+    counts = torch.tensor([123], dtype=torch.int64, device=dev)
+    recv = torch.empty_like(counts)
+    comm.all_to_all_counts(recv, counts)
+    assert recv.item() == 123
+    assert comm.exchange_counts(counts) == ([123], [123])
+    # dense Clock: reduce-scatter of the fp32 / fp64 gradient, in-place all-gather of the params
+    for dt in (torch.float32, torch.float64):
+        g = torch.randn(4096, dtype=dt, device=dev)
+        shard = torch.empty(4096, dtype=dt, device=dev)
+        comm.reduce_scatter(shard, g)
+        torch.testing.assert_close(shard, g, rtol=0, atol=0)
+    for dt in (torch.bfloat16, torch.float64):
+        full = torch.randn(4096, device=dev).to(dt)
+        ref = full.clone()
+        comm.all_gather(full, full[:4096])  # the shard aliases its slot of the full buffer
+        torch.testing.assert_close(full, ref, rtol=0, atol=0)
+    t = torch.tensor([1.5], dtype=torch.float64, device=dev)
+    comm.all_reduce_(t, op=dist.ReduceOp.MAX)
+    assert t.item() == 1.5
+    comm.barrier()
+    assert comm.stats.calls > 0
+
+
+def test_rccl_collectives_from_side_streams(nccl_comm):
+    """Collectives issued from the planning stream and a clock stream (as the tables do) complete
+    in issue order on the one communicator."""
+    comm = nccl_comm
+    dev = comm.device
+    ps, cs = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    a = torch.arange(64 * 33, dtype=torch.float32, device=dev).view(64, 33).to(torch.bfloat16)
+    b = torch.empty_like(a)
+    g = torch.randn(1 << 16, device=dev)
+    shard = torch.empty_like(g)
+    for _ in range(5):
+        with torch.cuda.stream(ps):
+            ps.wait_stream(torch.cuda.current_stream(dev))
+            comm.all_to_all_v(b, a, [64], [64])
+        with torch.cuda.stream(cs):
+            cs.wait_stream(torch.cuda.current_stream(dev))
+            comm.reduce_scatter(shard, g)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(b, a) and torch.equal(shard, g)
