@@ -645,6 +645,21 @@ void criteo_synth(int64_t seed, int64_t step, const c10::optional<at::Tensor>& s
                          stream_of(keys));
 }
 
+void uniform_synth(int64_t seed, int64_t step, int64_t rows, at::Tensor& dense, at::Tensor& keys, at::Tensor& labels) {
+  for (const at::Tensor* t : {(const at::Tensor*)&dense, (const at::Tensor*)&keys, (const at::Tensor*)&labels})
+    check_gpu(*t, "uniform_synth arg");
+  check_dtype(keys, at::kLong, "keys");
+  check_dtype(dense, at::kFloat, "dense");
+  check_dtype(labels, at::kFloat, "labels");
+  TORCH_CHECK(keys.dim() == 2 && dense.dim() == 2 && keys.is_contiguous() && dense.is_contiguous() &&
+                  labels.is_contiguous() && keys.size(0) == labels.numel() && dense.size(0) == labels.numel(),
+              "uniform_synth shapes: keys [B, F], dense [B, n], labels [B]");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  minips_k::uniform_synth((uint64_t)seed, (uint64_t)step, keys.size(0), (int)keys.size(1), (uint64_t)rows,
+                          (int)dense.size(1), ptr<float>(dense), ptr<int64_t>(keys), ptr<float>(labels),
+                          stream_of(keys));
+}
+
 void check_ln(const at::Tensor& t, int64_t C, const char* n) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(1) >= C && t.stride(0) % 4 == 0, n,
               " must be a row-major GPU matrix with >= C columns and a leading dim % 4 == 0");
@@ -1043,6 +1058,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_split3", &kmeans_split3);
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
+  m.def("uniform_synth", &uniform_synth);
   m.def("ipc_alloc", &ipc_alloc);
   m.def("kmeans_assign_csr", &kmeans_assign_csr);
   m.def("kmeans_csr_accum", &kmeans_csr_accum);

@@ -89,4 +89,42 @@ void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// DLRM-shaped batch (BASELINE config 5): keys uniform over the whole table (multiply-high of a
+// 64-bit hash: unbiased enough, no 128-bit modulo even for 10B rows), dense N(0,1), label =
+// dense[b][0] > 0 -- the same distribution as the torch.randint / randn generator it replaces,
+// in one launch (torch's int64 randint took 228 us per DLRM batch).
+__global__ void uniform_synth_kernel(uint64_t seed, uint64_t step, int64_t B, int F, uint64_t rows, int n_dense,
+                                     float* __restrict__ dense, int64_t* __restrict__ keys,
+                                     float* __restrict__ labels) {
+  const uint64_t base = splitmix(seed * 0x632be59bd9b4e019ULL + step);
+  const int64_t nk = B * F;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nk + B; e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < nk) {
+      const uint64_t h = splitmix(base ^ ((uint64_t)e * 0xd1342543de82ef95ULL));
+      keys[e] = (int64_t)__umul64hi(h, rows);
+    } else {
+      const int64_t b = e - nk;
+      const uint64_t sb = splitmix(base ^ ((uint64_t)b * 0x9e3779b97f4a7c15ULL) ^ 0x5bd1e995ULL);
+      for (int j = 0; j < n_dense; j += 2) {
+        const float u1 = u01f(splitmix(sb + 2 * j + 1)), u2 = u01f(splitmix(sb + 2 * j + 2));
+        const float r = sqrtf(-2.f * __logf(u1));
+        float sn, cs;
+        __sincosf(6.2831853f * u2, &sn, &cs);
+        dense[b * n_dense + j] = r * cs;
+        if (j == 0) labels[b] = r * cs > 0.f ? 1.f : 0.f;
+        if (j + 1 < n_dense) dense[b * n_dense + j + 1] = r * sn;
+      }
+    }
+  }
+}
+
+void uniform_synth(uint64_t seed, uint64_t step, int64_t B, int F, uint64_t rows, int n_dense, float* dense,
+                   int64_t* keys, float* labels, hipStream_t s) {
+  if (B <= 0) return;
+  if (rows == 0 || n_dense < 1) throw std::runtime_error("uniform_synth: rows > 0 and n_dense >= 1");
+  hipLaunchKernelGGL(uniform_synth_kernel, grid_for(B * (F + 1), 256, 4096), 256, 0, s, seed, step, B, F, rows,
+                     n_dense, dense, keys, labels);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace minips_k

@@ -362,11 +362,94 @@ __global__ __launch_bounds__(kXentThreads) void softmax_xent_kernel(bf16_t* __re
   }
 }
 
+// Few classes (V <= 64, the MLP's 10): one THREAD per row -- its <= 8 chunks stay in registers,
+// neighbouring threads read neighbouring rows (coalesced), no block reductions per row. The
+// block-per-row kernel above spends a 512-thread block and three barriers on each 10-wide row
+// (143 us of the MLP's 340 us step at batch 8192).
+constexpr int kXentSmallChunks = 8;
+__global__ __launch_bounds__(256) void softmax_xent_small_kernel(bf16_t* __restrict__ logits, int ld, int64_t M,
+                                                                 int V, const int64_t* __restrict__ labels,
+                                                                 float scale, float* loss_sum, float* correct) {
+  __shared__ float red[2][4];
+  const float L2E = 1.4426950408889634f;
+  const int nch = (V + 7) >> 3;
+  float loss_acc = 0.f, hit_acc = 0.f;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < M; r += (int64_t)gridDim.x * blockDim.x) {
+    bf16_t* row = logits + r * ld;
+    uint4 v[kXentSmallChunks];
+    float mx = -3.4e38f;
+#pragma unroll
+    for (int k = 0; k < kXentSmallChunks; ++k) {
+      if (k < nch) {
+        v[k] = *reinterpret_cast<const uint4*>(row + k * 8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (k * 8 + q < V) mx = fmaxf(mx, u4elem(v[k], q));
+      }
+    }
+    const float ml2 = mx * L2E;
+    float se = 0.f, zl = 0.f;
+    const int64_t lab = labels[r];
+#pragma unroll
+    for (int k = 0; k < kXentSmallChunks; ++k) {
+      if (k < nch) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float z = u4elem(v[k], q);
+          if (k * 8 + q < V) se += __builtin_amdgcn_exp2f(z * L2E - ml2);
+          if (k * 8 + q == lab) zl = z;
+        }
+      }
+    }
+    if (lab >= 0 && lab < V) {
+      loss_acc += mx + __logf(se) - zl;
+      hit_acc += zl >= mx ? 1.f : 0.f;
+    }
+    const float sinv = scale / se;
+#pragma unroll
+    for (int k = 0; k < kXentSmallChunks; ++k) {
+      if (k < nch) {
+        uint32_t o[4];
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+          float g[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int c = k * 8 + 2 * q2 + h;
+            g[h] = c < V ? __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2 + h) * L2E - ml2) * sinv - (c == lab ? scale : 0.f)
+                         : 0.f;
+          }
+          o[q2] = pack_bf2(g[0], g[1]);
+        }
+        *reinterpret_cast<uint4*>(row + k * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+  loss_acc = warp_sum(loss_acc);
+  hit_acc = warp_sum(hit_acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][w] = loss_acc;
+    red[1][w] = hit_acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(loss_sum, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    if (correct) atomicAdd(correct, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
 void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,
                   float* correct, hipStream_t s) {
   if (M <= 0) return;
   if ((V + 7) / 8 > kXentThreads * kXentChunks || ld % 8 || ld < (V + 7) / 8 * 8)
     throw std::runtime_error("softmax_xent: V <= 53248 and ld % 8 == 0, ld >= align8(V)");
+  if (V <= 8 * kXentSmallChunks) {
+    hipLaunchKernelGGL(softmax_xent_small_kernel, (int)std::min<int64_t>((M + 255) / 256, 1024), 256, 0, s, logits,
+                       ld, M, V, labels, scale, loss_sum, correct);
+    MINIPS_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(softmax_xent_kernel, (int)std::min<int64_t>(M, 4096), kXentThreads, 0, s, logits, ld, M, V,
                      labels, scale, loss_sum, correct);
   MINIPS_HIP_CHECK(hipGetLastError());

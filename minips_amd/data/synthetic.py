@@ -106,6 +106,35 @@ def _cumsum(xs):
         yield s
 
 
+class DLRMSynth:
+    """DLRM batches (BASELINE config 5): F keys per sample uniform over the whole table, n_dense
+    N(0,1) features, label = dense[:, 0] > 0. On the GPU one fused launch (csrc/kernels/data.hip
+    uniform_synth, counter-based RNG) per batch; on the CPU the torch generator."""
+
+    def __init__(self, batch: int, F: int, num_rows: int, n_dense: int = 13, device="cpu", seed: int = 0):
+        self.batch, self.F, self.num_rows, self.n_dense = batch, F, int(num_rows), n_dense
+        self.device = torch.device(device)
+        self.seed = int(seed)
+        self._step = 0
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+
+    def next(self):
+        B = self.batch
+        if self.device.type == "cuda":
+            from .._native import kernels
+
+            dense = torch.empty(B, self.n_dense, device=self.device)
+            keys = torch.empty(B, self.F, dtype=torch.int64, device=self.device)
+            labels = torch.empty(B, device=self.device)
+            kernels().uniform_synth(self.seed, self._step, self.num_rows, dense, keys, labels)
+            self._step += 1
+            return dense, keys, labels
+        dense = torch.randn(B, self.n_dense, generator=self.gen, device=self.device)
+        keys = torch.randint(0, self.num_rows, (B, self.F), generator=self.gen, device=self.device)
+        return dense, keys, (dense[:, 0] > 0).float()
+
+
 class MnistSynth:
     """784-dim inputs in [0,1) and 10-class labels from a fixed random linear teacher."""
 

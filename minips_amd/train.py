@@ -286,14 +286,12 @@ class _Batches:
 
 class _DLRMData:
     def __init__(self, B, cfg, dev, seed):
-        self.B, self.cfg, self.dev = B, cfg, dev
-        self.g = torch.Generator(device=dev)
-        self.g.manual_seed(seed)
+        from .data.synthetic import DLRMSynth
+
+        self.gen = DLRMSynth(B, cfg.F, cfg.num_rows, cfg.n_dense, device=dev, seed=seed)
 
     def next(self):
-        dense = torch.randn(self.B, self.cfg.n_dense, generator=self.g, device=self.dev)
-        keys = torch.randint(0, self.cfg.num_rows, (self.B, self.cfg.F), generator=self.g, device=self.dev)
-        return dense, keys, (dense[:, 0] > 0).float()
+        return self.gen.next()
 
 
 class _GaussData:

@@ -66,13 +66,12 @@ def build(args, comm):
         else:
             cfg = DLRMConfig(num_rows=args.rows, consistency=args.consistency, staleness=args.staleness)
         m = DLRM(cfg, comm)
-        g = torch.Generator(device=dev)
-        g.manual_seed(r)
+        from minips_amd.data.synthetic import DLRMSynth
+
+        gen = DLRMSynth(B, cfg.F, cfg.num_rows, cfg.n_dense, device=dev, seed=r)
 
         def batch():
-            dense = torch.randn(B, cfg.n_dense, generator=g, device=dev)
-            keys = torch.randint(0, cfg.num_rows, (B, cfg.F), generator=g, device=dev)
-            return dense, keys, (dense[:, 0] > 0).float()
+            return gen.next()
 
         state = {"cur": batch()}
 
