@@ -655,8 +655,125 @@ __global__ __launch_bounds__(256) void dlrm_interact_bwd_kernel(const bf16_t* __
   }
 }
 
+// ---- MFMA interaction (NV <= 32, D in {16, 32, 64}): one wave per sample. The sample's NV x D
+// matrix (padded to 32 rows, K padded to 32) is loaded straight into MFMA fragments (16 bytes per
+// lane per fragment: row = lane & 15 of the tile, k = 8 * (lane >> 4)); Z = V V^T is three 16x16
+// tiles of v_mfma_f32_16x16x32_bf16 (the lower triangle), written as the packed pairs.
+typedef __bf16 v8bf_i __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ v8s load_frag(const bf16_t* vb, int NV, int D, int row, int k) {
+  if (row < NV && k < D) return *reinterpret_cast<const v8s*>(vb + row * D + k);
+  return v8s{0, 0, 0, 0, 0, 0, 0, 0};
+}
+
+template <int KS>  // K-steps of 32 (D = 16 -> 1 with zero padding, 32 -> 1, 64 -> 2)
+__global__ __launch_bounds__(256) void dlrm_interact_fwd_mfma_kernel(const bf16_t* __restrict__ V, int64_t B, int NV,
+                                                                     int D, int dense_idx, bf16_t* __restrict__ out,
+                                                                     int ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  if (b >= B) return;
+  const bf16_t* vb = V + b * NV * D;
+  v8s f[2][KS];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) f[t][ks] = load_frag(vb, NV, D, t * 16 + (lane & 15), ks * 32 + 8 * (lane >> 4));
+  bf16_t* ob = out + b * ldo;
+  if (lane * 8 < D) *reinterpret_cast<v8s*>(ob + lane * 8) = *reinterpret_cast<const v8s*>(vb + dense_idx * D + lane * 8);
+#pragma unroll
+  for (int tile = 0; tile < 3; ++tile) {  // (0,0), (1,0), (1,1)
+    const int ti = tile == 0 ? 0 : 1, tj = tile == 2 ? 1 : 0;
+    v4f acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf_i, f[ti][ks]),
+                                                    __builtin_bit_cast(v8bf_i, f[tj][ks]), acc, 0, 0, 0);
+    const int col = tj * 16 + (lane & 15);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = ti * 16 + (lane >> 4) * 4 + e;
+      if (row < NV && col < row) ob[D + row * (row - 1) / 2 + col] = f2bf(acc[e]);
+    }
+  }
+}
+
+// dV = dZ V with dZ the symmetric matrix of the packed pair gradients (+ the dense pass-through),
+// one wave per sample: A = dZ fragments gathered from the packed dout (row = lane & 15 of the
+// tile, 8 k's), B = V^T fragments read from the sample's V staged in LDS (column n = lane & 15,
+// 8 consecutive vector indices), 2 x (D/16) output tiles of one v_mfma_f32_16x16x32_bf16 each.
+template <int D>
+__global__ __launch_bounds__(256) void dlrm_interact_bwd_mfma_kernel(const bf16_t* __restrict__ V, int64_t B, int NV,
+                                                                     int dense_idx, const bf16_t* __restrict__ dout,
+                                                                     int ldo, float* __restrict__ dV,
+                                                                     bf16_t* __restrict__ d_dense) {
+  __shared__ bf16_t sv[4][32 * D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const bool valid = b < B;
+  const bf16_t* vb = V + (valid ? b : 0) * NV * D;
+  const bf16_t* ob = dout + (valid ? b : 0) * ldo;
+  bf16_t* s = sv[w];
+  for (int e = lane * 8; e < 32 * D; e += 64 * 8) {
+    const int r = e / D;
+    *reinterpret_cast<v8s*>(s + e) =
+        (valid && r < NV) ? *reinterpret_cast<const v8s*>(vb + e) : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  __syncthreads();
+  if (!valid) return;
+  v8s a[2];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti) {
+    const int r = ti * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = 8 * (lane >> 4) + q;
+      bf16_t g = 0;
+      if (r < NV && c < NV && r != c) {
+        const int hi = r > c ? r : c, lo = r > c ? c : r;
+        g = ob[D + hi * (hi - 1) / 2 + lo];
+      }
+      a[ti][q] = (short)g;
+    }
+  }
+#pragma unroll
+  for (int tn = 0; tn < D / 16; ++tn) {
+    const int n = tn * 16 + (lane & 15);
+    v8s bt;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bt[q] = (short)s[(8 * (lane >> 4) + q) * D + n];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti) {
+      v4f acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf_i, a[ti]), __builtin_bit_cast(v8bf_i, bt),
+                                                    acc, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = ti * 16 + (lane >> 4) * 4 + e;
+        if (row < NV) {
+          float v = acc[e];
+          if (row == dense_idx) {
+            v += bf2f(ob[n]);
+            d_dense[b * D + n] = f2bf(bf2f(s[row * D + n]) > 0.f ? v : 0.f);
+          }
+          dV[(b * NV + row) * D + n] = v;
+        }
+      }
+    }
+  }
+}
+
 void dlrm_interact_fwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, bf16_t* out, int ldo, hipStream_t s) {
   if (B <= 0) return;
+  if (NV <= 32 && (D == 16 || D == 32 || D == 64) && ldo % 8 == 0) {
+    const unsigned grid = (unsigned)((B + 3) / 4);
+    if (D == 64)
+      hipLaunchKernelGGL(dlrm_interact_fwd_mfma_kernel<2>, grid, 256, 0, s, V, B, NV, D, dense_idx, out, ldo);
+    else
+      hipLaunchKernelGGL(dlrm_interact_fwd_mfma_kernel<1>, grid, 256, 0, s, V, B, NV, D, dense_idx, out, ldo);
+    MINIPS_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(dlrm_interact_fwd_kernel, (int)std::min<int64_t>(B, 8192), 256, NV * (D + 1)
                      * sizeof(float), s, V, B,
                      NV, D, dense_idx, out, ldo);
@@ -665,6 +782,20 @@ void dlrm_interact_fwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx,
 void dlrm_interact_bwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, const bf16_t* dout, int ldo,
                        float* dV, bf16_t* d_dense, hipStream_t s) {
   if (B <= 0) return;
+  if (NV <= 32 && (D == 16 || D == 32 || D == 64)) {
+    const unsigned grid = (unsigned)((B + 3) / 4);
+    if (D == 64)
+      hipLaunchKernelGGL(dlrm_interact_bwd_mfma_kernel<64>, grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
+                         d_dense);
+    else if (D == 32)
+      hipLaunchKernelGGL(dlrm_interact_bwd_mfma_kernel<32>, grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
+                         d_dense);
+    else
+      hipLaunchKernelGGL(dlrm_interact_bwd_mfma_kernel<16>, grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
+                         d_dense);
+    MINIPS_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(dlrm_interact_bwd_kernel, (int)std::min<int64_t>(B, 8192), 256,
                      (NV * D + NV * NV) * sizeof(float), s, V, B, NV, D, dense_idx, dout, ldo, dV, d_dense);
   MINIPS_HIP_CHECK(hipGetLastError());

@@ -97,20 +97,25 @@ def test_gelu_add(dev):
     _close(res[str(dev)][1], res["cpu"][1], 1e-2)
 
 
-def test_dlrm_interaction_and_lookup(dev):
-    g = torch.Generator().manual_seed(8)
-    B, NV, D, F = 96, 27, 64, 26
+@pytest.mark.parametrize("D,B", [(64, 96), (64, 97), (32, 50), (16, 1003)])
+def test_dlrm_interaction_and_lookup(dev, D, B):
+    """The MFMA interaction kernels (one wave per sample, 16x16x32 bf16 tiles; B not a multiple of
+    the 4 waves of a block) against the fp32 reference, for the DLRM (D = 64) and DLRM-10B (D = 16)
+    widths."""
+    g = torch.Generator().manual_seed(8 + D)
+    NV, F = 27, 26
     U = 500
+    ld = (D + NV * (NV - 1) // 2 + 7) // 8 * 8
     rows = _bf(torch.randn(U, D, generator=g))
     inv = torch.randint(0, U, (B * F,), generator=g)
     bottom = _bf(torch.relu(torch.randn(B, D, generator=g)) - 0.2)
-    dout = _bf(torch.randn(B, 416, generator=g))
+    dout = _bf(torch.randn(B, ld, generator=g))
     res = {}
     for d in ("cpu", dev):
         V = torch.zeros(B, NV * D, dtype=torch.bfloat16, device=d)
         ops.lookup_rows(rows.to(d), inv.to(d), F, D, V)
         V[:, F * D:] = bottom.to(d)
-        out = torch.zeros(B, 416, dtype=torch.bfloat16, device=d)
+        out = torch.zeros(B, ld, dtype=torch.bfloat16, device=d)
         ops.dlrm_interact_fwd(V, NV, D, out, dense_idx=F)
         dV = torch.empty(B, NV * D, device=d)
         dd = torch.empty(B, D, dtype=torch.bfloat16, device=d)
