@@ -416,8 +416,8 @@ __global__ __launch_bounds__(256) void softmax_xent_small_kernel(bf16_t* __restr
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int c = k * 8 + 2 * q2 + h;
-            g[h] = c < V ? __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2 + h) * L2E - ml2) * sinv - (c == lab ? scale : 0.f)
-                         : 0.f;
+            const float p = __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2 + h) * L2E - ml2) * sinv;
+            g[h] = c < V ? p - (c == lab ? scale : 0.f) : 0.f;
           }
           o[q2] = pack_bf2(g[0], g[1]);
         }
@@ -680,7 +680,8 @@ __global__ __launch_bounds__(256) void dlrm_interact_fwd_mfma_kernel(const bf16_
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) f[t][ks] = load_frag(vb, NV, D, t * 16 + (lane & 15), ks * 32 + 8 * (lane >> 4));
   bf16_t* ob = out + b * ldo;
-  if (lane * 8 < D) *reinterpret_cast<v8s*>(ob + lane * 8) = *reinterpret_cast<const v8s*>(vb + dense_idx * D + lane * 8);
+  if (lane * 8 < D)
+    *reinterpret_cast<v8s*>(ob + lane * 8) = *reinterpret_cast<const v8s*>(vb + dense_idx * D + lane * 8);
 #pragma unroll
   for (int tile = 0; tile < 3; ++tile) {  // (0,0), (1,0), (1,1)
     const int ti = tile == 0 ? 0 : 1, tj = tile == 2 ? 1 : 0;
