@@ -132,11 +132,14 @@ std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tenso
   TORCH_CHECK(bounds.dim() == 1 && bounds.numel() >= 2, "bounds must be [P+1]");
   const int64_t n = keys.numel();
   const int P = (int)bounds.numel() - 1;
-  // capacity: the next power of two above n (every key fits: U <= n < cap). Batches repeat ids
-  // heavily (Criteo-shaped: U ~ n/5), so the load factor stays low while the table (and its
-  // per-call zero fill) is half the size of a 2n table and stays closer to L2
+  // capacity: the smallest power of two >= 1.6 n (every key fits: U <= n < cap), so even a batch
+  // of all-distinct keys (DLRM / LR ids drawn uniformly from 10^8 rows: U ~ n) probes at load
+  // <= 0.63 -- at next_pow2(n) such a batch ran at load ~0.8 and its linear-probing inserts took
+  // 141 us for 426K keys (profiles/r2/dlrm_1gpu_kernels_before.txt). Criteo-shaped batches (U ~ n/5)
+  // use the sort planner (plan.hip) instead.
   int64_t cap = 1024;
-  while (cap <= n) cap <<= 1;
+  while (cap * 5 < n * 8) cap <<= 1;
+  if (cap <= n) cap <<= 1;
   auto opts = keys.options();
   // table_keys | counts[P] | total | shard counters [2*S*P] in one allocation: one zero memset
   const int64_t extra64 = (std::max<int64_t>(extra_zero_ints, 0) + 1) / 2;  // int32 count -> int64 words
