@@ -63,7 +63,8 @@ def test_softmax_xent(dev, V, ld, M):
     c, gp = res["cpu"], res[str(dev)]
     _close(gp[0], c[0], 1e-2)
     _close(gp[1], c[1], 1e-3 * M)
-    assert abs(float(gp[2]) - float(c[2])) <= 1 + M // 5000
+    # a hit is "label logit == row max" on the GPU, argmax (first index) on the CPU: bf16 ties differ
+    assert abs(float(gp[2]) - float(c[2])) <= 1 + M // 1000
 
 
 @pytest.mark.parametrize("T", [64, 128, 1024])
