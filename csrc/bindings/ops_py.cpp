@@ -876,6 +876,12 @@ void dlrm_interact_bwd(const at::Tensor& V, int64_t NV, int64_t D, int64_t dense
   const int64_t B = V.numel() / (NV * D);
   TORCH_CHECK(dV.numel() == V.numel() && dout.size(0) == B && d_dense.numel() == B * D, "interaction bwd shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA g(V.device());
+  if (dV.scalar_type() == at::kBFloat16) {
+    minips_k::dlrm_interact_bwd_bf16(ptr<bf16_t>(V), B, (int)NV, (int)D, (int)dense_idx, ptr<bf16_t>(dout),
+                                     (int)dout.size(1), ptr<bf16_t>(dV), ptr<bf16_t>(d_dense), stream_of(V));
+    return;
+  }
+  check_dtype(dV, at::kFloat, "dV");
   minips_k::dlrm_interact_bwd(ptr<bf16_t>(V), B, (int)NV, (int)D, (int)dense_idx, ptr<bf16_t>(dout), (int)dout.size(1),
                               ptr<float>(dV), ptr<bf16_t>(d_dense), stream_of(V));
 }

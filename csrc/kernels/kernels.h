@@ -206,6 +206,9 @@ void embed_bwd(const bf16_t* dx, int ldx, const int64_t* tok, int64_t M, int T, 
 // [V[b][dense_idx] | V_i.V_j for i > j]. Backward: dV fp32 for all vectors, and the dense
 // vector's gradient ReLU-masked by its value as bf16 (feeds the bottom MLP's backward).
 void dlrm_interact_fwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, bf16_t* out, int ldo, hipStream_t s);
+// bf16 dV (half the bytes for the embedding backward that reads it): NV <= 32, D in {16, 32, 64}.
+void dlrm_interact_bwd_bf16(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, const bf16_t* dout, int ldo,
+                            bf16_t* dV, bf16_t* d_dense, hipStream_t s);
 void dlrm_interact_bwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, const bf16_t* dout, int ldo,
                        float* dV, bf16_t* d_dense, hipStream_t s);
 

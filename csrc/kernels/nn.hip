@@ -703,10 +703,10 @@ __global__ __launch_bounds__(256) void dlrm_interact_fwd_mfma_kernel(const bf16_
 // one wave per sample: A = dZ fragments gathered from the packed dout (row = lane & 15 of the
 // tile, 8 k's), B = V^T fragments read from the sample's V staged in LDS (column n = lane & 15,
 // 8 consecutive vector indices), 2 x (D/16) output tiles of one v_mfma_f32_16x16x32_bf16 each.
-template <int D>
+template <int D, typename OutT>
 __global__ __launch_bounds__(256) void dlrm_interact_bwd_mfma_kernel(const bf16_t* __restrict__ V, int64_t B, int NV,
                                                                      int dense_idx, const bf16_t* __restrict__ dout,
-                                                                     int ldo, float* __restrict__ dV,
+                                                                     int ldo, OutT* __restrict__ dV,
                                                                      bf16_t* __restrict__ d_dense) {
   __shared__ bf16_t sv[4][32 * D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -757,7 +757,10 @@ __global__ __launch_bounds__(256) void dlrm_interact_bwd_mfma_kernel(const bf16_
             v += bf2f(ob[n]);
             d_dense[b * D + n] = f2bf(bf2f(s[row * D + n]) > 0.f ? v : 0.f);
           }
-          dV[(b * NV + row) * D + n] = v;
+          if constexpr (sizeof(OutT) == 2)
+            dV[(b * NV + row) * D + n] = f2bf(v);
+          else
+            dV[(b * NV + row) * D + n] = v;
         }
       }
     }
@@ -780,21 +783,36 @@ void dlrm_interact_fwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx,
                      NV, D, dense_idx, out, ldo);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
+template <typename OutT>
+static void interact_bwd_mfma(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, const bf16_t* dout, int ldo,
+                              OutT* dV, bf16_t* d_dense, hipStream_t s) {
+  const unsigned grid = (unsigned)((B + 3) / 4);
+  if (D == 64)
+    hipLaunchKernelGGL((dlrm_interact_bwd_mfma_kernel<64, OutT>), grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
+                       d_dense);
+  else if (D == 32)
+    hipLaunchKernelGGL((dlrm_interact_bwd_mfma_kernel<32, OutT>), grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
+                       d_dense);
+  else
+    hipLaunchKernelGGL((dlrm_interact_bwd_mfma_kernel<16, OutT>), grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
+                       d_dense);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+bool dlrm_interact_mfma_ok(int NV, int D) { return NV <= 32 && (D == 16 || D == 32 || D == 64); }
+
+void dlrm_interact_bwd_bf16(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, const bf16_t* dout, int ldo,
+                            bf16_t* dV, bf16_t* d_dense, hipStream_t s) {
+  if (B <= 0) return;
+  if (!dlrm_interact_mfma_ok(NV, D)) throw std::runtime_error("dlrm_interact_bwd: bf16 dV needs NV <= 32, D 16/32/64");
+  interact_bwd_mfma(V, B, NV, D, dense_idx, dout, ldo, dV, d_dense, s);
+}
+
 void dlrm_interact_bwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx, const bf16_t* dout, int ldo,
                        float* dV, bf16_t* d_dense, hipStream_t s) {
   if (B <= 0) return;
-  if (NV <= 32 && (D == 16 || D == 32 || D == 64)) {
-    const unsigned grid = (unsigned)((B + 3) / 4);
-    if (D == 64)
-      hipLaunchKernelGGL(dlrm_interact_bwd_mfma_kernel<64>, grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
-                         d_dense);
-    else if (D == 32)
-      hipLaunchKernelGGL(dlrm_interact_bwd_mfma_kernel<32>, grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
-                         d_dense);
-    else
-      hipLaunchKernelGGL(dlrm_interact_bwd_mfma_kernel<16>, grid, 256, 0, s, V, B, NV, dense_idx, dout, ldo, dV,
-                         d_dense);
-    MINIPS_HIP_CHECK(hipGetLastError());
+  if (dlrm_interact_mfma_ok(NV, D)) {
+    interact_bwd_mfma(V, B, NV, D, dense_idx, dout, ldo, dV, d_dense, s);
     return;
   }
   hipLaunchKernelGGL(dlrm_interact_bwd_kernel, (int)std::min<int64_t>(B, 8192), 256,

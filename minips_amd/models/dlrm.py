@@ -98,7 +98,10 @@ class DLRM(LookaheadPlans):
                 H=torch.empty(B, cfg.top[-1], **bf), dH=torch.empty(B, cfg.top[-1], **bf),
                 tgrads=[torch.empty(B, d, **bf) for d in cfg.top[:-1]],
                 dI=torch.zeros(B, align(self.n_int), **bf),
-                dV=torch.empty(B, self.NV * cfg.D, dtype=torch.float32, device=dev),
+                # bf16 interaction gradient: half the bytes the embedding backward gathers
+                # (the MFMA interaction kernel writes it directly; fp32 only off the MFMA shapes)
+                dV=torch.empty(B, self.NV * cfg.D, dtype=torch.bfloat16 if self.NV <= 32 and cfg.D in (16, 32, 64)
+                               and dev.type == "cuda" else torch.float32, device=dev),
                 dbot=torch.empty(B, cfg.D, **bf),
                 zero=torch.zeros(B, dtype=torch.float32, device=dev),
                 dwide=torch.empty(B, dtype=torch.float32, device=dev),
