@@ -83,7 +83,10 @@ class DLRM(LookaheadPlans):
         h[: cfg.top[-1]].uniform_(-cfg.top[-1] ** -0.5, cfg.top[-1] ** -0.5, generator=g)
         self.dense.load_full(full)
         self._bufs = {}
-        self._side = SideStream(comm.device, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
+        # weight gradients inline by default: with the round-2 MFMA interaction the dgrad chain is
+        # short and the side stream's contention costs more than the overlap gains (1 GPU: 0.686
+        # inline vs 0.714 ms/step forked); MINIPS_DLRM_WGRAD_STREAM=1 forks them
+        self._side = SideStream(comm.device, os.environ.get("MINIPS_DLRM_WGRAD_STREAM", "0") == "1")
 
     def _buffers(self, B):
         if B not in self._bufs:
