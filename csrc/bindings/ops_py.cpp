@@ -121,6 +121,31 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
                               stream_of(A), slab.defined() ? ptr<float>(slab) : nullptr);
 }
 
+// Bitmap planner of a bounded key space (keys, after the optional routing k * mult mod rn, in
+// [0, num_rows)): same outputs as unique_bucketize -- (sorted unique keys [n] (first U valid),
+// inverse [n], counts [P], U [1]) -- with no hash table.
+std::vector<at::Tensor> bitmap_plan(const at::Tensor& keys, const at::Tensor& bounds, int64_t num_rows,
+                                    int64_t route_mult, int64_t route_n) {
+  check_gpu(keys, "keys");
+  check_gpu(bounds, "bounds");
+  check_dtype(keys, at::kLong, "keys");
+  check_dtype(bounds, at::kLong, "bounds");
+  TORCH_CHECK(keys.is_contiguous() && bounds.dim() == 1 && bounds.numel() >= 2, "bitmap_plan args");
+  TORCH_CHECK(num_rows > 0 && num_rows <= (1LL << 36), "bitmap_plan: 0 < num_rows <= 2^36");
+  TORCH_CHECK(!route_mult || route_n == num_rows, "bitmap_plan: routing must map into [0, num_rows)");
+  const int64_t n = keys.numel();
+  const int P = (int)bounds.numel() - 1;
+  auto opts = keys.options();
+  auto ws = at::empty({minips_k::bitmap_plan_workspace_words(num_rows)}, opts);
+  auto uniq = at::empty({std::max<int64_t>(n, 1)}, opts), inverse = at::empty({n}, opts);
+  auto counts = at::empty({P + 1}, opts), U = at::empty({1}, opts);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  minips_k::bitmap_plan(ptr<int64_t>(keys), n, num_rows, ptr<int64_t>(bounds), P, (uint64_t)route_mult,
+                        (uint64_t)route_n, ptr<int64_t>(ws), ptr<int64_t>(uniq), ptr<int64_t>(inverse),
+                        ptr<int64_t>(counts), ptr<int64_t>(U), stream_of(keys));
+  return {uniq, inverse, counts.narrow(0, 0, P), U};
+}
+
 // Returns (unique keys grouped by owner [n] (first U valid), inverse [n], counts [P], U [1]).
 std::vector<at::Tensor> unique_bucketize(const at::Tensor& keys, const at::Tensor& bounds, int64_t F,
                                          int64_t route_mult, int64_t route_n, int64_t extra_zero_ints,
@@ -1067,6 +1092,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_split3", &kmeans_split3);
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
+  m.def("bitmap_plan", &bitmap_plan);
   m.def("uniform_synth", &uniform_synth);
   m.def("ipc_alloc", &ipc_alloc);
   m.def("kmeans_assign_csr", &kmeans_assign_csr);

@@ -48,6 +48,12 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
 // cursor are zeroed by the same memset (a workspace for a following op, e.g. emb_build_csr).
 // counter shards of unique_bucketize's zero buffer for P owners (table | counts | total | 2*S*P | extra)
 int ub_shards(int P);
+// Bitmap planning of a bounded key space [0, num_keys_space) (bitmap.hip): sorted unique keys,
+// inverse, per-owner counts (counts[P] = U) and U on the device. ws: bitmap_plan_workspace_words().
+int64_t bitmap_plan_workspace_words(int64_t num_keys_space);
+void bitmap_plan(const int64_t* keys, int64_t n, int64_t num_keys_space, const int64_t* bounds, int P,
+                 uint64_t rmult, uint64_t rn, int64_t* ws, int64_t* uniq, int64_t* inverse, int64_t* counts,
+                 int64_t* U, hipStream_t s);
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult = 0,

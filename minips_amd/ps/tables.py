@@ -513,6 +513,11 @@ class SparsePlan:
 
 # Key planning of [B, F] batches with disjoint column key ranges (SparseTable ``columns``) on one
 # rank: per-column radix sort without atomics (ops.plan_sorted) instead of the hash dedupe, whose
+# Bitmap planning (ops.bitmap_plan) for range tables whose key space is small next to the batch
+# (bitmap bytes <= _BITMAP_RATIO x keys): uniformly drawn ids (LR, DLRM) dedupe without a hash
+# table. MINIPS_BITMAP_PLAN=0 keeps the hash dedupe.
+_BITMAP_PLAN = os.environ.get("MINIPS_BITMAP_PLAN", "1") != "0"
+_BITMAP_RATIO = int(os.environ.get("MINIPS_BITMAP_RATIO", "256"))
 # memory-side atomics slow the concurrently running step; MINIPS_SORT_PLAN=0 keeps the hash path
 _SORT_PLAN = os.environ.get("MINIPS_SORT_PLAN", "1") != "0"
 
@@ -660,6 +665,17 @@ class SparseTable:
                 self.num_rows if rmult else 0, bits_dev=cols[2], bounds=self.bounds)
             pp.uniq, pp.inv, pp.counts, pp.U_dev = uniq, inv, counts, U_dev
             pp.csr = (members, memrow) if want_csr else None
+            pp.host = pp.event = pp.cev = None
+            pp.exchanged = self.comm.world == 1
+            if exchange:
+                self._exchange_counts(pp)
+            return pp
+        if (_BITMAP_PLAN and flat.is_cuda and cols is None and type(self)._route_keys is SparseTable._route_keys
+                and self.num_rows <= (1 << 36) and self.num_rows // 8 <= _BITMAP_RATIO * max(n, 1)):
+            # bounded key space: bitmap dedupe (sorted unique keys, grouped by owner by construction)
+            pp.flat = flat
+            pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.bitmap_plan(flat, self.bounds, self.num_rows, rmult)
+            pp.csr = ops.emb_build_csr(pp.inv, pp.F, n) if want_csr else None
             pp.host = pp.event = pp.cev = None
             pp.exchanged = self.comm.world == 1
             if exchange:

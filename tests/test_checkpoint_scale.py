@@ -211,7 +211,8 @@ def _save_text(rank, world, prefix):
     sparse.shard.copy_(rows[:, None] * 10 + torch.arange(W, dtype=torch.float32) + 1)
     ck = Checkpointer(comm, prefix, ring_bytes=RING, text_limit=-1)  # text for every shard, streamed
     ck.save({0: dense, 1: sparse}, iteration=3, blocking=True)
-    return dense.master.clone(), sparse.shard.reshape(-1).clone()
+    # plain lists: a tensor would travel as a shared-memory fd the exiting child may close first
+    return dense.master.tolist(), sparse.shard.reshape(-1).tolist()
 
 
 class _SaveText:
@@ -232,7 +233,8 @@ def test_streamed_text_checkpoint_and_reference_names(tmp_path):
     prefix = str(tmp_path / "ck_")
     out = run_world(_SaveText(prefix), world=2)
     for r in range(2):
-        dense_master, sparse_flat = out[r]
+        dense_master = torch.tensor(out[r][0], dtype=torch.float64)
+        sparse_flat = torch.tensor(out[r][1], dtype=torch.float32)
         got = load_text_params(f"{prefix}server_params_{r}", dense_master.numel()).to(torch.float64)
         assert torch.equal(got, dense_master)  # exact fp64 round trip through the text
         got1 = load_text_params(f"{prefix}server_params_{r}_t1", sparse_flat.numel()).float()

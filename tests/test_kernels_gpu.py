@@ -472,3 +472,25 @@ def test_plan_sorted_matches_reference(dev, B, cards, P):
     torch.testing.assert_close(got[4], ref[4])
     torch.testing.assert_close(got[5], ref[5])
     assert bool((got[1][got[4].long()] == got[5].long()).all())      # members belong to their row
+
+
+@pytest.mark.parametrize("num_rows,n,P,route", [(16_609_143, 200_000, 1, True), (1000, 5000, 3, False),
+                                                (100_000_000, 425_984, 8, True), (77, 1, 2, False)])
+def test_bitmap_plan_matches_sorted_unique(dev, num_rows, n, P, route):
+    """The bitmap planner (csrc/kernels/bitmap.hip) gives exactly the CPU reference plan: sorted
+    unique (routed) keys, inverse, per-owner counts and U, with duplicates and ragged owners."""
+    from minips_amd.ps.tables import _route_multiplier, even_bounds
+
+    g = torch.Generator().manual_seed(n)
+    keys = torch.randint(0, num_rows, (n,), generator=g)
+    keys[: n // 3] = keys[n // 3: 2 * (n // 3)]  # plenty of duplicates
+    bounds = torch.tensor(even_bounds(num_rows, P), dtype=torch.int64)
+    mult = _route_multiplier(num_rows) if route else 0
+    cu, ci, cc, cU = ops.bitmap_plan(keys, bounds, num_rows, mult)
+    gu, gi, gc, gU = ops.bitmap_plan(keys.to(dev), bounds.to(dev), num_rows, mult)
+    U = int(cU.reshape(-1)[0])
+    assert int(gU.reshape(-1)[0]) == U
+    assert torch.equal(gu[:U].cpu(), cu[:U])
+    assert torch.equal(gi.cpu(), ci)
+    assert torch.equal(gc.cpu(), cc)
+    assert torch.equal(cu[:U][ci], (keys * mult) % num_rows if route else keys)
