@@ -88,10 +88,11 @@ def build(args, comm):
         from minips_amd.models.lr import SparseLR, SparseLRConfig
 
         B = args.batch or 65536
-        m = SparseLR(SparseLRConfig(consistency=args.consistency, staleness=args.staleness), comm)
+        vdt = getattr(torch, args.value_dtype)
+        m = SparseLR(SparseLRConfig(consistency=args.consistency, staleness=args.staleness, value_dtype=vdt), comm)
         data = SparseLRSynth(B, nnz=64, device=dev, seed=r)
         return m, (lambda: m.train_step(*data.next())), B, "samples/s", \
-            dict(model="sparse LR, 16.6M features, 64 nnz/row", seq_len=None)
+            dict(model=f"sparse LR, 16.6M features, 64 nnz/row, {args.value_dtype} table", seq_len=None)
     if args.model == "kmeans":
         from minips_amd.models.kmeans import KMeans, KMeansConfig
 
@@ -136,6 +137,8 @@ def main():
                     help="mlp: capture the step in a HIP graph (one rank, BSP; off by default: at batch 8192 the "
                          "step is GPU-bound, 0.364 vs 0.350 ms measured)")
     ap.add_argument("--staleness", type=int, default=0)
+    ap.add_argument("--value-dtype", default="float32", choices=["float32", "float64"],
+                    help="lr: table precision (float64 = the reference's CreateTable<double>)")
     args = ap.parse_args()
     from minips_amd.ps.comm import init_distributed
 
