@@ -167,9 +167,9 @@ def main():
             "metric": f"{unit.split('/')[0]}/sec (whole job) {args.model} {cfg.pop('consistency', args.consistency)}",
             "value": round(per_step * comm.world * args.steps / el, 1), "unit": unit, "n_gpus": comm.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "dtype": "bf16" if args.model in ("mlp", "gpt2",
-                                                                                           "dlrm", "dlrm-10b",
-                                                                                            "widedeep-ssp") else "fp32",
+            "higher_is_better": True, "scaling": "weak",
+            "dtype": ("bf16" if args.model in ("mlp", "gpt2", "dlrm", "dlrm-10b", "widedeep-ssp")
+                      else ("fp64" if args.value_dtype == "float64" and args.model == "lr" else "fp32")),
             "data": "synthetic", "last": float(out.float().sum()) if torch.is_tensor(out) else None,
             "config": dict(cfg, parallelism=f"ps-dp{comm.world}"),
         }), flush=True)
