@@ -200,8 +200,9 @@ int TcpConnect(const std::string& host_in, int port) {
   }
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-  timeval tv{120, 0};  // a dead datanode fails the read instead of hanging the loader
+  timeval tv{120, 0};  // a dead datanode fails the read / write instead of hanging the loader
   setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
   return fd;
 }
 

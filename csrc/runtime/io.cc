@@ -249,6 +249,11 @@ void BlockAssignerServer::Loop() {
       if (c >= 0) {
         int one = 1;
         setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+        // a client that stalls inside a frame is dropped after 30 s instead of blocking the
+        // single-threaded service (every other loader waits on it)
+        timeval tv{30, 0};
+        setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+        setsockopt(c, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
         keep.push_back(c);
       }
     }
