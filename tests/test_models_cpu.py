@@ -223,3 +223,23 @@ def _km_init_fn(rank, world):
 def test_kmeans_init_broadcast_two_ranks():
     out = run_world(_km_init_fn)
     assert out[0] == out[1]  # rank 0 seeds, every rank loads the same centres
+
+
+def test_bitmap_plan_cpu_reference_and_dlrm_synth_cpu():
+    """CPU paths of the round-2 planner / generator: ops.bitmap_plan is the sorted-unique plan (the
+    GPU kernel is checked against it in test_kernels_gpu.py), DLRMSynth draws in-range keys with
+    labels = dense[:, 0] > 0."""
+    from minips_amd import ops
+    from minips_amd.data.synthetic import DLRMSynth
+
+    keys = torch.tensor([7, 3, 7, 99, 0, 3, 50])
+    bounds = torch.tensor([0, 40, 100])
+    u, inv, counts, U = ops.bitmap_plan(keys, bounds, 100)
+    n = int(U.reshape(-1)[0])
+    assert u[:n].tolist() == [0, 3, 7, 50, 99]
+    assert torch.equal(u[:n][inv], keys)
+    assert counts.tolist() == [3, 2]
+    d = DLRMSynth(64, 26, 1000, 13, device="cpu", seed=1)
+    dense, k, lab = d.next()
+    assert k.shape == (64, 26) and int(k.min()) >= 0 and int(k.max()) < 1000
+    assert torch.equal(lab, (dense[:, 0] > 0).float())
