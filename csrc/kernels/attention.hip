@@ -22,9 +22,6 @@
 // dQ is produced by its own sweep instead of float atomics (deterministic, 7 products per tile
 // pair instead of 5).
 // K/V (or Q/dO) tiles are double-buffered in LDS with a one-tile register prefetch.
-#include <cstdlib>
-#include <map>
-#include <mutex>
 #include <stdexcept>
 #include <string>
 
@@ -511,28 +508,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16_t* __restr
   store_transposed(base + 2 * dmodel, lddq, kw, T, dv, 1.f, lane);
 }
 
-// One extra stream (+ fork / join events) per device, created on first use and kept for the
-// process lifetime; the events are re-recorded by every call (a wait binds to the record before it).
-struct SideStreamRes {
-  hipStream_t stream = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-
-SideStreamRes& side_stream_for_current_device() {
-  static std::mutex mu;
-  static std::map<int, SideStreamRes> by_dev;
-  int dev = 0;
-  MINIPS_HIP_CHECK(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu);
-  SideStreamRes& r = by_dev[dev];
-  if (!r.stream) {
-    MINIPS_HIP_CHECK(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
-    MINIPS_HIP_CHECK(hipEventCreateWithFlags(&r.fork, hipEventDisableTiming));
-    MINIPS_HIP_CHECK(hipEventCreateWithFlags(&r.join, hipEventDisableTiming));
-  }
-  return r;
-}
-
 void check_attn(int T, int H, int dmodel, int ldq, int ldo) {
   if (dmodel != H * HD) throw std::runtime_error("attention: head dim must be 64");
   if (T <= 0 || ldq % 8 || ldo % 8) throw std::runtime_error("attention: leading dims must be multiples of 8");
@@ -556,32 +531,12 @@ void attn_bwd(const bf16_t* qkv, int ldq, const bf16_t* O, int ldo, const bf16_t
                      delta);
   MINIPS_HIP_CHECK(hipGetLastError());
   const int grid = ((T + BROWS - 1) / BROWS) * B * H;
-  // dQ and dK/dV are independent sweeps (disjoint column blocks of dqkv, same read-only inputs):
-  // the dK/dV sweep runs on a second stream of this device so the two kernels' causal tails
-  // (the late query / key blocks have little work) overlap. Opt-in (MINIPS_ATTN_BWD_STREAMS=1)
-  // until measured in the GPT-2 step; default: in series on the caller's stream
-  static const bool two_streams = [] {
-    const char* e = std::getenv("MINIPS_ATTN_BWD_STREAMS");
-    return e && std::atoi(e) != 0;
-  }();
-  hipStream_t sk = s;
-  SideStreamRes* side = nullptr;
-  if (two_streams) {
-    side = &side_stream_for_current_device();
-    MINIPS_HIP_CHECK(hipEventRecord(side->fork, s));
-    MINIPS_HIP_CHECK(hipStreamWaitEvent(side->stream, side->fork, 0));
-    sk = side->stream;
-  }
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, 256, 0, sk, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel,
-                     scale * kLog2e, scale, dqkv, lddq);
-  MINIPS_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel, scale * kLog2e,
                      scale, dqkv, lddq);
   MINIPS_HIP_CHECK(hipGetLastError());
-  if (side) {  // the caller's stream continues only after both sweeps
-    MINIPS_HIP_CHECK(hipEventRecord(side->join, side->stream));
-    MINIPS_HIP_CHECK(hipStreamWaitEvent(s, side->join, 0));
-  }
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel,
+                     scale * kLog2e, scale, dqkv, lddq);
+  MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace minips_k
