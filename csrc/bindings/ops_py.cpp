@@ -6,10 +6,15 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/extension.h>
 
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <tuple>
 
 #include "../kernels/kernels.h"
+#include "../kernels/onesided.h"
 
 namespace {
 
@@ -125,7 +130,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
 // [0, num_rows)): same outputs as unique_bucketize -- (sorted unique keys [n] (first U valid),
 // inverse [n], counts [P], U [1]) -- with no hash table.
 std::vector<at::Tensor> bitmap_plan(const at::Tensor& keys, const at::Tensor& bounds, int64_t num_rows,
-                                    int64_t route_mult, int64_t route_n) {
+                                    int64_t route_mult, int64_t route_n, const c10::optional<at::Tensor>& oor) {
   check_gpu(keys, "keys");
   check_gpu(bounds, "bounds");
   check_dtype(keys, at::kLong, "keys");
@@ -142,7 +147,8 @@ std::vector<at::Tensor> bitmap_plan(const at::Tensor& keys, const at::Tensor& bo
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::bitmap_plan(ptr<int64_t>(keys), n, num_rows, ptr<int64_t>(bounds), P, (uint64_t)route_mult,
                         (uint64_t)route_n, ptr<int64_t>(ws), ptr<int64_t>(uniq), ptr<int64_t>(inverse),
-                        ptr<int64_t>(counts), ptr<int64_t>(U), stream_of(keys));
+                        ptr<int64_t>(counts), ptr<int64_t>(U), stream_of(keys),
+                        opt_ptr<int64_t>(oor, at::kLong, "oor"));
   return {uniq, inverse, counts.narrow(0, 0, P), U};
 }
 
@@ -941,52 +947,216 @@ at::Tensor ipc_open(py::bytes handle, int64_t nbytes, int64_t device) {
                           at::TensorOptions().dtype(at::kByte).device(at::kCUDA, (c10::DeviceIndex)device));
 }
 
-void check_remote(const at::Tensor& bases, const at::Tensor& bounds, const at::Tensor& keys) {
-  check_gpu(bases, "bases");
-  check_gpu(bounds, "bounds");
-  check_gpu(keys, "keys");
-  check_dtype(bases, at::kLong, "bases");
-  check_dtype(bounds, at::kLong, "bounds");
-  check_dtype(keys, at::kLong, "keys");
-  TORCH_CHECK(bounds.numel() == bases.numel() + 1, "bounds must have P+1 entries");
+void check_long_dev(const at::Tensor& t, const char* name) {
+  check_gpu(t, name);
+  check_dtype(t, at::kLong, name);
 }
 
-void remote_gather(const at::Tensor& bases, const at::Tensor& bounds, const at::Tensor& keys,
-                   const c10::optional<at::Tensor>& n_dev, int64_t W, at::Tensor& out) {
-  check_remote(bases, bounds, keys);
+const int64_t* opt_count(const c10::optional<at::Tensor>& n_dev) {
+  if (!n_dev || !n_dev->defined()) return nullptr;
+  check_long_dev(*n_dev, "n_dev");
+  TORCH_CHECK(n_dev->numel() >= 1, "n_dev must hold a count");
+  return ptr<int64_t>(*n_dev);
+}
+
+// Requester -> owners push of one clock (onesided.hip): uniq/counts/U_dev of the plan, fp32
+// gradient rows [>= n, W], inbox = [P] int64 addresses of every owner's inbox as mapped here.
+void ps_push_rows(const at::Tensor& uniq, const at::Tensor& counts, const c10::optional<at::Tensor>& U_dev,
+                  int64_t n, const at::Tensor& g, const at::Tensor& inbox, int64_t slot_off, int64_t cap) {
+  check_long_dev(uniq, "uniq");
+  check_long_dev(counts, "counts");
+  check_long_dev(inbox, "inbox");
+  check_gpu(g, "grads");
+  check_dtype(g, at::kFloat, "grads");
+  const int64_t P = inbox.numel();
+  TORCH_CHECK(P >= 1 && P <= minips_k::kPsMaxWorld, "inbox must list 1..16 owners");
+  TORCH_CHECK(counts.numel() >= P, "counts must have >= P entries");
+  TORCH_CHECK(n >= 0 && uniq.numel() >= n && g.dim() == 2 && g.size(0) >= n, "push: uniq/grads shorter than n");
+  TORCH_CHECK(n <= cap && slot_off >= 0, "push: n exceeds the inbox slot capacity");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  minips_k::ps_push_rows(ptr<int64_t>(uniq), ptr<int64_t>(counts), opt_count(U_dev), n, ptr<float>(g),
+                         (int)g.size(1), ptr<int64_t>(inbox), (int)P, slot_off, cap, stream_of(g));
+}
+
+void ps_set_headers(const at::Tensor& inbox, int64_t slot_off, int64_t value) {
+  check_long_dev(inbox, "inbox");
+  TORCH_CHECK(inbox.numel() >= 1 && inbox.numel() <= minips_k::kPsMaxWorld, "inbox must list 1..16 owners");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(inbox.device());
+  minips_k::ps_set_headers(ptr<int64_t>(inbox), (int)inbox.numel(), slot_off, value, stream_of(inbox));
+}
+
+void ps_gather_rows(const at::Tensor& bases, const at::Tensor& bounds, const at::Tensor& keys,
+                    const c10::optional<at::Tensor>& n_dev, int64_t W, at::Tensor& out) {
+  check_long_dev(bases, "bases");
+  check_long_dev(bounds, "bounds");
+  check_long_dev(keys, "keys");
   check_gpu(out, "out");
+  TORCH_CHECK(bounds.numel() == bases.numel() + 1, "bounds must have P+1 entries");
+  TORCH_CHECK(bases.numel() >= 1 && bases.numel() <= minips_k::kPsMaxWorld, "1..16 owners");
   const int64_t n = keys.numel();
   TORCH_CHECK(out.dim() == 2 && out.size(0) >= n && out.size(1) == W, "out must be [>= n, W]");
   const bool bf = out.scalar_type() == at::kBFloat16;
   TORCH_CHECK(bf || out.scalar_type() == at::kFloat, "out must be fp32 or bf16");
-  const int64_t* nd = nullptr;
-  if (n_dev && n_dev->defined()) {
-    check_gpu(*n_dev, "n_dev");
-    check_dtype(*n_dev, at::kLong, "n_dev");
-    nd = ptr<int64_t>(*n_dev);
-  }
-  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
-  minips_k::remote_gather(ptr<int64_t>(bases), ptr<int64_t>(bounds), (int)bases.numel(), ptr<int64_t>(keys), n, nd,
-                          (int)W, out.data_ptr(), bf, stream_of(keys));
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(keys.device());
+  minips_k::ps_gather_rows(ptr<int64_t>(bases), ptr<int64_t>(bounds), (int)bases.numel(), ptr<int64_t>(keys), n,
+                           opt_count(n_dev), (int)W, out.data_ptr(), bf, stream_of(keys));
 }
 
-void remote_scatter_add(const at::Tensor& bases, const at::Tensor& bounds, const at::Tensor& keys,
-                        const at::Tensor& vals, double scale, const c10::optional<at::Tensor>& n_dev) {
-  check_remote(bases, bounds, keys);
-  check_gpu(vals, "vals");
-  check_dtype(vals, at::kFloat, "vals");
-  const int64_t n = keys.numel();
-  TORCH_CHECK(vals.dim() == 2 && vals.size(0) >= n, "vals must be [>= n, W]");
-  const int64_t* nd = nullptr;
-  if (n_dev && n_dev->defined()) {
-    check_gpu(*n_dev, "n_dev");
-    check_dtype(*n_dev, at::kLong, "n_dev");
-    nd = ptr<int64_t>(*n_dev);
+// The owner side of the asynchronous PS on a GPU rank: minips::AsyncServer (the server thread,
+// csrc/runtime/async_server.h) driving a HipApplier (the optimizer kernels on the owner's own
+// stream). Table buffers are passed as raw device addresses; the Python table keeps them alive
+// and stops the server before freeing them.
+class GpuAsyncServer {
+ public:
+  GpuAsyncServer(const std::string& board, int64_t world, int64_t rank, int64_t tables, int64_t device)
+      : device_((int)device), applier_((int)device, (int)tables),
+        server_(board, (int)world, (int)rank, (int)tables, &applier_) {
+    pub_ = std::thread([this] { PublishLoop(); });
   }
-  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
-  minips_k::remote_scatter_add(ptr<int64_t>(bases), ptr<int64_t>(bounds), (int)bases.numel(), ptr<int64_t>(keys), n,
-                               nd, ptr<float>(vals), (int)vals.size(1), (float)scale, stream_of(keys));
-}
+  ~GpuAsyncServer() {
+    {
+      std::lock_guard<std::mutex> lk(pmu_);
+      pstop_ = true;
+    }
+    pcv_.notify_all();
+    if (pub_.joinable()) pub_.join();
+    server_.Stop();
+  }
+
+  // Requester side: publish sent[t] = c once the work issued so far on the tensor's current
+  // stream (the clock's pushes) has completed -- an event waited for by a native thread, so no
+  // Python thread (and no GIL hand-off) sits between the GPU and the board.
+  void publish_after(int64_t t, int64_t c, const at::Tensor& on) {
+    check_gpu(on, "stream tensor");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(on.device());
+    hipEvent_t e;
+    TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "publish_after: event");
+    TORCH_CHECK(hipEventRecord(e, stream_of(on)) == hipSuccess, "publish_after: record");
+    {
+      std::lock_guard<std::mutex> lk(pmu_);
+      pq_.push_back({e, (int)t, c});
+      ++queued_;
+    }
+    pcv_.notify_one();
+  }
+  int64_t published() const { return published_.load(); }
+  int64_t queued() {
+    std::lock_guard<std::mutex> lk(pmu_);
+    return queued_;
+  }
+
+  void add_sparse(int64_t t, int64_t opt, int64_t table, int64_t ld, int64_t W, int64_t state, int64_t state2,
+                  int64_t D1, int64_t base, double lr, double eps, int64_t cap, int64_t inbox, int64_t slot_bytes,
+                  int64_t depth) {
+    TORCH_CHECK(cap % 2 == 0 && slot_bytes % 256 == 0 && depth >= 1, "sparse inbox layout");
+    TORCH_CHECK(slot_bytes >= minips_k::kPsSlotHeader + cap * (8 + 4 * W), "sparse inbox slot too small");
+    TORCH_CHECK(opt == minips_k::kPsAdd || opt == minips_k::kPsSgd || opt == minips_k::kPsRowwiseAdagrad,
+                "sparse optimizer ", opt);
+    TORCH_CHECK(opt != minips_k::kPsRowwiseAdagrad || state != 0, "row-wise Adagrad needs its state");
+    minips_k::PsSparseDesc d;
+    d.opt = (int)opt;
+    d.table = reinterpret_cast<float*>(table);
+    d.ld = ld;
+    d.W = (int)W;
+    d.state = reinterpret_cast<float*>(state);
+    d.state2 = reinterpret_cast<float*>(state2);
+    d.D1 = (int)D1;
+    d.base = base;
+    d.lr = (float)lr;
+    d.eps = (float)eps;
+    d.cap = cap;
+    d.inbox = reinterpret_cast<char*>(inbox);
+    d.slot_bytes = slot_bytes;
+    d.depth = (int)depth;
+    applier_.SetSparse((int)t, d);
+    server_.Enable((int)t);
+  }
+
+  void add_dense(int64_t t, int64_t opt, int64_t w, int64_t m, int64_t v, int64_t wb, int64_t n, double lr, double b1,
+                 double b2, double eps, double wd, int64_t step, int64_t inbox, int64_t slot_bytes, int64_t depth) {
+    TORCH_CHECK(slot_bytes % 256 == 0 && depth >= 1 && n % 4 == 0, "dense inbox layout");
+    TORCH_CHECK(slot_bytes >= minips_k::kPsSlotHeader + 4 * n, "dense inbox slot too small");
+    TORCH_CHECK(opt != minips_k::kPsRowwiseAdagrad, "dense optimizer ", opt);
+    TORCH_CHECK((opt != minips_k::kPsAdam || (m && v)) && (opt != minips_k::kPsAdagrad || m), "optimizer state");
+    minips_k::PsDenseDesc d;
+    d.opt = (int)opt;
+    d.w = reinterpret_cast<float*>(w);
+    d.m = reinterpret_cast<float*>(m);
+    d.v = reinterpret_cast<float*>(v);
+    d.wb = reinterpret_cast<bf16_t*>(wb);
+    d.n = n;
+    d.lr = (float)lr;
+    d.b1 = (float)b1;
+    d.b2 = (float)b2;
+    d.eps = (float)eps;
+    d.wd = (float)wd;
+    d.step = step;
+    d.inbox = reinterpret_cast<char*>(inbox);
+    d.slot_bytes = slot_bytes;
+    d.depth = (int)depth;
+    applier_.SetDense((int)t, d);
+    server_.Enable((int)t);
+  }
+
+  int64_t step(int64_t t) const { return applier_.Step((int)t); }
+  void set_step(int64_t t, int64_t s) { applier_.SetStep((int)t, s); }
+  void start() { server_.Start(); }
+  void stop() { server_.Stop(); }
+  void pause() { server_.Pause(); }
+  void resume() { server_.Resume(); }
+  bool running() const { return server_.Running(); }
+  std::string error() const { return server_.Error(); }
+  void set_log(bool on) { server_.SetLog(on); }
+  std::vector<int64_t> take_log() { return server_.TakeLog(); }
+  int64_t applied() const { return server_.Applied(); }
+  int64_t batches() const { return server_.Batches(); }
+  std::string publish_error() {
+    std::lock_guard<std::mutex> lk(pmu_);
+    return perr_;
+  }
+
+ private:
+  struct Pub {
+    hipEvent_t e;
+    int t;
+    int64_t c;
+  };
+  void PublishLoop() {
+    (void)hipSetDevice(device_);
+    for (;;) {
+      Pub p;
+      {
+        std::unique_lock<std::mutex> lk(pmu_);
+        pcv_.wait(lk, [&] { return pstop_ || !pq_.empty(); });
+        if (pq_.empty()) return;  // stop requested and nothing left
+        p = pq_.front();
+        pq_.pop_front();
+      }
+      const hipError_t err = hipEventSynchronize(p.e);
+      (void)hipEventDestroy(p.e);
+      {
+        std::lock_guard<std::mutex> lk(pmu_);
+        if (err != hipSuccess && perr_.empty()) perr_ = std::string("publish: ") + hipGetErrorString(err);
+        // never publish a clock whose pushes did not complete, nor any later one
+        if (!perr_.empty()) continue;
+      }
+      server_.board().PublishSent(p.t, p.c);
+      published_.fetch_add(1);
+    }
+  }
+
+  int device_;
+  minips_k::HipApplier applier_;
+  minips::AsyncServer server_;
+  std::thread pub_;
+  std::mutex pmu_;
+  std::condition_variable pcv_;
+  std::deque<Pub> pq_;
+  bool pstop_ = false;
+  int64_t queued_ = 0;
+  std::atomic<int64_t> published_{0};
+  std::string perr_;
+};
 
 void kmeans_assign_csr(const at::Tensor& rowptr, const at::Tensor& cols, const at::Tensor& vals, const at::Tensor& C,
                        at::Tensor& cnorm, at::Tensor& assign, const c10::optional<at::Tensor>& dist) {
@@ -1092,12 +1262,42 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_split3", &kmeans_split3);
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
-  m.def("bitmap_plan", &bitmap_plan);
+  m.def("bitmap_plan", &bitmap_plan, py::arg("keys"), py::arg("bounds"), py::arg("num_rows"), py::arg("route_mult"),
+        py::arg("route_n"), py::arg("oor") = py::none());
   m.def("uniform_synth", &uniform_synth);
   m.def("ipc_alloc", &ipc_alloc);
   m.def("kmeans_assign_csr", &kmeans_assign_csr);
   m.def("kmeans_csr_accum", &kmeans_csr_accum);
   m.def("ipc_open", &ipc_open);
-  m.def("remote_gather", &remote_gather);
-  m.def("remote_scatter_add", &remote_scatter_add);
+  m.def("ps_push_rows", &ps_push_rows, py::arg("uniq"), py::arg("counts"), py::arg("U_dev"), py::arg("n"),
+        py::arg("g"), py::arg("inbox"), py::arg("slot_off"), py::arg("cap"));
+  m.def("ps_set_headers", &ps_set_headers);
+  m.def("ps_gather_rows", &ps_gather_rows, py::arg("bases"), py::arg("bounds"), py::arg("keys"), py::arg("n_dev"),
+        py::arg("W"), py::arg("out"));
+  m.attr("PS_ADD") = (int)minips_k::kPsAdd;
+  m.attr("PS_SGD") = (int)minips_k::kPsSgd;
+  m.attr("PS_ROWWISE_ADAGRAD") = (int)minips_k::kPsRowwiseAdagrad;
+  m.attr("PS_ADAGRAD") = (int)minips_k::kPsAdagrad;
+  m.attr("PS_ADAM") = (int)minips_k::kPsAdam;
+  py::class_<GpuAsyncServer>(m, "AsyncServer")
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t, int64_t>(), py::arg("board"), py::arg("world"),
+           py::arg("rank"), py::arg("tables"), py::arg("device"))
+      .def("add_sparse", &GpuAsyncServer::add_sparse)
+      .def("publish_after", &GpuAsyncServer::publish_after)
+      .def_property_readonly("published", &GpuAsyncServer::published)
+      .def_property_readonly("queued", &GpuAsyncServer::queued)
+      .def("publish_error", &GpuAsyncServer::publish_error)
+      .def("add_dense", &GpuAsyncServer::add_dense)
+      .def("step", &GpuAsyncServer::step)
+      .def("set_step", &GpuAsyncServer::set_step)
+      .def("start", &GpuAsyncServer::start)
+      .def("stop", &GpuAsyncServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def("pause", &GpuAsyncServer::pause, py::call_guard<py::gil_scoped_release>())
+      .def("resume", &GpuAsyncServer::resume)
+      .def("running", &GpuAsyncServer::running)
+      .def("error", &GpuAsyncServer::error)
+      .def("set_log", &GpuAsyncServer::set_log)
+      .def("take_log", &GpuAsyncServer::take_log)
+      .def_property_readonly("applied", &GpuAsyncServer::applied)
+      .def_property_readonly("batches", &GpuAsyncServer::batches);
 }

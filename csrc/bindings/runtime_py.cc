@@ -6,13 +6,14 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "../runtime/async_server.h"
 #include "../runtime/checkpoint.h"
-#include "../runtime/clock_board.h"
 #include "../runtime/fs.h"
 #include "../runtime/io.h"
 #include "../runtime/comm.h"
 #include "../runtime/config.h"
 #include "../runtime/engine.h"
+#include "../runtime/ps_board.h"
 #include "../runtime/shard_io.h"
 
 namespace py = pybind11;
@@ -100,6 +101,45 @@ void BindTable(py::module& m, const char* name) {
       .def("checkpoint", &KVClientTable<Val>::CheckPoint, py::call_guard<py::gil_scoped_release>())
       .def("heartbeat", &KVClientTable<Val>::HeartBeat, py::arg("node_id"), py::arg("quit") = false);
 }
+
+// The owner side of the asynchronous PS on a CPU rank (gloo tests): the same server loop as the
+// GPU ranks (csrc/runtime/async_server.h), applying through a Python callable apply(t, r, c)
+// that runs the table's CPU optimizer on the inbox slot. Exceptions become the server's error.
+class PyApplier : public Applier {
+ public:
+  explicit PyApplier(py::function fn) : fn_(std::move(fn)) {}
+  ~PyApplier() override {
+    py::gil_scoped_acquire g;
+    fn_ = py::function();
+  }
+  void Apply(int t, int r, int64_t c) override {
+    py::gil_scoped_acquire g;
+    try {
+      fn_(t, r, c);
+    } catch (py::error_already_set& e) {
+      throw std::runtime_error(std::string("async server apply: ") + e.what());
+    }
+  }
+  void Flush() override {}
+
+ private:
+  py::function fn_;
+};
+
+class CpuAsyncServer {
+ public:
+  CpuAsyncServer(const std::string& board, int world, int rank, int tables, py::function apply)
+      : applier_(std::move(apply)), server_(board, world, rank, tables, &applier_) {}
+  ~CpuAsyncServer() {
+    py::gil_scoped_release rel;
+    server_.Stop();
+  }
+  AsyncServer& server() { return server_; }
+
+ private:
+  PyApplier applier_;
+  AsyncServer server_;
+};
 
 }  // namespace
 
@@ -396,17 +436,45 @@ PYBIND11_MODULE(_runtime, m) {
   });
   m.def("remote_bytes_read", &RemoteBytesRead);
   m.def("local_host_name", &LocalHostName);
-  py::class_<ClockBoard>(m, "ClockBoard")
-      .def(py::init<const std::string&, int, int, bool, double>(), py::arg("name"), py::arg("world"), py::arg("rank"),
-           py::arg("create"), py::arg("attach_timeout_s") = 30.0)
-      .def("publish", &ClockBoard::Publish)
-      .def("get", &ClockBoard::Get)
-      .def("min_clock", &ClockBoard::MinClock)
-      .def("snapshot", &ClockBoard::Snapshot)
-      .def("wait_min_at_least", &ClockBoard::WaitMinAtLeast, py::arg("target"), py::arg("timeout_s") = 0.0,
+  py::class_<PSBoard>(m, "PSBoard")
+      .def(py::init<const std::string&, int, int, int, double>(), py::arg("name"), py::arg("world"), py::arg("rank"),
+           py::arg("tables"), py::arg("attach_timeout_s") = 30.0)
+      .def("publish_sent", &PSBoard::PublishSent)
+      .def("sent", &PSBoard::Sent)
+      .def("min_sent", &PSBoard::MinSent)
+      .def("publish_applied", &PSBoard::PublishApplied)
+      .def("publish_applied_row", &PSBoard::PublishAppliedRow)
+      .def("applied", &PSBoard::Applied)
+      .def("min_applied", &PSBoard::MinApplied)
+      .def("min_applied_from", &PSBoard::MinAppliedFrom)
+      .def("owner_version", &PSBoard::OwnerVersion)
+      .def("pending", &PSBoard::Pending)
+      .def("wait_min_applied", &PSBoard::WaitMinApplied, py::arg("table"), py::arg("target"), py::arg("timeout_s"),
            py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("wakeups", &ClockBoard::Wakeups)
-      .def("unlink", &ClockBoard::Unlink);
+      .def("wait_applied_from", &PSBoard::WaitAppliedFrom, py::arg("table"), py::arg("requester"), py::arg("target"),
+           py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
+      .def("wait_sent_at_least", &PSBoard::WaitSentAtLeast, py::arg("table"), py::arg("rank"), py::arg("target"),
+           py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
+      .def("snapshot_sent", &PSBoard::SnapshotSent)
+      .def("snapshot_applied", &PSBoard::SnapshotApplied)
+      .def("wake", &PSBoard::Wake)
+      .def_property_readonly("wakeups", &PSBoard::Wakeups)
+      .def_property_readonly("epoch", &PSBoard::Epoch)
+      .def("unlink", &PSBoard::Unlink);
+  py::class_<CpuAsyncServer>(m, "AsyncServer")
+      .def(py::init<const std::string&, int, int, int, py::function>(), py::arg("board"), py::arg("world"),
+           py::arg("rank"), py::arg("tables"), py::arg("apply"))
+      .def("enable", [](CpuAsyncServer& s, int t) { s.server().Enable(t); })
+      .def("start", [](CpuAsyncServer& s) { s.server().Start(); })
+      .def("stop", [](CpuAsyncServer& s) { s.server().Stop(); }, py::call_guard<py::gil_scoped_release>())
+      .def("pause", [](CpuAsyncServer& s) { s.server().Pause(); }, py::call_guard<py::gil_scoped_release>())
+      .def("resume", [](CpuAsyncServer& s) { s.server().Resume(); })
+      .def("running", [](CpuAsyncServer& s) { return s.server().Running(); })
+      .def("error", [](CpuAsyncServer& s) { return s.server().Error(); })
+      .def("set_log", [](CpuAsyncServer& s, bool on) { s.server().SetLog(on); })
+      .def("take_log", [](CpuAsyncServer& s) { return s.server().TakeLog(); })
+      .def_property_readonly("applied", [](CpuAsyncServer& s) { return s.server().Applied(); })
+      .def_property_readonly("batches", [](CpuAsyncServer& s) { return s.server().Batches(); });
   py::class_<BlockAssignerServer>(m, "BlockAssignerServer")
       .def(py::init<int>(), py::arg("port") = 0)
       .def("start", &BlockAssignerServer::Start)

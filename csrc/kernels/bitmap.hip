@@ -24,10 +24,13 @@ __device__ __forceinline__ int64_t bm_route(int64_t key, uint64_t mult, uint64_t
 }
 
 __global__ void bm_set_kernel(const int64_t* __restrict__ keys, int64_t n, uint64_t rmult, uint64_t rn,
-                              int64_t space, uint32_t* __restrict__ bitmap) {
+                              int64_t space, uint32_t* __restrict__ bitmap, int64_t* __restrict__ oor) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = bm_route(keys[i], rmult, rn);
-    if ((uint64_t)k >= (uint64_t)space) continue;  // outside the table: never written (no fault)
+    if ((uint64_t)k >= (uint64_t)space) {  // outside the table: never written (no fault), but counted
+      if (oor) atomicAdd(reinterpret_cast<unsigned long long*>(oor), 1ull);
+      continue;
+    }
     const uint32_t bit = 1u << (k & 31);
     uint32_t* w = bitmap + (k >> 5);
     if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
@@ -162,7 +165,7 @@ int64_t bitmap_plan_workspace_words(int64_t num_keys_space) {
 
 void bitmap_plan(const int64_t* keys, int64_t n, int64_t num_keys_space, const int64_t* bounds, int P,
                  uint64_t rmult, uint64_t rn, int64_t* ws, int64_t* uniq, int64_t* inverse, int64_t* counts,
-                 int64_t* U, hipStream_t s) {
+                 int64_t* U, hipStream_t s, int64_t* oor) {
   if (num_keys_space <= 0) throw std::runtime_error("bitmap_plan: empty key space");
   const int64_t nwords = (num_keys_space + 31) / 32;
   const int64_t nb = (nwords + kBmWordsPerBlock - 1) / kBmWordsPerBlock;
@@ -172,7 +175,8 @@ void bitmap_plan(const int64_t* keys, int64_t n, int64_t num_keys_space, const i
   int64_t* block_sums = word_prefix + nwords;
   MINIPS_HIP_CHECK(hipMemsetAsync(bitmap, 0, sizeof(uint32_t) * (size_t)nwords, s));
   if (n > 0)
-    hipLaunchKernelGGL(bm_set_kernel, grid_for(n, 256, 8192), 256, 0, s, keys, n, rmult, rn, num_keys_space, bitmap);
+    hipLaunchKernelGGL(bm_set_kernel, grid_for(n, 256, 8192), 256, 0, s, keys, n, rmult, rn, num_keys_space, bitmap,
+                       oor);
   hipLaunchKernelGGL(bm_count_kernel, (unsigned)nb, kBmThreads, 0, s, bitmap, nwords, block_sums);
   hipLaunchKernelGGL(bm_scan_blocks_kernel, 1, 1024, 0, s, block_sums, (int)nb, U);
   hipLaunchKernelGGL(bm_emit_kernel, (unsigned)nb, kBmThreads, 0, s, bitmap, nwords, block_sums, word_prefix, uniq);

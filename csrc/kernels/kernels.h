@@ -51,9 +51,11 @@ int ub_shards(int P);
 // Bitmap planning of a bounded key space [0, num_keys_space) (bitmap.hip): sorted unique keys,
 // inverse, per-owner counts (counts[P] = U) and U on the device. ws: bitmap_plan_workspace_words().
 int64_t bitmap_plan_workspace_words(int64_t num_keys_space);
+// oor (nullable, device int64): += the number of keys outside [0, num_keys_space) after routing
+// (they get inverse 0; the caller checks the counter at its next host sync and raises).
 void bitmap_plan(const int64_t* keys, int64_t n, int64_t num_keys_space, const int64_t* bounds, int P,
                  uint64_t rmult, uint64_t rn, int64_t* ws, int64_t* uniq, int64_t* inverse, int64_t* counts,
-                 int64_t* U, hipStream_t s);
+                 int64_t* U, hipStream_t s, int64_t* oor = nullptr);
 void unique_bucketize(const int64_t* keys, int64_t n, int F, const int64_t* bounds, int P, int64_t* table_keys,
                       int64_t* table_pos, int64_t cap, int64_t* slot, int32_t* flags, int64_t* counts,
                       int64_t* cursor, int64_t* out_keys, int64_t* inverse, hipStream_t s, uint64_t route_mult = 0,
@@ -149,13 +151,14 @@ void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int
 
 // ------------------------------------------------------------------ optimizers (optim.hip)
 // Fused Adam(W) on an fp32 master shard; optionally writes the bf16 copy for all-gather.
+// active (nullable, device): the kernel does nothing when *active == 0 (an empty async push).
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2,
                 float eps, float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s,
-                    const int* step_dev = nullptr,
-                bool zero_g = false);
-void sgd_apply(float* w, const float* g, int64_t n, float lr, float grad_scale, bf16_t* w_bf16, hipStream_t s);
+                const int* step_dev = nullptr, bool zero_g = false, const int64_t* active = nullptr);
+void sgd_apply(float* w, const float* g, int64_t n, float lr, float grad_scale, bf16_t* w_bf16, hipStream_t s,
+               const int64_t* active = nullptr);
 void adagrad_apply(float* w, float* acc, const float* g, int64_t n, float lr, float eps, float grad_scale,
-                   bf16_t* w_bf16, hipStream_t s);
+                   bf16_t* w_bf16, hipStream_t s, const int64_t* active = nullptr);
 void cast_f32_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t s);
 void cast_bf16_f32(const bf16_t* x, float* y, int64_t n, hipStream_t s);
 
@@ -226,12 +229,7 @@ void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t
                   const int64_t* offsets, int n_dense, const float* w, float* dense, int64_t* keys, float* labels,
                   hipStream_t s);
 
-// ------------------------------------------------------------------ one-sided xGMI path (onesided.hip)
-// bases [P] int64 device pointers of the per-rank fp32 shards [rows_o, W]; bounds [P+1] key ranges
-void remote_gather(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,
-                   const int64_t* n_dev, int W, void* out, bool out_bf16, hipStream_t s);
-void remote_scatter_add(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,
-                        const int64_t* n_dev, const float* vals, int W, float scale, hipStream_t s);
+// (the asynchronous PS path over xGMI -- push / gather / owner apply -- is declared in onesided.h)
 
 // ------------------------------------------------------------------ fp64 parity tables (f64.hip, ml.hip)
 void gather_rows_f64(const double* table, int W, const int64_t* keys, int64_t base, int64_t n, const int64_t* n_dev,

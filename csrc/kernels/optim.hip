@@ -12,7 +12,8 @@ namespace minips_k {
 __global__ void adam_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                             float* __restrict__ g, int64_t n, float lr, float b1, float b2, float eps, float wd,
                             float bc1, float bc2, float gscale, bf16_t* __restrict__ wb,
-                            const int* __restrict__ step_dev, bool zero_g) {
+                            const int* __restrict__ step_dev, bool zero_g, const int64_t* __restrict__ active) {
+  if (active && *active == 0) return;  // an empty push (a Clock without an Add): nothing to apply
   if (step_dev) {  // device-side step (graph-replayable clocks): bias corrections from *step_dev
     const float t = (float)*step_dev;
     bc1 = 1.f - powf(b1, t);
@@ -59,7 +60,7 @@ static void check_align(const void* p, const char* what) {
 
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2, float eps,
                 float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s, const int* step_dev,
-                bool zero_g) {
+                bool zero_g, const int64_t* active) {
   if (n <= 0) return;
   check_align(w, "adam w");
   check_align(m, "adam m");
@@ -70,12 +71,13 @@ void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float l
   const int block = 256;
   hipLaunchKernelGGL(adam_kernel, grid_for((n + 3) / 4, block), block, 0, s, w, m, v, const_cast<float*>(g),
                      n, lr, beta1, beta2, eps,
-                     weight_decay, bc1, bc2, grad_scale, w_bf16, step_dev, zero_g);
+                     weight_decay, bc1, bc2, grad_scale, w_bf16, step_dev, zero_g, active);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 __global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, int64_t n, float lr, float gscale,
-                           bf16_t* __restrict__ wb) {
+                           bf16_t* __restrict__ wb, const int64_t* __restrict__ active) {
+  if (active && *active == 0) return;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float x = w[i] - lr * g[i] * gscale;
     w[i] = x;
@@ -83,15 +85,18 @@ __global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, i
   }
 }
 
-void sgd_apply(float* w, const float* g, int64_t n, float lr, float grad_scale, bf16_t* w_bf16, hipStream_t s) {
+void sgd_apply(float* w, const float* g, int64_t n, float lr, float grad_scale, bf16_t* w_bf16, hipStream_t s,
+               const int64_t* active) {
   if (n <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(sgd_kernel, grid_for(n, block), block, 0, s, w, g, n, lr, grad_scale, w_bf16);
+  hipLaunchKernelGGL(sgd_kernel, grid_for(n, block), block, 0, s, w, g, n, lr, grad_scale, w_bf16, active);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 __global__ void adagrad_kernel(float* __restrict__ w, float* __restrict__ acc, const float* __restrict__ g, int64_t n,
-                               float lr, float eps, float gscale, bf16_t* __restrict__ wb) {
+                               float lr, float eps, float gscale, bf16_t* __restrict__ wb,
+                               const int64_t* __restrict__ active) {
+  if (active && *active == 0) return;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float gg = g[i] * gscale;
     const float a = acc[i] + gg * gg;
@@ -103,10 +108,11 @@ __global__ void adagrad_kernel(float* __restrict__ w, float* __restrict__ acc, c
 }
 
 void adagrad_apply(float* w, float* acc, const float* g, int64_t n, float lr, float eps, float grad_scale,
-                   bf16_t* w_bf16, hipStream_t s) {
+                   bf16_t* w_bf16, hipStream_t s, const int64_t* active) {
   if (n <= 0) return;
   const int block = 256;
-  hipLaunchKernelGGL(adagrad_kernel, grid_for(n, block), block, 0, s, w, acc, g, n, lr, eps, grad_scale, w_bf16);
+  hipLaunchKernelGGL(adagrad_kernel, grid_for(n, block), block, 0, s, w, acc, g, n, lr, eps, grad_scale, w_bf16,
+                     active);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

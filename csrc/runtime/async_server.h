@@ -1,0 +1,82 @@
+// Server thread of the asynchronous parameter server: the owner side of every SSP / ASP table on
+// one rank (minips_amd/ps/onesided.py).
+//
+// Parity: server/server_thread.cpp:23-61 (an actor that pops requests and dispatches them to the
+// table's model) and server/consistency/{ssp,asp}_model.cpp (Add applies at the server as soon
+// as it arrives: ssp_model.cpp:54-56, asp_model.cpp:18-21). Requests are not messages here: a
+// requester writes its clock's (key, gradient row) batch straight into an inbox slot in the
+// owner's HBM (one slot ring per requester) and bumps its `sent` counter on the PSBoard; this
+// thread sleeps on the board's futex, finds (table, requester, clock) triples with sent > applied,
+// has the Applier run the optimizer on them (row-wise Adagrad / Adam / SGD with the owner's own
+// optimizer state), waits for that device work and publishes `applied`. Gets never come here:
+// they read the owner's rows one-sidedly, gated on `applied` (PSBoard).
+//
+// Apply order inside one wake-up: clock-major, requesters interleaved (r0 c, r1 c, ..., r0 c+1,
+// ...), per table -- recorded in the apply log when enabled, so a test can replay the exact order.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ps_board.h"
+
+namespace minips {
+
+class Applier {
+ public:
+  virtual ~Applier() = default;
+  virtual void ThreadInit() {}  // called once on the server thread (e.g. bind the device)
+  // Issue the apply of requester `r`'s clock `c` of table `t` (inbox slot c % depth); may return
+  // before the work completed.
+  virtual void Apply(int t, int r, int64_t c) = 0;
+  // Complete every issued apply: the updated rows must be visible to every rank afterwards.
+  virtual void Flush() = 0;
+};
+
+class AsyncServer {
+ public:
+  AsyncServer(const std::string& board_name, int world, int rank, int tables, Applier* applier);
+  ~AsyncServer();
+  AsyncServer(const AsyncServer&) = delete;
+  AsyncServer& operator=(const AsyncServer&) = delete;
+
+  void Enable(int table);  // serve `table` from now on (its descriptors exist)
+  void Start();
+  void Stop();
+  // Pause: returns once no apply is in flight and none will start until Resume() (a consistent
+  // point of this owner's shards for a checkpoint snapshot or a restore).
+  void Pause();
+  void Resume();
+  bool Running() const { return running_.load(); }
+  std::string Error() const;
+  void SetLog(bool on);
+  std::vector<int64_t> TakeLog();  // flat (table, requester, clock) triples in apply order
+  int64_t Applied() const { return applies_.load(); }
+  int64_t Batches() const { return batches_.load(); }
+  PSBoard& board() { return board_; }
+
+ private:
+  void Loop();
+
+  PSBoard board_;
+  Applier* applier_;
+  const int world_, rank_, tables_;
+  std::vector<std::atomic<bool>> enabled_;
+  std::thread th_;
+  std::atomic<bool> stop_{false}, running_{false};
+  std::atomic<int64_t> applies_{0}, batches_{0};
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  bool pause_req_ = false, paused_ = false;
+  std::string error_;
+  bool log_on_ = false;
+  std::vector<int64_t> log_;
+};
+
+}  // namespace minips

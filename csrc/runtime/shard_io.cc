@@ -166,7 +166,9 @@ ShardHeader ReadShardHeader(const std::string& path) {
   i.read(magic, 8);
   MINIPS_CHECK(i.good() && std::memcmp(magic, kMagic, 8) == 0, "not a minips shard file: " << path);
   const uint32_t ver = get<uint32_t>(i);
-  MINIPS_CHECK(ver == kVersion, "unsupported shard version " << ver << " in " << path);
+  // v1 (round-1 trees): the same header fields, but each array's bytes follow its descriptor
+  // (no offset field) -- still readable, so old checkpoints restore
+  MINIPS_CHECK(ver == kVersion || ver == 1, "unsupported shard version " << ver << " in " << path);
   ShardHeader h;
   h.meta.global_rows = get<uint64_t>(i);
   h.meta.base = get<uint64_t>(i);
@@ -186,8 +188,14 @@ ShardHeader ReadShardHeader(const std::string& path) {
     a.rows = get<uint64_t>(i);
     a.cols = get<uint64_t>(i);
     a.bytes = get<uint64_t>(i);
-    a.offset = get<uint64_t>(i);
     MINIPS_CHECK(a.bytes == a.rows * a.cols * DTypeSize(a.dtype), "array size mismatch in " << path);
+    if (ver == 1) {
+      a.offset = (uint64_t)i.tellg();
+      i.seekg((std::streamoff)a.bytes, std::ios::cur);
+      MINIPS_CHECK(i.good(), "truncated array " << a.name << " in " << path);
+    } else {
+      a.offset = get<uint64_t>(i);
+    }
     h.arrays.push_back(a);
   }
   return h;
@@ -257,10 +265,19 @@ void ShardFileWriter::WriteRows(int array, uint64_t row0, const void* src, uint6
 
 void ShardFileWriter::Close() {
   MINIPS_CHECK(fd_ >= 0, "ShardFileWriter already closed");
+  // durable before published: a committed 'latest' must never name data still in the page cache
+  // when the machine loses power
+  MINIPS_CHECK(::fsync(fd_) == 0, "fsync " << tmp_ << ": " << std::strerror(errno));
   MINIPS_CHECK(::close(fd_) == 0, "close " << tmp_);
   fd_ = -1;
   // atomic publish: a crash mid-write never leaves a truncated checkpoint under the real name
   MINIPS_CHECK(std::rename(tmp_.c_str(), path_.c_str()) == 0, "rename " << tmp_ << " -> " << path_);
+  const std::string dir = path_.find('/') == std::string::npos ? "." : path_.substr(0, path_.rfind('/') + 1);
+  const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+  if (dfd >= 0) {  // the rename itself (the directory entry) reaches the disk too
+    (void)::fsync(dfd);
+    ::close(dfd);
+  }
 }
 
 TextParamsWriter::TextParamsWriter(const std::string& path) : path_(path) {

@@ -6,6 +6,7 @@
 // comm/{sender,mailbox}_test) with identical expected values, plus the tests the reference
 // lacked: checkpoint round trips in all three models, BSP/ASP CheckPoint not hanging,
 // libsvm/dumper round trip, heartbeat failure detection. Ports are ephemeral (no races).
+#include <array>
 #include <atomic>
 #include <netinet/in.h>
 #include <sys/socket.h>
@@ -15,7 +16,7 @@
 #include <fstream>
 
 #include "../runtime/checkpoint.h"
-#include "../runtime/clock_board.h"
+#include "../runtime/async_server.h"
 #include "../runtime/comm.h"
 #include "../runtime/config.h"
 #include "../runtime/engine.h"
@@ -1158,40 +1159,144 @@ TEST(FS, UrlsAndGeneralStreams) {
   ::unlink(ParseUrl(p).path.c_str());
 }
 
-TEST(ClockBoard, SspGateWakesOnPublishAndTimesOut) {
-  // Two ranks' views of one segment (as two processes map it): rank 0 waits for min clock >= 3
-  // while rank 1 publishes 1, 2, 3; the wait returns only after the last publish. A stuck clock
-  // makes the gate throw after its timeout instead of hanging.
+TEST(PSBoard, SspGateWakesOnAppliedAndTimesOut) {
+  // Two ranks' views of one segment (as two processes map it). Rank 1 (an owner) applies rank 0's
+  // and its own clocks one by one; rank 0's SSP gate (min applied >= 3) returns only after the
+  // last publish, and a stuck owner makes the wait report a timeout instead of hanging.
   using namespace minips;
-  const std::string name = "minips_cb_test_" + std::to_string(::getpid());
-  ClockBoard r0(name, 2, 0, true), r1(name, 2, 1, false);
-  r0.Publish(5);
-  EXPECT_EQ(r1.Get(0), 5);
-  EXPECT_EQ(r0.MinClock(), 0);
+  const std::string name = "minips_psb_test_" + std::to_string(::getpid());
+  PSBoard r0(name, 2, 0, 2), r1(name, 2, 1, 2);
+  r0.PublishSent(1, 5);
+  EXPECT_EQ(r1.Sent(1, 0), 5);
+  EXPECT_EQ(r1.Sent(0, 0), 0);  // tables are independent
+  EXPECT_EQ(r0.MinSent(1), 0);
+  r0.PublishAppliedRow(1, 3);  // owner 0 has every requester's clocks < 3 of table 1
+  EXPECT_EQ(r1.Applied(1, 0, 1), 3);
+  EXPECT_EQ(r1.MinApplied(1), 0);
   std::atomic<int> published{0};
-  std::thread pub([&] {
+  std::thread owner([&] {
     for (int c = 1; c <= 3; ++c) {
       std::this_thread::sleep_for(std::chrono::milliseconds(20));
       published = c;
-      r1.Publish(c);
+      r1.PublishApplied(1, 0, c);
+      r1.PublishApplied(1, 1, c);
     }
   });
-  const double waited = r0.WaitMinAtLeast(3, 10.0);
+  const double waited = r0.WaitMinApplied(1, 3, 10.0);
   EXPECT_EQ(published.load(), 3);
   EXPECT_TRUE(waited > 0.03);
-  EXPECT_EQ(r0.MinClock(), 3);
-  pub.join();
-  bool threw = false;
-  try {
-    r0.WaitMinAtLeast(9, 0.05);
-  } catch (const CheckError&) {
-    threw = true;
-  }
-  EXPECT_TRUE(threw);
-  std::vector<int64_t> snap = r1.Snapshot();
-  EXPECT_EQ(snap[0], 5);
-  EXPECT_EQ(snap[1], 3);
+  EXPECT_EQ(r0.MinApplied(1), 3);
+  EXPECT_EQ(r0.MinAppliedFrom(1, 0), 3);
+  EXPECT_EQ(r0.OwnerVersion(1, 1), 6);
+  owner.join();
+  EXPECT_TRUE(r0.WaitMinApplied(1, 9, 0.05) < 0);  // timeout: reported, not thrown
+  EXPECT_EQ(r1.Pending(1), 2);                      // rank 0 sent 5 clocks, owner 1 applied 3
+  std::vector<int64_t> a = r0.SnapshotApplied(1);
+  EXPECT_EQ(a.size(), 4u);
+  EXPECT_EQ(a[0 * 2 + 1], 3);
   r0.Unlink();
+}
+
+namespace {
+struct RecordingApplier : minips::Applier {
+  std::vector<std::array<int64_t, 3>> seen;
+  int flushes = 0;
+  void Apply(int t, int r, int64_t c) override { seen.push_back({t, r, c}); }
+  void Flush() override { ++flushes; }
+};
+}  // namespace
+
+TEST(AsyncServer, AppliesArrivedClocksInOrderAndPauses) {
+  // The owner-side server thread: every (table, requester, clock) that arrived is applied exactly
+  // once, clock-major with the requesters interleaved, then published as applied; a paused
+  // server applies nothing until resumed.
+  using namespace minips;
+  const std::string name = "minips_srv_test_" + std::to_string(::getpid());
+  PSBoard req0(name, 2, 0, 2), req1(name, 2, 1, 2);
+  RecordingApplier ap;
+  AsyncServer srv(name, 2, 0, 2, &ap);
+  srv.SetLog(true);
+  srv.Enable(0);
+  srv.Start();
+  req1.PublishAppliedRow(0, 1000);  // owner 1 (no server in this test) has applied everything
+  req0.PublishSent(0, 2);
+  req1.PublishSent(0, 2);
+  EXPECT_TRUE(req0.WaitAppliedFrom(0, 0, 2, 5.0) >= 0);
+  EXPECT_TRUE(req1.WaitAppliedFrom(0, 1, 2, 5.0) >= 0);
+  srv.Pause();
+  req1.PublishSent(0, 3);
+  std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  EXPECT_EQ(req1.Applied(0, 0, 1), 2);  // paused: clock 2 of requester 1 waits
+  srv.Resume();
+  EXPECT_TRUE(req1.WaitAppliedFrom(0, 1, 3, 5.0) >= 0);
+  srv.Stop();
+  EXPECT_EQ(srv.Error(), "");
+  std::vector<int64_t> log = srv.TakeLog();
+  EXPECT_EQ(log.size(), 15u);  // 5 applies
+  EXPECT_EQ(srv.Applied(), 5);
+  // the first wake-up saw both requesters at clock 2 (or applied them as they came): every
+  // requester's clocks appear in increasing order
+  int64_t last[2] = {-1, -1};
+  for (size_t i = 0; i < log.size(); i += 3) {
+    EXPECT_EQ(log[i], 0);
+    EXPECT_TRUE(log[i + 2] == last[log[i + 1]] + 1);
+    last[log[i + 1]] = log[i + 2];
+  }
+  EXPECT_TRUE(ap.flushes >= 1);
+  req0.Unlink();
+}
+
+TEST(ShardIO, ReadsVersion1Files) {
+  // Round-1 shard files (v1: each array's bytes right after its descriptor, no offsets) still
+  // restore through the v2 reader (header parse + offset ranged reads).
+  using namespace minips;
+  const std::string path = "/tmp/minips_v1_" + std::to_string(::getpid()) + ".bin";
+  {
+    std::ofstream o(path, std::ios::binary);
+    auto put = [&](const auto& v) { o.write(reinterpret_cast<const char*>(&v), sizeof(v)); };
+    auto put_s = [&](const std::string& str) {
+      put((uint32_t)str.size());
+      o.write(str.data(), (std::streamsize)str.size());
+    };
+    o.write("MPSSHRD1", 8);
+    put((uint32_t)1);
+    put((uint64_t)10);  // global_rows
+    put((uint64_t)4);   // base
+    put((uint64_t)3);   // rows
+    put((uint64_t)2);   // cols
+    put((int64_t)7);    // clock
+    put((int32_t)0);
+    put((int32_t)1);
+    put((int32_t)2);
+    put_s("sparse");
+    put((uint32_t)2);
+    const float p[6] = {1, 2, 3, 4, 5, 6};
+    put_s("params");
+    put((uint32_t)DType::kF32);
+    put((uint64_t)3);
+    put((uint64_t)2);
+    put((uint64_t)24);
+    o.write(reinterpret_cast<const char*>(p), 24);
+    const float st[3] = {0.5f, 0.25f, 0.125f};
+    put_s("state");
+    put((uint32_t)DType::kF32);
+    put((uint64_t)3);
+    put((uint64_t)1);
+    put((uint64_t)12);
+    o.write(reinterpret_cast<const char*>(st), 12);
+  }
+  LoadedShard s = ReadShard(path);
+  EXPECT_EQ(s.meta.clock, 7);
+  EXPECT_EQ(s.meta.base, 4u);
+  EXPECT_EQ(s.arrays.size(), 2u);
+  const float* got = reinterpret_cast<const float*>(s.arrays[0].bytes.data());
+  EXPECT_EQ(got[5], 6.f);
+  const float* gs = reinterpret_cast<const float*>(s.arrays[1].bytes.data());
+  EXPECT_EQ(gs[2], 0.125f);
+  float row[2];
+  ReadRows(path, ReadShardHeader(path).arrays[0].offset, 8, 1, 1, row);  // partial (owner-range) read
+  EXPECT_EQ(row[0], 3.f);
+  ::unlink(path.c_str());
 }
 
 int main(int argc, char** argv) { return minitest::RunAll(argc, argv); }

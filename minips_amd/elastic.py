@@ -63,6 +63,7 @@ class Supervisor:
         self.startup_grace = startup_grace
         self.recovery = recovery
         self.progress_timeout = progress_timeout if progress_timeout is not None else 3 * heartbeat_interval
+        self.ckpt_timeout = float(os.environ.get("MINIPS_CKPT_TIMEOUT", "3600"))
         self.restarts = 0
         self.generation = 0
         self.procs: list[subprocess.Popen | None] = [None] * nproc
@@ -160,7 +161,9 @@ class Supervisor:
             if step != last or state == "recover":
                 self.progress[r] = (step, now)
                 continue
-            limit = self.startup_grace if step < 0 else self.progress_timeout
+            # a checkpoint write / commit advances no step: it gets its own, longer limit
+            limit = self.startup_grace if step < 0 else (self.ckpt_timeout if state == "ckpt"
+                                                         else self.progress_timeout)
             if now - since > limit:
                 stalled.append((r, state, step))
         if all_done:

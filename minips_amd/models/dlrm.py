@@ -6,8 +6,9 @@
           + 40 GB of state over 8 x 288 GB -- sized per rank by `rows`).
   dense:  bottom MLP 13 -> 512 -> 256 -> D, dot interaction of the D-vector with the 26
           embeddings (351 pairs + D), top MLP 416 -> 512 -> 256 -> 1, BCE. One DenseTable.
-Consistency "asp" runs every Clock's exchange (all-to-all-v over RCCL point-to-point
-send/recv + apply) on a side stream without gating the next Gets beyond a 2-clock bound;
+Consistency "asp" on the collective transport runs every Clock's exchange (all-to-all-v over
+RCCL point-to-point send/recv + apply) on a side stream, gating the next Gets at a 2-clock
+pipelining depth; transport "onesided" is the unbounded asynchronous PS (ps/onesided.py).
 "bsp"/"ssp" are available as for the other models.
 """
 from __future__ import annotations
@@ -38,9 +39,11 @@ class DLRMConfig:
     staleness: int = 0
     p2p: bool = True
     # "collective": SparseTable / DenseTable over RCCL (all-to-all-v / RS+AG, gated per consistency);
-    # "onesided": SSP / ASP async SGD with NO collective on the data path -- rows gathered from and
-    # atomically added into the owners' IPC-mapped HBM over xGMI (ps/onesided.py)
+    # "onesided": SSP / ASP with NO collective on the data path -- rows read from the owners'
+    # IPC-mapped HBM over xGMI, gradients pushed into the owners' inboxes, row-wise Adagrad / Adam
+    # applied by each owner's server thread with its own state (ps/onesided.py)
     transport: str = "collective"
+    max_batch: int = 16384       # onesided: inbox slots hold max_batch * F gradient rows
     seed: int = 0
     cards: list = field(default_factory=list)  # optional per-feature cardinalities (sum <= num_rows)
 
@@ -51,11 +54,11 @@ class DLRM(LookaheadPlans):
         D, F = cfg.D, cfg.F
         self.NV = F + 1
         if cfg.transport == "onesided":
-            from ..ps.onesided import OneSidedSparseTable
+            from ..ps.onesided import AsyncSparseTable
 
-            self.emb = OneSidedSparseTable(comm, cfg.num_rows, D, optimizer="sgd", lr=cfg.lr_sparse,
-                                           consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
-                                           seed=cfg.seed, pull_dtype=torch.bfloat16)
+            self.emb = AsyncSparseTable(comm, cfg.num_rows, D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
+                                        consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
+                                        seed=cfg.seed, max_keys=cfg.max_batch * F)
         else:
             self.emb = SparseTable(comm, cfg.num_rows, D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
                                    consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
@@ -68,10 +71,10 @@ class DLRM(LookaheadPlans):
         self.top = [Linear(self.layout, f"top{i}", tdims[i], tdims[i + 1]) for i in range(len(tdims) - 1)]
         self.layout.add("head", (cfg.top[-1] + 8,))
         if cfg.transport == "onesided":
-            from ..ps.onesided import OneSidedDenseTable
+            from ..ps.onesided import AsyncDenseTable
 
-            self.dense = OneSidedDenseTable(comm, self.layout.size, lr=cfg.lr_dense * 10,
-                                            consistency=cfg.consistency, staleness=cfg.staleness)
+            self.dense = AsyncDenseTable(comm, self.layout.size, optimizer="adam", lr=cfg.lr_dense,
+                                         consistency=cfg.consistency, staleness=cfg.staleness)
         else:
             self.dense = DenseTable(comm, self.layout.size, optimizer="adam", lr=cfg.lr_dense,
                                     consistency=cfg.consistency, staleness=cfg.staleness, p2p=False)

@@ -41,6 +41,11 @@ class WideDeepConfig:
     lr_sparse: float = 0.02
     consistency: str = "bsp"
     staleness: int = 0
+    # "collective": SparseTable / DenseTable over RCCL; "onesided": SSP / ASP with no collective on
+    # the data path -- rows pulled one-sidedly from the owners' HBM, gradients pushed into the
+    # owners' inboxes, row-wise Adagrad / Adam applied by each owner's server thread (ps/onesided.py)
+    transport: str = "collective"
+    max_batch: int = 16384       # onesided: inbox slots hold max_batch * F gradient rows
     seed: int = 0
 
     @property
@@ -85,9 +90,17 @@ class WideDeep(LookaheadPlans):
         F, D = cfg.F, cfg.emb_dim
         self.num_rows = int(sum(cfg.cards))
         bases = [sum(cfg.cards[:f]) for f in range(F)]  # feature f's ids start at its offset
-        self.emb = SparseTable(comm, self.num_rows, cfg.row_width, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
-                               consistency=cfg.consistency, staleness=cfg.staleness, split=D, table_id=0,
-                               init_std=0.01, seed=cfg.seed, columns=(bases, cfg.cards))
+        if cfg.transport == "onesided":
+            from ..ps.onesided import AsyncSparseTable
+
+            self.emb = AsyncSparseTable(comm, self.num_rows, cfg.row_width, optimizer="rowwise_adagrad",
+                                        lr=cfg.lr_sparse, consistency=cfg.consistency, staleness=cfg.staleness,
+                                        split=D, table_id=0, init_std=0.01, seed=cfg.seed,
+                                        columns=(bases, cfg.cards), max_keys=cfg.max_batch * F)
+        else:
+            self.emb = SparseTable(comm, self.num_rows, cfg.row_width, optimizer="rowwise_adagrad",
+                                   lr=cfg.lr_sparse, consistency=cfg.consistency, staleness=cfg.staleness, split=D,
+                                   table_id=0, init_std=0.01, seed=cfg.seed, columns=(bases, cfg.cards))
         # wide weights start at zero (columns >= D)
         self.emb.shard[:, D:].zero_()
         # Dense layout: each Linear is stored as W_ext [n_out, k_pad] with the bias in column k_in;
@@ -111,8 +124,14 @@ class WideDeep(LookaheadPlans):
         self.layout["w4"] = (off, (cfg.hidden[-1] + 8,))  # [w4 | b4 | pad]
         off += cfg.hidden[-1] + 8
         self.n_params = off
-        self.dense = DenseTable(comm, self.n_params, optimizer="adam", lr=cfg.lr_dense,
-                                consistency=cfg.consistency, staleness=cfg.staleness, table_id=1)
+        if cfg.transport == "onesided":
+            from ..ps.onesided import AsyncDenseTable
+
+            self.dense = AsyncDenseTable(comm, self.n_params, optimizer="adam", lr=cfg.lr_dense,
+                                         consistency=cfg.consistency, staleness=cfg.staleness, table_id=1)
+        else:
+            self.dense = DenseTable(comm, self.n_params, optimizer="adam", lr=cfg.lr_dense,
+                                    consistency=cfg.consistency, staleness=cfg.staleness, table_id=1)
         self.dense.load_full(self._init_dense(dev))
         self._bufs = {}
         self._side = SideStream(dev, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
@@ -235,7 +254,8 @@ class WideDeep(LookaheadPlans):
         # an async dense clock (its own stream) needs only the weight gradients: issued from the
         # side stream it starts as soon as the last wgrad ends, beside the embedding backward and
         # the sparse push, instead of behind them
-        dense_early = _DENSE_CLOCK_ON_SIDE and self.dense.pipe.async_ and side.stream is not None
+        pipe = getattr(self.dense, "pipe", None)  # (collective tables only)
+        dense_early = _DENSE_CLOCK_ON_SIDE and pipe is not None and pipe.async_ and side.stream is not None
         if dense_early:
             with torch.cuda.stream(side.stream):
                 self.dense.add()

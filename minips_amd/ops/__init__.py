@@ -209,15 +209,24 @@ def unique_bucketize_n(keys: torch.Tensor, bounds: torch.Tensor, F: int = 1, rou
     return out, inv, counts, torch.tensor([u.numel()], dtype=torch.int64)
 
 
-def bitmap_plan(keys: torch.Tensor, bounds: torch.Tensor, num_rows: int, route_mult: int = 0):
+def bitmap_plan(keys: torch.Tensor, bounds: torch.Tensor, num_rows: int, route_mult: int = 0, oor=None):
     """unique_bucketize_n for a bounded key space: keys (after the optional routing
     key * route_mult mod num_rows) in [0, num_rows). GPU: an N-bit map + popcount ranks
     (csrc/kernels/bitmap.hip), no hash table; the unique keys come out sorted, so the CPU
-    reference (torch.unique) produces the identical plan. Returns (uniq, inverse, counts, U)."""
+    reference (torch.unique) produces the identical plan. Returns (uniq, inverse, counts, U).
+    ``oor`` (device int64 [1], optional): accumulates the number of keys outside the key space
+    (they would alias row 0); the caller checks it at a host sync point (no sync here)."""
     if _gpu(keys):
         return tuple(kernels().bitmap_plan(keys.reshape(-1).contiguous(), bounds.contiguous(), int(num_rows),
-                                           int(route_mult), int(num_rows) if route_mult else 0))
-    return unique_bucketize_n(keys.reshape(-1), bounds, 1, int(route_mult), int(num_rows) if route_mult else 0)
+                                           int(route_mult), int(num_rows) if route_mult else 0, oor))
+    flat = keys.reshape(-1)
+    k = (flat * route_mult) % num_rows if route_mult else flat
+    bad = (k < 0) | (k >= num_rows)
+    if bool(bad.any()):
+        if oor is None:
+            raise ValueError(f"keys outside [0, {num_rows})")
+        oor += int(bad.sum())
+    return unique_bucketize_n(flat, bounds, 1, int(route_mult), int(num_rows) if route_mult else 0)
 
 
 _PLAN_BITS_CAP = int(__import__("os").environ.get("MINIPS_PLAN_BITS_CAP", "0"))

@@ -50,6 +50,7 @@ import torch
 
 from .._native import runtime
 from ..utils.metrics import get_logger
+from .fault import slow_io_delay
 
 _DT = {torch.float32: "float32", torch.bfloat16: "bfloat16", torch.float64: "float64", torch.int64: "int64",
        torch.int32: "int32"}
@@ -129,6 +130,12 @@ class Checkpointer:
         allc = torch.empty(self.comm.world * clocks.numel(), dtype=torch.float64, device=self.comm.device)
         self.comm.all_gather(allc, clocks)
         allc = allc.view(self.comm.world, -1).cpu()
+        # asynchronous tables: every rank drained its pushes (the all-gather above ordered that), so
+        # every push so far is applied; the owners' server threads now stop until the snapshot is
+        # taken (the reference SSPModel::Dump runs inside its server thread, ssp_model.cpp:112-125)
+        paused = [t for t in tables.values() if hasattr(t, "snapshot_begin")]
+        for t in paused:
+            t.snapshot_begin()
         jobs = []
         for k, (tid, table) in enumerate(sorted(tables.items())):
             meta, arrays = table.shard_state()
@@ -176,8 +183,16 @@ class Checkpointer:
             if self.cuda:
                 self._stream.wait_stream(cur)
 
+        if paused and mode != "stream":  # resume once the snapshot copies are complete
+            if ev is not None:
+                ev.synchronize()
+            for t in paused:
+                t.snapshot_end()
+            paused = []
+
         def work():
             try:
+                slow_io_delay(self.comm.rank)  # fault injection (tests): a slow checkpoint disk
                 if ev is not None:
                     ev.synchronize()
                 for tid, meta, arrs, clk in jobs:
@@ -193,7 +208,11 @@ class Checkpointer:
 
         self._pending_iter = int(iteration)
         if mode == "stream":  # no room for a snapshot: write from the live shards, training waits
-            work()
+            try:
+                work()
+            finally:
+                for t in paused:
+                    t.snapshot_end()
             self._thread = None
             if self._error is not None:
                 e, self._error = self._error, None
@@ -299,6 +318,7 @@ class Checkpointer:
         if self._pending_iter is None:
             return
         self.wait()
+        self.comm.store_barrier("ckpt_commit")  # write times differ by rank: no PG timeout here
         self.comm.barrier()
         it, self._pending_iter = self._pending_iter, None
         if self.comm.rank == 0:
@@ -429,6 +449,10 @@ class Checkpointer:
                                                  d[a - lo: b - lo])
             table.finish_restore(clock or 0)
         self._release_staging()
+        slow_io_delay(self.comm.rank)  # fault injection (tests): a rank whose restore reads are slow
+        # restore times differ by rank (owner-range reads): meet on a long-timeout host barrier
+        # before the next collective can start its PG timeout
+        self.comm.store_barrier("restore")
         cfg_path = _prefix_path(src, f"worker_config_{self.my_id}")
         if os.path.exists(cfg_path):
             cfg = runtime().load_config_data(cfg_path)

@@ -33,6 +33,7 @@ import contextlib
 import datetime
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 
 import torch
@@ -81,6 +82,7 @@ class Comm:
     def refresh(self):
         """Re-read rank / world / backend after the default process group was re-created (in-place
         rollback, minips_amd.train): every table keeps this same Comm object."""
+        self._sb = 0  # the new group's store starts its barrier counters afresh
         self.initialized = dist.is_available() and dist.is_initialized()
         self.rank = dist.get_rank(self.group) if self.initialized else 0
         self.world = dist.get_world_size(self.group) if self.initialized else 1
@@ -270,6 +272,31 @@ class Comm:
         with self.waiting():
             dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
         return t
+
+    def store_barrier(self, tag: str, timeout_s: float | None = None):
+        """Host barrier through the c10d store with its own long timeout (MINIPS_LONG_PHASE_TIMEOUT,
+        default 3600 s), for the end of a phase whose length differs by rank -- a checkpoint restore
+        (owner-range reads of up to ~85 GB per rank), a foreground checkpoint write. Without it the
+        next collective would start its PG timeout (MINIPS_PG_TIMEOUT, 60 s) on the fast ranks and
+        abort a healthy job; after it every rank is present and the collective completes at once.
+        The heartbeat reports "comm" meanwhile (a rank waiting for slow peers is not stuck)."""
+        if self.world == 1 and not self.force:
+            return
+        if not self.initialized:
+            return
+        store = dist.distributed_c10d._get_default_store()
+        self._sb = getattr(self, "_sb", 0) + 1
+        members = dist.get_process_group_ranks(self.group) if self.group is not None else range(self.world)
+        key = f"minips_sb/{tag}/{self._sb}/" + ",".join(str(r) for r in members)
+        store.add(key, 1)
+        limit = timeout_s if timeout_s is not None else float(os.environ.get("MINIPS_LONG_PHASE_TIMEOUT", "3600"))
+        t0 = time.monotonic()
+        with self.waiting():
+            while int(store.add(key, 0)) < self.world:
+                if time.monotonic() - t0 > limit:
+                    raise TimeoutError(f"store barrier {tag!r}: {int(store.add(key, 0))}/{self.world} ranks "
+                                       f"after {limit:.0f} s")
+                time.sleep(0.005)
 
     def barrier(self):
         if self.world == 1 and not self.force:

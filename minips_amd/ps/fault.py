@@ -111,3 +111,14 @@ class FaultInjector:
                   flush=True)
             while True:
                 time.sleep(3600)
+
+
+def slow_io_delay(rank: int):
+    """Fault injection for long-phase tests: MINIPS_FAULT_SLOW_IO="<rank>:<seconds>" makes each
+    checkpoint write and restore of that rank take that much longer (a slow disk / network FS)."""
+    spec = os.environ.get("MINIPS_FAULT_SLOW_IO", "")
+    if not spec:
+        return
+    r, secs = spec.split(":")
+    if int(r) == rank:
+        time.sleep(float(secs))

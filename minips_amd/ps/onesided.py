@@ -1,37 +1,39 @@
-"""Really asynchronous SSP / ASP for GPU ranks: one-sided row access over xGMI.
+"""Asynchronous SSP / ASP parameter server for GPU ranks: one-sided rows over xGMI and an
+owner-side optimizer apply.
 
 A collective rendezvous at every clock (all-to-all, reduce-scatter) makes every rank wait for the
-slowest one, whatever the staleness setting. The reference's ASPModel replies and applies
-immediately (server/consistency/asp_model.cpp:18-26) and SSPModel lets a worker run up to
-``staleness`` clocks ahead of the slowest worker (ssp_model.cpp:58-85, progress_tracker.cpp:46-72).
-This table gets the same semantics with NO collective on the data path:
+slowest one, whatever the staleness setting. The reference's servers apply each Add as it arrives
+(SSPModel::Add, server/consistency/ssp_model.cpp:54-56; ASPModel::Add, asp_model.cpp:18-21) with
+the table's own update rule, answer a Get immediately (ASP, asp_model.cpp:23-26) or once the
+slowest worker is within ``staleness`` clocks (SSP, ssp_model.cpp:58-85), and never make a worker
+wait for a peer's pushes. These tables do the same with no collective on the data path:
 
-* every rank hipMallocs its shard (equal key ranges, fp32 rows) and exports it with
-  hipIpcGetMemHandle; every rank maps every peer shard (hipIpcOpenMemHandle, peer access over
-  xGMI), so any GPU addresses the whole table through a device table of base pointers
-  (csrc/kernels/onesided.hip);
-* Get = direct gather of the requested rows from their owners' HBM; Add + Clock = atomic
-  scatter-add into the owners' rows (``add``: w += delta, the reference SubAdd; ``sgd``:
-  w -= lr * g, the ASP async SGD of the DLRM config) -- the owner does nothing;
-* progress: a clock vector in host shared memory (/dev/shm, one slot per rank; the native
-  csrc/runtime/clock_board.h, futex wake-ups). A rank
-  publishes clock c+1 only after its clock-c adds completed on the GPU (a publisher thread
-  waits on the event recorded after them), so a reader that sees clock c+1 sees those adds.
-* SSP gate (a Get at own clock c): wait until min over ranks >= c - staleness -- the
-  reference's "buffer the Get while progress > min_clock + staleness". ASP never waits.
+* every rank hipMallocs its shard and an inbox and exports both (hipIpcGetMemHandle); every rank
+  maps every peer's buffers (hipIpcOpenMemHandle, peer access over xGMI);
+* Get  = ``ps_gather_rows``: the requested rows straight from the owners' HBM (16-byte loads);
+* Add + Clock = ``ps_push_rows``: the requester writes its deduplicated (key, gradient row)
+  batch, grouped by owner, into slot ``clock % depth`` of its ring in each owner's inbox (the
+  per-owner row counts go into the slot headers on the device: no host round trip), then a
+  native thread publishes ``sent`` on the PSBoard once those writes completed;
+* the owner's AsyncServer thread (csrc/runtime/async_server.h) -- the ServerThread of
+  server/server_thread.cpp -- sleeps on the board, applies every arrived slot with the table's
+  optimizer and the OWNER's state (row-wise Adagrad, Adam, Adagrad, SGD or the reference's plain
+  add; csrc/kernels/onesided.hip HipApplier) on its own high-priority stream, and publishes
+  ``applied``;
+* SSP gate (a Get at own clock c): every owner has applied every requester's clocks < c - s,
+  i.e. min applied >= c - s (csrc/runtime/ps_board.h); ASP never waits (``asp_bound`` optionally
+  bounds it the same way); a requester reuses an inbox slot only after every owner applied it.
 
-The same code runs on CPU ranks (gloo tests) with the shards in /dev/shm files (np.memmap) and
-a per-owner file lock around the scatter-add in place of the GPU atomics.
+The same code runs on CPU ranks (gloo tests): shards and inboxes are /dev/shm files mapped by
+every rank, the server thread is the same C++ loop calling back into the PyTorch reference
+optimizers. Reference semantics kept: BSP stays on the collective tables (ps/tables.py).
 """
 from __future__ import annotations
 
-import fcntl
+import collections
 import os
-import queue
-import threading
 import time
 import uuid
-from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -39,346 +41,590 @@ import torch.distributed as dist
 
 from .. import ops
 from .comm import Comm
-from .tables import even_bounds
+from .tables import SparsePlan, SparseTable, _PendingPlan, column_spec, even_bounds, _route_multiplier
+
+_MAX_TABLES = 16
+_SLOT_HEADER = 64
 
 
-class ClockBoard:
-    """Per-rank clocks in a /dev/shm segment shared by the ranks of one node: the native board
-    (csrc/runtime/clock_board.h -- one cache line per rank, release stores, a futex the SSP gate
-    sleeps on instead of polling from Python)."""
+def _align(n: int, a: int) -> int:
+    return (n + a - 1) // a * a
 
-    def __init__(self, comm: Comm, name: str | None = None):
+
+_OPT_CODES = {"add": 0, "sgd": 1, "rowwise_adagrad": 2, "adagrad": 3, "adam": 4}
+
+
+class AsyncPS:
+    """The asynchronous PS context of one rank (one per Comm): the shared progress board, the
+    owner's server thread and the requester's clock publisher. Tables register in creation
+    order, which is the same on every rank."""
+
+    @classmethod
+    def of(cls, comm: Comm) -> "AsyncPS":
+        ps = getattr(comm, "_async_ps", None)
+        if ps is None or ps.closed:
+            ps = cls(comm)
+            comm._async_ps = ps
+        return ps
+
+    def __init__(self, comm: Comm):
         from .._native import runtime
 
         self.comm = comm
         self.world, self.rank = comm.world, comm.rank
-        if name is None:
-            name = f"minips_clock_{uuid.uuid4().hex}" if comm.rank == 0 else None
-            if comm.world > 1:
-                box = [name]
-                dist.broadcast_object_list(box, src=0, group=comm.group)
-                name = box[0]
-        self.path = os.path.join("/dev/shm", name)
-        self.owner = comm.rank == 0
-        self._b = runtime().ClockBoard(name, max(1, self.world), self.rank, self.owner)
-
-    def publish(self, clock: int):
-        self._b.publish(int(clock))
-
-    def get(self, rank: int) -> int:
-        return self._b.get(rank)
-
-    def min_clock(self) -> int:
-        return self._b.min_clock()
-
-    def wait_min(self, target: int, timeout_s: float = 0.0) -> float:
-        """Block (GIL released, futex sleep) until min clock >= target; returns seconds waited."""
-        return self._b.wait_min_at_least(int(target), float(timeout_s))
-
-    def snapshot(self) -> list:
-        return list(self._b.snapshot())
-
-    def close(self):
-        if self.owner:
-            self._b.unlink()
-
-
-@dataclass
-class OneSidedPlan:
-    """Routing of one batch: the unique keys (no per-owner grouping needed: the kernels find
-    each key's owner)."""
-    keys_n: int
-    inv: torch.Tensor        # [n] position of each requested key in the unique order
-    uniq: torch.Tensor       # [n] unique keys (first U valid)
-    cap: int
-    U_dev: torch.Tensor | None = None
-    csr: tuple | None = None
-    extra: dict = field(default_factory=dict)
-    _U: int | None = None
-
-    @property
-    def U(self) -> int:
-        if self._U is None:
-            self._U = self.cap if self.U_dev is None else int(self.U_dev.item())
-        return self._U
-
-
-class OneSidedSparseTable:
-    def __init__(self, comm: Comm, num_rows: int, width: int, optimizer: str = "sgd", lr: float = 0.01,
-                 consistency: str = "asp", staleness: int = 0, pull_dtype=torch.float32, init_std: float = 0.0,
-                 seed: int = 1234, table_id: int = 0):
-        if optimizer not in ("add", "sgd"):
-            raise ValueError("one-sided tables apply by atomic adds: optimizer 'add' or 'sgd'")
-        if consistency not in ("ssp", "asp"):
-            raise ValueError("one-sided tables serve SSP / ASP (BSP uses the collective SparseTable)")
-        self.comm, self.table_id = comm, table_id
-        self.num_rows, self.width = num_rows, width
-        self.optimizer, self.lr = optimizer, lr
-        self.consistency = consistency
-        self.staleness = staleness if consistency == "ssp" else 0
-        self.pull_dtype = pull_dtype
-        dev = comm.device
-        self.cuda = dev.type == "cuda"
-        b = even_bounds(num_rows, comm.world)
-        self.bounds_list = b
-        self.bounds = torch.tensor(b, dtype=torch.int64, device=dev)
-        self.base = b[comm.rank]
-        self.rows_local = b[comm.rank + 1] - b[comm.rank]
-        self._own_bounds = torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=dev)
-        rows_of = [b[r + 1] - b[r] for r in range(comm.world)]
-        nbytes = [max(4 * width * n, 256) for n in rows_of]
+        self.cuda = comm.device.type == "cuda"
+        name = f"minips_ps_{uuid.uuid4().hex[:16]}" if comm.rank == 0 else None
+        if comm.world > 1:
+            box = [name]
+            dist.broadcast_object_list(box, src=0, group=comm.group)
+            name = box[0]
+        self.name = name
+        self.board = runtime().PSBoard(name, self.world, self.rank, _MAX_TABLES)
         if self.cuda:
             from .._native import kernels
 
-            buf, handle = kernels().ipc_alloc(nbytes[comm.rank], dev.index)
+            self.server = kernels().AsyncServer(name, self.world, self.rank, _MAX_TABLES, comm.device.index or 0)
+            self._anchor = torch.zeros(1, device=comm.device)
+        else:
+            self.server = runtime().AsyncServer(name, self.world, self.rank, _MAX_TABLES, self._apply_cpu)
+        if os.environ.get("MINIPS_PS_APPLY_LOG") == "1":
+            self.server.set_log(True)
+        self.server.start()
+        self.tables: dict[int, object] = {}
+        # a straggler that never publishes again is a failure (the supervisor restarts the set),
+        # not an infinite hang of every other rank
+        self.timeout = float(os.environ.get("MINIPS_SSP_GATE_TIMEOUT", "600"))
+        self.closed = False
+        self._paused = 0
+        if comm.world > 1:
+            comm.barrier()  # every rank attached the board
+        if comm.rank == 0:
+            self.board.unlink()  # mapped everywhere: the name is no longer needed (no /dev/shm leak)
+
+    def register(self, table) -> int:
+        t = len(self.tables)
+        if t >= _MAX_TABLES:
+            raise RuntimeError(f"at most {_MAX_TABLES} asynchronous tables per rank")
+        self.tables[t] = table
+        return t
+
+    def _apply_cpu(self, t: int, r: int, c: int):
+        self.tables[t]._apply_slot_cpu(r, c)
+
+    def check(self):
+        err = self.server.error()
+        if err:
+            raise RuntimeError(f"async PS server of rank {self.rank}: {err}")
+        if self.cuda:
+            perr = self.server.publish_error()
+            if perr:
+                raise RuntimeError(f"async PS clock publisher of rank {self.rank}: {perr}")
+
+    def wait(self, fn, *args, what: str = "") -> float:
+        """Run a board wait in slices, surfacing a server error instead of waiting it out."""
+        t0 = time.perf_counter()
+        while True:
+            w = fn(*args, 0.25)
+            if w >= 0:
+                return time.perf_counter() - t0
+            self.check()
+            if 0 < self.timeout < time.perf_counter() - t0:
+                raise TimeoutError(f"async PS: {what} still waiting after {self.timeout:.0f} s (board "
+                                   f"sent {[self.board.snapshot_sent(t) for t in self.tables]})")
+
+    def publish(self, t: int, clock: int):
+        """sent[t] = clock once the work issued so far (this clock's pushes) has completed."""
+        if self.cuda:
+            self.server.publish_after(t, clock, self._anchor)
+        else:
+            self.board.publish_sent(t, clock)
+
+    def pause(self):
+        """Stop applying (checkpoint snapshot / restore); nested with resume()."""
+        if self._paused == 0:
+            self.server.pause()
+            self.check()
+        self._paused += 1
+
+    def resume(self):
+        self._paused = max(0, self._paused - 1)
+        if self._paused == 0:
+            self.server.resume()
+
+    def apply_log(self) -> list:
+        """(table, requester, clock) triples in this owner's apply order (MINIPS_PS_APPLY_LOG=1 or
+        set_log(True) before the applies)."""
+        flat = self.server.take_log()
+        return [tuple(flat[i: i + 3]) for i in range(0, len(flat), 3)]
+
+    def close(self):
+        if not self.closed:
+            self.server.stop()
+            self.closed = True
+
+
+class _AsyncTable:
+    """Shared parts of the asynchronous tables: shared buffers, clocks, gate, flow control."""
+
+    def _init_async(self, comm: Comm, consistency: str, staleness: int, depth, asp_bound):
+        if consistency not in ("ssp", "asp"):
+            raise ValueError("asynchronous tables serve SSP / ASP (BSP uses the collective tables)")
+        self.comm = comm
+        self.consistency = consistency
+        self.staleness = int(staleness) if consistency == "ssp" else 0
+        # ASP is unbounded (asp_model.cpp:23-26) unless asp_bound (or MINIPS_ASP_BOUND, the
+        # training driver's --asp_bound) sets the same gate as SSP
+        if asp_bound is None and os.environ.get("MINIPS_ASP_BOUND", "") not in ("", "none"):
+            asp_bound = int(os.environ["MINIPS_ASP_BOUND"])
+        self.asp_bound = None if asp_bound is None or consistency != "asp" else int(asp_bound)
+        self.cuda = comm.device.type == "cuda"
+        self.ps = AsyncPS.of(comm)
+        self.t = self.ps.register(self)
+        bound = self.staleness if consistency == "ssp" else (self.asp_bound or 0)
+        self.depth = int(depth) if depth else max(4, bound + 3)
+        self.clock_n = 0
+        self.waited_s = 0.0
+        self.gate_waits = 0
+        self.staleness_hist: collections.Counter = collections.Counter()
+        self._cpu_files: list = []
+
+    # -- shared buffers ---------------------------------------------------------------------
+    def _share(self, nbytes: list, tag: str) -> list:
+        """One buffer per rank (rank r's of nbytes[r] bytes, zero-filled), every one mapped here:
+        uint8 tensors [P]. GPU: hipMalloc + IPC handles; CPU: /dev/shm files."""
+        comm, me = self.comm, self.comm.rank
+        if self.cuda:
+            from .._native import kernels
+
+            buf, handle = kernels().ipc_alloc(max(256, int(nbytes[me])), comm.device.index or 0)
             handles = [None] * comm.world
             if comm.world > 1:
                 dist.all_gather_object(handles, handle, group=comm.group)
-            else:
-                handles = [handle]
-            self._mapped = [buf if r == comm.rank else kernels().ipc_open(handles[r], nbytes[r], dev.index)
-                            for r in range(comm.world)]
-            self.bases = torch.tensor([m.data_ptr() for m in self._mapped], dtype=torch.int64, device=dev)
-            self.shard = buf[: 4 * width * self.rows_local].view(torch.float32).view(self.rows_local, width)
-            self._locks = None
-        else:
-            name = f"minips_tab_{uuid.uuid4().hex}" if comm.rank == 0 else None
-            if comm.world > 1:
-                box = [name]
-                dist.broadcast_object_list(box, src=0, group=comm.group)
-                name = box[0]
-            self._paths = [os.path.join("/dev/shm", f"{name}_{r}") for r in range(comm.world)]
-            mine = np.memmap(self._paths[comm.rank], dtype=np.float32, mode="w+", shape=(max(1,
-                                                                                             self.rows_local), width))
-            mine[:] = 0
-            mine.flush()
-            if comm.world > 1:
-                dist.barrier(group=comm.group)  # every shard file exists
-            self._views = [torch.from_numpy(np.memmap(p, dtype=np.float32, mode="r+",
-                                                      shape=(max(1, rows_of[r]), width)))
-                           for r, p in enumerate(self._paths)]
-            self.shard = self._views[comm.rank][: self.rows_local]
-            self._locks = [open(p, "rb") for p in self._paths]
+            return [buf if r == me else kernels().ipc_open(handles[r], max(256, int(nbytes[r])), comm.device.index or 0)
+                    for r in range(comm.world)]
+        paths = [f"/dev/shm/{self.ps.name}_t{self.t}_{tag}_{r}" for r in range(comm.world)]
+        mine = np.memmap(paths[me], dtype=np.uint8, mode="w+", shape=(max(256, int(nbytes[me])),))
+        mine.flush()
+        self._cpu_files.append(paths[me])
+        if comm.world > 1:
+            dist.barrier(group=comm.group)  # every rank's file exists
+        return [torch.from_numpy(np.memmap(p, dtype=np.uint8, mode="r+", shape=(max(256, int(nbytes[r])),)))
+                for r, p in enumerate(paths)]
+
+    def _finish_init(self):
+        if self.comm.world > 1:
+            self.comm.barrier()  # every rank mapped every buffer and registered the table
+        for p in self._cpu_files:  # mapped everywhere: unlink now (nothing left behind in /dev/shm)
+            try:
+                os.unlink(p)
+            except FileNotFoundError:
+                pass
+        self._cpu_files = []
+
+    # -- clocks -----------------------------------------------------------------------------
+    def _gate(self):
+        """SSP: a Get at own clock c waits until every owner applied every worker's clocks
+        < c - s (ssp_model.cpp:58-85); ASP: no wait unless asp_bound is set."""
+        c = self.clock_n
+        bound = self.staleness if self.consistency == "ssp" else self.asp_bound
+        board, t = self.ps.board, self.t
+        if bound is not None and c - bound > 0 and board.min_applied(t) < c - bound:
+            self.waited_s += self.ps.wait(board.wait_min_applied, t, c - bound, what=f"SSP gate of table {t}")
+            self.gate_waits += 1
+        # observed staleness of this read: own clocks not yet in every shard
+        self.staleness_hist[c - min(c, board.min_applied(t))] += 1
+
+    def _reserve_slot(self) -> int:
+        """Inbox slot of the current clock, free once every owner applied clock c - depth."""
+        c = self.clock_n
+        need = c - self.depth + 1
+        board, t, me = self.ps.board, self.t, self.comm.rank
+        if need > 0 and board.min_applied_from(t, me) < need:
+            self.ps.wait(board.wait_applied_from, t, me, need, what=f"inbox slot of table {t}")
+        return c % self.depth
+
+    def _advance(self):
+        self.clock_n += 1
+        self.ps.publish(self.t, self.clock_n)
+
+    def drain(self):
+        """Until every owner applied this rank's clocks so far."""
+        if hasattr(self, "_check_keys"):
+            self._check_keys()
+        board, t, me = self.ps.board, self.t, self.comm.rank
+        if self.clock_n == 0:
+            return
+        self.ps.wait(board.wait_sent_at_least, t, me, self.clock_n, what="clock publisher")
+        self.ps.wait(board.wait_applied_from, t, me, self.clock_n, what=f"drain of table {self.t}")
+
+    def quiesce_owner(self):
+        """Until this rank's server applied everything sent to it so far (tests, snapshots)."""
+        board, t, me = self.ps.board, self.t, self.comm.rank
+        sent = board.snapshot_sent(t)
+        t0 = time.perf_counter()
+        while any(board.applied(t, me, r) < sent[r] for r in range(self.comm.world)):
+            self.ps.check()
+            if 0 < self.ps.timeout < time.perf_counter() - t0:
+                raise TimeoutError("async PS: owner quiesce timed out")
+            time.sleep(0.0005)
+
+    def staleness_stats(self) -> dict:
+        h = dict(sorted(self.staleness_hist.items()))
+        return dict(hist=h, max=max(h) if h else 0, gate_waits=self.gate_waits, waited_s=round(self.waited_s, 6))
+
+    # -- checkpoint / restore ---------------------------------------------------------------
+    def snapshot_begin(self):
+        """Checkpointer.save, after every rank drained: no apply runs until snapshot_end()."""
+        self.ps.pause()
+
+    def snapshot_end(self):
+        self.ps.resume()
+
+    def _restore_clock(self, clock: int):
+        """After the rows landed (server paused since restore_dst): every rank restarts at
+        ``clock`` -- its sent counter and its owner row of the board -- then all resume."""
+        board, t = self.ps.board, self.t
+        self.clock_n = int(clock)
+        board.publish_sent(t, self.clock_n)
+        board.publish_applied_row(t, self.clock_n)
+        self.staleness_hist.clear()
+        # nobody pushes before every rank reset its counters and rows (a host barrier with the long
+        # timeout: restore times differ by rank)
+        self.comm.store_barrier(f"async_restore_t{t}")
+        self.ps.resume()
+
+    def reset_after_rollback(self):
+        raise RuntimeError("asynchronous tables restart the whole rank set (no in-place rollback)")
+
+    def close(self):
+        self.drain()
+
+
+class AsyncSparseTable(_AsyncTable, SparseTable):
+    """Row table (equal key ranges, optional routing) with SSP / ASP over the one-sided path.
+    Same planning API as SparseTable (plan / plan_async / advance_plan / get / add /
+    add_lookup_grads / add_keys / clock), so the models switch transports by construction.
+
+    ``max_keys``: keys per clock a rank may push (an inbox slot holds that many rows; the models
+    pass B * F)."""
+
+    _exact_counts = False
+
+    def __init__(self, comm: Comm, num_rows: int, width: int, optimizer: str = "rowwise_adagrad", lr: float = 0.01,
+                 eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "ssp", staleness: int = 0,
+                 split: int | None = None, table_id: int = 0, init_std: float = 0.01, seed: int = 1234,
+                 route: str = "mix", columns=None, max_keys: int = 1 << 16, depth: int | None = None,
+                 asp_bound: int | None = None):
+        if optimizer not in ("add", "sgd", "rowwise_adagrad"):
+            raise ValueError(f"sparse optimizer {optimizer!r}: add | sgd | rowwise_adagrad")
+        self._init_async(comm, consistency, staleness, depth, asp_bound)
+        self.value_dtype = self.push_dtype = torch.float32
+        self.columns = column_spec(columns, comm.device)
+        self.route_mult = _route_multiplier(num_rows) if route == "mix" else 0
+        self.table_id = table_id
+        self.num_rows, self.width = num_rows, width
+        self.optimizer, self.lr, self.eps = optimizer, lr, eps
+        self.pull_dtype = pull_dtype
+        self.split = split
+        self.p2p = False
+        self._pending: list = []
+        self._own_bounds = torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=comm.device)
+        P, me, dev = comm.world, comm.rank, comm.device
+        b = even_bounds(num_rows, P)
+        self.bounds_list = b
+        self.bounds = torch.tensor(b, dtype=torch.int64, device=dev)
+        self.base = b[me]
+        self.rows_local = b[me + 1] - b[me]
+        rows_of = [b[r + 1] - b[r] for r in range(P)]
+        self.cap = _align(max(2, int(max_keys)), 2)
+        self.slot_bytes = _align(_SLOT_HEADER + self.cap * (8 + 4 * width), 256)
+        shards = self._share([4 * width * n for n in rows_of], "shard")
+        self._shards = shards
+        self._views = [s[: 4 * width * n].view(torch.float32).view(n, width) for s, n in zip(shards, rows_of)]
+        self.shard = self._views[me]
         if init_std > 0:
             g = torch.Generator(device=dev)
-            g.manual_seed(seed + 7919 * comm.rank)
+            g.manual_seed(seed + 7919 * me)
             self.shard.normal_(0.0, init_std, generator=g)
-        self.board = ClockBoard(comm)
-        # a straggler that never publishes again is a failure (the supervisor restarts the set),
-        # not an infinite hang of every other rank
-        self.gate_timeout_s = float(os.environ.get("MINIPS_SSP_GATE_TIMEOUT", "600"))
-        self.clock_n = 0
-        self._pending: list = []
-        self.waited_s = 0.0
-        self.staleness_seen: list = []
+        self.state = torch.zeros(self.rows_local, dtype=torch.float32, device=dev) \
+            if optimizer == "rowwise_adagrad" else None
+        self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
+        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox")
         if self.cuda:
-            self._pub_q: queue.Queue = queue.Queue()
-            self._pub = threading.Thread(target=self._publisher, name="minips-clock-pub", daemon=True)
-            self._pub.start()
-        if comm.world > 1:
-            comm.barrier()  # every rank mapped every shard and initialised its own rows
+            self.bases = torch.tensor([s.data_ptr() for s in shards], dtype=torch.int64, device=dev)
+            self.inbox_ptrs = torch.tensor([s.data_ptr() for s in self._inbox], dtype=torch.int64, device=dev)
+            D1 = split if split is not None else width
+            self.ps.server.add_sparse(self.t, _OPT_CODES[optimizer], self.shard.data_ptr(), width, width,
+                                      self.state.data_ptr() if self.state is not None else 0,
+                                      self.state2.data_ptr() if self.state2 is not None else 0, D1, self.base,
+                                      float(lr), float(eps), self.cap, self._inbox[me].data_ptr(), self.slot_bytes,
+                                      self.depth)
+            torch.cuda.synchronize(dev)  # shard init + state zeroing done before any peer reads
+        else:
+            self.ps.server.enable(self.t)
+        self._finish_init()
 
-    # ------------------------------------------------------------------------------ progress
-    def _publisher(self):
-        while True:
-            item = self._pub_q.get()
-            if item is None:
-                return
-            ev, c = item
-            ev.synchronize()  # this clock's atomic adds have completed in the owners' HBM
-            self.board.publish(c)
+    # -- planning: SparseTable's dedupe + owner grouping, no count exchange ----------------------
+    def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
+        if pp.event is not None:
+            torch.cuda.current_stream(self.comm.device).wait_event(pp.event)
+        n = pp.flat.numel()
+        if n > self.cap:
+            raise ValueError(f"a batch of {n} keys exceeds the inbox slot ({self.cap} rows): raise max_keys")
+        counts = pp.counts[: self.comm.world]
+        if not self.cuda:
+            U = int(pp.U_dev.reshape(-1)[0])
+            p = SparsePlan(n, pp.inv, pp.uniq, U, None, None, pp.uniq[:U], csr=pp.csr, _U=U)
+        else:
+            p = SparsePlan(n, pp.inv, pp.uniq, n, None, None, pp.uniq, U_dev=pp.U_dev, csr=pp.csr)
+        p.extra["counts"] = counts
+        return p
 
-    def _gate(self):
-        """SSP: a Get at own clock c waits while c > min_clock + staleness (ssp_model.cpp:58-85)."""
-        c = self.clock_n
-        if self.consistency == "ssp":
-            self.waited_s += self.board.wait_min(c - self.staleness, self.gate_timeout_s)
-        self.staleness_seen.append(c - self.board.min_clock())
+    def plan(self, keys: torch.Tensor, csr: bool = False) -> SparsePlan:
+        return self._finish_plan(self._start_plan(keys, csr, exchange=False))
 
-    # ------------------------------------------------------------------------------ KV API
-    def _plan(self, keys: torch.Tensor) -> OneSidedPlan:
-        flat = keys.reshape(-1).to(torch.int64)
-        uniq, inv, _, U_dev = ops.unique_bucketize_n(flat, self._own_bounds)
-        if self.cuda:
-            return OneSidedPlan(flat.numel(), inv, uniq, flat.numel(), U_dev=U_dev)
-        U = int(U_dev.reshape(-1)[0])
-        return OneSidedPlan(flat.numel(), inv, uniq, U, _U=U)
+    def plan_async(self, keys: torch.Tensor, csr: bool = False, keys_on_plan_stream: bool = False,
+                   fenced: bool = False):
+        if not self.cuda:
+            return self._start_plan(keys, csr, exchange=False)
+        ps = self.comm.plan_stream()
+        cur = torch.cuda.current_stream(self.comm.device)
+        if not keys_on_plan_stream:
+            ps.wait_stream(cur)
+        with torch.cuda.stream(ps):
+            pp = self._start_plan(keys, csr, exchange=False)
+            pp.event = torch.cuda.Event()
+            pp.event.record(ps)
+        if not fenced:
+            keys.record_stream(ps)
+            for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev, *(pp.csr or ())):
+                t.record_stream(cur)
+        return pp
 
+    def advance_plan(self, pending, finish: bool = True):
+        return pending  # nothing to exchange
+
+    def _fused_lookup_ok(self, *a) -> bool:
+        return False
+
+    # -- KV API -----------------------------------------------------------------------------
     def get(self, keys: torch.Tensor, plan=None):
-        """Rows of the unique keys ([cap, width], unique order) and the plan (rows[plan.inv[i]]
-        is the row of keys[i]). No collective: rows come straight from the owners' HBM."""
-        plan = plan or self._plan(keys)
+        """Rows of the unique keys ([cap, width], unique order) and the plan; rows[plan.inv[i]]
+        is the row of keys[i]. No collective: rows come straight from the owners' HBM."""
+        if plan is None:
+            plan = self.plan(keys)
+        elif isinstance(plan, _PendingPlan):
+            plan = self._finish_plan(plan)
         self._gate()
         out = torch.empty(max(plan.cap, 1), self.width, dtype=self.pull_dtype, device=self.comm.device)
         if self.cuda:
             from .._native import kernels
 
-            kernels().remote_gather(self.bases, self.bounds, plan.uniq, plan.U_dev, self.width, out)
+            kernels().ps_gather_rows(self.bases, self.bounds, plan.uniq, plan.U_dev, self.width, out)
         else:
             u = plan.uniq[: plan.U]
-            for r in range(self.comm.world):
-                lo, hi = self.bounds_list[r], self.bounds_list[r + 1]
+            for o in range(self.comm.world):
+                lo, hi = self.bounds_list[o], self.bounds_list[o + 1]
                 m = (u >= lo) & (u < hi)
                 if bool(m.any()):
-                    out[: plan.U][m] = self._views[r][u[m] - lo].to(out.dtype)
+                    out[: plan.U][m] = self._views[o][u[m] - lo].to(out.dtype)
         return out, plan
 
-    def get_rows(self, keys: torch.Tensor) -> torch.Tensor:
-        rows, plan = self.get(keys)
-        return rows[plan.inv]
-
-    # SparseTable-compatible planning API (models call plan / plan_async / advance_plan): a plan
-    # is a local dedupe only, there is no count exchange to overlap
-    def plan(self, keys: torch.Tensor, csr: bool = False) -> OneSidedPlan:
-        return self._plan(keys)
-
-    def plan_async(self, keys: torch.Tensor, csr: bool = False, keys_on_plan_stream: bool = False):
-        return self._plan(keys)
-
-    def advance_plan(self, pending, finish: bool = True):
-        return pending
-
-    def add(self, plan: OneSidedPlan, grad_rows: torch.Tensor):
-        assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == torch.float32
-        self._pending.append((plan, grad_rows))
-
-    def add_lookup_grads(self, plan: OneSidedPlan, dX: torch.Tensor, dwide, F: int, D: int, x_off: int = 0):
-        """Per-lookup gradients (SparseTable.add_lookup_grads): segment-summed per unique row here,
-        then atomically added into the owners' rows at the clock."""
-        dev = self.comm.device
-        g = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width, dtype=torch.float32,
-                                                                 device=dev)
-        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, g, x_off=x_off, U_dev=getattr(plan, "U_dev", None),
-                            csr=getattr(plan, "csr", None))
-        self.add(plan, g)
-
-    def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
-        plan = self._plan(keys)
-        g = torch.zeros(max(plan.cap, 1), self.width, dtype=torch.float32, device=self.comm.device)
-        ops.scatter_add_rows(vals.reshape(keys.numel(), self.width).to(torch.float32).contiguous(), plan.inv, g)
-        self.add(plan, g)
-
     def clock(self):
-        """Apply the buffered adds into the owners' rows (atomics), then publish clock+1."""
-        scale = 1.0 if self.optimizer == "add" else -self.lr
+        """Push this clock's gradient rows into the owners' inboxes, then publish the clock."""
         pending, self._pending = self._pending, []
-        for plan, g in pending:
-            if self.cuda:
-                from .._native import kernels
+        if len(pending) > 1:
+            pending = [self._merge(pending)]
+        slot = self._reserve_slot()
+        off = (self.comm.rank * self.depth + slot) * self.slot_bytes
+        if self.cuda:
+            from .._native import kernels
 
-                kernels().remote_scatter_add(self.bases, self.bounds, plan.uniq, g.contiguous(), scale, plan.U_dev)
+            if pending:
+                plan, g = pending[0]
+                kernels().ps_push_rows(plan.uniq, plan.extra["counts"], plan.U_dev, plan.cap, g.contiguous(),
+                                       self.inbox_ptrs, off, self.cap)
             else:
-                u = plan.uniq[: plan.U]
-                for r in range(self.comm.world):
-                    lo, hi = self.bounds_list[r], self.bounds_list[r + 1]
-                    m = (u >= lo) & (u < hi)
-                    if bool(m.any()):
-                        fcntl.flock(self._locks[r], fcntl.LOCK_EX)
-                        try:
-                            self._views[r].index_add_(0, u[m] - lo, scale * g[: plan.U][m])
-                        finally:
-                            fcntl.flock(self._locks[r], fcntl.LOCK_UN)
-        self.clock_n += 1
-        if self.cuda:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.comm.device))
-            self._pub_q.put((ev, self.clock_n))
+                kernels().ps_set_headers(self.inbox_ptrs, off, 0)
         else:
-            self.board.publish(self.clock_n)
+            self._push_cpu(pending[0] if pending else None, off)
+        self._advance()
 
-    def drain(self):
-        """Wait until this rank's clocks are applied and published."""
-        if self.cuda:
-            torch.cuda.current_stream(self.comm.device).synchronize()
-            while not self._pub_q.empty() or self.board.get(self.comm.rank) < self.clock_n:
-                time.sleep(0.0005)
+    def _merge(self, pending):
+        """Several Adds in one clock: one deduplicated batch (duplicates summed)."""
+        keys, rows = [], []
+        for plan, g in pending:
+            U = plan.U
+            keys.append(plan.uniq[:U])
+            rows.append(g[:U])
+        allk, allg = torch.cat(keys), torch.cat(rows)
+        uniq, inv, counts, U_dev = ops.unique_bucketize_n(allk, self.bounds)
+        g = torch.zeros(max(allk.numel(), 1), self.width, dtype=torch.float32, device=self.comm.device)
+        ops.scatter_add_rows(allg.contiguous(), inv, g)
+        U = int(U_dev.reshape(-1)[0])
+        p = SparsePlan(allk.numel(), inv, uniq, allk.numel() if self.cuda else U, None, None, uniq,
+                       U_dev=U_dev if self.cuda else None, _U=U)
+        p.extra["counts"] = counts[: self.comm.world]
+        return p, g
 
-    def close(self):
-        self.drain()
-        if self.cuda:
-            self._pub_q.put(None)
-            self._pub.join(timeout=5)
-        self.board.close()
-        if not self.cuda:
-            for f in self._locks:
-                f.close()
-            if self.comm.rank == 0:
-                for p in self._paths:
-                    try:
-                        os.unlink(p)
-                    except FileNotFoundError:
-                        pass
+    # -- CPU data path (gloo tests) ----------------------------------------------------------
+    def _push_cpu(self, item, off: int):
+        W, cap = self.width, self.cap
+        if item is None:
+            for o in range(self.comm.world):
+                self._inbox[o][off: off + 8].view(torch.int64)[0] = 0
+            return
+        plan, g = item
+        counts = [int(c) for c in plan.extra["counts"].tolist()]
+        s = 0
+        for o, n in enumerate(counts):
+            buf = self._inbox[o]
+            keys = buf[off + _SLOT_HEADER: off + _SLOT_HEADER + 8 * cap].view(torch.int64)
+            rows = buf[off + _SLOT_HEADER + 8 * cap: off + _SLOT_HEADER + 8 * cap + 4 * W * cap].view(torch.float32)
+            keys[:n] = plan.uniq[s: s + n]
+            rows.view(cap, W)[:n] = g[s: s + n].to(torch.float32)
+            buf[off: off + 8].view(torch.int64)[0] = n  # the header last (the board publish orders it)
+            s += n
+
+    def _apply_slot_cpu(self, r: int, c: int):
+        W, cap = self.width, self.cap
+        off = (r * self.depth + c % self.depth) * self.slot_bytes
+        buf = self._inbox[self.comm.rank]
+        n = int(buf[off: off + 8].view(torch.int64)[0])
+        if n == 0:
+            return
+        keys = buf[off + _SLOT_HEADER: off + _SLOT_HEADER + 8 * n].view(torch.int64).clone()
+        g = buf[off + _SLOT_HEADER + 8 * cap: off + _SLOT_HEADER + 8 * cap + 4 * W * n].view(torch.float32)
+        g = g.view(n, W).clone()
+        if self.optimizer == "rowwise_adagrad":
+            ops.sparse_rowwise_adagrad(self.shard, self.state, keys, self.base, g, self.lr, self.eps,
+                                       state2=self.state2, split=self.split)
+        else:
+            ops.sparse_sgd(self.shard, keys, self.base, g, 1.0 if self.optimizer == "add" else -self.lr)
 
     # -- checkpoint hooks (minips_amd.ps.checkpoint) -------------------------------------------
     def shard_state(self):
         self.drain()
+        arrays = {"params": self.shard}
+        if self.state is not None:
+            arrays["state"] = self.state
+        if self.state2 is not None:
+            arrays["state2"] = self.state2
         meta = dict(global_rows=self.num_rows, base=self.base, rows=self.rows_local, cols=self.width,
                     clock=self.clock_n, table_id=self.table_id, rank=self.comm.rank, world=self.comm.world,
                     kind="sparse")
-        return meta, {"params": self.shard}
+        return meta, arrays
 
     def restore_range(self):
         return self.base, self.base + self.rows_local
 
     def restore_dst(self):
-        return {"params": self.shard}
+        self.ps.pause()  # the rows land with no apply running (resumed in finish_restore)
+        out = {"params": self.shard}
+        if self.state is not None:
+            out["state"] = self.state.view(-1, 1)
+        if self.state2 is not None:
+            out["state2"] = self.state2.view(-1, 1)
+        return out
 
     def finish_restore(self, clock: int):
-        self.clock_n = int(clock)
-        self.board.publish(self.clock_n)
-
-    def reset_after_rollback(self):
-        self._pending = []
+        if self.cuda:
+            torch.cuda.synchronize(self.comm.device)
+        self._restore_clock(clock)
 
 
-class OneSidedDenseTable:
-    """A flat dense parameter vector on the one-sided path (ASP / SSP async SGD): the vector is
-    cut into rows of ``row`` values, row-partitioned over the ranks like a sparse table; Get
-    gathers every row from its owner's HBM (the pull), Add + Clock atomically adds -lr * grad
-    into the owners' rows. Same API as ps.tables.DenseTable (grad buffer written in place by
-    the models, get / add / clock / load_full / full_master)."""
+class AsyncDenseTable(_AsyncTable):
+    """A flat dense parameter vector (equal shards, like ps.tables.DenseTable) on the one-sided
+    path: Get pulls every owner's shard whose version changed since the last pull (bf16 copies
+    the owner's apply writes), Add + Clock pushes each owner's slice of the gradient into its
+    inbox, and the owner applies Adam / Adagrad / SGD / add with its own m / v state -- one
+    optimizer step per push, as an asynchronous PS server does (each Add is applied on arrival).
+    Same API as DenseTable (grad written in place by the models, get / add / clock / load_full /
+    full_master)."""
 
-    def __init__(self, comm: Comm, n_params: int, lr: float = 1e-3, consistency: str = "asp", staleness: int = 0,
-                 pull_dtype=torch.bfloat16, table_id: int = 0, row: int = 64, optimizer: str = "sgd"):
-        self.comm, self.n_params, self.table_id = comm, n_params, table_id
-        self.row = row
-        self.rows = -(-n_params // row)
-        self.n_pad = self.rows * row
-        self.lr = lr
+    buckets = None
+
+    def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
+                 consistency: str = "ssp", staleness: int = 0, pull_dtype=torch.bfloat16, table_id: int = 0,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, depth: int | None = None,
+                 asp_bound: int | None = None):
+        if optimizer not in ("add", "sgd", "adagrad", "adam"):
+            raise ValueError(f"dense optimizer {optimizer!r}: add | sgd | adagrad | adam")
+        self._init_async(comm, consistency, staleness, depth, asp_bound)
+        P, me, dev = comm.world, comm.rank, comm.device
+        self.table_id, self.n_params = table_id, n_params
+        self.optimizer, self.lr = optimizer, lr
+        self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
         self.pull_dtype = pull_dtype
-        self.optimizer = optimizer
-        self.t = OneSidedSparseTable(comm, self.rows, row, optimizer=optimizer, lr=lr, consistency=consistency,
-                                     staleness=staleness, pull_dtype=torch.float32, table_id=table_id)
-        dev = comm.device
-        self._keys = torch.arange(self.rows, dtype=torch.int64, device=dev)
-        self._plan = OneSidedPlan(self.rows, self._keys, self._keys, self.rows, _U=self.rows)
+        self.value_dtype = torch.float32
+        self.n_pad = _align(n_params, 64 * P)
+        self.shard = self.n_pad // P
+        self.base = me * self.shard
+        self.slot_bytes = _align(_SLOT_HEADER + 4 * self.shard, 256)
+        masters = self._share([4 * self.shard] * P, "master")
+        self._masters = [m[: 4 * self.shard].view(torch.float32) for m in masters]
+        self.master = self._masters[me]
+        # what peers pull: the bf16 copy the apply writes (half the xGMI bytes), or the fp32 master
+        self._pull_bf16 = self.cuda and pull_dtype == torch.bfloat16
+        if self._pull_bf16:
+            pulls = self._share([2 * self.shard] * P, "pull")
+            self._pulls = [p[: 2 * self.shard].view(torch.bfloat16) for p in pulls]
+        else:
+            self._pulls = self._masters
+        self.m = torch.zeros(self.shard, dtype=torch.float32, device=dev) if optimizer in ("adam", "adagrad") \
+            else None
+        self.v = torch.zeros_like(self.m) if optimizer == "adam" else None
+        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox")
         self.params = torch.zeros(self.n_pad, dtype=pull_dtype, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
-        self._full = torch.empty(self.rows, row, dtype=torch.float32, device=dev)
+        self._seen = [-1] * P
         self._pending = False
         self.step = 0
+        self.cpu_step = 0
+        if self.cuda:
+            self._inbox_ptrs = torch.tensor([b.data_ptr() for b in self._inbox], dtype=torch.int64, device=dev)
+            self._slot_views = [b for b in self._inbox]
+            self.ps.server.add_dense(self.t, _OPT_CODES[optimizer], self.master.data_ptr(),
+                                     self.m.data_ptr() if self.m is not None else 0,
+                                     self.v.data_ptr() if self.v is not None else 0,
+                                     self._pulls[me].data_ptr() if self._pull_bf16 else 0, self.shard, float(lr),
+                                     float(betas[0]), float(betas[1]), float(eps), float(weight_decay), 0,
+                                     self._inbox[me].data_ptr(), self.slot_bytes, self.depth)
+        else:
+            self.ps.server.enable(self.t)
+        self._finish_init()
 
     @property
-    def clock_n(self):
-        return self.t.clock_n
+    def clock_count(self):
+        return self.clock_n
 
     def load_full(self, full: torch.Tensor):
+        """Initialise from the full vector (identical on every rank)."""
         flat = torch.zeros(self.n_pad, dtype=torch.float32, device=self.comm.device)
         flat[: self.n_params] = full.to(self.comm.device, torch.float32)
-        lo, hi = self.t.base, self.t.base + self.t.rows_local
-        self.t.shard.copy_(flat.view(self.rows, self.row)[lo:hi])
+        self.master.copy_(flat[self.base: self.base + self.shard])
+        if self._pull_bf16:
+            self._pulls[self.comm.rank].copy_(self.master.to(torch.bfloat16))
         self.params.copy_(flat.to(self.pull_dtype))
+        self._seen = [self.ps.board.owner_version(self.t, o) for o in range(self.comm.world)]
+        if self.cuda:
+            torch.cuda.synchronize(self.comm.device)
         if self.comm.world > 1:
             self.comm.barrier()
 
     def full_master(self) -> torch.Tensor:
         self.drain()
-        rows, _ = self.t.get(self._keys, plan=self._plan)
-        return rows.reshape(-1)[: self.n_params]
+        return torch.cat([m.to(self.comm.device) for m in self._masters])[: self.n_params].clone()
 
     def get(self) -> torch.Tensor:
-        rows, _ = self.t.get(self._keys, plan=self._plan)
-        self.params.copy_(rows.reshape(-1).to(self.pull_dtype))
+        """Pull the owners' shards that changed since the last pull (SSP-gated)."""
+        self._gate()
+        board = self.ps.board
+        for o in range(self.comm.world):
+            v = board.owner_version(self.t, o)
+            if v != self._seen[o]:
+                self.params[o * self.shard: (o + 1) * self.shard].copy_(self._pulls[o])
+                self._seen[o] = v
         return self.params
 
     def add(self, grad: torch.Tensor | None = None):
@@ -387,36 +633,72 @@ class OneSidedDenseTable:
         self._pending = True
 
     def clock(self):
+        slot = self._reserve_slot()
+        off = (self.comm.rank * self.depth + slot) * self.slot_bytes
+        S = self.shard
         if self._pending:
-            self.t.add(self._plan, self.grad.view(self.rows, self.row).clone())
+            for o in range(self.comm.world):
+                dst = self._inbox[o][off + _SLOT_HEADER: off + _SLOT_HEADER + 4 * S].view(torch.float32)
+                dst.copy_(self.grad[o * S: (o + 1) * S])
             self.grad.zero_()
+        if self.cuda:
+            from .._native import kernels
+
+            kernels().ps_set_headers(self._inbox_ptrs, off, 1 if self._pending else 0)
+        else:
+            for o in range(self.comm.world):
+                self._inbox[o][off: off + 8].view(torch.int64)[0] = 1 if self._pending else 0
         self._pending = False
-        self.t.clock()
         self.step += 1
+        self._advance()
 
-    def drain(self):
-        self.t.drain()
+    def _apply_slot_cpu(self, r: int, c: int):
+        off = (r * self.depth + c % self.depth) * self.slot_bytes
+        buf = self._inbox[self.comm.rank]
+        if int(buf[off: off + 8].view(torch.int64)[0]) == 0:
+            return
+        g = buf[off + _SLOT_HEADER: off + _SLOT_HEADER + 4 * self.shard].view(torch.float32).clone()
+        if self.optimizer == "adam":
+            self.cpu_step += 1
+            ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
+                           self.weight_decay, self.cpu_step, 1.0, None)
+        elif self.optimizer == "adagrad":
+            ops.adagrad_apply(self.master, self.m, g, self.lr, self.eps, 1.0, None)
+        elif self.optimizer == "sgd":
+            ops.sgd_apply(self.master, g, self.lr, 1.0, None)
+        else:
+            self.master.add_(g)
 
-    def close(self):
-        self.t.close()
-
+    # -- checkpoint hooks ------------------------------------------------------------------------
     def shard_state(self):
-        meta, arrays = self.t.shard_state()
-        meta.update(global_rows=self.rows, kind="sparse")
+        self.drain()
+        rows = max(0, min(self.shard, self.n_params - self.base))
+        arrays = {"master": self.master[:rows]}
+        if self.m is not None:
+            arrays["m"] = self.m[:rows]
+        if self.v is not None:
+            arrays["v"] = self.v[:rows]
+        meta = dict(global_rows=self.n_params, base=self.base, rows=rows, cols=1, clock=self.clock_n,
+                    table_id=self.table_id, rank=self.comm.rank, world=self.comm.world, kind="dense")
         return meta, arrays
 
     def restore_range(self):
-        return self.t.restore_range()
+        return self.base, max(self.base, min(self.base + self.shard, self.n_params))
 
     def restore_dst(self):
-        return self.t.restore_dst()
+        self.ps.pause()
+        tabs = (("master", self.master), ("m", self.m), ("v", self.v))
+        return {n: t.view(-1, 1) for n, t in tabs if t is not None}
 
     def finish_restore(self, clock: int):
-        self.t.finish_restore(clock)
+        if self._pull_bf16:
+            self._pulls[self.comm.rank].copy_(self.master.to(torch.bfloat16))
+        steps = int(clock) * self.comm.world  # one optimizer step per push of every requester
+        if self.cuda:
+            self.ps.server.set_step(self.t, steps)
+            torch.cuda.synchronize(self.comm.device)
+        self.cpu_step = steps
         self.step = int(clock)
+        self._seen = [-1] * self.comm.world  # re-pull everything
+        self._restore_clock(clock)
         self.get()
-
-    def reset_after_rollback(self):
-        self.t.reset_after_rollback()
-        self._pending = False
-        self.grad.zero_()

@@ -61,7 +61,12 @@ class _Pipeline:
     def __init__(self, comm: Comm, consistency: str, staleness: int, overlap: bool | None = None,
                  kind: str = ""):
         self.consistency = consistency
-        self.staleness = staleness if consistency == "ssp" else (0 if consistency == "bsp" else 2)
+        # ASP on the collective path is pipelining, not a staleness model: its clocks are
+        # collectives every rank joins, so the Get gate only bounds how many clocks may be in
+        # flight (MINIPS_ASP_DEPTH, default 2). The unbounded ASP of the reference
+        # (asp_model.cpp:23-26) is the one-sided transport (ps/onesided.py, asp_bound=None).
+        asp_depth = int(os.environ.get("MINIPS_ASP_DEPTH", "2"))
+        self.staleness = staleness if consistency == "ssp" else (0 if consistency == "bsp" else asp_depth)
         overlap = _overlap_default() if overlap is None else overlap
         if consistency == "bsp":
             # one rank has no communication to hide; MINIPS_OVERLAP_W1 lists the table kinds that
@@ -467,6 +472,19 @@ class DenseTable:
         self.comm.all_gather(self.params, own)
 
 
+def column_spec(columns, device):
+    """(bases, cards) of [B, F] batches with disjoint column key ranges -> the per-column sort
+    planner's (base tensor, bit widths, device bit widths), or None when a column needs > 32 bits."""
+    if columns is None:
+        return None
+    bases, cards = columns
+    bits = [max(1, (int(c) - 1).bit_length()) for c in cards]
+    if max(bits) > 32:
+        return None
+    return (torch.as_tensor(list(bases), dtype=torch.int64, device=device), bits,
+            torch.tensor(bits, dtype=torch.int32, device=device))
+
+
 _ROUTE_PRIMES = (402653189, 201326611, 100663319, 50331653, 25165843, 12582917, 6291469, 3145739, 1572869)
 
 
@@ -569,13 +587,7 @@ class SparseTable:
             pull_dtype = push_dtype = torch.float64
         self.value_dtype = value_dtype
         self.comm = comm
-        self.columns = None
-        if columns is not None:
-            bases, cards = columns
-            bits = [max(1, (int(c) - 1).bit_length()) for c in cards]
-            if max(bits) <= 32:
-                self.columns = (torch.as_tensor(list(bases), dtype=torch.int64, device=comm.device), bits,
-                                torch.tensor(bits, dtype=torch.int32, device=comm.device))
+        self.columns = column_spec(columns, comm.device)
         # Key -> row placement. "range": row = key (the reference's contiguous range partition).
         # "mix" (default): row = key * A mod num_rows, a bijection (A prime, coprime to num_rows),
         # then the same equal ranges: contiguous key blocks (a big feature of a concatenated
@@ -677,7 +689,8 @@ class SparseTable:
                 and self.num_rows <= (1 << 36) and self.num_rows // 8 <= _BITMAP_RATIO * max(n, 1)):
             # bounded key space: bitmap dedupe (sorted unique keys, grouped by owner by construction)
             pp.flat = flat
-            pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.bitmap_plan(flat, self.bounds, self.num_rows, rmult)
+            pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.bitmap_plan(flat, self.bounds, self.num_rows, rmult,
+                                                                   oor=self._oor_counter())
             pp.csr = ops.emb_build_csr(pp.inv, pp.F, n) if want_csr else None
             pp.host = pp.event = pp.cev = None
             pp.exchanged = self.comm.world == 1
@@ -783,7 +796,8 @@ class SparseTable:
                     and 0 < self.rows_local // 8 <= _BITMAP_RATIO * M):
                 if getattr(self, "_own_local_bounds", None) is None:
                     self._own_local_bounds = torch.tensor([0, self.rows_local], dtype=torch.int64, device=dev)
-                ou, oi, _, oU = ops.bitmap_plan(recv_keys - self.base, self._own_local_bounds, self.rows_local)
+                ou, oi, _, oU = ops.bitmap_plan(recv_keys - self.base, self._own_local_bounds, self.rows_local,
+                                                oor=self._oor_counter())
                 ou = ou + self.base
             else:
                 ou, oi, _, oU = ops.unique_bucketize_n(recv_keys, self._own_bounds)
@@ -794,6 +808,23 @@ class SparseTable:
 
     def plan(self, keys: torch.Tensor, csr: bool = False) -> SparsePlan:
         return self._finish_plan(self._start_plan(keys, csr))
+
+    def _oor_counter(self) -> torch.Tensor:
+        """Device count of keys the bitmap planner found outside [0, num_rows) (they would alias
+        row 0); read at the next host sync point (drain), never per step."""
+        c = getattr(self, "_oor", None)
+        if c is None:
+            c = self._oor = torch.zeros(1, dtype=torch.int64, device=self.comm.device)
+        return c
+
+    def _check_keys(self):
+        c = getattr(self, "_oor", None)
+        if c is not None:
+            n = int(c.item())
+            if n:
+                c.zero_()
+                raise ValueError(f"table {self.table_id}: {n} keys outside [0, {self.num_rows}) were planned "
+                                 f"(their Gets read and their Adds wrote row 0)")
 
     def advance_plan(self, pending, finish: bool = True):
         """Later halves of lookahead planning, called once the current step is issued (so these
@@ -944,6 +975,7 @@ class SparseTable:
 
     def drain(self):
         self.pipe.drain()
+        self._check_keys()
 
     def reset_after_rollback(self):
         self.pipe.reset()

@@ -56,7 +56,13 @@ def parse(argv=None):
     ap.add_argument("--value_dtype", default="float32", choices=["float32", "float64"],
                     help="LR table precision; float64 = the reference's CreateTable<double> (lr_example.cpp:182)")
     ap.add_argument("--transport", default="collective", choices=["collective", "onesided"],
-                    help="DLRM SSP/ASP data path: RCCL collectives, or one-sided IPC row access (ps/onesided.py)")
+                    help="W&D / DLRM SSP/ASP data path: RCCL collectives, or the asynchronous PS "
+                         "(one-sided row reads, inbox pushes, owner-side optimizer apply; ps/onesided.py)")
+    ap.add_argument("--asp_bound", type=int, default=-1,
+                    help="ASP on the one-sided transport: >= 0 bounds how far a Get may run ahead of the "
+                         "owners' applies (the SSP gate); -1 (default): unbounded, the reference ASP")
+    ap.add_argument("--asp_depth", type=int, default=2,
+                    help="ASP on the collective transport: clocks in flight before a Get waits (pipelining)")
     ap.add_argument("--force_quit_rank", type=int, default=-1,
                     help="(LR --input) treat this rank's shard as empty: it ForceQuits, the others continue")
     ap.add_argument("--checkpoint_commit", default="eager", choices=["eager", "async"],
@@ -131,10 +137,10 @@ def build(args, comm):
         from .data.synthetic import CriteoSynth
         from .models.widedeep import WideDeep, WideDeepConfig
 
-        cfg = WideDeepConfig(consistency=args.consistency, staleness=args.staleness,
-                             **({"cards": SMALL_CARDS} if args.small else {}))
-        m = WideDeep(cfg, comm)
         B = args.batch or (64 if args.small else 16384)
+        cfg = WideDeepConfig(consistency=args.consistency, staleness=args.staleness, transport=args.transport,
+                             max_batch=B, **({"cards": SMALL_CARDS} if args.small else {}))
+        m = WideDeep(cfg, comm)
         return m, {0: m.emb, 1: m.dense}, (lambda: CriteoSynth(B, cards=cfg.cards, device=dev, seed=seed)), \
             (lambda b: m.train_step(*b)), B
     if args.model == "mlp":
@@ -148,10 +154,10 @@ def build(args, comm):
     if args.model == "dlrm":
         from .models.dlrm import DLRM, DLRMConfig
 
-        cfg = DLRMConfig(num_rows=20000 if args.small else 100_000_000, consistency=args.consistency,
-                         staleness=args.staleness, transport=args.transport)
-        m = DLRM(cfg, comm)
         B = args.batch or (64 if args.small else 16384)
+        cfg = DLRMConfig(num_rows=20000 if args.small else 100_000_000, consistency=args.consistency,
+                         staleness=args.staleness, transport=args.transport, max_batch=B)
+        m = DLRM(cfg, comm)
         return m, {0: m.emb, 1: m.dense}, (lambda: _Skippable(_DLRMData(B, cfg, dev, seed))), \
             (lambda b: m.train_step(*b)), B
     if args.model == "gpt2":
@@ -305,11 +311,16 @@ class _GaussData:
 
 
 def _is_comm_failure(e: BaseException) -> bool:
-    """A collective failed because a peer died / the communicator was aborted (gloo: connection
-    closed or reset; RCCL with TORCH_NCCL_ASYNC_ERROR_HANDLING=2: aborted / timed out)."""
-    msg = f"{type(e).__name__}: {e}"
-    return any(k in msg for k in ("Connection closed", "Connection reset", "Broken pipe", "DistBackendError",
-                                  "NCCL", "aborted", "timed out", "Timed out", "Gloo", "peer"))
+    """A collective failed because a peer died or the communicator was aborted -- by type, not by
+    message: RCCL (TORCH_NCCL_ASYNC_ERROR_HANDLING=2: an aborted / timed-out communicator) and the
+    c10d store raise the torch.distributed error classes (DistBackendError, DistNetworkError,
+    DistStoreError); gloo's transport raises a RuntimeError tagged with its gloo source location
+    ("[.../gloo/transport/tcp/pair.cc:547] Connection closed by peer"). Errors of this process's
+    own code (a failed kernel, the async PS server) are not peer failures and propagate."""
+    if isinstance(e, dist.DistError):
+        return True
+    head = str(e).split("]", 1)[0]
+    return isinstance(e, RuntimeError) and head.startswith("[") and "/gloo/" in head
 
 
 def _force_quit(comm, has_data: bool, rank: int):
@@ -340,6 +351,23 @@ def _force_quit(comm, has_data: bool, rank: int):
     return Comm(group=group, device=comm.device)
 
 
+class _ckpt_state:
+    """Heartbeat state "ckpt" while a checkpoint is written / committed: a multi-GB shard write
+    advances no step, and the supervisor gives that state its own (long) limit instead of the
+    stuck-in-a-step progress timeout."""
+
+    def __init__(self, hb):
+        self.hb = hb
+
+    def __enter__(self):
+        if self.hb is not None:
+            self.prev, self.hb.state = self.hb.state, "ckpt"
+
+    def __exit__(self, *exc):
+        if self.hb is not None:
+            self.hb.state = self.prev
+
+
 def _wait_directive(hb_dir: str, generation: int, timeout: float = 300.0) -> dict:
     """Rollback directive of the supervisor (minips_amd.elastic): a newer generation with the
     rendezvous port of the re-formed group (the reference's kRollBack, mailbox.cpp:172-191)."""
@@ -365,7 +393,12 @@ def main(argv=None):
 
     if args.metrics_dir:
         os.environ["MINIPS_METRICS_DIR"] = args.metrics_dir
-    inplace = args.recovery == "inplace" and bool(args.heartbeat_dir)
+    os.environ["MINIPS_ASP_DEPTH"] = str(max(0, args.asp_depth))
+    if args.asp_bound >= 0:
+        os.environ["MINIPS_ASP_BOUND"] = str(args.asp_bound)
+    # the asynchronous tables' peers hold IPC mappings of every shard and a shared board: a lost
+    # rank restarts the whole set from the checkpoint, never an in-place rollback
+    inplace = args.recovery == "inplace" and bool(args.heartbeat_dir) and args.transport != "onesided"
     if inplace:  # RCCL: a dead peer aborts the communicator and raises, instead of killing us
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
     comm = init_distributed()
@@ -452,10 +485,11 @@ def main(argv=None):
                 if comm.device.type == "cuda":
                     torch.cuda.synchronize(comm.device)
                 t_steady, n_steady = time.perf_counter(), args.steps - it
-            if args.checkpoint_commit == "async":
-                ck.try_commit()  # publishes an in-flight checkpoint once every rank's files are written
-            else:
-                ck.commit()  # publishes the checkpoint issued after the previous step (no-op otherwise)
+            with _ckpt_state(hb):  # checkpoint phases are not steps: their own heartbeat state
+                if args.checkpoint_commit == "async":
+                    ck.try_commit()  # publishes an in-flight checkpoint once every rank's files are written
+                else:
+                    ck.commit()  # publishes the checkpoint issued after the previous step (no-op otherwise)
             inj.step(it)
             t0 = time.perf_counter()
             with metrics.range(f"step {it}"):
@@ -474,7 +508,8 @@ def main(argv=None):
                 report.flush()
             if args.checkpoint_toggle and args.checkpoint_every > 0 and (it + 1) % args.checkpoint_every == 0 \
                     and it + 1 < args.steps:
-                ck.save(tables, iteration=it + 1)
+                with _ckpt_state(hb):
+                    ck.save(tables, iteration=it + 1)
             if hb:
                 hb.progress(it)
             it += 1
@@ -489,7 +524,8 @@ def main(argv=None):
     if comm.device.type == "cuda":
         torch.cuda.synchronize(comm.device)
     steady_ms = (time.perf_counter() - t_steady) * 1e3 / n_steady if t_steady is not None and n_steady else None
-    ck.commit()
+    with _ckpt_state(hb):
+        ck.commit()
     # parameter checksum over every table (identical on all ranks): the parameter values only
     # (hash tables also export their keys, which are not parameters)
     def _param_sum(t):

@@ -494,3 +494,39 @@ def test_bitmap_plan_matches_sorted_unique(dev, num_rows, n, P, route):
     assert torch.equal(gi.cpu(), ci)
     assert torch.equal(gc.cpu(), cc)
     assert torch.equal(cu[:U][ci], (keys * mult) % num_rows if route else keys)
+
+
+@pytest.mark.parametrize("base,rows,M", [(4_200_000, 4_200_000, 300_000), (7, 1000, 5000)])
+def test_owner_side_bitmap_dedupe_nonzero_base(dev, base, rows, M):
+    """the owner-side dedupe of the keys all requesters asked for (SparseTable._finish_plan
+    at N > 1) plans them relative to the owner's base with the bitmap planner; with synthetic
+    recv_keys in [base, base + rows) it must give what the hash dedupe gives on the absolute keys
+    (same unique set, an inverse that maps every key back, one owner holding all of them)."""
+    g = torch.Generator().manual_seed(M)
+    recv = torch.randint(base, base + rows, (M,), generator=g)
+    recv[: M // 4] = recv[M // 4: M // 2]
+    recv = recv.to(dev)
+    local = torch.tensor([0, rows], dtype=torch.int64, device=dev)
+    ou, oi, oc, oU = ops.bitmap_plan(recv - base, local, rows)
+    ou = ou + base
+    hu, hi, hc, hU = ops.unique_bucketize_n(recv, torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=dev))
+    U = int(oU.reshape(-1)[0])
+    assert U == int(hU.reshape(-1)[0]) == int(oc[0])
+    assert torch.equal(torch.sort(ou[:U]).values, torch.sort(hu[:U]).values)
+    assert torch.equal(ou[oi], recv) and torch.equal(hu[hi], recv)
+
+
+def test_bitmap_plan_counts_out_of_range_keys(dev):
+    """a key outside the planner's key space is never written and never silently
+    aliased: the device counter records it, and a table surfaces it at drain()."""
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.tables import SparseTable
+
+    oor = torch.zeros(1, dtype=torch.int64, device=dev)
+    keys = torch.tensor([3, 5, 1000, -2, 5], dtype=torch.int64, device=dev)
+    ops.bitmap_plan(keys, torch.tensor([0, 100], dtype=torch.int64, device=dev), 100, oor=oor)
+    assert int(oor) == 2
+    t = SparseTable(Comm(device=torch.device(dev)), 100, 4, optimizer="add", route="range", init_std=0.0)
+    t.get(torch.tensor([1, 2, 500], device=dev))  # bitmap planner (small key space)
+    with pytest.raises(ValueError, match="outside"):
+        t.drain()

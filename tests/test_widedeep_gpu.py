@@ -46,9 +46,42 @@ def test_widedeep_gpu_matches_cpu(dev):
     assert float((diff > 2e-3).float().mean()) < 1e-2
 
 
-def test_widedeep_ssp_runs(dev):
+@pytest.mark.parametrize("s", [1, 2])
+def test_collective_ssp_read_bound(dev, s):
+    """SSP(s) on the collective path (clocks on the table's side stream, reads gated at clock
+    c - s - 1): every read at clock c holds the pushes of clocks < c - s and never more than were
+    issued, and reads DO run ahead of a slow apply (the side stream is slowed by a spin kernel
+    before each clock) -- so the bound, not a synchronous apply, is what holds."""
+    from minips_amd.ps.tables import SparseTable
+
+    t = SparseTable(Comm(device=torch.device(dev)), 64, 4, optimizer="add", consistency="ssp", staleness=s,
+                    pull_dtype=torch.float32, init_std=0.0)
+    assert t.pipe.async_
+    k = torch.tensor([7], device=dev)
+    seen = []
+    for c in range(16):
+        v = float(t.get_rows(k)[0, 0])  # a Get at clock c
+        seen.append((c, v))
+        t.add_keys(k, torch.ones(1, 4, device=dev))
+        with torch.cuda.stream(t.pipe.stream):
+            torch.cuda._sleep(20_000_000)  # ~10 ms: the clock's apply lands late
+        t.clock()
+    t.drain()
+    for c, v in seen:
+        assert max(0, c - s) <= v <= c, (s, seen)
+    assert any(v < c for c, v in seen), seen  # the reads really were stale
+    assert float(t.get_rows(k)[0, 0]) == 16
+
+
+def test_widedeep_ssp_staleness_histogram(dev):
+    """W&D SSP s=1 end to end: the metrics log's observed-staleness histogram never exceeds s."""
+    from minips_amd.utils.metrics import get_logger
+
+    log = get_logger()
+    log.staleness_hist.clear()
     losses, _ = _run(dev, steps=10, consistency="ssp", staleness=1)
     assert all(l == l for l in losses) and losses[-1] < losses[0] + 0.05
+    assert log.staleness_hist and max(log.staleness_hist) <= 1, log.staleness_hist
 
 
 def test_widedeep_lookahead_depth_matches(dev):

@@ -62,9 +62,10 @@ def build(args, comm):
             # Adagrad state = 85 GB) per GPU; weak scaling keeps the per-GPU shard fixed
             rows = args.rows_per_gpu * comm.world
             cfg = DLRMConfig(num_rows=rows, D=16, consistency=args.consistency if args.consistency != "bsp"
-                             else "asp", staleness=args.staleness)
+                             else "asp", staleness=args.staleness, transport=args.transport, max_batch=B)
         else:
-            cfg = DLRMConfig(num_rows=args.rows, consistency=args.consistency, staleness=args.staleness)
+            cfg = DLRMConfig(num_rows=args.rows, consistency=args.consistency, staleness=args.staleness,
+                             transport=args.transport, max_batch=B)
         m = DLRM(cfg, comm)
         from minips_amd.data.synthetic import DLRMSynth
 
@@ -81,7 +82,7 @@ def build(args, comm):
             return m.train_step(*cur, next_keys=nxt[1])
 
         return m, step, B, "samples/s", dict(model=f"DLRM {cfg.num_rows} rows x {cfg.D} (26 sparse + 13 dense), "
-                                                   f"{cfg.consistency}", seq_len=None,
+                                                   f"{cfg.consistency}, {cfg.transport}", seq_len=None,
                                              rows_per_gpu=cfg.num_rows // comm.world, consistency=cfg.consistency)
     if args.model == "lr":
         from minips_amd.data.synthetic import SparseLRSynth
@@ -108,7 +109,8 @@ def build(args, comm):
         from minips_amd.models.widedeep import WideDeep, WideDeepConfig
 
         B = args.batch or 16384
-        cfg = WideDeepConfig(consistency="ssp", staleness=max(1, args.staleness))
+        cfg = WideDeepConfig(consistency="ssp", staleness=max(1, args.staleness), transport=args.transport,
+                             max_batch=B)
         m = WideDeep(cfg, comm)
         data = CriteoSynth(B, cards=cfg.cards, device=dev, seed=1000 + r)
         state = {"cur": data.next()}
@@ -118,8 +120,8 @@ def build(args, comm):
             cur, state["cur"] = state["cur"], nxt
             return m.train_step(*cur, next_keys=nxt[1])
 
-        return m, step, B, "samples/s", dict(model="Wide&Deep Criteo SSP", seq_len=None,
-                                             consistency=f"ssp{cfg.staleness}")
+        return m, step, B, "samples/s", dict(model=f"Wide&Deep Criteo SSP ({args.transport})", seq_len=None,
+                                             consistency=f"ssp{cfg.staleness}", transport=args.transport)
     raise SystemExit(f"unknown model {args.model}")
 
 
@@ -137,6 +139,8 @@ def main():
                     help="mlp: capture the step in a HIP graph (one rank, BSP; off by default: at batch 8192 the "
                          "step is GPU-bound, 0.364 vs 0.350 ms measured)")
     ap.add_argument("--staleness", type=int, default=0)
+    ap.add_argument("--transport", default="collective", choices=["collective", "onesided"],
+                    help="widedeep-ssp / dlrm: RCCL collectives or the asynchronous PS (ps/onesided.py)")
     ap.add_argument("--value-dtype", default="float32", choices=["float32", "float64"],
                     help="lr: table precision (float64 = the reference's CreateTable<double>)")
     args = ap.parse_args()

@@ -137,9 +137,14 @@ def build_apps(objs: list[str]) -> list[str]:
     return outs
 
 
+# runtime pieces the kernel module links too: the async PS server thread and its board
+# (csrc/runtime/async_server.h drives the HIP applier of csrc/kernels/onesided.hip)
+KERNEL_RT = ("ps_board", "async_server")
+
+
 def kernel_objs() -> list[str]:
     os.makedirs(OBJ, exist_ok=True)
-    hdrs = _headers("csrc/kernels")
+    hdrs = _headers("csrc/kernels") + [os.path.join(ROOT, "csrc/runtime", h + ".h") for h in KERNEL_RT]
     jobs, objs = [], []
     for src in sorted(glob.glob(os.path.join(ROOT, "csrc/kernels/*.hip"))):
         out = os.path.join(OBJ, "k_" + os.path.basename(src)[:-4] + ".o")
@@ -149,12 +154,14 @@ def kernel_objs() -> list[str]:
     return objs
 
 
-def build_ops_py(kobjs: list[str]) -> str:
+def build_ops_py(kobjs: list[str], robjs: list[str] = ()) -> str:
     src = os.path.join(ROOT, "csrc/bindings/ops_py.cpp")
     out = os.path.join(PKG, "_kernels" + EXT)
     bobj = os.path.join(OBJ, "ops_py.o")
     cflags, ldflags = _torch_flags()
-    hdrs = _headers("csrc/kernels", "csrc/bindings")
+    kobjs = list(kobjs) + [o for o in robjs if os.path.basename(o)[3:-2] in KERNEL_RT]
+    hdrs = _headers("csrc/kernels", "csrc/bindings") + [os.path.join(ROOT, "csrc/runtime", h + ".h")
+                                                        for h in KERNEL_RT]
     _compile_many([(bobj, [src] + hdrs, [HIPCC, "-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
                                          *cflags, "-c", src, "-o", bobj])])
     _compile_many([(out, [bobj] + kobjs,
@@ -206,7 +213,7 @@ def main(argv: list[str]) -> int:
             print("built", o)
     if targets & {"kernels", "ops_py"}:
         kobjs = kernel_objs()
-        print("built", build_ops_py(kobjs))  # always relink: a stale .so would silently run old kernels
+        print("built", build_ops_py(kobjs, objs))  # always relink: a stale .so would silently run old kernels
     return 0
 
 
