@@ -284,13 +284,15 @@ class _AsyncTable:
         """After the rows landed (server paused since restore_dst): every rank restarts at
         ``clock`` -- its sent counter and its owner row of the board -- then all resume."""
         board, t = self.ps.board, self.t
+        # host barriers with the long timeout (restore times differ by rank): (a) every rank is
+        # done reading this table's counters (a peer may still be draining its old clocks) before
+        # any rank resets them, (b) nobody pushes before every rank reset its sent counter and row
+        self.comm.store_barrier(f"async_restore_a_t{t}")
         self.clock_n = int(clock)
         board.publish_sent(t, self.clock_n)
         board.publish_applied_row(t, self.clock_n)
         self.staleness_hist.clear()
-        # nobody pushes before every rank reset its counters and rows (a host barrier with the long
-        # timeout: restore times differ by rank)
-        self.comm.store_barrier(f"async_restore_t{t}")
+        self.comm.store_barrier(f"async_restore_b_t{t}")
         self.ps.resume()
 
     def reset_after_rollback(self):

@@ -308,6 +308,7 @@ def _ckpt_run(rank, world, prefix):
     it = ck.load({0: sp, 1: dn})
     same = [torch.equal(a, b) for a, b in zip(snap, (sp.shard, sp.state, dn.master, dn.v))]
     clocks = (sp.clock_n, dn.clock_n, sp.ps.board.min_applied(sp.t))
+    comm.barrier()  # every rank compared before anyone pushes again
     # training continues after the restore
     keys, rows, dense = _push_of(rank, 50)
     sp.get(keys)
