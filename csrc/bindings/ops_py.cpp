@@ -49,7 +49,8 @@ T* opt_ptr(const c10::optional<at::Tensor>& t, at::ScalarType dt, const char* na
 void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K, bool a_km,
           bool b_kn, int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& mask,
           const c10::optional<at::Tensor>& colsum, double alpha, int64_t split_k, int64_t batch, int64_t inner,
-          int64_t lda_, int64_t ldb_, int64_t ldc_, std::vector<int64_t> strides) {
+          int64_t lda_, int64_t ldb_, int64_t ldc_, std::vector<int64_t> strides,
+          const c10::optional<at::Tensor>& perm, int64_t seg) {
   // 2-D operands may be column-sliced views: rows contiguous (stride(1) == 1), ld = stride(0).
   auto check_mat = [](const at::Tensor& t, const char* n) {
     TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
@@ -62,6 +63,15 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   check_dtype(B, at::kBFloat16, "B");
   const bool f32_out = epi == minips_k::kEpiStoreF32 || epi == minips_k::kEpiAtomicF32;
   check_dtype(C, f32_out ? at::kFloat : at::kBFloat16, "C");
+  const bool permuted = epi == minips_k::kEpiPermRowsBf16;
+  const int* perm_p = opt_ptr<int>(perm, at::kInt, "perm");
+  if (permuted) {
+    // C is [M * N / seg, seg] rows in the permuted order; perm lists M * N / seg distinct rows of it
+    TORCH_CHECK(perm_p && seg > 0 && seg % 8 == 0 && N % seg == 0 && batch <= 1 && split_k <= 1,
+                "permuted rows: perm, seg % 8 == 0, N % seg == 0, no batch / split-K");
+    TORCH_CHECK(perm->numel() >= M * (N / seg) && C.is_contiguous() && C.numel() >= M * N,
+                "permuted rows: perm [M*N/seg] and a contiguous C of >= M*N values");
+  }
   TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8");
   if (a_km) TORCH_CHECK(M % 8 == 0, "KM layout needs M % 8 == 0");
   if (b_kn) TORCH_CHECK(N % 8 == 0, "KN layout needs N % 8 == 0");
@@ -73,7 +83,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
     TORCH_CHECK(A.size(0) >= a_rows && A.size(1) >= a_cols, "A shape ", A.sizes(), " vs M,N,K=", M, ",", N, ",", K);
     TORCH_CHECK(B.size(0) >= b_rows && B.size(1) >= b_cols, "B shape ", B.sizes(), " vs M,N,K=", M, ",", N, ",", K);
-    TORCH_CHECK(C.size(0) >= M && C.size(1) >= N, "C shape ", C.sizes(), " vs M,N=", M, ",", N);
+    TORCH_CHECK(permuted || (C.size(0) >= M && C.size(1) >= N), "C shape ", C.sizes(), " vs M,N=", M, ",", N);
     lda = A.stride(0);
     ldb = B.stride(0);
     ldc = C.stride(0);
@@ -123,7 +133,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   minips_k::gemm_bf16_batched(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb,
                               (int)ldc, a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p, (float)alpha,
                               (int)split_k, (int)batch, (int)inner, st[0], st[1], st[2], st[3], st[4], st[5],
-                              stream_of(A), slab.defined() ? ptr<float>(slab) : nullptr);
+                              stream_of(A), slab.defined() ? ptr<float>(slab) : nullptr, perm_p, (int)seg);
 }
 
 // Bitmap planner of a bounded key space (keys, after the optional routing k * mult mod rn, in
@@ -221,11 +231,41 @@ void gather_rows(const at::Tensor& table, const at::Tensor& keys, int64_t base, 
                               stream_of(keys));
     return;
   }
-  check_dtype(table, at::kFloat, "table");
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "out must be fp32 or bf16");
+  if (table.scalar_type() == at::kBFloat16) {  // bf16 rows (bf16rows.hip)
+    TORCH_CHECK(D == table.size(1) && out.is_contiguous(), "bf16 table gather: whole rows");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+    minips_k::gather_rows_bf16tab(ptr<bf16_t>(table), table.stride(0), ptr<int64_t>(keys), n, base, D, out.data_ptr(),
+                                  out.scalar_type() == at::kBFloat16, stream_of(keys), count_ptr(n_dev));
+    return;
+  }
+  check_dtype(table, at::kFloat, "table");
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::gather_rows(ptr<float>(table), table.stride(0), ptr<int64_t>(keys), n, base, D, out.data_ptr(),
                         out.scalar_type() == at::kBFloat16, stream_of(keys), count_ptr(n_dev));
+}
+
+// fp32 gradient rows into bf16 table rows (stochastic rounding): opt 0 row-wise Adagrad, 1 w += scale*g
+void sparse_apply_bf16(int64_t opt, at::Tensor& table, const c10::optional<at::Tensor>& state,
+                       const c10::optional<at::Tensor>& state2, int64_t D1, const at::Tensor& keys, int64_t base,
+                       const at::Tensor& grads, double lr, double eps, double scale, int64_t step, int64_t seed,
+                       const c10::optional<at::Tensor>& n_dev) {
+  TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.stride(1) == 1, "table: row-major GPU matrix");
+  check_dtype(table, at::kBFloat16, "table");
+  check_gpu(keys, "keys");
+  check_dtype(keys, at::kLong, "keys");
+  check_gpu(grads, "grads");
+  check_dtype(grads, at::kFloat, "grads");
+  const int64_t n = keys.numel();
+  const int D = (int)table.size(1);
+  TORCH_CHECK(grads.dim() == 2 && grads.size(0) >= n && grads.size(1) == D, "grads [>= n, D]");
+  float* st = opt_ptr<float>(state, at::kFloat, "state");
+  float* st2 = opt_ptr<float>(state2, at::kFloat, "state2");
+  TORCH_CHECK(opt != 0 || (st && state->numel() >= table.size(0)), "row-wise Adagrad needs its state");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  minips_k::sparse_apply_bf16tab((int)opt, ptr<bf16_t>(table), table.stride(0), st, st2, (int)D1, ptr<int64_t>(keys),
+                                 n, base, D, ptr<float>(grads), (float)lr, (float)eps, (float)scale, (uint32_t)step,
+                                 (uint32_t)seed, stream_of(keys), count_ptr(n_dev));
 }
 
 void lookup_rows(const at::Tensor& rows, const at::Tensor& inv, int64_t F, int64_t D, at::Tensor& out) {
@@ -389,16 +429,22 @@ std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t 
 
 void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, const at::Tensor& inv, int64_t F,
                      int64_t D, at::Tensor& grad_rows, int64_t x_off, const c10::optional<at::Tensor>& U_dev,
-                     const c10::optional<at::Tensor>& members, const c10::optional<at::Tensor>& memrow) {
+                     const c10::optional<at::Tensor>& members, const c10::optional<at::Tensor>& memrow,
+                     bool sorted_rows) {
   check_gpu(dX, "dX");
   const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
   check_gpu(inv, "inv");
   check_gpu(grad_rows, "grad_rows");
   TORCH_CHECK(dX.scalar_type() == at::kFloat || dX.scalar_type() == at::kBFloat16, "dX must be fp32 or bf16");
   check_dtype(grad_rows, at::kFloat, "grad_rows");
-  const int64_t B = dX.size(0);
   TORCH_CHECK(dX.dim() == 2 && dX.stride(1) == 1, "dX must be a row-major matrix");
-  TORCH_CHECK(inv.numel() == B * F && dX.size(1) >= x_off + F * D && grad_rows.size(1) >= D + (dw ? 1 : 0), "shapes");
+  if (sorted_rows) {  // dX [B*F, D] in the CSR's member order (kEpiPermRowsBf16 dgrad output)
+    TORCH_CHECK(members.has_value() && members->defined() && x_off == 0 && dX.size(1) == D && dX.is_contiguous() &&
+                    dX.size(0) == inv.numel() && inv.numel() % F == 0, "sorted rows: dX [B*F, D] + the CSR");
+  }
+  const int64_t B = sorted_rows ? inv.numel() / F : dX.size(0);
+  TORCH_CHECK(inv.numel() == B * F && (sorted_rows || dX.size(1) >= x_off + F * D) &&
+                  grad_rows.size(1) >= D + (dw ? 1 : 0), "shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
   static const bool tile_mode = [] {
     const char* e = std::getenv("MINIPS_EMB_BWD");
@@ -417,7 +463,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
                   "members/memrow: int32 [B*F]");
       minips_k::emb_backward_csr(base0, bf0, (int)dX.stride(0), dw, B, (int)F, (int)D, members->data_ptr<int>(),
                                  memrow->data_ptr<int>(), ptr<float>(grad_rows), (int)grad_rows.stride(0), (int)U,
-                                 stream_of(dX), count_ptr(U_dev));
+                                 stream_of(dX), count_ptr(U_dev), sorted_rows);
       return;
     }
     at::Tensor ws = at::empty({3 * U + 1 + 2 * B * F + U / 1024 + 1}, inv.options().dtype(at::kInt));
@@ -440,7 +486,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
 // Returns (uniq, inv, counts [1], U_dev [1], members, memrow).
 std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& col_base, const at::Tensor& col_bits,
                                     std::vector<int64_t> col_bits_host, int64_t route_mult, int64_t route_n,
-                                    const at::Tensor& bounds) {
+                                    const at::Tensor& bounds, bool with_positions) {
   check_gpu(bounds, "bounds");
   check_dtype(bounds, at::kLong, "bounds");
   const int64_t P = bounds.numel() - 1;
@@ -465,12 +511,14 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
   auto ukey = at::empty({n}, o64), uniq = at::empty({n}, o64), inv = at::empty({n}, o64);
   auto members = at::empty({n}, o64.dtype(at::kInt)), memrow = at::empty({n}, o64.dtype(at::kInt));
   auto counts = at::empty({P + 1}, o64);
+  at::Tensor pos = with_positions ? at::empty({n}, o64.dtype(at::kInt)) : at::Tensor();
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), col_bits.data_ptr<int32_t>(),
                         (uint64_t)route_mult, (uint64_t)route_n, ptr<int64_t>(bounds), (int)P, ws.data_ptr<int32_t>(),
                         ptr<int64_t>(ukey),
                         ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
-                        ptr<int64_t>(counts), stream_of(keys));
+                        ptr<int64_t>(counts), stream_of(keys), with_positions ? pos.data_ptr<int32_t>() : nullptr);
+  if (with_positions) return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos};
   return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow};
 }
 
@@ -1002,6 +1050,16 @@ void ps_gather_rows(const at::Tensor& bases, const at::Tensor& bounds, const at:
                            opt_count(n_dev), (int)W, out.data_ptr(), bf, stream_of(keys));
 }
 
+// pos[members[m]] = m: where the dgrad's permuted-rows epilogue puts each lookup's gradient row.
+at::Tensor emb_csr_positions(const at::Tensor& members) {
+  check_gpu(members, "members");
+  check_dtype(members, at::kInt, "members");
+  at::Tensor pos = at::empty_like(members);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(members.device());
+  minips_k::emb_csr_positions(members.data_ptr<int>(), members.numel(), pos.data_ptr<int>(), stream_of(members));
+  return pos;
+}
+
 // The owner side of the asynchronous PS on a GPU rank: minips::AsyncServer (the server thread,
 // csrc/runtime/async_server.h) driving a HipApplier (the optimizer kernels on the owner's own
 // stream). Table buffers are passed as raw device addresses; the Python table keeps them alive
@@ -1208,7 +1266,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("a_km"), py::arg("b_kn"), py::arg("epi"), py::arg("bias"), py::arg("mask"), py::arg("colsum"),
         py::arg("alpha") = 1.0, py::arg("split_k") = 1, py::arg("batch") = 1, py::arg("inner") = 1,
-        py::arg("lda") = 0, py::arg("ldb") = 0, py::arg("ldc") = 0, py::arg("strides") = std::vector<int64_t>());
+        py::arg("lda") = 0, py::arg("ldb") = 0, py::arg("ldc") = 0, py::arg("strides") = std::vector<int64_t>(),
+        py::arg("perm") = py::none(), py::arg("seg") = 0);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("softmax_xent", &softmax_xent);
@@ -1244,11 +1303,13 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_head", &wd_head);
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
-        py::arg("members") = py::none(), py::arg("memrow") = py::none());
+        py::arg("members") = py::none(), py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);
   m.def("emb_seg_adagrad", &emb_seg_adagrad);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("cu_masked_stream", &cu_masked_stream);
-  m.def("plan_sorted", &plan_sorted);
+  m.def("plan_sorted", &plan_sorted, py::arg("keys"), py::arg("col_base"), py::arg("col_bits"),
+        py::arg("col_bits_host"), py::arg("route_mult"), py::arg("route_n"), py::arg("bounds"),
+        py::arg("with_positions") = false);
   m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none(),
         py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),
@@ -1272,6 +1333,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("ps_push_rows", &ps_push_rows, py::arg("uniq"), py::arg("counts"), py::arg("U_dev"), py::arg("n"),
         py::arg("g"), py::arg("inbox"), py::arg("slot_off"), py::arg("cap"));
   m.def("ps_set_headers", &ps_set_headers);
+  m.def("emb_csr_positions", &emb_csr_positions);
+  m.def("sparse_apply_bf16", &sparse_apply_bf16);
+  m.attr("EPI_PERM_ROWS_BF16") = (int)minips_k::kEpiPermRowsBf16;
   m.def("ps_gather_rows", &ps_gather_rows, py::arg("bases"), py::arg("bounds"), py::arg("keys"), py::arg("n_dev"),
         py::arg("W"), py::arg("out"));
   m.attr("PS_ADD") = (int)minips_k::kPsAdd;

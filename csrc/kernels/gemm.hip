@@ -111,7 +111,19 @@ struct EpiArgs {
   int inner;
   int64_t sa_o, sa_i, sb_o, sb_i, sc_o, sc_i;
   int64_t sc_split;  // split-K slab mode: C += blockIdx.z * sc_split (0 = all splits share C)
+  const int* perm;   // kEpiPermRowsBf16: segment positions [M][N / seg]
+  int seg;
 };
+
+// Destination of an output row segment (kEpiPermRowsBf16: the permuted row of its segment).
+template <int EPI>
+__device__ __forceinline__ int64_t out_offset(const EpiArgs& ep, int N, int row, int col) {
+  if (EPI == kEpiPermRowsBf16) {
+    const int s = col / ep.seg;
+    return (int64_t)ep.perm[(int64_t)row * (N / ep.seg) + s] * ep.seg + (col - s * ep.seg);
+  }
+  return (int64_t)row * ep.ldc + col;
+}
 
 // Fused epilogue of one wave's (16 MR) x 64 accumulator block at rows mb.., cols nb...
 template <int EPI, int MR>
@@ -133,7 +145,7 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
         const int row = mb + i * 16 + row_q + r;
         if (!(col_ok && row < M)) continue;
         float v = acc[i][j][r] * ep.alpha;
-        const int64_t off = (int64_t)row * ep.ldc + col;
+        const int64_t off = out_offset<EPI>(ep, N, row, col);
         if (EPI == kEpiStoreF32) {
           ((float*)ep.C)[off] = v;
         } else if (EPI == kEpiAtomicF32) {
@@ -146,7 +158,7 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
           float x = v + bias;
           float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
           ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
-        } else if (EPI == kEpiStoreBf16) {
+        } else if (EPI == kEpiStoreBf16 || EPI == kEpiPermRowsBf16) {
           ((bf16_t*)ep.C)[off] = f2bf(v);
         } else if (EPI == kEpiBiasGeluAuxBf16) {
           const float x = v + bias;
@@ -206,7 +218,7 @@ __device__ __forceinline__ float epi_apply(float v, float bias, float m, bf16_t*
     return v * gp;
   }
   if (EPI == kEpiReluMaskBf16) return m > 0.f ? v : 0.f;
-  return v;  // kEpiStoreBf16 / kEpiStoreF32
+  return v;  // kEpiStoreBf16 / kEpiPermRowsBf16 / kEpiStoreF32
 }
 
 template <int EPI, int MR>
@@ -218,7 +230,8 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
   constexpr bool READ_MASK = EPI == kEpiReluMaskBf16 || EPI == kEpiGeluGradBf16;
   const int col_l = lane & 15, row_q = (lane >> 4) * 4;
   // vector paths need 16-byte aligned row segments
-  const bool c_vec = ((ep.ldc & (F32OUT ? 3 : 7)) == 0) && ((reinterpret_cast<uintptr_t>(ep.C) & 15) == 0);
+  const bool c_vec = (EPI == kEpiPermRowsBf16 ? (ep.seg & 7) == 0 : (ep.ldc & (F32OUT ? 3 : 7)) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(ep.C) & 15) == 0);
   const bool m_vec = ((ep.ldmask & 7) == 0) && ((reinterpret_cast<uintptr_t>(ep.mask) & 15) == 0);
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   // the bias depends on the column only: this lane's 8 columns are loaded once (one 16-byte
@@ -312,9 +325,15 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
           }
         }
         if (!row_ok) continue;
-        bf16_t* dst = ((bf16_t*)ep.C) + (int64_t)row * ep.ldc + col;
+        // (kEpiPermRowsBf16 with seg % 8 == 0: a lane's 8 columns never cross a segment)
+        bf16_t* dst = ((bf16_t*)ep.C) + out_offset<EPI>(ep, N, row, col);
         if (c_vec && full) {
           *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        } else if (EPI == kEpiPermRowsBf16) {
+          for (int e = 0; e < 8; ++e)
+            if (col + e < N)
+              ((bf16_t*)ep.C)[out_offset<EPI>(ep, N, row, col + e)] =
+                  (bf16_t)((e & 1) ? (pk[e >> 1] >> 16) : (pk[e >> 1] & 0xffffu));
         } else {
           for (int e = 0; e < 8; ++e)
             if (col + e < N) dst[e] = (bf16_t)((e & 1) ? (pk[e >> 1] >> 16) : (pk[e >> 1] & 0xffffu));
@@ -856,6 +875,7 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
     MINIPS_EPI_CASE(AKM, BKN, kEpiReluMaskBf16)                                  \
     MINIPS_EPI_CASE(AKM, BKN, kEpiBiasGeluAuxBf16)                               \
     MINIPS_EPI_CASE(AKM, BKN, kEpiGeluGradBf16)                                  \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiPermRowsBf16)                                  \
     default:                                                                     \
       throw std::runtime_error("gemm: unknown epilogue " + std::to_string(epi)); \
   }
@@ -902,8 +922,11 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, int nsplit,
 void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                        bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
                        float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
-                       int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s, float* slab) {
+                       int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s, float* slab,
+                       const int* perm, int seg) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return;
+  if (epi == kEpiPermRowsBf16 && (!perm || seg <= 0 || seg % 8 || N % seg || batch != 1 || split_k > 1))
+    throw std::runtime_error("gemm: the permuted-rows epilogue needs perm, seg % 8 == 0, N % seg == 0, no batch");
   if (split_k < 1) split_k = 1;
   if (split_k > 1 && epi != kEpiAtomicF32) throw std::runtime_error("gemm: split_k needs the atomic epilogue");
   if (batch > 1 && (mask || colsum)) throw std::runtime_error("gemm: batched mode has no mask/colsum epilogue");
@@ -912,7 +935,7 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
   if (slab && split_k > 1 && batch == 1 && N % 4 == 0) {
     // split-K without atomics: every K slice stores its partial tile into its own slab plane,
     // one streaming kernel adds the planes into C (measured faster than fp32 atomics)
-    EpiArgs sp{slab, N, nullptr, nullptr, 0, nullptr, alpha, 1, 0, 0, 0, 0, 0, 0, (int64_t)M * N};
+    EpiArgs sp{slab, N, nullptr, nullptr, 0, nullptr, alpha, 1, 0, 0, 0, 0, 0, 0, (int64_t)M * N, nullptr, 0};
     EpiArgs& ep = sp;
     epi = kEpiStoreF32;
     if (!a_km && !b_kn) {
@@ -930,7 +953,7 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
     MINIPS_HIP_CHECK(hipGetLastError());
     return;
   }
-  EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i, 0};
+  EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i, 0, perm, seg};
   if (!a_km && !b_kn) {
     MINIPS_GEMM_EPI_DISPATCH(false, false)
   } else if (!a_km && b_kn) {

@@ -20,6 +20,10 @@ enum GemmEpilogue {
   kEpiBiasGeluBf16 = 6,  // C bf16 = gelu_tanh(acc + bias)
   kEpiBiasGeluAuxBf16 = 7,  // C bf16 = gelu_tanh(u), mask(aux) bf16 = u = acc + bias (saved for bwd)
   kEpiGeluGradBf16 = 8,     // C bf16 = acc * gelu'(mask)  (mask = saved pre-activation u)
+  // C bf16 = acc, row segments permuted: output (row, col) with s = col / seg lands at
+  // C[perm[row * (N / seg) + s] * seg + col % seg] -- the embedding dgrad writes every lookup's
+  // gradient row straight into the planner's row-sorted order (seg = D, seg % 8 == 0)
+  kEpiPermRowsBf16 = 9,
 };
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
@@ -30,7 +34,8 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
                        bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
                        float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
                        int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s,
-                       float* slab = nullptr);  // split-K workspace [split_k][M][N] (atomic epilogue only)
+                       float* slab = nullptr,  // split-K workspace [split_k][M][N] (atomic epilogue only)
+                       const int* perm = nullptr, int seg = 0);  // kEpiPermRowsBf16
 
 // ------------------------------------------------------------------ sparse keys (sparse.hip)
 // Hash-based dedupe + owner bucketing of int64 keys in 3 launches (no sort):
@@ -126,9 +131,14 @@ void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide
 // zeroed_cc (nullable): a pre-zeroed 2U-int block used for counts|cursor (ws then starts at offsets).
 void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* members, int* memrow, hipStream_t s,
                    int* zeroed_cc = nullptr, bool counts_ready = false);
+// sorted_rows: dX is [B*F, D] in the CSR's member order (dX row m = the gradient of lookup
+// members[m], written there by the dgrad GEMM's kEpiPermRowsBf16 epilogue): the segment sums read
+// it as one contiguous stream instead of gathering 2*D-byte pieces of [B, F*D] rows.
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                      const int64_t* U_dev = nullptr);
+                      const int64_t* U_dev = nullptr, bool sorted_rows = false);
+// pos[members[m]] = m (n entries): where each lookup's gradient row goes in member order.
+void emb_csr_positions(const int* members, int64_t n, int* pos, hipStream_t s);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                           float* grad_rows, int row_stride, hipStream_t s);
 // Sort-based key planning of a [B, F] batch with disjoint column key ranges (plan.hip): keys of
@@ -138,7 +148,8 @@ void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const i
 // by owner), inv [B*F], the lookup CSR members/memrow [B*F] int32, counts [P+1] = {per owner, U}.
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
-                 int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s);
+                 int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
+                 int32_t* pos = nullptr);  // pos (nullable): pos[members[m]] = m (emb_csr_positions fused)
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
 void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s);
 // Embedding backward fused with the row-wise Adagrad apply (one rank, local shard): the rows of
@@ -228,6 +239,16 @@ void uniform_synth(uint64_t seed, uint64_t step, int64_t B, int F, uint64_t rows
 void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t B, int F, const int64_t* cards,
                   const int64_t* offsets, int n_dense, const float* w, float* dense, int64_t* keys, float* labels,
                   hipStream_t s);
+
+// ------------------------------------------------------------------ bf16 table rows (bf16rows.hip)
+// Row gather from a bf16 table [R, ld] (D in {16, 32, 64}) to bf16 or fp32 out [n, D].
+void gather_rows_bf16tab(const bf16_t* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D,
+                         void* out, bool out_bf16, hipStream_t s, const int64_t* n_dev = nullptr);
+// Apply fp32 gradient rows to bf16 table rows with stochastic rounding: opt 0 row-wise Adagrad
+// (fp32 state / state2, column split D1), opt 1 w += scale * g. `step` / `seed` key the rounding.
+void sparse_apply_bf16tab(int opt, bf16_t* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
+                          int64_t n, int64_t base, int D, const float* grads, float lr, float eps, float scale,
+                          uint32_t step, uint32_t seed, hipStream_t s, const int64_t* n_dev = nullptr);
 
 // (the asynchronous PS path over xGMI -- push / gather / owner apply -- is declared in onesided.h)
 

@@ -598,7 +598,9 @@ __device__ __forceinline__ void seg_flush(float* __restrict__ grad_rows, int row
 // running sum at every row change: a plain store when the row lies entirely inside the group's
 // range, fp32 atomics when the row continues across the range boundary (grad_rows is zero-filled
 // first).
-template <typename TX, int D, int kSegG, int kSegBatch>
+// SORTED: dX holds the lookups' gradient rows in member order ([total, D], row m = lookup
+// members[m]): the loads become one contiguous stream and members is read only for dwide.
+template <typename TX, int D, int kSegG, int kSegBatch, bool SORTED>
 __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__ dX, int ldx,
                                                           const float* __restrict__ dwide, int F,
                                                           const int* __restrict__ members,
@@ -627,10 +629,15 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
       for (int q = 0; q < kSegBatch; ++q) {
         const int m = m0 + q;
         u[q] = m < b ? memrow[m] : -1;
-        const int j = m < b ? members[m] : 0;
-        bb[q] = j / F;
-        const int ff = j - bb[q] * F;
-        v[q] = m < b ? ld_grad4(dX + (int64_t)bb[q] * ldx + ff * D + 4 * l) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (SORTED) {
+          v[q] = m < b ? ld_grad4(dX + (int64_t)m * D + 4 * l) : make_float4(0.f, 0.f, 0.f, 0.f);
+          bb[q] = (wide && l == 0 && m < b) ? members[m] / F : 0;
+        } else {
+          const int j = m < b ? members[m] : 0;
+          bb[q] = j / F;
+          const int ff = j - bb[q] * F;
+          v[q] = m < b ? ld_grad4(dX + (int64_t)bb[q] * ldx + ff * D + 4 * l) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         vw[q] = (wide && l == 0 && m < b) ? dwide[bb[q]] : 0.f;
       }
 #pragma unroll
@@ -706,7 +713,7 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
 template <typename TX>
 static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, int F, int D, const int* members,
                         const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                        const int64_t* U_dev) {
+                        const int64_t* U_dev, bool sorted_rows = false) {
   const int total = (int)(B * F);
   if (U_dev && row_stride % 4 == 0)
     hipLaunchKernelGGL(zero_rows_dev_kernel, grid_for((int64_t)U * (row_stride / 4), 256, 4096), 256, 0, s, grad_rows,
@@ -726,9 +733,13 @@ static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, in
   const int G = cfg == 2 ? 8 : cfg == 3 ? 32 : 16;
   const int pieces = (total + (256 / D) * G - 1) / ((256 / D) * G);
   const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
-#define MINIPS_SEG_LAUNCH2(DD, GG, BB)                                                                              \
-  hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB>), blocks, 256, 0, s, dX, ldx, dwide, F, members, memrow,   \
-                     total, grad_rows, row_stride, diag);
+#define MINIPS_SEG_LAUNCH2(DD, GG, BB)                                                                               \
+  if (sorted_rows)                                                                                                  \
+    hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB, true>), blocks, 256, 0, s, dX, ldx, dwide, F, members,   \
+                       memrow, total, grad_rows, row_stride, diag);                                                 \
+  else                                                                                                              \
+    hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB, false>), blocks, 256, 0, s, dX, ldx, dwide, F, members,  \
+                       memrow, total, grad_rows, row_stride, diag);
 #define MINIPS_SEG_LAUNCH(DD)                  \
   if (cfg == 1) {                              \
     MINIPS_SEG_LAUNCH2(DD, 16, 16)             \
@@ -1008,15 +1019,26 @@ void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int
 
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                      const int64_t* U_dev) {
+                      const int64_t* U_dev, bool sorted_rows) {
   if (B <= 0 || U <= 0) return;
   if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("emb_backward_csr: row_stride too small");
   if (bf16)
     emb_seg_sum(static_cast<const bf16_t*>(dX), ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s,
-                U_dev);
+                U_dev, sorted_rows);
   else
     emb_seg_sum(static_cast<const float*>(dX), ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s,
-                U_dev);
+                U_dev, sorted_rows);
+}
+
+__global__ void emb_csr_positions_kernel(const int* __restrict__ members, int64_t n, int* __restrict__ pos) {
+  for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < n; m += (int64_t)gridDim.x * blockDim.x)
+    pos[members[m]] = (int)m;
+}
+
+void emb_csr_positions(const int* members, int64_t n, int* pos, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(emb_csr_positions_kernel, grid_for(n, 256, 4096), 256, 0, s, members, n, pos);
+  MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,

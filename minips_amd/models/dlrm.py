@@ -2,8 +2,8 @@
 (BASELINE config 5), asynchronous SGD by default.
 
   sparse: one SparseTable row per categorical id, width D (default 64), 64-bit keys, row-wise
-          Adagrad (1 float of optimizer state per row: 10B rows x 64 fp32 = 2.56 TB of weights
-          + 40 GB of state over 8 x 288 GB -- sized per rank by `rows`).
+          Adagrad (1 float of optimizer state per row), bf16 rows by default: 10B rows x 64 bf16 =
+          1.28 TB of weights + 40 GB of state over 8 x 288 GB (fp32 rows would be 2.56 TB).
   dense:  bottom MLP 13 -> 512 -> 256 -> D, dot interaction of the D-vector with the 26
           embeddings (351 pairs + D), top MLP 416 -> 512 -> 256 -> 1, BCE. One DenseTable.
 Consistency "asp" on the collective transport runs every Clock's exchange (all-to-all-v over
@@ -20,7 +20,7 @@ import torch
 
 from .. import ops
 from ..ps.comm import Comm
-from ..ps.tables import DenseTable, SparseTable
+from .widedeep import _table_maker
 from .layers import SideStream, Linear, ParamLayout, align, ext_activation
 from .feeder import LookaheadPlans
 
@@ -44,25 +44,26 @@ class DLRMConfig:
     # applied by each owner's server thread with its own state (ps/onesided.py)
     transport: str = "collective"
     max_batch: int = 16384       # onesided: inbox slots hold max_batch * F gradient rows
+    # embedding rows in bf16 (fp32 row-wise Adagrad state, stochastically rounded applies): the
+    # default 10B x 64 table is 1.28 TB of rows + 40 GB of state = 8 x 165 GB, inside 8 x 288 GB
+    # (fp32 rows would need 2.56 TB). The one-sided transport stores fp32 rows.
+    emb_dtype: str = "bfloat16"
     seed: int = 0
     cards: list = field(default_factory=list)  # optional per-feature cardinalities (sum <= num_rows)
 
 
 class DLRM(LookaheadPlans):
-    def __init__(self, cfg: DLRMConfig, comm: Comm):
+    def __init__(self, cfg: DLRMConfig, comm: Comm, engine=None):
         self.cfg, self.comm = cfg, comm
         D, F = cfg.D, cfg.F
         self.NV = F + 1
-        if cfg.transport == "onesided":
-            from ..ps.onesided import AsyncSparseTable
-
-            self.emb = AsyncSparseTable(comm, cfg.num_rows, D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
-                                        consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
-                                        seed=cfg.seed, max_keys=cfg.max_batch * F)
-        else:
-            self.emb = SparseTable(comm, cfg.num_rows, D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
-                                   consistency=cfg.consistency, staleness=cfg.staleness, init_std=0.01,
-                                   seed=cfg.seed, p2p=cfg.p2p)
+        make = _table_maker(comm, engine)
+        onesided = cfg.transport == "onesided"
+        self.emb = make("sparse", num_rows=cfg.num_rows, width=D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
+                        model=cfg.consistency, staleness=cfg.staleness, transport=cfg.transport, init_std=0.01,
+                        seed=cfg.seed, pull_dtype=torch.bfloat16,
+                        **({"max_keys": cfg.max_batch * F} if onesided else
+                           {"p2p": cfg.p2p, "value_dtype": getattr(torch, cfg.emb_dtype)}))
         self.layout = ParamLayout()
         dims = [cfg.n_dense, *cfg.bottom, D]
         self.bottom = [Linear(self.layout, f"bot{i}", dims[i], dims[i + 1]) for i in range(len(dims) - 1)]
@@ -70,14 +71,8 @@ class DLRM(LookaheadPlans):
         tdims = [self.n_int, *cfg.top]
         self.top = [Linear(self.layout, f"top{i}", tdims[i], tdims[i + 1]) for i in range(len(tdims) - 1)]
         self.layout.add("head", (cfg.top[-1] + 8,))
-        if cfg.transport == "onesided":
-            from ..ps.onesided import AsyncDenseTable
-
-            self.dense = AsyncDenseTable(comm, self.layout.size, optimizer="adam", lr=cfg.lr_dense,
-                                         consistency=cfg.consistency, staleness=cfg.staleness)
-        else:
-            self.dense = DenseTable(comm, self.layout.size, optimizer="adam", lr=cfg.lr_dense,
-                                    consistency=cfg.consistency, staleness=cfg.staleness, p2p=False)
+        self.dense = make("dense", n_params=self.layout.size, optimizer="adam", lr=cfg.lr_dense, model=cfg.consistency,
+                          staleness=cfg.staleness, transport=cfg.transport, **({} if onesided else {"p2p": False}))
         g = torch.Generator().manual_seed(cfg.seed + 3)
         full = torch.zeros(self.layout.size)
         for l in self.bottom + self.top:

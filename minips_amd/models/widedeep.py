@@ -26,7 +26,6 @@ from .. import ops
 from ..ps.comm import Comm
 from .layers import SideStream
 from .feeder import LookaheadPlans
-from ..ps.tables import DenseTable, SparseTable
 
 
 @dataclass
@@ -82,25 +81,31 @@ def _align(n, a=8):
     return (n + a - 1) // a * a
 
 
+def _table_maker(comm, engine):
+    from ..engine import create_table
+
+    if engine is not None:
+        return lambda kind, **kw: engine.table(engine.create_table(kind, **kw))
+    ids = iter(range(1 << 20))
+    return lambda kind, **kw: create_table(comm, kind, table_id=next(ids), **kw)
+
+
 class WideDeep(LookaheadPlans):
-    def __init__(self, cfg: WideDeepConfig, comm: Comm):
+    def __init__(self, cfg: WideDeepConfig, comm: Comm, engine=None):
         self.cfg = cfg
         self.comm = comm
         dev = comm.device
         F, D = cfg.F, cfg.emb_dim
         self.num_rows = int(sum(cfg.cards))
         bases = [sum(cfg.cards[:f]) for f in range(F)]  # feature f's ids start at its offset
-        if cfg.transport == "onesided":
-            from ..ps.onesided import AsyncSparseTable
-
-            self.emb = AsyncSparseTable(comm, self.num_rows, cfg.row_width, optimizer="rowwise_adagrad",
-                                        lr=cfg.lr_sparse, consistency=cfg.consistency, staleness=cfg.staleness,
-                                        split=D, table_id=0, init_std=0.01, seed=cfg.seed,
-                                        columns=(bases, cfg.cards), max_keys=cfg.max_batch * F)
-        else:
-            self.emb = SparseTable(comm, self.num_rows, cfg.row_width, optimizer="rowwise_adagrad",
-                                   lr=cfg.lr_sparse, consistency=cfg.consistency, staleness=cfg.staleness, split=D,
-                                   table_id=0, init_std=0.01, seed=cfg.seed, columns=(bases, cfg.cards))
+        # tables through the Engine factory (minips_amd.engine.create_table): an Engine given here
+        # owns them (its create_table / checkpoint / run), otherwise they are built on ``comm``
+        make = _table_maker(comm, engine)
+        onesided = cfg.transport == "onesided"
+        self.emb = make("sparse", num_rows=self.num_rows, width=cfg.row_width, optimizer="rowwise_adagrad",
+                        lr=cfg.lr_sparse, model=cfg.consistency, staleness=cfg.staleness, transport=cfg.transport,
+                        split=D, init_std=0.01, seed=cfg.seed, columns=(bases, cfg.cards), pull_dtype=torch.bfloat16,
+                        **({"max_keys": cfg.max_batch * F} if onesided else {}))
         # wide weights start at zero (columns >= D)
         self.emb.shard[:, D:].zero_()
         # Dense layout: each Linear is stored as W_ext [n_out, k_pad] with the bias in column k_in;
@@ -124,14 +129,8 @@ class WideDeep(LookaheadPlans):
         self.layout["w4"] = (off, (cfg.hidden[-1] + 8,))  # [w4 | b4 | pad]
         off += cfg.hidden[-1] + 8
         self.n_params = off
-        if cfg.transport == "onesided":
-            from ..ps.onesided import AsyncDenseTable
-
-            self.dense = AsyncDenseTable(comm, self.n_params, optimizer="adam", lr=cfg.lr_dense,
-                                         consistency=cfg.consistency, staleness=cfg.staleness, table_id=1)
-        else:
-            self.dense = DenseTable(comm, self.n_params, optimizer="adam", lr=cfg.lr_dense,
-                                    consistency=cfg.consistency, staleness=cfg.staleness, table_id=1)
+        self.dense = make("dense", n_params=self.n_params, optimizer="adam", lr=cfg.lr_dense, model=cfg.consistency,
+                          staleness=cfg.staleness, transport=cfg.transport)
         self.dense.load_full(self._init_dense(dev))
         self._bufs = {}
         self._side = SideStream(dev, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
@@ -250,7 +249,15 @@ class WideDeep(LookaheadPlans):
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         with side.fork():
             ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
-        ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
+        # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
+        # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
+        # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
+        sorted_rows = plan.csr is not None and len(plan.csr) == 3
+        if sorted_rows:
+            ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"].view(B * F, D),
+                             perm=plan.csr[2], seg=D)
+        else:
+            ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
         # an async dense clock (its own stream) needs only the weight gradients: issued from the
         # side stream it starts as soon as the last wgrad ends, beside the embedding backward and
         # the sparse push, instead of behind them
@@ -261,7 +268,8 @@ class WideDeep(LookaheadPlans):
                 self.dense.add()
                 self.dense.clock()
         issue_next("dgrad")
-        self.emb.add_lookup_grads(plan, b["dX"], b["dwide"], F, D)  # per-lookup gradients; the table reduces
+        dXe = b["dX"].view(B * F, D) if sorted_rows else b["dX"]
+        self.emb.add_lookup_grads(plan, dXe, b["dwide"], F, D, sorted_rows=sorted_rows)  # the table reduces
         self.emb.clock()
         side.join()
         if not dense_early:

@@ -23,6 +23,7 @@ EPI_RELU_MASK_BF16 = 5
 EPI_BIAS_GELU_BF16 = 6
 EPI_BIAS_GELU_AUX_BF16 = 7  # C = gelu(u), mask(aux) = u  (pre-activation saved for backward)
 EPI_GELU_GRAD_BF16 = 8      # C = acc * gelu'(mask)
+EPI_PERM_ROWS_BF16 = 9      # C rows of `seg` columns permuted by `perm` (embedding dgrad in planner order)
 
 
 def _gelu_grad(u):
@@ -37,10 +38,12 @@ def _gpu(t: torch.Tensor) -> bool:
 
 # ----------------------------------------------------------------------------- GEMM
 def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None, mask=None, colsum=None,
-         alpha=1.0, split_k=1):
-    """C[M,N] (op)= A.B.  A is [M][K] (a_km=False) or [K][M]; B is [N][K] (b_kn=False) or [K][N]."""
+         alpha=1.0, split_k=1, perm=None, seg=0):
+    """C[M,N] (op)= A.B.  A is [M][K] (a_km=False) or [K][M]; B is [N][K] (b_kn=False) or [K][N].
+    EPI_PERM_ROWS_BF16: C is [M*N/seg, seg] and output (row, col) goes to row perm[row*N/seg + col//seg]."""
     if _gpu(A):
-        kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k))
+        kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k),
+                       perm=perm, seg=int(seg))
         return C
     a = (A[:K, :M].t() if a_km else A[:M, :K]).float()
     b = (B[:K, :N] if b_kn else B[:N, :K].t()).float()
@@ -66,6 +69,8 @@ def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None,
         C[:M, :N] = acc.to(torch.bfloat16)
     elif epi == EPI_STORE_BF16:
         C[:M, :N] = acc.to(torch.bfloat16)
+    elif epi == EPI_PERM_ROWS_BF16:
+        C.view(-1, seg)[perm[: M * (N // seg)].long()] = acc.to(torch.bfloat16).reshape(-1, seg)
     elif epi == EPI_RELU_MASK_BF16:
         out = torch.where(mask[:M, :N].float() > 0, acc, torch.zeros_like(acc)).to(torch.bfloat16)
         C[:M, :N] = out
@@ -116,10 +121,16 @@ def colsum_add(x, out):
     return out
 
 
-def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=None):
-    """dx = dy w (dy [M,N], w [N,K]) -> bf16 masked by (mask > 0) (+colsum), or fp32."""
+def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=None, perm=None, seg=0):
+    """dx = dy w (dy [M,N], w [N,K]) -> bf16 masked by (mask > 0) (+colsum), or fp32. ``perm`` /
+    ``seg``: dx's row segments of ``seg`` columns go to rows perm[...] of out [M*K/seg, seg] (the
+    embedding gradient written straight into the key planner's row-sorted order)."""
     M, N = dy.shape
     K = w.shape[1] if n_cols is None else n_cols
+    if perm is not None:
+        if out is None:
+            out = torch.empty(M * K // seg, seg, dtype=torch.bfloat16, device=dy.device)
+        return gemm(dy, w, out, M, K, N, False, True, EPI_PERM_ROWS_BF16, perm=perm, seg=seg)
     if out is None:
         out = torch.empty(M, K, dtype=torch.float32 if out_f32 else torch.bfloat16, device=dy.device)
     epi = EPI_STORE_F32 if out_f32 else (EPI_RELU_MASK_BF16 if mask is not None else EPI_STORE_BF16)
@@ -232,7 +243,7 @@ def bitmap_plan(keys: torch.Tensor, bounds: torch.Tensor, num_rows: int, route_m
 _PLAN_BITS_CAP = int(__import__("os").environ.get("MINIPS_PLAN_BITS_CAP", "0"))
 
 
-def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None, bounds=None):
+def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None, bounds=None, positions=False):
     """Key planning of a [B, F] batch whose columns hold disjoint key ranges (column f's keys in
     [col_base[f], col_base[f] + 2**col_bits[f])): per-column radix sort, no global atomics
     (plan.hip). ``col_bits``: a list of ints (or one int for every column); ``bounds`` [P+1]: the
@@ -250,7 +261,7 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
         if bits_dev is None:  # (tables pass their cached device copy: no H2D copy per plan)
             bits_dev = torch.tensor(bits, dtype=torch.int32, device=keys.device)
         return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), bits_dev, bits,
-                                           int(route_mult), int(route_n), bounds.contiguous()))
+                                           int(route_mult), int(route_n), bounds.contiguous(), bool(positions)))
     B, F = keys.shape
     uniq_l, inv_l = [], []
     base = 0
@@ -273,8 +284,13 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
     inv_u = torch.stack(inv_l, 1).reshape(-1)                  # column-major u of each lookup
     order = torch.sort(inv_u, stable=True).indices             # lookups grouped by u (ascending)
     counts = torch.bincount(owner, minlength=P).to(torch.int64)
-    return (out, perm[inv_u], counts, torch.tensor([U], dtype=torch.int64), order.to(torch.int32),
-            perm[inv_u[order]].to(torch.int32))
+    res = (out, perm[inv_u], counts, torch.tensor([U], dtype=torch.int64), order.to(torch.int32),
+           perm[inv_u[order]].to(torch.int32))
+    if positions:  # members = order: pos[order[m]] = m
+        pos = torch.empty(B * F, dtype=torch.int32)
+        pos[order] = torch.arange(B * F, dtype=torch.int32)
+        res = res + (pos,)
+    return res
 
 
 def gather_rows(table, keys, base, out, n_dev=None):
@@ -306,6 +322,46 @@ def scatter_add_rows(src, idx, acc):
         return acc
     acc.index_add_(0, idx, src.to(acc.dtype))
     return acc
+
+
+def _sr_bf16(x: torch.Tensor, gen: torch.Generator | None = None) -> torch.Tensor:
+    """Stochastic rounding of fp32 to bf16 (CPU reference of bf16rows.hip): add 16 random bits
+    below the bf16 mantissa, truncate."""
+    b = x.contiguous().view(torch.int32)
+    r = torch.randint(0, 1 << 16, b.shape, dtype=torch.int32, generator=gen)
+    finite = (b & 0x7F800000) != 0x7F800000
+    b = torch.where(finite, b + r, b)
+    return (b & -65536).view(torch.float32).to(torch.bfloat16)
+
+
+def sparse_apply_bf16(opt, table, state, keys, base, grads, lr, eps=1e-8, scale=1.0, state2=None, split=None,
+                      step=0, seed=0, n_dev=None):
+    """fp32 gradient rows into a bf16 table with stochastic rounding (opt "rowwise_adagrad" |
+    "add" (w += scale * g))."""
+    D = table.shape[1]
+    D1 = D if split is None else split
+    code = 0 if opt == "rowwise_adagrad" else 1
+    if _gpu(table):
+        kernels().sparse_apply_bf16(code, table, state, state2, int(D1), keys, int(base), grads, float(lr), float(eps),
+                                    float(scale), int(step) & 0xFFFFFFFF, int(seed) & 0xFFFFFFFF, n_dev)
+        return
+    if n_dev is not None:
+        n = int(n_dev.reshape(-1)[0])
+        keys, grads = keys[:n], grads[:n]
+    rows = keys - base
+    w = table[rows].float()
+    g = grads[:, :D].float()
+    if code == 0:
+        s1 = state[rows] + (g[:, :D1] ** 2).mean(1)
+        state[rows] = s1
+        w[:, :D1] -= lr * g[:, :D1] / (s1.sqrt() + eps).unsqueeze(1)
+        if D1 < D:
+            s2 = state2[rows] + (g[:, D1:] ** 2).mean(1)
+            state2[rows] = s2
+            w[:, D1:] -= lr * g[:, D1:] / (s2.sqrt() + eps).unsqueeze(1)
+    else:
+        w += scale * g
+    table[rows] = _sr_bf16(w, torch.Generator().manual_seed((int(seed) * 1000003 + int(step)) & 0x7FFFFFFF))
 
 
 def sparse_rowwise_adagrad(table, state, keys, base, grads, lr, eps=1e-8, state2=None, split=None, n_dev=None):
@@ -406,6 +462,15 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
         dH_colsum += g.float().sum(0)
 
 
+def emb_csr_positions(members):
+    """pos[members[m]] = m (int32): the member-order row of every lookup (the dgrad's permutation)."""
+    if _gpu(members):
+        return kernels().emb_csr_positions(members)
+    pos = torch.empty_like(members)
+    pos[members.long()] = torch.arange(members.numel(), dtype=members.dtype)
+    return pos
+
+
 def emb_build_csr(inv, F, U, zeroed=None, counts_ready=False):
     """Lookups grouped by unique row: (members, memrow) int32 [n] with memrow sorted and
     members[i] the lookup id (b*F + f) of the i-th entry. Depends on ``inv`` only, so the PS
@@ -417,15 +482,21 @@ def emb_build_csr(inv, F, U, zeroed=None, counts_ready=False):
     return order.to(torch.int32), inv[order].to(torch.int32)
 
 
-def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=None):
+def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=None, sorted_rows=False):
     """grad_rows[u, :D] = sum of dX[b, x_off + f*D : ...] over the lookups (b, f) with
     inv[b*F+f] == u; column D likewise sums dwide[b] when given. On the GPU every row of
     grad_rows is written (rows without lookups become 0); the CPU reference adds into grad_rows,
-    so callers pass a zeroed buffer."""
+    so callers pass a zeroed buffer. ``sorted_rows``: dX is [B*F, D] in the CSR's member order
+    (row m = lookup csr[0][m]; linear_dgrad(perm=csr[2]) writes it)."""
     if _gpu(dX):
-        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), U_dev,
-                                  *(csr if csr is not None else (None, None)))
+        members, memrow = (csr[0], csr[1]) if csr is not None else (None, None)
+        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), U_dev, members, memrow,
+                                  bool(sorted_rows))
         return grad_rows
+    if sorted_rows:  # back to lookup order
+        un = torch.empty_like(dX)
+        un[csr[0].long()] = dX
+        dX, x_off = un.reshape(-1, F * D), 0
     B = dX.shape[0]
     g = dX[:, x_off: x_off + F * D].float().reshape(B * F, D)
     grad_rows[:, :D].index_add_(0, inv, g)

@@ -222,10 +222,11 @@ class _AsyncTable:
         self._cpu_files = []
 
     # -- clocks -----------------------------------------------------------------------------
-    def _gate(self):
+    def _gate(self, c: int | None = None):
         """SSP: a Get at own clock c waits until every owner applied every worker's clocks
-        < c - s (ssp_model.cpp:58-85); ASP: no wait unless asp_bound is set."""
-        c = self.clock_n
+        < c - s (ssp_model.cpp:58-85); ASP: no wait unless asp_bound is set. ``c``: the reading
+        worker's own progress when several workers share this rank (minips_amd.engine)."""
+        c = self.clock_n if c is None else int(c)
         bound = self.staleness if self.consistency == "ssp" else self.asp_bound
         board, t = self.ps.board, self.t
         if bound is not None and c - bound > 0 and board.min_applied(t) < c - bound:
@@ -410,14 +411,14 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         return False
 
     # -- KV API -----------------------------------------------------------------------------
-    def get(self, keys: torch.Tensor, plan=None):
+    def get(self, keys: torch.Tensor, plan=None, clock: int | None = None):
         """Rows of the unique keys ([cap, width], unique order) and the plan; rows[plan.inv[i]]
         is the row of keys[i]. No collective: rows come straight from the owners' HBM."""
         if plan is None:
             plan = self.plan(keys)
         elif isinstance(plan, _PendingPlan):
             plan = self._finish_plan(plan)
-        self._gate()
+        self._gate(clock)
         out = torch.empty(max(plan.cap, 1), self.width, dtype=self.pull_dtype, device=self.comm.device)
         if self.cuda:
             from .._native import kernels
@@ -618,9 +619,9 @@ class AsyncDenseTable(_AsyncTable):
         self.drain()
         return torch.cat([m.to(self.comm.device) for m in self._masters])[: self.n_params].clone()
 
-    def get(self) -> torch.Tensor:
+    def get(self, clock: int | None = None) -> torch.Tensor:
         """Pull the owners' shards that changed since the last pull (SSP-gated)."""
-        self._gate()
+        self._gate(clock)
         board = self.ps.board
         for o in range(self.comm.world):
             v = board.owner_version(self.t, o)

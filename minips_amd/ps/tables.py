@@ -499,6 +499,14 @@ def _route_multiplier(num_rows: int) -> int:
 # the dedupe counts each unique key's lookups for the embedding-backward CSR (one pass less);
 # MINIPS_CSR_FUSED=0 counts in emb_build_csr instead
 _CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
+# plans carry the CSR's inverse permutation (csr[2]: each lookup's row in member order) so the
+# embedding dgrad can write its output pre-sorted and the backward streams it contiguously
+# instead of gathering 64-byte pieces (MINIPS_SORTED_EMB=0: the gather path)
+SORTED_EMB = os.environ.get("MINIPS_SORTED_EMB", "1") != "0"
+
+
+def _with_positions(csr):
+    return (*csr, ops.emb_csr_positions(csr[0])) if SORTED_EMB else csr
 
 
 @dataclass
@@ -578,14 +586,24 @@ class SparseTable:
 
         ``columns`` = (bases, cards): a caller whose [B, F] key batches hold disjoint ranges per
         column (column f's keys in [bases[f], bases[f] + cards[f]), e.g. concatenated feature
-        tables) lets one-rank planning use the atomic-free per-column sort (ops.plan_sorted)."""
-        if value_dtype not in (torch.float32, torch.float64):
+        tables) lets one-rank planning use the atomic-free per-column sort (ops.plan_sorted).
+
+        ``value_dtype`` bfloat16: rows stored in bf16 (half the HBM: the 10B x 64 DLRM table fits
+        8 x 288 GB), gradients and optimizer state in fp32, applies rounded stochastically
+        (bf16rows.hip); rows of 16 / 32 / 64 values."""
+        if value_dtype not in (torch.float32, torch.float64, torch.bfloat16):
             raise ValueError(f"value_dtype {value_dtype}")
         if value_dtype == torch.float64:
             if optimizer != "add":
                 raise ValueError("fp64 sparse tables support the reference's plain add apply only")
             pull_dtype = push_dtype = torch.float64
+        if value_dtype == torch.bfloat16 and width not in (16, 32, 64):
+            raise ValueError("bf16 sparse rows hold 16, 32 or 64 values")
         self.value_dtype = value_dtype
+        # gradients / pushes of a bf16 table are fp32 (only the stored rows are bf16)
+        self.grad_dtype = torch.float32 if value_dtype == torch.bfloat16 else value_dtype
+        self._applies = 0  # apply counter: keys the stochastic rounding of bf16 rows
+        self.seed = seed
         self.comm = comm
         self.columns = column_spec(columns, comm.device)
         # Key -> row placement. "range": row = key (the reference's contiguous range partition).
@@ -675,11 +693,11 @@ class SparseTable:
             # disjoint column key ranges: atomic-free per-column sort (ops.plan_sorted), unique keys
             # regrouped by owner, and the embedding backward's lookup CSR on the way
             pp.flat = flat
-            uniq, inv, counts, U_dev, members, memrow = ops.plan_sorted(
-                keys if keys.dtype == torch.int64 else keys.to(torch.int64), cols[0], cols[1], rmult,
-                self.num_rows if rmult else 0, bits_dev=cols[2], bounds=self.bounds)
-            pp.uniq, pp.inv, pp.counts, pp.U_dev = uniq, inv, counts, U_dev
-            pp.csr = (members, memrow) if want_csr else None
+            res = ops.plan_sorted(keys if keys.dtype == torch.int64 else keys.to(torch.int64), cols[0], cols[1], rmult,
+                                  self.num_rows if rmult else 0, bits_dev=cols[2], bounds=self.bounds,
+                                  positions=want_csr and SORTED_EMB)
+            pp.uniq, pp.inv, pp.counts, pp.U_dev = res[:4]
+            pp.csr = tuple(res[4:]) if want_csr else None  # (members, memrow[, positions])
             pp.host = pp.event = pp.cev = None
             pp.exchanged = self.comm.world == 1
             if exchange:
@@ -691,7 +709,7 @@ class SparseTable:
             pp.flat = flat
             pp.uniq, pp.inv, pp.counts, pp.U_dev = ops.bitmap_plan(flat, self.bounds, self.num_rows, rmult,
                                                                    oor=self._oor_counter())
-            pp.csr = ops.emb_build_csr(pp.inv, pp.F, n) if want_csr else None
+            pp.csr = _with_positions(ops.emb_build_csr(pp.inv, pp.F, n)) if want_csr else None
             pp.host = pp.event = pp.cev = None
             pp.exchanged = self.comm.world == 1
             if exchange:
@@ -708,7 +726,8 @@ class SparseTable:
         if want_csr:  # the CSR's counters were cleared by the dedupe's single memset, and the
             res, zeroed = res  # dedupe already counted each unique key's lookups into them
         pp.uniq, pp.inv, pp.counts, pp.U_dev = res
-        pp.csr = ops.emb_build_csr(pp.inv, pp.F, n, zeroed=zeroed, counts_ready=fused) if want_csr else None
+        pp.csr = _with_positions(ops.emb_build_csr(pp.inv, pp.F, n, zeroed=zeroed, counts_ready=fused)) \
+            if want_csr else None
         pp.host = pp.event = pp.cev = None
         pp.exchanged = self.comm.world == 1
         if exchange:
@@ -883,22 +902,24 @@ class SparseTable:
 
     def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
         """Push gradient rows (aligned with the plan's unique order; rows >= U are ignored)."""
-        assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == getattr(self, "value_dtype", torch.float32)
+        assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == getattr(self, "grad_dtype", torch.float32)
         self._pending.append((plan, grad_rows))
 
-    def add_lookup_grads(self, plan: SparsePlan, dX: torch.Tensor, dwide, F: int, D: int, x_off: int = 0):
+    def add_lookup_grads(self, plan: SparsePlan, dX: torch.Tensor, dwide, F: int, D: int, x_off: int = 0,
+                         sorted_rows: bool = False):
         """Push the gradient of every lookup of ``plan``'s batch: dX[b, x_off + f*D : +D] for
         lookup (b, f) (+ dwide[b] into column D of the row). The table reduces them per unique
         row -- the Add of the reference's worker, which sends one summed row per key. One rank
         with row-wise Adagrad fuses that reduction into the apply (no gradient-row buffer,
         ops.emb_seg_adagrad); otherwise the rows are segment-summed here and pushed by add()."""
-        if self._fused_lookup_ok(plan, dX, dwide, D, x_off):
+        if not sorted_rows and self._fused_lookup_ok(plan, dX, dwide, D, x_off):
             self._pending.append((plan, _LookupGrads(dX[:, x_off:] if x_off else dX, dwide, F, D)))
             return
         dev = self.comm.device
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width,
                                                                          dtype=torch.float32, device=dev)
-        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, grad_rows, x_off=x_off, U_dev=plan.U_dev, csr=plan.csr)
+        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, grad_rows, x_off=x_off, U_dev=plan.U_dev, csr=plan.csr,
+                            sorted_rows=sorted_rows)
         self.add(plan, grad_rows)
 
     def _fused_lookup_ok(self, plan, dX, dwide, D, x_off) -> bool:
@@ -918,7 +939,7 @@ class SparseTable:
     def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
         """Reference-style Add(keys, vals) (duplicates are summed)."""
         plan = self.plan(keys)
-        vdt = getattr(self, "value_dtype", torch.float32)
+        vdt = getattr(self, "grad_dtype", torch.float32)
         g = torch.zeros(max(plan.cap, 1), self.width, dtype=vdt, device=self.comm.device)
         ops.scatter_add_rows(vals.reshape(keys.numel(), self.width).to(vdt).contiguous(), plan.inv, g)
         self.add(plan, g)
@@ -956,13 +977,22 @@ class SparseTable:
             if M == 0:
                 return
             n = plan.extra.get("own_U", M)
-            g = torch.zeros(n, self.width, dtype=getattr(self, "value_dtype", torch.float32), device=dev)
+            g = torch.zeros(n, self.width, dtype=getattr(self, "grad_dtype", torch.float32), device=dev)
             ops.scatter_add_rows(recv, plan.own_inv, g)
             keys, n_dev = plan.own_uniq, (None if "own_U" in plan.extra else plan.own_U_dev)
         keys, base = self._owner_rows(keys[:n], plan)
         self._apply_rows(keys, base, g[:n], n_dev)
 
     def _apply_rows(self, keys, base, g, n_dev=None):
+        if getattr(self, "value_dtype", None) == torch.bfloat16:
+            self._applies += 1
+            if self.optimizer not in ("rowwise_adagrad", "sgd", "add"):
+                raise ValueError(self.optimizer)
+            opt = "rowwise_adagrad" if self.optimizer == "rowwise_adagrad" else "add"
+            scale = -self.lr if self.optimizer == "sgd" else 1.0
+            ops.sparse_apply_bf16(opt, self.shard, self.state, keys, base, g.contiguous(), self.lr, self.eps, scale,
+                                  state2=self.state2, split=self.split, step=self._applies, seed=self.seed, n_dev=n_dev)
+            return
         if self.optimizer == "rowwise_adagrad":
             ops.sparse_rowwise_adagrad(self.shard, self.state, keys, base, g, self.lr, self.eps,
                                        state2=self.state2, split=self.split, n_dev=n_dev)

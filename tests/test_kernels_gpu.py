@@ -472,6 +472,9 @@ def test_plan_sorted_matches_reference(dev, B, cards, P):
     torch.testing.assert_close(got[4], ref[4])
     torch.testing.assert_close(got[5], ref[5])
     assert bool((got[1][got[4].long()] == got[5].long()).all())      # members belong to their row
+    pos = ops.plan_sorted(keys.to(dev), torch.tensor(bases, device=dev), bits, mult, R, bounds=bounds.to(dev),
+                          positions=True)[6].cpu()
+    assert torch.equal(pos[got[4].long()], torch.arange(keys.numel(), dtype=torch.int32))  # inverse of members
 
 
 @pytest.mark.parametrize("num_rows,n,P,route", [(16_609_143, 200_000, 1, True), (1000, 5000, 3, False),
@@ -530,3 +533,73 @@ def test_bitmap_plan_counts_out_of_range_keys(dev):
     t.get(torch.tensor([1, 2, 500], device=dev))  # bitmap planner (small key space)
     with pytest.raises(ValueError, match="outside"):
         t.drain()
+
+
+def test_dgrad_permuted_rows_and_sorted_emb_backward(dev):
+    """The embedding dgrad written in the planner's member order (EPI_PERM_ROWS_BF16) holds exactly
+    the rows of the plain dgrad, and the embedding backward over those sorted rows equals the
+    gather path (and the fp32 CPU reference within bf16 rounding)."""
+    B, F, D, H = 1024, 26, 32, 256
+    g = torch.Generator().manual_seed(5)
+    inv = torch.randint(0, 900, (B * F,), generator=g)
+    inv[::7] = 3  # a hot row
+    U = int(inv.max()) + 1
+    dH = (torch.randn(B, H, generator=g) * 0.1).to(torch.bfloat16).to(dev)
+    Wt = (torch.randn(H, F * D + 8, generator=g) * 0.1).to(torch.bfloat16).to(dev)
+    dwide = torch.randn(B, generator=g).to(dev)
+    inv_d = inv.to(dev)
+    members, memrow = ops.emb_build_csr(inv_d, F, U)
+    pos = ops.emb_csr_positions(members)
+    assert torch.equal(pos.cpu()[members.cpu().long()], torch.arange(B * F, dtype=torch.int32))
+    dX = ops.linear_dgrad(dH, Wt, n_cols=F * D)
+    dXs = ops.linear_dgrad(dH, Wt, n_cols=F * D, perm=pos, seg=D)
+    assert dXs.shape == (B * F, D)
+    assert torch.equal(dXs[pos.long()], dX.reshape(B * F, D))
+    W = D + 4
+    ga = torch.zeros(U, W, device=dev)
+    gb = torch.zeros(U, W, device=dev)
+    ops.wd_emb_backward(dX, dwide, inv_d, F, D, ga, csr=(members, memrow))
+    ops.wd_emb_backward(dXs, dwide, inv_d, F, D, gb, csr=(members, memrow, pos), sorted_rows=True)
+    torch.testing.assert_close(gb, ga, rtol=1e-5, atol=1e-5)
+    ref = torch.zeros(U, W)
+    ops.wd_emb_backward(dX.cpu(), dwide.cpu(), inv, F, D, ref)
+    torch.testing.assert_close(gb.cpu()[:, : D + 1], ref[:, : D + 1], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("D,split", [(64, None), (32, 24), (16, None)])
+def test_bf16_rows_apply_matches_fp32_within_rounding(dev, D, split):
+    """bf16 table rows (bf16rows.hip): the gather equals the rows, and one row-wise Adagrad apply
+    with stochastic rounding lands within one bf16 ulp of the fp32 reference apply."""
+    R, n = 5000, 1200
+    g = torch.Generator().manual_seed(D)
+    rows = (torch.randn(R, D, generator=g) * 0.05).to(torch.bfloat16)
+    keys = torch.randperm(R, generator=g)[:n] + 100
+    grads = torch.randn(n, D, generator=g)
+    t = rows.to(dev)
+    st = torch.zeros(R, device=dev)
+    st2 = torch.zeros(R, device=dev) if split else None
+    out = torch.empty(n, D, dtype=torch.float32, device=dev)
+    ops.gather_rows(t, keys.to(dev), 100, out)
+    assert torch.equal(out.cpu(), rows[keys - 100].float())
+    ops.sparse_apply_bf16("rowwise_adagrad", t, st, keys.to(dev), 100, grads.to(dev), 0.05, 1e-8, state2=st2,
+                          split=split, step=1, seed=3)
+    ref = rows.float().clone()
+    rs = torch.zeros(R)
+    rs2 = torch.zeros(R) if split else None
+    ops.sparse_rowwise_adagrad(ref, rs, keys, 100, grads, 0.05, 1e-8, state2=rs2, split=split)
+    torch.testing.assert_close(st.cpu(), rs)
+    ulp = ref.abs().clamp_min(1e-30) * 2.0 ** -7  # one bf16 ulp of the fp32 result (upper bound)
+    assert bool(((t.cpu().float() - ref).abs() <= ulp + 1e-12).all())
+
+
+def test_bf16_rows_stochastic_rounding_is_unbiased(dev):
+    """Updates far below half a bf16 ulp: round-to-nearest would never move the weights, the
+    stochastic rounding of the bf16 apply moves them by the right amount on average."""
+    R, D, steps = 4096, 16, 200
+    t = torch.ones(R, D, dtype=torch.bfloat16, device=dev)
+    keys = torch.arange(R, device=dev)
+    g = torch.full((R, D), 1e-4, device=dev)  # bf16 ulp at 1.0 is 2^-7 = 7.8e-3
+    for s in range(steps):
+        ops.sparse_apply_bf16("add", t, None, keys, 0, g, 0.0, scale=1.0, step=s, seed=11)
+    mean = float(t.float().mean())
+    assert abs(mean - (1.0 + steps * 1e-4)) < 2e-3, mean  # RNE would stay at exactly 1.0

@@ -135,9 +135,11 @@ def _replay_run(rank, world, dev=torch.device("cpu")):
     sp.drain()
     dn.drain()
     comm.barrier()
-    out = dict(log=sp.ps.apply_log(), shard=sp.shard.cpu().clone(), state=sp.state.cpu().clone(),
-               state2=sp.state2.cpu().clone(), base=sp.base, master=dn.master.cpu().clone(), m=dn.m.cpu().clone(),
-               v=dn.v.cpu().clone(), dbase=dn.base, dshard=dn.shard)
+    # numpy (pickled by value): torch tensors would travel as shared-memory handles that die with
+    # this process before the parent unpickles them
+    out = dict(log=sp.ps.apply_log(), shard=sp.shard.cpu().numpy().copy(), state=sp.state.cpu().numpy().copy(),
+               state2=sp.state2.cpu().numpy().copy(), base=sp.base, master=dn.master.cpu().numpy().copy(),
+               m=dn.m.cpu().numpy().copy(), v=dn.v.cpu().numpy().copy(), dbase=dn.base, dshard=dn.shard)
     comm.barrier()
     return out
 
@@ -146,6 +148,7 @@ def _replay_check(out, world=2):
     from minips_amd import ops
 
     for o, res in out.items():
+        res = {k: torch.from_numpy(v) if hasattr(v, "dtype") and not isinstance(v, int) else v for k, v in res.items()}
         log = res["log"]
         assert len(log) == 2 * world * STEPS, len(log)  # every clock of every requester, both tables
         lo, hi = res["base"], res["base"] + res["shard"].shape[0]

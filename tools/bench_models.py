@@ -7,7 +7,7 @@ barrier + synchronize, max over ranks, whole-job value, one JSON line on rank 0)
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_models.py --model dlrm
 
 models: mlp (config 2, samples/s), gpt2 (config 4, tokens/s), dlrm (config 5, samples/s),
-        dlrm-10b (config 5 at its per-GPU shard: 1.25B rows x 16 per GPU, ASP), lr (config 1 on GPUs,
+        dlrm-10b (config 5 at its per-GPU shard: 1.25B rows x 64 bf16 per GPU, ASP), lr (config 1 on GPUs,
         samples/s), kmeans (samples/s), widedeep-ssp (config 3).
 """
 from __future__ import annotations
@@ -61,7 +61,7 @@ def build(args, comm):
             # BASELINE config 5: a 10B-row table over 8 GPUs = 1.25B rows (x 16 fp32 + row-wise
             # Adagrad state = 85 GB) per GPU; weak scaling keeps the per-GPU shard fixed
             rows = args.rows_per_gpu * comm.world
-            cfg = DLRMConfig(num_rows=rows, D=16, consistency=args.consistency if args.consistency != "bsp"
+            cfg = DLRMConfig(num_rows=rows, D=args.dim, consistency=args.consistency if args.consistency != "bsp"
                              else "asp", staleness=args.staleness, transport=args.transport, max_batch=B)
         else:
             cfg = DLRMConfig(num_rows=args.rows, consistency=args.consistency, staleness=args.staleness,
@@ -81,7 +81,8 @@ def build(args, comm):
             cur, state["cur"] = state["cur"], nxt
             return m.train_step(*cur, next_keys=nxt[1])
 
-        return m, step, B, "samples/s", dict(model=f"DLRM {cfg.num_rows} rows x {cfg.D} (26 sparse + 13 dense), "
+        return m, step, B, "samples/s", dict(model=f"DLRM {cfg.num_rows} rows x {cfg.D} {cfg.emb_dtype} "
+                                                   f"(26 sparse + 13 dense), "
                                                    f"{cfg.consistency}, {cfg.transport}", seq_len=None,
                                              rows_per_gpu=cfg.num_rows // comm.world, consistency=cfg.consistency)
     if args.model == "lr":
@@ -134,6 +135,7 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--rows", type=int, default=100_000_000, help="DLRM embedding rows (whole table)")
     ap.add_argument("--rows-per-gpu", type=int, default=1_250_000_000, help="dlrm-10b: rows per GPU shard")
+    ap.add_argument("--dim", type=int, default=64, help="dlrm-10b: embedding width (bf16 rows: 64 fits 288 GB)")
     ap.add_argument("--consistency", default="bsp")
     ap.add_argument("--graph", type=lambda v: v.lower() in ("1", "true", "yes"), default=None,
                     help="mlp: capture the step in a HIP graph (one rank, BSP; off by default: at batch 8192 the "
