@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--test-cards", default="", help=argparse.SUPPRESS)
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed run: host issue time per step and a cProfile of N more steps (stderr)")
+    ap.add_argument("--sync-audit", type=int, default=0,
+                    help="after the timed run: N more steps under minips_amd.utils.syncaudit (host issue time, "
+                         "host syncs per step and their call sites; one '[sync-audit] {json}' line per rank, stderr)")
     args = ap.parse_args()
 
     from minips_amd.data.synthetic import CriteoSynth
@@ -147,6 +150,20 @@ def main():
             "loss_last": round(loss_last, 5),
         }
         print(json.dumps(out), flush=True)
+    if args.sync_audit > 0:  # after the timed region: host issue time + host waits per step
+        from minips_amd.utils.syncaudit import SyncAudit
+
+        t1 = time.perf_counter()
+        with SyncAudit() as audit:  # the steps only: the drain + synchronize below are not step syncs
+            for _ in range(args.sync_audit):
+                audit.step_begin()
+                step()
+                audit.step_end()
+        model.drain()
+        sync()
+        wall = time.perf_counter() - t1
+        rep = dict(rank=comm.rank, world=n, backend=comm.backend, **audit.report(wall))
+        print("[sync-audit] " + json.dumps(rep), file=sys.stderr, flush=True)
     if args.profile_steps > 0:  # after the timed region: host issue time per step + host hot spots
         import cProfile
         import pstats

@@ -148,6 +148,8 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
         const int64_t off = out_offset<EPI>(ep, N, row, col);
         if (EPI == kEpiStoreF32) {
           ((float*)ep.C)[off] = v;
+        } else if (EPI == kEpiAccumF32) {
+          ((float*)ep.C)[off] += v;
         } else if (EPI == kEpiAtomicF32) {
           atomicAdd(((float*)ep.C) + off, v);
         } else if (EPI == kEpiBiasReluBf16) {
@@ -224,7 +226,7 @@ __device__ __forceinline__ float epi_apply(float v, float bias, float m, bf16_t*
 template <int EPI, int MR>
 __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiArgs& ep, int M, int N, int mb, int nb,
                                              int lane, float* __restrict__ scr) {
-  constexpr bool F32OUT = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
+  constexpr bool F32OUT = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
   constexpr bool HAS_BIAS = EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 ||
                             EPI == kEpiBiasGeluAuxBf16;
   constexpr bool READ_MASK = EPI == kEpiReluMaskBf16 || EPI == kEpiGeluGradBf16;
@@ -274,14 +276,21 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
         const int rr = ro * 4 + (lane >> 4), c4 = (lane & 15) * 4;
         const int row = row0 + rr, col = nb + c4;
         if (row >= M) continue;
-        const float4 v = *reinterpret_cast<const float4*>(scr + rr * kScrPitch + c4);
+        float4 v = *reinterpret_cast<const float4*>(scr + rr * kScrPitch + c4);
         float* dst = ((float*)ep.C) + (int64_t)row * ep.ldc + col;
         if (c_vec && col + 4 <= N) {
+          if (EPI == kEpiAccumF32) {
+            const float4 o = *reinterpret_cast<const float4*>(dst);
+            v.x += o.x;
+            v.y += o.y;
+            v.z += o.z;
+            v.w += o.w;
+          }
           *reinterpret_cast<float4*>(dst) = v;
         } else {
           const float vv[4] = {v.x, v.y, v.z, v.w};
           for (int e = 0; e < 4; ++e)
-            if (col + e < N) dst[e] = vv[e];
+            if (col + e < N) dst[e] = EPI == kEpiAccumF32 ? dst[e] + vv[e] : vv[e];
         }
       }
     } else {
@@ -402,7 +411,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
     const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
-    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const int ke = min(K, kb + k_chunk);
@@ -563,7 +572,7 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
     const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
-    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
@@ -662,7 +671,7 @@ __global__ __launch_bounds__(512) void gemm_v3_kernel(const bf16_t* __restrict__
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
     const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
-    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
@@ -876,6 +885,7 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
     MINIPS_EPI_CASE(AKM, BKN, kEpiBiasGeluAuxBf16)                               \
     MINIPS_EPI_CASE(AKM, BKN, kEpiGeluGradBf16)                                  \
     MINIPS_EPI_CASE(AKM, BKN, kEpiPermRowsBf16)                                  \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiAccumF32)                                      \
     default:                                                                     \
       throw std::runtime_error("gemm: unknown epilogue " + std::to_string(epi)); \
   }
@@ -954,6 +964,13 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
     return;
   }
   EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i, 0, perm, seg};
+  // an accumulating GEMM with one K slice has one writer per output element: read-add-write
+  // instead of memory-side fp32 atomics (MINIPS_GEMM_ACCUM=0 keeps the atomics)
+  static const bool accum_ok = [] {
+    const char* e = std::getenv("MINIPS_GEMM_ACCUM");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (epi == kEpiAtomicF32 && split_k == 1 && accum_ok) epi = kEpiAccumF32;
   if (!a_km && !b_kn) {
     MINIPS_GEMM_EPI_DISPATCH(false, false)
   } else if (!a_km && b_kn) {

@@ -24,6 +24,10 @@ enum GemmEpilogue {
   // C[perm[row * (N / seg) + s] * seg + col % seg] -- the embedding dgrad writes every lookup's
   // gradient row straight into the planner's row-sorted order (seg = D, seg % 8 == 0)
   kEpiPermRowsBf16 = 9,
+  // C fp32 += alpha*acc without atomics: chosen by the launcher for an accumulating GEMM that is
+  // not split over K (every output element has exactly one writer), e.g. GPT-2's LM-head weight
+  // gradient (38.6M fp32 outputs: memory-side atomics cost it 1.75 ms/step)
+  kEpiAccumF32 = 10,
 };
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,

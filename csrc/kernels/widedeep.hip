@@ -592,22 +592,56 @@ __device__ __forceinline__ void seg_flush(float* __restrict__ grad_rows, int row
   }
 }
 
-// Piecewise segmented sum over the row-sorted lookups. A group of D/4 lanes reads one lookup's
-// D values as 4-wide vectors (64/(D/4) lookups per wave-instruction); each group owns kSegG
-// consecutive lookups, loaded kSegBatch at a time (independent loads in flight), and flushes its
-// running sum at every row change: a plain store when the row lies entirely inside the group's
-// range, fp32 atomics when the row continues across the range boundary (grad_rows is zero-filled
-// first).
+// Piecewise segmented sum over the row-sorted lookups. A group of D/VW lanes reads one lookup's
+// D values as VW-wide vectors (VW = 8: one 16-byte load of 8 bf16 per lane, 64/(D/8) lookups per
+// wave-instruction; VW = 4: 8-byte loads); each group owns kSegG consecutive lookups, loaded
+// kSegBatch at a time (independent loads in flight), and flushes its running sum at every row
+// change: a plain store when the row lies entirely inside the group's range, fp32 atomics when
+// the row continues across the range boundary (grad_rows is zero-filled first).
 // SORTED: dX holds the lookups' gradient rows in member order ([total, D], row m = lookup
 // members[m]): the loads become one contiguous stream and members is read only for dwide.
-template <typename TX, int D, int kSegG, int kSegBatch, bool SORTED>
+template <int VW>
+__device__ __forceinline__ void ld_gradv(const bf16_t* p, float (&v)[VW]) {
+  if constexpr (VW == 8) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[2 * e] = __uint_as_float(w[e] << 16);
+      v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+    }
+  } else {
+    const float4 f = ld_grad4(p);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  }
+}
+template <int VW>
+__device__ __forceinline__ void ld_gradv(const float* p, float (&v)[VW]) {
+#pragma unroll
+  for (int h = 0; h < VW / 4; ++h) {
+    const float4 f = *reinterpret_cast<const float4*>(p + 4 * h);
+    v[4 * h] = f.x; v[4 * h + 1] = f.y; v[4 * h + 2] = f.z; v[4 * h + 3] = f.w;
+  }
+}
+
+template <int D, int VW>
+__device__ __forceinline__ void seg_flushv(float* __restrict__ grad_rows, int row_stride, int row,
+                                           const float (&acc)[VW], float accw, bool wide, int prev_row, int next_row,
+                                           int l) {
+#pragma unroll
+  for (int h = 0; h < VW / 4; ++h)  // the wide weight goes out with chunk 0 only
+    seg_flush<D>(grad_rows, row_stride, row, make_float4(acc[4 * h], acc[4 * h + 1], acc[4 * h + 2], acc[4 * h + 3]),
+                 accw, wide && h == 0, prev_row, next_row, (VW / 4) * l + h);
+}
+
+template <typename TX, int D, int kSegG, int kSegBatch, bool SORTED, int VW>
 __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__ dX, int ldx,
                                                           const float* __restrict__ dwide, int F,
                                                           const int* __restrict__ members,
                                                           const int* __restrict__ memrow, int total,
                                                           float* __restrict__ grad_rows, int row_stride,
                                                           int diag) {
-  constexpr int L = D / 4, PER = 64 / L;
+  constexpr int L = D / VW, PER = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
   const bool wide = dwide != nullptr;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -619,40 +653,43 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
     const int prev_row = diag ? -2 : ((a > 0 && a <= total) ? memrow[a - 1] : -1);
     const int next_row = diag ? -2 : (b < total ? memrow[b] : -1);
     int cur = -1;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float acc[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) acc[e] = 0.f;
     float accw = 0.f;
     for (int m0 = a; m0 < b; m0 += kSegBatch) {
       int u[kSegBatch], bb[kSegBatch];
-      float4 v[kSegBatch];
+      float v[kSegBatch][VW];
       float vw[kSegBatch];
 #pragma unroll
       for (int q = 0; q < kSegBatch; ++q) {
         const int m = m0 + q;
         u[q] = m < b ? memrow[m] : -1;
+        const TX* src;
         if (SORTED) {
-          v[q] = m < b ? ld_grad4(dX + (int64_t)m * D + 4 * l) : make_float4(0.f, 0.f, 0.f, 0.f);
+          src = dX + (int64_t)(m < b ? m : a) * D + VW * l;
           bb[q] = (wide && l == 0 && m < b) ? members[m] / F : 0;
         } else {
           const int j = m < b ? members[m] : 0;
           bb[q] = j / F;
           const int ff = j - bb[q] * F;
-          v[q] = m < b ? ld_grad4(dX + (int64_t)bb[q] * ldx + ff * D + 4 * l) : make_float4(0.f, 0.f, 0.f, 0.f);
+          src = dX + (int64_t)bb[q] * ldx + ff * D + VW * l;
         }
+        ld_gradv<VW>(src, v[q]);
         vw[q] = (wide && l == 0 && m < b) ? dwide[bb[q]] : 0.f;
       }
 #pragma unroll
       for (int q = 0; q < kSegBatch; ++q) {
         if (u[q] < 0) break;
         if (u[q] != cur) {
-          if (cur >= 0) seg_flush<D>(grad_rows, row_stride, cur, acc, accw, wide, prev_row, next_row, l);
+          if (cur >= 0) seg_flushv<D, VW>(grad_rows, row_stride, cur, acc, accw, wide, prev_row, next_row, l);
           cur = u[q];
-          acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int e = 0; e < VW; ++e) acc[e] = 0.f;
           accw = 0.f;
         }
-        acc.x += v[q].x;
-        acc.y += v[q].y;
-        acc.z += v[q].z;
-        acc.w += v[q].w;
+#pragma unroll
+        for (int e = 0; e < VW; ++e) acc[e] += v[q][e];
         accw += vw[q];
       }
     }
@@ -663,16 +700,14 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
     if (!diag && __all(cur == c0) && c0 >= 0) {
 #pragma unroll
       for (int o = L; o < 64; o <<= 1) {
-        acc.x += __shfl_xor(acc.x, o, 64);
-        acc.y += __shfl_xor(acc.y, o, 64);
-        acc.z += __shfl_xor(acc.z, o, 64);
-        acc.w += __shfl_xor(acc.w, o, 64);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
         accw += __shfl_xor(accw, o, 64);
       }
       const int p0 = __shfl(prev_row, 0, 64), n1 = __shfl(next_row, 63, 64);
-      if (sub == 0) seg_flush<D>(grad_rows, row_stride, c0, acc, accw, wide, p0, n1, l);
+      if (sub == 0) seg_flushv<D, VW>(grad_rows, row_stride, c0, acc, accw, wide, p0, n1, l);
     } else if (cur >= 0) {
-      seg_flush<D>(grad_rows, row_stride, cur, acc, accw, wide, prev_row, next_row, l);
+      seg_flushv<D, VW>(grad_rows, row_stride, cur, acc, accw, wide, prev_row, next_row, l);
     }
   }
 }
@@ -731,15 +766,33 @@ static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, in
   // cfg 0: G=16 lookups per group loaded 8 at a time; 1: G=16 in one batch of 16; 2: G=8 x 8;
   // 3: G=32 x 16
   const int G = cfg == 2 ? 8 : cfg == 3 ? 32 : 16;
-  const int pieces = (total + (256 / D) * G - 1) / ((256 / D) * G);
+  // MINIPS_SEG_VEC=8: 16-byte gradient loads (8 values per lane; 16-byte aligned rows only).
+  // Measured slower in the W&D step (0.436 vs 0.417 ms, profiles/r3/ab_seg_vec.txt): fewer lanes
+  // per row halves the waves in flight on the latency-bound segment walk, so 8-byte loads stay
+  // the default.
+  static const int vec_env = [] {
+    const char* e = std::getenv("MINIPS_SEG_VEC");
+    return e ? std::atoi(e) : 4;
+  }();
+  const bool vec8 = vec_env == 8 && (sorted_rows ? true : (ldx % 8 == 0)) &&
+                    reinterpret_cast<uintptr_t>(dX) % 16 == 0;
+  const int VWn = vec8 ? 8 : 4;
+  const int per_wave = (64 / (D / VWn)) * G;  // lookups per wave piece
+  const int pieces = (total + per_wave - 1) / per_wave;
   const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
-#define MINIPS_SEG_LAUNCH2(DD, GG, BB)                                                                               \
+#define MINIPS_SEG_LAUNCH3(DD, GG, BB, VV)                                                                           \
   if (sorted_rows)                                                                                                  \
-    hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB, true>), blocks, 256, 0, s, dX, ldx, dwide, F, members,   \
-                       memrow, total, grad_rows, row_stride, diag);                                                 \
+    hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB, true, VV>), blocks, 256, 0, s, dX, ldx, dwide, F,        \
+                       members, memrow, total, grad_rows, row_stride, diag);                                        \
   else                                                                                                              \
-    hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB, false>), blocks, 256, 0, s, dX, ldx, dwide, F, members,  \
-                       memrow, total, grad_rows, row_stride, diag);
+    hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB, false, VV>), blocks, 256, 0, s, dX, ldx, dwide, F,       \
+                       members, memrow, total, grad_rows, row_stride, diag);
+#define MINIPS_SEG_LAUNCH2(DD, GG, BB)       \
+  if (vec8) {                               \
+    MINIPS_SEG_LAUNCH3(DD, GG, BB, 8)       \
+  } else {                                  \
+    MINIPS_SEG_LAUNCH3(DD, GG, BB, 4)       \
+  }
 #define MINIPS_SEG_LAUNCH(DD)                  \
   if (cfg == 1) {                              \
     MINIPS_SEG_LAUNCH2(DD, 16, 16)             \
@@ -763,6 +816,7 @@ static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, in
     default:
       throw std::runtime_error("emb_backward_seg: D must be 16, 32 or 64");
   }
+#undef MINIPS_SEG_LAUNCH3
 #undef MINIPS_SEG_LAUNCH2
 #undef MINIPS_SEG_LAUNCH
   MINIPS_HIP_CHECK(hipGetLastError());

@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import math
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 
@@ -48,6 +48,10 @@ class GPT2Config:
     # multi-rank: per-layer gradient buckets (~28 MB each at GPT-2 small) reduced + applied +
     # re-gathered as soon as the layer's backward finished (DenseTable bucket_ready)
     bucketed: bool = True
+    # one rank: the clock on the table's side stream too, each layer's bucket applied (Adam) as
+    # soon as its backward finished, overlapping the rest of the backward (DenseTable overlap_w1;
+    # MINIPS_GPT2_OVERLAP_W1=0: one Adam over the whole table after the backward)
+    overlap_w1: bool = field(default_factory=lambda: os.environ.get("MINIPS_GPT2_OVERLAP_W1", "1") == "1")
 
     @property
     def vocab_pad(self):
@@ -79,7 +83,7 @@ class GPT2:
         starts = [L.entries[f"h{i}.ln1_g"][0] for i in range(cfg.n_layer)] if cfg.bucketed else None
         self.table = DenseTable(comm, L.size, optimizer="adam", lr=cfg.lr, consistency=cfg.consistency,
                                 staleness=cfg.staleness, weight_decay=cfg.weight_decay, betas=(0.9, 0.95),
-                                buckets=starts)
+                                buckets=starts, overlap_w1=cfg.overlap_w1)
         self._layer_bucket = [self.table.bucket_for_layer(x) for x in starts] if starts else None
         g = torch.Generator().manual_seed(cfg.seed)
         full = torch.zeros(L.size)

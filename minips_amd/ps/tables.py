@@ -59,7 +59,7 @@ class _Pipeline:
     """
 
     def __init__(self, comm: Comm, consistency: str, staleness: int, overlap: bool | None = None,
-                 kind: str = ""):
+                 kind: str = "", w1: bool = False):
         self.consistency = consistency
         # ASP on the collective path is pipelining, not a staleness model: its clocks are
         # collectives every rank joins, so the Get gate only bounds how many clocks may be in
@@ -71,8 +71,8 @@ class _Pipeline:
         if consistency == "bsp":
             # one rank has no communication to hide; MINIPS_OVERLAP_W1 lists the table kinds that
             # still run their clock on a side stream there (the apply overlapping other compute)
-            w1 = os.environ.get("MINIPS_OVERLAP_W1", "").split(",")
-            self.async_ = comm.device.type == "cuda" and overlap and (comm.world > 1 or kind in w1)
+            w1_kinds = os.environ.get("MINIPS_OVERLAP_W1", "").split(",")
+            self.async_ = comm.device.type == "cuda" and overlap and (comm.world > 1 or w1 or kind in w1_kinds)
         else:
             self.async_ = comm.device.type == "cuda" and self.staleness > 0
         self.stream = torch.cuda.Stream(device=comm.device) if self.async_ else None
@@ -138,7 +138,7 @@ class DenseTable:
     def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
                  pull_dtype=torch.bfloat16, consistency: str = "bsp", staleness: int = 0, table_id: int = 0,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, p2p: bool = False,
-                 value_dtype=torch.float32, buckets=None):
+                 value_dtype=torch.float32, buckets=None, overlap_w1: bool = False):
         """``value_dtype`` float64 gives the reference's ``double`` tables (KVClientTable<double>
         with VectorStorage::SubAdd, server/vector_storage.hpp:28-38): optimizer "add" only, pulled
         in fp64, so BSP sums are exact for exactly representable deltas.
@@ -150,7 +150,12 @@ class DenseTable:
         layers overlaps the backward of the early ones (SURVEY §5.8 bucket sizing: per-layer
         buckets of 8-64 MB). Ownership is then bucket-major: rank r owns the r-th slice of every
         bucket (the shard buffers are those slices in bucket order); checkpoints keep the
-        canonical contiguous layout (shard_state / finish_restore convert)."""
+        canonical contiguous layout (shard_state / finish_restore convert).
+
+        ``overlap_w1``: at world 1 too, run the clock on the table's side stream and, with
+        ``buckets``, apply each bucket as soon as the backward finished its layer (one rank has
+        no communication to hide, but the per-bucket optimizer then overlaps the remaining
+        backward instead of running after it)."""
         if value_dtype not in (torch.float32, torch.float64):
             raise ValueError(f"value_dtype {value_dtype}")
         if value_dtype == torch.float64:
@@ -180,14 +185,14 @@ class DenseTable:
         # the Adam step also lives on the device (advanced inside the clock) so that a clock
         # captured in a HIP graph replays with the right bias correction
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.pipe = _Pipeline(comm, consistency, staleness, kind="dense")
+        self.pipe = _Pipeline(comm, consistency, staleness, kind="dense", w1=overlap_w1)
         self._pending = False
         # async clocks: a ring of staleness+2 gradient buffers, so the side stream reduces clock
         # t's gradients while the compute stream already writes clock t+1's.
         self._ring = [self.grad] + [torch.zeros_like(self.grad) for _ in range(self.pipe.staleness + 1)] \
             if self.pipe.async_ else [self.grad]
         self.buckets = None
-        if buckets is not None and comm.world > 1:
+        if buckets is not None and (comm.world > 1 or self.pipe.async_):
             self._init_buckets(buckets)
 
     # -- bucketed clocks ----------------------------------------------------------------------
@@ -247,18 +252,25 @@ class DenseTable:
         comm = self.comm
         sd = self._step_dev_for_clock(first=not self._issued)
         self._issued.add(k)
-        comm.reduce_scatter(self.grad_shard[off: off + sz], grad[lo:hi])
         sl = slice(off, off + sz)
+        local = comm.world == 1 and not comm.force  # one rank owns the whole bucket: no copy
+        if local:
+            gs = grad[lo:hi]
+        else:
+            comm.reduce_scatter(self.grad_shard[off: off + sz], grad[lo:hi])
+            gs = self.grad_shard[sl]
         out = self.params[g0: g0 + sz] if self.pull_dtype == torch.bfloat16 else None
+        zeroed = False
         if self.optimizer == "adam":
-            ops.adam_apply(self.master[sl], self.m[sl], self.v[sl], self.grad_shard[sl], self.lr, self.betas[0],
-                           self.betas[1], self.eps, self.weight_decay, step, 1.0, out, step_dev=sd)
+            ops.adam_apply(self.master[sl], self.m[sl], self.v[sl], gs, self.lr, self.betas[0], self.betas[1],
+                           self.eps, self.weight_decay, step, 1.0, out, step_dev=sd, zero_g=local)
+            zeroed = local  # the kernel cleared the gradient it read
         elif self.optimizer == "adagrad":
-            ops.adagrad_apply(self.master[sl], self.m[sl], self.grad_shard[sl], self.lr, self.eps, 1.0, out)
+            ops.adagrad_apply(self.master[sl], self.m[sl], gs, self.lr, self.eps, 1.0, out)
         elif self.optimizer == "sgd":
-            ops.sgd_apply(self.master[sl], self.grad_shard[sl], self.lr, 1.0, out)
+            ops.sgd_apply(self.master[sl], gs, self.lr, 1.0, out)
         elif self.optimizer == "add":
-            self.master[sl].add_(self.grad_shard[sl])
+            self.master[sl].add_(gs)
             if out is not None:
                 ops.cast_f32_bf16(self.master[sl], out)
         else:
@@ -266,7 +278,8 @@ class DenseTable:
         if out is None:
             self.params[g0: g0 + sz].copy_(self.master[sl])
         comm.all_gather(self.params[lo:hi], self.params[g0: g0 + sz])
-        grad[lo:hi].zero_()
+        if not zeroed:
+            grad[lo:hi].zero_()
         comm.stats.bucket_bytes[f"t{self.table_id}b{k}"] = comm.stats.bucket_bytes.get(f"t{self.table_id}b{k}", 0) + \
             (hi - lo) * grad.element_size() + (hi - lo) * self.params.element_size()
 
@@ -499,10 +512,12 @@ def _route_multiplier(num_rows: int) -> int:
 # the dedupe counts each unique key's lookups for the embedding-backward CSR (one pass less);
 # MINIPS_CSR_FUSED=0 counts in emb_build_csr instead
 _CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
-# plans carry the CSR's inverse permutation (csr[2]: each lookup's row in member order) so the
-# embedding dgrad can write its output pre-sorted and the backward streams it contiguously
-# instead of gathering 64-byte pieces (MINIPS_SORTED_EMB=0: the gather path)
-SORTED_EMB = os.environ.get("MINIPS_SORTED_EMB", "1") != "0"
+# MINIPS_SORTED_EMB=1: plans carry the CSR's inverse permutation (csr[2]: each lookup's row in
+# member order) so the embedding dgrad writes its output pre-sorted and the backward streams it
+# contiguously instead of gathering 64-byte pieces. Measured on one MI355X (W&D step, 3 x 400
+# steps each, tools/gpu_ab.sh): 0.4244 vs 0.4151 ms with the gather path -- the segment sums get
+# faster (66 -> 36 us) but the dgrad's scattered 64-byte stores cost more -- so it is off.
+SORTED_EMB = os.environ.get("MINIPS_SORTED_EMB", "0") == "1"
 
 
 def _with_positions(csr):

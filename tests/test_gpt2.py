@@ -47,7 +47,8 @@ def _check(dev):
     from minips_amd.ps.comm import Comm
 
     torch.manual_seed(0)
-    m = GPT2(GPT2Config(**TINY), Comm(device=torch.device(dev)))
+    # overlap_w1 off: the per-layer buckets would apply (and clear) the gradient during the backward
+    m = GPT2(GPT2Config(overlap_w1=False, **TINY), Comm(device=torch.device(dev)))
     g = torch.Generator().manual_seed(1)
     tokens = torch.randint(0, 500, (2, 64), generator=g)
     targets = torch.randint(0, 500, (2, 64), generator=g)
@@ -88,3 +89,27 @@ def test_gpt2_grads_match_autograd_gpu(dev):
 
     _native.kernels()
     _check(dev)
+
+
+@pytest.mark.gpu
+def test_gpt2_layer_buckets_world1_match_gpu(dev):
+    """One rank, overlap_w1: each layer's Adam runs on the clock stream as soon as its backward
+    finished (overlapping the rest of the backward) -- the same training as one Adam over the
+    whole table after the backward."""
+    from minips_amd.models.gpt2 import GPT2, GPT2Config
+    from minips_amd.ps.comm import Comm
+
+    res = {}
+    for ov in (False, True):
+        m = GPT2(GPT2Config(lr=1e-3, overlap_w1=ov, **TINY), Comm(device=torch.device(dev)))
+        assert (m.table.buckets is not None) == ov and m.table.pipe.async_ == ov
+        g = torch.Generator().manual_seed(2)
+        tokens = torch.randint(0, 500, (2, 64), generator=g).to(dev)
+        targets = torch.roll(tokens, -1, 1)
+        losses = [float(m.train_step(tokens, targets)) / tokens.numel() for _ in range(5)]
+        m.drain()
+        res[ov] = (losses, m.table.full_master().cpu())
+    (l0, p0), (l1, p1) = res[False], res[True]
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 1e-3 * abs(a) + 1e-4, (l0, l1)
+    assert float((p0 - p1).abs().max()) < 5 * 2e-3, float((p0 - p1).abs().max())

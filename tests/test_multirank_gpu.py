@@ -152,3 +152,135 @@ def test_gpt2_bucketed_clocks_gpu_streams():
         for a, b in zip(l0, l1):
             assert abs(a - b) <= 1e-3 * abs(a) + 1e-3, (rank, l0, l1)
         assert dmax < 4 * 2e-3, (rank, dmax)  # float-atomic wgrad order; Adam lr 1e-3 per step
+
+
+# ------------------------------------------------------------------------------ 4 / 8 ranks on one card
+# the world > 1 GPU data plane at 4 and 8 ranks (gloo staging, one shared card),
+# BSP losses equal to one rank's, SSP (collective and one-sided) tracking them within its bound.
+WD_TOTAL = 256
+
+
+def _wd_world(rank, world, consistency="bsp", staleness=0, transport="collective", steps=6):
+    from minips_amd.data.synthetic import CriteoSynth
+    from minips_amd.models.widedeep import WideDeep, WideDeepConfig
+    from minips_amd.ps.comm import Comm
+    from minips_amd.utils.metrics import get_logger
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    comm = Comm(device=dev)
+    per = WD_TOTAL // world
+    cfg = WideDeepConfig(cards=CARDS, consistency=consistency, staleness=staleness, transport=transport,
+                         max_batch=per)
+    m = WideDeep(cfg, comm)
+    g = torch.Generator().manual_seed(5)
+    full = torch.randn(m.num_rows, cfg.row_width, generator=g) * 0.01
+    full[:, cfg.emb_dim:] = 0
+    m.emb.shard.copy_(full[m.emb.base: m.emb.base + m.emb.rows_local].to(dev))
+    torch.cuda.synchronize()
+    comm.barrier()
+    data = CriteoSynth(WD_TOTAL, cards=CARDS, device=dev, seed=11)  # the same global batch on every rank
+    log = get_logger()
+    log.staleness_hist.clear()
+    losses = []
+    for _ in range(steps):
+        dense, keys, y = data.next()
+        sl = slice(rank * per, (rank + 1) * per)
+        t = m.train_step(dense[sl], keys[sl], y[sl]).clone()
+        comm.all_reduce_(t)
+        losses.append(float(t) / WD_TOTAL)
+    m.drain()
+    torch.cuda.synchronize()
+    st = m.emb.staleness_stats()["max"] if transport == "onesided" else max(log.staleness_hist or [0])
+    return losses, st
+
+
+def _wd_bsp(rank, world):
+    return _wd_world(rank, world)
+
+
+def _wd_ssp_coll(rank, world):
+    return _wd_world(rank, world, "ssp", 1)
+
+
+def _wd_ssp_onesided(rank, world):
+    return _wd_world(rank, world, "ssp", 1, "onesided")
+
+
+@pytest.fixture(scope="module")
+def wd_one_rank():
+    return run_world(_wd_bsp, world=1)[0][0]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_widedeep_bsp_world_matches_one_rank(world, wd_one_rank):
+    out = run_world(_wd_bsp, world=world)
+    for r in range(1, world):
+        assert out[r][0] == out[0][0], (r, out[r][0], out[0][0])  # all-reduced loss: same on every rank
+    for a, b in zip(out[0][0], wd_one_rank):
+        assert abs(a - b) <= 3e-3 * max(1.0, abs(b)), (world, out[0][0], wd_one_rank)
+
+
+@pytest.mark.parametrize("fn", [_wd_ssp_coll, _wd_ssp_onesided], ids=["collective", "onesided"])
+def test_widedeep_ssp_world4_tracks_one_rank_bsp(fn, wd_one_rank):
+    out = run_world(fn, world=4)
+    for r, (losses, st) in out.items():
+        assert st <= 1, (r, st)  # the SSP(1) read bound held on every rank
+        assert all(l == l for l in losses), losses
+        a, b = sum(losses) / len(losses), sum(wd_one_rank) / len(wd_one_rank)
+        assert abs(a - b) < 0.05 * b, (r, losses, wd_one_rank)
+
+
+def _torchrun(world, args, timeout=420):
+    import subprocess
+    import sys
+
+    from _util import ROOT, free_ports
+
+    env = dict(os.environ, MINIPS_SHARE_DEVICE="1", MINIPS_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_ports(1)[0])] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return r
+
+
+@pytest.mark.parametrize("world,consistency", [(4, "bsp"), (4, "ssp"), (8, "bsp"), (8, "ssp")])
+def test_bench_many_ranks_one_card(world, consistency):
+    """bench.py at 4 / 8 ranks (the driver's launch line, gloo staging on one card) in BSP and
+    SSP(1), with the host-sync audit: outside the gloo staging copies of this harness a step has
+    no host wait but the look-ahead count read."""
+    import json
+
+    r = _torchrun(world, ["bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "2", "--batch", "1024",
+                          "--consistency", consistency, "--staleness", "1" if consistency == "ssp" else "0",
+                          "--sync-audit", "3"])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["value"] > 0 and out["config"]["global_batch"] == 1024 * world
+    assert out["loss_last"] == out["loss_last"]
+    # 8 ranks write stderr concurrently: a line may carry more than one record, so decode each
+    # JSON object that follows a tag rather than whole lines
+    dec, tag = json.JSONDecoder(), "[sync-audit] "
+    audits = [dec.raw_decode(part)[0] for part in r.stderr.split(tag)[1:]]
+    assert len(audits) == world, r.stderr[-2000:]
+    for a in audits:
+        sites = a["sync_sites"]
+        # the look-ahead count read (ps/tables.py: the all-to-all splits of a planned batch)
+        others = {s: c for s, c in sites.items() if not s.startswith("minips_amd/ps/tables.py")}
+        assert not others, a
+        assert a["syncs_per_step"] <= 3, a
+
+
+@pytest.mark.parametrize("world,consistency", [(4, "ssp"), (8, "bsp")])
+def test_train_widedeep_many_ranks_one_card(world, consistency):
+    import json
+
+    r = _torchrun(world, ["-m", "minips_amd.train", "--model", "widedeep", "--steps", "20", "--batch", "512",
+                          "--consistency", consistency, "--staleness", "1" if consistency == "ssp" else "0"])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    out = json.loads(lines[-1])
+    assert out["world"] == world and out["steps"] == 20
+    losses = [l for _, l in out["losses"]]
+    assert all(l == l for l in losses) and losses[-1] < 0.75, losses

@@ -90,3 +90,64 @@ def test_rccl_collectives_from_side_streams(nccl_comm):
             comm.reduce_scatter(shard, g)
     torch.cuda.synchronize(dev)
     assert torch.equal(b, a) and torch.equal(shard, g)
+
+
+def test_rccl_destroy_reinit_restore(tmp_path, monkeypatch):
+    """The in-place rollback path of minips_amd.train (rollback(): destroy the broken group ->
+    re-init -> Comm.refresh -> reset_after_rollback -> restore the committed checkpoint -> go on)
+    on real RCCL state: a world-1 NCCL group with every table collective forced through it and
+    the tables' clock side streams active. Training after the restore repeats the losses of the
+    run that continued from the checkpoint without the rollback."""
+    from _util import free_ports
+    from minips_amd.data.synthetic import CriteoSynth
+    from minips_amd.models.widedeep import WideDeep, WideDeepConfig
+    from minips_amd.ps.checkpoint import Checkpointer
+    from minips_amd.ps.comm import Comm
+
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    monkeypatch.setenv("MINIPS_OVERLAP_W1", "sparse,dense")  # clocks on side streams at world 1
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+
+    def init():
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_ports(1)[0]}", rank=0, world_size=1,
+                                device_id=dev, timeout=datetime.timedelta(seconds=60))
+
+    cards = [1000, 50, 2000, 7, 300, 20, 5, 60, 90, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26]
+    init()
+    try:
+        comm = Comm(device=dev, force_collectives=True)
+        model = WideDeep(WideDeepConfig(cards=cards), comm)
+        assert model.emb.pipe.async_ and model.dense.pipe.async_
+        tables = {0: model.emb, 1: model.dense}
+        ck = Checkpointer(comm, prefix=str(tmp_path) + "/")
+        data = CriteoSynth(512, cards=cards, device=dev, seed=3)
+        batches = [data.next() for _ in range(7)]
+        for i in range(3):
+            model.train_step(*batches[i])
+        ck.save(tables, iteration=3)
+        ck.commit()
+        ref = [float(model.train_step(*batches[i]).item()) for i in range(3, 7)]
+        calls_before = comm.stats.calls
+        assert calls_before > 0  # the clocks really went through RCCL
+        model.drain()
+        torch.cuda.synchronize(dev)
+        dist.destroy_process_group()
+        init()
+        comm.refresh()
+        assert comm.backend == "nccl" and comm.world == 1
+        for t in tables.values():
+            t.reset_after_rollback()
+        if hasattr(model, "_pending_plans"):
+            model._pending_plans = []
+        assert ck.load(tables) == 3
+        again = [float(model.train_step(*batches[i]).item()) for i in range(3, 7)]
+        model.drain()
+        torch.cuda.synchronize(dev)
+        assert comm.stats.calls > calls_before
+        for a, b in zip(again, ref):
+            assert abs(a - b) <= 2e-3 * abs(b) + 1e-3, (again, ref)
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
