@@ -388,6 +388,31 @@ void wd_assemble(const at::Tensor& dense, const at::Tensor& rows, const at::Tens
                         (int)ones_col, stream_of(X), z);
 }
 
+// wd_assemble reading the fp32 table shard directly: row of lookup (b, f) = tab[uniq[inv] - base]
+void wd_assemble_tab(const at::Tensor& dense, const at::Tensor& tab, const at::Tensor& uniq, int64_t base,
+                     const at::Tensor& inv, int64_t F, int64_t D, at::Tensor& X, at::Tensor& wide_logit,
+                     int64_t ones_col, const c10::optional<at::Tensor>& zero) {
+  float* z = opt_ptr<float>(zero, at::kFloat, "zero");
+  if (z) TORCH_CHECK(zero->numel() >= 1, "zero: at least one element");
+  for (const at::Tensor* t : {&dense, &tab, &uniq, &inv, (const at::Tensor*)&X, (const at::Tensor*)&wide_logit})
+    check_gpu(*t, "wd_assemble_tab");
+  check_dtype(tab, at::kFloat, "tab");
+  check_dtype(uniq, at::kLong, "uniq");
+  check_dtype(inv, at::kLong, "inv");
+  check_dtype(X, at::kBFloat16, "X");
+  check_dtype(dense, at::kFloat, "dense");
+  TORCH_CHECK(tab.dim() == 2 && tab.stride(1) == 1, "tab must be a row-major [rows, W] matrix");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(tab.data_ptr()) % 16 == 0, "tab must be 16-byte aligned");
+  const int64_t B = X.size(0);
+  TORCH_CHECK(inv.numel() == B * F, "inv must be [B*F]");
+  TORCH_CHECK(dense.size(0) == B, "dense rows");
+  TORCH_CHECK(tab.size(1) > D, "tab rows must hold D deep values + the wide weight");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
+  minips_k::wd_assemble_tab(ptr<float>(dense), (int)dense.size(1), ptr<float>(tab), tab.stride(0),
+                            ptr<int64_t>(uniq), base, ptr<int64_t>(inv), B, (int)F, (int)D, ptr<bf16_t>(X),
+                            (int)X.size(1), ptr<float>(wide_logit), (int)ones_col, stream_of(X), z);
+}
+
 void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& wide_logit,
              const at::Tensor& labels, at::Tensor& dH, at::Tensor& dw, at::Tensor& db, at::Tensor& dwide,
              at::Tensor& loss_sum, const c10::optional<at::Tensor>& dH_colsum, double grad_scale) {
@@ -1301,6 +1326,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1, py::arg("zero") = py::none());
   m.def("wd_head", &wd_head);
+  m.def("wd_assemble_tab", &wd_assemble_tab);
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);

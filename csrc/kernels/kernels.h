@@ -114,6 +114,9 @@ void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_st
 //   z = H[b,:].w + b0 + wide[b]; dz = (sigmoid(z) - y) * grad_scale
 //   dH = dz * w * (H > 0) (bf16), dw += dz*H, db += dz, dH_colsum += dH, dwide[b] = dz,
 //   loss_sum += BCE(z, y)
+void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t tab_ld, const int64_t* uniq,
+                     int64_t base, const int64_t* inv, int64_t B, int F, int D, bf16_t* X, int ldx,
+                     float* wide_logit, int ones_col, hipStream_t s, float* zero_out);
 void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
              float grad_scale, hipStream_t s);

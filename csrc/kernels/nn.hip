@@ -251,10 +251,16 @@ void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t
 
 // ---------------------------------------------------------------------------- softmax-xent
 // logits are updated in place with the gradient ((softmax - onehot) * scale); columns [V, ld)
-// inside the last 8-wide chunk are zeroed. One 512-thread block per row; the row (up to
-// 512 * 8 * 13 = 53248 columns, GPT-2's 50304 included) stays in registers as packed 16-byte
-// chunks, so HBM sees exactly one read and one write of the logits.
-constexpr int kXentThreads = 512, kXentChunks = 13;
+// inside the last 8-wide chunk are zeroed. One 1024-thread block per row; the row (up to
+// 1024 * 8 * 7 = 57344 columns, GPT-2's 50304 included) stays in registers as PACKED 16-byte
+// chunks (28 VGPRs), so HBM sees exactly one read and one write of the logits.
+//   pass 1: per-thread online (max, sum of exp) over its chunks -> ONE block reduction of the
+//           (max, sum) pairs (rescaled merge)
+//   pass 2: g = exp(x - lse) * scale, packed stores
+// An empty asm on the packed registers between the passes keeps the compiler from carrying the
+// 56 unpacked floats of pass 1 into pass 2 (it did: 208 VGPRs, 2 waves/SIMD, one row per CU at a
+// time -- 548 us for GPT-2's 8192 x 50304 logits, 3 TB/s).
+constexpr int kXentThreads = 1024, kXentChunks = 7;
 
 // Component q of a uint4 without taking its address (keeps the chunk array in registers).
 __device__ __forceinline__ uint32_t u4get(const uint4& v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2
@@ -264,97 +270,114 @@ __device__ __forceinline__ float u4elem(const uint4& v, int q) {
   return (q & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
 }
 
-__device__ __forceinline__ float xent_block_max(float v, float* red) {
-  v = warp_max(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  float t = -3.4e38f;
-#pragma unroll
-  for (int i = 0; i < kXentThreads / 64; ++i) t = fmaxf(t, red[i]);
-  return t;
-}
-__device__ __forceinline__ float xent_block_sum(float v, float* red) {
-  v = warp_sum(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  float t = 0.f;
-#pragma unroll
-  for (int i = 0; i < kXentThreads / 64; ++i) t += red[i];
-  return t;
+// (m, s) <- merge of two partial softmax denominators, in log2 units: s = sum 2^(x - m)
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  s = s * __builtin_amdgcn_exp2f(m - mn) + s2 * __builtin_amdgcn_exp2f(m2 - mn);
+  m = mn;
 }
 
 __global__ __launch_bounds__(kXentThreads) void softmax_xent_kernel(bf16_t* __restrict__ logits, int ld, int64_t M,
                                                                     int V, const int64_t* __restrict__ labels,
                                                                     float scale, float* loss_sum, float* correct) {
-  __shared__ float red[kXentThreads / 64];
+  __shared__ float red_m[kXentThreads / 64], red_s[kXentThreads / 64], red_x[kXentThreads / 64];
   const int nfull = V >> 3;          // chunks with 8 valid columns
   const int tail = V & 7;            // valid columns of chunk nfull (0: none)
   const float L2E = 1.4426950408889634f;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // loss / hit sums accumulate in thread 0 over the block's rows: one atomic per block at the
   // end (one per row would serialise M same-address atomics at the memory side, ~12 ns each)
   float loss_acc = 0.f, hit_acc = 0.f;
+  // the next row's chunks are loaded while this row is reduced and written (one block per CU:
+  // the prefetch is what keeps HBM busy during the block's reductions)
+  auto load_row = [&](int64_t r, uint4 (&dst)[kXentChunks]) {
+    const bf16_t* row = logits + r * ld;
+#pragma unroll
+    for (int k = 0; k < kXentChunks; ++k) {
+      const int ch = threadIdx.x + k * kXentThreads;
+      dst[k] = (r < M && (ch < nfull || (ch == nfull && tail))) ? *reinterpret_cast<const uint4*>(row + ch * 8)
+                                                               : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  uint4 vn[kXentChunks];
+  load_row(blockIdx.x, vn);
   for (int64_t r = blockIdx.x; r < M; r += gridDim.x) {
     bf16_t* row = logits + r * ld;
     uint4 v[kXentChunks];
-    float mx = -3.4e38f;
+#pragma unroll
+    for (int k = 0; k < kXentChunks; ++k) v[k] = vn[k];
+    load_row(r + gridDim.x, vn);
+    // pass 1 (log2 units): running max m and s = sum 2^(x*L2E - m) over this thread's values
+    float m = -3.0e38f, sm = 0.f;
 #pragma unroll
     for (int k = 0; k < kXentChunks; ++k) {
       const int ch = threadIdx.x + k * kXentThreads;
-      if (ch < nfull) {
-        v[k] = *reinterpret_cast<const uint4*>(row + ch * 8);
+      const int nv = ch < nfull ? 8 : (ch == nfull ? tail : 0);
+      if (nv == 0) continue;
+      float x[8], cm = -3.0e38f;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) mx = fmaxf(mx, u4elem(v[k], q));
-      } else if (ch == nfull && tail) {
-        v[k] = *reinterpret_cast<const uint4*>(row + ch * 8);
-#pragma unroll 1
-        for (int q = 0; q < tail; ++q) mx = fmaxf(mx, bf2f(row[ch * 8 + q]));
+      for (int q = 0; q < 8; ++q) {
+        x[q] = q < nv ? u4elem(v[k], q) * L2E : -3.0e38f;
+        cm = fmaxf(cm, x[q]);
       }
-    }
-    mx = xent_block_max(mx, red);
-    const float ml2 = mx * L2E;
-    float se = 0.f;
+      float cs = 0.f;
 #pragma unroll
-    for (int k = 0; k < kXentChunks; ++k) {
-      const int ch = threadIdx.x + k * kXentThreads;
-      if (ch < nfull) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) se += __builtin_amdgcn_exp2f(u4elem(v[k], q) * L2E - ml2);
-      } else if (ch == nfull && tail) {
-#pragma unroll 1
-        for (int q = 0; q < tail; ++q) se += __builtin_amdgcn_exp2f(bf2f(row[ch * 8 + q]) * L2E - ml2);
-      }
+      for (int q = 0; q < 8; ++q) cs += q < nv ? __builtin_amdgcn_exp2f(x[q] - cm) : 0.f;
+      lse_merge(m, sm, cm, cs);
     }
-    se = xent_block_sum(se, red);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lse_merge(m, sm, __shfl_xor(m, o, 64), __shfl_xor(sm, o, 64));
     const int64_t lab = labels[r];
-    const float lse = mx + __logf(se);
-    if (threadIdx.x == 0 && lab >= 0 && lab < V) {  // (row[lab] is rewritten only after the block syncs)
-      const float zl = bf2f(row[lab]);
-      loss_acc += lse - zl;
-      hit_acc += zl >= mx ? 1.f : 0.f;
+    // the label's logit, read by its owner thread before any thread rewrites the row
+    const bool has_lab = lab >= 0 && lab < V;
+    const int lch = has_lab ? (int)(lab >> 3) : -1;
+    float zl_part = 0.f;
+#pragma unroll
+    for (int k = 0; k < kXentChunks; ++k)
+      if (threadIdx.x + k * kXentThreads == lch) zl_part = u4elem(v[k], (int)(lab & 7));
+    const bool own = (lch >= 0) && ((lch % kXentThreads) == (int)threadIdx.x);
+    zl_part = own ? zl_part : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) zl_part += __shfl_xor(zl_part, o, 64);
+    __syncthreads();  // the previous row's readers of red_* are done
+    if (lane == 0) {
+      red_m[w] = m;
+      red_s[w] = sm;
+      red_x[w] = zl_part;
     }
     __syncthreads();
-    const float sinv = scale / se;
+    float M2 = red_m[0], S2 = red_s[0], zl = red_x[0];
+#pragma unroll
+    for (int i = 1; i < kXentThreads / 64; ++i) {
+      lse_merge(M2, S2, red_m[i], red_s[i]);
+      zl += red_x[i];
+    }
+    const float lse2 = M2 + __log2f(S2);  // log2 of sum 2^(x*L2E)
+    if (threadIdx.x == 0 && has_lab) {
+      loss_acc += lse2 / L2E - zl;
+      hit_acc += zl * L2E >= M2 ? 1.f : 0.f;
+    }
+    // pass 2: the packed registers only (asm: the unpacked pass-1 values are dead here)
+#pragma unroll
+    for (int k = 0; k < kXentChunks; ++k) asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
 #pragma unroll
     for (int k = 0; k < kXentChunks; ++k) {
       const int ch = threadIdx.x + k * kXentThreads;
-      if (ch < nfull || (ch == nfull && tail)) {
-        const int nv = ch < nfull ? 8 : tail;
-        uint32_t o[4];
+      const int nv = ch < nfull ? 8 : (ch == nfull ? tail : 0);
+      if (nv == 0) continue;
+      uint32_t o[4];
 #pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2) {
-          const float g0 = __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2) * L2E - ml2) * sinv;
-          const float g1 = __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2 + 1) * L2E - ml2) * sinv;
-          o[q2] = pack_bf2(2 * q2 < nv ? g0 : 0.f, 2 * q2 + 1 < nv ? g1 : 0.f);
+      for (int q2 = 0; q2 < 4; ++q2) {
+        float g0 = __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2) * L2E - lse2) * scale;
+        float g1 = __builtin_amdgcn_exp2f(u4elem(v[k], 2 * q2 + 1) * L2E - lse2) * scale;
+        if (ch == lch) {  // the -onehot term, folded before rounding
+          if ((int)(lab & 7) == 2 * q2) g0 -= scale;
+          if ((int)(lab & 7) == 2 * q2 + 1) g1 -= scale;
         }
-        *reinterpret_cast<uint4*>(row + ch * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+        o[q2] = pack_bf2(2 * q2 < nv ? g0 : 0.f, 2 * q2 + 1 < nv ? g1 : 0.f);
       }
+      *reinterpret_cast<uint4*>(row + ch * 8) = make_uint4(o[0], o[1], o[2], o[3]);
     }
-    __syncthreads();
-    if (threadIdx.x == 0 && lab >= 0 && lab < V) row[lab] = f2bf(bf2f(row[lab]) - scale);  // the -onehot term
   }
   if (threadIdx.x == 0) {
     atomicAdd(loss_sum, loss_acc);
@@ -450,7 +473,14 @@ void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* label
     MINIPS_HIP_CHECK(hipGetLastError());
     return;
   }
-  hipLaunchKernelGGL(softmax_xent_kernel, (int)std::min<int64_t>(M, 4096), kXentThreads, 0, s, logits, ld, M, V,
+  // one 16-wave block per CU, each walking its rows with a one-row prefetch
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    MINIPS_HIP_CHECK(hipGetDevice(&dev));
+    MINIPS_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    return n > 0 ? n : 256;
+  }();
+  hipLaunchKernelGGL(softmax_xent_kernel, (int)std::min<int64_t>(M, ncu), kXentThreads, 0, s, logits, ld, M, V,
                      labels, scale, loss_sum, correct);
   MINIPS_HIP_CHECK(hipGetLastError());
 }

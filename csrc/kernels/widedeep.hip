@@ -89,6 +89,83 @@ void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_st
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// wd_assemble straight from the fp32 table shard (one rank: the Get's row gather folded in): the
+// row of lookup (b, f) is tab[uniq[inv[b*F + f]] - base], converted to bf16 exactly as the gather
+// kernel does (pack_bf2), so X is bit-identical to gather_rows + wd_assemble. Saves the gathered
+// [U, W] bf16 rows' write + re-read and one launch; repeated hot rows hit in L2 / MALL.
+__global__ void wd_assemble_tab_kernel(const float* __restrict__ dense, int n_dense, const float* __restrict__ tab,
+                                       int64_t tab_ld, const int64_t* __restrict__ uniq, int64_t base,
+                                       const int64_t* __restrict__ inv, int64_t B, int F, int D,
+                                       bf16_t* __restrict__ X, int ldx, float* __restrict__ wide_logit, int ones_col,
+                                       float* __restrict__ zero_out) {
+  if (zero_out && blockIdx.x == 0 && threadIdx.x == 0) *zero_out = 0.f;
+  const int chunks = ldx >> 3;
+  const int emb_cols = F * D;
+  const int64_t total = B * chunks;
+  const int64_t total_r = (total + 63) & ~63ll;
+  auto row_of = [&](int64_t b, int f) { return tab + (uniq[inv[b * F + f]] - base) * tab_ld; };
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total_r + 32 * B;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    if (c >= total_r) {
+      const int64_t k = c - total_r, b = k >> 5;
+      const int f = (int)(k & 31);
+      // the wide weight goes through bf16 as in the gathered path
+      float w = f < F ? __uint_as_float(pack_bf2(row_of(b, f)[D], 0.f) << 16) : 0.f;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+      if (f == 0) wide_logit[b] = w;
+      continue;
+    }
+    if (c >= total) continue;
+    const int64_t b = c / chunks;
+    const int col0 = (int)(c - b * chunks) * 8;
+    uint32_t packed[4];
+    if (col0 + 8 <= emb_cols && (D & 7) == 0) {
+      const int f = col0 / D, d = col0 - f * D;
+      const float* src = row_of(b, f) + d;
+      const float4 lo = *reinterpret_cast<const float4*>(src);
+      const float4 hi = *reinterpret_cast<const float4*>(src + 4);
+      packed[0] = pack_bf2(lo.x, lo.y);
+      packed[1] = pack_bf2(lo.z, lo.w);
+      packed[2] = pack_bf2(hi.x, hi.y);
+      packed[3] = pack_bf2(hi.z, hi.w);
+    } else {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = col0 + j;
+        if (col < emb_cols) {
+          const int f = col / D, d = col - f * D;
+          v[j] = __uint_as_float(pack_bf2(row_of(b, f)[d], 0.f) << 16);
+        } else if (col < emb_cols + n_dense) {
+          v[j] = dense[b * n_dense + (col - emb_cols)];
+        } else {
+          v[j] = col == ones_col ? 1.f : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) packed[j] = pack_bf2(v[2 * j], v[2 * j + 1]);
+    }
+    *reinterpret_cast<uint4*>(X + b * ldx + col0) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+  }
+}
+
+void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t tab_ld, const int64_t* uniq,
+                     int64_t base, const int64_t* inv, int64_t B, int F, int D, bf16_t* X, int ldx,
+                     float* wide_logit, int ones_col, hipStream_t s, float* zero_out) {
+  if (ldx % 8) throw std::runtime_error("wd_assemble_tab: ldx must be a multiple of 8");
+  if (F * D + n_dense > ldx) throw std::runtime_error("wd_assemble_tab: ldx too small");
+  if (ones_col >= ldx) throw std::runtime_error("wd_assemble_tab: ones_col out of range");
+  if (tab_ld % 4 || (D & 7) || tab_ld < D + 1) throw std::runtime_error("wd_assemble_tab: 16-byte rows, D % 8 == 0");
+  if (F > 32) throw std::runtime_error("wd_assemble_tab: at most 32 features");
+  if (B <= 0) return;
+  const int block = 256;
+  const int64_t items = ((B * (ldx / 8) + 63) & ~63ll) + 32 * B;
+  hipLaunchKernelGGL(wd_assemble_tab_kernel, (int)((items + block - 1) / block), block, 0, s, dense, n_dense, tab,
+                     tab_ld, uniq, base, inv, B, F, D, X, ldx, wide_logit, ones_col, zero_out);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 // One wave per sample (grid-stride); each lane owns Hd/64 columns and keeps its dw / colsum
 // partials in registers across all samples it visits: one atomic per lane per column at the end.
 constexpr int kHeadWaves = 16;  // 1024-thread blocks: 4x the waves in flight, same atomic count

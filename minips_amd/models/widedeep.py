@@ -225,9 +225,15 @@ class WideDeep(LookaheadPlans):
                 self.prefetch(nk, keys_on_plan_stream=next_on_plan_stream)
 
         issue_next("start")
-        rows, plan = self.emb.get(keys, plan=plan)
+        src = self.emb.get_source(keys, plan=plan)  # one rank: the rows are read in place
+        if src is not None:
+            plan, table, index, base = src
+            ops.wd_assemble_tab(dense, table, index, base, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0],
+                                zero=b["loss"])
+        else:
+            rows, plan = self.emb.get(keys, plan=plan)
+            ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
         G = self.dense.grad
-        ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
         P = self.dense.get()
         self._forward(b, P)
         scale = 1.0 / (B * self.comm.world)
@@ -238,7 +244,10 @@ class WideDeep(LookaheadPlans):
         issue_next("head")
         side = self._side
         # weight gradients fork onto a second stream as soon as their inputs exist, beside the
-        # dgrad chain (their split-K tails and reduces fill the gaps of the dependent chain)
+        # dgrad chain (their split-K tails and reduces fill the gaps of the dependent chain).
+        # Each fork records an event on the compute stream (~2-4 us queue bubble on MI355X), but
+        # fewer, later forks lose more overlap than they save: W3+W2 forked together 0.431-0.438,
+        # all three after dgrad1 0.446 vs 0.418-0.421 ms/step (profiles/r3/ab_wd_forks.txt)
         with side.fork():
             ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=self.k_in[2], out=b["dH2"])

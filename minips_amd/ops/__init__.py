@@ -443,6 +443,18 @@ def wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col=-1, zero=None):
     return X, wide_logit
 
 
+def wd_assemble_tab(dense, table, index, base, inv, F, D, X, wide_logit, ones_col=-1, zero=None):
+    """wd_assemble with the rows read in place: the row of unique u is table[index[u] - base]
+    (fp32), rounded to bf16 exactly as gather_rows(out bf16) does."""
+    if _gpu(X):
+        kernels().wd_assemble_tab(dense, table, index, int(base), inv, int(F), int(D), X, wide_logit, int(ones_col),
+                                  zero)
+        return X, wide_logit
+    U = int(inv.max()) + 1 if inv.numel() else 0
+    rows = table[index[:U] - base].to(torch.bfloat16)
+    return wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col, zero)
+
+
 def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum=None, grad_scale=1.0):
     if _gpu(H):
         kernels().wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, float(grad_scale))

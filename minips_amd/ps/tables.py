@@ -570,6 +570,9 @@ _SORT_PLAN = os.environ.get("MINIPS_SORT_PLAN", "1") != "0"
 # Wide&Deep step on one MI355X (0.473-0.477 vs 0.465 ms/step: the fused kernel's key -> row ->
 # table load chain costs more than the 2 x U x 144 B it saves; tools/gpu_ab.sh), so off by default.
 _FUSED_EMB_ADAGRAD = os.environ.get("MINIPS_FUSED_EMB_ADAGRAD", "0") == "1"
+# one rank: W&D assembles its input straight from the fp32 shard (SparseTable.get_source +
+# ops.wd_assemble_tab) instead of gathering the batch's unique rows first (MINIPS_FUSED_ASSEMBLE=0)
+_FUSED_ASSEMBLE = os.environ.get("MINIPS_FUSED_ASSEMBLE", "1") == "1"
 
 
 class _LookupGrads:
@@ -909,6 +912,26 @@ class SparseTable:
         rows = torch.empty(plan.cap, self.width, dtype=self.pull_dtype, device=dev)
         self.comm.all_to_all_v(rows, served, plan.send, plan.recv, p2p=self.p2p)
         return rows, plan
+
+    def get_source(self, keys: torch.Tensor, plan=None):
+        """The Get without its row gather, for a consumer that reads the rows in place (one rank,
+        fp32 range shard, bf16 pull): returns (plan, table, index, base) -- the row of unique u
+        is table[index[u] - base] -- after the same ordering as get() (plan ready, BSP/SSP read
+        gate). None when the rows must be gathered (several ranks, hash / bf16 / fp64 tables)."""
+        if not (self.comm.world == 1 and self.comm.device.type == "cuda" and type(self)._serve_index is
+                SparseTable._serve_index and self.shard.dtype == torch.float32
+                and self.pull_dtype == torch.bfloat16 and _FUSED_ASSEMBLE):
+            return None
+        if plan is None:
+            plan = self.plan(keys)
+        elif isinstance(plan, _PendingPlan):
+            plan = self._finish_plan(plan)
+        ready = plan.extra.pop("ready", None)
+        if ready is not None:
+            torch.cuda.current_stream(self.comm.device).wait_event(ready)
+        self.pipe.wait_for_read()
+        table, index, base = self._serve_index(plan)
+        return plan, table, index, base
 
     def get_rows(self, keys: torch.Tensor) -> torch.Tensor:
         """Reference-style Get: the values of every requested key, in request order."""

@@ -207,6 +207,55 @@ def test_widedeep_kernels(dev):
     torch.testing.assert_close(gr.cpu(), gr_ref, rtol=1e-4, atol=1e-4)
 
 
+def test_wd_assemble_tab_and_head_full_batch(dev):
+    """The one-rank fused Get+assemble (rows read in place from the fp32 shard) is bit-identical
+    to gather_rows(bf16) + wd_assemble; the head at the bench's batch (256 blocks, per-block
+    partials folded by atomics) matches the fp32 reference."""
+    g = torch.Generator().manual_seed(14)
+    B, F, D, nd, rows_local, base = 2048, 26, 32, 13, 5000, 1000
+    ldx = (F * D + nd + 1 + 63) // 64 * 64
+    shard = torch.randn(rows_local, 36, generator=g)
+    U = 1500
+    uniq = torch.randperm(rows_local, generator=g)[:U] + base
+    inv = torch.randint(0, U, (B * F,), generator=g)
+    dense = torch.randn(B, nd, generator=g)
+    d = lambda t: t.to(dev)  # noqa: E731
+    rows = torch.empty(U, 36, dtype=torch.bfloat16, device=dev)
+    ops.gather_rows(d(shard), d(uniq), base, rows)
+    X1, w1 = torch.empty(B, ldx, dtype=torch.bfloat16, device=dev), torch.empty(B, device=dev)
+    z1 = torch.ones(1, device=dev)
+    ops.wd_assemble(d(dense), rows, d(inv), F, D, X1, w1, ones_col=F * D + nd, zero=z1)
+    X2, w2 = torch.empty_like(X1), torch.empty_like(w1)
+    z2 = torch.ones(1, device=dev)
+    ops.wd_assemble_tab(d(dense), d(shard), d(uniq), base, d(inv), F, D, X2, w2, ones_col=F * D + nd, zero=z2)
+    assert torch.equal(X1, X2)
+    torch.testing.assert_close(w2, w1, rtol=1e-6, atol=1e-6)
+    assert float(z2) == 0.0
+    # CPU reference of the in-place form
+    X3, w3 = torch.empty(B, ldx, dtype=torch.bfloat16), torch.empty(B)
+    ops.wd_assemble_tab(dense, shard, uniq, base, inv, F, D, X3, w3, ones_col=F * D + nd)
+    assert torch.equal(X3, X1.cpu())
+    # head at the bench's batch
+    Bh, Hd = 16384, 256
+    H = _bf(torch.relu(torch.randn(Bh, Hd, generator=g)))
+    w = _bf(torch.randn(Hd, generator=g) * 0.1)
+    b0 = _bf(torch.tensor([0.1]))
+    wide = torch.randn(Bh, generator=g)
+    y = (torch.rand(Bh, generator=g) > 0.5).float()
+
+    def run(dv):
+        o = dict(dH=torch.empty(Bh, Hd, dtype=torch.bfloat16, device=dv), dw=torch.full((Hd,), 0.5, device=dv),
+                 db=torch.full((1,), 0.25, device=dv), dwide=torch.empty(Bh, device=dv),
+                 loss=torch.zeros(1, device=dv), cs=torch.zeros(Hd, device=dv))
+        ops.wd_head(H.to(dv), w.to(dv), b0.to(dv), wide.to(dv), y.to(dv), o["dH"], o["dw"], o["db"], o["dwide"],
+                    o["loss"], o["cs"], 1.0 / Bh)
+        return {k: v.cpu() for k, v in o.items()}
+
+    r, o = run("cpu"), run(dev)
+    for k in r:
+        torch.testing.assert_close(o[k].float(), r[k].float(), rtol=2e-2, atol=1e-4)
+
+
 def test_lr_and_kmeans(dev):
     g = torch.Generator().manual_seed(5)
     B, nnz, U = 64, 10, 200

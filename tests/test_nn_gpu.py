@@ -47,7 +47,8 @@ def test_layernorm(dev):
 
 
 @pytest.mark.parametrize("V,ld,M", [(10, 16, 64), (10, 16, 70000), (33, 48, 300), (64, 64, 500), (65, 72, 100),
-                                    (1000, 1000, 64), (50257, 50264, 64)])
+                                    (1000, 1000, 64), (50257, 50264, 64),
+                                    (50257, 50304, 700)])
 def test_softmax_xent(dev, V, ld, M):
     """V <= 64 runs the one-thread-per-row kernel (M = 70000: grid-stride rows), larger V the
     block-per-row kernel; both against the fp32 reference."""

@@ -106,3 +106,19 @@ def test_widedeep_lookahead_depth_matches(dev):
     for depth in (1, 2):
         for a, b in zip(res[depth], res[0]):
             assert abs(a - b) < 1e-4, (depth, res)
+
+
+def test_widedeep_fused_assemble_matches_gather(dev, monkeypatch):
+    """One rank: the input assembled straight from the shard (SparseTable.get_source) trains
+    exactly like the gathered Get + wd_assemble."""
+    import minips_amd.ps.tables as tables
+
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(tables, "_FUSED_ASSEMBLE", fused)
+        losses, m = _run(dev, steps=6)
+        res[fused] = (losses, m.emb.shard.cpu())
+    (l0, s0), (l1, s1) = res[False], res[True]
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (l0, l1)
+    assert float((s0 - s1).abs().max()) < 1e-3
