@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
 constexpr int BK2 = 64;
 constexpr uint32_t kOobOffset = 0x80000000u;
 #ifndef MINIPS_GEMM_SETPRIO
-#define MINIPS_GEMM_SETPRIO 0  // T5 setprio pair: measured -1..-4 % here (tools/gpu_gemm_ab.sh)
+#define MINIPS_GEMM_SETPRIO 0  // T5 setprio pair: measured -1..-4 % here (tools/gpu_ab.sh)
 #endif
 constexpr bool kSetPrio = MINIPS_GEMM_SETPRIO != 0;
 #ifndef MINIPS_GEMM_LDS_EPILOGUE
@@ -787,7 +787,7 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
   // v2 (LDS-DMA) needs every byte offset within one batch element below 2 GiB (32-bit voffset)
   const int64_t a_ext = (int64_t)((A_KM ? K : M) - 1) * lda + (A_KM ? M : K);
   const int64_t b_ext = (int64_t)((B_KN ? K : N) - 1) * ldb + (B_KN ? N : K);
-  // measured (tools/bench_gemm.py): v2 wins on forward / dgrad; the split-K wgrad (both operands
+  // measured (tools/bench_kernels.py gemm): v2 wins on forward / dgrad; the split-K wgrad (both operands
   // tr-read) stays on the register-staged BK=32 kernel, which is faster there
   // wgrad kernel (MINIPS_GEMM_WGRAD): v2 (default: LDS-DMA, tr-read operands, staged epilogue), v1
   // (register-staged BK=32, round-1 default), or v3 (256x256 phase-split tiles, split-K chosen by
@@ -805,7 +805,7 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
     // Tile choice by wave quantisation: a 256x256 workgroup fills a CU alone (128 KiB LDS), two
     // 128x128 ones share it; take the 256 tile when its last round of workgroups is at least as
     // full as the 128 tile's (it moves half the L2->LDS bytes per MFMA), else 128x128
-    // (tools/bench_gemm.py: gpt.fc 1536 vs 384 tiles -> 128 wins; W&D dgrad0 256 tiles -> 256 wins).
+    // (tools/bench_kernels.py gemm: gpt.fc 1536 vs 384 tiles -> 128 wins; W&D dgrad0 256 tiles -> 256 wins).
     static const int force_tile = [] {
       const char* e = std::getenv("MINIPS_GEMM_TILE");
       return e ? std::atoi(e) : 0;

@@ -5,7 +5,7 @@
 // device-scope atomics (CAS probes, per-key counts, shard cursors). Those execute at the memory
 // side on the multi-XCD part and slow every concurrently running kernel: the W&D step measured
 // 0.450 ms with per-step planning vs 0.360 ms stepping through pre-planned batches
-// (tools/step_ablation.py) even with the planning stream confined to 16 CUs. This planner uses
+// (tools/step_probe.py ablation) even with the planning stream confined to 16 CUs. This planner uses
 // no atomics at all:
 //
 //   plan_sort_col  one 1024-thread workgroup per column: the column's <= 16384 (key - base_f, b)

@@ -113,7 +113,7 @@ class WideDeep(LookaheadPlans):
         # weight-gradient GEMM yields its gradient (no bias epilogue, no column-sum atomics).
         # Layer 1's k_pad is a multiple of 64: whole 64-deep K-steps and 128-byte rows for the
         # LDS-DMA (K = 896: the 16384x1024 forward takes 30.7 us vs 38.8 us at align8's 848;
-        # tools/bench_gemm.py). MINIPS_WD_BIAS=vec gives layers 2/3 bias vectors instead (see
+        # tools/bench_kernels.py gemm). MINIPS_WD_BIAS=vec gives layers 2/3 bias vectors instead (see
         # _BIAS_VEC): dH3's column sums from wd_head, dH2's from a column-sum kernel.
         self.k_in = [cfg.F * cfg.emb_dim + cfg.n_dense, *cfg.hidden[:-1]]
         self.k_pad = [_align(self.k_in[0] + 1, _K1_ALIGN),

@@ -172,7 +172,7 @@ def linear_wgrad(dy, x, dw, split_k=None):
         t = 256 if _WGRAD_MODE == "v3" else 128
         tiles = ((N + t - 1) // t) * ((K + t - 1) // t)
         # about one workgroup per CU (v3: 256x256 tiles, 1 WG/CU; v1/v2: ~512 128x128 blocks), but
-        # a minimum number of reduction rows per split (tools/sweep_wgrad.py: shorter slices lose
+        # a minimum number of reduction rows per split (profiles/r2/gpt2_wgrad_sweep.txt: shorter slices lose
         # to their fixed prologue/epilogue cost; the slab reduce makes splits cheap)
         overlapped = getattr(_overlap_state, "on", False)
         min_rows = _WGRAD_MIN_ROWS_OVERLAP if overlapped else _WGRAD_MIN_ROWS

@@ -783,7 +783,7 @@ class SparseTable:
         (LookaheadFeeder's end-of-step fence), so the plan's buffers -- allocated on the planning
         stream and read on the compute stream -- need no per-tensor ``record_stream``: each
         record_stream costs an allocator event on the compute stream when the tensor is freed,
-        and those events cost the W&D step ~30 us (tools/step_ablation.py). Only valid while the
+        and those events cost the W&D step ~30 us (tools/step_probe.py ablation). Only valid while the
         plan is consumed inside the fenced step (one rank, synchronous clocks)."""
         if self._exact_counts:
             return self.plan(keys, csr)

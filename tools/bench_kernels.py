@@ -1,0 +1,271 @@
+#!/usr/bin/env python3
+"""Isolated kernel microbenchmarks on the model shapes (one MI355X), one entry point:
+
+    python tools/bench_kernels.py gemm [--set wd|gpt2] [--shapes name:M:N:K:layout,...]
+                                        ours vs torch.matmul (hipBLASLt), TFLOP/s per shape
+    python tools/bench_kernels.py kscan --M 16384 --N 1024 --layout nt
+                                        time vs K at fixed M, N: fixed cost vs per-K-step cost
+    python tools/bench_kernels.py pmc   model-shape GEMMs back to back (for rocprofv3 --pmc passes)
+    python tools/bench_kernels.py attn  fused causal attention vs torch SDPA
+    python tools/bench_kernels.py nn    GPT-2 memory-bound kernels (LayerNorm, add, softmax-xent): TB/s
+    python tools/bench_kernels.py emb   W&D embedding backward on a real Criteo-shaped plan
+    python tools/bench_kernels.py plan  key planning: per-column sort vs hash dedupe + CSR
+
+GEMM layouts: nt = forward (A [M,K], B [N,K]), nn = dgrad (B [K,N]), tn = wgrad (A [K,M],
+B [K,N], fp32 out; through ops.linear_wgrad, i.e. the model's split-K choice, unless
+GEMM_TN_MODEL=0). In the training steps these kernels share the GPU with side streams, so rocprof's
+in-step durations overstate their own cost; this separates the two.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from minips_amd import ops  # noqa: E402
+
+WD_SHAPES = [  # (name, M, N, K, layout)
+    ("wd.fwd1", 16384, 1024, 896, "nt"), ("wd.fwd2", 16384, 512, 1032, "nt"), ("wd.fwd3", 16384, 256, 520, "nt"),
+    ("wd.dgrad2", 16384, 512, 256, "nn"), ("wd.dgrad1", 16384, 1024, 512, "nn"), ("wd.dgrad0", 16384, 832, 1024, "nn"),
+    ("wd.wgrad3", 256, 520, 16384, "tn"), ("wd.wgrad2", 512, 1032, 16384, "tn"), ("wd.wgrad1", 1024, 896, 16384, "tn"),
+    ("sq4096", 4096, 4096, 4096, "nt"),
+]
+# every GEMM of one GPT-2 small step (B*T = 8192, d = 768, vocab 50304): forward, dgrad, wgrad
+GPT2_SHAPES = [
+    ("g.qkv.f", 8192, 2304, 768, "nt"), ("g.proj.f", 8192, 768, 768, "nt"), ("g.fc.f", 8192, 3072, 768, "nt"),
+    ("g.fc2.f", 8192, 768, 3072, "nt"), ("g.lm.f", 8192, 50304, 768, "nt"),
+    ("g.qkv.d", 8192, 768, 2304, "nn"), ("g.proj.d", 8192, 768, 768, "nn"), ("g.fc.d", 8192, 768, 3072, "nn"),
+    ("g.fc2.d", 8192, 3072, 768, "nn"), ("g.lm.d", 8192, 768, 50304, "nn"),
+    ("g.qkv.w", 2304, 768, 8192, "tn"), ("g.proj.w", 768, 768, 8192, "tn"), ("g.fc.w", 3072, 768, 8192, "tn"),
+    ("g.fc2.w", 768, 3072, 8192, "tn"), ("g.lm.w", 50304, 768, 8192, "tn"),
+]
+LAYOUTS = {"nt": (False, False), "nn": (False, True), "tn": (True, True)}
+
+
+def dev():
+    return torch.device("cuda")
+
+
+def timed(fn, iters=20, warm=3):
+    """Mean time per call in us (HIP events around `iters` back-to-back calls)."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def median_rounds(fns, rounds=20, per=5):
+    """Interleaved rounds of several callables; median us per call of each."""
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    times = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, f in fns.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(per):
+                f()
+            e.record()
+            e.synchronize()
+            times[k].append(s.elapsed_time(e) / per * 1e3)
+    return {k: sorted(v)[len(v) // 2] for k, v in times.items()}
+
+
+def gemm_operands(M, N, K, lay):
+    a_km, b_kn = LAYOUTS[lay]
+    A = torch.randn((K, M) if a_km else (M, K), device=dev()).to(torch.bfloat16)
+    B = torch.randn((K, N) if b_kn else (N, K), device=dev()).to(torch.bfloat16)
+    C = torch.zeros(M, N, device=dev(), dtype=torch.float32 if lay == "tn" else torch.bfloat16)
+    return A, B, C
+
+
+def ours_gemm(A, B, C, M, N, K, lay, split=1):
+    a_km, b_kn = LAYOUTS[lay]
+    if lay == "tn" and os.environ.get("GEMM_TN_MODEL", "1") == "1":
+        return lambda: ops.linear_wgrad(A, B, C)  # the model's wgrad path (split-K choice, slabs + reduce)
+    epi = ops.EPI_ATOMIC_F32 if lay == "tn" else ops.EPI_STORE_BF16
+    return lambda: ops.gemm(A, B, C, M, N, K, a_km, b_kn, epi, split_k=split)
+
+
+def cmd_gemm(a):
+    if a.shapes:
+        shapes = [(n, int(m), int(nn), int(k), lay) for n, m, nn, k, lay in (s.split(":") for s in a.shapes.split(","))]
+    else:
+        shapes = GPT2_SHAPES if a.set == "gpt2" else WD_SHAPES
+    tot = {"ours": 0.0, "hipblaslt": 0.0}
+    for name, M, N, K, lay in shapes:
+        a_km, b_kn = LAYOUTS[lay]
+        A, B, C = gemm_operands(M, N, K, lay)
+        At, Bt = (A.t() if a_km else A), (B if b_kn else B.t())
+        med = median_rounds({"ours": ours_gemm(A, B, C, M, N, K, lay), "hipblaslt": lambda: torch.matmul(At, Bt)})
+        for k in tot:
+            tot[k] += med[k]
+        fl = 2.0 * M * N * K
+        print(f"{name:10s} M={M:6d} N={N:5d} K={K:6d} {lay}  ours {med['ours']:8.1f}us {fl / med['ours'] / 1e6:7.1f} "
+              f"TF/s | hipBLASLt {med['hipblaslt']:8.1f}us {fl / med['hipblaslt'] / 1e6:7.1f} TF/s", flush=True)
+    print(f"sum: ours {tot['ours']:.1f} us | hipBLASLt {tot['hipblaslt']:.1f} us")
+
+
+def cmd_kscan(a):
+    M, N = a.M, a.N
+    for K in [int(k) for k in a.Ks.split(",")]:
+        A, B, C = gemm_operands(M, N, K, a.layout)
+        t = median_rounds({"k": ours_gemm(A, B, C, M, N, K, a.layout, a.split)}, rounds=15)["k"]
+        print(f"{a.tag:10s} M={M} N={N} K={K:5d} {a.layout} split={a.split} {t:8.1f} us "
+              f"{2.0 * M * N * K / t / 1e6:7.1f} TF/s", flush=True)
+
+
+def cmd_pmc(a):
+    def bf(*s):
+        return torch.randn(*s, device=dev()).to(torch.bfloat16)
+
+    X, W1, dH1 = bf(16384, 896), bf(1024, 896), bf(16384, 1024)
+    H = torch.empty(16384, 1024, device=dev(), dtype=torch.bfloat16)
+    dX = torch.empty(16384, 896, device=dev(), dtype=torch.bfloat16)
+    dW = torch.zeros(1024, 896, device=dev())
+    A4, B4 = bf(4096, 4096), bf(4096, 4096)
+    C4 = torch.empty(4096, 4096, device=dev(), dtype=torch.bfloat16)
+    for _ in range(a.reps):
+        ops.linear_fwd(X, W1, None, "relu", out=H)                  # fwd1 (nt)
+        ops.linear_dgrad(dH1, W1, out=dX)                           # dgrad0 (nn, tr-read B)
+        ops.linear_wgrad(dH1, X, dW)                                # wgrad1 (tn, split-K)
+        ops.gemm(A4, B4, C4, 4096, 4096, 4096, False, False, ops.EPI_STORE_BF16)  # sq4096
+    torch.cuda.synchronize()
+    print("done")
+
+
+def cmd_attn(a):
+    B, T, H = a.B, a.T, a.H
+    d = H * 64
+    qkv = torch.randn(B * T, 3 * d, device=dev()).to(torch.bfloat16)
+    dO = torch.randn(B * T, d, device=dev()).to(torch.bfloat16)
+    O = torch.empty(B * T, d + 8, device=dev(), dtype=torch.bfloat16)
+    lse = torch.empty(B * H * T, device=dev())
+    delta = torch.empty_like(lse)
+    dqkv = torch.empty_like(qkv)
+    fl = 4.0 * B * H * T * T / 2 * 64  # causal: 2 products over T^2/2 forward, 5 backward
+    tf = timed(lambda: ops.attn_fwd(qkv, B, T, H, 0.125, O, lse))
+    tb = timed(lambda: ops.attn_bwd(qkv, O, dO, lse, delta, B, T, H, 0.125, dqkv))
+    print(f"ours  fwd {tf:8.1f} us {fl / tf / 1e6:7.1f} TF/s   bwd {tb:8.1f} us {2.5 * fl / tb / 1e6:7.1f} TF/s")
+    q, k, v = (qkv[:, i * d:(i + 1) * d].reshape(B, T, H, 64).transpose(1, 2).contiguous() for i in range(3))
+    q.requires_grad_(True), k.requires_grad_(True), v.requires_grad_(True)
+    go = dO.reshape(B, T, H, 64).transpose(1, 2).contiguous()
+    F = torch.nn.functional.scaled_dot_product_attention
+    try:
+        tf2 = timed(lambda: F(q, k, v, is_causal=True))
+        out = F(q, k, v, is_causal=True)
+        tb2 = timed(lambda: torch.autograd.grad(out, (q, k, v), go, retain_graph=True))
+        print(f"sdpa  fwd {tf2:8.1f} us {fl / tf2 / 1e6:7.1f} TF/s   "
+              f"bwd {tb2:8.1f} us {2.5 * fl / tb2 / 1e6:7.1f} TF/s")
+    except Exception as e:  # pragma: no cover
+        print("sdpa unavailable:", e)
+
+
+def cmd_nn(a):
+    M, C, V = 8192, 768, 50304
+    bf = dict(dtype=torch.bfloat16, device=dev())
+    x, dy, dx = torch.randn(M, C, **bf), torch.randn(M, C, **bf), torch.randn(M, C, **bf)
+    g, bta = torch.randn(C, **bf), torch.randn(C, **bf)
+    y = torch.empty(M, C, **bf)
+    mean, rstd = torch.empty(M, device=dev()), torch.empty(M, device=dev())
+    dg, db = torch.zeros(C, device=dev()), torch.zeros(C, device=dev())
+    ops.layernorm_fwd(x, C, g, bta, 1e-5, y, mean, rstd)
+    rows = [
+        ("layernorm_fwd", timed(lambda: ops.layernorm_fwd(x, C, g, bta, 1e-5, y, mean, rstd), 50),
+         2 * M * C * 2 + 8 * M),
+        ("layernorm_bwd (accumulate dx)",
+         timed(lambda: ops.layernorm_bwd(x, dy, C, g, mean, rstd, dx, dg, db, accumulate=True), 50),
+         4 * M * C * 2 + 8 * M),
+        ("add_bf16", timed(lambda: ops.add_bf16(x, dy, y), 50), 3 * M * C * 2),
+    ]
+    logits = torch.randn(M, V, **bf)
+    labels = torch.randint(0, 50257, (M,), device=dev())
+    loss = torch.zeros(1, device=dev())
+    rows.append(("softmax_xent (in place)",
+                 timed(lambda: ops.softmax_xent(logits, 50257, labels, 1.0 / M, loss), 10), 2 * M * V * 2))
+    for name, us, nbytes in rows:
+        print(f"{name:32s} {us:9.1f} us  {nbytes / us / 1e6:6.2f} TB/s")
+
+
+def cmd_emb(a):
+    from minips_amd.data.synthetic import CriteoSynth
+
+    B = a.batch
+    dense, keys, y = CriteoSynth(B, device=dev(), seed=1).next()
+    bounds = torch.tensor([0, 1 << 62], dtype=torch.int64, device=dev())
+    uniq, inv, counts = ops.unique_bucketize(keys.reshape(-1), bounds, 26)
+    U = int(counts.sum())
+    dX = torch.randn(B, 26 * 32, device=dev()).to(torch.bfloat16)
+    dw = torch.randn(B, device=dev())
+    g = torch.zeros(U, 36, device=dev())
+    full = timed(lambda: ops.wd_emb_backward(dX, dw, inv, 26, 32, g))
+    csr = ops.emb_build_csr(inv, 26, U)
+    build = timed(lambda: ops.emb_build_csr(inv, 26, U))
+    seg = timed(lambda: ops.wd_emb_backward(dX, dw, inv, 26, 32, g, csr=csr))
+    print(f"U={U} lookups={B * 26}: build+sum {full:.1f} us, csr build {build:.1f} us, zero+segment sum {seg:.1f} us")
+
+
+def cmd_plan(a):
+    from minips_amd.data.synthetic import CRITEO_KAGGLE_CARDS, CriteoSynth
+
+    B, cards = a.batch, CRITEO_KAGGLE_CARDS
+    F = len(cards)
+    keys = CriteoSynth(B, device=dev(), seed=1).next()[1]
+    bases = torch.tensor([sum(cards[:f]) for f in range(F)], device=dev())
+    bits = [max(1, (c - 1).bit_length()) for c in cards]
+    R = sum(cards)
+    t_sort = timed(lambda: ops.plan_sorted(keys, bases, bits, 402653189, R))
+    bounds = torch.tensor([0, R], device=dev())
+
+    def hashed():
+        (uniq, inv, counts, U), z = ops.unique_bucketize_n(keys.reshape(-1), bounds, F, 402653189, R,
+                                                           extra_zero_ints=2 * B * F, csr_counts=True)
+        ops.emb_build_csr(inv, F, B * F, zeroed=z, counts_ready=True)
+
+    print(f"B={B} F={F}: sort plan {t_sort:.1f} us | hash dedupe + CSR {timed(hashed):.1f} us")
+    for nb in (4, 8, 16, 24, 32):
+        t = timed(lambda: ops.plan_sorted(keys, bases, [nb] * F, 402653189, R))
+        print(f"  all columns at {nb:2d} bits ({(nb + 3) // 4} passes): {t:.1f} us")
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("gemm")
+    p.add_argument("--set", default=os.environ.get("GEMM_SET", "wd"), choices=["wd", "gpt2"])
+    p.add_argument("--shapes", default=os.environ.get("GEMM_SHAPES", ""))
+    p = sub.add_parser("kscan")
+    p.add_argument("--M", type=int, default=16384)
+    p.add_argument("--N", type=int, default=1024)
+    p.add_argument("--Ks", default="128,256,512,848,1024,2048,4096")
+    p.add_argument("--layout", default="nt", choices=list(LAYOUTS))
+    p.add_argument("--split", type=int, default=1)
+    p.add_argument("--tag", default="")
+    p = sub.add_parser("pmc")
+    p.add_argument("--reps", type=int, default=10)
+    p = sub.add_parser("attn")
+    p.add_argument("--B", type=int, default=8)
+    p.add_argument("--T", type=int, default=1024)
+    p.add_argument("--H", type=int, default=12)
+    sub.add_parser("nn")
+    for name in ("emb", "plan"):
+        sub.add_parser(name).add_argument("--batch", type=int, default=16384)
+    a = ap.parse_args(argv)
+    from minips_amd import _native
+
+    _native.kernels()
+    globals()["cmd_" + a.cmd](a)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,9 +1,10 @@
 #!/bin/bash
-# Generic A/B of environment knobs on the GPU box (one script for every knob sweep; the
-# round-1 per-experiment scripts were folded into it). Variants are ';'-separated env lists:
+# Generic A/B of environment knobs on the GPU box (one script for every knob sweep; the earlier
+# per-experiment scripts were folded into it, e.g. the GPT-2 wgrad sweep is
+# CMD='python tools/bench_models.py --model gpt2 --steps 10 --warmup 3' AB='...'). Variants are ';'-separated env lists:
 #   AB='MINIPS_GEMM_WGRAD=v1;MINIPS_GEMM_WGRAD=v2 MINIPS_SPLITK_SLAB=0' bash tools/gpu_ab.sh
 #   RUNS=3 STEPS=300 BENCH_ARGS='--batch 8192' AB='...' bash tools/gpu_ab.sh
-#   CMD='python tools/gemm_kscan.py --Ks 848' AB='MINIPS_GEMM_TILE=128;MINIPS_GEMM_TILE=256' bash tools/gpu_ab.sh
+#   CMD='python tools/bench_kernels.py kscan --Ks 848' AB='MINIPS_GEMM_TILE=128;MINIPS_GEMM_TILE=256' bash tools/gpu_ab.sh
 # With the default CMD (bench.py) it prints ms/step per run; otherwise the command's output tail.
 set -eo pipefail
 cd "$(dirname "$0")/.."

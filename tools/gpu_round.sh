@@ -1,12 +1,20 @@
 #!/bin/bash
-# One GPU-box pass: smoke, GPU tests, short bench, rocprofv3 kernel stats / trace, host-sync audit.
-#   bash tools/gpu_round.sh [all|smoke|test|bench|prof|trace|audit]
-# Every GPU step has its own time limit; any failure stops the script (set -e + &&).
+# One GPU-box pass; every GPU step has its own time limit and any failure stops the script.
+#   bash tools/gpu_round.sh [all|smoke|test|bench|prof|trace|audit|micro|models|models-prof]
+#     all          smoke + GPU tests + short bench + rocprofv3 kernel stats of the bench
+#     trace        kernel trace of the W&D bench per MINIPS_GRAPH mode in MODES (default "0"), with the
+#                  steady-state step breakdown (tools/prof_summary.py trace)
+#     audit        host issue time + host syncs per step at world 1 (the real path) and 4 / 8 (gloo, one card)
+#     micro        isolated GPT-2 kernels: every GEMM shape vs hipBLASLt, memory-bound kernels, attention
+#     models       bench lines of the other BASELINE configs (MODELS, default "mlp dlrm dlrm-10b gpt2")
+#     models-prof  rocprofv3 kernel stats of those model steps (MODELS)
+# Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, MODES.
 set -eo pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 STAGE=${1:-all}
+prof_env() { cd /tmp && export TMPDIR=/tmp && cd - > /dev/null; }
 if [[ $STAGE == all || $STAGE == smoke ]]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
   tail -3 gpurun_out/smoke.log
@@ -20,19 +28,46 @@ if [[ $STAGE == all || $STAGE == bench ]]; then
   tail -2 gpurun_out/bench.log
 fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
-  cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+  prof_env
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 3 ${BENCH_ARGS} > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
   find gpurun_out/prof -name "*kernel_stats.csv" | head -3
 fi
-if [[ $STAGE == trace ]]; then  # per-queue kernel timeline of the default step (tools/trace_steps.py)
-  cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace -o run -- python bench.py --steps 30 --warmup 5 ${BENCH_ARGS} > gpurun_out/trace.log 2>&1 || { tail -30 gpurun_out/trace.log; exit 1; }
+if [[ $STAGE == trace ]]; then
+  prof_env
+  for g in ${MODES:-0}; do
+    d=gpurun_out/trace_g$g
+    rm -rf $d
+    MINIPS_GRAPH=$g timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python bench.py --steps 30 --warmup 5 ${BENCH_ARGS} > $d.log 2>&1 || { tail -30 $d.log; exit 1; }
+    f=$(find $d -name "*kernel_trace.csv" | head -1)
+    echo "=== MINIPS_GRAPH=$g ($f)"
+    python tools/prof_summary.py trace "$f" --anchor adam_kernel --skip 8 --top ${TOP:-30} | tee $d.summary.txt
+  done
 fi
-if [[ $STAGE == audit ]]; then  # host issue time + host syncs per step at world 1 (the real path) and 4 / 8 (gloo, one card)
+if [[ $STAGE == audit ]]; then
   timeout -k 10 200 python bench.py --steps 200 --warmup 10 --sync-audit 50 > gpurun_out/audit_w1.txt 2>&1
   for w in 4 8; do
     MINIPS_SHARE_DEVICE=1 MINIPS_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
       --nproc-per-node $w --master-addr 127.0.0.1 --master-port 2950$w bench.py --gpus $w --steps 10 --warmup 3 \
       --batch 4096 --sync-audit 10 > gpurun_out/audit_w$w.txt 2>&1
+  done
+fi
+if [[ $STAGE == micro ]]; then
+  timeout -k 10 300 python tools/bench_kernels.py gemm --set gpt2 > gpurun_out/micro_gemm_gpt2.txt 2>&1
+  timeout -k 10 200 python tools/bench_kernels.py nn > gpurun_out/micro_nn.txt 2>&1
+  timeout -k 10 200 python tools/bench_kernels.py attn > gpurun_out/micro_attn.txt 2>&1
+fi
+if [[ $STAGE == models ]]; then
+  for m in ${MODELS:-mlp dlrm dlrm-10b gpt2}; do
+    timeout -k 10 300 python tools/bench_models.py --model $m --steps ${STEPS:-30} --warmup 5 > gpurun_out/bench_$m.log 2>&1 || { tail -20 gpurun_out/bench_$m.log; exit 1; }
+    grep "^{" gpurun_out/bench_$m.log | cut -c1-300
+  done
+fi
+if [[ $STAGE == models-prof ]]; then
+  prof_env
+  for m in ${MODELS:-mlp dlrm gpt2}; do
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$m -o run -- python tools/bench_models.py --model $m --steps 6 --warmup 2 > gpurun_out/prof_$m.log 2>&1 || { tail -20 gpurun_out/prof_$m.log; exit 1; }
+    f=$(find gpurun_out/prof_$m -name "*kernel_stats.csv" | head -1)
+    python tools/prof_summary.py stats $f 8 > gpurun_out/${m}_kernels.txt
+    head -25 gpurun_out/${m}_kernels.txt
   done
 fi

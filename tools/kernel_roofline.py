@@ -6,7 +6,7 @@ rocprofv3 kernel trace (``--kernel-trace --output-format csv``) of bench.py:
 
 Kernels are identified by name + grid size and given the FLOPs / bytes of their W&D call (batch
 16384, 26 x 32-d embeddings + 13 dense, MLP 896(ext)-1024-512-256-1, bias-folded K of 1032 / 520,
-weight-gradient split-K slabs); ``U`` = unique keys per batch (tools/wd_unique.py). Durations
+weight-gradient split-K slabs); ``U`` = unique keys per batch (--measure-U). Durations
 are medians over the steady steps (the first 3 steps are skipped). Bytes are the compulsory
 traffic (each operand read once, outputs written once), so TB/s is a lower bound on what the
 kernel moved. Peaks: 2.5 PFLOP/s dense bf16 MFMA, 8 TB/s HBM3E."""
@@ -70,12 +70,41 @@ def spec(U):
     ]
 
 
+def measure_unique(batches=20):
+    """Average unique-key count U per batch of bench.py's synthetic Criteo data (needs the GPU)."""
+    import os
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from minips_amd import ops
+    from minips_amd.data.synthetic import CriteoSynth
+    from minips_amd.models.widedeep import WideDeepConfig
+
+    dev = torch.device("cuda", 0)
+    cfg = WideDeepConfig()
+    data = CriteoSynth(B, cards=cfg.cards, device=dev, seed=1)
+    bounds = torch.tensor([0, sum(cfg.cards)], device=dev)
+    us = []
+    for _ in range(batches):
+        _, keys, _ = data.next()
+        us.append(int(ops.unique_bucketize_n(keys, bounds, keys.shape[1])[3].item()))
+    print(f"U mean {sum(us) / len(us):.0f} over {batches} batches of {keys.numel()} lookups (min {min(us)}, "
+          f"max {max(us)})")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("trace")
-    ap.add_argument("--U", type=float, required=True, help="unique keys per batch (tools/wd_unique.py)")
+    ap.add_argument("trace", nargs="?")
+    ap.add_argument("--U", type=float, help="unique keys per batch (--measure-U prints it)")
+    ap.add_argument("--measure-U", action="store_true", help="measure U on the GPU and exit")
     ap.add_argument("--skip", type=int, default=3, help="steps to skip")
     a = ap.parse_args()
+    if a.measure_U:
+        return measure_unique()
+    if not a.trace or a.U is None:
+        ap.error("trace and --U are required")
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if "gather_rows" in r["Kernel_Name"]]

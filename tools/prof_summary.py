@@ -1,11 +1,28 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --stats kernel_stats.csv: total time and the top kernels (per call and
-share), optionally divided by a step count."""
+"""rocprofv3 output summaries (one entry point):
+
+    python tools/prof_summary.py stats run_kernel_stats.csv [steps] [--top 25]
+        total kernel time and the top kernels (per call and share), divided by a step count
+    python tools/prof_summary.py pmc counter_collection.csv [...]
+        counters summed per (kernel, counter), with MFMA busy / CU busy when both were collected
+    python tools/prof_summary.py trace run_kernel_trace.csv [--anchor adam_kernel] [--skip 3]
+        steady-state step breakdown: the window runs from the ``skip``-th to the last occurrence of
+        the anchor kernel (one per step); prints wall ms per step, the union of busy intervals over
+        all queues (GPU busy), per-queue busy time and the kernels by device time per step -- the
+        numbers that tell an overlap problem (busy << wall) from a kernel problem (busy ~ wall)
+
+(A bare path as the first argument means ``stats``.) Per-kernel TFLOP/s and TB/s of the W&D step:
+tools/kernel_roofline.py.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
 import csv
 import sys
 
 
-def main(path, steps=1, top=25):
+def stats(path, steps=1, top=25):
     rows = list(csv.DictReader(open(path)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     print(f"total kernel time {tot / 1e6:.3f} ms ({tot / 1e6 / steps:.3f} ms per step over {steps} steps)")
@@ -16,5 +33,85 @@ def main(path, steps=1, top=25):
         print(f"{t / 1e6 / steps:9.3f} {c:6d} {t / 1e3 / c:9.1f} {100 * t / tot:6.2f}%  {r['Name'][:100]}")
 
 
+def pmc(paths):
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
+    for path in paths:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                tot[row.get("Kernel_Name", "?")[:90]][row["Counter_Name"]] += float(row["Counter_Value"])
+    for k, c in tot.items():
+        print(k)
+        for name in sorted(c):
+            print(f"    {name:30s} {c[name]:.4g}")
+        if c.get("SQ_BUSY_CU_CYCLES") and c.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+            print(f"    MFMA busy / CU busy            {c['SQ_VALU_MFMA_BUSY_CYCLES'] / c['SQ_BUSY_CU_CYCLES']:.3f}")
+
+
+def trace(a):
+    rows = list(csv.DictReader(open(a.trace)))
+    ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Queue_Id", "0"))
+          for r in rows]
+    ks.sort()
+    anchors = [s for s, e, n, q in ks if a.anchor in n]
+    if len(anchors) < a.skip + 2:
+        raise SystemExit(f"only {len(anchors)} '{a.anchor}' kernels in the trace")
+    lo, hi = anchors[a.skip], anchors[-1]
+    steps = len(anchors) - 1 - a.skip
+    win = [(max(s, lo), min(e, hi), n, q) for s, e, n, q in ks if e > lo and s < hi]
+    wall = (hi - lo) / steps / 1e6
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _, _ in sorted(win):
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        busy += cur_e - cur_s
+    per_q = collections.Counter()
+    per_k = collections.Counter()
+    calls = collections.Counter()
+    for s, e, n, q in win:
+        per_q[q] += e - s
+        short = n.split("(")[0][:110]
+        per_k[short] += e - s
+        calls[short] += 1
+    tot = sum(per_k.values())
+    print(f"steps {steps}  wall {wall:.4f} ms/step  GPU busy (union) {busy / steps / 1e6:.4f} ms/step  "
+          f"kernel sum {tot / steps / 1e6:.4f} ms/step")
+    print("per queue busy ms/step: " + ", ".join(f"q{q}={t / steps / 1e6:.4f}" for q, t in sorted(per_q.items())))
+    print(f"{'ms/step':>9} {'calls/step':>10} {'us/call':>8}  kernel")
+    for n, t in per_k.most_common(a.top):
+        c = calls[n]
+        print(f"{t / steps / 1e6:9.4f} {c / steps:10.2f} {t / c / 1e3:8.1f}  {n}")
+
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if argv and argv[0] not in ("stats", "pmc", "trace", "-h", "--help"):
+        argv.insert(0, "stats")
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("stats")
+    p.add_argument("path")
+    p.add_argument("steps", nargs="?", type=int, default=1)
+    p.add_argument("--top", type=int, default=25)
+    sub.add_parser("pmc").add_argument("paths", nargs="+")
+    p = sub.add_parser("trace")
+    p.add_argument("trace")
+    p.add_argument("--anchor", default="adam_kernel")
+    p.add_argument("--skip", type=int, default=3)
+    p.add_argument("--top", type=int, default=30)
+    a = ap.parse_args(argv)
+    if a.cmd == "stats":
+        stats(a.path, a.steps, a.top)
+    elif a.cmd == "pmc":
+        pmc(a.paths)
+    else:
+        trace(a)
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1)
+    main()

@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Diagnostics of the 1-GPU Wide&Deep step (bench.py's loop: LookaheadFeeder, next batch generated
+and planned on the planning stream every step). One entry point:
+
+    python tools/step_probe.py issue     host issue time per step vs wall time per step (no syncs
+                                         inside: issue < wall means GPU-bound)
+    python tools/step_probe.py cprofile  cProfile of the host side, top functions by own time
+    python tools/step_probe.py events    HIP events: step start -> sparse Get done (a Get segment much
+                                         longer than the gather kernel = the compute stream waited
+                                         for the planning stream)
+    python tools/step_probe.py ablation  feeder step vs a ring of pre-planned batches (+ the planning
+                                         stream's work issued beside / after / without bookkeeping).
+                                         Diagnostic only: the ring numbers are not valid benchmarks.
+STEPS (env) sets the step count.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _setup():
+    from minips_amd.data.synthetic import CriteoSynth
+    from minips_amd.models.feeder import LookaheadFeeder
+    from minips_amd.models.widedeep import WideDeep, WideDeepConfig
+    from minips_amd.ps.comm import Comm
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    comm = Comm(device=dev)
+    cfg = WideDeepConfig()
+    model = WideDeep(cfg, comm)
+    data = CriteoSynth(16384, cards=cfg.cards, device=dev, seed=1)
+    return comm, model, data, LookaheadFeeder(model, data, comm)
+
+
+def _time(fn, n, warm=40):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e3
+
+
+def cmd_issue(n):
+    _, _, _, feeder = _setup()
+    for _ in range(10):
+        feeder.step()
+    torch.cuda.synchronize()
+    for rep in range(3):
+        t0 = time.perf_counter()
+        for _ in range(n):
+            feeder.step()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        print(f"rep {rep}: host issue {(t1 - t0) / n * 1e3:.4f} ms/step, wall {(t2 - t0) / n * 1e3:.4f} ms/step",
+              flush=True)
+
+
+def cmd_cprofile(n):
+    import cProfile
+    import pstats
+
+    _, _, _, feeder = _setup()
+    for _ in range(5):
+        feeder.step()
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(n):
+        feeder.step()
+    pr.disable()
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(int(os.environ.get("TOP", "35")))
+
+
+def cmd_events(n):
+    _, model, _, feeder = _setup()
+    marks = []
+    orig = model.emb.get_source if hasattr(model.emb, "get_source") else None
+    orig_get = model.emb.get
+
+    def mark(out):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        marks[-1].append(ev)
+        return out
+
+    model.emb.get = lambda keys, plan=None: mark(orig_get(keys, plan=plan))
+    if orig is not None:  # one rank: the Get is folded into the assembly; mark after the source lookup
+        model.emb.get_source = lambda keys, plan=None: mark(orig(keys, plan=plan))
+    for _ in range(n + 10):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        marks.append([e0])
+        feeder.step()
+    torch.cuda.synchronize()
+    marks = marks[10:]
+    get_ms = sorted(m[0].elapsed_time(m[1]) for m in marks if len(m) > 1)
+    step_ms = sorted(marks[i][0].elapsed_time(marks[i + 1][0]) for i in range(len(marks) - 1))
+    med = lambda v: v[len(v) // 2]  # noqa: E731
+    print(f"step {med(step_ms):.4f} ms (median), step start -> Get done {med(get_ms):.4f} ms "
+          f"(p10 {get_ms[len(get_ms) // 10]:.4f}, p90 {get_ms[9 * len(get_ms) // 10]:.4f})")
+
+
+def cmd_ablation(n):
+    comm, model, data, feeder = _setup()
+    full = _time(feeder.step, n)
+    ring = []
+    for _ in range(int(os.environ.get("RING", "48"))):  # distinct batches keep the row traffic real
+        dense, keys, labels = data.next()
+        ring.append((dense, keys, labels, model.emb.plan(keys, csr=True)))
+    torch.cuda.synchronize()
+    plans = {id(b[1]): b[3] for b in ring}
+    model._take_plan = lambda k: plans[id(k)]
+    pos = [0]
+
+    def step():
+        d, k, y, _ = ring[pos[0] % len(ring)]
+        pos[0] += 1
+        model.train_step(d, k, y)
+
+    ps = comm.plan_stream()
+
+    def plus_planning():
+        with torch.cuda.stream(ps):
+            k = data.next()[1]
+        model.emb.plan_async(k, csr=True, keys_on_plan_stream=True)
+        step()
+
+    def plus_data():
+        with torch.cuda.stream(ps):
+            data.next()
+        step()
+
+    def then_planning():
+        step()
+        with torch.cuda.stream(ps):
+            k = data.next()[1]
+        model.emb.plan_async(k, csr=True, keys_on_plan_stream=True)
+
+    def plus_bare_planning():  # the same kernels without plan_async's stream bookkeeping
+        with torch.cuda.stream(ps):
+            k = data.next()[1]
+            model.emb._start_plan(k, csr=True, exchange=False)
+        step()
+
+    fixed = _time(step, n)
+    both, data_only, after, bare = (_time(f, n) for f in (plus_planning, plus_data, then_planning, plus_bare_planning))
+    print(f"feeder step {full:.4f} ms | pre-planned ring of {len(ring)} batches {fixed:.4f} ms | data + planning "
+          f"cost {full - fixed:.4f} ms/step | ring + discarded planning {both:.4f} ms | ring + discarded batch "
+          f"generation only {data_only:.4f} ms | planning issued after the step {after:.4f} ms | ring + planning "
+          f"kernels without record_stream/events {bare:.4f} ms")
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("cmd", choices=["issue", "cprofile", "events", "ablation"])
+    a = ap.parse_args(argv)
+    n = int(os.environ.get("STEPS", "300"))
+    globals()["cmd_" + a.cmd](n)
+
+
+if __name__ == "__main__":
+    main()
