@@ -121,14 +121,25 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
                           epi == minips_k::kEpiGeluGradBf16;
   if (needs_mask) TORCH_CHECK(mask_p, "this epilogue needs mask/aux");
   float* colsum_p = opt_ptr<float>(colsum, at::kFloat, "colsum");
-  if (colsum_p) TORCH_CHECK(colsum->numel() >= N, "colsum too short");
+  if (epi == minips_k::kEpiXentStatsBf16) {
+    // colsum = the softmax partials [M][ceil(N/64)] float2, seg = the vocabulary (valid columns)
+    ldmask = (int)((N + 63) / 64);
+    TORCH_CHECK(colsum_p && colsum->is_contiguous() && colsum->numel() >= M * ldmask * 2 && seg > 0 && seg <= N &&
+                    batch <= 1 && split_k <= 1,
+                "xent-stats epilogue: stats of >= M * ceil(N/64) * 2 floats, 0 < seg (vocab) <= N, no batch/split-K");
+  } else if (colsum_p) {
+    TORCH_CHECK(colsum->numel() >= N, "colsum too short");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
   static const bool use_slab = [] {
     const char* e = std::getenv("MINIPS_SPLITK_SLAB");
     return !e || std::atoi(e) != 0;
   }();
   at::Tensor slab;
-  if (use_slab && split_k > 1 && batch <= 1 && epi == minips_k::kEpiAtomicF32 && N % 4 == 0)
+  if (epi == minips_k::kEpiStoreBf16 && split_k > 1)
+    TORCH_CHECK(batch <= 1 && N % 4 == 0 && ldc % 4 == 0, "split-K bf16 store: no batch, N % 4 == 0, ldc % 4 == 0");
+  if ((use_slab || epi == minips_k::kEpiStoreBf16) && split_k > 1 && batch <= 1 &&
+      (epi == minips_k::kEpiAtomicF32 || epi == minips_k::kEpiStoreBf16) && N % 4 == 0)
     slab = at::empty({split_k * M * N}, A.options().dtype(at::kFloat));  // caching allocator, stream-ordered
   minips_k::gemm_bf16_batched(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb,
                               (int)ldc, a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p, (float)alpha,
@@ -824,6 +835,24 @@ void softmax_xent(at::Tensor& logits, int64_t V, const at::Tensor& labels, doubl
                          (float)scale, ptr<float>(loss_sum), c, stream_of(logits));
 }
 
+void xent_from_stats(at::Tensor& logits, int64_t V, const at::Tensor& stats, const at::Tensor& labels, double scale,
+                     at::Tensor& loss_sum, const c10::optional<at::Tensor>& correct) {
+  check_gpu(logits, "logits");
+  check_gpu(labels, "labels");
+  check_gpu(stats, "stats");
+  check_dtype(logits, at::kBFloat16, "logits");
+  check_dtype(labels, at::kLong, "labels");
+  check_dtype(stats, at::kFloat, "stats");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous() && logits.size(1) >= V && labels.numel() == logits.size(0),
+              "xent_from_stats shapes");
+  const int64_t M = logits.size(0), nparts = (logits.size(1) + 63) / 64;
+  TORCH_CHECK(stats.is_contiguous() && stats.numel() >= M * nparts * 2, "xent_from_stats: stats [M][ceil(ld/64)][2]");
+  float* c = opt_ptr<float>(correct, at::kFloat, "correct");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  minips_k::xent_from_stats(ptr<bf16_t>(logits), (int)logits.size(1), M, (int)V, ptr<float>(stats), (int)nparts,
+                            ptr<int64_t>(labels), (float)scale, ptr<float>(loss_sum), c, stream_of(logits));
+}
+
 void causal_softmax_fwd(const at::Tensor& S, int64_t T, at::Tensor& P) {
   check_gpu(S, "S");
   check_gpu(P, "P");
@@ -1296,6 +1325,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("softmax_xent", &softmax_xent);
+  m.def("xent_from_stats", &xent_from_stats);
   m.def("causal_softmax_fwd", &causal_softmax_fwd);
   m.def("causal_softmax_bwd", &causal_softmax_bwd);
   m.def("gelu_bwd", &gelu_bwd);

@@ -160,8 +160,8 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
           float x = v + bias;
           float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
           ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
-        } else if (EPI == kEpiStoreBf16 || EPI == kEpiPermRowsBf16) {
-          ((bf16_t*)ep.C)[off] = f2bf(v);
+        } else if (EPI == kEpiStoreBf16 || EPI == kEpiPermRowsBf16 || EPI == kEpiXentStatsBf16) {
+          ((bf16_t*)ep.C)[off] = f2bf(v);  // (kEpiXentStatsBf16: the launcher takes the staged path)
         } else if (EPI == kEpiBiasGeluAuxBf16) {
           const float x = v + bias;
           const float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
@@ -220,7 +220,7 @@ __device__ __forceinline__ float epi_apply(float v, float bias, float m, bf16_t*
     return v * gp;
   }
   if (EPI == kEpiReluMaskBf16) return m > 0.f ? v : 0.f;
-  return v;  // kEpiStoreBf16 / kEpiPermRowsBf16 / kEpiStoreF32
+  return v;  // kEpiStoreBf16 / kEpiPermRowsBf16 / kEpiXentStatsBf16 / kEpiStoreF32
 }
 
 template <int EPI, int MR>
@@ -332,6 +332,30 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
             csum[2 * e] += __uint_as_float(pk[e] << 16);
             csum[2 * e + 1] += __uint_as_float(pk[e] & 0xffff0000u);
           }
+        }
+        if (EPI == kEpiXentStatsBf16) {
+          // softmax partial of this wave's 64 columns of `row` from the ROUNDED logits (the
+          // gradient pass exponentiates the same bf16 values): the row's 8 lanes each fold their
+          // 8 columns, then merge over lane bits 0..2 (all lanes take part in the shuffles)
+          constexpr float kL2E = 1.4426950408889634f;
+          float y[8], mx = -1.0e30f, sm = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xv = (e & 1) ? __uint_as_float(pk[e >> 1] & 0xffff0000u) : __uint_as_float(pk[e >> 1] << 16);
+            y[e] = col + e < ep.seg ? xv * kL2E : -1.0e30f;
+            mx = fmaxf(mx, y[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sm += col + e < ep.seg ? __builtin_amdgcn_exp2f(y[e] - mx) : 0.f;
+#pragma unroll
+          for (int o = 1; o < 8; o <<= 1) {
+            const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(sm, o, 64);
+            const float mn = fmaxf(mx, m2);
+            sm = sm * __builtin_amdgcn_exp2f(mx - mn) + s2 * __builtin_amdgcn_exp2f(m2 - mn);
+            mx = mn;
+          }
+          if ((lane & 7) == 0 && row_ok && nb < N)
+            reinterpret_cast<float2*>(ep.colsum)[(int64_t)row * ep.ldmask + nb / 64] = make_float2(mx, sm);
         }
         if (!row_ok) continue;
         // (kEpiPermRowsBf16 with seg % 8 == 0: a lane's 8 columns never cross a segment)
@@ -850,6 +874,7 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
     }
     return nsplit;
   }
+  if (EPI == kEpiXentStatsBf16) throw std::runtime_error("gemm: the xent-stats epilogue needs the v2 kernel");
   // BK=64 halves the barriers per FLOP; short K chunks keep BK=32 (less tail waste).
   const int kper = (K + split_k - 1) / split_k;
   static const int forced = [] {
@@ -886,6 +911,12 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
     MINIPS_EPI_CASE(AKM, BKN, kEpiGeluGradBf16)                                  \
     MINIPS_EPI_CASE(AKM, BKN, kEpiPermRowsBf16)                                  \
     MINIPS_EPI_CASE(AKM, BKN, kEpiAccumF32)                                      \
+    case kEpiXentStatsBf16:                                                      \
+      if constexpr (!AKM && !BKN) {                                              \
+        nsplit = launch<false, false, kEpiXentStatsBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); \
+        break;                                                                   \
+      }                                                                          \
+      [[fallthrough]];                                                           \
     default:                                                                     \
       throw std::runtime_error("gemm: unknown epilogue " + std::to_string(epi)); \
   }
@@ -929,6 +960,28 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, int nsplit,
   }
 }
 
+// out_bf16[r][c] (ldc) = sum_s slab[s][r][c]: the split-K form of a plain bf16-output GEMM (a long-K
+// dgrad such as GPT-2's LM head, dh = dlogits wte with K = 50304 and only 8192 x 768 outputs)
+__global__ void splitk_reduce_bf16_kernel(const float* __restrict__ slab, int nsplit, int M, int N,
+                                          bf16_t* __restrict__ out, int ldc) {
+  const int n4 = N >> 2;
+  const int64_t total = (int64_t)M * n4, plane = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / n4;
+    const int c = (int)(i - r * n4) * 4;
+    const float* p = slab + r * N + c;
+    float4 a = *reinterpret_cast<const float4*>(p);
+    for (int z = 1; z < nsplit; ++z) {
+      const float4 b = *reinterpret_cast<const float4*>(p + z * plane);
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    *reinterpret_cast<uint2*>(out + r * ldc + c) = make_uint2(pack_bf2(a.x, a.y), pack_bf2(a.z, a.w));
+  }
+}
+
 void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                        bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
                        float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
@@ -937,12 +990,19 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return;
   if (epi == kEpiPermRowsBf16 && (!perm || seg <= 0 || seg % 8 || N % seg || batch != 1 || split_k > 1))
     throw std::runtime_error("gemm: the permuted-rows epilogue needs perm, seg % 8 == 0, N % seg == 0, no batch");
+  if (epi == kEpiXentStatsBf16 &&
+      (!colsum || seg <= 0 || seg > N || ldmask < (N + 63) / 64 || a_km || b_kn || batch != 1 || split_k > 1 ||
+       gemm_impl() != 2 || !kLdsEpilogue))
+    throw std::runtime_error("gemm: the xent-stats epilogue needs stats [M][ceil(N/64)] float2, 0 < vocab <= N, "
+                             "the nt layout, no batch / split-K, the v2 kernel with the staged epilogue");
   if (split_k < 1) split_k = 1;
-  if (split_k > 1 && epi != kEpiAtomicF32) throw std::runtime_error("gemm: split_k needs the atomic epilogue");
+  if (split_k > 1 && epi != kEpiAtomicF32 && !(epi == kEpiStoreBf16 && slab))
+    throw std::runtime_error("gemm: split_k needs the atomic epilogue (or a plain bf16 store with a slab)");
   if (batch > 1 && (mask || colsum)) throw std::runtime_error("gemm: batched mode has no mask/colsum epilogue");
   if (inner < 1) inner = 1;
   int nsplit = 1;
   if (slab && split_k > 1 && batch == 1 && N % 4 == 0) {
+    const bool bf16_out = epi == kEpiStoreBf16;
     // split-K without atomics: every K slice stores its partial tile into its own slab plane,
     // one streaming kernel adds the planes into C (measured faster than fp32 atomics)
     EpiArgs sp{slab, N, nullptr, nullptr, 0, nullptr, alpha, 1, 0, 0, 0, 0, 0, 0, (int64_t)M * N, nullptr, 0};
@@ -958,8 +1018,12 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
       MINIPS_GEMM_EPI_DISPATCH(true, false)
     }
     MINIPS_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(splitk_reduce_kernel, grid_for((int64_t)M * (N / 4), 256, 4096), 256, 0, s, slab, nsplit, M, N,
-                       (float*)C, ldc);
+    if (bf16_out)
+      hipLaunchKernelGGL(splitk_reduce_bf16_kernel, grid_for((int64_t)M * (N / 4), 256, 4096), 256, 0, s, slab, nsplit,
+                         M, N, (bf16_t*)C, ldc);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel, grid_for((int64_t)M * (N / 4), 256, 4096), 256, 0, s, slab, nsplit, M,
+                         N, (float*)C, ldc);
     MINIPS_HIP_CHECK(hipGetLastError());
     return;
   }

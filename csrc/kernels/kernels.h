@@ -28,6 +28,11 @@ enum GemmEpilogue {
   // not split over K (every output element has exactly one writer), e.g. GPT-2's LM-head weight
   // gradient (38.6M fp32 outputs: memory-side atomics cost it 1.75 ms/step)
   kEpiAccumF32 = 10,
+  // C bf16 = acc (LM-head logits) plus softmax partials for the cross-entropy: for every row and
+  // every 64-column wave block, (max, sum 2^(y - max)) over its valid columns (< seg = vocab) in
+  // log2 units (y = bf16(acc) * log2 e), as a float2 at colsum[row * ldmask + col0 / 64]
+  // (ldmask = ceil(N / 64)); xent_from_stats then streams the gradient without a row reduction
+  kEpiXentStatsBf16 = 11,
 };
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
@@ -204,6 +209,11 @@ void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t
                    const float* mean, const float* rstd, bf16_t* dx, int lddx, float* dgamma, float* dbeta,
                    float* partial, bool accumulate_dx, hipStream_t s);
 // In place: logits [M, ld] bf16 become (softmax - onehot) * scale; loss_sum += sum CE.
+// Cross-entropy from the LM-head GEMM's kEpiXentStatsBf16 partials: lse per row from the [M][nparts]
+// float2 partials, loss_sum += sum CE (correct += argmax hits), then logits[:, :V] <- (softmax -
+// onehot) * scale and logits[:, V:ld) <- 0 in one streaming pass.
+void xent_from_stats(bf16_t* logits, int ld, int64_t M, int V, const float* stats, int nparts, const int64_t* labels,
+                     float scale, float* loss_sum, float* correct, hipStream_t s);
 void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,
                   float* correct, hipStream_t s);
 void causal_softmax_fwd(const float* S, int64_t rows, int T, bf16_t* P, hipStream_t s);

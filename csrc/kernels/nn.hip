@@ -462,6 +462,97 @@ __global__ __launch_bounds__(256) void softmax_xent_small_kernel(bf16_t* __restr
   }
 }
 
+// Cross-entropy from the LM-head GEMM's per-64-column softmax partials (kEpiXentStatsBf16): the
+// row reduction already happened in the GEMM epilogue, so this is a pure stream -- one read and one
+// write of the logits at full occupancy (256-thread blocks, few VGPRs, no row in registers):
+//   1. lse of the row from its nparts float2 partials (a strided merge + one block reduction)
+//   2. the label's logit read, the loss / hit folded into the block's thread-0 accumulators
+//   3. g = (2^(x L2E - lse) - onehot) * scale over 8-column chunks, 4 chunks in flight per thread;
+//      columns [V, ld) are zeroed
+// A block walks rows r = blockIdx.x + k * gridDim.x (one loss atomic per block).
+constexpr int kXsThreads = 256, kXsUnroll = 4;
+__global__ __launch_bounds__(kXsThreads) void xent_from_stats_kernel(bf16_t* __restrict__ logits, int ld, int64_t M,
+                                                                     int V, const float2* __restrict__ stats,
+                                                                     int nparts, const int64_t* __restrict__ labels,
+                                                                     float scale, float* loss_sum, float* correct) {
+  __shared__ float red_m[kXsThreads / 64], red_s[kXsThreads / 64];
+  const float L2E = 1.4426950408889634f;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nch = ld >> 3;
+  float loss_acc = 0.f, hit_acc = 0.f;
+  for (int64_t r = blockIdx.x; r < M; r += gridDim.x) {
+    bf16_t* row = logits + r * ld;
+    const float2* st = stats + r * nparts;
+    float m = -1.0e30f, sm = 0.f;
+    for (int p = threadIdx.x; p < nparts; p += kXsThreads) {
+      const float2 v = st[p];
+      lse_merge(m, sm, v.x, v.y);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lse_merge(m, sm, __shfl_xor(m, o, 64), __shfl_xor(sm, o, 64));
+    const int64_t lab = labels[r];
+    const bool has_lab = lab >= 0 && lab < V;
+    float zl = 0.f;
+    if (threadIdx.x == 0 && has_lab) zl = bf2f(row[lab]);  // before any thread rewrites the row
+    __syncthreads();  // the previous row's readers of red_* are done
+    if (lane == 0) {
+      red_m[w] = m;
+      red_s[w] = sm;
+    }
+    __syncthreads();
+    float M2 = red_m[0], S2 = red_s[0];
+#pragma unroll
+    for (int i = 1; i < kXsThreads / 64; ++i) lse_merge(M2, S2, red_m[i], red_s[i]);
+    const float lse2 = M2 + __log2f(S2);
+    if (threadIdx.x == 0 && has_lab) {
+      loss_acc += lse2 / L2E - zl;
+      hit_acc += zl * L2E >= M2 ? 1.f : 0.f;
+    }
+    const int lch = has_lab ? (int)(lab >> 3) : -1, lq = (int)(lab & 7);
+    for (int c0 = threadIdx.x; c0 < nch; c0 += kXsThreads * kXsUnroll) {
+      uint4 v[kXsUnroll];
+#pragma unroll
+      for (int u = 0; u < kXsUnroll; ++u) {
+        const int ch = c0 + u * kXsThreads;
+        v[u] = ch < nch ? *reinterpret_cast<const uint4*>(row + ch * 8) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < kXsUnroll; ++u) {
+        const int ch = c0 + u * kXsThreads;
+        if (ch >= nch) continue;
+        uint32_t o[4];
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+          const int c = ch * 8 + 2 * q2;
+          float g0 = c < V ? __builtin_amdgcn_exp2f(u4elem(v[u], 2 * q2) * L2E - lse2) * scale : 0.f;
+          float g1 = c + 1 < V ? __builtin_amdgcn_exp2f(u4elem(v[u], 2 * q2 + 1) * L2E - lse2) * scale : 0.f;
+          if (ch == lch) {  // the -onehot term, folded before rounding
+            if (lq == 2 * q2) g0 -= scale;
+            if (lq == 2 * q2 + 1) g1 -= scale;
+          }
+          o[q2] = pack_bf2(g0, g1);
+        }
+        *reinterpret_cast<uint4*>(row + ch * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(loss_sum, loss_acc);
+    if (correct) atomicAdd(correct, hit_acc);
+  }
+}
+
+void xent_from_stats(bf16_t* logits, int ld, int64_t M, int V, const float* stats, int nparts, const int64_t* labels,
+                     float scale, float* loss_sum, float* correct, hipStream_t s) {
+  if (M <= 0) return;
+  if (ld % 8 || V <= 0 || V > ld || nparts <= 0) throw std::runtime_error("xent_from_stats: ld % 8 == 0, 0 < V <= ld");
+  // ~8 blocks of 4 waves per CU at full occupancy; each block walks M / grid rows
+  const int grid = (int)std::min<int64_t>(M, 2048);
+  hipLaunchKernelGGL(xent_from_stats_kernel, grid, kXsThreads, 0, s, logits, ld, M, V,
+                     reinterpret_cast<const float2*>(stats), nparts, labels, scale, loss_sum, correct);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,
                   float* correct, hipStream_t s) {
   if (M <= 0) return;

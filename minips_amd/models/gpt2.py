@@ -15,7 +15,8 @@ Compute path (all gfx950 kernels from minips_amd.ops, no autograd):
   gemm + add_bf16             x_mid = x + O W_o^T
   gemm (GELU-aux epilogue)    g = gelu(ln2 W_fc^T), pre-activation u saved
   gemm + add_bf16             x_next = x_mid + g W_proj^T
-  gemm + softmax_xent         logits = ln_f(x) wte^T, fused softmax-CE forward/backward in place
+  gemm (xent-stats epilogue)  logits = ln_f(x) wte^T (bf16) + per-64-column softmax partials
+  xent_from_stats             lse from the partials, (softmax - onehot) / (B T) in place (one pass)
 The backward mirrors it with dgrad/wgrad GEMMs (GELU-grad epilogue), attn_bwd (recomputes P per
 tile; dQ and dK/dV sweeps), layernorm_bwd (accumulating into the residual gradient) and embed_bwd.
 """
@@ -56,6 +57,15 @@ class GPT2Config:
     @property
     def vocab_pad(self):
         return align(self.vocab, 64)
+
+
+# LM-head cross-entropy: "stats" (GEMM epilogue softmax partials + streaming gradient pass) or
+# "rowwise" (plain GEMM + block-per-row softmax_xent)
+_XENT = os.environ.get("MINIPS_GPT2_XENT", "stats")
+_LM_DGRAD_SPLIT = int(os.environ.get("MINIPS_LM_DGRAD_SPLIT", "4"))
+# LM-head GEMMs (logits, dgrad, wte wgrad): "ours" (gemm.hip + the xent-stats epilogue) or "lib"
+# (hipBLASLt through torch for these three plain GEMMs; the CPU reference path always uses ours)
+_LM_GEMM = os.environ.get("MINIPS_LM_GEMM", "ours")
 
 
 class GPT2:
@@ -130,6 +140,7 @@ class GPT2:
                 g=[ext_activation(M, 4 * d, dev) for _ in range(nl)],     # GELU out (+ ones)
                 hf=ext_activation(M, d, dev), stf=(torch.empty(M, **f32), torch.empty(M, **f32)),
                 logits=torch.empty(M, c.vocab_pad, **bf),
+                xstats=torch.empty(M * ((c.vocab_pad + 63) // 64) * 2, **f32),  # LM-head softmax partials
                 delta=torch.empty(B * H * T, **f32),
                 tmp=torch.empty(M, d, **bf), dx=torch.empty(M, d, **bf), dh=torch.empty(M, d, **bf),
                 dqkv=torch.empty(M, 3 * d, **bf), dao=torch.empty(M, d, **bf), du=torch.empty(M, 4 * d, **bf),
@@ -169,16 +180,33 @@ class GPT2:
         ops.layernorm_fwd(x[-1], d, v(P, "lnf_g"), v(P, "lnf_b"), 1e-5, hf, mf, rf)
         wte = v(P, "wte")
         logits = b["logits"]
-        ops.gemm(hf[:, :d], wte, logits, M, c.vocab_pad, d, False, False, ops.EPI_STORE_BF16)
         b["loss"].zero_()
-        ops.softmax_xent(logits, c.vocab, targets.reshape(-1), 1.0 / (M * self.comm.world), b["loss"])
+        if _LM_GEMM == "lib" and logits.is_cuda:  # hipBLASLt for the plain LM-head GEMM, then the row-wise softmax-xent
+            torch.matmul(hf[:, :d], wte.t(), out=logits)
+            ops.softmax_xent(logits, c.vocab, targets.reshape(-1), 1.0 / (M * self.comm.world), b["loss"])
+        elif _XENT == "stats":  # softmax partials in the LM-head GEMM epilogue, then one streaming pass
+            ops.lm_head_xent(hf[:, :d], wte, logits, b["xstats"], c.vocab, targets.reshape(-1),
+                             1.0 / (M * self.comm.world), b["loss"])
+        else:  # plain GEMM + the block-per-row softmax-xent (row reduction + gradient in one kernel)
+            ops.gemm(hf[:, :d], wte, logits, M, c.vocab_pad, d, False, False, ops.EPI_STORE_BF16)
+            ops.softmax_xent(logits, c.vocab, targets.reshape(-1), 1.0 / (M * self.comm.world), b["loss"])
         # ---- backward. Weight gradients fork onto a side stream beside the dgrad chain; before the
         # chain overwrites a buffer a forked wgrad reads (dx, du, dqkv), it waits for that wgrad.
         side = self._side
-        with side.fork():
-            ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"))
         dh = b["dh"]
-        ops.gemm(logits, wte, dh, M, d, c.vocab_pad, False, True, ops.EPI_STORE_BF16)
+        if _LM_GEMM == "lib" and logits.is_cuda:
+            # plain GEMMs with one operand streamed from HBM (the 824 MB dlogits): hipBLASLt's larger
+            # tiles / split-K schedule measured 1.6x ours here (profiles/r3/lm_head_gemm.txt); the
+            # weight gradient accumulates in fp32 (addmm out_dtype), the dgrad writes bf16
+            gw = v(G, "wte")
+            with side.fork():
+                torch.addmm(gw, logits.t(), hf[:, :d], out_dtype=torch.float32, out=gw)
+            torch.matmul(logits, wte, out=dh)
+        else:
+            with side.fork():
+                ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"))
+            # long K (the vocabulary), few outputs: split-K into fp32 slabs + one bf16 reduce
+            ops.gemm(logits, wte, dh, M, d, c.vocab_pad, False, True, ops.EPI_STORE_BF16, split_k=_LM_DGRAD_SPLIT)
         dx = b["dx"]
         ops.layernorm_bwd(x[-1], dh, d, v(P, "lnf_g"), mf, rf, dx, v(G, "lnf_g"), v(G, "lnf_b"))
         ev_du = ev_dqkv = None

@@ -24,6 +24,8 @@ EPI_BIAS_GELU_BF16 = 6
 EPI_BIAS_GELU_AUX_BF16 = 7  # C = gelu(u), mask(aux) = u  (pre-activation saved for backward)
 EPI_GELU_GRAD_BF16 = 8      # C = acc * gelu'(mask)
 EPI_PERM_ROWS_BF16 = 9      # C rows of `seg` columns permuted by `perm` (embedding dgrad in planner order)
+EPI_XENT_STATS_BF16 = 11    # C = acc (bf16 logits) + per-64-column softmax partials into colsum (seg = vocab)
+_L2E = 1.4426950408889634
 
 
 def _gelu_grad(u):
@@ -71,6 +73,16 @@ def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None,
         C[:M, :N] = acc.to(torch.bfloat16)
     elif epi == EPI_PERM_ROWS_BF16:
         C.view(-1, seg)[perm[: M * (N // seg)].long()] = acc.to(torch.bfloat16).reshape(-1, seg)
+    elif epi == EPI_XENT_STATS_BF16:
+        out = acc.to(torch.bfloat16)
+        C[:M, :N] = out
+        npart = (N + 63) // 64
+        y = torch.full((M, npart * 64), -1.0e30)
+        y[:, :seg] = out[:, :seg].float() * _L2E
+        y = y.view(M, npart, 64)
+        mx = y.amax(2)
+        sm = torch.where(y > -1.0e29, torch.exp2(y - mx[..., None]), torch.zeros_like(y)).sum(2)
+        colsum.view(-1)[: M * npart * 2] = torch.stack([mx, sm], 2).reshape(-1)
     elif epi == EPI_RELU_MASK_BF16:
         out = torch.where(mask[:M, :N].float() > 0, acc, torch.zeros_like(acc)).to(torch.bfloat16)
         C[:M, :N] = out
@@ -731,6 +743,37 @@ def softmax_xent(logits, V, labels, scale, loss_sum, correct=None):
     p[torch.arange(z.shape[0]), labels] -= 1.0
     logits[:, :V] = (p * scale).to(torch.bfloat16)
     return logits
+
+
+def xent_from_stats(logits, V, stats, labels, scale, loss_sum, correct=None):
+    """softmax_xent with the row reduction taken from the LM-head GEMM's EPI_XENT_STATS_BF16
+    partials ``stats`` [M, ceil(ld/64), 2]: in place logits[:, :V] <- (softmax - onehot) * scale,
+    logits[:, V:] <- 0; loss_sum += sum CE (correct += argmax hits)."""
+    if _gpu(logits):
+        kernels().xent_from_stats(logits, int(V), stats, labels, float(scale), loss_sum, correct)
+        return logits
+    M = logits.shape[0]
+    st = stats.reshape(-1)[: M * ((logits.shape[1] + 63) // 64) * 2].view(M, -1, 2)
+    mx = st[..., 0].amax(1)
+    lse2 = mx + torch.log2((st[..., 1] * torch.exp2(st[..., 0] - mx[:, None])).sum(1))
+    z = logits[:, :V].float()
+    zl = z.gather(1, labels[:, None]).squeeze(1)
+    loss_sum += (lse2 / _L2E - zl).sum()
+    if correct is not None:
+        correct += (zl * _L2E >= mx).float().sum()
+    p = torch.exp2(z * _L2E - lse2[:, None])
+    p[torch.arange(M), labels] -= 1.0
+    logits[:, :V] = (p * scale).to(torch.bfloat16)
+    logits[:, V:] = 0
+    return logits
+
+
+def lm_head_xent(h, w, logits, stats, V, labels, scale, loss_sum):
+    """logits = h w^T (bf16, [M, Vpad]) with the softmax partials in the GEMM epilogue, then the
+    in-place cross-entropy gradient (xent_from_stats): the logits are read once more, not twice."""
+    M, K = h.shape[0], w.shape[1]
+    gemm(h, w, logits, M, logits.shape[1], K, False, False, EPI_XENT_STATS_BF16, colsum=stats, seg=V)
+    return xent_from_stats(logits, V, stats, labels, scale, loss_sum)
 
 
 def causal_softmax_fwd(S, T, P):

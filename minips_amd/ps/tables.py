@@ -920,7 +920,8 @@ class SparseTable:
         gate). None when the rows must be gathered (several ranks, hash / bf16 / fp64 tables)."""
         if not (self.comm.world == 1 and self.comm.device.type == "cuda" and type(self)._serve_index is
                 SparseTable._serve_index and self.shard.dtype == torch.float32
-                and self.pull_dtype == torch.bfloat16 and _FUSED_ASSEMBLE):
+                and self.pull_dtype == torch.bfloat16 and _FUSED_ASSEMBLE
+                and getattr(self, "pipe", None) is not None):  # (the asynchronous one-sided table: no pipe)
             return None
         if plan is None:
             plan = self.plan(keys)

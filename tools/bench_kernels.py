@@ -6,6 +6,7 @@
     python tools/bench_kernels.py kscan --M 16384 --N 1024 --layout nt
                                         time vs K at fixed M, N: fixed cost vs per-K-step cost
     python tools/bench_kernels.py pmc   model-shape GEMMs back to back (for rocprofv3 --pmc passes)
+    python tools/bench_kernels.py one --shape name:M:N:K:layout [--lib]   one shape, repeated (--pmc target)
     python tools/bench_kernels.py attn  fused causal attention vs torch SDPA
     python tools/bench_kernels.py nn    GPT-2 memory-bound kernels (LayerNorm, add, softmax-xent): TB/s
     python tools/bench_kernels.py emb   W&D embedding backward on a real Criteo-shaped plan
@@ -107,13 +108,33 @@ def cmd_gemm(a):
         a_km, b_kn = LAYOUTS[lay]
         A, B, C = gemm_operands(M, N, K, lay)
         At, Bt = (A.t() if a_km else A), (B if b_kn else B.t())
-        med = median_rounds({"ours": ours_gemm(A, B, C, M, N, K, lay), "hipblaslt": lambda: torch.matmul(At, Bt)})
+        med = median_rounds({"ours": ours_gemm(A, B, C, M, N, K, lay, a.split),
+                             "hipblaslt": lambda: torch.matmul(At, Bt)})
         for k in tot:
             tot[k] += med[k]
         fl = 2.0 * M * N * K
         print(f"{name:10s} M={M:6d} N={N:5d} K={K:6d} {lay}  ours {med['ours']:8.1f}us {fl / med['ours'] / 1e6:7.1f} "
               f"TF/s | hipBLASLt {med['hipblaslt']:8.1f}us {fl / med['hipblaslt'] / 1e6:7.1f} TF/s", flush=True)
     print(f"sum: ours {tot['ours']:.1f} us | hipBLASLt {tot['hipblaslt']:.1f} us")
+
+
+def cmd_one(a):
+    """One shape, `reps` back-to-back launches of ours (or the library with --lib): a rocprofv3 --pmc target."""
+    name, M, N, K, lay = a.shape.split(":")
+    M, N, K = int(M), int(N), int(K)
+    A, B, C = gemm_operands(M, N, K, lay)
+    a_km, b_kn = LAYOUTS[lay]
+    if a.lib:
+        At, Bt = (A.t() if a_km else A), (B if b_kn else B.t())
+        Cf = torch.zeros(M, N, device=dev())
+        f = (lambda: torch.addmm(Cf, At, Bt, out_dtype=torch.float32, out=Cf)) if lay == "tn" else \
+            (lambda: torch.matmul(At, Bt))
+    else:
+        f = ours_gemm(A, B, C, M, N, K, lay, a.split)
+    for _ in range(a.reps):
+        f()
+    torch.cuda.synchronize()
+    print("done", name)
 
 
 def cmd_kscan(a):
@@ -193,8 +214,18 @@ def cmd_nn(a):
     loss = torch.zeros(1, device=dev())
     rows.append(("softmax_xent (in place)",
                  timed(lambda: ops.softmax_xent(logits, 50257, labels, 1.0 / M, loss), 10), 2 * M * V * 2))
+    stats = torch.empty(M * (V // 64) * 2, device=dev())
+    h = torch.randn(M, C, **bf)
+    w = torch.randn(V, C, **bf) * 0.05
+    ops.gemm(h, w, logits, M, V, C, False, False, ops.EPI_XENT_STATS_BF16, colsum=stats, seg=50257)
+    rows.append(("xent_from_stats (in place)",
+                 timed(lambda: ops.xent_from_stats(logits, 50257, stats, labels, 1.0 / M, loss), 10), 2 * M * V * 2))
+    t_plain = timed(lambda: ops.gemm(h, w, logits, M, V, C, False, False, ops.EPI_STORE_BF16), 10)
+    t_stats = timed(lambda: ops.gemm(h, w, logits, M, V, C, False, False, ops.EPI_XENT_STATS_BF16, colsum=stats,
+                                     seg=50257), 10)
     for name, us, nbytes in rows:
         print(f"{name:32s} {us:9.1f} us  {nbytes / us / 1e6:6.2f} TB/s")
+    print(f"LM-head GEMM 8192x50304x768: plain bf16 store {t_plain:.1f} us, with the xent-stats epilogue {t_stats:.1f} us")
 
 
 def cmd_emb(a):
@@ -244,6 +275,12 @@ def main(argv=None):
     p = sub.add_parser("gemm")
     p.add_argument("--set", default=os.environ.get("GEMM_SET", "wd"), choices=["wd", "gpt2"])
     p.add_argument("--shapes", default=os.environ.get("GEMM_SHAPES", ""))
+    p.add_argument("--split", type=int, default=1, help="split-K of the nt / nn shapes (slab + reduce)")
+    p = sub.add_parser("one")
+    p.add_argument("--shape", default="g.lm.d:8192:768:50304:nn")
+    p.add_argument("--split", type=int, default=1)
+    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--lib", action="store_true", help="torch.matmul / addmm(out_dtype=fp32) instead of ours")
     p = sub.add_parser("kscan")
     p.add_argument("--M", type=int, default=16384)
     p.add_argument("--N", type=int, default=1024)
