@@ -225,7 +225,8 @@ def cmd_nn(a):
                                      seg=50257), 10)
     for name, us, nbytes in rows:
         print(f"{name:32s} {us:9.1f} us  {nbytes / us / 1e6:6.2f} TB/s")
-    print(f"LM-head GEMM 8192x50304x768: plain bf16 store {t_plain:.1f} us, with the xent-stats epilogue {t_stats:.1f} us")
+    print(f"LM-head GEMM 8192x50304x768: plain bf16 store {t_plain:.1f} us, "
+          f"with the xent-stats epilogue {t_stats:.1f} us")
 
 
 def cmd_emb(a):
