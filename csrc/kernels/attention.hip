@@ -22,6 +22,8 @@
 // dQ is produced by its own sweep instead of float atomics (deterministic, 7 products per tile
 // pair instead of 5).
 // K/V (or Q/dO) tiles are double-buffered in LDS with a one-tile register prefetch.
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -121,7 +123,11 @@ __device__ __forceinline__ void store_transposed(bf16_t* out, int64_t ld, int ro
 }
 
 // ------------------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, int ldq, int T, int H,
+// OCC = waves per SIMD the register allocation must allow (amdgpu_waves_per_eu): the compiler left
+// to itself gave the forward 188 and the dK/dV kernel 290 registers (2 and 1 waves per SIMD: every
+// exp / LDS / barrier latency exposed); capped at 3 and 2 waves they fit without scratch
+template <int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, int ldq, int T, int H,
                                                        int dmodel, float sl2, bf16_t* __restrict__ O, int ldo,
                                                        float* __restrict__ lse) {
   __shared__ __attribute__((aligned(16))) bf16_t sm[2][2][TILE * LP];  // [buf][K|V]
@@ -383,7 +389,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restri
 }
 
 // ------------------------------------------------------------------------------ dK, dV
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv, int ldq,
+template <int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv, int ldq,
                                                            const bf16_t* __restrict__ dO, int lddo,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta, int T, int H, int dmodel,
@@ -508,6 +515,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16_t* __restr
   store_transposed(base + 2 * dmodel, lddq, kw, T, dv, 1.f, lane);
 }
 
+// MINIPS_ATTN_OCC=<fwd>,<dkv>: waves per SIMD of the forward (2 or 3) and the dK/dV kernel (1 or 2);
+// default 3,2 (2,1 = the uncapped allocation)
+struct AttnOcc {
+  int fwd = 3, dkv = 2;
+};
+static const AttnOcc& attn_occ() {
+  static const AttnOcc o = [] {
+    AttnOcc r;
+    if (const char* e = std::getenv("MINIPS_ATTN_OCC")) std::sscanf(e, "%d,%d", &r.fwd, &r.dkv);
+    return r;
+  }();
+  return o;
+}
+
 void check_attn(int T, int H, int dmodel, int ldq, int ldo) {
   if (dmodel != H * HD) throw std::runtime_error("attention: head dim must be 64");
   if (T <= 0 || ldq % 8 || ldo % 8) throw std::runtime_error("attention: leading dims must be multiples of 8");
@@ -519,7 +540,10 @@ void attn_fwd(const bf16_t* qkv, int ldq, int B, int T, int H, int dmodel, float
               hipStream_t s) {
   check_attn(T, H, dmodel, ldq, ldo);
   const int grid = ((T + BROWS - 1) / BROWS) * B * H;  // decoded as (block of T, head) in the kernels
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, 256, 0, s, qkv, ldq, T, H, dmodel, scale * kLog2e, O, ldo, lse);
+  if (attn_occ().fwd >= 3)
+    hipLaunchKernelGGL(attn_fwd_kernel<3>, grid, 256, 0, s, qkv, ldq, T, H, dmodel, scale * kLog2e, O, ldo, lse);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, 256, 0, s, qkv, ldq, T, H, dmodel, scale * kLog2e, O, ldo, lse);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
@@ -534,8 +558,12 @@ void attn_bwd(const bf16_t* qkv, int ldq, const bf16_t* O, int ldo, const bf16_t
   hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel, scale * kLog2e,
                      scale, dqkv, lddq);
   MINIPS_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel,
-                     scale * kLog2e, scale, dqkv, lddq);
+  if (attn_occ().dkv >= 2)
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<2>, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel,
+                       scale * kLog2e, scale, dqkv, lddq);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<1>, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel,
+                       scale * kLog2e, scale, dqkv, lddq);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

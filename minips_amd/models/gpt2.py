@@ -59,13 +59,14 @@ class GPT2Config:
         return align(self.vocab, 64)
 
 
-# LM-head cross-entropy: "stats" (GEMM epilogue softmax partials + streaming gradient pass) or
-# "rowwise" (plain GEMM + block-per-row softmax_xent)
-_XENT = os.environ.get("MINIPS_GPT2_XENT", "stats")
+# LM-head cross-entropy on our GEMM path: "rowwise" (plain GEMM + block-per-row softmax_xent) or
+# "stats" (softmax partials in the GEMM epilogue + a streaming gradient pass: the pass is 59 us
+# faster, the epilogue 68 us slower -- 13.87 vs 14.14 ms/step, profiles/r3/gpt2_lm_head.txt)
+_XENT = os.environ.get("MINIPS_GPT2_XENT", "rowwise")
 _LM_DGRAD_SPLIT = int(os.environ.get("MINIPS_LM_DGRAD_SPLIT", "4"))
-# LM-head GEMMs (logits, dgrad, wte wgrad): "ours" (gemm.hip + the xent-stats epilogue) or "lib"
-# (hipBLASLt through torch for these three plain GEMMs; the CPU reference path always uses ours)
-_LM_GEMM = os.environ.get("MINIPS_LM_GEMM", "ours")
+# LM-head GEMMs (logits, dgrad, wte wgrad): "lib" (hipBLASLt through torch for these three plain
+# GEMMs: 13.10 vs 13.87 ms/step) or "ours" (gemm.hip); the CPU reference path always uses ours
+_LM_GEMM = os.environ.get("MINIPS_LM_GEMM", "lib")
 
 
 class GPT2:
