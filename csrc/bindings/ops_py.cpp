@@ -43,6 +43,14 @@ T* opt_ptr(const c10::optional<at::Tensor>& t, at::ScalarType dt, const char* na
   return reinterpret_cast<T*>(t->data_ptr());
 }
 
+// fp32 1-D vector that may be a strided view (e.g. one column of a weight-gradient matrix)
+float* strided_vec_ptr(const c10::optional<at::Tensor>& t, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->dim() == 1 && t->stride(0) >= 1, name,
+              ": a 1-D fp32 GPU tensor (any positive stride)");
+  return t->data_ptr<float>();
+}
+
 // C = A . B with layout flags; see gemm.hip. Returns nothing (C preallocated).
 // Batched mode (batch > 1): operands are flat buffers addressed with 2-level strides; every
 // batch's extent is bounds-checked against the tensor sizes before launch.
@@ -120,7 +128,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   const bool needs_mask = epi == minips_k::kEpiReluMaskBf16 || epi == minips_k::kEpiBiasGeluAuxBf16 ||
                           epi == minips_k::kEpiGeluGradBf16;
   if (needs_mask) TORCH_CHECK(mask_p, "this epilogue needs mask/aux");
-  float* colsum_p = opt_ptr<float>(colsum, at::kFloat, "colsum");
+  float* colsum_p = epi == minips_k::kEpiXentStatsBf16 ? opt_ptr<float>(colsum, at::kFloat, "colsum")
+                                                      : strided_vec_ptr(colsum, "colsum");
   if (epi == minips_k::kEpiXentStatsBf16) {
     // colsum = the softmax partials [M][ceil(N/64)] float2, seg = the vocabulary (valid columns)
     ldmask = (int)((N + 63) / 64);
@@ -128,8 +137,10 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
                     batch <= 1 && split_k <= 1,
                 "xent-stats epilogue: stats of >= M * ceil(N/64) * 2 floats, 0 < seg (vocab) <= N, no batch/split-K");
   } else if (colsum_p) {
-    TORCH_CHECK(colsum->numel() >= N, "colsum too short");
+    // a 1-D view may be strided (a column of a weight-gradient matrix: the folded-bias column)
+    TORCH_CHECK(colsum->dim() == 1 && colsum->numel() >= N && colsum->stride(0) >= 1, "colsum: 1-D, >= N values");
   }
+  const int colsum_ld = (colsum_p && epi != minips_k::kEpiXentStatsBf16) ? (int)colsum->stride(0) : 1;
   c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
   static const bool use_slab = [] {
     const char* e = std::getenv("MINIPS_SPLITK_SLAB");
@@ -144,7 +155,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   minips_k::gemm_bf16_batched(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb,
                               (int)ldc, a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p, (float)alpha,
                               (int)split_k, (int)batch, (int)inner, st[0], st[1], st[2], st[3], st[4], st[5],
-                              stream_of(A), slab.defined() ? ptr<float>(slab) : nullptr, perm_p, (int)seg);
+                              stream_of(A), slab.defined() ? ptr<float>(slab) : nullptr, perm_p, (int)seg,
+                              colsum_ld);
 }
 
 // Bitmap planner of a bounded key space (keys, after the optional routing k * mult mod rn, in
@@ -439,6 +451,38 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
   minips_k::wd_head(ptr<bf16_t>(H), H.size(0), (int)H.size(1), ptr<bf16_t>(w), ptr<bf16_t>(b0),
                     ptr<float>(wide_logit), ptr<float>(labels), ptr<bf16_t>(dH), ptr<float>(dw), ptr<float>(db),
                     ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H));
+}
+
+// Last hidden layer + W&D head in one GEMM (minips_k::gemm_wd_head): A = H2 [B][>= K] bf16 (bias
+// column folded in), W = W3ext [N][>= K] bf16, w4 = [w | b] bf16 [>= N + 1], dw4 fp32 [>= N + 1].
+void wd_fwd_head(const at::Tensor& A, const at::Tensor& W, int64_t K, const at::Tensor& w4,
+                 const at::Tensor& wide_logit, const at::Tensor& labels, at::Tensor& dH, at::Tensor& dw4,
+                 at::Tensor& dwide, at::Tensor& loss_sum, double grad_scale,
+                 const c10::optional<at::Tensor>& dH_colsum) {
+  for (const at::Tensor* t : {&A, &W, &w4, &wide_logit, &labels, (const at::Tensor*)&dH, (const at::Tensor*)&dw4,
+                              (const at::Tensor*)&dwide, (const at::Tensor*)&loss_sum})
+    check_gpu(*t, "wd_fwd_head");
+  check_dtype(A, at::kBFloat16, "A");
+  check_dtype(W, at::kBFloat16, "W");
+  check_dtype(w4, at::kBFloat16, "w4");
+  check_dtype(dH, at::kBFloat16, "dH");
+  check_dtype(dw4, at::kFloat, "dw4");
+  check_dtype(wide_logit, at::kFloat, "wide_logit");
+  check_dtype(labels, at::kFloat, "labels");
+  check_dtype(dwide, at::kFloat, "dwide");
+  TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && dH.dim() == 2 && A.stride(1) == 1 && W.stride(1) == 1 &&
+                  dH.stride(1) == 1, "wd_fwd_head: 2-D operands with contiguous rows");
+  const int64_t M = A.size(0), N = W.size(0);
+  TORCH_CHECK(A.size(1) >= K && W.size(1) >= K && dH.size(0) == M && dH.size(1) >= N && w4.numel() >= N + 1 &&
+                  dw4.numel() >= N + 1 && wide_logit.numel() >= M && labels.numel() >= M && dwide.numel() >= M,
+              "wd_fwd_head shapes");
+  float* cs = strided_vec_ptr(dH_colsum, "dH_colsum");
+  if (cs) TORCH_CHECK(dH_colsum->numel() >= N, "dH_colsum: >= N values");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
+  minips_k::gemm_wd_head(ptr<bf16_t>(A), ptr<bf16_t>(W), (int)M, (int)N, (int)K, (int)A.stride(0), (int)W.stride(0),
+                         ptr<bf16_t>(dH), (int)dH.stride(0), ptr<bf16_t>(w4), ptr<float>(wide_logit),
+                         ptr<float>(labels), ptr<float>(dw4), ptr<float>(dwide), ptr<float>(loss_sum),
+                         (float)grad_scale, stream_of(A), cs, cs ? (int)dH_colsum->stride(0) : 1);
 }
 
 // Lookup CSR grouped by unique row (members/memrow int32 [B*F]) for U (upper-bound) rows.
@@ -1356,6 +1400,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1, py::arg("zero") = py::none());
   m.def("wd_head", &wd_head);
+  m.def("wd_fwd_head", &wd_fwd_head, py::arg("A"), py::arg("W"), py::arg("K"), py::arg("w4"), py::arg("wide_logit"),
+        py::arg("labels"), py::arg("dH"), py::arg("dw4"), py::arg("dwide"), py::arg("loss_sum"), py::arg("grad_scale"),
+        py::arg("dH_colsum") = py::none());
   m.def("wd_assemble_tab", &wd_assemble_tab);
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),

@@ -127,7 +127,8 @@ __device__ __forceinline__ void store_transposed(bf16_t* out, int64_t ld, int ro
 // to itself gave the forward 188 and the dK/dV kernel 290 registers (2 and 1 waves per SIMD: every
 // exp / LDS / barrier latency exposed); capped at 3 and 2 waves they fit without scratch
 template <int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, int ldq, int T, int H,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_fwd_kernel(
+    const bf16_t* __restrict__ qkv, int ldq, int T, int H,
                                                        int dmodel, float sl2, bf16_t* __restrict__ O, int ldo,
                                                        float* __restrict__ lse) {
   __shared__ __attribute__((aligned(16))) bf16_t sm[2][2][TILE * LP];  // [buf][K|V]
@@ -390,7 +391,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restri
 
 // ------------------------------------------------------------------------------ dK, dV
 template <int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv, int ldq,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_bwd_dkv_kernel(
+    const bf16_t* __restrict__ qkv, int ldq,
                                                            const bf16_t* __restrict__ dO, int lddo,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta, int T, int H, int dmodel,

@@ -113,6 +113,15 @@ struct EpiArgs {
   int64_t sc_split;  // split-K slab mode: C += blockIdx.z * sc_split (0 = all splits share C)
   const int* perm;   // kEpiPermRowsBf16: segment positions [M][N / seg]
   int seg;
+  // kEpiWdHead: the W&D output head folded into the last hidden layer's GEMM (see wd_head_epilogue)
+  const float* head_wide = nullptr;   // [M] wide-part logits
+  const float* head_label = nullptr;  // [M] labels (> 0.5 = positive)
+  float* head_dwide = nullptr;        // [M] dLoss/dlogit (the wide part's gradient)
+  float* head_loss = nullptr;         // [1] += sum of the BCE-with-logits losses
+  float head_scale = 0.f;             // gradient scale (1 / global batch)
+  float* head_dh_colsum = nullptr;    // [N] (stride head_dh_colsum_ld) += column sums of dH (optional)
+  int head_dh_colsum_ld = 1;
+  int colsum_ld = 1;                  // kEpiReluMaskBf16: colsum[col * colsum_ld] (a column of a matrix)
 };
 
 // Destination of an output row segment (kEpiPermRowsBf16: the permuted row of its segment).
@@ -185,7 +194,7 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
     if (EPI == kEpiReluMaskBf16 && ep.colsum) {
       csum += __shfl_xor(csum, 16, 64);
       csum += __shfl_xor(csum, 32, 64);
-      if (lane < 16 && col_ok) atomicAdd(ep.colsum + col, csum);
+      if (lane < 16 && col_ok) atomicAdd(ep.colsum + (int64_t)col * ep.colsum_ld, csum);
     }
   }
 }
@@ -396,7 +405,7 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
       c += __shfl_xor(c, 16, 64);
       c += __shfl_xor(c, 32, 64);
       const int col = nb + (lane & 7) * 8 + e;
-      if (lane < 8 && col < N) atomicAdd(ep.colsum + col, c);
+      if (lane < 8 && col < N) atomicAdd(ep.colsum + (int64_t)col * ep.colsum_ld, c);
     }
   }
 }
@@ -567,6 +576,110 @@ __device__ __forceinline__ v8s frag2(const bf16_t* S, int row_base, int ks, int 
   }
 }
 
+// W&D output head as the epilogue of the last hidden layer's forward GEMM (kEpiWdHead): one
+// workgroup owns TM rows and ALL N (<= TN) columns of H3 = relu(H2ext W3ext^T), so a row's head
+// logit z = H3[row] . w4 + b4 + wide[row] is a reduction across the workgroup's WN waves (one LDS
+// exchange). Then dz = (sigmoid(z) - label) * scale, dH3 = (H3 > 0) * bf16(dz * w4) goes out
+// through the staged bf16 epilogue, dw4 / db4 / loss / dwide are accumulated here -- H3 itself
+// never reaches HBM and the separate head kernel (H3 read + dH3 write, one wave per 4 samples)
+// disappears. Numerics as wd_head: H3 rounded to bf16 before the dot product and the mask.
+// ep.bias = w4 bf16 [N + 1] (b4 at N), ep.colsum = dw4 fp32 [N + 1] (db4 at N).
+template <int TM, int TN>
+__device__ __forceinline__ void wd_head_epilogue(v4f (&acc)[4][4], const EpiArgs& ep, int M, int N, int m0, int wm,
+                                                 int wn, int lane, float* __restrict__ lds) {
+  constexpr int WN = TN / 64, NW = (TM / 64) * WN;
+  const int col_l = lane & 15, row_q = (lane >> 4) * 4;
+  const int mb = m0 + wm * 64, nb = wn * 64;
+  float* zp = lds + NW * kScrFloats;  // [TM][WN] wave partials of z, past the per-wave scratch
+  float wv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = nb + j * 16 + col_l;
+    wv[j] = col < N ? bf2f(ep.bias[col]) : 0.f;
+  }
+  float zr[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float h = __uint_as_float(pack_bf2(fmaxf(acc[i][j][r] * ep.alpha, 0.f), 0.f) << 16);
+        acc[i][j][r] = h;
+        a += h * wv[j];
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) a += __shfl_xor(a, o, 64);
+      zr[i][r] = a;
+    }
+  if (col_l == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zp[(wm * 64 + i * 16 + row_q + r) * WN + wn] = zr[i][r];
+  }
+  __syncthreads();
+  const float b4 = bf2f(ep.bias[N]);
+  float dz[4][4], dbl = 0.f, lossl = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wm * 64 + i * 16 + row_q + r, row = m0 + rl;
+      float d = 0.f;
+      if (row < M) {
+        float z = b4 + ep.head_wide[row];
+#pragma unroll
+        for (int w = 0; w < WN; ++w) z += zp[rl * WN + w];
+        const float label = ep.head_label[row] > 0.5f ? 1.f : 0.f;
+        d = (sigmoidf_(z) - label) * ep.head_scale;
+        if (wn == 0 && col_l == 0) {
+          ep.head_dwide[row] = d;
+          dbl += d;
+          lossl += fmaxf(z, 0.f) - z * label + log1pf(__expf(-fabsf(z)));
+        }
+      }
+      dz[i][r] = d;
+    }
+  float cs[4] = {0.f, 0.f, 0.f, 0.f}, cg[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float h = acc[i][j][r];
+        cs[j] += dz[i][r] * h;
+        const float gv = h > 0.f ? dz[i][r] * wv[j] : 0.f;
+        acc[i][j][r] = gv;
+        cg[j] += __uint_as_float(pack_bf2(gv, 0.f) << 16);  // the stored (bf16) dH's column sums
+      }
+  EpiArgs st = ep;
+  st.alpha = 1.f;
+  epilogue_lds<kEpiStoreBf16, 4>(acc, st, M, N, mb, nb, lane, lds + (threadIdx.x >> 6) * kScrFloats);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    cs[j] += __shfl_xor(cs[j], 16, 64);
+    cs[j] += __shfl_xor(cs[j], 32, 64);
+    const int col = nb + j * 16 + lane;
+    if (lane < 16 && col < N) atomicAdd(ep.colsum + col, cs[j]);
+    if (ep.head_dh_colsum) {  // the next layer's folded-bias gradient (dH's column sums)
+      cg[j] += __shfl_xor(cg[j], 16, 64);
+      cg[j] += __shfl_xor(cg[j], 32, 64);
+      if (lane < 16 && col < N) atomicAdd(ep.head_dh_colsum + (int64_t)col * ep.head_dh_colsum_ld, cg[j]);
+    }
+  }
+  if (wn == 0) {
+    dbl = warp_sum(dbl);
+    lossl = warp_sum(lossl);
+    if (lane == 0) {
+      atomicAdd(ep.colsum + N, dbl);
+      atomicAdd(ep.head_loss, lossl);
+    }
+  }
+}
+
 // TM x TN output tile, (TM/64) x (TN/64) waves of 64x64 each (4, 8 or 16 waves). 128x128
 // keeps 2 workgroups per CU; the 256-wide tiles halve the L2->LDS bytes per MFMA (the loads,
 // not the MFMAs, bound this kernel at these sizes) and run one 16- or 8-wave workgroup per CU.
@@ -649,7 +762,9 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
     __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is refilled
     asm volatile("" ::: "memory");
   }
-  if (kLdsEpilogue)
+  if constexpr (EPI == kEpiWdHead)
+    wd_head_epilogue<TM, TN>(acc, ep, M, N, m0, wm, wn, lane, reinterpret_cast<float*>(&smem[0][0]));
+  else if (kLdsEpilogue)
     epilogue_lds<EPI, 4>(acc, ep, M, N, m0 + wm * 64, n0 + wn * 64, lane,
                          reinterpret_cast<float*>(&smem[0][0]) + wave * kScrFloats);
   else
@@ -986,7 +1101,7 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
                        bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
                        float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
                        int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s, float* slab,
-                       const int* perm, int seg) {
+                       const int* perm, int seg, int colsum_ld) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return;
   if (epi == kEpiPermRowsBf16 && (!perm || seg <= 0 || seg % 8 || N % seg || batch != 1 || split_k > 1))
     throw std::runtime_error("gemm: the permuted-rows epilogue needs perm, seg % 8 == 0, N % seg == 0, no batch");
@@ -1028,6 +1143,7 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
     return;
   }
   EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i, 0, perm, seg};
+  ep.colsum_ld = colsum_ld > 0 ? colsum_ld : 1;
   // an accumulating GEMM with one K slice has one writer per output element: read-add-write
   // instead of memory-side fp32 atomics (MINIPS_GEMM_ACCUM=0 keeps the atomics)
   static const bool accum_ok = [] {
@@ -1044,6 +1160,30 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
   } else {
     MINIPS_GEMM_EPI_DISPATCH(true, false)
   }
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void gemm_wd_head(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, bf16_t* dH, int lddh,
+                  const bf16_t* w4, const float* wide, const float* labels, float* dw4, float* dwide, float* loss,
+                  float scale, hipStream_t s, float* dh_colsum, int dh_colsum_ld) {
+  if (M <= 0) return;
+  if (N <= 0 || N > 256 || N % 8 || K % 8 || lda % 8 || ldb % 8 || lddh % 8)
+    throw std::runtime_error("gemm_wd_head: N <= 256, N / K / leading dims multiples of 8");
+  const int64_t a_ext = (int64_t)(M - 1) * lda + K, b_ext = (int64_t)(N - 1) * ldb + K;
+  if (a_ext * 2 >= 0x7ff00000ll || b_ext * 2 >= 0x7ff00000ll)
+    throw std::runtime_error("gemm_wd_head: operands > 2 GiB");
+  EpiArgs ep{dH, lddh, w4, nullptr, 0, dw4, 1.f, 1, 0, 0, 0, 0, 0, 0, 0, nullptr, 0};
+  ep.head_wide = wide;
+  ep.head_label = labels;
+  ep.head_dwide = dwide;
+  ep.head_loss = loss;
+  ep.head_scale = scale;
+  ep.head_dh_colsum = dh_colsum;
+  ep.head_dh_colsum_ld = dh_colsum_ld;
+  // 64 x 256 tiles: a workgroup holds whole rows (all N columns), 4 waves side by side along N;
+  // 80 KiB of LDS -> 2 workgroups per CU, M / 64 workgroups (256 at the W&D batch)
+  hipLaunchKernelGGL((gemm_v2_kernel<64, 256, false, false, kEpiWdHead>), dim3((M + 63) / 64, 1, 1), dim3(256), 0, s,
+                     A, B, M, N, K, lda, ldb, K, ep);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

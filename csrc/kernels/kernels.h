@@ -33,10 +33,19 @@ enum GemmEpilogue {
   // log2 units (y = bf16(acc) * log2 e), as a float2 at colsum[row * ldmask + col0 / 64]
   // (ldmask = ceil(N / 64)); xent_from_stats then streams the gradient without a row reduction
   kEpiXentStatsBf16 = 11,
+  // the W&D output head as the epilogue of the last hidden layer (gemm_wd_head only)
+  kEpiWdHead = 12,
 };
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
                float alpha, int split_k, hipStream_t s);
+// W&D last hidden layer + output head in one kernel: H3 = relu(A B^T) (A [M][K] = H2 with the bias
+// column folded in, B [N][K] = W3ext, N <= 256) stays on chip; z = H3 . w4[:N] + w4[N] + wide,
+// dz = (sigmoid(z) - label) * scale -> dH [M][N] bf16 = (H3 > 0) * dz * w4, dw4[:N] += dz H3,
+// dw4[N] += dz, dwide = dz, loss += BCE-with-logits (same numerics as wd_head on a bf16 H3)
+void gemm_wd_head(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, bf16_t* dH, int lddh,
+                  const bf16_t* w4, const float* wide, const float* labels, float* dw4, float* dwide, float* loss,
+                  float scale, hipStream_t s, float* dh_colsum = nullptr, int dh_colsum_ld = 1);
 // Batched form: `batch` GEMMs, z = blockIdx.y; operand offsets are (z / inner) * s_outer +
 // (z % inner) * s_inner elements (e.g. attention heads inside a [B*T, H*dh] activation).
 void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
@@ -44,7 +53,8 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
                        float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
                        int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s,
                        float* slab = nullptr,  // split-K workspace [split_k][M][N] (atomic epilogue only)
-                       const int* perm = nullptr, int seg = 0);  // kEpiPermRowsBf16
+                       const int* perm = nullptr, int seg = 0,  // kEpiPermRowsBf16
+                       int colsum_ld = 1);                      // colsum[col * colsum_ld]
 
 // ------------------------------------------------------------------ sparse keys (sparse.hip)
 // Hash-based dedupe + owner bucketing of int64 keys in 3 launches (no sort):

@@ -75,6 +75,14 @@ _DENSE_CLOCK_ON_SIDE = os.environ.get("MINIPS_DENSE_CLOCK_ON_SIDE", "0") == "1"
 # which crowd the dgrad chain), so "ext" with a 64-aligned layer-1 K is the default.
 _K1_ALIGN = int(os.environ.get("MINIPS_WD_K1_ALIGN", "64"))
 _BIAS_VEC = os.environ.get("MINIPS_WD_BIAS", "ext") == "vec"
+# MINIPS_WD_FUSED_HEAD=1: layer 3 and the output head as one GEMM (ops.wd_fwd_head, H3 never
+# written). Measured off: the fused kernel took 51 us vs 17 + 24 us for the GEMM + wd_head (its
+# dw4 / db4 / loss reductions are 256 same-address atomics per column from 256 workgroups).
+_FUSED_HEAD = os.environ.get("MINIPS_WD_FUSED_HEAD", "0") == "1"
+# MINIPS_WD_TRIM=1 (with the fused head): layer-2/3 weight gradients over the weight columns only,
+# their folded-bias columns as dH column sums in the producing epilogues. Measured off: 0.448 vs
+# 0.416-0.420 ms/step (per-wave column-sum atomics in the dgrad epilogue), profiles/r3/ab_wd_r3.txt
+_TRIM = os.environ.get("MINIPS_WD_TRIM", "0") == "1"
 
 
 def _align(n, a=8):
@@ -235,12 +243,21 @@ class WideDeep(LookaheadPlans):
             ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
         G = self.dense.grad
         P = self.dense.get()
-        self._forward(b, P)
         scale = 1.0 / (B * self.comm.world)
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
-        # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
-        ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1], b["dwide"],
-                    b["loss"], self.view(G, "b3") if _BIAS_VEC else None, scale)
+        if _FUSED_HEAD and not _BIAS_VEC:
+            # layer 3 + the output head in one GEMM: H3 never leaves the chip (ops.wd_fwd_head)
+            ops.linear_fwd(b["X"], self.view(P, "W1"), None, "relu", out=b["H1"])
+            ops.linear_fwd(b["H1"], self.view(P, "W2"), None, "relu", out=b["H2"])
+            # with _TRIM, dH3's column sums (the layer-3 folded-bias gradient) come from the head
+            ops.wd_fwd_head(b["H2"], self.view(P, "W3"), self.k_pad[2], w4, b["wide"], labels, b["dH3"], gw4,
+                            b["dwide"], b["loss"], scale,
+                            dH_colsum=self.view(G, "W3")[:, self.k_in[2]] if _TRIM else None)
+        else:
+            self._forward(b, P)
+            # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
+            ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
+                        b["dwide"], b["loss"], self.view(G, "b3") if _BIAS_VEC else None, scale)
         issue_next("head")
         side = self._side
         # weight gradients fork onto a second stream as soon as their inputs exist, beside the
@@ -248,13 +265,25 @@ class WideDeep(LookaheadPlans):
         # Each fork records an event on the compute stream (~2-4 us queue bubble on MI355X), but
         # fewer, later forks lose more overlap than they save: W3+W2 forked together 0.431-0.438,
         # all three after dgrad1 0.446 vs 0.418-0.421 ms/step (profiles/r3/ab_wd_forks.txt)
+        # _TRIM: the layer-2/3 weight gradients over the weight columns only (1024 / 512 instead of
+        # 1032 / 520: no near-empty last column tile); their folded-bias columns are the column sums
+        # of dH2 / dH3, taken by the dgrad epilogue / the fused head
+        trim = _TRIM and _FUSED_HEAD and not _BIAS_VEC
+        k2, k3 = self.k_in[1], self.k_in[2]
         with side.fork():
-            ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
-        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=self.k_in[2], out=b["dH2"])
+            if trim:
+                ops.linear_wgrad(b["dH3"], b["H2"][:, :k3], self.view(G, "W3")[:, :k3])
+            else:
+                ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
+        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"],
+                         colsum=self.view(G, "W2")[:, k2] if trim else None)
         with side.fork():
             if _BIAS_VEC:
                 ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
-            ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
+            if trim:
+                ops.linear_wgrad(b["dH2"], b["H1"][:, :k2], self.view(G, "W2")[:, :k2])
+            else:
+                ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         with side.fork():
             ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
