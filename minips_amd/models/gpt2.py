@@ -67,6 +67,7 @@ _LM_DGRAD_SPLIT = int(os.environ.get("MINIPS_LM_DGRAD_SPLIT", "4"))
 # LM-head GEMMs (logits, dgrad, wte wgrad): "lib" (hipBLASLt through torch for these three plain
 # GEMMs: 13.10 vs 13.87 ms/step) or "ours" (gemm.hip); the CPU reference path always uses ours
 _LM_GEMM = os.environ.get("MINIPS_LM_GEMM", "lib")
+_LM_WGRAD = os.environ.get("MINIPS_LM_WGRAD", "mm")  # lib form of the wte wgrad: "mm" (overwrite) | "addmm"
 
 
 class GPT2:
@@ -139,7 +140,9 @@ class GPT2:
                 ao=[ext_activation(M, d, dev) for _ in range(nl)],        # attention out (+ ones)
                 u=[torch.empty(M, 4 * d, **bf) for _ in range(nl)],       # pre-GELU
                 g=[ext_activation(M, 4 * d, dev) for _ in range(nl)],     # GELU out (+ ones)
-                hf=ext_activation(M, d, dev), stf=(torch.empty(M, **f32), torch.empty(M, **f32)),
+                # ln_f output: only the LM head reads it (no bias column), contiguous rows -- hipBLASLt
+                # takes a strided operand through an extra copy (+120 us on the wgrad)
+                hf=torch.empty(M, d, **bf), stf=(torch.empty(M, **f32), torch.empty(M, **f32)),
                 logits=torch.empty(M, c.vocab_pad, **bf),
                 xstats=torch.empty(M * ((c.vocab_pad + 63) // 64) * 2, **f32),  # LM-head softmax partials
                 delta=torch.empty(B * H * T, **f32),
@@ -201,7 +204,12 @@ class GPT2:
             # weight gradient accumulates in fp32 (addmm out_dtype), the dgrad writes bf16
             gw = v(G, "wte")
             with side.fork():
-                torch.addmm(gw, logits.t(), hf[:, :d], out_dtype=torch.float32, out=gw)
+                if _LM_WGRAD == "mm":
+                    # the first writer of the wte gradient in the step (embed_bwd adds after the
+                    # join): an overwriting fp32-output mm (710 us isolated vs addmm's 757 us)
+                    torch.mm(logits.t(), hf, out_dtype=torch.float32, out=gw)
+                else:
+                    torch.addmm(gw, logits.t(), hf, out_dtype=torch.float32, out=gw)
             torch.matmul(logits, wte, out=dh)
         else:
             with side.fork():

@@ -1,10 +1,3 @@
 set -eo pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-for v in 0 1; do
-  d=gpurun_out/trace_fh$v; rm -rf $d
-  MINIPS_WD_TRIM=0 MINIPS_WD_FUSED_HEAD=$v timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python bench.py --steps 30 --warmup 5 > $d.log 2>&1
-  f=$(find $d -name "*kernel_trace.csv" | head -1)
-  echo "=== FUSED_HEAD=$v"; python tools/prof_summary.py trace "$f" --anchor adam_kernel --skip 8 --top 24
-done
+for i in 1 2 3; do for v in mm addmm; do echo "gpt2 $v $(MINIPS_LM_WGRAD=$v timeout -k 10 300 python tools/bench_models.py --model gpt2 --steps 10 --warmup 3 2>&1 | grep '^{' | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])')"; done; done
