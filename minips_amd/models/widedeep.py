@@ -83,6 +83,9 @@ _FUSED_HEAD = os.environ.get("MINIPS_WD_FUSED_HEAD", "0") == "1"
 # their folded-bias columns as dH column sums in the producing epilogues. Measured off: 0.448 vs
 # 0.416-0.420 ms/step (per-wave column-sum atomics in the dgrad epilogue), profiles/r3/ab_wd_r3.txt
 _TRIM = os.environ.get("MINIPS_WD_TRIM", "0") == "1"
+# split-K workgroup target of the three weight gradients (ops.linear_wgrad blocks): W&D 0.402 ms at
+# 320 vs 0.409-0.412 at the default 512 (GPT-2 keeps 512: 12.90 vs 13.18 ms at 256), ab_wd_r3.txt
+_WGRAD_BLOCKS = int(os.environ.get("MINIPS_WD_WGRAD_BLOCKS", "320"))
 
 
 def _align(n, a=8):
@@ -272,21 +275,21 @@ class WideDeep(LookaheadPlans):
         k2, k3 = self.k_in[1], self.k_in[2]
         with side.fork():
             if trim:
-                ops.linear_wgrad(b["dH3"], b["H2"][:, :k3], self.view(G, "W3")[:, :k3])
+                ops.linear_wgrad(b["dH3"], b["H2"][:, :k3], self.view(G, "W3")[:, :k3], blocks=_WGRAD_BLOCKS)
             else:
-                ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
+                ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"), blocks=_WGRAD_BLOCKS)
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"],
                          colsum=self.view(G, "W2")[:, k2] if trim else None)
         with side.fork():
             if _BIAS_VEC:
                 ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
             if trim:
-                ops.linear_wgrad(b["dH2"], b["H1"][:, :k2], self.view(G, "W2")[:, :k2])
+                ops.linear_wgrad(b["dH2"], b["H1"][:, :k2], self.view(G, "W2")[:, :k2], blocks=_WGRAD_BLOCKS)
             else:
-                ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
+                ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"), blocks=_WGRAD_BLOCKS)
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         with side.fork():
-            ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"))
+            ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"), blocks=_WGRAD_BLOCKS)
         # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows

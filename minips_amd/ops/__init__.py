@@ -176,8 +176,9 @@ def overlap_mode(on: bool) -> bool:
     return prev
 
 
-def linear_wgrad(dy, x, dw, split_k=None):
-    """dw[N,K] += dy^T x (dy [M,N], x [M,K]); fp32 accumulate."""
+def linear_wgrad(dy, x, dw, split_k=None, blocks=None):
+    """dw[N,K] += dy^T x (dy [M,N], x [M,K]); fp32 accumulate. ``blocks``: the workgroup target of
+    the split-K choice (default MINIPS_WGRAD_BLOCKS; a model may tune its own)."""
     M, N = dy.shape
     K = x.shape[1]
     if split_k is None:
@@ -188,7 +189,8 @@ def linear_wgrad(dy, x, dw, split_k=None):
         # to their fixed prologue/epilogue cost; the slab reduce makes splits cheap)
         overlapped = getattr(_overlap_state, "on", False)
         min_rows = _WGRAD_MIN_ROWS_OVERLAP if overlapped else _WGRAD_MIN_ROWS
-        split_k = max(1, min(M // min_rows, (_WGRAD_BLOCKS + tiles - 1) // tiles))
+        target = _WGRAD_BLOCKS if blocks is None else int(blocks)
+        split_k = max(1, min(M // min_rows, (target + tiles - 1) // tiles))
         if overlapped and _WGRAD_MIN_BLOCKS_OVERLAP and split_k * tiles < _WGRAD_MIN_BLOCKS_OVERLAP:
             split_k = max(split_k, min(M // _WGRAD_MIN_ROWS, -(-_WGRAD_MIN_BLOCKS_OVERLAP // tiles)))
     return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
