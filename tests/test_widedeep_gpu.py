@@ -58,13 +58,17 @@ def test_collective_ssp_read_bound(dev, s):
                     pull_dtype=torch.float32, init_std=0.0)
     assert t.pipe.async_
     k = torch.tensor([7], device=dev)
+    # a deterministic delay on the side stream (a ~9 TFLOP GEMM, several ms on any MI355X clock),
+    # not a cycle-count spin, whose duration depends on the clock source
+    a = torch.randn(8192, 8192, device=dev).to(torch.bfloat16)
     seen = []
     for c in range(16):
         v = float(t.get_rows(k)[0, 0])  # a Get at clock c
         seen.append((c, v))
         t.add_keys(k, torch.ones(1, 4, device=dev))
         with torch.cuda.stream(t.pipe.stream):
-            torch.cuda._sleep(20_000_000)  # ~10 ms: the clock's apply lands late
+            for _ in range(8):
+                torch.matmul(a, a)  # the clock's apply lands late
         t.clock()
     t.drain()
     for c, v in seen:
