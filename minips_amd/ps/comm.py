@@ -41,6 +41,34 @@ import torch.distributed as dist
 
 
 @dataclass
+class _OwnedStream(torch.cuda.ExternalStream):
+    """An ExternalStream over a stream this process created; destroyed with its last reference."""
+
+    def __del__(self):
+        try:
+            from .._native import kernels
+
+            kernels().stream_destroy(int(self.cuda_stream))
+        except Exception:  # interpreter shutdown
+            pass
+
+
+def dedicated_stream(device, priority: int = 0):
+    """A HIP stream no other stream aliases. torch.cuda.Stream() draws from a 32-per-priority
+    round-robin pool, so a long-lived process that builds many tables (Engine.create_table, the
+    test suite) would otherwise get the SAME HIP stream for two "independent" lanes -- e.g. a
+    table's clock pipeline and the planning stream -- and serialise one behind the other. Falls
+    back to the pool when the native extension is not built."""
+    device = torch.device(device)
+    try:
+        from .._native import kernels
+
+        h = kernels().new_stream(device.index or 0, int(priority))
+    except Exception:
+        return torch.cuda.Stream(device=device, priority=priority)
+    return _OwnedStream(h, device=device)
+
+
 class CommStats:
     bytes_a2a: int = 0
     bytes_rs: int = 0
@@ -108,6 +136,10 @@ class Comm:
         if self.trace is not None:
             self.trace.append((op, str(t.dtype).replace("torch.", "") if t is not None else "", size))
 
+    def new_stream(self, priority: int = 0):
+        """A HIP stream of this rank's device that no other stream aliases (see dedicated_stream)."""
+        return dedicated_stream(self.device, priority)
+
     def plan_stream(self):
         """The HIP stream on which lookahead key planning runs (one per rank, shared by tables).
         MINIPS_PLAN_CUS=n confines it to n CUs spread over the chip (a CU-masked HIP stream), so
@@ -125,7 +157,7 @@ class Comm:
                 h = kernels().cu_masked_stream(self.device.index or 0, words)
                 self._plan_stream = torch.cuda.ExternalStream(h, device=self.device)
             else:
-                self._plan_stream = torch.cuda.Stream(device=self.device)
+                self._plan_stream = dedicated_stream(self.device)
         return self._plan_stream
 
     # -- helpers ------------------------------------------------------------------------

@@ -75,7 +75,7 @@ class _Pipeline:
             self.async_ = comm.device.type == "cuda" and overlap and (comm.world > 1 or w1 or kind in w1_kinds)
         else:
             self.async_ = comm.device.type == "cuda" and self.staleness > 0
-        self.stream = torch.cuda.Stream(device=comm.device) if self.async_ else None
+        self.stream = comm.new_stream() if self.async_ else None
         self.events: dict[int, torch.cuda.Event] = {}
         self.clock = 0
 
