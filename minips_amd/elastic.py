@@ -25,6 +25,19 @@ Recovery (at most one at a time; after ``max_restarts`` recoveries the job fails
   * restart: every rank is stopped and the whole set relaunched on a fresh rendezvous (also the
     fallback when the culprit is ambiguous or a survivor dies during an in-place recovery).
 A rank that exits 0 (finished, or kForceQuit for lack of data) is done, not failed.
+
+Live scale-out / scale-in (the reference's kScaleRollback, comm/mailbox.cpp:197-219, and
+Engine::UpdateAndRestart, driver/engine.cpp:96-112):
+
+    python -m minips_amd.elastic scale --run_dir <run_dir> --world M
+
+asks the running job to change its rank count to M. The supervisor writes a "scale" directive
+(new generation, rendezvous port, world M) next to the heartbeats and, for M > N, starts ranks
+N..M-1 with --use_weight_file=1. The running ranks agree on the iteration at which they saw it
+(a max all-reduce every --scale_check_every steps), save and commit a checkpoint there, leave the
+old group, and -- without leaving their processes -- ranks < M re-form the group at world M,
+rebuild their tables on the new shard ranges and restore that checkpoint (any N -> M reshard);
+ranks >= M retire (exit 0). The new ranks restore the same checkpoint and the job continues.
 """
 from __future__ import annotations
 
@@ -69,6 +82,8 @@ class Supervisor:
         self.procs: list[subprocess.Popen | None] = [None] * nproc
         self.failed_rank = -1
         self.port = 0
+        self.retired: set[int] = set()  # ranks >= the world of a scale-in (they exit by themselves)
+        self.scales = 0
 
     # ------------------------------------------------------------------------------ spawning
     def _env(self, r: int) -> dict:
@@ -140,6 +155,8 @@ class Supervisor:
         now = time.time()
         all_done, stalled = True, []
         for r, p in enumerate(self.procs):
+            if r in self.retired:
+                continue
             rc = p.poll()
             if rc is not None:
                 if rc != 0:
@@ -175,7 +192,7 @@ class Supervisor:
                 return "failed", r, f"no progress past step {self.progress[r][0]} for " \
                                     f"{now - self.progress[r][1]:.1f} s (stuck inside a step)", len(computing) == 1
             # everyone that stalled waits on peers: wait until every live rank has stalled
-            live = [r for r, p in enumerate(self.procs) if p.poll() is None]
+            live = [r for r, p in enumerate(self.procs) if p.poll() is None and r not in self.retired]
             if len(stalled) == len(live):
                 r = min(s[0] for s in stalled)
                 return "failed", r, "every rank waits on its peers (culprit ambiguous)", False
@@ -184,7 +201,7 @@ class Supervisor:
     # ------------------------------------------------------------------------------ recovery
     def _recover_inplace(self, rank: int) -> bool:
         """Relaunch only ``rank``; the survivors roll back in place. False: not possible."""
-        survivors = [r for r, p in enumerate(self.procs) if r != rank and p.poll() is None]
+        survivors = [r for r, p in enumerate(self.procs[:self.nproc]) if r != rank and p.poll() is None]
         if not survivors or len(survivors) != self.nproc - 1:
             return False
         self._stop([rank])
@@ -203,10 +220,45 @@ class Supervisor:
             self._reset_progress(r)
         return True
 
+    # ------------------------------------------------------------------------------ scaling
+    def _poll_scale(self):
+        """A pending ``scale`` request (<run_dir>/scale.json, written by ``elastic scale``)."""
+        path = os.path.join(self.run_dir, "scale.json")
+        try:
+            req = json.loads(open(path).read())
+        except (OSError, ValueError):
+            return
+        os.replace(path, os.path.join(self.run_dir, f"scale.{self.scales}.done.json"))
+        new = int(req.get("world", self.nproc))
+        if new < 1 or new == self.nproc:
+            return
+        old = self.nproc
+        self.scales += 1
+        self.generation += 1
+        self.port = _free_port()
+        self.failed_rank = -1
+        fault_tolerance_phase(3, f"scale {old} -> {new} ranks (generation {self.generation}): the running ranks "
+                                 f"checkpoint, re-form the group in place and reshard")
+        tmp = os.path.join(self.hb_dir, "rollback.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(dict(generation=self.generation, port=self.port, world=new, kind="scale", failed_rank=-1), f)
+        os.replace(tmp, os.path.join(self.hb_dir, "rollback.json"))
+        self.nproc = new
+        for r in range(min(old, new)):
+            self._reset_progress(r)
+        if new > old:
+            self.procs.extend([None] * (new - len(self.procs)))
+            for r in range(old, new):
+                self.retired.discard(r)
+                self._spawn_rank(r, resume=True)
+        else:
+            self.retired.update(range(new, old))
+
     def run(self) -> int:
         self._spawn_all(resume=False)
         while True:
             time.sleep(min(0.2, self.interval / 4) if self.interval > 0 else 0.2)
+            self._poll_scale()
             state, rank, reason, clear = self._check()
             if state == "done":
                 return 0
@@ -214,21 +266,38 @@ class Supervisor:
                 continue
             fault_tolerance_phase(2, f"rank {rank} failed (attempt {self.restarts}): {reason}")
             if self.restarts >= self.max_restarts:
-                self._stop(range(self.nproc))
+                self._stop(range(len(self.procs)))
                 print(f"[elastic] giving up after {self.restarts} restarts", file=sys.stderr, flush=True)
                 return 1
             if self.recovery == "inplace" and clear and self._recover_inplace(rank):
                 continue
-            self._stop(range(self.nproc))
+            self._stop(range(len(self.procs)))
             self.restarts += 1
             self.generation += 1
             self.failed_rank = rank
+            self.procs = self.procs[:self.nproc]
+            self.retired.clear()
             fault_tolerance_phase(3, f"relaunch {self.nproc} ranks from the last checkpoint")
             self._spawn_all(resume=True)
 
 
+def request_scale(run_dir: str, world: int):
+    """Ask the supervisor of the job under ``run_dir`` to change the rank count to ``world``."""
+    tmp = os.path.join(run_dir, "scale.json.tmp")
+    with open(tmp, "w") as f:
+        json.dump(dict(world=int(world), t=time.time()), f)
+    os.replace(tmp, os.path.join(run_dir, "scale.json"))
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
+    if argv and argv[0] == "scale":
+        ap = argparse.ArgumentParser(prog="python -m minips_amd.elastic scale")
+        ap.add_argument("--run_dir", required=True)
+        ap.add_argument("--world", type=int, required=True)
+        a = ap.parse_args(argv[1:])
+        request_scale(a.run_dir, a.world)
+        return 0
     if "--" not in argv:
         raise SystemExit("usage: python -m minips_amd.elastic [options] -- <rank command>")
     i = argv.index("--")

@@ -40,7 +40,6 @@ import torch
 import torch.distributed as dist
 
 
-@dataclass
 class _OwnedStream(torch.cuda.ExternalStream):
     """An ExternalStream over a stream this process created; destroyed with its last reference."""
 
@@ -69,6 +68,7 @@ def dedicated_stream(device, priority: int = 0):
     return _OwnedStream(h, device=device)
 
 
+@dataclass
 class CommStats:
     bytes_a2a: int = 0
     bytes_rs: int = 0

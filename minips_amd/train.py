@@ -50,6 +50,9 @@ def parse(argv=None):
     ap.add_argument("--fail_rank", type=int, default=-1)
     ap.add_argument("--fail_step", type=int, default=-1)
     ap.add_argument("--fail_mode", default="exit", choices=["exit", "hang", "hang_in_step"])
+    ap.add_argument("--scale_check_every", type=int, default=10,
+                    help="steps between checks for a supervisor scale directive (a max all-reduce of the "
+                         "directive generation the ranks saw; minips_amd.elastic scale)")
     ap.add_argument("--recovery", default="inplace", choices=["inplace", "restart"],
                     help="inplace: after a peer failure the survivors roll back in their processes and "
                          "the supervisor relaunches only the failed rank; restart: the whole rank set")
@@ -368,6 +371,15 @@ class _ckpt_state:
             self.hb.state = self.prev
 
 
+def _scale_directive(hb_dir: str, generation: int) -> dict | None:
+    """A supervisor scale directive newer than ``generation`` (None: none, or a failure rollback)."""
+    try:
+        d = json.loads(open(os.path.join(hb_dir, "rollback.json")).read())
+    except (OSError, ValueError):
+        return None
+    return d if d.get("kind") == "scale" and int(d.get("generation", -1)) > generation else None
+
+
 def _wait_directive(hb_dir: str, generation: int, timeout: float = 300.0) -> dict:
     """Rollback directive of the supervisor (minips_amd.elastic): a newer generation with the
     rendezvous port of the re-formed group (the reference's kRollBack, mailbox.cpp:172-191)."""
@@ -478,8 +490,60 @@ def main(argv=None):
         hb.progress(it0 - 1)
         return it0
 
+    def scale(it_now: int):
+        """Live rescale at a step boundary (the reference's kScaleRollback): every rank of the old
+        group checkpoints iteration ``it_now``, leaves the group; ranks < the new world re-form it
+        in this process, rebuild their tables on the new shard ranges and restore (reshard) that
+        checkpoint; the others retire. Returns the iteration to continue from, or None (retired)."""
+        nonlocal generation, data, losses, model, tables, make_data, step_fn, per_step, ck
+        hb.state = "recover"
+        model.drain()
+        with _ckpt_state(hb):
+            ck.save(tables, iteration=it_now, blocking=True)
+            ck.commit()
+        d = _wait_directive(args.heartbeat_dir, generation)
+        generation, world = int(d["generation"]), int(d["world"])
+        comm.barrier()
+        dist.destroy_process_group()
+        if rank >= world:
+            metrics.fault_tolerance_phase(5, f"rank {rank} retired by the scale to {world} ranks at iteration {it_now}")
+            hb.stop()
+            return None
+        os.environ.update(MASTER_PORT=str(d["port"]), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                          MINIPS_GENERATION=str(generation))
+        model = tables = step_fn = None  # free the old shards before the new ones are allocated
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        init_distributed()
+        comm.refresh()
+        model, tables, make_data, step_fn, per_step = build(args, comm)
+        ck = Checkpointer(comm, args.checkpoint_file_prefix, text_limit=args.checkpoint_text_limit)
+        it0 = ck.load(tables)
+        data = make_data()
+        data.skip(it0)
+        losses = [x for x in losses if x[0] < it0]
+        metrics.fault_tolerance_phase(5, f"rank {rank} rescaled in place to {world} ranks at iteration {it0} "
+                                         f"(generation {generation})")
+        hb.state = "run"
+        hb.progress(it0 - 1)
+        return it0
+
     it = start
     while it < args.steps:
+        # (the rule depends on ``it`` only: ranks started by a scale-out resume at the same
+        # iteration as the survivors and must take part in the same checks)
+        if hb is not None and args.scale_check_every > 0 and it % args.scale_check_every == 0:
+            # do the ranks agree that a scale directive is pending? (all of them act at THIS step)
+            d = _scale_directive(args.heartbeat_dir, generation)
+            flag = torch.tensor([float(d["generation"]) if d else 0.0], device=comm.device)
+            comm.all_reduce_(flag, op=dist.ReduceOp.MAX)
+            if float(flag) > generation:
+                nxt = scale(it)
+                if nxt is None:
+                    return 0
+                it = nxt
+                t_steady = None
+                continue
         try:
             if it == start + args.timing_skip and t_steady is None:
                 if comm.device.type == "cuda":
