@@ -618,18 +618,14 @@ int64_t cu_masked_stream(int64_t device, std::vector<int64_t> mask) {
 // A dedicated HIP stream (hipStreamCreateWithPriority), returned as an integer handle for
 // torch.cuda.ExternalStream. torch.cuda.Stream() hands out streams round-robin from a pool of 32 per
 // priority, so past 32 of them two "independent" streams silently alias (and a table's clock work
-// serialises behind another's planning); tables and the planning stream take their own instead.
-// stream_destroy releases one once the Python owner is gone (pending work completes first).
+// serialises behind another's planning); tables and the planning stream take their own instead
+// (never destroyed: the Python side reuses a dead owner's stream, see ps/comm.py).
 int64_t new_stream(int64_t device, int64_t priority) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
   hipStream_t st = nullptr;
   const hipError_t e = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, (int)priority);
   TORCH_CHECK(e == hipSuccess, "hipStreamCreateWithPriority: ", hipGetErrorString(e));
   return reinterpret_cast<int64_t>(st);
-}
-
-void stream_destroy(int64_t handle) {
-  if (handle) (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(handle));
 }
 
 void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
@@ -1388,7 +1384,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("softmax_xent", &softmax_xent);
   m.def("xent_from_stats", &xent_from_stats);
   m.def("new_stream", &new_stream);
-  m.def("stream_destroy", &stream_destroy);
   m.def("causal_softmax_fwd", &causal_softmax_fwd);
   m.def("causal_softmax_bwd", &causal_softmax_bwd);
   m.def("gelu_bwd", &gelu_bwd);

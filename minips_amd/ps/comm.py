@@ -40,32 +40,44 @@ import torch
 import torch.distributed as dist
 
 
+# handles of dedicated streams whose owner is gone, by (device index, priority): reused, never
+# destroyed -- the caching allocator may still record events on a stream a freed tensor was
+# record_stream()-ed to, so destroying one can crash a later free
+_FREE_STREAMS: dict[tuple[int, int], list[int]] = {}
+
+
 class _OwnedStream(torch.cuda.ExternalStream):
-    """An ExternalStream over a stream this process created; destroyed with its last reference."""
+    """An ExternalStream over a stream this process created; back to the free list with its last
+    reference (only LIVE users must not alias)."""
 
     def __del__(self):
         try:
-            from .._native import kernels
-
-            kernels().stream_destroy(int(self.cuda_stream))
+            _FREE_STREAMS.setdefault((self.device.index or 0, self._minips_prio), []).append(int(self.cuda_stream))
         except Exception:  # interpreter shutdown
             pass
 
 
 def dedicated_stream(device, priority: int = 0):
-    """A HIP stream no other stream aliases. torch.cuda.Stream() draws from a 32-per-priority
+    """A HIP stream no other live stream aliases. torch.cuda.Stream() draws from a 32-per-priority
     round-robin pool, so a long-lived process that builds many tables (Engine.create_table, the
     test suite) would otherwise get the SAME HIP stream for two "independent" lanes -- e.g. a
     table's clock pipeline and the planning stream -- and serialise one behind the other. Falls
     back to the pool when the native extension is not built."""
     device = torch.device(device)
-    try:
-        from .._native import kernels
+    idx = device.index or 0
+    free = _FREE_STREAMS.get((idx, int(priority)))
+    if free:
+        h = free.pop()
+    else:
+        try:
+            from .._native import kernels
 
-        h = kernels().new_stream(device.index or 0, int(priority))
-    except Exception:
-        return torch.cuda.Stream(device=device, priority=priority)
-    return _OwnedStream(h, device=device)
+            h = kernels().new_stream(idx, int(priority))
+        except Exception:
+            return torch.cuda.Stream(device=device, priority=priority)
+    s = _OwnedStream(h, device=device)
+    s._minips_prio = int(priority)
+    return s
 
 
 @dataclass
