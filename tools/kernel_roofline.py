@@ -28,45 +28,46 @@ def gemm(M, N, K, out_bytes, split=1):
     return flops, byts
 
 
+def _split(n_out, k_in, blocks=320, min_rows=1024):
+    """ops.linear_wgrad's split-K choice for W&D's overlapped weight gradients (blocks=320)."""
+    tiles = ((n_out + 127) // 128) * ((k_in + 127) // 128)
+    return max(1, min(B // min_rows, (blocks + tiles - 1) // tiles))
+
+
 def spec(U):
-    """(name regex, grid X or None, label, flops, bytes)"""
+    """(name regex, occurrence in the step, label, flops, bytes): the k-th kernel of the step (by
+    start time) whose name matches -- kernels of one name keep their issue order across streams."""
     n = B * F
+    s1, s2, s3 = _split(H1, K1), _split(H2, K2), _split(H3, K3)
     return [
-        (r"gemm_v2_kernel<256, 256, false, false", 262144, "fwd1 X.W1^T 16384x1024x896 +bias/ReLU",
-         *gemm(B, H1, K1, 2)),
-        (r"gemm_v2_kernel<128, 128, false, false", 131072, "fwd2 16384x512x1032 +ReLU", *gemm(B, H2, K2, 2)),
-        (r"gemm_v2_kernel<128, 128, false, false", 65536, "fwd3 16384x256x520 +ReLU", *gemm(B, H3, K3, 2)),
-        (r"gemm_v2_kernel<128, 128, false, true", 131072, "dgrad dH2 16384x512x256 (ReLU mask)",
+        (r"gemm_v2_kernel<256, 256, false, false", 0, "fwd1 X.W1^T 16384x1024x896 +bias/ReLU", *gemm(B, H1, K1, 2)),
+        (r"gemm_v2_kernel<128, 128, false, false", 0, "fwd2 16384x512x1032 +ReLU", *gemm(B, H2, K2, 2)),
+        (r"gemm_v2_kernel<128, 128, false, false", 1, "fwd3 16384x256x520 +ReLU", *gemm(B, H3, K3, 2)),
+        (r"gemm_v2_kernel<128, 128, false, true", 0, "dgrad dH2 16384x512x256 (ReLU mask)",
          gemm(B, H2, H3, 2)[0], gemm(B, H2, H3, 2)[1] + B * H2 * 2),
-        (r"gemm_v2_kernel<256, 256, false, true, 5", 262144, "dgrad dH1 16384x1024x512 (ReLU mask)",
+        (r"gemm_v2_kernel<256, 256, false, true, 5", 0, "dgrad dH1 16384x1024x512 (ReLU mask)",
          gemm(B, H1, H2, 2)[0], gemm(B, H1, H2, 2)[1] + B * H1 * 2),
-        (r"gemm_v2_kernel<256, 256, false, true, 4", 262144, "dgrad dX 16384x832x1024", *gemm(B, F * D, H1, 2)),
-        (r"gemm_v2_kernel<128, 128, true, true", None, "wgrad W3 256x520x16384 (split-K slabs)",
-         *gemm(H3, K3, B, 4, 16)),
-        (r"gemm_v2_kernel<256, 256, true, true", 10240, "wgrad W2 512x1032x16384 (split-K slabs)",
-         *gemm(H2, K2, B, 4, 15)),
-        (r"gemm_v2_kernel<256, 256, true, true", 16384, "wgrad W1 1024x896x16384 (split-K slabs)",
-         *gemm(H1, K1, B, 4, 10)),
-        (r"splitk_reduce_kernel", 33280, "split-K reduce W3 (16 planes)", 0, 16 * H3 * K3 * 4 + 2 * H3 * K3 * 4),
-        (r"splitk_reduce_kernel", 132096, "split-K reduce W2 (15 planes)", 0, 15 * H2 * K2 * 4 + 2 * H2 * K2 * 4),
-        (r"splitk_reduce_kernel", 229376, "split-K reduce W1 (10 planes)", 0, 10 * H1 * K1 * 4 + 2 * H1 * K1 * 4),
-        (r"gather_rows_vec4", None, "sparse Get: gather U rows -> bf16", 0, U * (W * 4 + W * 2 + 8)),
-        (r"wd_assemble_kernel", None, "assemble X (lookup + dense + wide sum)", 0,
-         B * K1 * 2 + n * (D * 2 + 8 + 2) + B * ND * 4 + B * 4),
-        (r"wd_head_kernel", None, "head Linear 256->1 + BCE fwd/bwd", 0, B * H3 * 2 * 2 + B * 12),
-        (r"zero_rows_dev_kernel", None, "zero grad rows", 0, U * W * 4),
-        (r"emb_seg_sum_kernel", None, "embedding backward (segment sums)", 0, n * (D * 2 + 8 + 4) + U * W * 4),
-        (r"sparse_rowwise_adagrad_v4", None, "row-wise Adagrad apply (U rows)", 0, U * (W * 4 * 3 + 8 + 8 + 8)),
-        (r"adam_kernel", None, "Adam (dense 1.58M params)", 0, 1582080 * (16 + 18)),
-        (r"criteo_synth_kernel", None, "synthetic batch (planning stream)", 0, B * (F * 8 + ND * 4 + 4)),
-        (r"plan_transpose_kernel", None, "plan: keys -> column-major (planning)", 0, n * (8 + 4)),
-        (r"plan_sort_col_kernel", None, "plan: per-column LDS radix sort, 26 WGs (planning)", 0,
-         n * (4 + 4 + 4) + U * 8),
-        (r"plan_emit_kernel", None, "plan: uniq / inv / lookup CSR (planning)", 0, n * (4 + 4 + 8 + 4 + 4) + U * 16),
-        (r"ub_insert_kernel", None, "hash dedupe: insert (planning, non-column tables)", 0, n * 8 * 2),
-        (r"ub_assign_kernel", None, "hash dedupe: assign (planning)", 0, n * 8 * 2 + U * 8),
-        (r"ub_inverse_kernel", None, "hash dedupe: inverse (planning)", 0, n * 8 * 2),
-        (r"emb_seg_fill_kernel", None, "lookup CSR fill (planning)", 0, n * (8 + 8)),
+        (r"gemm_v2_kernel<256, 256, false, true, 4", 0, "dgrad dX 16384x832x1024", *gemm(B, F * D, H1, 2)),
+        (r"gemm_v2_kernel<\d+, \d+, true, true", 0, f"wgrad W3 256x520x16384 ({s3} split-K slabs)",
+         *gemm(H3, K3, B, 4, s3)),
+        (r"gemm_v2_kernel<\d+, \d+, true, true", 1, f"wgrad W2 512x1032x16384 ({s2} split-K slabs)",
+         *gemm(H2, K2, B, 4, s2)),
+        (r"gemm_v2_kernel<\d+, \d+, true, true", 2, f"wgrad W1 1024x896x16384 ({s1} split-K slabs)",
+         *gemm(H1, K1, B, 4, s1)),
+        (r"splitk_reduce_kernel", 0, f"split-K reduce W3 ({s3} planes)", 0, s3 * H3 * K3 * 4 + 2 * H3 * K3 * 4),
+        (r"splitk_reduce_kernel", 1, f"split-K reduce W2 ({s2} planes)", 0, s2 * H2 * K2 * 4 + 2 * H2 * K2 * 4),
+        (r"splitk_reduce_kernel", 2, f"split-K reduce W1 ({s1} planes)", 0, s1 * H1 * K1 * 4 + 2 * H1 * K1 * 4),
+        (r"wd_assemble_tab_kernel", 0, "Get + assemble X (rows read from the fp32 shard + dense + wide sum)", 0,
+         B * K1 * 2 + n * (D * 4 + 4 + 8 + 8) + B * ND * 4 + B * 4),
+        (r"wd_head_kernel", 0, "head Linear 256->1 + BCE fwd/bwd", 0, B * H3 * 2 * 2 + B * 12),
+        (r"zero_rows_dev_kernel", 0, "zero grad rows", 0, U * W * 4),
+        (r"emb_seg_sum_kernel", 0, "embedding backward (segment sums)", 0, n * (D * 2 + 8 + 4) + U * W * 4),
+        (r"sparse_rowwise_adagrad_v4", 0, "row-wise Adagrad apply (U rows)", 0, U * (W * 4 * 3 + 8 + 8 + 8)),
+        (r"adam_kernel", 0, "Adam (dense 1.58M params)", 0, 1582080 * (16 + 18)),
+        (r"criteo_synth_kernel", 0, "synthetic batch (planning stream)", 0, B * (F * 8 + ND * 4 + 4)),
+        (r"plan_transpose_kernel", 0, "plan: keys -> column-major (planning)", 0, n * (8 + 4)),
+        (r"plan_sort_col_kernel", 0, "plan: per-column LDS radix sort, 26 WGs (planning)", 0, n * (4 + 4 + 4) + U * 8),
+        (r"plan_emit_kernel", 0, "plan: uniq / inv / lookup CSR (planning)", 0, n * (4 + 4 + 8 + 4 + 4) + U * 16),
     ]
 
 
@@ -107,23 +108,29 @@ def main():
         ap.error("trace and --U are required")
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "gather_rows" in r["Kernel_Name"]]
-    steps = [rows[starts[i]: starts[i + 1]] for i in range(a.skip, len(starts) - 1)]
+    # one step = from one Adam (the last kernel of a step) to the next
+    starts = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    steps = [rows[starts[i] + 1: starts[i + 1] + 1] for i in range(a.skip, len(starts) - 1)]
     specs = spec(a.U)
     per = {}
     for st in steps:
+        seen = {}
         for r in st:
-            name, gx = r["Kernel_Name"], int(r["Grid_Size_X"])
-            for pat, g, label, fl, by in specs:
-                if re.search(pat, name) and (g is None or g == gx):
-                    per.setdefault(label, (fl, by, []))[2].append((int(r["End_Timestamp"]) -
-                                                                  int(r["Start_Timestamp"])) / 1e3)
-                    break
+            name = r["Kernel_Name"]
+            for pat, k, label, fl, by in specs:
+                if re.search(pat, name):
+                    if seen.get(pat, 0) == k:
+                        per.setdefault(label, (fl, by, []))[2].append((int(r["End_Timestamp"]) -
+                                                                      int(r["Start_Timestamp"])) / 1e3)
+                        seen[pat] = k + 1
+                        break
+                    if seen.get(pat, 0) > k:
+                        continue
     print(f"# W&D 1-GPU step: per-kernel achieved rates ({len(steps)} steady steps, U = {a.U:.0f})\n")
     print("| kernel | us (median) | GFLOP | MB | TFLOP/s | % bf16 peak | TB/s | % HBM peak |")
     print("|---|---|---|---|---|---|---|---|")
     tot = 0.0
-    for _, _, label, _, _ in specs:
+    for _, _, label, _, _ in specs:  # (in spec order)
         if label not in per:
             continue
         fl, by, ds = per[label]
