@@ -126,7 +126,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     ldmask = (int)mask->stride(0);
   }
   const bool needs_mask = epi == minips_k::kEpiReluMaskBf16 || epi == minips_k::kEpiBiasGeluAuxBf16 ||
-                          epi == minips_k::kEpiGeluGradBf16;
+                          epi == minips_k::kEpiGeluGradBf16 || epi == minips_k::kEpiBiasGeluDAuxBf16 ||
+                          epi == minips_k::kEpiMulAuxBf16;
   if (needs_mask) TORCH_CHECK(mask_p, "this epilogue needs mask/aux");
   float* colsum_p = epi == minips_k::kEpiXentStatsBf16 ? opt_ptr<float>(colsum, at::kFloat, "colsum")
                                                       : strided_vec_ptr(colsum, "colsum");

@@ -144,8 +144,9 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
     const int col = nb + j * 16 + col_l;
     const bool col_ok = col < N;
     float bias = 0.f;
-    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16
-        || EPI == kEpiBiasGeluAuxBf16) bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
+    if (EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16 ||
+        EPI == kEpiBiasGeluDAuxBf16)
+      bias = (ep.bias && col_ok) ? bf2f(ep.bias[col]) : 0.f;
     float csum = 0.f;
 #pragma unroll
     for (int i = 0; i < MR; ++i) {
@@ -176,6 +177,15 @@ __device__ __forceinline__ void epilogue_at(const v4f (&acc)[MR][4], const EpiAr
           const float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
           ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
           const_cast<bf16_t*>(ep.mask)[(int64_t)row * ep.ldmask + col] = f2bf(x);
+        } else if (EPI == kEpiBiasGeluDAuxBf16) {
+          const float x = v + bias;
+          const float k = 0.7978845608f, c3 = 0.044715f;
+          const float t = tanhf(k * (x + c3 * x * x * x));
+          ((bf16_t*)ep.C)[off] = f2bf(0.5f * x * (1.f + t));
+          const_cast<bf16_t*>(ep.mask)[(int64_t)row * ep.ldmask + col] =
+              f2bf(0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * c3 * x * x));
+        } else if (EPI == kEpiMulAuxBf16) {
+          ((bf16_t*)ep.C)[off] = f2bf(v * bf2f(ep.mask[(int64_t)row * ep.ldmask + col]));
         } else if (EPI == kEpiGeluGradBf16) {
           const float u = bf2f(ep.mask[(int64_t)row * ep.ldmask + col]);
           const float k = 0.7978845608f, c3 = 0.044715f;
@@ -216,12 +226,16 @@ template <int EPI>
 __device__ __forceinline__ float epi_apply(float v, float bias, float m, bf16_t* aux_out) {
   if (EPI == kEpiBiasReluBf16) return fmaxf(v + bias, 0.f);
   if (EPI == kEpiBiasBf16) return v + bias;
-  if (EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16) {
+  if (EPI == kEpiBiasGeluBf16 || EPI == kEpiBiasGeluAuxBf16 || EPI == kEpiBiasGeluDAuxBf16) {
     const float x = v + bias;
     if (EPI == kEpiBiasGeluAuxBf16) *aux_out = f2bf(x);
-    const float t = tanhf(0.7978845608f * (x + 0.044715f * x * x * x));
+    const float k = 0.7978845608f, c3 = 0.044715f;
+    const float t = tanhf(k * (x + c3 * x * x * x));
+    if (EPI == kEpiBiasGeluDAuxBf16)
+      *aux_out = f2bf(0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * c3 * x * x));
     return 0.5f * x * (1.f + t);
   }
+  if (EPI == kEpiMulAuxBf16) return v * m;
   if (EPI == kEpiGeluGradBf16) {
     const float k = 0.7978845608f, c3 = 0.044715f;
     const float t = tanhf(k * (m + c3 * m * m * m));
@@ -237,8 +251,9 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
                                              int lane, float* __restrict__ scr) {
   constexpr bool F32OUT = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
   constexpr bool HAS_BIAS = EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 ||
-                            EPI == kEpiBiasGeluAuxBf16;
-  constexpr bool READ_MASK = EPI == kEpiReluMaskBf16 || EPI == kEpiGeluGradBf16;
+                            EPI == kEpiBiasGeluAuxBf16 || EPI == kEpiBiasGeluDAuxBf16;
+  constexpr bool READ_MASK = EPI == kEpiReluMaskBf16 || EPI == kEpiGeluGradBf16 || EPI == kEpiMulAuxBf16;
+  constexpr bool WRITE_AUX = EPI == kEpiBiasGeluAuxBf16 || EPI == kEpiBiasGeluDAuxBf16;
   const int col_l = lane & 15, row_q = (lane >> 4) * 4;
   // vector paths need 16-byte aligned row segments
   const bool c_vec = (EPI == kEpiPermRowsBf16 ? (ep.seg & 7) == 0 : (ep.ldc & (F32OUT ? 3 : 7)) == 0) &&
@@ -380,7 +395,7 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
           for (int e = 0; e < 8; ++e)
             if (col + e < N) dst[e] = (bf16_t)((e & 1) ? (pk[e >> 1] >> 16) : (pk[e >> 1] & 0xffffu));
         }
-        if (EPI == kEpiBiasGeluAuxBf16) {
+        if (WRITE_AUX) {
           bf16_t* adst = const_cast<bf16_t*>(ep.mask) + moff;
           if (m_vec && full) {
             uint32_t a[4];
@@ -1026,6 +1041,8 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
     MINIPS_EPI_CASE(AKM, BKN, kEpiGeluGradBf16)                                  \
     MINIPS_EPI_CASE(AKM, BKN, kEpiPermRowsBf16)                                  \
     MINIPS_EPI_CASE(AKM, BKN, kEpiAccumF32)                                      \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiBiasGeluDAuxBf16)                              \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiMulAuxBf16)                                    \
     case kEpiXentStatsBf16:                                                      \
       if constexpr (!AKM && !BKN) {                                              \
         nsplit = launch<false, false, kEpiXentStatsBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); \

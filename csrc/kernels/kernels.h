@@ -35,6 +35,10 @@ enum GemmEpilogue {
   kEpiXentStatsBf16 = 11,
   // the W&D output head as the epilogue of the last hidden layer (gemm_wd_head only)
   kEpiWdHead = 12,
+  // C bf16 = gelu_tanh(u), aux bf16 = gelu'(u), u = acc + bias: the backward multiplies by the stored
+  // derivative (kEpiMulAuxBf16) instead of re-evaluating tanh of the saved pre-activation
+  kEpiBiasGeluDAuxBf16 = 13,
+  kEpiMulAuxBf16 = 14,  // C bf16 = acc * mask(aux)
 };
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,

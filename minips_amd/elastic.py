@@ -83,6 +83,7 @@ class Supervisor:
         self.failed_rank = -1
         self.port = 0
         self.retired: set[int] = set()  # ranks >= the world of a scale-in (they exit by themselves)
+        self._last_state: dict[int, str] = {}
         self.scales = 0
 
     # ------------------------------------------------------------------------------ spawning
@@ -177,7 +178,14 @@ class Supervisor:
             last, since = self.progress.get(r, (None, now))
             if step != last or state == "recover":
                 self.progress[r] = (step, now)
+                self._last_state[r] = state
                 continue
+            if self._last_state.get(r) == "ckpt" and state != "ckpt":
+                # a checkpoint phase just ended: its (long-limit) time does not count against the
+                # step that follows it
+                self.progress[r] = (step, now)
+                since = now
+            self._last_state[r] = state
             # a checkpoint write / commit advances no step: it gets its own, longer limit
             limit = self.startup_grace if step < 0 else (self.ckpt_timeout if state == "ckpt"
                                                          else self.progress_timeout)

@@ -13,7 +13,7 @@ Compute path (all gfx950 kernels from minips_amd.ops, no autograd):
                               place from qkv, O written into the bias-folded proj input, only
                               the per-query log-sum-exp kept for the backward)
   gemm + add_bf16             x_mid = x + O W_o^T
-  gemm (GELU-aux epilogue)    g = gelu(ln2 W_fc^T), pre-activation u saved
+  gemm (GELU-aux epilogue)    g = gelu(ln2 W_fc^T), gelu'(u) saved for the fc2 dgrad
   gemm + add_bf16             x_next = x_mid + g W_proj^T
   gemm (xent-stats epilogue)  logits = ln_f(x) wte^T (bf16) + per-64-column softmax partials
   xent_from_stats             lse from the partials, (softmax - onehot) / (B T) in place (one pass)
@@ -67,7 +67,10 @@ _LM_DGRAD_SPLIT = int(os.environ.get("MINIPS_LM_DGRAD_SPLIT", "4"))
 # LM-head GEMMs (logits, dgrad, wte wgrad): "lib" (hipBLASLt through torch for these three plain
 # GEMMs: 13.10 vs 13.87 ms/step) or "ours" (gemm.hip); the CPU reference path always uses ours
 _LM_GEMM = os.environ.get("MINIPS_LM_GEMM", "lib")
-_LM_WGRAD = os.environ.get("MINIPS_LM_WGRAD", "mm")  # lib form of the wte wgrad: "mm" (overwrite) | "addmm"
+_LM_WGRAD = os.environ.get("MINIPS_LM_WGRAD", "mm")
+# MLP: the fc forward saves gelu'(u) (its tanh is computed there anyway) and the fc2 dgrad multiplies
+# by it; MINIPS_GPT2_GELU_D=0 saves u and re-evaluates tanh in the dgrad epilogue
+_GELU_D = os.environ.get("MINIPS_GPT2_GELU_D", "1") == "1"  # lib form of the wte wgrad: "mm" (overwrite) | "addmm"
 
 
 class GPT2:
@@ -176,7 +179,7 @@ class GPT2:
             ops.add_bf16(x[i], b["tmp"], b["xm"][i])
             m2, r2 = b["st2"][i]
             ops.layernorm_fwd(b["xm"][i], d, v(P, blk["ln2_g"]), v(P, blk["ln2_b"]), 1e-5, b["h2"][i], m2, r2)
-            blk["fc"].forward(P, b["h2"][i], b["g"][i], "gelu_aux", aux=b["u"][i])
+            blk["fc"].forward(P, b["h2"][i], b["g"][i], "gelu_daux" if _GELU_D else "gelu_aux", aux=b["u"][i])
             blk["fc2"].forward(P, b["g"][i], b["tmp"], "none")
             ops.add_bf16(b["xm"][i], b["tmp"], x[i + 1])
         mf, rf = b["stf"]
@@ -226,7 +229,10 @@ class GPT2:
                 blk["fc2"].wgrad(G, dx, b["g"][i])
             ev_dx = side.mark()
             side.wait(ev_du)  # du: read by the previous layer's fc wgrad
-            blk["fc2"].dgrad(P, dx, b["du"], gelu_u=b["u"][i])
+            if _GELU_D:
+                blk["fc2"].dgrad(P, dx, b["du"], gelu_d=b["u"][i])
+            else:
+                blk["fc2"].dgrad(P, dx, b["du"], gelu_u=b["u"][i])
             with side.fork():
                 blk["fc"].wgrad(G, b["du"], b["h2"][i])
             ev_du = side.mark()

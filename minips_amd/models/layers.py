@@ -75,6 +75,9 @@ class Linear:
         """out[:, :n_out] = act(x_ext W_ext^T); x_ext carries the ones column."""
         W = self.W(P)
         M = x_ext.shape[0]
+        if act == "gelu_daux":  # aux <- gelu'(u): the backward multiplies (dgrad gelu_d=aux)
+            return ops.gemm(x_ext, W, out, M, self.n_out, self.k_pad, False, False, ops.EPI_BIAS_GELU_DAUX_BF16,
+                            mask=aux)
         if act == "gelu_aux":
             return ops.gemm(x_ext, W, out, M, self.n_out, self.k_pad, False, False, ops.EPI_BIAS_GELU_AUX_BF16,
                             mask=aux)
@@ -85,7 +88,7 @@ class Linear:
         """G_W += dy^T x_ext (split-K; the bias gradient lands in column k_in)."""
         return ops.linear_wgrad(dy, x_ext, self.W(G))
 
-    def dgrad(self, P, dy, out, mask=None, gelu_u=None, out_f32=False, k_rows=None):
+    def dgrad(self, P, dy, out, mask=None, gelu_u=None, out_f32=False, k_rows=None, gelu_d=None):
         """out = dy W[:, :k_in] (ReLU-masked by `mask`, or times gelu'(gelu_u)).
 
         The [K][N] weight layout is read 8 columns at a time, so an unaligned k_in computes
@@ -97,6 +100,8 @@ class Linear:
         assert out.shape[1] >= N, f"dgrad output needs {N} columns"
         if out_f32:
             return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_STORE_F32)
+        if gelu_d is not None:  # times the saved derivative gelu'(u)
+            return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_MUL_AUX_BF16, mask=gelu_d)
         if gelu_u is not None:
             return ops.gemm(dy, W, out, M, N, K, False, True, ops.EPI_GELU_GRAD_BF16, mask=gelu_u)
         if mask is not None:

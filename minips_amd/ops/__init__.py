@@ -25,6 +25,8 @@ EPI_BIAS_GELU_AUX_BF16 = 7  # C = gelu(u), mask(aux) = u  (pre-activation saved 
 EPI_GELU_GRAD_BF16 = 8      # C = acc * gelu'(mask)
 EPI_PERM_ROWS_BF16 = 9      # C rows of `seg` columns permuted by `perm` (embedding dgrad in planner order)
 EPI_XENT_STATS_BF16 = 11    # C = acc (bf16 logits) + per-64-column softmax partials into colsum (seg = vocab)
+EPI_BIAS_GELU_DAUX_BF16 = 13  # C = gelu(u), mask(aux) = gelu'(u)  (the derivative saved for backward)
+EPI_MUL_AUX_BF16 = 14       # C = acc * mask(aux)
 _L2E = 1.4426950408889634
 
 
@@ -61,6 +63,13 @@ def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None,
         C[:M, :N] = torch.nn.functional.gelu(acc, approximate="tanh").to(torch.bfloat16)
     elif epi == EPI_GELU_GRAD_BF16:
         C[:M, :N] = (acc * _gelu_grad(mask[:M, :N].float())).to(torch.bfloat16)
+    elif epi == EPI_BIAS_GELU_DAUX_BF16:
+        if bias is not None:
+            acc = acc + bias[:N].float()
+        mask[:M, :N] = _gelu_grad(acc).to(torch.bfloat16)
+        C[:M, :N] = torch.nn.functional.gelu(acc, approximate="tanh").to(torch.bfloat16)
+    elif epi == EPI_MUL_AUX_BF16:
+        C[:M, :N] = (acc * mask[:M, :N].float()).to(torch.bfloat16)
     elif epi in (EPI_BIAS_RELU_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU_BF16):
         if bias is not None:
             acc = acc + bias[:N].float()

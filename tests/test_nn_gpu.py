@@ -175,9 +175,18 @@ def test_gemm_strided_batched_and_gelu(dev):
         dX = torch.empty(M, N, dtype=torch.bfloat16, device=d)
         ops.gemm(dY.to(d), torch.eye(N, dtype=torch.bfloat16, device=d), dX, M, N, N, False, True,
                  ops.EPI_GELU_GRAD_BF16, mask=U)
-        out[str(d)] = (C, U, dX)
+        # the derivative-saving form: aux = gelu'(u), then dX = dY * aux
+        C2 = torch.empty(M, N, dtype=torch.bfloat16, device=d)
+        Dg = torch.empty(M, N, dtype=torch.bfloat16, device=d)
+        ops.gemm(X.to(d), W.to(d), C2, M, N, K, False, False, ops.EPI_BIAS_GELU_DAUX_BF16, mask=Dg)
+        dX2 = torch.empty(M, N, dtype=torch.bfloat16, device=d)
+        ops.gemm(dY.to(d), torch.eye(N, dtype=torch.bfloat16, device=d), dX2, M, N, N, False, True,
+                 ops.EPI_MUL_AUX_BF16, mask=Dg)
+        out[str(d)] = (C, U, dX, C2, Dg, dX2)
     for a, b in zip(out[str(dev)], out["cpu"]):
         _close(a, b, 3e-2)
+    # both backward forms agree (gelu' of a bf16 u vs a bf16 gelu'(u): bf16 rounding apart)
+    _close(out[str(dev)][5], out[str(dev)][2], 3e-2)
 
 
 # ------------------------------------------------------------------------------ models
