@@ -67,10 +67,10 @@ _LM_DGRAD_SPLIT = int(os.environ.get("MINIPS_LM_DGRAD_SPLIT", "4"))
 # LM-head GEMMs (logits, dgrad, wte wgrad): "lib" (hipBLASLt through torch for these three plain
 # GEMMs: 13.10 vs 13.87 ms/step) or "ours" (gemm.hip); the CPU reference path always uses ours
 _LM_GEMM = os.environ.get("MINIPS_LM_GEMM", "lib")
-_LM_WGRAD = os.environ.get("MINIPS_LM_WGRAD", "mm")
+_LM_WGRAD = os.environ.get("MINIPS_LM_WGRAD", "mm")  # lib form of the wte wgrad: "mm" (overwrite) | "addmm"
 # MLP: the fc forward saves gelu'(u) (its tanh is computed there anyway) and the fc2 dgrad multiplies
 # by it; MINIPS_GPT2_GELU_D=0 saves u and re-evaluates tanh in the dgrad epilogue
-_GELU_D = os.environ.get("MINIPS_GPT2_GELU_D", "1") == "1"  # lib form of the wte wgrad: "mm" (overwrite) | "addmm"
+_GELU_D = os.environ.get("MINIPS_GPT2_GELU_D", "1") == "1"
 
 
 class GPT2:
