@@ -58,7 +58,7 @@ int ProgressTracker::DeleteNode(uint32_t node_id) {
         min_clock_ += 1;
         result = min_clock_;
       }
-      MINIPS_LOG(0, "DeleteNode: tid:" << it->first << ", progress:" << it->second);
+      MINIPS_LOG(0, "worker " << it->first << " of failed node " << node_id << " dropped at clock " << it->second);
       it = progresses_.erase(it);
     } else {
       ++it;
@@ -318,8 +318,8 @@ void BSPModel::AdvanceSuperstep() {
 void BSPModel::Add(Message& msg) {
   MINIPS_CHECK(tracker_.CheckThreadValid(msg.meta.sender), "unknown sender " << msg.meta.sender);
   int progress = tracker_.GetProgress(msg.meta.sender);
-  MINIPS_CHECK(progress == tracker_.GetMinClock(), "progress error in BSPModel::Add: progress " << progress
-                                                       << " min_clock " << tracker_.GetMinClock());
+  MINIPS_CHECK(progress == tracker_.GetMinClock(), "BSP add from worker at clock " << progress
+                                                       << " while the table is at " << tracker_.GetMinClock());
   add_buffer_.push_back(msg);
 }
 
@@ -331,9 +331,8 @@ void BSPModel::Get(Message& msg) {
   } else if (progress == tracker_.GetMinClock()) {
     ReplyGet(msg);
   } else {
-    MINIPS_CHECK(false, "progress error in BSPModel::Get { get progress: " << progress
-                                                                          << ", min clock: "
-                                                                          << tracker_.GetMinClock() << " }");
+    MINIPS_CHECK(false, "BSP get from worker at clock " << progress << " while the table is at "
+                                                                << tracker_.GetMinClock());
   }
 }
 
