@@ -86,6 +86,15 @@ _TRIM = os.environ.get("MINIPS_WD_TRIM", "0") == "1"
 # split-K workgroup target of the three weight gradients (ops.linear_wgrad blocks): W&D 0.402 ms at
 # 320 vs 0.409-0.412 at the default 512 (GPT-2 keeps 512: 12.90 vs 13.18 ms at 256), ab_wd_r3.txt
 _WGRAD_BLOCKS = int(os.environ.get("MINIPS_WD_WGRAD_BLOCKS", "320"))
+# MINIPS_WD_WGRAD=lib: the three weight gradients as overwriting hipBLASLt GEMMs with fp32 output
+# (each gradient has one writer per step) instead of the split-K gemm.hip path
+_WGRAD_LIB = os.environ.get("MINIPS_WD_WGRAD", "ours") == "lib"
+
+
+def _wgrad(dH, H, Gw):
+    if _WGRAD_LIB and dH.is_cuda:
+        return torch.mm(dH.t(), H, out_dtype=torch.float32, out=Gw[: dH.shape[1]])
+    return ops.linear_wgrad(dH, H, Gw, blocks=_WGRAD_BLOCKS)
 
 
 def _align(n, a=8):
@@ -277,7 +286,7 @@ class WideDeep(LookaheadPlans):
             if trim:
                 ops.linear_wgrad(b["dH3"], b["H2"][:, :k3], self.view(G, "W3")[:, :k3], blocks=_WGRAD_BLOCKS)
             else:
-                ops.linear_wgrad(b["dH3"], b["H2"], self.view(G, "W3"), blocks=_WGRAD_BLOCKS)
+                _wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"],
                          colsum=self.view(G, "W2")[:, k2] if trim else None)
         with side.fork():
@@ -286,10 +295,10 @@ class WideDeep(LookaheadPlans):
             if trim:
                 ops.linear_wgrad(b["dH2"], b["H1"][:, :k2], self.view(G, "W2")[:, :k2], blocks=_WGRAD_BLOCKS)
             else:
-                ops.linear_wgrad(b["dH2"], b["H1"], self.view(G, "W2"), blocks=_WGRAD_BLOCKS)
+                _wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         with side.fork():
-            ops.linear_wgrad(b["dH1"], b["X"], self.view(G, "W1"), blocks=_WGRAD_BLOCKS)
+            _wgrad(b["dH1"], b["X"], self.view(G, "W1"))
         # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
