@@ -11,6 +11,9 @@ and planned on the planning stream every step). One entry point:
     python tools/step_probe.py ablation  feeder step vs a ring of pre-planned batches (+ the planning
                                          stream's work issued beside / after / without bookkeeping).
                                          Diagnostic only: the ring numbers are not valid benchmarks.
+    python tools/step_probe.py curve     per-step GPU time (HIP events) of the first STEPS steps after
+                                         the model build, averaged over step ranges; SPIN_MS > 0 first
+                                         keeps the GPU busy with GEMMs for that long (clock-ramp test)
 STEPS (env) sets the step count.
 """
 from __future__ import annotations
@@ -163,9 +166,40 @@ def cmd_ablation(n):
           f"kernels without record_stream/events {bare:.4f} ms")
 
 
+def cmd_curve(n):
+    _, _, _, feeder = _setup()
+    spin = float(os.environ.get("SPIN_MS", "0"))
+    if spin > 0:
+        a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < spin:
+            for _ in range(8):
+                a @ a
+            torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    host = [0.0] * n
+    evs[0].record()
+    for i in range(n):
+        t = time.perf_counter()
+        feeder.step()
+        evs[i + 1].record()
+        host[i] = (time.perf_counter() - t) * 1e3
+    torch.cuda.synchronize()
+    ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
+    edges = [0, 1, 2, 5, 10, 20, 30, 50, 80, 120, 200, 300, 500]
+    print(f"spin {spin:.0f} ms before step 0; reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB, "
+          f"alloc retries {torch.cuda.memory_stats().get('num_alloc_retries', 0)}")
+    for lo, hi in zip(edges, edges[1:]):
+        if lo < n:
+            seg, hseg = ms[lo:min(hi, n)], host[lo:min(hi, n)]
+            print(f"steps {lo:4d}-{min(hi, n) - 1:4d}: GPU {sum(seg) / len(seg):.4f} ms/step, host issue "
+                  f"{sum(hseg) / len(hseg):.4f} ms/step", flush=True)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("cmd", choices=["issue", "cprofile", "events", "ablation"])
+    ap.add_argument("cmd", choices=["issue", "cprofile", "events", "ablation", "curve"])
     a = ap.parse_args(argv)
     n = int(os.environ.get("STEPS", "300"))
     globals()["cmd_" + a.cmd](n)
