@@ -13,7 +13,8 @@ and planned on the planning stream every step). One entry point:
                                          Diagnostic only: the ring numbers are not valid benchmarks.
     python tools/step_probe.py curve     per-step GPU time (HIP events) of the first STEPS steps after
                                          the model build, averaged over step ranges; SPIN_MS > 0 first
-                                         keeps the GPU busy with GEMMs for that long (clock-ramp test)
+                                         keeps the GPU busy with GEMMs for that long (clock-ramp test);
+                                         REPEAT=k measures k curves in one process, PAUSE_S idle between
 STEPS (env) sets the step count.
 """
 from __future__ import annotations
@@ -178,23 +179,26 @@ def cmd_curve(n):
                 a @ a
             torch.cuda.synchronize()
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
-    host = [0.0] * n
-    evs[0].record()
-    for i in range(n):
-        t = time.perf_counter()
-        feeder.step()
-        evs[i + 1].record()
-        host[i] = (time.perf_counter() - t) * 1e3
-    torch.cuda.synchronize()
-    ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
-    edges = [0, 1, 2, 5, 10, 20, 30, 50, 80, 120, 200, 300, 500]
-    print(f"spin {spin:.0f} ms before step 0; reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB, "
-          f"alloc retries {torch.cuda.memory_stats().get('num_alloc_retries', 0)}")
-    for lo, hi in zip(edges, edges[1:]):
-        if lo < n:
-            seg, hseg = ms[lo:min(hi, n)], host[lo:min(hi, n)]
-            print(f"steps {lo:4d}-{min(hi, n) - 1:4d}: GPU {sum(seg) / len(seg):.4f} ms/step, host issue "
-                  f"{sum(hseg) / len(hseg):.4f} ms/step", flush=True)
+    for rep in range(int(os.environ.get("REPEAT", "1"))):
+        if rep:
+            time.sleep(float(os.environ.get("PAUSE_S", "0.5")))  # idle, queue drained
+        host = [0.0] * n
+        evs[0].record()
+        for i in range(n):
+            t = time.perf_counter()
+            feeder.step()
+            evs[i + 1].record()
+            host[i] = (time.perf_counter() - t) * 1e3
+        torch.cuda.synchronize()
+        ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
+        edges = [0, 1, 2, 5, 10, 20, 30, 50, 80, 120, 200, 300, 500]
+        print(f"spin {spin:.0f} ms before step 0; reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB, "
+              f"alloc retries {torch.cuda.memory_stats().get('num_alloc_retries', 0)}")
+        for lo, hi in zip(edges, edges[1:]):
+            if lo < n:
+                seg, hseg = ms[lo:min(hi, n)], host[lo:min(hi, n)]
+                print(f"steps {lo:4d}-{min(hi, n) - 1:4d}: GPU {sum(seg) / len(seg):.4f} ms/step, host issue "
+                      f"{sum(hseg) / len(hseg):.4f} ms/step", flush=True)
 
 
 def main(argv=None):
