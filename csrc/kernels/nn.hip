@@ -224,7 +224,12 @@ __global__ __launch_bounds__(256) void layernorm_colsum_kernel(const float* __re
 
 // ~8 rows per 4-wave block: 4x the waves of a 32-rows-per-block split, so the row loop's
 // dependent load -> reduce -> store chain is hidden by occupancy instead of serialised.
-int layernorm_bwd_blocks(int64_t M) { return (int)std::min<int64_t>(std::max<int64_t>((M + 7) / 8, 1), 1024); }
+// MINIPS_LN_BWD_ROWS / MINIPS_LN_BWD_MAXB override the rows per block and the block cap (A/B knobs).
+int layernorm_bwd_blocks(int64_t M) {
+  static const int rows = [] { const char* e = std::getenv("MINIPS_LN_BWD_ROWS"); return e ? std::max(1, atoi(e)) : 8; }();
+  static const int cap = [] { const char* e = std::getenv("MINIPS_LN_BWD_MAXB"); return e ? std::max(1, atoi(e)) : 1024; }();
+  return (int)std::min<int64_t>(std::max<int64_t>((M + rows - 1) / rows, 1), cap);
+}
 
 void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gamma, const bf16_t* beta, float eps,
                    bf16_t* y, int ldy, float* mean, float* rstd, hipStream_t s) {
