@@ -226,8 +226,12 @@ __global__ __launch_bounds__(256) void layernorm_colsum_kernel(const float* __re
 // dependent load -> reduce -> store chain is hidden by occupancy instead of serialised.
 // MINIPS_LN_BWD_ROWS / MINIPS_LN_BWD_MAXB override the rows per block and the block cap (A/B knobs).
 int layernorm_bwd_blocks(int64_t M) {
-  static const int rows = [] { const char* e = std::getenv("MINIPS_LN_BWD_ROWS"); return e ? std::max(1, atoi(e)) : 8; }();
-  static const int cap = [] { const char* e = std::getenv("MINIPS_LN_BWD_MAXB"); return e ? std::max(1, atoi(e)) : 1024; }();
+  auto knob = [](const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::max(1, atoi(e)) : dflt;
+  };
+  static const int rows = knob("MINIPS_LN_BWD_ROWS", 8);
+  static const int cap = knob("MINIPS_LN_BWD_MAXB", 1024);
   return (int)std::min<int64_t>(std::max<int64_t>((M + rows - 1) / rows, 1), cap);
 }
 
