@@ -1079,11 +1079,21 @@ void dlrm_interact_bwd(const at::Tensor& V, int64_t NV, int64_t D, int64_t dense
 
 // --- one-sided shards over xGMI (minips_amd/ps/onesided.py) -------------------------------------
 // A hipMalloc'd, zero-filled buffer exported for IPC: (uint8 tensor owning it, 64-byte handle).
-std::tuple<at::Tensor, py::bytes> ipc_alloc(int64_t nbytes, int64_t device) {
+// kind: 0 coarse-grained (hipMalloc), 1 fine-grained (shards / pull copies / control lines: coherent
+// for peer reads and system-scope atomics), 2 uncached (inboxes: written by peers, read once by the
+// owner). The memory model of these buffers is written down in csrc/kernels/onesided.hip.
+std::tuple<at::Tensor, py::bytes> ipc_alloc(int64_t nbytes, int64_t device, int64_t kind) {
   TORCH_CHECK(nbytes > 0, "ipc_alloc: nbytes must be > 0");
   c10::hip::HIPGuardMasqueradingAsCUDA g(at::Device(at::kCUDA, (c10::DeviceIndex)device));
   void* p = nullptr;
-  TORCH_CHECK(hipMalloc(&p, (size_t)nbytes) == hipSuccess, "ipc_alloc: hipMalloc of ", nbytes, " bytes failed");
+  if (kind == 0) {
+    TORCH_CHECK(hipMalloc(&p, (size_t)nbytes) == hipSuccess, "ipc_alloc: hipMalloc of ", nbytes, " bytes failed");
+  } else {
+    TORCH_CHECK(hipExtMallocWithFlags(&p, (size_t)nbytes,
+                                      kind == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached) == hipSuccess,
+                "ipc_alloc: hipExtMallocWithFlags(", kind == 1 ? "fine-grained" : "uncached", ") of ", nbytes,
+                " bytes failed");
+  }
   TORCH_CHECK(hipMemset(p, 0, (size_t)nbytes) == hipSuccess, "ipc_alloc: hipMemset failed");
   hipIpcMemHandle_t h;
   TORCH_CHECK(hipIpcGetMemHandle(&h, p) == hipSuccess, "ipc_alloc: hipIpcGetMemHandle failed");
@@ -1162,6 +1172,92 @@ void ps_gather_rows(const at::Tensor& bases, const at::Tensor& bounds, const at:
                            opt_count(n_dev), (int)W, out.data_ptr(), bf, stream_of(keys));
 }
 
+void ps_gather_rows_bf16tab(const at::Tensor& bases, const at::Tensor& bounds, const at::Tensor& keys,
+                            const c10::optional<at::Tensor>& n_dev, int64_t W, at::Tensor& out) {
+  check_long_dev(bases, "bases");
+  check_long_dev(bounds, "bounds");
+  check_long_dev(keys, "keys");
+  check_gpu(out, "out");
+  TORCH_CHECK(bounds.numel() == bases.numel() + 1, "bounds must have P+1 entries");
+  TORCH_CHECK(bases.numel() >= 1 && bases.numel() <= minips_k::kPsMaxWorld, "1..16 owners");
+  const int64_t n = keys.numel();
+  TORCH_CHECK(out.dim() == 2 && out.size(0) >= n && out.size(1) == W && out.is_contiguous(), "out must be [>= n, W]");
+  const bool bf = out.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || out.scalar_type() == at::kFloat, "out must be fp32 or bf16");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(keys.device());
+  minips_k::ps_gather_rows_bf16tab(ptr<int64_t>(bases), ptr<int64_t>(bounds), (int)bases.numel(), ptr<int64_t>(keys),
+                                   n, opt_count(n_dev), (int)W, out.data_ptr(), bf, stream_of(keys));
+}
+
+void ps_hash_gather(const at::Tensor& hkeys, const at::Tensor& hvals, const at::Tensor& bounds, int64_t cap,
+                    const at::Tensor& keys, const c10::optional<at::Tensor>& n_dev, int64_t W, at::Tensor& out) {
+  check_long_dev(hkeys, "hkeys");
+  check_long_dev(hvals, "hvals");
+  check_long_dev(bounds, "bounds");
+  check_long_dev(keys, "keys");
+  check_gpu(out, "out");
+  TORCH_CHECK(hkeys.numel() == hvals.numel() && bounds.numel() == hkeys.numel() + 1, "P owners, P+1 bounds");
+  const int64_t n = keys.numel();
+  TORCH_CHECK(out.dim() == 2 && out.size(0) >= n && out.size(1) == W && out.is_contiguous(), "out must be [>= n, W]");
+  const bool bf = out.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || out.scalar_type() == at::kFloat, "out must be fp32 or bf16");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(keys.device());
+  minips_k::ps_hash_gather(ptr<int64_t>(hkeys), ptr<int64_t>(hvals), ptr<int64_t>(bounds), (int)hkeys.numel(), cap,
+                           ptr<int64_t>(keys), n, opt_count(n_dev), (int)W, out.data_ptr(), bf, stream_of(keys));
+}
+
+// dst[o * shard_bytes, ...) = srcs[o][0, shard_bytes) for the listed owners (one kernel)
+void ps_pull(const at::Tensor& srcs, const std::vector<int64_t>& owners, int64_t shard_bytes, at::Tensor& dst) {
+  check_long_dev(srcs, "srcs");
+  check_gpu(dst, "dst");
+  TORCH_CHECK(owners.size() <= (size_t)minips_k::kPsMaxWorld, "<= 16 owners");
+  TORCH_CHECK(dst.is_contiguous() && dst.numel() * dst.element_size() >= srcs.numel() * shard_bytes, "dst too small");
+  uint64_t packed = 0;
+  for (size_t i = 0; i < owners.size(); ++i) {
+    TORCH_CHECK(owners[i] >= 0 && owners[i] < srcs.numel(), "owner out of range");
+    packed |= (uint64_t)owners[i] << (4 * i);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
+  minips_k::ps_pull(ptr<int64_t>(srcs), packed, (int)owners.size(), shard_bytes, dst.data_ptr(), stream_of(dst));
+}
+
+// Reader side of the per-owner locks: `locks` [P] int64 device addresses of the owners' lock words,
+// `held` / `err` raw device addresses (a slot of the reader's held ring, the rank's error word).
+void ps_read_lock(const at::Tensor& locks, int64_t held, int64_t err) {
+  check_long_dev(locks, "locks");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(locks.device());
+  minips_k::ps_read_lock(ptr<int64_t>(locks), (int)locks.numel(), reinterpret_cast<uint32_t*>(held),
+                         reinterpret_cast<uint32_t*>(err), stream_of(locks));
+}
+
+void ps_read_unlock(const at::Tensor& locks, int64_t held) {
+  check_long_dev(locks, "locks");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(locks.device());
+  minips_k::ps_read_unlock(ptr<int64_t>(locks), (int)locks.numel(), reinterpret_cast<uint32_t*>(held),
+                           stream_of(locks));
+}
+
+// A host-resident, device-mapped 32-bit word (hipHostMalloc, coherent): the rank's error word of the
+// one-sided protocol (a device spin that timed out sets a bit; the host reads it with no sync).
+class HostWord {
+ public:
+  HostWord() {
+    TORCH_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_), 64, hipHostMallocMapped | hipHostMallocCoherent) ==
+                    hipSuccess,
+                "HostWord: hipHostMalloc");
+    *h_ = 0;
+    TORCH_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_), h_, 0) == hipSuccess, "HostWord: device ptr");
+  }
+  ~HostWord() { (void)hipHostFree(h_); }
+  int64_t value() const { return (int64_t)__atomic_load_n(h_, __ATOMIC_ACQUIRE); }
+  void clear() { __atomic_store_n(h_, 0u, __ATOMIC_RELEASE); }
+  int64_t device_ptr() const { return reinterpret_cast<int64_t>(d_); }
+
+ private:
+  uint32_t* h_ = nullptr;
+  uint32_t* d_ = nullptr;
+};
+
 // pos[members[m]] = m: where the dgrad's permuted-rows epilogue puts each lookup's gradient row.
 at::Tensor emb_csr_positions(const at::Tensor& members) {
   check_gpu(members, "members");
@@ -1215,9 +1311,11 @@ class GpuAsyncServer {
     return queued_;
   }
 
+  void set_error_word(int64_t err) { applier_.SetErrorWord(reinterpret_cast<uint32_t*>(err)); }
+
   void add_sparse(int64_t t, int64_t opt, int64_t table, int64_t ld, int64_t W, int64_t state, int64_t state2,
                   int64_t D1, int64_t base, double lr, double eps, int64_t cap, int64_t inbox, int64_t slot_bytes,
-                  int64_t depth) {
+                  int64_t depth, int64_t bf16, int64_t seed, int64_t hash_cap, int64_t hkeys, int64_t lock) {
     TORCH_CHECK(cap % 2 == 0 && slot_bytes % 256 == 0 && depth >= 1, "sparse inbox layout");
     TORCH_CHECK(slot_bytes >= minips_k::kPsSlotHeader + cap * (8 + 4 * W), "sparse inbox slot too small");
     TORCH_CHECK(opt == minips_k::kPsAdd || opt == minips_k::kPsSgd || opt == minips_k::kPsRowwiseAdagrad,
@@ -1238,12 +1336,21 @@ class GpuAsyncServer {
     d.inbox = reinterpret_cast<char*>(inbox);
     d.slot_bytes = slot_bytes;
     d.depth = (int)depth;
+    d.bf16 = (int)bf16;
+    d.seed = (uint32_t)seed;
+    d.hash_cap = hash_cap;
+    d.hkeys = reinterpret_cast<unsigned long long*>(hkeys);
+    d.lock = reinterpret_cast<uint32_t*>(lock);
+    d.flush = lock ? reinterpret_cast<uint32_t*>(lock) + 1 : nullptr;
+    TORCH_CHECK(!bf16 || (W == 16 || W == 32 || W == 64), "bf16 rows hold 16, 32 or 64 values");
+    TORCH_CHECK(hash_cap == 0 || ((hash_cap & (hash_cap - 1)) == 0 && hkeys), "hash capacity: a power of two");
     applier_.SetSparse((int)t, d);
     server_.Enable((int)t);
   }
 
   void add_dense(int64_t t, int64_t opt, int64_t w, int64_t m, int64_t v, int64_t wb, int64_t n, double lr, double b1,
-                 double b2, double eps, double wd, int64_t step, int64_t inbox, int64_t slot_bytes, int64_t depth) {
+                 double b2, double eps, double wd, int64_t step, int64_t inbox, int64_t slot_bytes, int64_t depth,
+                 int64_t lock) {
     TORCH_CHECK(slot_bytes % 256 == 0 && depth >= 1 && n % 4 == 0, "dense inbox layout");
     TORCH_CHECK(slot_bytes >= minips_k::kPsSlotHeader + 4 * n, "dense inbox slot too small");
     TORCH_CHECK(opt != minips_k::kPsRowwiseAdagrad, "dense optimizer ", opt);
@@ -1264,6 +1371,8 @@ class GpuAsyncServer {
     d.inbox = reinterpret_cast<char*>(inbox);
     d.slot_bytes = slot_bytes;
     d.depth = (int)depth;
+    d.lock = reinterpret_cast<uint32_t*>(lock);
+    d.flush = lock ? reinterpret_cast<uint32_t*>(lock) + 1 : nullptr;
     applier_.SetDense((int)t, d);
     server_.Enable((int)t);
   }
@@ -1375,6 +1484,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("EPI_BIAS_GELU_BF16") = (int)minips_k::kEpiBiasGeluBf16;
   m.attr("EPI_BIAS_GELU_AUX_BF16") = (int)minips_k::kEpiBiasGeluAuxBf16;
   m.attr("EPI_GELU_GRAD_BF16") = (int)minips_k::kEpiGeluGradBf16;
+  m.def("gemm_set_v4_mode", [](int64_t m) { minips_k::gemm_set_v4_mode((int)m); });
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("a_km"), py::arg("b_kn"), py::arg("epi"), py::arg("bias"), py::arg("mask"), py::arg("colsum"),
         py::arg("alpha") = 1.0, py::arg("split_k") = 1, py::arg("batch") = 1, py::arg("inner") = 1,
@@ -1444,13 +1554,28 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("bitmap_plan", &bitmap_plan, py::arg("keys"), py::arg("bounds"), py::arg("num_rows"), py::arg("route_mult"),
         py::arg("route_n"), py::arg("oor") = py::none());
   m.def("uniform_synth", &uniform_synth);
-  m.def("ipc_alloc", &ipc_alloc);
+  m.def("ipc_alloc", &ipc_alloc, py::arg("nbytes"), py::arg("device"), py::arg("kind") = 0);
   m.def("kmeans_assign_csr", &kmeans_assign_csr);
   m.def("kmeans_csr_accum", &kmeans_csr_accum);
   m.def("ipc_open", &ipc_open);
   m.def("ps_push_rows", &ps_push_rows, py::arg("uniq"), py::arg("counts"), py::arg("U_dev"), py::arg("n"),
         py::arg("g"), py::arg("inbox"), py::arg("slot_off"), py::arg("cap"));
   m.def("ps_set_headers", &ps_set_headers);
+  m.def("ps_gather_rows_bf16tab", &ps_gather_rows_bf16tab, py::arg("bases"), py::arg("bounds"), py::arg("keys"),
+        py::arg("n_dev"), py::arg("W"), py::arg("out"));
+  m.def("ps_hash_gather", &ps_hash_gather, py::arg("hkeys"), py::arg("hvals"), py::arg("bounds"), py::arg("cap"),
+        py::arg("keys"), py::arg("n_dev"), py::arg("W"), py::arg("out"));
+  m.def("ps_pull", &ps_pull);
+  m.def("ps_read_lock", &ps_read_lock);
+  m.def("ps_read_unlock", &ps_read_unlock);
+  m.attr("PS_CTRL_BYTES") = minips_k::kPsCtrlBytes;
+  m.attr("PS_CTRL_LINE") = minips_k::kPsCtrlLine;
+  m.attr("PS_HELD_SLOTS") = minips_k::kPsHeldSlots;
+  py::class_<HostWord>(m, "HostWord")
+      .def(py::init<>())
+      .def_property_readonly("value", &HostWord::value)
+      .def("clear", &HostWord::clear)
+      .def_property_readonly("device_ptr", &HostWord::device_ptr);
   m.def("emb_csr_positions", &emb_csr_positions);
   m.def("sparse_apply_bf16", &sparse_apply_bf16);
   m.attr("EPI_PERM_ROWS_BF16") = (int)minips_k::kEpiPermRowsBf16;
@@ -1465,6 +1590,7 @@ PYBIND11_MODULE(_kernels, m) {
       .def(py::init<const std::string&, int64_t, int64_t, int64_t, int64_t>(), py::arg("board"), py::arg("world"),
            py::arg("rank"), py::arg("tables"), py::arg("device"))
       .def("add_sparse", &GpuAsyncServer::add_sparse)
+      .def("set_error_word", &GpuAsyncServer::set_error_word)
       .def("publish_after", &GpuAsyncServer::publish_after)
       .def_property_readonly("published", &GpuAsyncServer::published)
       .def_property_readonly("queued", &GpuAsyncServer::queued)

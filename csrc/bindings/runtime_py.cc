@@ -121,6 +121,14 @@ class PyApplier : public Applier {
     }
   }
   void Flush() override {}
+  // the owner's write lock of the table on the board (the CPU twin of the GPU lock words)
+  void BeginTable(int t) override {
+    if (board_ && !board_->WriteLock(t, 30.0)) throw std::runtime_error("async server: write lock timed out");
+  }
+  void EndTable(int t) override {
+    if (board_) board_->WriteUnlock(t);
+  }
+  PSBoard* board_ = nullptr;
 
  private:
   py::function fn_;
@@ -129,7 +137,9 @@ class PyApplier : public Applier {
 class CpuAsyncServer {
  public:
   CpuAsyncServer(const std::string& board, int world, int rank, int tables, py::function apply)
-      : applier_(std::move(apply)), server_(board, world, rank, tables, &applier_) {}
+      : applier_(std::move(apply)), server_(board, world, rank, tables, &applier_) {
+    applier_.board_ = &server_.board();
+  }
   ~CpuAsyncServer() {
     py::gil_scoped_release rel;
     server_.Stop();
@@ -458,6 +468,14 @@ PYBIND11_MODULE(_runtime, m) {
       .def("snapshot_sent", &PSBoard::SnapshotSent)
       .def("snapshot_applied", &PSBoard::SnapshotApplied)
       .def("wake", &PSBoard::Wake)
+      .def("read_lock", &PSBoard::ReadLock, py::arg("table"), py::arg("timeout_s"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("read_unlock", &PSBoard::ReadUnlock)
+      .def("write_lock", &PSBoard::WriteLock, py::arg("table"), py::arg("timeout_s"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("write_unlock", &PSBoard::WriteUnlock)
+      .def("set_abort", &PSBoard::SetAbort)
+      .def_property_readonly("aborted", &PSBoard::Aborted)
       .def_property_readonly("wakeups", &PSBoard::Wakeups)
       .def_property_readonly("epoch", &PSBoard::Epoch)
       .def("unlink", &PSBoard::Unlink);

@@ -926,6 +926,224 @@ __global__ __launch_bounds__(512) void gemm_v3_kernel(const bf16_t* __restrict__
     epilogue_at<EPI, 8>(acc, ep, M, N, m0 + wr * 128, n0 + wc * 64, lane);
 }
 
+// ================================================================ v4: 256x256, 8 waves, quarter-staged A
+// The v3 tile with a staging schedule that keeps every DMA 4-7 phases ahead of its first read
+// (v2 / v3 leave one K-step, ~1 us, to cover an HBM miss):
+//   * 8 waves as 2 (M) x 4 (N), each wave 128 x 64 = 8 x 4 MFMA 16x16x32 tiles (128 acc VGPRs);
+//     a K-step (BK = 64) runs as 4 PHASES, phase q = the wave's rows [32q, 32q + 32) of its A half
+//     against all 4 of its B n-tiles (2 k sub-steps): 16 MFMAs per wave per phase;
+//   * the wave's B fragments of the K-step (4 n-tiles x 2 k) are read ONCE, in phase 0, and stay
+//     in registers -- so the whole B tile of the buffer is free after phase 0;
+//   * A lives in LDS as 8 quarter images (half h, quarter q: 32 rows x 64 k, 4 KiB each), and
+//     quarter q of a buffer is free after phase q;
+//   * so K-step t + 2 (same buffer as t) streams in WHILE t computes: A quarter q at phase q + 1,
+//     the B halves at phases 1 / 2, and A quarter 3 at phase 0 of t + 1; one counted
+//     vmcnt (7 = the DMAs of K-step t + 2 this wave issued during t) + one barrier per K-step
+//     retire K-step t + 1, and one barrier per phase orders the quarter reuse (WAR);
+//   * the next quarter's A fragments are read during the current phase's MFMAs (two register sets).
+// Images: MK quarter [32][64] with the v2 swizzle; KM quarter [64 k][32 rows] (64-byte rows) with
+// chunk' = chunk ^ swz_q(k), which keeps the 32-lane halves of the transposing reads on disjoint
+// bank groups for the plain and the permuted (wgrad) k order. B: the v2 128-row half images.
+// Tile order: grouped (4 row tiles x tiles_n) inside each XCD's contiguous run of tiles, so the
+// 32 workgroups one XCD runs at a time share 4 A panels and 8 B panels through its L2.
+constexpr int kQuarter = 32 * BK2;  // bf16 elements of one A quarter image
+
+__device__ __forceinline__ int swz_q(int k) { return 2 * (((k >> 2) ^ (k >> 3)) & 1); }
+
+// Piece p (0..3, 1 KiB) of the A quarter image at S holding rows [row0, row0 + 32) x k [k0, k0 + 64).
+template <bool KMAJOR>
+__device__ __forceinline__ void dma_quarter(__amdgpu_buffer_rsrc_t rsrc, int ld, int row0, int k0, int rows, int kend,
+                                            bf16_t* S, int p, int lane) {
+  uint32_t voff;
+  if (!KMAJOR) {
+    const int R = 8 * p + (lane >> 3);
+    const int c = (lane & 7) ^ ((R >> 1) & 7);
+    const int gr = row0 + R, gk = k0 + 8 * c;
+    voff = (gr < rows && gk < kend) ? (uint32_t)(((int64_t)gr * ld + gk) * 2) : kOobOffset;
+  } else {
+    const int kr = 16 * p + (lane >> 2);
+    const int c = (lane & 3) ^ swz_q(kr);
+    const int gk = k0 + kr, gm = row0 + 8 * c;
+    voff = (gk < kend && gm < rows) ? (uint32_t)(((int64_t)gk * ld + gm) * 2) : kOobOffset;
+  }
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(S + p * 512), 16, voff, 0,
+                                           0, 0);
+}
+
+// 16x16x32 A fragment of rows [16 i, 16 i + 16) of a quarter image, k sub-step ks.
+template <bool KMAJOR, bool PERM>
+__device__ __forceinline__ v8s frag_quarter(const bf16_t* S, int i, int ks, int lane) {
+  if (!KMAJOR) return frag2<false, PERM, 32>(S, 16 * i, ks, lane);
+  const int g = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+  const int r0 = 32 * ks + (PERM ? 4 * g : 8 * g) + q;
+  const int r1 = 32 * ks + (PERM ? 16 + 4 * g : 8 * g + 4) + q;
+  const int ch = 2 * i + (p >> 1), sub = 4 * (p & 1);
+  const v4s lo = ds_read_tr16(S + r0 * 32 + 8 * (ch ^ swz_q(r0)) + sub);
+  const v4s hi = ds_read_tr16(S + r1 * 32 + 8 * (ch ^ swz_q(r1)) + sub);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+#ifndef MINIPS_GEMM_V4_PRIO
+#define MINIPS_GEMM_V4_PRIO 1
+#endif
+#ifndef MINIPS_GEMM_V4_GROUP
+#define MINIPS_GEMM_V4_GROUP 4
+#endif
+
+// Tile (tm, tn) of block `bid`: XCD-contiguous runs (T1, bijective), row-grouped inside a run.
+__device__ __forceinline__ void v4_tile(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int nwg = tiles_m * tiles_n;
+  if (nwg >= 16) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    bid = base + (bid >> 3);
+  }
+  constexpr int G = MINIPS_GEMM_V4_GROUP;
+  const int per_group = G * tiles_n, group = bid / per_group;
+  const int first = group * G, gsz = min(tiles_m - first, G), in = bid - group * per_group;
+  tm = first + in % gsz;
+  tn = in / gsz;
+}
+
+template <bool A_KM, bool B_KN, int EPI>
+__global__ __launch_bounds__(512) void gemm_v4_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                      int M, int N, int K, int lda, int ldb, int k_chunk, EpiArgs ep) {
+  constexpr bool PERM = A_KM && B_KN;
+  constexpr int kA = 256 * BK2;  // A region of a buffer (8 quarters); B follows
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2][2 * 256 * BK2];
+  static_assert(sizeof(smem) >= sizeof(float) * 8 * kScrFloats, "epilogue scratch must fit the staging LDS");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = (N + 255) / 256, tiles_m = (M + 255) / 256;
+  int tm, tn;
+  v4_tile(blockIdx.x, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  {
+    const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
+    A += zo * ep.sa_o + zi * ep.sa_i;
+    B += zo * ep.sb_o + zi * ep.sb_i;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
+    ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
+  }
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7ffffff0, 0x00020000);
+  const int kb = blockIdx.z * k_chunk;
+  const int ke = min(K, kb + k_chunk);
+  const int nt = ke > kb ? (ke - kb + BK2 - 1) / BK2 : 0;
+
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // this wave's piece of A quarter q (both 128-row halves: waves 0-3 -> half 0, 4-7 -> half 1)
+  auto a_quarter = [&](int t, int q, int buf) {
+    const int h = wave >> 2;
+    dma_quarter<A_KM>(ra, lda, m0 + h * 128 + q * 32, kb + t * BK2, M, ke, smem[buf] + (h * 4 + q) * kQuarter,
+                      wave & 3, lane);
+  };
+  auto b_half = [&](int t, int hh, int buf) {
+    dma_tile<B_KN, 128, 8>(rb, ldb, n0 + hh * 128, kb + t * BK2, N, ke, smem[buf] + kA + hh * 128 * BK2, wave, lane);
+  };
+
+  if (nt > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a_quarter(0, q, 0);
+    b_half(0, 0, 0);
+    b_half(0, 1, 0);
+  }
+  if (nt > 1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a_quarter(1, q, 1);
+    b_half(1, 0, 1);
+    b_half(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-step 0 landed, K-step 1 in flight
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    const bf16_t* SA = smem[buf] + wr * 4 * kQuarter;
+    const bf16_t* SB = smem[buf] + kA + (wc >> 1) * 128 * BK2;
+    const int bcol = (wc & 1) * 64;
+    const bool more2 = t + 2 < nt;
+    v8s bfr[4][2], af[2][2][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // ---- DMA of this phase (into regions every wave finished reading before the last barrier)
+      if (q == 0) {
+        if (t >= 1 && t + 1 < nt) a_quarter(t + 1, 3, buf ^ 1);
+      } else if (more2) {
+        a_quarter(t + 2, q - 1, buf);
+        if (q < 3) b_half(t + 2, q - 1, buf);
+      }
+      // ---- fragments: all B + A quarter 0 at phase 0, then A quarter q + 1 ahead of its phase
+      if (q == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag2<B_KN, PERM, 128>(SB, bcol + 16 * j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) af[0][i][ks] = frag_quarter<A_KM, PERM>(SA, i, ks, lane);
+      }
+      if (q < 3) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            af[(q + 1) & 1][i][ks] = frag_quarter<A_KM, PERM>(SA + (q + 1) * kQuarter, i, ks, lane);
+      }
+      if (MINIPS_GEMM_V4_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[2 * q + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(v8bf, af[q & 1][i][ks]), __builtin_bit_cast(v8bf, bfr[j][ks]), acc[2 * q + i][j], 0,
+                0, 0);
+      if (MINIPS_GEMM_V4_PRIO) __builtin_amdgcn_s_setprio(0);
+      if (q < 3) {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's reads of quarter q (and of B at q = 0) retired
+        asm volatile("" ::: "memory");
+      }
+    }
+    // ---- end of the K-step: K-step t + 1 landed (K-step t + 2's 7 DMAs may stay in flight)
+    if (t + 1 < nt) {
+      if (more2) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the staging LDS becomes the epilogue scratch
+  asm volatile("" ::: "memory");
+  epilogue_lds<EPI, 8>(acc, ep, M, N, m0 + wr * 128, n0 + wc * 64, lane,
+                       reinterpret_cast<float*>(&smem[0][0]) + wave * kScrFloats);
+}
+
+// v4 selection (MINIPS_GEMM_V4 at start-up, gemm_set_v4_mode() at run time for in-process A/B):
+// 0 off, 1 where the 256x256 tile is picked, 2 every shape
+static int g_v4_mode = -1;
+static int gemm_v4_mode() {
+  if (g_v4_mode < 0) {
+    const char* e = std::getenv("MINIPS_GEMM_V4");
+    g_v4_mode = e ? std::atoi(e) : 0;
+  }
+  return g_v4_mode;
+}
+void gemm_set_v4_mode(int mode) { g_v4_mode = mode; }
+
 static int gemm_impl() {
   static const int v = [] {
     const char* e = std::getenv("MINIPS_GEMM_IMPL");
@@ -981,7 +1199,11 @@ static int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
       return !e || std::atoi(e) != 0;
     }();
     const bool use_v3 = v3 || (wgrad && wgrad_mode == 3);
-    if (pick == 256 && use_v3) {
+    const int v4 = gemm_v4_mode();
+    if (v4 == 2 || (v4 == 1 && pick == 256)) {  // 2: v4 for every shape
+      dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
+      hipLaunchKernelGGL((gemm_v4_kernel<A_KM, B_KN, EPI>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
+    } else if (pick == 256 && use_v3) {
       dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
       if (v3_early)
         hipLaunchKernelGGL((gemm_v3_kernel<A_KM, B_KN, EPI, true>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb, kc,

@@ -40,6 +40,8 @@ enum GemmEpilogue {
   kEpiBiasGeluDAuxBf16 = 13,
   kEpiMulAuxBf16 = 14,  // C bf16 = acc * mask(aux)
 };
+// v4 GEMM selection at run time (in-process A/B): 0 off, 1 where 256x256 tiles are picked, 2 always
+void gemm_set_v4_mode(int mode);
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
                float alpha, int split_k, hipStream_t s);

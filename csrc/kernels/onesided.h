@@ -30,6 +30,32 @@ void ps_set_headers(const int64_t* inbox, int P, int64_t slot_off, int64_t value
 void ps_gather_rows(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,
                     const int64_t* n_dev, int W, void* out, bool out_bf16, hipStream_t s);
 
+// out[i] = row of keys[i] from a bf16 shard (rows of W bf16, W in {16, 32, 64}).
+void ps_gather_rows_bf16tab(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,
+                            const int64_t* n_dev, int W, void* out, bool out_bf16, hipStream_t s);
+// Map storage: out[i] = the row of keys[i] in its owner's open-addressing table (hkeys[o], hvals[o]:
+// device addresses of owner o's key array [cap] and rows [cap, W] fp32), zeros when absent (the
+// reference's default-insert 0, server/map_storage.hpp:21-26).
+void ps_hash_gather(const int64_t* hkeys, const int64_t* hvals, const int64_t* bounds, int P, int64_t cap,
+                    const int64_t* keys, int64_t n, const int64_t* n_dev, int W, void* out, bool out_bf16,
+                    hipStream_t s);
+// Pull copies of a dense table: for every owner o in `owners` (a list of `count` 4-bit owner ids),
+// dst[o * shard_bytes ...] = srcs[o][0, shard_bytes) (srcs: device table of P addresses).
+void ps_pull(const int64_t* srcs, uint64_t owners, int count, int64_t shard_bytes, void* dst, hipStream_t s);
+
+// ---- per-owner reader / writer lock (the consistency of one-sided reads, see onesided.hip) ----
+constexpr uint32_t kPsWriter = 0x80000000u;  // lock word: bit 31 the owner's writer, bits 0..30 readers
+constexpr int kPsCtrlLine = 64;              // control buffer: one 64-byte line per table
+constexpr int kPsCtrlBytes = 64 * 64;        // 16 table lines + the flush counters
+constexpr int kPsHeldSlots = 256;            // reader-side ring of "locks held" masks
+enum PsLockError : uint32_t { kPsErrReadLock = 1, kPsErrWriteLock = 2, kPsErrHashFull = 4 };
+// Reader: take the read lock of every owner (ascending order), record the ones taken in *held.
+void ps_read_lock(const int64_t* locks, int P, uint32_t* held, uint32_t* err, hipStream_t s);
+void ps_read_unlock(const int64_t* locks, int P, uint32_t* held, hipStream_t s);
+// Owner: announce the writer, wait for the readers to drain / flush every XCD's L2, then release.
+void ps_write_lock(uint32_t* lock, uint32_t* err, hipStream_t s);
+void ps_write_unlock(uint32_t* lock, uint32_t* flush_count, hipStream_t s);
+
 // Owner-side descriptors. `inbox` is this owner's inbox buffer: requester r's slot k at
 // inbox + (r * depth + k) * slot_bytes.
 struct PsSparseDesc {
@@ -46,6 +72,12 @@ struct PsSparseDesc {
   char* inbox = nullptr;
   int64_t slot_bytes = 0;
   int depth = 1;
+  int bf16 = 0;                 // rows stored in bf16 (stochastic rounding; fp32 pushes and state)
+  uint32_t seed = 0;            //   ... the rounding stream's seed
+  int64_t hash_cap = 0;         // > 0: Map storage -- open addressing over hkeys[hash_cap], rows in table
+  unsigned long long* hkeys = nullptr;
+  uint32_t* lock = nullptr;     // this owner's lock word of the table (+ its flush counter)
+  uint32_t* flush = nullptr;
 };
 
 struct PsDenseDesc {
@@ -60,6 +92,8 @@ struct PsDenseDesc {
   char* inbox = nullptr;
   int64_t slot_bytes = 0;
   int depth = 1;
+  uint32_t* lock = nullptr;
+  uint32_t* flush = nullptr;
 };
 
 class HipApplier : public minips::Applier {
@@ -70,8 +104,13 @@ class HipApplier : public minips::Applier {
   void SetDense(int t, const PsDenseDesc& d);
   int64_t Step(int t) const { return descs_.at(t).step.load(); }
   void SetStep(int t, int64_t s) { descs_.at(t).step.store(s); }
+  void SetErrorWord(uint32_t* err) { err_ = err; }
   void ThreadInit() override;
+  void BeginTable(int t) override;
   void Apply(int t, int r, int64_t c) override;
+  void EndTable(int t) override;
+  uint64_t Submit() override;
+  void Wait(uint64_t ticket) override;
   void Flush() override;
 
  private:
@@ -79,11 +118,15 @@ class HipApplier : public minips::Applier {
     int kind = -1;  // 0 sparse, 1 dense
     PsSparseDesc sp;
     PsDenseDesc dn;
-    std::atomic<int64_t> step{0};
+    std::atomic<int64_t> step{0};  // Adam steps (dense) / applies (bf16 rows: the rounding stream)
   };
   int dev_;
   hipStream_t stream_ = nullptr;
   std::vector<Desc> descs_;
+  uint32_t* err_ = nullptr;
+  static constexpr int kEvents = 8;  // batches in flight at most (the server keeps <= 2)
+  hipEvent_t events_[kEvents] = {};
+  uint64_t submitted_ = 0;
 };
 
 }  // namespace minips_k

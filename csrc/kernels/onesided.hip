@@ -20,7 +20,33 @@
 //           owner's shard [n]
 //
 //   owner of key k   o = upper_bound(bounds, k) - 1   (bounds [P+1], equal key ranges)
-//   row              k - bounds[o]  in the shard at bases[o]  ([rows_o, W] fp32, row-major)
+//   row              k - bounds[o]  in the shard at bases[o]  ([rows_o, W] fp32 / bf16, row-major)
+//
+// Memory model (why a reader never sees a stale or a half-applied row):
+//   * allocation (ipc_alloc, csrc/bindings/ops_py.cpp): inboxes are UNCACHED device memory
+//     (hipDeviceMallocUncached: the owner's apply reads what the requester's xGMI writes put in
+//     HBM, never an L2 copy of the slot from `depth` clocks ago); shards, pull copies and the
+//     control lines are FINE-GRAINED (hipDeviceMallocFinegrained: coherent for peer access and
+//     system-scope atomics);
+//   * push: every block of ps_push_rows drains its stores (vmcnt(0)), meets at a barrier and
+//     issues a system-scope release (__threadfence_system) before it exits; the requester's
+//     publisher thread bumps `sent` only after the push kernels completed (an event);
+//   * apply: the owner's server thread brackets each table's applies of a batch with
+//     ps_write_lock / ps_write_unlock on its apply stream. The lock word (one per table, in the
+//     owner's fine-grained control line) has the writer bit 31 and a reader count. The writer
+//     sets the bit (new readers wait), waits for the readers inside to leave, then the applies run;
+//     ps_write_unlock runs 64 workgroups (every XCD) that each write back their XCD's L2 with a
+//     system-scope release, and the last one to arrive clears the writer bit. `applied` is
+//     published after that (an event again);
+//   * read: ps_read_lock takes the read lock of every owner of the table (ascending owner order,
+//     so readers and single-lock writers cannot deadlock), the gather / pull kernel starts each
+//     workgroup with a system-scope acquire (its CU / XCD caches drop stale lines), and
+//     ps_read_unlock leaves. A read therefore sees every owner's shard between two batches --
+//     never half of one -- which is what the reference's single server thread guarantees
+//     (server/server_thread.cpp:23-61: one Add or Get at a time per model);
+//   * every spin is bounded (kSpinLimit of the 100 MHz real-time counter, ~2 s); a timeout sets a
+//     bit of the rank's error word (host-mapped) and proceeds, and the host raises on it.
+#include <algorithm>
 #include <atomic>
 #include <stdexcept>
 #include <string>
@@ -33,6 +59,92 @@
 namespace minips_k {
 
 namespace {
+
+// every storing wave drains, the block meets, one lane publishes at system scope
+__device__ __forceinline__ void release_block() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// drop this CU's / XCD's cached copies of peer-written lines before reading them
+__device__ __forceinline__ void acquire_block() {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+constexpr uint64_t kSpinLimit = 200000000ull;  // ticks of the 100 MHz real-time counter: ~2 s
+
+__device__ __forceinline__ uint32_t ld_sys(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void flag_error(uint32_t* err, uint32_t bit) {
+  if (err) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void ps_read_lock_kernel(const int64_t* __restrict__ locks, int P, uint32_t* held, uint32_t* err) {
+  if (threadIdx.x != 0) return;
+  uint32_t mask = 0;
+  for (int o = 0; o < P; ++o) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(locks[o]);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      uint32_t v = ld_sys(w);
+      if (!(v & kPsWriter) && __hip_atomic_compare_exchange_strong(w, &v, v + 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_SYSTEM)) {
+        mask |= 1u << o;
+        break;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit) {
+        flag_error(err, kPsErrReadLock);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  __hip_atomic_store(held, mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void ps_read_unlock_kernel(const int64_t* __restrict__ locks, int P, uint32_t* held) {
+  if (threadIdx.x != 0) return;
+  const uint32_t mask = __hip_atomic_load(held, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int o = 0; o < P; ++o)
+    if (mask & (1u << o))
+      __hip_atomic_fetch_sub(reinterpret_cast<uint32_t*>(locks[o]), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void ps_write_lock_kernel(uint32_t* lock, uint32_t* err) {
+  if (threadIdx.x != 0) return;
+  __hip_atomic_fetch_or(lock, kPsWriter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (ld_sys(lock) & ~kPsWriter) {  // readers inside
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit) {
+      flag_error(err, kPsErrWriteLock);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+constexpr int kFlushBlocks = 64;  // dealt round-robin over the 8 XCDs: every XCD's L2 is written back
+
+__global__ void ps_write_unlock_kernel(uint32_t* lock, uint32_t* count) {
+  if (threadIdx.x != 0) return;
+  __threadfence_system();  // this XCD's dirty lines (the applies of the batch) reach memory
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (__hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == kFlushBlocks - 1) {
+    __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_and(lock, ~kPsWriter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 __device__ __forceinline__ int upper_owner(const int64_t* __restrict__ b, int P, int64_t k) {
   int lo = 0, hi = P;  // b[lo] <= k < b[hi]
@@ -83,11 +195,13 @@ __global__ __launch_bounds__(256) void ps_push_rows_kernel(const int64_t* __rest
       dst[j] = g[i * W + j];
     }
   }
+  release_block();
 }
 
 __global__ void ps_set_headers_kernel(const int64_t* __restrict__ inbox, int P, int64_t slot_off, int64_t value) {
   if (threadIdx.x < (unsigned)P)
     *reinterpret_cast<int64_t*>(reinterpret_cast<char*>(inbox[threadIdx.x]) + slot_off) = value;
+  release_block();
 }
 
 template <bool VEC, typename TO>
@@ -100,7 +214,7 @@ __global__ __launch_bounds__(256) void ps_gather_rows_kernel(const int64_t* __re
   __shared__ int64_t base_ptr[kPsMaxWorld];
   if (threadIdx.x <= (unsigned)P) b[threadIdx.x] = bounds[threadIdx.x];
   if (threadIdx.x < (unsigned)P) base_ptr[threadIdx.x] = bases[threadIdx.x];
-  __syncthreads();
+  acquire_block();
   const int64_t nn = n_dev ? min(n, *n_dev) : n;
   const int nv = VEC ? W / 4 : W;
   const int64_t total = nn * nv;
@@ -137,7 +251,219 @@ __global__ __launch_bounds__(256) void ps_gather_rows_kernel(const int64_t* __re
   }
 }
 
+// bf16 shards: 8 values per 16-byte load, W / 8 lanes per row
+template <typename TO>
+__global__ __launch_bounds__(256) void ps_gather_bf16_kernel(const int64_t* __restrict__ bases,
+                                                             const int64_t* __restrict__ bounds, int P,
+                                                             const int64_t* __restrict__ keys, int64_t n,
+                                                             const int64_t* __restrict__ n_dev, int W,
+                                                             TO* __restrict__ out) {
+  __shared__ int64_t b[kPsMaxWorld + 1];
+  __shared__ int64_t base_ptr[kPsMaxWorld];
+  if (threadIdx.x <= (unsigned)P) b[threadIdx.x] = bounds[threadIdx.x];
+  if (threadIdx.x < (unsigned)P) base_ptr[threadIdx.x] = bases[threadIdx.x];
+  acquire_block();
+  const int64_t nn = n_dev ? min(n, *n_dev) : n;
+  const int nv = W / 8;
+  const int64_t total = nn * nv;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = c / nv;
+    const int j = (int)(c - i * nv);
+    const int64_t k = keys[i];
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (k >= b[0] && k < b[P]) {
+      const int o = upper_owner(b, P, k);
+      v = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(base_ptr[o]) + (k - b[o]) * (int64_t)W)[j];
+    }
+    if constexpr (sizeof(TO) == 2) {
+      reinterpret_cast<uint4*>(out + i * W)[j] = v;
+    } else {
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      float4* d = reinterpret_cast<float4*>(out + i * W) + 2 * j;
+      d[0] = make_float4(__uint_as_float(w[0] << 16), __uint_as_float(w[0] & 0xffff0000u), __uint_as_float(w[1] << 16),
+                         __uint_as_float(w[1] & 0xffff0000u));
+      d[1] = make_float4(__uint_as_float(w[2] << 16), __uint_as_float(w[2] & 0xffff0000u), __uint_as_float(w[3] << 16),
+                         __uint_as_float(w[3] & 0xffff0000u));
+    }
+  }
+}
+
+// ---- Map storage (open addressing, linear probing; keys are the mixed 63-bit keys, ~0 = empty)
+constexpr unsigned long long kPsEmpty = ~0ull;
+
+__device__ __forceinline__ uint64_t ps_mix(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+// slot of key k in (hk, cap), -1 if absent (a reader: never inserts)
+__device__ __forceinline__ int64_t ps_hash_find(const unsigned long long* hk, int64_t cap, unsigned long long k) {
+  int64_t s = (int64_t)(ps_mix(k) & (uint64_t)(cap - 1));
+  for (int64_t probe = 0; probe < cap; ++probe) {
+    const unsigned long long cur = hk[s];
+    if (cur == k) return s;
+    if (cur == kPsEmpty) return -1;
+    s = (s + 1) & (cap - 1);
+  }
+  return -1;
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void ps_hash_gather_kernel(const int64_t* __restrict__ hkeys,
+                                                             const int64_t* __restrict__ hvals,
+                                                             const int64_t* __restrict__ bounds, int P, int64_t cap,
+                                                             const int64_t* __restrict__ keys, int64_t n,
+                                                             const int64_t* __restrict__ n_dev, int W,
+                                                             TO* __restrict__ out) {
+  __shared__ int64_t b[kPsMaxWorld + 1];
+  if (threadIdx.x <= (unsigned)P) b[threadIdx.x] = bounds[threadIdx.x];
+  acquire_block();
+  const int64_t nn = n_dev ? min(n, *n_dev) : n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nn; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = keys[i];
+    int64_t s = -1;
+    int o = 0;
+    if (k >= b[0] && k < b[P]) {
+      o = upper_owner(b, P, k);
+      s = ps_hash_find(reinterpret_cast<const unsigned long long*>(hkeys[o]), cap, (unsigned long long)k);
+    }
+    const float* row = s >= 0 ? reinterpret_cast<const float*>(hvals[o]) + s * (int64_t)W : nullptr;
+    for (int c = 0; c < W; ++c) {
+      const float v = row ? row[c] : 0.f;
+      if constexpr (sizeof(TO) == 2) out[i * W + c] = f2bf(v);
+      else out[i * W + c] = v;
+    }
+  }
+}
+
+// Owner-side apply of one inbox slot into the Map storage: one wave per row; lane 0 finds or
+// inserts the key (the owner is the only inserter; distinct keys race only on empty slots: CAS),
+// then the row is updated (OPT 0: w += scale g; 2: row-wise Adagrad with per-slot state).
+template <int OPT>
+__global__ __launch_bounds__(256) void ps_hash_apply_kernel(unsigned long long* __restrict__ hk, int64_t cap,
+                                                            float* __restrict__ vals, float* __restrict__ state,
+                                                            int W, const int64_t* __restrict__ keys,
+                                                            const float* __restrict__ g, const int64_t* __restrict__ cnt,
+                                                            int64_t n_max, float lr, float eps, float scale,
+                                                            uint32_t* err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t n = min(n_max, *cnt);
+  for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; i < n; i += nw) {
+    int64_t slot = -1;
+    if (lane == 0) {
+      const unsigned long long k = (unsigned long long)keys[i];
+      int64_t s = (int64_t)(ps_mix(k) & (uint64_t)(cap - 1));
+      for (int64_t probe = 0; probe < cap; ++probe) {
+        unsigned long long cur = hk[s];
+        if (cur == kPsEmpty) cur = atomicCAS(hk + s, kPsEmpty, k);
+        if (cur == kPsEmpty || cur == k) {  // claimed (the row is zero: MapStorage's default-insert) or found
+          slot = s;
+          break;
+        }
+        s = (s + 1) & (cap - 1);
+      }
+      if (slot < 0) flag_error(err, kPsErrHashFull);
+    }
+    slot = __shfl(slot, 0, 64);
+    if (slot < 0) continue;
+    float* row = vals + slot * (int64_t)W;
+    const float* gr = g + i * (int64_t)W;
+    float step = scale;
+    if (OPT == 2) {
+      float sq = 0.f;
+      for (int c = lane; c < W; c += 64) sq += gr[c] * gr[c];
+      sq = warp_sum(sq);
+      const float st = state[slot] + sq / (float)W;
+      if (lane == 0) state[slot] = st;
+      step = -lr / (sqrtf(st) + eps);
+    }
+    for (int c = lane; c < W; c += 64) row[c] += step * gr[c];
+  }
+}
+
+// Pull copies: 16-byte chunks of the selected owners' buffers (owner ids packed 4 bits each)
+__global__ __launch_bounds__(256) void ps_pull_kernel(const int64_t* __restrict__ srcs, uint64_t owners,
+                                                      int64_t chunks, char* __restrict__ dst, int64_t shard_bytes,
+                                                      int count) {
+  acquire_block();
+  const int64_t total = chunks * count;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+    const int sel = (int)(c / chunks);
+    const int64_t j = c - (int64_t)sel * chunks;
+    const int o = (int)((owners >> (4 * sel)) & 15);
+    const uint4 v = reinterpret_cast<const uint4*>(srcs[o])[j];
+    reinterpret_cast<uint4*>(dst + o * shard_bytes)[j] = v;
+  }
+}
+
 }  // namespace
+
+void ps_read_lock(const int64_t* locks, int P, uint32_t* held, uint32_t* err, hipStream_t s) {
+  if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_read_lock: P out of range");
+  hipLaunchKernelGGL(ps_read_lock_kernel, 1, 64, 0, s, locks, P, held, err);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void ps_read_unlock(const int64_t* locks, int P, uint32_t* held, hipStream_t s) {
+  hipLaunchKernelGGL(ps_read_unlock_kernel, 1, 64, 0, s, locks, P, held);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void ps_write_lock(uint32_t* lock, uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(ps_write_lock_kernel, 1, 64, 0, s, lock, err);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void ps_write_unlock(uint32_t* lock, uint32_t* flush_count, hipStream_t s) {
+  hipLaunchKernelGGL(ps_write_unlock_kernel, kFlushBlocks, 64, 0, s, lock, flush_count);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void ps_gather_rows_bf16tab(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,
+                            const int64_t* n_dev, int W, void* out, bool out_bf16, hipStream_t s) {
+  if (n <= 0) return;
+  if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_gather_rows_bf16tab: P out of range");
+  if (W % 8 || reinterpret_cast<uintptr_t>(out) % 16) throw std::runtime_error("bf16 gather: W % 8, aligned out");
+  const int grid = grid_for(n * (W / 8), 256, 8192);
+  if (out_bf16)
+    hipLaunchKernelGGL(ps_gather_bf16_kernel<bf16_t>, grid, 256, 0, s, bases, bounds, P, keys, n, n_dev, W,
+                       static_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(ps_gather_bf16_kernel<float>, grid, 256, 0, s, bases, bounds, P, keys, n, n_dev, W,
+                       static_cast<float*>(out));
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void ps_hash_gather(const int64_t* hkeys, const int64_t* hvals, const int64_t* bounds, int P, int64_t cap,
+                    const int64_t* keys, int64_t n, const int64_t* n_dev, int W, void* out, bool out_bf16,
+                    hipStream_t s) {
+  if (n <= 0) return;
+  if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_hash_gather: P out of range");
+  if (cap <= 0 || (cap & (cap - 1))) throw std::runtime_error("ps_hash_gather: capacity must be a power of two");
+  const int grid = grid_for(n, 256, 4096);
+  if (out_bf16)
+    hipLaunchKernelGGL(ps_hash_gather_kernel<bf16_t>, grid, 256, 0, s, hkeys, hvals, bounds, P, cap, keys, n, n_dev,
+                       W, static_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(ps_hash_gather_kernel<float>, grid, 256, 0, s, hkeys, hvals, bounds, P, cap, keys, n, n_dev,
+                       W, static_cast<float*>(out));
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void ps_pull(const int64_t* srcs, uint64_t owners, int count, int64_t shard_bytes, void* dst, hipStream_t s) {
+  if (count <= 0) return;
+  if (count > kPsMaxWorld || shard_bytes % 16 || reinterpret_cast<uintptr_t>(dst) % 16)
+    throw std::runtime_error("ps_pull: <= 16 owners, 16-byte aligned shards");
+  const int64_t chunks = shard_bytes / 16;
+  hipLaunchKernelGGL(ps_pull_kernel, grid_for(chunks * count, 256, 8192), 256, 0, s, srcs, owners, chunks,
+                     static_cast<char*>(dst), shard_bytes, count);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
 
 void ps_push_rows(const int64_t* uniq, const int64_t* counts, const int64_t* U_dev, int64_t n, const float* g, int W,
                   const int64_t* inbox, int P, int64_t slot_off, int64_t cap, hipStream_t s) {
@@ -186,6 +512,8 @@ HipApplier::HipApplier(int device, int tables) : dev_(device), descs_(tables) {
 }
 
 HipApplier::~HipApplier() {
+  for (auto& e : events_)
+    if (e) (void)hipEventDestroy(e);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -207,7 +535,30 @@ void HipApplier::ThreadInit() {
   // the owner's applies are short and on every requester's critical path (SSP gates on them):
   // the highest priority lets them start beside a running step
   MINIPS_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+  for (auto& e : events_) MINIPS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 }
+
+void HipApplier::BeginTable(int t) {
+  const Desc& d = descs_.at(t);
+  uint32_t* lock = d.kind == 0 ? d.sp.lock : d.dn.lock;
+  if (lock) ps_write_lock(lock, err_, stream_);
+}
+
+void HipApplier::EndTable(int t) {
+  const Desc& d = descs_.at(t);
+  uint32_t* lock = d.kind == 0 ? d.sp.lock : d.dn.lock;
+  uint32_t* flush = d.kind == 0 ? d.sp.flush : d.dn.flush;
+  if (lock) ps_write_unlock(lock, flush, stream_);
+}
+
+uint64_t HipApplier::Submit() {
+  const uint64_t ticket = submitted_++;
+  MINIPS_HIP_CHECK(hipEventRecord(events_[ticket % kEvents], stream_));
+  return ticket;
+}
+
+// (the server keeps at most 2 batches in flight, so an event is never re-recorded before its wait)
+void HipApplier::Wait(uint64_t ticket) { MINIPS_HIP_CHECK(hipEventSynchronize(events_[ticket % kEvents])); }
 
 void HipApplier::Apply(int t, int r, int64_t c) {
   Desc& d = descs_.at(t);
@@ -217,6 +568,27 @@ void HipApplier::Apply(int t, int r, int64_t c) {
     const int64_t* cnt = reinterpret_cast<const int64_t*>(slot);
     const int64_t* keys = reinterpret_cast<const int64_t*>(slot + kPsSlotHeader);
     const float* g = reinterpret_cast<const float*>(slot + kPsSlotHeader + 8 * p.cap);
+    if (p.hash_cap > 0) {  // Map storage
+      const int grid = (int)std::min<int64_t>((p.cap + 3) / 4, 4096);
+      const float scale = p.opt == kPsAdd ? 1.f : -p.lr;
+      if (p.opt == kPsRowwiseAdagrad)
+        hipLaunchKernelGGL(ps_hash_apply_kernel<2>, grid, 256, 0, stream_, p.hkeys, p.hash_cap, p.table, p.state, p.W,
+                           keys, g, cnt, p.cap, p.lr, p.eps, scale, err_);
+      else
+        hipLaunchKernelGGL(ps_hash_apply_kernel<0>, grid, 256, 0, stream_, p.hkeys, p.hash_cap, p.table, p.state, p.W,
+                           keys, g, cnt, p.cap, p.lr, p.eps, scale, err_);
+      MINIPS_HIP_CHECK(hipGetLastError());
+      return;
+    }
+    if (p.bf16) {  // bf16 rows: fp32 math and state, stochastic rounding keyed by the apply count
+      const uint32_t step = (uint32_t)d.step.fetch_add(1);
+      bf16_t* tab = reinterpret_cast<bf16_t*>(p.table);
+      const int code = p.opt == kPsRowwiseAdagrad ? 0 : 1;
+      const float scale = p.opt == kPsAdd ? 1.f : -p.lr;
+      sparse_apply_bf16tab(code, tab, p.ld, p.state, p.state2, p.D1, keys, p.cap, p.base, p.W, g, p.lr, p.eps, scale,
+                           step, p.seed, stream_, cnt);
+      return;
+    }
     switch (p.opt) {
       case kPsAdd: sparse_sgd(p.table, p.ld, keys, p.cap, p.base, p.W, g, 1.f, stream_, cnt); break;
       case kPsSgd: sparse_sgd(p.table, p.ld, keys, p.cap, p.base, p.W, g, -p.lr, stream_, cnt); break;

@@ -8,7 +8,7 @@ namespace minips {
 
 AsyncServer::AsyncServer(const std::string& board_name, int world, int rank, int tables, Applier* applier)
     : board_(board_name, world, rank, tables), applier_(applier), world_(world), rank_(rank), tables_(tables),
-      enabled_(tables) {
+      enabled_(tables), issued_((size_t)tables * world, 0) {
   MINIPS_CHECK(applier_ != nullptr, "async server: no applier");
   for (auto& e : enabled_) e.store(false);
 }
@@ -17,6 +17,11 @@ AsyncServer::~AsyncServer() { Stop(); }
 
 void AsyncServer::Enable(int table) {
   MINIPS_CHECK(table >= 0 && table < tables_, "async server: table " << table);
+  {
+    // the table's counters may be ahead of issued_ (a table registered after earlier traffic)
+    std::lock_guard<std::mutex> lk(mu_);
+    resync_ = true;
+  }
   enabled_[table].store(true, std::memory_order_release);
   board_.Wake();
 }
@@ -24,19 +29,28 @@ void AsyncServer::Enable(int table) {
 void AsyncServer::Start() {
   if (running_.exchange(true)) return;
   stop_.store(false);
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    resync_ = true;
+    loop_done_ = false;
+  }
+  pub_ = std::thread([this] { PublishLoop(); });
   th_ = std::thread([this] { Loop(); });
 }
 
 void AsyncServer::Stop() {
-  if (!th_.joinable()) return;
+  if (!th_.joinable() && !pub_.joinable()) return;
   stop_.store(true);
   {
     std::lock_guard<std::mutex> lk(mu_);
     pause_req_ = false;
   }
   cv_.notify_all();
+  pcv_.notify_all();
   board_.Wake();
-  th_.join();
+  if (th_.joinable()) th_.join();  // the publisher then drains what was issued and exits
+  pcv_.notify_all();
+  if (pub_.joinable()) pub_.join();
   running_.store(false);
 }
 
@@ -45,6 +59,7 @@ void AsyncServer::Pause() {
   pause_req_ = true;
   lk.unlock();
   board_.Wake();
+  pcv_.notify_all();
   lk.lock();
   cv_.wait(lk, [&] { return paused_ || !running_.load() || !error_.empty(); });
 }
@@ -86,14 +101,31 @@ void AsyncServer::Loop() {
       bool log_on;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        log_on = log_on_;
         if (pause_req_) {
+          // a consistent point: nothing issued and unpublished, nothing starts until Resume
+          pcv_.wait(lk, [&] { return inflight_.empty() || stop_.load() || !error_.empty(); });
           paused_ = true;
           cv_.notify_all();
           cv_.wait(lk, [&] { return !pause_req_ || stop_.load(); });
           paused_ = false;
+          resync_ = true;  // a restore may have rewound the board
           if (stop_.load()) break;
         }
+        // at most kInFlight batches issued and not yet published
+        pcv_.wait(lk, [&] { return (int)inflight_.size() < kInFlight || stop_.load() || pause_req_; });
+        if (stop_.load()) break;
+        if (pause_req_) continue;
+        if (resync_) {  // the pipeline is empty here (start / resume / enable)
+          if (inflight_.empty()) {
+            for (int t = 0; t < tables_; ++t)
+              for (int r = 0; r < world_; ++r) issued_[(size_t)t * world_ + r] = board_.Applied(t, rank_, r);
+            resync_ = false;
+          } else {
+            pcv_.wait(lk, [&] { return inflight_.empty() || stop_.load(); });
+            continue;
+          }
+        }
+        log_on = log_on_;
       }
       // read the epoch BEFORE scanning: a publish after the scan changes it, so the sleep below
       // returns at once instead of missing that work
@@ -102,7 +134,7 @@ void AsyncServer::Loop() {
       for (int t = 0; t < tables_; ++t) {
         if (!enabled_[t].load(std::memory_order_acquire)) continue;
         for (int r = 0; r < world_; ++r) {
-          const int64_t a = board_.Applied(t, rank_, r), s = board_.Sent(t, r);
+          const int64_t a = issued_[(size_t)t * world_ + r], s = board_.Sent(t, r);
           if (s > a) todo.push_back({t, r, a, s});
         }
       }
@@ -110,29 +142,37 @@ void AsyncServer::Loop() {
         board_.WaitEpoch(epoch, 0.05);
         continue;
       }
-      std::vector<int64_t> logged;
-      int64_t n = 0;
+      Batch b;
+      b.applies = 0;
       for (int t = 0; t < tables_; ++t) {
+        bool begun = false;
         for (int64_t k = 0;; ++k) {
           bool any = false;
           for (const Todo& w : todo) {
             if (w.t != t || w.from + k >= w.to) continue;
+            if (!begun) {
+              applier_->BeginTable(t);
+              begun = true;
+            }
             any = true;
             applier_->Apply(t, w.r, w.from + k);
-            ++n;
-            if (log_on) logged.insert(logged.end(), {(int64_t)t, (int64_t)w.r, w.from + k});
+            ++b.applies;
+            if (log_on) b.logged.insert(b.logged.end(), {(int64_t)t, (int64_t)w.r, w.from + k});
           }
           if (!any) break;
         }
+        if (begun) applier_->EndTable(t);
       }
-      applier_->Flush();  // the device work is complete: the rows are visible to every rank
-      for (const Todo& w : todo) board_.PublishApplied(w.t, w.r, w.to);
-      applies_.fetch_add(n);
-      batches_.fetch_add(1);
-      if (!logged.empty()) {
+      b.ticket = applier_->Submit();
+      for (const Todo& w : todo) {
+        issued_[(size_t)w.t * world_ + w.r] = w.to;
+        b.pub.insert(b.pub.end(), {(int64_t)w.t, (int64_t)w.r, w.to});
+      }
+      {
         std::lock_guard<std::mutex> lk(mu_);
-        log_.insert(log_.end(), logged.begin(), logged.end());
+        inflight_.push_back(std::move(b));
       }
+      pcv_.notify_all();
     }
   } catch (const std::exception& e) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -144,10 +184,54 @@ void AsyncServer::Loop() {
   {
     std::lock_guard<std::mutex> lk(mu_);
     paused_ = false;
+    loop_done_ = true;
   }
-  running_.store(false);
+  pcv_.notify_all();
   cv_.notify_all();
   board_.Wake();
+}
+
+// Publishes the batches in issue order once their device work completed (their rows are visible
+// to every rank), then wakes the waiters of the board.
+void AsyncServer::PublishLoop() {
+  for (;;) {
+    Batch* b = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      pcv_.wait(lk, [&] { return !inflight_.empty() || loop_done_; });
+      if (inflight_.empty()) break;  // the loop ended and everything issued is published
+      b = &inflight_.front();        // stays in the deque (only this thread pops)
+    }
+    bool ok = true;
+    try {
+      applier_->Wait(b->ticket);
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (error_.empty()) error_ = e.what();
+      ok = false;
+    }
+    if (ok) {  // never publish a batch whose device work failed
+      for (size_t i = 0; i + 2 < b->pub.size(); i += 3)
+        board_.PublishApplied((int)b->pub[i], (int)b->pub[i + 1], b->pub[i + 2]);
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (ok) {
+        applies_.fetch_add(b->applies);
+        batches_.fetch_add(1);
+        if (!b->logged.empty()) log_.insert(log_.end(), b->logged.begin(), b->logged.end());
+      }
+      inflight_.pop_front();
+      if (!ok) {
+        inflight_.clear();  // nothing later may be published either
+        stop_.store(true);
+      }
+    }
+    pcv_.notify_all();
+    cv_.notify_all();
+  }
+  cv_.notify_all();
+  running_.store(false);
 }
 
 }  // namespace minips

@@ -13,11 +13,18 @@
 //
 // Apply order inside one wake-up: clock-major, requesters interleaved (r0 c, r1 c, ..., r0 c+1,
 // ...), per table -- recorded in the apply log when enabled, so a test can replay the exact order.
+//
+// Pipelining: the thread does not wait for a batch's device work. It hands (ticket, what the batch
+// applied) to a publisher thread, which waits for the ticket and then publishes `applied`, and
+// scans for the next batch right away (up to kInFlight batches issued and unpublished), so the
+// applies of consecutive batches queue back to back on the owner's stream. `issued_` remembers
+// what is in flight; Pause() drains the pipeline.
 #pragma once
 
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -32,9 +39,20 @@ class Applier {
  public:
   virtual ~Applier() = default;
   virtual void ThreadInit() {}  // called once on the server thread (e.g. bind the device)
+  // Brackets of one table's applies in a batch (the GPU applier takes the owner's write lock of
+  // the table there, so no one-sided read sees half of the batch).
+  virtual void BeginTable(int /*t*/) {}
+  virtual void EndTable(int /*t*/) {}
   // Issue the apply of requester `r`'s clock `c` of table `t` (inbox slot c % depth); may return
   // before the work completed.
   virtual void Apply(int t, int r, int64_t c) = 0;
+  // Mark the end of a batch: Wait(ticket) returns once every apply issued before Submit completed
+  // and is visible to every rank. The default is synchronous (the work is done when Submit returns).
+  virtual uint64_t Submit() {
+    Flush();
+    return 0;
+  }
+  virtual void Wait(uint64_t /*ticket*/) {}
   // Complete every issued apply: the updated rows must be visible to every rank afterwards.
   virtual void Flush() = 0;
 };
@@ -63,6 +81,14 @@ class AsyncServer {
 
  private:
   void Loop();
+  void PublishLoop();
+  struct Batch {
+    uint64_t ticket;
+    std::vector<int64_t> pub;  // (table, requester, clock) triples to publish
+    int64_t applies;
+    std::vector<int64_t> logged;
+  };
+  static constexpr int kInFlight = 2;
 
   PSBoard board_;
   Applier* applier_;
@@ -77,6 +103,13 @@ class AsyncServer {
   std::string error_;
   bool log_on_ = false;
   std::vector<int64_t> log_;
+  // pipeline (guarded by mu_): batches issued, not yet published; issued_[t * world + r]
+  std::deque<Batch> inflight_;
+  std::vector<int64_t> issued_;
+  bool resync_ = true;  // re-read issued_ from the board (start, resume: a restore may rewind it)
+  bool loop_done_ = false;
+  std::condition_variable pcv_;
+  std::thread pub_;
 };
 
 }  // namespace minips

@@ -37,8 +37,10 @@ PSBoard::PSBoard(const std::string& name, int world, int rank, int tables, doubl
   MINIPS_CHECK(world >= 1 && world <= kMaxWorld && rank >= 0 && rank < world,
                "ps board: bad rank " << rank << "/" << world << " (at most " << kMaxWorld << " ranks)");
   MINIPS_CHECK(tables >= 1 && tables <= kMaxTables, "ps board: tables " << tables);
-  static_assert(sizeof(Header) == 64 && sizeof(SentLine) == 64 && sizeof(AppliedRow) == 128, "board layout");
-  bytes_ = sizeof(Header) + sizeof(SentLine) * (size_t)tables * world + sizeof(AppliedRow) * (size_t)tables * world;
+  static_assert(sizeof(Header) == 64 && sizeof(SentLine) == 64 && sizeof(AppliedRow) == 128 && sizeof(LockLine) == 64,
+                "board layout");
+  bytes_ = sizeof(Header) + sizeof(SentLine) * (size_t)tables * world + sizeof(AppliedRow) * (size_t)tables * world +
+           sizeof(LockLine) * (size_t)tables * world;
   const std::string path = "/dev/shm/" + name;
   int fd = -1;
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(attach_timeout_s);
@@ -57,6 +59,7 @@ PSBoard::PSBoard(const std::string& name, int world, int rank, int tables, doubl
   hdr_ = static_cast<Header*>(p);
   sent_ = reinterpret_cast<SentLine*>(static_cast<char*>(p) + sizeof(Header));
   applied_ = reinterpret_cast<AppliedRow*>(reinterpret_cast<char*>(sent_) + sizeof(SentLine) * (size_t)tables * world);
+  locks_ = reinterpret_cast<LockLine*>(reinterpret_cast<char*>(applied_) + sizeof(AppliedRow) * (size_t)tables * world);
   hdr_->magic = kBoardMagic;
   hdr_->world = world;
   hdr_->tables = tables;
@@ -142,6 +145,7 @@ double PSBoard::WaitUntil(Pred pred, double timeout_s) {
   for (;;) {
     const uint32_t e = hdr_->epoch.load(std::memory_order_acquire);
     if (pred()) break;  // checked after reading the epoch: no lost wake-up
+    if (Aborted()) return -2.0;
     if (timeout_s > 0 && Since(t0) >= timeout_s) return -1.0;
     timespec ts{0, 2000000};  // 2 ms: a bounded sleep also covers a publisher that died mid-publish
     FutexCall(&hdr_->epoch, FUTEX_WAIT, e, &ts);
@@ -183,6 +187,66 @@ std::vector<int64_t> PSBoard::SnapshotApplied(int table) const {
   for (int o = 0; o < world_; ++o)
     for (int r = 0; r < world_; ++r) out[(size_t)o * world_ + r] = Applied(table, o, r);
   return out;
+}
+
+void PSBoard::SetAbort(uint32_t code) {
+  hdr_->abort.store(code ? code : 1u, std::memory_order_release);
+  Bump();
+}
+
+namespace {
+constexpr uint32_t kWriter = 0x80000000u;
+
+template <typename Pred>
+bool SpinUntil(Pred pred, double timeout_s, const std::atomic<uint32_t>& abort) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0;; ++i) {
+    if (pred()) return true;
+    if (abort.load(std::memory_order_acquire)) return false;
+    if (timeout_s > 0 && Since(t0) >= timeout_s) return false;
+    if (i < 1000) {
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+}
+}  // namespace
+
+bool PSBoard::ReadLock(int table, double timeout_s) {
+  for (int o = 0; o < world_; ++o) {  // ascending owners: no reader waits on a lower lock while holding a higher one
+    std::atomic<uint32_t>& w = locks_[(size_t)table * world_ + o].word;
+    const bool ok = SpinUntil(
+        [&] {
+          uint32_t v = w.load(std::memory_order_relaxed);
+          return !(v & kWriter) && w.compare_exchange_weak(v, v + 1, std::memory_order_acquire);
+        },
+        timeout_s, hdr_->abort);
+    if (!ok) {
+      for (int p = 0; p < o; ++p) locks_[(size_t)table * world_ + p].word.fetch_sub(1, std::memory_order_release);
+      return false;
+    }
+  }
+  return true;
+}
+
+void PSBoard::ReadUnlock(int table) {
+  for (int o = 0; o < world_; ++o) locks_[(size_t)table * world_ + o].word.fetch_sub(1, std::memory_order_release);
+}
+
+bool PSBoard::WriteLock(int table, double timeout_s) {
+  std::atomic<uint32_t>& w = locks_[(size_t)table * world_ + rank_].word;
+  w.fetch_or(kWriter, std::memory_order_acq_rel);  // new readers wait from here on
+  if (SpinUntil([&] { return (w.load(std::memory_order_acquire) & ~kWriter) == 0; }, timeout_s, hdr_->abort))
+    return true;
+  w.fetch_and(~kWriter, std::memory_order_release);
+  return false;
+}
+
+void PSBoard::WriteUnlock(int table) {
+  locks_[(size_t)table * world_ + rank_].word.fetch_and(~kWriter, std::memory_order_release);
 }
 
 void PSBoard::Unlink() { ::unlink(("/dev/shm/" + name_).c_str()); }

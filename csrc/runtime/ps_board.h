@@ -64,7 +64,8 @@ class PSBoard {
 
   // Blocking waits (futex sleep on the epoch, GIL released by the bindings). They return the
   // seconds waited, or -1 if the condition still does not hold after `timeout_s` (> 0) -- the
-  // caller decides whether that is a failure (and can check the server's error in between).
+  // caller decides whether that is a failure (and can check the server's error in between) --
+  // or -2 once the board is aborted.
   double WaitMinApplied(int table, int64_t target, double timeout_s);
   double WaitAppliedFrom(int table, int requester, int64_t target, double timeout_s);
   double WaitSentAtLeast(int table, int rank, int64_t target, double timeout_s);
@@ -72,6 +73,19 @@ class PSBoard {
   uint32_t WaitEpoch(uint32_t seen, double max_s);
   uint32_t Epoch() const { return hdr_->epoch.load(std::memory_order_acquire); }
   void Wake();  // bump the epoch and wake every sleeper (shutdown, pause)
+
+  // Reader / writer lock per (table, owner) for the CPU data path (GPU ranks keep their lock words
+  // in the owners' HBM, csrc/kernels/onesided.hip): a reader takes every owner's read lock in
+  // ascending order, the owner's server thread takes its own write lock around a batch of applies,
+  // so no read sees half of a batch. Writer preference (a waiting writer blocks new readers).
+  bool ReadLock(int table, double timeout_s);  // false (nothing held) on timeout / abort
+  void ReadUnlock(int table);
+  bool WriteLock(int table, double timeout_s);
+  void WriteUnlock(int table);
+  // Job-wide abort word: a rank that knows the set cannot finish (a peer died, the supervisor
+  // restarts everyone) sets it; every wait on this board then gives up at once (returns -2).
+  void SetAbort(uint32_t code);
+  uint32_t Aborted() const { return hdr_->abort.load(std::memory_order_acquire); }
 
   std::vector<int64_t> SnapshotSent(int table) const;
   std::vector<int64_t> SnapshotApplied(int table) const;  // [owner][requester] row-major
@@ -84,7 +98,12 @@ class PSBoard {
     uint64_t magic;
     int32_t world, tables;
     std::atomic<uint32_t> epoch;  // futex word
-    char pad[44];
+    std::atomic<uint32_t> abort;
+    char pad[40];
+  };
+  struct LockLine {
+    std::atomic<uint32_t> word;  // bit 31 writer, bits 0..30 readers
+    char pad[60];
   };
   struct SentLine {
     std::atomic<int64_t> clock;
@@ -100,6 +119,7 @@ class PSBoard {
   Header* hdr_ = nullptr;
   SentLine* sent_ = nullptr;
   AppliedRow* applied_ = nullptr;
+  LockLine* locks_ = nullptr;
   size_t bytes_ = 0;
   int world_, rank_, tables_;
   std::string name_;

@@ -207,10 +207,26 @@ class Supervisor:
         return "running", -1, "", True
 
     # ------------------------------------------------------------------------------ recovery
+    def _inplace_capable(self) -> bool:
+        """Every rank said it can roll back in its own process (caps_<r>.json, written after its
+        tables exist). A rank of the one-sided transport cannot: its peers hold IPC mappings of its
+        shards and inboxes and a shared progress board, so only a whole-set restart is valid."""
+        for r in range(self.nproc):
+            try:
+                caps = json.loads(open(os.path.join(self.hb_dir, f"caps_{r}.json")).read())
+            except (OSError, ValueError):
+                continue  # not written yet (start-up): the exit-status / heartbeat rules decide
+            if not caps.get("inplace", True):
+                return False
+        return True
+
     def _recover_inplace(self, rank: int) -> bool:
         """Relaunch only ``rank``; the survivors roll back in place. False: not possible."""
         survivors = [r for r, p in enumerate(self.procs[:self.nproc]) if r != rank and p.poll() is None]
         if not survivors or len(survivors) != self.nproc - 1:
+            return False
+        if not self._inplace_capable():
+            fault_tolerance_phase(3, "a rank cannot roll back in place (one-sided tables): whole-set restart")
             return False
         self._stop([rank])
         self.restarts += 1

@@ -19,7 +19,7 @@ How the workers of one rank meet the GPU tables (one table shard per rank, not p
     SSP guarantee of ssp_model.cpp:58-85, with the slowest worker of every rank included (a
     rank publishes the min over its workers). Adds of all local workers join the rank's push of
     the clock in which they happened;
-  * transport "collective" (BSP, or SSP/ASP over RCCL, and Map storage): every table operation is
+  * transport "collective" (BSP, or SSP/ASP over RCCL): every table operation is
     a collective, so the local workers go in lockstep: their Gets of a clock are served by ONE
     combined Get (BSP: every worker of the superstep reads the same values, exactly the
     reference's), their Adds are summed into the one push of the clock. Workers must then issue
@@ -47,23 +47,27 @@ def create_table(comm: Comm, kind: str = "sparse", *, num_rows: int = 0, width: 
     tables in the same order). ``kind`` "sparse" (rows of ``width`` values, keys in [0, num_rows);
     storage "map": unbounded 63-bit keys in a GPU hash table) or "dense" (one vector of
     ``n_params``); ``model`` bsp | ssp | asp; ``transport`` collective (RCCL) | onesided (the
-    asynchronous PS, SSP / ASP only)."""
+    asynchronous PS, SSP / ASP only; range rows in fp32 or bf16, or Map storage)."""
     from .ps.tables import DenseTable, HashSparseTable, SparseTable
 
     model = model.lower()
     storage = storage.lower()
     if transport == "onesided":
-        from .ps.onesided import AsyncDenseTable, AsyncSparseTable
+        from .ps.onesided import AsyncDenseTable, AsyncHashTable, AsyncSparseTable
 
-        if storage == "map":
-            raise ValueError("Map storage runs on the collective transport (the one-sided path needs key ranges)")
-        if value_dtype != torch.float32:
-            raise ValueError("the one-sided transport stores fp32 rows")
         if kind == "dense":
+            if value_dtype != torch.float32:
+                raise ValueError("one-sided dense tables keep an fp32 master")
             return AsyncDenseTable(comm, n_params, optimizer=optimizer, lr=lr, consistency=model, staleness=staleness,
                                    pull_dtype=pull_dtype or torch.bfloat16, table_id=table_id, **kw)
+        if storage == "map":
+            if value_dtype != torch.float32:
+                raise ValueError("one-sided Map storage keeps fp32 rows (MapStorage sums exactly)")
+            return AsyncHashTable(comm, width, optimizer=optimizer, lr=lr, consistency=model, staleness=staleness,
+                                  pull_dtype=pull_dtype or torch.float32, table_id=table_id, **kw)
         return AsyncSparseTable(comm, num_rows, width, optimizer=optimizer, lr=lr, consistency=model,
-                                staleness=staleness, pull_dtype=pull_dtype or torch.float32, table_id=table_id, **kw)
+                                staleness=staleness, pull_dtype=pull_dtype or torch.float32, table_id=table_id,
+                                value_dtype=value_dtype, **kw)
     if kind == "dense":
         return DenseTable(comm, n_params, optimizer=optimizer, lr=lr, consistency=model, staleness=staleness,
                           pull_dtype=pull_dtype or (torch.float64 if value_dtype == torch.float64 else torch.bfloat16),

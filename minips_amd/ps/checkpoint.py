@@ -41,6 +41,7 @@ The reference defects are fixed: text restore parses its own format, BSP/ASP tab
 from __future__ import annotations
 
 import glob
+import json
 import os
 import threading
 import time
@@ -50,7 +51,7 @@ import torch
 
 from .._native import runtime
 from ..utils.metrics import get_logger
-from .fault import slow_io_delay
+from .fault import slow_io_delay, slow_pause_delay
 
 _DT = {torch.float32: "float32", torch.bfloat16: "bfloat16", torch.float64: "float64", torch.int64: "int64",
        torch.int32: "int32"}
@@ -58,6 +59,8 @@ _TD = {v: k for k, v in _DT.items()}
 WORKER_TID_OFFSET = 100  # SimpleIdMapper: workers of node n are n*1000 + [100, 1000)
 _RING_DEFAULT = int(os.environ.get("MINIPS_CKPT_RING_MB", "1024")) << 20
 
+
+_FIXED_META = ("global_rows", "base", "rows", "cols", "clock", "table_id", "rank", "world", "kind")
 
 def _prefix_path(prefix: str, name: str) -> str:
     return prefix + name
@@ -134,8 +137,15 @@ class Checkpointer:
         # every push so far is applied; the owners' server threads now stop until the snapshot is
         # taken (the reference SSPModel::Dump runs inside its server thread, ssp_model.cpp:112-125)
         paused = [t for t in tables.values() if hasattr(t, "snapshot_begin")]
+        if paused:
+            slow_pause_delay(self.comm.rank)  # fault injection (tests): a rank late to pause
         for t in paused:
             t.snapshot_begin()
+        if paused:
+            # every owner is paused before ANY rank resumes training: otherwise a fast rank could
+            # push clock c + 1 into a slow owner that has not paused yet, its snapshot would hold
+            # rows of c + 1 under meta clock c, and a restore would apply that push twice
+            self.comm.store_barrier(f"ckpt_pause_{int(iteration)}")
         jobs = []
         for k, (tid, table) in enumerate(sorted(tables.items())):
             meta, arrays = table.shard_state()
@@ -252,6 +262,10 @@ class Checkpointer:
         w.close()
         if text is not None:
             text.close()
+        extra = {k: v for k, v in meta.items() if k not in _FIXED_META}
+        if extra:  # table state beyond the binary header (e.g. the bf16 rows' rounding stream)
+            with open(_prefix_path(out, base + ".json"), "w") as f:
+                json.dump(extra, f)
 
     def _write_host_array(self, w, k: int, a: torch.Tensor, text=None):
         """Host-resident array: written in ring-sized pieces (a CPU table streams through the ring
@@ -447,6 +461,15 @@ class Checkpointer:
                         if d is not None:
                             self._read_rows_into(path, off, _TD[dt], int(cols), a - meta["base"], b - a,
                                                  d[a - lo: b - lo])
+            if hasattr(table, "restore_meta"):
+                extras = []
+                for path in files:
+                    jp = path[: -len(".bin")] + ".json"
+                    if os.path.exists(jp):
+                        with open(jp) as f:
+                            extras.append((f"server_params_{self.my_id}_t{tid}.bin" in path, json.load(f)))
+                if extras:  # this rank's own entry, else (a rescaled restore) the first one
+                    table.restore_meta(next((e for mine, e in extras if mine), extras[0][1]))
             table.finish_restore(clock or 0)
         self._release_staging()
         slow_io_delay(self.comm.rank)  # fault injection (tests): a rank whose restore reads are slow

@@ -39,6 +39,15 @@ class Heartbeat:
         self._th = threading.Thread(target=self._loop, name="minips-heartbeat", daemon=True)
         self._th.start()
 
+    def write_caps(self, **caps):
+        """Recovery capabilities of this rank (<dir>/caps_<rank>.json), read by the supervisor."""
+        d = os.path.dirname(self.path)
+        r = os.path.basename(self.path)[3:]
+        tmp = os.path.join(d, f"caps_{r}.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(caps, f)
+        os.replace(tmp, os.path.join(d, f"caps_{r}.json"))
+
     def progress(self, step: int):
         """Called by the training loop after each completed iteration (and at long phases:
         start-up, restore, checkpoint), so the stamp carries real progress."""
@@ -117,6 +126,18 @@ def slow_io_delay(rank: int):
     """Fault injection for long-phase tests: MINIPS_FAULT_SLOW_IO="<rank>:<seconds>" makes each
     checkpoint write and restore of that rank take that much longer (a slow disk / network FS)."""
     spec = os.environ.get("MINIPS_FAULT_SLOW_IO", "")
+    if not spec:
+        return
+    r, secs = spec.split(":")
+    if int(r) == rank:
+        time.sleep(float(secs))
+
+
+def slow_pause_delay(rank: int):
+    """Fault injection: MINIPS_FAULT_SLOW_PAUSE="<rank>:<seconds>" delays that rank between the
+    checkpoint's clock all-gather and the pause of its asynchronous servers (the window in which a
+    fast peer could otherwise resume and push into a not-yet-paused owner)."""
+    spec = os.environ.get("MINIPS_FAULT_SLOW_PAUSE", "")
     if not spec:
         return
     r, secs = spec.split(":")

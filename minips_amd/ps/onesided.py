@@ -22,7 +22,16 @@ wait for a peer's pushes. These tables do the same with no collective on the dat
   ``applied``;
 * SSP gate (a Get at own clock c): every owner has applied every requester's clocks < c - s,
   i.e. min applied >= c - s (csrc/runtime/ps_board.h); ASP never waits (``asp_bound`` optionally
-  bounds it the same way); a requester reuses an inbox slot only after every owner applied it.
+  bounds it the same way); a requester reuses an inbox slot only after every owner applied it;
+* consistency of one-sided reads: each owner's applies of a batch run under its write lock and
+  every Get / dense pull under the read locks of the owners (GPU: lock words in the owners'
+  fine-grained HBM, csrc/kernels/onesided.hip; CPU: the board's lock lines), so a read never sees
+  half of an owner's batch -- the reference's server thread serialises Add and Get the same way
+  (server/server_thread.cpp:23-61). Dense pulls are lazy: an owner's shard is re-pulled only when
+  the cached copy is older than the staleness bound allows;
+* storage: range rows in fp32 or bf16 (stochastic rounding, the 10B-row DLRM table), or Map
+  storage (AsyncHashTable: the owner's open-addressing table, insert on apply, a Get of an absent
+  key reads 0 -- server/map_storage.hpp:13-26).
 
 The same code runs on CPU ranks (gloo tests): shards and inboxes are /dev/shm files mapped by
 every rank, the server thread is the same C++ loop calling back into the PyTorch reference
@@ -31,6 +40,7 @@ optimizers. Reference semantics kept: BSP stays on the collective tables (ps/tab
 from __future__ import annotations
 
 import collections
+import contextlib
 import os
 import time
 import uuid
@@ -83,8 +93,24 @@ class AsyncPS:
         if self.cuda:
             from .._native import kernels
 
-            self.server = kernels().AsyncServer(name, self.world, self.rank, _MAX_TABLES, comm.device.index or 0)
+            k = kernels()
+            self.server = k.AsyncServer(name, self.world, self.rank, _MAX_TABLES, comm.device.index or 0)
             self._anchor = torch.zeros(1, device=comm.device)
+            # the rank's error word (a device spin that timed out sets a bit) and the control lines
+            # (one lock word per table) every rank maps from every owner
+            self.err = k.HostWord()
+            self.server.set_error_word(self.err.device_ptr)
+            dev_i = comm.device.index or 0
+            buf, handle = k.ipc_alloc(k.PS_CTRL_BYTES, dev_i, 1)
+            handles = [None] * comm.world
+            if comm.world > 1:
+                dist.all_gather_object(handles, handle, group=comm.group)
+            self.ctrl = [buf if r == comm.rank else k.ipc_open(handles[r], k.PS_CTRL_BYTES, dev_i)
+                         for r in range(comm.world)]
+            self._line = k.PS_CTRL_LINE
+            self.held = torch.zeros(k.PS_HELD_SLOTS, dtype=torch.int32, device=comm.device)
+            self._held_n = 0
+            self._locks: dict = {}
         else:
             self.server = runtime().AsyncServer(name, self.world, self.rank, _MAX_TABLES, self._apply_cpu)
         if os.environ.get("MINIPS_PS_APPLY_LOG") == "1":
@@ -119,6 +145,54 @@ class AsyncPS:
             perr = self.server.publish_error()
             if perr:
                 raise RuntimeError(f"async PS clock publisher of rank {self.rank}: {perr}")
+            bits = self.err.value
+            if bits:
+                raise RuntimeError(f"async PS of rank {self.rank}: device error bits {bits:#x} (1: a read lock "
+                                   "timed out, 2: a write lock timed out, 4: a Map-storage table is full)")
+        if self.board.aborted:
+            raise RuntimeError(f"async PS: the job was aborted (code {self.board.aborted}: a peer failed or the "
+                               "supervisor restarts the rank set)")
+
+    def abort(self, code: int = 1):
+        """Make every rank's waits on this board give up at once (a peer is gone)."""
+        self.board.set_abort(int(code))
+
+    # -- the owners' reader / writer locks ----------------------------------------------------
+    def own_lock(self, t: int) -> int:
+        """Device address of this owner's lock word of table t (0 on CPU ranks: board locks)."""
+        return self.ctrl[self.rank].data_ptr() + t * self._line if self.cuda else 0
+
+    def _lock_tensor(self, t: int) -> torch.Tensor:
+        lt = self._locks.get(t)
+        if lt is None:
+            lt = self._locks[t] = torch.tensor([c.data_ptr() + t * self._line for c in self.ctrl], dtype=torch.int64,
+                                               device=self.comm.device)
+        return lt
+
+    @contextlib.contextmanager
+    def read_locked(self, t: int):
+        """Every owner's read lock of table t around the enclosed reads (GPU: taken and released by
+        kernels on the current stream, around the read kernels issued inside)."""
+        if self.cuda:
+            from .._native import kernels
+
+            k = kernels()
+            slot = self.held.data_ptr() + 4 * (self._held_n % self.held.numel())
+            self._held_n += 1
+            locks = self._lock_tensor(t)
+            k.ps_read_lock(locks, slot, self.err.device_ptr)
+            try:
+                yield
+            finally:
+                k.ps_read_unlock(locks, slot)
+        else:
+            if not self.board.read_lock(t, self.timeout if self.timeout > 0 else 0.0):
+                self.check()
+                raise TimeoutError(f"async PS: read lock of table {t} timed out")
+            try:
+                yield
+            finally:
+                self.board.read_unlock(t)
 
     def wait(self, fn, *args, what: str = "") -> float:
         """Run a board wait in slices, surfacing a server error instead of waiting it out."""
@@ -189,14 +263,16 @@ class _AsyncTable:
         self._cpu_files: list = []
 
     # -- shared buffers ---------------------------------------------------------------------
-    def _share(self, nbytes: list, tag: str) -> list:
+    def _share(self, nbytes: list, tag: str, kind: int = 1) -> list:
         """One buffer per rank (rank r's of nbytes[r] bytes, zero-filled), every one mapped here:
-        uint8 tensors [P]. GPU: hipMalloc + IPC handles; CPU: /dev/shm files."""
+        uint8 tensors [P]. GPU: hipExtMallocWithFlags + IPC handles -- ``kind`` 1 fine-grained
+        (shards, pull copies: read by peers while the owner writes), 2 uncached (inboxes: written by
+        peers); CPU: /dev/shm files."""
         comm, me = self.comm, self.comm.rank
         if self.cuda:
             from .._native import kernels
 
-            buf, handle = kernels().ipc_alloc(max(256, int(nbytes[me])), comm.device.index or 0)
+            buf, handle = kernels().ipc_alloc(max(256, int(nbytes[me])), comm.device.index or 0, int(kind))
             handles = [None] * comm.world
             if comm.world > 1:
                 dist.all_gather_object(handles, handle, group=comm.group)
@@ -317,11 +393,20 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
                  eps: float = 1e-8, pull_dtype=torch.bfloat16, consistency: str = "ssp", staleness: int = 0,
                  split: int | None = None, table_id: int = 0, init_std: float = 0.01, seed: int = 1234,
                  route: str = "mix", columns=None, max_keys: int = 1 << 16, depth: int | None = None,
-                 asp_bound: int | None = None):
+                 asp_bound: int | None = None, value_dtype=torch.float32):
         if optimizer not in ("add", "sgd", "rowwise_adagrad"):
             raise ValueError(f"sparse optimizer {optimizer!r}: add | sgd | rowwise_adagrad")
+        if value_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"one-sided rows are fp32 or bf16, not {value_dtype}")
+        if value_dtype == torch.bfloat16 and width not in (16, 32, 64):
+            raise ValueError("bf16 rows hold 16, 32 or 64 values")
         self._init_async(comm, consistency, staleness, depth, asp_bound)
-        self.value_dtype = self.push_dtype = torch.float32
+        # bf16 rows: half the HBM (config 5's 10B x 64 table: 1.28 TB of rows over 8 x 288 GB); the
+        # owner's optimizer math and state stay fp32, the row goes back to bf16 by stochastic rounding
+        self.value_dtype = value_dtype
+        self.push_dtype = self.grad_dtype = torch.float32
+        self._applies = 0  # apply counter (CPU path): keys the stochastic rounding of bf16 rows
+        self.seed = int(seed)
         self.columns = column_spec(columns, comm.device)
         self.route_mult = _route_multiplier(num_rows) if route == "mix" else 0
         self.table_id = table_id
@@ -341,31 +426,43 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         rows_of = [b[r + 1] - b[r] for r in range(P)]
         self.cap = _align(max(2, int(max_keys)), 2)
         self.slot_bytes = _align(_SLOT_HEADER + self.cap * (8 + 4 * width), 256)
-        shards = self._share([4 * width * n for n in rows_of], "shard")
+        esz = 2 if value_dtype == torch.bfloat16 else 4
+        shards = self._share([esz * width * n for n in rows_of], "shard", kind=1)
         self._shards = shards
-        self._views = [s[: 4 * width * n].view(torch.float32).view(n, width) for s, n in zip(shards, rows_of)]
+        self._views = [s[: esz * width * n].view(value_dtype).view(n, width) for s, n in zip(shards, rows_of)]
         self.shard = self._views[me]
         if init_std > 0:
             g = torch.Generator(device=dev)
             g.manual_seed(seed + 7919 * me)
-            self.shard.normal_(0.0, init_std, generator=g)
+            if value_dtype == torch.float32:
+                self.shard.normal_(0.0, init_std, generator=g)
+            else:  # drawn in fp32 (chunks: the 10B-row shards), rounded to bf16
+                step = 1 << 24
+                for r0 in range(0, self.rows_local, step):
+                    tmp = torch.empty(min(step, self.rows_local - r0), width, dtype=torch.float32, device=dev)
+                    self.shard[r0: r0 + tmp.shape[0]].copy_(tmp.normal_(0.0, init_std, generator=g))
         self.state = torch.zeros(self.rows_local, dtype=torch.float32, device=dev) \
             if optimizer == "rowwise_adagrad" else None
         self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
-        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox")
+        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=2)
+        self._register_server()
+        self._finish_init()
+
+    def _register_server(self, hash_cap: int = 0, hkeys: int = 0):
+        comm, me, dev = self.comm, self.comm.rank, self.comm.device
         if self.cuda:
-            self.bases = torch.tensor([s.data_ptr() for s in shards], dtype=torch.int64, device=dev)
+            self.bases = torch.tensor([s.data_ptr() for s in self._shards], dtype=torch.int64, device=dev)
             self.inbox_ptrs = torch.tensor([s.data_ptr() for s in self._inbox], dtype=torch.int64, device=dev)
-            D1 = split if split is not None else width
-            self.ps.server.add_sparse(self.t, _OPT_CODES[optimizer], self.shard.data_ptr(), width, width,
-                                      self.state.data_ptr() if self.state is not None else 0,
+            D1 = self.split if self.split is not None else self.width
+            self.ps.server.add_sparse(self.t, _OPT_CODES[self.optimizer], self.shard.data_ptr(), self.width,
+                                      self.width, self.state.data_ptr() if self.state is not None else 0,
                                       self.state2.data_ptr() if self.state2 is not None else 0, D1, self.base,
-                                      float(lr), float(eps), self.cap, self._inbox[me].data_ptr(), self.slot_bytes,
-                                      self.depth)
+                                      float(self.lr), float(self.eps), self.cap, self._inbox[me].data_ptr(),
+                                      self.slot_bytes, self.depth, int(self.value_dtype == torch.bfloat16),
+                                      self.seed & 0xFFFFFFFF, int(hash_cap), int(hkeys), self.ps.own_lock(self.t))
             torch.cuda.synchronize(dev)  # shard init + state zeroing done before any peer reads
         else:
             self.ps.server.enable(self.t)
-        self._finish_init()
 
     # -- planning: SparseTable's dedupe + owner grouping, no count exchange ----------------------
     def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
@@ -420,10 +517,18 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             plan = self._finish_plan(plan)
         self._gate(clock)
         out = torch.empty(max(plan.cap, 1), self.width, dtype=self.pull_dtype, device=self.comm.device)
+        with self.ps.read_locked(self.t):
+            self._gather(plan, out)
+        return out, plan
+
+    def _gather(self, plan, out):
         if self.cuda:
             from .._native import kernels
 
-            kernels().ps_gather_rows(self.bases, self.bounds, plan.uniq, plan.U_dev, self.width, out)
+            if self.value_dtype == torch.bfloat16:
+                kernels().ps_gather_rows_bf16tab(self.bases, self.bounds, plan.uniq, plan.U_dev, self.width, out)
+            else:
+                kernels().ps_gather_rows(self.bases, self.bounds, plan.uniq, plan.U_dev, self.width, out)
         else:
             u = plan.uniq[: plan.U]
             for o in range(self.comm.world):
@@ -431,7 +536,6 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
                 m = (u >= lo) & (u < hi)
                 if bool(m.any()):
                     out[: plan.U][m] = self._views[o][u[m] - lo].to(out.dtype)
-        return out, plan
 
     def clock(self):
         """Push this clock's gradient rows into the owners' inboxes, then publish the clock."""
@@ -499,6 +603,16 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         keys = buf[off + _SLOT_HEADER: off + _SLOT_HEADER + 8 * n].view(torch.int64).clone()
         g = buf[off + _SLOT_HEADER + 8 * cap: off + _SLOT_HEADER + 8 * cap + 4 * W * n].view(torch.float32)
         g = g.view(n, W).clone()
+        self._apply_rows(keys, g)
+
+    def _apply_rows(self, keys, g):
+        if self.value_dtype == torch.bfloat16:
+            opt = "rowwise_adagrad" if self.optimizer == "rowwise_adagrad" else "add"
+            scale = 1.0 if self.optimizer == "add" else -self.lr
+            ops.sparse_apply_bf16(opt, self.shard, self.state, keys, self.base, g, self.lr, self.eps, scale,
+                                  state2=self.state2, split=self.split, step=self._applies, seed=self.seed)
+            self._applies += 1
+            return
         if self.optimizer == "rowwise_adagrad":
             ops.sparse_rowwise_adagrad(self.shard, self.state, keys, self.base, g, self.lr, self.eps,
                                        state2=self.state2, split=self.split)
@@ -515,8 +629,19 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             arrays["state2"] = self.state2
         meta = dict(global_rows=self.num_rows, base=self.base, rows=self.rows_local, cols=self.width,
                     clock=self.clock_n, table_id=self.table_id, rank=self.comm.rank, world=self.comm.world,
-                    kind="sparse")
+                    kind="sparse", applies=self._apply_count())
         return meta, arrays
+
+    def _apply_count(self) -> int:
+        return int(self.ps.server.step(self.t)) if self.cuda else int(self._applies)
+
+    def restore_meta(self, meta: dict):
+        """Checkpoint meta of this rank's shard (before finish_restore): the bf16 rounding stream."""
+        n = int(meta.get("applies", 0))
+        if self.cuda:
+            self.ps.server.set_step(self.t, n)
+        else:
+            self._applies = n
 
     def restore_range(self):
         return self.base, self.base + self.rows_local
@@ -534,6 +659,159 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         if self.cuda:
             torch.cuda.synchronize(self.comm.device)
         self._restore_clock(clock)
+
+
+class AsyncHashTable(AsyncSparseTable):
+    """Map storage on the one-sided path (reference MapStorage, server/map_storage.hpp:13-26):
+    keys in [0, 2^63) are mixed by the same bijection as the collective HashSparseTable and
+    range-partitioned over the owners; each owner keeps an open-addressing table of fixed
+    ``capacity`` (power of two) in its fine-grained HBM -- keys [cap] int64 (-1 empty) and rows
+    [cap, W] fp32 (+ row-wise Adagrad state). The owner's server thread inserts a key on its first
+    Add (row 0 + update); a Get probes the owners' tables one-sidedly and reads 0 for an absent
+    key (MapStorage::SubGet's default-insert, without the insert: a read never writes the
+    owner's table). Capacity is fixed (no rehash under one-sided readers): a full table is a
+    device error bit, raised at the next check."""
+
+    def __init__(self, comm: Comm, width: int, capacity: int = 1 << 16, optimizer: str = "add", lr: float = 0.01,
+                 eps: float = 1e-8, pull_dtype=torch.float32, consistency: str = "ssp", staleness: int = 0,
+                 table_id: int = 0, max_keys: int = 1 << 16, depth: int | None = None, asp_bound: int | None = None,
+                 **_unused):
+        from .tables import MASK63
+
+        if optimizer not in ("add", "sgd", "rowwise_adagrad"):
+            raise ValueError(f"sparse optimizer {optimizer!r}: add | sgd | rowwise_adagrad")
+        self._init_async(comm, consistency, staleness, depth, asp_bound)
+        self.value_dtype = self.push_dtype = self.grad_dtype = torch.float32
+        self._applies, self.seed = 0, 0
+        self.columns = None
+        self.route_mult = 0
+        self.table_id = table_id
+        self.num_rows, self.width = MASK63, width
+        self.optimizer, self.lr, self.eps = optimizer, lr, eps
+        self.pull_dtype = pull_dtype
+        self.split = None
+        self.p2p = False
+        self._pending: list = []
+        self._own_bounds = torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=comm.device)
+        P, me, dev = comm.world, comm.rank, comm.device
+        b = even_bounds(MASK63, P)
+        self.bounds_list = b
+        self.bounds = torch.tensor(b, dtype=torch.int64, device=dev)
+        self.base = 0  # rows are addressed by slot
+        self.capacity = cap = 1 << max(4, int(capacity - 1).bit_length())
+        self.rows_local = cap
+        self.cap = _align(max(2, int(max_keys)), 2)
+        self.slot_bytes = _align(_SLOT_HEADER + self.cap * (8 + 4 * width), 256)
+        self._hk = self._share([8 * cap] * P, "hkeys", kind=1)
+        self._hkeys = [h[: 8 * cap].view(torch.int64) for h in self._hk]
+        self._hkeys[me].fill_(-1)
+        shards = self._share([4 * width * cap] * P, "shard", kind=1)
+        self._shards = shards
+        self._views = [s[: 4 * width * cap].view(torch.float32).view(cap, width) for s in shards]
+        self.shard = self._views[me]
+        self.state = torch.zeros(cap, dtype=torch.float32, device=dev) if optimizer == "rowwise_adagrad" else None
+        self.state2 = None
+        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=2)
+        self._neg = None
+        if self.cuda:
+            self._hkey_ptrs = torch.tensor([h.data_ptr() for h in self._hk], dtype=torch.int64, device=dev)
+            self._hval_ptrs = torch.tensor([s.data_ptr() for s in shards], dtype=torch.int64, device=dev)
+        self._register_server(hash_cap=cap, hkeys=self._hkeys[me].data_ptr())
+        self._finish_init()
+
+    def _route_keys(self, keys: torch.Tensor) -> torch.Tensor:
+        from .tables import mix63
+
+        if keys.is_cuda:  # checked at drain (no host round trip per batch)
+            neg = (keys < 0).any()
+            self._neg = neg if self._neg is None else (self._neg | neg)
+        elif bool((keys < 0).any()):
+            raise ValueError("Map-storage keys must be in [0, 2^63)")
+        return mix63(keys)
+
+    def _check_keys(self):
+        if self._neg is not None:
+            neg, self._neg = bool(self._neg), None
+            if neg:
+                raise ValueError("Map-storage keys must be in [0, 2^63)")
+
+    def _gather(self, plan, out):
+        if self.cuda:
+            from .._native import kernels
+
+            kernels().ps_hash_gather(self._hkey_ptrs, self._hval_ptrs, self.bounds, self.capacity, plan.uniq,
+                                     plan.U_dev, self.width, out)
+            return
+        u = plan.uniq[: plan.U].tolist()
+        rows = torch.zeros(len(u), self.width, dtype=torch.float32)
+        for i, k in enumerate(u):
+            o = next(r for r in range(self.comm.world) if self.bounds_list[r] <= k < self.bounds_list[r + 1])
+            s = self._find_cpu(self._hkeys[o], k)
+            if s >= 0:
+                rows[i] = self._views[o][s]
+        out[: plan.U] = rows.to(out.dtype)
+
+    def _find_cpu(self, hk: torch.Tensor, k: int) -> int:
+        cap = self.capacity
+        s = ops._mix64_int(k) & (cap - 1)
+        for _ in range(cap):
+            cur = int(hk[s])
+            if cur == k:
+                return s
+            if cur == -1:
+                return -1
+            s = (s + 1) & (cap - 1)
+        return -1
+
+    def _apply_rows(self, keys, g):
+        slots = torch.empty(keys.numel(), dtype=torch.int64)
+        counters = torch.zeros(2, dtype=torch.int32)
+        ops.hash_slots(self._hkeys[self.comm.rank], keys, slots, self.shard, 0.0, 0, counters)
+        if int(counters[1]):
+            raise RuntimeError(f"one-sided Map-storage table full (capacity {self.capacity})")
+        if self.optimizer == "rowwise_adagrad":
+            ops.sparse_rowwise_adagrad(self.shard, self.state, slots, 0, g, self.lr, self.eps)
+        else:
+            ops.sparse_sgd(self.shard, slots, 0, g, 1.0 if self.optimizer == "add" else -self.lr)
+
+    def size(self) -> int:
+        """Occupied slots of this owner's table."""
+        self.drain()
+        return int((self._hkeys[self.comm.rank] >= 0).sum())
+
+    # -- checkpoint hooks: (key, row, state) of the occupied slots, sorted by key (the collective
+    # HashSparseTable's format, so either transport restores the other's files)
+    def shard_state(self):
+        self.drain()
+        hk = self._hkeys[self.comm.rank]
+        occ = (hk >= 0).nonzero().squeeze(1)
+        keys, order = torch.sort(hk[occ])
+        slots = occ[order]
+        arrays = {"keys": keys.view(-1, 1), "params": self.shard[slots]}
+        if self.state is not None:
+            arrays["state"] = self.state[slots].view(-1, 1)
+        from .tables import MASK63
+
+        meta = dict(global_rows=MASK63, base=0, rows=int(keys.numel()), cols=self.width, clock=self.clock_n,
+                    table_id=self.table_id, rank=self.comm.rank, world=self.comm.world, kind="hash")
+        return meta, arrays
+
+    def restore_range(self):
+        self.ps.pause()  # resumed in finish_restore
+        self._hkeys[self.comm.rank].fill_(-1)
+        self.shard.zero_()
+        if self.state is not None:
+            self.state.zero_()
+        return self.bounds_list[self.comm.rank], self.bounds_list[self.comm.rank + 1]
+
+    def restore_insert(self, chunk: dict):
+        keys = chunk["keys"].reshape(-1).to(self.comm.device)
+        slots = torch.empty(keys.numel(), dtype=torch.int64, device=self.comm.device)
+        counters = torch.zeros(2, dtype=torch.int32, device=self.comm.device)
+        ops.hash_slots(self._hkeys[self.comm.rank], keys, slots, self.shard, 0.0, 0, counters)
+        self.shard[slots] = chunk["params"].to(self.shard.dtype)
+        if self.state is not None and "state" in chunk:
+            self.state[slots] = chunk["state"].reshape(-1).to(self.state.dtype)
 
 
 class AsyncDenseTable(_AsyncTable):
@@ -564,35 +842,38 @@ class AsyncDenseTable(_AsyncTable):
         self.shard = self.n_pad // P
         self.base = me * self.shard
         self.slot_bytes = _align(_SLOT_HEADER + 4 * self.shard, 256)
-        masters = self._share([4 * self.shard] * P, "master")
+        masters = self._share([4 * self.shard] * P, "master", kind=1)
         self._masters = [m[: 4 * self.shard].view(torch.float32) for m in masters]
         self.master = self._masters[me]
         # what peers pull: the bf16 copy the apply writes (half the xGMI bytes), or the fp32 master
         self._pull_bf16 = self.cuda and pull_dtype == torch.bfloat16
         if self._pull_bf16:
-            pulls = self._share([2 * self.shard] * P, "pull")
+            pulls = self._share([2 * self.shard] * P, "pull", kind=1)
             self._pulls = [p[: 2 * self.shard].view(torch.bfloat16) for p in pulls]
         else:
             self._pulls = self._masters
         self.m = torch.zeros(self.shard, dtype=torch.float32, device=dev) if optimizer in ("adam", "adagrad") \
             else None
         self.v = torch.zeros_like(self.m) if optimizer == "adam" else None
-        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox")
+        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=2)
         self.params = torch.zeros(self.n_pad, dtype=pull_dtype, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
-        self._seen = [-1] * P
+        self._seen = [-1] * P          # owner version of the cached copy (sum of its applied clocks)
+        self._seen_applied = [-1] * P  # min over requesters of the owner's applied clocks at that pull
+        self.pulls = 0                 # owner shards pulled so far (lazy-pull accounting)
         self._pending = False
         self.step = 0
         self.cpu_step = 0
         if self.cuda:
             self._inbox_ptrs = torch.tensor([b.data_ptr() for b in self._inbox], dtype=torch.int64, device=dev)
+            self._pull_ptrs = torch.tensor([b.data_ptr() for b in self._pulls], dtype=torch.int64, device=dev)
             self._slot_views = [b for b in self._inbox]
             self.ps.server.add_dense(self.t, _OPT_CODES[optimizer], self.master.data_ptr(),
                                      self.m.data_ptr() if self.m is not None else 0,
                                      self.v.data_ptr() if self.v is not None else 0,
                                      self._pulls[me].data_ptr() if self._pull_bf16 else 0, self.shard, float(lr),
                                      float(betas[0]), float(betas[1]), float(eps), float(weight_decay), 0,
-                                     self._inbox[me].data_ptr(), self.slot_bytes, self.depth)
+                                     self._inbox[me].data_ptr(), self.slot_bytes, self.depth, self.ps.own_lock(self.t))
         else:
             self.ps.server.enable(self.t)
         self._finish_init()
@@ -609,7 +890,10 @@ class AsyncDenseTable(_AsyncTable):
         if self._pull_bf16:
             self._pulls[self.comm.rank].copy_(self.master.to(torch.bfloat16))
         self.params.copy_(flat.to(self.pull_dtype))
-        self._seen = [self.ps.board.owner_version(self.t, o) for o in range(self.comm.world)]
+        board = self.ps.board
+        self._seen = [board.owner_version(self.t, o) for o in range(self.comm.world)]
+        self._seen_applied = [min(board.applied(self.t, o, r) for r in range(self.comm.world))
+                              for o in range(self.comm.world)]
         if self.cuda:
             torch.cuda.synchronize(self.comm.device)
         if self.comm.world > 1:
@@ -620,14 +904,38 @@ class AsyncDenseTable(_AsyncTable):
         return torch.cat([m.to(self.comm.device) for m in self._masters])[: self.n_params].clone()
 
     def get(self, clock: int | None = None) -> torch.Tensor:
-        """Pull the owners' shards that changed since the last pull (SSP-gated)."""
+        """Pull the owners' shards the read needs (SSP-gated). Lazy: with a staleness bound s, an
+        owner's cached copy that already holds every requester's clocks < c - s is served as is
+        (it is as fresh as SSP requires), so a shard is re-pulled about every s clocks instead of
+        every clock; unbounded ASP re-pulls whatever changed. The pull runs under the owners' read
+        locks: every shard is copied between two of its owner's apply batches."""
         self._gate(clock)
-        board = self.ps.board
-        for o in range(self.comm.world):
-            v = board.owner_version(self.t, o)
-            if v != self._seen[o]:
-                self.params[o * self.shard: (o + 1) * self.shard].copy_(self._pulls[o])
-                self._seen[o] = v
+        board, t, P = self.ps.board, self.t, self.comm.world
+        c = self.clock_n if clock is None else int(clock)
+        bound = self.staleness if self.consistency == "ssp" else self.asp_bound
+        need, ver, app = [], {}, {}
+        for o in range(P):
+            v = board.owner_version(t, o)
+            if v == self._seen[o]:
+                continue
+            if bound is not None and self._seen_applied[o] >= c - bound:
+                continue
+            need.append(o)
+            # read BEFORE the copy: what the locked copy holds is at least this new
+            ver[o] = v
+            app[o] = min(board.applied(t, o, r) for r in range(P))
+        if need:
+            with self.ps.read_locked(t):
+                if self.cuda:
+                    from .._native import kernels
+
+                    kernels().ps_pull(self._pull_ptrs, need, self.shard * self.params.element_size(), self.params)
+                else:
+                    for o in need:
+                        self.params[o * self.shard: (o + 1) * self.shard].copy_(self._pulls[o])
+            for o in need:
+                self._seen[o], self._seen_applied[o] = ver[o], app[o]
+            self.pulls += len(need)
         return self.params
 
     def add(self, grad: torch.Tensor | None = None):
@@ -658,11 +966,12 @@ class AsyncDenseTable(_AsyncTable):
     def _apply_slot_cpu(self, r: int, c: int):
         off = (r * self.depth + c % self.depth) * self.slot_bytes
         buf = self._inbox[self.comm.rank]
+        if self.optimizer == "adam":
+            self.cpu_step += 1  # one optimizer step per push, an empty one included (as the GPU applier)
         if int(buf[off: off + 8].view(torch.int64)[0]) == 0:
             return
         g = buf[off + _SLOT_HEADER: off + _SLOT_HEADER + 4 * self.shard].view(torch.float32).clone()
         if self.optimizer == "adam":
-            self.cpu_step += 1
             ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
                            self.weight_decay, self.cpu_step, 1.0, None)
         elif self.optimizer == "adagrad":
@@ -703,5 +1012,6 @@ class AsyncDenseTable(_AsyncTable):
         self.cpu_step = steps
         self.step = int(clock)
         self._seen = [-1] * self.comm.world  # re-pull everything
+        self._seen_applied = [-1] * self.comm.world
         self._restore_clock(clock)
         self.get()

@@ -418,6 +418,11 @@ def main(argv=None):
     generation = int(os.environ.get("MINIPS_GENERATION", "0"))
     hb = Heartbeat(args.heartbeat_dir, rank, args.heartbeat_interval, state_fn=lambda: comm.state()) \
         if args.heartbeat_interval > 0 and args.heartbeat_dir else None
+    if hb is not None:
+        # what this rank can recover from: the supervisor takes the in-place branch only if EVERY
+        # rank can roll back in its process (the one-sided tables cannot: peers hold IPC mappings of
+        # the dead rank's shards and a shared progress board -- the whole set restarts instead)
+        hb.write_caps(inplace=inplace, transport=args.transport)
     if args.model in ("lr", "kmeans") and args.input:
         from .data.loader import LibsvmData
 
@@ -504,6 +509,13 @@ def main(argv=None):
         d = _wait_directive(args.heartbeat_dir, generation)
         generation, world = int(d["generation"]), int(d["world"])
         comm.barrier()
+        ps = getattr(comm, "_async_ps", None)
+        if ps is not None:
+            # one-sided tables: stop this owner's server thread (it holds raw pointers to the shards
+            # and inboxes freed below) and drop the board; build() makes a fresh AsyncPS on the new
+            # group, whose ranks (new ones included) all join its rendezvous
+            ps.close()
+            comm._async_ps = None
         dist.destroy_process_group()
         if rank >= world:
             metrics.fault_tolerance_phase(5, f"rank {rank} retired by the scale to {world} ranks at iteration {it_now}")

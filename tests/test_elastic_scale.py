@@ -17,12 +17,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HB = 0.5
 
 
-def _start(tmp, name, nproc, steps):
+def _start(tmp, name, nproc, steps, train_extra=()):
     run_dir = tmp / f"run_{name}"
     cmd = [sys.executable, "-m", "minips_amd.elastic", "--nproc", str(nproc), "--heartbeat_interval", str(HB),
            "--max_restarts", "1", "--run_dir", str(run_dir), "--log_dir", str(tmp / f"log_{name}"), "--",
            sys.executable, "-m", "minips_amd.train", "--model=widedeep", "--small=1", "--steps", str(steps),
-           "--scale_check_every", "5", f"--checkpoint_file_prefix={tmp}/ck_{name}/"]
+           "--scale_check_every", "5", f"--checkpoint_file_prefix={tmp}/ck_{name}/", *train_extra]
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     return subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True), run_dir
 
@@ -48,10 +48,15 @@ def _summary(logs):
     return json.loads(last[-1])
 
 
-@pytest.mark.parametrize("n0,n1", [(2, 3), (3, 2)])
-def test_live_rescale(tmp_path, n0, n1):
+ONESIDED = ("--transport=onesided", "--consistency=ssp", "--staleness=1")
+
+
+@pytest.mark.parametrize("n0,n1,extra", [(2, 3, ()), (3, 2, ()), (2, 3, ONESIDED)], ids=["2to3", "3to2", "2to3-onesided"])
+def test_live_rescale(tmp_path, n0, n1, extra):
+    """(the one-sided case: the old AsyncPS -- server thread, board, IPC maps -- is closed before
+    the group is left, and the re-formed group, new rank included, builds a fresh one)"""
     steps = 400
-    p, run_dir = _start(tmp_path, f"s{n0}{n1}", n0, steps)
+    p, run_dir = _start(tmp_path, f"s{n0}{n1}", n0, steps, extra)
     try:
         _wait_step(run_dir, 0, 12)
         subprocess.run([sys.executable, "-m", "minips_amd.elastic", "scale", "--run_dir", str(run_dir),

@@ -150,3 +150,30 @@ def test_slow_restore_survives_short_pg_timeout(tmp_path):
     assert second.returncode == 0, second.stderr[-3000:]
     out = json.loads([l for l in second.stdout.splitlines() if l.startswith("{")][-1])
     assert out["start"] == 4 and out["steps"] == 12, out  # the last commit of the first run
+
+
+def test_kill_rank_onesided_restarts_whole_set(tmp_path):
+    """--transport onesided (SSP s=1, owner-side applies over the PS board): rank 1 dies at step 9.
+    The ranks declared that they cannot roll back in place (their peers map the dead rank's shards
+    and share its board), so the supervisor restarts the whole set from the checkpoint committed
+    after iteration 8 -- promptly: the survivors blocked on the dead rank's clocks are stopped, no
+    SSP gate timeout is waited out."""
+    import time
+
+    extra = ["--model=widedeep", "--transport=onesided", "--consistency=ssp", "--staleness=1"]
+    t0 = time.time()
+    got, logs = _run(tmp_path, [*extra, "--fail_rank=1", "--fail_step=9"], "os1", nproc=2, recovery="inplace")
+    took = time.time() - t0
+    assert got.returncode == 0, (got.stderr[-3000:], {k: v[-1500:] for k, v in logs.items()})
+    err = got.stderr
+    assert "rank 1 failed" in err and "cannot roll back in place" in err, err[-3000:]
+    assert "relaunch 2 ranks from the last checkpoint" in err
+    assert "survivors roll back in place" not in err
+    assert sorted(k for k in logs if k.startswith("rank0_")) == ["rank0_attempt0.log", "rank0_attempt1.log"]
+    s = _summary(logs)
+    assert s["start"] == 8 and s["steps"] == 12 and s["generation"] == 1, s
+    assert all(l == l and l < 10 for _, l in s["losses"]), s["losses"]
+    d = re.search(r"\[Fault Tolerance\]\[Phase2\]\[(\d+)\]", err)
+    r = re.search(r"\[Fault Tolerance\]\[Phase3\]\[(\d+)\].*relaunch 2 ranks", err)
+    assert d and r and (int(r.group(1)) - int(d.group(1))) / 1000.0 <= 3 * HB + 10.0, err[-2000:]
+    assert took < 300, took  # no 600 s SSP gate timeout anywhere

@@ -1,0 +1,274 @@
+"""One-sided PS, round-4 additions (minips_amd/ps/onesided.py, csrc/kernels/onesided.hip):
+
+* no torn reads: the owners apply each batch under their write lock and every Get / dense pull
+  runs under the owners' read locks. With the reference's plain add, every apply adds 1.0 to every
+  element of an owner's shard, so each owner's part of any read must hold ONE value (a read that
+  mixes two applies would show two);
+* lazy dense pulls: under SSP s = 2 an owner's shard is re-pulled only when the cached copy is
+  older than the bound allows (fewer pulls than clocks x owners), and the reads stay exact;
+* bf16 rows: the owners' row-wise Adagrad on bf16 rows (fp32 state, stochastic rounding) follows an
+  fp32 replay of the same apply order within bf16 rounding;
+* Map storage: the reference basic app (apps/basic/basic_example.cpp:19-77: SSP s = 1, free-running
+  workers, MapStorage) over AsyncHashTable -- zero bound violations, exact final values;
+* checkpoint: a rank late to pause its server (MINIPS_FAULT_SLOW_PAUSE) cannot let a fast peer's
+  next push into its snapshot (pause barrier).
+CPU ranks: /dev/shm buffers and the board's lock lines; GPU: two processes share cuda:0.
+"""
+import os
+import time
+
+import pytest
+import torch
+
+from test_ps_gloo import run_world
+
+CLOCKS = 24
+
+
+def _torn_run(rank, world, dev, n_params, rows):
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.onesided import AsyncDenseTable, AsyncSparseTable
+
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    comm = Comm(device=dev)
+    dn = AsyncDenseTable(comm, n_params, optimizer="add", consistency="asp", pull_dtype=torch.float32)
+    sp = AsyncSparseTable(comm, num_rows=rows, width=16, optimizer="add", consistency="asp",
+                          pull_dtype=torch.float32, init_std=0.0, route="range", max_keys=rows)
+    keys = torch.arange(rows, device=dev)
+    ones = torch.ones(rows, 16, device=dev)
+    bad, reads = [], 0
+    S = dn.shard
+    for c in range(CLOCKS):
+        p = dn.get().clone()
+        r = sp.get_rows(keys).clone()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        for o in range(world):
+            part = p[o * S: min((o + 1) * S, n_params)]
+            if part.numel() and bool((part != part[0]).any()):
+                bad.append(("dense", c, o, float(part.min()), float(part.max())))
+            lo, hi = sp.bounds_list[o], sp.bounds_list[o + 1]
+            rp = r[lo:hi]
+            if rp.numel() and bool((rp != rp[0, 0]).any()):
+                bad.append(("sparse", c, o, float(rp.min()), float(rp.max())))
+            reads += 2
+        dn.add(torch.ones(n_params, device=dev))
+        dn.clock()
+        sp.add_keys(keys, ones)
+        sp.clock()
+    dn.drain()
+    sp.drain()
+    comm.barrier()
+    final_dense = float(dn.get()[:n_params].min()), float(dn.get()[:n_params].max())
+    final_sparse = float(sp.get_rows(keys).min()), float(sp.get_rows(keys).max())
+    comm.barrier()
+    return bad, reads, final_dense, final_sparse
+
+
+def _check_torn(out, world=2):
+    for rank, (bad, reads, fd, fs) in out.items():
+        assert not bad, (rank, bad[:5])
+        assert reads == 2 * world * CLOCKS
+        assert fd == (world * CLOCKS, world * CLOCKS) and fs == (world * CLOCKS, world * CLOCKS), (rank, fd, fs)
+
+
+def _torn_cpu(rank, world):
+    return _torn_run(rank, world, torch.device("cpu"), 200_000, 512)
+
+
+def test_no_torn_reads_cpu():
+    _check_torn(run_world(_torn_cpu, world=2))
+
+
+def _torn_gpu(rank, world):
+    return _torn_run(rank, world, torch.device("cuda", 0), 8 << 20, 1 << 16)
+
+
+@pytest.mark.gpu
+def test_no_torn_reads_gpu_ipc(dev):
+    """Two processes on cuda:0: the owners' apply batches (write lock kernels, L2 flush on every
+    XCD) and the one-sided gathers / pulls (read lock kernels) never interleave within a shard."""
+    _check_torn(run_world(_torn_gpu, world=2))
+
+
+# ------------------------------------------------------------------------------ lazy pulls
+def _lazy_run(rank, world, dev=torch.device("cpu")):
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.onesided import AsyncDenseTable
+
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    comm = Comm(device=dev)
+    s = 2
+    dn = AsyncDenseTable(comm, 4096, optimizer="add", consistency="ssp", staleness=s, pull_dtype=torch.float32)
+    low = []
+    for c in range(CLOCKS):
+        v = float(dn.get()[0])
+        if v < world * max(0, c - s):  # SSP: every rank's clocks < c - s are in the read
+            low.append((c, v))
+        dn.add(torch.ones(4096, device=dev))
+        dn.clock()
+    dn.drain()
+    comm.barrier()
+    return low, dn.pulls
+
+
+def test_lazy_dense_pulls_cpu():
+    out = run_world(_lazy_run, world=2)
+    for rank, (low, pulls) in out.items():
+        assert not low, (rank, low)
+        assert pulls < CLOCKS * 2 * 0.75, (rank, pulls)  # re-pulled about every s clocks, not every clock
+
+
+# ------------------------------------------------------------------------------ bf16 rows
+BR, BW = 97, 16
+
+
+def _bf16_push(r, c):
+    g = torch.Generator().manual_seed(500 * r + c)
+    return torch.randperm(BR, generator=g)[:24], torch.randn(24, BW, generator=g)
+
+
+def _bf16_run(rank, world, dev=torch.device("cpu")):
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.onesided import AsyncSparseTable
+
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    comm = Comm(device=dev)
+    sp = AsyncSparseTable(comm, num_rows=BR, width=BW, optimizer="rowwise_adagrad", lr=0.05, consistency="asp",
+                          pull_dtype=torch.float32, init_std=0.5, route="range", max_keys=64,
+                          value_dtype=torch.bfloat16, seed=11)
+    init = sp.shard.float().cpu().numpy().copy()
+    sp.ps.server.set_log(True)
+    for c in range(12):
+        keys, rows = _bf16_push(rank, c)
+        sp.add_keys(keys.to(dev), rows.to(dev))
+        sp.clock()
+    sp.drain()
+    comm.barrier()
+    out = dict(log=sp.ps.apply_log(), init=init, shard=sp.shard.float().cpu().numpy().copy(),
+               state=sp.state.cpu().numpy().copy(), base=sp.base, applies=sp._apply_count())
+    comm.barrier()
+    return out
+
+
+def _bf16_check(out, world=2):
+    from minips_amd import ops
+
+    for o, res in out.items():
+        lo = res["base"]
+        shard = torch.from_numpy(res["init"]).clone()
+        state = torch.zeros(shard.shape[0])
+        assert len(res["log"]) == world * 12 and res["applies"] == world * 12
+        for _, r, c in res["log"]:  # fp32 replay of the owner's apply order
+            keys, rows = _bf16_push(r, c)
+            mine = (keys >= lo) & (keys < lo + shard.shape[0])
+            ops.sparse_rowwise_adagrad(shard, state, keys[mine], lo, rows[mine], 0.05, 1e-8)
+        torch.testing.assert_close(torch.from_numpy(res["state"]), state, rtol=1e-5, atol=1e-6)
+        got = torch.from_numpy(res["shard"])
+        # bf16 keeps 8 significant bits; stochastic rounding errs by < 1 ulp per apply, unbiased
+        err = (got - shard).abs()
+        assert float(err.max()) < 0.05 and float(err.mean()) < 0.01, (float(err.max()), float(err.mean()))
+        assert float((got - torch.from_numpy(res["init"])).abs().max()) > 0.05  # the rows moved
+
+
+def test_bf16_rows_owner_apply_cpu():
+    _bf16_check(run_world(_bf16_run, world=2))
+
+
+def _g_bf16(rank, world):
+    return _bf16_run(rank, world, torch.device("cuda", 0))
+
+
+@pytest.mark.gpu
+def test_bf16_rows_owner_apply_gpu_ipc(dev):
+    """HipApplier's bf16 case (row-wise Adagrad, fp32 state, stochastic rounding) against the fp32
+    replay; peers read the bf16 rows with ps_gather_rows_bf16tab."""
+    _bf16_check(run_world(_g_bf16, world=2))
+
+
+# ------------------------------------------------------------------------------ Map storage (basic app)
+class _basic:
+    def __init__(self, workers, iters, max_key, dev="cpu"):
+        self.workers, self.iters, self.max_key, self.dev = workers, iters, max_key, dev
+
+    def __call__(self, rank, world):
+        from minips_amd.apps.basic import run
+        from minips_amd.engine import Engine
+        from minips_amd.ps.comm import Comm
+
+        dev = torch.device(self.dev, 0) if self.dev == "cuda" else torch.device("cpu")
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        eng = Engine(Comm(device=dev))
+        out = run(eng, workers=self.workers, iters=self.iters, max_key=self.max_key, model="ssp", staleness=1,
+                  storage="map", transport="onesided")
+        eng.stop()
+        return out
+
+
+def _basic_check(out, world):
+    for rank, res in out.items():
+        assert res["bound_violations"] == 0, res
+        assert res["final_min"] == res["final_max"] == res["expected"], res
+        assert res["ranks"] == world
+
+
+def test_basic_map_onesided_cpu_1rank():
+    _basic_check(run_world(_basic(4, 8, 64), world=1), 1)
+
+
+def test_basic_map_onesided_cpu_4ranks():
+    _basic_check(run_world(_basic(3, 6, 48), world=4), 4)
+
+
+@pytest.mark.gpu
+def test_basic_map_onesided_gpu(dev):
+    """The reference's 10 free-running SSP(1) workers per rank over one-sided Map storage (one
+    rank; the 4-rank run is the CPU test above)."""
+    _basic_check(run_world(_basic(10, 50, 1000, "cuda"), world=1), 1)
+
+
+# ------------------------------------------------------------------------------ checkpoint pause barrier
+def _pause_run(rank, world, prefix):
+    from minips_amd.ps.checkpoint import Checkpointer
+    from minips_amd.ps.comm import Comm
+    from minips_amd.ps.onesided import AsyncSparseTable
+
+    if rank == 1:
+        os.environ["MINIPS_FAULT_SLOW_PAUSE"] = "1:0.6"  # rank 1 pauses its server late
+    comm = Comm(device=torch.device("cpu"))
+    sp = AsyncSparseTable(comm, num_rows=64, width=4, optimizer="add", consistency="asp", pull_dtype=torch.float32,
+                          init_std=0.0, route="range", max_keys=64)
+    keys = torch.arange(64)
+    for _ in range(5):
+        sp.add_keys(keys, torch.ones(64, 4))
+        sp.clock()
+    ck = Checkpointer(comm, prefix)
+    ck.save({0: sp}, iteration=5, blocking=True)
+    # the fast rank trains on at once: before the fix its next push could land in the late owner's
+    # snapshot
+    sp.add_keys(keys, torch.ones(64, 4))
+    sp.clock()
+    sp.drain()
+    comm.barrier()
+    ck.load({0: sp})
+    v = sp.shard.clone()
+    comm.barrier()
+    return float(v.min()), float(v.max())
+
+
+class _pause_fn:
+    def __init__(self, prefix):
+        self.prefix = prefix
+
+    def __call__(self, rank, world):
+        return _pause_run(rank, world, self.prefix)
+
+
+def test_checkpoint_pause_barrier_cpu(tmp_path):
+    out = run_world(_pause_fn(str(tmp_path) + "/ck_"), world=2)
+    for rank, (lo, hi) in out.items():
+        assert lo == hi == 10.0, (rank, lo, hi)  # 2 ranks x 5 clocks, and nothing of clock 6

@@ -103,19 +103,35 @@ def cmd_gemm(a):
         shapes = [(n, int(m), int(nn), int(k), lay) for n, m, nn, k, lay in (s.split(":") for s in a.shapes.split(","))]
     else:
         shapes = GPT2_SHAPES if a.set == "gpt2" else WD_SHAPES
-    tot = {"ours": 0.0, "hipblaslt": 0.0}
+    # --v4 0,2: the same shapes under several v4 modes (ops.gemm_set_v4_mode), interleaved in one process
+    modes = [int(m) for m in a.v4.split(",")] if a.v4 else [None]
+    from minips_amd._native import kernels
+
+    def with_mode(m, f):
+        if m is None:
+            return f
+
+        def g():
+            kernels().gemm_set_v4_mode(m)
+            f()
+        return g
+
+    names = [f"ours{'' if m is None else f'[v4={m}]'}" for m in modes]
+    tot = {k: 0.0 for k in names + (["hipblaslt"] if a.lib else [])}
     for name, M, N, K, lay in shapes:
         a_km, b_kn = LAYOUTS[lay]
         A, B, C = gemm_operands(M, N, K, lay)
         At, Bt = (A.t() if a_km else A), (B if b_kn else B.t())
-        med = median_rounds({"ours": ours_gemm(A, B, C, M, N, K, lay, a.split),
-                             "hipblaslt": lambda: torch.matmul(At, Bt)})
+        fns = {n: with_mode(m, ours_gemm(A, B, C, M, N, K, lay, a.split)) for n, m in zip(names, modes)}
+        if a.lib:
+            fns["hipblaslt"] = lambda: torch.matmul(At, Bt)
+        med = median_rounds(fns)
         for k in tot:
             tot[k] += med[k]
         fl = 2.0 * M * N * K
-        print(f"{name:10s} M={M:6d} N={N:5d} K={K:6d} {lay}  ours {med['ours']:8.1f}us {fl / med['ours'] / 1e6:7.1f} "
-              f"TF/s | hipBLASLt {med['hipblaslt']:8.1f}us {fl / med['hipblaslt'] / 1e6:7.1f} TF/s", flush=True)
-    print(f"sum: ours {tot['ours']:.1f} us | hipBLASLt {tot['hipblaslt']:.1f} us")
+        cols = " | ".join(f"{k} {med[k]:8.1f}us {fl / med[k] / 1e6:7.1f} TF/s" for k in tot)
+        print(f"{name:10s} M={M:6d} N={N:5d} K={K:6d} {lay}  {cols}", flush=True)
+    print("sum: " + " | ".join(f"{k} {v:.1f} us" for k, v in tot.items()))
 
 
 def cmd_one(a):
@@ -275,6 +291,8 @@ def main(argv=None):
     sub = ap.add_subparsers(dest="cmd", required=True)
     p = sub.add_parser("gemm")
     p.add_argument("--set", default=os.environ.get("GEMM_SET", "wd"), choices=["wd", "gpt2"])
+    p.add_argument("--v4", default="", help="gemm: compare these v4 modes (e.g. 0,2) in one process")
+    p.add_argument("--no-lib", dest="lib", action="store_false", help="gemm: skip the hipBLASLt column")
     p.add_argument("--shapes", default=os.environ.get("GEMM_SHAPES", ""))
     p.add_argument("--split", type=int, default=1, help="split-K of the nt / nn shapes (slab + reduce)")
     p = sub.add_parser("one")
