@@ -593,12 +593,17 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
   auto members = at::empty({n}, o64.dtype(at::kInt)), memrow = at::empty({n}, o64.dtype(at::kInt));
   auto counts = at::empty({P + 1}, o64);
   at::Tensor pos = with_positions ? at::empty({n}, o64.dtype(at::kInt)) : at::Tensor();
+  // one owner: each row's lookup range in member order (the row-parallel embedding backward)
+  at::Tensor rowstart = (with_positions && P == 1) ? at::empty({n + 1}, o64.dtype(at::kInt)) : at::Tensor();
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), col_bits.data_ptr<int32_t>(),
                         (uint64_t)route_mult, (uint64_t)route_n, ptr<int64_t>(bounds), (int)P, ws.data_ptr<int32_t>(),
                         ptr<int64_t>(ukey),
                         ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
-                        ptr<int64_t>(counts), stream_of(keys), with_positions ? pos.data_ptr<int32_t>() : nullptr);
+                        ptr<int64_t>(counts), stream_of(keys), with_positions ? pos.data_ptr<int32_t>() : nullptr,
+                        rowstart.defined() ? rowstart.data_ptr<int32_t>() : nullptr);
+  if (rowstart.defined())
+    return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos, rowstart};
   if (with_positions) return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos};
   return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow};
 }
@@ -643,6 +648,39 @@ void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
 
 // Embedding backward fused with the row-wise Adagrad apply (see kernels.h). members/memrow: the
 // plan's lookup CSR; uniq: the plan's unique keys (memrow indexes it); scr: zeroed scratch.
+// Row-parallel embedding backward + row-wise Adagrad (one rank, row-sorted bf16 gradient rows).
+void emb_rows_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, int64_t F, int64_t D,
+                      const at::Tensor& members, const at::Tensor& rowstart, const at::Tensor& U_dev,
+                      const at::Tensor& uniq, int64_t base, at::Tensor& table, at::Tensor& state,
+                      const c10::optional<at::Tensor>& state2, int64_t D1, double lr, double eps, at::Tensor& ws,
+                      int64_t hot) {
+  check_gpu(dX, "dX");
+  check_dtype(dX, at::kBFloat16, "dX");
+  TORCH_CHECK(dX.is_contiguous() && dX.dim() == 2 && dX.size(1) == D, "dX: [total, D] contiguous (member order)");
+  check_dtype(members, at::kInt, "members");
+  check_dtype(rowstart, at::kInt, "rowstart");
+  check_dtype(table, at::kFloat, "table");
+  check_dtype(state, at::kFloat, "state");
+  check_dtype(ws, at::kInt, "ws");
+  const int64_t U_max = rowstart.numel() - 1;
+  TORCH_CHECK(ws.numel() >= U_max + 1, "ws: >= U + 1 ints");
+  TORCH_CHECK(D == 16 || D == 32 || D == 64, "D in {16, 32, 64}");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && table.size(1) % 4 == 0 && table.size(1) >= D + 1,
+              "table: [rows, W] fp32, W % 4 == 0, W > D");
+  const float* dw = nullptr;
+  if (dwide && dwide->defined()) {
+    check_dtype(*dwide, at::kFloat, "dwide");
+    dw = ptr<float>(*dwide);
+  }
+  float* st2 = (state2 && state2->defined()) ? ptr<float>(*state2) : nullptr;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
+  int* w = ws.data_ptr<int32_t>();
+  minips_k::emb_rows_adagrad(ptr<bf16_t>(dX), dw, (int)F, (int)D, members.data_ptr<int32_t>(),
+                             rowstart.data_ptr<int32_t>(), ptr<int64_t>(U_dev), U_max, ptr<int64_t>(uniq), base,
+                             ptr<float>(table), (int)table.size(1), (int)table.size(1), ptr<float>(state), st2,
+                             (int)D1, (float)lr, (float)eps, w + 1, w, (int)hot, stream_of(dX));
+}
+
 void emb_seg_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, int64_t F, int64_t D,
                      const at::Tensor& members, const at::Tensor& memrow, const at::Tensor& uniq, int64_t base,
                      at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
@@ -1532,6 +1570,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);
+  m.def("emb_rows_adagrad", &emb_rows_adagrad);
   m.def("emb_seg_adagrad", &emb_seg_adagrad);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("cu_masked_stream", &cu_masked_stream);

@@ -177,9 +177,19 @@ void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const i
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
-                 int32_t* pos = nullptr);  // pos (nullable): pos[members[m]] = m (emb_csr_positions fused)
+                 int32_t* pos = nullptr, int32_t* rowstart = nullptr);
+// (pos, nullable: pos[members[m]] = m, emb_csr_positions fused; rowstart, nullable, one owner only:
+// rowstart[u] = first member of row u, rowstart[U] = B*F)
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
 void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s);
+// Embedding backward + row-wise Adagrad of one rank, row-parallel over the row-sorted lookups
+// (dX [total, D] bf16 in member order, rowstart [U + 1] from plan_sorted): rows with at most
+// `hot` lookups are summed and applied by one lane group each; hotter rows are queued (hot_list /
+// hot_count: zeroed by the call) and reduced by a workgroup each.
+void emb_rows_adagrad(const bf16_t* dX, const float* dwide, int F, int D, const int* members, const int* rowstart,
+                      const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base, float* table, int ld,
+                      int W, float* state, float* state2, int D1, float lr, float eps, int* hot_list, int* hot_count,
+                      int hot, hipStream_t s);
 // Embedding backward fused with the row-wise Adagrad apply (one rank, local shard): the rows of
 // uniq[memrow] get Adagrad with the segment sums of their lookups' dX rows (+ dwide at column D)
 // without a grad_rows buffer. scr: [U, scr_ld >= D+1] fp32, all zero before and after the call.

@@ -424,7 +424,8 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
                                                         uint64_t rn, const int32_t* __restrict__ perm,
                                                         int64_t* __restrict__ uniq, int64_t* __restrict__ inv,
                                                         int32_t* __restrict__ members, int32_t* __restrict__ memrow,
-                                                        int64_t* __restrict__ counts, int32_t* __restrict__ pos_out) {
+                                                        int64_t* __restrict__ counts, int32_t* __restrict__ pos_out,
+                                                        int32_t* __restrict__ rowstart) {
   __shared__ int64_t basef[65];
   __shared__ int32_t ucf[64];
   const int t = threadIdx.x;
@@ -444,6 +445,10 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
     members[idx] = (int32_t)j;
     memrow[idx] = (int32_t)u;
     if (pos_out) pos_out[j] = (int32_t)idx;  // the member-order row of lookup j (sorted dgrad rows)
+    if (rowstart) {  // one owner: u's lookups are members [rowstart[u], rowstart[u + 1])
+      if (pos == 0 || local_u[idx - 1] != local_u[idx]) rowstart[u] = (int32_t)idx;
+      if (idx == n - 1) rowstart[U] = (int32_t)n;
+    }
     if (!perm && pos < ucf[c]) uniq[basef[c] + pos] = ps_route(ukey[idx], rmult, rn);
   }
 }
@@ -465,7 +470,8 @@ static int plan_reps(int bit) {
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
-                 int32_t* pos) {
+                 int32_t* pos, int32_t* rowstart) {
+  if (rowstart && P > 1) throw std::runtime_error("plan_sorted: row starts are for one owner");
   if (B < 1 || B > kPsMax) throw std::runtime_error("plan_sorted: 1 <= B <= 16384 rows per column");
   if (F < 1 || F > 64) throw std::runtime_error("plan_sorted: 1 <= F <= 64 columns");
   if (P < 1 || P > kPoMaxP) throw std::runtime_error("plan_sorted: 1 <= P <= 16 owners");
@@ -496,7 +502,8 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
   }
   for (int r = 0; r < plan_reps(4); ++r)
     hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
-                       route_mult, route_n, P > 1 ? perm : nullptr, uniq, inv, members, memrow, counts, pos);
+                       route_mult, route_n, P > 1 ? perm : nullptr, uniq, inv, members, memrow, counts, pos,
+                       rowstart);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -5,6 +5,8 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "common.h"
 #include "kernels.h"
@@ -215,7 +217,8 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
                                                       const bf16_t* __restrict__ w, const bf16_t* __restrict__ b0,
                                                       const float* __restrict__ wide, const float* __restrict__ y,
                                                       bf16_t* __restrict__ dH, float* dw, float* db, float* dwide,
-                                                      float* loss_sum, float* colsum, float scale) {
+                                                      float* loss_sum, float* colsum, float scale,
+                                                      float* __restrict__ slab, unsigned* ticket) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -270,9 +273,14 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
       head_store<PER_LANE>(dH + b * Hd + lane * PER_LANE, gv);
     }
   }
-  // reduce the 4 waves of the block in LDS, then one global atomic per column per block
-  __shared__ float red[2][kHeadWaves][64 * PER_LANE];
+  // reduce the waves of the block in LDS into the block's partial row of the slab; the LAST block
+  // to finish folds every partial row and adds the totals into dw / colsum / db / loss -- one
+  // writer per output instead of (blocks) same-address fp32 atomics per column, which serialise
+  // at the memory side (the head kernel took 24 us in the W&D step that way)
+  constexpr int NC = 64 * PER_LANE, NP = 2 * NC + 2;  // a partial row: dw | colsum | db | loss
+  __shared__ float red[2][kHeadWaves][NC];
   __shared__ float red_s[2][kHeadWaves];
+  __shared__ int last;
   const int wv = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < PER_LANE; ++j) {
@@ -284,15 +292,16 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
     red_s[1][wv] = lossl;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 64 * PER_LANE; c += blockDim.x) {
+  float* row = slab + (int64_t)blockIdx.x * NP;
+  for (int c = threadIdx.x; c < NC; c += blockDim.x) {
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int w = 0; w < kHeadWaves; ++w) {
       a += red[0][w][c];
       b += red[1][w][c];
     }
-    atomicAdd(dw + c, a);
-    if (colsum) atomicAdd(colsum + c, b);
+    row[c] = a;
+    row[NC + c] = b;
   }
   if (threadIdx.x == 0) {
     float a = 0.f, b = 0.f;
@@ -301,8 +310,42 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
       a += red_s[0][w];
       b += red_s[1][w];
     }
-    atomicAdd(db, a);
-    atomicAdd(loss_sum, b);
+    row[2 * NC] = a;
+    row[2 * NC + 1] = b;
+  }
+  // publish (cdna_hip_programming.md Guideline 16): every storing wave drains, the block meets,
+  // one lane releases at agent scope and takes a ticket; the last ticket acquires and reduces
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int c = threadIdx.x; c < NP; c += blockDim.x) {
+    if (c >= NC && c < 2 * NC && !colsum) continue;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int k = 0;
+    for (; k + 3 < (int)gridDim.x; k += 4) {  // 4 independent partial loads in flight
+      a0 += slab[(int64_t)k * NP + c];
+      a1 += slab[(int64_t)(k + 1) * NP + c];
+      a2 += slab[(int64_t)(k + 2) * NP + c];
+      a3 += slab[(int64_t)(k + 3) * NP + c];
+    }
+    for (; k < (int)gridDim.x; ++k) a0 += slab[(int64_t)k * NP + c];
+    const float tot = (a0 + a1) + (a2 + a3);
+    if (c < NC) dw[c] += tot;
+    else if (c < 2 * NC) colsum[c - NC] += tot;
+    else if (c == 2 * NC) *db += tot;
+    else *loss_sum += tot;
   }
 }
 
@@ -311,21 +354,37 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
              float grad_scale, hipStream_t s) {
   if (B <= 0) return;
   const int block = 64 * kHeadWaves;
-  // per-block LDS reduction, then atomics; one block per CU (128 blocks left half the chip idle)
+  // per-block LDS reduction, partial rows, the last block folds them (one block per CU at most)
   static const int max_blocks = [] {
     const char* e = std::getenv("MINIPS_HEAD_BLOCKS");
-    return e ? std::atoi(e) : 256;
+    return e ? std::atoi(e) : 128;
   }();
-  const int grid = (int)std::min<int64_t>(max_blocks, (B + 63) / 64);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(max_blocks, (B + 63) / 64));
+  // the partial slab + ticket of this device: allocated once (zero ticket), before any capture
+  static thread_local std::vector<std::pair<int, void*>> ws_cache;
+  int dev = 0;
+  MINIPS_HIP_CHECK(hipGetDevice(&dev));
+  void* ws = nullptr;
+  for (auto& e : ws_cache)
+    if (e.first == dev) ws = e.second;
+  const size_t slab_bytes = sizeof(float) * 256 * (2 * 512 + 2);
+  if (!ws) {
+    MINIPS_HIP_CHECK(hipMalloc(&ws, slab_bytes + 256));
+    MINIPS_HIP_CHECK(hipMemset(ws, 0, slab_bytes + 256));
+    ws_cache.push_back({dev, ws});
+  }
+  float* slab = static_cast<float*>(ws);
+  unsigned* ticket = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + slab_bytes);
+  if (grid > 256) throw std::runtime_error("wd_head: at most 256 blocks");
   switch (Hd) {
     case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
     case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
     case 64 * 4: hipLaunchKernelGGL(wd_head_kernel<4>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
     case 64 * 8: hipLaunchKernelGGL(wd_head_kernel<8>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
     default: throw std::runtime_error("wd_head: Hd must be 64, 128, 256 or 512, got " + std::to_string(Hd));
   }
   MINIPS_HIP_CHECK(hipGetLastError());
@@ -1100,6 +1159,214 @@ __global__ __launch_bounds__(256) void emb_cut_adagrad_kernel(const int* __restr
     const float s2 = a.state2 ? a.state2[row] : 0.f;
     seg_adagrad_apply<D>(a, row, g, gw, wide, t, tw, s1, s2, l);
   }
+}
+
+// ---------------------------------------------------------------- row-parallel backward + Adagrad
+// One rank, row-sorted gradient rows (the dgrad GEMM's permuted-rows epilogue writes dX[m] = the
+// gradient of lookup members[m], rows grouped by unique row u): row u's lookups are the contiguous
+// rows [rowstart[u], rowstart[u + 1]) of dX. Instead of cutting the lookup stream into fixed pieces
+// (emb_seg_sum / emb_seg_adagrad: a data-dependent flush per row change and fp32 atomics on every
+// row cut by a piece boundary -- 0.9 TB/s, plus a zero-filled grad_rows buffer read back by the
+// Adagrad kernel), each ROW is one unit of work:
+//   cold rows (<= hot lookups, nearly all of them): a group of D/8 lanes sums the row's lookups
+//     with 16-byte bf16 loads (4 lookups in flight per lane), its table row and Adagrad state are
+//     loaded before the sum (independent of it), and the update is written in place -- no
+//     intermediate buffer, no atomics, each row touched once;
+//   hot rows (Zipf heads: up to thousands of lookups) are appended to a list (one atomic per hot
+//   row) and summed by a whole workgroup each (64 lane groups + an LDS reduction), so no wave
+//   waits on a row thousands of lookups long.
+// Semantics of ops.sparse_rowwise_adagrad with state2 for columns [D1, W) (the wide weight + pad).
+struct RowsAdagradArgs {
+  const int64_t* uniq;
+  int64_t base;
+  float* table;
+  int ld, W, D1;
+  float* state;
+  float* state2;
+  float lr, eps;
+};
+
+__device__ __forceinline__ void acc_bf16x8(float (&acc)[8], uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    acc[2 * e] += __uint_as_float(w[e] << 16);
+    acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+  }
+}
+
+// new values of this lane's 8 deep columns (t0, t1) and of the wide column (lane 0 of the group)
+template <int L>
+__device__ __forceinline__ void rows_apply(const RowsAdagradArgs& a, int64_t trow, const float (&g)[8], float gw,
+                                           bool wide, float4 t0, float4 t1, float tw, float st1_old, float st2_old,
+                                           int l, int D) {
+  float sq = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sq += g[e] * g[e];
+  sq = group_sum<L>(sq);
+  const float sqw = group_sum<L>(l == 0 ? gw * gw : 0.f);
+  const bool split = a.D1 < a.W;
+  const float st1 = st1_old + (split ? sq : sq + sqw) / (float)a.D1;
+  const float st2 = split ? st2_old + sqw / (float)(a.W - a.D1) : 0.f;
+  const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
+  float* tr = a.table + trow * (int64_t)a.ld + 8 * l;
+  reinterpret_cast<float4*>(tr)[0] = make_float4(t0.x - s1 * g[0], t0.y - s1 * g[1], t0.z - s1 * g[2], t0.w - s1 * g[3]);
+  reinterpret_cast<float4*>(tr)[1] = make_float4(t1.x - s1 * g[4], t1.y - s1 * g[5], t1.z - s1 * g[6], t1.w - s1 * g[7]);
+  if (l == 0) {
+    if (wide) a.table[trow * (int64_t)a.ld + D] = tw - s2 * gw;
+    a.state[trow] = st1;
+    if (split) a.state2[trow] = st2;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __restrict__ dX,
+                                                               const float* __restrict__ dwide, int F,
+                                                               const int* __restrict__ members,
+                                                               const int* __restrict__ rowstart,
+                                                               const int64_t* __restrict__ U_dev, int64_t U_max,
+                                                               RowsAdagradArgs a, int* __restrict__ hot_list,
+                                                               int* __restrict__ hot_count, int hot) {
+  constexpr int L = D / 8, PER = 64 / L;
+  const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
+  const bool wide = dwide != nullptr;
+  const int64_t U = min(U_max, *U_dev);
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t u0 = wave * PER; u0 < U; u0 += nw * PER) {
+    const int64_t u = u0 + sub;
+    const bool ok = u < U;
+    const int s = ok ? rowstart[u] : 0, e = ok ? rowstart[u + 1] : 0;
+    const bool cold = ok && e - s <= hot;
+    if (ok && !cold && l == 0) hot_list[atomicAdd(hot_count, 1)] = (int)u;
+    // the row's current values and state: independent of the sum, loaded ahead of it
+    const int64_t trow = cold ? a.uniq[u] - a.base : 0;
+    float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0;
+    float tw = 0.f, st1 = 0.f, st2 = 0.f;
+    if (cold) {
+      const float* tr = a.table + trow * (int64_t)a.ld + 8 * l;
+      t0 = reinterpret_cast<const float4*>(tr)[0];
+      t1 = reinterpret_cast<const float4*>(tr)[1];
+      if (wide && l == 0) tw = a.table[trow * (int64_t)a.ld + D];
+      st1 = a.state[trow];
+      if (a.state2) st2 = a.state2[trow];
+    }
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float gw = 0.f;
+    const int end = cold ? e : s;
+    for (int m = s; m < end; m += 4) {
+      uint4 v[4];
+      float w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int mm = m + q;
+        const bool in = mm < end;
+        v[q] = in ? *reinterpret_cast<const uint4*>(dX + (int64_t)mm * D + 8 * l) : make_uint4(0, 0, 0, 0);
+        w[q] = (wide && l == 0 && in) ? dwide[members[mm] / F] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc_bf16x8(g, v[q]);
+        gw += w[q];
+      }
+    }
+    if (cold) rows_apply<L>(a, trow, g, gw, wide, t0, t1, tw, st1, st2, l, D);
+  }
+}
+
+// One workgroup per hot row: 256 / L lane groups stride over the row's lookups, an LDS reduction
+// folds them, and wave 0 applies the update (lane c: column c; lane 0: the wide column).
+template <int D>
+__global__ __launch_bounds__(256) void emb_hot_adagrad_kernel(const bf16_t* __restrict__ dX,
+                                                              const float* __restrict__ dwide, int F,
+                                                              const int* __restrict__ members,
+                                                              const int* __restrict__ rowstart, RowsAdagradArgs a,
+                                                              const int* __restrict__ hot_list,
+                                                              const int* __restrict__ hot_count) {
+  constexpr int L = D / 8, G = 256 / L;
+  __shared__ float red[G][D + 1];
+  const int t = threadIdx.x, g = t / L, l = t % L;
+  const bool wide = dwide != nullptr;
+  const int n = *hot_count;
+  for (int h = blockIdx.x; h < n; h += gridDim.x) {
+    const int u = hot_list[h];
+    const int s = rowstart[u], e = rowstart[u + 1];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float accw = 0.f;
+    for (int m = s + g; m < e; m += 2 * G) {
+      const bool in2 = m + G < e;
+      const uint4 v0 = *reinterpret_cast<const uint4*>(dX + (int64_t)m * D + 8 * l);
+      const uint4 v1 = in2 ? *reinterpret_cast<const uint4*>(dX + (int64_t)(m + G) * D + 8 * l) : make_uint4(0, 0, 0, 0);
+      if (wide && l == 0) {
+        accw += dwide[members[m] / F];
+        if (in2) accw += dwide[members[m + G] / F];
+      }
+      acc_bf16x8(acc, v0);
+      acc_bf16x8(acc, v1);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[g][8 * l + q] = acc[q];
+    if (l == 0) red[g][D] = accw;
+    __syncthreads();
+    if (t < 64) {  // wave 0: lane c < D folds column c, lane 0 also the wide column
+      float v = 0.f, vw = 0.f;
+      if (t < D)
+        for (int k = 0; k < G; ++k) v += red[k][t];
+      if (t == 0 && wide)
+        for (int k = 0; k < G; ++k) vw += red[k][D];
+      vw = __shfl(vw, 0, 64);
+      const float sq = warp_sum(t < D ? v * v : 0.f);
+      const float sqw = wide ? vw * vw : 0.f;
+      const int64_t trow = a.uniq[u] - a.base;
+      const bool split = a.D1 < a.W;
+      const float st1 = a.state[trow] + (split ? sq : sq + sqw) / (float)a.D1;
+      const float st2 = split ? a.state2[trow] + sqw / (float)(a.W - a.D1) : 0.f;
+      const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
+      float* tr = a.table + trow * (int64_t)a.ld;
+      if (t < D) tr[t] -= s1 * v;
+      if (t == 0 && wide) tr[D] -= s2 * vw;
+      if (t == 0) {
+        a.state[trow] = st1;
+        if (split) a.state2[trow] = st2;
+      }
+    }
+    __syncthreads();  // red is reused by the next hot row
+  }
+}
+
+void emb_rows_adagrad(const bf16_t* dX, const float* dwide, int F, int D, const int* members, const int* rowstart,
+                      const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base, float* table, int ld,
+                      int W, float* state, float* state2, int D1, float lr, float eps, int* hot_list, int* hot_count,
+                      int hot, hipStream_t s) {
+  if (U_max <= 0) return;
+  if (ld % 4 || reinterpret_cast<uintptr_t>(table) % 16 || reinterpret_cast<uintptr_t>(dX) % 16)
+    throw std::runtime_error("emb_rows_adagrad: 16-byte aligned rows");
+  if (D1 <= 0 || D1 > W) D1 = W;
+  if (D1 < W && !state2) throw std::runtime_error("emb_rows_adagrad: split rows need state2");
+  const RowsAdagradArgs a{uniq, base, table, ld, W, D1, state, state2, lr, eps};
+  MINIPS_HIP_CHECK(hipMemsetAsync(hot_count, 0, sizeof(int), s));
+  const int per_block = 4 * (64 / (D / 8));
+  const int grid = (int)std::min<int64_t>((U_max + per_block - 1) / per_block, 8192);
+#define MINIPS_ROWS_ADA(DD)                                                                                      \
+  hipLaunchKernelGGL((emb_rows_adagrad_kernel<DD>), grid, 256, 0, s, dX, dwide, F, members, rowstart, U_dev,     \
+                     U_max, a, hot_list, hot_count, hot);                                                         \
+  hipLaunchKernelGGL((emb_hot_adagrad_kernel<DD>), 256, 256, 0, s, dX, dwide, F, members, rowstart, a, hot_list, \
+                     hot_count);
+  switch (D) {
+    case 16:
+      MINIPS_ROWS_ADA(16)
+      break;
+    case 32:
+      MINIPS_ROWS_ADA(32)
+      break;
+    case 64:
+      MINIPS_ROWS_ADA(64)
+      break;
+    default:
+      throw std::runtime_error("emb_rows_adagrad: D must be 16, 32 or 64");
+  }
+#undef MINIPS_ROWS_ADA
+  MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,

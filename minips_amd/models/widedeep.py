@@ -302,7 +302,7 @@ class WideDeep(LookaheadPlans):
         # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
-        sorted_rows = plan.csr is not None and len(plan.csr) == 3
+        sorted_rows = plan.csr is not None and len(plan.csr) >= 3  # (members, memrow, positions[, rowstart])
         if sorted_rows:
             ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"].view(B * F, D),
                              perm=plan.csr[2], seg=D)

@@ -313,6 +313,11 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
         pos = torch.empty(B * F, dtype=torch.int32)
         pos[order] = torch.arange(B * F, dtype=torch.int32)
         res = res + (pos,)
+        if P == 1:  # row u's lookups are members [rowstart[u], rowstart[u + 1])
+            rs = torch.full((B * F + 1,), B * F, dtype=torch.int32)
+            rs[0] = 0
+            rs[1: U + 1] = torch.cumsum(torch.bincount(inv_u, minlength=U), 0).to(torch.int32)
+            res = res + (rs,)
     return res
 
 
@@ -556,6 +561,30 @@ def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=No
     if dwide is not None:
         grad_rows[:, D].index_add_(0, inv, dwide.repeat_interleave(F))
     return grad_rows
+
+
+def emb_rows_adagrad(dX, dwide, F, D, csr, U_dev, uniq, base, table, state, state2, split, lr, eps, ws, hot=32):
+    """Row-parallel embedding backward + row-wise Adagrad of one rank (widedeep.hip): dX [total, D]
+    bf16 holds the lookups' gradient rows in member order (csr = (members, memrow, positions,
+    rowstart) of plan_sorted), row u sums rows [rowstart[u], rowstart[u+1]) (+ dwide of their
+    samples at column D) and gets sparse_rowwise_adagrad in place. ``ws``: int32 [>= len(rowstart)]
+    (the hot-row list)."""
+    W = table.shape[1]
+    D1 = W if split is None else split
+    members, rowstart = csr[0], csr[3]
+    if _gpu(dX):
+        kernels().emb_rows_adagrad(dX, dwide, int(F), int(D), members, rowstart, U_dev, uniq, int(base), table, state,
+                                   state2, int(D1), float(lr), float(eps), ws, int(hot))
+        return
+    U = int(U_dev.reshape(-1)[0])
+    inv = torch.empty(dX.shape[0], dtype=torch.int64)
+    inv[members.long()] = csr[1].long()
+    un = torch.empty_like(dX)
+    un[members.long()] = dX
+    grad_rows = torch.zeros(max(U, 1), W, dtype=torch.float32)
+    wd_emb_backward(un.reshape(-1, F * D).float(), dwide, inv, F, D, grad_rows)
+    sparse_rowwise_adagrad(table, state, uniq[:U], base, grad_rows[:U], lr, eps, state2=state2,
+                           split=None if D1 == W else D1)
 
 
 def emb_seg_adagrad(dX, dwide, F, D, csr, uniq, U, base, table, state, state2, split, lr, eps, scratch):

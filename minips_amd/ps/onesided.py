@@ -55,6 +55,13 @@ from .tables import SparsePlan, SparseTable, _PendingPlan, column_spec, even_bou
 
 _MAX_TABLES = 16
 _SLOT_HEADER = 64
+# memory kind of the buffers peers read while their owner writes (shards, pull copies): 0
+# coarse-grained + the explicit release (ps_write_unlock: every XCD's L2 written back) / acquire
+# (the gathers' L2 invalidate) of onesided.hip, 1 fine-grained. Inboxes are always uncached, the
+# lock lines always fine-grained.
+_SHARD_MEM = int(os.environ.get("MINIPS_PS_SHARD_MEM", "0"))
+# MINIPS_PS_LOCKS=0: no owner locks (A/B timing only: reads may see half of a batch)
+_LOCKS = os.environ.get("MINIPS_PS_LOCKS", "1") != "0"
 
 
 def _align(n: int, a: int) -> int:
@@ -160,7 +167,7 @@ class AsyncPS:
     # -- the owners' reader / writer locks ----------------------------------------------------
     def own_lock(self, t: int) -> int:
         """Device address of this owner's lock word of table t (0 on CPU ranks: board locks)."""
-        return self.ctrl[self.rank].data_ptr() + t * self._line if self.cuda else 0
+        return self.ctrl[self.rank].data_ptr() + t * self._line if self.cuda and _LOCKS else 0
 
     def _lock_tensor(self, t: int) -> torch.Tensor:
         lt = self._locks.get(t)
@@ -173,7 +180,9 @@ class AsyncPS:
     def read_locked(self, t: int):
         """Every owner's read lock of table t around the enclosed reads (GPU: taken and released by
         kernels on the current stream, around the read kernels issued inside)."""
-        if self.cuda:
+        if self.cuda and not _LOCKS:
+            yield
+        elif self.cuda:
             from .._native import kernels
 
             k = kernels()
@@ -265,9 +274,8 @@ class _AsyncTable:
     # -- shared buffers ---------------------------------------------------------------------
     def _share(self, nbytes: list, tag: str, kind: int = 1) -> list:
         """One buffer per rank (rank r's of nbytes[r] bytes, zero-filled), every one mapped here:
-        uint8 tensors [P]. GPU: hipExtMallocWithFlags + IPC handles -- ``kind`` 1 fine-grained
-        (shards, pull copies: read by peers while the owner writes), 2 uncached (inboxes: written by
-        peers); CPU: /dev/shm files."""
+        uint8 tensors [P]. GPU: IPC handles of ipc_alloc memory -- ``kind`` 0 coarse-grained, 1
+        fine-grained, 2 uncached (inboxes: written by peers); CPU: /dev/shm files."""
         comm, me = self.comm, self.comm.rank
         if self.cuda:
             from .._native import kernels
@@ -427,7 +435,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         self.cap = _align(max(2, int(max_keys)), 2)
         self.slot_bytes = _align(_SLOT_HEADER + self.cap * (8 + 4 * width), 256)
         esz = 2 if value_dtype == torch.bfloat16 else 4
-        shards = self._share([esz * width * n for n in rows_of], "shard", kind=1)
+        shards = self._share([esz * width * n for n in rows_of], "shard", kind=_SHARD_MEM)
         self._shards = shards
         self._views = [s[: esz * width * n].view(value_dtype).view(n, width) for s, n in zip(shards, rows_of)]
         self.shard = self._views[me]
@@ -702,10 +710,10 @@ class AsyncHashTable(AsyncSparseTable):
         self.rows_local = cap
         self.cap = _align(max(2, int(max_keys)), 2)
         self.slot_bytes = _align(_SLOT_HEADER + self.cap * (8 + 4 * width), 256)
-        self._hk = self._share([8 * cap] * P, "hkeys", kind=1)
+        self._hk = self._share([8 * cap] * P, "hkeys", kind=_SHARD_MEM)
         self._hkeys = [h[: 8 * cap].view(torch.int64) for h in self._hk]
         self._hkeys[me].fill_(-1)
-        shards = self._share([4 * width * cap] * P, "shard", kind=1)
+        shards = self._share([4 * width * cap] * P, "shard", kind=_SHARD_MEM)
         self._shards = shards
         self._views = [s[: 4 * width * cap].view(torch.float32).view(cap, width) for s in shards]
         self.shard = self._views[me]
@@ -842,13 +850,13 @@ class AsyncDenseTable(_AsyncTable):
         self.shard = self.n_pad // P
         self.base = me * self.shard
         self.slot_bytes = _align(_SLOT_HEADER + 4 * self.shard, 256)
-        masters = self._share([4 * self.shard] * P, "master", kind=1)
+        masters = self._share([4 * self.shard] * P, "master", kind=_SHARD_MEM)
         self._masters = [m[: 4 * self.shard].view(torch.float32) for m in masters]
         self.master = self._masters[me]
         # what peers pull: the bf16 copy the apply writes (half the xGMI bytes), or the fp32 master
         self._pull_bf16 = self.cuda and pull_dtype == torch.bfloat16
         if self._pull_bf16:
-            pulls = self._share([2 * self.shard] * P, "pull", kind=1)
+            pulls = self._share([2 * self.shard] * P, "pull", kind=_SHARD_MEM)
             self._pulls = [p[: 2 * self.shard].view(torch.bfloat16) for p in pulls]
         else:
             self._pulls = self._masters

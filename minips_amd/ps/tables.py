@@ -512,6 +512,9 @@ def _route_multiplier(num_rows: int) -> int:
 # the dedupe counts each unique key's lookups for the embedding-backward CSR (one pass less);
 # MINIPS_CSR_FUSED=0 counts in emb_build_csr instead
 _CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
+# MINIPS_ROWS_ADAGRAD=0: keep the piecewise segment sum + separate Adagrad for row-sorted pushes
+# of one rank instead of the row-parallel fused apply (ops.emb_rows_adagrad)
+_ROWS_ADAGRAD = __import__("os").environ.get("MINIPS_ROWS_ADAGRAD", "1") == "1"
 # MINIPS_SORTED_EMB=1: plans carry the CSR's inverse permutation (csr[2]: each lookup's row in
 # member order) so the embedding dgrad writes its output pre-sorted and the backward streams it
 # contiguously instead of gathering 64-byte pieces. Measured on one MI355X (W&D step, 3 x 400
@@ -578,10 +581,11 @@ _FUSED_ASSEMBLE = os.environ.get("MINIPS_FUSED_ASSEMBLE", "1") == "1"
 class _LookupGrads:
     """A push in lookup form (SparseTable.add_lookup_grads): dX [B, >= F*D] holds one gradient
     row per lookup (b, f) at columns f*D.., dwide [B] the sample's wide-column gradient."""
-    __slots__ = ("dX", "dwide", "F", "D")
+    __slots__ = ("dX", "dwide", "F", "D", "sorted")
 
-    def __init__(self, dX, dwide, F, D):
+    def __init__(self, dX, dwide, F, D, sorted_rows=False):
         self.dX, self.dwide, self.F, self.D = dX, dwide, F, D
+        self.sorted = sorted_rows  # dX [B*F, D] in the CSR's member order (row-parallel apply)
 
 
 class _PendingPlan:
@@ -954,6 +958,12 @@ class SparseTable:
         if not sorted_rows and self._fused_lookup_ok(plan, dX, dwide, D, x_off):
             self._pending.append((plan, _LookupGrads(dX[:, x_off:] if x_off else dX, dwide, F, D)))
             return
+        if (sorted_rows and _ROWS_ADAGRAD and plan.csr is not None and len(plan.csr) >= 4 and dX.dtype == torch.bfloat16
+                and x_off == 0 and self._fused_lookup_ok(plan, dX, dwide, D, 0)):
+            # one rank, row-sorted gradient rows: each unique row sums its lookups and is updated in
+            # place (ops.emb_rows_adagrad) -- no grad_rows buffer, no zero fill, no atomics
+            self._pending.append((plan, _LookupGrads(dX, dwide, F, D, sorted_rows=True)))
+            return
         dev = self.comm.device
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width,
                                                                          dtype=torch.float32, device=dev)
@@ -998,6 +1008,16 @@ class SparseTable:
 
     def _push(self, plan: SparsePlan, grad_rows):
         dev = self.comm.device
+        if isinstance(grad_rows, _LookupGrads) and grad_rows.sorted:  # one rank, row-parallel
+            lg = grad_rows
+            n = plan.csr[3].numel()
+            ws = getattr(self, "_rows_ws", None)
+            if ws is None or ws.numel() < n:
+                ws = self._rows_ws = torch.empty(n, dtype=torch.int32, device=dev)
+            U_dev = plan.U_dev if plan.U_dev is not None else torch.tensor([plan.cap], dtype=torch.int64, device=dev)
+            ops.emb_rows_adagrad(lg.dX, lg.dwide, lg.F, lg.D, plan.csr, U_dev, plan.uniq, self.base, self.shard,
+                                 self.state, self.state2, self.split, self.lr, self.eps, ws)
+            return
         if isinstance(grad_rows, _LookupGrads):  # one rank, fused reduction + apply
             lg = grad_rows
             ops.emb_seg_adagrad(lg.dX, lg.dwide, lg.F, lg.D, plan.csr, plan.uniq, plan.cap, self.base, self.shard,

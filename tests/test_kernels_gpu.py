@@ -508,6 +508,50 @@ def test_fused_emb_backward_adagrad(dev, D, wide, split, dtype):
         assert int(scr.count_nonzero()) == 0
 
 
+@pytest.mark.parametrize("D,wide,split", [(32, True, True), (16, False, False), (64, True, True)])
+def test_rows_emb_backward_adagrad(dev, D, wide, split):
+    """ops.emb_rows_adagrad (row-parallel backward + row-wise Adagrad over the row-sorted bf16
+    gradient rows of plan_sorted) against the CPU reference of the separate ops, two steps: cold
+    rows, Zipf-hot rows of thousands of lookups (the workgroup-per-row path), single lookups."""
+    g = torch.Generator().manual_seed(D + 3 * wide)
+    B, F = 8192, 6
+    cards = [40000, 5, 3000, 700, 2, 20000]
+    base = torch.tensor([sum(cards[:f]) for f in range(F)], dtype=torch.int64)
+    bits = [max(1, (c - 1).bit_length()) for c in cards]
+    R = sum(cards)
+    W = D + 4
+    table = torch.randn(R, W, generator=g)
+    state = torch.rand(R, generator=g)
+    state2 = torch.rand(R, generator=g) if split else None
+    t_gpu, s_gpu = table.to(dev), state.to(dev)
+    s2_gpu = state2.to(dev) if split else None
+    t_ref, s_ref = table.clone(), state.clone()
+    s2_ref = state2.clone() if split else None
+    ws = torch.empty(B * F + 1, dtype=torch.int32, device=dev)
+    for step in range(2):
+        keys = torch.stack([torch.randint(0, c, (B,), generator=g) for c in cards], 1) + base
+        keys[:3000, 2] = base[2] + 17 + step  # a hot row: 3000 lookups
+        res = ops.plan_sorted(keys.to(dev), base.to(dev), bits, positions=True)
+        uniq, inv, counts, U_dev = res[:4]
+        csr = tuple(res[4:])
+        assert len(csr) == 4
+        lookups = torch.randn(B * F, D, generator=g).to(torch.bfloat16)  # lookup order
+        pos = csr[2].cpu().long()
+        dX = torch.empty_like(lookups)
+        dX[pos] = lookups  # member order: row m = lookup members[m]
+        dwide = torch.randn(B, generator=g) if wide else None
+        ops.emb_rows_adagrad(dX.to(dev), dwide.to(dev) if wide else None, F, D, csr, U_dev, uniq, 0, t_gpu, s_gpu,
+                             s2_gpu, D if split else None, 0.05, 1e-8, ws)
+        cres = ops.plan_sorted(keys, base, bits, positions=True)
+        ccsr = tuple(cres[4:])
+        ops.emb_rows_adagrad(lookups[ccsr[0].long()].float().to(torch.bfloat16), dwide, F, D, ccsr, cres[3],
+                             cres[0], 0, t_ref, s_ref, s2_ref, D if split else None, 0.05, 1e-8, None)
+        torch.testing.assert_close(t_gpu.cpu(), t_ref, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(s_gpu.cpu(), s_ref, rtol=1e-4, atol=1e-5)
+        if split:
+            torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-4, atol=1e-5)
+
+
 def test_colsum_bf16(dev):
     """ops.colsum_add (bias gradient of a Linear) against the fp32 column sums."""
     g = torch.Generator().manual_seed(11)

@@ -85,6 +85,18 @@ def trace(a):
     for n, t in per_k.most_common(a.top):
         c = calls[n]
         print(f"{t / steps / 1e6:9.4f} {c / steps:10.2f} {t / c / 1e3:8.1f}  {n}")
+    if a.timeline:
+        # one steady step, kernel by kernel: start offset and duration per queue, and the idle gap of
+        # each queue before the kernel -- what the critical path waits on
+        t0, t1 = anchors[a.skip + 1], anchors[a.skip + 2]
+        print(f"\ntimeline of one step ({(t1 - t0) / 1e3:.1f} us), anchor {a.anchor}: start_us dur_us gap_us queue kernel")
+        last_end = {}
+        for s, e, n, q in ks:
+            if s < t0 or s >= t1:
+                continue
+            gap = (s - last_end[q]) / 1e3 if q in last_end else 0.0
+            last_end[q] = e
+            print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {gap:7.1f}  q{q}  {n.split('(')[0][:90]}")
 
 
 
@@ -104,6 +116,7 @@ def main(argv=None):
     p.add_argument("--anchor", default="adam_kernel")
     p.add_argument("--skip", type=int, default=3)
     p.add_argument("--top", type=int, default=30)
+    p.add_argument("--timeline", action="store_true", help="also list one steady step kernel by kernel")
     a = ap.parse_args(argv)
     if a.cmd == "stats":
         stats(a.path, a.steps, a.top)
