@@ -39,6 +39,12 @@ def main():
     ap.add_argument("--test-cards", default="", help=argparse.SUPPRESS)
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed run: host issue time per step and a cProfile of N more steps (stderr)")
+    ap.add_argument("--bucket_mb", type=float, default=2.0,
+                    help="several ranks: dense-clock bucket size in MB (layers merged from the last one; 0 = one "
+                         "reduce-scatter + all-gather after the backward)")
+    ap.add_argument("--diag-steps", type=int, default=None,
+                    help="after the timed run: N more steps with per-collective timing and the host-sync audit, "
+                         "reported in the JSON line under 'diag' (default 10 with several ranks, else 0)")
     ap.add_argument("--sync-audit", type=int, default=0,
                     help="after the timed run: N more steps under minips_amd.utils.syncaudit (host issue time, "
                          "host syncs per step and their call sites; one '[sync-audit] {json}' line per rank, stderr)")
@@ -58,7 +64,7 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    cfg = WideDeepConfig(consistency=args.consistency, staleness=args.staleness)
+    cfg = WideDeepConfig(consistency=args.consistency, staleness=args.staleness, bucket_mb=args.bucket_mb)
     if args.test_cards:  # CPU/gloo plumbing tests only: a small table, NOT the benchmark config
         cfg.cards = [int(c) for c in args.test_cards.split(",")]
     model = WideDeep(cfg, comm)
@@ -113,6 +119,33 @@ def main():
     loss_last = float(l.item()) / args.batch
     samples = args.batch * n * args.steps
     value = samples / elapsed
+    # diagnostics AFTER the timed region (the timed steps ran without any of this): bytes and
+    # achieved GB/s per collective kind, host issue time and host syncs per step -- so a multi-GPU
+    # run explains its own number (comm-bound vs host-bound vs compute-bound)
+    diag_steps = args.diag_steps if args.diag_steps is not None else (10 if n > 1 else 0)
+    diag = None
+    if diag_steps > 0:
+        from minips_amd.utils.syncaudit import SyncAudit
+
+        comm.timing = []
+        t1 = time.perf_counter()
+        with SyncAudit() as audit:
+            for _ in range(diag_steps):
+                audit.step_begin()
+                step()
+                audit.step_end()
+        model.drain()
+        sync()
+        wall = time.perf_counter() - t1
+        rep = audit.report(wall)
+        diag = dict(steps=diag_steps, wall_ms_per_step=rep["wall_ms_per_step"],
+                    host_issue_ms_per_step=rep["host_issue_ms_median"], host_syncs_per_step=rep["syncs_per_step"],
+                    collectives=comm.timing_report(diag_steps))
+        comm.timing = None
+        if n > 1:  # rank 0 reports the slowest rank's host issue time
+            hi = torch.tensor([rep["host_issue_ms_median"]], dtype=torch.float64, device=dev)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            diag["host_issue_ms_per_step_max_rank"] = round(float(hi.item()), 4)
     if n == 1:
         # one rank owns every shard: Get/Add/Clock are local gathers/applies, no collective runs
         parallelism = f"ps-dp1 ({args.consistency}; single rank: local shards, no collectives)"
@@ -145,10 +178,13 @@ def main():
                 "hip_graph": use_graph,
                 "world_size": comm.world,
                 "backend": comm.backend,
+                "bucket_mb": args.bucket_mb if n > 1 else None,
             },
             "loss_first": round(loss0, 5) if loss0 is not None else None,
             "loss_last": round(loss_last, 5),
         }
+        if diag is not None:
+            out["diag"] = diag
         print(json.dumps(out), flush=True)
     if args.sync_audit > 0:  # after the timed region: host issue time + host waits per step
         from minips_amd.utils.syncaudit import SyncAudit

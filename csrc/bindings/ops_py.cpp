@@ -594,7 +594,7 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
   auto counts = at::empty({P + 1}, o64);
   at::Tensor pos = with_positions ? at::empty({n}, o64.dtype(at::kInt)) : at::Tensor();
   // one owner: each row's lookup range in member order (the row-parallel embedding backward)
-  at::Tensor rowstart = (with_positions && P == 1) ? at::empty({n + 1}, o64.dtype(at::kInt)) : at::Tensor();
+  at::Tensor rowstart = P == 1 ? at::empty({n + 1}, o64.dtype(at::kInt)) : at::Tensor();
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), col_bits.data_ptr<int32_t>(),
                         (uint64_t)route_mult, (uint64_t)route_n, ptr<int64_t>(bounds), (int)P, ws.data_ptr<int32_t>(),
@@ -602,6 +602,7 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
                         ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
                         ptr<int64_t>(counts), stream_of(keys), with_positions ? pos.data_ptr<int32_t>() : nullptr,
                         rowstart.defined() ? rowstart.data_ptr<int32_t>() : nullptr);
+  // (members, memrow, positions or None, rowstart) with one owner
   if (rowstart.defined())
     return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos, rowstart};
   if (with_positions) return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos};
@@ -653,10 +654,15 @@ void emb_rows_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwi
                       const at::Tensor& members, const at::Tensor& rowstart, const at::Tensor& U_dev,
                       const at::Tensor& uniq, int64_t base, at::Tensor& table, at::Tensor& state,
                       const c10::optional<at::Tensor>& state2, int64_t D1, double lr, double eps, at::Tensor& ws,
-                      int64_t hot) {
+                      int64_t hot, bool sorted_rows) {
   check_gpu(dX, "dX");
   check_dtype(dX, at::kBFloat16, "dX");
-  TORCH_CHECK(dX.is_contiguous() && dX.dim() == 2 && dX.size(1) == D, "dX: [total, D] contiguous (member order)");
+  TORCH_CHECK(dX.dim() == 2 && dX.stride(1) == 1 && dX.stride(0) % 8 == 0, "dX: 2-D, 16-byte aligned rows");
+  if (sorted_rows) {
+    TORCH_CHECK(dX.size(1) == D && dX.stride(0) == D, "dX: [total, D] contiguous (member order)");
+  } else {
+    TORCH_CHECK(dX.size(1) >= F * D && dX.size(0) * F == members.numel(), "dX: [B, >= F*D] (lookup order)");
+  }
   check_dtype(members, at::kInt, "members");
   check_dtype(rowstart, at::kInt, "rowstart");
   check_dtype(table, at::kFloat, "table");
@@ -675,10 +681,11 @@ void emb_rows_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwi
   float* st2 = (state2 && state2->defined()) ? ptr<float>(*state2) : nullptr;
   c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
   int* w = ws.data_ptr<int32_t>();
-  minips_k::emb_rows_adagrad(ptr<bf16_t>(dX), dw, (int)F, (int)D, members.data_ptr<int32_t>(),
-                             rowstart.data_ptr<int32_t>(), ptr<int64_t>(U_dev), U_max, ptr<int64_t>(uniq), base,
-                             ptr<float>(table), (int)table.size(1), (int)table.size(1), ptr<float>(state), st2,
-                             (int)D1, (float)lr, (float)eps, w + 1, w, (int)hot, stream_of(dX));
+  minips_k::emb_rows_adagrad(ptr<bf16_t>(dX), sorted_rows ? 0 : (int)dX.stride(0), dw, (int)F, (int)D,
+                             members.data_ptr<int32_t>(), rowstart.data_ptr<int32_t>(), ptr<int64_t>(U_dev), U_max,
+                             ptr<int64_t>(uniq), base, ptr<float>(table), (int)table.size(1), (int)table.size(1),
+                             ptr<float>(state), st2, (int)D1, (float)lr, (float)eps, w + 1, w, (int)hot,
+                             stream_of(dX));
 }
 
 void emb_seg_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, int64_t F, int64_t D,

@@ -32,7 +32,10 @@ __device__ __forceinline__ uint32_t sr_hash(uint64_t row, uint32_t col, uint32_t
 __device__ __forceinline__ bf16_t bf16_sr(float v, uint32_t rnd) {
   const uint32_t b = __float_as_uint(v);
   if ((b & 0x7f800000u) == 0x7f800000u) return (bf16_t)(b >> 16);  // inf / nan unchanged
-  return (bf16_t)((b + (rnd & 0xffffu)) >> 16);
+  const uint32_t r = b + (rnd & 0xffffu);
+  // a finite value never rounds up to inf: it saturates at the largest finite bf16 of its sign
+  if ((r & 0x7f800000u) == 0x7f800000u) return (bf16_t)(((b >> 16) & 0x8000u) | 0x7f7fu);
+  return (bf16_t)(r >> 16);
 }
 
 // 8 bf16 per lane (16-byte loads), D/8 lanes per row, rows grid-strided.

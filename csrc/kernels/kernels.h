@@ -186,7 +186,9 @@ void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStrea
 // (dX [total, D] bf16 in member order, rowstart [U + 1] from plan_sorted): rows with at most
 // `hot` lookups are summed and applied by one lane group each; hotter rows are queued (hot_list /
 // hot_count: zeroed by the call) and reduced by a workgroup each.
-void emb_rows_adagrad(const bf16_t* dX, const float* dwide, int F, int D, const int* members, const int* rowstart,
+// ldx: 0 = dX row-sorted [total, D] (member order); > 0 = lookup order [B, ldx >= F*D].
+void emb_rows_adagrad(const bf16_t* dX, int ldx, const float* dwide, int F, int D, const int* members,
+                      const int* rowstart,
                       const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base, float* table, int ld,
                       int W, float* state, float* state2, int D1, float lr, float eps, int* hot_list, int* hot_count,
                       int hot, hipStream_t s);

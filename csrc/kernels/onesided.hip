@@ -28,9 +28,10 @@
 //     HBM, never an L2 copy of the slot from `depth` clocks ago); shards, pull copies and the
 //     control lines are FINE-GRAINED (hipDeviceMallocFinegrained: coherent for peer access and
 //     system-scope atomics);
-//   * push: every block of ps_push_rows drains its stores (vmcnt(0)), meets at a barrier and
-//     issues a system-scope release (__threadfence_system) before it exits; the requester's
-//     publisher thread bumps `sent` only after the push kernels completed (an event);
+//   * push: ps_push_rows is followed on its stream by a 64-workgroup system-scope release
+//     (fence_l2: one write-back per XCD L2, after the push's stores drained at its kernel
+//     boundary); the requester's publisher thread bumps `sent` only after both completed (an
+//     event);
 //   * apply: the owner's server thread brackets each table's applies of a batch with
 //     ps_write_lock / ps_write_unlock on its apply stream. The lock word (one per table, in the
 //     owner's fine-grained control line) has the writer bit 31 and a reader count. The writer
@@ -39,8 +40,9 @@
 //     system-scope release, and the last one to arrive clears the writer bit. `applied` is
 //     published after that (an event again);
 //   * read: ps_read_lock takes the read lock of every owner of the table (ascending owner order,
-//     so readers and single-lock writers cannot deadlock), the gather / pull kernel starts each
-//     workgroup with a system-scope acquire (its CU / XCD caches drop stale lines), and
+//     so readers and single-lock writers cannot deadlock), a 64-workgroup system-scope acquire
+//     (fence_l2: every XCD's L2 drops peer-written lines; the next dispatch drops L1) precedes
+//     the gather / pull kernel, and
 //     ps_read_unlock leaves. A read therefore sees every owner's shard between two batches --
 //     never half of one -- which is what the reference's single server thread guarantees
 //     (server/server_thread.cpp:23-61: one Add or Get at a time per model);
@@ -60,23 +62,25 @@ namespace minips_k {
 
 namespace {
 
-// every storing wave drains, the block meets, one lane publishes at system scope
-__device__ __forceinline__ void release_block() {
+constexpr int kFlushBlocks = 64;  // dealt round-robin over the 8 XCDs: every XCD's L2 is covered
+
+// One system-scope fence per workgroup of a 64-workgroup launch -- once per XCD L2, not once per
+// workgroup of the data kernel: a system-scope write-back / invalidate acts on the whole XCD L2,
+// so 8192 gather / push workgroups each fencing flushed the L2 under every concurrently running
+// GEMM (the round-4 one-sided trace: a 240 us push, wgrads at 2.3x their time). RELEASE: the
+// preceding kernels' stores on this stream reach memory; acquire: later kernels on this stream
+// re-read peer-written lines (the kernel boundary drains and the next dispatch drops L1).
+template <bool RELEASE>
+__global__ void ps_fence_kernel() {
+  if (threadIdx.x != 0) return;
+  if constexpr (RELEASE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
 }
 
-// drop this CU's / XCD's cached copies of peer-written lines before reading them
-__device__ __forceinline__ void acquire_block() {
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
+void fence_l2(bool release, hipStream_t s) {
+  if (release) hipLaunchKernelGGL(ps_fence_kernel<true>, kFlushBlocks, 64, 0, s);
+  else hipLaunchKernelGGL(ps_fence_kernel<false>, kFlushBlocks, 64, 0, s);
 }
 
 constexpr uint64_t kSpinLimit = 200000000ull;  // ticks of the 100 MHz real-time counter: ~2 s
@@ -133,8 +137,6 @@ __global__ void ps_write_lock_kernel(uint32_t* lock, uint32_t* err) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
-
-constexpr int kFlushBlocks = 64;  // dealt round-robin over the 8 XCDs: every XCD's L2 is written back
 
 __global__ void ps_write_unlock_kernel(uint32_t* lock, uint32_t* count) {
   if (threadIdx.x != 0) return;
@@ -195,13 +197,11 @@ __global__ __launch_bounds__(256) void ps_push_rows_kernel(const int64_t* __rest
       dst[j] = g[i * W + j];
     }
   }
-  release_block();
 }
 
 __global__ void ps_set_headers_kernel(const int64_t* __restrict__ inbox, int P, int64_t slot_off, int64_t value) {
   if (threadIdx.x < (unsigned)P)
     *reinterpret_cast<int64_t*>(reinterpret_cast<char*>(inbox[threadIdx.x]) + slot_off) = value;
-  release_block();
 }
 
 template <bool VEC, typename TO>
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256) void ps_gather_rows_kernel(const int64_t* __re
   __shared__ int64_t base_ptr[kPsMaxWorld];
   if (threadIdx.x <= (unsigned)P) b[threadIdx.x] = bounds[threadIdx.x];
   if (threadIdx.x < (unsigned)P) base_ptr[threadIdx.x] = bases[threadIdx.x];
-  acquire_block();
+  __syncthreads();
   const int64_t nn = n_dev ? min(n, *n_dev) : n;
   const int nv = VEC ? W / 4 : W;
   const int64_t total = nn * nv;
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) void ps_gather_bf16_kernel(const int64_t* __re
   __shared__ int64_t base_ptr[kPsMaxWorld];
   if (threadIdx.x <= (unsigned)P) b[threadIdx.x] = bounds[threadIdx.x];
   if (threadIdx.x < (unsigned)P) base_ptr[threadIdx.x] = bases[threadIdx.x];
-  acquire_block();
+  __syncthreads();
   const int64_t nn = n_dev ? min(n, *n_dev) : n;
   const int nv = W / 8;
   const int64_t total = nn * nv;
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void ps_hash_gather_kernel(const int64_t* __re
                                                              TO* __restrict__ out) {
   __shared__ int64_t b[kPsMaxWorld + 1];
   if (threadIdx.x <= (unsigned)P) b[threadIdx.x] = bounds[threadIdx.x];
-  acquire_block();
+  __syncthreads();
   const int64_t nn = n_dev ? min(n, *n_dev) : n;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nn; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = keys[i];
@@ -347,7 +347,8 @@ template <int OPT>
 __global__ __launch_bounds__(256) void ps_hash_apply_kernel(unsigned long long* __restrict__ hk, int64_t cap,
                                                             float* __restrict__ vals, float* __restrict__ state,
                                                             int W, const int64_t* __restrict__ keys,
-                                                            const float* __restrict__ g, const int64_t* __restrict__ cnt,
+                                                            const float* __restrict__ g,
+                                                            const int64_t* __restrict__ cnt,
                                                             int64_t n_max, float lr, float eps, float scale,
                                                             uint32_t* err) {
   const int lane = threadIdx.x & 63;
@@ -390,7 +391,6 @@ __global__ __launch_bounds__(256) void ps_hash_apply_kernel(unsigned long long* 
 __global__ __launch_bounds__(256) void ps_pull_kernel(const int64_t* __restrict__ srcs, uint64_t owners,
                                                       int64_t chunks, char* __restrict__ dst, int64_t shard_bytes,
                                                       int count) {
-  acquire_block();
   const int64_t total = chunks * count;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
     const int sel = (int)(c / chunks);
@@ -430,6 +430,7 @@ void ps_gather_rows_bf16tab(const int64_t* bases, const int64_t* bounds, int P, 
   if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_gather_rows_bf16tab: P out of range");
   if (W % 8 || reinterpret_cast<uintptr_t>(out) % 16) throw std::runtime_error("bf16 gather: W % 8, aligned out");
   const int grid = grid_for(n * (W / 8), 256, 8192);
+  fence_l2(false, s);
   if (out_bf16)
     hipLaunchKernelGGL(ps_gather_bf16_kernel<bf16_t>, grid, 256, 0, s, bases, bounds, P, keys, n, n_dev, W,
                        static_cast<bf16_t*>(out));
@@ -446,6 +447,7 @@ void ps_hash_gather(const int64_t* hkeys, const int64_t* hvals, const int64_t* b
   if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_hash_gather: P out of range");
   if (cap <= 0 || (cap & (cap - 1))) throw std::runtime_error("ps_hash_gather: capacity must be a power of two");
   const int grid = grid_for(n, 256, 4096);
+  fence_l2(false, s);
   if (out_bf16)
     hipLaunchKernelGGL(ps_hash_gather_kernel<bf16_t>, grid, 256, 0, s, hkeys, hvals, bounds, P, cap, keys, n, n_dev,
                        W, static_cast<bf16_t*>(out));
@@ -460,6 +462,7 @@ void ps_pull(const int64_t* srcs, uint64_t owners, int count, int64_t shard_byte
   if (count > kPsMaxWorld || shard_bytes % 16 || reinterpret_cast<uintptr_t>(dst) % 16)
     throw std::runtime_error("ps_pull: <= 16 owners, 16-byte aligned shards");
   const int64_t chunks = shard_bytes / 16;
+  fence_l2(false, s);
   hipLaunchKernelGGL(ps_pull_kernel, grid_for(chunks * count, 256, 8192), 256, 0, s, srcs, owners, chunks,
                      static_cast<char*>(dst), shard_bytes, count);
   MINIPS_HIP_CHECK(hipGetLastError());
@@ -479,12 +482,14 @@ void ps_push_rows(const int64_t* uniq, const int64_t* counts, const int64_t* U_d
   else
     hipLaunchKernelGGL(ps_push_rows_kernel<false>, grid, block, 0, s, uniq, counts, U_dev, n, g, W, inbox, P,
                        slot_off, cap);
+  fence_l2(true, s);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 void ps_set_headers(const int64_t* inbox, int P, int64_t slot_off, int64_t value, hipStream_t s) {
   if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_set_headers: P out of range");
   hipLaunchKernelGGL(ps_set_headers_kernel, 1, 64, 0, s, inbox, P, slot_off, value);
+  fence_l2(true, s);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
@@ -495,6 +500,7 @@ void ps_gather_rows(const int64_t* bases, const int64_t* bounds, int P, const in
   const int block = 256;
   const bool vec = W % 4 == 0 && reinterpret_cast<uintptr_t>(out) % (out_bf16 ? 8 : 16) == 0;
   const int grid = grid_for(n * (vec ? W / 4 : W), block, 8192);
+  fence_l2(false, s);
 #define MINIPS_PS_GATHER(V, T)                                                                                \
   hipLaunchKernelGGL((ps_gather_rows_kernel<V, T>), grid, block, 0, s, bases, bounds, P, keys, n, n_dev, W, \
                      static_cast<T*>(out))

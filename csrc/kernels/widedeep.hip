@@ -1210,8 +1210,10 @@ __device__ __forceinline__ void rows_apply(const RowsAdagradArgs& a, int64_t tro
   const float st2 = split ? st2_old + sqw / (float)(a.W - a.D1) : 0.f;
   const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
   float* tr = a.table + trow * (int64_t)a.ld + 8 * l;
-  reinterpret_cast<float4*>(tr)[0] = make_float4(t0.x - s1 * g[0], t0.y - s1 * g[1], t0.z - s1 * g[2], t0.w - s1 * g[3]);
-  reinterpret_cast<float4*>(tr)[1] = make_float4(t1.x - s1 * g[4], t1.y - s1 * g[5], t1.z - s1 * g[6], t1.w - s1 * g[7]);
+  reinterpret_cast<float4*>(tr)[0] =
+      make_float4(t0.x - s1 * g[0], t0.y - s1 * g[1], t0.z - s1 * g[2], t0.w - s1 * g[3]);
+  reinterpret_cast<float4*>(tr)[1] =
+      make_float4(t1.x - s1 * g[4], t1.y - s1 * g[5], t1.z - s1 * g[6], t1.w - s1 * g[7]);
   if (l == 0) {
     if (wide) a.table[trow * (int64_t)a.ld + D] = tw - s2 * gw;
     a.state[trow] = st1;
@@ -1219,8 +1221,16 @@ __device__ __forceinline__ void rows_apply(const RowsAdagradArgs& a, int64_t tro
   }
 }
 
+// the gradient row of member m (lookup j = members[m]): row-sorted (ldx == 0) or lookup order
 template <int D>
-__global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __restrict__ dX,
+__device__ __forceinline__ const bf16_t* grad_row(const bf16_t* dX, int ldx, int F, int m, int j) {
+  if (ldx == 0) return dX + (int64_t)m * D;
+  const int b = j / F;
+  return dX + (int64_t)b * ldx + (j - b * F) * D;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __restrict__ dX, int ldx,
                                                                const float* __restrict__ dwide, int F,
                                                                const int* __restrict__ members,
                                                                const int* __restrict__ rowstart,
@@ -1261,8 +1271,9 @@ __global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __r
       for (int q = 0; q < 4; ++q) {
         const int mm = m + q;
         const bool in = mm < end;
-        v[q] = in ? *reinterpret_cast<const uint4*>(dX + (int64_t)mm * D + 8 * l) : make_uint4(0, 0, 0, 0);
-        w[q] = (wide && l == 0 && in) ? dwide[members[mm] / F] : 0.f;
+        const int j = (in && (ldx || wide)) ? members[mm] : 0;
+        v[q] = in ? *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, mm, j) + 8 * l) : make_uint4(0, 0, 0, 0);
+        w[q] = (wide && l == 0 && in) ? dwide[j / F] : 0.f;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1277,7 +1288,7 @@ __global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __r
 // One workgroup per hot row: 256 / L lane groups stride over the row's lookups, an LDS reduction
 // folds them, and wave 0 applies the update (lane c: column c; lane 0: the wide column).
 template <int D>
-__global__ __launch_bounds__(256) void emb_hot_adagrad_kernel(const bf16_t* __restrict__ dX,
+__global__ __launch_bounds__(256) void emb_hot_adagrad_kernel(const bf16_t* __restrict__ dX, int ldx,
                                                               const float* __restrict__ dwide, int F,
                                                               const int* __restrict__ members,
                                                               const int* __restrict__ rowstart, RowsAdagradArgs a,
@@ -1295,11 +1306,13 @@ __global__ __launch_bounds__(256) void emb_hot_adagrad_kernel(const bf16_t* __re
     float accw = 0.f;
     for (int m = s + g; m < e; m += 2 * G) {
       const bool in2 = m + G < e;
-      const uint4 v0 = *reinterpret_cast<const uint4*>(dX + (int64_t)m * D + 8 * l);
-      const uint4 v1 = in2 ? *reinterpret_cast<const uint4*>(dX + (int64_t)(m + G) * D + 8 * l) : make_uint4(0, 0, 0, 0);
+      const int j0 = (ldx || wide) ? members[m] : 0, j1 = (in2 && (ldx || wide)) ? members[m + G] : 0;
+      const uint4 v0 = *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, m, j0) + 8 * l);
+      const uint4 v1 =
+          in2 ? *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, m + G, j1) + 8 * l) : make_uint4(0, 0, 0, 0);
       if (wide && l == 0) {
-        accw += dwide[members[m] / F];
-        if (in2) accw += dwide[members[m + G] / F];
+        accw += dwide[j0 / F];
+        if (in2) accw += dwide[j1 / F];
       }
       acc_bf16x8(acc, v0);
       acc_bf16x8(acc, v1);
@@ -1334,12 +1347,12 @@ __global__ __launch_bounds__(256) void emb_hot_adagrad_kernel(const bf16_t* __re
   }
 }
 
-void emb_rows_adagrad(const bf16_t* dX, const float* dwide, int F, int D, const int* members, const int* rowstart,
-                      const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base, float* table, int ld,
-                      int W, float* state, float* state2, int D1, float lr, float eps, int* hot_list, int* hot_count,
-                      int hot, hipStream_t s) {
+void emb_rows_adagrad(const bf16_t* dX, int ldx, const float* dwide, int F, int D, const int* members,
+                      const int* rowstart, const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base,
+                      float* table, int ld, int W, float* state, float* state2, int D1, float lr, float eps,
+                      int* hot_list, int* hot_count, int hot, hipStream_t s) {
   if (U_max <= 0) return;
-  if (ld % 4 || reinterpret_cast<uintptr_t>(table) % 16 || reinterpret_cast<uintptr_t>(dX) % 16)
+  if (ld % 4 || reinterpret_cast<uintptr_t>(table) % 16 || reinterpret_cast<uintptr_t>(dX) % 16 || ldx % 8)
     throw std::runtime_error("emb_rows_adagrad: 16-byte aligned rows");
   if (D1 <= 0 || D1 > W) D1 = W;
   if (D1 < W && !state2) throw std::runtime_error("emb_rows_adagrad: split rows need state2");
@@ -1348,10 +1361,10 @@ void emb_rows_adagrad(const bf16_t* dX, const float* dwide, int F, int D, const 
   const int per_block = 4 * (64 / (D / 8));
   const int grid = (int)std::min<int64_t>((U_max + per_block - 1) / per_block, 8192);
 #define MINIPS_ROWS_ADA(DD)                                                                                      \
-  hipLaunchKernelGGL((emb_rows_adagrad_kernel<DD>), grid, 256, 0, s, dX, dwide, F, members, rowstart, U_dev,     \
-                     U_max, a, hot_list, hot_count, hot);                                                         \
-  hipLaunchKernelGGL((emb_hot_adagrad_kernel<DD>), 256, 256, 0, s, dX, dwide, F, members, rowstart, a, hot_list, \
-                     hot_count);
+  hipLaunchKernelGGL((emb_rows_adagrad_kernel<DD>), grid, 256, 0, s, dX, ldx, dwide, F, members, rowstart,     \
+                     U_dev, U_max, a, hot_list, hot_count, hot);                                                  \
+  hipLaunchKernelGGL((emb_hot_adagrad_kernel<DD>), 256, 256, 0, s, dX, ldx, dwide, F, members, rowstart, a,      \
+                     hot_list, hot_count);
   switch (D) {
     case 16:
       MINIPS_ROWS_ADA(16)

@@ -3,6 +3,7 @@
 #include <exception>
 
 #include "base.h"
+#include "trace.h"
 
 namespace minips {
 
@@ -144,6 +145,7 @@ void AsyncServer::Loop() {
       }
       Batch b;
       b.applies = 0;
+      TraceRange range("ps.owner.issue");  // the batch's lock / apply / unlock launches
       for (int t = 0; t < tables_; ++t) {
         bool begun = false;
         for (int64_t k = 0;; ++k) {
@@ -203,6 +205,7 @@ void AsyncServer::PublishLoop() {
       b = &inflight_.front();        // stays in the deque (only this thread pops)
     }
     bool ok = true;
+    TraceRange range("ps.owner.publish");  // wait for the batch's device work, then publish it
     try {
       applier_->Wait(b->ticket);
     } catch (const std::exception& e) {

@@ -41,15 +41,22 @@ class DLRMConfig:
     # "collective": SparseTable / DenseTable over RCCL (all-to-all-v / RS+AG, gated per consistency);
     # "onesided": SSP / ASP with NO collective on the data path -- rows read from the owners'
     # IPC-mapped HBM over xGMI, gradients pushed into the owners' inboxes, row-wise Adagrad / Adam
-    # applied by each owner's server thread with its own state (ps/onesided.py)
-    transport: str = "collective"
+    # applied by each owner's server thread with its own state (ps/onesided.py);
+    # "auto" (default): onesided for SSP / ASP (the asynchronous PS is what those models mean),
+    # collective for BSP
+    transport: str = "auto"
     max_batch: int = 16384       # onesided: inbox slots hold max_batch * F gradient rows
     # embedding rows in bf16 (fp32 row-wise Adagrad state, stochastically rounded applies): the
     # default 10B x 64 table is 1.28 TB of rows + 40 GB of state = 8 x 165 GB, inside 8 x 288 GB
-    # (fp32 rows would need 2.56 TB). The one-sided transport stores fp32 rows.
+    # (fp32 rows would need 2.56 TB). Both transports store them so (the one-sided owners apply
+    # in fp32 and round back stochastically, csrc/kernels/onesided.hip).
     emb_dtype: str = "bfloat16"
     seed: int = 0
     cards: list = field(default_factory=list)  # optional per-feature cardinalities (sum <= num_rows)
+
+    def __post_init__(self):
+        if self.transport == "auto":
+            self.transport = "onesided" if self.consistency in ("ssp", "asp") else "collective"
 
 
 class DLRM(LookaheadPlans):
@@ -62,8 +69,8 @@ class DLRM(LookaheadPlans):
         self.emb = make("sparse", num_rows=cfg.num_rows, width=D, optimizer="rowwise_adagrad", lr=cfg.lr_sparse,
                         model=cfg.consistency, staleness=cfg.staleness, transport=cfg.transport, init_std=0.01,
                         seed=cfg.seed, pull_dtype=torch.bfloat16,
-                        **({"max_keys": cfg.max_batch * F} if onesided else
-                           {"p2p": cfg.p2p, "value_dtype": getattr(torch, cfg.emb_dtype)}))
+                        value_dtype=getattr(torch, cfg.emb_dtype),
+                        **({"max_keys": cfg.max_batch * F} if onesided else {"p2p": cfg.p2p}))
         self.layout = ParamLayout()
         dims = [cfg.n_dense, *cfg.bottom, D]
         self.bottom = [Linear(self.layout, f"bot{i}", dims[i], dims[i + 1]) for i in range(len(dims) - 1)]

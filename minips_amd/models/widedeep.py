@@ -24,6 +24,7 @@ import torch
 
 from .. import ops
 from ..ps.comm import Comm
+from ..utils.metrics import traced
 from .layers import SideStream
 from .feeder import LookaheadPlans
 
@@ -46,6 +47,10 @@ class WideDeepConfig:
     transport: str = "collective"
     max_batch: int = 16384       # onesided: inbox slots hold max_batch * F gradient rows
     seed: int = 0
+    # several ranks: the dense clock runs per bucket of >= bucket_mb MB of gradient (layers merged
+    # from the last one), a bucket's reduce-scatter + Adam + all-gather issued as soon as its
+    # layers' weight gradients exist -- beside the remaining backward (0: one clock at the end)
+    bucket_mb: float = 2.0
 
     @property
     def F(self):
@@ -149,8 +154,13 @@ class WideDeep(LookaheadPlans):
         self.layout["w4"] = (off, (cfg.hidden[-1] + 8,))  # [w4 | b4 | pad]
         off += cfg.hidden[-1] + 8
         self.n_params = off
+        starts = [self.layout[f"W{i + 1}"][0] for i in range(len(cfg.hidden))]
+        bucketed = cfg.bucket_mb > 0 and cfg.transport == "collective" and comm.world > 1
         self.dense = make("dense", n_params=self.n_params, optimizer="adam", lr=cfg.lr_dense, model=cfg.consistency,
-                          staleness=cfg.staleness, transport=cfg.transport)
+                          staleness=cfg.staleness, transport=cfg.transport,
+                          **(dict(buckets=starts, bucket_mb=cfg.bucket_mb) if bucketed else {}))
+        # the bucket each layer's weight gradient completes (None: one clock at the end)
+        self._wbucket = [self.dense.bucket_for_layer(x) for x in starts] if bucketed else None
         self.dense.load_full(self._init_dense(dev))
         self._bufs = {}
         self._side = SideStream(dev, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
@@ -218,6 +228,7 @@ class WideDeep(LookaheadPlans):
         w4 = self.view(P, "w4").float()
         return b["H3"].float() @ w4[:h] + w4[h] + b["wide"]
 
+    @traced("wd.train_step")
     def train_step(self, dense, keys, labels, next_keys=None, next_on_plan_stream: bool = False) -> torch.Tensor:
         """One BSP superstep: Get, forward, backward, Add, Clock. Returns the summed loss
         (a device tensor; no host sync).
@@ -297,12 +308,14 @@ class WideDeep(LookaheadPlans):
             else:
                 _wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
+        self._bucket_done(1, side)  # (layers 2, 3 and the head: their weight gradients are issued)
         with side.fork():
             _wgrad(b["dH1"], b["X"], self.view(G, "W1"))
         # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
-        sorted_rows = plan.csr is not None and len(plan.csr) >= 3  # (members, memrow, positions[, rowstart])
+        # (members, memrow, positions or None[, rowstart]): positions -> the dgrad writes the rows sorted
+        sorted_rows = plan.csr is not None and len(plan.csr) >= 3 and plan.csr[2] is not None
         if sorted_rows:
             ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"].view(B * F, D),
                              perm=plan.csr[2], seg=D)
@@ -327,6 +340,16 @@ class WideDeep(LookaheadPlans):
             self.dense.clock()
         self._advance_next_plan()
         return b["loss"]
+
+    def _bucket_done(self, layer: int, side):
+        """Every layer >= ``layer`` has its weight gradient issued (on the side stream): the buckets
+        starting at or above layer ``layer``'s offset go out now (several ranks, bucketed clocks)."""
+        if self._wbucket is None:
+            return
+        k = self._wbucket[layer]
+        if k is not None and all(b is None or b >= k for b in self._wbucket[layer:]):
+            for j in sorted({b for b in self._wbucket[layer:] if b is not None}, reverse=True):
+                self.dense.bucket_ready(j, events=(side.mark(),))
 
     def drain(self):
         self.emb.drain()

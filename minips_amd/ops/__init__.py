@@ -309,16 +309,16 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
     counts = torch.bincount(owner, minlength=P).to(torch.int64)
     res = (out, perm[inv_u], counts, torch.tensor([U], dtype=torch.int64), order.to(torch.int32),
            perm[inv_u[order]].to(torch.int32))
+    pos = None
     if positions:  # members = order: pos[order[m]] = m
         pos = torch.empty(B * F, dtype=torch.int32)
         pos[order] = torch.arange(B * F, dtype=torch.int32)
-        res = res + (pos,)
-        if P == 1:  # row u's lookups are members [rowstart[u], rowstart[u + 1])
-            rs = torch.full((B * F + 1,), B * F, dtype=torch.int32)
-            rs[0] = 0
-            rs[1: U + 1] = torch.cumsum(torch.bincount(inv_u, minlength=U), 0).to(torch.int32)
-            res = res + (rs,)
-    return res
+    if P == 1:  # row u's lookups are members [rowstart[u], rowstart[u + 1]): (.., positions or None, rowstart)
+        rs = torch.full((B * F + 1,), B * F, dtype=torch.int32)
+        rs[0] = 0
+        rs[1: U + 1] = torch.cumsum(torch.bincount(inv_u, minlength=U), 0).to(torch.int32)
+        return res + (pos, rs)
+    return res + (pos,) if positions else res
 
 
 def gather_rows(table, keys, base, out, n_dev=None):
@@ -563,24 +563,30 @@ def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=No
     return grad_rows
 
 
-def emb_rows_adagrad(dX, dwide, F, D, csr, U_dev, uniq, base, table, state, state2, split, lr, eps, ws, hot=32):
-    """Row-parallel embedding backward + row-wise Adagrad of one rank (widedeep.hip): dX [total, D]
-    bf16 holds the lookups' gradient rows in member order (csr = (members, memrow, positions,
-    rowstart) of plan_sorted), row u sums rows [rowstart[u], rowstart[u+1]) (+ dwide of their
-    samples at column D) and gets sparse_rowwise_adagrad in place. ``ws``: int32 [>= len(rowstart)]
-    (the hot-row list)."""
+def emb_rows_adagrad(dX, dwide, F, D, csr, U_dev, uniq, base, table, state, state2, split, lr, eps, ws, hot=32,
+                     sorted_rows=True):
+    """Row-parallel embedding backward + row-wise Adagrad of one rank (widedeep.hip). csr =
+    (members, memrow, positions, rowstart) of plan_sorted: row u owns members [rowstart[u],
+    rowstart[u+1]); it sums their gradient rows (+ dwide of their samples at column D) and gets
+    sparse_rowwise_adagrad in place. dX bf16: ``sorted_rows`` [total, D] in member order, else
+    [B, >= F*D] in lookup order (row of lookup j = b*F + f at dX[b, f*D:]). ``ws``: int32
+    [>= len(rowstart)] (the hot-row list)."""
     W = table.shape[1]
     D1 = W if split is None else split
     members, rowstart = csr[0], csr[3]
     if _gpu(dX):
         kernels().emb_rows_adagrad(dX, dwide, int(F), int(D), members, rowstart, U_dev, uniq, int(base), table, state,
-                                   state2, int(D1), float(lr), float(eps), ws, int(hot))
+                                   state2, int(D1), float(lr), float(eps), ws, int(hot), bool(sorted_rows))
         return
     U = int(U_dev.reshape(-1)[0])
-    inv = torch.empty(dX.shape[0], dtype=torch.int64)
+    n = members.numel()
+    inv = torch.empty(n, dtype=torch.int64)
     inv[members.long()] = csr[1].long()
-    un = torch.empty_like(dX)
-    un[members.long()] = dX
+    if sorted_rows:
+        un = torch.empty_like(dX)
+        un[members.long()] = dX
+    else:
+        un = dX[:, : F * D]
     grad_rows = torch.zeros(max(U, 1), W, dtype=torch.float32)
     wd_emb_backward(un.reshape(-1, F * D).float(), dwide, inv, F, D, grad_rows)
     sparse_rowwise_adagrad(table, state, uniq[:U], base, grad_rows[:U], lr, eps, state2=state2,

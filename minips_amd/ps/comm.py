@@ -39,6 +39,8 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
+from ..utils.metrics import _ROCTX_ON, range as _mrange
+
 
 # handles of dedicated streams whose owner is gone, by (device index, priority): reused, never
 # destroyed -- the caching allocator may still record events on a stream a freed tensor was
@@ -118,6 +120,9 @@ class Comm:
         self.trace: list | None = [] if os.environ.get("MINIPS_COMM_TRACE") == "1" else None
         self._waiting = 0
         self._wlock = threading.Lock()
+        # per-collective timing (bench.py's N > 1 diagnostics): a list of (kind, bytes, start, end)
+        # -- HIP events on the issuing stream (GPU) or host clocks (gloo) -- when assigned
+        self.timing: list | None = None
 
     def refresh(self):
         """Re-read rank / world / backend after the default process group was re-created (in-place
@@ -143,6 +148,51 @@ class Comm:
 
     def state(self) -> str:
         return "comm" if self._waiting > 0 else "run"
+
+    @contextlib.contextmanager
+    def _timed(self, kind: str, nbytes: int):
+        """Around one collective when ``timing`` is on: its bytes and its time on the issuing
+        stream (an RCCL call leaves the current stream waiting for it, so the end event fires
+        when the collective completed)."""
+        if _ROCTX_ON:
+            with _mrange("comm." + kind):
+                yield from self._timed_inner(kind, nbytes)
+            return
+        yield from self._timed_inner(kind, nbytes)
+
+    def _timed_inner(self, kind: str, nbytes: int):
+        if self.timing is None:
+            yield
+            return
+        if self.device.type == "cuda":
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            yield
+            b.record()
+        else:
+            a = time.perf_counter()
+            yield
+            b = time.perf_counter()
+        self.timing.append((kind, int(nbytes), a, b))
+
+    def timing_report(self, steps: int) -> dict:
+        """Per collective kind: calls, bytes and ms per step, achieved GB/s (bytes / time spent in
+        the collective) of the recorded window; clears the record."""
+        rec, self.timing = self.timing or [], []
+        if rec and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        out: dict = {}
+        for kind, nb, a, b in rec:
+            ms = a.elapsed_time(b) if self.device.type == "cuda" else (b - a) * 1e3
+            e = out.setdefault(kind, {"calls": 0, "bytes": 0, "ms": 0.0})
+            e["calls"] += 1
+            e["bytes"] += nb
+            e["ms"] += ms
+        n = max(1, int(steps))
+        return {k: dict(calls_per_step=round(e["calls"] / n, 3), mb_per_step=round(e["bytes"] / n / 2**20, 4),
+                        ms_per_step=round(e["ms"] / n, 4),
+                        gbps=round(e["bytes"] / (e["ms"] * 1e-3) / 1e9, 3) if e["ms"] > 0 else None)
+                for k, e in sorted(out.items())}
 
     def _record(self, op: str, t: torch.Tensor | None = None, size=None):
         if self.trace is not None:
@@ -210,11 +260,12 @@ class Comm:
             if n:
                 out[:n].copy_(inp[:n])
             return out
-        self.stats.bytes_a2a += inp[: sum(send_splits)].numel() * inp.element_size()
+        nbytes = inp[: sum(send_splits)].numel() * inp.element_size()
+        self.stats.bytes_a2a += nbytes
         if not p2p:
             o = out[: sum(recv_splits)]
             i = inp[: sum(send_splits)]
-            with self.waiting():
+            with self.waiting(), self._timed("all_to_all_v", nbytes):
                 dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
             return out
         so = [0]
@@ -234,7 +285,7 @@ class Comm:
             if recv_splits[peer]:
                 ops_.append(dist.P2POp(dist.irecv, out[ro[peer]: ro[peer + 1]], peer, group=self.group))
         if ops_:
-            with self.waiting():
+            with self.waiting(), self._timed("p2p_send_recv", nbytes):
                 for r in dist.batch_isend_irecv(ops_):
                     r.wait()
         return out
@@ -278,7 +329,7 @@ class Comm:
             out_shard.copy_(inp)
             return out_shard
         self.stats.bytes_rs += inp.numel() * inp.element_size()
-        with self.waiting():
+        with self.waiting(), self._timed("reduce_scatter", inp.numel() * inp.element_size()):
             dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
         return out_shard
 
@@ -299,7 +350,7 @@ class Comm:
         if self.backend == "gloo" and shard.data_ptr() >= out_full.data_ptr() and \
                 shard.data_ptr() < out_full.data_ptr() + out_full.numel() * out_full.element_size():
             shard = shard.clone()  # gloo does not support the in-place (aliased) form
-        with self.waiting():
+        with self.waiting(), self._timed("all_gather", out_full.numel() * out_full.element_size()):
             dist.all_gather_into_tensor(out_full, shard, group=self.group)
         return out_full
 
@@ -313,7 +364,7 @@ class Comm:
                 dist.all_reduce(h, op=op or dist.ReduceOp.SUM, group=self.group)
             t.copy_(h)
             return t
-        with self.waiting():
+        with self.waiting(), self._timed("all_reduce", t.numel() * t.element_size()):
             dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
         return t
 

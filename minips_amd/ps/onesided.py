@@ -51,6 +51,7 @@ import torch.distributed as dist
 
 from .. import ops
 from .comm import Comm
+from ..utils.metrics import traced
 from .tables import SparsePlan, SparseTable, _PendingPlan, column_spec, even_bounds, _route_multiplier
 
 _MAX_TABLES = 16
@@ -60,6 +61,9 @@ _SLOT_HEADER = 64
 # (the gathers' L2 invalidate) of onesided.hip, 1 fine-grained. Inboxes are always uncached, the
 # lock lines always fine-grained.
 _SHARD_MEM = int(os.environ.get("MINIPS_PS_SHARD_MEM", "0"))
+# inbox memory kind (default 2 uncached: the owner's apply reads what peers wrote, never an L2
+# copy of the slot from `depth` clocks ago); MINIPS_PS_INBOX_MEM=0 is an A/B timing knob only
+_INBOX_MEM = int(os.environ.get("MINIPS_PS_INBOX_MEM", "2"))
 # MINIPS_PS_LOCKS=0: no owner locks (A/B timing only: reads may see half of a batch)
 _LOCKS = os.environ.get("MINIPS_PS_LOCKS", "1") != "0"
 
@@ -203,6 +207,7 @@ class AsyncPS:
             finally:
                 self.board.read_unlock(t)
 
+    @traced("ps.wait")
     def wait(self, fn, *args, what: str = "") -> float:
         """Run a board wait in slices, surfacing a server error instead of waiting it out."""
         t0 = time.perf_counter()
@@ -452,7 +457,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         self.state = torch.zeros(self.rows_local, dtype=torch.float32, device=dev) \
             if optimizer == "rowwise_adagrad" else None
         self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
-        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=2)
+        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=_INBOX_MEM)
         self._register_server()
         self._finish_init()
 
@@ -516,6 +521,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         return False
 
     # -- KV API -----------------------------------------------------------------------------
+    @traced("async_sparse.get")
     def get(self, keys: torch.Tensor, plan=None, clock: int | None = None):
         """Rows of the unique keys ([cap, width], unique order) and the plan; rows[plan.inv[i]]
         is the row of keys[i]. No collective: rows come straight from the owners' HBM."""
@@ -545,6 +551,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
                 if bool(m.any()):
                     out[: plan.U][m] = self._views[o][u[m] - lo].to(out.dtype)
 
+    @traced("async_sparse.clock")
     def clock(self):
         """Push this clock's gradient rows into the owners' inboxes, then publish the clock."""
         pending, self._pending = self._pending, []
@@ -719,7 +726,7 @@ class AsyncHashTable(AsyncSparseTable):
         self.shard = self._views[me]
         self.state = torch.zeros(cap, dtype=torch.float32, device=dev) if optimizer == "rowwise_adagrad" else None
         self.state2 = None
-        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=2)
+        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=_INBOX_MEM)
         self._neg = None
         if self.cuda:
             self._hkey_ptrs = torch.tensor([h.data_ptr() for h in self._hk], dtype=torch.int64, device=dev)
@@ -863,7 +870,7 @@ class AsyncDenseTable(_AsyncTable):
         self.m = torch.zeros(self.shard, dtype=torch.float32, device=dev) if optimizer in ("adam", "adagrad") \
             else None
         self.v = torch.zeros_like(self.m) if optimizer == "adam" else None
-        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=2)
+        self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=_INBOX_MEM)
         self.params = torch.zeros(self.n_pad, dtype=pull_dtype, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self._seen = [-1] * P          # owner version of the cached copy (sum of its applied clocks)
@@ -911,6 +918,7 @@ class AsyncDenseTable(_AsyncTable):
         self.drain()
         return torch.cat([m.to(self.comm.device) for m in self._masters])[: self.n_params].clone()
 
+    @traced("async_dense.get")
     def get(self, clock: int | None = None) -> torch.Tensor:
         """Pull the owners' shards the read needs (SSP-gated). Lazy: with a staleness bound s, an
         owner's cached copy that already holds every requester's clocks < c - s is served as is
@@ -946,11 +954,13 @@ class AsyncDenseTable(_AsyncTable):
             self.pulls += len(need)
         return self.params
 
+    @traced("async_dense.add")
     def add(self, grad: torch.Tensor | None = None):
         if grad is not None:
             self.grad[: grad.numel()] += grad.reshape(-1).to(torch.float32)
         self._pending = True
 
+    @traced("async_dense.clock")
     def clock(self):
         slot = self._reserve_slot()
         off = (self.comm.rank * self.depth + slot) * self.slot_bytes

@@ -32,6 +32,7 @@ import torch
 
 from .. import ops
 from .comm import Comm
+from ..utils.metrics import traced
 
 
 def even_bounds(num_rows: int, parts: int) -> list[int]:
@@ -134,11 +135,23 @@ class _Pipeline:
         self.events.clear()
 
 
+def merge_buckets(starts, n_params: int, min_elems: float) -> list:
+    """Layer start offsets -> bucket start offsets: walking down from the last layer, a bucket is
+    closed at a layer start once it holds >= ``min_elems`` elements (the first bucket takes what is
+    left); offset 0 always starts one."""
+    cuts, top = [], n_params
+    for s in sorted({int(x) for x in starts} - {0}, reverse=True):
+        if top - s >= min_elems:
+            cuts.append(s)
+            top = s
+    return [0] + sorted(cuts)
+
+
 class DenseTable:
     def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
                  pull_dtype=torch.bfloat16, consistency: str = "bsp", staleness: int = 0, table_id: int = 0,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, p2p: bool = False,
-                 value_dtype=torch.float32, buckets=None, overlap_w1: bool = False):
+                 value_dtype=torch.float32, buckets=None, overlap_w1: bool = False, bucket_mb: float | None = None):
         """``value_dtype`` float64 gives the reference's ``double`` tables (KVClientTable<double>
         with VectorStorage::SubAdd, server/vector_storage.hpp:28-38): optimizer "add" only, pulled
         in fp64, so BSP sums are exact for exactly representable deltas.
@@ -151,6 +164,11 @@ class DenseTable:
         buckets of 8-64 MB). Ownership is then bucket-major: rank r owns the r-th slice of every
         bucket (the shard buffers are those slices in bucket order); checkpoints keep the
         canonical contiguous layout (shard_state / finish_restore convert).
+
+        ``bucket_mb`` (with ``buckets``): merge consecutive layers into buckets of at least this many
+        MB of fp32 gradient, walking from the last layer (the first whose backward completes) -- few,
+        large collectives for the per-link bandwidth of the xGMI mesh instead of one per small
+        layer; MINIPS_BUCKET_MB overrides it.
 
         ``overlap_w1``: at world 1 too, run the clock on the table's side stream and, with
         ``buckets``, apply each bucket as soon as the backward finished its layer (one rank has
@@ -192,6 +210,11 @@ class DenseTable:
         self._ring = [self.grad] + [torch.zeros_like(self.grad) for _ in range(self.pipe.staleness + 1)] \
             if self.pipe.async_ else [self.grad]
         self.buckets = None
+        env_mb = __import__("os").environ.get("MINIPS_BUCKET_MB")
+        if env_mb:
+            bucket_mb = float(env_mb)
+        if buckets is not None and bucket_mb:
+            buckets = merge_buckets(buckets, n_params, bucket_mb * 2**20 / self.master.element_size())
         if buckets is not None and (comm.world > 1 or self.pipe.async_):
             self._init_buckets(buckets)
 
@@ -341,16 +364,19 @@ class DenseTable:
         return out[: self.n_params]
 
     # -- KV API -----------------------------------------------------------------------------
+    @traced("dense.get")
     def get(self) -> torch.Tensor:
         self.pipe.wait_for_read()
         return self.params
 
+    @traced("dense.add")
     def add(self, grad: torch.Tensor | None = None):
         """Accumulate a gradient (or mark the in-place-written self.grad as pushed)."""
         if grad is not None:
             self.grad[: grad.numel()] += grad.reshape(-1).to(self.value_dtype)
         self._pending = True
 
+    @traced("dense.clock")
     def clock(self):
         grad = self.grad
         step = self.step + 1
@@ -581,11 +607,12 @@ _FUSED_ASSEMBLE = os.environ.get("MINIPS_FUSED_ASSEMBLE", "1") == "1"
 class _LookupGrads:
     """A push in lookup form (SparseTable.add_lookup_grads): dX [B, >= F*D] holds one gradient
     row per lookup (b, f) at columns f*D.., dwide [B] the sample's wide-column gradient."""
-    __slots__ = ("dX", "dwide", "F", "D", "sorted")
+    __slots__ = ("dX", "dwide", "F", "D", "sorted", "rows")
 
-    def __init__(self, dX, dwide, F, D, sorted_rows=False):
+    def __init__(self, dX, dwide, F, D, sorted_rows=False, rows=False):
         self.dX, self.dwide, self.F, self.D = dX, dwide, F, D
-        self.sorted = sorted_rows  # dX [B*F, D] in the CSR's member order (row-parallel apply)
+        self.sorted = sorted_rows  # dX [B*F, D] in the CSR's member order
+        self.rows = rows  # row-parallel apply (ops.emb_rows_adagrad), else ops.emb_seg_adagrad
 
 
 class _PendingPlan:
@@ -719,7 +746,7 @@ class SparseTable:
                                   self.num_rows if rmult else 0, bits_dev=cols[2], bounds=self.bounds,
                                   positions=want_csr and SORTED_EMB)
             pp.uniq, pp.inv, pp.counts, pp.U_dev = res[:4]
-            pp.csr = tuple(res[4:]) if want_csr else None  # (members, memrow[, positions])
+            pp.csr = tuple(res[4:]) if want_csr else None  # (members, memrow[, positions][, rowstart])
             pp.host = pp.event = pp.cev = None
             pp.exchanged = self.comm.world == 1
             if exchange:
@@ -805,7 +832,8 @@ class SparseTable:
             return pp
         keys.record_stream(ps)
         for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev, *(pp.csr or ())):
-            t.record_stream(cur)  # produced on the planning stream, consumed on the compute stream
+            if t is not None:  # produced on the planning stream, consumed on the compute stream
+                t.record_stream(cur)
         return pp
 
     def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
@@ -896,6 +924,7 @@ class SparseTable:
         plan.extra["ready"] = ev
         return plan
 
+    @traced("sparse.get")
     def get(self, keys: torch.Tensor, plan=None):
         """Pull rows of ``keys``. Returns (rows [cap, width] in unique order, plan); the row of
         keys[i] is rows[plan.inv[i]]. ``plan`` may be a plan_async() handle for these keys."""
@@ -943,11 +972,13 @@ class SparseTable:
         rows, plan = self.get(keys)
         return rows[plan.inv]
 
+    @traced("sparse.add")
     def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
         """Push gradient rows (aligned with the plan's unique order; rows >= U are ignored)."""
         assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == getattr(self, "grad_dtype", torch.float32)
         self._pending.append((plan, grad_rows))
 
+    @traced("sparse.add_lookup_grads")
     def add_lookup_grads(self, plan: SparsePlan, dX: torch.Tensor, dwide, F: int, D: int, x_off: int = 0,
                          sorted_rows: bool = False):
         """Push the gradient of every lookup of ``plan``'s batch: dX[b, x_off + f*D : +D] for
@@ -955,14 +986,15 @@ class SparseTable:
         row -- the Add of the reference's worker, which sends one summed row per key. One rank
         with row-wise Adagrad fuses that reduction into the apply (no gradient-row buffer,
         ops.emb_seg_adagrad); otherwise the rows are segment-summed here and pushed by add()."""
-        if not sorted_rows and self._fused_lookup_ok(plan, dX, dwide, D, x_off):
-            self._pending.append((plan, _LookupGrads(dX[:, x_off:] if x_off else dX, dwide, F, D)))
+        if (_ROWS_ADAGRAD and plan.csr is not None and len(plan.csr) >= 4 and dX.dtype == torch.bfloat16
+                and x_off == 0 and dX.stride(0) % 8 == 0 and self._rows_apply_ok(plan, dX, dwide, D, 0)):
+            # one rank: each unique row sums its lookups' gradient rows (row-sorted or in lookup
+            # order) and is updated in place (ops.emb_rows_adagrad) -- no grad_rows buffer, no zero
+            # fill, no atomics
+            self._pending.append((plan, _LookupGrads(dX, dwide, F, D, sorted_rows=sorted_rows, rows=True)))
             return
-        if (sorted_rows and _ROWS_ADAGRAD and plan.csr is not None and len(plan.csr) >= 4 and dX.dtype == torch.bfloat16
-                and x_off == 0 and self._fused_lookup_ok(plan, dX, dwide, D, 0)):
-            # one rank, row-sorted gradient rows: each unique row sums its lookups and is updated in
-            # place (ops.emb_rows_adagrad) -- no grad_rows buffer, no zero fill, no atomics
-            self._pending.append((plan, _LookupGrads(dX, dwide, F, D, sorted_rows=True)))
+        if not sorted_rows and _FUSED_EMB_ADAGRAD and self._rows_apply_ok(plan, dX, dwide, D, x_off):
+            self._pending.append((plan, _LookupGrads(dX[:, x_off:] if x_off else dX, dwide, F, D)))
             return
         dev = self.comm.device
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width,
@@ -971,8 +1003,9 @@ class SparseTable:
                             sorted_rows=sorted_rows)
         self.add(plan, grad_rows)
 
-    def _fused_lookup_ok(self, plan, dX, dwide, D, x_off) -> bool:
-        return (_FUSED_EMB_ADAGRAD and self.comm.world == 1 and dX.is_cuda and self.optimizer == "rowwise_adagrad"
+    def _rows_apply_ok(self, plan, dX, dwide, D, x_off) -> bool:
+        """One rank, row-wise Adagrad on a local fp32 shard: the embedding backward can apply."""
+        return (self.comm.world == 1 and dX.is_cuda and self.optimizer == "rowwise_adagrad"
                 and self.value_dtype == torch.float32 and type(self)._owner_rows is SparseTable._owner_rows
                 and plan.csr is not None and D in (16, 32, 64) and x_off % 4 == 0 and dX.stride(0) % 4 == 0
                 and self.width % 4 == 0 and self.width >= D + (dwide is not None)
@@ -993,6 +1026,7 @@ class SparseTable:
         ops.scatter_add_rows(vals.reshape(keys.numel(), self.width).to(vdt).contiguous(), plan.inv, g)
         self.add(plan, g)
 
+    @traced("sparse.clock")
     def clock(self):
         pending, self._pending = self._pending, []
         for plan, g in pending:
@@ -1006,9 +1040,10 @@ class SparseTable:
 
         self.pipe.run(work)
 
+    @traced("sparse.push")
     def _push(self, plan: SparsePlan, grad_rows):
         dev = self.comm.device
-        if isinstance(grad_rows, _LookupGrads) and grad_rows.sorted:  # one rank, row-parallel
+        if isinstance(grad_rows, _LookupGrads) and grad_rows.rows:  # one rank, row-parallel
             lg = grad_rows
             n = plan.csr[3].numel()
             ws = getattr(self, "_rows_ws", None)
@@ -1016,7 +1051,7 @@ class SparseTable:
                 ws = self._rows_ws = torch.empty(n, dtype=torch.int32, device=dev)
             U_dev = plan.U_dev if plan.U_dev is not None else torch.tensor([plan.cap], dtype=torch.int64, device=dev)
             ops.emb_rows_adagrad(lg.dX, lg.dwide, lg.F, lg.D, plan.csr, U_dev, plan.uniq, self.base, self.shard,
-                                 self.state, self.state2, self.split, self.lr, self.eps, ws)
+                                 self.state, self.state2, self.split, self.lr, self.eps, ws, sorted_rows=lg.sorted)
             return
         if isinstance(grad_rows, _LookupGrads):  # one rank, fused reduction + apply
             lg = grad_rows
@@ -1081,7 +1116,15 @@ class SparseTable:
         meta = dict(global_rows=self.num_rows, base=self.base, rows=self.rows_local, cols=self.width,
                     clock=self.pipe.clock, table_id=self.table_id, rank=self.comm.rank, world=self.comm.world,
                     kind="sparse")
+        if self.value_dtype == torch.bfloat16:
+            meta["applies"] = int(self._applies)  # the stochastic-rounding stream resumes where it was
         return meta, arrays
+
+    def restore_meta(self, meta: dict):
+        """Checkpoint meta of this rank's shard (ps/checkpoint.py, before the rows land): bf16 rows
+        continue their stochastic-rounding stream instead of replaying steps 0, 1, ...."""
+        if "applies" in meta:
+            self._applies = int(meta["applies"])
 
     def restore_range(self):
         return self.base, self.base + self.rows_local
@@ -1235,6 +1278,7 @@ class HashSparseTable(SparseTable):
         plan.extra["served_cap"] = self.capacity
         return self.shard, slots, 0
 
+    @traced("hash.add")
     def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
         """Resolve (insert-on-miss) the owner slots NOW, on the issuing stream: the clock's apply
         may run on the pipe stream, where a table growth must never happen."""

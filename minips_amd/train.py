@@ -58,9 +58,10 @@ def parse(argv=None):
                          "the supervisor relaunches only the failed rank; restart: the whole rank set")
     ap.add_argument("--value_dtype", default="float32", choices=["float32", "float64"],
                     help="LR table precision; float64 = the reference's CreateTable<double> (lr_example.cpp:182)")
-    ap.add_argument("--transport", default="collective", choices=["collective", "onesided"],
+    ap.add_argument("--transport", default="auto", choices=["auto", "collective", "onesided"],
                     help="W&D / DLRM SSP/ASP data path: RCCL collectives, or the asynchronous PS "
-                         "(one-sided row reads, inbox pushes, owner-side optimizer apply; ps/onesided.py)")
+                         "(one-sided row reads, inbox pushes, owner-side optimizer apply; ps/onesided.py); "
+                         "auto = the model's default (DLRM SSP/ASP: onesided, otherwise collective)")
     ap.add_argument("--asp_bound", type=int, default=-1,
                     help="ASP on the one-sided transport: >= 0 bounds how far a Get may run ahead of the "
                          "owners' applies (the SSP gate); -1 (default): unbounded, the reference ASP")
@@ -95,7 +96,10 @@ def parse(argv=None):
     ap.add_argument("--assigner_master_port", type=int, default=0,
                     help="> 0: rank 0 serves locality-aware block assignment (HDFSBlockAssigner) on this port")
     ap.add_argument("--num_dims", type=int, default=0, help="feature count (reference flag; 0: infer / default)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.transport == "auto":  # DLRMConfig's rule (models/dlrm.py)
+        args.transport = "onesided" if args.model == "dlrm" and args.consistency in ("ssp", "asp") else "collective"
+    return args
 
 
 def _load_input(args, comm):

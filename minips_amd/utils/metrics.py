@@ -4,8 +4,11 @@ MetricsLogger   structured JSONL per rank (``$MINIPS_METRICS_DIR/rank<r>.jsonl``
                 step records (step time, samples/s, bytes pushed/pulled per collective and the
                 achieved GB/s, staleness histogram, pending-buffer depth) and events (checkpoint,
                 restore, fault-tolerance phases). Without the env var it only keeps counters.
-range(name)     roctx range (libroctx64) around Get / Add / Clock / apply / collectives, so the
-                phases show up in rocprofv3 --marker-trace timelines; a no-op when roctx is absent.
+range(name)     roctx range around Get / Add / Clock / collectives (and, natively, the owner's
+traced(name)    apply batches: csrc/runtime/trace.h), so the phases show up in
+                ``rocprofv3 --marker-trace`` timelines. Off unless MINIPS_ROCTX=1 (then
+                librocprofiler-sdk-roctx is loaded): a disabled ``traced`` leaves the method
+                untouched and a disabled ``range`` returns a shared null context.
 fault_tolerance_phase(n, detail)
                 the reference's "[Fault Tolerance][PhaseN][ts] ..." line (base/utils.hpp:24-53).
 """
@@ -22,14 +25,17 @@ import time
 
 _ROCTX = None
 _ROCTX_TRIED = False
+_ROCTX_ON = os.environ.get("MINIPS_ROCTX", "0") == "1"
+_NULL = contextlib.nullcontext()
 
 
 def _roctx():
     global _ROCTX, _ROCTX_TRIED
     if not _ROCTX_TRIED:
         _ROCTX_TRIED = True
-        if os.environ.get("MINIPS_ROCTX", "1") != "0":
-            for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+        if _ROCTX_ON:
+            for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+                         "libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
                 try:
                     lib = ctypes.CDLL(name)
                     lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
@@ -37,21 +43,55 @@ def _roctx():
                     lib.roctxRangePop.restype = ctypes.c_int
                     _ROCTX = lib
                     break
-                except OSError:
+                except (OSError, AttributeError):
                     continue
     return _ROCTX
 
 
-@contextlib.contextmanager
+class _Range:
+    __slots__ = ("lib", "name")
+
+    def __init__(self, lib, name: str):
+        self.lib, self.name = lib, name.encode()
+
+    def __enter__(self):
+        self.lib.roctxRangePushA(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        self.lib.roctxRangePop()
+        return False
+
+
 def range(name: str):  # noqa: A001 - mirrors the roctx naming
-    lib = _roctx()
-    if lib is not None:
-        lib.roctxRangePushA(name.encode())
-    try:
-        yield
-    finally:
-        if lib is not None:
-            lib.roctxRangePop()
+    """roctx range context (a shared no-op context when roctx is off)."""
+    lib = _roctx() if _ROCTX_ON else None
+    return _NULL if lib is None else _Range(lib, name)
+
+
+def traced(name: str):
+    """Method decorator: the call runs inside roctx range ``name`` when MINIPS_ROCTX=1 at import;
+    otherwise the method is returned unchanged (zero cost on the step's host path)."""
+
+    def deco(fn):
+        if not _ROCTX_ON:
+            return fn
+        import functools
+
+        @functools.wraps(fn)
+        def wrapped(*args, **kwargs):
+            lib = _roctx()
+            if lib is None:
+                return fn(*args, **kwargs)
+            lib.roctxRangePushA(name.encode())
+            try:
+                return fn(*args, **kwargs)
+            finally:
+                lib.roctxRangePop()
+
+        return wrapped
+
+    return deco
 
 
 class MetricsLogger:

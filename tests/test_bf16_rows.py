@@ -31,10 +31,13 @@ def _bf16_vs_fp32(rank, world, prefix=None):
 
         ck = Checkpointer(comm, prefix)
         ck.save({0: tb}, iteration=6, blocking=True)
-        snap = tb.shard.clone()
+        snap, applies = tb.shard.clone(), tb._applies
         tb.shard.zero_()
+        tb._applies = 0
         ck.load({0: tb})
         out["restored"] = bool(torch.equal(tb.shard, snap))
+        # the stochastic-rounding stream resumes where it was, not at step 0
+        out["applies"] = (applies, tb._applies)
     return out
 
 
@@ -52,3 +55,4 @@ def test_bf16_rows_track_fp32_and_checkpoint(tmp_path):
         assert o["dtype"] == "torch.bfloat16"
         assert o["err"] <= 2 ** -7 * o["scale"] * 2 + 1e-3, o  # within a couple of bf16 ulps
         assert o["restored"], o
+        assert o["applies"][0] > 0 and o["applies"][0] == o["applies"][1], o

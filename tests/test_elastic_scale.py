@@ -51,7 +51,8 @@ def _summary(logs):
 ONESIDED = ("--transport=onesided", "--consistency=ssp", "--staleness=1")
 
 
-@pytest.mark.parametrize("n0,n1,extra", [(2, 3, ()), (3, 2, ()), (2, 3, ONESIDED)], ids=["2to3", "3to2", "2to3-onesided"])
+@pytest.mark.parametrize("n0,n1,extra", [(2, 3, ()), (3, 2, ()), (2, 3, ONESIDED)],
+                         ids=["2to3", "3to2", "2to3-onesided"])
 def test_live_rescale(tmp_path, n0, n1, extra):
     """(the one-sided case: the old AsyncPS -- server thread, board, IPC maps -- is closed before
     the group is left, and the re-formed group, new rank included, builds a fresh one)"""

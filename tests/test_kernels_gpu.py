@@ -508,11 +508,14 @@ def test_fused_emb_backward_adagrad(dev, D, wide, split, dtype):
         assert int(scr.count_nonzero()) == 0
 
 
-@pytest.mark.parametrize("D,wide,split", [(32, True, True), (16, False, False), (64, True, True)])
-def test_rows_emb_backward_adagrad(dev, D, wide, split):
-    """ops.emb_rows_adagrad (row-parallel backward + row-wise Adagrad over the row-sorted bf16
-    gradient rows of plan_sorted) against the CPU reference of the separate ops, two steps: cold
-    rows, Zipf-hot rows of thousands of lookups (the workgroup-per-row path), single lookups."""
+@pytest.mark.parametrize("D,wide,split,sorted_rows", [(32, True, True, True), (16, False, False, True),
+                                                      (64, True, True, True), (32, True, False, False),
+                                                      (64, False, True, False), (16, True, False, False)])
+def test_rows_emb_backward_adagrad(dev, D, wide, split, sorted_rows):
+    """ops.emb_rows_adagrad (row-parallel backward + row-wise Adagrad over the bf16 gradient rows
+    -- row-sorted, or in lookup order with a padded row stride -- and the row ranges of
+    plan_sorted) against the CPU reference of the separate ops, two steps: cold rows, Zipf-hot rows
+    of thousands of lookups (the workgroup-per-row path), single lookups."""
     g = torch.Generator().manual_seed(D + 3 * wide)
     B, F = 8192, 6
     cards = [40000, 5, 3000, 700, 2, 20000]
@@ -531,17 +534,23 @@ def test_rows_emb_backward_adagrad(dev, D, wide, split):
     for step in range(2):
         keys = torch.stack([torch.randint(0, c, (B,), generator=g) for c in cards], 1) + base
         keys[:3000, 2] = base[2] + 17 + step  # a hot row: 3000 lookups
-        res = ops.plan_sorted(keys.to(dev), base.to(dev), bits, positions=True)
+        res = ops.plan_sorted(keys.to(dev), base.to(dev), bits, positions=sorted_rows)
         uniq, inv, counts, U_dev = res[:4]
         csr = tuple(res[4:])
-        assert len(csr) == 4
+        assert len(csr) == 4 and (csr[2] is None) == (not sorted_rows)
         lookups = torch.randn(B * F, D, generator=g).to(torch.bfloat16)  # lookup order
-        pos = csr[2].cpu().long()
-        dX = torch.empty_like(lookups)
-        dX[pos] = lookups  # member order: row m = lookup members[m]
+        if sorted_rows:
+            pos = csr[2].cpu().long()
+            dX = torch.empty_like(lookups)
+            dX[pos] = lookups  # member order: row m = lookup members[m]
+        else:  # lookup order, [B, F*D] inside a padded [B, F*D + 8] buffer
+            dX = torch.zeros(B, F * D + 8, dtype=torch.bfloat16)
+            dX[:, : F * D] = lookups.reshape(B, F * D)
         dwide = torch.randn(B, generator=g) if wide else None
-        ops.emb_rows_adagrad(dX.to(dev), dwide.to(dev) if wide else None, F, D, csr, U_dev, uniq, 0, t_gpu, s_gpu,
-                             s2_gpu, D if split else None, 0.05, 1e-8, ws)
+        dXg = dX.to(dev)
+        ops.emb_rows_adagrad(dXg if sorted_rows else dXg[:, : F * D], dwide.to(dev) if wide else None, F, D, csr,
+                             U_dev, uniq, 0, t_gpu, s_gpu, s2_gpu, D if split else None, 0.05, 1e-8, ws,
+                             sorted_rows=sorted_rows)
         cres = ops.plan_sorted(keys, base, bits, positions=True)
         ccsr = tuple(cres[4:])
         ops.emb_rows_adagrad(lookups[ccsr[0].long()].float().to(torch.bfloat16), dwide, F, D, ccsr, cres[3],

@@ -15,7 +15,6 @@
 CPU ranks: /dev/shm buffers and the board's lock lines; GPU: two processes share cuda:0.
 """
 import os
-import time
 
 import pytest
 import torch

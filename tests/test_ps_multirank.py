@@ -205,7 +205,7 @@ def _dlrm_run(rank, world, steps=4):
 
     torch.set_num_threads(1)
     comm = Comm(device=torch.device("cpu"))
-    cfg = DLRMConfig(num_rows=5003)
+    cfg = DLRMConfig(num_rows=5003, transport="collective")  # ASP over collectives: exact across world sizes
     m = DLRM(cfg, comm)
     g = torch.Generator().manual_seed(9)
     full = torch.randn(cfg.num_rows, cfg.D, generator=g) * 0.05

@@ -141,11 +141,14 @@ def main():
                     help="mlp: capture the step in a HIP graph (one rank, BSP; off by default: at batch 8192 the "
                          "step is GPU-bound, 0.364 vs 0.350 ms measured)")
     ap.add_argument("--staleness", type=int, default=0)
-    ap.add_argument("--transport", default="collective", choices=["collective", "onesided"],
-                    help="widedeep-ssp / dlrm: RCCL collectives or the asynchronous PS (ps/onesided.py)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "collective", "onesided"],
+                    help="widedeep-ssp / dlrm: RCCL collectives or the asynchronous PS (ps/onesided.py); auto = "
+                         "the model's default (DLRM SSP/ASP: onesided; widedeep-ssp: collective)")
     ap.add_argument("--value-dtype", default="float32", choices=["float32", "float64"],
                     help="lr: table precision (float64 = the reference's CreateTable<double>)")
     args = ap.parse_args()
+    if args.transport == "auto" and not args.model.startswith("dlrm"):
+        args.transport = "collective"
     from minips_amd.ps.comm import init_distributed
 
     comm = init_distributed()

@@ -11,6 +11,10 @@
         all queues (GPU busy), per-queue busy time and the kernels by device time per step -- the
         numbers that tell an overlap problem (busy << wall) from a kernel problem (busy ~ wall)
 
+    python tools/prof_summary.py markers run_marker_api_trace.csv [--steps N]
+        roctx ranges (MINIPS_ROCTX=1 under ``rocprofv3 --marker-trace``): count and host time per
+        range name (Get / Add / Clock / collectives / the owner's apply batches)
+
 (A bare path as the first argument means ``stats``.) Per-kernel TFLOP/s and TB/s of the W&D step:
 tools/kernel_roofline.py.
 """
@@ -20,6 +24,13 @@ import argparse
 import collections
 import csv
 import sys
+
+
+
+def _short(name: str) -> str:
+    """Kernel name without its argument list (keeps '(anonymous namespace)::' qualifiers)."""
+    n = name.replace("(anonymous namespace)::", "")
+    return n.split("(")[0][:110]
 
 
 def stats(path, steps=1, top=25):
@@ -74,7 +85,7 @@ def trace(a):
     calls = collections.Counter()
     for s, e, n, q in win:
         per_q[q] += e - s
-        short = n.split("(")[0][:110]
+        short = _short(n)
         per_k[short] += e - s
         calls[short] += 1
     tot = sum(per_k.values())
@@ -89,20 +100,51 @@ def trace(a):
         # one steady step, kernel by kernel: start offset and duration per queue, and the idle gap of
         # each queue before the kernel -- what the critical path waits on
         t0, t1 = anchors[a.skip + 1], anchors[a.skip + 2]
-        print(f"\ntimeline of one step ({(t1 - t0) / 1e3:.1f} us), anchor {a.anchor}: start_us dur_us gap_us queue kernel")
+        print(f"\ntimeline of one step ({(t1 - t0) / 1e3:.1f} us), anchor {a.anchor}: "
+              "start_us dur_us gap_us queue kernel")
         last_end = {}
         for s, e, n, q in ks:
             if s < t0 or s >= t1:
                 continue
             gap = (s - last_end[q]) / 1e3 if q in last_end else 0.0
             last_end[q] = e
-            print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {gap:7.1f}  q{q}  {n.split('(')[0][:90]}")
+            print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {gap:7.1f}  q{q}  {_short(n)[:90]}")
+
+
+def markers(a):
+    """roctx ranges of a ``--marker-trace`` run (MINIPS_ROCTX=1): per range name its count, total
+    and mean host time, per thread; ``--steps`` divides the totals into per-step figures."""
+    rows = list(csv.DictReader(open(a.path)))
+    if not rows:
+        raise SystemExit("no marker records")
+    keys = rows[0].keys()
+    name_col = next((c for c in ("Message", "Marker_Name", "Name", "Function") if c in keys), None)
+    if name_col is None:
+        raise SystemExit(f"no name column among {list(keys)}")
+    tid_col = "Thread_Id" if "Thread_Id" in keys else None
+    agg = collections.defaultdict(lambda: [0, 0])
+    threads = collections.defaultdict(set)
+    for r in rows:
+        try:
+            d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        except (KeyError, ValueError):
+            continue
+        n = r[name_col]
+        agg[n][0] += 1
+        agg[n][1] += d
+        if tid_col:
+            threads[n].add(r[tid_col])
+    steps = max(1, a.steps)
+    print(f"{'calls/step':>10} {'ms/step':>9} {'us/call':>9} {'threads':>7}  range   ({len(rows)} records, "
+          f"per step over {steps})")
+    for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"{c / steps:10.2f} {t / steps / 1e6:9.4f} {t / c / 1e3:9.1f} {len(threads[n]):7d}  {n[:80]}")
 
 
 
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    if argv and argv[0] not in ("stats", "pmc", "trace", "-h", "--help"):
+    if argv and argv[0] not in ("stats", "pmc", "trace", "markers", "-h", "--help"):
         argv.insert(0, "stats")
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -117,8 +159,13 @@ def main(argv=None):
     p.add_argument("--skip", type=int, default=3)
     p.add_argument("--top", type=int, default=30)
     p.add_argument("--timeline", action="store_true", help="also list one steady step kernel by kernel")
+    p = sub.add_parser("markers")
+    p.add_argument("path")
+    p.add_argument("--steps", type=int, default=1)
     a = ap.parse_args(argv)
-    if a.cmd == "stats":
+    if a.cmd == "markers":
+        markers(a)
+    elif a.cmd == "stats":
         stats(a.path, a.steps, a.top)
     elif a.cmd == "pmc":
         pmc(a.paths)
