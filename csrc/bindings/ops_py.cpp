@@ -655,7 +655,7 @@ void emb_rows_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwi
                       const at::Tensor& uniq, int64_t base, at::Tensor& table, at::Tensor& state,
                       const c10::optional<at::Tensor>& state2, int64_t D1, double lr, double eps, at::Tensor& ws,
                       int64_t hot, bool sorted_rows) {
-  check_gpu(dX, "dX");
+  TORCH_CHECK(dX.is_cuda(), "dX must be a GPU tensor");  // lookup order may be a column slice
   check_dtype(dX, at::kBFloat16, "dX");
   TORCH_CHECK(dX.dim() == 2 && dX.stride(1) == 1 && dX.stride(0) % 8 == 0, "dX: 2-D, 16-byte aligned rows");
   if (sorted_rows) {

@@ -1137,8 +1137,201 @@ __global__ __launch_bounds__(512) void gemm_v4_kernel(const bf16_t* __restrict__
                        reinterpret_cast<float*>(&smem[0][0]) + wave * kScrFloats);
 }
 
+// ================================================================ v5: 256x256, 8 waves, ping-pong
+// The 256x256 / BK = 64 / 8-wave tile (2 (M) x 4 (N) waves of 128 x 64) with the two 4-wave row
+// groups STAGGERED by one barrier: every phase is {ds_reads + DMA issue | barrier | 16 MFMAs |
+// barrier} and group 1 runs one barrier behind group 0, so at any moment one group issues its
+// LDS reads and DMAs while the other runs its MFMA cluster (the ping-pong that keeps the matrix
+// cores fed at one workgroup per CU). A K-step is 4 phases over the wave's quadrants:
+//   q0: A rows 0-63 (8 frags) + B n-tiles 0-1 (4) -> acc[0..3][0..1]
+//   q1: B n-tiles 2-3 (4)                          -> acc[0..3][2..3]
+//   q2: A rows 64-127 (8)                          -> acc[4..7][0..1]
+//   q3: -                                          -> acc[4..7][2..3]
+// LDS: [buf][A0 | A1 | B0 | B1] half tiles of 16 KiB (the v2 swizzled images), 2 buffers = 128 KiB.
+// A half g is staged and read by row group g only (two 64-row DMA parts, or one 128-row part for
+// KM operands); the B halves by all 8 waves. Staging of K-step t+1 runs through the phases of K-step
+// t (B0 at q3 of t-1, B1 at q0, A lo at q1, A hi at q2: each region is refilled >= 1 barrier after
+// every wave's reads of it retired), and two counted waits retire it: vmcnt at q3 (everything but
+// A hi and the next step's B0) and vmcnt at q1 of t+1 (A hi, read at q2). Every read follows the
+// issuing waves' wait by at least one barrier of the reading group, counted with the stagger.
+template <bool A_KM, bool B_KN, int EPI>
+__global__ __launch_bounds__(512) void gemm_v5_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                      int M, int N, int K, int lda, int ldb, int k_chunk, EpiArgs ep) {
+  constexpr bool PERM = A_KM && B_KN;
+  constexpr int kHalf = 128 * BK2;  // bf16 elements of one half-tile image
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2][4 * kHalf];
+  static_assert(sizeof(smem) >= sizeof(float) * 8 * kScrFloats, "epilogue scratch must fit the staging LDS");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3, gw = wave & 3;
+  // wave-uniform in a scalar register: the stagger's extra s_barrier must be a scalar branch
+  const bool group1 = __builtin_amdgcn_readfirstlane(tid) >= 256;
+  const int tiles_n = (N + 255) / 256, tiles_m = (M + 255) / 256;
+  int tm, tn;
+  v4_tile(blockIdx.x, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  {
+    const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
+    A += zo * ep.sa_o + zi * ep.sa_i;
+    B += zo * ep.sb_o + zi * ep.sb_i;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
+    ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
+  }
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7ffffff0, 0x00020000);
+  const int kb = blockIdx.z * k_chunk;
+  const int ke = min(K, kb + k_chunk);
+  const int nt = ke > kb ? (ke - kb + BK2 - 1) / BK2 : 0;
+
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // DMA issue per thread: B half 2, A part 2 (MK: 64 rows) or 4 (KM: the whole 128-row half)
+  auto stage_b = [&](int t, int h, int buf) {
+    dma_tile<B_KN, 128, 8>(rb, ldb, n0 + h * 128, kb + t * BK2, N, ke, smem[buf] + (2 + h) * kHalf, wave, lane);
+  };
+  auto stage_a = [&](int t, int part, int buf) {
+    bf16_t* S = smem[buf] + wr * kHalf;
+    if constexpr (!A_KM)
+      dma_tile<false, 64, 4>(ra, lda, m0 + wr * 128 + part * 64, kb + t * BK2, M, ke, S + part * 64 * BK2, gw, lane);
+    else if (part == 0)
+      dma_tile<true, 128, 4>(ra, lda, m0 + wr * 128, kb + t * BK2, M, ke, S, gw, lane);
+  };
+  auto bar = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // vmcnt of the q1 wait (A hi of this K-step) / the q3 wait (the next K-step but its A hi),
+  // steady state: DMAs issued after the one to retire (MK: 2 per stage; KM: A is one 4-DMA stage
+  // at q1 and nothing at q2, so the q1 wait has nothing to retire and q3 waits for all but B0)
+  constexpr int kVmQ1 = A_KM ? 8 : 6;
+  constexpr int kVmQ3 = A_KM ? 2 : 4;
+
+  if (nt > 0) {
+    stage_b(0, 0, 0);
+    stage_b(0, 1, 0);
+    stage_a(0, 0, 0);
+    stage_a(0, 1, 0);
+  }
+  if (nt > 1) {
+    stage_b(1, 0, 1);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // K-step 0 landed, B0 of K-step 1 in flight
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  if (group1) bar();  // the stagger: group 1 runs one barrier behind group 0
+
+  const int bcol = (wc & 1) * 64;
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1, nb = buf ^ 1;
+    const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
+    const bf16_t* SA = smem[buf] + wr * kHalf;
+    const bf16_t* SB = smem[buf] + (2 + (wc >> 1)) * kHalf;
+    v8s af[4][2], bf0[2][2], bf1[2][2];
+    // ---- q0
+    if (more1) stage_b(t + 1, 1, nb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag2<A_KM, PERM, 128>(SA, 16 * i, ks, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bf0[j][ks] = frag2<B_KN, PERM, 128>(SB, bcol + 16 * j, ks, lane);
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i][ks]),
+                                                              __builtin_bit_cast(v8bf, bf0[j][ks]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- q1
+    if (more1) {
+      stage_a(t + 1, 0, nb);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVmQ1) : "memory");  // A hi of this K-step landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bf1[j][ks] = frag2<B_KN, PERM, 128>(SB, bcol + 32 + 16 * j, ks, lane);
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(v8bf, af[i][ks]), __builtin_bit_cast(v8bf, bf1[j][ks]), acc[i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- q2
+    if (more1) stage_a(t + 1, 1, nb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag2<A_KM, PERM, 128>(SA, 64 + 16 * i, ks, lane);
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(v8bf, af[i][ks]), __builtin_bit_cast(v8bf, bf0[j][ks]), acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- q3: B0 of K-step t + 2 into this buffer (every wave's B reads of it retired at q1)
+    if (more2) {
+      stage_b(t + 2, 0, buf);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVmQ3) : "memory");  // K-step t+1 landed but A hi
+    } else if (more1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVmQ3 - 2) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(v8bf, af[i][ks]), __builtin_bit_cast(v8bf, bf1[j][ks]), acc[4 + i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+  if (!group1) bar();  // group 0 catches up the stagger barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  bar();  // the staging LDS becomes the epilogue scratch
+  epilogue_lds<EPI, 8>(acc, ep, M, N, m0 + wr * 128, n0 + wc * 64, lane,
+                       reinterpret_cast<float*>(&smem[0][0]) + wave * kScrFloats);
+}
+
 // v4 selection (MINIPS_GEMM_V4 at start-up, gemm_set_v4_mode() at run time for in-process A/B):
-// 0 off, 1 where the 256x256 tile is picked, 2 every shape
+// 0 off, 1 where the 256x256 tile is picked, 2 every shape; v5 (ping-pong): 3 where the 256x256
+// tile is picked, 4 every shape
 inline int& gemm_v4_mode_ref() {
   static int mode = [] {
     const char* e = std::getenv("MINIPS_GEMM_V4");
@@ -1204,7 +1397,10 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
     }();
     const bool use_v3 = v3 || (wgrad && wgrad_mode == 3);
     const int v4 = gemm_v4_mode();
-    if (v4 == 2 || (v4 == 1 && pick == 256)) {  // 2: v4 for every shape
+    if (EPI != kEpiWdHead && (v4 == 4 || (v4 == 3 && pick == 256))) {
+      dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
+      hipLaunchKernelGGL((gemm_v5_kernel<A_KM, B_KN, EPI>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
+    } else if (v4 == 2 || (v4 == 1 && pick == 256)) {  // 2: v4 for every shape
       dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
       hipLaunchKernelGGL((gemm_v4_kernel<A_KM, B_KN, EPI>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
     } else if (pick == 256 && use_v3) {

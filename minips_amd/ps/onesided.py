@@ -393,6 +393,7 @@ class _AsyncTable:
 
 
 class AsyncSparseTable(_AsyncTable, SparseTable):
+    _local_apply = False  # pushes go to the owners' inboxes: no in-place apply in the backward
     """Row table (equal key ranges, optional routing) with SSP / ASP over the one-sided path.
     Same planning API as SparseTable (plan / plan_async / advance_plan / get / add /
     add_lookup_grads / add_keys / clock), so the models switch transports by construction.

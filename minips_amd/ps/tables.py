@@ -621,6 +621,7 @@ class _PendingPlan:
 
 
 class SparseTable:
+    _local_apply = True  # this rank applies its pushes itself (the one-sided tables' owners apply)
     # hash tables need exact host counts (insert-on-miss must not see padding keys)
     _exact_counts = False
 
@@ -1005,7 +1006,7 @@ class SparseTable:
 
     def _rows_apply_ok(self, plan, dX, dwide, D, x_off) -> bool:
         """One rank, row-wise Adagrad on a local fp32 shard: the embedding backward can apply."""
-        return (self.comm.world == 1 and dX.is_cuda and self.optimizer == "rowwise_adagrad"
+        return (self._local_apply and self.comm.world == 1 and dX.is_cuda and self.optimizer == "rowwise_adagrad"
                 and self.value_dtype == torch.float32 and type(self)._owner_rows is SparseTable._owner_rows
                 and plan.csr is not None and D in (16, 32, 64) and x_off % 4 == 0 and dX.stride(0) % 4 == 0
                 and self.width % 4 == 0 and self.width >= D + (dwide is not None)

@@ -20,3 +20,5 @@ timeout -k 10 200 python tools/bench_models.py --model widedeep-ssp --steps 50 -
 echo "collective ssp $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r4/wd_coll.log)"
 bash tools/r4_prof.sh
 bash tools/r4_markers.sh
+timeout -k 10 500 python tools/bench_models.py --model dlrm-10b --steps 30 --warmup 5 > gpurun_out/r4/dlrm10b_os.log 2>&1
+echo "dlrm-10b onesided: $(tail -1 gpurun_out/r4/dlrm10b_os.log)"
