@@ -654,7 +654,7 @@ void emb_rows_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwi
                       const at::Tensor& members, const at::Tensor& rowstart, const at::Tensor& U_dev,
                       const at::Tensor& uniq, int64_t base, at::Tensor& table, at::Tensor& state,
                       const c10::optional<at::Tensor>& state2, int64_t D1, double lr, double eps, at::Tensor& ws,
-                      int64_t hot, bool sorted_rows) {
+                      at::Tensor& hot_acc, at::Tensor& hot_tick, int64_t hot, bool sorted_rows) {
   TORCH_CHECK(dX.is_cuda(), "dX must be a GPU tensor");  // lookup order may be a column slice
   check_dtype(dX, at::kBFloat16, "dX");
   TORCH_CHECK(dX.dim() == 2 && dX.stride(1) == 1 && dX.stride(0) % 8 == 0, "dX: 2-D, 16-byte aligned rows");
@@ -669,8 +669,15 @@ void emb_rows_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwi
   check_dtype(state, at::kFloat, "state");
   check_dtype(ws, at::kInt, "ws");
   const int64_t U_max = rowstart.numel() - 1;
-  TORCH_CHECK(ws.numel() >= U_max + 1, "ws: >= U + 1 ints");
   TORCH_CHECK(D == 16 || D == 32 || D == 64, "D in {16, 32, 64}");
+  TORCH_CHECK(hot >= 1, "hot >= 1");
+  TORCH_CHECK(ws.is_cuda() && ws.numel() >= minips_k::emb_rows_ws_ints(U_max, (int)hot, (int)D),
+              "ws: >= emb_rows_ws_ints(n, hot, D) ints");
+  check_dtype(hot_acc, at::kFloat, "hot_acc");
+  check_dtype(hot_tick, at::kInt, "hot_tick");
+  const int64_t hmax = minips_k::emb_rows_hot_rows(U_max, (int)hot, (int)D);
+  TORCH_CHECK(hot_acc.is_cuda() && hot_acc.numel() >= hmax * (D + 1) && hot_tick.is_cuda() && hot_tick.numel() >= hmax,
+              "hot_acc: >= emb_rows_hot_rows * (D + 1) floats, hot_tick: >= emb_rows_hot_rows ints (both zero)");
   TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && table.size(1) % 4 == 0 && table.size(1) >= D + 1,
               "table: [rows, W] fp32, W % 4 == 0, W > D");
   const float* dw = nullptr;
@@ -684,8 +691,8 @@ void emb_rows_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwi
   minips_k::emb_rows_adagrad(ptr<bf16_t>(dX), sorted_rows ? 0 : (int)dX.stride(0), dw, (int)F, (int)D,
                              members.data_ptr<int32_t>(), rowstart.data_ptr<int32_t>(), ptr<int64_t>(U_dev), U_max,
                              ptr<int64_t>(uniq), base, ptr<float>(table), (int)table.size(1), (int)table.size(1),
-                             ptr<float>(state), st2, (int)D1, (float)lr, (float)eps, w + 1, w, (int)hot,
-                             stream_of(dX));
+                             ptr<float>(state), st2, (int)D1, (float)lr, (float)eps, w, ptr<float>(hot_acc),
+                             reinterpret_cast<unsigned*>(hot_tick.data_ptr<int32_t>()), (int)hot, stream_of(dX));
 }
 
 void emb_seg_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, int64_t F, int64_t D,
@@ -1303,6 +1310,32 @@ class HostWord {
   uint32_t* d_ = nullptr;
 };
 
+// A same-device stream-ordering event: no timing, no system-scope fence (hipEventDisableSystemFence).
+// The fork / join events of a step order streams of ONE device, which needs agent scope only; the
+// default event's system-scope release on every record cost the W&D step's main queue 7-9 us per
+// fork (rocprofv3 timeline, profiles/r4).
+class FastEvent {
+ public:
+  FastEvent() {
+    TORCH_CHECK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess,
+                "FastEvent: hipEventCreateWithFlags");
+  }
+  ~FastEvent() {
+    if (ev_) (void)hipEventDestroy(ev_);
+  }
+  void record(int64_t stream) {
+    TORCH_CHECK(hipEventRecord(ev_, reinterpret_cast<hipStream_t>(stream)) == hipSuccess, "FastEvent: record");
+  }
+  void wait(int64_t stream) {
+    TORCH_CHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev_, 0) == hipSuccess, "FastEvent: wait");
+  }
+  bool query() { return hipEventQuery(ev_) == hipSuccess; }
+  void synchronize() { TORCH_CHECK(hipEventSynchronize(ev_) == hipSuccess, "FastEvent: synchronize"); }
+
+ private:
+  hipEvent_t ev_ = nullptr;
+};
+
 // pos[members[m]] = m: where the dgrad's permuted-rows epilogue puts each lookup's gradient row.
 at::Tensor emb_csr_positions(const at::Tensor& members) {
   check_gpu(members, "members");
@@ -1530,6 +1563,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("EPI_BIAS_GELU_AUX_BF16") = (int)minips_k::kEpiBiasGeluAuxBf16;
   m.attr("EPI_GELU_GRAD_BF16") = (int)minips_k::kEpiGeluGradBf16;
   m.def("gemm_set_v4_mode", [](int64_t m) { minips_k::gemm_set_v4_mode((int)m); });
+  m.def("gemm_set_fold", [](int64_t on) { minips_k::gemm_set_fold((int)on); });
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("a_km"), py::arg("b_kn"), py::arg("epi"), py::arg("bias"), py::arg("mask"), py::arg("colsum"),
         py::arg("alpha") = 1.0, py::arg("split_k") = 1, py::arg("batch") = 1, py::arg("inner") = 1,
@@ -1577,6 +1611,10 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
         py::arg("members") = py::none(), py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);
+  m.def("emb_rows_ws_ints",
+        [](int64_t n, int64_t hot, int64_t D) { return minips_k::emb_rows_ws_ints(n, (int)hot, (int)D); });
+  m.def("emb_rows_hot_rows",
+        [](int64_t n, int64_t hot, int64_t D) { return minips_k::emb_rows_hot_rows(n, (int)hot, (int)D); });
   m.def("emb_rows_adagrad", &emb_rows_adagrad);
   m.def("emb_seg_adagrad", &emb_seg_adagrad);
   m.def("colsum_bf16", &colsum_bf16);
@@ -1617,6 +1655,12 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("PS_CTRL_BYTES") = minips_k::kPsCtrlBytes;
   m.attr("PS_CTRL_LINE") = minips_k::kPsCtrlLine;
   m.attr("PS_HELD_SLOTS") = minips_k::kPsHeldSlots;
+  py::class_<FastEvent>(m, "FastEvent")
+      .def(py::init<>())
+      .def("record", &FastEvent::record)
+      .def("wait", &FastEvent::wait)
+      .def("query", &FastEvent::query)
+      .def("synchronize", &FastEvent::synchronize);
   py::class_<HostWord>(m, "HostWord")
       .def(py::init<>())
       .def_property_readonly("value", &HostWord::value)

@@ -3,12 +3,47 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <vector>
+#include <algorithm>
 
 #include "gemm_kernels.h"
 
 namespace minips_k {
 
 void gemm_set_v4_mode(int mode) { gemm_v4_mode_ref() = mode; }
+
+// split-K fold (kEpiFoldF32) instead of the separate slab reduce: MINIPS_SPLITK_FOLD=1 (default 0
+// until measured in the W&D step); gemm_set_fold() switches it at run time (in-process A/B)
+static int& fold_mode() {
+  static int m = [] {
+    const char* e = std::getenv("MINIPS_SPLITK_FOLD");
+    return e ? std::atoi(e) : 0;
+  }();
+  return m;
+}
+void gemm_set_fold(int on) { fold_mode() = on; }
+
+// per-(device, stream) tile ticket counters of the fold: zeroed once, re-zeroed by every tile's
+// last K slice, so back-to-back GEMMs on one stream reuse them (kernel boundaries order them)
+static unsigned* fold_counters(hipStream_t s, int64_t tiles) {
+  struct Entry {
+    int dev;
+    hipStream_t s;
+    unsigned* p;
+    int64_t n;
+  };
+  static thread_local std::vector<Entry> cache;
+  int dev = 0;
+  MINIPS_HIP_CHECK(hipGetDevice(&dev));
+  for (auto& e : cache)
+    if (e.dev == dev && e.s == s && e.n >= tiles) return e.p;
+  const int64_t n = std::max<int64_t>(tiles, 1 << 16);
+  unsigned* p = nullptr;
+  MINIPS_HIP_CHECK(hipMalloc(&p, n * sizeof(unsigned)));
+  MINIPS_HIP_CHECK(hipMemset(p, 0, n * sizeof(unsigned)));
+  cache.push_back({dev, s, p, n});
+  return p;
+}
 
 static int dispatch_layout(bool a_km, bool b_kn, int epi, const bf16_t* A, const bf16_t* B, int M, int N, int K,
                            int lda, int ldb, int split_k, const EpiArgs& ep, int batch, hipStream_t s) {
@@ -103,6 +138,19 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
     // split-K without atomics: every K slice stores its partial tile into its own slab plane,
     // one streaming kernel adds the planes into C (measured faster than fp32 atomics)
     EpiArgs sp{slab, N, nullptr, nullptr, 0, nullptr, alpha, 1, 0, 0, 0, 0, 0, 0, (int64_t)M * N, nullptr, 0};
+    if (!bf16_out && fold_mode()) {
+      // the K slices' planes fold inside the GEMM: the tile's last slice adds them into C
+      const int kper = (K + split_k - 1) / split_k;
+      const int kc = (kper + 63) / 64 * 64;
+      sp.fold_out = (float*)C;
+      sp.fold_ldc = ldc;
+      sp.fold_nsplit = (K + kc - 1) / kc;  // == the launcher's nsplit (v2: BK = 64 chunks)
+      sp.fold_cnt = fold_counters(s, (int64_t)((M + 127) / 128) * ((N + 127) / 128));
+      nsplit = dispatch_layout(a_km, b_kn, kEpiFoldF32, A, B, M, N, K, lda, ldb, split_k, sp, batch, s);
+      if (nsplit != sp.fold_nsplit) throw std::runtime_error("gemm: split-K fold slice count mismatch");
+      MINIPS_HIP_CHECK(hipGetLastError());
+      return;
+    }
     nsplit = dispatch_layout(a_km, b_kn, kEpiStoreF32, A, B, M, N, K, lda, ldb, split_k, sp, batch, s);
     MINIPS_HIP_CHECK(hipGetLastError());
     if (bf16_out)

@@ -32,6 +32,7 @@
 namespace minips_k {
 
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128;
 
@@ -127,6 +128,12 @@ struct EpiArgs {
   float* head_dh_colsum = nullptr;    // [N] (stride head_dh_colsum_ld) += column sums of dH (optional)
   int head_dh_colsum_ld = 1;
   int colsum_ld = 1;                  // kEpiReluMaskBf16: colsum[col * colsum_ld] (a column of a matrix)
+  // kEpiFoldF32: C is this K slice's slab plane; the tile's last slice adds every plane into
+  // fold_out (ldc fold_ldc); fold_cnt[tile] counts the slices that arrived (the last one re-zeroes it)
+  float* fold_out = nullptr;
+  int fold_ldc = 0;
+  unsigned* fold_cnt = nullptr;
+  int fold_nsplit = 1;
 };
 
 // Destination of an output row segment (kEpiPermRowsBf16: the permuted row of its segment).
@@ -254,7 +261,7 @@ __device__ __forceinline__ float epi_apply(float v, float bias, float m, bf16_t*
 template <int EPI, int MR>
 __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiArgs& ep, int M, int N, int mb, int nb,
                                              int lane, float* __restrict__ scr) {
-  constexpr bool F32OUT = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
+  constexpr bool F32OUT = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32 || EPI == kEpiFoldF32;
   constexpr bool HAS_BIAS = EPI == kEpiBiasReluBf16 || EPI == kEpiBiasBf16 || EPI == kEpiBiasGeluBf16 ||
                             EPI == kEpiBiasGeluAuxBf16 || EPI == kEpiBiasGeluDAuxBf16;
   constexpr bool READ_MASK = EPI == kEpiReluMaskBf16 || EPI == kEpiGeluGradBf16 || EPI == kEpiMulAuxBf16;
@@ -307,6 +314,21 @@ __device__ __forceinline__ void epilogue_lds(const v4f (&acc)[MR][4], const EpiA
         if (row >= M) continue;
         float4 v = *reinterpret_cast<const float4*>(scr + rr * kScrPitch + c4);
         float* dst = ((float*)ep.C) + (int64_t)row * ep.ldc + col;
+        if constexpr (EPI == kEpiFoldF32) {
+          // write-through (sc1) stores: the folding workgroup reads them on another CU / XCD
+          // after one agent-scope acquire, no release fence (cdna_hip_programming.md G16, R1)
+          if (c_vec && col + 4 <= N) {
+            const __amdgpu_buffer_rsrc_t rc =
+                __builtin_amdgcn_make_buffer_rsrc(ep.C, (short)0, 0x7ffffff0, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rc,
+                                                   (int)(((int64_t)row * ep.ldc + col) * 4), 0, 16);
+          } else {
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+            for (int e = 0; e < 4; ++e)
+              if (col + e < N) __hip_atomic_store(dst + e, vv[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          continue;
+        }
         if (c_vec && col + 4 <= N) {
           if (EPI == kEpiAccumF32) {
             const float4 o = *reinterpret_cast<const float4*>(dst);
@@ -464,7 +486,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
     const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
-    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32 || EPI == kEpiFoldF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const int ke = min(K, kb + k_chunk);
@@ -700,6 +722,62 @@ __device__ __forceinline__ void wd_head_epilogue(v4f (&acc)[4][4], const EpiArgs
   }
 }
 
+// kEpiFoldF32 tail of a split-K workgroup (after its slab plane was stored write-through): one
+// relaxed agent-scope ticket per tile; the K slice drawing the last ticket acquires (agent scope:
+// this CU's L1 drops the planes' lines) and adds the tile's nsplit planes into ep.fold_out.
+// Correct for any placement of a tile's slices over CUs / XCDs (cdna_hip_programming.md G16 R1).
+template <int TM, int TN>
+__device__ __forceinline__ void splitk_fold(const EpiArgs& ep, int M, int N, int m0, int n0, int tile,
+                                            unsigned* __restrict__ flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its plane stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ep.fold_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = t == (unsigned)ep.fold_nsplit - 1;
+    if (last) {
+      __hip_atomic_store(ep.fold_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const int64_t plane = ep.sc_split;
+  const float* p0 = (const float*)ep.C - (int64_t)blockIdx.z * plane;
+  constexpr int PER_ROW = TN / 4;
+  for (int i = threadIdx.x; i < TM * PER_ROW; i += blockDim.x) {
+    const int rr = i / PER_ROW, c4 = (i - rr * PER_ROW) * 4;
+    const int row = m0 + rr, col = n0 + c4;
+    if (row >= M || col >= N) continue;
+    const float* p = p0 + (int64_t)row * ep.ldc + col;
+    float4 a = *reinterpret_cast<const float4*>(p);
+    int z = 1;
+    for (; z + 3 < ep.fold_nsplit; z += 4) {
+      const float4 b0 = *reinterpret_cast<const float4*>(p + z * plane);
+      const float4 b1 = *reinterpret_cast<const float4*>(p + (z + 1) * plane);
+      const float4 b2 = *reinterpret_cast<const float4*>(p + (z + 2) * plane);
+      const float4 b3 = *reinterpret_cast<const float4*>(p + (z + 3) * plane);
+      a.x += (b0.x + b1.x) + (b2.x + b3.x);
+      a.y += (b0.y + b1.y) + (b2.y + b3.y);
+      a.z += (b0.z + b1.z) + (b2.z + b3.z);
+      a.w += (b0.w + b1.w) + (b2.w + b3.w);
+    }
+    for (; z < ep.fold_nsplit; ++z) {
+      const float4 b = *reinterpret_cast<const float4*>(p + z * plane);
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    float* o = ep.fold_out + (int64_t)row * ep.fold_ldc + col;
+    o[0] += a.x;
+    o[1] += a.y;
+    o[2] += a.z;
+    o[3] += a.w;
+  }
+}
+
 // TM x TN output tile, (TM/64) x (TN/64) waves of 64x64 each (4, 8 or 16 waves). 128x128
 // keeps 2 workgroups per CU; the 256-wide tiles halve the L2->LDS bytes per MFMA (the loads,
 // not the MFMAs, bound this kernel at these sizes) and run one 16- or 8-wave workgroup per CU.
@@ -729,7 +807,7 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
     const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
-    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32 || EPI == kEpiFoldF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
@@ -784,11 +862,14 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
   }
   if constexpr (EPI == kEpiWdHead)
     wd_head_epilogue<TM, TN>(acc, ep, M, N, m0, wm, wn, lane, reinterpret_cast<float*>(&smem[0][0]));
-  else if (kLdsEpilogue)
+  else if (kLdsEpilogue || EPI == kEpiFoldF32)
     epilogue_lds<EPI, 4>(acc, ep, M, N, m0 + wm * 64, n0 + wn * 64, lane,
                          reinterpret_cast<float*>(&smem[0][0]) + wave * kScrFloats);
   else
     epilogue<EPI>(acc, ep, M, N, m0, n0, wm, wn, lane);
+  if constexpr (EPI == kEpiFoldF32)  // (the flag word lies past every wave's epilogue scratch)
+    splitk_fold<TM, TN>(ep, M, N, m0, n0, bid,
+                        reinterpret_cast<unsigned*>(reinterpret_cast<float*>(&smem[0][0]) + NWAVES * kScrFloats));
 }
 
 // ================================================================ v3: 256x256, 8 waves, phase-split K-step
@@ -830,7 +911,7 @@ __global__ __launch_bounds__(512) void gemm_v3_kernel(const bf16_t* __restrict__
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
     const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
-    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32 || EPI == kEpiFoldF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
@@ -1028,7 +1109,7 @@ __global__ __launch_bounds__(512) void gemm_v4_kernel(const bf16_t* __restrict__
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
     const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
-    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32 || EPI == kEpiFoldF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
@@ -1174,7 +1255,7 @@ __global__ __launch_bounds__(512) void gemm_v5_kernel(const bf16_t* __restrict__
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
     const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
-    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32 || EPI == kEpiFoldF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
@@ -1367,7 +1448,9 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
     return std::string(e) == "v3" ? 3 : (std::string(e) == "v2" ? 2 : 1);
   }();
   const bool wgrad = A_KM && B_KN;
-  if (gemm_impl() == 2 && (!wgrad || wgrad_mode >= 2) && a_ext * 2 < 0x7ff00000ll && b_ext * 2 < 0x7ff00000ll) {
+  const bool v2_ok = a_ext * 2 < 0x7ff00000ll && b_ext * 2 < 0x7ff00000ll;
+  if (EPI == kEpiFoldF32 && !v2_ok) throw std::runtime_error("gemm: the split-K fold needs operands < 2 GiB (v2)");
+  if ((EPI == kEpiFoldF32 || (gemm_impl() == 2 && (!wgrad || wgrad_mode >= 2))) && v2_ok) {
     const int kper = (K + split_k - 1) / split_k;
     const int kc = (kper + BK2 - 1) / BK2 * BK2;
     const int nsplit = (K + kc - 1) / kc;
@@ -1395,8 +1478,8 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
       const char* e = std::getenv("MINIPS_GEMM_V3_EARLY");
       return !e || std::atoi(e) != 0;
     }();
-    const bool use_v3 = v3 || (wgrad && wgrad_mode == 3);
-    const int v4 = gemm_v4_mode();
+    const bool use_v3 = EPI != kEpiFoldF32 && (v3 || (wgrad && wgrad_mode == 3));
+    const int v4 = EPI == kEpiFoldF32 ? 0 : gemm_v4_mode();  // the fold tail lives in v2 only
     if (EPI != kEpiWdHead && (v4 == 4 || (v4 == 3 && pick == 256))) {
       dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
       hipLaunchKernelGGL((gemm_v5_kernel<A_KM, B_KN, EPI>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
@@ -1426,7 +1509,8 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
     }
     return nsplit;
   }
-  if (EPI == kEpiXentStatsBf16) throw std::runtime_error("gemm: the xent-stats epilogue needs the v2 kernel");
+  if (EPI == kEpiXentStatsBf16 || EPI == kEpiFoldF32)
+    throw std::runtime_error("gemm: the xent-stats / split-K fold epilogues need the v2 kernel");
   // BK=64 halves the barriers per FLOP; short K chunks keep BK=32 (less tail waste).
   const int kper = (K + split_k - 1) / split_k;
   static const int forced = [] {
@@ -1465,6 +1549,7 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
     MINIPS_EPI_CASE(AKM, BKN, kEpiAccumF32)                                      \
     MINIPS_EPI_CASE(AKM, BKN, kEpiBiasGeluDAuxBf16)                              \
     MINIPS_EPI_CASE(AKM, BKN, kEpiMulAuxBf16)                                    \
+    MINIPS_EPI_CASE(AKM, BKN, kEpiFoldF32)                                       \
     case kEpiXentStatsBf16:                                                      \
       if constexpr (!AKM && !BKN) {                                              \
         nsplit = launch<false, false, kEpiXentStatsBf16>(A, B, M, N, K, lda, ldb, split_k, ep, batch, s); \

@@ -39,9 +39,14 @@ enum GemmEpilogue {
   // derivative (kEpiMulAuxBf16) instead of re-evaluating tanh of the saved pre-activation
   kEpiBiasGeluDAuxBf16 = 13,
   kEpiMulAuxBf16 = 14,  // C bf16 = acc * mask(aux)
+  // split-K slab plane written through (sc1) + in-kernel fold: the last K slice of a tile to
+  // arrive adds the tile's nsplit planes into the fp32 output (no separate reduce launch; v2 only)
+  kEpiFoldF32 = 15,
 };
 // v4 GEMM selection at run time (in-process A/B): 0 off, 1 where 256x256 tiles are picked, 2 always
 void gemm_set_v4_mode(int mode);
+// split-K fold (kEpiFoldF32) instead of the slab reduce kernel: 0 off, 1 on (in-process A/B)
+void gemm_set_fold(int on);
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
                float alpha, int split_k, hipStream_t s);
@@ -182,16 +187,18 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
 // rowstart[u] = first member of row u, rowstart[U] = B*F)
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
 void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s);
-// Embedding backward + row-wise Adagrad of one rank, row-parallel over the row-sorted lookups
-// (dX [total, D] bf16 in member order, rowstart [U + 1] from plan_sorted): rows with at most
-// `hot` lookups are summed and applied by one lane group each; hotter rows are queued (hot_list /
-// hot_count: zeroed by the call) and reduced by a workgroup each.
+// Embedding backward + row-wise Adagrad of one rank, row-parallel over the lookups of each unique
+// row (rowstart [U + 1] from plan_sorted): rows with at most `hot` lookups are summed and applied by
+// one lane group each; hotter rows are cut into workgroup chunks (ws: emb_rows_ws_ints scratch
+// ints, zero at allocation; every call leaves its counters zero) whose partial sums meet in hot_acc
+// ([emb_rows_hot_rows][D + 1] fp32) / hot_tick (ints): both zero before and after every call.
 // ldx: 0 = dX row-sorted [total, D] (member order); > 0 = lookup order [B, ldx >= F*D].
 void emb_rows_adagrad(const bf16_t* dX, int ldx, const float* dwide, int F, int D, const int* members,
-                      const int* rowstart,
-                      const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base, float* table, int ld,
-                      int W, float* state, float* state2, int D1, float lr, float eps, int* hot_list, int* hot_count,
-                      int hot, hipStream_t s);
+                      const int* rowstart, const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base,
+                      float* table, int ld, int W, float* state, float* state2, int D1, float lr, float eps,
+                      int* ws, float* hot_acc, unsigned* hot_tick, int hot, hipStream_t s);
+int64_t emb_rows_ws_ints(int64_t n, int hot, int D);
+int64_t emb_rows_hot_rows(int64_t n, int hot, int D);
 // Embedding backward fused with the row-wise Adagrad apply (one rank, local shard): the rows of
 // uniq[memrow] get Adagrad with the segment sums of their lookups' dX rows (+ dwide at column D)
 // without a grad_rows buffer. scr: [U, scr_ld >= D+1] fp32, all zero before and after the call.

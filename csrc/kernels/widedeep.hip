@@ -1235,9 +1235,13 @@ __global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __r
                                                                const int* __restrict__ members,
                                                                const int* __restrict__ rowstart,
                                                                const int64_t* __restrict__ U_dev, int64_t U_max,
-                                                               RowsAdagradArgs a, int* __restrict__ hot_list,
-                                                               int* __restrict__ hot_count, int hot) {
-  constexpr int L = D / 8, PER = 64 / L;
+                                                               RowsAdagradArgs a, int* __restrict__ ws,
+                                                               int hmax, int hot) {
+  constexpr int L = D / 8, PER = 64 / L, CHW = 8 * (256 / L);
+  int* cnt = ws;  // {hot rows, chunks, hot-kernel block ticket}
+  int* hot_row = ws + 4;
+  int* hot_need = hot_row + hmax;
+  int2* chunk = reinterpret_cast<int2*>(hot_need + hmax + (hmax & 1));
   const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
   const bool wide = dwide != nullptr;
   const int64_t U = min(U_max, *U_dev);
@@ -1248,7 +1252,13 @@ __global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __r
     const bool ok = u < U;
     const int s = ok ? rowstart[u] : 0, e = ok ? rowstart[u + 1] : 0;
     const bool cold = ok && e - s <= hot;
-    if (ok && !cold && l == 0) hot_list[atomicAdd(hot_count, 1)] = (int)u;
+    if (ok && !cold && l == 0) {  // a hot row: its chunks go to emb_hot_adagrad_kernel
+      const int h = atomicAdd(cnt, 1), nc = (e - s + CHW - 1) / CHW;
+      const int c0 = atomicAdd(cnt + 1, nc);
+      hot_row[h] = (int)u;
+      hot_need[h] = nc;
+      for (int k = 0; k < nc; ++k) chunk[c0 + k] = make_int2(h, k);
+    }
     // the row's current values and state: independent of the sum, loaded ahead of it
     const int64_t trow = cold ? a.uniq[u] - a.base : 0;
     float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0;
@@ -1285,86 +1295,162 @@ __global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __r
   }
 }
 
-// One workgroup per hot row: 256 / L lane groups stride over the row's lookups, an LDS reduction
-// folds them, and wave 0 applies the update (lane c: column c; lane 0: the wide column).
+// Hot rows in workgroup chunks of G * 8 lookups (G = 256 / L lane groups, 8 loads in flight per
+// lane): a chunk folds in LDS; a row of one chunk is applied by that workgroup, a longer row's
+// chunks add their partial rows into hot_acc (memory-side fp32 atomics, one per column per chunk:
+// a row thousands of lookups long costs ~10 atomics per address, not thousands) and draw a ticket;
+// the row's last chunk applies (agent-scope acquire, then the sums) and re-zeroes hot_acc / the
+// ticket for the next call. The cold kernel wrote the chunk list: ws = {hot rows, chunks, block
+// ticket, pad, hot_row [Hmax], hot_need [Hmax], chunk (hot index, chunk index) [Cmax]}; the hot
+// kernel's last block re-zeroes the counters.
+template <int D>
+__device__ __forceinline__ void hot_apply(const RowsAdagradArgs& a, int64_t trow, int t, float v, float vw,
+                                          bool wide) {
+  const float sq = warp_sum(t < D ? v * v : 0.f);
+  const float sqw = wide ? vw * vw : 0.f;
+  const bool split = a.D1 < a.W;
+  const float st1 = a.state[trow] + (split ? sq : sq + sqw) / (float)a.D1;
+  const float st2 = split ? a.state2[trow] + sqw / (float)(a.W - a.D1) : 0.f;
+  const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
+  float* tr = a.table + trow * (int64_t)a.ld;
+  if (t < D) tr[t] -= s1 * v;
+  if (t == 0 && wide) tr[D] -= s2 * vw;
+  if (t == 0) {
+    a.state[trow] = st1;
+    if (split) a.state2[trow] = st2;
+  }
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void emb_hot_adagrad_kernel(const bf16_t* __restrict__ dX, int ldx,
                                                               const float* __restrict__ dwide, int F,
                                                               const int* __restrict__ members,
                                                               const int* __restrict__ rowstart, RowsAdagradArgs a,
-                                                              const int* __restrict__ hot_list,
-                                                              const int* __restrict__ hot_count) {
-  constexpr int L = D / 8, G = 256 / L;
+                                                              int* __restrict__ ws, int hmax,
+                                                              float* __restrict__ hot_acc,
+                                                              unsigned* __restrict__ hot_tick) {
+  constexpr int L = D / 8, G = 256 / L, CHW = 8 * G;
   __shared__ float red[G][D + 1];
   const int t = threadIdx.x, g = t / L, l = t % L;
   const bool wide = dwide != nullptr;
-  const int n = *hot_count;
-  for (int h = blockIdx.x; h < n; h += gridDim.x) {
-    const int u = hot_list[h];
-    const int s = rowstart[u], e = rowstart[u + 1];
+  const int* hot_row = ws + 4;
+  const int* hot_need = hot_row + hmax;
+  const int2* chunk = reinterpret_cast<const int2*>(hot_need + hmax);
+  const int nch = ws[1];
+  for (int c = blockIdx.x; c < nch; c += gridDim.x) {
+    const int2 hk = chunk[c];
+    const int u = hot_row[hk.x], need = hot_need[hk.x];
+    const int s = rowstart[u] + hk.y * CHW, e = min(rowstart[u + 1], s + CHW);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float accw = 0.f;
-    for (int m = s + g; m < e; m += 2 * G) {
-      const bool in2 = m + G < e;
-      const int j0 = (ldx || wide) ? members[m] : 0, j1 = (in2 && (ldx || wide)) ? members[m + G] : 0;
-      const uint4 v0 = *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, m, j0) + 8 * l);
-      const uint4 v1 =
-          in2 ? *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, m + G, j1) + 8 * l) : make_uint4(0, 0, 0, 0);
-      if (wide && l == 0) {
-        accw += dwide[j0 / F];
-        if (in2) accw += dwide[j1 / F];
-      }
-      acc_bf16x8(acc, v0);
-      acc_bf16x8(acc, v1);
+    int jj[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int m = s + g + q * G;
+      jj[q] = (m < e && (ldx || wide)) ? members[m] : 0;
     }
+    uint4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int m = s + g + q * G;
+      v[q] = m < e ? *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, m, jj[q]) + 8 * l)
+                   : make_uint4(0, 0, 0, 0);
+      if (wide && l == 0 && m < e) accw += dwide[jj[q] / F];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc_bf16x8(acc, v[q]);
 #pragma unroll
     for (int q = 0; q < 8; ++q) red[g][8 * l + q] = acc[q];
     if (l == 0) red[g][D] = accw;
     __syncthreads();
     if (t < 64) {  // wave 0: lane c < D folds column c, lane 0 also the wide column
-      float v = 0.f, vw = 0.f;
+      float vv = 0.f, vw = 0.f;
       if (t < D)
-        for (int k = 0; k < G; ++k) v += red[k][t];
+        for (int k = 0; k < G; ++k) vv += red[k][t];
       if (t == 0 && wide)
         for (int k = 0; k < G; ++k) vw += red[k][D];
-      vw = __shfl(vw, 0, 64);
-      const float sq = warp_sum(t < D ? v * v : 0.f);
-      const float sqw = wide ? vw * vw : 0.f;
       const int64_t trow = a.uniq[u] - a.base;
-      const bool split = a.D1 < a.W;
-      const float st1 = a.state[trow] + (split ? sq : sq + sqw) / (float)a.D1;
-      const float st2 = split ? a.state2[trow] + sqw / (float)(a.W - a.D1) : 0.f;
-      const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
-      float* tr = a.table + trow * (int64_t)a.ld;
-      if (t < D) tr[t] -= s1 * v;
-      if (t == 0 && wide) tr[D] -= s2 * vw;
-      if (t == 0) {
-        a.state[trow] = st1;
-        if (split) a.state2[trow] = st2;
+      if (need == 1) {
+        hot_apply<D>(a, trow, t, vv, __shfl(vw, 0, 64), wide);
+      } else {
+        float* ha = hot_acc + (int64_t)hk.x * (D + 1);
+        if (t < D) atomicAdd(ha + t, vv);
+        if (t == 0 && wide) atomicAdd(ha + D, vw);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adds performed before its ticket
+        unsigned last = 0;
+        if (t == 0) {
+          last = __hip_atomic_fetch_add(hot_tick + hk.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned)need - 1;
+          if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        }
+        last = __shfl(last, 0, 64);
+        if (last) {  // every chunk of the row has added: its sum is complete
+          const float sv = t < D ? __hip_atomic_load(ha + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+          const float sw = wide ? __hip_atomic_load(ha + D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+          hot_apply<D>(a, trow, t, sv, sw, wide);
+          if (t < D) __hip_atomic_store(ha + t, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (t == 0) {
+            if (wide) __hip_atomic_store(ha + D, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(hot_tick + hk.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
       }
     }
-    __syncthreads();  // red is reused by the next hot row
+    __syncthreads();  // red is reused by the next chunk
   }
+  // the last block to finish zeroes the counters for the next call (every block read them at its
+  // start): no memset node in front of every call (7 us of queue time per W&D step), graph-safe
+  if (t == 0 && atomicAdd(ws + 2, 1) == (int)gridDim.x - 1) {
+    ws[0] = 0;
+    ws[1] = 0;
+    ws[2] = 0;
+  }
+}
+
+// hot-row capacities of emb_rows_adagrad for n lookups and threshold hot: rows with more than
+// `hot` lookups (Hmax) and their chunks (Cmax)
+static inline void rows_hot_caps(int64_t n, int hot, int D, int64_t& hmax, int64_t& cmax) {
+  const int chw = 8 * (256 / (D / 8));
+  hmax = n / (hot + 1) + 1;
+  cmax = hmax + n / chw + 1;
+}
+
+int64_t emb_rows_ws_ints(int64_t n, int hot, int D) {
+  int64_t hmax, cmax;
+  rows_hot_caps(n, hot, D, hmax, cmax);
+  return 4 + 2 * hmax + 2 * cmax;
+}
+
+int64_t emb_rows_hot_rows(int64_t n, int hot, int D) {
+  int64_t hmax, cmax;
+  rows_hot_caps(n, hot, D, hmax, cmax);
+  return hmax;
 }
 
 void emb_rows_adagrad(const bf16_t* dX, int ldx, const float* dwide, int F, int D, const int* members,
                       const int* rowstart, const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base,
                       float* table, int ld, int W, float* state, float* state2, int D1, float lr, float eps,
-                      int* hot_list, int* hot_count, int hot, hipStream_t s) {
+                      int* ws, float* hot_acc, unsigned* hot_tick, int hot, hipStream_t s) {
   if (U_max <= 0) return;
   if (ld % 4 || reinterpret_cast<uintptr_t>(table) % 16 || reinterpret_cast<uintptr_t>(dX) % 16 || ldx % 8)
     throw std::runtime_error("emb_rows_adagrad: 16-byte aligned rows");
   if (D1 <= 0 || D1 > W) D1 = W;
   if (D1 < W && !state2) throw std::runtime_error("emb_rows_adagrad: split rows need state2");
+  if (D != 16 && D != 32 && D != 64) throw std::runtime_error("emb_rows_adagrad: D must be 16, 32 or 64");
+  int64_t hmax, cmax;
+  rows_hot_caps(U_max, hot, D, hmax, cmax);  // U_max = the lookups (rowstart has n + 1 entries)
   const RowsAdagradArgs a{uniq, base, table, ld, W, D1, state, state2, lr, eps};
-  MINIPS_HIP_CHECK(hipMemsetAsync(hot_count, 0, sizeof(int), s));
   const int per_block = 4 * (64 / (D / 8));
   const int grid = (int)std::min<int64_t>((U_max + per_block - 1) / per_block, 8192);
+  const int hgrid = (int)std::min<int64_t>(cmax, 2048);
 #define MINIPS_ROWS_ADA(DD)                                                                                      \
   hipLaunchKernelGGL((emb_rows_adagrad_kernel<DD>), grid, 256, 0, s, dX, ldx, dwide, F, members, rowstart,     \
-                     U_dev, U_max, a, hot_list, hot_count, hot);                                                  \
-  hipLaunchKernelGGL((emb_hot_adagrad_kernel<DD>), 256, 256, 0, s, dX, ldx, dwide, F, members, rowstart, a,      \
-                     hot_list, hot_count);
+                     U_dev, U_max, a, ws, (int)hmax, hot);                                                        \
+  hipLaunchKernelGGL((emb_hot_adagrad_kernel<DD>), hgrid, 256, 0, s, dX, ldx, dwide, F, members, rowstart, a, ws, \
+                     (int)hmax, hot_acc, hot_tick);
   switch (D) {
     case 16:
       MINIPS_ROWS_ADA(16)
@@ -1372,11 +1458,9 @@ void emb_rows_adagrad(const bf16_t* dX, int ldx, const float* dwide, int F, int 
     case 32:
       MINIPS_ROWS_ADA(32)
       break;
-    case 64:
+    default:
       MINIPS_ROWS_ADA(64)
       break;
-    default:
-      throw std::runtime_error("emb_rows_adagrad: D must be 16, 32 or 64");
   }
 #undef MINIPS_ROWS_ADA
   MINIPS_HIP_CHECK(hipGetLastError());

@@ -9,6 +9,7 @@ Linear        bias folded into the weight: W_ext [n_out, k_pad] with the bias in
 from __future__ import annotations
 
 import contextlib
+import os
 
 import math
 
@@ -123,6 +124,9 @@ def compute_priority() -> int:
     return -1 if os.environ.get("MINIPS_COMPUTE_PRIORITY", "0") == "1" else 0
 
 
+_FAST_EVENTS = os.environ.get("MINIPS_FAST_EVENTS", "1") != "0"
+
+
 class SideStream:
     """Fork-join helper: independent work (weight gradients) issued on a second HIP stream.
 
@@ -134,8 +138,15 @@ class SideStream:
         self.stream = torch.cuda.Stream(device=device, priority=compute_priority()) \
             if enabled and torch.device(device).type == "cuda" else None
         # fork / join events are re-recorded every step (a wait binds to the record issued before
-        # it): no event objects created and destroyed per fork
-        self._evs = [torch.cuda.Event() for _ in range(8)] if self.stream is not None else []
+        # it): no event objects created and destroyed per fork. Same-device ordering only, so
+        # fence-free native events (ops_py FastEvent, MINIPS_FAST_EVENTS=0: torch events)
+        self._fast = self.stream is not None and _FAST_EVENTS
+        if self._fast:
+            from .._native import kernels
+
+            self._evs = [kernels().FastEvent() for _ in range(8)]
+        else:
+            self._evs = [torch.cuda.Event() for _ in range(8)] if self.stream is not None else []
         self._ev_i = 0
 
     def _event(self):
@@ -150,8 +161,12 @@ class SideStream:
             return
         cur = torch.cuda.current_stream(self.stream.device)
         ev = self._event()
-        ev.record(cur)
-        self.stream.wait_event(ev)
+        if self._fast:
+            ev.record(cur.cuda_stream)
+            ev.wait(self.stream.cuda_stream)
+        else:
+            ev.record(cur)
+            self.stream.wait_event(ev)
         prev = ops.overlap_mode(True)  # forked work: GEMM splits chosen for throughput, not latency
         try:
             with torch.cuda.stream(self.stream):
@@ -162,18 +177,26 @@ class SideStream:
     def join(self):
         if self.stream is not None:
             ev = self._event()
-            ev.record(self.stream)
-            torch.cuda.current_stream(self.stream.device).wait_event(ev)
+            if self._fast:
+                ev.record(self.stream.cuda_stream)
+                ev.wait(torch.cuda.current_stream(self.stream.device).cuda_stream)
+            else:
+                ev.record(self.stream)
+                torch.cuda.current_stream(self.stream.device).wait_event(ev)
 
     def mark(self):
         """Event after the work forked so far (None when disabled)."""
         if self.stream is None:
             return None
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event()  # (a torch event: callers hand it to torch streams)
         ev.record(self.stream)
         return ev
 
     def wait(self, ev):
         """The current stream waits for ``ev`` (before it overwrites a buffer forked work reads)."""
-        if ev is not None:
+        if ev is None:
+            return
+        if self._fast and not isinstance(ev, torch.cuda.Event):
+            ev.wait(torch.cuda.current_stream(self.stream.device).cuda_stream)
+        else:
             torch.cuda.current_stream(self.stream.device).wait_event(ev)

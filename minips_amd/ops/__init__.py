@@ -563,20 +563,33 @@ def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=No
     return grad_rows
 
 
-def emb_rows_adagrad(dX, dwide, F, D, csr, U_dev, uniq, base, table, state, state2, split, lr, eps, ws, hot=32,
+def emb_rows_workspace(n, D, device, hot=16):
+    """Scratch of emb_rows_adagrad for n lookups: (ints, hot_acc, hot_tick, hot). Keep it per table
+    and reuse it on one stream: the counters / hot_acc / hot_tick are zero at allocation and every
+    call leaves them zero."""
+    k = kernels()
+    ws = torch.zeros(k.emb_rows_ws_ints(n, hot, D), dtype=torch.int32, device=device)
+    h = k.emb_rows_hot_rows(n, hot, D)
+    return (ws, torch.zeros(h * (D + 1), dtype=torch.float32, device=device),
+            torch.zeros(h, dtype=torch.int32, device=device), hot)
+
+
+def emb_rows_adagrad(dX, dwide, F, D, csr, U_dev, uniq, base, table, state, state2, split, lr, eps, ws,
                      sorted_rows=True):
     """Row-parallel embedding backward + row-wise Adagrad of one rank (widedeep.hip). csr =
     (members, memrow, positions, rowstart) of plan_sorted: row u owns members [rowstart[u],
     rowstart[u+1]); it sums their gradient rows (+ dwide of their samples at column D) and gets
     sparse_rowwise_adagrad in place. dX bf16: ``sorted_rows`` [total, D] in member order, else
-    [B, >= F*D] in lookup order (row of lookup j = b*F + f at dX[b, f*D:]). ``ws``: int32
-    [>= len(rowstart)] (the hot-row list)."""
+    [B, >= F*D] in lookup order (row of lookup j = b*F + f at dX[b, f*D:]). ``ws``:
+    emb_rows_workspace(n, D, device) (GPU; None on the CPU)."""
     W = table.shape[1]
     D1 = W if split is None else split
     members, rowstart = csr[0], csr[3]
     if _gpu(dX):
+        wsi, hot_acc, hot_tick, hot = ws
         kernels().emb_rows_adagrad(dX, dwide, int(F), int(D), members, rowstart, U_dev, uniq, int(base), table, state,
-                                   state2, int(D1), float(lr), float(eps), ws, int(hot), bool(sorted_rows))
+                                   state2, int(D1), float(lr), float(eps), wsi, hot_acc, hot_tick, int(hot),
+                                   bool(sorted_rows))
         return
     U = int(U_dev.reshape(-1)[0])
     n = members.numel()

@@ -512,7 +512,8 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         if not fenced:
             keys.record_stream(ps)
             for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev, *(pp.csr or ())):
-                t.record_stream(cur)
+                if t is not None:  # (csr: positions may be None)
+                    t.record_stream(cur)
         return pp
 
     def advance_plan(self, pending, finish: bool = True):

@@ -540,6 +540,8 @@ def _route_multiplier(num_rows: int) -> int:
 _CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
 # MINIPS_ROWS_ADAGRAD=0: keep the piecewise segment sum + separate Adagrad for row-sorted pushes
 # of one rank instead of the row-parallel fused apply (ops.emb_rows_adagrad)
+# lookups above which a row is reduced by workgroup chunks instead of one lane group
+_ROWS_HOT = int(os.environ.get("MINIPS_ROWS_HOT", "32"))
 _ROWS_ADAGRAD = __import__("os").environ.get("MINIPS_ROWS_ADAGRAD", "1") == "1"
 # MINIPS_SORTED_EMB=1: plans carry the CSR's inverse permutation (csr[2]: each lookup's row in
 # member order) so the embedding dgrad writes its output pre-sorted and the backward streams it
@@ -1046,10 +1048,11 @@ class SparseTable:
         dev = self.comm.device
         if isinstance(grad_rows, _LookupGrads) and grad_rows.rows:  # one rank, row-parallel
             lg = grad_rows
-            n = plan.csr[3].numel()
+            n = plan.csr[3].numel() - 1
             ws = getattr(self, "_rows_ws", None)
-            if ws is None or ws.numel() < n:
-                ws = self._rows_ws = torch.empty(n, dtype=torch.int32, device=dev)
+            if ws is None or ws[0] != (n, lg.D):  # (hot_acc / hot_tick stay zero between calls)
+                ws = self._rows_ws = ((n, lg.D), ops.emb_rows_workspace(n, lg.D, dev, hot=_ROWS_HOT))
+            ws = ws[1]
             U_dev = plan.U_dev if plan.U_dev is not None else torch.tensor([plan.cap], dtype=torch.int64, device=dev)
             ops.emb_rows_adagrad(lg.dX, lg.dwide, lg.F, lg.D, plan.csr, U_dev, plan.uniq, self.base, self.shard,
                                  self.state, self.state2, self.split, self.lr, self.eps, ws, sorted_rows=lg.sorted)

@@ -65,6 +65,7 @@ print("ok", worst)
 
 @pytest.mark.parametrize("env", [
     {"MINIPS_GEMM_V4": "4"},                                    # v5 (ping-pong 256x256) everywhere
+    {"MINIPS_SPLITK_FOLD": "1"},                                # split-K planes folded in the GEMM
     {"MINIPS_GEMM_V4": "2"},                                    # v4 (quarter-staged 256x256) everywhere
     {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "1"},         # v3
     {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "1", "MINIPS_GEMM_V3_EARLY": "0", "MINIPS_GEMM_WGRAD": "v3"},

@@ -530,7 +530,7 @@ def test_rows_emb_backward_adagrad(dev, D, wide, split, sorted_rows):
     s2_gpu = state2.to(dev) if split else None
     t_ref, s_ref = table.clone(), state.clone()
     s2_ref = state2.clone() if split else None
-    ws = torch.empty(B * F + 1, dtype=torch.int32, device=dev)
+    ws = ops.emb_rows_workspace(B * F, D, dev)
     for step in range(2):
         keys = torch.stack([torch.randint(0, c, (B,), generator=g) for c in cards], 1) + base
         keys[:3000, 2] = base[2] + 17 + step  # a hot row: 3000 lookups
@@ -559,6 +559,9 @@ def test_rows_emb_backward_adagrad(dev, D, wide, split, sorted_rows):
         torch.testing.assert_close(s_gpu.cpu(), s_ref, rtol=1e-4, atol=1e-5)
         if split:
             torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-4, atol=1e-5)
+        # the chunked hot rows leave their accumulators and tickets zero for the next call
+        assert int(ws[1].count_nonzero()) == 0 and int(ws[2].count_nonzero()) == 0
+        assert int(ws[0][:3].count_nonzero()) == 0  # counters re-zeroed by the hot kernel's last block
 
 
 def test_colsum_bf16(dev):
