@@ -173,6 +173,7 @@ void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t 
 // One wave per sample (grid-stride); each lane owns Hd/64 columns and keeps its dw / colsum
 // partials in registers across all samples it visits: one atomic per lane per column at the end.
 constexpr int kHeadWaves = 16;  // 1024-thread blocks: 4x the waves in flight, same atomic count
+constexpr int kHeadGroup = 16, kHeadMaxGroups = 16;  // two-level fold: <= 256 blocks
 
 // PER_LANE consecutive bf16 of a row as one vector access (8 B for 4, 16 B for 8): the
 // element-wise 2-byte loads / stores cost 4-8 memory instructions per lane instead of one
@@ -292,6 +293,15 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
     red_s[1][wv] = lossl;
   }
   __syncthreads();
+  // Two-level fold of the blocks' partial rows (slab [blocks + groups][NP]), every hand-off in the
+  // write-through form of cdna_hip_programming.md Guideline 16 (R1: sc1 stores, drain, relaxed
+  // ticket; the reader acquires once): the last block of each group of kHeadGroup folds its
+  // group's rows (kHeadGroup independent loads per column, one round trip), the last group folder
+  // folds the group rows into dw / colsum / db / loss. (One last block folding all 128 rows --
+  // 32 dependent round trips per column -- was most of the kernel's 27-36 us.)
+  const int nb = (int)gridDim.x, ngroups = (nb + kHeadGroup - 1) / kHeadGroup;
+  const int grp = blockIdx.x / kHeadGroup;
+  const int g0 = grp * kHeadGroup, gn = min(kHeadGroup, nb - g0);
   float* row = slab + (int64_t)blockIdx.x * NP;
   for (int c = threadIdx.x; c < NC; c += blockDim.x) {
     float a = 0.f, b = 0.f;
@@ -300,8 +310,8 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
       a += red[0][w][c];
       b += red[1][w][c];
     }
-    row[c] = a;
-    row[NC + c] = b;
+    __hip_atomic_store(row + c, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(row + NC + c, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (threadIdx.x == 0) {
     float a = 0.f, b = 0.f;
@@ -310,38 +320,53 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
       a += red_s[0][w];
       b += red_s[1][w];
     }
-    row[2 * NC] = a;
-    row[2 * NC + 1] = b;
+    __hip_atomic_store(row + 2 * NC, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(row + 2 * NC + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // publish (cdna_hip_programming.md Guideline 16): every storing wave drains, the block meets,
-  // one lane releases at agent scope and takes a ticket; the last ticket acquires and reduces
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ticket + 1 + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (unsigned)gn - 1;
+    if (last) {
+      __hip_atomic_store(ticket + 1 + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  float* grow = slab + (int64_t)(nb + grp) * NP;  // this group's folded row
+  for (int c = threadIdx.x; c < NP; c += blockDim.x) {
+    float v[kHeadGroup];
+#pragma unroll
+    for (int k = 0; k < kHeadGroup; ++k) v[k] = k < gn ? slab[(int64_t)(g0 + k) * NP + c] : 0.f;
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kHeadGroup; ++k) tot += v[k];
+    __hip_atomic_store(grow + c, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == gridDim.x - 1;
+    last = t == (unsigned)ngroups - 1;
     if (last) {
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
     }
   }
   __syncthreads();
   if (!last) return;
   for (int c = threadIdx.x; c < NP; c += blockDim.x) {
     if (c >= NC && c < 2 * NC && !colsum) continue;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int k = 0;
-    for (; k + 3 < (int)gridDim.x; k += 4) {  // 4 independent partial loads in flight
-      a0 += slab[(int64_t)k * NP + c];
-      a1 += slab[(int64_t)(k + 1) * NP + c];
-      a2 += slab[(int64_t)(k + 2) * NP + c];
-      a3 += slab[(int64_t)(k + 3) * NP + c];
-    }
-    for (; k < (int)gridDim.x; ++k) a0 += slab[(int64_t)k * NP + c];
-    const float tot = (a0 + a1) + (a2 + a3);
+    float v[kHeadMaxGroups];
+#pragma unroll
+    for (int k = 0; k < kHeadMaxGroups; ++k) v[k] = k < ngroups ? slab[(int64_t)(nb + k) * NP + c] : 0.f;
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kHeadMaxGroups; ++k) tot += v[k];
     if (c < NC) dw[c] += tot;
     else if (c < 2 * NC) colsum[c - NC] += tot;
     else if (c == 2 * NC) *db += tot;
@@ -367,7 +392,7 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
   void* ws = nullptr;
   for (auto& e : ws_cache)
     if (e.first == dev) ws = e.second;
-  const size_t slab_bytes = sizeof(float) * 256 * (2 * 512 + 2);
+  const size_t slab_bytes = sizeof(float) * (256 + kHeadMaxGroups) * (2 * 512 + 2);
   if (!ws) {
     MINIPS_HIP_CHECK(hipMalloc(&ws, slab_bytes + 256));
     MINIPS_HIP_CHECK(hipMemset(ws, 0, slab_bytes + 256));
@@ -1274,21 +1299,55 @@ __global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __r
     float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float gw = 0.f;
     const int end = cold ? e : s;
-    for (int m = s; m < end; m += 4) {
-      uint4 v[4];
-      float w[4];
+    if (ldx != 0 && hot <= 32) {
+      // lookup order: the group's lanes fetch the row's member list cooperatively (one round
+      // trip), then every lookup's j comes by a lane shuffle and its gradient slice loads 8 at a
+      // time -- 2 + cnt / 8 dependent round trips instead of 2 per 4 lookups
+      constexpr int MK = (32 + L - 1) / L;
+      const int cnt = end - s, gbase = lane - l;
+      int mj[MK];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int mm = m + q;
-        const bool in = mm < end;
-        const int j = (in && (ldx || wide)) ? members[mm] : 0;
-        v[q] = in ? *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, mm, j) + 8 * l) : make_uint4(0, 0, 0, 0);
-        w[q] = (wide && l == 0 && in) ? dwide[j / F] : 0.f;
+      for (int k = 0; k < MK; ++k) {
+        const int q = l + L * k;
+        mj[k] = q < cnt ? members[s + q] : 0;
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc_bf16x8(g, v[q]);
-        gw += w[q];
+      for (int q0 = 0; q0 < 32; q0 += 8) {
+        uint4 v[8];
+        float w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int q = q0 + i;
+          const int j = __shfl(mj[q / L], gbase + q % L, 64);
+          const bool in = q < cnt;
+          const int b = j / F;
+          v[i] = in ? *reinterpret_cast<const uint4*>(dX + (int64_t)b * ldx + (j - b * F) * D + 8 * l)
+                    : make_uint4(0, 0, 0, 0);
+          w[i] = (wide && l == 0 && in) ? dwide[b] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc_bf16x8(g, v[i]);
+          gw += w[i];
+        }
+      }
+    } else {
+      for (int m = s; m < end; m += 4) {
+        uint4 v[4];
+        float w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int mm = m + q;
+          const bool in = mm < end;
+          const int j = (in && (ldx || wide)) ? members[mm] : 0;
+          v[q] = in ? *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, mm, j) + 8 * l) : make_uint4(0, 0, 0, 0);
+          w[q] = (wide && l == 0 && in) ? dwide[j / F] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc_bf16x8(g, v[q]);
+          gw += w[q];
+        }
       }
     }
     if (cold) rows_apply<L>(a, trow, g, gw, wide, t0, t1, tw, st1, st2, l, D);

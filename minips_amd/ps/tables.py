@@ -538,11 +538,13 @@ def _route_multiplier(num_rows: int) -> int:
 # the dedupe counts each unique key's lookups for the embedding-backward CSR (one pass less);
 # MINIPS_CSR_FUSED=0 counts in emb_build_csr instead
 _CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
-# MINIPS_ROWS_ADAGRAD=0: keep the piecewise segment sum + separate Adagrad for row-sorted pushes
-# of one rank instead of the row-parallel fused apply (ops.emb_rows_adagrad)
-# lookups above which a row is reduced by workgroup chunks instead of one lane group
+# MINIPS_ROWS_ADAGRAD=1: one rank's embedding backward as the row-parallel fused apply
+# (ops.emb_rows_adagrad) instead of the piecewise segment sum + separate row-wise Adagrad. Off:
+# W&D step 0.417 vs 0.397 ms (lookup order), 0.435 with row-sorted dgrad output
+# (profiles/r4/ab_emb_backward.txt) -- the per-row dependent gathers lose to the piecewise sum.
+# MINIPS_ROWS_HOT: lookups above which a row is reduced by workgroup chunks instead of one lane group
 _ROWS_HOT = int(os.environ.get("MINIPS_ROWS_HOT", "32"))
-_ROWS_ADAGRAD = __import__("os").environ.get("MINIPS_ROWS_ADAGRAD", "1") == "1"
+_ROWS_ADAGRAD = os.environ.get("MINIPS_ROWS_ADAGRAD", "0") == "1"
 # MINIPS_SORTED_EMB=1: plans carry the CSR's inverse permutation (csr[2]: each lookup's row in
 # member order) so the embedding dgrad writes its output pre-sorted and the backward streams it
 # contiguously instead of gathering 64-byte pieces. Measured on one MI355X (W&D step, 3 x 400
