@@ -415,7 +415,8 @@ void wd_assemble(const at::Tensor& dense, const at::Tensor& rows, const at::Tens
 // wd_assemble reading the fp32 table shard directly: row of lookup (b, f) = tab[uniq[inv] - base]
 void wd_assemble_tab(const at::Tensor& dense, const at::Tensor& tab, const at::Tensor& uniq, int64_t base,
                      const at::Tensor& inv, int64_t F, int64_t D, at::Tensor& X, at::Tensor& wide_logit,
-                     int64_t ones_col, const c10::optional<at::Tensor>& zero) {
+                     int64_t ones_col, const c10::optional<at::Tensor>& zero,
+                     const c10::optional<at::Tensor>& rowidx) {
   float* z = opt_ptr<float>(zero, at::kFloat, "zero");
   if (z) TORCH_CHECK(zero->numel() >= 1, "zero: at least one element");
   for (const at::Tensor* t : {&dense, &tab, &uniq, &inv, (const at::Tensor*)&X, (const at::Tensor*)&wide_logit})
@@ -431,10 +432,17 @@ void wd_assemble_tab(const at::Tensor& dense, const at::Tensor& tab, const at::T
   TORCH_CHECK(inv.numel() == B * F, "inv must be [B*F]");
   TORCH_CHECK(dense.size(0) == B, "dense rows");
   TORCH_CHECK(tab.size(1) > D, "tab rows must hold D deep values + the wide weight");
+  const int32_t* ri = nullptr;
+  if (rowidx && rowidx->defined()) {
+    check_gpu(*rowidx, "rowidx");
+    check_dtype(*rowidx, at::kInt, "rowidx");
+    TORCH_CHECK(rowidx->numel() == B * F, "rowidx must be [B*F]");
+    ri = rowidx->data_ptr<int32_t>();
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
   minips_k::wd_assemble_tab(ptr<float>(dense), (int)dense.size(1), ptr<float>(tab), tab.stride(0),
                             ptr<int64_t>(uniq), base, ptr<int64_t>(inv), B, (int)F, (int)D, ptr<bf16_t>(X),
-                            (int)X.size(1), ptr<float>(wide_logit), (int)ones_col, stream_of(X), z);
+                            (int)X.size(1), ptr<float>(wide_logit), (int)ones_col, stream_of(X), z, ri);
 }
 
 void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& wide_logit,
@@ -595,16 +603,21 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
   at::Tensor pos = with_positions ? at::empty({n}, o64.dtype(at::kInt)) : at::Tensor();
   // one owner: each row's lookup range in member order (the row-parallel embedding backward)
   at::Tensor rowstart = P == 1 ? at::empty({n + 1}, o64.dtype(at::kInt)) : at::Tensor();
+  // one owner, routed keys below 2^31: each lookup's table row (the input assembly's index)
+  at::Tensor rowidx = (P == 1 && route_mult && route_n > 0 && route_n <= INT32_MAX)
+                          ? at::empty({n}, o64.dtype(at::kInt))
+                          : at::Tensor();
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), col_bits.data_ptr<int32_t>(),
                         (uint64_t)route_mult, (uint64_t)route_n, ptr<int64_t>(bounds), (int)P, ws.data_ptr<int32_t>(),
                         ptr<int64_t>(ukey),
                         ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
                         ptr<int64_t>(counts), stream_of(keys), with_positions ? pos.data_ptr<int32_t>() : nullptr,
-                        rowstart.defined() ? rowstart.data_ptr<int32_t>() : nullptr);
-  // (members, memrow, positions or None, rowstart) with one owner
+                        rowstart.defined() ? rowstart.data_ptr<int32_t>() : nullptr,
+                        rowidx.defined() ? rowidx.data_ptr<int32_t>() : nullptr);
+  // (members, memrow, positions or None, rowstart, rowidx or None) with one owner
   if (rowstart.defined())
-    return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos, rowstart};
+    return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos, rowstart, rowidx};
   if (with_positions) return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos};
   return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow};
 }
@@ -735,7 +748,8 @@ void emb_seg_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
 
 void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g, double lr, double beta1,
                 double beta2, double eps, double weight_decay, int64_t step, double grad_scale,
-                const c10::optional<at::Tensor>& w_bf16, const c10::optional<at::Tensor>& step_dev, bool zero_g) {
+                const c10::optional<at::Tensor>& w_bf16, const c10::optional<at::Tensor>& step_dev, bool zero_g,
+                const std::vector<std::tuple<at::Tensor, int64_t, int64_t, int64_t>>& slabs) {
   for (auto* t : {&w, &m, &v}) {
     check_gpu(*t, "adam state");
     check_dtype(*t, at::kFloat, "adam state");
@@ -745,10 +759,44 @@ void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g
   TORCH_CHECK(w.numel() == m.numel() && w.numel() == v.numel() && w.numel() == g.numel(), "adam sizes differ");
   bf16_t* wb = opt_ptr<bf16_t>(w_bf16, at::kBFloat16, "w_bf16");
   if (wb) TORCH_CHECK(w_bf16->numel() == w.numel(), "w_bf16 size");
+  // (slab [nsplit * plane] fp32, nsplit, plane, offset of its region in g): the region's length is the plane
+  minips_k::AdamSlabs sl;
+  TORCH_CHECK(slabs.size() <= 4, "adam: at most 4 slab regions");
+  for (const auto& t : slabs) {
+    const at::Tensor& p = std::get<0>(t);
+    const int64_t ns = std::get<1>(t), plane = std::get<2>(t), off = std::get<3>(t);
+    check_gpu(p, "slab");
+    check_dtype(p, at::kFloat, "slab");
+    TORCH_CHECK(ns >= 1 && p.numel() >= ns * plane && off >= 0 && off + plane <= g.numel(), "adam slab bounds");
+    sl.p[sl.n] = ptr<float>(p);
+    sl.nsplit[sl.n] = (int)ns;
+    sl.plane[sl.n] = plane;
+    sl.len[sl.n] = plane;
+    sl.off[sl.n] = off;
+    ++sl.n;
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA gd(w.device());
   minips_k::adam_apply(ptr<float>(w), ptr<float>(m), ptr<float>(v), ptr<float>(g), w.numel(), (float)lr, (float)beta1,
                        (float)beta2, (float)eps, (float)weight_decay, (int)step, (float)grad_scale, wb, stream_of(w),
-                       step_dev.has_value() && step_dev->defined() ? step_dev->data_ptr<int>() : nullptr, zero_g);
+                       step_dev.has_value() && step_dev->defined() ? step_dev->data_ptr<int>() : nullptr, zero_g,
+                       nullptr, sl.n ? &sl : nullptr);
+}
+
+// split-K GEMM into slab planes without their reduction (the Adam kernel folds them): returns nsplit
+int64_t gemm_slab(const at::Tensor& A, const at::Tensor& B, at::Tensor& slab, int64_t M, int64_t N, int64_t K,
+                  bool a_km, bool b_kn, int64_t split_k) {
+  check_gpu(A, "A");
+  check_gpu(B, "B");
+  check_gpu(slab, "slab");
+  check_dtype(A, at::kBFloat16, "A");
+  check_dtype(B, at::kBFloat16, "B");
+  check_dtype(slab, at::kFloat, "slab");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "2-D operands");
+  TORCH_CHECK(slab.numel() >= split_k * M * N, "slab: >= split_k * M * N floats");
+  const int64_t lda = A.stride(0), ldb = B.stride(0);
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(A.device());
+  return minips_k::gemm_slab(ptr<bf16_t>(A), ptr<bf16_t>(B), ptr<float>(slab), (int)M, (int)N, (int)K, (int)lda,
+                             (int)ldb, a_km, b_kn, (int)split_k, stream_of(A));
 }
 
 void sgd_apply(at::Tensor& w, const at::Tensor& g, double lr, double grad_scale,
@@ -1626,7 +1674,9 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),
         py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"),
-        py::arg("grad_scale"), py::arg("w_bf16"), py::arg("step_dev") = py::none(), py::arg("zero_g") = false);
+        py::arg("grad_scale"), py::arg("w_bf16"), py::arg("step_dev") = py::none(), py::arg("zero_g") = false,
+        py::arg("slabs") = std::vector<std::tuple<at::Tensor, int64_t, int64_t, int64_t>>());
+  m.def("gemm_slab", &gemm_slab);
   m.def("sgd_apply", &sgd_apply);
   m.def("adagrad_apply", &adagrad_apply);
   m.def("cast_f32_bf16", &cast_f32_bf16);

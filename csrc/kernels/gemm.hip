@@ -176,6 +176,16 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+int gemm_slab(const bf16_t* A, const bf16_t* B, float* slab, int M, int N, int K, int lda, int ldb, bool a_km,
+              bool b_kn, int split_k, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (N % 4) throw std::runtime_error("gemm_slab: N % 4 == 0");
+  EpiArgs sp{slab, N, nullptr, nullptr, 0, nullptr, 1.f, 1, 0, 0, 0, 0, 0, 0, (int64_t)M * N, nullptr, 0};
+  const int nsplit = dispatch_layout(a_km, b_kn, kEpiStoreF32, A, B, M, N, K, lda, ldb, std::max(1, split_k), sp, 1, s);
+  MINIPS_HIP_CHECK(hipGetLastError());
+  return nsplit;
+}
+
 void gemm_wd_head(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, bf16_t* dH, int lddh,
                   const bf16_t* w4, const float* wide, const float* labels, float* dw4, float* dwide, float* loss,
                   float scale, hipStream_t s, float* dh_colsum, int dh_colsum_ld) {

@@ -142,7 +142,8 @@ void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_st
 //   loss_sum += BCE(z, y)
 void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t tab_ld, const int64_t* uniq,
                      int64_t base, const int64_t* inv, int64_t B, int F, int D, bf16_t* X, int ldx,
-                     float* wide_logit, int ones_col, hipStream_t s, float* zero_out);
+                     float* wide_logit, int ones_col, hipStream_t s, float* zero_out,
+                     const int32_t* rowidx = nullptr);  // rowidx: lookup j's row + base (plan_sorted)
 void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
              float grad_scale, hipStream_t s);
@@ -182,7 +183,7 @@ void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const i
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
-                 int32_t* pos = nullptr, int32_t* rowstart = nullptr);
+                 int32_t* pos = nullptr, int32_t* rowstart = nullptr, int32_t* rowidx = nullptr);
 // (pos, nullable: pos[members[m]] = m, emb_csr_positions fused; rowstart, nullable, one owner only:
 // rowstart[u] = first member of row u, rowstart[U] = B*F)
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
@@ -210,9 +211,22 @@ void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int
 // ------------------------------------------------------------------ optimizers (optim.hip)
 // Fused Adam(W) on an fp32 master shard; optionally writes the bf16 copy for all-gather.
 // active (nullable, device): the kernel does nothing when *active == 0 (an empty async push).
+// slabs (nullable): split-K weight-gradient planes left unreduced (gemm_slab): element off + e of
+// the gradient gets sum_z p[z * plane + e] for e < len (offsets / lengths / planes multiples of 4).
+struct AdamSlabs {
+  int n = 0;
+  const float* p[4] = {nullptr, nullptr, nullptr, nullptr};
+  int64_t off[4] = {0, 0, 0, 0}, len[4] = {0, 0, 0, 0}, plane[4] = {0, 0, 0, 0};
+  int nsplit[4] = {0, 0, 0, 0};
+};
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2,
                 float eps, float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s,
-                const int* step_dev = nullptr, bool zero_g = false, const int64_t* active = nullptr);
+                const int* step_dev = nullptr, bool zero_g = false, const int64_t* active = nullptr,
+                const AdamSlabs* slabs = nullptr);
+// split-K GEMM whose K slices stay in their fp32 slab planes [nsplit][M][N] (no reduce launch):
+// the consumer folds them (adam_apply slabs). Returns nsplit.
+int gemm_slab(const bf16_t* A, const bf16_t* B, float* slab, int M, int N, int K, int lda, int ldb, bool a_km,
+              bool b_kn, int split_k, hipStream_t s);
 void sgd_apply(float* w, const float* g, int64_t n, float lr, float grad_scale, bf16_t* w_bf16, hipStream_t s,
                const int64_t* active = nullptr);
 void adagrad_apply(float* w, float* acc, const float* g, int64_t n, float lr, float eps, float grad_scale,

@@ -12,7 +12,8 @@ namespace minips_k {
 __global__ void adam_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                             float* __restrict__ g, int64_t n, float lr, float b1, float b2, float eps, float wd,
                             float bc1, float bc2, float gscale, bf16_t* __restrict__ wb,
-                            const int* __restrict__ step_dev, bool zero_g, const int64_t* __restrict__ active) {
+                            const int* __restrict__ step_dev, bool zero_g, const int64_t* __restrict__ active,
+                            AdamSlabs sl) {
   if (active && *active == 0) return;  // an empty push (a Clock without an Add): nothing to apply
   if (step_dev) {  // device-side step (graph-replayable clocks): bias corrections from *step_dev
     const float t = (float)*step_dev;
@@ -27,7 +28,33 @@ __global__ void adam_kernel(float* __restrict__ w, float* __restrict__ m, float*
     float* Wp = &W.x;
     float* Mp = &M.x;
     float* Vp = &V.x;
-    const float* Gp = &G.x;
+    float4 Gs = G;
+    // split-K weight gradients left in their slab planes (adam_slabs): their sum lands here, the
+    // one kernel that reads the gradient anyway (no separate reduce pass over the planes)
+    for (int k = 0; k < sl.n; ++k) {
+      const int64_t e = 4 * i - sl.off[k];
+      if (e < 0 || e >= sl.len[k]) continue;
+      const float* p = sl.p[k] + e;
+      int z = 0;
+      for (; z + 3 < sl.nsplit[k]; z += 4) {
+        const float4 a0 = *reinterpret_cast<const float4*>(p + z * sl.plane[k]);
+        const float4 a1 = *reinterpret_cast<const float4*>(p + (z + 1) * sl.plane[k]);
+        const float4 a2 = *reinterpret_cast<const float4*>(p + (z + 2) * sl.plane[k]);
+        const float4 a3 = *reinterpret_cast<const float4*>(p + (z + 3) * sl.plane[k]);
+        Gs.x += (a0.x + a1.x) + (a2.x + a3.x);
+        Gs.y += (a0.y + a1.y) + (a2.y + a3.y);
+        Gs.z += (a0.z + a1.z) + (a2.z + a3.z);
+        Gs.w += (a0.w + a1.w) + (a2.w + a3.w);
+      }
+      for (; z < sl.nsplit[k]; ++z) {
+        const float4 a = *reinterpret_cast<const float4*>(p + z * sl.plane[k]);
+        Gs.x += a.x;
+        Gs.y += a.y;
+        Gs.z += a.z;
+        Gs.w += a.w;
+      }
+    }
+    const float* Gp = &Gs.x;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float gg = Gp[j] * gscale;
@@ -60,7 +87,15 @@ static void check_align(const void* p, const char* what) {
 
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2, float eps,
                 float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s, const int* step_dev,
-                bool zero_g, const int64_t* active) {
+                bool zero_g, const int64_t* active, const AdamSlabs* slabs) {
+  AdamSlabs sl{};
+  if (slabs) {
+    sl = *slabs;
+    for (int k = 0; k < sl.n; ++k)
+      if ((sl.off[k] & 3) || (sl.len[k] & 3) || (sl.plane[k] & 3) || sl.off[k] < 0 || sl.off[k] + sl.len[k] > n ||
+          (reinterpret_cast<uintptr_t>(sl.p[k]) & 15))
+        throw std::runtime_error("adam slabs: 16-byte aligned planes and ranges inside the shard");
+  }
   if (n <= 0) return;
   check_align(w, "adam w");
   check_align(m, "adam m");
@@ -71,7 +106,7 @@ void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float l
   const int block = 256;
   hipLaunchKernelGGL(adam_kernel, grid_for((n + 3) / 4, block), block, 0, s, w, m, v, const_cast<float*>(g),
                      n, lr, beta1, beta2, eps,
-                     weight_decay, bc1, bc2, grad_scale, w_bf16, step_dev, zero_g, active);
+                     weight_decay, bc1, bc2, grad_scale, w_bf16, step_dev, zero_g, active, sl);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

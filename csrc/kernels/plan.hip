@@ -425,7 +425,8 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
                                                         int64_t* __restrict__ uniq, int64_t* __restrict__ inv,
                                                         int32_t* __restrict__ members, int32_t* __restrict__ memrow,
                                                         int64_t* __restrict__ counts, int32_t* __restrict__ pos_out,
-                                                        int32_t* __restrict__ rowstart) {
+                                                        int32_t* __restrict__ rowstart,
+                                                        int32_t* __restrict__ rowidx) {
   __shared__ int64_t basef[65];
   __shared__ int32_t ucf[64];
   const int t = threadIdx.x;
@@ -450,6 +451,9 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
       if (idx == n - 1) rowstart[U] = (int32_t)n;
     }
     if (!perm && pos < ucf[c]) uniq[basef[c] + pos] = ps_route(ukey[idx], rmult, rn);
+    // one owner: lookup j's table row (its routed key), so the input assembly reads the row
+    // with one index load instead of the inv -> uniq chain
+    if (rowidx) rowidx[j] = (int32_t)ps_route(ukey[(int64_t)c * B + local_u[idx]], rmult, rn);
   }
 }
 
@@ -470,8 +474,10 @@ static int plan_reps(int bit) {
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
-                 int32_t* pos, int32_t* rowstart) {
+                 int32_t* pos, int32_t* rowstart, int32_t* rowidx) {
   if (rowstart && P > 1) throw std::runtime_error("plan_sorted: row starts are for one owner");
+  if (rowidx && (P > 1 || !route_mult || route_n > (uint64_t)INT32_MAX))
+    throw std::runtime_error("plan_sorted: per-lookup rows need one owner and routed keys below 2^31");
   if (B < 1 || B > kPsMax) throw std::runtime_error("plan_sorted: 1 <= B <= 16384 rows per column");
   if (F < 1 || F > 64) throw std::runtime_error("plan_sorted: 1 <= F <= 64 columns");
   if (P < 1 || P > kPoMaxP) throw std::runtime_error("plan_sorted: 1 <= P <= 16 owners");
@@ -503,7 +509,7 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
   for (int r = 0; r < plan_reps(4); ++r)
     hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
                        route_mult, route_n, P > 1 ? perm : nullptr, uniq, inv, members, memrow, counts, pos,
-                       rowstart);
+                       rowstart, rowidx);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

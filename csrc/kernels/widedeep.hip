@@ -99,13 +99,17 @@ __global__ void wd_assemble_tab_kernel(const float* __restrict__ dense, int n_de
                                        int64_t tab_ld, const int64_t* __restrict__ uniq, int64_t base,
                                        const int64_t* __restrict__ inv, int64_t B, int F, int D,
                                        bf16_t* __restrict__ X, int ldx, float* __restrict__ wide_logit, int ones_col,
-                                       float* __restrict__ zero_out) {
+                                       float* __restrict__ zero_out, const int32_t* __restrict__ rowidx) {
   if (zero_out && blockIdx.x == 0 && threadIdx.x == 0) *zero_out = 0.f;
   const int chunks = ldx >> 3;
   const int emb_cols = F * D;
   const int64_t total = B * chunks;
   const int64_t total_r = (total + 63) & ~63ll;
-  auto row_of = [&](int64_t b, int f) { return tab + (uniq[inv[b * F + f]] - base) * tab_ld; };
+  // the planner's per-lookup row (one coalesced index load) or the inv -> uniq chain
+  auto row_of = [&](int64_t b, int f) {
+    const int64_t r = rowidx ? (int64_t)rowidx[b * F + f] : uniq[inv[b * F + f]];
+    return tab + (r - base) * tab_ld;
+  };
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total_r + 32 * B;
        c += (int64_t)gridDim.x * blockDim.x) {
     if (c >= total_r) {
@@ -154,7 +158,7 @@ __global__ void wd_assemble_tab_kernel(const float* __restrict__ dense, int n_de
 
 void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t tab_ld, const int64_t* uniq,
                      int64_t base, const int64_t* inv, int64_t B, int F, int D, bf16_t* X, int ldx,
-                     float* wide_logit, int ones_col, hipStream_t s, float* zero_out) {
+                     float* wide_logit, int ones_col, hipStream_t s, float* zero_out, const int32_t* rowidx) {
   if (ldx % 8) throw std::runtime_error("wd_assemble_tab: ldx must be a multiple of 8");
   if (F * D + n_dense > ldx) throw std::runtime_error("wd_assemble_tab: ldx too small");
   if (ones_col >= ldx) throw std::runtime_error("wd_assemble_tab: ones_col out of range");
@@ -166,7 +170,7 @@ void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t 
   // per sample -- ran the W&D step 15 us slower: 26 rows per wave-instruction vs 8 here)
   const int64_t items = ((B * (ldx / 8) + 63) & ~63ll) + 32 * B;
   hipLaunchKernelGGL(wd_assemble_tab_kernel, (int)((items + block - 1) / block), block, 0, s, dense, n_dense, tab,
-                     tab_ld, uniq, base, inv, B, F, D, X, ldx, wide_logit, ones_col, zero_out);
+                     tab_ld, uniq, base, inv, B, F, D, X, ldx, wide_logit, ones_col, zero_out, rowidx);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -96,10 +96,14 @@ _WGRAD_BLOCKS = int(os.environ.get("MINIPS_WD_WGRAD_BLOCKS", "320"))
 _WGRAD_LIB = os.environ.get("MINIPS_WD_WGRAD", "ours") == "lib"
 
 
-def _wgrad(dH, H, Gw):
+# MINIPS_ROWIDX=0: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
+_ROWIDX = os.environ.get("MINIPS_ROWIDX", "1") != "0"
+
+
+def _wgrad(dH, H, Gw, sink=None):
     if _WGRAD_LIB and dH.is_cuda:
         return torch.mm(dH.t(), H, out_dtype=torch.float32, out=Gw[: dH.shape[1]])
-    return ops.linear_wgrad(dH, H, Gw, blocks=_WGRAD_BLOCKS)
+    return ops.linear_wgrad(dH, H, Gw, blocks=_WGRAD_BLOCKS, defer=sink)
 
 
 def _align(n, a=8):
@@ -259,8 +263,10 @@ class WideDeep(LookaheadPlans):
         src = self.emb.get_source(keys, plan=plan)  # one rank: the rows are read in place
         if src is not None:
             plan, table, index, base = src
+            # (members, memrow, positions, rowstart, rowidx): the planner's per-lookup rows
+            rowidx = plan.csr[4] if plan.csr is not None and len(plan.csr) >= 5 and _ROWIDX else None
             ops.wd_assemble_tab(dense, table, index, base, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0],
-                                zero=b["loss"])
+                                zero=b["loss"], rowidx=rowidx)
         else:
             rows, plan = self.emb.get(keys, plan=plan)
             ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
@@ -292,12 +298,14 @@ class WideDeep(LookaheadPlans):
         # 1032 / 520: no near-empty last column tile); their folded-bias columns are the column sums
         # of dH2 / dH3, taken by the dgrad epilogue / the fused head
         trim = _TRIM and _FUSED_HEAD and not _BIAS_VEC
+        # one rank: the weight gradients' split-K slices are folded by the dense table's Adam
+        sink = self.dense.slab_sink() if hasattr(self.dense, "slab_sink") else None
         k2, k3 = self.k_in[1], self.k_in[2]
         with side.fork():
             if trim:
                 ops.linear_wgrad(b["dH3"], b["H2"][:, :k3], self.view(G, "W3")[:, :k3], blocks=_WGRAD_BLOCKS)
             else:
-                _wgrad(b["dH3"], b["H2"], self.view(G, "W3"))
+                _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink)
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"],
                          colsum=self.view(G, "W2")[:, k2] if trim else None)
         with side.fork():
@@ -306,11 +314,11 @@ class WideDeep(LookaheadPlans):
             if trim:
                 ops.linear_wgrad(b["dH2"], b["H1"][:, :k2], self.view(G, "W2")[:, :k2], blocks=_WGRAD_BLOCKS)
             else:
-                _wgrad(b["dH2"], b["H1"], self.view(G, "W2"))
+                _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink)
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         self._bucket_done(1, side)  # (layers 2, 3 and the head: their weight gradients are issued)
         with side.fork():
-            _wgrad(b["dH1"], b["X"], self.view(G, "W1"))
+            _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
         # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows

@@ -185,9 +185,12 @@ def overlap_mode(on: bool) -> bool:
     return prev
 
 
-def linear_wgrad(dy, x, dw, split_k=None, blocks=None):
+def linear_wgrad(dy, x, dw, split_k=None, blocks=None, defer=None):
     """dw[N,K] += dy^T x (dy [M,N], x [M,K]); fp32 accumulate. ``blocks``: the workgroup target of
-    the split-K choice (default MINIPS_WGRAD_BLOCKS; a model may tune its own)."""
+    the split-K choice (default MINIPS_WGRAD_BLOCKS; a model may tune its own). ``defer``: a
+    DenseTable slab sink (DenseTable.slab_sink()): the K slices stay in fp32 slab planes that the
+    table's next Adam folds in (no reduce kernel); dw must be a contiguous [N, K] region of the
+    table's gradient, which the sum then never passes through."""
     M, N = dy.shape
     K = x.shape[1]
     if split_k is None:
@@ -202,6 +205,12 @@ def linear_wgrad(dy, x, dw, split_k=None, blocks=None):
         split_k = max(1, min(M // min_rows, (target + tiles - 1) // tiles))
         if overlapped and _WGRAD_MIN_BLOCKS_OVERLAP and split_k * tiles < _WGRAD_MIN_BLOCKS_OVERLAP:
             split_k = max(split_k, min(M // _WGRAD_MIN_ROWS, -(-_WGRAD_MIN_BLOCKS_OVERLAP // tiles)))
+    if (defer is not None and _gpu(dy) and split_k > 1 and K % 4 == 0 and dw.dim() == 2
+            and dw.stride(1) == 1 and dw.stride(0) == K and defer.accepts(dw)):
+        slab = defer.slab(dw, split_k)
+        nsplit = kernels().gemm_slab(dy, x, slab, N, K, M, True, True, int(split_k))
+        defer.add(dw, slab, nsplit)
+        return dw
     return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
 
 
@@ -313,11 +322,13 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
     if positions:  # members = order: pos[order[m]] = m
         pos = torch.empty(B * F, dtype=torch.int32)
         pos[order] = torch.arange(B * F, dtype=torch.int32)
-    if P == 1:  # row u's lookups are members [rowstart[u], rowstart[u + 1]): (.., positions or None, rowstart)
+    if P == 1:  # row u's lookups are members [rowstart[u], rowstart[u + 1]): (.., positions or None, rowstart,
+        # rowidx or None) -- rowidx: each lookup's table row (routed key) when routed keys fit int32
         rs = torch.full((B * F + 1,), B * F, dtype=torch.int32)
         rs[0] = 0
         rs[1: U + 1] = torch.cumsum(torch.bincount(inv_u, minlength=U), 0).to(torch.int32)
-        return res + (pos, rs)
+        ri = uniq[inv_u].to(torch.int32) if route_mult and 0 < route_n <= 0x7FFFFFFF else None
+        return res + (pos, rs, ri)
     return res + (pos,) if positions else res
 
 
@@ -471,12 +482,13 @@ def wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col=-1, zero=None):
     return X, wide_logit
 
 
-def wd_assemble_tab(dense, table, index, base, inv, F, D, X, wide_logit, ones_col=-1, zero=None):
+def wd_assemble_tab(dense, table, index, base, inv, F, D, X, wide_logit, ones_col=-1, zero=None, rowidx=None):
     """wd_assemble with the rows read in place: the row of unique u is table[index[u] - base]
-    (fp32), rounded to bf16 exactly as gather_rows(out bf16) does."""
+    (fp32), rounded to bf16 exactly as gather_rows(out bf16) does. ``rowidx`` (plan_sorted, one
+    owner): lookup j's row + base directly (the same rows, one index load per lookup)."""
     if _gpu(X):
         kernels().wd_assemble_tab(dense, table, index, int(base), inv, int(F), int(D), X, wide_logit, int(ones_col),
-                                  zero)
+                                  zero, rowidx)
         return X, wide_logit
     U = int(inv.max()) + 1 if inv.numel() else 0
     rows = table[index[:U] - base].to(torch.bfloat16)
@@ -630,14 +642,21 @@ def emb_seg_adagrad(dX, dwide, F, D, csr, uniq, U, base, table, state, state2, s
 
 # ----------------------------------------------------------------------------- optimizers
 def adam_apply(w, m, v, g, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=1, grad_scale=1.0,
-               w_bf16=None, step_dev=None, zero_g=False):
+               w_bf16=None, step_dev=None, zero_g=False, slabs=()):
     """Fused Adam(W). ``step_dev`` (int32 [1] device tensor): the bias-correction step is read on the
     device, so a captured (HIP graph) clock stays correct on replay. ``zero_g``: the kernel also
-    clears ``g`` after reading it (the gradient accumulator of the next clock; no fill kernel)."""
+    clears ``g`` after reading it (the gradient accumulator of the next clock; no fill kernel).
+    ``slabs``: (slab, nsplit, plane, offset) split-K gradient planes folded into g[offset:offset+plane]."""
     if _gpu(w):
         kernels().adam_apply(w, m, v, g, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
-                             int(step), float(grad_scale), w_bf16, step_dev, bool(zero_g))
+                             int(step), float(grad_scale), w_bf16, step_dev, bool(zero_g),
+                             [(s, int(n), int(p), int(o)) for s, n, p, o in slabs])
         return
+    g_in = g
+    if slabs:
+        g = g.clone()
+        for s, n, p, o in slabs:
+            g[o: o + p] += s[: n * p].view(n, p).sum(0)
     if step_dev is not None:
         step = int(step_dev.reshape(-1)[0])
     gg = g * grad_scale
@@ -648,7 +667,7 @@ def adam_apply(w, m, v, g, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.
     if w_bf16 is not None:
         w_bf16.copy_(w.to(torch.bfloat16))
     if zero_g:
-        g.zero_()
+        g_in.zero_()
 
 
 def sgd_apply(w, g, lr, grad_scale=1.0, w_bf16=None):

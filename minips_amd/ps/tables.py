@@ -147,6 +147,46 @@ def merge_buckets(starts, n_params: int, min_elems: float) -> list:
     return [0] + sorted(cuts)
 
 
+# MINIPS_WGRAD_DEFER=0: split-K weight gradients of one rank reduce into the gradient buffer (a
+# reduce kernel per GEMM) instead of being folded by the Adam kernel
+_WGRAD_DEFER = os.environ.get("MINIPS_WGRAD_DEFER", "1") != "0"
+
+
+class _SlabSink:
+    """Split-K weight-gradient slabs pending for a DenseTable's next Adam (DenseTable.slab_sink):
+    persistent fp32 planes per gradient region (re-used every step: the next step's GEMM is issued
+    after this step's Adam on the stream order of the step), folded by the Adam kernel."""
+
+    def __init__(self, table):
+        self.t = table
+        self._bufs = {}
+        self._pending = []
+
+    def accepts(self, dw) -> bool:
+        g = self.t.grad
+        return (dw.device == g.device and dw.dtype == g.dtype and len(self._pending) < 4
+                and g.data_ptr() <= dw.data_ptr() < g.data_ptr() + g.numel() * g.element_size()
+                and (dw.data_ptr() - g.data_ptr()) % 16 == 0)
+
+    def slab(self, dw, split_k: int):
+        key = (dw.data_ptr(), dw.numel())
+        buf = self._bufs.get(key)
+        need = int(split_k) * dw.numel()
+        if buf is None or buf.numel() < need:
+            buf = self._bufs[key] = torch.empty(need, dtype=torch.float32, device=dw.device)
+        return buf
+
+    def add(self, dw, slab, nsplit: int):
+        off = (dw.data_ptr() - self.t.grad.data_ptr()) // dw.element_size()
+        self._pending.append((slab, int(nsplit), dw.numel(), int(off)))
+
+    def take(self, g):
+        """The pending slabs of gradient buffer ``g`` (cleared)."""
+        out, self._pending = self._pending, []
+        base = (self.t.grad.data_ptr() - g.data_ptr()) // 4
+        return [(s, n, p, o + base) for s, n, p, o in out]
+
+
 class DenseTable:
     def __init__(self, comm: Comm, n_params: int, optimizer: str = "adam", lr: float = 1e-3,
                  pull_dtype=torch.bfloat16, consistency: str = "bsp", staleness: int = 0, table_id: int = 0,
@@ -424,12 +464,28 @@ class DenseTable:
             self.grad = self._ring[step % len(self._ring)]
             self.pipe.wait_clock(step - len(self._ring))
 
+    def slab_sink(self):
+        """A sink for split-K weight gradients whose K slices this table's next Adam folds in
+        (ops.linear_wgrad(defer=...): no reduce kernel, no pass of the sum through the gradient
+        buffer); None where the clock does not apply the whole gradient in one Adam kernel (several
+        ranks, buckets, other optimizers) or MINIPS_WGRAD_DEFER=0."""
+        if (not _WGRAD_DEFER or self.comm.world != 1 or self.buckets is not None or self.optimizer != "adam"
+                or self.comm.device.type != "cuda" or self.pipe.async_):
+            # (an asynchronous clock may apply after the next step's GEMMs rewrote the planes)
+            return None
+        sink = getattr(self, "_sink", None)
+        if sink is None:
+            sink = self._sink = _SlabSink(self)
+        return sink
+
     def _apply(self, g: torch.Tensor, step: int, zero_g: bool = False, step_dev=None) -> bool:
         """Apply the optimizer to the owned shard; True if ``g`` was cleared on the way."""
         out = self.params[self.base: self.base + self.shard] if self.pull_dtype == torch.bfloat16 else None
         if self.optimizer == "adam":
+            sink = getattr(self, "_sink", None)
+            slabs = sink.take(g) if sink is not None else ()
             ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
-                           self.weight_decay, step, 1.0, out, step_dev=step_dev, zero_g=zero_g)
+                           self.weight_decay, step, 1.0, out, step_dev=step_dev, zero_g=zero_g, slabs=slabs)
             if out is None:
                 self.params[self.base: self.base + self.shard].copy_(self.master)
             return zero_g

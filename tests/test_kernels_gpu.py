@@ -608,6 +608,11 @@ def test_plan_sorted_matches_reference(dev, B, cards, P):
     pos = ops.plan_sorted(keys.to(dev), torch.tensor(bases, device=dev), bits, mult, R, bounds=bounds.to(dev),
                           positions=True)[6].cpu()
     assert torch.equal(pos[got[4].long()], torch.arange(keys.numel(), dtype=torch.int32))  # inverse of members
+    if P == 1:  # rowstart, and each lookup's table row (routed key) for the input assembly
+        assert len(got) == 9 and len(ref) == 9
+        torch.testing.assert_close(got[7][: U + 1], ref[7][: U + 1])
+        torch.testing.assert_close(got[8], ref[8])
+        torch.testing.assert_close(got[8].long(), (keys.reshape(-1) * mult) % R)
 
 
 @pytest.mark.parametrize("num_rows,n,P,route", [(16_609_143, 200_000, 1, True), (1000, 5000, 3, False),

@@ -148,3 +148,22 @@ def test_widedeep_fused_head_and_trimmed_wgrads(dev, monkeypatch, fused, trim):
     # Adam steps every element by ~lr: near-zero gradients may flip under a different summation order
     diff = (p0 - p1).abs()
     assert float((diff > 2e-4).float().mean()) < 1e-2
+
+
+def test_widedeep_wgrad_slabs_folded_by_adam(dev, monkeypatch):
+    """One rank: the split-K weight gradients left in their slab planes and folded by the dense
+    table's Adam kernel (DenseTable.slab_sink) train like the reduce-kernel path."""
+    import minips_amd.ps.tables as tables
+
+    res = {}
+    for defer in (False, True):
+        monkeypatch.setattr(tables, "_WGRAD_DEFER", defer)
+        losses, m = _run(dev, steps=4)
+        if defer:
+            assert m.dense.slab_sink() is not None and not m.dense._sink._pending
+        res[defer] = (losses, m.dense.master.cpu())
+    (l0, p0), (l1, p1) = res[False], res[True]
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (l0, l1)
+    diff = (p0 - p1).abs()
+    assert float((diff > 2e-4).float().mean()) < 1e-2
