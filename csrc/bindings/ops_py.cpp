@@ -1700,6 +1700,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("ps_hash_gather", &ps_hash_gather, py::arg("hkeys"), py::arg("hvals"), py::arg("bounds"), py::arg("cap"),
         py::arg("keys"), py::arg("n_dev"), py::arg("W"), py::arg("out"));
   m.def("ps_pull", &ps_pull);
+  m.def("ps_set_fences", [](bool on) { minips_k::ps_set_fences(on); });
   m.def("ps_read_lock", &ps_read_lock);
   m.def("ps_read_unlock", &ps_read_unlock);
   m.attr("PS_CTRL_BYTES") = minips_k::kPsCtrlBytes;

@@ -51,6 +51,8 @@ constexpr int kPsHeldSlots = 256;            // reader-side ring of "locks held"
 enum PsLockError : uint32_t { kPsErrReadLock = 1, kPsErrWriteLock = 2, kPsErrHashFull = 4 };
 // Reader: take the read lock of every owner (ascending order), record the ones taken in *held.
 void ps_read_lock(const int64_t* locks, int P, uint32_t* held, uint32_t* err, hipStream_t s);
+// false: every owner is on this device (one rank): no system-scope fence launches
+void ps_set_fences(bool on);
 void ps_read_unlock(const int64_t* locks, int P, uint32_t* held, hipStream_t s);
 // Owner: announce the writer, wait for the readers to drain / flush every XCD's L2, then release.
 void ps_write_lock(uint32_t* lock, uint32_t* err, hipStream_t s);

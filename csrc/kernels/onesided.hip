@@ -78,7 +78,13 @@ __global__ void ps_fence_kernel() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// One-rank process (every owner is this device): the kernel boundaries of one stream and the
+// owner's lock kernels order everything at agent scope, so the system-scope fences are skipped
+// (ps_set_fences(false); each fence launch costs ~5 us of queue time).
+static bool g_ps_fences = true;
+
 void fence_l2(bool release, hipStream_t s) {
+  if (!g_ps_fences) return;
   if (release) hipLaunchKernelGGL(ps_fence_kernel<true>, kFlushBlocks, 64, 0, s);
   else hipLaunchKernelGGL(ps_fence_kernel<false>, kFlushBlocks, 64, 0, s);
 }
@@ -146,6 +152,12 @@ __global__ void ps_write_unlock_kernel(uint32_t* lock, uint32_t* count) {
     __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_fetch_and(lock, ~kPsWriter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// one-rank form: every reader is on this device, so an agent-scope release suffices
+__global__ void ps_write_unlock_local_kernel(uint32_t* lock) {
+  if (threadIdx.x != 0) return;
+  __hip_atomic_fetch_and(lock, ~kPsWriter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ int upper_owner(const int64_t* __restrict__ b, int P, int64_t k) {
@@ -403,6 +415,8 @@ __global__ __launch_bounds__(256) void ps_pull_kernel(const int64_t* __restrict_
 
 }  // namespace
 
+void ps_set_fences(bool on) { g_ps_fences = on; }
+
 void ps_read_lock(const int64_t* locks, int P, uint32_t* held, uint32_t* err, hipStream_t s) {
   if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_read_lock: P out of range");
   hipLaunchKernelGGL(ps_read_lock_kernel, 1, 64, 0, s, locks, P, held, err);
@@ -420,6 +434,11 @@ void ps_write_lock(uint32_t* lock, uint32_t* err, hipStream_t s) {
 }
 
 void ps_write_unlock(uint32_t* lock, uint32_t* flush_count, hipStream_t s) {
+  if (!g_ps_fences) {
+    hipLaunchKernelGGL(ps_write_unlock_local_kernel, 1, 64, 0, s, lock);
+    MINIPS_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(ps_write_unlock_kernel, kFlushBlocks, 64, 0, s, lock, flush_count);
   MINIPS_HIP_CHECK(hipGetLastError());
 }

@@ -105,6 +105,8 @@ class AsyncPS:
             from .._native import kernels
 
             k = kernels()
+            # one rank: every owner is this device -- agent-scope ordering suffices, no system fences
+            k.ps_set_fences(comm.world > 1)
             self.server = k.AsyncServer(name, self.world, self.rank, _MAX_TABLES, comm.device.index or 0)
             self._anchor = torch.zeros(1, device=comm.device)
             # the rank's error word (a device spin that timed out sets a bit) and the control lines
