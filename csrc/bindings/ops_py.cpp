@@ -332,7 +332,7 @@ void scatter_add_rows(const at::Tensor& src, const at::Tensor& idx, at::Tensor& 
 
 void sparse_rowwise_adagrad(at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
                             const at::Tensor& keys, int64_t base, const at::Tensor& grads, double lr, double eps,
-                            const c10::optional<at::Tensor>& n_dev) {
+                            const c10::optional<at::Tensor>& n_dev, bool zero_g) {
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.stride(1) == 1, "table must be a row-major GPU matrix");
   check_gpu(state, "state");
   check_gpu(keys, "keys");
@@ -344,7 +344,7 @@ void sparse_rowwise_adagrad(at::Tensor& table, at::Tensor& state, const c10::opt
   c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
   minips_k::sparse_rowwise_adagrad(ptr<float>(table), table.stride(0), ptr<float>(state), s2, (int)D1,
                                    ptr<int64_t>(keys), keys.numel(), base, (int)grads.size(1), ptr<float>(grads),
-                                   (float)lr, (float)eps, stream_of(table), count_ptr(n_dev));
+                                   (float)lr, (float)eps, stream_of(table), count_ptr(n_dev), zero_g);
 }
 
 void sparse_sgd(at::Tensor& table, const at::Tensor& keys, int64_t base, const at::Tensor& grads, double scale,
@@ -519,7 +519,7 @@ std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t 
 void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, const at::Tensor& inv, int64_t F,
                      int64_t D, at::Tensor& grad_rows, int64_t x_off, const c10::optional<at::Tensor>& U_dev,
                      const c10::optional<at::Tensor>& members, const c10::optional<at::Tensor>& memrow,
-                     bool sorted_rows) {
+                     bool sorted_rows, bool zeroed) {
   check_gpu(dX, "dX");
   const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
   check_gpu(inv, "inv");
@@ -552,7 +552,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
                   "members/memrow: int32 [B*F]");
       minips_k::emb_backward_csr(base0, bf0, (int)dX.stride(0), dw, B, (int)F, (int)D, members->data_ptr<int>(),
                                  memrow->data_ptr<int>(), ptr<float>(grad_rows), (int)grad_rows.stride(0), (int)U,
-                                 stream_of(dX), count_ptr(U_dev), sorted_rows);
+                                 stream_of(dX), count_ptr(U_dev), sorted_rows, zeroed);
       return;
     }
     at::Tensor ws = at::empty({3 * U + 1 + 2 * B * F + U / 1024 + 1}, inv.options().dtype(at::kInt));
@@ -1644,7 +1644,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("sparse_rowwise_adagrad", &sparse_rowwise_adagrad, py::arg("table"), py::arg("state"), py::arg("state2"),
         py::arg("D1"), py::arg("keys"), py::arg("base"), py::arg("grads"), py::arg("lr"), py::arg("eps"),
-        py::arg("n_dev") = py::none());
+        py::arg("n_dev") = py::none(), py::arg("zero_g") = false);
   m.def("sparse_sgd", &sparse_sgd, py::arg("table"), py::arg("keys"), py::arg("base"), py::arg("grads"),
         py::arg("scale"), py::arg("n_dev") = py::none());
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
@@ -1658,7 +1658,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_assemble_tab", &wd_assemble_tab);
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
-        py::arg("members") = py::none(), py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);
+        py::arg("members") = py::none(), py::arg("memrow") = py::none(), py::arg("sorted_rows") = false,
+        py::arg("zeroed") = false);
   m.def("emb_rows_ws_ints",
         [](int64_t n, int64_t hot, int64_t D) { return minips_k::emb_rows_ws_ints(n, (int)hot, (int)D); });
   m.def("emb_rows_hot_rows",

@@ -113,7 +113,7 @@ void scatter_add_rows_bf16(const bf16_t* src, int64_t n, int D, const int64_t* i
 // Columns [D1, D) may use a second accumulator state2 (D1 = D: single group).
 void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
                             int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s,
-                            const int64_t* n_dev = nullptr);
+                            const int64_t* n_dev = nullptr, bool zero_g = false);  // zero_g: clear grads after
 // Plain SGD on rows: w[row,:] += scale * g  (the reference's "w += delta" server apply)
 void sparse_sgd(float* table, int64_t ld, const int64_t* keys, int64_t n, int64_t base, int D, const float* grads,
                 float scale, hipStream_t s, const int64_t* n_dev = nullptr);
@@ -170,7 +170,8 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
 // it as one contiguous stream instead of gathering 2*D-byte pieces of [B, F*D] rows.
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                      const int64_t* U_dev = nullptr, bool sorted_rows = false);
+                      const int64_t* U_dev = nullptr, bool sorted_rows = false, bool zeroed = false);
+// (zeroed: grad_rows rows [0, U) are already zero -- no clearing pass)
 // pos[members[m]] = m (n entries): where each lookup's gradient row goes in member order.
 void emb_csr_positions(const int* members, int64_t n, int* pos, hipStream_t s);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,

@@ -414,7 +414,8 @@ __global__ __launch_bounds__(256) void sparse_rowwise_adagrad_v4_kernel(float* t
                                                                         const int64_t* __restrict__ keys, int64_t n,
                                                                         int64_t base, int D,
                                                                         const float* __restrict__ grads, float lr,
-                                                                        float eps, const int64_t* n_dev) {
+                                                                        float eps, const int64_t* n_dev,
+                                                                        float* __restrict__ zero_g) {
   n = dev_count(n, n_dev);
   const int lane = threadIdx.x & 63, sub = lane >> 3, l = lane & 7;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -433,6 +434,10 @@ __global__ __launch_bounds__(256) void sparse_rowwise_adagrad_v4_kernel(float* t
       if (has1) {
         g1 = *reinterpret_cast<const float4*>(grads + i * D + c1);
         t1 = *reinterpret_cast<const float4*>(tr + c1);
+      }
+      if (zero_g) {  // (grads == zero_g) the next push's accumulator, cleared after the read
+        *reinterpret_cast<float4*>(zero_g + i * D + c0) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (has1) *reinterpret_cast<float4*>(zero_g + i * D + c1) = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
     const float st_old1 = ok ? state[row] : 0.f;
@@ -512,7 +517,7 @@ static bool adagrad_v4_enabled() {
 
 void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
                             int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s,
-                            const int64_t* n_dev) {
+                            const int64_t* n_dev, bool zero_g) {
   if (n <= 0) return;
   if (D1 <= 0 || D1 > D) D1 = D;
   if (D1 < D && !state2) throw std::runtime_error("sparse_rowwise_adagrad: split rows need state2");
@@ -521,7 +526,9 @@ void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state
                     reinterpret_cast<uintptr_t>(grads) % 16 == 0 && adagrad_v4_enabled();
   if (vec4) {
     hipLaunchKernelGGL(sparse_rowwise_adagrad_v4_kernel, grid_for(n * 8, block, 16384), block, 0, s, table, ld, state,
-                       state2, D1, keys, n, base, D, grads, lr, eps, n_dev);
+                       state2, D1, keys, n, base, D, grads, lr, eps, n_dev,
+                       zero_g ? const_cast<float*>(grads) : nullptr);
+    zero_g = false;
   } else if (D <= 64) {
     hipLaunchKernelGGL(sparse_rowwise_adagrad_half_kernel, grid_for(n * 32, block, 8192), block, 0, s, table, ld,
                        state, state2, D1, keys, n, base, D, grads, lr, eps, n_dev);
@@ -529,6 +536,8 @@ void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state
     hipLaunchKernelGGL(sparse_rowwise_adagrad_kernel, grid_for(n * 64, block, 4096), block, 0, s, table, ld, state,
                        state2, D1, keys, n, base, D, grads, lr, eps, n_dev);
   }
+  // the other forms clear the gradient rows with a fill after the apply
+  if (zero_g) MINIPS_HIP_CHECK(hipMemsetAsync(const_cast<float*>(grads), 0, sizeof(float) * (size_t)n * D, s));
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

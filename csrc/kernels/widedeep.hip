@@ -915,9 +915,11 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
 template <typename TX>
 static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, int F, int D, const int* members,
                         const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                        const int64_t* U_dev, bool sorted_rows = false) {
+                        const int64_t* U_dev, bool sorted_rows = false, bool zeroed = false) {
   const int total = (int)(B * F);
-  if (U_dev && row_stride % 4 == 0)
+  if (zeroed) {
+    // the buffer's rows are zero already (the previous apply cleared them after reading)
+  } else if (U_dev && row_stride % 4 == 0)
     hipLaunchKernelGGL(zero_rows_dev_kernel, grid_for((int64_t)U * (row_stride / 4), 256, 4096), 256, 0, s, grad_rows,
                        row_stride, (int64_t)U, U_dev);
   else
@@ -1579,15 +1581,15 @@ void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int
 
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                      const int64_t* U_dev, bool sorted_rows) {
+                      const int64_t* U_dev, bool sorted_rows, bool zeroed) {
   if (B <= 0 || U <= 0) return;
   if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("emb_backward_csr: row_stride too small");
   if (bf16)
     emb_seg_sum(static_cast<const bf16_t*>(dX), ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s,
-                U_dev, sorted_rows);
+                U_dev, sorted_rows, zeroed);
   else
     emb_seg_sum(static_cast<const float*>(dX), ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s,
-                U_dev, sorted_rows);
+                U_dev, sorted_rows, zeroed);
 }
 
 __global__ void emb_csr_positions_kernel(const int* __restrict__ members, int64_t n, int* __restrict__ pos) {

@@ -403,12 +403,15 @@ def sparse_apply_bf16(opt, table, state, keys, base, grads, lr, eps=1e-8, scale=
     table[rows] = _sr_bf16(w, torch.Generator().manual_seed((int(seed) * 1000003 + int(step)) & 0x7FFFFFFF))
 
 
-def sparse_rowwise_adagrad(table, state, keys, base, grads, lr, eps=1e-8, state2=None, split=None, n_dev=None):
+def sparse_rowwise_adagrad(table, state, keys, base, grads, lr, eps=1e-8, state2=None, split=None, n_dev=None,
+                           zero_g=False):
+    """Row-wise Adagrad on table rows keys - base. ``zero_g``: the kernel clears the gradient rows
+    after reading them (a persistent, pre-zeroed push buffer stays zero for the next push)."""
     D = grads.shape[1]
     D1 = D if split is None else split
     if _gpu(table):
         kernels().sparse_rowwise_adagrad(table, state, state2, D1, keys, int(base), grads, float(lr), float(eps),
-                                         n_dev)
+                                         n_dev, bool(zero_g))
         return
     if n_dev is not None:
         n = int(n_dev.reshape(-1)[0])
@@ -552,16 +555,18 @@ def emb_build_csr(inv, F, U, zeroed=None, counts_ready=False):
     return order.to(torch.int32), inv[order].to(torch.int32)
 
 
-def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=None, sorted_rows=False):
+def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=None, sorted_rows=False,
+                    zeroed=False):
     """grad_rows[u, :D] = sum of dX[b, x_off + f*D : ...] over the lookups (b, f) with
     inv[b*F+f] == u; column D likewise sums dwide[b] when given. On the GPU every row of
     grad_rows is written (rows without lookups become 0); the CPU reference adds into grad_rows,
     so callers pass a zeroed buffer. ``sorted_rows``: dX is [B*F, D] in the CSR's member order
-    (row m = lookup csr[0][m]; linear_dgrad(perm=csr[2]) writes it)."""
+    (row m = lookup csr[0][m]; linear_dgrad(perm=csr[2]) writes it). ``zeroed``: grad_rows rows
+    [0, U) are zero already (a persistent buffer the apply clears; no clearing pass)."""
     if _gpu(dX):
         members, memrow = (csr[0], csr[1]) if csr is not None else (None, None)
         kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), U_dev, members, memrow,
-                                  bool(sorted_rows))
+                                  bool(sorted_rows), bool(zeroed and members is not None))
         return grad_rows
     if sorted_rows:  # back to lookup order
         un = torch.empty_like(dX)

@@ -594,6 +594,8 @@ def _route_multiplier(num_rows: int) -> int:
 # the dedupe counts each unique key's lookups for the embedding-backward CSR (one pass less);
 # MINIPS_CSR_FUSED=0 counts in emb_build_csr instead
 _CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
+# MINIPS_PERSIST_PUSH=0: a fresh push buffer per clock, cleared by the segment sum (one rank)
+_PERSIST_PUSH = os.environ.get("MINIPS_PERSIST_PUSH", "1") != "0"
 # MINIPS_ROWS_ADAGRAD=1: one rank's embedding backward as the row-parallel fused apply
 # (ops.emb_rows_adagrad) instead of the piecewise segment sum + separate row-wise Adagrad. Off:
 # W&D step 0.417 vs 0.397 ms (lookup order), 0.435 with row-sorted dgrad output
@@ -1058,11 +1060,32 @@ class SparseTable:
             self._pending.append((plan, _LookupGrads(dX[:, x_off:] if x_off else dX, dwide, F, D)))
             return
         dev = self.comm.device
-        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width,
-                                                                         dtype=torch.float32, device=dev)
+        persist = self._persistent_push_ok(plan)
+        if persist:
+            # one rank, synchronous clock: a persistent push buffer the Adagrad apply clears after
+            # reading it (zero_g), so the segment sum needs no clearing pass of its own
+            grad_rows = self._zero_push_rows(max(plan.cap, 1))
+        else:
+            grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width,
+                                                                             dtype=torch.float32, device=dev)
         ops.wd_emb_backward(dX, dwide, plan.inv, F, D, grad_rows, x_off=x_off, U_dev=plan.U_dev, csr=plan.csr,
-                            sorted_rows=sorted_rows)
+                            sorted_rows=sorted_rows, zeroed=persist)
+        if persist:
+            plan.extra["zero_g"] = True
         self.add(plan, grad_rows)
+
+    def _persistent_push_ok(self, plan) -> bool:
+        return (_PERSIST_PUSH and self._local_apply and self.comm.world == 1 and self.comm.device.type == "cuda"
+                and self.optimizer == "rowwise_adagrad" and self.value_dtype == torch.float32
+                and getattr(self, "grad_dtype", torch.float32) == torch.float32 and not self.pipe.async_
+                and plan.csr is not None and plan.U_dev is not None
+                and type(self)._owner_rows is SparseTable._owner_rows)
+
+    def _zero_push_rows(self, n: int) -> torch.Tensor:
+        buf = getattr(self, "_push_rows", None)
+        if buf is None or buf.shape[0] < n:
+            buf = self._push_rows = torch.zeros(max(n, 1), self.width, dtype=torch.float32, device=self.comm.device)
+        return buf[:n]
 
     def _rows_apply_ok(self, plan, dX, dwide, D, x_off) -> bool:
         """One rank, row-wise Adagrad on a local fp32 shard: the embedding backward can apply."""
@@ -1137,9 +1160,9 @@ class SparseTable:
             ops.scatter_add_rows(recv, plan.own_inv, g)
             keys, n_dev = plan.own_uniq, (None if "own_U" in plan.extra else plan.own_U_dev)
         keys, base = self._owner_rows(keys[:n], plan)
-        self._apply_rows(keys, base, g[:n], n_dev)
+        self._apply_rows(keys, base, g[:n], n_dev, zero_g=bool(plan.extra.get("zero_g")))
 
-    def _apply_rows(self, keys, base, g, n_dev=None):
+    def _apply_rows(self, keys, base, g, n_dev=None, zero_g=False):
         if getattr(self, "value_dtype", None) == torch.bfloat16:
             self._applies += 1
             if self.optimizer not in ("rowwise_adagrad", "sgd", "add"):
@@ -1151,7 +1174,7 @@ class SparseTable:
             return
         if self.optimizer == "rowwise_adagrad":
             ops.sparse_rowwise_adagrad(self.shard, self.state, keys, base, g, self.lr, self.eps,
-                                       state2=self.state2, split=self.split, n_dev=n_dev)
+                                       state2=self.state2, split=self.split, n_dev=n_dev, zero_g=zero_g)
         elif self.optimizer == "sgd":
             ops.sparse_sgd(self.shard, keys, base, g.contiguous(), -self.lr, n_dev=n_dev)
         elif self.optimizer == "add":

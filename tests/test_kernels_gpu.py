@@ -537,7 +537,7 @@ def test_rows_emb_backward_adagrad(dev, D, wide, split, sorted_rows):
         res = ops.plan_sorted(keys.to(dev), base.to(dev), bits, positions=sorted_rows)
         uniq, inv, counts, U_dev = res[:4]
         csr = tuple(res[4:])
-        assert len(csr) == 4 and (csr[2] is None) == (not sorted_rows)
+        assert len(csr) == 5 and (csr[2] is None) == (not sorted_rows)  # (.., rowidx: None without routing)
         lookups = torch.randn(B * F, D, generator=g).to(torch.bfloat16)  # lookup order
         if sorted_rows:
             pos = csr[2].cpu().long()
