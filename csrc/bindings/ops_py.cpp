@@ -1248,6 +1248,15 @@ void ps_push_rows(const at::Tensor& uniq, const at::Tensor& counts, const c10::o
                          (int)g.size(1), ptr<int64_t>(inbox), (int)P, slot_off, cap, stream_of(g));
 }
 
+void ps_push_dense(at::Tensor& grad, const at::Tensor& inbox, int64_t data_off, int64_t S) {
+  check_gpu(grad, "grad");
+  check_dtype(grad, at::kFloat, "grad");
+  check_gpu(inbox, "inbox");
+  TORCH_CHECK(grad.numel() >= inbox.numel() * S, "grad: >= P * S floats");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(grad.device());
+  minips_k::ps_push_dense(ptr<float>(grad), ptr<int64_t>(inbox), (int)inbox.numel(), data_off, S, stream_of(grad));
+}
+
 void ps_set_headers(const at::Tensor& inbox, int64_t slot_off, int64_t value) {
   check_long_dev(inbox, "inbox");
   TORCH_CHECK(inbox.numel() >= 1 && inbox.numel() <= minips_k::kPsMaxWorld, "inbox must list 1..16 owners");
@@ -1696,6 +1705,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("ps_push_rows", &ps_push_rows, py::arg("uniq"), py::arg("counts"), py::arg("U_dev"), py::arg("n"),
         py::arg("g"), py::arg("inbox"), py::arg("slot_off"), py::arg("cap"));
   m.def("ps_set_headers", &ps_set_headers);
+  m.def("ps_push_dense", &ps_push_dense);
   m.def("ps_gather_rows_bf16tab", &ps_gather_rows_bf16tab, py::arg("bases"), py::arg("bounds"), py::arg("keys"),
         py::arg("n_dev"), py::arg("W"), py::arg("out"));
   m.def("ps_hash_gather", &ps_hash_gather, py::arg("hkeys"), py::arg("hvals"), py::arg("bounds"), py::arg("cap"),

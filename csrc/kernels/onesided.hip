@@ -505,6 +505,30 @@ void ps_push_rows(const int64_t* uniq, const int64_t* counts, const int64_t* U_d
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// The dense push of one clock: owner o's slice grad[o * S, (o + 1) * S) into the data area of slot
+// `slot_off` of its inbox, and grad cleared for the next clock -- one pass (read once, write the
+// slot and the zero) instead of P copies and a fill.
+__global__ __launch_bounds__(256) void ps_push_dense_kernel(float* __restrict__ grad, const int64_t* __restrict__ inbox,
+                                                            int P, int64_t data_off, int64_t S4) {
+  const int64_t total = (int64_t)P * S4;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int o = (int)(e / S4);
+    const int64_t k = e - (int64_t)o * S4;
+    const float4 v = reinterpret_cast<const float4*>(grad)[e];
+    reinterpret_cast<float4*>(reinterpret_cast<char*>(inbox[o]) + data_off)[k] = v;
+    reinterpret_cast<float4*>(grad)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+void ps_push_dense(float* grad, const int64_t* inbox, int P, int64_t data_off, int64_t S, hipStream_t s) {
+  if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_push_dense: P out of range");
+  if (S % 4 || data_off % 16 || reinterpret_cast<uintptr_t>(grad) % 16)
+    throw std::runtime_error("ps_push_dense: 16-byte aligned shards");
+  hipLaunchKernelGGL(ps_push_dense_kernel, grid_for((int64_t)P * (S / 4), 256, 8192), 256, 0, s, grad, inbox, P,
+                     data_off, S / 4);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 void ps_set_headers(const int64_t* inbox, int P, int64_t slot_off, int64_t value, hipStream_t s) {
   if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_set_headers: P out of range");
   hipLaunchKernelGGL(ps_set_headers_kernel, 1, 64, 0, s, inbox, P, slot_off, value);

@@ -970,10 +970,15 @@ class AsyncDenseTable(_AsyncTable):
         off = (self.comm.rank * self.depth + slot) * self.slot_bytes
         S = self.shard
         if self._pending:
-            for o in range(self.comm.world):
-                dst = self._inbox[o][off + _SLOT_HEADER: off + _SLOT_HEADER + 4 * S].view(torch.float32)
-                dst.copy_(self.grad[o * S: (o + 1) * S])
-            self.grad.zero_()
+            if self.cuda and S % 4 == 0:  # one pass: every owner's slice into its slot, grad cleared
+                from .._native import kernels
+
+                kernels().ps_push_dense(self.grad, self._inbox_ptrs, off + _SLOT_HEADER, S)
+            else:
+                for o in range(self.comm.world):
+                    dst = self._inbox[o][off + _SLOT_HEADER: off + _SLOT_HEADER + 4 * S].view(torch.float32)
+                    dst.copy_(self.grad[o * S: (o + 1) * S])
+                self.grad.zero_()
         if self.cuda:
             from .._native import kernels
 

@@ -4,7 +4,7 @@
 set -eo pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out/r4
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_widedeep_gpu.py tests/test_onesided.py tests/test_onesided_consistency.py -x -q -m gpu -k "widedeep or adagrad or emb" --timeout 280 --timeout-method thread > gpurun_out/r4/wd3_tests.log 2>&1 || { tail -60 gpurun_out/r4/wd3_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_widedeep_gpu.py tests/test_onesided.py tests/test_onesided_consistency.py -x -q -m gpu -k "widedeep or adagrad or emb or onesided or torn or lazy" --timeout 280 --timeout-method thread > gpurun_out/r4/wd3_tests.log 2>&1 || { tail -60 gpurun_out/r4/wd3_tests.log; exit 1; }
 tail -2 gpurun_out/r4/wd3_tests.log
 for i in 1 2; do
   for cfg in "MINIPS_PERSIST_PUSH=1" "MINIPS_PERSIST_PUSH=0"; do
