@@ -77,9 +77,11 @@ _DENSE_CLOCK_ON_SIDE = os.environ.get("MINIPS_DENSE_CLOCK_ON_SIDE", "0") == "1"
 # In the whole W&D step on one MI355X (tools/gpu_ab.sh, ms/step): ext/8 0.453, ext/64 0.451,
 # vec/8 0.460, vec/64 0.457 -- the isolated GEMM gains of "vec" (fwd2 -7 us, W2 wgrad -10 us)
 # do not survive the 3-stream overlap (its W2 weight gradient switches to 512 128x128 blocks,
-# which crowd the dgrad chain), so "ext" with a 64-aligned layer-1 K is the default.
+# which crowd the dgrad chain), so "ext" with a 64-aligned layer-1 K was the default through round 3.
+# Round 4 (split-K planes folded by Adam, fence-free forks, the rest of this round's step): vec
+# 0.3879 / 0.3882 vs ext 0.4016 / 0.4021 ms/step (profiles/r4/ab_wd_knobs.txt) -- "vec" by default.
 _K1_ALIGN = int(os.environ.get("MINIPS_WD_K1_ALIGN", "64"))
-_BIAS_VEC = os.environ.get("MINIPS_WD_BIAS", "ext") == "vec"
+_BIAS_VEC = os.environ.get("MINIPS_WD_BIAS", "vec") == "vec"
 # MINIPS_WD_FUSED_HEAD=1: layer 3 and the output head as one GEMM (ops.wd_fwd_head, H3 never
 # written). Measured off: the fused kernel took 51 us vs 17 + 24 us for the GEMM + wd_head (its
 # dw4 / db4 / loss reductions are 256 same-address atomics per column from 256 workgroups).
