@@ -98,6 +98,8 @@ _WGRAD_BLOCKS = int(os.environ.get("MINIPS_WD_WGRAD_BLOCKS", "320"))
 _WGRAD_LIB = os.environ.get("MINIPS_WD_WGRAD", "ours") == "lib"
 
 
+# MINIPS_DENSE_ON_SIDE=0: one rank's dense Adam on the main stream at the step end (joined)
+_DENSE_ON_SIDE = os.environ.get("MINIPS_DENSE_ON_SIDE", "1") != "0"
 # MINIPS_ROWIDX=0: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
 _ROWIDX = os.environ.get("MINIPS_ROWIDX", "1") != "0"
 
@@ -226,6 +228,9 @@ class WideDeep(LookaheadPlans):
         """Forward only (eval): returns logits [B] fp32."""
         B = dense.shape[0]
         b = self._buffers(B)
+        pend_side = self.__dict__.pop("_side_pending", None)
+        if pend_side is not None:  # the last train step's Adam (side stream) before W is read
+            torch.cuda.current_stream(self.comm.device).wait_event(pend_side[1])
         P = self.dense.get()
         F, D = self.cfg.F, self.cfg.emb_dim
         ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0])
@@ -262,6 +267,9 @@ class WideDeep(LookaheadPlans):
                 self.prefetch(nk, keys_on_plan_stream=next_on_plan_stream)
 
         issue_next("start")
+        pend_side = self.__dict__.pop("_side_pending", None)
+        if pend_side is not None:  # the previous step's weight gradients read X: done before it is rewritten
+            torch.cuda.current_stream(self.comm.device).wait_event(pend_side[0])
         src = self.emb.get_source(keys, plan=plan)  # one rank: the rows are read in place
         if src is not None:
             plan, table, index, base = src
@@ -272,6 +280,8 @@ class WideDeep(LookaheadPlans):
         else:
             rows, plan = self.emb.get(keys, plan=plan)
             ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
+        if pend_side is not None:  # ... and its dense Adam ran (side stream) before the forward reads W
+            torch.cuda.current_stream(self.comm.device).wait_event(pend_side[1])
         G = self.dense.grad
         P = self.dense.get()
         scale = 1.0 / (B * self.comm.world)
@@ -344,10 +354,23 @@ class WideDeep(LookaheadPlans):
         dXe = b["dX"].view(B * F, D) if sorted_rows else b["dX"]
         self.emb.add_lookup_grads(plan, dXe, b["dwide"], F, D, sorted_rows=sorted_rows)  # the table reduces
         self.emb.clock()
-        side.join()
-        if not dense_early:
-            self.dense.add()
-            self.dense.clock()
+        dense_side = (_DENSE_ON_SIDE and not dense_early and side.stream is not None and self.comm.world == 1
+                      and pipe is not None and not pipe.async_ and not torch.cuda.is_current_stream_capturing())
+        if dense_side:
+            # one rank, synchronous clock: the dense Adam runs on the side stream right behind the
+            # last weight gradient, and the main stream does not join here -- the next step waits
+            # for the weight gradients before its assembly rewrites X and for the Adam before its
+            # forward reads W, so the Adam overlaps the next step's input assembly
+            ev_x = side.mark()
+            with torch.cuda.stream(side.stream):
+                self.dense.add()
+                self.dense.clock()
+            self._side_pending = (ev_x, side.mark())
+        else:
+            side.join()
+            if not dense_early:
+                self.dense.add()
+                self.dense.clock()
         self._advance_next_plan()
         return b["loss"]
 
@@ -362,5 +385,8 @@ class WideDeep(LookaheadPlans):
                 self.dense.bucket_ready(j, events=(side.mark(),))
 
     def drain(self):
+        pend_side = self.__dict__.pop("_side_pending", None)
+        if pend_side is not None:
+            torch.cuda.current_stream(self.comm.device).wait_event(pend_side[1])
         self.emb.drain()
         self.dense.drain()
