@@ -71,9 +71,8 @@ _LM_WGRAD = os.environ.get("MINIPS_LM_WGRAD", "mm")  # lib form of the wte wgrad
 # MLP: the fc forward saves gelu'(u) (its tanh is computed there anyway) and the fc2 dgrad multiplies
 # by it; MINIPS_GPT2_GELU_D=0 saves u and re-evaluates tanh in the dgrad epilogue
 _GELU_D = os.environ.get("MINIPS_GPT2_GELU_D", "1") == "1"
-# per-layer weight gradients: "ours" (split-K gemm.hip, atomic fp32) or "lib" (each gradient has one
-# writer per step: an overwriting hipBLASLt GEMM with fp32 output)
-_WGRAD = os.environ.get("MINIPS_GPT2_WGRAD", "ours")
+# per-layer weight gradients: split-K gemm.hip (the hipBLASLt form, MINIPS_GPT2_WGRAD=lib, measured
+# 13.0-13.1 vs 12.78 ms/step in round 3 and was removed in round 4)
 
 
 class GPT2:
@@ -225,12 +224,11 @@ class GPT2:
         dx = b["dx"]
         ops.layernorm_bwd(x[-1], dh, d, v(P, "lnf_g"), mf, rf, dx, v(G, "lnf_g"), v(G, "lnf_b"))
         ev_du = ev_dqkv = None
-        wl = _WGRAD == "lib"
         for i in range(c.n_layer - 1, -1, -1):
             blk = self.blocks[i]
             # MLP branch
             with side.fork():
-                blk["fc2"].wgrad(G, dx, b["g"][i], wl)
+                blk["fc2"].wgrad(G, dx, b["g"][i])
             ev_dx = side.mark()
             side.wait(ev_du)  # du: read by the previous layer's fc wgrad
             if _GELU_D:
@@ -238,7 +236,7 @@ class GPT2:
             else:
                 blk["fc2"].dgrad(P, dx, b["du"], gelu_u=b["u"][i])
             with side.fork():
-                blk["fc"].wgrad(G, b["du"], b["h2"][i], wl)
+                blk["fc"].wgrad(G, b["du"], b["h2"][i])
             ev_du = side.mark()
             blk["fc"].dgrad(P, b["du"], dh)
             m2, r2 = b["st2"][i]
@@ -247,13 +245,13 @@ class GPT2:
                               v(G, blk["ln2_b"]), accumulate=True)
             # attention branch
             with side.fork():
-                blk["proj"].wgrad(G, dx, b["ao"][i], wl)
+                blk["proj"].wgrad(G, dx, b["ao"][i])
             ev_dx = side.mark()
             blk["proj"].dgrad(P, dx, b["dao"])
             side.wait(ev_dqkv)  # dqkv: read by the previous layer's qkv wgrad
             ops.attn_bwd(b["qkv"][i], b["ao"][i], b["dao"], b["lse"][i], b["delta"], B, T, c.n_head, scale, b["dqkv"])
             with side.fork():
-                blk["qkv"].wgrad(G, b["dqkv"], b["h1"][i], wl)
+                blk["qkv"].wgrad(G, b["dqkv"], b["h1"][i])
             ev_dqkv = side.mark()
             blk["qkv"].dgrad(P, b["dqkv"], dh)
             m1, r1 = b["st1"][i]

@@ -85,12 +85,8 @@ class Linear:
         epi = {"relu": ops.EPI_BIAS_RELU_BF16, "none": ops.EPI_BIAS_BF16}[act]
         return ops.gemm(x_ext, W, out, M, self.n_out, self.k_pad, False, False, epi)
 
-    def wgrad(self, G, dy, x_ext, overwrite_lib=False):
-        """G_W += dy^T x_ext (split-K; the bias gradient lands in column k_in). ``overwrite_lib``
-        (the step's only writer of this gradient, GPU): G_W = dy^T x_ext as one hipBLASLt GEMM with
-        fp32 output."""
-        if overwrite_lib and dy.is_cuda:
-            return torch.mm(dy.t(), x_ext, out_dtype=torch.float32, out=self.W(G)[: self.n_out])
+    def wgrad(self, G, dy, x_ext):
+        """G_W += dy^T x_ext (split-K gemm.hip; the bias gradient lands in column k_in)."""
         return ops.linear_wgrad(dy, x_ext, self.W(G))
 
     def dgrad(self, P, dy, out, mask=None, gelu_u=None, out_f32=False, k_rows=None, gelu_d=None):

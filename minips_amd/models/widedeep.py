@@ -93,9 +93,6 @@ _TRIM = os.environ.get("MINIPS_WD_TRIM", "0") == "1"
 # split-K workgroup target of the three weight gradients (ops.linear_wgrad blocks): W&D 0.402 ms at
 # 320 vs 0.409-0.412 at the default 512 (GPT-2 keeps 512: 12.90 vs 13.18 ms at 256), ab_wd_r3.txt
 _WGRAD_BLOCKS = int(os.environ.get("MINIPS_WD_WGRAD_BLOCKS", "320"))
-# MINIPS_WD_WGRAD=lib: the three weight gradients as overwriting hipBLASLt GEMMs with fp32 output
-# (each gradient has one writer per step) instead of the split-K gemm.hip path
-_WGRAD_LIB = os.environ.get("MINIPS_WD_WGRAD", "ours") == "lib"
 
 
 # MINIPS_DENSE_ON_SIDE=0: one rank's dense Adam on the main stream at the step end (joined)
@@ -105,8 +102,7 @@ _ROWIDX = os.environ.get("MINIPS_ROWIDX", "1") != "0"
 
 
 def _wgrad(dH, H, Gw, sink=None):
-    if _WGRAD_LIB and dH.is_cuda:
-        return torch.mm(dH.t(), H, out_dtype=torch.float32, out=Gw[: dH.shape[1]])
+    # (round 4: the hipBLASLt alternative, MINIPS_WD_WGRAD=lib, measured slower and removed)
     return ops.linear_wgrad(dH, H, Gw, blocks=_WGRAD_BLOCKS, defer=sink)
 
 
