@@ -467,7 +467,7 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
 void wd_fwd_head(const at::Tensor& A, const at::Tensor& W, int64_t K, const at::Tensor& w4,
                  const at::Tensor& wide_logit, const at::Tensor& labels, at::Tensor& dH, at::Tensor& dw4,
                  at::Tensor& dwide, at::Tensor& loss_sum, double grad_scale,
-                 const c10::optional<at::Tensor>& dH_colsum) {
+                 const c10::optional<at::Tensor>& dH_colsum, const c10::optional<at::Tensor>& bias) {
   for (const at::Tensor* t : {&A, &W, &w4, &wide_logit, &labels, (const at::Tensor*)&dH, (const at::Tensor*)&dw4,
                               (const at::Tensor*)&dwide, (const at::Tensor*)&loss_sum})
     check_gpu(*t, "wd_fwd_head");
@@ -487,11 +487,13 @@ void wd_fwd_head(const at::Tensor& A, const at::Tensor& W, int64_t K, const at::
               "wd_fwd_head shapes");
   float* cs = strided_vec_ptr(dH_colsum, "dH_colsum");
   if (cs) TORCH_CHECK(dH_colsum->numel() >= N, "dH_colsum: >= N values");
+  const bf16_t* bp = opt_ptr<bf16_t>(bias, at::kBFloat16, "bias");
+  if (bp) TORCH_CHECK(bias->numel() >= N, "bias: >= N values");
   c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
   minips_k::gemm_wd_head(ptr<bf16_t>(A), ptr<bf16_t>(W), (int)M, (int)N, (int)K, (int)A.stride(0), (int)W.stride(0),
                          ptr<bf16_t>(dH), (int)dH.stride(0), ptr<bf16_t>(w4), ptr<float>(wide_logit),
                          ptr<float>(labels), ptr<float>(dw4), ptr<float>(dwide), ptr<float>(loss_sum),
-                         (float)grad_scale, stream_of(A), cs, cs ? (int)dH_colsum->stride(0) : 1);
+                         (float)grad_scale, stream_of(A), cs, cs ? (int)dH_colsum->stride(0) : 1, bp);
 }
 
 // Lookup CSR grouped by unique row (members/memrow int32 [B*F]) for U (upper-bound) rows.
@@ -1663,7 +1665,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_head", &wd_head);
   m.def("wd_fwd_head", &wd_fwd_head, py::arg("A"), py::arg("W"), py::arg("K"), py::arg("w4"), py::arg("wide_logit"),
         py::arg("labels"), py::arg("dH"), py::arg("dw4"), py::arg("dwide"), py::arg("loss_sum"), py::arg("grad_scale"),
-        py::arg("dH_colsum") = py::none());
+        py::arg("dH_colsum") = py::none(), py::arg("bias") = py::none());
   m.def("wd_assemble_tab", &wd_assemble_tab);
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),

@@ -188,7 +188,7 @@ int gemm_slab(const bf16_t* A, const bf16_t* B, float* slab, int M, int N, int K
 
 void gemm_wd_head(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, bf16_t* dH, int lddh,
                   const bf16_t* w4, const float* wide, const float* labels, float* dw4, float* dwide, float* loss,
-                  float scale, hipStream_t s, float* dh_colsum, int dh_colsum_ld) {
+                  float scale, hipStream_t s, float* dh_colsum, int dh_colsum_ld, const bf16_t* bias) {
   if (M <= 0) return;
   if (N <= 0 || N > 256 || N % 8 || K % 8 || lda % 8 || ldb % 8 || lddh % 8)
     throw std::runtime_error("gemm_wd_head: N <= 256, N / K / leading dims multiples of 8");
@@ -203,6 +203,26 @@ void gemm_wd_head(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda
   ep.head_scale = scale;
   ep.head_dh_colsum = dh_colsum;
   ep.head_dh_colsum_ld = dh_colsum_ld;
+  ep.head_bias = bias;
+  // the two-level fold of the workgroups' partial rows (<= 256 workgroups: 16 groups of 16);
+  // per-device slab + tickets allocated once (tickets zero), before any capture
+  const int nwg = (M + 63) / 64;
+  if (nwg <= 256) {
+    static thread_local std::vector<std::pair<int, void*>> cache;
+    int dev = 0;
+    MINIPS_HIP_CHECK(hipGetDevice(&dev));
+    void* ws = nullptr;
+    for (auto& e : cache)
+      if (e.first == dev) ws = e.second;
+    const size_t slab_bytes = sizeof(float) * (256 + 16) * (2 * 256 + 2);
+    if (!ws) {
+      MINIPS_HIP_CHECK(hipMalloc(&ws, slab_bytes + 256));
+      MINIPS_HIP_CHECK(hipMemset(ws, 0, slab_bytes + 256));
+      cache.push_back({dev, ws});
+    }
+    ep.head_slab = static_cast<float*>(ws);
+    ep.head_ticket = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + slab_bytes);
+  }
   // 64 x 256 tiles: a workgroup holds whole rows (all N columns), 4 waves side by side along N;
   // 80 KiB of LDS -> 2 workgroups per CU, M / 64 workgroups (256 at the W&D batch)
   hipLaunchKernelGGL((gemm_v2_kernel<64, 256, false, false, kEpiWdHead>), dim3((M + 63) / 64, 1, 1), dim3(256), 0, s,

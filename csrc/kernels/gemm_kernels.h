@@ -127,6 +127,9 @@ struct EpiArgs {
   float head_scale = 0.f;             // gradient scale (1 / global batch)
   float* head_dh_colsum = nullptr;    // [N] (stride head_dh_colsum_ld) += column sums of dH (optional)
   int head_dh_colsum_ld = 1;
+  const bf16_t* head_bias = nullptr;  // [N] the hidden layer's bias (nullptr: folded into K)
+  float* head_slab = nullptr;         // [workgroups + groups][2N + 2] partial rows of the fold
+  unsigned* head_ticket = nullptr;    // 1 + groups tickets (zero before and after a launch)
   int colsum_ld = 1;                  // kEpiReluMaskBf16: colsum[col * colsum_ld] (a column of a matrix)
   // kEpiFoldF32: C is this K slice's slab plane; the tile's last slice adds every plane into
   // fold_out (ldc fold_ldc); fold_cnt[tile] counts the slices that arrived (the last one re-zeroes it)
@@ -633,11 +636,12 @@ __device__ __forceinline__ void wd_head_epilogue(v4f (&acc)[4][4], const EpiArgs
   const int col_l = lane & 15, row_q = (lane >> 4) * 4;
   const int mb = m0 + wm * 64, nb = wn * 64;
   float* zp = lds + NW * kScrFloats;  // [TM][WN] wave partials of z, past the per-wave scratch
-  float wv[4];
+  float wv[4], bv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = nb + j * 16 + col_l;
     wv[j] = col < N ? bf2f(ep.bias[col]) : 0.f;
+    bv[j] = (ep.head_bias && col < N) ? bf2f(ep.head_bias[col]) : 0.f;
   }
   float zr[4][4];
 #pragma unroll
@@ -647,7 +651,7 @@ __device__ __forceinline__ void wd_head_epilogue(v4f (&acc)[4][4], const EpiArgs
       float a = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float h = __uint_as_float(pack_bf2(fmaxf(acc[i][j][r] * ep.alpha, 0.f), 0.f) << 16);
+        const float h = __uint_as_float(pack_bf2(fmaxf(acc[i][j][r] * ep.alpha + bv[j], 0.f), 0.f) << 16);
         acc[i][j][r] = h;
         a += h * wv[j];
       }
@@ -704,21 +708,103 @@ __device__ __forceinline__ void wd_head_epilogue(v4f (&acc)[4][4], const EpiArgs
   for (int j = 0; j < 4; ++j) {
     cs[j] += __shfl_xor(cs[j], 16, 64);
     cs[j] += __shfl_xor(cs[j], 32, 64);
-    const int col = nb + j * 16 + lane;
-    if (lane < 16 && col < N) atomicAdd(ep.colsum + col, cs[j]);
-    if (ep.head_dh_colsum) {  // the next layer's folded-bias gradient (dH's column sums)
-      cg[j] += __shfl_xor(cg[j], 16, 64);
-      cg[j] += __shfl_xor(cg[j], 32, 64);
-      if (lane < 16 && col < N) atomicAdd(ep.head_dh_colsum + (int64_t)col * ep.head_dh_colsum_ld, cg[j]);
-    }
+    cg[j] += __shfl_xor(cg[j], 16, 64);
+    cg[j] += __shfl_xor(cg[j], 32, 64);
   }
   if (wn == 0) {
     dbl = warp_sum(dbl);
     lossl = warp_sum(lossl);
-    if (lane == 0) {
+  }
+  if (!ep.head_slab) {  // (no fold workspace: same-address atomics, one per column per workgroup)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = nb + j * 16 + lane;
+      if (lane < 16 && col < N) atomicAdd(ep.colsum + col, cs[j]);
+      if (ep.head_dh_colsum && lane < 16 && col < N)
+        atomicAdd(ep.head_dh_colsum + (int64_t)col * ep.head_dh_colsum_ld, cg[j]);
+    }
+    if (wn == 0 && lane == 0) {
       atomicAdd(ep.colsum + N, dbl);
       atomicAdd(ep.head_loss, lossl);
     }
+    return;
+  }
+  // Two-level fold of the workgroups' partial rows {dw4 [N] | dH colsum [N] | db4 | loss}, every
+  // hand-off write-through (cdna_hip_programming.md Guideline 16 R1: sc1 stores, drain, relaxed
+  // ticket, one acquire by the folder): 256 workgroups x 2N same-address atomics were what made
+  // this fused head slower than the GEMM + wd_head pair (51 vs 41 us, round 3).
+  static_assert(TM == 64 && TN == 256, "the fold's partial row is laid out for one 64 x 256 tile per row band");
+  constexpr int G = 16;  // workgroups per group
+  const int NP = 2 * N + 2;
+  const int nb_ = (int)gridDim.x, ngroups = (nb_ + G - 1) / G, blk = blockIdx.x, grp = blk / G;
+  float* prow = ep.head_slab + (int64_t)blk * NP;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = nb + j * 16 + lane;
+    if (lane < 16 && col < N) {
+      __hip_atomic_store(prow + col, cs[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(prow + N + col, cg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (wn == 0 && lane == 0) {
+    __hip_atomic_store(prow + 2 * N, dbl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(prow + 2 * N + 1, lossl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  int* flag = reinterpret_cast<int*>(zp + TM * WN);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int gn = min(G, nb_ - grp * G);
+    const unsigned t = __hip_atomic_fetch_add(ep.head_ticket + 1 + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == (unsigned)gn - 1;
+    if (last) {
+      __hip_atomic_store(ep.head_ticket + 1 + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  {
+    const int g0 = grp * G, gn = min(G, nb_ - g0);
+    float* grow = ep.head_slab + (int64_t)(nb_ + grp) * NP;
+    for (int c = threadIdx.x; c < NP; c += blockDim.x) {
+      float v[G];
+#pragma unroll
+      for (int k = 0; k < G; ++k) v[k] = k < gn ? ep.head_slab[(int64_t)(g0 + k) * NP + c] : 0.f;
+      float tot = 0.f;
+#pragma unroll
+      for (int k = 0; k < G; ++k) tot += v[k];
+      __hip_atomic_store(grow + c, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ep.head_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == (unsigned)ngroups - 1;
+    if (last) {
+      __hip_atomic_store(ep.head_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  for (int c = threadIdx.x; c < NP; c += blockDim.x) {
+    float v[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) v[k] = k < ngroups ? ep.head_slab[(int64_t)(nb_ + k) * NP + c] : 0.f;
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < G; ++k) tot += v[k];
+    if (c < N) ep.colsum[c] += tot;
+    else if (c < 2 * N) {
+      if (ep.head_dh_colsum) ep.head_dh_colsum[(int64_t)(c - N) * ep.head_dh_colsum_ld] += tot;
+    } else if (c == 2 * N) ep.colsum[N] += tot;
+    else *ep.head_loss += tot;
   }
 }
 

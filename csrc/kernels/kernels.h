@@ -56,7 +56,8 @@ void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, i
 // dw4[N] += dz, dwide = dz, loss += BCE-with-logits (same numerics as wd_head on a bf16 H3)
 void gemm_wd_head(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, bf16_t* dH, int lddh,
                   const bf16_t* w4, const float* wide, const float* labels, float* dw4, float* dwide, float* loss,
-                  float scale, hipStream_t s, float* dh_colsum = nullptr, int dh_colsum_ld = 1);
+                  float scale, hipStream_t s, float* dh_colsum = nullptr, int dh_colsum_ld = 1,
+                  const bf16_t* bias = nullptr);  // bias: the hidden layer's bias vector (H3 = relu(. + bias))
 // Batched form: `batch` GEMMs, z = blockIdx.y; operand offsets are (z / inner) * s_outer +
 // (z % inner) * s_inner elements (e.g. attention heads inside a [B*T, H*dh] activation).
 void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,

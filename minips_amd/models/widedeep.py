@@ -282,7 +282,14 @@ class WideDeep(LookaheadPlans):
         P = self.dense.get()
         scale = 1.0 / (B * self.comm.world)
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
-        if _FUSED_HEAD and not _BIAS_VEC:
+        if _FUSED_HEAD and _BIAS_VEC:
+            # layer 3 + the output head in one GEMM (H3 never leaves the chip): the head's sums fold
+            # in two write-through levels; dH3's column sums are the layer-3 bias gradient
+            ops.linear_fwd(b["X"], self.view(P, "W1"), None, "relu", out=b["H1"])
+            ops.linear_fwd(b["H1"], self.view(P, "W2"), self.view(P, "b2"), "relu", out=b["H2"])
+            ops.wd_fwd_head(b["H2"], self.view(P, "W3"), self.k_in[2], w4, b["wide"], labels, b["dH3"], gw4,
+                            b["dwide"], b["loss"], scale, dH_colsum=self.view(G, "b3"), bias=self.view(P, "b3"))
+        elif _FUSED_HEAD:
             # layer 3 + the output head in one GEMM: H3 never leaves the chip (ops.wd_fwd_head)
             ops.linear_fwd(b["X"], self.view(P, "W1"), None, "relu", out=b["H1"])
             ops.linear_fwd(b["H1"], self.view(P, "W2"), None, "relu", out=b["H2"])

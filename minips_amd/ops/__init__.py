@@ -518,17 +518,20 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
 
 
 def wd_fwd_head(A, W, K, w4, wide_logit, labels, dH, dw4, dwide, loss_sum, grad_scale=1.0, H_out=None,
-                dH_colsum=None):
+                dH_colsum=None, bias=None):
     """Last hidden layer + W&D output head fused (GPU: one GEMM, H3 stays on chip): H3 =
-    relu(A[:, :K] W[:, :K]^T) rounded to bf16, then wd_head(H3, w4[:N], w4[N], ...) with dw4[:N]
-    / dw4[N] the head's weight / bias gradients; ``dH_colsum`` (a 1-D, possibly strided view)
-    += the column sums of dH. ``H_out`` (CPU only) receives H3."""
+    relu(A[:, :K] W[:, :K]^T (+ bias)) rounded to bf16, then wd_head(H3, w4[:N], w4[N], ...) with
+    dw4[:N] / dw4[N] the head's weight / bias gradients; ``dH_colsum`` (a 1-D, possibly strided
+    view) += the column sums of dH. ``H_out`` (CPU only) receives H3."""
     N = W.shape[0]
     if _gpu(A):
         kernels().wd_fwd_head(A, W, int(K), w4, wide_logit, labels, dH, dw4, dwide, loss_sum, float(grad_scale),
-                              dH_colsum)
+                              dH_colsum, bias)
         return
-    H = torch.relu(A[:, :K].float() @ W[:, :K].float().t()).to(torch.bfloat16)
+    acc = A[:, :K].float() @ W[:, :K].float().t()
+    if bias is not None:
+        acc = acc + bias[:N].float()
+    H = torch.relu(acc).to(torch.bfloat16)
     if H_out is not None:
         H_out.copy_(H)
     wd_head(H, w4[:N], w4[N:N + 1], wide_logit, labels, dH, dw4[:N], dw4[N:N + 1], dwide, loss_sum,
