@@ -137,6 +137,11 @@ struct EpiArgs {
   int fold_ldc = 0;
   unsigned* fold_cnt = nullptr;
   int fold_nsplit = 1;
+  // split-K launches (gridDim.z > 1, gridDim.y == 1): deal (K slice, tile) pairs to the XCDs in
+  // contiguous runs, tile fastest, so an XCD's workgroups share one K slice's operand rows through
+  // its L2 (the plain tile remap gives each XCD whole tile rows over every slice: each XCD then
+  // streams the full other operand)
+  int zmap = 0;
 };
 
 // Destination of an output row segment (kEpiPermRowsBf16: the permuted row of its segment).
@@ -813,7 +818,7 @@ __device__ __forceinline__ void wd_head_epilogue(v4f (&acc)[4][4], const EpiArgs
 // this CU's L1 drops the planes' lines) and adds the tile's nsplit planes into ep.fold_out.
 // Correct for any placement of a tile's slices over CUs / XCDs (cdna_hip_programming.md G16 R1).
 template <int TM, int TN>
-__device__ __forceinline__ void splitk_fold(const EpiArgs& ep, int M, int N, int m0, int n0, int tile,
+__device__ __forceinline__ void splitk_fold(const EpiArgs& ep, int M, int N, int m0, int n0, int tile, int ks,
                                             unsigned* __restrict__ flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its plane stores
   __syncthreads();
@@ -830,7 +835,7 @@ __device__ __forceinline__ void splitk_fold(const EpiArgs& ep, int M, int N, int
   __syncthreads();
   if (!*flag) return;
   const int64_t plane = ep.sc_split;
-  const float* p0 = (const float*)ep.C - (int64_t)blockIdx.z * plane;
+  const float* p0 = (const float*)ep.C - (int64_t)ks * plane;
   constexpr int PER_ROW = TN / 4;
   for (int i = threadIdx.x; i < TM * PER_ROW; i += blockDim.x) {
     const int rr = i / PER_ROW, c4 = (i - rr * PER_ROW) * 4;
@@ -880,8 +885,15 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_n = (N + TN - 1) / TN, tiles_m = (M + TM - 1) / TM;
   const int nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  if (nwg >= 16) {
+  int bid = blockIdx.x, ks = blockIdx.z;
+  if (ep.zmap && gridDim.z > 1 && gridDim.y == 1) {
+    // dispatch order is x fastest: L = x + nwg * z; XCD-contiguous runs over w = slice * nwg + tile
+    const int W = nwg * (int)gridDim.z, L = bid + nwg * ks;
+    const int xcd = L & 7, q = W >> 3, r = W & 7;
+    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+    ks = w / nwg;
+    bid = w - ks * nwg;
+  } else if (nwg >= 16) {
     int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
     bid = base + (bid >> 3);
@@ -892,13 +904,13 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
     const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
     A += zo * ep.sa_o + zi * ep.sa_i;
     B += zo * ep.sb_o + zi * ep.sb_i;
-    const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)blockIdx.z * ep.sc_split;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)ks * ep.sc_split;
     const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32 || EPI == kEpiFoldF32;
     ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
   }
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7ffffff0, 0x00020000);
-  const int kb = blockIdx.z * k_chunk;
+  const int kb = ks * k_chunk;
   const int ke = min(K, kb + k_chunk);
   const int nt = ke > kb ? (ke - kb + BK2 - 1) / BK2 : 0;
 
@@ -954,7 +966,7 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
   else
     epilogue<EPI>(acc, ep, M, N, m0, n0, wm, wn, lane);
   if constexpr (EPI == kEpiFoldF32)  // (the flag word lies past every wave's epilogue scratch)
-    splitk_fold<TM, TN>(ep, M, N, m0, n0, bid,
+    splitk_fold<TM, TN>(ep, M, N, m0, n0, bid, ks,
                         reinterpret_cast<unsigned*>(reinterpret_cast<float*>(&smem[0][0]) + NWAVES * kScrFloats));
 }
 
@@ -1580,18 +1592,27 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
       else
         hipLaunchKernelGGL((gemm_v3_kernel<A_KM, B_KN, EPI, false>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb,
                            kc, ep);
-    } else if (pick == 256) {
-      dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
-      hipLaunchKernelGGL((gemm_v2_kernel<256, 256, A_KM, B_KN, EPI>), grid, dim3(1024), 0, s, A, B, M, N, K, lda, ldb,
-                         kc, ep);
-    } else if (pick == 200) {  // 256 x 128
-      dim3 grid(((M + 255) / 256) * ((N + 127) / 128), batch, nsplit);
-      hipLaunchKernelGGL((gemm_v2_kernel<256, 128, A_KM, B_KN, EPI>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb,
-                         kc, ep);
     } else {
-      dim3 grid(tiles, batch, nsplit);
-      hipLaunchKernelGGL((gemm_v2_kernel<128, 128, A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb,
-                         kc, ep);
+      // MINIPS_GEMM_ZMAP: split-K slice-major XCD runs (EpiArgs::zmap)
+      static const int zmap = [] {
+        const char* e = std::getenv("MINIPS_GEMM_ZMAP");
+        return e ? std::atoi(e) : 1;
+      }();
+      EpiArgs e2 = ep;
+      e2.zmap = zmap;
+      if (pick == 256) {
+        dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
+        hipLaunchKernelGGL((gemm_v2_kernel<256, 256, A_KM, B_KN, EPI>), grid, dim3(1024), 0, s, A, B, M, N, K, lda,
+                           ldb, kc, e2);
+      } else if (pick == 200) {  // 256 x 128
+        dim3 grid(((M + 255) / 256) * ((N + 127) / 128), batch, nsplit);
+        hipLaunchKernelGGL((gemm_v2_kernel<256, 128, A_KM, B_KN, EPI>), grid, dim3(512), 0, s, A, B, M, N, K, lda,
+                           ldb, kc, e2);
+      } else {
+        dim3 grid(tiles, batch, nsplit);
+        hipLaunchKernelGGL((gemm_v2_kernel<128, 128, A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda,
+                           ldb, kc, e2);
+      }
     }
     return nsplit;
   }

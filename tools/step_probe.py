@@ -171,18 +171,33 @@ def cmd_curve(n):
     _, _, _, feeder = _setup()
     spin = float(os.environ.get("SPIN_MS", "0"))
     if spin > 0:
+        # SPIN_KIND=gemm: compute-bound (4096^3 bf16 GEMMs); mem: HBM-bound (1 GiB device copies)
+        mem = os.environ.get("SPIN_KIND", "gemm") == "mem"
         a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        if mem:
+            src = torch.empty(1 << 28, device="cuda", dtype=torch.float32)
+            dst = torch.empty_like(src)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         while (time.perf_counter() - t0) * 1e3 < spin:
             for _ in range(8):
-                a @ a
+                if mem:
+                    dst.copy_(src)
+                else:
+                    a @ a
             torch.cuda.synchronize()
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    # PRELOAD_MS: queue that much GPU work (GEMMs, no sync) right before step 0, so the host starts
+    # the timed steps already ahead of the GPU (host-proximity test of the early-step curve)
+    preload = float(os.environ.get("PRELOAD_MS", "0"))
+    pa = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16) if preload > 0 else None
     for rep in range(int(os.environ.get("REPEAT", "1"))):
         if rep:
             time.sleep(float(os.environ.get("PAUSE_S", "0.5")))  # idle, queue drained
         host = [0.0] * n
+        if pa is not None:
+            for _ in range(max(1, int(preload / 0.12))):  # ~0.12 ms per 4096^3 GEMM
+                pa @ pa
         evs[0].record()
         for i in range(n):
             t = time.perf_counter()
@@ -191,8 +206,8 @@ def cmd_curve(n):
             host[i] = (time.perf_counter() - t) * 1e3
         torch.cuda.synchronize()
         ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
-        edges = [0, 1, 2, 5, 10, 20, 30, 50, 80, 120, 200, 300, 500]
-        print(f"spin {spin:.0f} ms before step 0; reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB, "
+        edges = [0, 1, 2, 5, 10, 20, 30, 50, 80, 120, 200, 300, 500, 1000, 1500]
+        print(f"spin {spin:.0f} ms ({os.environ.get('SPIN_KIND', 'gemm')}), preload {preload:.0f} ms before step 0; reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB, "
               f"alloc retries {torch.cuda.memory_stats().get('num_alloc_retries', 0)}")
         for lo, hi in zip(edges, edges[1:]):
             if lo < n:
