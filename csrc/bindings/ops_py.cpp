@@ -923,6 +923,14 @@ void criteo_synth(int64_t seed, int64_t step, const c10::optional<at::Tensor>& s
                          stream_of(keys));
 }
 
+// out: int64 [2] on the GPU; launched on `stream` (a torch stream handle; 0 = out's current stream)
+void clock_probe(at::Tensor& out, int64_t spin_ticks, int64_t stream) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.numel() >= 2 && out.is_contiguous(),
+              "clock_probe: out must be a contiguous int64 CUDA tensor of >= 2 elements");
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : stream_of(out);
+  minips_k::clock_probe(ptr<int64_t>(out), (int)spin_ticks, s);
+}
+
 void uniform_synth(int64_t seed, int64_t step, int64_t rows, at::Tensor& dense, at::Tensor& keys, at::Tensor& labels) {
   for (const at::Tensor* t : {(const at::Tensor*)&dense, (const at::Tensor*)&keys, (const at::Tensor*)&labels})
     check_gpu(*t, "uniform_synth arg");
@@ -1697,6 +1705,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_split3", &kmeans_split3);
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
+  m.def("clock_probe", &clock_probe, py::arg("out"), py::arg("spin_ticks") = 2000, py::arg("stream") = 0);
   m.def("bitmap_plan", &bitmap_plan, py::arg("keys"), py::arg("bounds"), py::arg("num_rows"), py::arg("route_mult"),
         py::arg("route_n"), py::arg("oor") = py::none());
   m.def("uniform_synth", &uniform_synth);

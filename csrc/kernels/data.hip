@@ -127,4 +127,26 @@ void uniform_synth(uint64_t seed, uint64_t step, int64_t B, int F, uint64_t rows
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ---- clock probe (diagnostics): one lane counts shader-clock cycles (s_memtime) against the
+// constant 100 MHz real-time counter (s_memrealtime) over ~spin ticks, so the effective SCLK at that
+// moment is cycles / ticks * 100 MHz. A one-wave launch on a side stream samples the clock while a
+// workload runs (tools/step_probe.py curve, CLOCK_PROBE=1). Bounded spin.
+__global__ __launch_bounds__(64) void clock_probe_kernel(int64_t* __restrict__ out, int spin) {
+  if (threadIdx.x != 0) return;
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  uint64_t r1 = r0;
+  for (int guard = 0; r1 - r0 < (uint64_t)spin && guard < (1 << 22); ++guard) r1 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t c1 = __builtin_amdgcn_s_memtime();
+  r1 = __builtin_amdgcn_s_memrealtime();
+  out[0] = (int64_t)(c1 - c0);
+  out[1] = (int64_t)(r1 - r0);
+}
+
+void clock_probe(int64_t* out, int spin_ticks, hipStream_t s) {
+  if (spin_ticks < 1 || spin_ticks > 1000000) throw std::runtime_error("clock_probe: 1 <= spin_ticks <= 1e6");
+  hipLaunchKernelGGL(clock_probe_kernel, 1, 64, 0, s, out, spin_ticks);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace minips_k

@@ -304,6 +304,8 @@ void dlrm_interact_bwd(const bf16_t* V, int64_t B, int NV, int D, int dense_idx,
 // DLRM batch: keys uniform in [0, rows), dense N(0,1), labels = dense[:, 0] > 0 (data.hip).
 void uniform_synth(uint64_t seed, uint64_t step, int64_t B, int F, uint64_t rows, int n_dense, float* dense,
                    int64_t* keys, float* labels, hipStream_t s);
+// out[0] = shader-clock cycles, out[1] = 100 MHz real-time ticks over ~spin_ticks (one wave; diagnostics)
+void clock_probe(int64_t* out, int spin_ticks, hipStream_t s);
 void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t B, int F, const int64_t* cards,
                   const int64_t* offsets, int n_dense, const float* w, float* dense, int64_t* keys, float* labels,
                   hipStream_t s);

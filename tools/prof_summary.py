@@ -141,10 +141,36 @@ def markers(a):
         print(f"{c / steps:10.2f} {t / steps / 1e6:9.4f} {t / c / 1e3:9.1f} {len(threads[n]):7d}  {n[:80]}")
 
 
+def early(a):
+    """Per kernel name: mean duration in the step windows [lo, hi) of a kernel trace (steps counted
+    by the anchor kernel), to see which kernels carry the slow early steps; plus the step length."""
+    rows = list(csv.DictReader(open(a.trace)))
+    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), _short(r["Kernel_Name"])) for r in rows)
+    anchors = [s for s, e, n in ks if a.anchor in n]
+    wins = [tuple(int(x) for x in w.split("-")) for w in a.windows.split(",")]
+    wins = [(lo, min(hi, len(anchors) - 1)) for lo, hi in wins if lo < len(anchors) - 1]
+    agg = collections.defaultdict(dict)
+    steplen = {}
+    for lo, hi in wins:
+        t0, t1 = anchors[lo], anchors[hi]
+        steplen[(lo, hi)] = (t1 - t0) / (hi - lo) / 1e3
+        d = collections.defaultdict(list)
+        for s, e, n in ks:
+            if t0 <= s < t1:
+                d[n].append(e - s)
+        for n, v in d.items():
+            agg[n][(lo, hi)] = sum(v) / (hi - lo) / 1e3  # us per step
+    hdr = " ".join(f"{f'{lo}-{hi}':>9}" for lo, hi in wins)
+    print(f"us per step in step windows (anchor {a.anchor})\n{'':60s} {hdr}")
+    print(f"{'step length':60s} " + " ".join(f"{steplen[w]:9.1f}" for w in wins))
+    last = wins[-1]
+    for n in sorted(agg, key=lambda n: -agg[n].get(last, 0.0))[: a.top]:
+        print(f"{n[:60]:60s} " + " ".join(f"{agg[n].get(w, 0.0):9.1f}" for w in wins))
+
 
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    if argv and argv[0] not in ("stats", "pmc", "trace", "markers", "-h", "--help"):
+    if argv and argv[0] not in ("stats", "pmc", "trace", "markers", "early", "-h", "--help"):
         argv.insert(0, "stats")
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -159,6 +185,11 @@ def main(argv=None):
     p.add_argument("--skip", type=int, default=3)
     p.add_argument("--top", type=int, default=30)
     p.add_argument("--timeline", action="store_true", help="also list one steady step kernel by kernel")
+    p = sub.add_parser("early")
+    p.add_argument("trace")
+    p.add_argument("--anchor", default="adam_kernel")
+    p.add_argument("--windows", default="2-10,10-30,30-60,150-290")
+    p.add_argument("--top", type=int, default=25)
     p = sub.add_parser("markers")
     p.add_argument("path")
     p.add_argument("--steps", type=int, default=1)
@@ -169,6 +200,8 @@ def main(argv=None):
         stats(a.path, a.steps, a.top)
     elif a.cmd == "pmc":
         pmc(a.paths)
+    elif a.cmd == "early":
+        early(a)
     else:
         trace(a)
 

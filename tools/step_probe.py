@@ -190,6 +190,13 @@ def cmd_curve(n):
     # PRELOAD_MS: queue that much GPU work (GEMMs, no sync) right before step 0, so the host starts
     # the timed steps already ahead of the GPU (host-proximity test of the early-step curve)
     preload = float(os.environ.get("PRELOAD_MS", "0"))
+    # CLOCK_PROBE=1: the effective shader clock after every step (ops_py clock_probe: s_memtime
+    # cycles over s_memrealtime ticks), printed per step window beside the step times
+    probes = None
+    if os.environ.get("CLOCK_PROBE", "0") == "1":
+        from minips_amd._native import kernels
+
+        probes = torch.zeros(n, 2, dtype=torch.int64, device="cuda")
     pa = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16) if preload > 0 else None
     for rep in range(int(os.environ.get("REPEAT", "1"))):
         if rep:
@@ -202,18 +209,22 @@ def cmd_curve(n):
         for i in range(n):
             t = time.perf_counter()
             feeder.step()
+            if probes is not None:  # one wave, ~10 us, in order after the step's main-stream work
+                kernels().clock_probe(probes[i], 1000, 0)
             evs[i + 1].record()
             host[i] = (time.perf_counter() - t) * 1e3
         torch.cuda.synchronize()
         ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
+        mhz = (probes[:, 0].double() / probes[:, 1].double() * 100.0).tolist() if probes is not None else None
         edges = [0, 1, 2, 5, 10, 20, 30, 50, 80, 120, 200, 300, 500, 1000, 1500]
         print(f"spin {spin:.0f} ms ({os.environ.get('SPIN_KIND', 'gemm')}), preload {preload:.0f} ms before step 0; reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB, "
               f"alloc retries {torch.cuda.memory_stats().get('num_alloc_retries', 0)}")
         for lo, hi in zip(edges, edges[1:]):
             if lo < n:
                 seg, hseg = ms[lo:min(hi, n)], host[lo:min(hi, n)]
+                clk = f", SCLK {sum(mhz[lo:min(hi, n)]) / len(seg):.0f} MHz" if mhz is not None else ""
                 print(f"steps {lo:4d}-{min(hi, n) - 1:4d}: GPU {sum(seg) / len(seg):.4f} ms/step, host issue "
-                      f"{sum(hseg) / len(hseg):.4f} ms/step", flush=True)
+                      f"{sum(hseg) / len(hseg):.4f} ms/step{clk}", flush=True)
 
 
 def main(argv=None):
