@@ -923,6 +923,33 @@ void criteo_synth(int64_t seed, int64_t step, const c10::optional<at::Tensor>& s
                          stream_of(keys));
 }
 
+// dst[i].copy_(src[i]) for every pair, in one launch on dst[0]'s current stream (same byte sizes,
+// contiguous, one device; at most 16 pairs per launch)
+void multi_copy(const std::vector<at::Tensor>& dst, const std::vector<at::Tensor>& src) {
+  TORCH_CHECK(dst.size() == src.size() && !dst.empty(), "multi_copy: matching non-empty lists");
+  for (size_t base = 0; base < dst.size(); base += minips_k::kMultiCopyMax) {
+    minips_k::MultiCopyArgs a{};
+    a.n = (int)std::min<size_t>(minips_k::kMultiCopyMax, dst.size() - base);
+    a.start[0] = 0;
+    for (int t = 0; t < a.n; ++t) {
+      const at::Tensor& d = dst[base + t];
+      const at::Tensor& s = src[base + t];
+      TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.get_device() == s.get_device(), "multi_copy: one GPU");
+      TORCH_CHECK(d.is_contiguous() && s.is_contiguous(), "multi_copy: contiguous tensors");
+      const int64_t nb = d.numel() * d.element_size();
+      TORCH_CHECK(nb == s.numel() * s.element_size(), "multi_copy: byte sizes differ");
+      a.dst[t] = d.data_ptr();
+      a.src[t] = s.data_ptr();
+      const bool al = (reinterpret_cast<uintptr_t>(a.dst[t]) & 15) == 0 &&
+                      (reinterpret_cast<uintptr_t>(a.src[t]) & 15) == 0;
+      a.n16[t] = al ? nb / 16 : 0;
+      a.tail[t] = nb - a.n16[t] * 16;
+      a.start[t + 1] = a.start[t] + a.n16[t] + a.tail[t];
+    }
+    minips_k::multi_copy(a, stream_of(dst[base]));
+  }
+}
+
 // out: int64 [2] on the GPU; launched on `stream` (a torch stream handle; 0 = out's current stream)
 void clock_probe(at::Tensor& out, int64_t spin_ticks, int64_t stream) {
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.numel() >= 2 && out.is_contiguous(),
@@ -1705,6 +1732,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_split3", &kmeans_split3);
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
+  m.def("multi_copy", &multi_copy);
   m.def("clock_probe", &clock_probe, py::arg("out"), py::arg("spin_ticks") = 2000, py::arg("stream") = 0);
   m.def("bitmap_plan", &bitmap_plan, py::arg("keys"), py::arg("bounds"), py::arg("num_rows"), py::arg("route_mult"),
         py::arg("route_n"), py::arg("oor") = py::none());

@@ -149,4 +149,30 @@ void clock_probe(int64_t* out, int spin_ticks, hipStream_t s) {
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ---- several device-to-device copies in ONE launch (a HIP-graph step's static input slots are
+// refilled by 11 copies: as separate copy nodes each cost a dispatch gap, ~110 us in a row).
+// 16-byte vectors over the 16-byte body of each pair, bytes over its tail.
+__global__ __launch_bounds__(256) void multi_copy_kernel(MultiCopyArgs a) {
+  const int64_t total = a.start[a.n];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int t = 0;
+    while (t + 1 < a.n && a.start[t + 1] <= i) ++t;
+    const int64_t j = i - a.start[t];
+    if (j < a.n16[t]) {
+      reinterpret_cast<uint4*>(a.dst[t])[j] = reinterpret_cast<const uint4*>(a.src[t])[j];
+    } else {
+      const int64_t b = a.n16[t] * 16 + (j - a.n16[t]);
+      static_cast<char*>(a.dst[t])[b] = static_cast<const char*>(a.src[t])[b];
+    }
+  }
+}
+
+void multi_copy(const MultiCopyArgs& a, hipStream_t s) {
+  if (a.n < 1 || a.n > kMultiCopyMax) throw std::runtime_error("multi_copy: 1..16 pairs");
+  const int64_t total = a.start[a.n];
+  if (total <= 0) return;
+  hipLaunchKernelGGL(multi_copy_kernel, grid_for(total, 256, 2048), 256, 0, s, a);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace minips_k

@@ -306,6 +306,18 @@ void uniform_synth(uint64_t seed, uint64_t step, int64_t B, int F, uint64_t rows
                    int64_t* keys, float* labels, hipStream_t s);
 // out[0] = shader-clock cycles, out[1] = 100 MHz real-time ticks over ~spin_ticks (one wave; diagnostics)
 void clock_probe(int64_t* out, int spin_ticks, hipStream_t s);
+// up to 16 device-to-device copies in one launch: pair t copies n16[t] 16-byte vectors then tail[t]
+// bytes (src / dst 16-byte aligned when n16 > 0); start[] = exclusive prefix of n16 + tail
+constexpr int kMultiCopyMax = 16;
+struct MultiCopyArgs {
+  const void* src[kMultiCopyMax];
+  void* dst[kMultiCopyMax];
+  int64_t n16[kMultiCopyMax];
+  int64_t tail[kMultiCopyMax];
+  int64_t start[kMultiCopyMax + 1];
+  int n;
+};
+void multi_copy(const MultiCopyArgs& a, hipStream_t s);
 void criteo_synth(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t B, int F, const int64_t* cards,
                   const int64_t* offsets, int n_dense, const float* w, float* dense, int64_t* keys, float* labels,
                   hipStream_t s);

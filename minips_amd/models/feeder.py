@@ -15,6 +15,8 @@ import os
 
 import torch
 
+from ..utils import streams
+
 
 def default_depth(world: int) -> int:
     # one rank: depth 1 (measured neutral, 1/2/3 within 0.522-0.530 ms/step); several ranks: 2,
@@ -42,6 +44,13 @@ class LookaheadFeeder:
         self.fence = bool(fence and self.cuda)
         if self.fence:
             model._fenced = True
+        # batch-ready and fence events: reused from rings (a wait binds to the record before it;
+        # each event's wait is issued within depth + 1 steps of its record)
+        if self.cuda:
+            from ..utils.streams import EventRing
+
+            self._evring = EventRing(2 * self.depth + 4)
+            self._fence_ring = EventRing(4)
         self.queue = collections.deque(self._produce() for _ in range(self.depth))
         for (_, k, _), _ev in list(self.queue)[1:]:
             model.prefetch(k, keys_on_plan_stream=self.cuda)
@@ -49,9 +58,9 @@ class LookaheadFeeder:
     def _produce(self):
         if not self.cuda:
             return self.data.next(), None
-        with torch.cuda.stream(self.plan_stream):
+        with streams.use(self.plan_stream):
             b = self.data.next()
-            ev = torch.cuda.Event()
+            ev = self._evring.next()
             ev.record(self.plan_stream)
         if not self.fence:
             for t in b:
@@ -73,7 +82,7 @@ class LookaheadFeeder:
 
         loss = self.model.train_step(dense, keys, labels, next_keys=next_keys, next_on_plan_stream=self.cuda)
         if self.fence:  # the planning stream's later work (and buffer reuse) follows this step
-            ev = torch.cuda.Event()
+            ev = self._fence_ring.next()
             ev.record(self.main)
             self.plan_stream.wait_event(ev)
         return loss
@@ -156,6 +165,9 @@ class GraphedFeeder:
                 raise ValueError("GraphedFeeder needs synchronous clocks")
         self.f, self.tables = f, list(tables)
         torch.cuda.synchronize(f.comm.device)
+        # an eager step may leave its side-stream tail for the next step to wait on (WideDeep's
+        # _side_pending); it is complete now, and a capture must not wait on events from outside it
+        f.model.__dict__.pop("_side_pending", None)
         batch, _ev = f.queue[0]
         pend = f.model._pending_plans
         if len(pend) != 1 or pend[0][0] is not batch[1]:
@@ -184,8 +196,15 @@ class GraphedFeeder:
             produced = _batch_plan_tensors(nb, npp)
             if [(t.shape, t.dtype) for t in produced] != [(t.shape, t.dtype) for t in static]:
                 raise RuntimeError("GraphedFeeder: the step's batch/plan layout is not static")
-            for dst, src in zip(static, produced):
-                dst.copy_(src)
+            # one launch for every slot (11 separate copy nodes cost ~110 us of dispatch gaps)
+            pairs = [(d, s) for d, s in zip(static, produced) if d.numel()]
+            if pairs and all(d.is_contiguous() and s.is_contiguous() for d, s in pairs):
+                from .._native import kernels
+
+                kernels().multi_copy([d for d, _ in pairs], [s for _, s in pairs])
+            else:
+                for dst, src in pairs:
+                    dst.copy_(src)
         # the capture ran nothing: restore the host view (static batch + plan are the next input)
         f.queue.clear()
         f.queue.append((batch, None))

@@ -8,7 +8,6 @@ Linear        bias folded into the weight: W_ext [n_out, k_pad] with the bias in
 """
 from __future__ import annotations
 
-import contextlib
 import os
 
 import math
@@ -16,6 +15,7 @@ import math
 import torch
 
 from .. import ops
+from ..utils import streams
 
 
 def align(n: int, a: int = 8) -> int:
@@ -123,12 +123,49 @@ def compute_priority() -> int:
 _FAST_EVENTS = os.environ.get("MINIPS_FAST_EVENTS", "1") != "0"
 
 
+class _Fork:
+    """SideStream.fork()'s context: the side stream waits for the current stream, then the block
+    runs on the side stream (GEMM splits in overlap mode)."""
+
+    __slots__ = ("side", "prev", "mode")
+
+    def __init__(self, side):
+        self.side = side
+
+    def __enter__(self):
+        sd = self.side
+        st = sd.stream
+        if st is None:
+            return None
+        idx = st.device_index
+        ev = sd._event()
+        if sd._fast:
+            ev.record(streams.current_raw(idx))
+            ev.wait(sd._raw)
+        else:
+            ev.record(streams.current(idx))
+            st.wait_event(ev)
+        self.mode = ops.overlap_mode(True)  # forked work: GEMM splits chosen for throughput, not latency
+        self.prev = streams._get(idx)
+        streams._set(stream_id=st.stream_id, device_index=idx, device_type=st.device_type)
+        return st
+
+    def __exit__(self, *exc):
+        if self.side.stream is None:
+            return False
+        p = self.prev
+        streams._set(stream_id=p[0], device_index=p[1], device_type=p[2])
+        ops.overlap_mode(self.mode)
+        return False
+
+
 class SideStream:
     """Fork-join helper: independent work (weight gradients) issued on a second HIP stream.
 
     ``with side.fork():`` makes the side stream wait for everything issued so far on the current
     stream, then runs the block on the side stream; ``join()`` makes the current stream wait for
-    all forked work. Disabled (or on CPU) it is a no-op and the block runs inline."""
+    all forked work. Disabled (or on CPU) it is a no-op and the block runs inline. Stream changes
+    go through utils/streams (no per-call device resolution: this is the step's hottest host path)."""
 
     def __init__(self, device, enabled: bool = True):
         self.stream = torch.cuda.Stream(device=device, priority=compute_priority()) \
@@ -143,6 +180,7 @@ class SideStream:
             self._evs = [kernels().FastEvent() for _ in range(8)]
         else:
             self._evs = [torch.cuda.Event() for _ in range(8)] if self.stream is not None else []
+        self._raw = self.stream.cuda_stream if self.stream is not None else 0
         self._ev_i = 0
 
     def _event(self):
@@ -150,41 +188,29 @@ class SideStream:
         self._ev_i += 1
         return ev
 
-    @contextlib.contextmanager
     def fork(self):
-        if self.stream is None:
-            yield
-            return
-        cur = torch.cuda.current_stream(self.stream.device)
-        ev = self._event()
-        if self._fast:
-            ev.record(cur.cuda_stream)
-            ev.wait(self.stream.cuda_stream)
-        else:
-            ev.record(cur)
-            self.stream.wait_event(ev)
-        prev = ops.overlap_mode(True)  # forked work: GEMM splits chosen for throughput, not latency
-        try:
-            with torch.cuda.stream(self.stream):
-                yield
-        finally:
-            ops.overlap_mode(prev)
+        return _Fork(self)
 
     def join(self):
         if self.stream is not None:
             ev = self._event()
+            idx = self.stream.device_index
             if self._fast:
-                ev.record(self.stream.cuda_stream)
-                ev.wait(torch.cuda.current_stream(self.stream.device).cuda_stream)
+                ev.record(self._raw)
+                ev.wait(streams.current_raw(idx))
             else:
                 ev.record(self.stream)
-                torch.cuda.current_stream(self.stream.device).wait_event(ev)
+                streams.current(idx).wait_event(ev)
 
     def mark(self):
-        """Event after the work forked so far (None when disabled)."""
+        """Event after the work forked so far (None when disabled). A torch event (callers hand it
+        to torch streams) from a ring of 16: every caller issues its wait within a few marks."""
         if self.stream is None:
             return None
-        ev = torch.cuda.Event()  # (a torch event: callers hand it to torch streams)
+        ring = self.__dict__.get("_marks")
+        if ring is None:
+            ring = self._marks = streams.EventRing(16)
+        ev = ring.next()
         ev.record(self.stream)
         return ev
 
@@ -192,7 +218,8 @@ class SideStream:
         """The current stream waits for ``ev`` (before it overwrites a buffer forked work reads)."""
         if ev is None:
             return
+        idx = self.stream.device_index
         if self._fast and not isinstance(ev, torch.cuda.Event):
-            ev.wait(torch.cuda.current_stream(self.stream.device).cuda_stream)
+            ev.wait(streams.current_raw(idx))
         else:
-            torch.cuda.current_stream(self.stream.device).wait_event(ev)
+            streams.current(idx).wait_event(ev)

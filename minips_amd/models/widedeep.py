@@ -24,6 +24,7 @@ import torch
 
 from .. import ops
 from ..ps.comm import Comm
+from ..utils import streams
 from ..utils.metrics import traced
 from .layers import SideStream
 from .feeder import LookaheadPlans
@@ -182,11 +183,22 @@ class WideDeep(LookaheadPlans):
         return full.to(dev)
 
     def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
-        off, shape = self.layout[name]
-        n = 1
-        for s in shape:
-            n *= s
-        return buf[off: off + n].view(shape)
+        # ~15 views of the persistent parameter / gradient buffers per step: cached by address
+        # (a live cached view keeps its storage, so no other buffer can take that address)
+        key = (buf.data_ptr(), buf.dtype, name)
+        views = self.__dict__.setdefault("_views", {})
+        v = views.get(key)
+        if v is None:
+            off, shape = self.layout[name]
+            n = 1
+            for s in shape:
+                n *= s
+            v = buf[off: off + n].view(shape)
+            if buf.is_cuda:
+                if len(views) > 256:
+                    views.clear()
+                views[key] = v
+        return v
 
     def _buffers(self, B):
         if B not in self._bufs:
@@ -226,7 +238,7 @@ class WideDeep(LookaheadPlans):
         b = self._buffers(B)
         pend_side = self.__dict__.pop("_side_pending", None)
         if pend_side is not None:  # the last train step's Adam (side stream) before W is read
-            torch.cuda.current_stream(self.comm.device).wait_event(pend_side[1])
+            streams.current(self.comm.device).wait_event(pend_side[1])
         P = self.dense.get()
         F, D = self.cfg.F, self.cfg.emb_dim
         ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0])
@@ -265,7 +277,7 @@ class WideDeep(LookaheadPlans):
         issue_next("start")
         pend_side = self.__dict__.pop("_side_pending", None)
         if pend_side is not None:  # the previous step's weight gradients read X: done before it is rewritten
-            torch.cuda.current_stream(self.comm.device).wait_event(pend_side[0])
+            streams.current(self.comm.device).wait_event(pend_side[0])
         src = self.emb.get_source(keys, plan=plan)  # one rank: the rows are read in place
         if src is not None:
             plan, table, index, base = src
@@ -277,7 +289,7 @@ class WideDeep(LookaheadPlans):
             rows, plan = self.emb.get(keys, plan=plan)
             ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
         if pend_side is not None:  # ... and its dense Adam ran (side stream) before the forward reads W
-            torch.cuda.current_stream(self.comm.device).wait_event(pend_side[1])
+            streams.current(self.comm.device).wait_event(pend_side[1])
         G = self.dense.grad
         P = self.dense.get()
         scale = 1.0 / (B * self.comm.world)
@@ -350,7 +362,7 @@ class WideDeep(LookaheadPlans):
         pipe = getattr(self.dense, "pipe", None)  # (collective tables only)
         dense_early = _DENSE_CLOCK_ON_SIDE and pipe is not None and pipe.async_ and side.stream is not None
         if dense_early:
-            with torch.cuda.stream(side.stream):
+            with streams.use(side.stream):
                 self.dense.add()
                 self.dense.clock()
         issue_next("dgrad")
@@ -365,7 +377,7 @@ class WideDeep(LookaheadPlans):
             # for the weight gradients before its assembly rewrites X and for the Adam before its
             # forward reads W, so the Adam overlaps the next step's input assembly
             ev_x = side.mark()
-            with torch.cuda.stream(side.stream):
+            with streams.use(side.stream):
                 self.dense.add()
                 self.dense.clock()
             self._side_pending = (ev_x, side.mark())
@@ -390,6 +402,6 @@ class WideDeep(LookaheadPlans):
     def drain(self):
         pend_side = self.__dict__.pop("_side_pending", None)
         if pend_side is not None:
-            torch.cuda.current_stream(self.comm.device).wait_event(pend_side[1])
+            streams.current(self.comm.device).wait_event(pend_side[1])
         self.emb.drain()
         self.dense.drain()

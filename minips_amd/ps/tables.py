@@ -32,6 +32,7 @@ import torch
 
 from .. import ops
 from .comm import Comm
+from ..utils import streams
 from ..utils.metrics import traced
 
 
@@ -85,9 +86,9 @@ class _Pipeline:
         if not self.async_:
             fn()
         else:
-            cur = torch.cuda.current_stream(self.stream.device)
+            cur = streams.current(self.stream.device)
             self.stream.wait_stream(cur)  # inputs produced on the compute stream
-            with torch.cuda.stream(self.stream):
+            with streams.use(self.stream):
                 fn()
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
@@ -98,7 +99,7 @@ class _Pipeline:
         """Make the compute stream wait until the Clock number ``c`` has been applied."""
         if not self.async_ or c < 0:
             return
-        cur = torch.cuda.current_stream(self.stream.device)
+        cur = streams.current(self.stream.device)
         done = [k for k in self.events if k <= c]
         if done:
             cur.wait_event(self.events[max(done)])  # the side stream is in-order
@@ -126,7 +127,7 @@ class _Pipeline:
 
     def drain(self):
         if self.async_:
-            cur = torch.cuda.current_stream(self.stream.device)
+            cur = streams.current(self.stream.device)
             cur.wait_stream(self.stream)
             self.events.clear()
 
@@ -356,12 +357,12 @@ class DenseTable:
         grad, step = self.grad, self.step + 1
         if self.pipe.async_:
             st = self.pipe.stream
-            st.wait_stream(torch.cuda.current_stream(st.device))
+            st.wait_stream(streams.current(st.device))
             for ev in events:
                 if ev is not None:
                     st.wait_event(ev)
             self.pipe.keep_alive(grad)
-            with torch.cuda.stream(st):
+            with streams.use(st):
                 self._bucket_work(k, grad, step)
         else:
             self._bucket_work(k, grad, step)
@@ -884,12 +885,15 @@ class SparseTable:
         if self.comm.device.type != "cuda":
             return self._start_plan(keys, csr, exchange=False)
         ps = self.comm.plan_stream()
-        cur = torch.cuda.current_stream(self.comm.device)
+        cur = streams.current(self.comm.device)
         if not keys_on_plan_stream:
             ps.wait_stream(cur)  # the keys are produced on the compute stream
-        with torch.cuda.stream(ps):
+        with streams.use(ps):
             pp = self._start_plan(keys, csr, exchange=False)
-            pp.event = torch.cuda.Event()
+            ring = self.__dict__.get("_plan_evs")
+            if ring is None:  # (plans are consumed within a few steps of their issue)
+                ring = self._plan_evs = streams.EventRing(16)
+            pp.event = ring.next()
             pp.event.record(ps)
         if fenced and self.comm.world == 1 and not self.pipe.async_:
             return pp
@@ -904,7 +908,7 @@ class SparseTable:
         comm = self.comm
         n = pp.flat.numel()
         if pp.event is not None:
-            torch.cuda.current_stream(dev).wait_event(pp.event)
+            streams.current(dev).wait_event(pp.event)
         if not pp.exchanged:  # nobody issued the count exchange yet: do it here
             self._exchange_counts(pp)
         if self.comm.world == 1:
@@ -971,13 +975,13 @@ class SparseTable:
             self._exchange_counts(pending)
             return self._finish_plan(pending) if finish else pending
         ps = self.comm.plan_stream()
-        cur = torch.cuda.current_stream(self.comm.device)
+        cur = streams.current(self.comm.device)
         if not pending.exchanged:
-            with torch.cuda.stream(ps):
+            with streams.use(ps):
                 self._exchange_counts(pending)
         if not finish:
             return pending
-        with torch.cuda.stream(ps):
+        with streams.use(ps):
             plan = self._finish_plan(pending)
             ev = torch.cuda.Event()
             ev.record(ps)
@@ -997,7 +1001,7 @@ class SparseTable:
             plan = self._finish_plan(plan)
         ready = plan.extra.pop("ready", None)
         if ready is not None:  # keys exchanged on the planning stream (advance_plan)
-            torch.cuda.current_stream(self.comm.device).wait_event(ready)
+            streams.current(self.comm.device).wait_event(ready)
         self.pipe.wait_for_read()  # BSP: the previous Clock's apply; SSP: clock c-s-1
         dev = self.comm.device
         served = torch.empty(len(plan.recv_keys), self.width, dtype=self.pull_dtype, device=dev)
@@ -1025,7 +1029,7 @@ class SparseTable:
             plan = self._finish_plan(plan)
         ready = plan.extra.pop("ready", None)
         if ready is not None:
-            torch.cuda.current_stream(self.comm.device).wait_event(ready)
+            streams.current(self.comm.device).wait_event(ready)
         self.pipe.wait_for_read()
         table, index, base = self._serve_index(plan)
         return plan, table, index, base

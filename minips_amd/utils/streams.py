@@ -1,0 +1,84 @@
+"""Low-overhead HIP stream helpers for the per-step issue path.
+
+``torch.cuda.current_stream(dev)`` and ``with torch.cuda.stream(s):`` resolve the device through
+several Python layers (``_get_device_index`` -> ``_get_device_attr`` -> ``is_available`` ...) on
+every call: ~19 such resolutions per W&D step cost ~25-40 us of its ~0.3 ms host issue
+(tools/step_probe.py cprofile). These helpers go straight to the C entry points torch itself ends
+in (``_cuda_getCurrentStream`` / ``_cuda_setStream`` / ``_cuda_getCurrentRawStream``), with the
+same semantics for a stream of the process's own device (one device per rank here).
+"""
+from __future__ import annotations
+
+import torch
+
+_get = torch._C._cuda_getCurrentStream if hasattr(torch._C, "_cuda_getCurrentStream") else None
+_set = torch._C._cuda_setStream if hasattr(torch._C, "_cuda_setStream") else None
+_raw = torch._C._cuda_getCurrentRawStream if hasattr(torch._C, "_cuda_getCurrentRawStream") else None
+
+
+def _index(dev) -> int:
+    if isinstance(dev, int):
+        return dev
+    if isinstance(dev, torch.device) and dev.index is not None:
+        return dev.index
+    if isinstance(dev, torch.cuda.Stream):
+        return dev.device_index
+    return torch.cuda.current_device()
+
+
+def current(dev=None) -> torch.cuda.Stream:
+    """torch.cuda.current_stream(dev) without the device resolution layers."""
+    d = _get(_index(dev))
+    return torch.cuda.Stream(stream_id=d[0], device_index=d[1], device_type=d[2])
+
+
+def current_raw(dev=None) -> int:
+    """The current stream's hipStream_t handle (torch.cuda.current_stream(dev).cuda_stream)."""
+    return _raw(_index(dev))
+
+
+class use:
+    """``with use(stream):`` == ``with torch.cuda.stream(stream):`` for a stream of the current
+    device (restores the previous current stream of that device on exit); ``None``: no-op."""
+
+    __slots__ = ("s", "prev")
+
+    def __init__(self, s):
+        self.s = s
+        self.prev = None
+
+    def __enter__(self):
+        s = self.s
+        if s is not None:
+            self.prev = _get(s.device_index)
+            _set(stream_id=s.stream_id, device_index=s.device_index, device_type=s.device_type)
+        return s
+
+    def __exit__(self, *exc):
+        p = self.prev
+        if p is not None:
+            _set(stream_id=p[0], device_index=p[1], device_type=p[2])
+            self.prev = None
+        return False
+
+
+class EventRing:
+    """A fixed ring of reusable events (torch.cuda.Event, or ops_py FastEvent when ``fast``):
+    a stream wait binds to the record issued before it, so re-recording an event after its waits
+    were issued is safe -- no event object created and destroyed per use."""
+
+    __slots__ = ("evs", "i")
+
+    def __init__(self, n: int = 8, fast: bool = False):
+        if fast:
+            from .._native import kernels
+
+            self.evs = [kernels().FastEvent() for _ in range(n)]
+        else:
+            self.evs = [torch.cuda.Event() for _ in range(n)]
+        self.i = 0
+
+    def next(self):
+        ev = self.evs[self.i]
+        self.i = (self.i + 1) % len(self.evs)
+        return ev

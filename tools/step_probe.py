@@ -85,7 +85,10 @@ def cmd_cprofile(n):
         feeder.step()
     pr.disable()
     torch.cuda.synchronize()
-    pstats.Stats(pr).sort_stats("tottime").print_stats(int(os.environ.get("TOP", "35")))
+    st = pstats.Stats(pr)
+    st.sort_stats(os.environ.get("SORT", "tottime")).print_stats(int(os.environ.get("TOP", "35")))
+    if os.environ.get("CALLERS"):  # who calls the named functions (e.g. CALLERS=current_stream)
+        st.print_callers(os.environ["CALLERS"])
 
 
 def cmd_events(n):
@@ -217,7 +220,9 @@ def cmd_curve(n):
         ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
         mhz = (probes[:, 0].double() / probes[:, 1].double() * 100.0).tolist() if probes is not None else None
         edges = [0, 1, 2, 5, 10, 20, 30, 50, 80, 120, 200, 300, 500, 1000, 1500]
-        print(f"spin {spin:.0f} ms ({os.environ.get('SPIN_KIND', 'gemm')}), preload {preload:.0f} ms before step 0; reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB, "
+        kind = os.environ.get('SPIN_KIND', 'gemm')
+        print(f"spin {spin:.0f} ms ({kind}), preload {preload:.0f} ms before step 0; "
+              f"reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB, "
               f"alloc retries {torch.cuda.memory_stats().get('num_alloc_retries', 0)}")
         for lo, hi in zip(edges, edges[1:]):
             if lo < n:
