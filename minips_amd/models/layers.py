@@ -203,13 +203,13 @@ class SideStream:
                 streams.current(idx).wait_event(ev)
 
     def mark(self):
-        """Event after the work forked so far (None when disabled). A torch event (callers hand it
-        to torch streams) from a ring of 16: every caller issues its wait within a few marks."""
+        """Event after the work forked so far (None when disabled), from a ring of 16 (every caller
+        issues its wait within a few marks); torch-compatible (streams.FastEvent duck-types it)."""
         if self.stream is None:
             return None
         ring = self.__dict__.get("_marks")
         if ring is None:
-            ring = self._marks = streams.EventRing(16)
+            ring = self._marks = streams.EventRing(16, fast=self._fast)
         ev = ring.next()
         ev.record(self.stream)
         return ev
@@ -219,7 +219,7 @@ class SideStream:
         if ev is None:
             return
         idx = self.stream.device_index
-        if self._fast and not isinstance(ev, torch.cuda.Event):
-            ev.wait(streams.current_raw(idx))
-        else:
+        if isinstance(ev, torch.cuda.Event):
             streams.current(idx).wait_event(ev)
+        else:  # ops_py FastEvent or streams.FastEvent
+            getattr(ev, "ev", ev).wait(streams.current_raw(idx))

@@ -51,6 +51,7 @@ import torch.distributed as dist
 
 from .. import ops
 from .comm import Comm
+from ..utils import streams
 from ..utils.metrics import traced
 from .tables import SparsePlan, SparseTable, _PendingPlan, column_spec, even_bounds, _route_multiplier
 
@@ -483,7 +484,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
     # -- planning: SparseTable's dedupe + owner grouping, no count exchange ----------------------
     def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
         if pp.event is not None:
-            torch.cuda.current_stream(self.comm.device).wait_event(pp.event)
+            streams.current(self.comm.device).wait_event(pp.event)
         n = pp.flat.numel()
         if n > self.cap:
             raise ValueError(f"a batch of {n} keys exceeds the inbox slot ({self.cap} rows): raise max_keys")
@@ -504,12 +505,15 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         if not self.cuda:
             return self._start_plan(keys, csr, exchange=False)
         ps = self.comm.plan_stream()
-        cur = torch.cuda.current_stream(self.comm.device)
+        cur = streams.current(self.comm.device)
         if not keys_on_plan_stream:
             ps.wait_stream(cur)
-        with torch.cuda.stream(ps):
+        with streams.use(ps):
             pp = self._start_plan(keys, csr, exchange=False)
-            pp.event = torch.cuda.Event()
+            ring = self.__dict__.get("_plan_evs")
+            if ring is None:
+                ring = self._plan_evs = streams.EventRing(16, fast=streams.FAST)
+            pp.event = ring.next()
             pp.event.record(ps)
         if not fenced:
             keys.record_stream(ps)

@@ -9,7 +9,12 @@ same semantics for a stream of the process's own device (one device per rank her
 """
 from __future__ import annotations
 
+import os
+
 import torch
+
+# MINIPS_FAST_EVENTS=0: the step's ordering events are plain torch events (A/B)
+FAST = os.environ.get("MINIPS_FAST_EVENTS", "1") != "0"
 
 _get = torch._C._cuda_getCurrentStream if hasattr(torch._C, "_cuda_getCurrentStream") else None
 _set = torch._C._cuda_setStream if hasattr(torch._C, "_cuda_setStream") else None
@@ -62,20 +67,41 @@ class use:
         return False
 
 
+class FastEvent:
+    """A same-device ordering event with torch.cuda.Event's record / wait / query / synchronize
+    (duck-typed: torch's Stream.wait_event(ev) calls ev.wait(stream)), backed by ops_py FastEvent
+    (hipEventDisableTiming | hipEventDisableSystemFence: its record does not write back the L2 for
+    the host, which the default event does on every record -- a queue bubble of several us)."""
+
+    __slots__ = ("ev",)
+
+    def __init__(self):
+        from .._native import kernels
+
+        self.ev = kernels().FastEvent()
+
+    def record(self, stream=None):
+        self.ev.record(stream.cuda_stream if stream is not None else _raw(torch.cuda.current_device()))
+
+    def wait(self, stream=None):
+        self.ev.wait(stream.cuda_stream if stream is not None else _raw(torch.cuda.current_device()))
+
+    def query(self) -> bool:
+        return self.ev.query()
+
+    def synchronize(self):
+        self.ev.synchronize()
+
+
 class EventRing:
-    """A fixed ring of reusable events (torch.cuda.Event, or ops_py FastEvent when ``fast``):
+    """A fixed ring of reusable events (torch.cuda.Event, or FastEvent when ``fast``):
     a stream wait binds to the record issued before it, so re-recording an event after its waits
     were issued is safe -- no event object created and destroyed per use."""
 
     __slots__ = ("evs", "i")
 
     def __init__(self, n: int = 8, fast: bool = False):
-        if fast:
-            from .._native import kernels
-
-            self.evs = [kernels().FastEvent() for _ in range(n)]
-        else:
-            self.evs = [torch.cuda.Event() for _ in range(n)]
+        self.evs = [FastEvent() if fast else torch.cuda.Event() for _ in range(n)]
         self.i = 0
 
     def next(self):

@@ -114,15 +114,30 @@ def build(args, comm):
                              max_batch=B)
         m = WideDeep(cfg, comm)
         data = CriteoSynth(B, cards=cfg.cards, device=dev, seed=1000 + r)
-        state = {"cur": data.next()}
+        if args.feeder == "inline":  # the next batch generated on the compute stream at step start
+            state = {"cur": data.next()}
 
-        def step():
-            nxt = data.next()
-            cur, state["cur"] = state["cur"], nxt
-            return m.train_step(*cur, next_keys=nxt[1])
+            def step():
+                nxt = data.next()
+                cur, state["cur"] = state["cur"], nxt
+                return m.train_step(*cur, next_keys=nxt[1])
 
-        return m, step, B, "samples/s", dict(model=f"Wide&Deep Criteo SSP ({args.transport})", seq_len=None,
-                                             consistency=f"ssp{cfg.staleness}", transport=args.transport)
+            return m, step, B, "samples/s", dict(model=f"Wide&Deep Criteo SSP ({args.transport})", seq_len=None,
+                                                 consistency=f"ssp{cfg.staleness}", transport=args.transport,
+                                                 feeder="inline")
+        # bench.py's driver: the step on its own stream, the next batch generated and planned on
+        # the planning stream a step ahead (LookaheadFeeder), for either transport
+        from minips_amd.models.feeder import LookaheadFeeder
+        from minips_amd.models.layers import compute_priority
+
+        if dev.type == "cuda":
+            main = torch.cuda.Stream(device=dev, priority=compute_priority())
+            main.wait_stream(torch.cuda.default_stream(dev))
+            torch.cuda.set_stream(main)
+        feeder = LookaheadFeeder(m, data, comm)
+        return m, feeder.step, B, "samples/s", dict(model=f"Wide&Deep Criteo SSP ({args.transport})", seq_len=None,
+                                             consistency=f"ssp{cfg.staleness}", transport=args.transport,
+                                             feeder="lookahead")
     raise SystemExit(f"unknown model {args.model}")
 
 
@@ -141,6 +156,9 @@ def main():
                     help="mlp: capture the step in a HIP graph (one rank, BSP; off by default: at batch 8192 the "
                          "step is GPU-bound, 0.364 vs 0.350 ms measured)")
     ap.add_argument("--staleness", type=int, default=0)
+    ap.add_argument("--feeder", default="lookahead", choices=["lookahead", "inline"],
+                    help="widedeep-ssp: next batch generated + planned a step ahead on the planning stream "
+                         "(bench.py's LookaheadFeeder) or generated inline at the step start")
     ap.add_argument("--transport", default="auto", choices=["auto", "collective", "onesided"],
                     help="widedeep-ssp / dlrm: RCCL collectives or the asynchronous PS (ps/onesided.py); auto = "
                          "the model's default (DLRM SSP/ASP: onesided; widedeep-ssp: collective)")

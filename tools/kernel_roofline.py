@@ -18,7 +18,7 @@ import statistics
 PEAK_TF, PEAK_TB = 2500.0, 8.0
 B, F, D, ND = 16384, 26, 32, 13
 K1, H1, H2, H3 = 896, 1024, 512, 256
-K2, K3 = 1032, 520            # bias-folded K of layers 2 / 3 (ext layout)
+K2, K3 = 1024, 512            # layers 2 / 3 K (bias vectors, MINIPS_WD_BIAS=vec default since round 4)
 W = 36                        # sparse row: 32 emb + wide + pad (fp32 in the table)
 
 
@@ -41,16 +41,16 @@ def spec(U):
     s1, s2, s3 = _split(H1, K1), _split(H2, K2), _split(H3, K3)
     return [
         (r"gemm_v2_kernel<256, 256, false, false", 0, "fwd1 X.W1^T 16384x1024x896 +bias/ReLU", *gemm(B, H1, K1, 2)),
-        (r"gemm_v2_kernel<128, 128, false, false", 0, "fwd2 16384x512x1032 +ReLU", *gemm(B, H2, K2, 2)),
-        (r"gemm_v2_kernel<128, 128, false, false", 1, "fwd3 16384x256x520 +ReLU", *gemm(B, H3, K3, 2)),
+        (r"gemm_v2_kernel<128, 128, false, false", 0, f"fwd2 16384x512x{K2} +bias/ReLU", *gemm(B, H2, K2, 2)),
+        (r"gemm_v2_kernel<128, 128, false, false", 1, f"fwd3 16384x256x{K3} +bias/ReLU", *gemm(B, H3, K3, 2)),
         (r"gemm_v2_kernel<128, 128, false, true", 0, "dgrad dH2 16384x512x256 (ReLU mask)",
          gemm(B, H2, H3, 2)[0], gemm(B, H2, H3, 2)[1] + B * H2 * 2),
         (r"gemm_v2_kernel<256, 256, false, true, 5", 0, "dgrad dH1 16384x1024x512 (ReLU mask)",
          gemm(B, H1, H2, 2)[0], gemm(B, H1, H2, 2)[1] + B * H1 * 2),
         (r"gemm_v2_kernel<256, 256, false, true, 4", 0, "dgrad dX 16384x832x1024", *gemm(B, F * D, H1, 2)),
-        (r"gemm_v2_kernel<\d+, \d+, true, true", 0, f"wgrad W3 256x520x16384 ({s3} split-K slabs)",
+        (r"gemm_v2_kernel<\d+, \d+, true, true", 0, f"wgrad W3 256x{K3}x16384 ({s3} split-K slabs)",
          *gemm(H3, K3, B, 4, s3)),
-        (r"gemm_v2_kernel<\d+, \d+, true, true", 1, f"wgrad W2 512x1032x16384 ({s2} split-K slabs)",
+        (r"gemm_v2_kernel<\d+, \d+, true, true", 1, f"wgrad W2 512x{K2}x16384 ({s2} split-K slabs)",
          *gemm(H2, K2, B, 4, s2)),
         (r"gemm_v2_kernel<\d+, \d+, true, true", 2, f"wgrad W1 1024x896x16384 ({s1} split-K slabs)",
          *gemm(H1, K1, B, 4, s1)),
@@ -59,11 +59,13 @@ def spec(U):
         (r"splitk_reduce_kernel", 2, f"split-K reduce W1 ({s1} planes)", 0, s1 * H1 * K1 * 4 + 2 * H1 * K1 * 4),
         (r"wd_assemble_tab_kernel", 0, "Get + assemble X (rows read from the fp32 shard + dense + wide sum)", 0,
          B * K1 * 2 + n * (D * 4 + 4 + 8 + 8) + B * ND * 4 + B * 4),
-        (r"wd_head_kernel", 0, "head Linear 256->1 + BCE fwd/bwd", 0, B * H3 * 2 * 2 + B * 12),
+        (r"wd_head_kernel", 0, "head Linear 256->1 + BCE fwd/bwd (+ dH3 column sums)", 0, B * H3 * 2 * 2 + B * 12),
+        (r"colsum_bf16_kernel", 0, "layer-2 bias gradient (dH2 column sums)", 0, B * H2 * 2),
         (r"zero_rows_dev_kernel", 0, "zero grad rows", 0, U * W * 4),
         (r"emb_seg_sum_kernel", 0, "embedding backward (segment sums)", 0, n * (D * 2 + 8 + 4) + U * W * 4),
         (r"sparse_rowwise_adagrad_v4", 0, "row-wise Adagrad apply (U rows)", 0, U * (W * 4 * 3 + 8 + 8 + 8)),
-        (r"adam_kernel", 0, "Adam (dense 1.58M params)", 0, 1582080 * (16 + 18)),
+        (r"adam_kernel", 0, f"Adam (dense 1.58M params, folds the {s1}+{s2}+{s3} wgrad slab planes)", 0,
+         1582080 * (16 + 18) + 4 * (s1 * H1 * K1 + s2 * H2 * K2 + s3 * H3 * K3)),
         (r"criteo_synth_kernel", 0, "synthetic batch (planning stream)", 0, B * (F * 8 + ND * 4 + 4)),
         (r"plan_transpose_kernel", 0, "plan: keys -> column-major (planning)", 0, n * (8 + 4)),
         (r"plan_sort_col_kernel", 0, "plan: per-column LDS radix sort, 26 WGs (planning)", 0, n * (4 + 4 + 4) + U * 8),
