@@ -20,8 +20,13 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# 8 HIP hardware queues (the step's 6-7 streams otherwise share 4 and serialise; see
+# minips_amd/__init__.py): HIP reads this when torch loads it, so before the torch import
+if os.environ.get("GPU_MAX_HW_QUEUES", "4") == "4":  # unset or HIP's default (the GPU box exports 4)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MINIPS_HW_QUEUES", "8")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 

@@ -369,13 +369,20 @@ class WideDeep(LookaheadPlans):
         dXe = b["dX"].view(B * F, D) if sorted_rows else b["dX"]
         self.emb.add_lookup_grads(plan, dXe, b["dwide"], F, D, sorted_rows=sorted_rows)  # the table reduces
         self.emb.clock()
+        capturing = side.stream is not None and torch.cuda.is_current_stream_capturing()
         dense_side = (_DENSE_ON_SIDE and not dense_early and side.stream is not None and self.comm.world == 1
-                      and pipe is not None and not pipe.async_ and not torch.cuda.is_current_stream_capturing())
+                      and pipe is not None and not pipe.async_ and not capturing)
+        # the one-sided dense table (ps/onesided.py): its clock -- the push into the owners' inboxes
+        # -- only needs the weight gradients, and the next step's reads are SSP-stale anyway, so it
+        # goes on the side stream too (the next step's Get and assembly overlap the wgrad tail)
+        dense_side = dense_side or (_DENSE_ON_SIDE and side.stream is not None and pipe is None
+                                    and getattr(self.dense, "side_clock_ok", False) and not capturing)
         if dense_side:
             # one rank, synchronous clock: the dense Adam runs on the side stream right behind the
             # last weight gradient, and the main stream does not join here -- the next step waits
-            # for the weight gradients before its assembly rewrites X and for the Adam before its
-            # forward reads W, so the Adam overlaps the next step's input assembly
+            # for the weight gradients before its assembly rewrites X and for the Adam (or the
+            # one-sided push, which reads and clears the gradient buffer) before its forward reads W
+            # and its head writes gradients, so the clock overlaps the next step's input assembly
             ev_x = side.mark()
             with streams.use(side.stream):
                 self.dense.add()

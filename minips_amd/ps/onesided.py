@@ -901,6 +901,10 @@ class AsyncDenseTable(_AsyncTable):
             self.ps.server.enable(self.t)
         self._finish_init()
 
+    # the clock (push + headers + host publish of this stream's event) may be issued from any
+    # stream of the device: WideDeep issues it on its weight-gradient side stream
+    side_clock_ok = True
+
     @property
     def clock_count(self):
         return self.clock_n

@@ -365,6 +365,15 @@ class DenseTable:
             with streams.use(st):
                 self._bucket_work(k, grad, step)
         else:
+            # synchronous clocks: the bucket's collectives run on the current stream, which must
+            # still wait for the gradients' producers on other streams (the weight-gradient side
+            # stream) -- with the HIP default of 4 hardware queues the two streams happened to
+            # share a queue, which hid the missing wait; with 8 they run concurrently
+            if grad.is_cuda:
+                cur = streams.current(grad.device)
+                for ev in events:
+                    if ev is not None:
+                        cur.wait_event(ev)
             self._bucket_work(k, grad, step)
 
     def _full_from_pieces(self, t: torch.Tensor) -> torch.Tensor:

@@ -107,9 +107,12 @@ def test_widedeep_lookahead_depth_matches(dev):
             losses.append(float(m.train_step(dense, keys, y, next_keys=nk).item()) / 512)
         m.drain()
         res[depth] = losses
+    # (float atomics in the layer-2 bias column sums and the embedding segment sums make two runs
+    # of the same schedule differ by ~1e-4 in the loss after a few Adam steps, more often since the
+    # streams run on separate hardware queues (GPU_MAX_HW_QUEUES=8))
     for depth in (1, 2):
         for a, b in zip(res[depth], res[0]):
-            assert abs(a - b) < 1e-4, (depth, res)
+            assert abs(a - b) < 5e-4, (depth, res)
 
 
 def test_widedeep_fused_assemble_matches_gather(dev, monkeypatch):
