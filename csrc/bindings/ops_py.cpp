@@ -598,7 +598,7 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
   const int64_t n = B * F;
   auto o64 = keys.options();
   const int64_t nchunks = (n + 1023) / 1024;
-  auto ws = at::empty({4 * n + F + 4 + 2 * nchunks * P}, o64.dtype(at::kInt));  // see kernels.h
+  auto ws = at::empty({7 * n + F + 4 + 2 * nchunks * P}, o64.dtype(at::kInt));  // see kernels.h
   auto ukey = at::empty({n}, o64), uniq = at::empty({n}, o64), inv = at::empty({n}, o64);
   auto members = at::empty({n}, o64.dtype(at::kInt)), memrow = at::empty({n}, o64.dtype(at::kInt));
   auto counts = at::empty({P + 1}, o64);

@@ -179,7 +179,7 @@ void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const i
                           float* grad_rows, int row_stride, hipStream_t s);
 // Sort-based key planning of a [B, F] batch with disjoint column key ranges (plan.hip): keys of
 // column f lie in [col_base[f], col_base[f] + 2^col_bits[f]), 1 <= col_bits[f] <= 32 (device
-// arrays); P owners with routed-key bounds [P+1] (1 <= P <= 16). ws: int32 [4*B*F + F + 4 +
+// arrays); P owners with routed-key bounds [P+1] (1 <= P <= 16). ws: int32 [7*B*F + F + 4 +
 // 2*ceil(B*F/1024)*P], ukey: int64 [B*F]. Outputs: uniq [B*F] (first U valid, routed, grouped
 // by owner), inv [B*F], the lookup CSR members/memrow [B*F] int32, counts [P+1] = {per owner, U}.
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,

@@ -191,6 +191,73 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __rest
   }
 }
 
+// One wave per block, no LDS: the wave's column partials go straight to its partial row. The
+// 4-wave variant above combines its waves in 32 KB of LDS, so beside a 256x256 GEMM workgroup
+// (128 KB) only one of its blocks fits a CU; in GPT-2's backward it runs next to the side
+// stream's weight-gradient GEMMs (the default; MINIPS_LN_BWD_WAVE=0 selects the 4-wave kernel).
+__global__ __launch_bounds__(64) void layernorm_bwd_wave_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                                const bf16_t* __restrict__ dy, int lddy, int64_t M,
+                                                                int C, const bf16_t* __restrict__ gamma,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                bf16_t* __restrict__ dx, int lddx,
+                                                                float* __restrict__ partial, bool accumulate_dx) {
+  const int lane = threadIdx.x;
+  float gm[kLnK][4], ag[kLnK][4], ab[kLnK][4];
+#pragma unroll
+  for (int k = 0; k < kLnK; ++k) {
+    const int c = k * 256 + lane * 4;
+    if (c < C) ld4(gamma + c, gm[k]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ag[k][q] = ab[k][q] = 0.f;
+  }
+  for (int64_t r = blockIdx.x; r < M; r += gridDim.x) {
+    const float mu = mean[r], rs = rstd[r];
+    float xh[kLnK][4], g[kLnK][4];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLnK; ++k) {
+      const int c = k * 256 + lane * 4;
+      if (c < C) {
+        float d[4];
+        ld4(x + r * ldx + c, xh[k]);
+        ld4(dy + r * lddy + c, d);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          xh[k][q] = (xh[k][q] - mu) * rs;
+          g[k][q] = d[q] * gm[k][q];
+          a += g[k][q];
+          b += g[k][q] * xh[k][q];
+          ag[k][q] += d[q] * xh[k][q];
+          ab[k][q] += d[q];
+        }
+      }
+    }
+    a = warp_sum(a) / C;
+    b = warp_sum(b) / C;
+#pragma unroll
+    for (int k = 0; k < kLnK; ++k) {
+      const int c = k * 256 + lane * 4;
+      if (c < C) {
+        float o[4], prev[4];
+        if (accumulate_dx) ld4(dx + r * lddx + c, prev);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = rs * (g[k][q] - a - xh[k][q] * b) + (accumulate_dx ? prev[q] : 0.f);
+        st4(dx + r * lddx + c, o);
+      }
+    }
+  }
+  float* out = partial + (int64_t)blockIdx.x * 2 * C;
+#pragma unroll
+  for (int k = 0; k < kLnK; ++k) {
+    const int c = k * 256 + lane * 4;
+    if (c < C) {
+      *reinterpret_cast<float4*>(out + c) = make_float4(ag[k][0], ag[k][1], ag[k][2], ag[k][3]);
+      *reinterpret_cast<float4*>(out + C + c) = make_float4(ab[k][0], ab[k][1], ab[k][2], ab[k][3]);
+    }
+  }
+}
+
 // dgamma/dbeta[j] += sum_g partial[g][j], j < 2C: 64 columns per block (coalesced rows), the
 // block's 4 waves split the G partial rows and combine in LDS.
 // blockIdx.y takes a slice of the G partial rows (kColsumSlices slices, fp32 atomics into the
@@ -225,7 +292,7 @@ __global__ __launch_bounds__(256) void layernorm_colsum_kernel(const float* __re
 // ~8 rows per 4-wave block: 4x the waves of a 32-rows-per-block split, so the row loop's
 // dependent load -> reduce -> store chain is hidden by occupancy instead of serialised.
 // MINIPS_LN_BWD_ROWS / MINIPS_LN_BWD_MAXB override the rows per block and the block cap (A/B knobs).
-int layernorm_bwd_blocks(int64_t M) {
+static int ln_bwd_blocks4(int64_t M) {
   auto knob = [](const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e ? std::max(1, atoi(e)) : dflt;
@@ -234,6 +301,28 @@ int layernorm_bwd_blocks(int64_t M) {
   static const int cap = knob("MINIPS_LN_BWD_MAXB", 1024);
   return (int)std::min<int64_t>(std::max<int64_t>((M + rows - 1) / rows, 1), cap);
 }
+
+// one-wave variant (default; MINIPS_LN_BWD_WAVE=0: the 4-wave LDS-combining kernel), 8 rows per
+// wave (MINIPS_LN_BWD_WROWS): GPT-2 12.69-12.70 vs 12.74-12.75 ms/step (4 rows 12.86, 16 rows
+// 13.2; profiles/r4/ab_gpt2_ln_bwd.txt). Its blocks are the partial rows.
+static bool ln_bwd_wave() {
+  static const bool on = [] {
+    const char* e = std::getenv("MINIPS_LN_BWD_WAVE");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+static int ln_bwd_wave_blocks(int64_t M) {
+  static const int rows = [] {
+    const char* e = std::getenv("MINIPS_LN_BWD_WROWS");
+    return e ? std::max(1, std::atoi(e)) : 8;
+  }();
+  return (int)std::min<int64_t>(std::max<int64_t>((M + rows - 1) / rows, 1), 4096);
+}
+
+// partial rows of layernorm_bwd (the scratch it needs: rows * 2 * C floats)
+int layernorm_bwd_blocks(int64_t M) { return ln_bwd_wave() ? ln_bwd_wave_blocks(M) : ln_bwd_blocks4(M); }
 
 void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gamma, const bf16_t* beta, float eps,
                    bf16_t* y, int ldy, float* mean, float* rstd, hipStream_t s) {
@@ -249,9 +338,14 @@ void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t
                    float* partial, bool accumulate_dx, hipStream_t s) {
   if (M <= 0) return;
   if (C > 1024 || C % 4) throw std::runtime_error("layernorm: C <= 1024 and C % 4 == 0");
-  const int G = layernorm_bwd_blocks(M);
-  hipLaunchKernelGGL(layernorm_bwd_kernel, G, 256, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx, partial,
-                     accumulate_dx);
+  const bool wave = ln_bwd_wave();
+  const int G = wave ? ln_bwd_wave_blocks(M) : ln_bwd_blocks4(M);
+  if (wave)
+    hipLaunchKernelGGL(layernorm_bwd_wave_kernel, G, 64, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx,
+                       partial, accumulate_dx);
+  else
+    hipLaunchKernelGGL(layernorm_bwd_kernel, G, 256, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx,
+                       partial, accumulate_dx);
   MINIPS_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(layernorm_colsum_kernel, dim3((2 * C + 63) / 64, G >= 64 ? kColsumSlices : 1), 256, 0, s,
                      partial, G, C, dgamma, dbeta);

@@ -225,6 +225,261 @@ __global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const uint32_
   if (t == 0) ucount[f] = (int32_t)total;
 }
 
+// ---- the same column sort spread over 4 workgroups per column (F x 4 = 104 for W&D instead of
+// 26 one-CU workgroups holding 128 KB of LDS each: beside a 256x256 GEMM those left the GEMM's
+// 256 tiles a second round). Three launches:
+//   plan_sort_chunk  (F, ceil(B / 4096)) x 256 threads: each 4096-lookup chunk of a column LSD
+//                    radix-sorted in 32 KB of LDS (the algorithm of plan_sort_col at 256 threads)
+//                    -> chunk-sorted keys ck / row ids cv
+//   plan_merge       (F, chunks) x 256: every chunk's keys of the column in LDS; an item's merged
+//                    position = its chunk rank + its rank in each other chunk (binary search for
+//                    a thread's first item, then a merge walk over its 16 consecutive items; ties
+//                    ordered by chunk: stable) -> merged keys mk, sorted_b
+//   plan_heads       F x 1024: run heads of mk, block scan -> local_u, ukey, ucount
+constexpr int kPcThreads = 256, kPcItems = 16, kPcChunk = kPcThreads * kPcItems;  // 4096 lookups
+
+// exclusive scan of one value per thread over a T-thread block (T/64 <= 64 waves); *total = sum
+template <int T>
+__device__ __forceinline__ uint32_t pc_block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
+  constexpr int NW = T / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) ws[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t w = lane < NW ? ws[lane] : 0u;
+    uint32_t s = w;
+#pragma unroll
+    for (int o = 1; o < NW; o <<= 1) {
+      const uint32_t y = __shfl_up(s, o, 64);
+      if (lane >= o) s += y;
+    }
+    if (lane < NW) ws[lane] = s - w;
+    if (lane == NW - 1) ws[NW] = s;
+  }
+  __syncthreads();
+  const uint32_t res = ws[wave] + x - v;
+  *total = ws[NW];
+  __syncthreads();
+  return res;
+}
+
+__global__ __launch_bounds__(kPcThreads) void plan_sort_chunk_kernel(const uint32_t* __restrict__ krel, int B,
+                                                                     const int32_t* __restrict__ col_bits,
+                                                                     uint32_t* __restrict__ ck,
+                                                                     int32_t* __restrict__ cv) {
+  __shared__ __attribute__((aligned(16))) uint16_t cnt[16 * kPcThreads];
+  __shared__ __attribute__((aligned(16))) uint32_t skey[kPcChunk];
+  __shared__ __attribute__((aligned(16))) uint16_t sval[kPcChunk];
+  __shared__ uint32_t ws[8];
+  const int t = threadIdx.x, f = blockIdx.x, c = blockIdx.y;
+  const int c0 = c * kPcChunk, len = min(kPcChunk, B - c0);
+  const int nbits = col_bits[f];
+  const uint32_t* col = krel + (int64_t)f * B + c0;
+  uint32_t k[kPcItems], v[kPcItems];
+  if ((B & 3) == 0 && t * kPcItems + kPcItems <= len) {
+    const uint4* p = reinterpret_cast<const uint4*>(col + t * kPcItems);  // krel and c0 16-byte aligned
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint4 u = p[e];
+      k[4 * e] = u.x;
+      k[4 * e + 1] = u.y;
+      k[4 * e + 2] = u.z;
+      k[4 * e + 3] = u.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kPcItems; ++q) {
+      const int i = t * kPcItems + q;
+      k[q] = i < len ? col[i] : 0xffffffffu;  // padding sorts behind every real item (stable)
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kPcItems; ++q) v[q] = (uint32_t)(c0 + t * kPcItems + q);
+  for (int shift = 0; shift < nbits; shift += 4) {
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int q = 0; q < kPcItems; ++q) {
+      const int d = (int)((k[q] >> shift) & 15u);
+      if (d < 8) lo += 1ull << (8 * d);
+      else hi += 1ull << (8 * (d - 8));
+    }
+#pragma unroll
+    for (int d = 0; d < 16; ++d) cnt[d * kPcThreads + t] = (uint16_t)ps_count(lo, hi, d);
+    __syncthreads();
+    uint4* cvv = reinterpret_cast<uint4*>(cnt) + 2 * t;
+    const uint4 q0 = cvv[0], q1 = cvv[1];
+    const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    uint32_t o[8];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t a = w[e] & 0xffffu, b = w[e] >> 16;
+      o[e] = sum | ((sum + a) << 16);
+      sum += a + b;
+    }
+    uint32_t tot;
+    const uint32_t pre = pc_block_scan<kPcThreads>(sum, ws, &tot);
+    const uint32_t pre2 = pre | (pre << 16);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] += pre2;
+    cvv[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    cvv[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    __syncthreads();
+    uint64_t slo = 0, shi = 0;
+#pragma unroll
+    for (int q = 0; q < kPcItems; ++q) {
+      const int d = (int)((k[q] >> shift) & 15u);
+      const uint32_t r = ps_count(slo, shi, d);
+      if (d < 8) slo += 1ull << (8 * d);
+      else shi += 1ull << (8 * (d - 8));
+      const uint32_t pos = (uint32_t)cnt[d * kPcThreads + t] + r;
+      skey[pos] = k[q];
+      sval[pos] = (uint16_t)v[q];
+    }
+    __syncthreads();
+    {
+      const uint4* kp = reinterpret_cast<const uint4*>(skey + t * kPcItems);
+      const uint4* vp = reinterpret_cast<const uint4*>(sval + t * kPcItems);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint4 u = kp[e];
+        k[4 * e] = u.x;
+        k[4 * e + 1] = u.y;
+        k[4 * e + 2] = u.z;
+        k[4 * e + 3] = u.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const uint4 u = vp[e];
+        const uint32_t w2[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          v[8 * e + 2 * h] = w2[h] & 0xffffu;
+          v[8 * e + 2 * h + 1] = w2[h] >> 16;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  uint32_t* ko = ck + (int64_t)f * B + c0;
+  int32_t* vo = cv + (int64_t)f * B + c0;
+#pragma unroll
+  for (int q = 0; q < kPcItems; ++q) {
+    const int i = t * kPcItems + q;
+    if (i < len) {
+      ko[i] = k[q];
+      vo[i] = (int32_t)v[q];
+    }
+  }
+}
+
+// smallest i in [p, n) with !go(a[i]) (n if none), go(x) = x <= key (UPPER) / x < key: galloping
+// from p (doubling steps, then a binary search), so a cursor that moves by d costs O(log d) reads --
+// a low-cardinality column puts thousands of equal keys between a thread's consecutive items
+template <bool UPPER>
+__device__ __forceinline__ int pc_gallop(const uint32_t* a, int p, int n, uint32_t key) {
+  auto go = [&](int i) { return UPPER ? a[i] <= key : a[i] < key; };
+  if (p >= n || !go(p)) return p;
+  int lo = p, step = 1, hi = p + 1;  // go(lo); hi: the next probe
+  while (hi < n && go(hi)) {
+    lo = hi;
+    step <<= 1;
+    hi = lo + step;
+  }
+  if (hi > n) hi = n;  // now hi == n or !go(hi)
+  int l = lo + 1, r = hi;
+  while (l < r) {
+    const int m = (l + r) >> 1;
+    if (go(m)) l = m + 1;
+    else r = m;
+  }
+  return l;
+}
+
+constexpr int kPmMaxChunks = kPsMax / kPcChunk;  // 4
+
+__global__ __launch_bounds__(kPcThreads) void plan_merge_kernel(const uint32_t* __restrict__ ck,
+                                                                const int32_t* __restrict__ cv, int B,
+                                                                uint32_t* __restrict__ mk,
+                                                                int32_t* __restrict__ sorted_b) {
+  __shared__ __attribute__((aligned(16))) uint32_t keys[kPsMax];
+  const int t = threadIdx.x, f = blockIdx.x, c = blockIdx.y, nch = gridDim.y;
+  const uint32_t* col = ck + (int64_t)f * B;
+  for (int i = t; i < B; i += kPcThreads) keys[i] = col[i];
+  __syncthreads();
+  const int c0 = c * kPcChunk, len = min(kPcChunk, B - c0);
+  const int i0 = t * kPcItems;
+  if (i0 >= len) return;
+  const int cnt = min(kPcItems, len - i0);
+  // cursors into the other chunks, advanced by galloping from item to item
+  int cur[kPmMaxChunks] = {0, 0, 0, 0};
+  uint32_t* mko = mk + (int64_t)f * B;
+  int32_t* sbo = sorted_b + (int64_t)f * B;
+  const int32_t* cvi = cv + (int64_t)f * B + c0;
+  for (int q = 0; q < cnt; ++q) {
+    const int i = i0 + q;
+    const uint32_t key = keys[c0 + i];
+    int pos = i;
+    for (int o = 0; o < nch; ++o) {
+      if (o == c) continue;
+      const int o0 = o * kPcChunk, ol = min(kPcChunk, B - o0);
+      // equal keys of earlier chunks come first (stable)
+      const int p = o < c ? pc_gallop<true>(keys + o0, cur[o], ol, key) : pc_gallop<false>(keys + o0, cur[o], ol, key);
+      cur[o] = p;
+      pos += p;
+    }
+    mko[pos] = key;
+    sbo[pos] = cvi[i];
+  }
+}
+
+__global__ __launch_bounds__(kPsThreads) void plan_heads_kernel(const uint32_t* __restrict__ mk, int B,
+                                                                const int64_t* __restrict__ col_base,
+                                                                int32_t* __restrict__ local_u,
+                                                                int64_t* __restrict__ ukey,
+                                                                int32_t* __restrict__ ucount) {
+  __shared__ uint32_t ws[20];
+  const int t = threadIdx.x, f = blockIdx.x;
+  const int64_t base = col_base[f];
+  const uint32_t* col = mk + (int64_t)f * B;
+  uint32_t k[kPsItems];
+#pragma unroll
+  for (int q = 0; q < kPsItems; ++q) {
+    const int i = t * kPsItems + q;
+    k[q] = i < B ? col[i] : 0u;
+  }
+  const int first = t * kPsItems;
+  const uint32_t before = (first > 0 && first < B) ? col[first - 1] : 0u;
+  uint32_t heads = 0;
+#pragma unroll
+  for (int q = 0; q < kPsItems; ++q) {
+    const int pos = first + q;
+    const uint32_t prev = q == 0 ? before : k[q - 1];
+    heads += (pos < B && (pos == 0 || k[q] != prev)) ? 1u : 0u;
+  }
+  uint32_t total;
+  uint32_t run = pc_block_scan<kPsThreads>(heads, ws, &total);
+  const int64_t col0 = (int64_t)f * B;
+#pragma unroll
+  for (int q = 0; q < kPsItems; ++q) {
+    const int pos = first + q;
+    if (pos >= B) break;
+    const uint32_t prev = q == 0 ? before : k[q - 1];
+    const bool h = pos == 0 || k[q] != prev;
+    if (h) ++run;
+    const uint32_t lu = run - 1;
+    local_u[col0 + pos] = (int32_t)lu;
+    if (h) ukey[col0 + lu] = base + (int64_t)k[q];
+  }
+  if (t == 0) ucount[f] = (int32_t)total;
+}
+
 __device__ __forceinline__ int64_t ps_route(int64_t key, uint64_t mult, uint64_t rn) {
   return mult ? (int64_t)(((uint64_t)key * mult) % rn) : key;
 }
@@ -484,7 +739,8 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
   if (route_mult && !route_n) throw std::runtime_error("plan_sorted: routing needs the row count");
   const int64_t n = (int64_t)B * F;
   // ws: sorted_b [n] | local_u [n] | ucount [F] | (16-byte aligned) column-major keys [n] | perm [n] |
-  //     owner counts / offsets [2 * nchunks * P]
+  //     owner counts / offsets [2 * nchunks * P] | (16-byte aligned) chunk-sorted keys ck [n], row
+  //     ids cv [n], merged keys mk [n] (the chunked sort)
   int32_t* sorted_b = ws;
   int32_t* local_u = ws + n;
   int32_t* ucount = ws + 2 * n;
@@ -496,9 +752,28 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
   int32_t* ooff = ocnt + (int64_t)nchunks * P;
   for (int r = 0; r < plan_reps(1); ++r)
     hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, krel);
-  for (int r = 0; r < plan_reps(2); ++r)
-    hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u,
-                       ukey, ucount);
+  // MINIPS_PLAN_SORT=1 (default): one 1024-thread workgroup per column; 4: the chunked sort over
+  // F x 4 workgroups -- measured slower in the W&D step (0.3708 vs 0.3657 ms: chunk sort 26 +
+  // merge 66 + heads 29 us against 70 us for the one-workgroup sort; profiles/r4/ab_wd_knobs.txt)
+  static const int sort_mode = [] {
+    const char* e = std::getenv("MINIPS_PLAN_SORT");
+    return e ? std::atoi(e) : 1;
+  }();
+  const int nch = (B + kPcChunk - 1) / kPcChunk;
+  for (int r = 0; r < plan_reps(2); ++r) {
+    if (sort_mode == 1 || nch == 1) {
+      hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u,
+                         ukey, ucount);
+    } else {
+      // (ck / cv / mk: past the owner counts at the workspace end; see the layout above)
+      uint32_t* ck = reinterpret_cast<uint32_t*>(ooff + (int64_t)nchunks * P);
+      int32_t* cv = reinterpret_cast<int32_t*>(ck + n);
+      uint32_t* mk = reinterpret_cast<uint32_t*>(cv + n);
+      hipLaunchKernelGGL(plan_sort_chunk_kernel, dim3(F, nch), kPcThreads, 0, s, krel, B, col_bits, ck, cv);
+      hipLaunchKernelGGL(plan_merge_kernel, dim3(F, nch), kPcThreads, 0, s, ck, cv, B, mk, sorted_b);
+      hipLaunchKernelGGL(plan_heads_kernel, F, kPsThreads, 0, s, mk, B, col_base, local_u, ukey, ucount);
+    }
+  }
   if (P > 1) {
     hipLaunchKernelGGL(plan_owner_count_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
                        route_n, ocnt);
