@@ -384,9 +384,11 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
   if (B <= 0) return;
   const int block = 64 * kHeadWaves;
   // per-block LDS reduction, partial rows, the last block folds them (one block per CU at most)
+  // 256 blocks (every CU, one sample iteration per wave): W&D 0.3632-0.3637 vs 0.3672-0.3678 ms at
+  // 128 (profiles/r4/ab_wd_knobs.txt); the two-level fold takes at most 256
   static const int max_blocks = [] {
     const char* e = std::getenv("MINIPS_HEAD_BLOCKS");
-    return e ? std::atoi(e) : 128;
+    return e ? std::atoi(e) : 256;
   }();
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(max_blocks, (B + 63) / 64));
   // the partial slab + ticket of this device: allocated once (zero ticket), before any capture

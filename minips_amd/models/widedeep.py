@@ -98,6 +98,10 @@ _WGRAD_BLOCKS = int(os.environ.get("MINIPS_WD_WGRAD_BLOCKS", "320"))
 
 # MINIPS_DENSE_ON_SIDE=0: one rank's dense Adam on the main stream at the step end (joined)
 _DENSE_ON_SIDE = os.environ.get("MINIPS_DENSE_ON_SIDE", "1") != "0"
+# MINIPS_WD_W1_LATE=1: fork the layer-1 weight gradient after the embedding dgrad (beside the
+# embedding backward rather than beside the dgrad: two big GEMMs at once only share the CUs);
+# round 3 measured it 5 % slower (profiles/r3/ab_wd_r3.txt)
+_W1_LATE = os.environ.get("MINIPS_WD_W1_LATE", "0") == "1"
 # MINIPS_ROWIDX=0: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
 _ROWIDX = os.environ.get("MINIPS_ROWIDX", "1") != "0"
 
@@ -344,8 +348,9 @@ class WideDeep(LookaheadPlans):
                 _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink)
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         self._bucket_done(1, side)  # (layers 2, 3 and the head: their weight gradients are issued)
-        with side.fork():
-            _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
+        if not _W1_LATE:
+            with side.fork():
+                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
         # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
@@ -356,6 +361,9 @@ class WideDeep(LookaheadPlans):
                              perm=plan.csr[2], seg=D)
         else:
             ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
+        if _W1_LATE:  # the layer-1 weight gradient beside the memory-bound embedding backward instead
+            with side.fork():
+                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
         # an async dense clock (its own stream) needs only the weight gradients: issued from the
         # side stream it starts as soon as the last wgrad ends, beside the embedding backward and
         # the sparse push, instead of behind them
