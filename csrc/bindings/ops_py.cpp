@@ -1285,13 +1285,32 @@ void ps_push_rows(const at::Tensor& uniq, const at::Tensor& counts, const c10::o
                          (int)g.size(1), ptr<int64_t>(inbox), (int)P, slot_off, cap, stream_of(g));
 }
 
-void ps_push_dense(at::Tensor& grad, const at::Tensor& inbox, int64_t data_off, int64_t S) {
+void ps_push_dense(at::Tensor& grad, const at::Tensor& inbox, int64_t data_off, int64_t S,
+                   const std::vector<std::tuple<at::Tensor, int64_t, int64_t, int64_t>>& slabs) {
   check_gpu(grad, "grad");
   check_dtype(grad, at::kFloat, "grad");
   check_gpu(inbox, "inbox");
   TORCH_CHECK(grad.numel() >= inbox.numel() * S, "grad: >= P * S floats");
+  // (slab [nsplit * plane] fp32, nsplit, plane, offset of its region in grad), as adam_apply's
+  minips_k::AdamSlabs sl;
+  TORCH_CHECK(slabs.size() <= 4, "ps_push_dense: at most 4 slab regions");
+  for (const auto& t : slabs) {
+    const at::Tensor& p = std::get<0>(t);
+    const int64_t ns = std::get<1>(t), plane = std::get<2>(t), off = std::get<3>(t);
+    check_gpu(p, "slab");
+    check_dtype(p, at::kFloat, "slab");
+    TORCH_CHECK(ns >= 1 && p.numel() >= ns * plane && off >= 0 && off + plane <= inbox.numel() * S,
+                "ps_push_dense slab bounds");
+    sl.p[sl.n] = ptr<float>(p);
+    sl.nsplit[sl.n] = (int)ns;
+    sl.plane[sl.n] = plane;
+    sl.len[sl.n] = plane;
+    sl.off[sl.n] = off;
+    ++sl.n;
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(grad.device());
-  minips_k::ps_push_dense(ptr<float>(grad), ptr<int64_t>(inbox), (int)inbox.numel(), data_off, S, stream_of(grad));
+  minips_k::ps_push_dense(ptr<float>(grad), ptr<int64_t>(inbox), (int)inbox.numel(), data_off, S, stream_of(grad),
+                          sl.n ? &sl : nullptr);
 }
 
 void ps_set_headers(const at::Tensor& inbox, int64_t slot_off, int64_t value) {
@@ -1744,7 +1763,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("ps_push_rows", &ps_push_rows, py::arg("uniq"), py::arg("counts"), py::arg("U_dev"), py::arg("n"),
         py::arg("g"), py::arg("inbox"), py::arg("slot_off"), py::arg("cap"));
   m.def("ps_set_headers", &ps_set_headers);
-  m.def("ps_push_dense", &ps_push_dense);
+  m.def("ps_push_dense", &ps_push_dense, py::arg("grad"), py::arg("inbox"), py::arg("data_off"), py::arg("S"),
+        py::arg("slabs") = std::vector<std::tuple<at::Tensor, int64_t, int64_t, int64_t>>());
   m.def("ps_gather_rows_bf16tab", &ps_gather_rows_bf16tab, py::arg("bases"), py::arg("bounds"), py::arg("keys"),
         py::arg("n_dev"), py::arg("W"), py::arg("out"));
   m.def("ps_hash_gather", &ps_hash_gather, py::arg("hkeys"), py::arg("hvals"), py::arg("bounds"), py::arg("cap"),

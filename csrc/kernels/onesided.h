@@ -13,6 +13,7 @@
 namespace minips_k {
 
 typedef uint16_t bf16_t;
+struct AdamSlabs;  // (kernels.h) split-K planes folded by ps_push_dense
 
 constexpr int kPsMaxWorld = 16;
 constexpr int64_t kPsSlotHeader = 64;
@@ -26,7 +27,8 @@ void ps_push_rows(const int64_t* uniq, const int64_t* counts, const int64_t* U_d
 // Every owner's slot header := value (0: a clock without an Add; a dense push marks its slot 1).
 void ps_set_headers(const int64_t* inbox, int P, int64_t slot_off, int64_t value, hipStream_t s);
 // dense push: grad[o * S, (o + 1) * S) -> inbox[o] + data_off for every owner o, grad cleared
-void ps_push_dense(float* grad, const int64_t* inbox, int P, int64_t data_off, int64_t S, hipStream_t s);
+void ps_push_dense(float* grad, const int64_t* inbox, int P, int64_t data_off, int64_t S, hipStream_t s,
+                   const AdamSlabs* slabs = nullptr);
 // out[i] = row of keys[i] (i < min(n, *n_dev)) from its owner's fp32 shard at bases[o]
 // ([rows_o, W]); out fp32 or bf16 [n, W].
 void ps_gather_rows(const int64_t* bases, const int64_t* bounds, int P, const int64_t* keys, int64_t n,

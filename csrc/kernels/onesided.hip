@@ -507,25 +507,46 @@ void ps_push_rows(const int64_t* uniq, const int64_t* counts, const int64_t* U_d
 
 // The dense push of one clock: owner o's slice grad[o * S, (o + 1) * S) into the data area of slot
 // `slot_off` of its inbox, and grad cleared for the next clock -- one pass (read once, write the
-// slot and the zero) instead of P copies and a fill.
+// slot and the zero) instead of P copies and a fill. `sl`: split-K weight-gradient planes whose
+// sums are added on the way (the regions' offsets in grad; no reduce kernels before the push).
 __global__ __launch_bounds__(256) void ps_push_dense_kernel(float* __restrict__ grad, const int64_t* __restrict__ inbox,
-                                                            int P, int64_t data_off, int64_t S4) {
+                                                            int P, int64_t data_off, int64_t S4, AdamSlabs sl) {
   const int64_t total = (int64_t)P * S4;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int o = (int)(e / S4);
     const int64_t k = e - (int64_t)o * S4;
-    const float4 v = reinterpret_cast<const float4*>(grad)[e];
+    float4 v = reinterpret_cast<const float4*>(grad)[e];
+    for (int r = 0; r < sl.n; ++r) {
+      const int64_t x = 4 * e - sl.off[r];
+      if (x < 0 || x >= sl.len[r]) continue;
+      const float* p = sl.p[r] + x;
+      for (int z = 0; z < sl.nsplit[r]; ++z) {
+        const float4 a = *reinterpret_cast<const float4*>(p + z * sl.plane[r]);
+        v.x += a.x;
+        v.y += a.y;
+        v.z += a.z;
+        v.w += a.w;
+      }
+    }
     reinterpret_cast<float4*>(reinterpret_cast<char*>(inbox[o]) + data_off)[k] = v;
     reinterpret_cast<float4*>(grad)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
-void ps_push_dense(float* grad, const int64_t* inbox, int P, int64_t data_off, int64_t S, hipStream_t s) {
+void ps_push_dense(float* grad, const int64_t* inbox, int P, int64_t data_off, int64_t S, hipStream_t s,
+                   const AdamSlabs* slabs) {
   if (P < 1 || P > kPsMaxWorld) throw std::runtime_error("ps_push_dense: P out of range");
   if (S % 4 || data_off % 16 || reinterpret_cast<uintptr_t>(grad) % 16)
     throw std::runtime_error("ps_push_dense: 16-byte aligned shards");
+  AdamSlabs sl;
+  if (slabs) {
+    sl = *slabs;
+    for (int r = 0; r < sl.n; ++r)
+      if (sl.off[r] % 4 || sl.len[r] % 4 || sl.plane[r] % 4 || reinterpret_cast<uintptr_t>(sl.p[r]) % 16)
+        throw std::runtime_error("ps_push_dense: slab regions must be 16-byte aligned");
+  }
   hipLaunchKernelGGL(ps_push_dense_kernel, grid_for((int64_t)P * (S / 4), 256, 8192), 256, 0, s, grad, inbox, P,
-                     data_off, S / 4);
+                     data_off, S / 4, sl);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

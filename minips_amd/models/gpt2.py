@@ -63,6 +63,7 @@ class GPT2Config:
 # "stats" (softmax partials in the GEMM epilogue + a streaming gradient pass: the pass is 59 us
 # faster, the epilogue 68 us slower -- 13.87 vs 14.14 ms/step, profiles/r3/gpt2_lm_head.txt)
 _XENT = os.environ.get("MINIPS_GPT2_XENT", "rowwise")
+_WGRAD_DEFER_GPT2 = os.environ.get("MINIPS_GPT2_WGRAD_DEFER", "0") == "1"
 _LM_DGRAD_SPLIT = int(os.environ.get("MINIPS_LM_DGRAD_SPLIT", "4"))
 # LM-head GEMMs (logits, dgrad, wte wgrad): "lib" (hipBLASLt through torch for these three plain
 # GEMMs: 13.10 vs 13.87 ms/step) or "ours" (gemm.hip); the CPU reference path always uses ours
@@ -224,11 +225,15 @@ class GPT2:
         dx = b["dx"]
         ops.layernorm_bwd(x[-1], dh, d, v(P, "lnf_g"), mf, rf, dx, v(G, "lnf_g"), v(G, "lnf_b"))
         ev_du = ev_dqkv = None
+        # MINIPS_GPT2_WGRAD_DEFER=1: the per-layer weight gradients' split-K planes folded by their
+        # bucket's Adam instead of reduce kernels -- measured neutral here (12.66-12.68 vs 12.48-12.64
+        # ms/step; profiles/r4/ab_gpt2_knobs.txt), so the reduces stay by default
+        sink = self.table.slab_sink() if _WGRAD_DEFER_GPT2 and hasattr(self.table, "slab_sink") else None
         for i in range(c.n_layer - 1, -1, -1):
             blk = self.blocks[i]
             # MLP branch
             with side.fork():
-                blk["fc2"].wgrad(G, dx, b["g"][i])
+                blk["fc2"].wgrad(G, dx, b["g"][i], sink)
             ev_dx = side.mark()
             side.wait(ev_du)  # du: read by the previous layer's fc wgrad
             if _GELU_D:
@@ -236,7 +241,7 @@ class GPT2:
             else:
                 blk["fc2"].dgrad(P, dx, b["du"], gelu_u=b["u"][i])
             with side.fork():
-                blk["fc"].wgrad(G, b["du"], b["h2"][i])
+                blk["fc"].wgrad(G, b["du"], b["h2"][i], sink)
             ev_du = side.mark()
             blk["fc"].dgrad(P, b["du"], dh)
             m2, r2 = b["st2"][i]
@@ -245,13 +250,13 @@ class GPT2:
                               v(G, blk["ln2_b"]), accumulate=True)
             # attention branch
             with side.fork():
-                blk["proj"].wgrad(G, dx, b["ao"][i])
+                blk["proj"].wgrad(G, dx, b["ao"][i], sink)
             ev_dx = side.mark()
             blk["proj"].dgrad(P, dx, b["dao"])
             side.wait(ev_dqkv)  # dqkv: read by the previous layer's qkv wgrad
             ops.attn_bwd(b["qkv"][i], b["ao"][i], b["dao"], b["lse"][i], b["delta"], B, T, c.n_head, scale, b["dqkv"])
             with side.fork():
-                blk["qkv"].wgrad(G, b["dqkv"], b["h1"][i])
+                blk["qkv"].wgrad(G, b["dqkv"], b["h1"][i], sink)
             ev_dqkv = side.mark()
             blk["qkv"].dgrad(P, b["dqkv"], dh)
             m1, r1 = b["st1"][i]

@@ -85,9 +85,10 @@ class Linear:
         epi = {"relu": ops.EPI_BIAS_RELU_BF16, "none": ops.EPI_BIAS_BF16}[act]
         return ops.gemm(x_ext, W, out, M, self.n_out, self.k_pad, False, False, epi)
 
-    def wgrad(self, G, dy, x_ext):
-        """G_W += dy^T x_ext (split-K gemm.hip; the bias gradient lands in column k_in)."""
-        return ops.linear_wgrad(dy, x_ext, self.W(G))
+    def wgrad(self, G, dy, x_ext, sink=None):
+        """G_W += dy^T x_ext (split-K gemm.hip; the bias gradient lands in column k_in). ``sink``: a
+        DenseTable.slab_sink() -- the K slices stay in planes its Adam folds (no reduce kernel)."""
+        return ops.linear_wgrad(dy, x_ext, self.W(G), defer=sink)
 
     def dgrad(self, P, dy, out, mask=None, gelu_u=None, out_f32=False, k_rows=None, gelu_d=None):
         """out = dy W[:, :k_in] (ReLU-masked by `mask`, or times gelu'(gelu_u)).

@@ -972,16 +972,34 @@ class AsyncDenseTable(_AsyncTable):
             self.grad[: grad.numel()] += grad.reshape(-1).to(torch.float32)
         self._pending = True
 
+    def slab_sink(self):
+        """Split-K weight gradients left in fp32 planes that this table's push sums on the way into
+        the inboxes (ops.linear_wgrad(defer=...): no reduce kernels, no pass through self.grad);
+        None off the GPU push path or with MINIPS_WGRAD_DEFER=0. The planes are rewritten by the
+        next clock's GEMMs, which the stream order puts after this clock's push."""
+        from .tables import _WGRAD_DEFER, _SlabSink
+
+        if not (_WGRAD_DEFER and self.cuda and self.shard % 4 == 0):
+            return None
+        sink = self.__dict__.get("_sink")
+        if sink is None:
+            sink = self._sink = _SlabSink(self)
+        return sink
+
     @traced("async_dense.clock")
     def clock(self):
         slot = self._reserve_slot()
         off = (self.comm.rank * self.depth + slot) * self.slot_bytes
         S = self.shard
+        sink = self.__dict__.get("_sink")
+        slabs = sink.take(self.grad) if sink is not None else []
+        if slabs and not (self._pending and self.cuda and S % 4 == 0):
+            raise RuntimeError("async dense table: deferred weight-gradient planes need the GPU push path")
         if self._pending:
             if self.cuda and S % 4 == 0:  # one pass: every owner's slice into its slot, grad cleared
                 from .._native import kernels
 
-                kernels().ps_push_dense(self.grad, self._inbox_ptrs, off + _SLOT_HEADER, S)
+                kernels().ps_push_dense(self.grad, self._inbox_ptrs, off + _SLOT_HEADER, S, slabs)
             else:
                 for o in range(self.comm.world):
                     dst = self._inbox[o][off + _SLOT_HEADER: off + _SLOT_HEADER + 4 * S].view(torch.float32)

@@ -156,18 +156,35 @@ _WGRAD_DEFER = os.environ.get("MINIPS_WGRAD_DEFER", "1") != "0"
 class _SlabSink:
     """Split-K weight-gradient slabs pending for a DenseTable's next Adam (DenseTable.slab_sink):
     persistent fp32 planes per gradient region (re-used every step: the next step's GEMM is issued
-    after this step's Adam on the stream order of the step), folded by the Adam kernel."""
+    after this step's Adam on the stream order of the step; with a ring of gradient buffers each
+    buffer has its own planes, reused under the ring's own clock wait), folded by the Adam kernel
+    that applies the region -- the whole-gradient Adam, or the Adam of the bucket holding it (at
+    most 4 regions per Adam launch)."""
 
     def __init__(self, table):
         self.t = table
         self._bufs = {}
-        self._pending = []
+        self._pending = []  # (byte address of the region, slab, nsplit, elements)
+
+    def _range_of(self, dw):
+        """Byte range [a, b) of the Adam launch that will apply ``dw``: its bucket or the gradient."""
+        g = self.t.grad
+        if getattr(self.t, "buckets", None) is None:
+            return g.data_ptr(), g.data_ptr() + g.numel() * g.element_size()
+        off = (dw.data_ptr() - g.data_ptr()) // g.element_size()
+        lo, hi = self.t.buckets[self.t.bucket_of(off)]
+        if off + dw.numel() > hi:
+            return None  # the region spans two buckets
+        return g.data_ptr() + lo * g.element_size(), g.data_ptr() + hi * g.element_size()
 
     def accepts(self, dw) -> bool:
         g = self.t.grad
-        return (dw.device == g.device and dw.dtype == g.dtype and len(self._pending) < 4
+        if not (dw.device == g.device and dw.dtype == g.dtype
                 and g.data_ptr() <= dw.data_ptr() < g.data_ptr() + g.numel() * g.element_size()
-                and (dw.data_ptr() - g.data_ptr()) % 16 == 0)
+                and (dw.data_ptr() - g.data_ptr()) % 16 == 0):
+            return False
+        r = self._range_of(dw)
+        return r is not None and sum(1 for a, _, _, _ in self._pending if r[0] <= a < r[1]) < 4
 
     def slab(self, dw, split_k: int):
         key = (dw.data_ptr(), dw.numel())
@@ -178,14 +195,20 @@ class _SlabSink:
         return buf
 
     def add(self, dw, slab, nsplit: int):
-        off = (dw.data_ptr() - self.t.grad.data_ptr()) // dw.element_size()
-        self._pending.append((slab, int(nsplit), dw.numel(), int(off)))
+        self._pending.append((dw.data_ptr(), slab, int(nsplit), dw.numel()))
 
     def take(self, g):
-        """The pending slabs of gradient buffer ``g`` (cleared)."""
-        out, self._pending = self._pending, []
-        base = (self.t.grad.data_ptr() - g.data_ptr()) // 4
-        return [(s, n, p, o + base) for s, n, p, o in out]
+        """The pending slabs inside gradient range ``g`` (removed), offsets relative to ``g``."""
+        gp, ge = g.data_ptr(), g.data_ptr() + g.numel() * g.element_size()
+        out, keep = [], []
+        for e in self._pending:
+            a, slab, nsplit, numel = e
+            if gp <= a and a + 4 * numel <= ge:
+                out.append((slab, nsplit, numel, (a - gp) // 4))
+            else:
+                keep.append(e)
+        self._pending = keep
+        return out
 
 
 class DenseTable:
@@ -326,8 +349,10 @@ class DenseTable:
         out = self.params[g0: g0 + sz] if self.pull_dtype == torch.bfloat16 else None
         zeroed = False
         if self.optimizer == "adam":
+            sink = getattr(self, "_sink", None)  # (one rank: the bucket's split-K wgrad planes)
+            slabs = sink.take(gs) if sink is not None and local else ()
             ops.adam_apply(self.master[sl], self.m[sl], self.v[sl], gs, self.lr, self.betas[0], self.betas[1],
-                           self.eps, self.weight_decay, step, 1.0, out, step_dev=sd, zero_g=local)
+                           self.eps, self.weight_decay, step, 1.0, out, step_dev=sd, zero_g=local, slabs=slabs)
             zeroed = local  # the kernel cleared the gradient it read
         elif self.optimizer == "adagrad":
             ops.adagrad_apply(self.master[sl], self.m[sl], gs, self.lr, self.eps, 1.0, out)
@@ -479,9 +504,10 @@ class DenseTable:
         (ops.linear_wgrad(defer=...): no reduce kernel, no pass of the sum through the gradient
         buffer); None where the clock does not apply the whole gradient in one Adam kernel (several
         ranks, buckets, other optimizers) or MINIPS_WGRAD_DEFER=0."""
-        if (not _WGRAD_DEFER or self.comm.world != 1 or self.buckets is not None or self.optimizer != "adam"
-                or self.comm.device.type != "cuda" or self.pipe.async_):
-            # (an asynchronous clock may apply after the next step's GEMMs rewrote the planes)
+        if (not _WGRAD_DEFER or self.comm.world != 1 or self.optimizer != "adam" or self.comm.device.type != "cuda"
+                or (self.pipe.async_ and len(self._ring) < 2)):
+            # (an asynchronous clock applies after the next step's GEMMs ran: those write the next
+            # buffer of the gradient ring -- and its own planes -- which the ring's clock wait protects)
             return None
         sink = getattr(self, "_sink", None)
         if sink is None:

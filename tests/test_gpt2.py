@@ -54,6 +54,8 @@ def _check(dev):
     targets = torch.randint(0, 500, (2, 64), generator=g)
     ref_loss, ref_grad = _reference_loss_and_grads(m, tokens, targets)
     m.table.clock = lambda: None  # keep the gradient for inspection (no optimizer step)
+    # ... and keep every weight gradient in it: no split-K planes deferred to the (skipped) Adam
+    m.table.slab_sink = lambda: None
     loss = float(m.train_step(tokens.to(dev), targets.to(dev)))
     grad = m.table.grad[: m.layout.size].float().cpu()
     assert abs(loss - ref_loss) < 1e-2 * abs(ref_loss), (loss, ref_loss)
