@@ -150,10 +150,13 @@ class DLRM(LookaheadPlans):
         # sparse push lane while the weight-gradient GEMMs run on the compute stream
         dy = b["dH"]
         side = self._side
+        # split-K weight-gradient planes summed by the dense update (the Adam, or the one-sided push)
+        # instead of reduce kernels (up to 4 regions: the top MLP's, issued first)
+        sink = self.dense.slab_sink() if hasattr(self.dense, "slab_sink") else None
         for i in range(len(self.top) - 1, -1, -1):
             l = self.top[i]
             with side.fork():  # weight gradients beside the dgrad chain (per-layer buffers: no reuse)
-                l.wgrad(G, dy, ta[i])
+                l.wgrad(G, dy, ta[i], sink)
             if i > 0:
                 dx = b["tgrads"][i - 1]
                 l.dgrad(P, dy, dx, mask=ta[i])
@@ -168,7 +171,7 @@ class DLRM(LookaheadPlans):
         for i in range(len(self.bottom) - 1, -1, -1):
             l = self.bottom[i]
             with side.fork():
-                l.wgrad(G, dy, ba[i])
+                l.wgrad(G, dy, ba[i], sink)
             if i > 0:
                 dx = b["bgrads"][i - 1]
                 l.dgrad(P, dy, dx, mask=ba[i])
