@@ -74,10 +74,13 @@ class MLP:
         ops.softmax_xent(logits, self.cfg.classes, y, 1.0 / (B * self.comm.world), b["loss"], b["correct"])
         dy = logits  # in place: (softmax - onehot) / global batch, zero padding columns
         side = self._side
+        # split-K weight-gradient planes summed by the table's Adam (no reduce kernels; None for
+        # other optimizers / several ranks)
+        sink = self.table.slab_sink()
         for i in range(len(self.layers) - 1, -1, -1):
             l = self.layers[i]
             with side.fork():
-                l.wgrad(G, dy, acts[i])
+                l.wgrad(G, dy, acts[i], sink)
             if i > 0:
                 dx = b["grads"][i - 1]
                 l.dgrad(P, dy, dx, mask=acts[i])
