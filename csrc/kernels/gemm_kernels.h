@@ -1565,7 +1565,15 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
     const int64_t t128 = work * (int64_t)tiles;
     const double eff256 = (double)t256 / (double)(((t256 + 255) / 256) * 256);
     const double eff128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
-    const int pick = force_tile ? force_tile : ((wgrad && wgrad_mode == 3) || eff256 >= eff128 ? 256 : 128);
+    // MINIPS_WGRAD_TILE=256: split-K weight gradients (both operands K-major) on the 256x256 tile
+    // (ops.linear_wgrad then sizes its splits for that tile)
+    static const int wgrad_tile = [] {
+      const char* e = std::getenv("MINIPS_WGRAD_TILE");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int pick = force_tile ? force_tile
+                     : (wgrad && wgrad_tile) ? wgrad_tile
+                     : ((wgrad && wgrad_mode == 3) || eff256 >= eff128 ? 256 : 128);
     // v3 (experimental, MINIPS_GEMM_V3=1): measured within +-3 % of v2 on the forward shapes and
     // 10-25 % slower on the tr-read (dgrad/wgrad) shapes (tools/gpu_v3.sh), so v2 stays the default
     static const bool v3 = [] {

@@ -176,6 +176,8 @@ _WGRAD_MIN_ROWS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROW
 # add slab traffic; tools/gpu_ab.sh), so it stays off.
 _WGRAD_MIN_BLOCKS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_BLOCKS_OVERLAP", "0"))
 _overlap_state = __import__("threading").local()
+# MINIPS_WGRAD_TILE=256: the split-K weight gradients on 256x256 tiles (gemm_kernels.h reads it too)
+_WGRAD_TILE = int(__import__("os").environ.get("MINIPS_WGRAD_TILE", "0"))
 
 
 def overlap_mode(on: bool) -> bool:
@@ -194,7 +196,7 @@ def linear_wgrad(dy, x, dw, split_k=None, blocks=None, defer=None):
     M, N = dy.shape
     K = x.shape[1]
     if split_k is None:
-        t = 256 if _WGRAD_MODE == "v3" else 128
+        t = 256 if (_WGRAD_MODE == "v3" or _WGRAD_TILE == 256) else 128
         tiles = ((N + t - 1) // t) * ((K + t - 1) // t)
         # about one workgroup per CU (v3: 256x256 tiles, 1 WG/CU; v1/v2: ~512 128x128 blocks), but
         # a minimum number of reduction rows per split (profiles/r2/gpt2_wgrad_sweep.txt: shorter slices lose
