@@ -11,4 +11,4 @@ for i in 1 2; do
     echo "$cfg $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r4/bench_graph.log)"
   done
 done
-bash tools/r4_graph_trace.sh
+bash tools/gpu_runs/r4/r4_graph_trace.sh

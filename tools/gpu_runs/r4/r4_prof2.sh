@@ -3,5 +3,5 @@
 set -eo pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out/r4
-bash tools/r4_prof.sh
-bash tools/r4_markers.sh
+bash tools/gpu_runs/r4/r4_prof.sh
+bash tools/gpu_runs/r4/r4_markers.sh

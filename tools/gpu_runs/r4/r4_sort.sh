@@ -15,4 +15,4 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4/psort -o run -- python bench.py --steps 40 --warmup 10 > gpurun_out/r4/psort.log 2>&1
 python tools/prof_summary.py stats gpurun_out/r4/psort/run_kernel_stats.csv 50 --top 30 > gpurun_out/r4/psort_stats.txt
 grep -i "plan\|gemm_v2_kernel<256, 256, false, false" gpurun_out/r4/psort_stats.txt
-cd "$GRAFT_REPO_ROOT" && bash tools/r4_ln.sh
+cd "$GRAFT_REPO_ROOT" && bash tools/gpu_runs/r4/r4_ln.sh

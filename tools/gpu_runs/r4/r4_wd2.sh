@@ -18,7 +18,7 @@ for e in "MINIPS_PS_INBOX_MEM=2" "MINIPS_PS_INBOX_MEM=0" "MINIPS_PS_INBOX_MEM=1"
 done
 timeout -k 10 200 python tools/bench_models.py --model widedeep-ssp --steps 50 --warmup 10 > gpurun_out/r4/wd_coll.log 2>&1
 echo "collective ssp $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r4/wd_coll.log)"
-bash tools/r4_prof.sh
-bash tools/r4_markers.sh
+bash tools/gpu_runs/r4/r4_prof.sh
+bash tools/gpu_runs/r4/r4_markers.sh
 timeout -k 10 500 python tools/bench_models.py --model dlrm-10b --steps 30 --warmup 5 > gpurun_out/r4/dlrm10b_os.log 2>&1
 echo "dlrm-10b onesided: $(tail -1 gpurun_out/r4/dlrm10b_os.log)"
