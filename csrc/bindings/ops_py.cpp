@@ -577,7 +577,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
 // Returns (uniq, inv, counts [1], U_dev [1], members, memrow).
 std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& col_base, const at::Tensor& col_bits,
                                     std::vector<int64_t> col_bits_host, int64_t route_mult, int64_t route_n,
-                                    const at::Tensor& bounds, bool with_positions) {
+                                    const at::Tensor& bounds, bool with_positions, int64_t sort_mode) {
   check_gpu(bounds, "bounds");
   check_dtype(bounds, at::kLong, "bounds");
   const int64_t P = bounds.numel() - 1;
@@ -616,7 +616,7 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
                         ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
                         ptr<int64_t>(counts), stream_of(keys), with_positions ? pos.data_ptr<int32_t>() : nullptr,
                         rowstart.defined() ? rowstart.data_ptr<int32_t>() : nullptr,
-                        rowidx.defined() ? rowidx.data_ptr<int32_t>() : nullptr);
+                        rowidx.defined() ? rowidx.data_ptr<int32_t>() : nullptr, (int)sort_mode);
   // (members, memrow, positions or None, rowstart, rowidx or None) with one owner
   if (rowstart.defined())
     return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos, rowstart, rowidx};
@@ -1735,7 +1735,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("cu_masked_stream", &cu_masked_stream);
   m.def("plan_sorted", &plan_sorted, py::arg("keys"), py::arg("col_base"), py::arg("col_bits"),
         py::arg("col_bits_host"), py::arg("route_mult"), py::arg("route_n"), py::arg("bounds"),
-        py::arg("with_positions") = false);
+        py::arg("with_positions") = false, py::arg("sort_mode") = -1);
   m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none(),
         py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),

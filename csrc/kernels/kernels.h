@@ -185,7 +185,9 @@ void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const i
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
-                 int32_t* pos = nullptr, int32_t* rowstart = nullptr, int32_t* rowidx = nullptr);
+                 int32_t* pos = nullptr, int32_t* rowstart = nullptr, int32_t* rowidx = nullptr,
+                 int sort_mode = -1);
+// (sort_mode: 1 = one workgroup per column, 4 = the chunked sort, -1 = MINIPS_PLAN_SORT / default)
 // (pos, nullable: pos[members[m]] = m, emb_csr_positions fused; rowstart, nullable, one owner only:
 // rowstart[u] = first member of row u, rowstart[U] = B*F)
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.

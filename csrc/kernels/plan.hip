@@ -729,7 +729,7 @@ static int plan_reps(int bit) {
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
-                 int32_t* pos, int32_t* rowstart, int32_t* rowidx) {
+                 int32_t* pos, int32_t* rowstart, int32_t* rowidx, int sort_mode_arg) {
   if (rowstart && P > 1) throw std::runtime_error("plan_sorted: row starts are for one owner");
   if (rowidx && (P > 1 || !route_mult || route_n > (uint64_t)INT32_MAX))
     throw std::runtime_error("plan_sorted: per-lookup rows need one owner and routed keys below 2^31");
@@ -760,8 +760,9 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
     return e ? std::atoi(e) : 1;
   }();
   const int nch = (B + kPcChunk - 1) / kPcChunk;
+  const int mode = sort_mode_arg > 0 ? sort_mode_arg : sort_mode;
   for (int r = 0; r < plan_reps(2); ++r) {
-    if (sort_mode == 1 || nch == 1) {
+    if (mode == 1 || nch == 1) {
       hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u,
                          ukey, ucount);
     } else {

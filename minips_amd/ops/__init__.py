@@ -277,14 +277,16 @@ def bitmap_plan(keys: torch.Tensor, bounds: torch.Tensor, num_rows: int, route_m
 _PLAN_BITS_CAP = int(__import__("os").environ.get("MINIPS_PLAN_BITS_CAP", "0"))
 
 
-def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None, bounds=None, positions=False):
+def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None, bounds=None, positions=False,
+                sort_mode=-1):
     """Key planning of a [B, F] batch whose columns hold disjoint key ranges (column f's keys in
     [col_base[f], col_base[f] + 2**col_bits[f])): per-column radix sort, no global atomics
     (plan.hip). ``col_bits``: a list of ints (or one int for every column); ``bounds`` [P+1]: the
     owners' routed-key ranges (None: one owner). Returns (uniq [n] (first U valid, routed; column-
     major, ascending inside a column, then stably grouped by owner), inv [n], counts [P], U_dev [1],
     members [n] int32, memrow [n] int32) -- the unique_bucketize_n outputs plus the lookup CSR of
-    emb_build_csr (rows contiguous, in column-major key order)."""
+    emb_build_csr (rows contiguous, in column-major key order). ``sort_mode`` (GPU): 1 = one
+    workgroup per column, 4 = the chunked sort over F x 4 workgroups, -1 = MINIPS_PLAN_SORT / default."""
     if bounds is None:
         bounds = torch.tensor([0, (1 << 62)], dtype=torch.int64, device=keys.device)
     if _gpu(keys):
@@ -295,7 +297,8 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
         if bits_dev is None:  # (tables pass their cached device copy: no H2D copy per plan)
             bits_dev = torch.tensor(bits, dtype=torch.int32, device=keys.device)
         return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), bits_dev, bits,
-                                           int(route_mult), int(route_n), bounds.contiguous(), bool(positions)))
+                                           int(route_mult), int(route_n), bounds.contiguous(), bool(positions),
+                                           int(sort_mode)))
     B, F = keys.shape
     uniq_l, inv_l = [], []
     base = 0
