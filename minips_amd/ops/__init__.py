@@ -41,13 +41,17 @@ def _gpu(t: torch.Tensor) -> bool:
 
 
 # ----------------------------------------------------------------------------- GEMM
+_NO_STRIDES: list = []
+
+
 def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None, mask=None, colsum=None,
          alpha=1.0, split_k=1, perm=None, seg=0):
     """C[M,N] (op)= A.B.  A is [M][K] (a_km=False) or [K][M]; B is [N][K] (b_kn=False) or [K][N].
     EPI_PERM_ROWS_BF16: C is [M*N/seg, seg] and output (row, col) goes to row perm[row*N/seg + col//seg]."""
     if _gpu(A):
-        kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k),
-                       perm=perm, seg=int(seg))
+        # (all positional: pybind's keyword / default-argument path costs ~1 us per call)
+        kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k), 1, 1, 0, 0,
+                       0, _NO_STRIDES, perm, int(seg))
         return C
     a = (A[:K, :M].t() if a_km else A[:M, :K]).float()
     b = (B[:K, :N] if b_kn else B[:N, :K].t()).float()
@@ -123,14 +127,16 @@ def gemm_batched(A, B, C, M, N, K, a_km, b_kn, epi, batch, inner, lda, ldb, ldc,
     return C
 
 
+_FWD_EPI = {"relu": EPI_BIAS_RELU_BF16, "none": EPI_BIAS_BF16, "gelu": EPI_BIAS_GELU_BF16}
+
+
 def linear_fwd(x, w, bias=None, act="relu", out=None):
     """y = act(x w^T + b) in bf16 (x [M,K], w [N,K])."""
     M, K = x.shape[0], w.shape[1]
     N = w.shape[0]
     if out is None:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    epi = {"relu": EPI_BIAS_RELU_BF16, "none": EPI_BIAS_BF16, "gelu": EPI_BIAS_GELU_BF16}[act]
-    return gemm(x, w, out, M, N, K, False, False, epi, bias=bias)
+    return gemm(x, w, out, M, N, K, False, False, _FWD_EPI[act], bias=bias)
 
 
 def colsum_add(x, out):
