@@ -65,6 +65,7 @@ _SHARD_MEM = int(os.environ.get("MINIPS_PS_SHARD_MEM", "0"))
 # inbox memory kind (default 2 uncached: the owner's apply reads what peers wrote, never an L2
 # copy of the slot from `depth` clocks ago); MINIPS_PS_INBOX_MEM=0 is an A/B timing knob only
 _INBOX_MEM = int(os.environ.get("MINIPS_PS_INBOX_MEM", "2"))
+_PUSH_STREAM = os.environ.get("MINIPS_PS_PUSH_STREAM", "0") == "1"
 # MINIPS_PS_LOCKS=0: no owner locks (A/B timing only: reads may see half of a batch)
 _LOCKS = os.environ.get("MINIPS_PS_LOCKS", "1") != "0"
 
@@ -570,15 +571,38 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         if self.cuda:
             from .._native import kernels
 
-            if pending:
-                plan, g = pending[0]
-                kernels().ps_push_rows(plan.uniq, plan.extra["counts"], plan.U_dev, plan.cap, g.contiguous(),
-                                       self.inbox_ptrs, off, self.cap)
-            else:
-                kernels().ps_set_headers(self.inbox_ptrs, off, 0)
-        else:
-            self._push_cpu(pending[0] if pending else None, off)
+            # MINIPS_PS_PUSH_STREAM=1: the push (and the publish event behind it) on a stream of its
+            # own, after the compute stream's work so far; nothing later on the compute stream
+            # depends on it (reads are gated by the board), so the step's remaining backward runs
+            # beside the copy into the inboxes
+            pst = self._push_stream() if _PUSH_STREAM else None
+            if pst is not None:
+                ev = self._push_evs.next()
+                ev.record(streams.current(self.comm.device))
+                pst.wait_event(ev)
+            with streams.use(pst):
+                if pending:
+                    plan, g = pending[0]
+                    g = g.contiguous()
+                    kernels().ps_push_rows(plan.uniq, plan.extra["counts"], plan.U_dev, plan.cap, g,
+                                           self.inbox_ptrs, off, self.cap)
+                    if pst is not None:  # produced on the compute stream, read on the push stream
+                        for t in (g, plan.uniq, plan.extra["counts"], plan.U_dev):
+                            if isinstance(t, torch.Tensor) and t.is_cuda:
+                                t.record_stream(pst)
+                else:
+                    kernels().ps_set_headers(self.inbox_ptrs, off, 0)
+                self._advance()
+            return
+        self._push_cpu(pending[0] if pending else None, off)
         self._advance()
+
+    def _push_stream(self):
+        st = self.__dict__.get("_pst")
+        if st is None:
+            st = self._pst = self.comm.new_stream()
+            self._push_evs = streams.EventRing(8, fast=streams.FAST)
+        return st
 
     def _merge(self, pending):
         """Several Adds in one clock: one deduplicated batch (duplicates summed)."""

@@ -1,7 +1,18 @@
 #!/bin/bash
+# round-4 kernel tests; one-sided push stream A/B; GPT-2 tile A/B
 set -eo pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out/r4
 timeout -k 10 300 python -u -m pytest tests/test_round4_gpu.py tests/test_kernels_gpu.py -x -q -m gpu -k "round4 or plan or chunked or multi_copy or clock or push" --timeout 200 --timeout-method thread > gpurun_out/r4/new_tests.log 2>&1 || { tail -40 gpurun_out/r4/new_tests.log; exit 1; }
 tail -2 gpurun_out/r4/new_tests.log
-bash tools/gpu_runs/r4/r4_g2tile.sh
+MINIPS_PS_PUSH_STREAM=1 timeout -k 10 600 python -u -m pytest tests/test_onesided.py tests/test_onesided_consistency.py -x -q -m gpu --timeout 280 --timeout-method thread > gpurun_out/r4/pst_tests.log 2>&1 || { tail -40 gpurun_out/r4/pst_tests.log; exit 1; }
+tail -2 gpurun_out/r4/pst_tests.log
+for i in 1 2; do
+  for cfg in "MINIPS_PS_PUSH_STREAM=0" "MINIPS_PS_PUSH_STREAM=1"; do
+    env $cfg timeout -k 10 300 python tools/bench_models.py --model widedeep-ssp --transport onesided --steps 200 --warmup 20 > gpurun_out/r4/w.log 2>&1
+    echo "wd-ssp-os $cfg $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r4/w.log | tail -1)"
+    env $cfg timeout -k 10 400 python tools/bench_models.py --model dlrm-10b --steps 100 --warmup 20 > gpurun_out/r4/d.log 2>&1
+    echo "dlrm-10b $cfg $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r4/d.log | tail -1)"
+  done
+done
+timeout -k 10 200 python bench.py --steps 300 --warmup 20 > gpurun_out/r4/b.log 2>&1 && echo "bsp $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r4/b.log)"
