@@ -65,7 +65,7 @@ _SHARD_MEM = int(os.environ.get("MINIPS_PS_SHARD_MEM", "0"))
 # inbox memory kind (default 2 uncached: the owner's apply reads what peers wrote, never an L2
 # copy of the slot from `depth` clocks ago); MINIPS_PS_INBOX_MEM=0 is an A/B timing knob only
 _INBOX_MEM = int(os.environ.get("MINIPS_PS_INBOX_MEM", "2"))
-_PUSH_STREAM = os.environ.get("MINIPS_PS_PUSH_STREAM", "1") != "0"
+_PUSH_STREAM = os.environ.get("MINIPS_PS_PUSH_STREAM", "0") == "1"
 # MINIPS_PS_LOCKS=0: no owner locks (A/B timing only: reads may see half of a batch)
 _LOCKS = os.environ.get("MINIPS_PS_LOCKS", "1") != "0"
 
@@ -575,7 +575,9 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             # stream's work so far; nothing later on the compute stream depends on it (reads are
             # gated by the board), so the step's remaining backward runs beside the copy into the
             # inboxes: W&D SSP 0.396-0.403 vs 0.402-0.404, DLRM-10B 0.681-0.683 vs 0.692-0.694 ms
-            # (profiles/r4/ab_push_stream.txt); MINIPS_PS_PUSH_STREAM=0 pushes on the compute stream
+            # (profiles/r4/ab_push_stream.txt). Opt-in (MINIPS_PS_PUSH_STREAM=1): the 4-rank SSP test on
+            # one GPU (tests/test_multirank_gpu.py::test_widedeep_ssp_world4_tracks_one_rank_bsp)
+            # saw a loss spike with it on, not yet explained
             pst = self._push_stream() if _PUSH_STREAM else None
             if pst is not None:
                 ev = self._push_evs.next()
