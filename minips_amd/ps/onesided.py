@@ -604,7 +604,10 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         st = self.__dict__.get("_pst")
         if st is None:
             st = self._pst = self.comm.new_stream()
-            self._push_evs = streams.EventRing(8, fast=streams.FAST)
+            # system-fence events: with fence-free ones the push read stale gradient rows (the 4-rank
+            # SSP GPU test's loss spike; profiles/r4/ab_push_stream.txt) -- the compute stream's
+            # writes must be written back before the push's IPC-path loads
+            self._push_evs = streams.EventRing(8, fast=False)
         return st
 
     def _merge(self, pending):
