@@ -49,8 +49,8 @@ class LookaheadFeeder:
         if self.cuda:
             from ..utils.streams import EventRing
 
-            self._evring = EventRing(2 * self.depth + 4, fast=streams.FAST)
-            self._fence_ring = EventRing(4, fast=streams.FAST)
+            self._evring = EventRing(2 * self.depth + 4, fast=streams.FAST_PLAN)
+            self._fence_ring = EventRing(4, fast=streams.FAST_PLAN)
         self.queue = collections.deque(self._produce() for _ in range(self.depth))
         for (_, k, _), _ev in list(self.queue)[1:]:
             model.prefetch(k, keys_on_plan_stream=self.cuda)

@@ -513,7 +513,10 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             pp = self._start_plan(keys, csr, exchange=False)
             ring = self.__dict__.get("_plan_evs")
             if ring is None:
-                ring = self._plan_evs = streams.EventRing(16, fast=streams.FAST)
+                # (with the push stream the plan's keys / counts are read there, after a hand-off
+                # through the compute stream: those need the system-fence form, measured --
+                # profiles/r4/ab_push_stream.txt)
+                ring = self._plan_evs = streams.EventRing(16, fast=streams.FAST_PLAN and not _PUSH_STREAM)
             pp.event = ring.next()
             pp.event.record(ps)
         if not fenced:

@@ -927,7 +927,7 @@ class SparseTable:
             pp = self._start_plan(keys, csr, exchange=False)
             ring = self.__dict__.get("_plan_evs")
             if ring is None:  # (plans are consumed within a few steps of their issue)
-                ring = self._plan_evs = streams.EventRing(16, fast=streams.FAST)
+                ring = self._plan_evs = streams.EventRing(16, fast=streams.FAST_PLAN)
             pp.event = ring.next()
             pp.event.record(ps)
         if fenced and self.comm.world == 1 and not self.pipe.async_:

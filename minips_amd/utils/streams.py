@@ -13,8 +13,10 @@ import os
 
 import torch
 
-# MINIPS_FAST_EVENTS=0: the step's ordering events are plain torch events (A/B)
+# MINIPS_FAST_EVENTS=0: the step's ordering events are plain torch events (A/B);
+# MINIPS_FAST_PLAN_EVENTS=0: only the planning stream's hand-off events (diagnostics)
 FAST = os.environ.get("MINIPS_FAST_EVENTS", "1") != "0"
+FAST_PLAN = FAST and os.environ.get("MINIPS_FAST_PLAN_EVENTS", "1") != "0"
 
 _get = torch._C._cuda_getCurrentStream if hasattr(torch._C, "_cuda_getCurrentStream") else None
 _set = torch._C._cuda_setStream if hasattr(torch._C, "_cuda_setStream") else None
