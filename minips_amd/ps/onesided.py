@@ -580,7 +580,8 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             # inboxes: W&D SSP 0.396-0.403 vs 0.402-0.404, DLRM-10B 0.681-0.683 vs 0.692-0.694 ms
             # (profiles/r4/ab_push_stream.txt). Opt-in (MINIPS_PS_PUSH_STREAM=1): the 4-rank SSP test on
             # one GPU (tests/test_multirank_gpu.py::test_widedeep_ssp_world4_tracks_one_rank_bsp)
-            # saw a loss spike with it on, not yet explained
+            # saw a loss spike with it on unless the planning stream's hand-off events (feeder and
+            # plan) carry a system fence too (MINIPS_FAST_PLAN_EVENTS=0): use the two together
             pst = self._push_stream() if _PUSH_STREAM else None
             if pst is not None:
                 ev = self._push_evs.next()
