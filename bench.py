@@ -50,6 +50,15 @@ def main():
     ap.add_argument("--diag-steps", type=int, default=None,
                     help="after the timed run: N more steps with per-collective timing and the host-sync audit, "
                          "reported in the JSON line under 'diag' (default 10 with several ranks, else 0)")
+    ap.add_argument("--nccl-algo", default=None,
+                    help="RCCL algorithm selection passed through as NCCL_ALGO (e.g. Ring, Tree; "
+                         "tools/bench_kernels.py rccl measures the choices against the 7-link bound)")
+    ap.add_argument("--nccl-proto", default=None, help="RCCL protocol passed through as NCCL_PROTO (Simple, LL, LL128)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="one process emulates rank --emulate-rank of an N-rank job: tables sized and routed as "
+                         "that rank, every world > 1 code path, collectives replaced by loopback copies of the "
+                         "same bytes (ps.comm.LoopbackComm; wire time excluded). Reports per-rank throughput")
+    ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--sync-audit", type=int, default=0,
                     help="after the timed run: N more steps under minips_amd.utils.syncaudit (host issue time, "
                          "host syncs per step and their call sites; one '[sync-audit] {json}' line per rank, stderr)")
@@ -59,9 +68,19 @@ def main():
     from minips_amd.models.widedeep import WideDeep, WideDeepConfig
     from minips_amd.ps.comm import init_distributed
 
-    comm = init_distributed()
+    for k, v in (("NCCL_ALGO", args.nccl_algo), ("NCCL_PROTO", args.nccl_proto)):
+        if v:  # read by RCCL when the communicator is created
+            os.environ[k] = v
+    if args.emulate_world > 1:
+        from minips_amd.ps.comm import LoopbackComm
+
+        init_distributed()  # (one process: device selection only)
+        comm = LoopbackComm(args.emulate_world, args.emulate_rank)
+    else:
+        comm = init_distributed()
     n = comm.world
-    if n != args.gpus and comm.rank == 0:
+    emulated = comm.emulated
+    if n != args.gpus and comm.rank == 0 and not emulated:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {n}", file=sys.stderr)
     dev = comm.device
 
@@ -118,11 +137,11 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if n > 1:
+    if n > 1 and comm.initialized:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     loss_last = float(l.item()) / args.batch
-    samples = args.batch * n * args.steps
+    samples = args.batch * (1 if emulated else n) * args.steps
     value = samples / elapsed
     # diagnostics AFTER the timed region (the timed steps ran without any of this): bytes and
     # achieved GB/s per collective kind, host issue time and host syncs per step -- so a multi-GPU
@@ -147,22 +166,26 @@ def main():
                     host_issue_ms_per_step=rep["host_issue_ms_median"], host_syncs_per_step=rep["syncs_per_step"],
                     collectives=comm.timing_report(diag_steps))
         comm.timing = None
-        if n > 1:  # rank 0 reports the slowest rank's host issue time
+        if n > 1 and comm.initialized:  # rank 0 reports the slowest rank's host issue time
             hi = torch.tensor([rep["host_issue_ms_median"]], dtype=torch.float64, device=dev)
             dist.all_reduce(hi, op=dist.ReduceOp.MAX)
             diag["host_issue_ms_per_step_max_rank"] = round(float(hi.item()), 4)
-    if n == 1:
+    if emulated:
+        parallelism = (f"EMULATED rank {comm.rank} of ps-dp{n} ({args.consistency}; one process, loopback "
+                       "collectives: the per-rank program of an N-rank step, wire time excluded)")
+    elif n == 1:
         # one rank owns every shard: Get/Add/Clock are local gathers/applies, no collective runs
         parallelism = f"ps-dp1 ({args.consistency}; single rank: local shards, no collectives)"
     else:
         parallelism = (f"ps-dp{n} ({args.consistency}" + (f" s={args.staleness}" if args.consistency != "bsp" else "")
                        + f" over {comm.backend}: a2a sparse rows, RS/AG dense)")
-    if comm.rank == 0:
+    if comm.rank == 0 or emulated:
         out = {
-            "metric": METRIC,
+            "metric": METRIC if not emulated else
+            f"samples/sec of ONE emulated rank of a {n}-rank Wide&Deep BSP step (loopback collectives)",
             "value": round(value, 1),
             "unit": "samples/s",
-            "n_gpus": n,
+            "n_gpus": 1 if emulated else n,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
@@ -175,7 +198,7 @@ def main():
                 "model": ("PLUMBING TEST (small tables, not the benchmark) " if args.test_cards else "")
                 + "Wide&Deep: 26 sparse (33.76M rows, emb 32 + wide 1, row-wise Adagrad) + 13 dense; "
                 "deep MLP 848-1024-512-256-1 (Adam)",
-                "global_batch": args.batch * n,
+                "global_batch": args.batch * (1 if emulated else n),
                 "seq_len": None,
                 "parallelism": parallelism,
                 "per_gpu_batch": args.batch,
@@ -184,6 +207,8 @@ def main():
                 "world_size": comm.world,
                 "backend": comm.backend,
                 "bucket_mb": args.bucket_mb if n > 1 else None,
+                **({k.lower(): os.environ[k] for k in ("NCCL_ALGO", "NCCL_PROTO") if os.environ.get(k)}),
+                **({"emulated_world": n, "emulated_rank": comm.rank} if emulated else {}),
             },
             "loss_first": round(loss0, 5) if loss0 is not None else None,
             "loss_last": round(loss_last, 5),
@@ -226,7 +251,7 @@ def main():
               f"{issue[len(issue) // 2] * 1e3:.3f} ms, min {issue[0] * 1e3:.3f}, max {issue[-1] * 1e3:.3f}",
               file=sys.stderr, flush=True)
         pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(18)
-    if n > 1:
+    if n > 1 and comm.initialized:
         dist.barrier()
         dist.destroy_process_group()
 

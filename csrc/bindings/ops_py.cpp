@@ -330,6 +330,48 @@ void scatter_add_rows(const at::Tensor& src, const at::Tensor& idx, at::Tensor& 
                                     ptr<float>(acc), stream_of(src));
 }
 
+// slots [cap * P] int32 of the owned unique rows (see kernels.h owner_slots)
+at::Tensor owner_slots(const at::Tensor& own_inv, std::vector<int64_t> splits, int64_t cap) {
+  check_gpu(own_inv, "own_inv");
+  check_dtype(own_inv, at::kLong, "own_inv");
+  const int P = (int)splits.size();
+  TORCH_CHECK(P >= 1 && P <= minips_k::kOwnerMaxP, "owner_slots: 1..16 requesters");
+  minips_k::OwnerSegs segs{};
+  int64_t off = 0;
+  for (int p = 0; p < P; ++p) {
+    segs.off[p] = off;
+    off += splits[p];
+  }
+  segs.off[P] = off;
+  TORCH_CHECK(off == own_inv.numel(), "owner_slots: splits must sum to the received rows");
+  at::Tensor slots = at::empty({std::max<int64_t>(cap, 1) * P}, own_inv.options().dtype(at::kInt));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(own_inv.device());
+  minips_k::owner_slots(ptr<int64_t>(own_inv), own_inv.numel(), segs, P, slots.data_ptr<int>(),
+                        std::max<int64_t>(cap, 1), stream_of(own_inv));
+  return slots;
+}
+
+void owner_rows_adagrad(at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
+                        const at::Tensor& keys, int64_t n, const c10::optional<at::Tensor>& n_dev, int64_t base,
+                        const at::Tensor& recv, int64_t P, const at::Tensor& slots, double lr, double eps) {
+  TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.stride(1) == 1, "table must be a row-major GPU matrix");
+  check_dtype(table, at::kFloat, "table");
+  check_gpu(state, "state");
+  check_gpu(keys, "keys");
+  check_gpu(recv, "recv");
+  check_gpu(slots, "slots");
+  check_dtype(slots, at::kInt, "slots");
+  TORCH_CHECK(recv.scalar_type() == at::kFloat || recv.scalar_type() == at::kBFloat16, "recv: fp32 or bf16 rows");
+  TORCH_CHECK(recv.dim() == 2 && recv.is_contiguous() && recv.size(1) <= table.size(1), "recv [M, D] contiguous");
+  TORCH_CHECK(keys.numel() >= n && slots.numel() >= n * P, "keys / slots shorter than n");
+  float* s2 = opt_ptr<float>(state2, at::kFloat, "state2");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  minips_k::owner_rows_adagrad(ptr<float>(table), table.stride(0), ptr<float>(state), s2, (int)D1, ptr<int64_t>(keys),
+                               n, count_ptr(n_dev), base, (int)recv.size(1), recv.data_ptr(),
+                               recv.scalar_type() == at::kBFloat16, (int)P, slots.data_ptr<int>(), (float)lr,
+                               (float)eps, stream_of(table));
+}
+
 void sparse_rowwise_adagrad(at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
                             const at::Tensor& keys, int64_t base, const at::Tensor& grads, double lr, double eps,
                             const c10::optional<at::Tensor>& n_dev, bool zero_g) {
@@ -519,15 +561,15 @@ std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t 
 }
 
 void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, const at::Tensor& inv, int64_t F,
-                     int64_t D, at::Tensor& grad_rows, int64_t x_off, const c10::optional<at::Tensor>& U_dev,
-                     const c10::optional<at::Tensor>& members, const c10::optional<at::Tensor>& memrow,
-                     bool sorted_rows, bool zeroed) {
+                     int64_t D, at::Tensor& grad_rows, int64_t x_off, const c10::optional<at::Tensor>& members,
+                     const c10::optional<at::Tensor>& memrow, bool sorted_rows) {
   check_gpu(dX, "dX");
   const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
   check_gpu(inv, "inv");
   check_gpu(grad_rows, "grad_rows");
   TORCH_CHECK(dX.scalar_type() == at::kFloat || dX.scalar_type() == at::kBFloat16, "dX must be fp32 or bf16");
-  check_dtype(grad_rows, at::kFloat, "grad_rows");
+  const bool out_bf = grad_rows.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(out_bf || grad_rows.scalar_type() == at::kFloat, "grad_rows must be fp32 or bf16");
   TORCH_CHECK(dX.dim() == 2 && dX.stride(1) == 1, "dX must be a row-major matrix");
   if (sorted_rows) {  // dX [B*F, D] in the CSR's member order (kEpiPermRowsBf16 dgrad output)
     TORCH_CHECK(members.has_value() && members->defined() && x_off == 0 && dX.size(1) == D && dX.is_contiguous() &&
@@ -537,34 +579,30 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
   TORCH_CHECK(inv.numel() == B * F && (sorted_rows || dX.size(1) >= x_off + F * D) &&
                   grad_rows.size(1) >= D + (dw ? 1 : 0), "shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
-  static const bool tile_mode = [] {
-    const char* e = std::getenv("MINIPS_EMB_BWD");
-    return e && std::string(e) == "tile";
-  }();
-  if (!tile_mode && (D == 16 || D == 32 || D == 64) && grad_rows.size(0) < (1ll << 31) && B * F < (1ll << 31) &&
-      x_off % 4 == 0 && dX.stride(0) % 4 == 0) {
-    // segment-sum path: overwrites rows [0, U) of grad_rows
+  if ((D == 16 || D == 32 || D == 64) && grad_rows.size(0) < (1ll << 31) && B * F < (1ll << 31) && x_off % 4 == 0 &&
+      dX.stride(0) % 4 == 0) {
+    // segment-sum path: writes rows [0, U) of grad_rows exactly once (deterministic)
     const int64_t U = grad_rows.size(0);
     TORCH_CHECK(grad_rows.stride(1) == 1, "grad_rows must be row-major");
     const bool bf0 = dX.scalar_type() == at::kBFloat16;
     const void* base0 = bf0 ? (const void*)(ptr<bf16_t>(dX) + x_off) : (const void*)(ptr<float>(dX) + x_off);
+    at::Tensor part = at::empty({minips_k::emb_seg_part_floats(B * F, D)}, dX.options().dtype(at::kFloat));
     if (members.has_value() && members->defined()) {  // CSR prebuilt at planning time
       TORCH_CHECK(memrow.has_value() && members->numel() == B * F && memrow->numel() == B * F &&
                       members->scalar_type() == at::kInt && memrow->scalar_type() == at::kInt,
                   "members/memrow: int32 [B*F]");
       minips_k::emb_backward_csr(base0, bf0, (int)dX.stride(0), dw, B, (int)F, (int)D, members->data_ptr<int>(),
-                                 memrow->data_ptr<int>(), ptr<float>(grad_rows), (int)grad_rows.stride(0), (int)U,
-                                 stream_of(dX), count_ptr(U_dev), sorted_rows, zeroed);
+                                 memrow->data_ptr<int>(), grad_rows.data_ptr(), out_bf, (int)grad_rows.stride(0),
+                                 part.data_ptr<float>(), stream_of(dX), sorted_rows);
       return;
     }
     at::Tensor ws = at::empty({3 * U + 1 + 2 * B * F + U / 1024 + 1}, inv.options().dtype(at::kInt));
-    const bool bf = dX.scalar_type() == at::kBFloat16;
-    const void* base = bf ? (const void*)(ptr<bf16_t>(dX) + x_off) : (const void*)(ptr<float>(dX) + x_off);
-    minips_k::emb_backward_segment(base, bf, (int)dX.stride(0), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
-                                   ptr<float>(grad_rows), (int)grad_rows.stride(0), (int)U, ws.data_ptr<int>(),
-                                   stream_of(dX), count_ptr(U_dev));
+    minips_k::emb_backward_segment(base0, bf0, (int)dX.stride(0), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
+                                   grad_rows.data_ptr(), out_bf, (int)grad_rows.stride(0), (int)U, ws.data_ptr<int>(),
+                                   part.data_ptr<float>(), stream_of(dX));
     return;
   }
+  TORCH_CHECK(!out_bf, "bf16 gradient rows need the segment-sum path (D 16 / 32 / 64, 4-aligned strides)");
   if (dX.scalar_type() == at::kFloat)
     minips_k::wd_emb_backward(ptr<float>(dX) + x_off, (int)dX.stride(0), dw, ptr<int64_t>(inv), B, (int)F, (int)D,
                               ptr<float>(grad_rows), (int)grad_rows.size(1), stream_of(dX));
@@ -660,92 +698,6 @@ void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "colsum: x must be 16-byte aligned");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   minips_k::colsum_bf16(ptr<bf16_t>(x), x.size(0), (int)x.size(1), (int)x.stride(0), ptr<float>(out), stream_of(x));
-}
-
-// Embedding backward fused with the row-wise Adagrad apply (see kernels.h). members/memrow: the
-// plan's lookup CSR; uniq: the plan's unique keys (memrow indexes it); scr: zeroed scratch.
-// Row-parallel embedding backward + row-wise Adagrad (one rank, row-sorted bf16 gradient rows).
-void emb_rows_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, int64_t F, int64_t D,
-                      const at::Tensor& members, const at::Tensor& rowstart, const at::Tensor& U_dev,
-                      const at::Tensor& uniq, int64_t base, at::Tensor& table, at::Tensor& state,
-                      const c10::optional<at::Tensor>& state2, int64_t D1, double lr, double eps, at::Tensor& ws,
-                      at::Tensor& hot_acc, at::Tensor& hot_tick, int64_t hot, bool sorted_rows) {
-  TORCH_CHECK(dX.is_cuda(), "dX must be a GPU tensor");  // lookup order may be a column slice
-  check_dtype(dX, at::kBFloat16, "dX");
-  TORCH_CHECK(dX.dim() == 2 && dX.stride(1) == 1 && dX.stride(0) % 8 == 0, "dX: 2-D, 16-byte aligned rows");
-  if (sorted_rows) {
-    TORCH_CHECK(dX.size(1) == D && dX.stride(0) == D, "dX: [total, D] contiguous (member order)");
-  } else {
-    TORCH_CHECK(dX.size(1) >= F * D && dX.size(0) * F == members.numel(), "dX: [B, >= F*D] (lookup order)");
-  }
-  check_dtype(members, at::kInt, "members");
-  check_dtype(rowstart, at::kInt, "rowstart");
-  check_dtype(table, at::kFloat, "table");
-  check_dtype(state, at::kFloat, "state");
-  check_dtype(ws, at::kInt, "ws");
-  const int64_t U_max = rowstart.numel() - 1;
-  TORCH_CHECK(D == 16 || D == 32 || D == 64, "D in {16, 32, 64}");
-  TORCH_CHECK(hot >= 1, "hot >= 1");
-  TORCH_CHECK(ws.is_cuda() && ws.numel() >= minips_k::emb_rows_ws_ints(U_max, (int)hot, (int)D),
-              "ws: >= emb_rows_ws_ints(n, hot, D) ints");
-  check_dtype(hot_acc, at::kFloat, "hot_acc");
-  check_dtype(hot_tick, at::kInt, "hot_tick");
-  const int64_t hmax = minips_k::emb_rows_hot_rows(U_max, (int)hot, (int)D);
-  TORCH_CHECK(hot_acc.is_cuda() && hot_acc.numel() >= hmax * (D + 1) && hot_tick.is_cuda() && hot_tick.numel() >= hmax,
-              "hot_acc: >= emb_rows_hot_rows * (D + 1) floats, hot_tick: >= emb_rows_hot_rows ints (both zero)");
-  TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && table.size(1) % 4 == 0 && table.size(1) >= D + 1,
-              "table: [rows, W] fp32, W % 4 == 0, W > D");
-  const float* dw = nullptr;
-  if (dwide && dwide->defined()) {
-    check_dtype(*dwide, at::kFloat, "dwide");
-    dw = ptr<float>(*dwide);
-  }
-  float* st2 = (state2 && state2->defined()) ? ptr<float>(*state2) : nullptr;
-  c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
-  int* w = ws.data_ptr<int32_t>();
-  minips_k::emb_rows_adagrad(ptr<bf16_t>(dX), sorted_rows ? 0 : (int)dX.stride(0), dw, (int)F, (int)D,
-                             members.data_ptr<int32_t>(), rowstart.data_ptr<int32_t>(), ptr<int64_t>(U_dev), U_max,
-                             ptr<int64_t>(uniq), base, ptr<float>(table), (int)table.size(1), (int)table.size(1),
-                             ptr<float>(state), st2, (int)D1, (float)lr, (float)eps, w, ptr<float>(hot_acc),
-                             reinterpret_cast<unsigned*>(hot_tick.data_ptr<int32_t>()), (int)hot, stream_of(dX));
-}
-
-void emb_seg_adagrad(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, int64_t F, int64_t D,
-                     const at::Tensor& members, const at::Tensor& memrow, const at::Tensor& uniq, int64_t base,
-                     at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
-                     double lr, double eps, at::Tensor& scr) {
-  TORCH_CHECK(dX.is_cuda() && dX.dim() == 2 && dX.stride(1) == 1, "dX: row-major GPU matrix");
-  TORCH_CHECK(dX.scalar_type() == at::kFloat || dX.scalar_type() == at::kBFloat16, "dX must be fp32 or bf16");
-  const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
-  const int64_t B = dX.size(0);
-  TORCH_CHECK(D == 16 || D == 32 || D == 64, "D must be 16, 32 or 64");
-  TORCH_CHECK(dX.size(1) >= F * D && dX.stride(0) % 4 == 0, "dX shape / row stride");
-  for (auto* t : {&members, &memrow}) {
-    check_gpu(*t, "csr");
-    check_dtype(*t, at::kInt, "csr");
-    TORCH_CHECK(t->numel() == B * F, "members/memrow: int32 [B*F]");
-  }
-  check_gpu(uniq, "uniq");
-  check_dtype(uniq, at::kLong, "uniq");
-  check_gpu(table, "table");
-  check_dtype(table, at::kFloat, "table");
-  check_gpu(state, "state");
-  check_dtype(state, at::kFloat, "state");
-  check_gpu(scr, "scr");
-  check_dtype(scr, at::kFloat, "scr");
-  const int64_t W = table.size(1);
-  TORCH_CHECK(table.dim() == 2 && W % 4 == 0 && W >= D + (dw ? 1 : 0), "table: [rows, W], W % 4 == 0, W > D");
-  TORCH_CHECK(state.numel() == table.size(0), "state: one value per table row");
-  float* s2 = opt_ptr<float>(state2, at::kFloat, "state2");
-  TORCH_CHECK(D1 == W || (D1 == D && s2 && state2->numel() == table.size(0)), "split: D1 == W, or D1 == D with state2");
-  // memrow < U <= uniq.numel() <= scr rows; uniq holds this rank's routed keys (its shard = all rows)
-  TORCH_CHECK(uniq.numel() <= B * F && scr.dim() == 2 && scr.size(0) >= uniq.numel() && scr.size(1) >= D + 1 &&
-                  scr.size(1) % 4 == 0, "scr: [>= U, >= D+1] fp32, row stride % 4 == 0");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(dX.device());
-  minips_k::emb_seg_adagrad(dX.data_ptr(), dX.scalar_type() == at::kBFloat16, (int)dX.stride(0), dw, B, (int)F,
-                            (int)D, members.data_ptr<int>(), memrow.data_ptr<int>(), ptr<int64_t>(uniq), base,
-                            ptr<float>(table), (int)W, (int)W, ptr<float>(state), s2, (int)D1, (float)lr, (float)eps,
-                            ptr<float>(scr), (int)scr.size(1), stream_of(dX));
 }
 
 void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g, double lr, double beta1,
@@ -1721,16 +1673,13 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("labels"), py::arg("dH"), py::arg("dw4"), py::arg("dwide"), py::arg("loss_sum"), py::arg("grad_scale"),
         py::arg("dH_colsum") = py::none(), py::arg("bias") = py::none());
   m.def("wd_assemble_tab", &wd_assemble_tab);
+  m.def("owner_slots", &owner_slots, py::arg("own_inv"), py::arg("splits"), py::arg("cap"));
+  m.def("owner_rows_adagrad", &owner_rows_adagrad, py::arg("table"), py::arg("state"), py::arg("state2"),
+        py::arg("D1"), py::arg("keys"), py::arg("n"), py::arg("n_dev"), py::arg("base"), py::arg("recv"),
+        py::arg("P"), py::arg("slots"), py::arg("lr"), py::arg("eps"));
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
-        py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("U_dev") = py::none(),
-        py::arg("members") = py::none(), py::arg("memrow") = py::none(), py::arg("sorted_rows") = false,
-        py::arg("zeroed") = false);
-  m.def("emb_rows_ws_ints",
-        [](int64_t n, int64_t hot, int64_t D) { return minips_k::emb_rows_ws_ints(n, (int)hot, (int)D); });
-  m.def("emb_rows_hot_rows",
-        [](int64_t n, int64_t hot, int64_t D) { return minips_k::emb_rows_hot_rows(n, (int)hot, (int)D); });
-  m.def("emb_rows_adagrad", &emb_rows_adagrad);
-  m.def("emb_seg_adagrad", &emb_seg_adagrad);
+        py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("members") = py::none(),
+        py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("cu_masked_stream", &cu_masked_stream);
   m.def("plan_sorted", &plan_sorted, py::arg("keys"), py::arg("col_base"), py::arg("col_bits"),

@@ -970,6 +970,117 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
                         reinterpret_cast<unsigned*>(reinterpret_cast<float*>(&smem[0][0]) + NWAVES * kScrFloats));
 }
 
+// ================================================================ v6: 256x256, 4 waves of 128x128
+// The LDS-read bound of the 64x64-per-wave tiles: a wave reads 64 A + 64 B fragment rows per k for
+// 64x64 MACs, so a 16-wave 256x256 workgroup pulls 256 KiB of fragments out of LDS per 64-deep
+// K-step -- 2048 LDS cycles at 128 B/clk, the same as its 2048 MFMA cycles (SQ_WAIT_INST_LDS
+// dominates the LM-head profile, profiles/r4/pmc_lm_dgrad_v2_v5.txt). Here ONE wave per SIMD owns
+// a 128x128 block (8 x 8 MFMA 16x16x32 tiles, 256 fp32 accumulators: the AGPR half of the
+// 512-entry register file at one wave per SIMD), reading 128 + 128 fragment rows per k for 4x the
+// MACs: 128 KiB per K-step, half the MFMA time. Staging is v2's: BK = 64, two LDS-DMA stages of
+// 64 KiB (swizzled images, zero-filled tails), one counted vmcnt + barrier per stage; inside a
+// K-step the fragments of k-half 1 are read while k-half 0's 64 MFMAs run. XCD-contiguous tile
+// order as v2; staged epilogue (epilogue_lds, two 128x64 halves per wave).
+template <bool A_KM, bool B_KN, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_v6_kernel(
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, int M, int N, int K, int lda, int ldb, int k_chunk,
+    EpiArgs ep) {
+  constexpr bool PERM = A_KM && B_KN;
+  constexpr int TM = 256, TN = 256, NWAVES = 4;
+  constexpr int VM_STAGE = (TM / 8 + TN / 8) / NWAVES;  // DMA instructions per thread per stage (16)
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2][(TM + TN) * BK2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = (N + TN - 1) / TN, tiles_m = (M + TM - 1) / TM;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x, ks = blockIdx.z;
+  if (ep.zmap && gridDim.z > 1 && gridDim.y == 1) {
+    const int W = nwg * (int)gridDim.z, L = bid + nwg * ks;
+    const int xcd = L & 7, q = W >> 3, r = W & 7;
+    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+    ks = w / nwg;
+    bid = w - ks * nwg;
+  } else if (nwg >= 16) {
+    int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    bid = base + (bid >> 3);
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * TM, n0 = tn * TN;
+  {
+    const int z = blockIdx.y, zo = z / ep.inner, zi = z - zo * ep.inner;
+    A += zo * ep.sa_o + zi * ep.sa_i;
+    B += zo * ep.sb_o + zi * ep.sb_i;
+    const int64_t co = zo * ep.sc_o + zi * ep.sc_i + (int64_t)ks * ep.sc_split;
+    const bool f32 = EPI == kEpiStoreF32 || EPI == kEpiAtomicF32 || EPI == kEpiAccumF32 || EPI == kEpiFoldF32;
+    ep.C = f32 ? (void*)((float*)ep.C + co) : (void*)((bf16_t*)ep.C + co);
+  }
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7ffffff0, 0x00020000);
+  const int kb = ks * k_chunk;
+  const int ke = min(K, kb + k_chunk);
+  const int nt = ke > kb ? (ke - kb + BK2 - 1) / BK2 : 0;
+
+  v4f acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+    dma_tile<A_KM, TM, NWAVES>(ra, lda, m0, kb, M, ke, smem[0], wave, lane);
+    dma_tile<B_KN, TN, NWAVES>(rb, ldb, n0, kb, N, ke, smem[0] + TM * BK2, wave, lane);
+  }
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) {
+      const int k1 = kb + (t + 1) * BK2;
+      dma_tile<A_KM, TM, NWAVES>(ra, lda, m0, k1, M, ke, smem[cur ^ 1], wave, lane);
+      dma_tile<B_KN, TN, NWAVES>(rb, ldb, n0, k1, N, ke, smem[cur ^ 1] + TM * BK2, wave, lane);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_STAGE) : "memory");  // this stage retired, the next in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bf16_t* SA = smem[cur];
+    const bf16_t* SB = smem[cur] + TM * BK2;
+    v8s af[2][8], bfr[2][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[0][i] = frag2<A_KM, PERM, TM>(SA, wm * 128 + i * 16, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bfr[0][j] = frag2<B_KN, PERM, TN>(SB, wn * 128 + j * 16, 0, lane);
+#pragma unroll
+    for (int h = 0; h < BK2 / 32; ++h) {
+      if (h + 1 < BK2 / 32) {  // the next k-half's fragments while this half's MFMAs run
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[(h + 1) & 1][i] = frag2<A_KM, PERM, TM>(SA, wm * 128 + i * 16, h + 1, lane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bfr[(h + 1) & 1][j] = frag2<B_KN, PERM, TN>(SB, wn * 128 + j * 16, h + 1, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(v8bf, af[h & 1][i]), __builtin_bit_cast(v8bf, bfr[h & 1][j]), acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is refilled
+    asm volatile("" ::: "memory");
+  }
+  float* scr = reinterpret_cast<float*>(&smem[0][0]) + wave * kScrFloats;
+#pragma unroll
+  for (int jh = 0; jh < 2; ++jh) {
+    v4f half[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) half[i][j] = acc[i][4 * jh + j];
+    epilogue_lds<EPI, 8>(half, ep, M, N, m0 + wm * 128, n0 + wn * 128 + 64 * jh, lane, scr);
+  }
+}
+
 // ================================================================ v3: 256x256, 8 waves, phase-split K-step
 // 256x256 output tile, 8 waves as 2 (M) x 4 (N), each wave 128x64 = 8x4 MFMA 16x16 tiles (128
 // accumulator registers), BK = 64, operands staged by LDS-DMA (same swizzled images as v2) as
@@ -1586,7 +1697,12 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
     }();
     const bool use_v3 = EPI != kEpiFoldF32 && (v3 || (wgrad && wgrad_mode == 3));
     const int v4 = EPI == kEpiFoldF32 ? 0 : gemm_v4_mode();  // the fold tail lives in v2 only
-    if (EPI != kEpiWdHead && (v4 == 4 || (v4 == 3 && pick == 256))) {
+    if (EPI != kEpiWdHead && EPI != kEpiFoldF32 && (v4 == 6 || (v4 == 5 && pick == 256))) {
+      dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
+      EpiArgs e6 = ep;
+      e6.zmap = 1;
+      hipLaunchKernelGGL((gemm_v6_kernel<A_KM, B_KN, EPI>), grid, dim3(256), 0, s, A, B, M, N, K, lda, ldb, kc, e6);
+    } else if (EPI != kEpiWdHead && (v4 == 4 || (v4 == 3 && pick == 256))) {
       dim3 grid(((M + 255) / 256) * ((N + 255) / 256), batch, nsplit);
       hipLaunchKernelGGL((gemm_v5_kernel<A_KM, B_KN, EPI>), grid, dim3(512), 0, s, A, B, M, N, K, lda, ldb, kc, ep);
     } else if (v4 == 2 || (v4 == 1 && pick == 256)) {  // 2: v4 for every shape

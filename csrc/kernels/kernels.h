@@ -107,6 +107,20 @@ void gather_rows(const float* table, int64_t ld, const int64_t* keys, int64_t n,
 void lookup_rows(const bf16_t* rows, int row_stride, const int64_t* inv, int64_t B, int F, int D, bf16_t* out, int ldo,
                  hipStream_t s);
 // Scatter-add rows: acc[idx[i], :] += src[i, :] (fp32, float atomics, 2 rows per wave-instr).
+// Owner side of a multi-rank sparse push (sparse.hip): received rows are grouped by requester
+// (segment s = rows [off[s], off[s+1])); slots[u * P + s] = the received row of requester s for
+// owned unique row u (own_inv[i] = u), -1 when s did not push u (cap rows, memset first).
+constexpr int kOwnerMaxP = 16;
+struct OwnerSegs {
+  int64_t off[kOwnerMaxP + 1];
+};
+void owner_slots(const int64_t* own_inv, int64_t M, const OwnerSegs& segs, int P, int* slots, int64_t cap,
+                 hipStream_t s);
+// Row-wise Adagrad of owned rows keys[0, min(n, *n_dev)) with the gradient = the sum, in requester
+// order, of their received rows recv[slots[u * P + s]] (fp32 or bf16 [M, D]): one pass, no atomics.
+void owner_rows_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys, int64_t n,
+                        const int64_t* n_dev, int64_t base, int D, const void* recv, bool recv_bf16, int P,
+                        const int* slots, float lr, float eps, hipStream_t s);
 void scatter_add_rows(const float* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s);
 void scatter_add_rows_bf16(const bf16_t* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s);
 // Row-wise Adagrad on a shard (one accumulator per row, DLRM style):
@@ -153,14 +167,16 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
 // pre-zeroed).
 void wd_emb_backward(const float* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
                      float* grad_rows, int row_stride, hipStream_t s);
-// Segment-sum form of the embedding backward: grad_rows[u] = sum over lookups j with
-// inv[j] == u for every row u < U (zero-filled first, padding included); lookups are grouped
-// by row (count / scan / fill) and summed piecewise, float atomics only where a piece boundary
-// cuts a row. ws: (3U + 2 + 2*B*F + U/1024) int32 workspace. U_dev (nullable): the device-side
-// unique count (U is then its upper bound; only rows < *U_dev are zero-filled).
+// Segment-sum form of the embedding backward: out[u] = sum over lookups j with inv[j] == u for
+// every row u < U (columns [0, D) the lookups' dX values, column D the samples' dwide, [D+1,
+// row_stride) zero), written exactly once per row in a fixed summation order (deterministic, no
+// atomics, no zero-fill): lookups are grouped by row (count / scan / fill) and summed piecewise,
+// rows cut by piece boundaries finished by a second kernel over the pieces' partials. out: fp32
+// or bf16 (out_bf16) [U, row_stride]. ws: (3U + 2 + 2*B*F + U/1024) int32; part:
+// emb_seg_part_floats(B*F, D) floats.
 void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,
-                          int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s,
-                          const int64_t* U_dev = nullptr);
+                          int D, void* out, bool out_bf16, int row_stride, int U, int* ws, float* part, hipStream_t s);
+int64_t emb_seg_part_floats(int64_t total, int D);
 // The two halves of emb_backward_segment: the lookup CSR (depends on inv only; ws: counts[U] |
 // cursor[U] | offsets[U+1] | tiles[U/1024+1]; members/memrow [B*F]) and the segmented sum.
 // zeroed_cc (nullable): a pre-zeroed 2U-int block used for counts|cursor (ws then starts at offsets).
@@ -170,9 +186,8 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
 // members[m], written there by the dgrad GEMM's kEpiPermRowsBf16 epilogue): the segment sums read
 // it as one contiguous stream instead of gathering 2*D-byte pieces of [B, F*D] rows.
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
-                      const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                      const int64_t* U_dev = nullptr, bool sorted_rows = false, bool zeroed = false);
-// (zeroed: grad_rows rows [0, U) are already zero -- no clearing pass)
+                      const int* members, const int* memrow, void* out, bool out_bf16, int row_stride, float* part,
+                      hipStream_t s, bool sorted_rows = false);
 // pos[members[m]] = m (n entries): where each lookup's gradient row goes in member order.
 void emb_csr_positions(const int* members, int64_t n, int* pos, hipStream_t s);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,
@@ -192,25 +207,6 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
 // rowstart[u] = first member of row u, rowstart[U] = B*F)
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
 void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s);
-// Embedding backward + row-wise Adagrad of one rank, row-parallel over the lookups of each unique
-// row (rowstart [U + 1] from plan_sorted): rows with at most `hot` lookups are summed and applied by
-// one lane group each; hotter rows are cut into workgroup chunks (ws: emb_rows_ws_ints scratch
-// ints, zero at allocation; every call leaves its counters zero) whose partial sums meet in hot_acc
-// ([emb_rows_hot_rows][D + 1] fp32) / hot_tick (ints): both zero before and after every call.
-// ldx: 0 = dX row-sorted [total, D] (member order); > 0 = lookup order [B, ldx >= F*D].
-void emb_rows_adagrad(const bf16_t* dX, int ldx, const float* dwide, int F, int D, const int* members,
-                      const int* rowstart, const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base,
-                      float* table, int ld, int W, float* state, float* state2, int D1, float lr, float eps,
-                      int* ws, float* hot_acc, unsigned* hot_tick, int hot, hipStream_t s);
-int64_t emb_rows_ws_ints(int64_t n, int hot, int D);
-int64_t emb_rows_hot_rows(int64_t n, int hot, int D);
-// Embedding backward fused with the row-wise Adagrad apply (one rank, local shard): the rows of
-// uniq[memrow] get Adagrad with the segment sums of their lookups' dX rows (+ dwide at column D)
-// without a grad_rows buffer. scr: [U, scr_ld >= D+1] fp32, all zero before and after the call.
-void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
-                     const int* members, const int* memrow, const int64_t* uniq, int64_t base, float* table, int ld,
-                     int W, float* state, float* state2, int D1, float lr, float eps, float* scr, int scr_ld,
-                     hipStream_t s);
 
 // ------------------------------------------------------------------ optimizers (optim.hip)
 // Fused Adam(W) on an fp32 master shard; optionally writes the bf16 copy for all-gather.

@@ -541,6 +541,132 @@ void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ------------------------------------------------------------ owner side of a multi-rank push
+// At N > 1 each owner receives one deduplicated gradient row per (requester, key) -- a key is
+// pushed by at most P requesters -- and the owner-side dedupe (bitmap / hash planner) gives each
+// received row its owned unique index own_inv[i]. owner_slots records, per owned unique row u,
+// the received row of every requester s (slots[u * P + s], -1 = none); owner_rows_adagrad then
+// sums each row's <= P contributions in requester order and applies the row-wise Adagrad in the
+// same pass: no zeroed accumulator, no float atomics (the sum has one fixed order: deterministic),
+// no second read of a gradient buffer. Rows are balanced by construction (<= P members each).
+__global__ void owner_slots_kernel(const int64_t* __restrict__ own_inv, int64_t M, OwnerSegs segs, int P,
+                                   int* __restrict__ slots) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+    int seg = 0;
+    while (seg + 1 < P && i >= segs.off[seg + 1]) ++seg;
+    slots[own_inv[i] * P + seg] = (int)i;
+  }
+}
+
+void owner_slots(const int64_t* own_inv, int64_t M, const OwnerSegs& segs, int P, int* slots, int64_t cap,
+                 hipStream_t s) {
+  if (P < 1 || P > kOwnerMaxP) throw std::runtime_error("owner_slots: 1..16 requesters");
+  MINIPS_HIP_CHECK(hipMemsetAsync(slots, 0xff, sizeof(int) * (size_t)cap * P, s));
+  if (M <= 0) return;
+  hipLaunchKernelGGL(owner_slots_kernel, grid_for(M, 256, 4096), 256, 0, s, own_inv, M, segs, P, slots);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+__device__ __forceinline__ float4 ld_row4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld_row4(const bf16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+// 8 lanes per owned row (the v4 Adagrad layout: a float4 of columns [0, 32), a second of [32, D)
+// on the first (D - 32) / 4 lanes); lane l holds slot l (and l + 8) of the row.
+template <typename TG>
+__global__ __launch_bounds__(256) void owner_rows_adagrad_kernel(float* table, int64_t ld, float* state,
+                                                                 float* state2, int D1,
+                                                                 const int64_t* __restrict__ keys, int64_t n,
+                                                                 const int64_t* n_dev, int64_t base, int D,
+                                                                 const TG* __restrict__ recv, int P,
+                                                                 const int* __restrict__ slots, float lr, float eps) {
+  n = dev_count(n, n_dev);
+  const int lane = threadIdx.x & 63, sub = lane >> 3, l = lane & 7;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int c0 = 4 * l, c1 = 32 + 4 * l;
+  const bool has0 = c0 < D, has1 = c1 < D;
+  for (int64_t i0 = wave * 8; i0 < n; i0 += nwaves * 8) {
+    const int64_t i = i0 + sub;
+    const bool ok = i < n;
+    const int64_t row = ok ? keys[i] - base : 0;
+    const int sl0 = ok && l < P ? slots[i * P + l] : -1;
+    const int sl1 = ok && l + 8 < P ? slots[i * P + l + 8] : -1;
+    float* tr = table + row * ld;
+    float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0, g0 = t0, g1 = t0;
+    if (ok && has0) {
+      t0 = *reinterpret_cast<const float4*>(tr + c0);
+      if (has1) t1 = *reinterpret_cast<const float4*>(tr + c1);
+    }
+    const float st_old1 = ok ? state[row] : 0.f;
+    const float st_old2 = ok && D1 < D ? state2[row] : 0.f;
+#pragma unroll
+    for (int s = 0; s < kOwnerMaxP; ++s) {
+      if (s >= P) break;
+      const int m = __shfl(s < 8 ? sl0 : sl1, (sub << 3) + (s & 7), 64);
+      if (m >= 0 && has0) {
+        const float4 v = ld_row4(recv + (int64_t)m * D + c0);
+        g0.x += v.x; g0.y += v.y; g0.z += v.z; g0.w += v.w;
+        if (has1) {
+          const float4 w = ld_row4(recv + (int64_t)m * D + c1);
+          g1.x += w.x; g1.y += w.y; g1.z += w.z; g1.w += w.w;
+        }
+      }
+    }
+    float sq1 = 0.f, sq2 = 0.f;
+    const float a[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (q < 4 ? c0 : c1) + (q & 3);
+      const float sq = a[q] * a[q];
+      if (c < D1) sq1 += sq;
+      else sq2 += sq;
+    }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+      sq1 += __shfl_xor(sq1, o, 64);
+      sq2 += __shfl_xor(sq2, o, 64);
+    }
+    if (!ok) continue;
+    const float st1 = st_old1 + sq1 / (float)D1;
+    const float st2 = D1 < D ? st_old2 + sq2 / (float)(D - D1) : 0.f;
+    if (l == 0) {
+      state[row] = st1;
+      if (D1 < D) state2[row] = st2;
+    }
+    const float s1 = lr / (sqrtf(st1) + eps), s2 = lr / (sqrtf(st2) + eps);
+    float o[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (q < 4 ? c0 : c1) + (q & 3);
+      o[q] -= (c < D1 ? s1 : s2) * a[q];
+    }
+    if (has0) *reinterpret_cast<float4*>(tr + c0) = make_float4(o[0], o[1], o[2], o[3]);
+    if (has1) *reinterpret_cast<float4*>(tr + c1) = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
+void owner_rows_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys, int64_t n,
+                        const int64_t* n_dev, int64_t base, int D, const void* recv, bool recv_bf16, int P,
+                        const int* slots, float lr, float eps, hipStream_t s) {
+  if (n <= 0) return;
+  if (D1 <= 0 || D1 > D) D1 = D;
+  if (D1 < D && !state2) throw std::runtime_error("owner_rows_adagrad: split rows need state2");
+  if (!(D > 16 && D <= 64 && D % 4 == 0 && ld % 4 == 0 && P >= 1 && P <= kOwnerMaxP))
+    throw std::runtime_error("owner_rows_adagrad: rows of 16 < D <= 64 (D % 4 == 0), 1..16 requesters");
+  const int block = 256;
+  if (recv_bf16)
+    hipLaunchKernelGGL(owner_rows_adagrad_kernel<bf16_t>, grid_for(n * 8, block, 16384), block, 0, s, table, ld, state,
+                       state2, D1, keys, n, n_dev, base, D, static_cast<const bf16_t*>(recv), P, slots, lr, eps);
+  else
+    hipLaunchKernelGGL(owner_rows_adagrad_kernel<float>, grid_for(n * 8, block, 16384), block, 0, s, table, ld, state,
+                       state2, D1, keys, n, n_dev, base, D, static_cast<const float*>(recv), P, slots, lr, eps);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 __global__ void sparse_sgd_kernel(float* table, int64_t ld, const int64_t* __restrict__ keys, int64_t n, int64_t base,
                                   int D, const float* __restrict__ grads, float scale, const int64_t* n_dev) {
   const int64_t total = dev_count(n, n_dev) * D;

@@ -423,14 +423,16 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
 
 // out[c] += sum_r x[r, c] (x bf16 [M, N] row-major, ld; N % 8 == 0): the bias gradient of a
 // Linear from its output gradient. A block owns a 64-column strip and a chunk of rows; each
-// thread sums 8 columns (one 16-byte load per row) over every 32nd row of the chunk, the
-// block folds its 32 row-lanes in LDS and issues one atomic per column. Chunks are sized for
-// ~2 blocks per CU, so a column takes only M / rows_per_block same-address atomics (fp32
-// atomics from every XCD meet at the memory side: a per-wave atomic in a GEMM epilogue --
-// 256 per column -- cost the W&D dgrad 44 us).
+// thread sums 8 columns (one 16-byte load per row) over every 32nd row of the chunk, the block
+// folds its 32 row-lanes in LDS and writes its partial row; the LAST block of a strip (a ticket per
+// strip) adds the strip's partial rows in chunk order into out. One fixed summation order --
+// deterministic, unlike one same-address fp32 atomic per block and column -- and one writer per
+// column. Hand-offs in the write-through form of wd_head (cdna_hip_programming.md Guideline 16).
 __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restrict__ x, int64_t M, int N, int ld,
-                                                          int rows_per_block, float* __restrict__ out) {
+                                                          int rows_per_block, float* __restrict__ out,
+                                                          float* __restrict__ slab, unsigned* __restrict__ ticket) {
   __shared__ float red[32][65];
+  __shared__ int last;
   const int t = threadIdx.x, c8 = (t & 7) * 8, rl = t >> 3;
   const int col0 = blockIdx.x * 64 + c8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
@@ -450,13 +452,32 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restri
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[rl][c8 + e] = acc[e];
   __syncthreads();
+  const int nchunk = (int)gridDim.y;
+  float* strip = slab + (int64_t)blockIdx.x * nchunk * 64;
   if (t < 64) {
     float v = 0.f;
 #pragma unroll 8
     for (int i = 0; i < 32; ++i) v += red[i][t];
-    const int col = blockIdx.x * 64 + t;
-    if (col < N) atomicAdd(out + col, v);
+    __hip_atomic_store(strip + (int64_t)blockIdx.y * 64 + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const unsigned k = __hip_atomic_fetch_add(ticket + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = k == (unsigned)nchunk - 1;
+    if (last) {
+      __hip_atomic_store(ticket + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last || t >= 64) return;
+  const int col = blockIdx.x * 64 + t;
+  float tot = 0.f;
+  for (int i = 0; i < nchunk; ++i) tot += __hip_atomic_load(strip + (int64_t)i * 64 + t, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+  if (col < N) out[col] += tot;
 }
 
 void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s) {
@@ -465,7 +486,34 @@ void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStrea
   const int strips = (N + 63) / 64;
   const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(512 / strips, (M + 255) / 256));
   const int rpb = (int)((M + chunks - 1) / chunks);
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(strips, (unsigned)chunks), 256, 0, s, x, M, N, ld, rpb, out);
+  // the partial slab + strip tickets of this device, grown on demand (zero tickets; every call
+  // leaves them zero); allocated by the first eager call, before any graph capture
+  static thread_local std::vector<std::pair<int, std::pair<void*, size_t>>> ws_cache;
+  int dev = 0;
+  MINIPS_HIP_CHECK(hipGetDevice(&dev));
+  // [1024 strip tickets (4 KiB, a fixed place: every call's tickets stay zero between calls) | slab]
+  if (strips > 1024) throw std::runtime_error("colsum_bf16: N > 65536");
+  const size_t slab_bytes = sizeof(float) * (size_t)strips * chunks * 64, need = 4096 + slab_bytes;
+  std::pair<void*, size_t>* ws = nullptr;
+  for (auto& e : ws_cache)
+    if (e.first == dev) ws = &e.second;
+  if (!ws || ws->second < need) {
+    if (ws) {
+      MINIPS_HIP_CHECK(hipStreamSynchronize(s));
+      MINIPS_HIP_CHECK(hipFree(ws->first));
+    } else {
+      ws_cache.push_back({dev, {nullptr, 0}});
+      ws = &ws_cache.back().second;
+    }
+    const size_t cap = std::max<size_t>(need, sizeof(float) * 512 * 64 + 4096);
+    MINIPS_HIP_CHECK(hipMalloc(&ws->first, cap));
+    MINIPS_HIP_CHECK(hipMemset(ws->first, 0, cap));
+    ws->second = cap;
+  }
+  unsigned* ticket = static_cast<unsigned*>(ws->first);
+  float* slab = reinterpret_cast<float*>(static_cast<char*>(ws->first) + 4096);
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(strips, (unsigned)chunks), 256, 0, s, x, M, N, ld, rpb, out, slab,
+                     ticket);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
@@ -723,13 +771,6 @@ __global__ __launch_bounds__(kEmbTB) void emb_seg_fill_kernel(const int64_t* __r
   }
 }
 
-// Piecewise segmented sum over the row-sorted lookups: a wave owns a piece of 64/D x kSegG
-// consecutive members, each D-lane group a contiguous kSegG of them, read kSegBatch at a time
-// (independent loads in flight). A group flushes its running sum at every row change: a plain
-// store when the row lies entirely inside the group's range, an fp32 atomic otherwise (only
-// rows cut by a range boundary -- grad_rows is zero-filled first).
-constexpr int kSegG = 16, kSegBatch = 8;  // defaults; MINIPS_SEG_CFG picks other (G, batch) pairs
-
 // 4 consecutive gradient values of one lookup row segment.
 __device__ __forceinline__ float4 ld_grad4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float4 ld_grad4(const bf16_t* p) {
@@ -738,37 +779,6 @@ __device__ __forceinline__ float4 ld_grad4(const bf16_t* p) {
                      __uint_as_float(u.y & 0xffff0000u));
 }
 
-template <int D>
-__device__ __forceinline__ void seg_flush(float* __restrict__ grad_rows, int row_stride, int row, float4 acc,
-                                          float accw, bool wide, int prev_row, int next_row, int l) {
-  float* out = grad_rows + (int64_t)row * row_stride + 4 * l;
-  if (row != prev_row && row != next_row) {  // the whole row lies inside this group's range
-    if ((row_stride & 3) == 0)
-      *reinterpret_cast<float4*>(out) = acc;  // 16-byte rows: one vector store
-    else {
-      out[0] = acc.x;
-      out[1] = acc.y;
-      out[2] = acc.z;
-      out[3] = acc.w;
-    }
-    if (wide && l == 0) out[D] = accw;
-  } else {
-    atomicAdd(out + 0, acc.x);
-    atomicAdd(out + 1, acc.y);
-    atomicAdd(out + 2, acc.z);
-    atomicAdd(out + 3, acc.w);
-    if (wide && l == 0) atomicAdd(out + D, accw);
-  }
-}
-
-// Piecewise segmented sum over the row-sorted lookups. A group of D/VW lanes reads one lookup's
-// D values as VW-wide vectors (VW = 8: one 16-byte load of 8 bf16 per lane, 64/(D/8) lookups per
-// wave-instruction; VW = 4: 8-byte loads); each group owns kSegG consecutive lookups, loaded
-// kSegBatch at a time (independent loads in flight), and flushes its running sum at every row
-// change: a plain store when the row lies entirely inside the group's range, fp32 atomics when
-// the row continues across the range boundary (grad_rows is zero-filled first).
-// SORTED: dX holds the lookups' gradient rows in member order ([total, D], row m = lookup
-// members[m]): the loads become one contiguous stream and members is read only for dwide.
 template <int VW>
 __device__ __forceinline__ void ld_gradv(const bf16_t* p, float (&v)[VW]) {
   if constexpr (VW == 8) {
@@ -793,45 +803,93 @@ __device__ __forceinline__ void ld_gradv(const float* p, float (&v)[VW]) {
   }
 }
 
-template <int D, int VW>
-__device__ __forceinline__ void seg_flushv(float* __restrict__ grad_rows, int row_stride, int row,
-                                           const float (&acc)[VW], float accw, bool wide, int prev_row, int next_row,
-                                           int l) {
+// Deterministic piecewise segmented sum over the row-sorted lookups (no atomics: two identical
+// runs produce bit-identical rows -- the reference BSP applies each superstep's buffered Adds in
+// one fixed order, server/consistency/bsp_model.cpp:14-32). A group of L = D/VW lanes reads one
+// lookup's D values as VW-wide vectors; each group owns G consecutive lookups (loaded BATCH at a
+// time, independent loads in flight) and a wave the PER = 64/L consecutive groups of a "piece".
+//   * a row entirely inside one group is summed in registers and stored once;
+//   * a row cut by group boundaries inside the piece is completed by an in-wave carry chain: the
+//     groups hand their boundary partials to the next group in group order (shuffles), and the
+//     group where the row ends stores it;
+//   * a row cut by a piece boundary leaves its piece partials in `part` (HEAD: the piece's part of
+//     a row that started in an earlier piece, TAIL: the part of the row the piece ends inside), and
+//     emb_seg_fix_kernel sums them in piece order -- a Zipf-hot row spanning many pieces costs one
+//     partial per piece, not one per lookup.
+// Every row [0, U) is written exactly once, wide column and the pad columns [D+1, row_stride) too:
+// no zero-fill pass. Output fp32 (the local apply) or bf16 (the push payload at N > 1).
+// SORTED: dX holds the lookups' gradient rows in member order ([total, D], row m = lookup members[m]).
+template <int VW>
+__device__ __forceinline__ void st_row_vals(float* p, const float (&v)[VW]) {
 #pragma unroll
-  for (int h = 0; h < VW / 4; ++h)  // the wide weight goes out with chunk 0 only
-    seg_flush<D>(grad_rows, row_stride, row, make_float4(acc[4 * h], acc[4 * h + 1], acc[4 * h + 2], acc[4 * h + 3]),
-                 accw, wide && h == 0, prev_row, next_row, (VW / 4) * l + h);
+  for (int h = 0; h < VW / 4; ++h)
+    reinterpret_cast<float4*>(p)[h] = make_float4(v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]);
+}
+template <int VW>
+__device__ __forceinline__ void st_row_vals(bf16_t* p, const float (&v)[VW]) {
+#pragma unroll
+  for (int h = 0; h < VW / 4; ++h)
+    reinterpret_cast<uint2*>(p)[h] = make_uint2(pack_bf2(v[4 * h], v[4 * h + 1]), pack_bf2(v[4 * h + 2], v[4 * h + 3]));
+}
+__device__ __forceinline__ void st_scalar(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st_scalar(bf16_t* p, float v) { *p = f2bf(v); }
+
+// lane l of a row's group stores its VW values; lane 0 also the wide column D and zero pads
+template <typename TO, int D, int VW>
+__device__ __forceinline__ void seg_store_row(TO* __restrict__ out, int row_stride, int row, const float (&acc)[VW],
+                                              float accw, bool wide, int l) {
+  TO* o = out + (int64_t)row * row_stride;
+  if ((row_stride & 3) == 0) {
+    st_row_vals<VW>(o + VW * l, acc);
+  } else {  // (rows not 16-byte aligned: scalar stores)
+#pragma unroll
+    for (int e = 0; e < VW; ++e) st_scalar(o + VW * l + e, acc[e]);
+  }
+  if (l == 0)
+    for (int c = D; c < row_stride; ++c) st_scalar(o + c, (c == D && wide) ? accw : 0.f);
 }
 
-template <typename TX, int D, int kSegG, int kSegBatch, bool SORTED, int VW>
-__global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__ dX, int ldx,
+constexpr int seg_part_stride(int D) { return D + 4; }
+
+template <int D, int VW>
+__device__ __forceinline__ void seg_store_part(float* __restrict__ part, int64_t slot, const float (&acc)[VW],
+                                               float accw, int l) {
+  float* o = part + slot * seg_part_stride(D);
+  st_row_vals<VW>(o + VW * l, acc);
+  if (l == 0) o[D] = accw;
+}
+
+template <typename TX, typename TO, int D, int G, int BATCH, bool SORTED, int VW>
+__global__ __launch_bounds__(256) void emb_seg_det_kernel(const TX* __restrict__ dX, int ldx,
                                                           const float* __restrict__ dwide, int F,
                                                           const int* __restrict__ members,
                                                           const int* __restrict__ memrow, int total,
-                                                          float* __restrict__ grad_rows, int row_stride,
-                                                          int diag) {
-  constexpr int L = D / VW, PER = 64 / L;
+                                                          TO* __restrict__ out, int row_stride,
+                                                          float* __restrict__ part) {
+  constexpr int L = D / VW, PER = 64 / L, PW = PER * G;
   const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
   const bool wide = dwide != nullptr;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t piece = wave; piece * (PER * kSegG) < total; piece += nw) {
-    const int a = (int)(piece * (PER * kSegG)) + sub * kSegG;
-    const int b = min(total, a + kSegG);
-    // diag (MINIPS_SEG_DIAG=1, timing only, wrong sums): every flush is a plain store
-    const int prev_row = diag ? -2 : ((a > 0 && a <= total) ? memrow[a - 1] : -1);
-    const int next_row = diag ? -2 : (b < total ? memrow[b] : -1);
-    int cur = -1;
-    float acc[VW];
+  for (int64_t piece = wave; piece * PW < total; piece += nw) {
+    const int wbase = (int)(piece * PW);
+    const int a = wbase + sub * G, b = min(total, a + G);
+    const bool has = a < b;
+    const int prev_row = (has && a > 0) ? memrow[a - 1] : -1;
+    const int next_row = (has && b < total) ? memrow[b] : -1;
+    const int wave_prev = wbase > 0 ? memrow[wbase - 1] : -1;
+    int cur = -1, rf = -1, rl = -1;
+    bool first = true, hasF = false, interior = false, hasL = false;
+    float acc[VW], fv[VW], lv[VW];
 #pragma unroll
-    for (int e = 0; e < VW; ++e) acc[e] = 0.f;
-    float accw = 0.f;
-    for (int m0 = a; m0 < b; m0 += kSegBatch) {
-      int u[kSegBatch], bb[kSegBatch];
-      float v[kSegBatch][VW];
-      float vw[kSegBatch];
+    for (int e = 0; e < VW; ++e) acc[e] = fv[e] = lv[e] = 0.f;
+    float accw = 0.f, fw = 0.f, lw = 0.f;
+    for (int m0 = a; m0 < b; m0 += BATCH) {
+      int u[BATCH], bb[BATCH];
+      float v[BATCH][VW];
+      float vw[BATCH];
 #pragma unroll
-      for (int q = 0; q < kSegBatch; ++q) {
+      for (int q = 0; q < BATCH; ++q) {
         const int m = m0 + q;
         u[q] = m < b ? memrow[m] : -1;
         const TX* src;
@@ -839,7 +897,7 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
           src = dX + (int64_t)(m < b ? m : a) * D + VW * l;
           bb[q] = (wide && l == 0 && m < b) ? members[m] / F : 0;
         } else {
-          const int j = m < b ? members[m] : 0;
+          const int j = m < b ? members[m] : members[a];
           bb[q] = j / F;
           const int ff = j - bb[q] * F;
           src = dX + (int64_t)bb[q] * ldx + ff * D + VW * l;
@@ -848,10 +906,21 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
         vw[q] = (wide && l == 0 && m < b) ? dwide[bb[q]] : 0.f;
       }
 #pragma unroll
-      for (int q = 0; q < kSegBatch; ++q) {
+      for (int q = 0; q < BATCH; ++q) {
         if (u[q] < 0) break;
         if (u[q] != cur) {
-          if (cur >= 0) seg_flushv<D, VW>(grad_rows, row_stride, cur, acc, accw, wide, prev_row, next_row, l);
+          if (cur >= 0) {  // a finished row that is not the group's last
+            if (first && cur == prev_row) {  // it came from the previous group
+#pragma unroll
+              for (int e = 0; e < VW; ++e) fv[e] = acc[e];
+              fw = accw;
+              hasF = true;
+              rf = cur;
+            } else {
+              seg_store_row<TO, D, VW>(out, row_stride, cur, acc, accw, wide, l);
+            }
+            first = false;
+          }
           cur = u[q];
 #pragma unroll
           for (int e = 0; e < VW; ++e) acc[e] = 0.f;
@@ -862,31 +931,103 @@ __global__ __launch_bounds__(256) void emb_seg_sum_kernel(const TX* __restrict__
         accw += vw[q];
       }
     }
-    // A Zipf-hot row covers whole waves: combine the groups' partials in registers first, so a
-    // hot row takes one atomic per wave instead of one per group (same-address atomics serialise
-    // at the memory side).
-    const int c0 = __shfl(cur, 0, 64);
-    if (!diag && __all(cur == c0) && c0 >= 0) {
+    if (cur >= 0) {  // the group's last row
+      if (first && cur == prev_row) {
 #pragma unroll
-      for (int o = L; o < 64; o <<= 1) {
+        for (int e = 0; e < VW; ++e) fv[e] = acc[e];
+        fw = accw;
+        hasF = true;
+        rf = cur;
+        interior = cur == next_row;  // the whole group is one row that also continues
+      } else if (cur == next_row) {
 #pragma unroll
-        for (int e = 0; e < VW; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
-        accw += __shfl_xor(accw, o, 64);
+        for (int e = 0; e < VW; ++e) lv[e] = acc[e];
+        lw = accw;
+        hasL = true;
+        rl = cur;
+      } else {
+        seg_store_row<TO, D, VW>(out, row_stride, cur, acc, accw, wide, l);
       }
-      const int p0 = __shfl(prev_row, 0, 64), n1 = __shfl(next_row, 63, 64);
-      if (sub == 0) seg_flushv<D, VW>(grad_rows, row_stride, c0, acc, accw, wide, p0, n1, l);
-    } else if (cur >= 0) {
-      seg_flushv<D, VW>(grad_rows, row_stride, cur, acc, accw, wide, prev_row, next_row, l);
     }
+    // in-wave carry chain, in group order: group s receives group s-1's carry (the partial of the
+    // row that continues into s) and completes or extends it
+    float cv[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) cv[e] = 0.f;
+    float cw = 0.f;
+    int crow = -1;
+    const int src = (lane - L) & 63;
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+      float iv[VW];
+#pragma unroll
+      for (int e = 0; e < VW; ++e) iv[e] = __shfl(cv[e], src, 64);
+      const float iw = __shfl(cw, src, 64);
+      const int irow = __shfl(crow, src, 64);
+      if (sub == s) {
+        const bool carried = s > 0 && irow >= 0 && irow == rf;
+        if (hasF) {
+          float tv[VW];
+#pragma unroll
+          for (int e = 0; e < VW; ++e) tv[e] = carried ? iv[e] + fv[e] : fv[e];
+          const float tw = carried ? iw + fw : fw;
+          if (interior) {
+#pragma unroll
+            for (int e = 0; e < VW; ++e) cv[e] = tv[e];
+            cw = tw;
+            crow = rf;
+          } else {
+            if (wbase > 0 && rf == wave_prev) seg_store_part<D, VW>(part, 2 * piece, tv, tw, l);  // HEAD
+            else seg_store_row<TO, D, VW>(out, row_stride, rf, tv, tw, wide, l);
+#pragma unroll
+            for (int e = 0; e < VW; ++e) cv[e] = lv[e];
+            cw = lw;
+            crow = hasL ? rl : -1;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < VW; ++e) cv[e] = lv[e];
+          cw = lw;
+          crow = hasL ? rl : -1;
+        }
+      }
+    }
+    if (sub == PER - 1 && crow >= 0) seg_store_part<D, VW>(part, 2 * piece + 1, cv, cw, l);  // TAIL
   }
 }
 
-// Zero rows [0, min(U, *U_dev)) of an fp32 [*, stride] matrix (float4 stores; stride % 4 == 0).
-__global__ void zero_rows_dev_kernel(float* __restrict__ rows, int stride, int64_t U,
-                                     const int64_t* __restrict__ U_dev) {
-  const int64_t n = min(U, *U_dev) * (stride >> 2);
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
-    reinterpret_cast<float4*>(rows)[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+// Rows cut by piece boundaries: one L-lane group per piece whose last row starts inside it and
+// continues; it adds TAIL of its own piece, TAIL of every piece the row covers whole, and HEAD of
+// the piece where the row ends -- in piece order.
+template <typename TO, int D, int VW, int PW>
+__global__ __launch_bounds__(256) void emb_seg_fix_kernel(const int* __restrict__ memrow, int total,
+                                                          const float* __restrict__ part, TO* __restrict__ out,
+                                                          int row_stride, bool wide) {
+  constexpr int L = D / VW, SP = seg_part_stride(D);
+  const int64_t gid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / L;
+  const int l = threadIdx.x % L;
+  const int64_t npieces = ((int64_t)total + PW - 1) / PW;
+  if (gid >= npieces) return;
+  const int bw = (int)(gid * PW), ew = (int)min((int64_t)total, (gid + 1) * PW);
+  const int r = memrow[ew - 1];
+  if (!(ew < total && memrow[ew] == r)) return;              // ends inside this piece: done there
+  if (bw > 0 && memrow[bw] == r && memrow[bw - 1] == r) return;  // started in an earlier piece
+  float s[VW];
+  const float* t = part + (2 * gid + 1) * SP;
+  ld_gradv<VW>(t + VW * l, s);
+  float sw = t[D];
+  for (int64_t q = gid + 1;; ++q) {
+    const int eq = (int)min((int64_t)total, (q + 1) * PW);
+    const bool through = eq < total && memrow[eq] == r;
+    const float* p = part + (2 * q + (through ? 1 : 0)) * SP;
+    float v[VW];
+    ld_gradv<VW>(p + VW * l, v);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) s[e] += v[e];
+    sw += p[D];
+    if (!through) break;
+  }
+  seg_store_row<TO, D, VW>(out, row_stride, r, s, sw, wide, l);
 }
 
 // CSR of the lookups grouped by unique row (depends on `inv` only, so the PS builds it at
@@ -914,684 +1055,67 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
-template <typename TX>
-static void emb_seg_sum(const TX* dX, int ldx, const float* dwide, int64_t B, int F, int D, const int* members,
-                        const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                        const int64_t* U_dev, bool sorted_rows = false, bool zeroed = false) {
+constexpr int kSegG = 16, kSegBatch = 8, kSegVW = 4;
+
+constexpr int seg_per_piece(int D) { return (64 / (D / kSegVW)) * kSegG; }
+
+int64_t emb_seg_part_floats(int64_t total, int D) {
+  const int64_t pw = seg_per_piece(D);
+  return 2 * ((total + pw - 1) / pw) * seg_part_stride(D);
+}
+
+template <typename TX, typename TO>
+static void emb_seg_det(const TX* dX, int ldx, const float* dwide, int64_t B, int F, int D, const int* members,
+                        const int* memrow, TO* out, int row_stride, float* part, hipStream_t s, bool sorted_rows) {
   const int total = (int)(B * F);
-  if (zeroed) {
-    // the buffer's rows are zero already (the previous apply cleared them after reading)
-  } else if (U_dev && row_stride % 4 == 0)
-    hipLaunchKernelGGL(zero_rows_dev_kernel, grid_for((int64_t)U * (row_stride / 4), 256, 4096), 256, 0, s, grad_rows,
-                       row_stride, (int64_t)U, U_dev);
-  else
-    MINIPS_HIP_CHECK(hipMemsetAsync(grad_rows, 0, sizeof(float) * (size_t)U * row_stride, s));
-  static const int cfg = [] {
-    const char* e = std::getenv("MINIPS_SEG_CFG");
-    return e ? std::atoi(e) : 0;
-  }();
-  static const int diag = [] {
-    const char* e = std::getenv("MINIPS_SEG_DIAG");
-    return e ? std::atoi(e) : 0;
-  }();
-  // cfg 0: G=16 lookups per group loaded 8 at a time; 1: G=16 in one batch of 16; 2: G=8 x 8;
-  // 3: G=32 x 16
-  const int G = cfg == 2 ? 8 : cfg == 3 ? 32 : 16;
-  // MINIPS_SEG_VEC=8: 16-byte gradient loads (8 values per lane; 16-byte aligned rows only).
-  // Measured slower in the W&D step (0.436 vs 0.417 ms, profiles/r3/ab_seg_vec.txt): fewer lanes
-  // per row halves the waves in flight on the latency-bound segment walk, so 8-byte loads stay
-  // the default.
-  static const int vec_env = [] {
-    const char* e = std::getenv("MINIPS_SEG_VEC");
-    return e ? std::atoi(e) : 4;
-  }();
-  const bool vec8 = vec_env == 8 && (sorted_rows ? true : (ldx % 8 == 0)) &&
-                    reinterpret_cast<uintptr_t>(dX) % 16 == 0;
-  const int VWn = vec8 ? 8 : 4;
-  const int per_wave = (64 / (D / VWn)) * G;  // lookups per wave piece
-  const int pieces = (total + per_wave - 1) / per_wave;
-  const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
-#define MINIPS_SEG_LAUNCH3(DD, GG, BB, VV)                                                                           \
-  if (sorted_rows)                                                                                                  \
-    hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB, true, VV>), blocks, 256, 0, s, dX, ldx, dwide, F,        \
-                       members, memrow, total, grad_rows, row_stride, diag);                                        \
-  else                                                                                                              \
-    hipLaunchKernelGGL((emb_seg_sum_kernel<TX, DD, GG, BB, false, VV>), blocks, 256, 0, s, dX, ldx, dwide, F,       \
-                       members, memrow, total, grad_rows, row_stride, diag);
-#define MINIPS_SEG_LAUNCH2(DD, GG, BB)       \
-  if (vec8) {                               \
-    MINIPS_SEG_LAUNCH3(DD, GG, BB, 8)       \
-  } else {                                  \
-    MINIPS_SEG_LAUNCH3(DD, GG, BB, 4)       \
-  }
-#define MINIPS_SEG_LAUNCH(DD)                  \
-  if (cfg == 1) {                              \
-    MINIPS_SEG_LAUNCH2(DD, 16, 16)             \
-  } else if (cfg == 2) {                       \
-    MINIPS_SEG_LAUNCH2(DD, 8, 8)               \
-  } else if (cfg == 3) {                       \
-    MINIPS_SEG_LAUNCH2(DD, 32, 16)             \
-  } else {                                     \
-    MINIPS_SEG_LAUNCH2(DD, kSegG, kSegBatch)   \
-  }
+  const int64_t pw = seg_per_piece(D);
+  const int64_t pieces = (total + pw - 1) / pw;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((pieces + 3) / 4, 65535));
+  const int fix_blocks = (int)std::max<int64_t>(1, (pieces * (D / kSegVW) + 255) / 256);
+#define MINIPS_SEG_DET(DD)                                                                                         \
+  if (sorted_rows)                                                                                                \
+    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, true, kSegVW>), blocks, 256, 0, s, dX,    \
+                       ldx, dwide, F, members, memrow, total, out, row_stride, part);                             \
+  else                                                                                                            \
+    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, false, kSegVW>), blocks, 256, 0, s, dX,   \
+                       ldx, dwide, F, members, memrow, total, out, row_stride, part);                             \
+  if (pieces > 1)                                                                                                 \
+    hipLaunchKernelGGL((emb_seg_fix_kernel<TO, DD, kSegVW, seg_per_piece(DD)>), fix_blocks, 256, 0, s, memrow,     \
+                       total, part, out, row_stride, dwide != nullptr);
   switch (D) {
     case 16:
-      MINIPS_SEG_LAUNCH(16)
+      MINIPS_SEG_DET(16)
       break;
     case 32:
-      MINIPS_SEG_LAUNCH(32)
+      MINIPS_SEG_DET(32)
       break;
     case 64:
-      MINIPS_SEG_LAUNCH(64)
+      MINIPS_SEG_DET(64)
       break;
     default:
       throw std::runtime_error("emb_backward_seg: D must be 16, 32 or 64");
   }
-#undef MINIPS_SEG_LAUNCH3
-#undef MINIPS_SEG_LAUNCH2
-#undef MINIPS_SEG_LAUNCH
-  MINIPS_HIP_CHECK(hipGetLastError());
-}
-
-// ---------------------------------------------------------------- fused backward + row-wise Adagrad
-// One rank (the PS shard is local): the segmented sum above feeds the row-wise Adagrad apply
-// directly instead of writing grad_rows [U, W] fp32 and reading it back in a second kernel
-// (sparse_rowwise_adagrad), and no zero-fill of grad_rows. Same piecewise traversal (a D/4-lane
-// group owns G consecutive row-sorted lookups); when a group reaches a row's first lookup it
-// also loads that row's table values and Adagrad state in the same batch as the gradient loads
-// (no dependent load at the flush). A row that lies entirely inside one group's range is
-// updated in place at its flush; a row cut by a group boundary (Zipf-hot rows, range edges)
-// is accumulated with fp32 atomics into a persistent zeroed scratch [U, scr_ld], and a second
-// kernel applies it -- one thread group per group boundary that is the row's FIRST cut -- and
-// clears the scratch row again. Semantics of ops.sparse_rowwise_adagrad with state2 for
-// columns [D1, W): sq1 = mean over [0, D1), sq2 = mean over [D1, W) (zero pad columns count).
-struct SegAdagradArgs {
-  const int64_t* uniq;  // [U] unique keys (table row = key - base)
-  int64_t base;
-  float* table;         // [rows, ld] fp32
-  int ld, W, D1;
-  float* state;         // [rows]
-  float* state2;        // [rows] or null (D1 == W)
-  float lr, eps;
-  float* scr;           // [U, scr_ld] fp32, zero outside a call
-  int scr_ld;
-};
-
-// sum over the L lanes of one row group (xor partners stay inside the group: all active)
-template <int L>
-__device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int o = 1; o < L; o <<= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Row-wise Adagrad of one row held by the L lanes of a group: acc = emb gradient columns
-// [4l, 4l+4), accw = wide gradient at column D (lane 0). t/tw = the row's current values,
-// st1_old/st2_old its Adagrad state (on every lane of the group).
-template <int D>
-__device__ __forceinline__ void seg_adagrad_apply(const SegAdagradArgs& a, int64_t row, float4 acc, float accw,
-                                                  bool wide, float4 t, float tw, float st1_old, float st2_old, int l) {
-  constexpr int L = D / 4;
-  const float sq_e = group_sum<L>(acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w);
-  const float sq_w = group_sum<L>(l == 0 ? accw * accw : 0.f);
-  const bool split = a.D1 < a.W;  // D1 == D: the wide column (and the pad) has its own state
-  const float st1 = st1_old + (split ? sq_e : sq_e + sq_w) / (float)a.D1;
-  const float st2 = split ? st2_old + sq_w / (float)(a.W - a.D1) : 0.f;
-  const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
-  float* tr = a.table + row * (int64_t)a.ld;
-  *reinterpret_cast<float4*>(tr + 4 * l) =
-      make_float4(t.x - s1 * acc.x, t.y - s1 * acc.y, t.z - s1 * acc.z, t.w - s1 * acc.w);
-  if (l == 0) {
-    if (wide) tr[D] = tw - s2 * accw;
-    a.state[row] = st1;
-    if (split) a.state2[row] = st2;
-  }
-}
-
-template <typename TX, int D, int G, int NB>
-__global__ __launch_bounds__(256) void emb_seg_adagrad_kernel(const TX* __restrict__ dX, int ldx,
-                                                              const float* __restrict__ dwide, int F,
-                                                              const int* __restrict__ members,
-                                                              const int* __restrict__ memrow, int total,
-                                                              SegAdagradArgs a) {
-  constexpr int L = D / 4, PER = 64 / L;
-  const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
-  const bool wide = dwide != nullptr;
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t piece = wave; piece * (PER * G) < total; piece += nw) {
-    const int ga = (int)(piece * (PER * G)) + sub * G;
-    const int gb = min(total, ga + G);
-    const int prev_row = (ga > 0 && ga <= total) ? memrow[ga - 1] : -1;
-    const int next_row = gb < total ? memrow[gb] : -1;
-    int cur = -1, last = prev_row;
-    bool cur_has = false;
-    int64_t cur_trow = 0;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), ct = acc;
-    float accw = 0.f, ctw = 0.f, cs1 = 0.f, cs2 = 0.f;
-    auto flush = [&]() {
-      if (cur != prev_row && cur != next_row) {  // whole row inside this group: apply now
-        if (cur_has) seg_adagrad_apply<D>(a, cur_trow, acc, accw, wide, ct, ctw, cs1, cs2, l);
-      } else {
-        float* out = a.scr + (int64_t)cur * a.scr_ld + 4 * l;
-        atomicAdd(out + 0, acc.x);
-        atomicAdd(out + 1, acc.y);
-        atomicAdd(out + 2, acc.z);
-        atomicAdd(out + 3, acc.w);
-        if (wide && l == 0) atomicAdd(a.scr + (int64_t)cur * a.scr_ld + D, accw);
-      }
-    };
-    for (int m0 = ga; m0 < gb; m0 += NB) {
-      int u[NB];
-      bool st[NB];
-      int64_t trow[NB];
-      float4 v[NB], t[NB];
-      float vw[NB], tw[NB], s1[NB], s2[NB];
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int m = m0 + q;
-        const bool ok = m < gb;
-        u[q] = ok ? memrow[m] : -1;
-        const int j = ok ? members[m] : 0;
-        const int bb = j / F, ff = j - bb * F;
-        v[q] = ok ? ld_grad4(dX + (int64_t)bb * ldx + ff * D + 4 * l) : make_float4(0.f, 0.f, 0.f, 0.f);
-        vw[q] = (wide && l == 0 && ok) ? dwide[bb] : 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {  // the first lookup of a row in this range: its table row too
-        st[q] = u[q] >= 0 && u[q] != (q == 0 ? last : u[q - 1]);
-        trow[q] = st[q] ? a.uniq[u[q]] - a.base : 0;
-      }
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        t[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        tw[q] = s1[q] = s2[q] = 0.f;
-        if (st[q]) {
-          const float* tr = a.table + trow[q] * (int64_t)a.ld;
-          t[q] = *reinterpret_cast<const float4*>(tr + 4 * l);
-          if (wide && l == 0) tw[q] = tr[D];
-          s1[q] = a.state[trow[q]];  // every lane: each scales its own columns
-          if (a.state2) s2[q] = a.state2[trow[q]];
-        }
-      }
-      last = u[NB - 1] >= 0 ? u[NB - 1] : last;
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        if (u[q] < 0) break;
-        if (u[q] != cur) {
-          if (cur >= 0) flush();
-          cur = u[q];
-          cur_has = st[q];
-          cur_trow = trow[q];
-          ct = t[q];
-          ctw = tw[q];
-          cs1 = s1[q];
-          cs2 = s2[q];
-          acc = make_float4(0.f, 0.f, 0.f, 0.f);
-          accw = 0.f;
-        }
-        acc.x += v[q].x;
-        acc.y += v[q].y;
-        acc.z += v[q].z;
-        acc.w += v[q].w;
-        accw += vw[q];
-      }
-    }
-    // A Zipf-hot row spanning the whole wave: combine the groups' partials in registers first
-    // (one atomic per wave instead of one per group: same-address atomics serialise at the
-    // memory side). Such a row is cut by group boundaries, so the cut-row kernel applies it.
-    const int c0 = __shfl(cur, 0, 64);
-    if (__all(cur == c0) && c0 >= 0) {
-#pragma unroll
-      for (int o = L; o < 64; o <<= 1) {
-        acc.x += __shfl_xor(acc.x, o, 64);
-        acc.y += __shfl_xor(acc.y, o, 64);
-        acc.z += __shfl_xor(acc.z, o, 64);
-        acc.w += __shfl_xor(acc.w, o, 64);
-        accw += __shfl_xor(accw, o, 64);
-      }
-      if (sub == 0) {
-        float* out = a.scr + (int64_t)c0 * a.scr_ld + 4 * l;
-        atomicAdd(out + 0, acc.x);
-        atomicAdd(out + 1, acc.y);
-        atomicAdd(out + 2, acc.z);
-        atomicAdd(out + 3, acc.w);
-        if (wide && l == 0) atomicAdd(a.scr + (int64_t)c0 * a.scr_ld + D, accw);
-      }
-    } else if (cur >= 0) {
-      flush();
-    }
-  }
-}
-
-// Rows cut by a group boundary: boundary b = k*G handles the row iff the row continues across
-// b and b is its first cut (the previous boundary does not cut the same row).
-template <int D>
-__global__ __launch_bounds__(256) void emb_cut_adagrad_kernel(const int* __restrict__ memrow, int total, int G,
-                                                              bool wide, SegAdagradArgs a) {
-  constexpr int L = D / 4, PER = 64 / L;
-  const int lane = threadIdx.x & 63, l = lane % L;
-  const int64_t nb = (total - 1) / G;  // boundaries 1..nb
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t k = 1 + wave * PER + lane / L; k <= nb; k += nw * PER) {
-    const int b = (int)(k * G);
-    const int u = memrow[b];
-    if (memrow[b - 1] != u) continue;
-    if (b - G > 0 && memrow[b - G - 1] == u) continue;
-    float* sr = a.scr + (int64_t)u * a.scr_ld;
-    const float4 g = *reinterpret_cast<const float4*>(sr + 4 * l);
-    const float gw = (wide && l == 0) ? sr[D] : 0.f;
-    *reinterpret_cast<float4*>(sr + 4 * l) = make_float4(0.f, 0.f, 0.f, 0.f);  // scratch clean for the next call
-    if (wide && l == 0) sr[D] = 0.f;
-    const int64_t row = a.uniq[u] - a.base;
-    const float* tr = a.table + row * (int64_t)a.ld;
-    const float4 t = *reinterpret_cast<const float4*>(tr + 4 * l);
-    const float tw = (wide && l == 0) ? tr[D] : 0.f;
-    const float s1 = a.state[row];
-    const float s2 = a.state2 ? a.state2[row] : 0.f;
-    seg_adagrad_apply<D>(a, row, g, gw, wide, t, tw, s1, s2, l);
-  }
-}
-
-// ---------------------------------------------------------------- row-parallel backward + Adagrad
-// One rank, row-sorted gradient rows (the dgrad GEMM's permuted-rows epilogue writes dX[m] = the
-// gradient of lookup members[m], rows grouped by unique row u): row u's lookups are the contiguous
-// rows [rowstart[u], rowstart[u + 1]) of dX. Instead of cutting the lookup stream into fixed pieces
-// (emb_seg_sum / emb_seg_adagrad: a data-dependent flush per row change and fp32 atomics on every
-// row cut by a piece boundary -- 0.9 TB/s, plus a zero-filled grad_rows buffer read back by the
-// Adagrad kernel), each ROW is one unit of work:
-//   cold rows (<= hot lookups, nearly all of them): a group of D/8 lanes sums the row's lookups
-//     with 16-byte bf16 loads (4 lookups in flight per lane), its table row and Adagrad state are
-//     loaded before the sum (independent of it), and the update is written in place -- no
-//     intermediate buffer, no atomics, each row touched once;
-//   hot rows (Zipf heads: up to thousands of lookups) are appended to a list (one atomic per hot
-//   row) and summed by a whole workgroup each (64 lane groups + an LDS reduction), so no wave
-//   waits on a row thousands of lookups long.
-// Semantics of ops.sparse_rowwise_adagrad with state2 for columns [D1, W) (the wide weight + pad).
-struct RowsAdagradArgs {
-  const int64_t* uniq;
-  int64_t base;
-  float* table;
-  int ld, W, D1;
-  float* state;
-  float* state2;
-  float lr, eps;
-};
-
-__device__ __forceinline__ void acc_bf16x8(float (&acc)[8], uint4 v) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    acc[2 * e] += __uint_as_float(w[e] << 16);
-    acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
-  }
-}
-
-// new values of this lane's 8 deep columns (t0, t1) and of the wide column (lane 0 of the group)
-template <int L>
-__device__ __forceinline__ void rows_apply(const RowsAdagradArgs& a, int64_t trow, const float (&g)[8], float gw,
-                                           bool wide, float4 t0, float4 t1, float tw, float st1_old, float st2_old,
-                                           int l, int D) {
-  float sq = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) sq += g[e] * g[e];
-  sq = group_sum<L>(sq);
-  const float sqw = group_sum<L>(l == 0 ? gw * gw : 0.f);
-  const bool split = a.D1 < a.W;
-  const float st1 = st1_old + (split ? sq : sq + sqw) / (float)a.D1;
-  const float st2 = split ? st2_old + sqw / (float)(a.W - a.D1) : 0.f;
-  const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
-  float* tr = a.table + trow * (int64_t)a.ld + 8 * l;
-  reinterpret_cast<float4*>(tr)[0] =
-      make_float4(t0.x - s1 * g[0], t0.y - s1 * g[1], t0.z - s1 * g[2], t0.w - s1 * g[3]);
-  reinterpret_cast<float4*>(tr)[1] =
-      make_float4(t1.x - s1 * g[4], t1.y - s1 * g[5], t1.z - s1 * g[6], t1.w - s1 * g[7]);
-  if (l == 0) {
-    if (wide) a.table[trow * (int64_t)a.ld + D] = tw - s2 * gw;
-    a.state[trow] = st1;
-    if (split) a.state2[trow] = st2;
-  }
-}
-
-// the gradient row of member m (lookup j = members[m]): row-sorted (ldx == 0) or lookup order
-template <int D>
-__device__ __forceinline__ const bf16_t* grad_row(const bf16_t* dX, int ldx, int F, int m, int j) {
-  if (ldx == 0) return dX + (int64_t)m * D;
-  const int b = j / F;
-  return dX + (int64_t)b * ldx + (j - b * F) * D;
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void emb_rows_adagrad_kernel(const bf16_t* __restrict__ dX, int ldx,
-                                                               const float* __restrict__ dwide, int F,
-                                                               const int* __restrict__ members,
-                                                               const int* __restrict__ rowstart,
-                                                               const int64_t* __restrict__ U_dev, int64_t U_max,
-                                                               RowsAdagradArgs a, int* __restrict__ ws,
-                                                               int hmax, int hot) {
-  constexpr int L = D / 8, PER = 64 / L, CHW = 8 * (256 / L);
-  int* cnt = ws;  // {hot rows, chunks, hot-kernel block ticket}
-  int* hot_row = ws + 4;
-  int* hot_need = hot_row + hmax;
-  int2* chunk = reinterpret_cast<int2*>(hot_need + hmax + (hmax & 1));
-  const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
-  const bool wide = dwide != nullptr;
-  const int64_t U = min(U_max, *U_dev);
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t u0 = wave * PER; u0 < U; u0 += nw * PER) {
-    const int64_t u = u0 + sub;
-    const bool ok = u < U;
-    const int s = ok ? rowstart[u] : 0, e = ok ? rowstart[u + 1] : 0;
-    const bool cold = ok && e - s <= hot;
-    if (ok && !cold && l == 0) {  // a hot row: its chunks go to emb_hot_adagrad_kernel
-      const int h = atomicAdd(cnt, 1), nc = (e - s + CHW - 1) / CHW;
-      const int c0 = atomicAdd(cnt + 1, nc);
-      hot_row[h] = (int)u;
-      hot_need[h] = nc;
-      for (int k = 0; k < nc; ++k) chunk[c0 + k] = make_int2(h, k);
-    }
-    // the row's current values and state: independent of the sum, loaded ahead of it
-    const int64_t trow = cold ? a.uniq[u] - a.base : 0;
-    float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0;
-    float tw = 0.f, st1 = 0.f, st2 = 0.f;
-    if (cold) {
-      const float* tr = a.table + trow * (int64_t)a.ld + 8 * l;
-      t0 = reinterpret_cast<const float4*>(tr)[0];
-      t1 = reinterpret_cast<const float4*>(tr)[1];
-      if (wide && l == 0) tw = a.table[trow * (int64_t)a.ld + D];
-      st1 = a.state[trow];
-      if (a.state2) st2 = a.state2[trow];
-    }
-    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float gw = 0.f;
-    const int end = cold ? e : s;
-    if (ldx != 0 && hot <= 32) {
-      // lookup order: the group's lanes fetch the row's member list cooperatively (one round
-      // trip), then every lookup's j comes by a lane shuffle and its gradient slice loads 8 at a
-      // time -- 2 + cnt / 8 dependent round trips instead of 2 per 4 lookups
-      constexpr int MK = (32 + L - 1) / L;
-      const int cnt = end - s, gbase = lane - l;
-      int mj[MK];
-#pragma unroll
-      for (int k = 0; k < MK; ++k) {
-        const int q = l + L * k;
-        mj[k] = q < cnt ? members[s + q] : 0;
-      }
-#pragma unroll
-      for (int q0 = 0; q0 < 32; q0 += 8) {
-        uint4 v[8];
-        float w[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int q = q0 + i;
-          const int j = __shfl(mj[q / L], gbase + q % L, 64);
-          const bool in = q < cnt;
-          const int b = j / F;
-          v[i] = in ? *reinterpret_cast<const uint4*>(dX + (int64_t)b * ldx + (j - b * F) * D + 8 * l)
-                    : make_uint4(0, 0, 0, 0);
-          w[i] = (wide && l == 0 && in) ? dwide[b] : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          acc_bf16x8(g, v[i]);
-          gw += w[i];
-        }
-      }
-    } else {
-      for (int m = s; m < end; m += 4) {
-        uint4 v[4];
-        float w[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int mm = m + q;
-          const bool in = mm < end;
-          const int j = (in && (ldx || wide)) ? members[mm] : 0;
-          v[q] = in ? *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, mm, j) + 8 * l) : make_uint4(0, 0, 0, 0);
-          w[q] = (wide && l == 0 && in) ? dwide[j / F] : 0.f;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          acc_bf16x8(g, v[q]);
-          gw += w[q];
-        }
-      }
-    }
-    if (cold) rows_apply<L>(a, trow, g, gw, wide, t0, t1, tw, st1, st2, l, D);
-  }
-}
-
-// Hot rows in workgroup chunks of G * 8 lookups (G = 256 / L lane groups, 8 loads in flight per
-// lane): a chunk folds in LDS; a row of one chunk is applied by that workgroup, a longer row's
-// chunks add their partial rows into hot_acc (memory-side fp32 atomics, one per column per chunk:
-// a row thousands of lookups long costs ~10 atomics per address, not thousands) and draw a ticket;
-// the row's last chunk applies (agent-scope acquire, then the sums) and re-zeroes hot_acc / the
-// ticket for the next call. The cold kernel wrote the chunk list: ws = {hot rows, chunks, block
-// ticket, pad, hot_row [Hmax], hot_need [Hmax], chunk (hot index, chunk index) [Cmax]}; the hot
-// kernel's last block re-zeroes the counters.
-template <int D>
-__device__ __forceinline__ void hot_apply(const RowsAdagradArgs& a, int64_t trow, int t, float v, float vw,
-                                          bool wide) {
-  const float sq = warp_sum(t < D ? v * v : 0.f);
-  const float sqw = wide ? vw * vw : 0.f;
-  const bool split = a.D1 < a.W;
-  const float st1 = a.state[trow] + (split ? sq : sq + sqw) / (float)a.D1;
-  const float st2 = split ? a.state2[trow] + sqw / (float)(a.W - a.D1) : 0.f;
-  const float s1 = a.lr / (sqrtf(st1) + a.eps), s2 = split ? a.lr / (sqrtf(st2) + a.eps) : s1;
-  float* tr = a.table + trow * (int64_t)a.ld;
-  if (t < D) tr[t] -= s1 * v;
-  if (t == 0 && wide) tr[D] -= s2 * vw;
-  if (t == 0) {
-    a.state[trow] = st1;
-    if (split) a.state2[trow] = st2;
-  }
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void emb_hot_adagrad_kernel(const bf16_t* __restrict__ dX, int ldx,
-                                                              const float* __restrict__ dwide, int F,
-                                                              const int* __restrict__ members,
-                                                              const int* __restrict__ rowstart, RowsAdagradArgs a,
-                                                              int* __restrict__ ws, int hmax,
-                                                              float* __restrict__ hot_acc,
-                                                              unsigned* __restrict__ hot_tick) {
-  constexpr int L = D / 8, G = 256 / L, CHW = 8 * G;
-  __shared__ float red[G][D + 1];
-  const int t = threadIdx.x, g = t / L, l = t % L;
-  const bool wide = dwide != nullptr;
-  const int* hot_row = ws + 4;
-  const int* hot_need = hot_row + hmax;
-  const int2* chunk = reinterpret_cast<const int2*>(hot_need + hmax);
-  const int nch = ws[1];
-  for (int c = blockIdx.x; c < nch; c += gridDim.x) {
-    const int2 hk = chunk[c];
-    const int u = hot_row[hk.x], need = hot_need[hk.x];
-    const int s = rowstart[u] + hk.y * CHW, e = min(rowstart[u + 1], s + CHW);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float accw = 0.f;
-    int jj[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int m = s + g + q * G;
-      jj[q] = (m < e && (ldx || wide)) ? members[m] : 0;
-    }
-    uint4 v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int m = s + g + q * G;
-      v[q] = m < e ? *reinterpret_cast<const uint4*>(grad_row<D>(dX, ldx, F, m, jj[q]) + 8 * l)
-                   : make_uint4(0, 0, 0, 0);
-      if (wide && l == 0 && m < e) accw += dwide[jj[q] / F];
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) acc_bf16x8(acc, v[q]);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) red[g][8 * l + q] = acc[q];
-    if (l == 0) red[g][D] = accw;
-    __syncthreads();
-    if (t < 64) {  // wave 0: lane c < D folds column c, lane 0 also the wide column
-      float vv = 0.f, vw = 0.f;
-      if (t < D)
-        for (int k = 0; k < G; ++k) vv += red[k][t];
-      if (t == 0 && wide)
-        for (int k = 0; k < G; ++k) vw += red[k][D];
-      const int64_t trow = a.uniq[u] - a.base;
-      if (need == 1) {
-        hot_apply<D>(a, trow, t, vv, __shfl(vw, 0, 64), wide);
-      } else {
-        float* ha = hot_acc + (int64_t)hk.x * (D + 1);
-        if (t < D) atomicAdd(ha + t, vv);
-        if (t == 0 && wide) atomicAdd(ha + D, vw);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adds performed before its ticket
-        unsigned last = 0;
-        if (t == 0) {
-          last = __hip_atomic_fetch_add(hot_tick + hk.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (unsigned)need - 1;
-          if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-        }
-        last = __shfl(last, 0, 64);
-        if (last) {  // every chunk of the row has added: its sum is complete
-          const float sv = t < D ? __hip_atomic_load(ha + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-          const float sw = wide ? __hip_atomic_load(ha + D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-          hot_apply<D>(a, trow, t, sv, sw, wide);
-          if (t < D) __hip_atomic_store(ha + t, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (t == 0) {
-            if (wide) __hip_atomic_store(ha + D, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(hot_tick + hk.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      }
-    }
-    __syncthreads();  // red is reused by the next chunk
-  }
-  // the last block to finish zeroes the counters for the next call (every block read them at its
-  // start): no memset node in front of every call (7 us of queue time per W&D step), graph-safe
-  if (t == 0 && atomicAdd(ws + 2, 1) == (int)gridDim.x - 1) {
-    ws[0] = 0;
-    ws[1] = 0;
-    ws[2] = 0;
-  }
-}
-
-// hot-row capacities of emb_rows_adagrad for n lookups and threshold hot: rows with more than
-// `hot` lookups (Hmax) and their chunks (Cmax)
-static inline void rows_hot_caps(int64_t n, int hot, int D, int64_t& hmax, int64_t& cmax) {
-  const int chw = 8 * (256 / (D / 8));
-  hmax = n / (hot + 1) + 1;
-  cmax = hmax + n / chw + 1;
-}
-
-int64_t emb_rows_ws_ints(int64_t n, int hot, int D) {
-  int64_t hmax, cmax;
-  rows_hot_caps(n, hot, D, hmax, cmax);
-  return 4 + 2 * hmax + 2 * cmax;
-}
-
-int64_t emb_rows_hot_rows(int64_t n, int hot, int D) {
-  int64_t hmax, cmax;
-  rows_hot_caps(n, hot, D, hmax, cmax);
-  return hmax;
-}
-
-void emb_rows_adagrad(const bf16_t* dX, int ldx, const float* dwide, int F, int D, const int* members,
-                      const int* rowstart, const int64_t* U_dev, int64_t U_max, const int64_t* uniq, int64_t base,
-                      float* table, int ld, int W, float* state, float* state2, int D1, float lr, float eps,
-                      int* ws, float* hot_acc, unsigned* hot_tick, int hot, hipStream_t s) {
-  if (U_max <= 0) return;
-  if (ld % 4 || reinterpret_cast<uintptr_t>(table) % 16 || reinterpret_cast<uintptr_t>(dX) % 16 || ldx % 8)
-    throw std::runtime_error("emb_rows_adagrad: 16-byte aligned rows");
-  if (D1 <= 0 || D1 > W) D1 = W;
-  if (D1 < W && !state2) throw std::runtime_error("emb_rows_adagrad: split rows need state2");
-  if (D != 16 && D != 32 && D != 64) throw std::runtime_error("emb_rows_adagrad: D must be 16, 32 or 64");
-  int64_t hmax, cmax;
-  rows_hot_caps(U_max, hot, D, hmax, cmax);  // U_max = the lookups (rowstart has n + 1 entries)
-  const RowsAdagradArgs a{uniq, base, table, ld, W, D1, state, state2, lr, eps};
-  const int per_block = 4 * (64 / (D / 8));
-  const int grid = (int)std::min<int64_t>((U_max + per_block - 1) / per_block, 8192);
-  const int hgrid = (int)std::min<int64_t>(cmax, 2048);
-#define MINIPS_ROWS_ADA(DD)                                                                                      \
-  hipLaunchKernelGGL((emb_rows_adagrad_kernel<DD>), grid, 256, 0, s, dX, ldx, dwide, F, members, rowstart,     \
-                     U_dev, U_max, a, ws, (int)hmax, hot);                                                        \
-  hipLaunchKernelGGL((emb_hot_adagrad_kernel<DD>), hgrid, 256, 0, s, dX, ldx, dwide, F, members, rowstart, a, ws, \
-                     (int)hmax, hot_acc, hot_tick);
-  switch (D) {
-    case 16:
-      MINIPS_ROWS_ADA(16)
-      break;
-    case 32:
-      MINIPS_ROWS_ADA(32)
-      break;
-    default:
-      MINIPS_ROWS_ADA(64)
-      break;
-  }
-#undef MINIPS_ROWS_ADA
-  MINIPS_HIP_CHECK(hipGetLastError());
-}
-
-void emb_seg_adagrad(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
-                     const int* members, const int* memrow, const int64_t* uniq, int64_t base, float* table, int ld,
-                     int W, float* state, float* state2, int D1, float lr, float eps, float* scr, int scr_ld,
-                     hipStream_t s) {
-  const int total = (int)(B * F);
-  if (total <= 0) return;
-  const SegAdagradArgs a{uniq, base, table, ld, W, D1, state, state2, lr, eps, scr, scr_ld};
-  static const int nb_cfg = [] {
-    const char* e = std::getenv("MINIPS_SEGADA_NB");
-    return e ? std::atoi(e) : 4;  // W&D step: NB 4 0.473, 8 0.487, 16 0.515 ms (unfused 0.465)
-  }();
-  constexpr int G = 16;
-  const int pieces = (total + (256 / D) * G - 1) / ((256 / D) * G);
-  const int blocks = std::max(1, std::min((pieces + 3) / 4, 65535));
-  const int64_t nbound = (total - 1) / G;
-  const int cut_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((nbound * (D / 4) + 255) / 256, 65535));
-#define MINIPS_SEGADA(DD)                                                                                       \
-  if (bf16 && nb_cfg == 16)                                                                                     \
-    hipLaunchKernelGGL((emb_seg_adagrad_kernel<bf16_t, DD, G, 16>), blocks, 256, 0, s,                          \
-                       static_cast<const bf16_t*>(dX), ldx, dwide, F, members, memrow, total, a);              \
-  else if (bf16 && nb_cfg == 4)                                                                                 \
-    hipLaunchKernelGGL((emb_seg_adagrad_kernel<bf16_t, DD, G, 4>), blocks, 256, 0, s,                           \
-                       static_cast<const bf16_t*>(dX), ldx, dwide, F, members, memrow, total, a);              \
-  else if (bf16)                                                                                                \
-    hipLaunchKernelGGL((emb_seg_adagrad_kernel<bf16_t, DD, G, 8>), blocks, 256, 0, s,                           \
-                       static_cast<const bf16_t*>(dX), ldx, dwide, F, members, memrow, total, a);              \
-  else                                                                                                          \
-    hipLaunchKernelGGL((emb_seg_adagrad_kernel<float, DD, G, 8>), blocks, 256, 0, s,                           \
-                       static_cast<const float*>(dX), ldx, dwide, F, members, memrow, total, a);               \
-  if (nbound > 0)                                                                                               \
-    hipLaunchKernelGGL((emb_cut_adagrad_kernel<DD>), cut_blocks, 256, 0, s, memrow, total, G, dwide != nullptr, a);
-  switch (D) {
-    case 16:
-      MINIPS_SEGADA(16)
-      break;
-    case 32:
-      MINIPS_SEGADA(32)
-      break;
-    case 64:
-      MINIPS_SEGADA(64)
-      break;
-    default:
-      throw std::runtime_error("emb_seg_adagrad: D must be 16, 32 or 64");
-  }
-#undef MINIPS_SEGADA
+#undef MINIPS_SEG_DET
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
-                      const int* members, const int* memrow, float* grad_rows, int row_stride, int U, hipStream_t s,
-                      const int64_t* U_dev, bool sorted_rows, bool zeroed) {
-  if (B <= 0 || U <= 0) return;
+                      const int* members, const int* memrow, void* out, bool out_bf16, int row_stride, float* part,
+                      hipStream_t s, bool sorted_rows) {
+  if (B <= 0) return;
   if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("emb_backward_csr: row_stride too small");
-  if (bf16)
-    emb_seg_sum(static_cast<const bf16_t*>(dX), ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s,
-                U_dev, sorted_rows, zeroed);
+  if (bf16 && out_bf16)
+    emb_seg_det(static_cast<const bf16_t*>(dX), ldx, dwide, B, F, D, members, memrow, static_cast<bf16_t*>(out),
+                row_stride, part, s, sorted_rows);
+  else if (bf16)
+    emb_seg_det(static_cast<const bf16_t*>(dX), ldx, dwide, B, F, D, members, memrow, static_cast<float*>(out),
+                row_stride, part, s, sorted_rows);
+  else if (out_bf16)
+    emb_seg_det(static_cast<const float*>(dX), ldx, dwide, B, F, D, members, memrow, static_cast<bf16_t*>(out),
+                row_stride, part, s, sorted_rows);
   else
-    emb_seg_sum(static_cast<const float*>(dX), ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s,
-                U_dev, sorted_rows, zeroed);
+    emb_seg_det(static_cast<const float*>(dX), ldx, dwide, B, F, D, members, memrow, static_cast<float*>(out),
+                row_stride, part, s, sorted_rows);
 }
 
 __global__ void emb_csr_positions_kernel(const int* __restrict__ members, int64_t n, int* __restrict__ pos) {
@@ -1606,14 +1130,13 @@ void emb_csr_positions(const int* members, int64_t n, int* pos, hipStream_t s) {
 }
 
 void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F,
-                          int D, float* grad_rows, int row_stride, int U, int* ws, hipStream_t s,
-                          const int64_t* U_dev) {
+                          int D, void* out, bool out_bf16, int row_stride, int U, int* ws, float* part, hipStream_t s) {
   if (B <= 0 || U <= 0) return;
   // ws: counts[U] | cursor[U] | offsets[U+1] | tiles[U/1024+1] | members[B*F] | memrow[B*F]
   int* members = ws + 3 * U + 1 + (U / 1024 + 1);
   int* memrow = members + B * F;
   emb_build_csr(inv, B, F, U, ws, members, memrow, s);
-  emb_backward_csr(dX, bf16, ldx, dwide, B, F, D, members, memrow, grad_rows, row_stride, U, s, U_dev);
+  emb_backward_csr(dX, bf16, ldx, dwide, B, F, D, members, memrow, out, out_bf16, row_stride, part, s, false);
 }
 
 }  // namespace minips_k

@@ -96,9 +96,11 @@ class Supervisor:
         return env
 
     def _spawn_rank(self, r: int, resume: bool):
-        for suffix in ("", ".quit"):  # the previous process's stamp must not count for this one
+        # the previous process's stamp -- and its recovery capabilities, possibly left by an earlier
+        # run in the same directory -- must not count for this one
+        for name in (f"hb_{r}", f"hb_{r}.quit", f"caps_{r}.json"):
             try:
-                os.remove(os.path.join(self.hb_dir, f"hb_{r}{suffix}"))
+                os.remove(os.path.join(self.hb_dir, name))
             except FileNotFoundError:
                 pass
         self.t_spawn[r] = time.time()

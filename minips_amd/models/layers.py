@@ -149,6 +149,8 @@ class _Fork:
         self.mode = ops.overlap_mode(True)  # forked work: GEMM splits chosen for throughput, not latency
         self.prev = streams._get(idx)
         streams._set(stream_id=st.stream_id, device_index=idx, device_type=st.device_type)
+        if streams.DELAY_US > 0 and "fork" in streams.DELAY_WHERE:
+            streams.delay(sd._raw, idx)
         return st
 
     def __exit__(self, *exc):

@@ -44,14 +44,20 @@ class WideDeepConfig:
     staleness: int = 0
     # "collective": SparseTable / DenseTable over RCCL; "onesided": SSP / ASP with no collective on
     # the data path -- rows pulled one-sidedly from the owners' HBM, gradients pushed into the
-    # owners' inboxes, row-wise Adagrad / Adam applied by each owner's server thread (ps/onesided.py)
-    transport: str = "collective"
+    # owners' inboxes, row-wise Adagrad / Adam applied by each owner's server thread (ps/onesided.py);
+    # "auto" (default): one-sided for SSP / ASP (the reference's asynchronous servers, and faster on
+    # one MI355X: 0.402 vs 0.411 ms/step, profiles/r4/ssp_onesided_vs_collective.txt), collective for BSP
+    transport: str = "auto"
     max_batch: int = 16384       # onesided: inbox slots hold max_batch * F gradient rows
     seed: int = 0
     # several ranks: the dense clock runs per bucket of >= bucket_mb MB of gradient (layers merged
     # from the last one), a bucket's reduce-scatter + Adam + all-gather issued as soon as its
     # layers' weight gradients exist -- beside the remaining backward (0: one clock at the end)
     bucket_mb: float = 2.0
+
+    def __post_init__(self):
+        if self.transport == "auto":
+            self.transport = "onesided" if self.consistency in ("ssp", "asp") else "collective"
 
     @property
     def F(self):
@@ -396,6 +402,8 @@ class WideDeep(LookaheadPlans):
                 self.dense.add()
                 self.dense.clock()
             self._side_pending = (ev_x, side.mark())
+            if hasattr(self.dense, "hold"):  # a checkpoint (drain) waits for this Adam too
+                self.dense.hold(self._side_pending[1])
         else:
             side.join()
             if not dense_early:

@@ -439,6 +439,40 @@ def sparse_rowwise_adagrad(table, state, keys, base, grads, lr, eps=1e-8, state2
         table[rows, D1:D] -= lr * g2 / (s2.sqrt() + eps).unsqueeze(1)
 
 
+def owner_slots(own_inv, splits, cap):
+    """Owner side of a multi-rank push: the received rows come grouped by requester (``splits``,
+    host ints); returns int32 slots [cap * P] with slots[u * P + s] = the received row requester s
+    sent for owned unique row u (own_inv[i] = u), -1 where s sent none."""
+    P = len(splits)
+    if _gpu(own_inv):
+        return kernels().owner_slots(own_inv, [int(c) for c in splits], int(cap))
+    slots = torch.full((max(int(cap), 1) * P,), -1, dtype=torch.int32)
+    seg = torch.repeat_interleave(torch.arange(P), torch.tensor([int(c) for c in splits], dtype=torch.int64))
+    slots[own_inv * P + seg] = torch.arange(own_inv.numel(), dtype=torch.int32)
+    return slots
+
+
+def owner_rows_adagrad(table, state, keys, n, base, recv, slots, P, lr, eps=1e-8, state2=None, split=None, n_dev=None):
+    """Row-wise Adagrad of owned rows keys[:n] (n_dev: device bound) with the gradient of row u =
+    sum over s in 0..P-1 of recv[slots[u * P + s]] (bf16 / fp32 rows, fp32 sum in requester order)
+    -- ops.sparse_rowwise_adagrad of the owner-side segment sums, in one pass."""
+    D = recv.shape[1]
+    D1 = D if split is None else split
+    if _gpu(table):
+        kernels().owner_rows_adagrad(table, state, state2, int(D1), keys, int(n), n_dev, int(base), recv, int(P), slots,
+                                     float(lr), float(eps))
+        return
+    if n_dev is not None:
+        n = min(int(n), int(n_dev.reshape(-1)[0]))
+    sl = slots[: n * P].view(n, P).long()
+    g = torch.zeros(n, D, dtype=torch.float32)
+    for s in range(P):  # requester order (the GPU sum's order)
+        m = sl[:, s]
+        hit = m >= 0
+        g[hit] += recv[m[hit]].float()
+    sparse_rowwise_adagrad(table, state, keys[:n], base, g, lr, eps, state2=state2, split=split)
+
+
 def sparse_sgd(table, keys, base, grads, scale, n_dev=None):
     if _gpu(table):
         kernels().sparse_sgd(table, keys, int(base), grads, float(scale), n_dev)
@@ -569,18 +603,18 @@ def emb_build_csr(inv, F, U, zeroed=None, counts_ready=False):
     return order.to(torch.int32), inv[order].to(torch.int32)
 
 
-def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=None, sorted_rows=False,
-                    zeroed=False):
+def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, csr=None, sorted_rows=False):
     """grad_rows[u, :D] = sum of dX[b, x_off + f*D : ...] over the lookups (b, f) with
-    inv[b*F+f] == u; column D likewise sums dwide[b] when given. On the GPU every row of
-    grad_rows is written (rows without lookups become 0); the CPU reference adds into grad_rows,
-    so callers pass a zeroed buffer. ``sorted_rows``: dX is [B*F, D] in the CSR's member order
-    (row m = lookup csr[0][m]; linear_dgrad(perm=csr[2]) writes it). ``zeroed``: grad_rows rows
-    [0, U) are zero already (a persistent buffer the apply clears; no clearing pass)."""
+    inv[b*F+f] == u; column D likewise sums dwide[b] when given, columns D+1.. are 0. On the GPU
+    (D 16 / 32 / 64) every row that has lookups (every unique row of a plan) is written exactly
+    once, in a fixed summation order -- the same bits on every run; rows without lookups are left
+    untouched -- and ``grad_rows`` may be fp32 or bf16 (the multi-rank push payload);
+    the CPU reference adds into grad_rows, so callers pass a zeroed buffer. ``sorted_rows``: dX is
+    [B*F, D] in the CSR's member order (row m = lookup csr[0][m]; linear_dgrad(perm=csr[2]) writes it)."""
     if _gpu(dX):
         members, memrow = (csr[0], csr[1]) if csr is not None else (None, None)
-        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), U_dev, members, memrow,
-                                  bool(sorted_rows), bool(zeroed and members is not None))
+        kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), members, memrow,
+                                  bool(sorted_rows))
         return grad_rows
     if sorted_rows:  # back to lookup order
         un = torch.empty_like(dX)
@@ -588,75 +622,13 @@ def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, U_dev=None, csr=No
         dX, x_off = un.reshape(-1, F * D), 0
     B = dX.shape[0]
     g = dX[:, x_off: x_off + F * D].float().reshape(B * F, D)
-    grad_rows[:, :D].index_add_(0, inv, g)
+    acc = grad_rows if grad_rows.dtype == torch.float32 else grad_rows.float()
+    acc[:, :D].index_add_(0, inv, g)
     if dwide is not None:
-        grad_rows[:, D].index_add_(0, inv, dwide.repeat_interleave(F))
+        acc[:, D].index_add_(0, inv, dwide.repeat_interleave(F))
+    if acc is not grad_rows:
+        grad_rows.copy_(acc)
     return grad_rows
-
-
-def emb_rows_workspace(n, D, device, hot=16):
-    """Scratch of emb_rows_adagrad for n lookups: (ints, hot_acc, hot_tick, hot). Keep it per table
-    and reuse it on one stream: the counters / hot_acc / hot_tick are zero at allocation and every
-    call leaves them zero."""
-    k = kernels()
-    ws = torch.zeros(k.emb_rows_ws_ints(n, hot, D), dtype=torch.int32, device=device)
-    h = k.emb_rows_hot_rows(n, hot, D)
-    return (ws, torch.zeros(h * (D + 1), dtype=torch.float32, device=device),
-            torch.zeros(h, dtype=torch.int32, device=device), hot)
-
-
-def emb_rows_adagrad(dX, dwide, F, D, csr, U_dev, uniq, base, table, state, state2, split, lr, eps, ws,
-                     sorted_rows=True):
-    """Row-parallel embedding backward + row-wise Adagrad of one rank (widedeep.hip). csr =
-    (members, memrow, positions, rowstart) of plan_sorted: row u owns members [rowstart[u],
-    rowstart[u+1]); it sums their gradient rows (+ dwide of their samples at column D) and gets
-    sparse_rowwise_adagrad in place. dX bf16: ``sorted_rows`` [total, D] in member order, else
-    [B, >= F*D] in lookup order (row of lookup j = b*F + f at dX[b, f*D:]). ``ws``:
-    emb_rows_workspace(n, D, device) (GPU; None on the CPU)."""
-    W = table.shape[1]
-    D1 = W if split is None else split
-    members, rowstart = csr[0], csr[3]
-    if _gpu(dX):
-        wsi, hot_acc, hot_tick, hot = ws
-        kernels().emb_rows_adagrad(dX, dwide, int(F), int(D), members, rowstart, U_dev, uniq, int(base), table, state,
-                                   state2, int(D1), float(lr), float(eps), wsi, hot_acc, hot_tick, int(hot),
-                                   bool(sorted_rows))
-        return
-    U = int(U_dev.reshape(-1)[0])
-    n = members.numel()
-    inv = torch.empty(n, dtype=torch.int64)
-    inv[members.long()] = csr[1].long()
-    if sorted_rows:
-        un = torch.empty_like(dX)
-        un[members.long()] = dX
-    else:
-        un = dX[:, : F * D]
-    grad_rows = torch.zeros(max(U, 1), W, dtype=torch.float32)
-    wd_emb_backward(un.reshape(-1, F * D).float(), dwide, inv, F, D, grad_rows)
-    sparse_rowwise_adagrad(table, state, uniq[:U], base, grad_rows[:U], lr, eps, state2=state2,
-                           split=None if D1 == W else D1)
-
-
-def emb_seg_adagrad(dX, dwide, F, D, csr, uniq, U, base, table, state, state2, split, lr, eps, scratch):
-    """Embedding backward fused with the row-wise Adagrad apply of one rank's local shard: the
-    rows uniq[:U] get sparse_rowwise_adagrad with the gradient wd_emb_backward would produce
-    (segment sums of the lookups' dX rows, dwide at column D), without the grad_rows buffer.
-    ``csr`` = the plan's (members, memrow); ``scratch`` [>= len(uniq), W] fp32, zero before and
-    after (the GPU kernel accumulates rows cut by its piece boundaries there). ``U`` is used on
-    the CPU only (the GPU reads the rows off memrow)."""
-    W = table.shape[1]
-    D1 = W if split is None else split
-    if _gpu(dX):
-        kernels().emb_seg_adagrad(dX, dwide, int(F), int(D), csr[0], csr[1], uniq, int(base), table, state,
-                                  state2, int(D1), float(lr), float(eps), scratch)
-        return
-    B = dX.shape[0]
-    inv = torch.empty(B * F, dtype=torch.int64)
-    inv[csr[0].long()] = csr[1].long()
-    grad_rows = torch.zeros(max(U, 1), W, dtype=torch.float32)
-    wd_emb_backward(dX.float(), dwide, inv, F, D, grad_rows)
-    sparse_rowwise_adagrad(table, state, uniq[:U], base, grad_rows[:U], lr, eps, state2=state2,
-                           split=None if D1 == W else D1)
 
 
 # ----------------------------------------------------------------------------- optimizers

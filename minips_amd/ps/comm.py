@@ -99,6 +99,8 @@ class Comm:
     """Rank/world/device bookkeeping plus the collectives used by the tables (one ordered
     communicator per rank: see the module docstring)."""
 
+    emulated = False  # LoopbackComm: one rank of an N-rank job emulated on one device
+
     def __init__(self, group=None, device: torch.device | None = None, force_collectives: bool = False):
         """``force_collectives``: run every collective through the process group even at world 1
         (tests: the RCCL calls of the multi-rank data plane, with the tables' dtypes and layouts,
@@ -401,6 +403,92 @@ class Comm:
         if t.is_cuda:
             with self.waiting():
                 torch.cuda.synchronize(self.device)
+
+
+class LoopbackComm(Comm):
+    """Rank ``rank`` of a ``world``-rank job, emulated in ONE process on one device: every table is
+    built and routed as that rank of the N-rank job (shard sizes, key ranges, buckets, ring
+    buffers, lookahead depth) and takes every ``world > 1`` code path, but each collective is a
+    loopback that moves the same bytes through this device's HBM instead of the fabric:
+
+      all-to-all(counts)   recv = counts (every peer asks this owner for what it asks each peer)
+      all-to-all-v         out = inp (requires recv_splits == send_splits, which the symmetric
+                           counts give); the KEY exchange's segments are re-based into this
+                           rank's own row range by the caller (SparseTable, ``emulated``), so the
+                           owner-side dedupe and applies run on in-range rows of realistic count
+      reduce-scatter       out = sum of the N equal slices of inp (reads N x shard, like the real
+                           reduction of the peers' contributions)
+      all-gather           every slot of out = this rank's shard (writes N x shard)
+      barrier / all-reduce no-ops
+
+    Wire time is therefore excluded by construction: ``bench.py --emulate-world N`` times the
+    per-rank GPU and host program of an N-rank step on one GPU, so the step's kernels, host syncs
+    and launch count can be profiled (rocprofv3) before an N-GPU node is available."""
+
+    emulated = True
+
+    def __init__(self, world: int, rank: int = 0, device: torch.device | None = None):
+        if world < 2 or not 0 <= rank < world:
+            raise ValueError(f"LoopbackComm: rank {rank} of world {world}")
+        super().__init__(device=device)
+        self.world, self.rank = int(world), int(rank)
+        self.backend = "loopback"
+        self.initialized = False
+
+    def refresh(self):
+        self._sb = 0
+
+    def all_to_all_v(self, out, inp, recv_splits, send_splits, p2p: bool = False):
+        if list(recv_splits) != list(send_splits):
+            raise ValueError("LoopbackComm: an emulated exchange needs symmetric splits")
+        self.stats.calls += 1
+        self._record("a2av_p2p" if p2p else "a2av", inp, tuple(inp.shape[1:]))
+        n = int(sum(send_splits))
+        nbytes = n * inp[:1].numel() * inp.element_size()
+        self.stats.bytes_a2a += nbytes
+        with self._timed("p2p_send_recv" if p2p else "all_to_all_v", nbytes):
+            if n and out.data_ptr() != inp.data_ptr():
+                out[:n].copy_(inp[:n])
+        return out
+
+    def all_to_all_counts(self, recv, counts):
+        self._record("a2a_counts", counts, counts.numel())
+        recv.copy_(counts)
+        return recv
+
+    def exchange_counts(self, counts):
+        c = counts.tolist()
+        return c, c
+
+    def reduce_scatter(self, out_shard, inp):
+        self.stats.calls += 1
+        self._record("reduce_scatter", inp, inp.numel())
+        self.stats.bytes_rs += inp.numel() * inp.element_size()
+        with self._timed("reduce_scatter", inp.numel() * inp.element_size()):
+            torch.sum(inp.view(self.world, -1), 0, out=out_shard.view(-1))
+        return out_shard
+
+    def all_gather(self, out_full, shard):
+        self.stats.calls += 1
+        self._record("all_gather", out_full, out_full.numel())
+        self.stats.bytes_ag += out_full.numel() * out_full.element_size()
+        with self._timed("all_gather", out_full.numel() * out_full.element_size()):
+            lo, hi = out_full.data_ptr(), out_full.data_ptr() + out_full.numel() * out_full.element_size()
+            if lo <= shard.data_ptr() < hi:
+                shard = shard.clone()  # (the in-place form: this rank's slot of out_full)
+            out_full.view(self.world, -1).copy_(shard.reshape(1, -1).expand(self.world, -1))
+        return out_full
+
+    def all_reduce_(self, t, op=None):
+        self._record("all_reduce", t, t.numel())
+        return t
+
+    def store_barrier(self, tag: str, timeout_s: float | None = None):
+        return
+
+    def barrier(self):
+        if self.trace is not None:  # (the real barrier is a 1-element fp32 all-reduce)
+            self._record("all_reduce", torch.zeros(1), 1)
 
 
 def init_distributed(backend: str | None = None) -> Comm:

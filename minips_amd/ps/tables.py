@@ -539,12 +539,23 @@ class DenseTable:
             self.params[self.base: self.base + self.shard].copy_(self.master)
         return False
 
+    def hold(self, event):
+        """A clock of this table was issued on another stream (WideDeep runs one rank's dense Adam
+        on its weight-gradient side stream and does not join it): ``event`` marks its end, and the
+        next drain() -- every checkpoint's shard_state() -- makes the current stream wait for it, so
+        a snapshot never copies master / m / v from the middle of that Adam."""
+        self._held = event
+
     def drain(self):
         self.pipe.drain()
+        ev = self.__dict__.pop("_held", None)
+        if ev is not None:
+            streams.current(self.comm.device).wait_event(ev)
 
     def reset_after_rollback(self):
         self.pipe.reset()
         self._pending = False
+        self.__dict__.pop("_held", None)
         for g in self._ring:
             g.zero_()
 
@@ -630,15 +641,6 @@ def _route_multiplier(num_rows: int) -> int:
 # the dedupe counts each unique key's lookups for the embedding-backward CSR (one pass less);
 # MINIPS_CSR_FUSED=0 counts in emb_build_csr instead
 _CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
-# MINIPS_PERSIST_PUSH=0: a fresh push buffer per clock, cleared by the segment sum (one rank)
-_PERSIST_PUSH = os.environ.get("MINIPS_PERSIST_PUSH", "1") != "0"
-# MINIPS_ROWS_ADAGRAD=1: one rank's embedding backward as the row-parallel fused apply
-# (ops.emb_rows_adagrad) instead of the piecewise segment sum + separate row-wise Adagrad. Off:
-# W&D step 0.417 vs 0.397 ms (lookup order), 0.435 with row-sorted dgrad output
-# (profiles/r4/ab_emb_backward.txt) -- the per-row dependent gathers lose to the piecewise sum.
-# MINIPS_ROWS_HOT: lookups above which a row is reduced by workgroup chunks instead of one lane group
-_ROWS_HOT = int(os.environ.get("MINIPS_ROWS_HOT", "32"))
-_ROWS_ADAGRAD = os.environ.get("MINIPS_ROWS_ADAGRAD", "0") == "1"
 # MINIPS_SORTED_EMB=1: plans carry the CSR's inverse permutation (csr[2]: each lookup's row in
 # member order) so the embedding dgrad writes its output pre-sorted and the backward streams it
 # contiguously instead of gathering 64-byte pieces. Measured on one MI355X (W&D step, 3 x 400
@@ -667,6 +669,7 @@ class SparsePlan:
     own_uniq: torch.Tensor | None = None
     own_inv: torch.Tensor | None = None
     own_U_dev: torch.Tensor | None = None
+    own_slots: torch.Tensor | None = None  # [own cap * P] received row per (owned row, requester)
     csr: tuple | None = None   # (members, memrow) lookups grouped by unique row (emb backward)
     extra: dict = field(default_factory=dict)
     _U: int | None = None
@@ -692,25 +695,9 @@ _BITMAP_RATIO = int(os.environ.get("MINIPS_BITMAP_RATIO", "16"))
 # memory-side atomics slow the concurrently running step; MINIPS_SORT_PLAN=0 keeps the hash path
 _SORT_PLAN = os.environ.get("MINIPS_SORT_PLAN", "1") != "0"
 
-# one rank + row-wise Adagrad: MINIPS_FUSED_EMB_ADAGRAD=1 feeds the embedding backward's segment
-# sums to the apply directly (ops.emb_seg_adagrad, no grad_rows buffer). Measured slower in the
-# Wide&Deep step on one MI355X (0.473-0.477 vs 0.465 ms/step: the fused kernel's key -> row ->
-# table load chain costs more than the 2 x U x 144 B it saves; tools/gpu_ab.sh), so off by default.
-_FUSED_EMB_ADAGRAD = os.environ.get("MINIPS_FUSED_EMB_ADAGRAD", "0") == "1"
 # one rank: W&D assembles its input straight from the fp32 shard (SparseTable.get_source +
 # ops.wd_assemble_tab) instead of gathering the batch's unique rows first (MINIPS_FUSED_ASSEMBLE=0)
 _FUSED_ASSEMBLE = os.environ.get("MINIPS_FUSED_ASSEMBLE", "1") == "1"
-
-
-class _LookupGrads:
-    """A push in lookup form (SparseTable.add_lookup_grads): dX [B, >= F*D] holds one gradient
-    row per lookup (b, f) at columns f*D.., dwide [B] the sample's wide-column gradient."""
-    __slots__ = ("dX", "dwide", "F", "D", "sorted", "rows")
-
-    def __init__(self, dX, dwide, F, D, sorted_rows=False, rows=False):
-        self.dX, self.dwide, self.F, self.D = dX, dwide, F, D
-        self.sorted = sorted_rows  # dX [B*F, D] in the CSR's member order
-        self.rows = rows  # row-parallel apply (ops.emb_rows_adagrad), else ops.emb_seg_adagrad
 
 
 class _PendingPlan:
@@ -951,13 +938,19 @@ class SparseTable:
                 U = int(pp.U_dev.item())
                 return SparsePlan(n, pp.inv, pp.uniq, U, [U], [U], pp.uniq[:U], csr=pp.csr, _U=U)
             return SparsePlan(n, pp.inv, pp.uniq, n, None, None, pp.uniq, U_dev=pp.U_dev, csr=pp.csr)
-        if pp.cev is not None:
+        if pp.cev is not None and not pp.cev.query():
+            # the only possible host wait of a step: the all-to-all splits (with look-ahead depth 2
+            # they were exchanged a step earlier, so normally they are in already: no wait)
             with self.comm.waiting():
-                pp.cev.synchronize()  # the only host wait of a step: the all-to-all splits
+                pp.cev.synchronize()
         send, recv = pp.host[0].tolist(), pp.host[1].tolist()
         U, M = int(sum(send)), int(sum(recv))
         recv_keys = torch.empty(M, dtype=torch.int64, device=dev)
         comm.all_to_all_v(recv_keys, pp.uniq, recv, send, p2p=self.p2p)
+        if comm.emulated and M and type(self)._route_keys is SparseTable._route_keys:
+            # LoopbackComm: the keys came back as this rank's own requests to every owner; re-base
+            # them into its own row range, as the peers' requests to this owner would be
+            recv_keys.remainder_(self.rows_local).add_(self.base)
         p = SparsePlan(n, pp.inv, pp.uniq, U, send, recv, recv_keys, csr=pp.csr, _U=U)
         if M > 0:
             # owner-side dedupe of the keys requested by all ranks (the push sums their rows): they
@@ -975,7 +968,20 @@ class SparseTable:
             p.own_uniq, p.own_inv, p.own_U_dev = ou, oi, oU
             if self._exact_counts:
                 p.extra["own_U"] = int(oU.item())
+            if self._owner_fused_ok():
+                # per owned row, the received row of every requester (each requester pushes a key
+                # at most once): the clock's apply sums them in requester order in one kernel
+                p.own_slots = ops.owner_slots(oi, recv, M)
         return p
+
+    def _owner_fused_ok(self) -> bool:
+        """Several ranks, row-wise Adagrad on an fp32 range shard: the owner applies its pushes
+        with ops.owner_rows_adagrad (segment sums + apply fused, deterministic) instead of
+        scatter-add into a zeroed buffer + a separate apply."""
+        return (self.comm.world > 1 and self.comm.world <= 16 and self._local_apply
+                and self.optimizer == "rowwise_adagrad" and self.value_dtype == torch.float32
+                and type(self)._owner_rows is SparseTable._owner_rows and 16 < self.width <= 64
+                and self.width % 4 == 0)
 
     def plan(self, keys: torch.Tensor, csr: bool = False) -> SparsePlan:
         return self._finish_plan(self._start_plan(keys, csr))
@@ -1077,7 +1083,8 @@ class SparseTable:
     @traced("sparse.add")
     def add(self, plan: SparsePlan, grad_rows: torch.Tensor):
         """Push gradient rows (aligned with the plan's unique order; rows >= U are ignored)."""
-        assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype == getattr(self, "grad_dtype", torch.float32)
+        assert grad_rows.shape[0] >= plan.cap and grad_rows.dtype in (getattr(self, "grad_dtype", torch.float32),
+                                                                      self.push_dtype)
         self._pending.append((plan, grad_rows))
 
     @traced("sparse.add_lookup_grads")
@@ -1085,61 +1092,15 @@ class SparseTable:
                          sorted_rows: bool = False):
         """Push the gradient of every lookup of ``plan``'s batch: dX[b, x_off + f*D : +D] for
         lookup (b, f) (+ dwide[b] into column D of the row). The table reduces them per unique
-        row -- the Add of the reference's worker, which sends one summed row per key. One rank
-        with row-wise Adagrad fuses that reduction into the apply (no gradient-row buffer,
-        ops.emb_seg_adagrad); otherwise the rows are segment-summed here and pushed by add()."""
-        if (_ROWS_ADAGRAD and plan.csr is not None and len(plan.csr) >= 4 and dX.dtype == torch.bfloat16
-                and x_off == 0 and dX.stride(0) % 8 == 0 and self._rows_apply_ok(plan, dX, dwide, D, 0)):
-            # one rank: each unique row sums its lookups' gradient rows (row-sorted or in lookup
-            # order) and is updated in place (ops.emb_rows_adagrad) -- no grad_rows buffer, no zero
-            # fill, no atomics
-            self._pending.append((plan, _LookupGrads(dX, dwide, F, D, sorted_rows=sorted_rows, rows=True)))
-            return
-        if not sorted_rows and _FUSED_EMB_ADAGRAD and self._rows_apply_ok(plan, dX, dwide, D, x_off):
-            self._pending.append((plan, _LookupGrads(dX[:, x_off:] if x_off else dX, dwide, F, D)))
-            return
+        row -- the Add of the reference's worker, which sends one summed row per key -- with the
+        deterministic segment sum (ops.wd_emb_backward), straight into the push dtype (bf16 rows
+        at several GPU ranks: no cast pass), then pushes them by add()."""
         dev = self.comm.device
-        persist = self._persistent_push_ok(plan)
-        if persist:
-            # one rank, synchronous clock: a persistent push buffer the Adagrad apply clears after
-            # reading it (zero_g), so the segment sum needs no clearing pass of its own
-            grad_rows = self._zero_push_rows(max(plan.cap, 1))
-        else:
-            grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width,
-                                                                             dtype=torch.float32, device=dev)
-        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, grad_rows, x_off=x_off, U_dev=plan.U_dev, csr=plan.csr,
-                            sorted_rows=sorted_rows, zeroed=persist)
-        if persist:
-            plan.extra["zero_g"] = True
+        gdt = self.push_dtype if self.comm.world > 1 else getattr(self, "grad_dtype", torch.float32)
+        grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width, dtype=gdt,
+                                                                         device=dev)
+        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, grad_rows, x_off=x_off, csr=plan.csr, sorted_rows=sorted_rows)
         self.add(plan, grad_rows)
-
-    def _persistent_push_ok(self, plan) -> bool:
-        return (_PERSIST_PUSH and self._local_apply and self.comm.world == 1 and self.comm.device.type == "cuda"
-                and self.optimizer == "rowwise_adagrad" and self.value_dtype == torch.float32
-                and getattr(self, "grad_dtype", torch.float32) == torch.float32 and not self.pipe.async_
-                and plan.csr is not None and plan.U_dev is not None
-                and type(self)._owner_rows is SparseTable._owner_rows)
-
-    def _zero_push_rows(self, n: int) -> torch.Tensor:
-        buf = getattr(self, "_push_rows", None)
-        if buf is None or buf.shape[0] < n:
-            buf = self._push_rows = torch.zeros(max(n, 1), self.width, dtype=torch.float32, device=self.comm.device)
-        return buf[:n]
-
-    def _rows_apply_ok(self, plan, dX, dwide, D, x_off) -> bool:
-        """One rank, row-wise Adagrad on a local fp32 shard: the embedding backward can apply."""
-        return (self._local_apply and self.comm.world == 1 and dX.is_cuda and self.optimizer == "rowwise_adagrad"
-                and self.value_dtype == torch.float32 and type(self)._owner_rows is SparseTable._owner_rows
-                and plan.csr is not None and D in (16, 32, 64) and x_off % 4 == 0 and dX.stride(0) % 4 == 0
-                and self.width % 4 == 0 and self.width >= D + (dwide is not None)
-                and (self.split is None or self.split == D))
-
-    def _seg_scratch(self, n: int) -> torch.Tensor:
-        """Zeroed fp32 [>= n, width] accumulator of the fused apply (the kernel leaves it zero)."""
-        s = getattr(self, "_scr", None)
-        if s is None or s.shape[0] < n:
-            s = self._scr = torch.zeros(n, self.width, dtype=torch.float32, device=self.comm.device)
-        return s
 
     def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
         """Reference-style Add(keys, vals) (duplicates are summed)."""
@@ -1153,9 +1114,8 @@ class SparseTable:
     def clock(self):
         pending, self._pending = self._pending, []
         for plan, g in pending:
-            held = (g.dX, g.dwide, *plan.csr) if isinstance(g, _LookupGrads) else (g,)
-            self.pipe.keep_alive(*held, plan.uniq, plan.recv_keys, plan.own_uniq, plan.own_inv, plan.U_dev,
-                                 plan.own_U_dev)
+            self.pipe.keep_alive(g, plan.uniq, plan.recv_keys, plan.own_uniq, plan.own_inv, plan.U_dev,
+                                 plan.own_U_dev, plan.own_slots)
 
         def work():
             for plan, grad_rows in pending:
@@ -1166,23 +1126,6 @@ class SparseTable:
     @traced("sparse.push")
     def _push(self, plan: SparsePlan, grad_rows):
         dev = self.comm.device
-        if isinstance(grad_rows, _LookupGrads) and grad_rows.rows:  # one rank, row-parallel
-            lg = grad_rows
-            n = plan.csr[3].numel() - 1
-            ws = getattr(self, "_rows_ws", None)
-            if ws is None or ws[0] != (n, lg.D):  # (hot_acc / hot_tick stay zero between calls)
-                ws = self._rows_ws = ((n, lg.D), ops.emb_rows_workspace(n, lg.D, dev, hot=_ROWS_HOT))
-            ws = ws[1]
-            U_dev = plan.U_dev if plan.U_dev is not None else torch.tensor([plan.cap], dtype=torch.int64, device=dev)
-            ops.emb_rows_adagrad(lg.dX, lg.dwide, lg.F, lg.D, plan.csr, U_dev, plan.uniq, self.base, self.shard,
-                                 self.state, self.state2, self.split, self.lr, self.eps, ws, sorted_rows=lg.sorted)
-            return
-        if isinstance(grad_rows, _LookupGrads):  # one rank, fused reduction + apply
-            lg = grad_rows
-            ops.emb_seg_adagrad(lg.dX, lg.dwide, lg.F, lg.D, plan.csr, plan.uniq, plan.cap, self.base, self.shard,
-                                self.state, self.state2, self.split, self.lr, self.eps,
-                                self._seg_scratch(plan.uniq.numel()))
-            return
         if self.comm.world == 1:
             keys, g, n_dev, n = plan.uniq, grad_rows, plan.U_dev, plan.cap
         else:
@@ -1194,14 +1137,19 @@ class SparseTable:
             self.comm.all_to_all_v(recv, send, plan.recv, plan.send, p2p=self.p2p)
             if M == 0:
                 return
+            if plan.own_slots is not None:  # segment sums + row-wise Adagrad in one pass
+                ops.owner_rows_adagrad(self.shard, self.state, plan.own_uniq, M, self.base, recv, plan.own_slots,
+                                       len(plan.recv), self.lr, self.eps, state2=self.state2, split=self.split,
+                                       n_dev=plan.own_U_dev)
+                return
             n = plan.extra.get("own_U", M)
             g = torch.zeros(n, self.width, dtype=getattr(self, "grad_dtype", torch.float32), device=dev)
             ops.scatter_add_rows(recv, plan.own_inv, g)
             keys, n_dev = plan.own_uniq, (None if "own_U" in plan.extra else plan.own_U_dev)
         keys, base = self._owner_rows(keys[:n], plan)
-        self._apply_rows(keys, base, g[:n], n_dev, zero_g=bool(plan.extra.get("zero_g")))
+        self._apply_rows(keys, base, g[:n], n_dev)
 
-    def _apply_rows(self, keys, base, g, n_dev=None, zero_g=False):
+    def _apply_rows(self, keys, base, g, n_dev=None):
         if getattr(self, "value_dtype", None) == torch.bfloat16:
             self._applies += 1
             if self.optimizer not in ("rowwise_adagrad", "sgd", "add"):
@@ -1213,7 +1161,7 @@ class SparseTable:
             return
         if self.optimizer == "rowwise_adagrad":
             ops.sparse_rowwise_adagrad(self.shard, self.state, keys, base, g, self.lr, self.eps,
-                                       state2=self.state2, split=self.split, n_dev=n_dev, zero_g=zero_g)
+                                       state2=self.state2, split=self.split, n_dev=n_dev)
         elif self.optimizer == "sgd":
             ops.sparse_sgd(self.shard, keys, base, g.contiguous(), -self.lr, n_dev=n_dev)
         elif self.optimizer == "add":

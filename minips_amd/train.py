@@ -97,8 +97,9 @@ def parse(argv=None):
                     help="> 0: rank 0 serves locality-aware block assignment (HDFSBlockAssigner) on this port")
     ap.add_argument("--num_dims", type=int, default=0, help="feature count (reference flag; 0: infer / default)")
     args = ap.parse_args(argv)
-    if args.transport == "auto":  # DLRMConfig's rule (models/dlrm.py)
-        args.transport = "onesided" if args.model == "dlrm" and args.consistency in ("ssp", "asp") else "collective"
+    if args.transport == "auto":  # SSP / ASP run on the asynchronous one-sided PS (W&D, DLRM), BSP on collectives
+        args.transport = ("onesided" if args.model in ("dlrm", "widedeep") and args.consistency in ("ssp", "asp")
+                          else "collective")
     return args
 
 

@@ -18,6 +18,29 @@ import torch
 FAST = os.environ.get("MINIPS_FAST_EVENTS", "1") != "0"
 FAST_PLAN = FAST and os.environ.get("MINIPS_FAST_PLAN_EVENTS", "1") != "0"
 
+# MINIPS_STREAM_DELAY_US=n (race diagnostics, tests/test_multirank_gpu.py): every work segment
+# issued on another stream through use() or SideStream.fork() starts with an n-us device spin, so a
+# consumer that misses its wait on a producer stream reads stale data deterministically instead of
+# by timing luck -- and a missing edge no longer hides behind the latency of a system-fence event
+DELAY_US = int(os.environ.get("MINIPS_STREAM_DELAY_US", "0"))
+# where: "use" (streams.use segments: planning, clock pipelines, the one-sided push stream),
+# "fork" (SideStream.fork: the weight-gradient side stream) or both (default) -- to bisect a race
+DELAY_WHERE = set(os.environ.get("MINIPS_STREAM_DELAY_WHERE", "use,fork").split(","))
+_delay_bufs: dict = {}
+
+
+def delay(raw_stream: int, dev_index: int):
+    """Spin DELAY_US microseconds on ``raw_stream`` (a one-wave kernel on the 100 MHz clock)."""
+    if DELAY_US <= 0:
+        return
+    buf = _delay_bufs.get(dev_index)
+    if buf is None:
+        buf = _delay_bufs[dev_index] = torch.zeros(2, dtype=torch.int64, device=torch.device("cuda", dev_index))
+    from .._native import kernels
+
+    kernels().clock_probe(buf, min(1_000_000, DELAY_US * 100), raw_stream)
+
+
 _get = torch._C._cuda_getCurrentStream if hasattr(torch._C, "_cuda_getCurrentStream") else None
 _set = torch._C._cuda_setStream if hasattr(torch._C, "_cuda_setStream") else None
 _raw = torch._C._cuda_getCurrentRawStream if hasattr(torch._C, "_cuda_getCurrentRawStream") else None
@@ -59,6 +82,8 @@ class use:
         if s is not None:
             self.prev = _get(s.device_index)
             _set(stream_id=s.stream_id, device_index=s.device_index, device_type=s.device_type)
+            if DELAY_US > 0 and "use" in DELAY_WHERE:
+                delay(_raw(s.device_index), s.device_index)
         return s
 
     def __exit__(self, *exc):

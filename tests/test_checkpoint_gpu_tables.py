@@ -14,7 +14,8 @@ CARDS = [50, 7, 300, 20, 5, 60, 90, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 
 def _wd(comm, consistency="bsp", staleness=0):
     from minips_amd.models.widedeep import WideDeep, WideDeepConfig
 
-    m = WideDeep(WideDeepConfig(cards=CARDS, consistency=consistency, staleness=staleness), comm)
+    m = WideDeep(WideDeepConfig(cards=CARDS, consistency=consistency, staleness=staleness,
+                                 transport="collective"), comm)
     g = torch.Generator().manual_seed(5)
     full = torch.randn(m.num_rows, m.cfg.row_width, generator=g) * 0.01
     full[:, m.cfg.emb_dim:] = 0

@@ -26,7 +26,8 @@ def _schedule_fn(consistency, staleness):
 
         torch.set_num_threads(1)
         comm = Comm(device=torch.device("cpu"))
-        model = WideDeep(WideDeepConfig(cards=CARDS, consistency=consistency, staleness=staleness), comm)
+        model = WideDeep(WideDeepConfig(cards=CARDS, consistency=consistency, staleness=staleness,
+                                       transport="collective"), comm)
         # different data per rank: different all-to-all splits, same op sequence
         data = CriteoSynth(32 + 8 * rank, cards=CARDS, device="cpu", seed=100 + rank)
         comm.trace = []
@@ -87,7 +88,8 @@ def test_no_extra_communicators():
         from minips_amd.models.widedeep import WideDeep, WideDeepConfig
         from minips_amd.ps.comm import Comm
 
-        WideDeep(WideDeepConfig(cards=CARDS, consistency="ssp", staleness=1), Comm(device=torch.device("cpu")))
+        WideDeep(WideDeepConfig(cards=CARDS, consistency="ssp", staleness=1, transport="collective"),
+                 Comm(device=torch.device("cpu")))
     finally:
         dist.new_group = orig
     assert calls == []
@@ -114,3 +116,35 @@ def test_bench_four_ranks_cpu():
     assert out["n_gpus"] == 4 and out["config"]["world_size"] == 4 and out["config"]["backend"] == "gloo"
     assert out["config"]["global_batch"] == 256 and "over gloo" in out["config"]["parallelism"]
     assert out["config"]["model"].startswith("PLUMBING TEST")
+
+
+def _emulated_trace(world, consistency, staleness):
+    from minips_amd.data.synthetic import CriteoSynth
+    from minips_amd.models.feeder import LookaheadFeeder
+    from minips_amd.models.widedeep import WideDeep, WideDeepConfig
+    from minips_amd.ps.comm import LoopbackComm
+
+    torch.set_num_threads(1)
+    comm = LoopbackComm(world, 0, device=torch.device("cpu"))
+    model = WideDeep(WideDeepConfig(cards=CARDS, consistency=consistency, staleness=staleness,
+                                       transport="collective"), comm)
+    data = CriteoSynth(32, cards=CARDS, device="cpu", seed=100)
+    comm.trace = []
+    feeder = LookaheadFeeder(model, data, comm, depth=2)
+    losses = [float(feeder.step()) for _ in range(4)]
+    model.drain()
+    comm.barrier()
+    return comm.trace, losses, model
+
+
+@pytest.mark.parametrize("fn,cons", [(_bsp, ("bsp", 0)), (_ssp, ("ssp", 1))], ids=["bsp", "ssp1"])
+def test_emulated_rank_issues_the_real_rank_program(fn, cons):
+    """bench.py --emulate-world: one process running rank 0 of a 4-rank job over LoopbackComm
+    issues exactly the collective sequence (op, dtype, row width) of a real 4-rank gloo job, so
+    its profile is the per-rank program of the N-rank step; the owner applies land in its own
+    row range and the loss stays finite."""
+    real = run_world(fn, world=4)[0]
+    emu, losses, model = _emulated_trace(4, *cons)
+    assert emu == real
+    assert all(l == l and abs(l) < 1e6 for l in losses)
+    assert model.emb.rows_local == model.emb.bounds_list[1] and model.dense.shard * 4 == model.dense.n_pad

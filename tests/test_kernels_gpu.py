@@ -345,8 +345,9 @@ def test_criteo_synth_kernel(dev):
 
 @pytest.mark.parametrize("D,dtype", [(32, torch.bfloat16), (64, torch.float32), (16, torch.bfloat16)])
 def test_embedding_backward_segment_hot_rows(dev, D, dtype):
-    """Segment-sum embedding backward incl. Zipf-hot rows (> 2048 lookups, split over waves) and
-    rows without lookups (written as zero)."""
+    """Segment-sum embedding backward incl. Zipf-hot rows (thousands of lookups: spanning many
+    pieces, finished by the fix-up kernel over the pieces' partials); rows without lookups are
+    not written (a plan's unique rows always have lookups)."""
     g = torch.Generator().manual_seed(D)
     B, F, U = 8192, 3, 5000
     inv = torch.randint(0, U - 100, (B * F,), generator=g)  # the last 100 rows get no lookups
@@ -354,12 +355,94 @@ def test_embedding_backward_segment_hot_rows(dev, D, dtype):
     inv[6000: 8500] = 11                                    # and one just above the split size
     dX = torch.randn(B, F * D + 8, generator=g).to(dtype)
     dwide = torch.randn(B, generator=g)
-    ref = torch.zeros(U, D + 1)
+    ref = torch.zeros(U, D + 4)
     ops.wd_emb_backward(dX.float(), dwide, inv, F, D, ref)
-    gr = torch.full((U, D + 1), float("nan"), device=dev)  # every row must be overwritten
+    gr = torch.full((U, D + 4), float("nan"), device=dev)
     ops.wd_emb_backward(dX.to(dev), dwide.to(dev), inv.to(dev), F, D, gr)
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-3
-    torch.testing.assert_close(gr.cpu(), ref, rtol=1e-4, atol=tol * 8)
+    hit = torch.zeros(U, dtype=torch.bool)
+    hit[inv] = True
+    torch.testing.assert_close(gr.cpu()[hit], ref[hit], rtol=1e-4, atol=tol * 8)
+    assert bool(torch.isnan(gr.cpu()[~hit]).all())  # untouched
+
+
+@pytest.mark.parametrize("D,out_dtype", [(32, torch.float32), (32, torch.bfloat16), (64, torch.bfloat16),
+                                         (16, torch.float32)])
+def test_embedding_backward_deterministic(dev, D, out_dtype):
+    """The segment sum has one fixed summation order (no atomics): repeated runs are bit-identical,
+    for fp32 and bf16 output rows (the multi-rank push payload), Criteo-shaped batches with hot rows
+    that span many pieces; the wide column and the zero pad columns are written."""
+    g = torch.Generator().manual_seed(40 + D)
+    B, F = 16384, 26
+    cards = [3, 50, 1000, 20000] * 6 + [7, 100000]
+    keys = torch.stack([torch.randint(0, c, (B,), generator=g) for c in cards], 1)
+    keys[:5000, 1] = 4  # a very hot row (5000 lookups)
+    base = torch.tensor([sum(cards[:f]) for f in range(F)], dtype=torch.int64)
+    bits = [max(1, (c - 1).bit_length()) for c in cards]
+    res = ops.plan_sorted((keys + base).to(dev), base.to(dev), bits)
+    inv, U = res[1], int(res[3].item())
+    csr = (res[4], res[5])
+    W = D + 4
+    dX = (torch.randn(B, F * D, generator=g) * 0.1).to(torch.bfloat16).to(dev)
+    dwide = torch.randn(B, generator=g).to(dev)
+    outs = []
+    for _ in range(3):
+        gr = torch.full((B * F, W), float("nan"), dtype=out_dtype, device=dev)
+        ops.wd_emb_backward(dX, dwide, inv, F, D, gr, csr=csr)
+        outs.append(gr[:U].clone())
+    for o in outs[1:]:
+        assert torch.equal(o.view(torch.int16) if out_dtype == torch.bfloat16 else o.view(torch.int32),
+                           outs[0].view(torch.int16) if out_dtype == torch.bfloat16 else outs[0].view(torch.int32))
+    ref = torch.zeros(U, W)
+    ops.wd_emb_backward(dX.cpu().float(), dwide.cpu(), inv.cpu(), F, D, ref)
+    tol = 2e-2 if out_dtype == torch.bfloat16 else 2e-3
+    torch.testing.assert_close(outs[0].float().cpu(), ref, rtol=tol, atol=tol)
+    assert bool((outs[0][:, D + 1:] == 0).all())
+
+
+@pytest.mark.parametrize("P,recv_dtype", [(8, torch.bfloat16), (3, torch.float32), (16, torch.bfloat16)])
+def test_owner_rows_adagrad(dev, P, recv_dtype):
+    """Owner side of a multi-rank push: owner_slots + owner_rows_adagrad (per owned row the <= P
+    requesters' rows summed in requester order, row-wise Adagrad with the split state) against the
+    scatter-add + sparse_rowwise_adagrad reference, bit-identical across runs, rows past the device
+    count untouched."""
+    g = torch.Generator().manual_seed(P)
+    R, W, D1, base = 50000, 36, 32, 1000
+    splits = [int(x) for x in torch.randint(500, 3000, (P,), generator=g)]
+    # each requester pushes distinct keys; requesters overlap (hot keys pushed by everyone)
+    segs = [torch.cat([torch.arange(5), torch.randperm(R - 5, generator=g)[: n - 5] + 5]) + base for n in splits]
+    recv_keys = torch.cat(segs)
+    uniq, own_inv = torch.unique(recv_keys, return_inverse=True)
+    U, M = uniq.numel(), recv_keys.numel()
+    own_uniq = torch.full((M,), -1, dtype=torch.int64)
+    own_uniq[:U] = uniq
+    recv = (torch.randn(M, W, generator=g) * 0.1).to(recv_dtype)
+    table = torch.randn(R, W, generator=g)
+    state, state2 = torch.rand(R, generator=g), torch.rand(R, generator=g)
+    # reference: scatter-add, then the plain apply
+    gsum = torch.zeros(U, W)
+    gsum.index_add_(0, own_inv, recv.float())
+    t_ref, s_ref, s2_ref = table.clone(), state.clone(), state2.clone()
+    ops.sparse_rowwise_adagrad(t_ref, s_ref, uniq, base, gsum, 0.05, 1e-8, state2=s2_ref, split=D1)
+    slots = ops.owner_slots(own_inv.to(dev), splits, M)
+    cslots = ops.owner_slots(own_inv, splits, M)
+    assert torch.equal(slots.cpu(), cslots)
+    U_dev = torch.tensor([U], device=dev)
+    runs = []
+    for _ in range(2):
+        t, s1, s2 = table.to(dev), state.to(dev), state2.to(dev)
+        ops.owner_rows_adagrad(t, s1, own_uniq.to(dev), M, base, recv.to(dev), slots, P, 0.05, 1e-8, state2=s2,
+                               split=D1, n_dev=U_dev)
+        runs.append((t.cpu(), s1.cpu(), s2.cpu()))
+    assert all(torch.equal(a, b) for a, b in zip(runs[0], runs[1]))
+    torch.testing.assert_close(runs[0][0], t_ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(runs[0][1], s_ref, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(runs[0][2], s2_ref, rtol=1e-4, atol=1e-6)
+    # the CPU reference of the fused op agrees too
+    t_c, s_c, s2_c = table.clone(), state.clone(), state2.clone()
+    ops.owner_rows_adagrad(t_c, s_c, own_uniq, M, base, recv, cslots, P, 0.05, 1e-8, state2=s2_c, split=D1,
+                           n_dev=torch.tensor([U]))
+    torch.testing.assert_close(t_c, t_ref, rtol=1e-5, atol=1e-6)
 
 
 def test_device_counts_and_prebuilt_csr(dev):
@@ -386,7 +469,7 @@ def test_device_counts_and_prebuilt_csr(dev):
     ops.wd_emb_backward(dX.float(), dwide, inv.cpu(), F, D, ref)
     csr = ops.emb_build_csr(inv, F, n)
     gr = torch.full((n, D + 1), float("nan"), device=dev)
-    ops.wd_emb_backward(dX.to(dev), dwide.to(dev), inv, F, D, gr, U_dev=U_dev, csr=csr)
+    ops.wd_emb_backward(dX.to(dev), dwide.to(dev), inv, F, D, gr, csr=csr)
     torch.testing.assert_close(gr[:U].cpu(), ref, rtol=1e-4, atol=0.16)
     # row-wise Adagrad bounded by the device count: keys past U (garbage) never applied
     t_gpu = table.to(dev)
@@ -475,100 +558,6 @@ def test_sparse_lr_fp64_matches_cpu(dev):
     assert res["cpu"].abs().sum() > 0
 
 
-@pytest.mark.parametrize("D,wide,split,dtype", [(32, True, True, torch.bfloat16), (32, True, False, torch.float32),
-                                                (16, False, False, torch.bfloat16), (64, True, True, torch.bfloat16)])
-def test_fused_emb_backward_adagrad(dev, D, wide, split, dtype):
-    """ops.emb_seg_adagrad (one-rank fused embedding backward + row-wise Adagrad) against the
-    fp32 reference of the two separate ops, over two steps (the scratch must come back zero):
-    Zipf-hot rows covering whole waves, rows cut by piece boundaries, single-lookup rows."""
-    g = torch.Generator().manual_seed(D + 3 * wide + 5 * split)
-    B, F, R = 4096, 5, 20000
-    W = D + 4
-    table = torch.randn(R, W, generator=g)
-    state = torch.rand(R, generator=g)
-    state2 = torch.rand(R, generator=g) if split else None
-    t_gpu, s_gpu = table.to(dev), state.to(dev)
-    s2_gpu = state2.to(dev) if split else None
-    t_ref, s_ref = table.clone(), state.clone()
-    s2_ref = state2.clone() if split else None
-    scr = torch.zeros(B * F, W, device=dev)
-    bounds = torch.tensor([0, R], device=dev)
-    for step in range(2):
-        keys = torch.randint(0, R, (B, F), generator=g)
-        keys.view(-1)[:6000] = 7 + step        # hot rows: thousands of lookups, cut by many boundaries
-        keys.view(-1)[6000:6040] = 11           # a row just over two pieces
-        uniq, inv, _, U_dev = ops.unique_bucketize_n(keys.to(dev), bounds, F)
-        U = int(U_dev.item())
-        csr = ops.emb_build_csr(inv, F, keys.numel())
-        dX = torch.randn(B, F * D + 8, generator=g).to(dtype)
-        dwide = torch.randn(B, generator=g) if wide else None
-        ops.emb_seg_adagrad(dX.to(dev), dwide.to(dev) if wide else None, F, D, csr, uniq, U, 0, t_gpu, s_gpu,
-                            s2_gpu, D if split else None, 0.05, 1e-8, scr)
-        ops.emb_seg_adagrad(dX.float(), dwide, F, D, (csr[0].cpu(), csr[1].cpu()), uniq.cpu(), U, 0, t_ref, s_ref,
-                            s2_ref, D if split else None, 0.05, 1e-8, None)
-        torch.testing.assert_close(t_gpu.cpu(), t_ref, rtol=1e-4, atol=1e-5)
-        torch.testing.assert_close(s_gpu.cpu(), s_ref, rtol=1e-4, atol=1e-5)
-        if split:
-            torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-4, atol=1e-5)
-        assert int(scr.count_nonzero()) == 0
-
-
-@pytest.mark.parametrize("D,wide,split,sorted_rows", [(32, True, True, True), (16, False, False, True),
-                                                      (64, True, True, True), (32, True, False, False),
-                                                      (64, False, True, False), (16, True, False, False)])
-def test_rows_emb_backward_adagrad(dev, D, wide, split, sorted_rows):
-    """ops.emb_rows_adagrad (row-parallel backward + row-wise Adagrad over the bf16 gradient rows
-    -- row-sorted, or in lookup order with a padded row stride -- and the row ranges of
-    plan_sorted) against the CPU reference of the separate ops, two steps: cold rows, Zipf-hot rows
-    of thousands of lookups (the workgroup-per-row path), single lookups."""
-    g = torch.Generator().manual_seed(D + 3 * wide)
-    B, F = 8192, 6
-    cards = [40000, 5, 3000, 700, 2, 20000]
-    base = torch.tensor([sum(cards[:f]) for f in range(F)], dtype=torch.int64)
-    bits = [max(1, (c - 1).bit_length()) for c in cards]
-    R = sum(cards)
-    W = D + 4
-    table = torch.randn(R, W, generator=g)
-    state = torch.rand(R, generator=g)
-    state2 = torch.rand(R, generator=g) if split else None
-    t_gpu, s_gpu = table.to(dev), state.to(dev)
-    s2_gpu = state2.to(dev) if split else None
-    t_ref, s_ref = table.clone(), state.clone()
-    s2_ref = state2.clone() if split else None
-    ws = ops.emb_rows_workspace(B * F, D, dev)
-    for step in range(2):
-        keys = torch.stack([torch.randint(0, c, (B,), generator=g) for c in cards], 1) + base
-        keys[:3000, 2] = base[2] + 17 + step  # a hot row: 3000 lookups
-        res = ops.plan_sorted(keys.to(dev), base.to(dev), bits, positions=sorted_rows)
-        uniq, inv, counts, U_dev = res[:4]
-        csr = tuple(res[4:])
-        assert len(csr) == 5 and (csr[2] is None) == (not sorted_rows)  # (.., rowidx: None without routing)
-        lookups = torch.randn(B * F, D, generator=g).to(torch.bfloat16)  # lookup order
-        if sorted_rows:
-            pos = csr[2].cpu().long()
-            dX = torch.empty_like(lookups)
-            dX[pos] = lookups  # member order: row m = lookup members[m]
-        else:  # lookup order, [B, F*D] inside a padded [B, F*D + 8] buffer
-            dX = torch.zeros(B, F * D + 8, dtype=torch.bfloat16)
-            dX[:, : F * D] = lookups.reshape(B, F * D)
-        dwide = torch.randn(B, generator=g) if wide else None
-        dXg = dX.to(dev)
-        ops.emb_rows_adagrad(dXg if sorted_rows else dXg[:, : F * D], dwide.to(dev) if wide else None, F, D, csr,
-                             U_dev, uniq, 0, t_gpu, s_gpu, s2_gpu, D if split else None, 0.05, 1e-8, ws,
-                             sorted_rows=sorted_rows)
-        cres = ops.plan_sorted(keys, base, bits, positions=True)
-        ccsr = tuple(cres[4:])
-        ops.emb_rows_adagrad(lookups[ccsr[0].long()].float().to(torch.bfloat16), dwide, F, D, ccsr, cres[3],
-                             cres[0], 0, t_ref, s_ref, s2_ref, D if split else None, 0.05, 1e-8, None)
-        torch.testing.assert_close(t_gpu.cpu(), t_ref, rtol=1e-4, atol=1e-5)
-        torch.testing.assert_close(s_gpu.cpu(), s_ref, rtol=1e-4, atol=1e-5)
-        if split:
-            torch.testing.assert_close(s2_gpu.cpu(), s2_ref, rtol=1e-4, atol=1e-5)
-        # the chunked hot rows leave their accumulators and tickets zero for the next call
-        assert int(ws[1].count_nonzero()) == 0 and int(ws[2].count_nonzero()) == 0
-        assert int(ws[0][:3].count_nonzero()) == 0  # counters re-zeroed by the hot kernel's last block
-
-
 def test_colsum_bf16(dev):
     """ops.colsum_add (bias gradient of a Linear) against the fp32 column sums."""
     g = torch.Generator().manual_seed(11)
@@ -578,6 +567,8 @@ def test_colsum_bf16(dev):
         ref = out + x.float().sum(0)
         got = ops.colsum_add(x.to(dev), out.to(dev))
         torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-3)
+        again = ops.colsum_add(x.to(dev), out.to(dev))  # one summation order: bit-identical
+        assert torch.equal(again.cpu(), got.cpu())
 
 
 @pytest.mark.parametrize("B,cards,P", [(16384, [3, 1460, 10131227, 583, 24, 2202608], 1),

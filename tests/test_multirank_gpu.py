@@ -88,10 +88,10 @@ def _widedeep_overlap_vs_sync(rank, world):
 def test_widedeep_overlap_matches_sync():
     out = run_world(_widedeep_overlap_vs_sync)
     for rank, (l0, l1, dd, de, dmean, emean) in out.items():
-        # (the bias-vector gradients are column sums with float atomics: a different summation order
-        # per run, which Adam amplifies over the steps -- 0.26 % at step 6 measured)
+        # (round 5: the bias column sums, the embedding segment sums and the owners' push sums have one
+        # fixed summation order -- no float atomics -- so the two schedules agree to the round-3 bound)
         for a, b in zip(l0, l1):
-            assert abs(a - b) <= 5e-3 * abs(a) + 1e-3, (rank, l0, l1)
+            assert abs(a - b) <= 2e-3 * abs(a) + 1e-3, (rank, l0, l1)
         # the two runs differ only in float-atomic summation order; Adam (lr 1e-3) turns a sign
         # flip of a near-zero gradient into a full-size step, so bound the max by 6 steps x 2 lr
         # and require the typical (mean) deviation to be tiny

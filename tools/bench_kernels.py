@@ -11,6 +11,11 @@
     python tools/bench_kernels.py nn    GPT-2 memory-bound kernels (LayerNorm, add, softmax-xent): TB/s
     python tools/bench_kernels.py emb   W&D embedding backward on a real Criteo-shaped plan
     python tools/bench_kernels.py plan  key planning: per-column sort vs hash dedupe + CSR
+    torchrun --nproc-per-node N tools/bench_kernels.py rccl [--min-mb 0.25 --max-mb 256]
+                                        RCCL bytes vs time per collective of the PS data plane
+                                        (reduce-scatter, all-gather, all-to-all, all-to-all-v),
+                                        bus GB/s against the 7 x 153 GB/s xGMI links of one GPU;
+                                        NCCL_ALGO / NCCL_PROTO / NCCL_* from the environment
 
 GEMM layouts: nt = forward (A [M,K], B [N,K]), nn = dgrad (B [K,N]), tn = wgrad (A [K,M],
 B [K,N], fp32 out; through ops.linear_wgrad, i.e. the model's split-K choice, unless
@@ -286,6 +291,96 @@ def cmd_plan(a):
         print(f"  all columns at {nb:2d} bits ({(nb + 3) // 4} passes): {t:.1f} us")
 
 
+XGMI_LINKS, XGMI_LINK_GBPS = 7, 153.0  # per MI355X: 7 links to the other 7 GPUs of the node
+
+
+def cmd_rccl(a):
+    """Bytes vs time of the PS data plane's collectives over RCCL (one process per GPU, torchrun).
+    For each message size (per-rank payload): median time of ``iters`` calls, algorithm bandwidth
+    (payload / time) and bus bandwidth -- the bytes each GPU moves over its links: (N-1)/N of the
+    payload for reduce-scatter / all-gather / all-to-all -- as a fraction of the 7-link bound. The
+    all-to-all-v uses a Zipf-like split (owner r gets ~1/(r+1) of the rows), the shape of an
+    unrouted sparse push; the routed tables' splits are near-uniform (plain all-to-all)."""
+    import json
+    import statistics
+    import time
+
+    import torch.distributed as dist
+
+    from minips_amd.ps.comm import init_distributed
+
+    comm = init_distributed()
+    N, rank, dev = comm.world, comm.rank, comm.device
+    if N < 2:
+        raise SystemExit("rccl: launch with torchrun --nproc-per-node N (N >= 2)")
+    env = {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_")) and "DEBUG" not in k}
+    sizes, mb = [], a.min_mb
+    while mb <= a.max_mb:
+        sizes.append(mb)
+        mb *= 2
+    bound = XGMI_LINKS * XGMI_LINK_GBPS
+    bf = torch.bfloat16 if dev.type == "cuda" else torch.float32  # (gloo plumbing runs: no bf16)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def run(op, n_bytes):
+        if op == "reduce_scatter":  # fp32 gradients, n_bytes per rank in, n_bytes / N out
+            n = max(N, (n_bytes // 4) // N * N)
+            inp, out = torch.ones(n, device=dev), torch.empty(n // N, device=dev)
+            fn, moved = (lambda: dist.reduce_scatter_tensor(out, inp)), n * 4 * (N - 1) / N
+        elif op == "all_gather":  # bf16 parameters, n_bytes per rank out
+            n = max(N, (n_bytes // 2) // N * N)
+            out, inp = torch.empty(n, dtype=bf, device=dev), torch.ones(n // N, dtype=bf,
+                                                                                    device=dev)
+            fn, moved = (lambda: dist.all_gather_into_tensor(out, inp)), n * 2 * (N - 1) / N
+        elif op == "all_to_all":  # bf16 rows, equal splits
+            n = max(N, (n_bytes // 2) // N * N)
+            inp, out = torch.ones(n, dtype=bf, device=dev), torch.empty(n, dtype=bf, device=dev)
+            fn, moved = (lambda: dist.all_to_all_single(out, inp)), n * 2 * (N - 1) / N
+        else:  # all_to_all_v: row splits ~ 1 / (owner + 1), 72-byte rows (W&D bf16 push rows)
+            rows = max(N, n_bytes // 72)
+            w = [1.0 / (r + 1) for r in range(N)]
+            send = [int(rows * x / sum(w)) for x in w]
+            send[0] += rows - sum(send)
+            # every rank sends the same split vector, so rank r receives send[r] rows from each peer
+            recv = [send[rank]] * N
+            inp = torch.ones(sum(send), 36, dtype=bf, device=dev)
+            out = torch.empty(sum(recv), 36, dtype=bf, device=dev)
+            fn = lambda: dist.all_to_all_single(out, inp, recv, send)  # noqa: E731
+            moved = (sum(send) - send[rank]) * 72
+        for _ in range(a.warmup):
+            fn()
+        sync()
+        ts = []
+        for _ in range(a.iters):
+            dist.barrier()
+            sync()
+            t0 = time.perf_counter()
+            fn()
+            sync()
+            ts.append(time.perf_counter() - t0)
+        t = torch.tensor([statistics.median(ts)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), moved
+
+    ops_ = a.ops.split(",")
+    if rank == 0:
+        print(f"# RCCL over {N} ranks, 7-link bound {bound:.0f} GB/s per GPU, env {json.dumps(env)}", flush=True)
+        print(f"{'op':16s} {'MB/rank':>9s} {'us':>10s} {'algo GB/s':>10s} {'bus GB/s':>9s} {'of bound':>8s}")
+    for op in ops_:
+        for mb in sizes:
+            n_bytes = int(mb * 2**20)
+            t, moved = run(op, n_bytes)
+            if rank == 0:
+                bus = moved / t / 1e9
+                print(f"{op:16s} {mb:9.2f} {t * 1e6:10.1f} {n_bytes / t / 1e9:10.1f} {bus:9.1f} {bus / bound:8.1%}",
+                      flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -316,6 +411,12 @@ def main(argv=None):
     sub.add_parser("nn")
     for name in ("emb", "plan"):
         sub.add_parser(name).add_argument("--batch", type=int, default=16384)
+    p = sub.add_parser("rccl")
+    p.add_argument("--min-mb", type=float, default=0.25)
+    p.add_argument("--max-mb", type=float, default=256.0)
+    p.add_argument("--iters", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--ops", default="reduce_scatter,all_gather,all_to_all,all_to_all_v")
     a = ap.parse_args(argv)
     from minips_amd import _native
 

@@ -8,6 +8,7 @@
 #     micro        isolated GPT-2 kernels: every GEMM shape vs hipBLASLt, memory-bound kernels, attention
 #     models       bench lines of the other BASELINE configs (MODELS, default "mlp dlrm dlrm-10b gpt2")
 #     models-prof  rocprofv3 kernel stats of those model steps (MODELS)
+#     emu          bench.py --emulate-world N (EMU_WORLDS, default "2 8") next to N=1, kernel trace of N=EMU_PROF
 # Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, MODES.
 set -eo pipefail
 cd "$(dirname "$0")/.."
@@ -70,4 +71,22 @@ if [[ $STAGE == models-prof ]]; then
     python tools/prof_summary.py stats $f 8 > gpurun_out/${m}_kernels.txt
     head -25 gpurun_out/${m}_kernels.txt
   done
+fi
+if [[ $STAGE == emu ]]; then
+  # the per-rank program of an N-rank step on this one GPU (bench.py --emulate-world: loopback
+  # collectives, wire time excluded) next to the one-rank step, then a kernel trace of the largest N
+  timeout -k 10 300 python bench.py --steps ${STEPS:-100} --warmup 10 ${BENCH_ARGS} > gpurun_out/emu_w1.log 2>&1 || { tail -30 gpurun_out/emu_w1.log; exit 1; }
+  grep "^{" gpurun_out/emu_w1.log | cut -c1-200
+  for w in ${EMU_WORLDS:-2 8}; do
+    timeout -k 10 300 python bench.py --steps ${STEPS:-100} --warmup 10 --emulate-world $w ${BENCH_ARGS} > gpurun_out/emu_w$w.log 2>&1 || { tail -30 gpurun_out/emu_w$w.log; exit 1; }
+    grep "^{" gpurun_out/emu_w$w.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('emulated', $w, d['ms_per_step'], 'ms/step', json.dumps(d.get('diag')))"
+  done
+  prof_env
+  w=${EMU_PROF:-8}
+  d=gpurun_out/emu_prof_w$w
+  rm -rf $d
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- python bench.py --steps 40 --warmup 10 --emulate-world $w --diag-steps 0 ${BENCH_ARGS} > $d.log 2>&1 || { tail -30 $d.log; exit 1; }
+  python tools/prof_summary.py stats $d/run_kernel_stats.csv 50 --top 40 > $d.stats.txt
+  python tools/prof_summary.py trace $d/run_kernel_trace.csv --anchor wd_head_kernel --skip 8 --top 40 > $d.trace.txt
+  head -60 $d.trace.txt
 fi
