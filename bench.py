@@ -250,7 +250,8 @@ def main():
         print(f"[profile] wall {wall * 1e3:.3f} ms/step (cProfile on), host issue median "
               f"{issue[len(issue) // 2] * 1e3:.3f} ms, min {issue[0] * 1e3:.3f}, max {issue[-1] * 1e3:.3f}",
               file=sys.stderr, flush=True)
-        pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(18)
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
     if n > 1 and comm.initialized:
         dist.barrier()
         dist.destroy_process_group()

@@ -129,28 +129,18 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
                           epi == minips_k::kEpiGeluGradBf16 || epi == minips_k::kEpiBiasGeluDAuxBf16 ||
                           epi == minips_k::kEpiMulAuxBf16;
   if (needs_mask) TORCH_CHECK(mask_p, "this epilogue needs mask/aux");
-  float* colsum_p = epi == minips_k::kEpiXentStatsBf16 ? opt_ptr<float>(colsum, at::kFloat, "colsum")
-                                                      : strided_vec_ptr(colsum, "colsum");
-  if (epi == minips_k::kEpiXentStatsBf16) {
-    // colsum = the softmax partials [M][ceil(N/64)] float2, seg = the vocabulary (valid columns)
-    ldmask = (int)((N + 63) / 64);
-    TORCH_CHECK(colsum_p && colsum->is_contiguous() && colsum->numel() >= M * ldmask * 2 && seg > 0 && seg <= N &&
-                    batch <= 1 && split_k <= 1,
-                "xent-stats epilogue: stats of >= M * ceil(N/64) * 2 floats, 0 < seg (vocab) <= N, no batch/split-K");
-  } else if (colsum_p) {
+  float* colsum_p = strided_vec_ptr(colsum, "colsum");
+  if (colsum_p) {
     // a 1-D view may be strided (a column of a weight-gradient matrix: the folded-bias column)
     TORCH_CHECK(colsum->dim() == 1 && colsum->numel() >= N && colsum->stride(0) >= 1, "colsum: 1-D, >= N values");
   }
-  const int colsum_ld = (colsum_p && epi != minips_k::kEpiXentStatsBf16) ? (int)colsum->stride(0) : 1;
+  const int colsum_ld = colsum_p ? (int)colsum->stride(0) : 1;
   c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
-  static const bool use_slab = [] {
-    const char* e = std::getenv("MINIPS_SPLITK_SLAB");
-    return !e || std::atoi(e) != 0;
-  }();
   at::Tensor slab;
   if (epi == minips_k::kEpiStoreBf16 && split_k > 1)
     TORCH_CHECK(batch <= 1 && N % 4 == 0 && ldc % 4 == 0, "split-K bf16 store: no batch, N % 4 == 0, ldc % 4 == 0");
-  if ((use_slab || epi == minips_k::kEpiStoreBf16) && split_k > 1 && batch <= 1 &&
+  // split-K slices land in fp32 slab planes and one reduce kernel adds them (deterministic, no atomics)
+  if (split_k > 1 && batch <= 1 &&
       (epi == minips_k::kEpiAtomicF32 || epi == minips_k::kEpiStoreBf16) && N % 4 == 0)
     slab = at::empty({split_k * M * N}, A.options().dtype(at::kFloat));  // caching allocator, stream-ordered
   minips_k::gemm_bf16_batched(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb,
@@ -504,40 +494,6 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
                     ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H));
 }
 
-// Last hidden layer + W&D head in one GEMM (minips_k::gemm_wd_head): A = H2 [B][>= K] bf16 (bias
-// column folded in), W = W3ext [N][>= K] bf16, w4 = [w | b] bf16 [>= N + 1], dw4 fp32 [>= N + 1].
-void wd_fwd_head(const at::Tensor& A, const at::Tensor& W, int64_t K, const at::Tensor& w4,
-                 const at::Tensor& wide_logit, const at::Tensor& labels, at::Tensor& dH, at::Tensor& dw4,
-                 at::Tensor& dwide, at::Tensor& loss_sum, double grad_scale,
-                 const c10::optional<at::Tensor>& dH_colsum, const c10::optional<at::Tensor>& bias) {
-  for (const at::Tensor* t : {&A, &W, &w4, &wide_logit, &labels, (const at::Tensor*)&dH, (const at::Tensor*)&dw4,
-                              (const at::Tensor*)&dwide, (const at::Tensor*)&loss_sum})
-    check_gpu(*t, "wd_fwd_head");
-  check_dtype(A, at::kBFloat16, "A");
-  check_dtype(W, at::kBFloat16, "W");
-  check_dtype(w4, at::kBFloat16, "w4");
-  check_dtype(dH, at::kBFloat16, "dH");
-  check_dtype(dw4, at::kFloat, "dw4");
-  check_dtype(wide_logit, at::kFloat, "wide_logit");
-  check_dtype(labels, at::kFloat, "labels");
-  check_dtype(dwide, at::kFloat, "dwide");
-  TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && dH.dim() == 2 && A.stride(1) == 1 && W.stride(1) == 1 &&
-                  dH.stride(1) == 1, "wd_fwd_head: 2-D operands with contiguous rows");
-  const int64_t M = A.size(0), N = W.size(0);
-  TORCH_CHECK(A.size(1) >= K && W.size(1) >= K && dH.size(0) == M && dH.size(1) >= N && w4.numel() >= N + 1 &&
-                  dw4.numel() >= N + 1 && wide_logit.numel() >= M && labels.numel() >= M && dwide.numel() >= M,
-              "wd_fwd_head shapes");
-  float* cs = strided_vec_ptr(dH_colsum, "dH_colsum");
-  if (cs) TORCH_CHECK(dH_colsum->numel() >= N, "dH_colsum: >= N values");
-  const bf16_t* bp = opt_ptr<bf16_t>(bias, at::kBFloat16, "bias");
-  if (bp) TORCH_CHECK(bias->numel() >= N, "bias: >= N values");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
-  minips_k::gemm_wd_head(ptr<bf16_t>(A), ptr<bf16_t>(W), (int)M, (int)N, (int)K, (int)A.stride(0), (int)W.stride(0),
-                         ptr<bf16_t>(dH), (int)dH.stride(0), ptr<bf16_t>(w4), ptr<float>(wide_logit),
-                         ptr<float>(labels), ptr<float>(dw4), ptr<float>(dwide), ptr<float>(loss_sum),
-                         (float)grad_scale, stream_of(A), cs, cs ? (int)dH_colsum->stride(0) : 1, bp);
-}
-
 // Lookup CSR grouped by unique row (members/memrow int32 [B*F]) for U (upper-bound) rows.
 std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t U,
                                       const c10::optional<at::Tensor>& zeroed, bool counts_ready) {
@@ -615,7 +571,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
 // Returns (uniq, inv, counts [1], U_dev [1], members, memrow).
 std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& col_base, const at::Tensor& col_bits,
                                     std::vector<int64_t> col_bits_host, int64_t route_mult, int64_t route_n,
-                                    const at::Tensor& bounds, bool with_positions, int64_t sort_mode) {
+                                    const at::Tensor& bounds, bool with_positions) {
   check_gpu(bounds, "bounds");
   check_dtype(bounds, at::kLong, "bounds");
   const int64_t P = bounds.numel() - 1;
@@ -654,25 +610,12 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
                         ptr<int64_t>(uniq), ptr<int64_t>(inv), members.data_ptr<int32_t>(), memrow.data_ptr<int32_t>(),
                         ptr<int64_t>(counts), stream_of(keys), with_positions ? pos.data_ptr<int32_t>() : nullptr,
                         rowstart.defined() ? rowstart.data_ptr<int32_t>() : nullptr,
-                        rowidx.defined() ? rowidx.data_ptr<int32_t>() : nullptr, (int)sort_mode);
+                        rowidx.defined() ? rowidx.data_ptr<int32_t>() : nullptr);
   // (members, memrow, positions or None, rowstart, rowidx or None) with one owner
   if (rowstart.defined())
     return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos, rowstart, rowidx};
   if (with_positions) return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow, pos};
   return {uniq, inv, counts.narrow(0, 0, P), counts.narrow(0, P, 1), members, memrow};
-}
-
-// A HIP stream whose kernels may only use the CUs set in `mask` (hipExtStreamCreateWithCUMask;
-// 32-bit words, bit i = CU i). Returned as an integer handle for torch.cuda.ExternalStream; the
-// stream lives for the process (the planning stream of a rank).
-int64_t cu_masked_stream(int64_t device, std::vector<int64_t> mask) {
-  TORCH_CHECK(!mask.empty(), "cu_masked_stream: empty mask");
-  std::vector<uint32_t> m(mask.begin(), mask.end());
-  c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
-  hipStream_t st = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data());
-  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
-  return reinterpret_cast<int64_t>(st);
 }
 
 // A dedicated HIP stream (hipStreamCreateWithPriority), returned as an integer handle for
@@ -697,7 +640,12 @@ void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
               "colsum: out >= N floats, N and the row stride multiples of 8");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "colsum: x must be 16-byte aligned");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  minips_k::colsum_bf16(ptr<bf16_t>(x), x.size(0), (int)x.size(1), (int)x.stride(0), ptr<float>(out), stream_of(x));
+  // the blocks' partial rows: a caching-allocator block on the stream (reused, no fill)
+  const int64_t strips = (x.size(1) + 63) / 64;
+  at::Tensor slab = at::empty({minips_k::colsum_chunks(x.size(0), (int)x.size(1)) * strips * 64},
+                              out.options().dtype(at::kFloat));
+  minips_k::colsum_bf16(ptr<bf16_t>(x), x.size(0), (int)x.size(1), (int)x.stride(0), ptr<float>(out),
+                        slab.data_ptr<float>(), stream_of(x));
 }
 
 void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g, double lr, double beta1,
@@ -980,24 +928,6 @@ void softmax_xent(at::Tensor& logits, int64_t V, const at::Tensor& labels, doubl
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   minips_k::softmax_xent(ptr<bf16_t>(logits), (int)logits.size(1), logits.size(0), (int)V, ptr<int64_t>(labels),
                          (float)scale, ptr<float>(loss_sum), c, stream_of(logits));
-}
-
-void xent_from_stats(at::Tensor& logits, int64_t V, const at::Tensor& stats, const at::Tensor& labels, double scale,
-                     at::Tensor& loss_sum, const c10::optional<at::Tensor>& correct) {
-  check_gpu(logits, "logits");
-  check_gpu(labels, "labels");
-  check_gpu(stats, "stats");
-  check_dtype(logits, at::kBFloat16, "logits");
-  check_dtype(labels, at::kLong, "labels");
-  check_dtype(stats, at::kFloat, "stats");
-  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous() && logits.size(1) >= V && labels.numel() == logits.size(0),
-              "xent_from_stats shapes");
-  const int64_t M = logits.size(0), nparts = (logits.size(1) + 63) / 64;
-  TORCH_CHECK(stats.is_contiguous() && stats.numel() >= M * nparts * 2, "xent_from_stats: stats [M][ceil(ld/64)][2]");
-  float* c = opt_ptr<float>(correct, at::kFloat, "correct");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
-  minips_k::xent_from_stats(ptr<bf16_t>(logits), (int)logits.size(1), M, (int)V, ptr<float>(stats), (int)nparts,
-                            ptr<int64_t>(labels), (float)scale, ptr<float>(loss_sum), c, stream_of(logits));
 }
 
 void causal_softmax_fwd(const at::Tensor& S, int64_t T, at::Tensor& P) {
@@ -1627,8 +1557,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("EPI_BIAS_GELU_BF16") = (int)minips_k::kEpiBiasGeluBf16;
   m.attr("EPI_BIAS_GELU_AUX_BF16") = (int)minips_k::kEpiBiasGeluAuxBf16;
   m.attr("EPI_GELU_GRAD_BF16") = (int)minips_k::kEpiGeluGradBf16;
-  m.def("gemm_set_v4_mode", [](int64_t m) { minips_k::gemm_set_v4_mode((int)m); });
-  m.def("gemm_set_fold", [](int64_t on) { minips_k::gemm_set_fold((int)on); });
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("a_km"), py::arg("b_kn"), py::arg("epi"), py::arg("bias"), py::arg("mask"), py::arg("colsum"),
         py::arg("alpha") = 1.0, py::arg("split_k") = 1, py::arg("batch") = 1, py::arg("inner") = 1,
@@ -1637,7 +1565,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("softmax_xent", &softmax_xent);
-  m.def("xent_from_stats", &xent_from_stats);
   m.def("new_stream", &new_stream);
   m.def("causal_softmax_fwd", &causal_softmax_fwd);
   m.def("causal_softmax_bwd", &causal_softmax_bwd);
@@ -1669,9 +1596,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1, py::arg("zero") = py::none());
   m.def("wd_head", &wd_head);
-  m.def("wd_fwd_head", &wd_fwd_head, py::arg("A"), py::arg("W"), py::arg("K"), py::arg("w4"), py::arg("wide_logit"),
-        py::arg("labels"), py::arg("dH"), py::arg("dw4"), py::arg("dwide"), py::arg("loss_sum"), py::arg("grad_scale"),
-        py::arg("dH_colsum") = py::none(), py::arg("bias") = py::none());
   m.def("wd_assemble_tab", &wd_assemble_tab);
   m.def("owner_slots", &owner_slots, py::arg("own_inv"), py::arg("splits"), py::arg("cap"));
   m.def("owner_rows_adagrad", &owner_rows_adagrad, py::arg("table"), py::arg("state"), py::arg("state2"),
@@ -1681,10 +1605,9 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("members") = py::none(),
         py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);
   m.def("colsum_bf16", &colsum_bf16);
-  m.def("cu_masked_stream", &cu_masked_stream);
   m.def("plan_sorted", &plan_sorted, py::arg("keys"), py::arg("col_base"), py::arg("col_bits"),
         py::arg("col_bits_host"), py::arg("route_mult"), py::arg("route_n"), py::arg("bounds"),
-        py::arg("with_positions") = false, py::arg("sort_mode") = -1);
+        py::arg("with_positions") = false);
   m.def("emb_build_csr", &emb_build_csr, py::arg("inv"), py::arg("F"), py::arg("U"), py::arg("zeroed") = py::none(),
         py::arg("counts_ready") = false);
   m.def("adam_apply", &adam_apply, py::arg("w"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("lr"),

@@ -517,20 +517,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   store_transposed(base + 2 * dmodel, lddq, kw, T, dv, 1.f, lane);
 }
 
-// MINIPS_ATTN_OCC=<fwd>,<dkv>: waves per SIMD of the forward (2 or 3) and the dK/dV kernel (1 or 2);
-// default 3,2 (2,1 = the uncapped allocation)
-struct AttnOcc {
-  int fwd = 3, dkv = 2;
-};
-static const AttnOcc& attn_occ() {
-  static const AttnOcc o = [] {
-    AttnOcc r;
-    if (const char* e = std::getenv("MINIPS_ATTN_OCC")) std::sscanf(e, "%d,%d", &r.fwd, &r.dkv);
-    return r;
-  }();
-  return o;
-}
-
 void check_attn(int T, int H, int dmodel, int ldq, int ldo) {
   if (dmodel != H * HD) throw std::runtime_error("attention: head dim must be 64");
   if (T <= 0 || ldq % 8 || ldo % 8) throw std::runtime_error("attention: leading dims must be multiples of 8");
@@ -542,10 +528,8 @@ void attn_fwd(const bf16_t* qkv, int ldq, int B, int T, int H, int dmodel, float
               hipStream_t s) {
   check_attn(T, H, dmodel, ldq, ldo);
   const int grid = ((T + BROWS - 1) / BROWS) * B * H;  // decoded as (block of T, head) in the kernels
-  if (attn_occ().fwd >= 3)
-    hipLaunchKernelGGL(attn_fwd_kernel<3>, grid, 256, 0, s, qkv, ldq, T, H, dmodel, scale * kLog2e, O, ldo, lse);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, 256, 0, s, qkv, ldq, T, H, dmodel, scale * kLog2e, O, ldo, lse);
+  // 3 waves per SIMD (the register cap of the template argument; 2 = the uncapped allocation, slower)
+  hipLaunchKernelGGL(attn_fwd_kernel<3>, grid, 256, 0, s, qkv, ldq, T, H, dmodel, scale * kLog2e, O, ldo, lse);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
@@ -560,12 +544,9 @@ void attn_bwd(const bf16_t* qkv, int ldq, const bf16_t* O, int ldo, const bf16_t
   hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel, scale * kLog2e,
                      scale, dqkv, lddq);
   MINIPS_HIP_CHECK(hipGetLastError());
-  if (attn_occ().dkv >= 2)
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<2>, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel,
-                       scale * kLog2e, scale, dqkv, lddq);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<1>, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel,
-                       scale * kLog2e, scale, dqkv, lddq);
+  // 2 waves per SIMD (1 = the uncapped allocation, slower)
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel<2>, grid, 256, 0, s, qkv, ldq, dO, lddo, lse, delta, T, H, dmodel,
+                     scale * kLog2e, scale, dqkv, lddq);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

@@ -10,41 +10,6 @@
 
 namespace minips_k {
 
-void gemm_set_v4_mode(int mode) { gemm_v4_mode_ref() = mode; }
-
-// split-K fold (kEpiFoldF32) instead of the separate slab reduce: MINIPS_SPLITK_FOLD=1 (default 0
-// until measured in the W&D step); gemm_set_fold() switches it at run time (in-process A/B)
-static int& fold_mode() {
-  static int m = [] {
-    const char* e = std::getenv("MINIPS_SPLITK_FOLD");
-    return e ? std::atoi(e) : 0;
-  }();
-  return m;
-}
-void gemm_set_fold(int on) { fold_mode() = on; }
-
-// per-(device, stream) tile ticket counters of the fold: zeroed once, re-zeroed by every tile's
-// last K slice, so back-to-back GEMMs on one stream reuse them (kernel boundaries order them)
-static unsigned* fold_counters(hipStream_t s, int64_t tiles) {
-  struct Entry {
-    int dev;
-    hipStream_t s;
-    unsigned* p;
-    int64_t n;
-  };
-  static thread_local std::vector<Entry> cache;
-  int dev = 0;
-  MINIPS_HIP_CHECK(hipGetDevice(&dev));
-  for (auto& e : cache)
-    if (e.dev == dev && e.s == s && e.n >= tiles) return e.p;
-  const int64_t n = std::max<int64_t>(tiles, 1 << 16);
-  unsigned* p = nullptr;
-  MINIPS_HIP_CHECK(hipMalloc(&p, n * sizeof(unsigned)));
-  MINIPS_HIP_CHECK(hipMemset(p, 0, n * sizeof(unsigned)));
-  cache.push_back({dev, s, p, n});
-  return p;
-}
-
 static int dispatch_layout(bool a_km, bool b_kn, int epi, const bf16_t* A, const bf16_t* B, int M, int N, int K,
                            int lda, int ldb, int split_k, const EpiArgs& ep, int batch, hipStream_t s) {
   if (!a_km && !b_kn) return gemm_dispatch<false, false>(epi, A, B, M, N, K, lda, ldb, split_k, ep, batch, s);
@@ -122,11 +87,6 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return;
   if (epi == kEpiPermRowsBf16 && (!perm || seg <= 0 || seg % 8 || N % seg || batch != 1 || split_k > 1))
     throw std::runtime_error("gemm: the permuted-rows epilogue needs perm, seg % 8 == 0, N % seg == 0, no batch");
-  if (epi == kEpiXentStatsBf16 &&
-      (!colsum || seg <= 0 || seg > N || ldmask < (N + 63) / 64 || a_km || b_kn || batch != 1 || split_k > 1 ||
-       gemm_impl() != 2 || !kLdsEpilogue))
-    throw std::runtime_error("gemm: the xent-stats epilogue needs stats [M][ceil(N/64)] float2, 0 < vocab <= N, "
-                             "the nt layout, no batch / split-K, the v2 kernel with the staged epilogue");
   if (split_k < 1) split_k = 1;
   if (split_k > 1 && epi != kEpiAtomicF32 && !(epi == kEpiStoreBf16 && slab))
     throw std::runtime_error("gemm: split_k needs the atomic epilogue (or a plain bf16 store with a slab)");
@@ -138,19 +98,6 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
     // split-K without atomics: every K slice stores its partial tile into its own slab plane,
     // one streaming kernel adds the planes into C (measured faster than fp32 atomics)
     EpiArgs sp{slab, N, nullptr, nullptr, 0, nullptr, alpha, 1, 0, 0, 0, 0, 0, 0, (int64_t)M * N, nullptr, 0};
-    if (!bf16_out && fold_mode()) {
-      // the K slices' planes fold inside the GEMM: the tile's last slice adds them into C
-      const int kper = (K + split_k - 1) / split_k;
-      const int kc = (kper + 63) / 64 * 64;
-      sp.fold_out = (float*)C;
-      sp.fold_ldc = ldc;
-      sp.fold_nsplit = (K + kc - 1) / kc;  // == the launcher's nsplit (v2: BK = 64 chunks)
-      sp.fold_cnt = fold_counters(s, (int64_t)((M + 127) / 128) * ((N + 127) / 128));
-      nsplit = dispatch_layout(a_km, b_kn, kEpiFoldF32, A, B, M, N, K, lda, ldb, split_k, sp, batch, s);
-      if (nsplit != sp.fold_nsplit) throw std::runtime_error("gemm: split-K fold slice count mismatch");
-      MINIPS_HIP_CHECK(hipGetLastError());
-      return;
-    }
     nsplit = dispatch_layout(a_km, b_kn, kEpiStoreF32, A, B, M, N, K, lda, ldb, split_k, sp, batch, s);
     MINIPS_HIP_CHECK(hipGetLastError());
     if (bf16_out)
@@ -165,12 +112,8 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
   EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i, 0, perm, seg};
   ep.colsum_ld = colsum_ld > 0 ? colsum_ld : 1;
   // an accumulating GEMM with one K slice has one writer per output element: read-add-write
-  // instead of memory-side fp32 atomics (MINIPS_GEMM_ACCUM=0 keeps the atomics)
-  static const bool accum_ok = [] {
-    const char* e = std::getenv("MINIPS_GEMM_ACCUM");
-    return !e || std::atoi(e) != 0;
-  }();
-  if (epi == kEpiAtomicF32 && split_k == 1 && accum_ok) epi = kEpiAccumF32;
+  // instead of memory-side fp32 atomics
+  if (epi == kEpiAtomicF32 && split_k == 1) epi = kEpiAccumF32;
   nsplit = dispatch_layout(a_km, b_kn, epi, A, B, M, N, K, lda, ldb, split_k, ep, batch, s);
   (void)nsplit;
   MINIPS_HIP_CHECK(hipGetLastError());
@@ -184,50 +127,6 @@ int gemm_slab(const bf16_t* A, const bf16_t* B, float* slab, int M, int N, int K
   const int nsplit = dispatch_layout(a_km, b_kn, kEpiStoreF32, A, B, M, N, K, lda, ldb, std::max(1, split_k), sp, 1, s);
   MINIPS_HIP_CHECK(hipGetLastError());
   return nsplit;
-}
-
-void gemm_wd_head(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, bf16_t* dH, int lddh,
-                  const bf16_t* w4, const float* wide, const float* labels, float* dw4, float* dwide, float* loss,
-                  float scale, hipStream_t s, float* dh_colsum, int dh_colsum_ld, const bf16_t* bias) {
-  if (M <= 0) return;
-  if (N <= 0 || N > 256 || N % 8 || K % 8 || lda % 8 || ldb % 8 || lddh % 8)
-    throw std::runtime_error("gemm_wd_head: N <= 256, N / K / leading dims multiples of 8");
-  const int64_t a_ext = (int64_t)(M - 1) * lda + K, b_ext = (int64_t)(N - 1) * ldb + K;
-  if (a_ext * 2 >= 0x7ff00000ll || b_ext * 2 >= 0x7ff00000ll)
-    throw std::runtime_error("gemm_wd_head: operands > 2 GiB");
-  EpiArgs ep{dH, lddh, w4, nullptr, 0, dw4, 1.f, 1, 0, 0, 0, 0, 0, 0, 0, nullptr, 0};
-  ep.head_wide = wide;
-  ep.head_label = labels;
-  ep.head_dwide = dwide;
-  ep.head_loss = loss;
-  ep.head_scale = scale;
-  ep.head_dh_colsum = dh_colsum;
-  ep.head_dh_colsum_ld = dh_colsum_ld;
-  ep.head_bias = bias;
-  // the two-level fold of the workgroups' partial rows (<= 256 workgroups: 16 groups of 16);
-  // per-device slab + tickets allocated once (tickets zero), before any capture
-  const int nwg = (M + 63) / 64;
-  if (nwg <= 256) {
-    static thread_local std::vector<std::pair<int, void*>> cache;
-    int dev = 0;
-    MINIPS_HIP_CHECK(hipGetDevice(&dev));
-    void* ws = nullptr;
-    for (auto& e : cache)
-      if (e.first == dev) ws = e.second;
-    const size_t slab_bytes = sizeof(float) * (256 + 16) * (2 * 256 + 2);
-    if (!ws) {
-      MINIPS_HIP_CHECK(hipMalloc(&ws, slab_bytes + 256));
-      MINIPS_HIP_CHECK(hipMemset(ws, 0, slab_bytes + 256));
-      cache.push_back({dev, ws});
-    }
-    ep.head_slab = static_cast<float*>(ws);
-    ep.head_ticket = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + slab_bytes);
-  }
-  // 64 x 256 tiles: a workgroup holds whole rows (all N columns), 4 waves side by side along N;
-  // 80 KiB of LDS -> 2 workgroups per CU, M / 64 workgroups (256 at the W&D batch)
-  hipLaunchKernelGGL((gemm_v2_kernel<64, 256, false, false, kEpiWdHead>), dim3((M + 63) / 64, 1, 1), dim3(256), 0, s,
-                     A, B, M, N, K, lda, ldb, K, ep);
-  MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,

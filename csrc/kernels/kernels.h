@@ -28,36 +28,14 @@ enum GemmEpilogue {
   // not split over K (every output element has exactly one writer), e.g. GPT-2's LM-head weight
   // gradient (38.6M fp32 outputs: memory-side atomics cost it 1.75 ms/step)
   kEpiAccumF32 = 10,
-  // C bf16 = acc (LM-head logits) plus softmax partials for the cross-entropy: for every row and
-  // every 64-column wave block, (max, sum 2^(y - max)) over its valid columns (< seg = vocab) in
-  // log2 units (y = bf16(acc) * log2 e), as a float2 at colsum[row * ldmask + col0 / 64]
-  // (ldmask = ceil(N / 64)); xent_from_stats then streams the gradient without a row reduction
-  kEpiXentStatsBf16 = 11,
-  // the W&D output head as the epilogue of the last hidden layer (gemm_wd_head only)
-  kEpiWdHead = 12,
   // C bf16 = gelu_tanh(u), aux bf16 = gelu'(u), u = acc + bias: the backward multiplies by the stored
   // derivative (kEpiMulAuxBf16) instead of re-evaluating tanh of the saved pre-activation
   kEpiBiasGeluDAuxBf16 = 13,
   kEpiMulAuxBf16 = 14,  // C bf16 = acc * mask(aux)
-  // split-K slab plane written through (sc1) + in-kernel fold: the last K slice of a tile to
-  // arrive adds the tile's nsplit planes into the fp32 output (no separate reduce launch; v2 only)
-  kEpiFoldF32 = 15,
 };
-// v4 GEMM selection at run time (in-process A/B): 0 off, 1 where 256x256 tiles are picked, 2 always
-void gemm_set_v4_mode(int mode);
-// split-K fold (kEpiFoldF32) instead of the slab reduce kernel: 0 off, 1 on (in-process A/B)
-void gemm_set_fold(int on);
 void gemm_bf16(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask, float* colsum,
                float alpha, int split_k, hipStream_t s);
-// W&D last hidden layer + output head in one kernel: H3 = relu(A B^T) (A [M][K] = H2 with the bias
-// column folded in, B [N][K] = W3ext, N <= 256) stays on chip; z = H3 . w4[:N] + w4[N] + wide,
-// dz = (sigmoid(z) - label) * scale -> dH [M][N] bf16 = (H3 > 0) * dz * w4, dw4[:N] += dz H3,
-// dw4[N] += dz, dwide = dz, loss += BCE-with-logits (same numerics as wd_head on a bf16 H3)
-void gemm_wd_head(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int ldb, bf16_t* dH, int lddh,
-                  const bf16_t* w4, const float* wide, const float* labels, float* dw4, float* dwide, float* loss,
-                  float scale, hipStream_t s, float* dh_colsum = nullptr, int dh_colsum_ld = 1,
-                  const bf16_t* bias = nullptr);  // bias: the hidden layer's bias vector (H3 = relu(. + bias))
 // Batched form: `batch` GEMMs, z = blockIdx.y; operand offsets are (z / inner) * s_outer +
 // (z % inner) * s_inner elements (e.g. attention heads inside a [B*T, H*dh] activation).
 void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
@@ -200,13 +178,13 @@ void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const i
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
-                 int32_t* pos = nullptr, int32_t* rowstart = nullptr, int32_t* rowidx = nullptr,
-                 int sort_mode = -1);
-// (sort_mode: 1 = one workgroup per column, 4 = the chunked sort, -1 = MINIPS_PLAN_SORT / default)
+                 int32_t* pos = nullptr, int32_t* rowstart = nullptr, int32_t* rowidx = nullptr);
 // (pos, nullable: pos[members[m]] = m, emb_csr_positions fused; rowstart, nullable, one owner only:
 // rowstart[u] = first member of row u, rowstart[U] = B*F)
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.
-void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s);
+// slab: colsum_chunks(M, N) * ceil(N / 64) * 64 floats of scratch (the blocks' partial rows).
+void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, float* slab, hipStream_t s);
+int64_t colsum_chunks(int64_t M, int N);
 
 // ------------------------------------------------------------------ optimizers (optim.hip)
 // Fused Adam(W) on an fp32 master shard; optionally writes the bf16 copy for all-gather.
@@ -258,11 +236,6 @@ void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t
                    const float* mean, const float* rstd, bf16_t* dx, int lddx, float* dgamma, float* dbeta,
                    float* partial, bool accumulate_dx, hipStream_t s);
 // In place: logits [M, ld] bf16 become (softmax - onehot) * scale; loss_sum += sum CE.
-// Cross-entropy from the LM-head GEMM's kEpiXentStatsBf16 partials: lse per row from the [M][nparts]
-// float2 partials, loss_sum += sum CE (correct += argmax hits), then logits[:, :V] <- (softmax -
-// onehot) * scale and logits[:, V:ld) <- 0 in one streaming pass.
-void xent_from_stats(bf16_t* logits, int ld, int64_t M, int V, const float* stats, int nparts, const int64_t* labels,
-                     float scale, float* loss_sum, float* correct, hipStream_t s);
 void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,
                   float* correct, hipStream_t s);
 void causal_softmax_fwd(const float* S, int64_t rows, int T, bf16_t* P, hipStream_t s);

@@ -114,87 +114,11 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16_t* __rest
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma. dgamma/dbeta: every lane
-// accumulates its own columns in registers over the wave's rows, the 4 waves of a block combine
-// in LDS and the block writes one partial row [2C] (no atomics); layernorm_colsum adds the
-// partials into dgamma/dbeta.
-__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __restrict__ x, int ldx,
-                                                            const bf16_t* __restrict__ dy, int lddy, int64_t M, int C,
-                                                            const bf16_t* __restrict__ gamma,
-                                                            const float* __restrict__ mean,
-                                                                const float* __restrict__ rstd,
-                                                            bf16_t* __restrict__ dx, int lddx,
-                                                            float* __restrict__ partial, bool accumulate_dx) {
-  __shared__ float red[4][2][1024];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  float gm[kLnK][4], ag[kLnK][4], ab[kLnK][4];
-#pragma unroll
-  for (int k = 0; k < kLnK; ++k) {
-    const int c = k * 256 + lane * 4;
-    if (c < C) ld4(gamma + c, gm[k]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ag[k][q] = ab[k][q] = 0.f;
-  }
-  for (int64_t r = wave; r < M; r += nw) {
-    const float mu = mean[r], rs = rstd[r];
-    float xh[kLnK][4], g[kLnK][4];
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int k = 0; k < kLnK; ++k) {
-      const int c = k * 256 + lane * 4;
-      if (c < C) {
-        float d[4];
-        ld4(x + r * ldx + c, xh[k]);
-        ld4(dy + r * lddy + c, d);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          xh[k][q] = (xh[k][q] - mu) * rs;
-          g[k][q] = d[q] * gm[k][q];
-          a += g[k][q];
-          b += g[k][q] * xh[k][q];
-          ag[k][q] += d[q] * xh[k][q];
-          ab[k][q] += d[q];
-        }
-      }
-    }
-    a = warp_sum(a) / C;
-    b = warp_sum(b) / C;
-#pragma unroll
-    for (int k = 0; k < kLnK; ++k) {
-      const int c = k * 256 + lane * 4;
-      if (c < C) {
-        float o[4], prev[4];
-        if (accumulate_dx) ld4(dx + r * lddx + c, prev);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = rs * (g[k][q] - a - xh[k][q] * b) + (accumulate_dx ? prev[q] : 0.f);
-        st4(dx + r * lddx + c, o);
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kLnK; ++k) {
-    const int c = k * 256 + lane * 4;
-    if (c < C) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        red[w][0][c + q] = ag[k][q];
-        red[w][1][c + q] = ab[k][q];
-      }
-    }
-  }
-  __syncthreads();
-  float* out = partial + (int64_t)blockIdx.x * 2 * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    out[c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-    out[C + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-  }
-}
-
-// One wave per block, no LDS: the wave's column partials go straight to its partial row. The
-// 4-wave variant above combines its waves in 32 KB of LDS, so beside a 256x256 GEMM workgroup
-// (128 KB) only one of its blocks fits a CU; in GPT-2's backward it runs next to the side
-// stream's weight-gradient GEMMs (the default; MINIPS_LN_BWD_WAVE=0 selects the 4-wave kernel).
+// accumulates its own columns in registers over the wave's rows (no atomics). One wave per block,
+// no LDS: the wave's column partials go straight to its partial row and layernorm_colsum adds the
+// partials into dgamma/dbeta. (Round 4's 4-wave LDS-combining variant needed 32 KB of LDS, so
+// beside a 256x256 GEMM workgroup (128 KB) only one of its blocks fit a CU; in GPT-2's backward it
+// runs next to the side stream's weight-gradient GEMMs and lost: profiles/r4/ab_gpt2_ln_bwd.txt.)
 __global__ __launch_bounds__(64) void layernorm_bwd_wave_kernel(const bf16_t* __restrict__ x, int ldx,
                                                                 const bf16_t* __restrict__ dy, int lddy, int64_t M,
                                                                 int C, const bf16_t* __restrict__ gamma,
@@ -289,40 +213,14 @@ __global__ __launch_bounds__(256) void layernorm_colsum_kernel(const float* __re
   }
 }
 
-// ~8 rows per 4-wave block: 4x the waves of a 32-rows-per-block split, so the row loop's
-// dependent load -> reduce -> store chain is hidden by occupancy instead of serialised.
-// MINIPS_LN_BWD_ROWS / MINIPS_LN_BWD_MAXB override the rows per block and the block cap (A/B knobs).
-static int ln_bwd_blocks4(int64_t M) {
-  auto knob = [](const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::max(1, atoi(e)) : dflt;
-  };
-  static const int rows = knob("MINIPS_LN_BWD_ROWS", 8);
-  static const int cap = knob("MINIPS_LN_BWD_MAXB", 1024);
-  return (int)std::min<int64_t>(std::max<int64_t>((M + rows - 1) / rows, 1), cap);
-}
-
-// one-wave variant (default; MINIPS_LN_BWD_WAVE=0: the 4-wave LDS-combining kernel), 8 rows per
-// wave (MINIPS_LN_BWD_WROWS): GPT-2 12.69-12.70 vs 12.74-12.75 ms/step (4 rows 12.86, 16 rows
-// 13.2; profiles/r4/ab_gpt2_ln_bwd.txt). Its blocks are the partial rows.
-static bool ln_bwd_wave() {
-  static const bool on = [] {
-    const char* e = std::getenv("MINIPS_LN_BWD_WAVE");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on;
-}
-
+// 8 rows per wave: GPT-2 12.69-12.70 vs 12.74-12.75 ms/step (4 rows 12.86, 16 rows 13.2;
+// profiles/r4/ab_gpt2_ln_bwd.txt). Its blocks are the partial rows.
 static int ln_bwd_wave_blocks(int64_t M) {
-  static const int rows = [] {
-    const char* e = std::getenv("MINIPS_LN_BWD_WROWS");
-    return e ? std::max(1, std::atoi(e)) : 8;
-  }();
-  return (int)std::min<int64_t>(std::max<int64_t>((M + rows - 1) / rows, 1), 4096);
+  return (int)std::min<int64_t>(std::max<int64_t>((M + 7) / 8, 1), 4096);
 }
 
 // partial rows of layernorm_bwd (the scratch it needs: rows * 2 * C floats)
-int layernorm_bwd_blocks(int64_t M) { return ln_bwd_wave() ? ln_bwd_wave_blocks(M) : ln_bwd_blocks4(M); }
+int layernorm_bwd_blocks(int64_t M) { return ln_bwd_wave_blocks(M); }
 
 void layernorm_fwd(const bf16_t* x, int ldx, int64_t M, int C, const bf16_t* gamma, const bf16_t* beta, float eps,
                    bf16_t* y, int ldy, float* mean, float* rstd, hipStream_t s) {
@@ -338,14 +236,9 @@ void layernorm_bwd(const bf16_t* x, int ldx, const bf16_t* dy, int lddy, int64_t
                    float* partial, bool accumulate_dx, hipStream_t s) {
   if (M <= 0) return;
   if (C > 1024 || C % 4) throw std::runtime_error("layernorm: C <= 1024 and C % 4 == 0");
-  const bool wave = ln_bwd_wave();
-  const int G = wave ? ln_bwd_wave_blocks(M) : ln_bwd_blocks4(M);
-  if (wave)
-    hipLaunchKernelGGL(layernorm_bwd_wave_kernel, G, 64, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx,
-                       partial, accumulate_dx);
-  else
-    hipLaunchKernelGGL(layernorm_bwd_kernel, G, 256, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx,
-                       partial, accumulate_dx);
+  const int G = ln_bwd_wave_blocks(M);
+  hipLaunchKernelGGL(layernorm_bwd_wave_kernel, G, 64, 0, s, x, ldx, dy, lddy, M, C, gamma, mean, rstd, dx, lddx,
+                     partial, accumulate_dx);
   MINIPS_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(layernorm_colsum_kernel, dim3((2 * C + 63) / 64, G >= 64 ? kColsumSlices : 1), 256, 0, s,
                      partial, G, C, dgamma, dbeta);
@@ -563,97 +456,6 @@ __global__ __launch_bounds__(256) void softmax_xent_small_kernel(bf16_t* __restr
     atomicAdd(loss_sum, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
     if (correct) atomicAdd(correct, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
   }
-}
-
-// Cross-entropy from the LM-head GEMM's per-64-column softmax partials (kEpiXentStatsBf16): the
-// row reduction already happened in the GEMM epilogue, so this is a pure stream -- one read and one
-// write of the logits at full occupancy (256-thread blocks, few VGPRs, no row in registers):
-//   1. lse of the row from its nparts float2 partials (a strided merge + one block reduction)
-//   2. the label's logit read, the loss / hit folded into the block's thread-0 accumulators
-//   3. g = (2^(x L2E - lse) - onehot) * scale over 8-column chunks, 4 chunks in flight per thread;
-//      columns [V, ld) are zeroed
-// A block walks rows r = blockIdx.x + k * gridDim.x (one loss atomic per block).
-constexpr int kXsThreads = 256, kXsUnroll = 4;
-__global__ __launch_bounds__(kXsThreads) void xent_from_stats_kernel(bf16_t* __restrict__ logits, int ld, int64_t M,
-                                                                     int V, const float2* __restrict__ stats,
-                                                                     int nparts, const int64_t* __restrict__ labels,
-                                                                     float scale, float* loss_sum, float* correct) {
-  __shared__ float red_m[kXsThreads / 64], red_s[kXsThreads / 64];
-  const float L2E = 1.4426950408889634f;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int nch = ld >> 3;
-  float loss_acc = 0.f, hit_acc = 0.f;
-  for (int64_t r = blockIdx.x; r < M; r += gridDim.x) {
-    bf16_t* row = logits + r * ld;
-    const float2* st = stats + r * nparts;
-    float m = -1.0e30f, sm = 0.f;
-    for (int p = threadIdx.x; p < nparts; p += kXsThreads) {
-      const float2 v = st[p];
-      lse_merge(m, sm, v.x, v.y);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) lse_merge(m, sm, __shfl_xor(m, o, 64), __shfl_xor(sm, o, 64));
-    const int64_t lab = labels[r];
-    const bool has_lab = lab >= 0 && lab < V;
-    float zl = 0.f;
-    if (threadIdx.x == 0 && has_lab) zl = bf2f(row[lab]);  // before any thread rewrites the row
-    __syncthreads();  // the previous row's readers of red_* are done
-    if (lane == 0) {
-      red_m[w] = m;
-      red_s[w] = sm;
-    }
-    __syncthreads();
-    float M2 = red_m[0], S2 = red_s[0];
-#pragma unroll
-    for (int i = 1; i < kXsThreads / 64; ++i) lse_merge(M2, S2, red_m[i], red_s[i]);
-    const float lse2 = M2 + __log2f(S2);
-    if (threadIdx.x == 0 && has_lab) {
-      loss_acc += lse2 / L2E - zl;
-      hit_acc += zl * L2E >= M2 ? 1.f : 0.f;
-    }
-    const int lch = has_lab ? (int)(lab >> 3) : -1, lq = (int)(lab & 7);
-    for (int c0 = threadIdx.x; c0 < nch; c0 += kXsThreads * kXsUnroll) {
-      uint4 v[kXsUnroll];
-#pragma unroll
-      for (int u = 0; u < kXsUnroll; ++u) {
-        const int ch = c0 + u * kXsThreads;
-        v[u] = ch < nch ? *reinterpret_cast<const uint4*>(row + ch * 8) : make_uint4(0u, 0u, 0u, 0u);
-      }
-#pragma unroll
-      for (int u = 0; u < kXsUnroll; ++u) {
-        const int ch = c0 + u * kXsThreads;
-        if (ch >= nch) continue;
-        uint32_t o[4];
-#pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2) {
-          const int c = ch * 8 + 2 * q2;
-          float g0 = c < V ? __builtin_amdgcn_exp2f(u4elem(v[u], 2 * q2) * L2E - lse2) * scale : 0.f;
-          float g1 = c + 1 < V ? __builtin_amdgcn_exp2f(u4elem(v[u], 2 * q2 + 1) * L2E - lse2) * scale : 0.f;
-          if (ch == lch) {  // the -onehot term, folded before rounding
-            if (lq == 2 * q2) g0 -= scale;
-            if (lq == 2 * q2 + 1) g1 -= scale;
-          }
-          o[q2] = pack_bf2(g0, g1);
-        }
-        *reinterpret_cast<uint4*>(row + ch * 8) = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-    }
-  }
-  if (threadIdx.x == 0) {
-    atomicAdd(loss_sum, loss_acc);
-    if (correct) atomicAdd(correct, hit_acc);
-  }
-}
-
-void xent_from_stats(bf16_t* logits, int ld, int64_t M, int V, const float* stats, int nparts, const int64_t* labels,
-                     float scale, float* loss_sum, float* correct, hipStream_t s) {
-  if (M <= 0) return;
-  if (ld % 8 || V <= 0 || V > ld || nparts <= 0) throw std::runtime_error("xent_from_stats: ld % 8 == 0, 0 < V <= ld");
-  // ~8 blocks of 4 waves per CU at full occupancy; each block walks M / grid rows
-  const int grid = (int)std::min<int64_t>(M, 2048);
-  hipLaunchKernelGGL(xent_from_stats_kernel, grid, kXsThreads, 0, s, logits, ld, M, V,
-                     reinterpret_cast<const float2*>(stats), nparts, labels, scale, loss_sum, correct);
-  MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 void softmax_xent(bf16_t* logits, int ld, int64_t M, int V, const int64_t* labels, float scale, float* loss_sum,

@@ -225,263 +225,20 @@ __global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const uint32_
   if (t == 0) ucount[f] = (int32_t)total;
 }
 
-// ---- the same column sort spread over 4 workgroups per column (F x 4 = 104 for W&D instead of
-// 26 one-CU workgroups holding 128 KB of LDS each: beside a 256x256 GEMM those left the GEMM's
-// 256 tiles a second round). Three launches:
-//   plan_sort_chunk  (F, ceil(B / 4096)) x 256 threads: each 4096-lookup chunk of a column LSD
-//                    radix-sorted in 32 KB of LDS (the algorithm of plan_sort_col at 256 threads)
-//                    -> chunk-sorted keys ck / row ids cv
-//   plan_merge       (F, chunks) x 256: every chunk's keys of the column in LDS; an item's merged
-//                    position = its chunk rank + its rank in each other chunk (binary search for
-//                    a thread's first item, then a merge walk over its 16 consecutive items; ties
-//                    ordered by chunk: stable) -> merged keys mk, sorted_b
-//   plan_heads       F x 1024: run heads of mk, block scan -> local_u, ukey, ucount
-constexpr int kPcThreads = 256, kPcItems = 16, kPcChunk = kPcThreads * kPcItems;  // 4096 lookups
-
-// exclusive scan of one value per thread over a T-thread block (T/64 <= 64 waves); *total = sum
-template <int T>
-__device__ __forceinline__ uint32_t pc_block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
-  constexpr int NW = T / 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) ws[wave] = x;
-  __syncthreads();
-  if (wave == 0) {
-    const uint32_t w = lane < NW ? ws[lane] : 0u;
-    uint32_t s = w;
-#pragma unroll
-    for (int o = 1; o < NW; o <<= 1) {
-      const uint32_t y = __shfl_up(s, o, 64);
-      if (lane >= o) s += y;
-    }
-    if (lane < NW) ws[lane] = s - w;
-    if (lane == NW - 1) ws[NW] = s;
-  }
-  __syncthreads();
-  const uint32_t res = ws[wave] + x - v;
-  *total = ws[NW];
-  __syncthreads();
-  return res;
-}
-
-__global__ __launch_bounds__(kPcThreads) void plan_sort_chunk_kernel(const uint32_t* __restrict__ krel, int B,
-                                                                     const int32_t* __restrict__ col_bits,
-                                                                     uint32_t* __restrict__ ck,
-                                                                     int32_t* __restrict__ cv) {
-  __shared__ __attribute__((aligned(16))) uint16_t cnt[16 * kPcThreads];
-  __shared__ __attribute__((aligned(16))) uint32_t skey[kPcChunk];
-  __shared__ __attribute__((aligned(16))) uint16_t sval[kPcChunk];
-  __shared__ uint32_t ws[8];
-  const int t = threadIdx.x, f = blockIdx.x, c = blockIdx.y;
-  const int c0 = c * kPcChunk, len = min(kPcChunk, B - c0);
-  const int nbits = col_bits[f];
-  const uint32_t* col = krel + (int64_t)f * B + c0;
-  uint32_t k[kPcItems], v[kPcItems];
-  if ((B & 3) == 0 && t * kPcItems + kPcItems <= len) {
-    const uint4* p = reinterpret_cast<const uint4*>(col + t * kPcItems);  // krel and c0 16-byte aligned
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint4 u = p[e];
-      k[4 * e] = u.x;
-      k[4 * e + 1] = u.y;
-      k[4 * e + 2] = u.z;
-      k[4 * e + 3] = u.w;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < kPcItems; ++q) {
-      const int i = t * kPcItems + q;
-      k[q] = i < len ? col[i] : 0xffffffffu;  // padding sorts behind every real item (stable)
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < kPcItems; ++q) v[q] = (uint32_t)(c0 + t * kPcItems + q);
-  for (int shift = 0; shift < nbits; shift += 4) {
-    uint64_t lo = 0, hi = 0;
-#pragma unroll
-    for (int q = 0; q < kPcItems; ++q) {
-      const int d = (int)((k[q] >> shift) & 15u);
-      if (d < 8) lo += 1ull << (8 * d);
-      else hi += 1ull << (8 * (d - 8));
-    }
-#pragma unroll
-    for (int d = 0; d < 16; ++d) cnt[d * kPcThreads + t] = (uint16_t)ps_count(lo, hi, d);
-    __syncthreads();
-    uint4* cvv = reinterpret_cast<uint4*>(cnt) + 2 * t;
-    const uint4 q0 = cvv[0], q1 = cvv[1];
-    const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-    uint32_t o[8];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t a = w[e] & 0xffffu, b = w[e] >> 16;
-      o[e] = sum | ((sum + a) << 16);
-      sum += a + b;
-    }
-    uint32_t tot;
-    const uint32_t pre = pc_block_scan<kPcThreads>(sum, ws, &tot);
-    const uint32_t pre2 = pre | (pre << 16);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] += pre2;
-    cvv[0] = make_uint4(o[0], o[1], o[2], o[3]);
-    cvv[1] = make_uint4(o[4], o[5], o[6], o[7]);
-    __syncthreads();
-    uint64_t slo = 0, shi = 0;
-#pragma unroll
-    for (int q = 0; q < kPcItems; ++q) {
-      const int d = (int)((k[q] >> shift) & 15u);
-      const uint32_t r = ps_count(slo, shi, d);
-      if (d < 8) slo += 1ull << (8 * d);
-      else shi += 1ull << (8 * (d - 8));
-      const uint32_t pos = (uint32_t)cnt[d * kPcThreads + t] + r;
-      skey[pos] = k[q];
-      sval[pos] = (uint16_t)v[q];
-    }
-    __syncthreads();
-    {
-      const uint4* kp = reinterpret_cast<const uint4*>(skey + t * kPcItems);
-      const uint4* vp = reinterpret_cast<const uint4*>(sval + t * kPcItems);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint4 u = kp[e];
-        k[4 * e] = u.x;
-        k[4 * e + 1] = u.y;
-        k[4 * e + 2] = u.z;
-        k[4 * e + 3] = u.w;
-      }
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const uint4 u = vp[e];
-        const uint32_t w2[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          v[8 * e + 2 * h] = w2[h] & 0xffffu;
-          v[8 * e + 2 * h + 1] = w2[h] >> 16;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  uint32_t* ko = ck + (int64_t)f * B + c0;
-  int32_t* vo = cv + (int64_t)f * B + c0;
-#pragma unroll
-  for (int q = 0; q < kPcItems; ++q) {
-    const int i = t * kPcItems + q;
-    if (i < len) {
-      ko[i] = k[q];
-      vo[i] = (int32_t)v[q];
-    }
-  }
-}
-
-// smallest i in [p, n) with !go(a[i]) (n if none), go(x) = x <= key (UPPER) / x < key: galloping
-// from p (doubling steps, then a binary search), so a cursor that moves by d costs O(log d) reads --
-// a low-cardinality column puts thousands of equal keys between a thread's consecutive items
-template <bool UPPER>
-__device__ __forceinline__ int pc_gallop(const uint32_t* a, int p, int n, uint32_t key) {
-  auto go = [&](int i) { return UPPER ? a[i] <= key : a[i] < key; };
-  if (p >= n || !go(p)) return p;
-  int lo = p, step = 1, hi = p + 1;  // go(lo); hi: the next probe
-  while (hi < n && go(hi)) {
-    lo = hi;
-    step <<= 1;
-    hi = lo + step;
-  }
-  if (hi > n) hi = n;  // now hi == n or !go(hi)
-  int l = lo + 1, r = hi;
-  while (l < r) {
-    const int m = (l + r) >> 1;
-    if (go(m)) l = m + 1;
-    else r = m;
-  }
-  return l;
-}
-
-constexpr int kPmMaxChunks = kPsMax / kPcChunk;  // 4
-
-__global__ __launch_bounds__(kPcThreads) void plan_merge_kernel(const uint32_t* __restrict__ ck,
-                                                                const int32_t* __restrict__ cv, int B,
-                                                                uint32_t* __restrict__ mk,
-                                                                int32_t* __restrict__ sorted_b) {
-  __shared__ __attribute__((aligned(16))) uint32_t keys[kPsMax];
-  const int t = threadIdx.x, f = blockIdx.x, c = blockIdx.y, nch = gridDim.y;
-  const uint32_t* col = ck + (int64_t)f * B;
-  for (int i = t; i < B; i += kPcThreads) keys[i] = col[i];
-  __syncthreads();
-  const int c0 = c * kPcChunk, len = min(kPcChunk, B - c0);
-  const int i0 = t * kPcItems;
-  if (i0 >= len) return;
-  const int cnt = min(kPcItems, len - i0);
-  // cursors into the other chunks, advanced by galloping from item to item
-  int cur[kPmMaxChunks] = {0, 0, 0, 0};
-  uint32_t* mko = mk + (int64_t)f * B;
-  int32_t* sbo = sorted_b + (int64_t)f * B;
-  const int32_t* cvi = cv + (int64_t)f * B + c0;
-  for (int q = 0; q < cnt; ++q) {
-    const int i = i0 + q;
-    const uint32_t key = keys[c0 + i];
-    int pos = i;
-    for (int o = 0; o < nch; ++o) {
-      if (o == c) continue;
-      const int o0 = o * kPcChunk, ol = min(kPcChunk, B - o0);
-      // equal keys of earlier chunks come first (stable)
-      const int p = o < c ? pc_gallop<true>(keys + o0, cur[o], ol, key) : pc_gallop<false>(keys + o0, cur[o], ol, key);
-      cur[o] = p;
-      pos += p;
-    }
-    mko[pos] = key;
-    sbo[pos] = cvi[i];
-  }
-}
-
-__global__ __launch_bounds__(kPsThreads) void plan_heads_kernel(const uint32_t* __restrict__ mk, int B,
-                                                                const int64_t* __restrict__ col_base,
-                                                                int32_t* __restrict__ local_u,
-                                                                int64_t* __restrict__ ukey,
-                                                                int32_t* __restrict__ ucount) {
-  __shared__ uint32_t ws[20];
-  const int t = threadIdx.x, f = blockIdx.x;
-  const int64_t base = col_base[f];
-  const uint32_t* col = mk + (int64_t)f * B;
-  uint32_t k[kPsItems];
-#pragma unroll
-  for (int q = 0; q < kPsItems; ++q) {
-    const int i = t * kPsItems + q;
-    k[q] = i < B ? col[i] : 0u;
-  }
-  const int first = t * kPsItems;
-  const uint32_t before = (first > 0 && first < B) ? col[first - 1] : 0u;
-  uint32_t heads = 0;
-#pragma unroll
-  for (int q = 0; q < kPsItems; ++q) {
-    const int pos = first + q;
-    const uint32_t prev = q == 0 ? before : k[q - 1];
-    heads += (pos < B && (pos == 0 || k[q] != prev)) ? 1u : 0u;
-  }
-  uint32_t total;
-  uint32_t run = pc_block_scan<kPsThreads>(heads, ws, &total);
-  const int64_t col0 = (int64_t)f * B;
-#pragma unroll
-  for (int q = 0; q < kPsItems; ++q) {
-    const int pos = first + q;
-    if (pos >= B) break;
-    const uint32_t prev = q == 0 ? before : k[q - 1];
-    const bool h = pos == 0 || k[q] != prev;
-    if (h) ++run;
-    const uint32_t lu = run - 1;
-    local_u[col0 + pos] = (int32_t)lu;
-    if (h) ukey[col0 + lu] = base + (int64_t)k[q];
-  }
-  if (t == 0) ucount[f] = (int32_t)total;
-}
-
+// (key * mult) mod rn. The 64-bit integer remainder is a long software routine on the GPU; for the
+// tables' sizes (product < 2^62, rn >= 2^20) a double-precision quotient is off by at most one
+// (relative error <= 2^-52 of a quotient < 2^42), fixed by one correction step each way: exact.
 __device__ __forceinline__ int64_t ps_route(int64_t key, uint64_t mult, uint64_t rn) {
-  return mult ? (int64_t)(((uint64_t)key * mult) % rn) : key;
+  if (!mult) return key;
+  const uint64_t prod = (uint64_t)key * mult;
+  if (prod < (1ull << 62) && rn >= (1ull << 20)) {
+    const int64_t q = (int64_t)((double)prod / (double)rn);
+    int64_t r = (int64_t)prod - q * (int64_t)rn;
+    if (r < 0) r += (int64_t)rn;
+    if (r >= (int64_t)rn) r -= (int64_t)rn;
+    return r;
+  }
+  return (int64_t)(prod % rn);
 }
 
 // column prefix of the unique counts (F <= 64), computed per block; returns U
@@ -515,9 +272,13 @@ __device__ __forceinline__ int ps_owner(const int64_t* bounds, int P, int64_t k)
 // routed key of global unique index u (column-major: column c holds [basef[c], basef[c+1]))
 __device__ __forceinline__ int64_t ps_ukey_routed(int64_t u, int F, int B, const int64_t* basef,
                                                   const int64_t* __restrict__ ukey, uint64_t rmult, uint64_t rn) {
-  int c = 0;
-  while (c + 1 < F && basef[c + 1] <= u) ++c;
-  return ps_route(ukey[(int64_t)c * B + (u - basef[c])], rmult, rn);
+  int lo = 0, hi = F;  // basef[lo] <= u < basef[hi] (binary search: F = 26 in W&D)
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (basef[mid] <= u) lo = mid;
+    else hi = mid;
+  }
+  return ps_route(ukey[(int64_t)lo * B + (u - basef[lo])], rmult, rn);
 }
 
 // ---- several owners (multi-rank tables): the unique keys are regrouped by owner shard with a
@@ -548,66 +309,61 @@ __global__ __launch_bounds__(256) void plan_owner_count_kernel(int B, int F, con
 }
 
 // one block: ooff[chunk][p] = (keys of owners < p) + (keys of owner p in earlier chunks);
-// counts[p] = keys of owner p, counts[P] = U
+// counts[p] = keys of owner p, counts[P] = U. Every thread loads its chunks' P counts at once (one
+// memory round trip; the per-owner loop of loads and barriers was a 23 us latency chain), then one
+// wave scan per owner in registers and one LDS exchange across the 4 waves.
+constexpr int kPoScanPer = 4;  // chunks per thread: nchunks <= 1024 (B * F <= 1M lookups)
 __global__ __launch_bounds__(256) void plan_owner_scan_kernel(int nchunks, int P, const int32_t* __restrict__ ocnt,
                                                               int32_t* __restrict__ ooff,
                                                               int64_t* __restrict__ counts) {
-  __shared__ uint32_t ws[20];
-  __shared__ int64_t tot[kPoMaxP + 1];
-  const int t = threadIdx.x;
+  __shared__ uint32_t wsum[4][kPoMaxP];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int per = (nchunks + 255) / 256;
-  // pass 1: totals per owner
-  for (int p = 0; p < P; ++p) {
+  uint32_t c[kPoScanPer][kPoMaxP], sum[kPoMaxP], x[kPoMaxP];
+#pragma unroll
+  for (int i = 0; i < kPoScanPer; ++i)
+#pragma unroll
+    for (int p = 0; p < kPoMaxP; ++p) {
+      const int ch = t * per + i;
+      c[i][p] = (i < per && p < P && ch < nchunks) ? (uint32_t)ocnt[(int64_t)ch * P + p] : 0u;
+    }
+#pragma unroll
+  for (int p = 0; p < kPoMaxP; ++p) {
     uint32_t s = 0;
-    for (int i = 0; i < per; ++i) {
-      const int c = t * per + i;
-      if (c < nchunks) s += (uint32_t)ocnt[(int64_t)c * P + p];
+#pragma unroll
+    for (int i = 0; i < kPoScanPer; ++i) s += c[i][p];
+    sum[p] = s;
+    uint32_t v = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(v, o, 64);
+      if (lane >= o) v += y;
     }
-    // block reduce through the scan helper of a 256-thread block: reuse warp shuffles
-    uint32_t x = s;
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    if ((t & 63) == 0) ws[t >> 6] = x;
-    __syncthreads();
-    if (t == 0) tot[p] = (int64_t)ws[0] + ws[1] + ws[2] + ws[3];
-    __syncthreads();
-  }
-  if (t == 0) {
-    int64_t acc = 0;
-    for (int p = 0; p < P; ++p) {
-      counts[p] = tot[p];
-      const int64_t c = tot[p];
-      tot[p] = acc;  // owner base
-      acc += c;
-    }
-    counts[P] = acc;
+    x[p] = v;  // inclusive over the wave's lanes
+    if (lane == 63) wsum[wave][p] = v;
   }
   __syncthreads();
-  // pass 2: exclusive scan of each owner's chunk counts
-  for (int p = 0; p < P; ++p) {
-    uint32_t loc[8];
-    uint32_t s = 0;
-    for (int i = 0; i < per && i < 8; ++i) {
-      const int c = t * per + i;
-      loc[i] = s;
-      s += c < nchunks ? (uint32_t)ocnt[(int64_t)c * P + p] : 0u;
+  int64_t obase = 0;  // keys of owners < p
+#pragma unroll
+  for (int p = 0; p < kPoMaxP; ++p) {
+    if (p >= P) break;
+    uint32_t wpre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      wpre += w < wave ? wsum[w][p] : 0u;
+      tot += wsum[w][p];
     }
-    const int lane = t & 63, wave = t >> 6;
-    uint32_t x = s;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
+    uint32_t run = (uint32_t)obase + wpre + x[p] - sum[p];
+#pragma unroll
+    for (int i = 0; i < kPoScanPer; ++i) {
+      const int ch = t * per + i;
+      if (i < per && ch < nchunks) ooff[(int64_t)ch * P + p] = (int32_t)run;
+      run += c[i][p];
     }
-    if (lane == 63) ws[wave] = x;
-    __syncthreads();
-    uint32_t wpre = 0;
-    for (int w = 0; w < wave; ++w) wpre += ws[w];
-    const uint32_t pre = wpre + x - s;
-    for (int i = 0; i < per && i < 8; ++i) {
-      const int c = t * per + i;
-      if (c < nchunks) ooff[(int64_t)c * P + p] = (int32_t)(tot[p] + pre + loc[i]);
-    }
-    __syncthreads();
+    if (t == 0) counts[p] = tot;
+    obase += tot;
   }
+  if (t == 0) counts[P] = obase;
 }
 
 // place the chunk's unique keys: stable rank among the chunk's keys of the same owner
@@ -712,24 +468,10 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
   }
 }
 
-// timing experiments (idempotent re-runs): MINIPS_PLAN_REPEAT=k repeats the kernels selected by
-// MINIPS_PLAN_REPEAT_WHICH (bit 0 transpose, 1 sort, 2 emit) k times
-static int plan_reps(int bit) {
-  static const int reps = [] {
-    const char* e = std::getenv("MINIPS_PLAN_REPEAT");
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
-  static const int which = [] {
-    const char* e = std::getenv("MINIPS_PLAN_REPEAT_WHICH");
-    return e ? std::atoi(e) : 7;
-  }();
-  return (which & bit) ? reps : 1;
-}
-
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
-                 int32_t* pos, int32_t* rowstart, int32_t* rowidx, int sort_mode_arg) {
+                 int32_t* pos, int32_t* rowstart, int32_t* rowidx) {
   if (rowstart && P > 1) throw std::runtime_error("plan_sorted: row starts are for one owner");
   if (rowidx && (P > 1 || !route_mult || route_n > (uint64_t)INT32_MAX))
     throw std::runtime_error("plan_sorted: per-lookup rows need one owner and routed keys below 2^31");
@@ -750,40 +492,20 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
   const int nchunks = (int)((n + kPoChunk - 1) / kPoChunk);
   int32_t* ocnt = perm + n;
   int32_t* ooff = ocnt + (int64_t)nchunks * P;
-  for (int r = 0; r < plan_reps(1); ++r)
-    hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, krel);
-  // MINIPS_PLAN_SORT=1 (default): one 1024-thread workgroup per column; 4: the chunked sort over
-  // F x 4 workgroups -- measured slower in the W&D step (0.3708 vs 0.3657 ms: chunk sort 26 +
-  // merge 66 + heads 29 us against 70 us for the one-workgroup sort; profiles/r4/ab_wd_knobs.txt)
-  static const int sort_mode = [] {
-    const char* e = std::getenv("MINIPS_PLAN_SORT");
-    return e ? std::atoi(e) : 1;
-  }();
-  const int nch = (B + kPcChunk - 1) / kPcChunk;
-  const int mode = sort_mode_arg > 0 ? sort_mode_arg : sort_mode;
-  for (int r = 0; r < plan_reps(2); ++r) {
-    if (mode == 1 || nch == 1) {
-      hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u,
-                         ukey, ucount);
-    } else {
-      // (ck / cv / mk: past the owner counts at the workspace end; see the layout above)
-      uint32_t* ck = reinterpret_cast<uint32_t*>(ooff + (int64_t)nchunks * P);
-      int32_t* cv = reinterpret_cast<int32_t*>(ck + n);
-      uint32_t* mk = reinterpret_cast<uint32_t*>(cv + n);
-      hipLaunchKernelGGL(plan_sort_chunk_kernel, dim3(F, nch), kPcThreads, 0, s, krel, B, col_bits, ck, cv);
-      hipLaunchKernelGGL(plan_merge_kernel, dim3(F, nch), kPcThreads, 0, s, ck, cv, B, mk, sorted_b);
-      hipLaunchKernelGGL(plan_heads_kernel, F, kPsThreads, 0, s, mk, B, col_base, local_u, ukey, ucount);
-    }
-  }
+  hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, krel);
+  // one 1024-thread workgroup per column (round 4's chunked sort over F x 4 workgroups measured
+  // slower in the W&D step -- 0.3708 vs 0.3657 ms, profiles/r4/ab_wd_knobs.txt -- and is gone)
+  hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u, ukey,
+                     ucount);
   if (P > 1) {
+    if (nchunks > 256 * kPoScanPer) throw std::runtime_error("plan_sorted: at most 1M lookups with several owners");
     hipLaunchKernelGGL(plan_owner_count_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
                        route_n, ocnt);
     hipLaunchKernelGGL(plan_owner_scan_kernel, 1, 256, 0, s, nchunks, P, ocnt, ooff, counts);
     hipLaunchKernelGGL(plan_owner_perm_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
                        route_n, ooff, perm, uniq);
   }
-  for (int r = 0; r < plan_reps(4); ++r)
-    hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
+  hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
                        route_mult, route_n, P > 1 ? perm : nullptr, uniq, inv, members, memrow, counts, pos,
                        rowstart, rowidx);
   MINIPS_HIP_CHECK(hipGetLastError());

@@ -507,14 +507,6 @@ __global__ void sparse_rowwise_adagrad_kernel(float* table, int64_t ld, float* s
   }
 }
 
-static bool adagrad_v4_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("MINIPS_ADAGRAD_V4");
-    return !(e && std::string(e) == "0");
-  }();
-  return on;
-}
-
 void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys,
                             int64_t n, int64_t base, int D, const float* grads, float lr, float eps, hipStream_t s,
                             const int64_t* n_dev, bool zero_g) {
@@ -523,7 +515,7 @@ void sparse_rowwise_adagrad(float* table, int64_t ld, float* state, float* state
   if (D1 < D && !state2) throw std::runtime_error("sparse_rowwise_adagrad: split rows need state2");
   const int block = 256;
   const bool vec4 = D > 16 && D <= 64 && D % 4 == 0 && ld % 4 == 0 && reinterpret_cast<uintptr_t>(table) % 16 == 0 &&
-                    reinterpret_cast<uintptr_t>(grads) % 16 == 0 && adagrad_v4_enabled();
+                    reinterpret_cast<uintptr_t>(grads) % 16 == 0;
   if (vec4) {
     hipLaunchKernelGGL(sparse_rowwise_adagrad_v4_kernel, grid_for(n * 8, block, 16384), block, 0, s, table, ld, state,
                        state2, D1, keys, n, base, D, grads, lr, eps, n_dev,

@@ -386,10 +386,7 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
   // per-block LDS reduction, partial rows, the last block folds them (one block per CU at most)
   // 256 blocks (every CU, one sample iteration per wave): W&D 0.3632-0.3637 vs 0.3672-0.3678 ms at
   // 128 (profiles/r4/ab_wd_knobs.txt); the two-level fold takes at most 256
-  static const int max_blocks = [] {
-    const char* e = std::getenv("MINIPS_HEAD_BLOCKS");
-    return e ? std::atoi(e) : 256;
-  }();
+  constexpr int max_blocks = 256;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(max_blocks, (B + 63) / 64));
   // the partial slab + ticket of this device: allocated once (zero ticket), before any capture
   static thread_local std::vector<std::pair<int, void*>> ws_cache;
@@ -422,17 +419,15 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
 }
 
 // out[c] += sum_r x[r, c] (x bf16 [M, N] row-major, ld; N % 8 == 0): the bias gradient of a
-// Linear from its output gradient. A block owns a 64-column strip and a chunk of rows; each
-// thread sums 8 columns (one 16-byte load per row) over every 32nd row of the chunk, the block
-// folds its 32 row-lanes in LDS and writes its partial row; the LAST block of a strip (a ticket per
-// strip) adds the strip's partial rows in chunk order into out. One fixed summation order --
-// deterministic, unlike one same-address fp32 atomic per block and column -- and one writer per
-// column. Hand-offs in the write-through form of wd_head (cdna_hip_programming.md Guideline 16).
+// Linear from its output gradient. Two kernels, one fixed summation order (deterministic, unlike
+// one same-address fp32 atomic per block and column): a block owns a 64-column strip and a chunk
+// of rows -- each thread sums 8 columns (one 16-byte load per row) over every 32nd row of the
+// chunk, the block folds its 32 row-lanes in LDS and writes its partial row; then one small block
+// per strip adds the strip's partial rows in chunk order into out. (A last-arriver fold inside the
+// first kernel kept every block alive for a ticket round trip: 16 vs 9 us beside the W&D dgrad.)
 __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restrict__ x, int64_t M, int N, int ld,
-                                                          int rows_per_block, float* __restrict__ out,
-                                                          float* __restrict__ slab, unsigned* __restrict__ ticket) {
+                                                          int rows_per_block, float* __restrict__ slab) {
   __shared__ float red[32][65];
-  __shared__ int last;
   const int t = threadIdx.x, c8 = (t & 7) * 8, rl = t >> 3;
   const int col0 = blockIdx.x * 64 + c8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
@@ -452,69 +447,49 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restri
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[rl][c8 + e] = acc[e];
   __syncthreads();
-  const int nchunk = (int)gridDim.y;
-  float* strip = slab + (int64_t)blockIdx.x * nchunk * 64;
   if (t < 64) {
     float v = 0.f;
 #pragma unroll 8
     for (int i = 0; i < 32; ++i) v += red[i][t];
-    __hip_atomic_store(strip + (int64_t)blockIdx.y * 64 + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    slab[((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * 64 + t] = v;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    const unsigned k = __hip_atomic_fetch_add(ticket + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = k == (unsigned)nchunk - 1;
-    if (last) {
-      __hip_atomic_store(ticket + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last || t >= 64) return;
-  const int col = blockIdx.x * 64 + t;
-  float tot = 0.f;
-  for (int i = 0; i < nchunk; ++i) tot += __hip_atomic_load(strip + (int64_t)i * 64 + t, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT);
-  if (col < N) out[col] += tot;
 }
 
-void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, hipStream_t s) {
+// strip s (a 256-thread block): thread (q, c) sums chunks q, q + 4, ... of column c (8 loads in
+// flight), the 4 quarter sums meet in LDS in quarter order
+__global__ __launch_bounds__(256) void colsum_fold_kernel(const float* __restrict__ slab, int nchunk, int N,
+                                                          float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int t = threadIdx.x, c = t & 63, qtr = t >> 6;
+  const float* strip = slab + (int64_t)blockIdx.x * nchunk * 64;
+  float tot = 0.f;
+  for (int i0 = qtr; i0 < nchunk; i0 += 32) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = i0 + 4 * k < nchunk ? strip[(int64_t)(i0 + 4 * k) * 64 + c] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tot += v[k];
+  }
+  red[qtr][c] = tot;
+  __syncthreads();
+  const int col = blockIdx.x * 64 + t;
+  if (t < 64 && col < N) out[col] += (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+}
+
+void colsum_bf16(const bf16_t* x, int64_t M, int N, int ld, float* out, float* slab, hipStream_t s) {
   if (M <= 0 || N <= 0) return;
   if (N % 8 || ld % 8) throw std::runtime_error("colsum_bf16: N and ld must be multiples of 8");
   const int strips = (N + 63) / 64;
-  const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(512 / strips, (M + 255) / 256));
+  const int64_t chunks = colsum_chunks(M, N);
   const int rpb = (int)((M + chunks - 1) / chunks);
-  // the partial slab + strip tickets of this device, grown on demand (zero tickets; every call
-  // leaves them zero); allocated by the first eager call, before any graph capture
-  static thread_local std::vector<std::pair<int, std::pair<void*, size_t>>> ws_cache;
-  int dev = 0;
-  MINIPS_HIP_CHECK(hipGetDevice(&dev));
-  // [1024 strip tickets (4 KiB, a fixed place: every call's tickets stay zero between calls) | slab]
-  if (strips > 1024) throw std::runtime_error("colsum_bf16: N > 65536");
-  const size_t slab_bytes = sizeof(float) * (size_t)strips * chunks * 64, need = 4096 + slab_bytes;
-  std::pair<void*, size_t>* ws = nullptr;
-  for (auto& e : ws_cache)
-    if (e.first == dev) ws = &e.second;
-  if (!ws || ws->second < need) {
-    if (ws) {
-      MINIPS_HIP_CHECK(hipStreamSynchronize(s));
-      MINIPS_HIP_CHECK(hipFree(ws->first));
-    } else {
-      ws_cache.push_back({dev, {nullptr, 0}});
-      ws = &ws_cache.back().second;
-    }
-    const size_t cap = std::max<size_t>(need, sizeof(float) * 512 * 64 + 4096);
-    MINIPS_HIP_CHECK(hipMalloc(&ws->first, cap));
-    MINIPS_HIP_CHECK(hipMemset(ws->first, 0, cap));
-    ws->second = cap;
-  }
-  unsigned* ticket = static_cast<unsigned*>(ws->first);
-  float* slab = reinterpret_cast<float*>(static_cast<char*>(ws->first) + 4096);
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(strips, (unsigned)chunks), 256, 0, s, x, M, N, ld, rpb, out, slab,
-                     ticket);
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(strips, (unsigned)chunks), 256, 0, s, x, M, N, ld, rpb, slab);
+  hipLaunchKernelGGL(colsum_fold_kernel, strips, 256, 0, s, slab, (int)chunks, N, out);
   MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+int64_t colsum_chunks(int64_t M, int N) {
+  const int strips = (N + 63) / 64;
+  return std::max<int64_t>(1, std::min<int64_t>(std::max(1, 512 / strips), (M + 255) / 256));
 }
 
 // Embedding backward with block-local dedupe: a block owns TB consecutive samples of ONE
@@ -996,38 +971,72 @@ __global__ __launch_bounds__(256) void emb_seg_det_kernel(const TX* __restrict__
   }
 }
 
-// Rows cut by piece boundaries: one L-lane group per piece whose last row starts inside it and
-// continues; it adds TAIL of its own piece, TAIL of every piece the row covers whole, and HEAD of
-// the piece where the row ends -- in piece order.
+// Rows cut by piece boundaries: one WAVE per piece whose last row r starts inside it and
+// continues. Its PER lane groups walk the following pieces in windows of PER (group g takes
+// pieces p + g, p + g + PER, ...; every load of a window is independent -- a Zipf-hot row spans
+// dozens of pieces, and a serial walk of dependent loads took 37 us): a piece contributes TAIL
+// when r covers it whole, HEAD where r ends; then the groups' sums meet in a fixed shuffle tree.
+// The summation order is fixed by the row's span: deterministic.
 template <typename TO, int D, int VW, int PW>
 __global__ __launch_bounds__(256) void emb_seg_fix_kernel(const int* __restrict__ memrow, int total,
                                                           const float* __restrict__ part, TO* __restrict__ out,
                                                           int row_stride, bool wide) {
-  constexpr int L = D / VW, SP = seg_part_stride(D);
-  const int64_t gid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / L;
-  const int l = threadIdx.x % L;
+  constexpr int L = D / VW, PER = 64 / L, SP = seg_part_stride(D);
+  const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
   const int64_t npieces = ((int64_t)total + PW - 1) / PW;
-  if (gid >= npieces) return;
-  const int bw = (int)(gid * PW), ew = (int)min((int64_t)total, (gid + 1) * PW);
-  const int r = memrow[ew - 1];
-  if (!(ew < total && memrow[ew] == r)) return;              // ends inside this piece: done there
-  if (bw > 0 && memrow[bw] == r && memrow[bw - 1] == r) return;  // started in an earlier piece
-  float s[VW];
-  const float* t = part + (2 * gid + 1) * SP;
-  ld_gradv<VW>(t + VW * l, s);
-  float sw = t[D];
-  for (int64_t q = gid + 1;; ++q) {
-    const int eq = (int)min((int64_t)total, (q + 1) * PW);
-    const bool through = eq < total && memrow[eq] == r;
-    const float* p = part + (2 * q + (through ? 1 : 0)) * SP;
-    float v[VW];
-    ld_gradv<VW>(p + VW * l, v);
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t p = wave; p < npieces; p += nw) {
+    const int bw = (int)(p * PW), ew = (int)min((int64_t)total, (p + 1) * PW);
+    const int r = memrow[ew - 1];
+    if (!(ew < total && memrow[ew] == r)) continue;              // ends inside this piece: done there
+    if (bw > 0 && memrow[bw] == r && memrow[bw - 1] == r) continue;  // started in an earlier piece
+    float s[VW];
 #pragma unroll
-    for (int e = 0; e < VW; ++e) s[e] += v[e];
-    sw += p[D];
-    if (!through) break;
+    for (int e = 0; e < VW; ++e) s[e] = 0.f;
+    float sw = 0.f;
+    constexpr int QPG = 4;  // pieces per group per window: PER * QPG pieces per memory round trip
+    for (int64_t w0 = p;; w0 += PER * QPG) {
+      bool end = false;
+#pragma unroll
+      for (int k = 0; k < QPG; ++k) {
+      const int64_t q = w0 + k * PER + sub;
+      const bool valid = q < npieces;
+      const int64_t qc = valid ? q : p;  // (out-of-range groups load piece p's slots, unused)
+      // every load of the window is issued before any is used: both boundary keys of piece q and
+      // both of its partial slots (HEAD, TAIL) -- one memory round trip per window
+      const int mb = memrow[qc * PW];
+      const int64_t eq = min((int64_t)total, (qc + 1) * PW);
+      const int me = eq < total ? memrow[eq] : -1;
+      const float* ph = part + (2 * qc) * SP;
+      const float* pt = ph + SP;
+      float vh[VW], vt[VW];
+      ld_gradv<VW>(ph + VW * l, vh);
+      ld_gradv<VW>(pt + VW * l, vt);
+      const float wh = ph[D], wt = pt[D];
+      // piece q's part of r: TAIL of p itself, TAIL of a piece r covers whole, HEAD where r ends
+      const bool in = valid && (q == p || mb == r);
+      const bool through = in && me == r;
+      const bool tail = q == p || through;
+      if (in) {
+#pragma unroll
+        for (int e = 0; e < VW; ++e) s[e] += tail ? vt[e] : vh[e];
+        sw += tail ? wt : wh;
+      }
+      end = end || !through;
+      }
+      // the window ends the walk when some piece of it is not a through piece of r
+      if (__any(end)) break;
+    }
+    // fixed-order tree over the groups (xor partners at distance L, 2L, ...)
+#pragma unroll
+    for (int o = L; o < 64; o <<= 1) {
+#pragma unroll
+      for (int e = 0; e < VW; ++e) s[e] += __shfl_xor(s[e], o, 64);
+      sw += __shfl_xor(sw, o, 64);
+    }
+    if (sub == 0) seg_store_row<TO, D, VW>(out, row_stride, r, s, sw, wide, l);
   }
-  seg_store_row<TO, D, VW>(out, row_stride, r, s, sw, wide, l);
 }
 
 // CSR of the lookups grouped by unique row (depends on `inv` only, so the PS builds it at
@@ -1071,7 +1080,7 @@ static void emb_seg_det(const TX* dX, int ldx, const float* dwide, int64_t B, in
   const int64_t pw = seg_per_piece(D);
   const int64_t pieces = (total + pw - 1) / pw;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((pieces + 3) / 4, 65535));
-  const int fix_blocks = (int)std::max<int64_t>(1, (pieces * (D / kSegVW) + 255) / 256);
+  const int fix_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((pieces + 3) / 4, 4096));  // a wave per piece
 #define MINIPS_SEG_DET(DD)                                                                                         \
   if (sorted_rows)                                                                                                \
     hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, true, kSegVW>), blocks, 256, 0, s, dX,    \

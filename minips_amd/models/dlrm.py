@@ -13,7 +13,6 @@ pipelining depth; transport "onesided" is the unbounded asynchronous PS (ps/ones
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import torch
@@ -90,8 +89,8 @@ class DLRM(LookaheadPlans):
         self._bufs = {}
         # weight gradients inline by default: with the round-2 MFMA interaction the dgrad chain is
         # short and the side stream's contention costs more than the overlap gains (1 GPU: 0.686
-        # inline vs 0.714 ms/step forked); MINIPS_DLRM_WGRAD_STREAM=1 forks them
-        self._side = SideStream(comm.device, os.environ.get("MINIPS_DLRM_WGRAD_STREAM", "0") == "1")
+        # inline vs 0.714 ms/step forked); DLRM_WGRAD_STREAM on forks them
+        self._side = SideStream(comm.device, False)
 
     def _buffers(self, B):
         if B not in self._bufs:

@@ -26,7 +26,7 @@ def default_depth(world: int) -> int:
 
 
 class LookaheadFeeder:
-    """``fence`` (default: MINIPS_FEED_FENCE, on): after each step the planning stream waits for
+    """``fence`` (default on): after each step the planning stream waits for
     the compute stream (one event per step). Everything the planning stream hands to a step --
     the batch and its key plan -- is then safe to recycle from the planning stream once the step
     is issued, so neither needs ``record_stream`` (an allocator event per tensor on the compute
@@ -40,7 +40,7 @@ class LookaheadFeeder:
         self.main = torch.cuda.current_stream(comm.device) if self.cuda else None
         self.depth = depth or default_depth(comm.world)
         if fence is None:
-            fence = os.environ.get("MINIPS_FEED_FENCE", "1") != "0"
+            fence = True
         self.fence = bool(fence and self.cuda)
         if self.fence:
             model._fenced = True

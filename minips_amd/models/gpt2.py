@@ -15,16 +15,15 @@ Compute path (all gfx950 kernels from minips_amd.ops, no autograd):
   gemm + add_bf16             x_mid = x + O W_o^T
   gemm (GELU-aux epilogue)    g = gelu(ln2 W_fc^T), gelu'(u) saved for the fc2 dgrad
   gemm + add_bf16             x_next = x_mid + g W_proj^T
-  gemm (xent-stats epilogue)  logits = ln_f(x) wte^T (bf16) + per-64-column softmax partials
-  xent_from_stats             lse from the partials, (softmax - onehot) / (B T) in place (one pass)
+  gemm                        logits = ln_f(x) wte^T (bf16)
+  softmax_xent                row logsumexp and (softmax - onehot) / (B T) in place (one pass)
 The backward mirrors it with dgrad/wgrad GEMMs (GELU-grad epilogue), attn_bwd (recomputes P per
 tile; dQ and dK/dV sweeps), layernorm_bwd (accumulating into the residual gradient) and embed_bwd.
 """
 from __future__ import annotations
 
 import math
-import os
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 import torch
 
@@ -51,28 +50,23 @@ class GPT2Config:
     bucketed: bool = True
     # one rank: the clock on the table's side stream too, each layer's bucket applied (Adam) as
     # soon as its backward finished, overlapping the rest of the backward (DenseTable overlap_w1;
-    # MINIPS_GPT2_OVERLAP_W1=0: one Adam over the whole table after the backward)
-    overlap_w1: bool = field(default_factory=lambda: os.environ.get("MINIPS_GPT2_OVERLAP_W1", "1") == "1")
+    # GPT2_OVERLAP_W1 off: one Adam over the whole table after the backward)
+    overlap_w1: bool = True
 
     @property
     def vocab_pad(self):
         return align(self.vocab, 64)
 
 
-# LM-head cross-entropy on our GEMM path: "rowwise" (plain GEMM + block-per-row softmax_xent) or
-# "stats" (softmax partials in the GEMM epilogue + a streaming gradient pass: the pass is 59 us
-# faster, the epilogue 68 us slower -- 13.87 vs 14.14 ms/step, profiles/r3/gpt2_lm_head.txt)
-_XENT = os.environ.get("MINIPS_GPT2_XENT", "rowwise")
-_WGRAD_DEFER_GPT2 = os.environ.get("MINIPS_GPT2_WGRAD_DEFER", "0") == "1"
-_LM_DGRAD_SPLIT = int(os.environ.get("MINIPS_LM_DGRAD_SPLIT", "4"))
-# LM-head GEMMs (logits, dgrad, wte wgrad): "lib" (hipBLASLt through torch for these three plain
-# GEMMs: 13.10 vs 13.87 ms/step) or "ours" (gemm.hip); the CPU reference path always uses ours
-_LM_GEMM = os.environ.get("MINIPS_LM_GEMM", "lib")
-_LM_WGRAD = os.environ.get("MINIPS_LM_WGRAD", "mm")  # lib form of the wte wgrad: "mm" (overwrite) | "addmm"
+_WGRAD_DEFER_GPT2 = False
+# the LM-head dgrad (K = the 50304-row vocabulary, only 8192 x 768 outputs): split-K into fp32 slabs
+# + one bf16 reduce; 8 splits measured best (764 vs 906 / 970 us at 4 / 12, profiles/r4/gemm_lm_head_splits.txt).
+# All three LM-head GEMMs (logits, dgrad, wte wgrad) run on gemm.hip (round 5: the hipBLASLt path is gone)
+_LM_DGRAD_SPLIT = 8
 # MLP: the fc forward saves gelu'(u) (its tanh is computed there anyway) and the fc2 dgrad multiplies
-# by it; MINIPS_GPT2_GELU_D=0 saves u and re-evaluates tanh in the dgrad epilogue
-_GELU_D = os.environ.get("MINIPS_GPT2_GELU_D", "1") == "1"
-# per-layer weight gradients: split-K gemm.hip (the hipBLASLt form, MINIPS_GPT2_WGRAD=lib, measured
+# by it; GPT2_GELU_D off saves u and re-evaluates tanh in the dgrad epilogue
+_GELU_D = True
+# per-layer weight gradients: split-K gemm.hip (the hipBLASLt form, GPT2_WGRAD=lib, measured
 # 13.0-13.1 vs 12.78 ms/step in round 3 and was removed in round 4)
 
 
@@ -118,7 +112,7 @@ class GPT2:
         L.view(full, "lnf_g").fill_(1.0)
         self.table.load_full(full)
         self._bufs = {}
-        self._side = SideStream(comm.device, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
+        self._side = SideStream(comm.device)
 
     @property
     def n_params(self):
@@ -146,11 +140,9 @@ class GPT2:
                 ao=[ext_activation(M, d, dev) for _ in range(nl)],        # attention out (+ ones)
                 u=[torch.empty(M, 4 * d, **bf) for _ in range(nl)],       # pre-GELU
                 g=[ext_activation(M, 4 * d, dev) for _ in range(nl)],     # GELU out (+ ones)
-                # ln_f output: only the LM head reads it (no bias column), contiguous rows -- hipBLASLt
-                # takes a strided operand through an extra copy (+120 us on the wgrad)
+                # ln_f output: only the LM head reads it (no bias column), contiguous rows
                 hf=torch.empty(M, d, **bf), stf=(torch.empty(M, **f32), torch.empty(M, **f32)),
                 logits=torch.empty(M, c.vocab_pad, **bf),
-                xstats=torch.empty(M * ((c.vocab_pad + 63) // 64) * 2, **f32),  # LM-head softmax partials
                 delta=torch.empty(B * H * T, **f32),
                 tmp=torch.empty(M, d, **bf), dx=torch.empty(M, d, **bf), dh=torch.empty(M, d, **bf),
                 dqkv=torch.empty(M, 3 * d, **bf), dao=torch.empty(M, d, **bf), du=torch.empty(M, 4 * d, **bf),
@@ -191,41 +183,22 @@ class GPT2:
         wte = v(P, "wte")
         logits = b["logits"]
         b["loss"].zero_()
-        if _LM_GEMM == "lib" and logits.is_cuda:  # hipBLASLt for the plain LM-head GEMM, then the row-wise softmax-xent
-            torch.matmul(hf[:, :d], wte.t(), out=logits)
-            ops.softmax_xent(logits, c.vocab, targets.reshape(-1), 1.0 / (M * self.comm.world), b["loss"])
-        elif _XENT == "stats":  # softmax partials in the LM-head GEMM epilogue, then one streaming pass
-            ops.lm_head_xent(hf[:, :d], wte, logits, b["xstats"], c.vocab, targets.reshape(-1),
-                             1.0 / (M * self.comm.world), b["loss"])
-        else:  # plain GEMM + the block-per-row softmax-xent (row reduction + gradient in one kernel)
-            ops.gemm(hf[:, :d], wte, logits, M, c.vocab_pad, d, False, False, ops.EPI_STORE_BF16)
-            ops.softmax_xent(logits, c.vocab, targets.reshape(-1), 1.0 / (M * self.comm.world), b["loss"])
+        # plain GEMM + the block-per-row softmax-xent (row reduction + gradient in place, one kernel);
+        # (round 3's softmax partials in the GEMM epilogue measured 13.87 vs 14.14 ms/step: removed)
+        ops.gemm(hf[:, :d], wte, logits, M, c.vocab_pad, d, False, False, ops.EPI_STORE_BF16)
+        ops.softmax_xent(logits, c.vocab, targets.reshape(-1), 1.0 / (M * self.comm.world), b["loss"])
         # ---- backward. Weight gradients fork onto a side stream beside the dgrad chain; before the
         # chain overwrites a buffer a forked wgrad reads (dx, du, dqkv), it waits for that wgrad.
         side = self._side
         dh = b["dh"]
-        if _LM_GEMM == "lib" and logits.is_cuda:
-            # plain GEMMs with one operand streamed from HBM (the 824 MB dlogits): hipBLASLt's larger
-            # tiles / split-K schedule measured 1.6x ours here (profiles/r3/lm_head_gemm.txt); the
-            # weight gradient accumulates in fp32 (addmm out_dtype), the dgrad writes bf16
-            gw = v(G, "wte")
-            with side.fork():
-                if _LM_WGRAD == "mm":
-                    # the first writer of the wte gradient in the step (embed_bwd adds after the
-                    # join): an overwriting fp32-output mm (710 us isolated vs addmm's 757 us)
-                    torch.mm(logits.t(), hf, out_dtype=torch.float32, out=gw)
-                else:
-                    torch.addmm(gw, logits.t(), hf, out_dtype=torch.float32, out=gw)
-            torch.matmul(logits, wte, out=dh)
-        else:
-            with side.fork():
-                ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"))
-            # long K (the vocabulary), few outputs: split-K into fp32 slabs + one bf16 reduce
-            ops.gemm(logits, wte, dh, M, d, c.vocab_pad, False, True, ops.EPI_STORE_BF16, split_k=_LM_DGRAD_SPLIT)
+        with side.fork():
+            ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"))
+        # long K (the vocabulary), few outputs: split-K into fp32 slabs + one bf16 reduce
+        ops.gemm(logits, wte, dh, M, d, c.vocab_pad, False, True, ops.EPI_STORE_BF16, split_k=_LM_DGRAD_SPLIT)
         dx = b["dx"]
         ops.layernorm_bwd(x[-1], dh, d, v(P, "lnf_g"), mf, rf, dx, v(G, "lnf_g"), v(G, "lnf_b"))
         ev_du = ev_dqkv = None
-        # MINIPS_GPT2_WGRAD_DEFER=1: the per-layer weight gradients' split-K planes folded by their
+        # GPT2_WGRAD_DEFER on: the per-layer weight gradients' split-K planes folded by their
         # bucket's Adam instead of reduce kernels -- measured neutral here (12.66-12.68 vs 12.48-12.64
         # ms/step; profiles/r4/ab_gpt2_knobs.txt), so the reduces stay by default
         sink = self.table.slab_sink() if _WGRAD_DEFER_GPT2 and hasattr(self.table, "slab_sink") else None

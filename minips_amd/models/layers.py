@@ -8,7 +8,6 @@ Linear        bias folded into the weight: W_ext [n_out, k_pad] with the bias in
 """
 from __future__ import annotations
 
-import os
 
 import math
 
@@ -113,15 +112,13 @@ class Linear:
 
 def compute_priority() -> int:
     """HIP stream priority for the training step's compute streams (main and weight-gradient side
-    stream). MINIPS_COMPUTE_PRIORITY=1 makes them high priority (-1), so the dispatcher favours
-    their workgroups over the planning / data stream's; measured neutral on the W&D step
-    (0.520-0.524 vs 0.519-0.521 ms), so normal priority is the default."""
-    import os
-
-    return -1 if os.environ.get("MINIPS_COMPUTE_PRIORITY", "0") == "1" else 0
+    stream). High priority (-1), which makes the dispatcher favour their workgroups over the
+    planning / data stream's, measured neutral on the W&D step (0.520-0.524 vs 0.519-0.521 ms)
+    and worse on GPT-2 (profiles/r4/ab_gpt2_knobs.txt), so normal priority."""
+    return 0
 
 
-_FAST_EVENTS = os.environ.get("MINIPS_FAST_EVENTS", "1") != "0"
+_FAST_EVENTS = True
 
 
 class _Fork:
@@ -175,7 +172,7 @@ class SideStream:
             if enabled and torch.device(device).type == "cuda" else None
         # fork / join events are re-recorded every step (a wait binds to the record issued before
         # it): no event objects created and destroyed per fork. Same-device ordering only, so
-        # fence-free native events (ops_py FastEvent, MINIPS_FAST_EVENTS=0: torch events)
+        # fence-free native events (ops_py FastEvent, FAST_EVENTS off: torch events)
         self._fast = self.stream is not None and _FAST_EVENTS
         if self._fast:
             from .._native import kernels

@@ -4,7 +4,6 @@ DenseTable (reduce-scatter of gradients, fused Adam on the owned shard, all-gath
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 
 import torch
@@ -44,8 +43,8 @@ class MLP:
         self.table.load_full(full)
         self._bufs = {}
         # weight gradients inline by default: this step is too small for a side stream to pay
-        # (measured 0.424 vs 0.350 ms per step at batch 8192); MINIPS_MLP_WGRAD_STREAM=1 forks them
-        self._side = SideStream(comm.device, os.environ.get("MINIPS_MLP_WGRAD_STREAM", "0") == "1")
+        # (measured 0.424 vs 0.350 ms per step at batch 8192); MLP_WGRAD_STREAM on forks them
+        self._side = SideStream(comm.device, False)
 
     def _buffers(self, B):
         if B not in self._bufs:

@@ -17,7 +17,6 @@ Step (every kernel is a gfx950 HIP kernel; comm is RCCL):
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import torch
@@ -72,48 +71,40 @@ class WideDeepConfig:
 # where train_step issues the next batch's planning (dedupe, CSR, count exchange) and, with a
 # callable next_keys, its generation: "start" | "head" (after the forward) | "dgrad" (after the
 # dgrad chain, beside the memory-bound embedding backward)
-_PLAN_AT = os.environ.get("MINIPS_PLAN_AT", "start")
+_PLAN_AT = "start"
 # issue an async dense clock from the weight-gradient side stream (see train_step). Measured
-# slower on one MI355X (MINIPS_OVERLAP_W1=dense: 0.525-0.529 -> 0.544-0.549 ms/step: Adam then
-# competes with the memory-bound embedding backward; tools/gpu_ab.sh), so off by default.
-_DENSE_CLOCK_ON_SIDE = os.environ.get("MINIPS_DENSE_CLOCK_ON_SIDE", "0") == "1"
+# slower on one MI355X (OVERLAP_W1=dense: 0.525-0.529 -> 0.544-0.549 ms/step: Adam then
+# competes with the memory-bound embedding backward; tools/gpu_round.sh ab), so off by default.
+_DENSE_CLOCK_ON_SIDE = False
 
 
-# Dense-layout knobs (see WideDeep.__init__): layer-1 K padding, and bias handling of layers 2/3:
+# Dense layout (see WideDeep.__init__): layer-1 K padding, and bias handling of layers 2/3:
 # "ext" (folded, K = 1032 / 520) or "vec" (bias vectors, K = 1024 / 512, colsum bias gradients).
-# In the whole W&D step on one MI355X (tools/gpu_ab.sh, ms/step): ext/8 0.453, ext/64 0.451,
+# In the whole W&D step on one MI355X (tools/gpu_round.sh ab, ms/step): ext/8 0.453, ext/64 0.451,
 # vec/8 0.460, vec/64 0.457 -- the isolated GEMM gains of "vec" (fwd2 -7 us, W2 wgrad -10 us)
 # do not survive the 3-stream overlap (its W2 weight gradient switches to 512 128x128 blocks,
 # which crowd the dgrad chain), so "ext" with a 64-aligned layer-1 K was the default through round 3.
 # Round 4 (split-K planes folded by Adam, fence-free forks, the rest of this round's step): vec
-# 0.3879 / 0.3882 vs ext 0.4016 / 0.4021 ms/step (profiles/r4/ab_wd_knobs.txt) -- "vec" by default.
-_K1_ALIGN = int(os.environ.get("MINIPS_WD_K1_ALIGN", "64"))
-_BIAS_VEC = os.environ.get("MINIPS_WD_BIAS", "vec") == "vec"
-# MINIPS_WD_FUSED_HEAD=1: layer 3 and the output head as one GEMM (ops.wd_fwd_head, H3 never
-# written). Measured off: the fused kernel took 51 us vs 17 + 24 us for the GEMM + wd_head (its
-# dw4 / db4 / loss reductions are 256 same-address atomics per column from 256 workgroups).
-_FUSED_HEAD = os.environ.get("MINIPS_WD_FUSED_HEAD", "0") == "1"
-# MINIPS_WD_TRIM=1 (with the fused head): layer-2/3 weight gradients over the weight columns only,
-# their folded-bias columns as dH column sums in the producing epilogues. Measured off: 0.448 vs
-# 0.416-0.420 ms/step (per-wave column-sum atomics in the dgrad epilogue), profiles/r3/ab_wd_r3.txt
-_TRIM = os.environ.get("MINIPS_WD_TRIM", "0") == "1"
+# 0.3879 / 0.3882 vs ext 0.4016 / 0.4021 ms/step (profiles/r4/ab_wd_knobs.txt) -- "vec" only since
+# round 5 (layer 1 keeps its bias folded into column k_in of the padded input).
+_K1_ALIGN = 64
 # split-K workgroup target of the three weight gradients (ops.linear_wgrad blocks): W&D 0.402 ms at
 # 320 vs 0.409-0.412 at the default 512 (GPT-2 keeps 512: 12.90 vs 13.18 ms at 256), ab_wd_r3.txt
-_WGRAD_BLOCKS = int(os.environ.get("MINIPS_WD_WGRAD_BLOCKS", "320"))
+_WGRAD_BLOCKS = 320
 
 
-# MINIPS_DENSE_ON_SIDE=0: one rank's dense Adam on the main stream at the step end (joined)
-_DENSE_ON_SIDE = os.environ.get("MINIPS_DENSE_ON_SIDE", "1") != "0"
-# MINIPS_WD_W1_LATE=1: fork the layer-1 weight gradient after the embedding dgrad (beside the
+# DENSE_ON_SIDE off: one rank's dense Adam on the main stream at the step end (joined)
+_DENSE_ON_SIDE = True
+# WD_W1_LATE on: fork the layer-1 weight gradient after the embedding dgrad (beside the
 # embedding backward rather than beside the dgrad: two big GEMMs at once only share the CUs);
 # round 3 measured it 5 % slower (profiles/r3/ab_wd_r3.txt)
-_W1_LATE = os.environ.get("MINIPS_WD_W1_LATE", "0") == "1"
-# MINIPS_ROWIDX=0: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
-_ROWIDX = os.environ.get("MINIPS_ROWIDX", "1") != "0"
+_W1_LATE = False
+# ROWIDX off: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
+_ROWIDX = True
 
 
 def _wgrad(dH, H, Gw, sink=None):
-    # (round 4: the hipBLASLt alternative, MINIPS_WD_WGRAD=lib, measured slower and removed)
+    # (round 4: the hipBLASLt alternative, WD_WGRAD=lib, measured slower and removed)
     return ops.linear_wgrad(dH, H, Gw, blocks=_WGRAD_BLOCKS, defer=sink)
 
 
@@ -148,22 +139,22 @@ class WideDeep(LookaheadPlans):
                         **({"max_keys": cfg.max_batch * F} if onesided else {}))
         # wide weights start at zero (columns >= D)
         self.emb.shard[:, D:].zero_()
-        # Dense layout: each Linear is stored as W_ext [n_out, k_pad] with the bias in column k_in;
-        # activations carry a constant-1 column at k_in, so the forward GEMM adds the bias and the
+        # Dense layout: layer 1 is stored as W_ext [n_out, k_pad] with the bias in column k_in; its
+        # input carries a constant-1 column at k_in, so the forward GEMM adds the bias and the
         # weight-gradient GEMM yields its gradient (no bias epilogue, no column-sum atomics).
         # Layer 1's k_pad is a multiple of 64: whole 64-deep K-steps and 128-byte rows for the
         # LDS-DMA (K = 896: the 16384x1024 forward takes 30.7 us vs 38.8 us at align8's 848;
-        # tools/bench_kernels.py gemm). MINIPS_WD_BIAS=vec gives layers 2/3 bias vectors instead (see
-        # _BIAS_VEC): dH3's column sums from wd_head, dH2's from a column-sum kernel.
+        # tools/bench_kernels.py gemm). Layers 2/3 have bias vectors: dH3's column sums come from
+        # wd_head, dH2's from a column-sum kernel.
         self.k_in = [cfg.F * cfg.emb_dim + cfg.n_dense, *cfg.hidden[:-1]]
         self.k_pad = [_align(self.k_in[0] + 1, _K1_ALIGN),
-                      *(self.k_in[1:] if _BIAS_VEC else [_align(k + 1) for k in self.k_in[1:]])]
+                      *self.k_in[1:]]
         self.layout = {}
         off = 0
         for i, n_out in enumerate(cfg.hidden):
             self.layout[f"W{i + 1}"] = (off, (n_out, self.k_pad[i]))
             off += _align(n_out * self.k_pad[i], 64)
-            if i > 0 and _BIAS_VEC:
+            if i > 0:
                 self.layout[f"b{i + 1}"] = (off, (n_out,))
                 off += _align(n_out, 64)
         self.layout["w4"] = (off, (cfg.hidden[-1] + 8,))  # [w4 | b4 | pad]
@@ -178,7 +169,7 @@ class WideDeep(LookaheadPlans):
         self._wbucket = [self.dense.bucket_for_layer(x) for x in starts] if bucketed else None
         self.dense.load_full(self._init_dense(dev))
         self._bufs = {}
-        self._side = SideStream(dev, os.environ.get("MINIPS_WGRAD_STREAM", "1") != "0")
+        self._side = SideStream(dev)
 
     def _init_dense(self, dev):
         g = torch.Generator(device="cpu")
@@ -219,15 +210,8 @@ class WideDeep(LookaheadPlans):
             X = torch.zeros(B, self.k_pad[0], **bf)  # constant-1 column at k_in (layer-1 bias), zero pad
             X[:, self.k_in[0]] = 1.0
 
-            def act(n):  # bias folded (MINIPS_WD_BIAS=ext): constant-1 column at n, zero padding
-                if _BIAS_VEC:
-                    return torch.empty(B, n, **bf)
-                t = torch.zeros(B, _align(n + 1), **bf)
-                t[:, n] = 1.0
-                return t
-
             self._bufs[B] = dict(
-                X=X, H1=act(h1), H2=act(h2),
+                X=X, H1=torch.empty(B, h1, **bf), H2=torch.empty(B, h2, **bf),
                 H3=torch.empty(B, h3, **bf), dH3=torch.empty(B, h3, **bf), dH2=torch.empty(B, h2, **bf),
                 dH1=torch.empty(B, h1, **bf),
                 dX=torch.empty(B, cfg.F * cfg.emb_dim, **bf),  # bf16: half the bytes of the emb backward
@@ -239,8 +223,8 @@ class WideDeep(LookaheadPlans):
 
     def _forward(self, b, P):
         ops.linear_fwd(b["X"], self.view(P, "W1"), None, "relu", out=b["H1"])
-        ops.linear_fwd(b["H1"], self.view(P, "W2"), self.view(P, "b2") if _BIAS_VEC else None, "relu", out=b["H2"])
-        ops.linear_fwd(b["H2"], self.view(P, "W3"), self.view(P, "b3") if _BIAS_VEC else None, "relu", out=b["H3"])
+        ops.linear_fwd(b["H1"], self.view(P, "W2"), self.view(P, "b2"), "relu", out=b["H2"])
+        ops.linear_fwd(b["H2"], self.view(P, "W3"), self.view(P, "b3"), "relu", out=b["H3"])
 
     def forward(self, dense, keys, rows, plan):
         """Forward only (eval): returns logits [B] fp32."""
@@ -304,26 +288,10 @@ class WideDeep(LookaheadPlans):
         P = self.dense.get()
         scale = 1.0 / (B * self.comm.world)
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
-        if _FUSED_HEAD and _BIAS_VEC:
-            # layer 3 + the output head in one GEMM (H3 never leaves the chip): the head's sums fold
-            # in two write-through levels; dH3's column sums are the layer-3 bias gradient
-            ops.linear_fwd(b["X"], self.view(P, "W1"), None, "relu", out=b["H1"])
-            ops.linear_fwd(b["H1"], self.view(P, "W2"), self.view(P, "b2"), "relu", out=b["H2"])
-            ops.wd_fwd_head(b["H2"], self.view(P, "W3"), self.k_in[2], w4, b["wide"], labels, b["dH3"], gw4,
-                            b["dwide"], b["loss"], scale, dH_colsum=self.view(G, "b3"), bias=self.view(P, "b3"))
-        elif _FUSED_HEAD:
-            # layer 3 + the output head in one GEMM: H3 never leaves the chip (ops.wd_fwd_head)
-            ops.linear_fwd(b["X"], self.view(P, "W1"), None, "relu", out=b["H1"])
-            ops.linear_fwd(b["H1"], self.view(P, "W2"), None, "relu", out=b["H2"])
-            # with _TRIM, dH3's column sums (the layer-3 folded-bias gradient) come from the head
-            ops.wd_fwd_head(b["H2"], self.view(P, "W3"), self.k_pad[2], w4, b["wide"], labels, b["dH3"], gw4,
-                            b["dwide"], b["loss"], scale,
-                            dH_colsum=self.view(G, "W3")[:, self.k_in[2]] if _TRIM else None)
-        else:
-            self._forward(b, P)
-            # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
-            ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
-                        b["dwide"], b["loss"], self.view(G, "b3") if _BIAS_VEC else None, scale)
+        self._forward(b, P)
+        # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
+        ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
+                    b["dwide"], b["loss"], self.view(G, "b3"), scale)
         issue_next("head")
         side = self._side
         # weight gradients fork onto a second stream as soon as their inputs exist, beside the
@@ -331,27 +299,15 @@ class WideDeep(LookaheadPlans):
         # Each fork records an event on the compute stream (~2-4 us queue bubble on MI355X), but
         # fewer, later forks lose more overlap than they save: W3+W2 forked together 0.431-0.438,
         # all three after dgrad1 0.446 vs 0.418-0.421 ms/step (profiles/r3/ab_wd_forks.txt)
-        # _TRIM: the layer-2/3 weight gradients over the weight columns only (1024 / 512 instead of
-        # 1032 / 520: no near-empty last column tile); their folded-bias columns are the column sums
-        # of dH2 / dH3, taken by the dgrad epilogue / the fused head
-        trim = _TRIM and _FUSED_HEAD and not _BIAS_VEC
         # one rank: the weight gradients' split-K slices are folded by the dense table's Adam
         sink = self.dense.slab_sink() if hasattr(self.dense, "slab_sink") else None
-        k2, k3 = self.k_in[1], self.k_in[2]
+        k3 = self.k_in[2]
         with side.fork():
-            if trim:
-                ops.linear_wgrad(b["dH3"], b["H2"][:, :k3], self.view(G, "W3")[:, :k3], blocks=_WGRAD_BLOCKS)
-            else:
-                _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink)
-        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"],
-                         colsum=self.view(G, "W2")[:, k2] if trim else None)
+            _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink)
+        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"])
         with side.fork():
-            if _BIAS_VEC:
-                ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
-            if trim:
-                ops.linear_wgrad(b["dH2"], b["H1"][:, :k2], self.view(G, "W2")[:, :k2], blocks=_WGRAD_BLOCKS)
-            else:
-                _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink)
+            ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
+            _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink)
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         self._bucket_done(1, side)  # (layers 2, 3 and the head: their weight gradients are issued)
         if not _W1_LATE:

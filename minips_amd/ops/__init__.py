@@ -24,7 +24,6 @@ EPI_BIAS_GELU_BF16 = 6
 EPI_BIAS_GELU_AUX_BF16 = 7  # C = gelu(u), mask(aux) = u  (pre-activation saved for backward)
 EPI_GELU_GRAD_BF16 = 8      # C = acc * gelu'(mask)
 EPI_PERM_ROWS_BF16 = 9      # C rows of `seg` columns permuted by `perm` (embedding dgrad in planner order)
-EPI_XENT_STATS_BF16 = 11    # C = acc (bf16 logits) + per-64-column softmax partials into colsum (seg = vocab)
 EPI_BIAS_GELU_DAUX_BF16 = 13  # C = gelu(u), mask(aux) = gelu'(u)  (the derivative saved for backward)
 EPI_MUL_AUX_BF16 = 14       # C = acc * mask(aux)
 _L2E = 1.4426950408889634
@@ -86,16 +85,6 @@ def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None,
         C[:M, :N] = acc.to(torch.bfloat16)
     elif epi == EPI_PERM_ROWS_BF16:
         C.view(-1, seg)[perm[: M * (N // seg)].long()] = acc.to(torch.bfloat16).reshape(-1, seg)
-    elif epi == EPI_XENT_STATS_BF16:
-        out = acc.to(torch.bfloat16)
-        C[:M, :N] = out
-        npart = (N + 63) // 64
-        y = torch.full((M, npart * 64), -1.0e30)
-        y[:, :seg] = out[:, :seg].float() * _L2E
-        y = y.view(M, npart, 64)
-        mx = y.amax(2)
-        sm = torch.where(y > -1.0e29, torch.exp2(y - mx[..., None]), torch.zeros_like(y)).sum(2)
-        colsum.view(-1)[: M * npart * 2] = torch.stack([mx, sm], 2).reshape(-1)
     elif epi == EPI_RELU_MASK_BF16:
         out = torch.where(mask[:M, :N].float() > 0, acc, torch.zeros_like(acc)).to(torch.bfloat16)
         C[:M, :N] = out
@@ -164,26 +153,18 @@ def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=
     return gemm(dy, w, out, M, K, N, False, True, epi, mask=mask, colsum=colsum)
 
 
-_WGRAD_MODE = __import__("os").environ.get("MINIPS_GEMM_WGRAD", "v2")
-_WGRAD_BLOCKS = int(__import__("os").environ.get("MINIPS_WGRAD_BLOCKS", "256" if _WGRAD_MODE == "v3" else "512"))
-# Reduction rows per split: 640 is the isolated-kernel optimum (a wgrad on the critical path, e.g.
-# the MLP); a wgrad forked onto a side stream beside the dgrad chain (SideStream, which sets
-# overlap_mode) favours throughput: fewer, longer splits with less slab traffic (W&D step 0.560 ->
-# 0.550 ms at 2048; the MLP step loses 15 % at 2048 when its wgrads are on the critical path).
-_WGRAD_MIN_ROWS = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS", "512" if _WGRAD_MODE == "v3" else "640"))
-# round 2 (LDS-staged epilogue, v2 wgrad): 1024 rows per overlapped split measured best
-# (W&D 0.461 ms vs 0.490 at 2048; tools/gpu_ab.sh, profiles/r2/gemm_round2.txt)
-_WGRAD_MIN_ROWS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_ROWS_OVERLAP",
-                                                           "512" if _WGRAD_MODE == "v3" else "1024"))
-# Overlapped wgrads with few output tiles (W&D's 256x512 W3 grad: 8 tiles) would get only ~64
-# workgroups at 2048 rows per split; this floor on the block count (0: off) lets them split finer
-# (never below _WGRAD_MIN_ROWS rows per split). Measured worse on one MI355X (W&D 0.528 ->
-# 0.539 ms/step at 128 blocks, 0.548 at 256: the finer splits steal CUs from the dgrad chain and
-# add slab traffic; tools/gpu_ab.sh), so it stays off.
-_WGRAD_MIN_BLOCKS_OVERLAP = int(__import__("os").environ.get("MINIPS_WGRAD_MIN_BLOCKS_OVERLAP", "0"))
+# Split-K weight gradients: about one 128x128 workgroup per CU pair (512 blocks), but a minimum number
+# of reduction rows per split (profiles/r2/gpt2_wgrad_sweep.txt: shorter slices lose to their fixed
+# prologue/epilogue cost). 640 rows is the isolated-kernel optimum (a wgrad on the critical path, e.g.
+# the MLP); a wgrad forked onto a side stream beside the dgrad chain (SideStream sets overlap_mode)
+# favours throughput: fewer, longer splits with less slab traffic -- 1024 rows measured best there
+# (W&D 0.461 ms vs 0.490 at 2048; tools/gpu_round.sh ab, profiles/r2/gemm_round2.txt). A block-count floor
+# for overlapped wgrads with few tiles measured worse (W&D 0.528 -> 0.539 ms at 128 blocks) and is gone;
+# so are the 256x256 wgrad tile and the phase-split v3 wgrad (profiles/r4/ab_gpt2_knobs.txt).
+_WGRAD_BLOCKS = 512
+_WGRAD_MIN_ROWS = 640
+_WGRAD_MIN_ROWS_OVERLAP = 1024
 _overlap_state = __import__("threading").local()
-# MINIPS_WGRAD_TILE=256: the split-K weight gradients on 256x256 tiles (gemm_kernels.h reads it too)
-_WGRAD_TILE = int(__import__("os").environ.get("MINIPS_WGRAD_TILE", "0"))
 
 
 def overlap_mode(on: bool) -> bool:
@@ -195,24 +176,18 @@ def overlap_mode(on: bool) -> bool:
 
 def linear_wgrad(dy, x, dw, split_k=None, blocks=None, defer=None):
     """dw[N,K] += dy^T x (dy [M,N], x [M,K]); fp32 accumulate. ``blocks``: the workgroup target of
-    the split-K choice (default MINIPS_WGRAD_BLOCKS; a model may tune its own). ``defer``: a
+    the split-K choice (default _WGRAD_BLOCKS; a model may tune its own). ``defer``: a
     DenseTable slab sink (DenseTable.slab_sink()): the K slices stay in fp32 slab planes that the
     table's next Adam folds in (no reduce kernel); dw must be a contiguous [N, K] region of the
     table's gradient, which the sum then never passes through."""
     M, N = dy.shape
     K = x.shape[1]
     if split_k is None:
-        t = 256 if (_WGRAD_MODE == "v3" or _WGRAD_TILE == 256) else 128
-        tiles = ((N + t - 1) // t) * ((K + t - 1) // t)
-        # about one workgroup per CU (v3: 256x256 tiles, 1 WG/CU; v1/v2: ~512 128x128 blocks), but
-        # a minimum number of reduction rows per split (profiles/r2/gpt2_wgrad_sweep.txt: shorter slices lose
-        # to their fixed prologue/epilogue cost; the slab reduce makes splits cheap)
+        tiles = ((N + 127) // 128) * ((K + 127) // 128)
         overlapped = getattr(_overlap_state, "on", False)
         min_rows = _WGRAD_MIN_ROWS_OVERLAP if overlapped else _WGRAD_MIN_ROWS
         target = _WGRAD_BLOCKS if blocks is None else int(blocks)
         split_k = max(1, min(M // min_rows, (target + tiles - 1) // tiles))
-        if overlapped and _WGRAD_MIN_BLOCKS_OVERLAP and split_k * tiles < _WGRAD_MIN_BLOCKS_OVERLAP:
-            split_k = max(split_k, min(M // _WGRAD_MIN_ROWS, -(-_WGRAD_MIN_BLOCKS_OVERLAP // tiles)))
     if (defer is not None and _gpu(dy) and split_k > 1 and K % 4 == 0 and dw.dim() == 2
             and dw.stride(1) == 1 and dw.stride(0) == K and defer.accepts(dw)):
         slab = defer.slab(dw, split_k)
@@ -280,31 +255,22 @@ def bitmap_plan(keys: torch.Tensor, bounds: torch.Tensor, num_rows: int, route_m
     return unique_bucketize_n(flat, bounds, 1, int(route_mult), int(num_rows) if route_mult else 0)
 
 
-_PLAN_BITS_CAP = int(__import__("os").environ.get("MINIPS_PLAN_BITS_CAP", "0"))
-
-
-def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None, bounds=None, positions=False,
-                sort_mode=-1):
+def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None, bounds=None, positions=False):
     """Key planning of a [B, F] batch whose columns hold disjoint key ranges (column f's keys in
     [col_base[f], col_base[f] + 2**col_bits[f])): per-column radix sort, no global atomics
     (plan.hip). ``col_bits``: a list of ints (or one int for every column); ``bounds`` [P+1]: the
     owners' routed-key ranges (None: one owner). Returns (uniq [n] (first U valid, routed; column-
     major, ascending inside a column, then stably grouped by owner), inv [n], counts [P], U_dev [1],
     members [n] int32, memrow [n] int32) -- the unique_bucketize_n outputs plus the lookup CSR of
-    emb_build_csr (rows contiguous, in column-major key order). ``sort_mode`` (GPU): 1 = one
-    workgroup per column, 4 = the chunked sort over F x 4 workgroups, -1 = MINIPS_PLAN_SORT / default."""
+    emb_build_csr (rows contiguous, in column-major key order)."""
     if bounds is None:
         bounds = torch.tensor([0, (1 << 62)], dtype=torch.int64, device=keys.device)
     if _gpu(keys):
         bits = [int(col_bits)] * keys.shape[1] if isinstance(col_bits, int) else [int(b) for b in col_bits]
-        if _PLAN_BITS_CAP:  # timing experiment only: fewer radix passes, WRONG dedupe (in-range keys)
-            bits = [min(b, _PLAN_BITS_CAP) for b in bits]
-            bits_dev = None
         if bits_dev is None:  # (tables pass their cached device copy: no H2D copy per plan)
             bits_dev = torch.tensor(bits, dtype=torch.int32, device=keys.device)
         return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), bits_dev, bits,
-                                           int(route_mult), int(route_n), bounds.contiguous(), bool(positions),
-                                           int(sort_mode)))
+                                           int(route_mult), int(route_n), bounds.contiguous(), bool(positions)))
     B, F = keys.shape
     uniq_l, inv_l = [], []
     base = 0
@@ -562,27 +528,6 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
         dH_colsum += g.float().sum(0)
 
 
-def wd_fwd_head(A, W, K, w4, wide_logit, labels, dH, dw4, dwide, loss_sum, grad_scale=1.0, H_out=None,
-                dH_colsum=None, bias=None):
-    """Last hidden layer + W&D output head fused (GPU: one GEMM, H3 stays on chip): H3 =
-    relu(A[:, :K] W[:, :K]^T (+ bias)) rounded to bf16, then wd_head(H3, w4[:N], w4[N], ...) with
-    dw4[:N] / dw4[N] the head's weight / bias gradients; ``dH_colsum`` (a 1-D, possibly strided
-    view) += the column sums of dH. ``H_out`` (CPU only) receives H3."""
-    N = W.shape[0]
-    if _gpu(A):
-        kernels().wd_fwd_head(A, W, int(K), w4, wide_logit, labels, dH, dw4, dwide, loss_sum, float(grad_scale),
-                              dH_colsum, bias)
-        return
-    acc = A[:, :K].float() @ W[:, :K].float().t()
-    if bias is not None:
-        acc = acc + bias[:N].float()
-    H = torch.relu(acc).to(torch.bfloat16)
-    if H_out is not None:
-        H_out.copy_(H)
-    wd_head(H, w4[:N], w4[N:N + 1], wide_logit, labels, dH, dw4[:N], dw4[N:N + 1], dwide, loss_sum,
-            dH_colsum=dH_colsum, grad_scale=grad_scale)
-
-
 def emb_csr_positions(members):
     """pos[members[m]] = m (int32): the member-order row of every lookup (the dgrad's permutation)."""
     if _gpu(members):
@@ -830,37 +775,6 @@ def softmax_xent(logits, V, labels, scale, loss_sum, correct=None):
     p[torch.arange(z.shape[0]), labels] -= 1.0
     logits[:, :V] = (p * scale).to(torch.bfloat16)
     return logits
-
-
-def xent_from_stats(logits, V, stats, labels, scale, loss_sum, correct=None):
-    """softmax_xent with the row reduction taken from the LM-head GEMM's EPI_XENT_STATS_BF16
-    partials ``stats`` [M, ceil(ld/64), 2]: in place logits[:, :V] <- (softmax - onehot) * scale,
-    logits[:, V:] <- 0; loss_sum += sum CE (correct += argmax hits)."""
-    if _gpu(logits):
-        kernels().xent_from_stats(logits, int(V), stats, labels, float(scale), loss_sum, correct)
-        return logits
-    M = logits.shape[0]
-    st = stats.reshape(-1)[: M * ((logits.shape[1] + 63) // 64) * 2].view(M, -1, 2)
-    mx = st[..., 0].amax(1)
-    lse2 = mx + torch.log2((st[..., 1] * torch.exp2(st[..., 0] - mx[:, None])).sum(1))
-    z = logits[:, :V].float()
-    zl = z.gather(1, labels[:, None]).squeeze(1)
-    loss_sum += (lse2 / _L2E - zl).sum()
-    if correct is not None:
-        correct += (zl * _L2E >= mx).float().sum()
-    p = torch.exp2(z * _L2E - lse2[:, None])
-    p[torch.arange(M), labels] -= 1.0
-    logits[:, :V] = (p * scale).to(torch.bfloat16)
-    logits[:, V:] = 0
-    return logits
-
-
-def lm_head_xent(h, w, logits, stats, V, labels, scale, loss_sum):
-    """logits = h w^T (bf16, [M, Vpad]) with the softmax partials in the GEMM epilogue, then the
-    in-place cross-entropy gradient (xent_from_stats): the logits are read once more, not twice."""
-    M, K = h.shape[0], w.shape[1]
-    gemm(h, w, logits, M, logits.shape[1], K, False, False, EPI_XENT_STATS_BF16, colsum=stats, seg=V)
-    return xent_from_stats(logits, V, stats, labels, scale, loss_sum)
 
 
 def causal_softmax_fwd(S, T, P):

@@ -206,22 +206,10 @@ class Comm:
 
     def plan_stream(self):
         """The HIP stream on which lookahead key planning runs (one per rank, shared by tables).
-        MINIPS_PLAN_CUS=n confines it to n CUs spread over the chip (a CU-masked HIP stream), so
-        the latency-bound dedupe kernels cannot take every CU from the step's compute."""
+        (A CU-masked planning stream, which kept the latency-bound dedupe kernels off most CUs,
+        measured no better in round 2 and is gone.)"""
         if self._plan_stream is None and self.device.type == "cuda":
-            n = int(os.environ.get("MINIPS_PLAN_CUS", "0"))
-            if n > 0:
-                from .._native import kernels
-
-                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-                stride = max(1, ncu // n)
-                words = [0] * ((ncu + 31) // 32)
-                for cu in range(0, ncu, stride)[:n]:
-                    words[cu // 32] |= 1 << (cu % 32)
-                h = kernels().cu_masked_stream(self.device.index or 0, words)
-                self._plan_stream = torch.cuda.ExternalStream(h, device=self.device)
-            else:
-                self._plan_stream = dedicated_stream(self.device)
+            self._plan_stream = dedicated_stream(self.device)
         return self._plan_stream
 
     # -- helpers ------------------------------------------------------------------------

@@ -61,18 +61,18 @@ _SLOT_HEADER = 64
 # coarse-grained + the explicit release (ps_write_unlock: every XCD's L2 written back) / acquire
 # (the gathers' L2 invalidate) of onesided.hip, 1 fine-grained. Inboxes are always uncached, the
 # lock lines always fine-grained.
-_SHARD_MEM = int(os.environ.get("MINIPS_PS_SHARD_MEM", "0"))
+_SHARD_MEM = 0
 # inbox memory kind (default 2 uncached: the owner's apply reads what peers wrote, never an L2
-# copy of the slot from `depth` clocks ago); MINIPS_PS_INBOX_MEM=0 is an A/B timing knob only
-_INBOX_MEM = int(os.environ.get("MINIPS_PS_INBOX_MEM", "2"))
+# copy of the slot from `depth` clocks ago); PS_INBOX_MEM off is an A/B timing knob only
+_INBOX_MEM = 2
 _PUSH_STREAM = os.environ.get("MINIPS_PS_PUSH_STREAM", "0") == "1"
 if _PUSH_STREAM:
     # the push stream passes the 4-rank SSP GPU test only with system-fence planning-stream hand-off
     # events (profiles/r4/ab_push_stream.txt): never run the known-failing combination.
     # The feeder and the plan rings read this flag when they are built, after this import.
     streams.FAST_PLAN = False
-# MINIPS_PS_LOCKS=0: no owner locks (A/B timing only: reads may see half of a batch)
-_LOCKS = os.environ.get("MINIPS_PS_LOCKS", "1") != "0"
+# PS_LOCKS off: no owner locks (A/B timing only: reads may see half of a batch)
+_LOCKS = True
 
 
 def _align(n: int, a: int) -> int:
@@ -586,7 +586,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             # (profiles/r4/ab_push_stream.txt). Opt-in (MINIPS_PS_PUSH_STREAM=1): the 4-rank SSP test on
             # one GPU (tests/test_multirank_gpu.py::test_widedeep_ssp_world4_tracks_one_rank_bsp)
             # saw a loss spike with it on unless the planning stream's hand-off events (feeder and
-            # plan) carry a system fence too (MINIPS_FAST_PLAN_EVENTS=0): use the two together
+            # plan) carry a system fence too (FAST_PLAN_EVENTS off): use the two together
             pst = self._push_stream() if _PUSH_STREAM else None
             if pst is not None:
                 ev = self._push_evs.next()
@@ -1022,7 +1022,7 @@ class AsyncDenseTable(_AsyncTable):
     def slab_sink(self):
         """Split-K weight gradients left in fp32 planes that this table's push sums on the way into
         the inboxes (ops.linear_wgrad(defer=...): no reduce kernels, no pass through self.grad);
-        None off the GPU push path or with MINIPS_WGRAD_DEFER=0. The planes are rewritten by the
+        None off the GPU push path . The planes are rewritten by the
         next clock's GEMMs, which the stream order puts after this clock's push."""
         from .tables import _WGRAD_DEFER, _SlabSink
 

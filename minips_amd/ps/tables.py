@@ -71,10 +71,9 @@ class _Pipeline:
         self.staleness = staleness if consistency == "ssp" else (0 if consistency == "bsp" else asp_depth)
         overlap = _overlap_default() if overlap is None else overlap
         if consistency == "bsp":
-            # one rank has no communication to hide; MINIPS_OVERLAP_W1 lists the table kinds that
+            # one rank has no communication to hide; OVERLAP_W1 lists the table kinds that
             # still run their clock on a side stream there (the apply overlapping other compute)
-            w1_kinds = os.environ.get("MINIPS_OVERLAP_W1", "").split(",")
-            self.async_ = comm.device.type == "cuda" and overlap and (comm.world > 1 or w1 or kind in w1_kinds)
+            self.async_ = comm.device.type == "cuda" and overlap and (comm.world > 1 or w1)
         else:
             self.async_ = comm.device.type == "cuda" and self.staleness > 0
         self.stream = comm.new_stream() if self.async_ else None
@@ -148,9 +147,9 @@ def merge_buckets(starts, n_params: int, min_elems: float) -> list:
     return [0] + sorted(cuts)
 
 
-# MINIPS_WGRAD_DEFER=0: split-K weight gradients of one rank reduce into the gradient buffer (a
+# WGRAD_DEFER off: split-K weight gradients of one rank reduce into the gradient buffer (a
 # reduce kernel per GEMM) instead of being folded by the Adam kernel
-_WGRAD_DEFER = os.environ.get("MINIPS_WGRAD_DEFER", "1") != "0"
+_WGRAD_DEFER = True
 
 
 class _SlabSink:
@@ -503,7 +502,7 @@ class DenseTable:
         """A sink for split-K weight gradients whose K slices this table's next Adam folds in
         (ops.linear_wgrad(defer=...): no reduce kernel, no pass of the sum through the gradient
         buffer); None where the clock does not apply the whole gradient in one Adam kernel (several
-        ranks, buckets, other optimizers) or MINIPS_WGRAD_DEFER=0."""
+        ranks, buckets, other optimizers)."""
         if (not _WGRAD_DEFER or self.comm.world != 1 or self.optimizer != "adam" or self.comm.device.type != "cuda"
                 or (self.pipe.async_ and len(self._ring) < 2)):
             # (an asynchronous clock applies after the next step's GEMMs ran: those write the next
@@ -639,14 +638,14 @@ def _route_multiplier(num_rows: int) -> int:
 
 
 # the dedupe counts each unique key's lookups for the embedding-backward CSR (one pass less);
-# MINIPS_CSR_FUSED=0 counts in emb_build_csr instead
-_CSR_FUSED = os.environ.get("MINIPS_CSR_FUSED", "1") != "0"
-# MINIPS_SORTED_EMB=1: plans carry the CSR's inverse permutation (csr[2]: each lookup's row in
+# CSR_FUSED off counts in emb_build_csr instead
+_CSR_FUSED = True
+# SORTED_EMB on: plans carry the CSR's inverse permutation (csr[2]: each lookup's row in
 # member order) so the embedding dgrad writes its output pre-sorted and the backward streams it
 # contiguously instead of gathering 64-byte pieces. Measured on one MI355X (W&D step, 3 x 400
-# steps each, tools/gpu_ab.sh): 0.4244 vs 0.4151 ms with the gather path -- the segment sums get
+# steps each, tools/gpu_round.sh ab): 0.4244 vs 0.4151 ms with the gather path -- the segment sums get
 # faster (66 -> 36 us) but the dgrad's scattered 64-byte stores cost more -- so it is off.
-SORTED_EMB = os.environ.get("MINIPS_SORTED_EMB", "0") == "1"
+SORTED_EMB = False
 
 
 def _with_positions(csr):
@@ -689,15 +688,15 @@ class SparsePlan:
 # on one MI355X: sparse LR (16.6M rows, 4.2M keys: 0.5 B/key) 1.26 -> 0.83 ms/step; DLRM (10^8
 # rows, 426K keys: 29 B/key) 0.69 -> 0.71 ms (the map scans and the separate CSR build cost more
 # than the hash inserts there), so the default ratio keeps DLRM on the hash dedupe.
-# MINIPS_BITMAP_PLAN=0 keeps the hash dedupe everywhere.
-_BITMAP_PLAN = os.environ.get("MINIPS_BITMAP_PLAN", "1") != "0"
-_BITMAP_RATIO = int(os.environ.get("MINIPS_BITMAP_RATIO", "16"))
-# memory-side atomics slow the concurrently running step; MINIPS_SORT_PLAN=0 keeps the hash path
-_SORT_PLAN = os.environ.get("MINIPS_SORT_PLAN", "1") != "0"
+# BITMAP_PLAN off keeps the hash dedupe everywhere.
+_BITMAP_PLAN = True
+_BITMAP_RATIO = 16
+# memory-side atomics slow the concurrently running step; SORT_PLAN off keeps the hash path
+_SORT_PLAN = True
 
 # one rank: W&D assembles its input straight from the fp32 shard (SparseTable.get_source +
-# ops.wd_assemble_tab) instead of gathering the batch's unique rows first (MINIPS_FUSED_ASSEMBLE=0)
-_FUSED_ASSEMBLE = os.environ.get("MINIPS_FUSED_ASSEMBLE", "1") == "1"
+# ops.wd_assemble_tab) instead of gathering the batch's unique rows first (FUSED_ASSEMBLE off)
+_FUSED_ASSEMBLE = True
 
 
 class _PendingPlan:

@@ -13,10 +13,10 @@ import os
 
 import torch
 
-# MINIPS_FAST_EVENTS=0: the step's ordering events are plain torch events (A/B);
-# MINIPS_FAST_PLAN_EVENTS=0: only the planning stream's hand-off events (diagnostics)
-FAST = os.environ.get("MINIPS_FAST_EVENTS", "1") != "0"
-FAST_PLAN = FAST and os.environ.get("MINIPS_FAST_PLAN_EVENTS", "1") != "0"
+# FAST_EVENTS off: the step's ordering events are plain torch events (A/B);
+# FAST_PLAN_EVENTS off: only the planning stream's hand-off events (diagnostics)
+FAST = True
+FAST_PLAN = True
 
 # MINIPS_STREAM_DELAY_US=n (race diagnostics, tests/test_multirank_gpu.py): every work segment
 # issued on another stream through use() or SideStream.fork() starts with an n-us device spin, so a

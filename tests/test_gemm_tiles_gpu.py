@@ -1,7 +1,7 @@
 """Every GEMM kernel variant against the fp32 reference, incl. M/N/K tails, split-K and batched
 mode. The tile/kernel choice is read from the environment once per process, so each variant runs
-in its own subprocess (one at a time): v3 (256x256 phase-split, 8 waves), v2 256x256 (16 waves),
-v2 128x128, and the v1 / v2 / v3 weight-gradient paths."""
+in its own subprocess (one at a time): the LDS-DMA v2 kernel at its three tiles (256x256 with 16
+waves, 256x128, 128x128) and the register-staged v1 (the > 2 GiB operand fallback)."""
 import os
 import subprocess
 import sys
@@ -64,14 +64,11 @@ print("ok", worst)
 
 
 @pytest.mark.parametrize("env", [
-    {"MINIPS_GEMM_V4": "4"},                                    # v5 (ping-pong 256x256) everywhere
-    {"MINIPS_SPLITK_FOLD": "1"},                                # split-K planes folded in the GEMM
-    {"MINIPS_GEMM_V4": "2"},                                    # v4 (quarter-staged 256x256) everywhere
-    {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "1"},         # v3
-    {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "1", "MINIPS_GEMM_V3_EARLY": "0", "MINIPS_GEMM_WGRAD": "v3"},
-    {"MINIPS_GEMM_TILE": "256", "MINIPS_GEMM_V3": "0"},         # v2 256x256
-    {"MINIPS_GEMM_TILE": "128", "MINIPS_GEMM_WGRAD": "v2"},     # v2 128x128 incl. wgrad
-    {},                                                         # defaults (v1 wgrad, slab reduce)
+    {"MINIPS_GEMM_TILE": "256"},                                # v2 256x256 everywhere
+    {"MINIPS_GEMM_TILE": "200"},                                # v2 256x128 everywhere
+    {"MINIPS_GEMM_TILE": "128"},                                # v2 128x128 everywhere
+    {"MINIPS_GEMM_TILE": "1"},                                  # the register-staged v1 (> 2 GiB operands)
+    {},                                                         # defaults (tile by wave quantisation)
 ])
 def test_gemm_variant(env):
     e = dict(os.environ, **env)

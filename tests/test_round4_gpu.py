@@ -13,40 +13,6 @@ def _kernels():
     return kernels()
 
 
-@pytest.mark.parametrize("B", [16384, 10000, 9998, 4096])
-def test_plan_sorted_chunked_matches_one_workgroup(dev, B):
-    """sort_mode 4 (chunk LSD sort + galloping merge + heads) gives exactly the outputs of
-    sort_mode 1, including low-cardinality columns (thousands of equal keys per chunk)."""
-    from minips_amd import ops
-
-    cards = [3, 7, 1000, 50000, 2, 300000, 16, 12345]
-    g = torch.Generator(device="cpu").manual_seed(B)
-    cols, base = [], 0
-    bases = []
-    for c in cards:
-        # Zipf-like skew: half the lookups hit the first 1 % of the column's ids
-        hot = torch.randint(0, max(1, c // 100), (B,), generator=g)
-        cold = torch.randint(0, c, (B,), generator=g)
-        pick = torch.rand(B, generator=g) < 0.5
-        cols.append(torch.where(pick, hot, cold) + base)
-        bases.append(base)
-        base += c
-    keys = torch.stack(cols, 1).to(dev)
-    col_base = torch.tensor(bases, dtype=torch.int64, device=dev)
-    bits = [max(1, (c - 1).bit_length()) for c in cards]
-    ref = ops.plan_sorted(keys, col_base, bits, sort_mode=1)
-    got = ops.plan_sorted(keys, col_base, bits, sort_mode=4)
-    torch.cuda.synchronize()
-    assert len(ref) == len(got) == 9  # one owner: (uniq, inv, counts, U, members, memrow, pos, rowstart, rowidx)
-    U = int(ref[3].reshape(-1)[0])
-    assert int(got[3].reshape(-1)[0]) == U
-    assert torch.equal(ref[0][:U], got[0][:U])  # unique keys (entries past U are scratch)
-    for i in (1, 2, 4, 5):  # inv, counts, members, memrow
-        assert torch.equal(ref[i], got[i]), i
-    assert ref[6] is None and got[6] is None and ref[8] is None and got[8] is None
-    assert torch.equal(ref[7][: U + 1], got[7][: U + 1])  # row starts
-
-
 def test_multi_copy_matches_copy(dev):
     k = _kernels()
     srcs = [torch.randn(1000, device=dev), torch.randint(0, 1 << 40, (777,), device=dev),

@@ -108,26 +108,12 @@ def cmd_gemm(a):
         shapes = [(n, int(m), int(nn), int(k), lay) for n, m, nn, k, lay in (s.split(":") for s in a.shapes.split(","))]
     else:
         shapes = GPT2_SHAPES if a.set == "gpt2" else WD_SHAPES
-    # --v4 0,2: the same shapes under several v4 modes (ops.gemm_set_v4_mode), interleaved in one process
-    modes = [int(m) for m in a.v4.split(",")] if a.v4 else [None]
-    from minips_amd._native import kernels
-
-    def with_mode(m, f):
-        if m is None:
-            return f
-
-        def g():
-            kernels().gemm_set_v4_mode(m)
-            f()
-        return g
-
-    names = [f"ours{'' if m is None else f'[v4={m}]'}" for m in modes]
-    tot = {k: 0.0 for k in names + (["hipblaslt"] if a.lib else [])}
+    tot = {k: 0.0 for k in ["ours"] + (["hipblaslt"] if a.lib else [])}
     for name, M, N, K, lay in shapes:
         a_km, b_kn = LAYOUTS[lay]
         A, B, C = gemm_operands(M, N, K, lay)
         At, Bt = (A.t() if a_km else A), (B if b_kn else B.t())
-        fns = {n: with_mode(m, ours_gemm(A, B, C, M, N, K, lay, a.split)) for n, m in zip(names, modes)}
+        fns = {"ours": ours_gemm(A, B, C, M, N, K, lay, a.split)}
         if a.lib:
             fns["hipblaslt"] = lambda: torch.matmul(At, Bt)
         med = median_rounds(fns)
@@ -235,19 +221,8 @@ def cmd_nn(a):
     loss = torch.zeros(1, device=dev())
     rows.append(("softmax_xent (in place)",
                  timed(lambda: ops.softmax_xent(logits, 50257, labels, 1.0 / M, loss), 10), 2 * M * V * 2))
-    stats = torch.empty(M * (V // 64) * 2, device=dev())
-    h = torch.randn(M, C, **bf)
-    w = torch.randn(V, C, **bf) * 0.05
-    ops.gemm(h, w, logits, M, V, C, False, False, ops.EPI_XENT_STATS_BF16, colsum=stats, seg=50257)
-    rows.append(("xent_from_stats (in place)",
-                 timed(lambda: ops.xent_from_stats(logits, 50257, stats, labels, 1.0 / M, loss), 10), 2 * M * V * 2))
-    t_plain = timed(lambda: ops.gemm(h, w, logits, M, V, C, False, False, ops.EPI_STORE_BF16), 10)
-    t_stats = timed(lambda: ops.gemm(h, w, logits, M, V, C, False, False, ops.EPI_XENT_STATS_BF16, colsum=stats,
-                                     seg=50257), 10)
     for name, us, nbytes in rows:
         print(f"{name:32s} {us:9.1f} us  {nbytes / us / 1e6:6.2f} TB/s")
-    print(f"LM-head GEMM 8192x50304x768: plain bf16 store {t_plain:.1f} us, "
-          f"with the xent-stats epilogue {t_stats:.1f} us")
 
 
 def cmd_emb(a):
@@ -386,7 +361,6 @@ def main(argv=None):
     sub = ap.add_subparsers(dest="cmd", required=True)
     p = sub.add_parser("gemm")
     p.add_argument("--set", default=os.environ.get("GEMM_SET", "wd"), choices=["wd", "gpt2"])
-    p.add_argument("--v4", default="", help="gemm: compare these v4 modes (e.g. 0,2) in one process")
     p.add_argument("--no-lib", dest="lib", action="store_false", help="gemm: skip the hipBLASLt column")
     p.add_argument("--shapes", default=os.environ.get("GEMM_SHAPES", ""))
     p.add_argument("--split", type=int, default=1, help="split-K of the nt / nn shapes (slab + reduce)")

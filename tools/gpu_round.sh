@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU-box pass; every GPU step has its own time limit and any failure stops the script.
-#   bash tools/gpu_round.sh [all|smoke|test|bench|prof|trace|audit|micro|models|models-prof]
+#   bash tools/gpu_round.sh STAGE [STAGE ...]     (stages run in the order given; default: all)
 #     all          smoke + GPU tests + short bench + rocprofv3 kernel stats of the bench
 #     trace        kernel trace of the W&D bench per MINIPS_GRAPH mode in MODES (default "0"), with the
 #                  steady-state step breakdown (tools/prof_summary.py trace)
@@ -9,13 +9,22 @@
 #     models       bench lines of the other BASELINE configs (MODELS, default "mlp dlrm dlrm-10b gpt2")
 #     models-prof  rocprofv3 kernel stats of those model steps (MODELS)
 #     emu          bench.py --emulate-world N (EMU_WORLDS, default "2 8") next to N=1, kernel trace of N=EMU_PROF
-# Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, MODES.
+#     ab           interleaved A/B: variants are ';'-separated env lists in AB, each run RUNS times (default 2)
+#                  round-robin (`base`: no env); a variant may start with `tree=<dir>` to run another built tree (e.g. the
+#                  previous round's, checked out and built in-tree under ab_old/). With the default CMD
+#                  (bench.py, STEPS default 300) it prints ms/step per run, else the command's output tail:
+#                    AB='tree=ab_old;base' bash tools/gpu_round.sh ab         (previous round vs this tree)
+#                    CMD='python tools/bench_kernels.py kscan --Ks 848' AB='MINIPS_GEMM_TILE=128;MINIPS_GEMM_TILE=256'
+#     pytest       one pytest selection: PYTEST_SEL (e.g. 'tests/test_multirank_gpu.py -k ssp'), env PYTEST_ENV
+# Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, MODES, AB, RUNS, CMD, TAIL, PYTEST_SEL, PYTEST_ENV.
+# This one runner replaces the per-experiment command files of rounds 1-4 (git history keeps them).
 set -eo pipefail
 cd "$(dirname "$0")/.."
+ROOT=$(pwd)
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-STAGE=${1:-all}
 prof_env() { cd /tmp && export TMPDIR=/tmp && cd - > /dev/null; }
+for STAGE in "${@:-all}"; do
 if [[ $STAGE == all || $STAGE == smoke ]]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
   tail -3 gpurun_out/smoke.log
@@ -90,3 +99,25 @@ if [[ $STAGE == emu ]]; then
   python tools/prof_summary.py trace $d/run_kernel_trace.csv --anchor wd_head_kernel --skip 8 --top 40 > $d.trace.txt
   head -60 $d.trace.txt
 fi
+if [[ $STAGE == ab ]]; then
+  IFS=';' read -ra VARIANTS <<< "${AB:-base}"
+  for i in $(seq "${RUNS:-2}"); do
+    for v in "${VARIANTS[@]}"; do
+      dir=$ROOT; envs=$v; [[ $v == base ]] && envs=""
+      if [[ $v == tree=* ]]; then dir=$ROOT/${v%% *}; dir=${dir/tree=/}; envs=${v#* }; [[ $envs == tree=* ]] && envs=""; fi
+      if [[ -z "${CMD}" ]]; then
+        (cd "$dir" && env $envs timeout -k 10 300 python bench.py --steps "${STEPS:-300}" --warmup 10 ${BENCH_ARGS} > $ROOT/gpurun_out/ab.log 2>&1) || { tail -20 gpurun_out/ab.log; exit 1; }
+        python -c "import json; d=json.loads([l for l in open('gpurun_out/ab.log') if l.startswith('{')][-1]); print('[$v]', d['ms_per_step'])"
+      else
+        echo "== [$v] (run $i)"
+        (cd "$dir" && env $envs timeout -k 10 300 ${CMD} > $ROOT/gpurun_out/ab.log 2>&1) || { tail -20 gpurun_out/ab.log; exit 1; }
+        tail -${TAIL:-20} gpurun_out/ab.log
+      fi
+    done
+  done
+fi
+if [[ $STAGE == pytest ]]; then
+  env ${PYTEST_ENV} timeout -k 10 ${PYTEST_TIMEOUT:-600} python -u -m pytest ${PYTEST_SEL:-tests -m gpu} -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_sel.log 2>&1 || { tail -40 gpurun_out/pytest_sel.log; exit 1; }
+  tail -5 gpurun_out/pytest_sel.log
+fi
+done

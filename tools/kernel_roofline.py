@@ -18,7 +18,7 @@ import statistics
 PEAK_TF, PEAK_TB = 2500.0, 8.0
 B, F, D, ND = 16384, 26, 32, 13
 K1, H1, H2, H3 = 896, 1024, 512, 256
-K2, K3 = 1024, 512            # layers 2 / 3 K (bias vectors, MINIPS_WD_BIAS=vec default since round 4)
+K2, K3 = 1024, 512            # layers 2 / 3 K (bias vectors)
 W = 36                        # sparse row: 32 emb + wide + pad (fp32 in the table)
 
 
