@@ -22,6 +22,8 @@ import time
 
 # 8 HIP hardware queues (the step's 6-7 streams otherwise share 4 and serialise; see
 # minips_amd/__init__.py): HIP reads this when torch loads it, so before the torch import
+if "--host-phases" in sys.argv:  # before the package import: metrics reads it once
+    os.environ["MINIPS_ROCTX"] = "host"
 if os.environ.get("GPU_MAX_HW_QUEUES", "4") == "4":  # unset or HIP's default (the GPU box exports 4)
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MINIPS_HW_QUEUES", "8")
 
@@ -47,6 +49,8 @@ def main():
     ap.add_argument("--bucket_mb", type=float, default=2.0,
                     help="several ranks: dense-clock bucket size in MB (layers merged from the last one; 0 = one "
                          "reduce-scatter + all-gather after the backward)")
+    ap.add_argument("--host-phases", type=int, default=0,
+                    help="after the timed region: this many steps with per-phase host issue time (stderr)")
     ap.add_argument("--diag-steps", type=int, default=None,
                     help="after the timed run: N more steps with per-collective timing and the host-sync audit, "
                          "reported in the JSON line under 'diag' (default 10 with several ranks, else 0)")
@@ -252,6 +256,25 @@ def main():
               file=sys.stderr, flush=True)
         pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
         pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
+    if args.host_phases > 0:  # after the timed region: inclusive host time per phase, per step
+        from minips_amd.utils import metrics
+
+        metrics.host_times_reset()
+        t1 = time.perf_counter()
+        for _ in range(args.host_phases):
+            with metrics.phase("step"):
+                step()
+        issue = (time.perf_counter() - t1) / args.host_phases
+        model.drain()
+        sync()
+        wall = (time.perf_counter() - t1) / args.host_phases
+        rows = sorted(metrics.HOST_TIMES.items(), key=lambda kv: -kv[1][0])
+        print(f"[host-phases] issue {issue * 1e3:.4f} ms/step, wall {wall * 1e3:.4f} ms/step "
+              f"(world {n}{' emulated' if emulated else ''})", file=sys.stderr)
+        for name, (ns, calls) in rows:
+            print(f"[host-phases] {ns / 1e3 / args.host_phases:9.1f} us/step {calls / args.host_phases:6.2f} "
+                  f"calls/step  {name}", file=sys.stderr)
+        sys.stderr.flush()
     if n > 1 and comm.initialized:
         dist.barrier()
         dist.destroy_process_group()

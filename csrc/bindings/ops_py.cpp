@@ -24,6 +24,25 @@ hipStream_t stream_of(const at::Tensor& t) {
   return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
+// Several outputs carved out of ONE caching-allocator block (256-byte aligned views): a planner
+// call hands back ~10 tensors, and one allocation + views costs a fraction of ten allocations on
+// the step's host path. The block lives while any of its views does.
+std::vector<at::Tensor> carve(const at::TensorOptions& o, const std::vector<std::pair<int64_t, at::ScalarType>>& parts) {
+  std::vector<int64_t> offs;
+  int64_t total = 0;
+  for (const auto& p : parts) {
+    offs.push_back(total);
+    total += (p.first * (int64_t)c10::elementSize(p.second) + 255) & ~int64_t(255);
+  }
+  at::Tensor buf = at::empty({std::max<int64_t>(total, 256)}, o.dtype(at::kByte));
+  std::vector<at::Tensor> out;
+  out.reserve(parts.size());
+  for (size_t i = 0; i < parts.size(); ++i)
+    out.push_back(buf.narrow(0, offs[i], parts[i].first * (int64_t)c10::elementSize(parts[i].second))
+                      .view(parts[i].second));
+  return out;
+}
+
 void check_gpu(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
@@ -362,6 +381,40 @@ void owner_rows_adagrad(at::Tensor& table, at::Tensor& state, const c10::optiona
                                (float)eps, stream_of(table));
 }
 
+// direct-addressed owner apply of one push (kernels.h owner_push_adagrad); rs: int32 [rows_local * P * 2]
+void owner_push_adagrad(at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
+                        const at::Tensor& keys, int64_t base, const at::Tensor& recv, std::vector<int64_t> splits,
+                        at::Tensor& rs, int64_t stamp, double lr, double eps) {
+  TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.stride(1) == 1, "table must be a row-major GPU matrix");
+  check_dtype(table, at::kFloat, "table");
+  check_gpu(state, "state");
+  check_gpu(keys, "keys");
+  check_dtype(keys, at::kLong, "keys");
+  check_gpu(recv, "recv");
+  check_gpu(rs, "rs");
+  check_dtype(rs, at::kInt, "rs");
+  TORCH_CHECK(recv.scalar_type() == at::kFloat || recv.scalar_type() == at::kBFloat16, "recv: fp32 or bf16 rows");
+  TORCH_CHECK(recv.dim() == 2 && recv.is_contiguous() && recv.size(1) <= table.size(1), "recv [M, D] contiguous");
+  const int P = (int)splits.size();
+  TORCH_CHECK(P >= 1 && P <= minips_k::kOwnerMaxP, "owner_push_adagrad: 1..16 requesters");
+  minips_k::OwnerSegs segs{};
+  int64_t off = 0;
+  for (int p = 0; p < P; ++p) {
+    segs.off[p] = off;
+    off += splits[p];
+  }
+  segs.off[P] = off;
+  TORCH_CHECK(off == keys.numel() && off <= recv.size(0), "owner_push_adagrad: splits must sum to the received keys");
+  TORCH_CHECK(rs.is_contiguous() && rs.numel() >= table.size(0) * P * 2, "owner_push_adagrad: rs [rows * P] int2");
+  TORCH_CHECK(off < (int64_t)INT32_MAX, "owner_push_adagrad: < 2^31 received rows");
+  float* s2 = opt_ptr<float>(state2, at::kFloat, "state2");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  minips_k::owner_push_adagrad(ptr<float>(table), table.stride(0), ptr<float>(state), s2, (int)D1, ptr<int64_t>(keys),
+                               off, base, table.size(0), (int)recv.size(1), recv.data_ptr(),
+                               recv.scalar_type() == at::kBFloat16, segs, P, rs.data_ptr(), (int)stamp, (float)lr,
+                               (float)eps, stream_of(table));
+}
+
 void sparse_rowwise_adagrad(at::Tensor& table, at::Tensor& state, const c10::optional<at::Tensor>& state2, int64_t D1,
                             const at::Tensor& keys, int64_t base, const at::Tensor& grads, double lr, double eps,
                             const c10::optional<at::Tensor>& n_dev, bool zero_g) {
@@ -588,21 +641,22 @@ std::vector<at::Tensor> plan_sorted(const at::Tensor& keys, const at::Tensor& co
   TORCH_CHECK(col_base.numel() == F && col_bits.numel() == F && (int64_t)col_bits_host.size() == F,
               "one base / bit count per column");
   // the host copy of the device bit counts is what is validated (the kernel trusts the device one)
-  for (int64_t b : col_bits_host) TORCH_CHECK(b >= 1 && b <= 32, "col_bits: 1..32");
+  const int obits = P > 1 ? minips_k::plan_owner_bits((int)P) : 0;
+  for (int64_t b : col_bits_host)
+    TORCH_CHECK(b >= 1 && b + obits <= 32, "col_bits: 1..32, owner bits included (plan_sorted_ok)");
   const int64_t n = B * F;
-  auto o64 = keys.options();
-  const int64_t nchunks = (n + 1023) / 1024;
-  auto ws = at::empty({7 * n + F + 4 + 2 * nchunks * P}, o64.dtype(at::kInt));  // see kernels.h
-  auto ukey = at::empty({n}, o64), uniq = at::empty({n}, o64), inv = at::empty({n}, o64);
-  auto members = at::empty({n}, o64.dtype(at::kInt)), memrow = at::empty({n}, o64.dtype(at::kInt));
-  auto counts = at::empty({P + 1}, o64);
-  at::Tensor pos = with_positions ? at::empty({n}, o64.dtype(at::kInt)) : at::Tensor();
-  // one owner: each row's lookup range in member order (the row-parallel embedding backward)
-  at::Tensor rowstart = P == 1 ? at::empty({n + 1}, o64.dtype(at::kInt)) : at::Tensor();
+  // one owner: each row's lookup range in member order (the row-parallel embedding backward);
   // one owner, routed keys below 2^31: each lookup's table row (the input assembly's index)
-  at::Tensor rowidx = (P == 1 && route_mult && route_n > 0 && route_n <= INT32_MAX)
-                          ? at::empty({n}, o64.dtype(at::kInt))
-                          : at::Tensor();
+  const bool want_rs = P == 1, want_ri = P == 1 && route_mult && route_n > 0 && route_n <= INT32_MAX;
+  auto parts = carve(keys.options(), {{minips_k::plan_sorted_ws_ints(n, (int)F, (int)P), at::kInt},
+                                      {n, at::kLong}, {n, at::kLong}, {n, at::kLong}, {n, at::kInt}, {n, at::kInt},
+                                      {P + 1, at::kLong}, {with_positions ? n : 0, at::kInt},
+                                      {want_rs ? n + 1 : 0, at::kInt}, {want_ri ? n : 0, at::kInt}});
+  auto &ws = parts[0], &ukey = parts[1], &uniq = parts[2], &inv = parts[3], &members = parts[4], &memrow = parts[5],
+       &counts = parts[6];
+  at::Tensor pos = with_positions ? parts[7] : at::Tensor();
+  at::Tensor rowstart = want_rs ? parts[8] : at::Tensor();
+  at::Tensor rowidx = want_ri ? parts[9] : at::Tensor();
   c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
   minips_k::plan_sorted(ptr<int64_t>(keys), (int)B, (int)F, ptr<int64_t>(col_base), col_bits.data_ptr<int32_t>(),
                         (uint64_t)route_mult, (uint64_t)route_n, ptr<int64_t>(bounds), (int)P, ws.data_ptr<int32_t>(),
@@ -1601,6 +1655,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("owner_rows_adagrad", &owner_rows_adagrad, py::arg("table"), py::arg("state"), py::arg("state2"),
         py::arg("D1"), py::arg("keys"), py::arg("n"), py::arg("n_dev"), py::arg("base"), py::arg("recv"),
         py::arg("P"), py::arg("slots"), py::arg("lr"), py::arg("eps"));
+  m.def("owner_push_adagrad", &owner_push_adagrad, py::arg("table"), py::arg("state"), py::arg("state2"),
+        py::arg("D1"), py::arg("keys"), py::arg("base"), py::arg("recv"), py::arg("splits"), py::arg("rs"),
+        py::arg("stamp"), py::arg("lr"), py::arg("eps"));
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("members") = py::none(),
         py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);

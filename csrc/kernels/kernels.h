@@ -99,6 +99,11 @@ void owner_slots(const int64_t* own_inv, int64_t M, const OwnerSegs& segs, int P
 void owner_rows_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys, int64_t n,
                         const int64_t* n_dev, int64_t base, int D, const void* recv, bool recv_bf16, int P,
                         const int* slots, float lr, float eps, hipStream_t s);
+// owner_mark + owner_apply: the direct-addressed owner apply of one push (rs: [rows_local * P]
+// int2 {stamp, received row}, persistent; stamp: this push's number, >= 0, increasing)
+void owner_push_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys, int64_t M,
+                        int64_t base, int64_t rows_local, int D, const void* recv, bool recv_bf16,
+                        const OwnerSegs& segs, int P, void* rs, int stamp, float lr, float eps, hipStream_t s);
 void scatter_add_rows(const float* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s);
 void scatter_add_rows_bf16(const bf16_t* src, int64_t n, int D, const int64_t* idx, float* acc, hipStream_t s);
 // Row-wise Adagrad on a shard (one accumulator per row, DLRM style):
@@ -179,6 +184,9 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
                  uint64_t route_mult, uint64_t route_n, const int64_t* bounds, int P, int32_t* ws, int64_t* ukey,
                  int64_t* uniq, int64_t* inv, int32_t* members, int32_t* memrow, int64_t* counts, hipStream_t s,
                  int32_t* pos = nullptr, int32_t* rowstart = nullptr, int32_t* rowidx = nullptr);
+// plan_sorted's int32 workspace for n = B * F lookups; owner bits of the sort key for P owners
+int64_t plan_sorted_ws_ints(int64_t n, int F, int P);
+int plan_owner_bits(int P);
 // (pos, nullable: pos[members[m]] = m, emb_csr_positions fused; rowstart, nullable, one owner only:
 // rowstart[u] = first member of row u, rowstart[U] = B*F)
 // out[c] += column sums of x (bf16 [M, N], row stride ld; N, ld multiples of 8): a bias gradient.

@@ -19,9 +19,12 @@
 //                  free -- members (lookup ids grouped by u, ascending) and memrow (their u).
 //
 // Deterministic (no global atomics, stable sort); unique keys come out column-major, ascending
-// inside a column; with several owners (P > 1, a multi-rank table) they are then regrouped by
-// owner shard (plan_owner_*: stable counting sort over chunks), inv/memrow pointing at the
-// regrouped positions.
+// inside a column. With several owners (P > 1, a multi-rank table) the sort key carries the
+// owner shard of the routed key above the column-relative key (plan_transpose computes it), so
+// each column's unique keys come out grouped by owner; plan_sort_col counts them per owner and
+// plan_emit places unique (column c, owner p, k-th) at
+//   (keys of owners < p) + (owner p's keys in columns < c) + k
+// -- grouped by owner, column-major inside an owner -- with no separate regrouping pass.
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
@@ -69,20 +72,38 @@ __device__ __forceinline__ uint32_t ps_count(uint64_t lo, uint64_t hi, int d) {
 
 // [B, F] int64 keys -> column-major [F, B] uint32 (key - base_f) through a 64 x F LDS tile: the
 // sort reads its column as contiguous 16-byte vectors instead of one 8-byte key per 208-byte row
-// (that strided column gather pulled the whole batch through each sorting CU: ~70 us fixed cost)
+// (that strided column gather pulled the whole batch through each sorting CU: ~70 us fixed cost).
+// P > 1: the owner shard of the routed key goes above bit col_bits[f] (the sort then groups by it).
+__device__ __forceinline__ int64_t ps_route(int64_t key, uint64_t mult, uint64_t rn);
+__device__ __forceinline__ int ps_owner(const int64_t* bounds, int P, int64_t k);
+
 __global__ __launch_bounds__(256) void plan_transpose_kernel(const int64_t* __restrict__ keys, int B, int F,
                                                              const int64_t* __restrict__ col_base,
+                                                             const int32_t* __restrict__ col_bits,
+                                                             const int64_t* __restrict__ bounds, int P,
+                                                             uint64_t rmult, uint64_t rn,
                                                              uint32_t* __restrict__ krel) {
   __shared__ uint32_t tile[64][65];
   __shared__ int64_t basef[64];
+  __shared__ int bitsf[64];
+  __shared__ int64_t sb[17];
   const int t = threadIdx.x;
-  if (t < F) basef[t] = col_base[t];
+  if (t < F) {
+    basef[t] = col_base[t];
+    bitsf[t] = col_bits[t];
+  }
+  if (t <= P && P > 1) sb[t] = bounds[t];
   const int b0 = blockIdx.x * 64;
   __syncthreads();
   for (int e = t; e < 64 * F; e += 256) {  // coalesced row-major reads
     const int r = e / F, c = e - r * F;
     const int b = b0 + r;
-    if (b < B) tile[c][r] = (uint32_t)(keys[(int64_t)b * F + c] - basef[c]);
+    if (b < B) {
+      const int64_t key = keys[(int64_t)b * F + c];
+      uint32_t v = (uint32_t)(key - basef[c]);
+      if (P > 1) v |= (uint32_t)ps_owner(sb, P, ps_route(key, rmult, rn)) << bitsf[c];
+      tile[c][r] = v;
+    }
   }
   __syncthreads();
   for (int e = t; e < 64 * F; e += 256) {  // coalesced column-major writes
@@ -95,17 +116,23 @@ __global__ __launch_bounds__(256) void plan_transpose_kernel(const int64_t* __re
 __global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const uint32_t* __restrict__ krel, int B,
                                                                    const int64_t* __restrict__ col_base,
                                                                    const int32_t* __restrict__ col_bits,
+                                                                   int obits, int P,
                                                                    int32_t* __restrict__ sorted_b,
                                                                    int32_t* __restrict__ local_u,
                                                                    int64_t* __restrict__ ukey,
-                                                                   int32_t* __restrict__ ucount) {
+                                                                   int32_t* __restrict__ ucount,
+                                                                   int32_t* __restrict__ ocnt) {
   __shared__ __attribute__((aligned(16))) uint16_t cnt[16 * kPsThreads];  // [digit][thread] counts -> offsets
   __shared__ __attribute__((aligned(16))) uint32_t skey[kPsMax];
   __shared__ __attribute__((aligned(16))) uint16_t sval[kPsMax];
   __shared__ uint32_t ws[20];
+  __shared__ uint32_t lc[16];  // unique keys per owner (P > 1)
   const int t = threadIdx.x, f = blockIdx.x;
   const int64_t base = col_base[f];
-  const int nbits = col_bits[f];  // a small-cardinality column sorts in fewer passes
+  const int kbits = col_bits[f];
+  const int nbits = kbits + obits;  // a small-cardinality column sorts in fewer passes
+  const uint32_t kmask = kbits >= 32 ? 0xffffffffu : ((1u << kbits) - 1u);
+  if (t < 16) lc[t] = 0;
   uint32_t k[kPsItems];
   uint32_t v[kPsItems];
   const uint32_t* col = krel + (int64_t)f * B;
@@ -220,9 +247,16 @@ __global__ __launch_bounds__(kPsThreads) void plan_sort_col_kernel(const uint32_
     const uint32_t lu = run - 1;
     sorted_b[col0 + pos] = (int32_t)v[q];
     local_u[col0 + pos] = (int32_t)lu;
-    if (h) ukey[col0 + lu] = base + (int64_t)k[q];
+    if (h) {
+      ukey[col0 + lu] = base + (int64_t)(k[q] & kmask);
+      if (P > 1) atomicAdd(&lc[k[q] >> kbits], 1u);  // (LDS: the owner bits above the key)
+    }
   }
   if (t == 0) ucount[f] = (int32_t)total;
+  if (P > 1) {
+    __syncthreads();
+    if (t < P) ocnt[f * P + t] = (int32_t)lc[t];
+  }
 }
 
 // (key * mult) mod rn. The 64-bit integer remainder is a long software routine on the GPU; for the
@@ -281,158 +315,56 @@ __device__ __forceinline__ int64_t ps_ukey_routed(int64_t u, int F, int B, const
   return ps_route(ukey[(int64_t)lo * B + (u - basef[lo])], rmult, rn);
 }
 
-// ---- several owners (multi-rank tables): the unique keys are regrouped by owner shard with a
-// stable counting sort over chunks of kPoChunk unique indices -- per-chunk owner counts, one
-// scan per owner over the chunks, then each chunk places its keys (no atomics anywhere).
-constexpr int kPoChunk = 1024, kPoMaxP = 16;
+constexpr int kPoMaxP = 16;
 
-__global__ __launch_bounds__(256) void plan_owner_count_kernel(int B, int F, const int64_t* __restrict__ ukey,
-                                                               const int32_t* __restrict__ ucount,
-                                                               const int64_t* __restrict__ bounds, int P,
-                                                               uint64_t rmult, uint64_t rn,
-                                                               int32_t* __restrict__ ocnt) {
-  __shared__ int64_t basef[65];
-  __shared__ int32_t ucf[64];
-  __shared__ int64_t sb[kPoMaxP + 1];
-  __shared__ uint32_t lc[kPoMaxP];
+// P > 1: per block, from the per-column per-owner unique counts ocnt[F][P]: the owner offsets
+// obase[p], the column prefixes colpre[c][p] (owner p's keys in columns < c) and the column-local
+// starts cstart[c][p] (the column's keys of owners < p)
+struct PoLayout {
+  int64_t obase[kPoMaxP + 1];
+  int32_t colpre[64][kPoMaxP];
+  int32_t cstart[64][kPoMaxP + 1];
+};
+
+__device__ void po_layout(const int32_t* __restrict__ ocnt, int F, int P, PoLayout* L) {
   const int t = threadIdx.x;
-  if (t <= P) sb[t] = bounds[t];
-  if (t < P) lc[t] = 0;
-  const int64_t U = ps_col_prefix(ucount, F, basef, ucf);
-  const int64_t u0 = (int64_t)blockIdx.x * kPoChunk;
-  for (int e = t; e < kPoChunk; e += 256) {
-    const int64_t u = u0 + e;
-    if (u < U) atomicAdd(&lc[ps_owner(sb, P, ps_ukey_routed(u, F, B, basef, ukey, rmult, rn))], 1u);
+  if (t < P) {  // one owner per thread: prefix over the columns
+    int32_t acc = 0;
+    for (int c = 0; c < F; ++c) {
+      L->colpre[c][t] = acc;
+      acc += ocnt[c * P + t];
+    }
+    L->obase[t + 1] = acc;  // (owner t's total, prefixed below)
+  }
+  if (t >= 64 && t < 64 + F) {  // one column per thread: prefix over the owners
+    const int c = t - 64;
+    int32_t acc = 0;
+    for (int p = 0; p < P; ++p) {
+      L->cstart[c][p] = acc;
+      acc += ocnt[c * P + p];
+    }
+    L->cstart[c][P] = acc;
   }
   __syncthreads();
-  if (t < P) ocnt[(int64_t)blockIdx.x * P + t] = (int32_t)lc[t];
+  if (t == 0) {
+    L->obase[0] = 0;
+    for (int p = 0; p < P; ++p) L->obase[p + 1] += L->obase[p];
+  }
+  __syncthreads();
 }
 
-// one block: ooff[chunk][p] = (keys of owners < p) + (keys of owner p in earlier chunks);
-// counts[p] = keys of owner p, counts[P] = U. Every thread loads its chunks' P counts at once (one
-// memory round trip; the per-owner loop of loads and barriers was a 23 us latency chain), then one
-// wave scan per owner in registers and one LDS exchange across the 4 waves.
-constexpr int kPoScanPer = 4;  // chunks per thread: nchunks <= 1024 (B * F <= 1M lookups)
-__global__ __launch_bounds__(256) void plan_owner_scan_kernel(int nchunks, int P, const int32_t* __restrict__ ocnt,
-                                                              int32_t* __restrict__ ooff,
-                                                              int64_t* __restrict__ counts) {
-  __shared__ uint32_t wsum[4][kPoMaxP];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int per = (nchunks + 255) / 256;
-  uint32_t c[kPoScanPer][kPoMaxP], sum[kPoMaxP], x[kPoMaxP];
-#pragma unroll
-  for (int i = 0; i < kPoScanPer; ++i)
-#pragma unroll
-    for (int p = 0; p < kPoMaxP; ++p) {
-      const int ch = t * per + i;
-      c[i][p] = (i < per && p < P && ch < nchunks) ? (uint32_t)ocnt[(int64_t)ch * P + p] : 0u;
-    }
-#pragma unroll
-  for (int p = 0; p < kPoMaxP; ++p) {
-    uint32_t s = 0;
-#pragma unroll
-    for (int i = 0; i < kPoScanPer; ++i) s += c[i][p];
-    sum[p] = s;
-    uint32_t v = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(v, o, 64);
-      if (lane >= o) v += y;
-    }
-    x[p] = v;  // inclusive over the wave's lanes
-    if (lane == 63) wsum[wave][p] = v;
-  }
-  __syncthreads();
-  int64_t obase = 0;  // keys of owners < p
-#pragma unroll
-  for (int p = 0; p < kPoMaxP; ++p) {
-    if (p >= P) break;
-    uint32_t wpre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      wpre += w < wave ? wsum[w][p] : 0u;
-      tot += wsum[w][p];
-    }
-    uint32_t run = (uint32_t)obase + wpre + x[p] - sum[p];
-#pragma unroll
-    for (int i = 0; i < kPoScanPer; ++i) {
-      const int ch = t * per + i;
-      if (i < per && ch < nchunks) ooff[(int64_t)ch * P + p] = (int32_t)run;
-      run += c[i][p];
-    }
-    if (t == 0) counts[p] = tot;
-    obase += tot;
-  }
-  if (t == 0) counts[P] = obase;
-}
-
-// place the chunk's unique keys: stable rank among the chunk's keys of the same owner
-__global__ __launch_bounds__(256) void plan_owner_perm_kernel(int B, int F, const int64_t* __restrict__ ukey,
-                                                              const int32_t* __restrict__ ucount,
-                                                              const int64_t* __restrict__ bounds, int P,
-                                                              uint64_t rmult, uint64_t rn,
-                                                              const int32_t* __restrict__ ooff,
-                                                              int32_t* __restrict__ perm, int64_t* __restrict__ uniq) {
-  __shared__ int64_t basef[65];
-  __shared__ int32_t ucf[64];
-  __shared__ int64_t sb[kPoMaxP + 1];
-  __shared__ uint32_t cnt[kPoMaxP][256];  // [owner][thread] -> exclusive offsets inside the chunk
-  __shared__ uint32_t ws[20];
-  const int t = threadIdx.x;
-  if (t <= P) sb[t] = bounds[t];
-  const int64_t U = ps_col_prefix(ucount, F, basef, ucf);
-  const int64_t u0 = (int64_t)blockIdx.x * kPoChunk + 4 * t;  // 4 consecutive unique indices per thread
-  int own[4];
-  int64_t rk[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    own[e] = -1;
-    if (u0 + e < U) {
-      rk[e] = ps_ukey_routed(u0 + e, F, B, basef, ukey, rmult, rn);
-      own[e] = ps_owner(sb, P, rk[e]);
-    }
-  }
-  for (int p = 0; p < P; ++p) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) c += own[e] == p ? 1u : 0u;
-    cnt[p][t] = c;
-  }
-  __syncthreads();
-  // exclusive scan over [owner][thread]: owner by owner (P <= 16 block scans of 256 values)
-  for (int p = 0; p < P; ++p) {
-    const uint32_t v = cnt[p][t];
-    const int lane = t & 63, wave = t >> 6;
-    uint32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) ws[wave] = x;
-    __syncthreads();
-    uint32_t wpre = 0;
-    for (int w = 0; w < wave; ++w) wpre += ws[w];
-    cnt[p][t] = wpre + x - v;
-    __syncthreads();
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (own[e] < 0) continue;
-    uint32_t r = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (q < e && own[q] == own[e]) ++r;
-    const int64_t pos = (int64_t)ooff[(int64_t)blockIdx.x * P + own[e]] + cnt[own[e]][t] + r;
-    perm[u0 + e] = (int32_t)pos;
-    uniq[pos] = rk[e];
-  }
+// global position of column c's local unique index lu (P > 1)
+__device__ __forceinline__ int64_t po_place(const PoLayout* L, int c, int P, int32_t lu) {
+  int p = 0;
+  while (p + 1 < P && L->cstart[c][p + 1] <= lu) ++p;
+  return L->obase[p] + L->colpre[c][p] + (lu - L->cstart[c][p]);
 }
 
 __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int32_t* __restrict__ sorted_b,
                                                         const int32_t* __restrict__ local_u,
                                                         const int64_t* __restrict__ ukey,
                                                         const int32_t* __restrict__ ucount, uint64_t rmult,
-                                                        uint64_t rn, const int32_t* __restrict__ perm,
+                                                        uint64_t rn, int P, const int32_t* __restrict__ ocnt,
                                                         int64_t* __restrict__ uniq, int64_t* __restrict__ inv,
                                                         int32_t* __restrict__ members, int32_t* __restrict__ memrow,
                                                         int64_t* __restrict__ counts, int32_t* __restrict__ pos_out,
@@ -440,32 +372,41 @@ __global__ __launch_bounds__(256) void plan_emit_kernel(int B, int F, const int3
                                                         int32_t* __restrict__ rowidx) {
   __shared__ int64_t basef[65];
   __shared__ int32_t ucf[64];
+  __shared__ PoLayout L;
   const int t = threadIdx.x;
   const int64_t U = ps_col_prefix(ucount, F, basef, ucf);
-  if (!perm && blockIdx.x == 0 && t == 0) {
-    counts[0] = U;  // one owner: counts[0] = U
-    counts[1] = U;  // the device-side U
+  if (P > 1) po_layout(ocnt, F, P, &L);
+  if (blockIdx.x == 0 && t <= P) {
+    if (P == 1) counts[t] = U;  // counts[0] = U, counts[1] = the device-side U
+    else counts[t] = t < P ? L.obase[t + 1] - L.obase[t] : U;
   }
   const int64_t n = (int64_t)B * F;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + t; idx < n; idx += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(idx / B);
     const int pos = (int)(idx - (int64_t)c * B);
-    int64_t u = basef[c] + local_u[idx];
-    if (perm) u = perm[u];  // owner-grouped position
+    const int32_t lu = local_u[idx];
+    const int64_t u = P > 1 ? po_place(&L, c, P, lu) : basef[c] + lu;
     const int64_t j = (int64_t)sorted_b[idx] * F + c;
     inv[j] = u;
     members[idx] = (int32_t)j;
     memrow[idx] = (int32_t)u;
     if (pos_out) pos_out[j] = (int32_t)idx;  // the member-order row of lookup j (sorted dgrad rows)
     if (rowstart) {  // one owner: u's lookups are members [rowstart[u], rowstart[u + 1])
-      if (pos == 0 || local_u[idx - 1] != local_u[idx]) rowstart[u] = (int32_t)idx;
+      if (pos == 0 || local_u[idx - 1] != lu) rowstart[u] = (int32_t)idx;
       if (idx == n - 1) rowstart[U] = (int32_t)n;
     }
-    if (!perm && pos < ucf[c]) uniq[basef[c] + pos] = ps_route(ukey[idx], rmult, rn);
+    if (pos < ucf[c])  // column c's unique key number pos
+      uniq[P > 1 ? po_place(&L, c, P, pos) : basef[c] + pos] = ps_route(ukey[idx], rmult, rn);
     // one owner: lookup j's table row (its routed key), so the input assembly reads the row
     // with one index load instead of the inv -> uniq chain
-    if (rowidx) rowidx[j] = (int32_t)ps_route(ukey[(int64_t)c * B + local_u[idx]], rmult, rn);
+    if (rowidx) rowidx[j] = (int32_t)ps_route(ukey[(int64_t)c * B + lu], rmult, rn);
   }
+}
+
+int plan_owner_bits(int P) {
+  int b = 0;
+  while ((1 << b) < P) ++b;
+  return b;
 }
 
 void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, const int32_t* col_bits,
@@ -480,35 +421,26 @@ void plan_sorted(const int64_t* keys, int B, int F, const int64_t* col_base, con
   if (P < 1 || P > kPoMaxP) throw std::runtime_error("plan_sorted: 1 <= P <= 16 owners");
   if (route_mult && !route_n) throw std::runtime_error("plan_sorted: routing needs the row count");
   const int64_t n = (int64_t)B * F;
-  // ws: sorted_b [n] | local_u [n] | ucount [F] | (16-byte aligned) column-major keys [n] | perm [n] |
-  //     owner counts / offsets [2 * nchunks * P] | (16-byte aligned) chunk-sorted keys ck [n], row
-  //     ids cv [n], merged keys mk [n] (the chunked sort)
+  // ws (plan_sorted_ws_ints): sorted_b [n] | local_u [n] | ucount [F] | (16-byte aligned)
+  // column-major keys [n] | per-column owner counts [F * P]
   int32_t* sorted_b = ws;
   int32_t* local_u = ws + n;
   int32_t* ucount = ws + 2 * n;
   const int64_t kofs = (2 * n + F + 3) & ~int64_t(3);
   uint32_t* krel = reinterpret_cast<uint32_t*>(ws + kofs);  // 16-byte aligned
-  int32_t* perm = ws + kofs + n;
-  const int nchunks = (int)((n + kPoChunk - 1) / kPoChunk);
-  int32_t* ocnt = perm + n;
-  int32_t* ooff = ocnt + (int64_t)nchunks * P;
-  hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, krel);
+  int32_t* ocnt = ws + kofs + n;
+  const int obits = P > 1 ? plan_owner_bits(P) : 0;
+  hipLaunchKernelGGL(plan_transpose_kernel, (B + 63) / 64, 256, 0, s, keys, B, F, col_base, col_bits, bounds, P,
+                     route_mult, route_n, krel);
   // one 1024-thread workgroup per column (round 4's chunked sort over F x 4 workgroups measured
   // slower in the W&D step -- 0.3708 vs 0.3657 ms, profiles/r4/ab_wd_knobs.txt -- and is gone)
-  hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, sorted_b, local_u, ukey,
-                     ucount);
-  if (P > 1) {
-    if (nchunks > 256 * kPoScanPer) throw std::runtime_error("plan_sorted: at most 1M lookups with several owners");
-    hipLaunchKernelGGL(plan_owner_count_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
-                       route_n, ocnt);
-    hipLaunchKernelGGL(plan_owner_scan_kernel, 1, 256, 0, s, nchunks, P, ocnt, ooff, counts);
-    hipLaunchKernelGGL(plan_owner_perm_kernel, nchunks, 256, 0, s, B, F, ukey, ucount, bounds, P, route_mult,
-                       route_n, ooff, perm, uniq);
-  }
+  hipLaunchKernelGGL(plan_sort_col_kernel, F, kPsThreads, 0, s, krel, B, col_base, col_bits, obits, P, sorted_b,
+                     local_u, ukey, ucount, ocnt);
   hipLaunchKernelGGL(plan_emit_kernel, grid_for(n, 256, 2048), 256, 0, s, B, F, sorted_b, local_u, ukey, ucount,
-                       route_mult, route_n, P > 1 ? perm : nullptr, uniq, inv, members, memrow, counts, pos,
-                       rowstart, rowidx);
+                     route_mult, route_n, P, ocnt, uniq, inv, members, memrow, counts, pos, rowstart, rowidx);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
+
+int64_t plan_sorted_ws_ints(int64_t n, int F, int P) { return ((2 * n + F + 3) & ~int64_t(3)) + n + (int64_t)F * P; }
 
 }  // namespace minips_k

@@ -659,6 +659,124 @@ void owner_rows_adagrad(float* table, int64_t ld, float* state, float* state2, i
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// Direct-addressed owner apply (no owner-side dedupe): a persistent table rs[row * P + s] =
+// {stamp, received row} per owned row and requester. owner_mark stamps the received keys of this
+// push (each requester sends a key at most once: one writer per entry, no atomics); owner_apply
+// takes 8 lanes per RECEIVED row, and the group whose requester is the lowest one that sent the
+// row (the leader) sums the row's <= P contributions in requester order and applies the row-wise
+// Adagrad -- the same arithmetic, in the same order, as owner_rows_adagrad over a deduplicated
+// plan, without the bitmap planner, the slot scatter and their host calls. The stamp (the push
+// number) retires the previous pushes' entries without clearing the table.
+__device__ __forceinline__ int owner_seg(int64_t i, const OwnerSegs& segs, int P) {
+  int seg = 0;
+  while (seg + 1 < P && i >= segs.off[seg + 1]) ++seg;
+  return seg;
+}
+
+__global__ void owner_mark_kernel(const int64_t* __restrict__ keys, int64_t M, int64_t base, OwnerSegs segs, int P,
+                                  int2* __restrict__ rs, int stamp) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x)
+    rs[(keys[i] - base) * P + owner_seg(i, segs, P)] = make_int2(stamp, (int)i);
+}
+
+template <typename TG>
+__global__ __launch_bounds__(256) void owner_apply_kernel(float* table, int64_t ld, float* state, float* state2,
+                                                          int D1, const int64_t* __restrict__ keys, int64_t M,
+                                                          int64_t base, int D, const TG* __restrict__ recv,
+                                                          OwnerSegs segs, int P, const int2* __restrict__ rs,
+                                                          int stamp, float lr, float eps) {
+  const int lane = threadIdx.x & 63, sub = lane >> 3, l = lane & 7;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int c0 = 4 * l, c1 = 32 + 4 * l;
+  const bool has0 = c0 < D, has1 = c1 < D;
+  for (int64_t i0 = wave * 8; i0 < M; i0 += nwaves * 8) {
+    const int64_t i = i0 + sub;
+    const int me = i < M ? owner_seg(i, segs, P) : 0;
+    const int64_t row = i < M ? keys[i] - base : 0;
+    const int2* e = rs + row * P;
+    const int2 e0 = i < M && l < P ? e[l] : make_int2(-1, -1);
+    const int2 e1 = i < M && l + 8 < P ? e[l + 8] : make_int2(-1, -1);
+    const int sl0 = e0.x == stamp ? e0.y : -1, sl1 = e1.x == stamp ? e1.y : -1;
+    // the leader: no lower requester sent this row in this push
+    const unsigned long long lower = __ballot(sl0 >= 0 && l < me) | __ballot(sl1 >= 0 && l + 8 < me);
+    const bool ok = i < M && ((lower >> (sub << 3)) & 0xffull) == 0;
+    float* tr = table + row * ld;
+    float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0, g0 = t0, g1 = t0;
+    if (ok && has0) {
+      t0 = *reinterpret_cast<const float4*>(tr + c0);
+      if (has1) t1 = *reinterpret_cast<const float4*>(tr + c1);
+    }
+    const float st_old1 = ok ? state[row] : 0.f;
+    const float st_old2 = ok && D1 < D ? state2[row] : 0.f;
+#pragma unroll
+    for (int s = 0; s < kOwnerMaxP; ++s) {
+      if (s >= P) break;
+      const int m = __shfl(s < 8 ? sl0 : sl1, (sub << 3) + (s & 7), 64);
+      if (ok && m >= 0 && has0) {
+        const float4 v = ld_row4(recv + (int64_t)m * D + c0);
+        g0.x += v.x; g0.y += v.y; g0.z += v.z; g0.w += v.w;
+        if (has1) {
+          const float4 w = ld_row4(recv + (int64_t)m * D + c1);
+          g1.x += w.x; g1.y += w.y; g1.z += w.z; g1.w += w.w;
+        }
+      }
+    }
+    float sq1 = 0.f, sq2 = 0.f;
+    const float a[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (q < 4 ? c0 : c1) + (q & 3);
+      const float sq = a[q] * a[q];
+      if (c < D1) sq1 += sq;
+      else sq2 += sq;
+    }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+      sq1 += __shfl_xor(sq1, o, 64);
+      sq2 += __shfl_xor(sq2, o, 64);
+    }
+    if (!ok) continue;
+    const float st1 = st_old1 + sq1 / (float)D1;
+    const float st2 = D1 < D ? st_old2 + sq2 / (float)(D - D1) : 0.f;
+    if (l == 0) {
+      state[row] = st1;
+      if (D1 < D) state2[row] = st2;
+    }
+    const float s1 = lr / (sqrtf(st1) + eps), s2 = lr / (sqrtf(st2) + eps);
+    float o[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (q < 4 ? c0 : c1) + (q & 3);
+      o[q] -= (c < D1 ? s1 : s2) * a[q];
+    }
+    if (has0) *reinterpret_cast<float4*>(tr + c0) = make_float4(o[0], o[1], o[2], o[3]);
+    if (has1) *reinterpret_cast<float4*>(tr + c1) = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
+void owner_push_adagrad(float* table, int64_t ld, float* state, float* state2, int D1, const int64_t* keys, int64_t M,
+                        int64_t base, int64_t rows_local, int D, const void* recv, bool recv_bf16,
+                        const OwnerSegs& segs, int P, void* rs, int stamp, float lr, float eps, hipStream_t s) {
+  if (M <= 0) return;
+  if (D1 <= 0 || D1 > D) D1 = D;
+  if (D1 < D && !state2) throw std::runtime_error("owner_push_adagrad: split rows need state2");
+  if (!(D > 16 && D <= 64 && D % 4 == 0 && ld % 4 == 0 && P >= 1 && P <= kOwnerMaxP && stamp >= 0))
+    throw std::runtime_error("owner_push_adagrad: rows of 16 < D <= 64 (D % 4 == 0), 1..16 requesters");
+  (void)rows_local;
+  int2* e = static_cast<int2*>(rs);
+  hipLaunchKernelGGL(owner_mark_kernel, grid_for(M, 256, 4096), 256, 0, s, keys, M, base, segs, P, e, stamp);
+  MINIPS_HIP_CHECK(hipGetLastError());
+  const int block = 256;
+  if (recv_bf16)
+    hipLaunchKernelGGL(owner_apply_kernel<bf16_t>, grid_for(M * 8, block, 16384), block, 0, s, table, ld, state,
+                       state2, D1, keys, M, base, D, static_cast<const bf16_t*>(recv), segs, P, e, stamp, lr, eps);
+  else
+    hipLaunchKernelGGL(owner_apply_kernel<float>, grid_for(M * 8, block, 16384), block, 0, s, table, ld, state,
+                       state2, D1, keys, M, base, D, static_cast<const float*>(recv), segs, P, e, stamp, lr, eps);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 __global__ void sparse_sgd_kernel(float* table, int64_t ld, const int64_t* __restrict__ keys, int64_t n, int64_t base,
                                   int D, const float* __restrict__ grads, float scale, const int64_t* n_dev) {
   const int64_t total = dev_count(n, n_dev) * D;

@@ -16,6 +16,7 @@ import os
 import torch
 
 from ..utils import streams
+from ..utils.metrics import traced
 
 
 def default_depth(world: int) -> int:
@@ -49,12 +50,13 @@ class LookaheadFeeder:
         if self.cuda:
             from ..utils.streams import EventRing
 
-            self._evring = EventRing(2 * self.depth + 4, fast=streams.FAST_PLAN)
-            self._fence_ring = EventRing(4, fast=streams.FAST_PLAN)
+            self._evring = EventRing(2 * self.depth + 4, fast=streams.fast_for("plan"))
+            self._fence_ring = EventRing(4, fast=streams.fast_for("plan"))
         self.queue = collections.deque(self._produce() for _ in range(self.depth))
         for (_, k, _), _ev in list(self.queue)[1:]:
             model.prefetch(k, keys_on_plan_stream=self.cuda)
 
+    @traced("feeder.produce")
     def _produce(self):
         if not self.cuda:
             return self.data.next(), None
@@ -67,6 +69,7 @@ class LookaheadFeeder:
                 t.record_stream(self.main)
         return b, ev
 
+    @traced("feeder.step")
     def step(self):
         (dense, keys, labels), ev = self.queue.popleft()
         # the batch was generated on the planning stream before its key plan: a step whose plan

@@ -118,9 +118,6 @@ def compute_priority() -> int:
     return 0
 
 
-_FAST_EVENTS = True
-
-
 class _Fork:
     """SideStream.fork()'s context: the side stream waits for the current stream, then the block
     runs on the side stream (GEMM splits in overlap mode)."""
@@ -172,8 +169,8 @@ class SideStream:
             if enabled and torch.device(device).type == "cuda" else None
         # fork / join events are re-recorded every step (a wait binds to the record issued before
         # it): no event objects created and destroyed per fork. Same-device ordering only, so
-        # fence-free native events (ops_py FastEvent, FAST_EVENTS off: torch events)
-        self._fast = self.stream is not None and _FAST_EVENTS
+        # fence-free native events (ops_py FastEvent; MINIPS_STREAM_DEBUG sysfence=side: torch events)
+        self._fast = self.stream is not None and streams.fast_for("side")
         if self._fast:
             from .._native import kernels
 

@@ -24,7 +24,7 @@ import torch
 from .. import ops
 from ..ps.comm import Comm
 from ..utils import streams
-from ..utils.metrics import traced
+from ..utils.metrics import phase, traced
 from .layers import SideStream
 from .feeder import LookaheadPlans
 
@@ -268,10 +268,13 @@ class WideDeep(LookaheadPlans):
                 nk = next_keys() if callable(next_keys) else next_keys
                 self.prefetch(nk, keys_on_plan_stream=next_on_plan_stream)
 
-        issue_next("start")
+        with phase("wd.plan_next"):
+            issue_next("start")
         pend_side = self.__dict__.pop("_side_pending", None)
         if pend_side is not None:  # the previous step's weight gradients read X: done before it is rewritten
             streams.current(self.comm.device).wait_event(pend_side[0])
+        ph = phase("wd.get_assemble")
+        ph.__enter__()
         src = self.emb.get_source(keys, plan=plan)  # one rank: the rows are read in place
         if src is not None:
             plan, table, index, base = src
@@ -284,6 +287,9 @@ class WideDeep(LookaheadPlans):
             ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
         if pend_side is not None:  # ... and its dense Adam ran (side stream) before the forward reads W
             streams.current(self.comm.device).wait_event(pend_side[1])
+        ph.__exit__(None, None, None)
+        ph = phase("wd.fwd_head")
+        ph.__enter__()
         G = self.dense.grad
         P = self.dense.get()
         scale = 1.0 / (B * self.comm.world)
@@ -292,6 +298,9 @@ class WideDeep(LookaheadPlans):
         # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
                     b["dwide"], b["loss"], self.view(G, "b3"), scale)
+        ph.__exit__(None, None, None)
+        ph = phase("wd.bwd_dense")
+        ph.__enter__()
         issue_next("head")
         side = self._side
         # weight gradients fork onto a second stream as soon as their inputs exist, beside the
@@ -336,9 +345,15 @@ class WideDeep(LookaheadPlans):
                 self.dense.add()
                 self.dense.clock()
         issue_next("dgrad")
+        ph.__exit__(None, None, None)
+        ph = phase("wd.emb_push")
+        ph.__enter__()
         dXe = b["dX"].view(B * F, D) if sorted_rows else b["dX"]
         self.emb.add_lookup_grads(plan, dXe, b["dwide"], F, D, sorted_rows=sorted_rows)  # the table reduces
         self.emb.clock()
+        ph.__exit__(None, None, None)
+        ph = phase("wd.dense_clock")
+        ph.__enter__()
         capturing = side.stream is not None and torch.cuda.is_current_stream_capturing()
         dense_side = (_DENSE_ON_SIDE and not dense_early and side.stream is not None and self.comm.world == 1
                       and pipe is not None and not pipe.async_ and not capturing)
@@ -365,7 +380,9 @@ class WideDeep(LookaheadPlans):
             if not dense_early:
                 self.dense.add()
                 self.dense.clock()
-        self._advance_next_plan()
+        ph.__exit__(None, None, None)
+        with phase("wd.advance_plans"):
+            self._advance_next_plan()
         return b["loss"]
 
     def _bucket_done(self, layer: int, side):

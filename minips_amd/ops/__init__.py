@@ -260,9 +260,10 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
     [col_base[f], col_base[f] + 2**col_bits[f])): per-column radix sort, no global atomics
     (plan.hip). ``col_bits``: a list of ints (or one int for every column); ``bounds`` [P+1]: the
     owners' routed-key ranges (None: one owner). Returns (uniq [n] (first U valid, routed; column-
-    major, ascending inside a column, then stably grouped by owner), inv [n], counts [P], U_dev [1],
-    members [n] int32, memrow [n] int32) -- the unique_bucketize_n outputs plus the lookup CSR of
-    emb_build_csr (rows contiguous, in column-major key order)."""
+    major, inside a column by (owner, key) -- ascending keys for one owner -- then stably grouped by
+    owner), inv [n], counts [P], U_dev [1], members [n] int32, memrow [n] int32) -- the
+    unique_bucketize_n outputs plus the lookup CSR of emb_build_csr (rows contiguous, in that
+    column-major order)."""
     if bounds is None:
         bounds = torch.tensor([0, (1 << 62)], dtype=torch.int64, device=keys.device)
     if _gpu(keys):
@@ -272,10 +273,17 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
         return tuple(kernels().plan_sorted(keys.contiguous(), col_base.contiguous(), bits_dev, bits,
                                            int(route_mult), int(route_n), bounds.contiguous(), bool(positions)))
     B, F = keys.shape
+    P = bounds.numel() - 1
     uniq_l, inv_l = [], []
     base = 0
     for f in range(F):
         u, i = torch.unique(keys[:, f], sorted=True, return_inverse=True)
+        if P > 1:  # inside a column the keys sort by (owner shard of the routed key, key)
+            r = (u * route_mult) % route_n if route_mult else u
+            o = torch.sort(torch.bucketize(r, bounds[1:-1], right=True), stable=True).indices
+            rank = torch.empty_like(o)
+            rank[o] = torch.arange(o.numel())
+            u, i = u[o], rank[i]
         uniq_l.append(u)
         inv_l.append(i + base)
         base += u.numel()
@@ -283,7 +291,6 @@ def plan_sorted(keys, col_base, col_bits, route_mult=0, route_n=0, bits_dev=None
     uniq = torch.cat(uniq_l)
     if route_mult:
         uniq = (uniq * route_mult) % route_n
-    P = bounds.numel() - 1
     owner = torch.bucketize(uniq, bounds[1:-1], right=True)
     perm_order = torch.sort(owner, stable=True).indices      # regrouped position -> u
     perm = torch.empty(U, dtype=torch.int64)
@@ -416,6 +423,29 @@ def owner_slots(own_inv, splits, cap):
     seg = torch.repeat_interleave(torch.arange(P), torch.tensor([int(c) for c in splits], dtype=torch.int64))
     slots[own_inv * P + seg] = torch.arange(own_inv.numel(), dtype=torch.int32)
     return slots
+
+
+def owner_push_adagrad(table, state, keys, base, recv, splits, rs, stamp, lr, eps=1e-8, state2=None, split=None):
+    """Owner apply of one push without an owner-side dedupe: received key i (requester segments
+    ``splits``, each requester's keys distinct) carries gradient row recv[i]; every touched row gets
+    the row-wise Adagrad of the sum of its received rows in requester order -- owner_rows_adagrad's
+    arithmetic. ``rs``: a persistent int32 [rows * P * 2] {stamp, row} table (GPU), ``stamp`` this
+    push's number (increasing, >= 0)."""
+    D = recv.shape[1]
+    D1 = D if split is None else split
+    if _gpu(table):
+        kernels().owner_push_adagrad(table, state, state2, int(D1), keys, int(base), recv.contiguous(),
+                                     [int(c) for c in splits], rs, int(stamp), float(lr), float(eps))
+        return
+    M = keys.numel()
+    if M == 0:
+        return
+    uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
+    P = len(splits)
+    seg = torch.repeat_interleave(torch.arange(P), torch.tensor([int(c) for c in splits], dtype=torch.int64))
+    slots = torch.full((uniq.numel() * P,), -1, dtype=torch.int32)
+    slots[inv * P + seg] = torch.arange(M, dtype=torch.int32)
+    owner_rows_adagrad(table, state, uniq, uniq.numel(), base, recv, slots, P, lr, eps, state2=state2, split=split)
 
 
 def owner_rows_adagrad(table, state, keys, n, base, recv, slots, P, lr, eps=1e-8, state2=None, split=None, n_dev=None):

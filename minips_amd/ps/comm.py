@@ -39,7 +39,7 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
-from ..utils.metrics import _ROCTX_ON, range as _mrange
+from ..utils.metrics import _HOST_ON, _ROCTX_ON, range as _mrange
 
 
 # handles of dedicated streams whose owner is gone, by (device index, priority): reused, never
@@ -156,7 +156,7 @@ class Comm:
         """Around one collective when ``timing`` is on: its bytes and its time on the issuing
         stream (an RCCL call leaves the current stream waiting for it, so the end event fires
         when the collective completed)."""
-        if _ROCTX_ON:
+        if _ROCTX_ON or _HOST_ON:
             with _mrange("comm." + kind):
                 yield from self._timed_inner(kind, nbytes)
             return

@@ -66,11 +66,6 @@ _SHARD_MEM = 0
 # copy of the slot from `depth` clocks ago); PS_INBOX_MEM off is an A/B timing knob only
 _INBOX_MEM = 2
 _PUSH_STREAM = os.environ.get("MINIPS_PS_PUSH_STREAM", "0") == "1"
-if _PUSH_STREAM:
-    # the push stream passes the 4-rank SSP GPU test only with system-fence planning-stream hand-off
-    # events (profiles/r4/ab_push_stream.txt): never run the known-failing combination.
-    # The feeder and the plan rings read this flag when they are built, after this import.
-    streams.FAST_PLAN = False
 # PS_LOCKS off: no owner locks (A/B timing only: reads may see half of a batch)
 _LOCKS = True
 
@@ -521,7 +516,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
                 # (with the push stream the plan's keys / counts are read there, after a hand-off
                 # through the compute stream: those need the system-fence form, measured --
                 # profiles/r4/ab_push_stream.txt)
-                ring = self._plan_evs = streams.EventRing(16, fast=streams.FAST_PLAN and not _PUSH_STREAM)
+                ring = self._plan_evs = streams.EventRing(16, fast=streams.fast_for("plan"))
             pp.event = ring.next()
             pp.event.record(ps)
         if not fenced:
@@ -616,7 +611,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             # system-fence events: with fence-free ones the push read stale gradient rows (the 4-rank
             # SSP GPU test's loss spike; profiles/r4/ab_push_stream.txt) -- the compute stream's
             # writes must be written back before the push's IPC-path loads
-            self._push_evs = streams.EventRing(8, fast=False)
+            self._push_evs = streams.EventRing(8, fast=streams.fast_for("push"))
         return st
 
     def _merge(self, pending):

@@ -71,14 +71,28 @@ class _Pipeline:
         self.staleness = staleness if consistency == "ssp" else (0 if consistency == "bsp" else asp_depth)
         overlap = _overlap_default() if overlap is None else overlap
         if consistency == "bsp":
-            # one rank has no communication to hide; OVERLAP_W1 lists the table kinds that
-            # still run their clock on a side stream there (the apply overlapping other compute)
-            self.async_ = comm.device.type == "cuda" and overlap and (comm.world > 1 or w1)
+            # one rank has no communication to hide; ``w1`` (or a communicator that forces every
+            # collective through its group at world 1, as an N-rank job would) still runs the
+            # clock on a side stream there (the apply overlapping other compute)
+            self.async_ = comm.device.type == "cuda" and overlap and (comm.world > 1 or w1
+                                                                       or getattr(comm, "force", False))
         else:
             self.async_ = comm.device.type == "cuda" and self.staleness > 0
         self.stream = comm.new_stream() if self.async_ else None
-        self.events: dict[int, torch.cuda.Event] = {}
+        self.events: dict = {}
         self.clock = 0
+        # fence-free ordering events from rings (no event object per clock, no system-scope
+        # release: every consumer is on this device)
+        if self.async_:
+            self._evs = streams.EventRing(self.staleness + 8, fast=streams.fast_for("pipe"))
+            self._forks = streams.EventRing(4, fast=streams.fast_for("pipe"))
+        # ``retain`` (set by tables driven by a fencing LookaheadFeeder): the tensors a clock reads
+        # on the side stream are kept referenced until the compute stream has waited for that
+        # clock, plus one step (the feeder's fence then also orders the planning stream after
+        # it), instead of record_stream -- which costs an allocator event per tensor per clock
+        self.retain = False
+        self._held: dict = {}
+        self._grace: list = []
 
     def run(self, fn):
         """Run ``fn`` (the clock's communication+apply) for the current clock."""
@@ -86,10 +100,12 @@ class _Pipeline:
             fn()
         else:
             cur = streams.current(self.stream.device)
-            self.stream.wait_stream(cur)  # inputs produced on the compute stream
+            fork = self._forks.next()
+            fork.record(cur)
+            self.stream.wait_event(fork)  # inputs produced on the compute stream
             with streams.use(self.stream):
                 fn()
-                ev = torch.cuda.Event()
+                ev = self._evs.next()
                 ev.record(self.stream)
             self.events[self.clock] = ev
         self.clock += 1
@@ -104,11 +120,15 @@ class _Pipeline:
             cur.wait_event(self.events[max(done)])  # the side stream is in-order
             for k in done:
                 del self.events[k]
+        if self._held or self._grace:
+            self._grace = [v for k, v in self._held.items() if k <= c]  # (the previous grace list dies)
+            for k in [k for k in self._held if k <= c]:
+                del self._held[k]
 
     def wait_for_read(self):
         """Before a Get at clock c: updates of clocks <= c - s - 1 must be applied."""
         self.wait_clock(self.clock - self.staleness - 1)
-        if self.async_ and self.events:
+        if self.async_ and self.events and self.consistency != "bsp":
             # observed staleness of this read: earlier clocks whose update is still in flight
             # (non-blocking event queries; the metrics JSONL reports the histogram per step)
             from ..utils.metrics import get_logger
@@ -118,8 +138,12 @@ class _Pipeline:
             log.observe_staleness(sum(1 for ev in self.events.values() if not ev.query()))
 
     def keep_alive(self, *tensors):
-        """Tensors produced on the compute stream and consumed on the side stream."""
+        """Tensors produced on the compute stream and consumed on the side stream (by the clock
+        about to run)."""
         if self.async_:
+            if self.retain:
+                self._held.setdefault(self.clock, []).extend(tensors)
+                return
             for t in tensors:
                 if isinstance(t, torch.Tensor) and t.is_cuda:
                     t.record_stream(self.stream)
@@ -129,10 +153,14 @@ class _Pipeline:
             cur = streams.current(self.stream.device)
             cur.wait_stream(self.stream)
             self.events.clear()
+            self._grace = [v for v in self._held.values()]
+            self._held.clear()
 
     def reset(self):
         """In-place rollback: forget in-flight clocks (issued on the broken communicator)."""
         self.events.clear()
+        self._held.clear()
+        self._grace = []
 
 
 def merge_buckets(starts, n_params: int, min_elems: float) -> list:
@@ -296,6 +324,8 @@ class DenseTable:
             off += (hi - lo) // W
         assert off == self.shard
         self._issued: set = set()
+        self._bstat = [(f"t{self.table_id}b{k}", (hi - lo) * (self.grad.element_size() + self.params.element_size()))
+                       for k, (lo, hi) in enumerate(self.buckets)]
 
     def bucket_of(self, offset: int) -> int:
         """Index of the bucket holding element ``offset``."""
@@ -332,6 +362,7 @@ class DenseTable:
         """Before a HIP-graph capture: the device step twin = the host step."""
         self.step_dev.fill_(int(self.step))
 
+    @traced("dense.bucket_work")
     def _bucket_work(self, k: int, grad: torch.Tensor, step: int):
         lo, hi = self.buckets[k]
         off, sz, g0 = self._own_piece(k)
@@ -368,9 +399,11 @@ class DenseTable:
         comm.all_gather(self.params[lo:hi], self.params[g0: g0 + sz])
         if not zeroed:
             grad[lo:hi].zero_()
-        comm.stats.bucket_bytes[f"t{self.table_id}b{k}"] = comm.stats.bucket_bytes.get(f"t{self.table_id}b{k}", 0) + \
-            (hi - lo) * grad.element_size() + (hi - lo) * self.params.element_size()
+        key, nb = self._bstat[k]
+        bb = comm.stats.bucket_bytes
+        bb[key] = bb.get(key, 0) + nb
 
+    @traced("dense.bucket_ready")
     def bucket_ready(self, k: int, events=()):
         """The gradients of bucket ``k`` are complete (every writer is on the current stream or
         behind ``events``): issue its reduce-scatter + apply + all-gather now (on the clock
@@ -381,11 +414,13 @@ class DenseTable:
         grad, step = self.grad, self.step + 1
         if self.pipe.async_:
             st = self.pipe.stream
-            st.wait_stream(streams.current(st.device))
+            fork = self.pipe._forks.next()
+            fork.record(streams.current(st.device))
+            st.wait_event(fork)
             for ev in events:
                 if ev is not None:
                     st.wait_event(ev)
-            self.pipe.keep_alive(grad)
+            # (the gradient ring's buffers are persistent: nothing to keep alive)
             with streams.use(st):
                 self._bucket_work(k, grad, step)
         else:
@@ -807,6 +842,7 @@ class SparseTable:
             return None
         return plan.own_uniq[: plan.extra.get("own_U", len(plan.recv_keys))]
 
+    @traced("sparse.start_plan")
     def _start_plan(self, keys: torch.Tensor, csr: bool = False, exchange: bool = True) -> _PendingPlan:
         """Dedupe + owner bucketing (+ the all-to-all of the per-owner counts unless
         ``exchange`` is False: _exchange_counts does it later), issued on the current stream;
@@ -823,7 +859,8 @@ class SparseTable:
         zeroed = None
         cols = getattr(self, "columns", None)  # (HashSparseTable has no column ranges)
         if (cols is not None and _SORT_PLAN and flat.is_cuda and self.comm.world <= 16 and keys.dim() == 2
-                and keys.shape[0] <= 16384 and keys.shape[1] == cols[0].numel()):
+                and keys.shape[0] <= 16384 and keys.shape[1] == cols[0].numel()
+                and max(cols[1]) + (self.comm.world - 1).bit_length() <= 32):  # (owner bits ride in the sort key)
             # disjoint column key ranges: atomic-free per-column sort (ops.plan_sorted), unique keys
             # regrouped by owner, and the embedding backward's lookup CSR on the way
             pp.flat = flat
@@ -868,23 +905,38 @@ class SparseTable:
             self._exchange_counts(pp)
         return pp
 
+    @traced("sparse.exchange_counts")
     def _exchange_counts(self, pp: _PendingPlan):
         """All-to-all of the plan's per-owner counts on the current stream; the counts land in
         pinned host memory behind ``pp.cev`` (the host reads them to size the key exchange)."""
         if pp.exchanged:
             return
         pp.exchanged = True
-        recv = torch.empty_like(pp.counts)
-        self.comm.all_to_all_counts(recv, pp.counts)
-        both = torch.stack([pp.counts, recv])
-        if both.is_cuda:
-            pp.host = torch.empty(both.shape, dtype=both.dtype, pin_memory=True)
-            pp.host.copy_(both, non_blocking=True)
-            pp.cev = torch.cuda.Event()
-            pp.cev.record()
-        else:
-            pp.host = both
+        if not pp.counts.is_cuda:
+            recv = torch.empty_like(pp.counts)
+            self.comm.all_to_all_counts(recv, pp.counts)
+            pp.host = torch.stack([pp.counts, recv])
+            return
+        # [send counts | received counts] in one device buffer -> one copy into a pinned slot of a
+        # ring (no pinned allocation, no event object per plan); the event carries the system-scope
+        # release the host read needs
+        ring = self.__dict__.get("_count_ring")
+        P = pp.counts.numel()
+        if ring is None or ring[0][0][0].shape[1] != P:
+            n = 8  # > look-ahead depth + 2 plans in flight
+            ring = self._count_ring = ([(torch.empty(2, P, dtype=torch.int64, device=pp.counts.device),
+                                         torch.empty(2, P, dtype=torch.int64, pin_memory=True),
+                                         torch.cuda.Event()) for _ in range(n)], [0])
+        slots, i = ring
+        both, host, ev = slots[i[0]]
+        i[0] = (i[0] + 1) % len(slots)
+        both[0].copy_(pp.counts)
+        self.comm.all_to_all_counts(both[1], pp.counts)
+        host.copy_(both, non_blocking=True)
+        ev.record()
+        pp.host, pp.cev = host, ev
 
+    @traced("sparse.plan_async")
     def plan_async(self, keys: torch.Tensor, csr: bool = False, keys_on_plan_stream: bool = False,
                    fenced: bool = False):
         """Lookahead: start planning ``keys`` (a LATER batch) on the planning stream, so its
@@ -913,10 +965,13 @@ class SparseTable:
             pp = self._start_plan(keys, csr, exchange=False)
             ring = self.__dict__.get("_plan_evs")
             if ring is None:  # (plans are consumed within a few steps of their issue)
-                ring = self._plan_evs = streams.EventRing(16, fast=streams.FAST_PLAN)
+                ring = self._plan_evs = streams.EventRing(16, fast=streams.fast_for("plan"))
             pp.event = ring.next()
             pp.event.record(ps)
-        if fenced and self.comm.world == 1 and not self.pipe.async_:
+        if fenced:
+            # the feeder fences the planning stream after every step and the clocks retain what
+            # their side streams read (_Pipeline.retain): no per-tensor stream bookkeeping
+            self.pipe.retain = True
             return pp
         keys.record_stream(ps)
         for t in (pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev, *(pp.csr or ())):
@@ -924,6 +979,7 @@ class SparseTable:
                 t.record_stream(cur)
         return pp
 
+    @traced("sparse.finish_plan")
     def _finish_plan(self, pp: _PendingPlan) -> SparsePlan:
         dev = self.comm.device
         comm = self.comm
@@ -951,7 +1007,9 @@ class SparseTable:
             # them into its own row range, as the peers' requests to this owner would be
             recv_keys.remainder_(self.rows_local).add_(self.base)
         p = SparsePlan(n, pp.inv, pp.uniq, U, send, recv, recv_keys, csr=pp.csr, _U=U)
-        if M > 0:
+        if M > 0 and self._owner_direct_ok():
+            p.extra["direct"] = True  # the push applies by direct addressing: no owner-side plan
+        elif M > 0:
             # owner-side dedupe of the keys requested by all ranks (the push sums their rows): they
             # lie in this rank's own row range, a bounded space -> the bitmap planner when its map
             # is small per key (W&D at 8 ranks: 4.2M local rows for ~10^5-10^6 requested keys)
@@ -972,6 +1030,15 @@ class SparseTable:
                 # at most once): the clock's apply sums them in requester order in one kernel
                 p.own_slots = ops.owner_slots(oi, recv, M)
         return p
+
+    # the direct-addressed owner apply keeps an int2 {stamp, row} per (owned row, requester)
+    _direct_max_bytes = 2 << 30
+
+    def _owner_direct_ok(self) -> bool:
+        """The fused owner apply (below) by direct addressing (ops.owner_push_adagrad): no bitmap
+        dedupe, no slot scatter at planning time, when the rows x requesters table fits the budget
+        (W&D at 8 ranks: 4.2M rows x 8 x 8 B = 270 MB; a 10^9-row shard keeps the planned path)."""
+        return self._owner_fused_ok() and self.rows_local * self.comm.world * 8 <= self._direct_max_bytes
 
     def _owner_fused_ok(self) -> bool:
         """Several ranks, row-wise Adagrad on an fp32 range shard: the owner applies its pushes
@@ -1002,6 +1069,7 @@ class SparseTable:
                 raise ValueError(f"table {self.table_id}: {n} keys outside [0, {self.num_rows}) were planned "
                                  f"(their Gets read and their Adds wrote row 0)")
 
+    @traced("sparse.advance_plan")
     def advance_plan(self, pending, finish: bool = True):
         """Later halves of lookahead planning, called once the current step is issued (so these
         collectives follow the step's own row exchanges and clocks in the rank's single ordered
@@ -1023,11 +1091,15 @@ class SparseTable:
             return pending
         with streams.use(ps):
             plan = self._finish_plan(pending)
-            ev = torch.cuda.Event()
+            ring = self.__dict__.get("_ready_evs")
+            if ring is None:
+                ring = self._ready_evs = streams.EventRing(16, fast=streams.fast_for("plan"))
+            ev = ring.next()
             ev.record(ps)
-        for t in (plan.recv_keys, plan.own_uniq, plan.own_inv, plan.own_U_dev):
-            if t is not None:
-                t.record_stream(cur)
+        if not self.pipe.retain:  # (retain: the plan's tensors live until its clock was waited for)
+            for t in (plan.recv_keys, plan.own_uniq, plan.own_inv, plan.own_U_dev, plan.own_slots):
+                if t is not None:
+                    t.record_stream(cur)
         plan.extra["ready"] = ev
         return plan
 
@@ -1053,6 +1125,7 @@ class SparseTable:
         self.comm.all_to_all_v(rows, served, plan.send, plan.recv, p2p=self.p2p)
         return rows, plan
 
+    @traced("sparse.get_source")
     def get_source(self, keys: torch.Tensor, plan=None):
         """The Get without its row gather, for a consumer that reads the rows in place (one rank,
         fp32 range shard, bf16 pull): returns (plan, table, index, base) -- the row of unique u
@@ -1135,6 +1208,15 @@ class SparseTable:
                 send = send.to(self.push_dtype)
             self.comm.all_to_all_v(recv, send, plan.recv, plan.send, p2p=self.p2p)
             if M == 0:
+                return
+            if plan.extra.get("direct"):  # stamp + sum + row-wise Adagrad, no owner-side plan
+                rs = self.__dict__.get("_rs")
+                if rs is None and dev.type == "cuda":
+                    rs = self._rs = torch.full((self.rows_local * self.comm.world * 2,), -1, dtype=torch.int32,
+                                               device=dev)
+                self._stamp = self.__dict__.get("_stamp", -1) + 1
+                ops.owner_push_adagrad(self.shard, self.state, plan.recv_keys, self.base, recv, plan.recv, rs,
+                                       self._stamp, self.lr, self.eps, state2=self.state2, split=self.split)
                 return
             if plan.own_slots is not None:  # segment sums + row-wise Adagrad in one pass
                 ops.owner_rows_adagrad(self.shard, self.state, plan.own_uniq, M, self.base, recv, plan.own_slots,

@@ -9,6 +9,9 @@ traced(name)    apply batches: csrc/runtime/trace.h), so the phases show up in
                 ``rocprofv3 --marker-trace`` timelines. Off unless MINIPS_ROCTX=1 (then
                 librocprofiler-sdk-roctx is loaded): a disabled ``traced`` leaves the method
                 untouched and a disabled ``range`` returns a shared null context.
+                MINIPS_ROCTX=host instead accumulates each range's inclusive HOST time
+                (perf_counter_ns) in HOST_TIMES -- the per-phase issue cost of a step
+                (bench.py --host-phases prints it per step).
 fault_tolerance_phase(n, detail)
                 the reference's "[Fault Tolerance][PhaseN][ts] ..." line (base/utils.hpp:24-53).
 """
@@ -26,7 +29,27 @@ import time
 _ROCTX = None
 _ROCTX_TRIED = False
 _ROCTX_ON = os.environ.get("MINIPS_ROCTX", "0") == "1"
+_HOST_ON = os.environ.get("MINIPS_ROCTX", "0") == "host"
 _NULL = contextlib.nullcontext()
+# MINIPS_ROCTX=host: name -> [inclusive ns, calls]
+HOST_TIMES: dict = collections.defaultdict(lambda: [0, 0])
+
+
+class _HostRange:
+    __slots__ = ("name", "t0")
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        self.t0 = time.perf_counter_ns()
+        return self
+
+    def __exit__(self, *exc):
+        e = HOST_TIMES[self.name]
+        e[0] += time.perf_counter_ns() - self.t0
+        e[1] += 1
+        return False
 
 
 def _roctx():
@@ -63,8 +86,19 @@ class _Range:
         return False
 
 
+def phase(name: str):
+    """A host-time phase (MINIPS_ROCTX=host), else the shared null context (one global check)."""
+    return _HostRange(name) if _HOST_ON else _NULL
+
+
+def host_times_reset():
+    HOST_TIMES.clear()
+
+
 def range(name: str):  # noqa: A001 - mirrors the roctx naming
     """roctx range context (a shared no-op context when roctx is off)."""
+    if _HOST_ON:
+        return _HostRange(name)
     lib = _roctx() if _ROCTX_ON else None
     return _NULL if lib is None else _Range(lib, name)
 
@@ -74,9 +108,17 @@ def traced(name: str):
     otherwise the method is returned unchanged (zero cost on the step's host path)."""
 
     def deco(fn):
+        import functools
+
+        if _HOST_ON:
+            @functools.wraps(fn)
+            def timed(*args, **kwargs):
+                with _HostRange(name):
+                    return fn(*args, **kwargs)
+
+            return timed
         if not _ROCTX_ON:
             return fn
-        import functools
 
         @functools.wraps(fn)
         def wrapped(*args, **kwargs):

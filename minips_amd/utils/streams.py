@@ -13,19 +13,37 @@ import os
 
 import torch
 
-# FAST_EVENTS off: the step's ordering events are plain torch events (A/B);
-# FAST_PLAN_EVENTS off: only the planning stream's hand-off events (diagnostics)
-FAST = True
-FAST_PLAN = True
+# MINIPS_STREAM_DEBUG (race diagnostics; tests/test_multirank_gpu.py, tools/gpu_round.sh race): comma-separated
+#   delay=<us>         every work segment issued on another stream through use() or SideStream.fork()
+#                      starts with an n-us device spin, so a consumer that misses its wait on a producer
+#                      stream reads stale data deterministically instead of by timing luck -- and a
+#                      missing edge no longer hides behind the latency of a system-fence event
+#   where=use+fork     which segments get the spin: "use" (streams.use: planning, clock pipelines, the
+#                      one-sided push stream), "fork" (SideStream.fork: the weight-gradient stream)
+#   sysfence=<groups>  the ordering events of these groups ('+'-separated) carry a system-scope fence
+#                      instead of none: side (SideStream fork / join / marks), pipe (table clock
+#                      pipelines), plan (planning-stream hand-offs: feeder, plans), push (the one-sided
+#                      push stream's hand-off), all
+def _parse_debug(spec: str) -> dict:
+    out = {}
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        k, _, v = item.partition("=")
+        out[k] = v
+    return out
 
-# MINIPS_STREAM_DELAY_US=n (race diagnostics, tests/test_multirank_gpu.py): every work segment
-# issued on another stream through use() or SideStream.fork() starts with an n-us device spin, so a
-# consumer that misses its wait on a producer stream reads stale data deterministically instead of
-# by timing luck -- and a missing edge no longer hides behind the latency of a system-fence event
-DELAY_US = int(os.environ.get("MINIPS_STREAM_DELAY_US", "0"))
-# where: "use" (streams.use segments: planning, clock pipelines, the one-sided push stream),
-# "fork" (SideStream.fork: the weight-gradient side stream) or both (default) -- to bisect a race
-DELAY_WHERE = set(os.environ.get("MINIPS_STREAM_DELAY_WHERE", "use,fork").split(","))
+
+_DEBUG = _parse_debug(os.environ.get("MINIPS_STREAM_DEBUG", ""))
+DELAY_US = int(_DEBUG.get("delay", "0") or 0)
+DELAY_WHERE = set(_DEBUG.get("where", "use+fork").split("+"))
+SYSFENCE = set(filter(None, _DEBUG.get("sysfence", "").split("+")))
+
+
+def fast_for(group: str) -> bool:
+    """Fence-free (same-device ordering only) events for ``group`` unless the debug mode asks for
+    system-scope fences there."""
+    return group not in SYSFENCE and "all" not in SYSFENCE
+
+
 _delay_bufs: dict = {}
 
 

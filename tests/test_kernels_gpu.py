@@ -412,6 +412,43 @@ def test_owner_rows_adagrad(dev, P, recv_dtype):
     torch.testing.assert_close(t_c, t_ref, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("P,recv_dtype", [(2, torch.float32), (8, torch.bfloat16), (13, torch.bfloat16)])
+def test_owner_push_adagrad_direct(dev, P, recv_dtype):
+    """The direct-addressed owner apply (stamp table, no owner-side plan) is bit-identical to the
+    planned fused apply (owner_slots + owner_rows_adagrad) over three consecutive pushes that share
+    one stamp table -- entries of earlier pushes must retire by their stamp -- and agrees with its
+    CPU reference."""
+    g = torch.Generator().manual_seed(100 + P)
+    R, W, D1, base = 40000, 36, 32, 700
+    table = torch.randn(R, W, generator=g)
+    state, state2 = torch.rand(R, generator=g), torch.rand(R, generator=g)
+    t_a, s_a, s2_a = table.to(dev), state.to(dev), state2.to(dev)
+    t_b, s_b, s2_b = table.to(dev), state.to(dev), state2.to(dev)
+    t_c, s_c, s2_c = table.clone(), state.clone(), state2.clone()
+    rs = torch.full((R * P * 2,), -1, dtype=torch.int32, device=dev)
+    for push in range(3):
+        splits = [int(x) for x in torch.randint(0 if push == 1 else 300, 2500, (P,), generator=g)]
+        segs = [torch.cat([torch.arange(min(n, 4)), torch.randperm(R - 4, generator=g)[: max(0, n - 4)] + 4]) + base
+                for n in splits]
+        recv_keys = torch.cat(segs)
+        M = recv_keys.numel()
+        recv = (torch.randn(M, W, generator=g) * 0.1).to(recv_dtype)
+        uniq, own_inv = torch.unique(recv_keys, return_inverse=True)
+        U = uniq.numel()
+        own_uniq = torch.full((max(M, 1),), -1, dtype=torch.int64)
+        own_uniq[:U] = uniq
+        slots = ops.owner_slots(own_inv.to(dev), splits, M)
+        ops.owner_rows_adagrad(t_a, s_a, own_uniq.to(dev), M, base, recv.to(dev), slots, P, 0.05, 1e-8, state2=s2_a,
+                               split=D1, n_dev=torch.tensor([U], device=dev))
+        ops.owner_push_adagrad(t_b, s_b, recv_keys.to(dev), base, recv.to(dev), splits, rs, push, 0.05, 1e-8,
+                               state2=s2_b, split=D1)
+        ops.owner_push_adagrad(t_c, s_c, recv_keys, base, recv, splits, None, push, 0.05, 1e-8, state2=s2_c, split=D1)
+    assert torch.equal(t_a.cpu(), t_b.cpu()) and torch.equal(s_a.cpu(), s_b.cpu())
+    assert torch.equal(s2_a.cpu(), s2_b.cpu())
+    torch.testing.assert_close(t_b.cpu(), t_c, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(s_b.cpu(), s_c, rtol=1e-5, atol=1e-6)
+
+
 def test_device_counts_and_prebuilt_csr(dev):
     """unique_bucketize_n's device-side U bounds gather / row-wise Adagrad / the embedding
     backward without a host sync; the CSR prebuilt at planning time gives the same gradient."""
@@ -540,11 +577,12 @@ def test_colsum_bf16(dev):
 
 @pytest.mark.parametrize("B,cards,P", [(16384, [3, 1460, 10131227, 583, 24, 2202608], 1),
                                        (16384, [3, 1460, 10131227, 583, 24, 2202608], 8), (1000, [5, 70000], 3),
-                                       (16384, [1 << 24], 1)])
+                                       (16384, [1 << 24], 1), (4096, [1 << 27, 7, 1], 16)])
 def test_plan_sorted_matches_reference(dev, B, cards, P):
     """Atomic-free sort-based planning (plan.hip) vs the CPU reference of the same op: unique keys
-    column-major / ascending, stably regrouped by owner for P > 1 owners; uniq[inv] == routed
-    keys; the lookup CSR with contiguous rows; per-owner counts."""
+    column-major / ascending, stably regrouped by owner for P > 1 owners (the owner bits ride above
+    the key in the sort: 27 + 4 bits for 16 owners); uniq[inv] == routed keys; the lookup CSR with
+    contiguous rows; per-owner counts."""
     g = torch.Generator().manual_seed(B + len(cards) + P)
     bases = [sum(cards[:f]) for f in range(len(cards))]
     cols = []

@@ -106,7 +106,6 @@ def test_rccl_destroy_reinit_restore(tmp_path, monkeypatch):
 
     if dist.is_initialized():
         pytest.skip("a process group is already initialised in this process")
-    monkeypatch.setenv("MINIPS_OVERLAP_W1", "sparse,dense")  # clocks on side streams at world 1
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
 

@@ -356,6 +356,70 @@ def cmd_rccl(a):
     dist.destroy_process_group()
 
 
+def cmd_issue(a):
+    """HOST issue cost per call (no sync between calls) of the step's building blocks on one GPU:
+    c10d collectives over a one-rank RCCL group (the Python + ProcessGroupNCCL + RCCL enqueue path
+    each rank pays per call on an N-rank job), one of our kernel bindings, a torch elementwise op,
+    and event record / wait -- the units a step's host budget is spent in."""
+    import time
+
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29731", world_size=1, rank=0,
+                                device_id=dev)
+    from minips_amd import ops
+
+    n = 1 << 16
+    f = torch.ones(n, device=dev)
+    o = torch.empty(n, device=dev)
+    bfv = torch.ones(n, dtype=torch.bfloat16, device=dev)
+    bo = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    keys = torch.arange(4096, device=dev)
+    table = torch.randn(8192, 36, device=dev)
+    rows = torch.empty(4096, 36, dtype=torch.bfloat16, device=dev)
+    ev = torch.cuda.Event()
+    s2 = torch.cuda.Stream(dev)
+    from minips_amd.utils import streams
+
+    fev = streams.FastEvent()
+    cur = torch.cuda.current_stream(dev)
+    pin = torch.zeros(8, dtype=torch.int64, pin_memory=True)
+    cases = {
+        "c10d all_to_all_single (equal)": lambda: dist.all_to_all_single(bo, bfv),
+        "c10d all_to_all_single (splits)": lambda: dist.all_to_all_single(bo, bfv, [n], [n]),
+        "c10d reduce_scatter_tensor": lambda: dist.reduce_scatter_tensor(o, f),
+        "c10d all_gather_into_tensor": lambda: dist.all_gather_into_tensor(bo, bfv),
+        "c10d all_reduce": lambda: dist.all_reduce(f),
+        "ops.gather_rows (binding)": lambda: ops.gather_rows(table, keys, 0, rows),
+        "torch add_ (elementwise)": lambda: o.add_(f),
+        "torch.empty": lambda: torch.empty(n, device=dev),
+        "event record + wait": lambda: (ev.record(), s2.wait_event(ev)),
+        "FastEvent record + wait": lambda: (fev.record(cur), fev.wait(s2)),
+        "torch.cuda.Event() create + record": lambda: torch.cuda.Event().record(),
+        "stream.wait_stream": lambda: s2.wait_stream(cur),
+        "tensor.record_stream": lambda: f.record_stream(s2),
+        "streams.current()": lambda: streams.current(dev),
+        "pinned empty(16)": lambda: torch.empty(16, dtype=torch.int64, pin_memory=True),
+        "tensor.tolist() (pinned, 8)": lambda: pin.tolist(),
+        "slice view": lambda: f[128:4096],
+    }
+    print(f"{'call':40s} {'host us/call':>12s}")
+    for name, fn in cases.items():
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            fn()
+        t = (time.perf_counter() - t0) / a.iters
+        torch.cuda.synchronize()
+        print(f"{name:40s} {t * 1e6:12.2f}", flush=True)
+    dist.destroy_process_group()
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -391,6 +455,7 @@ def main(argv=None):
     p.add_argument("--iters", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--ops", default="reduce_scatter,all_gather,all_to_all,all_to_all_v")
+    sub.add_parser("issue").add_argument("--iters", type=int, default=200)
     a = ap.parse_args(argv)
     from minips_amd import _native
 

@@ -15,6 +15,10 @@
 #                  (bench.py, STEPS default 300) it prints ms/step per run, else the command's output tail:
 #                    AB='tree=ab_old;base' bash tools/gpu_round.sh ab         (previous round vs this tree)
 #                    CMD='python tools/bench_kernels.py kscan --Ks 848' AB='MINIPS_GEMM_TILE=128;MINIPS_GEMM_TILE=256'
+#     host         per-phase host issue time (bench.py --host-phases) at world 1 and emulated EMU_PROF (8), and
+#                  the host cost per call of c10d collectives / bindings / events (bench_kernels.py issue)
+#     race         the 4-rank SSP one-sided test with the push stream on, once per MINIPS_STREAM_DEBUG variant in
+#                  RACE_VARIANTS (';'-separated; a failing test goes on to the next variant, a crash stops)
 #     pytest       one pytest selection: PYTEST_SEL (e.g. 'tests/test_multirank_gpu.py -k ssp'), env PYTEST_ENV
 # Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, MODES, AB, RUNS, CMD, TAIL, PYTEST_SEL, PYTEST_ENV.
 # This one runner replaces the per-experiment command files of rounds 1-4 (git history keeps them).
@@ -114,6 +118,27 @@ if [[ $STAGE == ab ]]; then
         tail -${TAIL:-20} gpurun_out/ab.log
       fi
     done
+  done
+fi
+if [[ $STAGE == host ]]; then
+  timeout -k 10 300 python bench.py --steps 100 --warmup 10 --host-phases 100 ${BENCH_ARGS} > gpurun_out/host_w1.log 2>&1 || { tail -30 gpurun_out/host_w1.log; exit 1; }
+  grep "host-phases" gpurun_out/host_w1.log | head -40
+  timeout -k 10 300 python bench.py --steps 100 --warmup 10 --emulate-world ${EMU_PROF:-8} --diag-steps 0 --host-phases 100 ${BENCH_ARGS} > gpurun_out/host_emu.log 2>&1 || { tail -30 gpurun_out/host_emu.log; exit 1; }
+  grep "host-phases" gpurun_out/host_emu.log | head -40
+  timeout -k 10 200 python tools/bench_kernels.py issue > gpurun_out/host_issue_calls.txt 2>&1 || { tail -30 gpurun_out/host_issue_calls.txt; exit 1; }
+  cat gpurun_out/host_issue_calls.txt
+fi
+if [[ $STAGE == race ]]; then
+  IFS=';' read -ra RV <<< "${RACE_VARIANTS:-none;delay=300;delay=300,where=use;delay=300,where=fork}"
+  sel='tests/test_multirank_gpu.py::test_widedeep_ssp_world4_tracks_one_rank_bsp[onesided]'
+  for v in "${RV[@]}"; do
+    dbg=$v; [[ $v == none ]] && dbg=""
+    rc=0
+    MINIPS_PS_PUSH_STREAM=${PUSH:-1} MINIPS_STREAM_DEBUG="$dbg" timeout -k 10 300 python -u -m pytest "$sel" -x -q \
+      --timeout 240 --timeout-method thread > gpurun_out/race.log 2>&1 || rc=$?
+    echo "[race] push=${PUSH:-1} debug='$v' rc=$rc $(grep -Eo '[0-9]+ (passed|failed)[^=]*' gpurun_out/race.log | tail -1)"
+    grep -Eo "AssertionError: \(.{0,200}" gpurun_out/race.log | head -2 || true
+    if [[ $rc -ne 0 && $rc -ne 1 ]]; then tail -20 gpurun_out/race.log; exit 1; fi
   done
 fi
 if [[ $STAGE == pytest ]]; then
