@@ -109,25 +109,11 @@ def main():
         torch.cuda.set_stream(main_stream)
     feeder = LookaheadFeeder(model, data, comm)
     step = feeder.step
-    # one rank: after eager warm-up steps the whole step is captured into one HIP graph
-    # (GraphedFeeder) and the remaining warm-up and all timed steps are graph replays
-    use_graph = dev.type == "cuda" and n == 1 and args.consistency == "bsp" and os.environ.get("MINIPS_GRAPH",
-                                                                                               "0") == "1"
-    eager_warm = max(1, args.warmup - 1) if use_graph else args.warmup
-
     loss0 = None
     for i in range(args.warmup):
-        if use_graph and i == eager_warm:
-            from minips_amd.models.feeder import GraphedFeeder
-
-            step = GraphedFeeder(feeder, [model.emb, model.dense]).step
         l = step()
         if i == 0:
             loss0 = float(l.item()) / args.batch
-    if use_graph and args.warmup <= eager_warm:
-        from minips_amd.models.feeder import GraphedFeeder
-
-        step = GraphedFeeder(feeder, [model.emb, model.dense]).step
     model.drain()
     sync()
     comm.barrier()
@@ -207,7 +193,6 @@ def main():
                 "parallelism": parallelism,
                 "per_gpu_batch": args.batch,
                 "consistency": args.consistency,
-                "hip_graph": use_graph,
                 "world_size": comm.world,
                 "backend": comm.backend,
                 "bucket_mb": args.bucket_mb if n > 1 else None,

@@ -27,7 +27,8 @@ hipStream_t stream_of(const at::Tensor& t) {
 // Several outputs carved out of ONE caching-allocator block (256-byte aligned views): a planner
 // call hands back ~10 tensors, and one allocation + views costs a fraction of ten allocations on
 // the step's host path. The block lives while any of its views does.
-std::vector<at::Tensor> carve(const at::TensorOptions& o, const std::vector<std::pair<int64_t, at::ScalarType>>& parts) {
+std::vector<at::Tensor> carve(const at::TensorOptions& o,
+                              const std::vector<std::pair<int64_t, at::ScalarType>>& parts) {
   std::vector<int64_t> offs;
   int64_t total = 0;
   for (const auto& p : parts) {

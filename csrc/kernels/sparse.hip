@@ -692,23 +692,26 @@ __global__ __launch_bounds__(256) void owner_apply_kernel(float* table, int64_t 
   const bool has0 = c0 < D, has1 = c1 < D;
   for (int64_t i0 = wave * 8; i0 < M; i0 += nwaves * 8) {
     const int64_t i = i0 + sub;
-    const int me = i < M ? owner_seg(i, segs, P) : 0;
-    const int64_t row = i < M ? keys[i] - base : 0;
+    const bool in = i < M;
+    const int me = in ? owner_seg(i, segs, P) : 0;
+    const int64_t row = in ? keys[i] - base : 0;
+    // everything that depends on the row alone is loaded together (one round trip after the key):
+    // the stamp entries, the table row and its state -- the leader test then costs no extra trip
     const int2* e = rs + row * P;
-    const int2 e0 = i < M && l < P ? e[l] : make_int2(-1, -1);
-    const int2 e1 = i < M && l + 8 < P ? e[l + 8] : make_int2(-1, -1);
-    const int sl0 = e0.x == stamp ? e0.y : -1, sl1 = e1.x == stamp ? e1.y : -1;
-    // the leader: no lower requester sent this row in this push
-    const unsigned long long lower = __ballot(sl0 >= 0 && l < me) | __ballot(sl1 >= 0 && l + 8 < me);
-    const bool ok = i < M && ((lower >> (sub << 3)) & 0xffull) == 0;
+    const int2 e0 = in && l < P ? e[l] : make_int2(-1, -1);
+    const int2 e1 = in && l + 8 < P ? e[l + 8] : make_int2(-1, -1);
     float* tr = table + row * ld;
     float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0, g0 = t0, g1 = t0;
-    if (ok && has0) {
+    if (in && has0) {
       t0 = *reinterpret_cast<const float4*>(tr + c0);
       if (has1) t1 = *reinterpret_cast<const float4*>(tr + c1);
     }
-    const float st_old1 = ok ? state[row] : 0.f;
-    const float st_old2 = ok && D1 < D ? state2[row] : 0.f;
+    const float st_old1 = in ? state[row] : 0.f;
+    const float st_old2 = in && D1 < D ? state2[row] : 0.f;
+    const int sl0 = e0.x == stamp ? e0.y : -1, sl1 = e1.x == stamp ? e1.y : -1;
+    // the leader: no lower requester sent this row in this push
+    const unsigned long long lower = __ballot(sl0 >= 0 && l < me) | __ballot(sl1 >= 0 && l + 8 < me);
+    const bool ok = in && ((lower >> (sub << 3)) & 0xffull) == 0;
 #pragma unroll
     for (int s = 0; s < kOwnerMaxP; ++s) {
       if (s >= P) break;

@@ -21,16 +21,14 @@ std::mutex g_log_mu;
 }
 int VerboseLevel() {
   static int v = [] {
-    const char* s = std::getenv("MINIPS_V");
-    if (!s) s = std::getenv("GLOG_v");
+    const char* s = std::getenv("GLOG_v");  // glog's names (the reference logs through glog)
     return s ? std::atoi(s) : 0;
   }();
   return v;
 }
 void LogLine(int level, const std::string& line) {
   static int min_level = [] {
-    const char* s = std::getenv("MINIPS_MINLOGLEVEL");
-    if (!s) s = std::getenv("GLOG_minloglevel");
+    const char* s = std::getenv("GLOG_minloglevel");
     return s ? std::atoi(s) : 0;
   }();
   if (level < min_level) return;

@@ -65,7 +65,7 @@ struct CheckError : std::runtime_error {
     }                                                                                  \
   } while (0)
 
-// Log sink: one line per call, thread-safe. Level 0=INFO 1=WARN 2=ERROR. MINIPS_V gates
+// Log sink: one line per call, thread-safe. Level 0=INFO 1=WARN 2=ERROR. GLOG_v gates
 // verbose lines (the reference's GLOG_v / VLOG(1) lifecycle traces).
 void LogLine(int level, const std::string& line);
 int VerboseLevel();

@@ -11,7 +11,6 @@ issues exactly the collective sequence of a GPU run (ps/comm.py, ordering contra
 from __future__ import annotations
 
 import collections
-import os
 
 import torch
 
@@ -22,8 +21,8 @@ from ..utils.metrics import traced
 def default_depth(world: int) -> int:
     # one rank: depth 1 (measured neutral, 1/2/3 within 0.522-0.530 ms/step); several ranks: 2,
     # so the one host wait of a step (a plan's all-to-all split sizes) lands on counts issued a
-    # whole step earlier
-    return max(1, int(os.environ.get("MINIPS_LOOKAHEAD", "2" if world > 1 else "1")))
+    # whole step earlier (LookaheadFeeder(depth=...) overrides it)
+    return 2 if world > 1 else 1
 
 
 class LookaheadFeeder:
@@ -132,99 +131,3 @@ class LookaheadPlans:
             e[1] = self.emb.advance_plan(e[1], finish=True)
         if pend:
             pend[-1][1] = self.emb.advance_plan(pend[-1][1], finish=False)
-
-
-def _batch_plan_tensors(batch, pp) -> list:
-    """The device tensors one step hands to the next: the look-ahead batch and its pending key
-    plan (deduplicated by storage: the flat key view aliases the batch keys)."""
-    out, seen = [], set()
-    for t in (*batch, pp.flat, pp.uniq, pp.inv, pp.counts, pp.U_dev, *(pp.csr or ())):
-        if t is None or t.data_ptr() in seen:
-            continue
-        seen.add(t.data_ptr())
-        out.append(t)
-    return out
-
-
-class GraphedFeeder:
-    """One rank's whole training step -- next batch generation and key planning on the planning
-    stream, sparse Get, forward, backward (weight gradients on the side stream), Add, Clock --
-    captured into ONE HIP graph and replayed (torch.cuda.CUDAGraph = hipGraph on ROCm). This
-    removes the host issue cost (~0.37 ms of Python + launches per step) from the critical path.
-
-    Why a one-rank step is capturable: every size is static (buffers sized by the batch, unique
-    counts kept on the device and consumed by n_dev-bounded kernels), the Adam step and the data
-    generator's counter advance on the device, and nothing syncs with the host. The step consumes
-    the batch + plan produced by the previous step: the captured step copies the batch + plan it
-    produced into those static input slots at its end (after every reader joined), so the graph
-    replays in a closed loop. Host-side clocks (checkpoint metadata) advance per replay."""
-
-    def __init__(self, feeder: LookaheadFeeder, tables=()):
-        f = feeder
-        if not (f.cuda and f.comm.world == 1 and f.depth == 1):
-            raise ValueError("GraphedFeeder: one rank on a GPU with look-ahead depth 1")
-        for t in tables:
-            if getattr(t, "pipe", None) is not None and t.pipe.async_:
-                raise ValueError("GraphedFeeder needs synchronous clocks")
-        self.f, self.tables = f, list(tables)
-        torch.cuda.synchronize(f.comm.device)
-        # an eager step may leave its side-stream tail for the next step to wait on (WideDeep's
-        # _side_pending); it is complete now, and a capture must not wait on events from outside it
-        f.model.__dict__.pop("_side_pending", None)
-        batch, _ev = f.queue[0]
-        pend = f.model._pending_plans
-        if len(pend) != 1 or pend[0][0] is not batch[1]:
-            raise ValueError("GraphedFeeder: expected exactly the next batch's pending plan")
-        pp = pend[0][1]
-        pp.event = None  # already complete; a capture must not wait on an event recorded outside it
-        f.queue[0] = (batch, None)
-        static = _batch_plan_tensors(batch, pp)
-        saved = [(getattr(t, "step", None), t.pipe.clock) for t in self.tables]
-        # device twins of the host counters (Adam step, data draw): eager steps leave them alone,
-        # the captured step advances them on the device
-        for t in self.tables:
-            if hasattr(t, "sync_step_dev"):
-                t.sync_step_dev()
-        if hasattr(f.data, "graph_prepare"):
-            f.data.graph_prepare()
-        saved_draws = getattr(f.data, "_host_step", None)
-        self.graph = torch.cuda.CUDAGraph()
-        main, ps = f.main, f.plan_stream
-        with torch.cuda.graph(self.graph, stream=main):
-            ps.wait_stream(main)  # fork: the planning stream's work joins the capture
-            self.loss = f.step()
-            main.wait_stream(ps)  # join before the static slots are overwritten
-            (nb, _), = f.queue
-            npp = pend[-1][1]
-            produced = _batch_plan_tensors(nb, npp)
-            if [(t.shape, t.dtype) for t in produced] != [(t.shape, t.dtype) for t in static]:
-                raise RuntimeError("GraphedFeeder: the step's batch/plan layout is not static")
-            # one launch for every slot (11 separate copy nodes cost ~110 us of dispatch gaps)
-            pairs = [(d, s) for d, s in zip(static, produced) if d.numel()]
-            if pairs and all(d.is_contiguous() and s.is_contiguous() for d, s in pairs):
-                from .._native import kernels
-
-                kernels().multi_copy([d for d, _ in pairs], [s for _, s in pairs])
-            else:
-                for dst, src in pairs:
-                    dst.copy_(src)
-        # the capture ran nothing: restore the host view (static batch + plan are the next input)
-        f.queue.clear()
-        f.queue.append((batch, None))
-        pend[:] = [[batch[1], pp]]
-        for t, (st, ck) in zip(self.tables, saved):
-            if st is not None:
-                t.step = st
-            t.pipe.clock = ck
-        if saved_draws is not None:
-            f.data._host_step = saved_draws
-
-    def step(self):
-        self.graph.replay()
-        for t in self.tables:  # the host-side counters an eager step advances
-            if hasattr(t, "step"):
-                t.step += 1
-            t.pipe.clock += 1
-        if hasattr(self.f.data, "graph_replayed"):
-            self.f.data.graph_replayed(1)
-        return self.loss

@@ -47,6 +47,7 @@ class WideDeepConfig:
     # "auto" (default): one-sided for SSP / ASP (the reference's asynchronous servers, and faster on
     # one MI355X: 0.402 vs 0.411 ms/step, profiles/r4/ssp_onesided_vs_collective.txt), collective for BSP
     transport: str = "auto"
+    dense_transport: str | None = None  # (None: ``transport``) the dense table's, when it differs
     max_batch: int = 16384       # onesided: inbox slots hold max_batch * F gradient rows
     seed: int = 0
     # several ranks: the dense clock runs per bucket of >= bucket_mb MB of gradient (layers merged
@@ -57,6 +58,8 @@ class WideDeepConfig:
     def __post_init__(self):
         if self.transport == "auto":
             self.transport = "onesided" if self.consistency in ("ssp", "asp") else "collective"
+        if self.dense_transport is None:
+            self.dense_transport = self.transport
 
     @property
     def F(self):
@@ -161,9 +164,9 @@ class WideDeep(LookaheadPlans):
         off += cfg.hidden[-1] + 8
         self.n_params = off
         starts = [self.layout[f"W{i + 1}"][0] for i in range(len(cfg.hidden))]
-        bucketed = cfg.bucket_mb > 0 and cfg.transport == "collective" and comm.world > 1
+        bucketed = cfg.bucket_mb > 0 and cfg.dense_transport == "collective" and comm.world > 1
         self.dense = make("dense", n_params=self.n_params, optimizer="adam", lr=cfg.lr_dense, model=cfg.consistency,
-                          staleness=cfg.staleness, transport=cfg.transport,
+                          staleness=cfg.staleness, transport=cfg.dense_transport,
                           **(dict(buckets=starts, bucket_mb=cfg.bucket_mb) if bucketed else {}))
         # the bucket each layer's weight gradient completes (None: one clock at the end)
         self._wbucket = [self.dense.bucket_for_layer(x) for x in starts] if bucketed else None

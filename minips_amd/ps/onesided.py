@@ -128,8 +128,6 @@ class AsyncPS:
             self._locks: dict = {}
         else:
             self.server = runtime().AsyncServer(name, self.world, self.rank, _MAX_TABLES, self._apply_cpu)
-        if os.environ.get("MINIPS_PS_APPLY_LOG") == "1":
-            self.server.set_log(True)
         self.server.start()
         self.tables: dict[int, object] = {}
         # a straggler that never publishes again is a failure (the supervisor restarts the set),
@@ -244,8 +242,8 @@ class AsyncPS:
             self.server.resume()
 
     def apply_log(self) -> list:
-        """(table, requester, clock) triples in this owner's apply order (MINIPS_PS_APPLY_LOG=1 or
-        set_log(True) before the applies)."""
+        """(table, requester, clock) triples in this owner's apply order (server.set_log(True)
+        before the applies)."""
         flat = self.server.take_log()
         return [tuple(flat[i: i + 3]) for i in range(0, len(flat), 3)]
 
@@ -885,6 +883,11 @@ class AsyncDenseTable(_AsyncTable):
     the owner's apply writes), Add + Clock pushes each owner's slice of the gradient into its
     inbox, and the owner applies Adam / Adagrad / SGD / add with its own m / v state -- one
     optimizer step per push, as an asynchronous PS server does (each Add is applied on arrival).
+    Every rank pushes the whole gradient every clock, so one clock is P pushes: the scale-invariant
+    optimizers (Adam, Adagrad: a step moves ~lr whatever the gradient's size) take lr / P per push
+    (``push_lr``), so one clock of the job moves the parameters about as far as one BSP step --
+    with lr per push the 4-rank SSP W&D run moved them 4x as far and spiked (tools/ssp_probe.py,
+    profiles/r5/ssp_probe.txt). SGD / add are linear: the P pushes sum to the BSP step at lr.
     Same API as DenseTable (grad written in place by the models, get / add / clock / load_full /
     full_master)."""
 
@@ -900,6 +903,7 @@ class AsyncDenseTable(_AsyncTable):
         P, me, dev = comm.world, comm.rank, comm.device
         self.table_id, self.n_params = table_id, n_params
         self.optimizer, self.lr = optimizer, lr
+        self.push_lr = lr / P if optimizer in ("adam", "adagrad") else lr
         self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
         self.pull_dtype = pull_dtype
         self.value_dtype = torch.float32
@@ -936,7 +940,8 @@ class AsyncDenseTable(_AsyncTable):
             self.ps.server.add_dense(self.t, _OPT_CODES[optimizer], self.master.data_ptr(),
                                      self.m.data_ptr() if self.m is not None else 0,
                                      self.v.data_ptr() if self.v is not None else 0,
-                                     self._pulls[me].data_ptr() if self._pull_bf16 else 0, self.shard, float(lr),
+                                     self._pulls[me].data_ptr() if self._pull_bf16 else 0, self.shard,
+                                     float(self.push_lr),
                                      float(betas[0]), float(betas[1]), float(eps), float(weight_decay), 0,
                                      self._inbox[me].data_ptr(), self.slot_bytes, self.depth, self.ps.own_lock(self.t))
         else:
@@ -1067,10 +1072,10 @@ class AsyncDenseTable(_AsyncTable):
             return
         g = buf[off + _SLOT_HEADER: off + _SLOT_HEADER + 4 * self.shard].view(torch.float32).clone()
         if self.optimizer == "adam":
-            ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
+            ops.adam_apply(self.master, self.m, self.v, g, self.push_lr, self.betas[0], self.betas[1], self.eps,
                            self.weight_decay, self.cpu_step, 1.0, None)
         elif self.optimizer == "adagrad":
-            ops.adagrad_apply(self.master, self.m, g, self.lr, self.eps, 1.0, None)
+            ops.adagrad_apply(self.master, self.m, g, self.push_lr, self.eps, 1.0, None)
         elif self.optimizer == "sgd":
             ops.sgd_apply(self.master, g, self.lr, 1.0, None)
         else:

@@ -43,8 +43,13 @@ def even_bounds(num_rows: int, parts: int) -> list[int]:
     return b
 
 
+# multi-rank BSP clocks on the tables' side streams (OVERLAP False: inline on the compute stream --
+# the overlap-vs-sync numerics test flips it before building its tables)
+OVERLAP = True
+
+
 def _overlap_default() -> bool:
-    return os.environ.get("MINIPS_OVERLAP", "1") != "0"
+    return OVERLAP
 
 
 class _Pipeline:
@@ -259,7 +264,7 @@ class DenseTable:
         ``bucket_mb`` (with ``buckets``): merge consecutive layers into buckets of at least this many
         MB of fp32 gradient, walking from the last layer (the first whose backward completes) -- few,
         large collectives for the per-link bandwidth of the xGMI mesh instead of one per small
-        layer; MINIPS_BUCKET_MB overrides it.
+        layer.
 
         ``overlap_w1``: at world 1 too, run the clock on the table's side stream and, with
         ``buckets``, apply each bucket as soon as the backward finished its layer (one rank has
@@ -301,9 +306,6 @@ class DenseTable:
         self._ring = [self.grad] + [torch.zeros_like(self.grad) for _ in range(self.pipe.staleness + 1)] \
             if self.pipe.async_ else [self.grad]
         self.buckets = None
-        env_mb = __import__("os").environ.get("MINIPS_BUCKET_MB")
-        if env_mb:
-            bucket_mb = float(env_mb)
         if buckets is not None and bucket_mb:
             buckets = merge_buckets(buckets, n_params, bucket_mb * 2**20 / self.master.element_size())
         if buckets is not None and (comm.world > 1 or self.pipe.async_):
@@ -349,7 +351,7 @@ class DenseTable:
 
     def _step_dev_for_clock(self, first: bool = True):
         """The Adam step's device twin ``step_dev`` advances only inside a HIP-graph capture (a
-        replayed step must read a fresh step on the device; GraphedStep / GraphedFeeder set it
+        replayed step must read a fresh step on the device; GraphedStep sets it
         from the host step before capturing). Eager clocks pass the host step: no extra kernel
         on the clock's stream. Returns the step_dev argument for adam_apply."""
         if not (self.master.is_cuda and torch.cuda.is_current_stream_capturing()):
@@ -362,43 +364,56 @@ class DenseTable:
         """Before a HIP-graph capture: the device step twin = the host step."""
         self.step_dev.fill_(int(self.step))
 
+    def _bucket_views(self, k: int, grad: torch.Tensor):
+        """The views one bucket's clock works on (persistent buffers: built once per bucket and
+        gradient buffer of the ring -- ~10 slicing ops per bucket per clock off the host path)."""
+        key = (k, grad.data_ptr())
+        cache = self.__dict__.setdefault("_bview", {})
+        v = cache.get(key)
+        if v is None:
+            lo, hi = self.buckets[k]
+            off, sz, g0 = self._own_piece(k)
+            sl = slice(off, off + sz)
+            v = cache[key] = (grad[lo:hi], self.grad_shard[sl], self.master[sl],
+                              self.m[sl] if self.m is not None else None, self.v[sl] if self.v is not None else None,
+                              self.params[g0: g0 + sz], self.params[lo:hi])
+        return v
+
     @traced("dense.bucket_work")
     def _bucket_work(self, k: int, grad: torch.Tensor, step: int):
-        lo, hi = self.buckets[k]
-        off, sz, g0 = self._own_piece(k)
         comm = self.comm
         sd = self._step_dev_for_clock(first=not self._issued)
         self._issued.add(k)
-        sl = slice(off, off + sz)
+        g_b, gs_own, w, m, v, p_own, p_b = self._bucket_views(k, grad)
         local = comm.world == 1 and not comm.force  # one rank owns the whole bucket: no copy
         if local:
-            gs = grad[lo:hi]
+            gs = g_b
         else:
-            comm.reduce_scatter(self.grad_shard[off: off + sz], grad[lo:hi])
-            gs = self.grad_shard[sl]
-        out = self.params[g0: g0 + sz] if self.pull_dtype == torch.bfloat16 else None
+            comm.reduce_scatter(gs_own, g_b)
+            gs = gs_own
+        out = p_own if self.pull_dtype == torch.bfloat16 else None
         zeroed = False
         if self.optimizer == "adam":
             sink = getattr(self, "_sink", None)  # (one rank: the bucket's split-K wgrad planes)
             slabs = sink.take(gs) if sink is not None and local else ()
-            ops.adam_apply(self.master[sl], self.m[sl], self.v[sl], gs, self.lr, self.betas[0], self.betas[1],
-                           self.eps, self.weight_decay, step, 1.0, out, step_dev=sd, zero_g=local, slabs=slabs)
+            ops.adam_apply(w, m, v, gs, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, step, 1.0,
+                           out, step_dev=sd, zero_g=local, slabs=slabs)
             zeroed = local  # the kernel cleared the gradient it read
         elif self.optimizer == "adagrad":
-            ops.adagrad_apply(self.master[sl], self.m[sl], gs, self.lr, self.eps, 1.0, out)
+            ops.adagrad_apply(w, m, gs, self.lr, self.eps, 1.0, out)
         elif self.optimizer == "sgd":
-            ops.sgd_apply(self.master[sl], gs, self.lr, 1.0, out)
+            ops.sgd_apply(w, gs, self.lr, 1.0, out)
         elif self.optimizer == "add":
-            self.master[sl].add_(gs)
+            w.add_(gs)
             if out is not None:
-                ops.cast_f32_bf16(self.master[sl], out)
+                ops.cast_f32_bf16(w, out)
         else:
             raise ValueError(self.optimizer)
         if out is None:
-            self.params[g0: g0 + sz].copy_(self.master[sl])
-        comm.all_gather(self.params[lo:hi], self.params[g0: g0 + sz])
+            p_own.copy_(w)
+        comm.all_gather(p_b, p_own)
         if not zeroed:
-            grad[lo:hi].zero_()
+            g_b.zero_()
         key, nb = self._bstat[k]
         bb = comm.stats.bucket_bytes
         bb[key] = bb.get(key, 0) + nb

@@ -171,7 +171,7 @@ def _replay_check(out, world=2):
                 g = torch.zeros(S)
                 n = max(0, min(S, NP - db))
                 g[:n] = dense[db: db + n]
-                ops.adam_apply(w, m, v, g, 0.01, 0.9, 0.999, 1e-8, 0.0, step, 1.0, None)
+                ops.adam_apply(w, m, v, g, 0.01 / world, 0.9, 0.999, 1e-8, 0.0, step, 1.0, None)  # (push_lr)
         torch.testing.assert_close(res["shard"], shard, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(res["state"], state, rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(res["state2"], state2, rtol=1e-5, atol=1e-7)

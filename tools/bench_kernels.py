@@ -243,6 +243,45 @@ def cmd_emb(a):
     print(f"U={U} lookups={B * 26}: build+sum {full:.1f} us, csr build {build:.1f} us, zero+segment sum {seg:.1f} us")
 
 
+def cmd_embstep(a):
+    """The one-rank W&D step's non-GEMM critical chain on its real shapes, each kernel alone:
+    the embedding backward (deterministic segment sums, fp32 rows), the row-wise Adagrad of the
+    unique rows on the full 33.76M x 36 shard, and the input assembly read in place from the shard.
+    Planned by the real planner (plan_sorted, one owner). Median us and effective TB/s."""
+    from minips_amd.data.synthetic import CRITEO_KAGGLE_CARDS, CriteoSynth
+
+    B, cards = a.batch, CRITEO_KAGGLE_CARDS
+    F, D, W = len(cards), 32, 36
+    R = sum(cards)
+    dense, keys, _ = CriteoSynth(B, device=dev(), seed=1).next()
+    bases = torch.tensor([sum(cards[:f]) for f in range(F)], device=dev())
+    bits = [max(1, (c - 1).bit_length()) for c in cards]
+    mult = 402653189 if R % 402653189 else 201326611
+    res = ops.plan_sorted(keys, bases, bits, mult, R)
+    uniq, inv, U_dev, members, memrow, rowstart, rowidx = res[0], res[1], res[3], res[4], res[5], res[7], res[8]
+    U = int(U_dev.item())
+    table = torch.randn(R, W, device=dev()) * 0.01
+    state, state2 = torch.zeros(R, device=dev()), torch.zeros(R, device=dev())
+    dX = (torch.randn(B, F * D, device=dev()) * 0.01).to(torch.bfloat16)
+    dw = torch.randn(B, device=dev()) * 0.01
+    g = torch.zeros(B * F, W, device=dev())
+    X = torch.empty(B, 896, device=dev(), dtype=torch.bfloat16)
+    wide = torch.empty(B, device=dev())
+    n = B * F
+    t_emb = timed(lambda: ops.wd_emb_backward(dX, dw, inv, F, D, g, csr=(members, memrow)))
+    t_ada = timed(lambda: ops.sparse_rowwise_adagrad(table, state, uniq, 0, g, 0.01, 1e-8, state2=state2, split=D,
+                                                     n_dev=U_dev))
+    t_asm = timed(lambda: ops.wd_assemble_tab(dense, table, uniq, 0, inv, F, D, X, wide, ones_col=F * D + 13,
+                                              rowidx=rowidx))
+    mb_emb = (n * D * 2 + n * 8 + B * 4 + U * W * 4) / 1e6
+    mb_ada = (U * W * 4 * 3 + U * 16) / 1e6
+    mb_asm = (n * 4 + n * 128 + B * 896 * 2) / 1e6
+    print(f"U={U} lookups={n}")
+    for name, t, mb in (("emb backward", t_emb, mb_emb), ("rowwise adagrad", t_ada, mb_ada),
+                        ("assemble (in place)", t_asm, mb_asm)):
+        print(f"{name:22s} {t:8.1f} us  {mb:7.1f} MB  {mb / t:6.2f} TB/s")
+
+
 def cmd_plan(a):
     from minips_amd.data.synthetic import CRITEO_KAGGLE_CARDS, CriteoSynth
 
@@ -447,7 +486,7 @@ def main(argv=None):
     p.add_argument("--T", type=int, default=1024)
     p.add_argument("--H", type=int, default=12)
     sub.add_parser("nn")
-    for name in ("emb", "plan"):
+    for name in ("emb", "plan", "embstep"):
         sub.add_parser(name).add_argument("--batch", type=int, default=16384)
     p = sub.add_parser("rccl")
     p.add_argument("--min-mb", type=float, default=0.25)

@@ -65,13 +65,24 @@ def _headers(*dirs: str) -> list[str]:
     return hs
 
 
+def _run_to(out: str, cmd: list[str]) -> None:
+    """Link shared objects to a temporary name and rename: a copy of the tree taken meanwhile (a
+    GPU run's snapshot) sees the old library or the new one, never a half-written file."""
+    if not out.endswith(".so"):
+        _run(cmd)
+        return
+    tmp = out + ".tmp"
+    _run([tmp if c == out else c for c in cmd])
+    os.replace(tmp, out)
+
+
 def _compile_many(jobs: list[tuple[str, list[str], list[str]]]) -> None:
     """jobs: (out, inputs, cmd)."""
     todo = [j for j in jobs if _stale(j[0], j[1])]
     if not todo:
         return
     with cf.ThreadPoolExecutor(JOBS) as ex:
-        futs = [ex.submit(_run, cmd) for _, _, cmd in todo]
+        futs = [ex.submit(_run_to, out, cmd) for out, _, cmd in todo]
         for f in futs:
             f.result()
 

@@ -2,8 +2,8 @@
 # One GPU-box pass; every GPU step has its own time limit and any failure stops the script.
 #   bash tools/gpu_round.sh STAGE [STAGE ...]     (stages run in the order given; default: all)
 #     all          smoke + GPU tests + short bench + rocprofv3 kernel stats of the bench
-#     trace        kernel trace of the W&D bench per MINIPS_GRAPH mode in MODES (default "0"), with the
-#                  steady-state step breakdown (tools/prof_summary.py trace)
+#     trace        kernel trace of the W&D bench (BENCH_ARGS), with the steady-state step breakdown and
+#                  one step's timeline (tools/prof_summary.py trace; ANCHOR: the kernel a step starts at)
 #     audit        host issue time + host syncs per step at world 1 (the real path) and 4 / 8 (gloo, one card)
 #     micro        isolated GPT-2 kernels: every GEMM shape vs hipBLASLt, memory-bound kernels, attention
 #     models       bench lines of the other BASELINE configs (MODELS, default "mlp dlrm dlrm-10b gpt2")
@@ -20,7 +20,7 @@
 #     race         the 4-rank SSP one-sided test with the push stream on, once per MINIPS_STREAM_DEBUG variant in
 #                  RACE_VARIANTS (';'-separated; a failing test goes on to the next variant, a crash stops)
 #     pytest       one pytest selection: PYTEST_SEL (e.g. 'tests/test_multirank_gpu.py -k ssp'), env PYTEST_ENV
-# Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, MODES, AB, RUNS, CMD, TAIL, PYTEST_SEL, PYTEST_ENV.
+# Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, ANCHOR, AB, RUNS, CMD, TAIL, PYTEST_SEL, PYTEST_ENV.
 # This one runner replaces the per-experiment command files of rounds 1-4 (git history keeps them).
 set -eo pipefail
 cd "$(dirname "$0")/.."
@@ -48,13 +48,13 @@ if [[ $STAGE == all || $STAGE == prof ]]; then
 fi
 if [[ $STAGE == trace ]]; then
   prof_env
-  for g in ${MODES:-0}; do
+  for g in 0; do
     d=gpurun_out/trace_g$g
     rm -rf $d
-    MINIPS_GRAPH=$g timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python bench.py --steps 30 --warmup 5 ${BENCH_ARGS} > $d.log 2>&1 || { tail -30 $d.log; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python bench.py --steps 30 --warmup 5 ${BENCH_ARGS} > $d.log 2>&1 || { tail -30 $d.log; exit 1; }
     f=$(find $d -name "*kernel_trace.csv" | head -1)
-    echo "=== MINIPS_GRAPH=$g ($f)"
-    python tools/prof_summary.py trace "$f" --anchor adam_kernel --skip 8 --top ${TOP:-30} | tee $d.summary.txt
+    echo "=== trace ($f)"
+    python tools/prof_summary.py trace "$f" --anchor ${ANCHOR:-wd_head_kernel} --skip 8 --top ${TOP:-30} --timeline | tee $d.summary.txt
   done
 fi
 if [[ $STAGE == audit ]]; then
