@@ -46,7 +46,7 @@ def main():
     ap.add_argument("--test-cards", default="", help=argparse.SUPPRESS)
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed run: host issue time per step and a cProfile of N more steps (stderr)")
-    ap.add_argument("--bucket_mb", type=float, default=2.0,
+    ap.add_argument("--bucket_mb", type=float, default=0.0,
                     help="several ranks: dense-clock bucket size in MB (layers merged from the last one; 0 = one "
                          "reduce-scatter + all-gather after the backward)")
     ap.add_argument("--host-phases", type=int, default=0,

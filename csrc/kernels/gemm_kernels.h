@@ -599,6 +599,8 @@ __global__ __launch_bounds__(TM * TN / 64) void gemm_v2_kernel(const bf16_t* __r
     int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
     bid = base + (bid >> 3);
   }
+  // (a grouped order for wide grids -- ~tiles_m / 8 row tiles walked column by column per XCD, so
+  // the LM head's tiles share B panels in L2 -- measured slower: 676 -> 730 us on the logits GEMM)
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * TM, n0 = tn * TN;
   {
@@ -703,8 +705,8 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
     const double eff128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
     const int pick = force ? force : (eff256 >= eff128 ? 256 : 128);
     // (round 4's 8-wave 256x256 variants -- phase-split v3, quarter-staged v4, ping-pong v5 -- and
-    // round 5's 4-wave 128x128-per-wave v6 measured slower than v2 on the model shapes and are gone:
-    // profiles/r4/gemm_*_v5.txt, profiles/r5/gemm_v6.txt)
+    // round 5's 4-wave 128x128-per-wave v6 and 4-deep ring of 32-deep K-steps v7 measured slower
+    // than v2 on the model shapes and are gone: profiles/r4/gemm_*_v5.txt, profiles/r5/gemm_v7_ring.txt)
     EpiArgs e2 = ep;
     e2.zmap = 1;  // split-K slice-major XCD runs (EpiArgs::zmap)
     if (pick == 256) {

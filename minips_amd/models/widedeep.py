@@ -52,8 +52,11 @@ class WideDeepConfig:
     seed: int = 0
     # several ranks: the dense clock runs per bucket of >= bucket_mb MB of gradient (layers merged
     # from the last one), a bucket's reduce-scatter + Adam + all-gather issued as soon as its
-    # layers' weight gradients exist -- beside the remaining backward (0: one clock at the end)
-    bucket_mb: float = 2.0
+    # layers' weight gradients exist -- beside the remaining backward (0: one clock at the end).
+    # The 6.3 MB of W&D gradients: one reduce-scatter + all-gather after the backward measured
+    # 6 % faster than two buckets at 8 emulated ranks (0.475-0.503 vs 0.517-0.530 ms/step: half
+    # the collective calls and clock issue on the host-bound step; profiles/r5/ab_dense_buckets.txt)
+    bucket_mb: float = 0.0
 
     def __post_init__(self):
         if self.transport == "auto":

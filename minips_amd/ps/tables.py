@@ -33,7 +33,7 @@ import torch
 from .. import ops
 from .comm import Comm
 from ..utils import streams
-from ..utils.metrics import traced
+from ..utils.metrics import phase, traced
 
 
 def even_bounds(num_rows: int, parts: int) -> list[int]:
@@ -1011,7 +1011,7 @@ class SparseTable:
         if pp.cev is not None and not pp.cev.query():
             # the only possible host wait of a step: the all-to-all splits (with look-ahead depth 2
             # they were exchanged a step earlier, so normally they are in already: no wait)
-            with self.comm.waiting():
+            with self.comm.waiting(), phase("sparse.count_wait"):
                 pp.cev.synchronize()
         send, recv = pp.host[0].tolist(), pp.host[1].tolist()
         U, M = int(sum(send)), int(sum(recv))

@@ -18,7 +18,8 @@ from minips_amd import ops
 dev = torch.device("cuda", 0)
 bf = lambda x: x.to(torch.bfloat16)
 worst = 0.0
-for (M, N, K) in [(256, 256, 64), (520, 264, 200), (1000, 776, 848), (64, 1024, 1032), (300, 2048, 72)]:
+for (M, N, K) in [(256, 256, 64), (520, 264, 200), (1000, 776, 848), (64, 1024, 1032), (300, 2048, 72),
+                  (4160, 4200, 72)]:  # (>= 16 x 16 tiles: the grouped wide-grid order)
     for layout in ("nt", "nn", "tn"):
         a_km, b_kn = {"nt": (False, False), "nn": (False, True), "tn": (True, True)}[layout]
         if (a_km and M % 8) or (b_kn and N % 8):

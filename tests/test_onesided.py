@@ -124,6 +124,7 @@ def _replay_run(rank, world, dev=torch.device("cpu")):
                           pull_dtype=torch.float32, init_std=0.0, route="range", max_keys=64, split=6)
     dn = AsyncDenseTable(comm, NP, optimizer="adam", lr=0.01, consistency="asp", pull_dtype=torch.float32)
     sp.ps.server.set_log(True)
+    comm.barrier()  # every owner logs before any peer pushes (else its first applies go unlogged)
     for c in range(STEPS):
         if rank == 1 and c % 3 == 0:
             time.sleep(0.01)  # vary the interleaving

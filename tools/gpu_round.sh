@@ -10,7 +10,8 @@
 #     models-prof  rocprofv3 kernel stats of those model steps (MODELS)
 #     emu          bench.py --emulate-world N (EMU_WORLDS, default "2 8") next to N=1, kernel trace of N=EMU_PROF
 #     ab           interleaved A/B: variants are ';'-separated env lists in AB, each run RUNS times (default 2)
-#                  round-robin (`base`: no env); a variant may start with `tree=<dir>` to run another built tree (e.g. the
+#                  round-robin (`base`: no env; `args=<bench flags>`: extra bench.py flags); a variant may start
+#                  with `tree=<dir>` to run another built tree (e.g. the
 #                  previous round's, checked out and built in-tree under ab_old/). With the default CMD
 #                  (bench.py, STEPS default 300) it prints ms/step per run, else the command's output tail:
 #                    AB='tree=ab_old;base' bash tools/gpu_round.sh ab         (previous round vs this tree)
@@ -107,10 +108,11 @@ if [[ $STAGE == ab ]]; then
   IFS=';' read -ra VARIANTS <<< "${AB:-base}"
   for i in $(seq "${RUNS:-2}"); do
     for v in "${VARIANTS[@]}"; do
-      dir=$ROOT; envs=$v; [[ $v == base ]] && envs=""
+      dir=$ROOT; envs=$v; extra=""; [[ $v == base ]] && envs=""
       if [[ $v == tree=* ]]; then dir=$ROOT/${v%% *}; dir=${dir/tree=/}; envs=${v#* }; [[ $envs == tree=* ]] && envs=""; fi
+      if [[ $v == args=* ]]; then extra=${v#args=}; envs=""; fi
       if [[ -z "${CMD}" ]]; then
-        (cd "$dir" && env $envs timeout -k 10 300 python bench.py --steps "${STEPS:-300}" --warmup 10 ${BENCH_ARGS} > $ROOT/gpurun_out/ab.log 2>&1) || { tail -20 gpurun_out/ab.log; exit 1; }
+        (cd "$dir" && env $envs timeout -k 10 300 python bench.py --steps "${STEPS:-300}" --warmup 10 ${BENCH_ARGS} $extra > $ROOT/gpurun_out/ab.log 2>&1) || { tail -20 gpurun_out/ab.log; exit 1; }
         python -c "import json; d=json.loads([l for l in open('gpurun_out/ab.log') if l.startswith('{')][-1]); print('[$v]', d['ms_per_step'])"
       else
         echo "== [$v] (run $i)"
