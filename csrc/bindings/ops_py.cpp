@@ -9,6 +9,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <tuple>
@@ -74,11 +75,38 @@ float* strided_vec_ptr(const c10::optional<at::Tensor>& t, const char* name) {
 // C = A . B with layout flags; see gemm.hip. Returns nothing (C preallocated).
 // Batched mode (batch > 1): operands are flat buffers addressed with 2-level strides; every
 // batch's extent is bounds-checked against the tensor sizes before launch.
-void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K, bool a_km,
-          bool b_kn, int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& mask,
-          const c10::optional<at::Tensor>& colsum, double alpha, int64_t split_k, int64_t batch, int64_t inner,
-          int64_t lda_, int64_t ldb_, int64_t ldc_, std::vector<int64_t> strides,
-          const c10::optional<at::Tensor>& perm, int64_t seg) {
+// One validated GEMM launch: every pointer, dimension and epilogue argument of gemm_bf16_batched,
+// so that a LaunchList can replay it without re-validating (the checks ran when it was prepared).
+struct GemmLaunch {
+  const bf16_t *A, *B;
+  void* C;
+  int M, N, K, lda, ldb, ldc;
+  bool a_km, b_kn;
+  int epi;
+  const bf16_t *bias, *mask;
+  int ldmask;
+  float* colsum;
+  float alpha;
+  int split_k, batch, inner;
+  int64_t st[6];
+  float* slab;
+  const int* perm;
+  int seg, colsum_ld;
+  void launch(hipStream_t s) const {
+    minips_k::gemm_bf16_batched(A, B, C, M, N, K, lda, ldb, ldc, a_km, b_kn, epi, bias, mask, ldmask, colsum, alpha,
+                                split_k, batch, inner, st[0], st[1], st[2], st[3], st[4], st[5], s, slab, perm, seg,
+                                colsum_ld);
+  }
+};
+
+// Validates a gemm() call and returns its launch; ``slab`` receives the split-K planes it needs
+// (a caching-allocator block), if any.
+GemmLaunch prepare_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K,
+                        bool a_km, bool b_kn, int64_t epi, const c10::optional<at::Tensor>& bias,
+                        const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& colsum, double alpha,
+                        int64_t split_k, int64_t batch, int64_t inner, int64_t lda_, int64_t ldb_, int64_t ldc_,
+                        const std::vector<int64_t>& strides, const c10::optional<at::Tensor>& perm, int64_t seg,
+                        at::Tensor& slab) {
   // 2-D operands may be column-sliced views: rows contiguous (stride(1) == 1), ld = stride(0).
   auto check_mat = [](const at::Tensor& t, const char* n) {
     TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
@@ -155,19 +183,29 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     TORCH_CHECK(colsum->dim() == 1 && colsum->numel() >= N && colsum->stride(0) >= 1, "colsum: 1-D, >= N values");
   }
   const int colsum_ld = colsum_p ? (int)colsum->stride(0) : 1;
-  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
-  at::Tensor slab;
   if (epi == minips_k::kEpiStoreBf16 && split_k > 1)
     TORCH_CHECK(batch <= 1 && N % 4 == 0 && ldc % 4 == 0, "split-K bf16 store: no batch, N % 4 == 0, ldc % 4 == 0");
   // split-K slices land in fp32 slab planes and one reduce kernel adds them (deterministic, no atomics)
   if (split_k > 1 && batch <= 1 &&
       (epi == minips_k::kEpiAtomicF32 || epi == minips_k::kEpiStoreBf16) && N % 4 == 0)
     slab = at::empty({split_k * M * N}, A.options().dtype(at::kFloat));  // caching allocator, stream-ordered
-  minips_k::gemm_bf16_batched(ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb,
-                              (int)ldc, a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p, (float)alpha,
-                              (int)split_k, (int)batch, (int)inner, st[0], st[1], st[2], st[3], st[4], st[5],
-                              stream_of(A), slab.defined() ? ptr<float>(slab) : nullptr, perm_p, (int)seg,
-                              colsum_ld);
+  GemmLaunch g{ptr<bf16_t>(A), ptr<bf16_t>(B), C.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc,
+               a_km, b_kn, (int)epi, bias_p, mask_p, ldmask, colsum_p, (float)alpha, (int)split_k, (int)batch,
+               (int)inner, {st[0], st[1], st[2], st[3], st[4], st[5]}, slab.defined() ? ptr<float>(slab) : nullptr,
+               perm_p, (int)seg, colsum_ld};
+  return g;
+}
+
+void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K, bool a_km,
+          bool b_kn, int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& mask,
+          const c10::optional<at::Tensor>& colsum, double alpha, int64_t split_k, int64_t batch, int64_t inner,
+          int64_t lda_, int64_t ldb_, int64_t ldc_, std::vector<int64_t> strides,
+          const c10::optional<at::Tensor>& perm, int64_t seg) {
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(A.device());
+  at::Tensor slab;
+  prepare_gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, alpha, split_k, batch, inner, lda_, ldb_, ldc_,
+               strides, perm, seg, slab)
+      .launch(stream_of(A));
 }
 
 // Bitmap planner of a bounded key space (keys, after the optional routing k * mult mod rn, in
@@ -686,7 +724,15 @@ int64_t new_stream(int64_t device, int64_t priority) {
   return reinterpret_cast<int64_t>(st);
 }
 
-void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
+struct ColsumLaunch {
+  const bf16_t* x;
+  int64_t M;
+  int N, ld;
+  float *out, *slab;
+  void launch(hipStream_t s) const { minips_k::colsum_bf16(x, M, N, ld, out, slab, s); }
+};
+
+ColsumLaunch prepare_colsum(const at::Tensor& x, at::Tensor& out, at::Tensor& slab) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x: row-major GPU matrix");
   check_dtype(x, at::kBFloat16, "x");
   check_gpu(out, "out");
@@ -694,13 +740,17 @@ void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
   TORCH_CHECK(out.numel() >= x.size(1) && x.size(1) % 8 == 0 && x.stride(0) % 8 == 0,
               "colsum: out >= N floats, N and the row stride multiples of 8");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "colsum: x must be 16-byte aligned");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   // the blocks' partial rows: a caching-allocator block on the stream (reused, no fill)
   const int64_t strips = (x.size(1) + 63) / 64;
-  at::Tensor slab = at::empty({minips_k::colsum_chunks(x.size(0), (int)x.size(1)) * strips * 64},
-                              out.options().dtype(at::kFloat));
-  minips_k::colsum_bf16(ptr<bf16_t>(x), x.size(0), (int)x.size(1), (int)x.stride(0), ptr<float>(out),
-                        slab.data_ptr<float>(), stream_of(x));
+  slab = at::empty({minips_k::colsum_chunks(x.size(0), (int)x.size(1)) * strips * 64}, out.options().dtype(at::kFloat));
+  return ColsumLaunch{ptr<bf16_t>(x), x.size(0), (int)x.size(1), (int)x.stride(0), ptr<float>(out),
+                      slab.data_ptr<float>()};
+}
+
+void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor slab;
+  prepare_colsum(x, out, slab).launch(stream_of(x));
 }
 
 void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g, double lr, double beta1,
@@ -1386,6 +1436,116 @@ class FastEvent {
   hipEvent_t ev_ = nullptr;
 };
 
+// A recorded launch sequence over two streams (0: the step's compute stream, 1: its side stream),
+// replayed from C++ with no per-launch validation, argument conversion or Python dispatch. The
+// recording IS the first execution: every op below launches on the current stream (which must be
+// one of the list's two) and appends its validated launch; fork() orders the two streams with an
+// event the list owns. run() replays the whole sequence onto the streams it is given. The list
+// holds every tensor a launch addresses (operands and its own split-K planes), so no recorded
+// address can be freed and handed to another buffer while the list lives; callers key lists by
+// the buffers they address and record again when those change. Replaces ~25 binding calls of the
+// W&D dense forward / backward per step (ops.gemm's argument conversion is 4-6 us of host each).
+class LaunchList {
+ public:
+  LaunchList(int64_t main, int64_t side)
+      : rec_{reinterpret_cast<hipStream_t>(main), reinterpret_cast<hipStream_t>(side)} {}
+  ~LaunchList() {
+    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+  }
+  LaunchList(const LaunchList&) = delete;
+  LaunchList& operator=(const LaunchList&) = delete;
+
+  void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K, bool a_km,
+            bool b_kn, int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& mask,
+            const c10::optional<at::Tensor>& colsum, double alpha, int64_t split_k,
+            const c10::optional<at::Tensor>& perm, int64_t seg) {
+    c10::hip::HIPGuardMasqueradingAsCUDA gd(A.device());
+    at::Tensor slab;
+    const GemmLaunch g = prepare_gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, alpha, split_k, 1, 1, 0,
+                                      0, 0, {}, perm, seg, slab);
+    const int k = slot(A);
+    g.launch(rec_[k]);
+    for (const auto* t : {&bias, &mask, &colsum, &perm})
+      if (t->has_value() && (*t)->defined()) keep_.push_back(**t);
+    hold({A, B, C, slab});
+    ops_.push_back([g, k](const hipStream_t* s) { g.launch(s[k]); });
+  }
+
+  int64_t gemm_slab(const at::Tensor& A, const at::Tensor& B, at::Tensor& slab, int64_t M, int64_t N, int64_t K,
+                    bool a_km, bool b_kn, int64_t split_k) {
+    check_gpu(A, "A");
+    check_gpu(B, "B");
+    check_gpu(slab, "slab");
+    check_dtype(A, at::kBFloat16, "A");
+    check_dtype(B, at::kBFloat16, "B");
+    check_dtype(slab, at::kFloat, "slab");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "2-D operands");
+    TORCH_CHECK(slab.numel() >= split_k * M * N, "slab: >= split_k * M * N floats");
+    c10::hip::HIPGuardMasqueradingAsCUDA gd(A.device());
+    const bf16_t *a = ptr<bf16_t>(A), *b = ptr<bf16_t>(B);
+    float* p = ptr<float>(slab);
+    const int lda = (int)A.stride(0), ldb = (int)B.stride(0), m = (int)M, n = (int)N, kk = (int)K, sk = (int)split_k;
+    const int k = slot(A);
+    const int nsplit = minips_k::gemm_slab(a, b, p, m, n, kk, lda, ldb, a_km, b_kn, sk, rec_[k]);
+    hold({A, B, slab});
+    ops_.push_back(
+        [=](const hipStream_t* s) { (void)minips_k::gemm_slab(a, b, p, m, n, kk, lda, ldb, a_km, b_kn, sk, s[k]); });
+    return nsplit;
+  }
+
+  void colsum_bf16(const at::Tensor& x, at::Tensor& out) {
+    c10::hip::HIPGuardMasqueradingAsCUDA gd(x.device());
+    at::Tensor slab;
+    const ColsumLaunch c = prepare_colsum(x, out, slab);
+    const int k = slot(x);
+    c.launch(rec_[k]);
+    hold({x, out, slab});
+    ops_.push_back([c, k](const hipStream_t* s) { c.launch(s[k]); });
+  }
+
+  // stream ``dst`` waits for the work issued so far on stream ``src`` (raw stream handles of the
+  // recording: the list's two streams)
+  void fork(int64_t src, int64_t dst) {
+    const int a = slot_raw(reinterpret_cast<hipStream_t>(src)), b = slot_raw(reinterpret_cast<hipStream_t>(dst));
+    TORCH_CHECK(a != b, "LaunchList.fork: one stream");
+    hipEvent_t ev = nullptr;
+    TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess,
+                "LaunchList: hipEventCreateWithFlags");
+    events_.push_back(ev);
+    auto op = [ev, a, b](const hipStream_t* s) {
+      TORCH_CHECK(hipEventRecord(ev, s[a]) == hipSuccess, "LaunchList: event record");
+      TORCH_CHECK(hipStreamWaitEvent(s[b], ev, 0) == hipSuccess, "LaunchList: stream wait");
+    };
+    op(rec_);
+    ops_.push_back(op);
+  }
+
+  void run(int64_t main, int64_t side) {
+    const hipStream_t s[2] = {reinterpret_cast<hipStream_t>(main), reinterpret_cast<hipStream_t>(side)};
+    for (const auto& op : ops_) op(s);
+  }
+
+  int64_t size() const { return (int64_t)ops_.size(); }
+
+ private:
+  int slot_raw(hipStream_t st) const {
+    for (int i = 0; i < 2; ++i)
+      if (st == rec_[i]) return i;
+    TORCH_CHECK(false, "LaunchList: an op on a stream that is neither the list's compute nor its side stream");
+    return 0;
+  }
+  int slot(const at::Tensor& t) const { return slot_raw(stream_of(t)); }
+  void hold(std::initializer_list<at::Tensor> ts) {
+    for (const auto& t : ts)
+      if (t.defined()) keep_.push_back(t);
+  }
+
+  hipStream_t rec_[2];
+  std::vector<std::function<void(const hipStream_t*)>> ops_;
+  std::vector<at::Tensor> keep_;
+  std::vector<hipEvent_t> events_;
+};
+
 // pos[members[m]] = m: where the dgrad's permuted-rows epilogue puts each lookup's gradient row.
 at::Tensor emb_csr_positions(const at::Tensor& members) {
   check_gpu(members, "members");
@@ -1706,6 +1866,14 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("PS_CTRL_BYTES") = minips_k::kPsCtrlBytes;
   m.attr("PS_CTRL_LINE") = minips_k::kPsCtrlLine;
   m.attr("PS_HELD_SLOTS") = minips_k::kPsHeldSlots;
+  py::class_<LaunchList>(m, "LaunchList")
+      .def(py::init<int64_t, int64_t>())
+      .def("gemm", &LaunchList::gemm)
+      .def("gemm_slab", &LaunchList::gemm_slab)
+      .def("colsum_bf16", &LaunchList::colsum_bf16)
+      .def("fork", &LaunchList::fork)
+      .def("run", &LaunchList::run)
+      .def("size", &LaunchList::size);
   py::class_<FastEvent>(m, "FastEvent")
       .def(py::init<>())
       .def("record", &FastEvent::record)

@@ -133,11 +133,15 @@ class _Fork:
         if st is None:
             return None
         idx = st.device_index
-        ev = sd._event()
-        if sd._fast:
+        rec = ops._REC
+        if rec is not None:  # recorded into a LaunchList: its own event orders the two streams
+            rec.lst.fork(streams.current_raw(idx), sd._raw)
+        elif sd._fast:
+            ev = sd._event()
             ev.record(streams.current_raw(idx))
             ev.wait(sd._raw)
         else:
+            ev = sd._event()
             ev.record(streams.current(idx))
             st.wait_event(ev)
         self.mode = ops.overlap_mode(True)  # forked work: GEMM splits chosen for throughput, not latency
@@ -190,8 +194,11 @@ class SideStream:
 
     def join(self):
         if self.stream is not None:
-            ev = self._event()
             idx = self.stream.device_index
+            if ops._REC is not None:
+                ops._REC.lst.fork(self._raw, streams.current_raw(idx))
+                return
+            ev = self._event()
             if self._fast:
                 ev.record(self._raw)
                 ev.wait(streams.current_raw(idx))
@@ -220,3 +227,36 @@ class SideStream:
             streams.current(idx).wait_event(ev)
         else:  # ops_py FastEvent or streams.FastEvent
             getattr(ev, "ev", ev).wait(streams.current_raw(idx))
+
+
+class Replayer:
+    """Record-once, replay-after launch sequences of a step (ops.recording into a native
+    LaunchList, csrc/bindings/ops_py.cpp). ``replayer(key, fn)``: the first call with ``key`` runs
+    ``fn`` -- GEMM-family ops and SideStream forks only -- recording it; later calls replay the
+    recorded launches on the current and side streams and repeat the slab-sink registrations. The
+    key must name every buffer ``fn`` addresses (a list holds its tensors, so a recorded address
+    is never handed to another buffer while the list lives)."""
+
+    def __init__(self, side: SideStream, cap: int = 8):
+        self.side = side
+        self.cap = cap
+        self._lists: dict = {}
+
+    def __call__(self, key, fn):
+        idx = self.side.stream.device_index
+        main = streams.current_raw(idx)
+        e = self._lists.get(key)
+        if e is None:
+            from .._native import kernels
+
+            if len(self._lists) >= self.cap:
+                self._lists.clear()
+            lst = kernels().LaunchList(main, self.side._raw)
+            with ops.recording(lst) as rec:
+                fn()
+            self._lists[key] = (lst, rec.sink_adds)
+            return
+        lst, adds = e
+        lst.run(main, self.side._raw)
+        for sink, dw, slab, nsplit in adds:
+            sink.add(dw, slab, nsplit)

@@ -25,7 +25,7 @@ from .. import ops
 from ..ps.comm import Comm
 from ..utils import streams
 from ..utils.metrics import phase, traced
-from .layers import SideStream
+from .layers import Replayer, SideStream
 from .feeder import LookaheadPlans
 
 
@@ -107,6 +107,10 @@ _DENSE_ON_SIDE = True
 _W1_LATE = False
 # ROWIDX off: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
 _ROWIDX = True
+# the dense forward and the backward GEMM chain up to the embedding dgrad, recorded once per set of
+# buffers and replayed from a native launch list (layers.Replayer): ~25 binding calls per step
+# leave the host path (MINIPS_LAUNCH_LIST=0: issued op by op)
+_REPLAY = __import__("os").environ.get("MINIPS_LAUNCH_LIST", "1") != "0"
 
 
 def _wgrad(dH, H, Gw, sink=None):
@@ -176,6 +180,7 @@ class WideDeep(LookaheadPlans):
         self.dense.load_full(self._init_dense(dev))
         self._bufs = {}
         self._side = SideStream(dev)
+        self._replay = Replayer(self._side) if self._side.stream is not None else None
 
     def _init_dense(self, dev):
         g = torch.Generator(device="cpu")
@@ -300,7 +305,14 @@ class WideDeep(LookaheadPlans):
         P = self.dense.get()
         scale = 1.0 / (B * self.comm.world)
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
-        self._forward(b, P)
+        sink = self.dense.slab_sink() if hasattr(self.dense, "slab_sink") else None
+        rp = self._replay if (self._replay is not None and _REPLAY and self._wbucket is None
+                              and streams.DELAY_US <= 0 and not torch.cuda.is_current_stream_capturing()) else None
+        key = (B, P.data_ptr(), G.data_ptr(), sink is not None)
+        if rp is not None:
+            rp(("fwd",) + key, lambda: self._forward(b, P))
+        else:
+            self._forward(b, P)
         # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
                     b["dwide"], b["loss"], self.view(G, "b3"), scale)
@@ -314,20 +326,11 @@ class WideDeep(LookaheadPlans):
         # Each fork records an event on the compute stream (~2-4 us queue bubble on MI355X), but
         # fewer, later forks lose more overlap than they save: W3+W2 forked together 0.431-0.438,
         # all three after dgrad1 0.446 vs 0.418-0.421 ms/step (profiles/r3/ab_wd_forks.txt)
-        # one rank: the weight gradients' split-K slices are folded by the dense table's Adam
-        sink = self.dense.slab_sink() if hasattr(self.dense, "slab_sink") else None
-        k3 = self.k_in[2]
-        with side.fork():
-            _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink)
-        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"])
-        with side.fork():
-            ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
-            _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink)
-        ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
-        self._bucket_done(1, side)  # (layers 2, 3 and the head: their weight gradients are issued)
-        if not _W1_LATE:
-            with side.fork():
-                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
+        # one rank: the weight gradients' split-K slices are folded by the dense table's Adam (sink)
+        if rp is not None:
+            rp(("bwd",) + key, lambda: self._backward_chain(b, P, G, sink, side))
+        else:
+            self._backward_chain(b, P, G, sink, side)
         # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
@@ -390,6 +393,22 @@ class WideDeep(LookaheadPlans):
         with phase("wd.advance_plans"):
             self._advance_next_plan()
         return b["loss"]
+
+    def _backward_chain(self, b, P, G, sink, side):
+        """dgrad chain down to dH1 with the three weight gradients (and the layer-2 bias gradient)
+        forked beside it: GEMM-family ops and forks only (replayable, see layers.Replayer)."""
+        k3 = self.k_in[2]
+        with side.fork():
+            _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink)
+        ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"])
+        with side.fork():
+            ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
+            _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink)
+        ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
+        self._bucket_done(1, side)  # (layers 2, 3 and the head: their weight gradients are issued)
+        if not _W1_LATE:
+            with side.fork():
+                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
 
     def _bucket_done(self, layer: int, side):
         """Every layer >= ``layer`` has its weight gradient issued (on the side stream): the buckets

@@ -41,6 +41,28 @@ def _gpu(t: torch.Tensor) -> bool:
 
 # ----------------------------------------------------------------------------- GEMM
 _NO_STRIDES: list = []
+_REC = None  # the active ops.recording, if any
+
+
+class recording:
+    """Inside ``with ops.recording(lst):`` the GEMM-family ops (gemm, linear_fwd / dgrad / wgrad,
+    colsum_add) run through ``lst``, a native LaunchList (csrc/bindings/ops_py.cpp): each launches
+    as usual AND is appended, validated, for ``lst.run()`` to replay with no Python or binding cost.
+    ``sink_adds`` collects the slab-sink registrations the replay must repeat (linear_wgrad defer)."""
+
+    def __init__(self, lst):
+        self.lst = lst
+        self.sink_adds: list = []
+
+    def __enter__(self):
+        global _REC
+        self.prev, _REC = _REC, self
+        return self
+
+    def __exit__(self, *exc):
+        global _REC
+        _REC = self.prev
+        return False
 
 
 def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None, mask=None, colsum=None,
@@ -48,6 +70,10 @@ def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None,
     """C[M,N] (op)= A.B.  A is [M][K] (a_km=False) or [K][M]; B is [N][K] (b_kn=False) or [K][N].
     EPI_PERM_ROWS_BF16: C is [M*N/seg, seg] and output (row, col) goes to row perm[row*N/seg + col//seg]."""
     if _gpu(A):
+        if _REC is not None:
+            _REC.lst.gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k), perm,
+                          int(seg))
+            return C
         # (all positional: pybind's keyword / default-argument path costs ~1 us per call)
         kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k), 1, 1, 0, 0,
                        0, _NO_STRIDES, perm, int(seg))
@@ -99,6 +125,8 @@ def gemm_batched(A, B, C, M, N, K, a_km, b_kn, epi, batch, inner, lda, ldb, ldc,
     """``batch`` GEMMs over flat buffers; operand z starts at (z//inner)*s_outer + (z%inner)*s_inner
     (strides = [sa_o, sa_i, sb_o, sb_i, sc_o, sc_i] in elements), leading dims lda/ldb/ldc."""
     if _gpu(A):
+        if _REC is not None:
+            raise RuntimeError("ops.recording: batched GEMMs are not recordable")
         kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, None, None, float(alpha), 1, int(batch), int(inner),
                        int(lda), int(ldb), int(ldc), [int(x) for x in strides])
         return C
@@ -131,7 +159,7 @@ def linear_fwd(x, w, bias=None, act="relu", out=None):
 def colsum_add(x, out):
     """out[:N] += x.sum(0) in fp32 (x bf16 [M, N]): a Linear's bias gradient from its dy."""
     if _gpu(x):
-        kernels().colsum_bf16(x, out)
+        (kernels() if _REC is None else _REC.lst).colsum_bf16(x, out)
         return out
     out[: x.shape[1]] += x.float().sum(0)
     return out
@@ -191,8 +219,10 @@ def linear_wgrad(dy, x, dw, split_k=None, blocks=None, defer=None):
     if (defer is not None and _gpu(dy) and split_k > 1 and K % 4 == 0 and dw.dim() == 2
             and dw.stride(1) == 1 and dw.stride(0) == K and defer.accepts(dw)):
         slab = defer.slab(dw, split_k)
-        nsplit = kernels().gemm_slab(dy, x, slab, N, K, M, True, True, int(split_k))
+        nsplit = (kernels() if _REC is None else _REC.lst).gemm_slab(dy, x, slab, N, K, M, True, True, int(split_k))
         defer.add(dw, slab, nsplit)
+        if _REC is not None:
+            _REC.sink_adds.append((defer, dw, slab, nsplit))
         return dw
     return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
 

@@ -742,3 +742,51 @@ def test_bf16_rows_stochastic_rounding_is_unbiased(dev):
         ops.sparse_apply_bf16("add", t, None, keys, 0, g, 0.0, scale=1.0, step=s, seed=11)
     mean = float(t.float().mean())
     assert abs(mean - (1.0 + steps * 1e-4)) < 2e-3, mean  # RNE would stay at exactly 1.0
+
+
+def test_launch_list_replays_on_new_data(dev):
+    """A native LaunchList (ops.recording) replays its GEMMs, split-K slab GEMM, column sum and
+    cross-stream fork on the current contents of the recorded buffers: after the inputs change, a
+    replay gives what the op-by-op issue gives (fp32 CPU reference of the same ops)."""
+    from minips_amd.models.layers import SideStream
+    from minips_amd.utils import streams
+
+    g = torch.Generator().manual_seed(9)
+    M, N, K = 512, 256, 192
+    X = _bf(torch.randn(M, K, generator=g)).to(dev)
+    W = _bf(torch.randn(N, K, generator=g) * 0.1).to(dev)
+    H = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    cs = torch.zeros(N, device=dev)
+    dW = torch.zeros(N, K, device=dev)
+    slab = torch.empty(4 * N * K, device=dev)
+    side = SideStream(dev)
+    nsplit = []
+
+    def fn():
+        ops.linear_fwd(X, W, None, "relu", out=H)
+        with side.fork():
+            ops.colsum_add(H, cs)
+            ops.gemm(H, X, dW, N, K, M, True, True, ops.EPI_ATOMIC_F32, split_k=2)
+            nsplit.append((ops._REC.lst if ops._REC is not None else _native.kernels()).gemm_slab(
+                H, X, slab, N, K, M, True, True, 4))
+        side.join()
+
+    lst = _native.kernels().LaunchList(streams.current_raw(0), side._raw)
+    with ops.recording(lst):
+        fn()
+    assert lst.size() >= 6 and nsplit[0] >= 1
+    for _ in range(2):  # new inputs, then a replay
+        X.copy_(_bf(torch.randn(M, K, generator=g)))
+        cs.zero_()
+        dW.zero_()
+        lst.run(streams.current_raw(0), side._raw)
+        torch.cuda.synchronize()
+        Xc, Wc = X.float().cpu(), W.float().cpu()
+        Hr = torch.relu(Xc @ Wc.t())
+        torch.testing.assert_close(H.float().cpu(), Hr, rtol=2e-2, atol=2e-2)
+        Hb = H.float().cpu()
+        torch.testing.assert_close(cs.cpu(), Hb.sum(0), rtol=1e-3, atol=1e-2)
+        ref = Hb.t() @ Xc
+        torch.testing.assert_close(dW.cpu(), ref, rtol=1e-3, atol=5e-2)
+        planes = slab[: nsplit[0] * N * K].view(nsplit[0], N, K).sum(0).cpu()
+        torch.testing.assert_close(planes, ref, rtol=1e-3, atol=5e-2)

@@ -168,3 +168,29 @@ def test_widedeep_wgrad_slabs_folded_by_adam(dev, monkeypatch):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (l0, l1)
     diff = (p0 - p1).abs()
     assert float((diff > 2e-4).float().mean()) < 1e-2
+
+
+@pytest.mark.parametrize("defer", [True, False])
+def test_widedeep_launch_list_replay_bit_identical(dev, monkeypatch, defer):
+    """The dense forward and backward chain replayed from the native launch list (layers.Replayer)
+    train bit-identically to the op-by-op issue, with the split-K planes folded by Adam (defer) and
+    with the list's own persistent reduce planes (no slab sink: the several-rank path)."""
+    import minips_amd.models.widedeep as wd
+    import minips_amd.ps.tables as tables
+    from minips_amd.models.feeder import LookaheadFeeder
+
+    monkeypatch.setattr(tables, "_WGRAD_DEFER", defer)
+    out = {}
+    for replay in (False, True):
+        monkeypatch.setattr(wd, "_REPLAY", replay)
+        comm = Comm(device=torch.device(dev))
+        m = WideDeep(WideDeepConfig(cards=CARDS), comm)
+        feeder = LookaheadFeeder(m, CriteoSynth(4096, cards=CARDS, device=dev, seed=11), comm)
+        losses = [feeder.step().clone() for _ in range(6)]
+        m.drain()
+        torch.cuda.synchronize()
+        if replay:
+            assert len(m._replay._lists) >= 2  # the forward and the backward chain were recorded
+        out[replay] = (torch.stack(losses).cpu(), m.dense.full_master().cpu(), m.emb.shard.cpu().clone())
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)
