@@ -19,10 +19,10 @@ from ..utils.metrics import traced
 
 
 def default_depth(world: int) -> int:
-    # one rank: depth 1 (measured neutral, 1/2/3 within 0.522-0.530 ms/step); several ranks: 2,
-    # so the one host wait of a step (a plan's all-to-all split sizes) lands on counts issued a
-    # whole step earlier (LookaheadFeeder(depth=...) overrides it)
-    return 2 if world > 1 else 1
+    # several ranks: the one host wait of a step (a plan's all-to-all split sizes) lands on counts
+    # issued a whole step earlier; one rank: the planning starts mid-step (plan_wait below), so its
+    # batch is planned two steps ahead (LookaheadFeeder(depth=...) overrides it)
+    return 2
 
 
 class LookaheadFeeder:
@@ -44,13 +44,21 @@ class LookaheadFeeder:
         self.fence = bool(fence and self.cuda)
         if self.fence:
             model._fenced = True
+        # one rank: the look-ahead planning (batch generation, key sort, CSR) waits for the point of
+        # the step where the model issues it (WideDeep: after the dgrad chain), so its ~120 us of
+        # kernels run beside the memory-bound embedding backward instead of squeezing the forward
+        # GEMMs (a 256x256-tile GEMM that loses the 26 CUs of the per-column sort runs a second
+        # round of tiles): W&D 0.351-0.352 vs 0.368 ms/step at depth 2 (profiles/r5/ab_plan_wait.txt).
+        # Several ranks keep it at the step start: the next plan's count exchange then waits less
+        # (emulated 8 ranks: 0.575-0.586 vs 0.500-0.505 ms with the wait)
+        self.plan_wait = self.fence and comm.world == 1
         # batch-ready and fence events: reused from rings (a wait binds to the record before it;
         # each event's wait is issued within depth + 1 steps of its record)
         if self.cuda:
             from ..utils.streams import EventRing
 
             self._evring = EventRing(2 * self.depth + 4, fast=streams.fast_for("plan"))
-            self._fence_ring = EventRing(4, fast=streams.fast_for("plan"))
+            self._fence_ring = EventRing(8, fast=streams.fast_for("plan"))
         self.queue = collections.deque(self._produce() for _ in range(self.depth))
         for (_, k, _), _ev in list(self.queue)[1:]:
             model.prefetch(k, keys_on_plan_stream=self.cuda)
@@ -79,6 +87,10 @@ class LookaheadFeeder:
             self.main.wait_event(ev)
 
         def next_keys():  # called by train_step where it issues the look-ahead planning
+            if self.plan_wait:  # the planning work starts on the GPU at this point of the step
+                ev = self._fence_ring.next()
+                ev.record(self.main)
+                self.plan_stream.wait_event(ev)
             self.queue.append(self._produce())
             return self.queue[-1][0][1]
 

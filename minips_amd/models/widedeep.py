@@ -76,8 +76,11 @@ class WideDeepConfig:
 
 # where train_step issues the next batch's planning (dedupe, CSR, count exchange) and, with a
 # callable next_keys, its generation: "start" | "head" (after the forward) | "dgrad" (after the
-# dgrad chain, beside the memory-bound embedding backward)
-_PLAN_AT = "start"
+# dgrad chain, beside the memory-bound embedding backward) | "push" (after the sparse clock), per
+# world size {1: one rank, 2: several}. One rank: "dgrad" with the feeder's plan wait (the GPU
+# starts the planning there; feeder.LookaheadFeeder.plan_wait); "head" / "push" measured 0.389 /
+# 0.371 vs 0.352 ms/step (profiles/r5/ab_plan_wait.txt)
+_PLAN_AT = {1: "dgrad", 2: "start"}
 # issue an async dense clock from the weight-gradient side stream (see train_step). Measured
 # slower on one MI355X (OVERLAP_W1=dense: 0.525-0.529 -> 0.544-0.549 ms/step: Adam then
 # competes with the memory-bound embedding backward; tools/gpu_round.sh ab), so off by default.
@@ -275,7 +278,7 @@ class WideDeep(LookaheadPlans):
         def issue_next(point):
             # next_keys may be a callable that produces the next batch (on the planning stream)
             # when called: the planning work then starts at _PLAN_AT, not at the step start
-            if next_keys is not None and point == _PLAN_AT:
+            if next_keys is not None and point == _PLAN_AT[min(2, self.comm.world)]:
                 nk = next_keys() if callable(next_keys) else next_keys
                 self.prefetch(nk, keys_on_plan_stream=next_on_plan_stream)
 
@@ -360,6 +363,7 @@ class WideDeep(LookaheadPlans):
         dXe = b["dX"].view(B * F, D) if sorted_rows else b["dX"]
         self.emb.add_lookup_grads(plan, dXe, b["dwide"], F, D, sorted_rows=sorted_rows)  # the table reduces
         self.emb.clock()
+        issue_next("push")
         ph.__exit__(None, None, None)
         ph = phase("wd.dense_clock")
         ph.__enter__()
