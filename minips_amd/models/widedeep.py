@@ -111,9 +111,11 @@ _W1_LATE = False
 # ROWIDX off: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
 _ROWIDX = True
 # the dense forward and the backward GEMM chain up to the embedding dgrad, recorded once per set of
-# buffers and replayed from a native launch list (layers.Replayer): ~25 binding calls per step
-# leave the host path (MINIPS_LAUNCH_LIST=0: issued op by op)
-_REPLAY = __import__("os").environ.get("MINIPS_LAUNCH_LIST", "1") != "0"
+# buffers and replayed from a native launch list (layers.Replayer): ~25 binding calls per step leave
+# the host path -- wd.bwd_dense host 71 -> 53 us at one rank; step time unchanged there (GPU-bound:
+# 0.368-0.370 either way) and at 8 emulated ranks (0.491-0.499 vs 0.488-0.502 ms), where the step
+# waits on the planning's count exchange instead (profiles/r5/host_issue.txt). False: op by op.
+_REPLAY = True
 
 
 def _wgrad(dH, H, Gw, sink=None):

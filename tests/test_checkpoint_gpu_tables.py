@@ -234,3 +234,43 @@ def test_async_checkpoint_is_consistent_while_training(dev, tmp_path, ring):
     assert Checkpointer(comm, str(tmp_path / "ck_"), ring_bytes=ring).load({0: m2.emb, 1: m2.dense}) == 2
     assert torch.equal(m2.emb.shard, ref_emb) and torch.equal(m2.emb.state, ref_state)
     assert torch.equal(m2.dense.master, ref_dense)
+
+
+@pytest.mark.gpu
+def test_checkpoint_without_drain_waits_for_side_stream_adam(dev, tmp_path, monkeypatch):
+    """One rank runs the dense Adam on the weight-gradient side stream and the main stream does not
+    join it (WideDeep dense_side); a checkpoint saved right after a step, without model.drain(),
+    must still hold the state after that Adam (DenseTable.hold -> drain): the Adam is held back
+    10 ms by a spin kernel on the side stream, so a snapshot that did not wait would copy the
+    pre-update master / m / v."""
+    from minips_amd.data.synthetic import CriteoSynth
+    from minips_amd.models.widedeep import WideDeep, WideDeepConfig
+    from minips_amd.ps.checkpoint import Checkpointer
+    from minips_amd.ps.comm import Comm
+    from minips_amd.utils import streams
+
+    comm = Comm(device=dev)
+    cfg = WideDeepConfig(cards=[1000, 50, 20000, 7, 300] + [20] * 21)
+    m = WideDeep(cfg, comm)
+    data = CriteoSynth(1024, cards=cfg.cards, device=dev, seed=2)
+    for _ in range(2):
+        m.train_step(*data.next())
+    idx = torch.device(dev).index or 0
+    orig_clock = m.dense.clock
+
+    def slow_clock():  # (on the side stream: the clock's Adam starts 10 ms late)
+        streams.delay(streams.current_raw(idx), idx)
+        orig_clock()
+
+    monkeypatch.setattr(streams, "DELAY_US", 10000)
+    monkeypatch.setattr(m.dense, "clock", slow_clock)
+    m.train_step(*data.next())
+    monkeypatch.setattr(streams, "DELAY_US", 0)
+    assert m.__dict__.get("_side_pending") is not None  # the Adam was issued on the side stream
+    Checkpointer(comm, str(tmp_path / "ck_")).save({0: m.emb, 1: m.dense}, iteration=3, blocking=True)
+    m.drain()
+    torch.cuda.synchronize()
+    m2 = WideDeep(WideDeepConfig(cards=cfg.cards), comm)
+    assert Checkpointer(comm, str(tmp_path / "ck_")).load({0: m2.emb, 1: m2.dense}) == 3
+    assert torch.equal(m2.dense.master, m.dense.master)
+    assert torch.equal(m2.dense.m, m.dense.m) and torch.equal(m2.dense.v, m.dense.v)
