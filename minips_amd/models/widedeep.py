@@ -354,8 +354,8 @@ class WideDeep(LookaheadPlans):
         # the sparse push, instead of behind them
         pipe = getattr(self.dense, "pipe", None)  # (collective tables only)
         dense_early = _DENSE_CLOCK_ON_SIDE and pipe is not None and pipe.async_ and side.stream is not None
-        if dense_early:
-            with streams.use(side.stream):
+        if dense_early:  # (side.fork: the clock's Adam rewrites W after the embedding dgrad read it)
+            with side.fork():
                 self.dense.add()
                 self.dense.clock()
         issue_next("dgrad")
@@ -383,8 +383,13 @@ class WideDeep(LookaheadPlans):
             # for the weight gradients before its assembly rewrites X and for the Adam (or the
             # one-sided push, which reads and clears the gradient buffer) before its forward reads W
             # and its head writes gradients, so the clock overlaps the next step's input assembly
+            # The Adam rewrites W, which this step's embedding dgrad (issued on the compute stream
+            # after the last weight-gradient fork) still reads: the side stream first waits for the
+            # compute stream (side.fork). Without that edge the Adam could overwrite W1 under the
+            # dgrad when it ran long -- rare, timing-dependent loss divergence at the 4th decimal
+            # (tools/gpu_round.sh; the op-by-op bit-identity test caught it, profiles/r5/race_dgrad_adam.txt)
             ev_x = side.mark()
-            with streams.use(side.stream):
+            with side.fork():
                 self.dense.add()
                 self.dense.clock()
             self._side_pending = (ev_x, side.mark())
