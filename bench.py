@@ -63,6 +63,8 @@ def main():
                          "that rank, every world > 1 code path, collectives replaced by loopback copies of the "
                          "same bytes (ps.comm.LoopbackComm; wire time excluded). Reports per-rank throughput")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--lookahead", type=int, default=0,
+                    help="batches generated + key-planned ahead (0: feeder.default_depth, 2)")
     ap.add_argument("--sync-audit", type=int, default=0,
                     help="after the timed run: N more steps under minips_amd.utils.syncaudit (host issue time, "
                          "host syncs per step and their call sites; one '[sync-audit] {json}' line per rank, stderr)")
@@ -107,7 +109,7 @@ def main():
         main_stream = torch.cuda.Stream(device=dev, priority=compute_priority())
         main_stream.wait_stream(torch.cuda.default_stream(dev))  # model init ran on the default stream
         torch.cuda.set_stream(main_stream)
-    feeder = LookaheadFeeder(model, data, comm)
+    feeder = LookaheadFeeder(model, data, comm, depth=args.lookahead or None)
     step = feeder.step
     loss0 = None
     for i in range(args.warmup):

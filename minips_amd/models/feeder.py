@@ -19,10 +19,12 @@ from ..utils.metrics import traced
 
 
 def default_depth(world: int) -> int:
-    # several ranks: the one host wait of a step (a plan's all-to-all split sizes) lands on counts
-    # issued a whole step earlier; one rank: the planning starts mid-step (plan_wait below), so its
-    # batch is planned two steps ahead (LookaheadFeeder(depth=...) overrides it)
-    return 2
+    # several ranks: 3 -- the one host wait of a step (a plan's all-to-all split sizes) lands on
+    # counts issued two steps earlier: 8 emulated ranks 0.467 vs 0.494-0.502 ms/step at depth 2
+    # (depth 4: 0.467-0.470; profiles/r5/ab_lookahead.txt); one rank: the planning starts mid-step
+    # (plan_wait below), so its batch is planned two steps ahead (3: 0.358 either way).
+    # LookaheadFeeder(depth=...) / bench.py --lookahead override it.
+    return 3 if world > 1 else 2
 
 
 class LookaheadFeeder:
@@ -44,14 +46,14 @@ class LookaheadFeeder:
         self.fence = bool(fence and self.cuda)
         if self.fence:
             model._fenced = True
-        # one rank: the look-ahead planning (batch generation, key sort, CSR) waits for the point of
-        # the step where the model issues it (WideDeep: after the dgrad chain), so its ~120 us of
-        # kernels run beside the memory-bound embedding backward instead of squeezing the forward
-        # GEMMs (a 256x256-tile GEMM that loses the 26 CUs of the per-column sort runs a second
-        # round of tiles): W&D 0.351-0.352 vs 0.368 ms/step at depth 2 (profiles/r5/ab_plan_wait.txt).
-        # Several ranks keep it at the step start: the next plan's count exchange then waits less
-        # (emulated 8 ranks: 0.575-0.586 vs 0.500-0.505 ms with the wait)
-        self.plan_wait = self.fence and comm.world == 1
+        # the look-ahead planning (batch generation, key sort, CSR) waits for the point of the step
+        # where the model issues it (WideDeep: after the dgrad chain), so its ~120 us of kernels run
+        # beside the memory-bound embedding backward instead of squeezing the forward GEMMs (a
+        # 256x256-tile GEMM that loses the 26 CUs of the per-column sort runs a second round of
+        # tiles): one rank 0.351-0.352 vs 0.368 ms/step at depth 2; 8 emulated ranks at depth 3
+        # 0.428-0.433 vs 0.463-0.506 (profiles/r5/ab_plan_wait.txt; at depth 2 the next plan's count
+        # exchange waited instead: 0.575-0.586 vs 0.500-0.505)
+        self.plan_wait = self.fence
         # batch-ready and fence events: reused from rings (a wait binds to the record before it;
         # each event's wait is issued within depth + 1 steps of its record)
         if self.cuda:
