@@ -62,7 +62,8 @@ def spec(U):
         (r"wd_head_kernel", 0, "head Linear 256->1 + BCE fwd/bwd (+ dH3 column sums)", 0, B * H3 * 2 * 2 + B * 12),
         (r"colsum_bf16_kernel", 0, "layer-2 bias gradient (dH2 column sums)", 0, B * H2 * 2),
         (r"zero_rows_dev_kernel", 0, "zero grad rows", 0, U * W * 4),
-        (r"emb_seg_det_kernel", 0, "embedding backward: deterministic segment sums (member-order dX rows)", 0, n * (D * 2 + 8 + 4) + U * W * 4),
+        (r"emb_seg_det_kernel", 0, "embedding backward: deterministic segment sums (member-order dX rows)", 0,
+         n * (D * 2 + 8 + 4) + U * W * 4),
         (r"emb_seg_fix_kernel", 0, "embedding backward: rows cut by piece boundaries (partials)", 0,
          (n // 128) * 2 * (D + 4) * 4 * 2),
         (r"sparse_rowwise_adagrad_v4", 0, "row-wise Adagrad apply (U rows)", 0, U * (W * 4 * 3 + 8 + 8 + 8)),
