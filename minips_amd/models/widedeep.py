@@ -98,7 +98,8 @@ _DENSE_CLOCK_ON_SIDE = False
 # round 5 (layer 1 keeps its bias folded into column k_in of the padded input).
 _K1_ALIGN = 64
 # split-K workgroup target of the three weight gradients (ops.linear_wgrad blocks): W&D 0.402 ms at
-# 320 vs 0.409-0.412 at the default 512 (GPT-2 keeps 512: 12.90 vs 13.18 ms at 256), ab_wd_r3.txt
+# 320 vs 0.409-0.412 at the default 512 (GPT-2 keeps 512: 12.90 vs 13.18 ms at 256), ab_wd_r3.txt;
+# round 5 (planning mid-step): 0.349-0.351 vs 0.357-0.359 at 192, 0.360-0.361 at 512 (ab_wd_r5.txt)
 _WGRAD_BLOCKS = 320
 
 
