@@ -118,6 +118,11 @@ def compute_priority() -> int:
     return 0
 
 
+def _prev_raw(prev) -> int:
+    """Raw handle of the stream saved by streams._get (stream_id, device_index, device_type)."""
+    return torch.cuda.Stream(stream_id=prev[0], device_index=prev[1], device_type=prev[2]).cuda_stream
+
+
 class _Fork:
     """SideStream.fork()'s context: the side stream waits for the current stream, then the block
     runs on the side stream (GEMM splits in overlap mode)."""
@@ -147,8 +152,11 @@ class _Fork:
         self.mode = ops.overlap_mode(True)  # forked work: GEMM splits chosen for throughput, not latency
         self.prev = streams._get(idx)
         streams._set(stream_id=st.stream_id, device_index=idx, device_type=st.device_type)
-        if streams.DELAY_US > 0 and "fork" in streams.DELAY_WHERE:
-            streams.delay(sd._raw, idx)
+        if streams.DELAY_US > 0:
+            if "fork" in streams.DELAY_WHERE:  # the forked work starts late
+                streams.delay(sd._raw, idx)
+            if "main" in streams.DELAY_WHERE:  # the stream forked FROM continues late
+                streams.delay(_prev_raw(self.prev), idx)
         return st
 
     def __exit__(self, *exc):

@@ -386,9 +386,8 @@ class WideDeep(LookaheadPlans):
             # and its head writes gradients, so the clock overlaps the next step's input assembly
             # The Adam rewrites W, which this step's embedding dgrad (issued on the compute stream
             # after the last weight-gradient fork) still reads: the side stream first waits for the
-            # compute stream (side.fork). Without that edge the Adam could overwrite W1 under the
-            # dgrad when it ran long -- rare, timing-dependent loss divergence at the 4th decimal
-            # (tools/gpu_round.sh; the op-by-op bit-identity test caught it, profiles/r5/race_dgrad_adam.txt)
+            # compute stream (side.fork) -- a missing edge by construction. With the edge, repeated
+            # op-by-op runs stopped varying at the 4th decimal (profiles/r5/race_dgrad_adam.txt)
             ev_x = side.mark()
             with side.fork():
                 self.dense.add()

@@ -19,7 +19,10 @@ import torch
 #                      stream reads stale data deterministically instead of by timing luck -- and a
 #                      missing edge no longer hides behind the latency of a system-fence event
 #   where=use+fork     which segments get the spin: "use" (streams.use: planning, clock pipelines, the
-#                      one-sided push stream), "fork" (SideStream.fork: the weight-gradient stream)
+#                      one-sided push stream), "fork" (SideStream.fork: the weight-gradient stream),
+#                      "main" (at every SideStream.fork the stream forked FROM continues late: a side
+#                      stream that writes what the compute stream still reads then runs first -- the
+#                      hazard the other spins hide; tests/test_widedeep_gpu.py stream-delay test)
 #   sysfence=<groups>  the ordering events of these groups ('+'-separated) carry a system-scope fence
 #                      instead of none: side (SideStream fork / join / marks), pipe (table clock
 #                      pipelines), plan (planning-stream hand-offs: feeder, plans), push (the one-sided

@@ -194,3 +194,31 @@ def test_widedeep_launch_list_replay_bit_identical(dev, monkeypatch, defer):
         out[replay] = (torch.stack(losses).cpu(), m.dense.full_master().cpu(), m.emb.shard.cpu().clone())
     for a, b in zip(out[False], out[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("where", ["main", "fork", "use", "use+fork+main"])
+def test_widedeep_one_rank_invariant_under_stream_delays(dev, monkeypatch, where):
+    """Cross-stream ordering check of the one-rank BSP step: 300-us spins injected where streams
+    hand off (MINIPS_STREAM_DEBUG delay modes: the forked side stream late, the compute stream late
+    after each fork, the planning / clock streams late) leave the loss trajectory, the dense master
+    and the embedding shard bit-identical. A consumer that misses its wait on a producer stream then
+    reads data of the wrong step deterministically (the "main" spin exposed the side-stream Adam
+    rewriting W1 under the embedding dgrad, profiles/r5/race_dgrad_adam.txt)."""
+    from minips_amd.models.feeder import LookaheadFeeder
+    from minips_amd.utils import streams
+
+    def run():
+        comm = Comm(device=torch.device(dev))
+        m = WideDeep(WideDeepConfig(cards=CARDS), comm)
+        feeder = LookaheadFeeder(m, CriteoSynth(4096, cards=CARDS, device=dev, seed=11), comm)
+        losses = [feeder.step().clone() for _ in range(6)]
+        m.drain()
+        torch.cuda.synchronize()
+        return torch.stack(losses).cpu(), m.dense.full_master().cpu(), m.emb.shard.cpu().clone()
+
+    ref = run()
+    monkeypatch.setattr(streams, "DELAY_US", 300)
+    monkeypatch.setattr(streams, "DELAY_WHERE", set(where.split("+")))
+    got = run()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b), where
