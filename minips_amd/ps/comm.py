@@ -151,6 +151,12 @@ class Comm:
     def state(self) -> str:
         return "comm" if self._waiting > 0 else "run"
 
+    def _plain(self) -> bool:
+        """A collective can be enqueued bare: RCCL calls return at once (no host wait for the
+        heartbeat's "comm" state to cover) and no timing / tracing wraps it -- the two generator
+        context managers cost ~3-4 us per collective on the step's host path."""
+        return self.backend == "nccl" and self.timing is None and not (_ROCTX_ON or _HOST_ON)
+
     @contextlib.contextmanager
     def _timed(self, kind: str, nbytes: int):
         """Around one collective when ``timing`` is on: its bytes and its time on the issuing
@@ -255,6 +261,9 @@ class Comm:
         if not p2p:
             o = out[: sum(recv_splits)]
             i = inp[: sum(send_splits)]
+            if self._plain():
+                dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
+                return out
             with self.waiting(), self._timed("all_to_all_v", nbytes):
                 dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
             return out
@@ -291,6 +300,8 @@ class Comm:
             with self.waiting():
                 dist.all_to_all_single(r, counts.cpu(), group=self.group)
             recv.copy_(r)
+        elif self._plain():
+            dist.all_to_all_single(recv, counts, group=self.group)
         else:
             with self.waiting():
                 dist.all_to_all_single(recv, counts, group=self.group)
@@ -319,6 +330,9 @@ class Comm:
             out_shard.copy_(inp)
             return out_shard
         self.stats.bytes_rs += inp.numel() * inp.element_size()
+        if self._plain():
+            dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
+            return out_shard
         with self.waiting(), self._timed("reduce_scatter", inp.numel() * inp.element_size()):
             dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
         return out_shard
@@ -340,6 +354,9 @@ class Comm:
         if self.backend == "gloo" and shard.data_ptr() >= out_full.data_ptr() and \
                 shard.data_ptr() < out_full.data_ptr() + out_full.numel() * out_full.element_size():
             shard = shard.clone()  # gloo does not support the in-place (aliased) form
+        if self._plain():
+            dist.all_gather_into_tensor(out_full, shard, group=self.group)
+            return out_full
         with self.waiting(), self._timed("all_gather", out_full.numel() * out_full.element_size()):
             dist.all_gather_into_tensor(out_full, shard, group=self.group)
         return out_full
@@ -426,6 +443,9 @@ class LoopbackComm(Comm):
     def refresh(self):
         self._sb = 0
 
+    def _plain(self) -> bool:  # (the loopback copies stand in for RCCL's bare enqueue)
+        return self.timing is None and not (_ROCTX_ON or _HOST_ON)
+
     def all_to_all_v(self, out, inp, recv_splits, send_splits, p2p: bool = False):
         if list(recv_splits) != list(send_splits):
             raise ValueError("LoopbackComm: an emulated exchange needs symmetric splits")
@@ -434,6 +454,10 @@ class LoopbackComm(Comm):
         n = int(sum(send_splits))
         nbytes = n * inp[:1].numel() * inp.element_size()
         self.stats.bytes_a2a += nbytes
+        if self._plain():
+            if n and out.data_ptr() != inp.data_ptr():
+                out[:n].copy_(inp[:n])
+            return out
         with self._timed("p2p_send_recv" if p2p else "all_to_all_v", nbytes):
             if n and out.data_ptr() != inp.data_ptr():
                 out[:n].copy_(inp[:n])
@@ -452,6 +476,9 @@ class LoopbackComm(Comm):
         self.stats.calls += 1
         self._record("reduce_scatter", inp, inp.numel())
         self.stats.bytes_rs += inp.numel() * inp.element_size()
+        if self._plain():
+            torch.sum(inp.view(self.world, -1), 0, out=out_shard.view(-1))
+            return out_shard
         with self._timed("reduce_scatter", inp.numel() * inp.element_size()):
             torch.sum(inp.view(self.world, -1), 0, out=out_shard.view(-1))
         return out_shard
@@ -460,7 +487,8 @@ class LoopbackComm(Comm):
         self.stats.calls += 1
         self._record("all_gather", out_full, out_full.numel())
         self.stats.bytes_ag += out_full.numel() * out_full.element_size()
-        with self._timed("all_gather", out_full.numel() * out_full.element_size()):
+        with contextlib.nullcontext() if self._plain() else self._timed(
+                "all_gather", out_full.numel() * out_full.element_size()):
             lo, hi = out_full.data_ptr(), out_full.data_ptr() + out_full.numel() * out_full.element_size()
             if lo <= shard.data_ptr() < hi:
                 shard = shard.clone()  # (the in-place form: this rank's slot of out_full)
