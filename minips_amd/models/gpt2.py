@@ -61,7 +61,8 @@ class GPT2Config:
 _WGRAD_DEFER_GPT2 = False
 # the LM-head dgrad (K = the 50304-row vocabulary, only 8192 x 768 outputs): split-K into fp32 slabs
 # + one bf16 reduce; 8 splits measured best (764 vs 906 / 970 us at 4 / 12, profiles/r4/gemm_lm_head_splits.txt;
-# in the round-5 step 13.25-13.28 ms vs 13.29-13.32 / 13.26 / 13.33-13.34 at 4 / 6 / 12, profiles/r5/ab_gpt2_lm_split.txt).
+# in the round-5 step 13.25-13.28 ms vs 13.29-13.32 / 13.26 / 13.33-13.34 at 4 / 6 / 12,
+# profiles/r5/ab_gpt2_lm_split.txt).
 # All three LM-head GEMMs (logits, dgrad, wte wgrad) run on gemm.hip (round 5: the hipBLASLt path is gone)
 _LM_DGRAD_SPLIT = 8
 # MLP: the fc forward saves gelu'(u) (its tanh is computed there anyway) and the fc2 dgrad multiplies
