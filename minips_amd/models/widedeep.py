@@ -79,7 +79,8 @@ class WideDeepConfig:
 # dgrad chain, beside the memory-bound embedding backward) | "push" (after the sparse clock), per
 # world size {1: one rank, 2: several}: "dgrad" with the feeder's plan wait (the GPU starts the
 # planning there; feeder.LookaheadFeeder.plan_wait); one rank "head" / "push" measured 0.389 /
-# 0.371 vs 0.352 ms/step (profiles/r5/ab_plan_wait.txt)
+# 0.371 vs 0.352 ms/step, 8 emulated ranks 0.436-0.452 / 0.437-0.449 vs 0.427-0.441
+# (profiles/r5/ab_plan_wait.txt)
 _PLAN_AT = {1: "dgrad", 2: "dgrad"}
 # issue an async dense clock from the weight-gradient side stream (see train_step). Measured
 # slower on one MI355X (OVERLAP_W1=dense: 0.525-0.529 -> 0.544-0.549 ms/step: Adam then
