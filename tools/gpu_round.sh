@@ -21,7 +21,10 @@
 #     race         the 4-rank SSP one-sided test with the push stream on, once per MINIPS_STREAM_DEBUG variant in
 #                  RACE_VARIANTS (';'-separated; a failing test goes on to the next variant, a crash stops)
 #     pytest       one pytest selection: PYTEST_SEL (e.g. 'tests/test_multirank_gpu.py -k ssp'), env PYTEST_ENV
-# Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, ANCHOR, AB, RUNS, CMD, TAIL, PYTEST_SEL, PYTEST_ENV.
+#     pmc          hardware counters of the W&D step (BENCH_ARGS), one rocprofv3 --pmc pass per counter group
+#                  (8 SQ counters; FETCH_SIZE and WRITE_SIZE each alone -- one run holds at most 4 TCC
+#                  counters), merged per kernel by tools/prof_summary.py pmctable (MATCH: kernel regex)
+# Knobs: STEPS, BENCH_ARGS, PYTEST_ARGS, MODELS, ANCHOR, AB, RUNS, CMD, TAIL, PYTEST_SEL, PYTEST_ENV, MATCH.
 # This one runner replaces the per-experiment command files of rounds 1-4 (git history keeps them).
 set -eo pipefail
 cd "$(dirname "$0")/.."
@@ -121,6 +124,17 @@ if [[ $STAGE == ab ]]; then
       fi
     done
   done
+fi
+if [[ $STAGE == pmc ]]; then
+  prof_env
+  files=()
+  for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES" FETCH_SIZE WRITE_SIZE; do
+    tag=${grp%% *}; d=gpurun_out/pmc_$tag
+    rm -rf $d
+    timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d $d -o run -- python bench.py --steps 6 --warmup 2 ${BENCH_ARGS} > $d.log 2>&1 || { tail -20 $d.log; exit 1; }
+    files+=("$(find $d -name "*counter_collection.csv" | head -1)")
+  done
+  python tools/prof_summary.py pmctable "${files[@]}" --match "${MATCH:-}" | tee gpurun_out/pmc_table.txt
 fi
 if [[ $STAGE == host ]]; then
   timeout -k 10 300 python bench.py --steps 100 --warmup 10 --host-phases 100 ${BENCH_ARGS} > gpurun_out/host_w1.log 2>&1 || { tail -30 gpurun_out/host_w1.log; exit 1; }

@@ -58,6 +58,37 @@ def pmc(paths):
             print(f"    MFMA busy / CU busy            {c['SQ_VALU_MFMA_BUSY_CYCLES'] / c['SQ_BUSY_CU_CYCLES']:.3f}")
 
 
+def pmc_table(paths, match=""):
+    """Per-dispatch averages of every counter, one row per kernel (counter_collection.csv files of
+    separate passes merge by kernel name): waves, VALU / LDS instructions per wave, LDS bank-conflict
+    cycles per LDS instruction, HBM MB fetched / written per dispatch (FETCH_SIZE / WRITE_SIZE, KB)."""
+    import re
+
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(lambda: collections.defaultdict(set))
+    for path in paths:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                k = re.sub(r"void |minips_k::", "", re.sub(r"\(.*", "", row.get("Kernel_Name", "?")))[:56]
+                if match and not re.search(match, k):
+                    continue
+                tot[k][row["Counter_Name"]] += float(row["Counter_Value"])
+                disp[k][row["Counter_Name"]].add(row.get("Dispatch_Id", ""))
+    print(f"{'kernel':56s} {'waves':>8} {'VALU/w':>8} {'LDS/w':>7} {'conf/LDS':>8} {'fetchMB':>8} {'writeMB':>8}")
+    for k in sorted(tot):
+        c, d = tot[k], disp[k]
+
+        def per(name):
+            n = len(d.get(name, ())) or 1
+            return c.get(name, 0.0) / n
+
+        waves = c.get("SQ_WAVES", 0.0)
+        lds = c.get("SQ_INSTS_LDS", 0.0)
+        print(f"{k:56s} {per('SQ_WAVES'):8.0f} {c.get('SQ_INSTS_VALU', 0.0) / max(waves, 1):8.1f} "
+              f"{lds / max(waves, 1):7.1f} {c.get('SQ_LDS_BANK_CONFLICT', 0.0) / max(lds, 1):8.2f} "
+              f"{per('FETCH_SIZE') / 1024:8.1f} {per('WRITE_SIZE') / 1024:8.1f}")
+
+
 def trace(a):
     rows = list(csv.DictReader(open(a.trace)))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Queue_Id", "0"))
@@ -170,7 +201,7 @@ def early(a):
 
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    if argv and argv[0] not in ("stats", "pmc", "trace", "markers", "early", "-h", "--help"):
+    if argv and argv[0] not in ("stats", "pmc", "pmctable", "trace", "markers", "early", "-h", "--help"):
         argv.insert(0, "stats")
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -179,6 +210,9 @@ def main(argv=None):
     p.add_argument("steps", nargs="?", type=int, default=1)
     p.add_argument("--top", type=int, default=25)
     sub.add_parser("pmc").add_argument("paths", nargs="+")
+    pt = sub.add_parser("pmctable")
+    pt.add_argument("paths", nargs="+")
+    pt.add_argument("--match", default="", help="regex on the kernel name")
     p = sub.add_parser("trace")
     p.add_argument("trace")
     p.add_argument("--anchor", default="adam_kernel")
@@ -200,6 +234,8 @@ def main(argv=None):
         stats(a.path, a.steps, a.top)
     elif a.cmd == "pmc":
         pmc(a.paths)
+    elif a.cmd == "pmctable":
+        pmc_table(a.paths, a.match)
     elif a.cmd == "early":
         early(a)
     else:
