@@ -189,7 +189,7 @@ def main():
             "config": {
                 "model": ("PLUMBING TEST (small tables, not the benchmark) " if args.test_cards else "")
                 + "Wide&Deep: 26 sparse (33.76M rows, emb 32 + wide 1, row-wise Adagrad) + 13 dense; "
-                "deep MLP 848-1024-512-256-1 (Adam)",
+                "deep MLP 845-1024-512-256-1 (Adam; layer-1 bias folded, K padded to 896)",
                 "global_batch": args.batch * (1 if emulated else n),
                 "seq_len": None,
                 "parallelism": parallelism,
@@ -198,6 +198,7 @@ def main():
                 "world_size": comm.world,
                 "backend": comm.backend,
                 "bucket_mb": args.bucket_mb if n > 1 else None,
+                "lookahead": feeder.depth,
                 **({k.lower(): os.environ[k] for k in ("NCCL_ALGO", "NCCL_PROTO") if os.environ.get(k)}),
                 **({"emulated_world": n, "emulated_rank": comm.rank} if emulated else {}),
             },
