@@ -213,9 +213,14 @@ class Comm:
     def plan_stream(self):
         """The HIP stream on which lookahead key planning runs (one per rank, shared by tables).
         (A CU-masked planning stream, which kept the latency-bound dedupe kernels off most CUs,
-        measured no better in round 2 and is gone.)"""
+        measured no better in round 2 and is gone.) One rank: a low-priority HIP stream (priority 1,
+        below the default 0 of the compute streams), so the dispatcher favours the step's own
+        workgroups over the look-ahead planning's: W&D 0.358-0.359 vs 0.363-0.365 ms/step. Several
+        ranks keep priority 0: the planning stream also carries the plan's count and key exchanges,
+        which the next step's host waits on (8 emulated ranks 0.477-0.482 vs 0.440-0.444 at low
+        priority; profiles/r5/ab_plan_priority.txt)."""
         if self._plan_stream is None and self.device.type == "cuda":
-            self._plan_stream = dedicated_stream(self.device)
+            self._plan_stream = dedicated_stream(self.device, 1 if self.world == 1 else 0)
         return self._plan_stream
 
     # -- helpers ------------------------------------------------------------------------
