@@ -14,6 +14,7 @@
 #include <thread>
 #include <tuple>
 
+#include "../comm/rccl_comm.h"
 #include "../kernels/kernels.h"
 #include "../kernels/onesided.h"
 
@@ -1556,6 +1557,87 @@ at::Tensor emb_csr_positions(const at::Tensor& members) {
   return pos;
 }
 
+// The rank's native RCCL data plane (csrc/comm/rccl_comm.h) over torch tensors: each call is one
+// enqueue on the tensors' current HIP stream (minips_amd/ps/comm.py Comm uses it for every
+// collective of the step when the backend is RCCL).
+int rccl_dtype(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kChar: case at::kByte: case at::kBool: return minips::RcclComm::kI8;
+    case at::kInt: return minips::RcclComm::kI32;
+    case at::kLong: return minips::RcclComm::kI64;
+    case at::kHalf: return minips::RcclComm::kF16;
+    case at::kBFloat16: return minips::RcclComm::kBF16;
+    case at::kFloat: return minips::RcclComm::kF32;
+    case at::kDouble: return minips::RcclComm::kF64;
+    default: TORCH_CHECK(false, "rccl: dtype ", t.scalar_type());
+  }
+  return 0;
+}
+
+class PyRccl {
+ public:
+  // (id: the 128 raw bytes of the unique id; pybind converts Python bytes to std::string before
+  // the GIL is released around the communicator's rendezvous)
+  PyRccl(const std::string& lib, const std::string& id, int64_t world, int64_t rank, int64_t device, double timeout_s,
+         bool teardown)
+      : c_(lib, id, (int)world, (int)rank, (int)device, timeout_s, teardown) {}
+  // out / inp: row-major [rows, ...] (a row = one element of a 1-D tensor); splits in rows
+  void all_to_all_v(const at::Tensor& out, const at::Tensor& inp, const std::vector<int64_t>& recv,
+                    const std::vector<int64_t>& send) {
+    check_gpu(out, "out");
+    check_gpu(inp, "inp");
+    TORCH_CHECK(out.scalar_type() == inp.scalar_type(), "rccl all_to_all_v: dtypes differ");
+    const int64_t row = inp.dim() > 1 ? inp[0].numel() * inp.element_size() : inp.element_size();
+    int64_t ns = 0, nr = 0;
+    for (int64_t v : send) ns += v;
+    for (int64_t v : recv) nr += v;
+    TORCH_CHECK(ns * row <= inp.numel() * inp.element_size() && nr * row <= out.numel() * out.element_size(),
+                "rccl all_to_all_v: splits exceed the buffers");
+    const hipStream_t s = stream_of(inp);
+    py::gil_scoped_release rel;
+    c_.AllToAllV(inp.data_ptr(), send, out.data_ptr(), recv, row, s);
+  }
+  void all_to_all(const at::Tensor& out, const at::Tensor& inp) {
+    check_gpu(out, "out");
+    check_gpu(inp, "inp");
+    const int64_t nb = inp.numel() * inp.element_size();
+    TORCH_CHECK(nb % c_.world() == 0 && out.numel() * out.element_size() == nb, "rccl all_to_all: equal blocks");
+    const hipStream_t s = stream_of(inp);
+    py::gil_scoped_release rel;
+    c_.AllToAll(inp.data_ptr(), out.data_ptr(), nb / c_.world(), s);
+  }
+  void reduce_scatter(const at::Tensor& out, const at::Tensor& inp) {
+    check_gpu(out, "out");
+    check_gpu(inp, "inp");
+    TORCH_CHECK(inp.numel() == out.numel() * c_.world() && inp.scalar_type() == out.scalar_type(),
+                "rccl reduce_scatter: inp = world x out");
+    const hipStream_t s = stream_of(inp);
+    py::gil_scoped_release rel;
+    c_.ReduceScatter(inp.data_ptr(), out.data_ptr(), out.numel(), rccl_dtype(out), s);
+  }
+  void all_gather(const at::Tensor& out, const at::Tensor& inp) {
+    check_gpu(out, "out");
+    check_gpu(inp, "inp");
+    TORCH_CHECK(out.numel() == inp.numel() * c_.world() && inp.scalar_type() == out.scalar_type(),
+                "rccl all_gather: out = world x inp");
+    const hipStream_t s = stream_of(inp);
+    py::gil_scoped_release rel;
+    c_.AllGather(inp.data_ptr(), out.data_ptr(), inp.numel(), rccl_dtype(inp), s);
+  }
+  void all_reduce(const at::Tensor& t, int64_t op) {
+    check_gpu(t, "t");
+    const hipStream_t s = stream_of(t);
+    py::gil_scoped_release rel;
+    c_.AllReduce(t.data_ptr(), t.data_ptr(), t.numel(), rccl_dtype(t), (int)op, s);
+  }
+  std::string async_error() { return c_.AsyncError(); }
+  void abort(const std::string& why) { c_.Abort(why); }
+  bool aborted() const { return c_.aborted(); }
+
+ private:
+  minips::RcclComm c_;
+};
+
 // The owner side of the asynchronous PS on a GPU rank: minips::AsyncServer (the server thread,
 // csrc/runtime/async_server.h) driving a HipApplier (the optimizer kernels on the owner's own
 // stream). Table buffers are passed as raw device addresses; the Python table keeps them alive
@@ -1603,7 +1685,8 @@ class GpuAsyncServer {
 
   void add_sparse(int64_t t, int64_t opt, int64_t table, int64_t ld, int64_t W, int64_t state, int64_t state2,
                   int64_t D1, int64_t base, double lr, double eps, int64_t cap, int64_t inbox, int64_t slot_bytes,
-                  int64_t depth, int64_t bf16, int64_t seed, int64_t hash_cap, int64_t hkeys, int64_t lock) {
+                  int64_t depth, int64_t bf16, int64_t seed, int64_t hash_cap, int64_t hkeys, int64_t lock, int64_t rs,
+                  bool coalesce) {
     TORCH_CHECK(cap % 2 == 0 && slot_bytes % 256 == 0 && depth >= 1, "sparse inbox layout");
     TORCH_CHECK(slot_bytes >= minips_k::kPsSlotHeader + cap * (8 + 4 * W), "sparse inbox slot too small");
     TORCH_CHECK(opt == minips_k::kPsAdd || opt == minips_k::kPsSgd || opt == minips_k::kPsRowwiseAdagrad,
@@ -1632,13 +1715,18 @@ class GpuAsyncServer {
     d.flush = lock ? reinterpret_cast<uint32_t*>(lock) + 1 : nullptr;
     TORCH_CHECK(!bf16 || (W == 16 || W == 32 || W == 64), "bf16 rows hold 16, 32 or 64 values");
     TORCH_CHECK(hash_cap == 0 || ((hash_cap & (hash_cap - 1)) == 0 && hkeys), "hash capacity: a power of two");
+    d.rs = reinterpret_cast<void*>(rs);
+    TORCH_CHECK(!coalesce || opt != minips_k::kPsRowwiseAdagrad || hash_cap != 0 || rs != 0,
+                "clock-coalesced row-wise Adagrad needs its (stamp, index) table");
+    TORCH_CHECK(W % 4 == 0 && W <= 64 && cap < (int64_t)INT32_MAX, "sparse rows: W % 4 == 0, W <= 64");
     applier_.SetSparse((int)t, d);
+    server_.SetCoalesce((int)t, coalesce);
     server_.Enable((int)t);
   }
 
   void add_dense(int64_t t, int64_t opt, int64_t w, int64_t m, int64_t v, int64_t wb, int64_t n, double lr, double b1,
                  double b2, double eps, double wd, int64_t step, int64_t inbox, int64_t slot_bytes, int64_t depth,
-                 int64_t lock) {
+                 int64_t lock, int64_t sum, int64_t sum_active, bool coalesce) {
     TORCH_CHECK(slot_bytes % 256 == 0 && depth >= 1 && n % 4 == 0, "dense inbox layout");
     TORCH_CHECK(slot_bytes >= minips_k::kPsSlotHeader + 4 * n, "dense inbox slot too small");
     TORCH_CHECK(opt != minips_k::kPsRowwiseAdagrad, "dense optimizer ", opt);
@@ -1661,7 +1749,12 @@ class GpuAsyncServer {
     d.depth = (int)depth;
     d.lock = reinterpret_cast<uint32_t*>(lock);
     d.flush = lock ? reinterpret_cast<uint32_t*>(lock) + 1 : nullptr;
+    d.sum = reinterpret_cast<float*>(sum);
+    d.sum_active = reinterpret_cast<int64_t*>(sum_active);
+    TORCH_CHECK(!coalesce || opt == minips_k::kPsAdd || opt == minips_k::kPsSgd || (sum && sum_active),
+                "clock-coalesced Adam / Adagrad needs the sum buffer");
     applier_.SetDense((int)t, d);
+    server_.SetCoalesce((int)t, coalesce);
     server_.Enable((int)t);
   }
 
@@ -1866,6 +1959,20 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("PS_CTRL_BYTES") = minips_k::kPsCtrlBytes;
   m.attr("PS_CTRL_LINE") = minips_k::kPsCtrlLine;
   m.attr("PS_HELD_SLOTS") = minips_k::kPsHeldSlots;
+  m.def("rccl_unique_id", [](const std::string& lib) { return py::bytes(minips::RcclComm::UniqueId(lib)); });
+  py::class_<PyRccl>(m, "Rccl")
+      .def(py::init<const std::string&, const std::string&, int64_t, int64_t, int64_t, double, bool>(),
+           py::arg("lib"), py::arg("unique_id"), py::arg("world"), py::arg("rank"), py::arg("device"),
+           py::arg("timeout_s") = 60.0, py::arg("teardown") = false, py::call_guard<py::gil_scoped_release>())
+      .def("all_to_all_v", &PyRccl::all_to_all_v)
+      .def("all_to_all", &PyRccl::all_to_all)
+      .def("reduce_scatter", &PyRccl::reduce_scatter)
+      .def("all_gather", &PyRccl::all_gather)
+      .def("all_reduce", &PyRccl::all_reduce)
+      .def("async_error", &PyRccl::async_error)
+      .def("abort", &PyRccl::abort, py::arg("why") = "aborted by the caller",
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("aborted", &PyRccl::aborted);
   py::class_<LaunchList>(m, "LaunchList")
       .def(py::init<int64_t, int64_t>())
       .def("gemm", &LaunchList::gemm)
@@ -1898,13 +2005,20 @@ PYBIND11_MODULE(_kernels, m) {
   py::class_<GpuAsyncServer>(m, "AsyncServer")
       .def(py::init<const std::string&, int64_t, int64_t, int64_t, int64_t>(), py::arg("board"), py::arg("world"),
            py::arg("rank"), py::arg("tables"), py::arg("device"))
-      .def("add_sparse", &GpuAsyncServer::add_sparse)
+      .def("add_sparse", &GpuAsyncServer::add_sparse, py::arg("t"), py::arg("opt"), py::arg("table"), py::arg("ld"),
+           py::arg("W"), py::arg("state"), py::arg("state2"), py::arg("D1"), py::arg("base"), py::arg("lr"),
+           py::arg("eps"), py::arg("cap"), py::arg("inbox"), py::arg("slot_bytes"), py::arg("depth"), py::arg("bf16"),
+           py::arg("seed"), py::arg("hash_cap"), py::arg("hkeys"), py::arg("lock"), py::arg("rs") = 0,
+           py::arg("coalesce") = false)
       .def("set_error_word", &GpuAsyncServer::set_error_word)
       .def("publish_after", &GpuAsyncServer::publish_after)
       .def_property_readonly("published", &GpuAsyncServer::published)
       .def_property_readonly("queued", &GpuAsyncServer::queued)
       .def("publish_error", &GpuAsyncServer::publish_error)
-      .def("add_dense", &GpuAsyncServer::add_dense)
+      .def("add_dense", &GpuAsyncServer::add_dense, py::arg("t"), py::arg("opt"), py::arg("w"), py::arg("m"),
+           py::arg("v"), py::arg("wb"), py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
+           py::arg("wd"), py::arg("step"), py::arg("inbox"), py::arg("slot_bytes"), py::arg("depth"), py::arg("lock"),
+           py::arg("sum") = 0, py::arg("sum_active") = 0, py::arg("coalesce") = false)
       .def("step", &GpuAsyncServer::step)
       .def("set_step", &GpuAsyncServer::set_step)
       .def("start", &GpuAsyncServer::start)

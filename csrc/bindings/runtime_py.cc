@@ -120,6 +120,8 @@ class PyApplier : public Applier {
       throw std::runtime_error(std::string("async server apply: ") + e.what());
     }
   }
+  // a clock-coalesced table: apply(t, -1, c) applies every requester's slot of clock c at once
+  void ApplyClock(int t, int64_t c, int /*world*/) override { Apply(t, -1, c); }
   void Flush() override {}
   // the owner's write lock of the table on the board (the CPU twin of the GPU lock words)
   void BeginTable(int t) override {
@@ -483,6 +485,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def(py::init<const std::string&, int, int, int, py::function>(), py::arg("board"), py::arg("world"),
            py::arg("rank"), py::arg("tables"), py::arg("apply"))
       .def("enable", [](CpuAsyncServer& s, int t) { s.server().Enable(t); })
+      .def("set_coalesce", [](CpuAsyncServer& s, int t, bool on) { s.server().SetCoalesce(t, on); })
       .def("start", [](CpuAsyncServer& s) { s.server().Start(); })
       .def("stop", [](CpuAsyncServer& s) { s.server().Stop(); }, py::call_guard<py::gil_scoped_release>())
       .def("pause", [](CpuAsyncServer& s) { s.server().Pause(); }, py::call_guard<py::gil_scoped_release>())

@@ -19,25 +19,6 @@ namespace minips_k {
 
 namespace {
 
-__device__ __forceinline__ uint32_t sr_hash(uint64_t row, uint32_t col, uint32_t step, uint32_t seed) {
-  uint64_t x = row * 0x9E3779B97F4A7C15ull ^ ((uint64_t)col << 32 | step) ^ ((uint64_t)seed * 0xD1B54A32D192ED03ull);
-  x ^= x >> 31;
-  x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 29;
-  x *= 0x94D049BB133111EBull;
-  x ^= x >> 32;
-  return (uint32_t)x;
-}
-
-__device__ __forceinline__ bf16_t bf16_sr(float v, uint32_t rnd) {
-  const uint32_t b = __float_as_uint(v);
-  if ((b & 0x7f800000u) == 0x7f800000u) return (bf16_t)(b >> 16);  // inf / nan unchanged
-  const uint32_t r = b + (rnd & 0xffffu);
-  // a finite value never rounds up to inf: it saturates at the largest finite bf16 of its sign
-  if ((r & 0x7f800000u) == 0x7f800000u) return (bf16_t)(((b >> 16) & 0x8000u) | 0x7f7fu);
-  return (bf16_t)(r >> 16);
-}
-
 // 8 bf16 per lane (16-byte loads), D/8 lanes per row, rows grid-strided.
 template <typename TO>
 __global__ __launch_bounds__(256) void gather_bf16_rows_kernel(const bf16_t* __restrict__ table, int64_t ld,

@@ -44,6 +44,27 @@ __device__ __forceinline__ float warp_sum(float v) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
+// Stochastic rounding of bf16 rows (csrc/kernels/bf16rows.hip, the one-sided clock apply): a
+// stateless hash of (row, column, apply counter, seed) gives the random bits, so runs reproduce.
+__device__ __forceinline__ uint32_t sr_hash(uint64_t row, uint32_t col, uint32_t step, uint32_t seed) {
+  uint64_t x = row * 0x9E3779B97F4A7C15ull ^ ((uint64_t)col << 32 | step) ^ ((uint64_t)seed * 0xD1B54A32D192ED03ull);
+  x ^= x >> 31;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 29;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 32;
+  return (uint32_t)x;
+}
+
+__device__ __forceinline__ bf16_t bf16_sr(float v, uint32_t rnd) {
+  const uint32_t b = __float_as_uint(v);
+  if ((b & 0x7f800000u) == 0x7f800000u) return (bf16_t)(b >> 16);  // inf / nan unchanged
+  const uint32_t r = b + (rnd & 0xffffu);
+  // a finite value never rounds up to inf: it saturates at the largest finite bf16 of its sign
+  if ((r & 0x7f800000u) == 0x7f800000u) return (bf16_t)(((b >> 16) & 0x8000u) | 0x7f7fu);
+  return (bf16_t)(r >> 16);
+}
+
 // Grid size for grid-stride memory-bound kernels: ~8 blocks/CU on 256 CUs.
 inline int grid_for(int64_t work, int block, int cap = 2048) {
   int64_t g = (work + block - 1) / block;

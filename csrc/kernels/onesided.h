@@ -84,6 +84,7 @@ struct PsSparseDesc {
   unsigned long long* hkeys = nullptr;
   uint32_t* lock = nullptr;     // this owner's lock word of the table (+ its flush counter)
   uint32_t* flush = nullptr;
+  void* rs = nullptr;           // clock-coalesced row-wise Adagrad: int2 [rows_local * P] (stamp, index)
 };
 
 struct PsDenseDesc {
@@ -100,6 +101,8 @@ struct PsDenseDesc {
   int depth = 1;
   uint32_t* lock = nullptr;
   uint32_t* flush = nullptr;
+  float* sum = nullptr;          // clock-coalesced Adam / Adagrad: the clock's summed gradient [n]
+  int64_t* sum_active = nullptr;  //   ... and its number of active pushes (device word)
 };
 
 class HipApplier : public minips::Applier {
@@ -114,6 +117,7 @@ class HipApplier : public minips::Applier {
   void ThreadInit() override;
   void BeginTable(int t) override;
   void Apply(int t, int r, int64_t c) override;
+  void ApplyClock(int t, int64_t c, int world) override;
   void EndTable(int t) override;
   uint64_t Submit() override;
   void Wait(uint64_t ticket) override;
@@ -125,6 +129,7 @@ class HipApplier : public minips::Applier {
     PsSparseDesc sp;
     PsDenseDesc dn;
     std::atomic<int64_t> step{0};  // Adam steps (dense) / applies (bf16 rows: the rounding stream)
+    int64_t stamp = 0;             // clock-coalesced sparse applies issued (the rs table's stamps)
   };
   int dev_;
   hipStream_t stream_ = nullptr;

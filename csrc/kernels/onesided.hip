@@ -576,6 +576,158 @@ void ps_gather_rows(const int64_t* bases, const int64_t* bounds, int P, const in
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------- clock-coalesced owner applies
+// SSP tables with a stateful optimizer (AsyncServer::SetCoalesce): clock c's slots of the P
+// requesters are applied as ONE optimizer step, with the gradient rows of a key summed in
+// requester order -- the BSP update of that clock (tables.py owner_push_adagrad: same per-row
+// arithmetic). Slot r of clock c: inbox + r * stride_r + slot_off.
+//
+// Sparse: a persistent direct-addressed table rs[row * P + r] = {stamp, index in r's slot}
+// (ps_clock_mark: each requester's slot holds a key at most once -- one writer per entry); the
+// apply takes 8 lanes per received row and the group of the LOWEST requester that sent the row
+// sums the <= P contributions and applies the row-wise Adagrad (fp32 rows, or bf16 rows with
+// stochastic rounding). The stamp (an apply counter of the owner, never rewound) retires older
+// entries without clearing the table.
+__global__ void ps_clock_mark_kernel(const char* __restrict__ inbox, int64_t stride_r, int64_t slot_off, int64_t base,
+                                     int P, int2* __restrict__ rs, int stamp) {
+  const int r = blockIdx.y;
+  const char* slot = inbox + r * stride_r + slot_off;
+  const int64_t n = *reinterpret_cast<const int64_t*>(slot);
+  const int64_t* keys = reinterpret_cast<const int64_t*>(slot + kPsSlotHeader);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    rs[(keys[i] - base) * P + r] = make_int2(stamp, (int)i);
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void ps_clock_adagrad_kernel(void* table, int64_t ld, float* state, float* state2,
+                                                               int D1, const char* __restrict__ inbox, int64_t stride_r,
+                                                               int64_t slot_off, int64_t cap, int64_t base, int D,
+                                                               int P, const int2* __restrict__ rs, int stamp, float lr,
+                                                               float eps, uint32_t step, uint32_t seed) {
+  const int me = blockIdx.y;  // the requester whose slot this block walks (wave-uniform)
+  const char* slot = inbox + me * stride_r + slot_off;
+  const int64_t n = *reinterpret_cast<const int64_t*>(slot);
+  const int64_t* keys = reinterpret_cast<const int64_t*>(slot + kPsSlotHeader);
+  const int64_t rows_off = kPsSlotHeader + 8 * cap;
+  const int lane = threadIdx.x & 63, sub = lane >> 3, l = lane & 7;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int c0 = 4 * l, c1 = 32 + 4 * l;
+  const bool has0 = c0 < D, has1 = c1 < D;
+  for (int64_t i0 = wave * 8; i0 < n; i0 += nwaves * 8) {
+    const int64_t i = i0 + sub;
+    const bool in = i < n;
+    const int64_t row = in ? keys[i] - base : 0;
+    const int2* e = rs + row * P;
+    const int2 e0 = in && l < P ? e[l] : make_int2(-1, -1);
+    const int2 e1 = in && l + 8 < P ? e[l + 8] : make_int2(-1, -1);
+    float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (in && has0) {
+      if constexpr (BF16) {
+        const bf16_t* tr = static_cast<const bf16_t*>(table) + row * ld;
+        const uint2 a = *reinterpret_cast<const uint2*>(tr + c0);
+        t[0] = __uint_as_float(a.x << 16); t[1] = __uint_as_float(a.x & 0xffff0000u);
+        t[2] = __uint_as_float(a.y << 16); t[3] = __uint_as_float(a.y & 0xffff0000u);
+        if (has1) {
+          const uint2 b = *reinterpret_cast<const uint2*>(tr + c1);
+          t[4] = __uint_as_float(b.x << 16); t[5] = __uint_as_float(b.x & 0xffff0000u);
+          t[6] = __uint_as_float(b.y << 16); t[7] = __uint_as_float(b.y & 0xffff0000u);
+        }
+      } else {
+        const float* tr = static_cast<const float*>(table) + row * ld;
+        const float4 a = *reinterpret_cast<const float4*>(tr + c0);
+        t[0] = a.x; t[1] = a.y; t[2] = a.z; t[3] = a.w;
+        if (has1) {
+          const float4 b = *reinterpret_cast<const float4*>(tr + c1);
+          t[4] = b.x; t[5] = b.y; t[6] = b.z; t[7] = b.w;
+        }
+      }
+    }
+    const float st_old1 = in ? state[row] : 0.f;
+    const float st_old2 = in && D1 < D ? state2[row] : 0.f;
+    const int sl0 = e0.x == stamp ? e0.y : -1, sl1 = e1.x == stamp ? e1.y : -1;
+    // the leader: no lower requester sent this row in this clock
+    const unsigned long long lower = __ballot(sl0 >= 0 && l < me) | __ballot(sl1 >= 0 && l + 8 < me);
+    const bool ok = in && ((lower >> (sub << 3)) & 0xffull) == 0;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < P; ++s) {
+      const int m = __shfl(s < 8 ? sl0 : sl1, (sub << 3) + (s & 7), 64);
+      if (ok && m >= 0 && has0) {
+        const float* g = reinterpret_cast<const float*>(inbox + s * stride_r + slot_off + rows_off) + (int64_t)m * D;
+        const float4 v = *reinterpret_cast<const float4*>(g + c0);
+        a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
+        if (has1) {
+          const float4 w = *reinterpret_cast<const float4*>(g + c1);
+          a[4] += w.x; a[5] += w.y; a[6] += w.z; a[7] += w.w;
+        }
+      }
+    }
+    float sq1 = 0.f, sq2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (q < 4 ? c0 : c1) + (q & 3);
+      if (c < D1) sq1 += a[q] * a[q];
+      else if (c < D) sq2 += a[q] * a[q];
+    }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+      sq1 += __shfl_xor(sq1, o, 64);
+      sq2 += __shfl_xor(sq2, o, 64);
+    }
+    if (!ok) continue;
+    const float st1 = st_old1 + sq1 / (float)D1;
+    const float st2 = D1 < D ? st_old2 + sq2 / (float)(D - D1) : 0.f;
+    if (l == 0) {
+      state[row] = st1;
+      if (D1 < D) state2[row] = st2;
+    }
+    const float s1 = lr / (sqrtf(st1) + eps), s2 = lr / (sqrtf(st2) + eps);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (q < 4 ? c0 : c1) + (q & 3);
+      t[q] -= (c < D1 ? s1 : s2) * a[q];
+    }
+    if constexpr (BF16) {
+      bf16_t* tr = static_cast<bf16_t*>(table) + row * ld;
+      uint32_t o[4];
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        const int c = (e2 < 2 ? c0 : c1) + 2 * (e2 & 1);
+        const uint32_t rnd = sr_hash((uint64_t)(row + base), (uint32_t)c, step, seed);
+        o[e2] = (uint32_t)bf16_sr(t[2 * e2], rnd) | ((uint32_t)bf16_sr(t[2 * e2 + 1], rnd >> 16) << 16);
+      }
+      if (has0) *reinterpret_cast<uint2*>(tr + c0) = make_uint2(o[0], o[1]);
+      if (has1) *reinterpret_cast<uint2*>(tr + c1) = make_uint2(o[2], o[3]);
+    } else {
+      float* tr = static_cast<float*>(table) + row * ld;
+      if (has0) *reinterpret_cast<float4*>(tr + c0) = make_float4(t[0], t[1], t[2], t[3]);
+      if (has1) *reinterpret_cast<float4*>(tr + c1) = make_float4(t[4], t[5], t[6], t[7]);
+    }
+  }
+}
+
+// Dense: out = sum over requesters (in order) of the active slots' gradients; *active_out = the
+// number of active pushes (the optimizer kernel skips a clock nobody added to).
+__global__ __launch_bounds__(256) void ps_clock_sum_dense_kernel(const char* __restrict__ inbox, int64_t stride_r,
+                                                                 int64_t slot_off, int P, int64_t n4,
+                                                                 float* __restrict__ out,
+                                                                 int64_t* __restrict__ active_out) {
+  uint32_t act = 0;  // requesters whose slot holds a push (bit r)
+  for (int r = 0; r < P; ++r)
+    if (*reinterpret_cast<const int64_t*>(inbox + r * stride_r + slot_off) != 0) act |= 1u << r;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *active_out = __popc(act);
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n4; j += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < P; ++r) {
+      if (!(act >> r & 1u)) continue;
+      const float4 v =
+          reinterpret_cast<const float4*>(inbox + r * stride_r + slot_off + kPsSlotHeader)[j];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[j] = acc;
+  }
+}
+
 // ------------------------------------------------------------------------------ owner-side apply
 HipApplier::HipApplier(int device, int tables) : dev_(device), descs_(tables) {
   for (auto& d : descs_) d.kind = -1;
@@ -689,6 +841,48 @@ void HipApplier::Apply(int t, int r, int64_t c) {
   } else {
     throw std::runtime_error("async server: table " + std::to_string(t) + " has no descriptor");
   }
+}
+
+void HipApplier::ApplyClock(int t, int64_t c, int world) {
+  Desc& d = descs_.at(t);
+  if (d.kind == 0 && d.sp.rs && d.sp.opt == kPsRowwiseAdagrad && d.sp.hash_cap == 0) {
+    const PsSparseDesc& p = d.sp;
+    const int64_t stride = (int64_t)p.depth * p.slot_bytes, off = (c % p.depth) * p.slot_bytes;
+    const int stamp = (int)(++d.stamp);
+    const uint32_t step = p.bf16 ? (uint32_t)d.step.fetch_add(1) : 0u;
+    const int D1 = p.D1 <= 0 || p.D1 > p.W ? p.W : p.D1;
+    dim3 gm((unsigned)std::max<int64_t>(1, std::min<int64_t>((p.cap + 255) / 256, 2048 / world)), (unsigned)world);
+    hipLaunchKernelGGL(ps_clock_mark_kernel, gm, 256, 0, stream_, p.inbox, stride, off, p.base, world,
+                       reinterpret_cast<int2*>(p.rs), stamp);
+    dim3 ga((unsigned)std::max<int64_t>(1, std::min<int64_t>((p.cap * 8 + 255) / 256, 8192 / world)), (unsigned)world);
+    if (p.bf16)
+      hipLaunchKernelGGL(ps_clock_adagrad_kernel<true>, ga, 256, 0, stream_, (void*)p.table, p.ld, p.state, p.state2, D1,
+                         p.inbox, stride, off, p.cap, p.base, p.W, world, reinterpret_cast<const int2*>(p.rs), stamp,
+                         p.lr, p.eps, step, p.seed);
+    else
+      hipLaunchKernelGGL(ps_clock_adagrad_kernel<false>, ga, 256, 0, stream_, (void*)p.table, p.ld, p.state, p.state2,
+                         D1, p.inbox, stride, off, p.cap, p.base, p.W, world, reinterpret_cast<const int2*>(p.rs),
+                         stamp, p.lr, p.eps, step, p.seed);
+    MINIPS_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (d.kind == 1 && d.dn.sum && (d.dn.opt == kPsAdam || d.dn.opt == kPsAdagrad)) {
+    const PsDenseDesc& p = d.dn;
+    const int64_t stride = (int64_t)p.depth * p.slot_bytes, off = (c % p.depth) * p.slot_bytes;
+    hipLaunchKernelGGL(ps_clock_sum_dense_kernel, grid_for(p.n / 4, 256, 4096), 256, 0, stream_, p.inbox, stride, off,
+                       world, p.n / 4, p.sum, p.sum_active);
+    MINIPS_HIP_CHECK(hipGetLastError());
+    if (p.opt == kPsAdam) {
+      // one optimizer step per clock (BSP's count), whatever the number of pushes
+      const int64_t step = d.step.fetch_add(1) + 1;
+      adam_apply(p.w, p.m, p.v, p.sum, p.n, p.lr, p.b1, p.b2, p.eps, p.wd, (int)step, 1.f, p.wb, stream_, nullptr,
+                 false, p.sum_active);
+    } else {
+      adagrad_apply(p.w, p.m, p.sum, p.n, p.lr, p.eps, 1.f, p.wb, stream_, p.sum_active);
+    }
+    return;
+  }
+  Applier::ApplyClock(t, c, world);  // linear rules (add / SGD), Map storage: push by push
 }
 
 void HipApplier::Flush() { MINIPS_HIP_CHECK(hipStreamSynchronize(stream_)); }

@@ -1,5 +1,7 @@
 #include "async_server.h"
 
+#include <algorithm>
+#include <climits>
 #include <exception>
 
 #include "base.h"
@@ -9,9 +11,16 @@ namespace minips {
 
 AsyncServer::AsyncServer(const std::string& board_name, int world, int rank, int tables, Applier* applier)
     : board_(board_name, world, rank, tables), applier_(applier), world_(world), rank_(rank), tables_(tables),
-      enabled_(tables), issued_((size_t)tables * world, 0) {
+      enabled_(tables), coalesce_(tables), issued_((size_t)tables * world, 0) {
   MINIPS_CHECK(applier_ != nullptr, "async server: no applier");
   for (auto& e : enabled_) e.store(false);
+  for (auto& e : coalesce_) e.store(false);
+}
+
+void AsyncServer::SetCoalesce(int table, bool on) {
+  MINIPS_CHECK(table >= 0 && table < tables_, "async server: table " << table);
+  MINIPS_CHECK(!enabled_[table].load(), "async server: SetCoalesce before Enable (table " << table << ")");
+  coalesce_[table].store(on, std::memory_order_release);
 }
 
 AsyncServer::~AsyncServer() { Stop(); }
@@ -134,6 +143,14 @@ void AsyncServer::Loop() {
       todo.clear();
       for (int t = 0; t < tables_; ++t) {
         if (!enabled_[t].load(std::memory_order_acquire)) continue;
+        if (coalesce_[t].load(std::memory_order_relaxed)) {
+          // whole clocks only: every requester sent them (issued_ is the same for every requester)
+          const int64_t a = issued_[(size_t)t * world_];
+          int64_t s = INT64_MAX;
+          for (int r = 0; r < world_; ++r) s = std::min(s, board_.Sent(t, r));
+          if (s > a) todo.push_back({t, -1, a, s});
+          continue;
+        }
         for (int r = 0; r < world_; ++r) {
           const int64_t a = issued_[(size_t)t * world_ + r], s = board_.Sent(t, r);
           if (s > a) todo.push_back({t, r, a, s});
@@ -157,6 +174,13 @@ void AsyncServer::Loop() {
               begun = true;
             }
             any = true;
+            if (w.r < 0) {  // a coalesced clock: every requester's slot in one apply
+              applier_->ApplyClock(t, w.from + k, world_);
+              b.applies += world_;
+              if (log_on)
+                for (int r = 0; r < world_; ++r) b.logged.insert(b.logged.end(), {(int64_t)t, (int64_t)r, w.from + k});
+              continue;
+            }
             applier_->Apply(t, w.r, w.from + k);
             ++b.applies;
             if (log_on) b.logged.insert(b.logged.end(), {(int64_t)t, (int64_t)w.r, w.from + k});
@@ -167,8 +191,10 @@ void AsyncServer::Loop() {
       }
       b.ticket = applier_->Submit();
       for (const Todo& w : todo) {
-        issued_[(size_t)w.t * world_ + w.r] = w.to;
-        b.pub.insert(b.pub.end(), {(int64_t)w.t, (int64_t)w.r, w.to});
+        for (int r = w.r < 0 ? 0 : w.r; r < (w.r < 0 ? world_ : w.r + 1); ++r) {
+          issued_[(size_t)w.t * world_ + r] = w.to;
+          b.pub.insert(b.pub.end(), {(int64_t)w.t, (int64_t)r, w.to});
+        }
       }
       {
         std::lock_guard<std::mutex> lk(mu_);

@@ -46,6 +46,13 @@ class Applier {
   // Issue the apply of requester `r`'s clock `c` of table `t` (inbox slot c % depth); may return
   // before the work completed.
   virtual void Apply(int t, int r, int64_t c) = 0;
+  // Issue ONE apply of clock `c` of table `t` that covers every requester's slot (a table served
+  // clock-coalesced, AsyncServer::SetCoalesce): the rows of the P pushes summed per key in
+  // requester order, one optimizer step per row per clock. The default applies the P pushes one
+  // by one (exact for the linear add / SGD rules).
+  virtual void ApplyClock(int t, int64_t c, int world) {
+    for (int r = 0; r < world; ++r) Apply(t, r, c);
+  }
   // Mark the end of a batch: Wait(ticket) returns once every apply issued before Submit completed
   // and is visible to every rank. The default is synchronous (the work is done when Submit returns).
   virtual uint64_t Submit() {
@@ -65,6 +72,14 @@ class AsyncServer {
   AsyncServer& operator=(const AsyncServer&) = delete;
 
   void Enable(int table);  // serve `table` from now on (its descriptors exist)
+  // Clock-coalesced service of `table` (SSP tables with a stateful optimizer): clock c is applied
+  // once every requester sent it, as one Applier::ApplyClock, and published for all requesters
+  // together. The reference's SSP server applies each Add on arrival as `+=`
+  // (server/consistency/ssp_model.cpp:54-56) -- linear in the pushes, so P pushes of a clock sum
+  // to the BSP update; a row-wise Adagrad / Adam step per push is not (each push would be its own
+  // scale-invariant step: a key every rank pushed moved up to ~2.8x a BSP step at 4 ranks). Set
+  // before Enable.
+  void SetCoalesce(int table, bool on);
   void Start();
   void Stop();
   // Pause: returns once no apply is in flight and none will start until Resume() (a consistent
@@ -93,7 +108,7 @@ class AsyncServer {
   PSBoard board_;
   Applier* applier_;
   const int world_, rank_, tables_;
-  std::vector<std::atomic<bool>> enabled_;
+  std::vector<std::atomic<bool>> enabled_, coalesce_;
   std::thread th_;
   std::atomic<bool> stop_{false}, running_{false};
   std::atomic<int64_t> applies_{0}, batches_{0};

@@ -151,6 +151,19 @@ class Comm:
     def state(self) -> str:
         return "comm" if self._waiting > 0 else "run"
 
+    def _bare(self, fn, *args, **kw):
+        """A collective enqueued bare (_plain): no generator context managers, but still counted as
+        a possible host wait -- an enqueue can block (the first collective of a communicator sets
+        it up; a full proxy queue), and a rank blocked there on a stuck peer must report "comm"."""
+        wl = self._wlock
+        with wl:
+            self._waiting += 1
+        try:
+            return fn(*args, **kw)
+        finally:
+            with wl:
+                self._waiting -= 1
+
     def _plain(self) -> bool:
         """A collective can be enqueued bare: RCCL calls return at once (no host wait for the
         heartbeat's "comm" state to cover) and no timing / tracing wraps it -- the two generator
@@ -267,7 +280,7 @@ class Comm:
             o = out[: sum(recv_splits)]
             i = inp[: sum(send_splits)]
             if self._plain():
-                dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
+                self._bare(dist.all_to_all_single, o, i, recv_splits, send_splits, group=self.group)
                 return out
             with self.waiting(), self._timed("all_to_all_v", nbytes):
                 dist.all_to_all_single(o, i, recv_splits, send_splits, group=self.group)
@@ -306,7 +319,7 @@ class Comm:
                 dist.all_to_all_single(r, counts.cpu(), group=self.group)
             recv.copy_(r)
         elif self._plain():
-            dist.all_to_all_single(recv, counts, group=self.group)
+            self._bare(dist.all_to_all_single, recv, counts, group=self.group)
         else:
             with self.waiting():
                 dist.all_to_all_single(recv, counts, group=self.group)
@@ -336,7 +349,7 @@ class Comm:
             return out_shard
         self.stats.bytes_rs += inp.numel() * inp.element_size()
         if self._plain():
-            dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
+            self._bare(dist.reduce_scatter_tensor, out_shard, inp, group=self.group)
             return out_shard
         with self.waiting(), self._timed("reduce_scatter", inp.numel() * inp.element_size()):
             dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
@@ -360,7 +373,7 @@ class Comm:
                 shard.data_ptr() < out_full.data_ptr() + out_full.numel() * out_full.element_size():
             shard = shard.clone()  # gloo does not support the in-place (aliased) form
         if self._plain():
-            dist.all_gather_into_tensor(out_full, shard, group=self.group)
+            self._bare(dist.all_gather_into_tensor, out_full, shard, group=self.group)
             return out_full
         with self.waiting(), self._timed("all_gather", out_full.numel() * out_full.element_size()):
             dist.all_gather_into_tensor(out_full, shard, group=self.group)

@@ -20,6 +20,13 @@ wait for a peer's pushes. These tables do the same with no collective on the dat
   optimizer and the OWNER's state (row-wise Adagrad, Adam, Adagrad, SGD or the reference's plain
   add; csrc/kernels/onesided.hip HipApplier) on its own high-priority stream, and publishes
   ``applied``;
+* SSP tables with a stateful optimizer (row-wise Adagrad, Adam, Adagrad) are served
+  clock-coalesced (AsyncServer::SetCoalesce): the owner applies clock c once every requester
+  sent it, as ONE optimizer step over the P pushes summed per key in requester order -- the BSP
+  update of that clock. The reference's SSP server applies each Add on arrival as ``+=``
+  (ssp_model.cpp:54-56), which is linear in the pushes; one scale-invariant Adagrad / Adam step
+  per push is not (a key pushed by all 4 ranks moved up to ~2.8x a BSP step: the round-5 4-rank
+  loss spike, profiles/r5/ssp_probe.txt). ASP keeps the per-arrival apply (asp_model.cpp:18-21);
 * SSP gate (a Get at own clock c): every owner has applied every requester's clocks < c - s,
   i.e. min applied >= c - s (csrc/runtime/ps_board.h); ASP never waits (``asp_bound`` optionally
   bounds it the same way); a requester reuses an inbox slot only after every owner applied it;
@@ -66,6 +73,10 @@ _SHARD_MEM = 0
 # copy of the slot from `depth` clocks ago); PS_INBOX_MEM off is an A/B timing knob only
 _INBOX_MEM = 2
 _PUSH_STREAM = os.environ.get("MINIPS_PS_PUSH_STREAM", "0") == "1"
+# clock-coalesced SSP applies need a (stamp, index) entry per owned row and requester: 8 * P bytes
+# per row (W&D at 8 ranks: 34 MB per rank); above this many bytes a table falls back to applying
+# push by push (the 10B-row DLRM table would need 80 GB per rank at 8 ranks -- it runs ASP)
+_COALESCE_MAX_BYTES = 32 << 30
 # PS_LOCKS off: no owner locks (A/B timing only: reads may see half of a batch)
 _LOCKS = True
 
@@ -148,7 +159,10 @@ class AsyncPS:
         return t
 
     def _apply_cpu(self, t: int, r: int, c: int):
-        self.tables[t]._apply_slot_cpu(r, c)
+        if r < 0:  # a clock-coalesced table: every requester's slot of clock c in one apply
+            self.tables[t]._apply_clock_cpu(c)
+        else:
+            self.tables[t]._apply_slot_cpu(r, c)
 
     def check(self):
         err = self.server.error()
@@ -460,6 +474,12 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         self.state = torch.zeros(self.rows_local, dtype=torch.float32, device=dev) \
             if optimizer == "rowwise_adagrad" else None
         self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
+        # SSP + row-wise Adagrad: one Adagrad step per row per clock over every requester's push
+        # (module docstring); the owner's direct-addressed (stamp, index) table of that apply
+        self.coalesced = (consistency == "ssp" and optimizer == "rowwise_adagrad"
+                          and 8 * P * self.rows_local <= _COALESCE_MAX_BYTES)
+        self._rs = torch.zeros(2 * P * self.rows_local, dtype=torch.int32, device=dev) \
+            if self.coalesced and self.cuda else None
         self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=_INBOX_MEM)
         self._register_server()
         self._finish_init()
@@ -475,9 +495,12 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
                                       self.state2.data_ptr() if self.state2 is not None else 0, D1, self.base,
                                       float(self.lr), float(self.eps), self.cap, self._inbox[me].data_ptr(),
                                       self.slot_bytes, self.depth, int(self.value_dtype == torch.bfloat16),
-                                      self.seed & 0xFFFFFFFF, int(hash_cap), int(hkeys), self.ps.own_lock(self.t))
+                                      self.seed & 0xFFFFFFFF, int(hash_cap), int(hkeys), self.ps.own_lock(self.t),
+                                      rs=self._rs.data_ptr() if getattr(self, "_rs", None) is not None else 0,
+                                      coalesce=bool(getattr(self, "coalesced", False)))
             torch.cuda.synchronize(dev)  # shard init + state zeroing done before any peer reads
         else:
+            self.ps.server.set_coalesce(self.t, bool(getattr(self, "coalesced", False)))
             self.ps.server.enable(self.t)
 
     # -- planning: SparseTable's dedupe + owner grouping, no count exchange ----------------------
@@ -511,9 +534,7 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             pp = self._start_plan(keys, csr, exchange=False)
             ring = self.__dict__.get("_plan_evs")
             if ring is None:
-                # (with the push stream the plan's keys / counts are read there, after a hand-off
-                # through the compute stream: those need the system-fence form, measured --
-                # profiles/r4/ab_push_stream.txt)
+                # (same-device ordering: fence-free unless MINIPS_STREAM_DEBUG sysfence=plan)
                 ring = self._plan_evs = streams.EventRing(16, fast=streams.fast_for("plan"))
             pp.event = ring.next()
             pp.event.record(ps)
@@ -576,10 +597,11 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
             # stream's work so far; nothing later on the compute stream depends on it (reads are
             # gated by the board), so the step's remaining backward runs beside the copy into the
             # inboxes: W&D SSP 0.396-0.403 vs 0.402-0.404, DLRM-10B 0.681-0.683 vs 0.692-0.694 ms
-            # (profiles/r4/ab_push_stream.txt). Opt-in (MINIPS_PS_PUSH_STREAM=1): the 4-rank SSP test on
-            # one GPU (tests/test_multirank_gpu.py::test_widedeep_ssp_world4_tracks_one_rank_bsp)
-            # saw a loss spike with it on unless the planning stream's hand-off events (feeder and
-            # plan) carry a system fence too (FAST_PLAN_EVENTS off): use the two together
+            # (profiles/r4/ab_push_stream.txt). Opt-in (MINIPS_PS_PUSH_STREAM=1). The hand-off events
+            # are same-device stream orderings and fence-free (streams.fast_for): the 4-rank SSP loss
+            # spike once blamed on them showed with every event system-fenced and with the push
+            # stream off too -- it was the per-push optimizer step, fixed by the clock-coalesced SSP
+            # apply (profiles/r5/ssp_probe.txt)
             pst = self._push_stream() if _PUSH_STREAM else None
             if pst is not None:
                 ev = self._push_evs.next()
@@ -606,9 +628,10 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         st = self.__dict__.get("_pst")
         if st is None:
             st = self._pst = self.comm.new_stream()
-            # system-fence events: with fence-free ones the push read stale gradient rows (the 4-rank
-            # SSP GPU test's loss spike; profiles/r4/ab_push_stream.txt) -- the compute stream's
-            # writes must be written back before the push's IPC-path loads
+            # fence-free by default (streams.fast_for("push"); MINIPS_STREAM_DEBUG sysfence=push
+            # fences them): the push reads the gradient rows on the same device, which the stream
+            # order alone makes visible; its IPC stores into peers' inboxes are released by the
+            # publish event's system-scope completion (onesided.hip header)
             self._push_evs = streams.EventRing(8, fast=streams.fast_for("push"))
         return st
 
@@ -659,6 +682,27 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         g = buf[off + _SLOT_HEADER + 8 * cap: off + _SLOT_HEADER + 8 * cap + 4 * W * n].view(torch.float32)
         g = g.view(n, W).clone()
         self._apply_rows(keys, g)
+
+    def _apply_clock_cpu(self, c: int):
+        """Clock-coalesced apply (CPU twin of ps_clock_adagrad): every requester's rows of clock
+        c summed per key in requester order, one optimizer step per row."""
+        W, cap = self.width, self.cap
+        buf = self._inbox[self.comm.rank]
+        keys, rows = [], []
+        for r in range(self.comm.world):
+            off = (r * self.depth + c % self.depth) * self.slot_bytes
+            n = int(buf[off: off + 8].view(torch.int64)[0])
+            if n:
+                keys.append(buf[off + _SLOT_HEADER: off + _SLOT_HEADER + 8 * n].view(torch.int64).clone())
+                g = buf[off + _SLOT_HEADER + 8 * cap: off + _SLOT_HEADER + 8 * cap + 4 * W * n].view(torch.float32)
+                rows.append(g.view(n, W).clone())
+        if not keys:
+            return
+        allk = torch.cat(keys)
+        uniq, inv = torch.unique(allk, return_inverse=True)
+        g = torch.zeros(uniq.numel(), W, dtype=torch.float32)
+        g.index_add_(0, inv, torch.cat(rows))  # sequential on the CPU: requester order per key
+        self._apply_rows(uniq, g)
 
     def _apply_rows(self, keys, g):
         if self.value_dtype == torch.bfloat16:
@@ -766,6 +810,7 @@ class AsyncHashTable(AsyncSparseTable):
         self.shard = self._views[me]
         self.state = torch.zeros(cap, dtype=torch.float32, device=dev) if optimizer == "rowwise_adagrad" else None
         self.state2 = None
+        self.coalesced, self._rs = False, None  # (Map storage applies push by push)
         self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=_INBOX_MEM)
         self._neg = None
         if self.cuda:
@@ -881,13 +926,15 @@ class AsyncDenseTable(_AsyncTable):
     """A flat dense parameter vector (equal shards, like ps.tables.DenseTable) on the one-sided
     path: Get pulls every owner's shard whose version changed since the last pull (bf16 copies
     the owner's apply writes), Add + Clock pushes each owner's slice of the gradient into its
-    inbox, and the owner applies Adam / Adagrad / SGD / add with its own m / v state -- one
-    optimizer step per push, as an asynchronous PS server does (each Add is applied on arrival).
-    Every rank pushes the whole gradient every clock, so one clock is P pushes: the scale-invariant
-    optimizers (Adam, Adagrad: a step moves ~lr whatever the gradient's size) take lr / P per push
-    (``push_lr``), so one clock of the job moves the parameters about as far as one BSP step --
-    with lr per push the 4-rank SSP W&D run moved them 4x as far and spiked (tools/ssp_probe.py,
-    profiles/r5/ssp_probe.txt). SGD / add are linear: the P pushes sum to the BSP step at lr.
+    inbox, and the owner applies Adam / Adagrad / SGD / add with its own m / v state.
+    SSP (Adam / Adagrad): clock-coalesced -- the owner sums the P pushes of a clock (requester
+    order) and takes ONE optimizer step at lr, one Adam step count per clock: BSP's update.
+    ASP: one optimizer step per push, as an asynchronous PS server does (each Add applied on
+    arrival); every rank pushes the whole gradient every clock, so one clock is P pushes and the
+    scale-invariant optimizers (a step moves ~lr whatever the gradient's size) take lr / P per
+    push (``push_lr``) -- with lr per push a 4-rank run moved the weights 4x as far and spiked
+    (tools/ssp_probe.py, profiles/r5/ssp_probe.txt). SGD / add are linear: the P pushes sum to the
+    BSP step at lr either way.
     Same API as DenseTable (grad written in place by the models, get / add / clock / load_full /
     full_master)."""
 
@@ -903,7 +950,8 @@ class AsyncDenseTable(_AsyncTable):
         P, me, dev = comm.world, comm.rank, comm.device
         self.table_id, self.n_params = table_id, n_params
         self.optimizer, self.lr = optimizer, lr
-        self.push_lr = lr / P if optimizer in ("adam", "adagrad") else lr
+        self.coalesced = consistency == "ssp" and optimizer in ("adam", "adagrad")
+        self.push_lr = lr / P if optimizer in ("adam", "adagrad") and not self.coalesced else lr
         self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
         self.pull_dtype = pull_dtype
         self.value_dtype = torch.float32
@@ -937,14 +985,21 @@ class AsyncDenseTable(_AsyncTable):
             self._inbox_ptrs = torch.tensor([b.data_ptr() for b in self._inbox], dtype=torch.int64, device=dev)
             self._pull_ptrs = torch.tensor([b.data_ptr() for b in self._pulls], dtype=torch.int64, device=dev)
             self._slot_views = [b for b in self._inbox]
+            # the coalesced apply's summed gradient and its active-push count
+            self._sum = torch.zeros(self.shard, dtype=torch.float32, device=dev) if self.coalesced else None
+            self._sum_active = torch.zeros(1, dtype=torch.int64, device=dev) if self.coalesced else None
             self.ps.server.add_dense(self.t, _OPT_CODES[optimizer], self.master.data_ptr(),
                                      self.m.data_ptr() if self.m is not None else 0,
                                      self.v.data_ptr() if self.v is not None else 0,
                                      self._pulls[me].data_ptr() if self._pull_bf16 else 0, self.shard,
                                      float(self.push_lr),
                                      float(betas[0]), float(betas[1]), float(eps), float(weight_decay), 0,
-                                     self._inbox[me].data_ptr(), self.slot_bytes, self.depth, self.ps.own_lock(self.t))
+                                     self._inbox[me].data_ptr(), self.slot_bytes, self.depth, self.ps.own_lock(self.t),
+                                     sum=self._sum.data_ptr() if self.coalesced else 0,
+                                     sum_active=self._sum_active.data_ptr() if self.coalesced else 0,
+                                     coalesce=self.coalesced)
         else:
+            self.ps.server.set_coalesce(self.t, self.coalesced)
             self.ps.server.enable(self.t)
         self._finish_init()
 
@@ -1081,6 +1136,26 @@ class AsyncDenseTable(_AsyncTable):
         else:
             self.master.add_(g)
 
+    def _apply_clock_cpu(self, c: int):
+        """Clock-coalesced apply (CPU twin of ps_clock_sum_dense + the optimizer): the active pushes
+        of clock c summed in requester order, one optimizer step at lr."""
+        buf = self._inbox[self.comm.rank]
+        if self.optimizer == "adam":
+            self.cpu_step += 1  # one optimizer step per clock (BSP's count)
+        g, active = torch.zeros(self.shard, dtype=torch.float32), 0
+        for r in range(self.comm.world):
+            off = (r * self.depth + c % self.depth) * self.slot_bytes
+            if int(buf[off: off + 8].view(torch.int64)[0]) != 0:
+                g += buf[off + _SLOT_HEADER: off + _SLOT_HEADER + 4 * self.shard].view(torch.float32)
+                active += 1
+        if not active:
+            return
+        if self.optimizer == "adam":
+            ops.adam_apply(self.master, self.m, self.v, g, self.lr, self.betas[0], self.betas[1], self.eps,
+                           self.weight_decay, self.cpu_step, 1.0, None)
+        else:
+            ops.adagrad_apply(self.master, self.m, g, self.lr, self.eps, 1.0, None)
+
     # -- checkpoint hooks ------------------------------------------------------------------------
     def shard_state(self):
         self.drain()
@@ -1105,7 +1180,8 @@ class AsyncDenseTable(_AsyncTable):
     def finish_restore(self, clock: int):
         if self._pull_bf16:
             self._pulls[self.comm.rank].copy_(self.master.to(torch.bfloat16))
-        steps = int(clock) * self.comm.world  # one optimizer step per push of every requester
+        # one optimizer step per clock (coalesced) or per push of every requester
+        steps = int(clock) * (1 if self.coalesced else self.comm.world)
         if self.cuda:
             self.ps.server.set_step(self.t, steps)
             torch.cuda.synchronize(self.comm.device)

@@ -814,14 +814,18 @@ class SparseTable:
         self.bounds = torch.tensor(b, dtype=torch.int64, device=dev)
         self.base = b[comm.rank]
         self.rows_local = b[comm.rank + 1] - b[comm.rank]
+        # LoopbackComm re-bases the keys this rank asks of owner s to offset (key - bounds[s]) of its
+        # own range (_finish_plan); the last owner's range is up to P - 1 rows longer than the
+        # others', so an emulated shard carries that many spare rows (offsets stay collision-free)
+        self._rows_alloc = self.rows_local + (num_rows % comm.world if comm.emulated else 0)
         g = torch.Generator(device=dev)
         g.manual_seed(seed + 7919 * comm.rank)
-        self.shard = torch.empty(self.rows_local, width, dtype=value_dtype, device=dev)
+        self.shard = torch.empty(self._rows_alloc, width, dtype=value_dtype, device=dev)
         if init_std > 0:
             self.shard.normal_(0.0, init_std, generator=g)
         else:
             self.shard.zero_()
-        self.state = torch.zeros(self.rows_local, dtype=torch.float32, device=dev) \
+        self.state = torch.zeros(self._rows_alloc, dtype=torch.float32, device=dev) \
             if optimizer == "rowwise_adagrad" else None
         self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
         self._init_comm(consistency, staleness, p2p)
@@ -1019,8 +1023,13 @@ class SparseTable:
         comm.all_to_all_v(recv_keys, pp.uniq, recv, send, p2p=self.p2p)
         if comm.emulated and M and type(self)._route_keys is SparseTable._route_keys:
             # LoopbackComm: the keys came back as this rank's own requests to every owner; re-base
-            # them into its own row range, as the peers' requests to this owner would be
-            recv_keys.remainder_(self.rows_local).add_(self.base)
+            # them into its own row range, as the peers' requests to this owner would be: offset
+            # key - bounds[s] within owner s's range (s = min(key // step, P - 1)), so distinct keys
+            # of one requester segment stay distinct (the direct owner apply has one writer per
+            # (row, requester) entry) -- the shard has the last range's spare rows (_rows_alloc)
+            step = self.bounds_list[1]
+            q = torch.div(recv_keys, step, rounding_mode="floor").clamp_(max=comm.world - 1)
+            recv_keys.sub_(q.mul_(step)).add_(self.base)
         p = SparsePlan(n, pp.inv, pp.uniq, U, send, recv, recv_keys, csr=pp.csr, _U=U)
         if M > 0 and self._owner_direct_ok():
             p.extra["direct"] = True  # the push applies by direct addressing: no owner-side plan
@@ -1029,10 +1038,10 @@ class SparseTable:
             # lie in this rank's own row range, a bounded space -> the bitmap planner when its map
             # is small per key (W&D at 8 ranks: 4.2M local rows for ~10^5-10^6 requested keys)
             if (_BITMAP_PLAN and recv_keys.is_cuda and type(self)._route_keys is SparseTable._route_keys
-                    and 0 < self.rows_local // 8 <= _BITMAP_RATIO * M):
+                    and 0 < self._rows_alloc // 8 <= _BITMAP_RATIO * M):
                 if getattr(self, "_own_local_bounds", None) is None:
-                    self._own_local_bounds = torch.tensor([0, self.rows_local], dtype=torch.int64, device=dev)
-                ou, oi, _, oU = ops.bitmap_plan(recv_keys - self.base, self._own_local_bounds, self.rows_local,
+                    self._own_local_bounds = torch.tensor([0, self._rows_alloc], dtype=torch.int64, device=dev)
+                ou, oi, _, oU = ops.bitmap_plan(recv_keys - self.base, self._own_local_bounds, self._rows_alloc,
                                                 oor=self._oor_counter())
                 ou = ou + self.base
             else:
@@ -1227,7 +1236,7 @@ class SparseTable:
             if plan.extra.get("direct"):  # stamp + sum + row-wise Adagrad, no owner-side plan
                 rs = self.__dict__.get("_rs")
                 if rs is None and dev.type == "cuda":
-                    rs = self._rs = torch.full((self.rows_local * self.comm.world * 2,), -1, dtype=torch.int32,
+                    rs = self._rs = torch.full((self._rows_alloc * self.comm.world * 2,), -1, dtype=torch.int32,
                                                device=dev)
                 self._stamp = self.__dict__.get("_stamp", -1) + 1
                 ops.owner_push_adagrad(self.shard, self.state, plan.recv_keys, self.base, recv, plan.recv, rs,

@@ -226,21 +226,19 @@ def test_widedeep_bsp_world_matches_one_rank(world, wd_one_rank):
 
 @pytest.mark.parametrize("fn", [_wd_ssp_coll, _wd_ssp_onesided], ids=["collective", "onesided"])
 def test_widedeep_ssp_world4_tracks_one_rank_bsp(fn, wd_one_rank):
-    """SSP(1) at 4 ranks tracks the one-rank BSP run. The one-sided owners apply each requester's
-    push on arrival (the reference's SSP server) as its own row-wise Adagrad step, and Adagrad's
-    first step is scale-invariant: a key all 4 ranks pushed at clock 0 moves up to ~2.8x as far as
-    in one BSP step. Whether step 1 or 2 reads those applies is timing (SSP(1) lets step 1 read
-    before them; the push stream lands them sooner), so those two steps may spike -- a transient of
-    the first clock, not a race: it shows with every ordering event system-fenced and with the push
-    stream off too, and never with the collective sparse table (tools/ssp_probe.py,
-    profiles/r5/ssp_probe.txt). Steps 3.. are compared; no step may leave 2x the reference."""
+    """SSP(1) at 4 ranks tracks the one-rank BSP run at EVERY step. The one-sided owners serve SSP
+    clock-coalesced (one row-wise Adagrad / Adam step per row per clock over the summed pushes,
+    ps/onesided.py): with an optimizer step per push, a key all 4 ranks pushed at clock 0 moved up
+    to ~2.8x a BSP step and step 1 spiked to loss ~1.03 in every run (profiles/r5/ssp_probe.txt).
+    Bound: each step within 0.1 of the reference (tools/ssp_probe.py's spike threshold: SSP(1)
+    reads may miss the previous clock), the mean over all steps within 5 %."""
     out = run_world(fn, world=4)
     ref = wd_one_rank
     for r, (losses, st) in out.items():
         assert st <= 1, (r, st)  # the SSP(1) read bound held on every rank
         assert all(l == l for l in losses), losses
-        assert all(l < 2.0 * max(ref) for l in losses), (r, losses, ref)
-        a, b = sum(losses[3:]) / len(losses[3:]), sum(ref[3:]) / len(ref[3:])
+        assert all(abs(l - b) < 0.1 for l, b in zip(losses, ref)), (r, losses, ref)
+        a, b = sum(losses) / len(losses), sum(ref) / len(ref)
         assert abs(a - b) < 0.05 * b, (r, losses, ref)
 
 

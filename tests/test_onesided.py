@@ -113,16 +113,19 @@ def _push_of(r, c):
     return keys, rows, dense
 
 
-def _replay_run(rank, world, dev=torch.device("cpu")):
+def _replay_run(rank, world, dev=torch.device("cpu"), consistency="asp"):
     from minips_amd.ps.comm import Comm
     from minips_amd.ps.onesided import AsyncDenseTable, AsyncSparseTable
 
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     comm = Comm(device=dev)
-    sp = AsyncSparseTable(comm, num_rows=ROWS, width=W, optimizer="rowwise_adagrad", lr=0.1, consistency="asp",
-                          pull_dtype=torch.float32, init_std=0.0, route="range", max_keys=64, split=6)
-    dn = AsyncDenseTable(comm, NP, optimizer="adam", lr=0.01, consistency="asp", pull_dtype=torch.float32)
+    # (SSP: staleness 3 -- the straggler's sleeps then interleave the applies with the pushes)
+    sp = AsyncSparseTable(comm, num_rows=ROWS, width=W, optimizer="rowwise_adagrad", lr=0.1, consistency=consistency,
+                          pull_dtype=torch.float32, init_std=0.0, route="range", max_keys=64, split=6, staleness=3)
+    dn = AsyncDenseTable(comm, NP, optimizer="adam", lr=0.01, consistency=consistency, pull_dtype=torch.float32,
+                         staleness=3)
+    assert sp.coalesced == dn.coalesced == (consistency == "ssp")
     sp.ps.server.set_log(True)
     comm.barrier()  # every owner logs before any peer pushes (else its first applies go unlogged)
     for c in range(STEPS):
@@ -145,7 +148,9 @@ def _replay_run(rank, world, dev=torch.device("cpu")):
     return out
 
 
-def _replay_check(out, world=2):
+def _replay_check(out, world=2, coalesced=False):
+    """ASP: replay every push in this owner's apply order. SSP (clock-coalesced): per clock, the
+    requesters' rows summed per key in requester order and ONE row-wise Adagrad / Adam step at lr."""
     from minips_amd import ops
 
     for o, res in out.items():
@@ -161,6 +166,25 @@ def _replay_check(out, world=2):
         m = torch.zeros(S)
         v = torch.zeros(S)
         step = 0
+        if coalesced:
+            for t, r, c in log:  # whole clocks, requesters in order
+                assert r == [x for x in log if x[0] == t and x[2] == c].index((t, r, c)), log
+            for c in range(STEPS):
+                agg, dsum = {}, torch.zeros(NP)
+                for r in range(world):
+                    keys, rows, dense = _push_of(r, c)
+                    for k, row in zip(keys.tolist(), rows):
+                        if lo <= k < hi:
+                            agg[k] = agg[k] + row if k in agg else row.clone()
+                    dsum += dense
+                ks = sorted(agg)
+                ops.sparse_rowwise_adagrad(shard, state, torch.tensor(ks, dtype=torch.int64), lo,
+                                           torch.stack([agg[k] for k in ks]), 0.1, 1e-8, state2=state2, split=6)
+                g = torch.zeros(S)
+                n = max(0, min(S, NP - db))
+                g[:n] = dsum[db: db + n]
+                ops.adam_apply(w, m, v, g, 0.01, 0.9, 0.999, 1e-8, 0.0, c + 1, 1.0, None)
+            log = []
         for t, r, c in log:  # this owner's apply order
             keys, rows, dense = _push_of(r, c)
             if t == 0:
@@ -185,6 +209,20 @@ def test_owner_apply_replay_cpu():
     _replay_check(run_world(_replay_run, world=2))
 
 
+def _replay_ssp(rank, world):
+    return _replay_run(rank, world, consistency="ssp")
+
+
+def _g_replay_ssp(rank, world):
+    return _replay_run(rank, world, torch.device("cuda", 0), consistency="ssp")
+
+
+def test_owner_apply_replay_ssp_coalesced_cpu():
+    """SSP: the owner applies a clock once every requester sent it, one optimizer step over the
+    summed pushes (the reference's linear Add, ssp_model.cpp:54-56)."""
+    _replay_check(run_world(_replay_ssp, world=2), coalesced=True)
+
+
 def _g_replay(rank, world):
     return _replay_run(rank, world, torch.device("cuda", 0))
 
@@ -194,6 +232,14 @@ def test_owner_apply_replay_gpu_ipc(dev):
     """The owners' HIP applies (row-wise Adagrad with a split state, Adam) match an fp32 CPU replay
     of the same apply order."""
     _replay_check(run_world(_g_replay, world=2))
+
+
+@pytest.mark.gpu
+def test_owner_apply_replay_ssp_coalesced_gpu_ipc(dev):
+    """The clock-coalesced HIP applies (ps_clock_adagrad with a split state, summed dense push +
+    one Adam step per clock) match the fp32 CPU replay, at 2 and 4 requesters."""
+    _replay_check(run_world(_g_replay_ssp, world=2), coalesced=True)
+    _replay_check(run_world(_g_replay_ssp, world=4), world=4, coalesced=True)
 
 
 # ------------------------------------------------------------------------------ models

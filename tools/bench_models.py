@@ -148,7 +148,8 @@ def build(args, comm):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--model", default="gpt2", choices=["mlp", "gpt2", "dlrm", "dlrm-10b", "lr", "kmeans",
+                                                         "widedeep-ssp"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (samples or sequences)")

@@ -7,6 +7,7 @@ Targets
   tests     csrc/tests/runtime_test.cc   -> build/bin/runtime_test
   apps      csrc/apps/*.cc               -> build/bin/<app>
   kernels   csrc/kernels/*.hip           -> build/obj/k_*.o   (hipcc --offload-arch=gfx950)
+  comm      csrc/comm/*.cc               -> build/obj/c_*.o   (native RCCL data plane, linked into ops_py)
   ops_py    csrc/bindings/ops_py.cpp     -> minips_amd/_kernels*.so   (hipcc, torch headers)
   san_thread / san_address   runtime + runtime_test + apps built with -fsanitize=thread|address
             (host code only) -> build/san_<kind>/bin/ (race detection on the runtime)
@@ -165,18 +166,34 @@ def kernel_objs() -> list[str]:
     return objs
 
 
+def comm_objs() -> list[str]:
+    """csrc/comm/*.cc (the native RCCL data plane: host code over hip / rccl headers; RCCL itself is
+    dlopen'ed at run time, the copy torch loaded)."""
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = _headers("csrc/comm")
+    jobs, objs = [], []
+    for src in sorted(glob.glob(os.path.join(ROOT, "csrc/comm/*.cc"))):
+        out = os.path.join(OBJ, "c_" + os.path.basename(src)[:-3] + ".o")
+        objs.append(out)
+        jobs.append((out, [src] + hdrs, [HIPCC, "-O2", "-std=c++17", "-fPIC", "-Wall", "-I/opt/rocm/include", "-c", src,
+                                         "-o", out]))
+    _compile_many(jobs)
+    return objs
+
+
 def build_ops_py(kobjs: list[str], robjs: list[str] = ()) -> str:
     src = os.path.join(ROOT, "csrc/bindings/ops_py.cpp")
     out = os.path.join(PKG, "_kernels" + EXT)
     bobj = os.path.join(OBJ, "ops_py.o")
     cflags, ldflags = _torch_flags()
     kobjs = list(kobjs) + [o for o in robjs if os.path.basename(o)[3:-2] in KERNEL_RT]
-    hdrs = _headers("csrc/kernels", "csrc/bindings") + [os.path.join(ROOT, "csrc/runtime", h + ".h")
-                                                        for h in KERNEL_RT]
+    hdrs = _headers("csrc/kernels", "csrc/bindings", "csrc/comm") + [os.path.join(ROOT, "csrc/runtime", h + ".h")
+                                                                     for h in KERNEL_RT]
     _compile_many([(bobj, [src] + hdrs, [HIPCC, "-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
                                          *cflags, "-c", src, "-o", bobj])])
     _compile_many([(out, [bobj] + kobjs,
-                    [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", bobj, *kobjs, "-o", out, *ldflags])])
+                    [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", bobj, *kobjs, "-o", out, *ldflags,
+                     "-ldl"])])
     return out
 
 
@@ -223,7 +240,7 @@ def main(argv: list[str]) -> int:
         for o in build_apps(objs):
             print("built", o)
     if targets & {"kernels", "ops_py"}:
-        kobjs = kernel_objs()
+        kobjs = kernel_objs() + comm_objs()
         print("built", build_ops_py(kobjs, objs))  # always relink: a stale .so would silently run old kernels
     return 0
 
