@@ -63,6 +63,10 @@ def main():
                          "that rank, every world > 1 code path, collectives replaced by loopback copies of the "
                          "same bytes (ps.comm.LoopbackComm; wire time excluded). Reports per-rank throughput")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--emu-wire", default=None, choices=["none", "ring", "direct"],
+                    help="emulated world: model each collective's link time (LoopbackComm wire model, SURVEY "
+                         "§5.8: 7 xGMI links of --emu-link-gbps; RS/AG ring or direct) as a device spin")
+    ap.add_argument("--emu-link-gbps", type=float, default=None)
     ap.add_argument("--lookahead", type=int, default=0,
                     help="batches generated + key-planned ahead (0: feeder.default_depth, 2)")
     ap.add_argument("--sync-audit", type=int, default=0,
@@ -81,7 +85,7 @@ def main():
         from minips_amd.ps.comm import LoopbackComm
 
         init_distributed()  # (one process: device selection only)
-        comm = LoopbackComm(args.emulate_world, args.emulate_rank)
+        comm = LoopbackComm(args.emulate_world, args.emulate_rank, wire=args.emu_wire, link_gbps=args.emu_link_gbps)
     else:
         comm = init_distributed()
     n = comm.world
@@ -120,6 +124,7 @@ def main():
     sync()
     comm.barrier()
     sync()
+    wire0 = getattr(comm, "wire_us", 0.0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         l = step()
@@ -163,8 +168,10 @@ def main():
             dist.all_reduce(hi, op=dist.ReduceOp.MAX)
             diag["host_issue_ms_per_step_max_rank"] = round(float(hi.item()), 4)
     if emulated:
+        wire = ("wire time excluded" if comm.wire == "none" else
+                f"modelled wire time: {comm.wire} RS/AG, {comm.link_gbps:g} GB/s links, {comm.latency_us:g} us latency")
         parallelism = (f"EMULATED rank {comm.rank} of ps-dp{n} ({args.consistency}; one process, loopback "
-                       "collectives: the per-rank program of an N-rank step, wire time excluded)")
+                       f"collectives: the per-rank program of an N-rank step, {wire})")
     elif n == 1:
         # one rank owns every shard: Get/Add/Clock are local gathers/applies, no collective runs
         parallelism = f"ps-dp1 ({args.consistency}; single rank: local shards, no collectives)"
@@ -200,7 +207,9 @@ def main():
                 "bucket_mb": args.bucket_mb if n > 1 else None,
                 "lookahead": feeder.depth,
                 **({k.lower(): os.environ[k] for k in ("NCCL_ALGO", "NCCL_PROTO") if os.environ.get(k)}),
-                **({"emulated_world": n, "emulated_rank": comm.rank} if emulated else {}),
+                **({"emulated_world": n, "emulated_rank": comm.rank, "emu_wire": comm.wire,
+                    "emu_wire_us_per_step": round((comm.wire_us - wire0) / args.steps, 2)}
+                   if emulated else {}),
             },
             "loss_first": round(loss0, 5) if loss0 is not None else None,
             "loss_last": round(loss_last, 5),

@@ -1935,6 +1935,11 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
   m.def("multi_copy", &multi_copy);
+  m.def("wire_spin", [](int64_t ticks, int64_t blocks, int64_t stream) {
+    minips_k::wire_spin((int)ticks, (int)blocks,
+                       stream ? reinterpret_cast<hipStream_t>(stream)
+                              : c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  });
   m.def("clock_probe", &clock_probe, py::arg("out"), py::arg("spin_ticks") = 2000, py::arg("stream") = 0);
   m.def("bitmap_plan", &bitmap_plan, py::arg("keys"), py::arg("bounds"), py::arg("num_rows"), py::arg("route_mult"),
         py::arg("route_n"), py::arg("oor") = py::none());

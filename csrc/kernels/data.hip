@@ -143,6 +143,25 @@ __global__ __launch_bounds__(64) void clock_probe_kernel(int64_t* __restrict__ o
   out[1] = (int64_t)(r1 - r0);
 }
 
+// ---- modelled link time of an emulated collective (ps/comm.py LoopbackComm wire model): `blocks`
+// one-wave workgroups -- the CUs an RCCL collective's channels occupy -- spin `ticks` of the 100 MHz
+// real-time counter on the collective's stream. Bounded spin; writes nothing.
+__global__ __launch_bounds__(64) void wire_spin_kernel(int spin) {
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t r1 = r0;
+  for (int guard = 0; r1 - r0 < (uint64_t)spin && guard < (1 << 22); ++guard) {
+    __builtin_amdgcn_s_sleep(2);
+    r1 = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+void wire_spin(int spin_ticks, int blocks, hipStream_t s) {
+  if (spin_ticks < 1 || spin_ticks > 1000000 || blocks < 1 || blocks > 256)
+    throw std::runtime_error("wire_spin: 1 <= spin_ticks <= 1e6, 1 <= blocks <= 256");
+  hipLaunchKernelGGL(wire_spin_kernel, blocks, 64, 0, s, spin_ticks);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 void clock_probe(int64_t* out, int spin_ticks, hipStream_t s) {
   if (spin_ticks < 1 || spin_ticks > 1000000) throw std::runtime_error("clock_probe: 1 <= spin_ticks <= 1e6");
   hipLaunchKernelGGL(clock_probe_kernel, 1, 64, 0, s, out, spin_ticks);

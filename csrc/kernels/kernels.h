@@ -285,6 +285,7 @@ void uniform_synth(uint64_t seed, uint64_t step, int64_t B, int F, uint64_t rows
                    int64_t* keys, float* labels, hipStream_t s);
 // out[0] = shader-clock cycles, out[1] = 100 MHz real-time ticks over ~spin_ticks (one wave; diagnostics)
 void clock_probe(int64_t* out, int spin_ticks, hipStream_t s);
+void wire_spin(int spin_ticks, int blocks, hipStream_t s);
 // up to 16 device-to-device copies in one launch: pair t copies n16[t] 16-byte vectors then tail[t]
 // bytes (src / dst 16-byte aligned when n16 > 0); start[] = exclusive prefix of n16 + tail
 constexpr int kMultiCopyMax = 16;

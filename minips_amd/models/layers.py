@@ -127,10 +127,11 @@ class _Fork:
     """SideStream.fork()'s context: the side stream waits for the current stream, then the block
     runs on the side stream (GEMM splits in overlap mode)."""
 
-    __slots__ = ("side", "prev", "mode")
+    __slots__ = ("side", "prev", "mode", "after")
 
-    def __init__(self, side):
+    def __init__(self, side, after=None):
         self.side = side
+        self.after = after
 
     def __enter__(self):
         sd = self.side
@@ -139,7 +140,12 @@ class _Fork:
             return None
         idx = st.device_index
         rec = ops._REC
-        if rec is not None:  # recorded into a LaunchList: its own event orders the two streams
+        if self.after is not None:  # an earlier point of the current stream (SideStream.point)
+            if sd._fast:
+                self.after.wait(sd._raw)
+            else:
+                st.wait_event(self.after)
+        elif rec is not None:  # recorded into a LaunchList: its own event orders the two streams
             rec.lst.fork(streams.current_raw(idx), sd._raw)
         elif sd._fast:
             ev = sd._event()
@@ -197,8 +203,21 @@ class SideStream:
         self._ev_i += 1
         return ev
 
-    def fork(self):
-        return _Fork(self)
+    def fork(self, after=None):
+        """``after``: an event of the current stream from point() -- the side stream waits for the
+        current stream only up to that point (work issued since then may overlap the block)."""
+        return _Fork(self, after)
+
+    def point(self):
+        """An event at the current stream's position now (for fork(after=...)); None when disabled."""
+        if self.stream is None:
+            return None
+        ev = self._event()
+        if self._fast:
+            ev.record(streams.current_raw(self.stream.device_index))
+        else:
+            ev.record(streams.current(self.stream.device_index))
+        return ev
 
     def join(self):
         if self.stream is not None:

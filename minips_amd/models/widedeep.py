@@ -17,6 +17,7 @@ Step (every kernel is a gfx950 HIP kernel; comm is RCCL):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -109,7 +110,10 @@ _DENSE_ON_SIDE = True
 # WD_W1_LATE on: fork the layer-1 weight gradient after the embedding dgrad (beside the
 # embedding backward rather than beside the dgrad: two big GEMMs at once only share the CUs);
 # round 3 measured it 5 % slower (profiles/r3/ab_wd_r3.txt)
-_W1_LATE = False
+_W1_LATE = os.environ.get("MINIPS_WD_W1_LATE", "0") == "1"
+# the one-rank side-stream Adam waits for the compute stream only up to the embedding dgrad (the
+# last reader of W), not up to the end of the step's issue (ADAM_EDGE=end: the round-5 fork)
+_ADAM_AFTER_DGRAD = os.environ.get("MINIPS_WD_ADAM_EDGE", "dgrad") == "dgrad"
 # ROWIDX off: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
 _ROWIDX = True
 # the dense forward and the backward GEMM chain up to the embedding dgrad, recorded once per set of
@@ -348,6 +352,8 @@ class WideDeep(LookaheadPlans):
                              perm=plan.csr[2], seg=D)
         else:
             ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"])
+        # W's last reader of the step is issued: a side-stream dense Adam may start after this point
+        w_read = side.point() if _ADAM_AFTER_DGRAD and self.comm.world == 1 else None
         if _W1_LATE:  # the layer-1 weight gradient beside the memory-bound embedding backward instead
             with side.fork():
                 _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
@@ -390,7 +396,7 @@ class WideDeep(LookaheadPlans):
             # compute stream (side.fork) -- a missing edge by construction. With the edge, repeated
             # op-by-op runs stopped varying at the 4th decimal (profiles/r5/race_dgrad_adam.txt)
             ev_x = side.mark()
-            with side.fork():
+            with side.fork(after=w_read):
                 self.dense.add()
                 self.dense.clock()
             self._side_pending = (ev_x, side.mark())

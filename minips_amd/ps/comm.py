@@ -42,6 +42,72 @@ import torch.distributed as dist
 from ..utils.metrics import _HOST_ON, _ROCTX_ON, range as _mrange
 
 
+# The native RCCL data plane (csrc/comm/rccl_comm.h, ops_py Rccl): every collective of the step
+# enqueued from C++ straight onto the issuing stream -- no c10d work object, no stream-sync events,
+# no per-call Python beyond one binding call (c10d: 13-31 us of host time per collective,
+# profiles/r5/host_issue.txt). NATIVE_RCCL off: the c10d ProcessGroupNCCL calls.
+_NATIVE_RCCL = os.environ.get("MINIPS_NATIVE_RCCL", "1") != "0"
+# process group -> (group, native communicator): one communicator per group, shared by every Comm
+_RCCL_CACHE: dict = {}
+
+
+def _rccl_lib() -> str:
+    """The RCCL shared object torch loaded (dlopen'ed again by the native side: one RCCL per process)."""
+    return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+
+
+def _native_rccl(comm: "Comm"):
+    """The native communicator of ``comm``'s group: rank 0 of the group creates the unique id, the
+    others read it from the c10d store and acknowledge, rank 0 then deletes the keys (a re-formed
+    group later finds none of them), and every rank joins ncclCommInitRank. Collective: called at
+    the same point of every rank's program (the first collective of the group)."""
+    from .._native import kernels
+
+    pg = comm.group if comm.group is not None else dist.group.WORLD
+    hit = _RCCL_CACHE.get(id(pg))
+    if hit is not None and hit[0] is pg and not hit[1].aborted:
+        return hit[1]
+    k = kernels()
+    lib = _rccl_lib()
+    store = dist.distributed_c10d._get_default_store()
+    tag = "minips_rccl/" + ",".join(str(r) for r in dist.get_process_group_ranks(pg))
+    mode = os.environ.get("TORCH_NCCL_ASYNC_ERROR_HANDLING", "")
+    with comm.waiting():
+        if comm.rank == 0:
+            store.set(tag + "/id", k.rccl_unique_id(lib))
+        uid = store.get(tag + "/id")
+        if comm.rank != 0:
+            store.add(tag + "/ack", 1)
+        else:
+            t0 = time.monotonic()
+            while int(store.add(tag + "/ack", 0)) < comm.world - 1:
+                if time.monotonic() - t0 > float(os.environ.get("MINIPS_PG_TIMEOUT", "60")):
+                    raise dist.DistBackendError(f"native RCCL rendezvous {tag}: peers missing")
+                time.sleep(0.001)
+            store.delete_key(tag + "/id")
+            store.delete_key(tag + "/ack")
+        # the watchdog's timeout and failure mode follow the process group's: TORCH_NCCL_ASYNC_ERROR_
+        # HANDLING 1 / 3 end the process on a stuck collective, 2 (in-place rollback) raises instead
+        rc = k.Rccl(lib, uid, comm.world, comm.rank, comm.device.index or 0,
+                    timeout_s=float(os.environ.get("MINIPS_PG_TIMEOUT", "60")), teardown=mode in ("1", "3"))
+    _RCCL_CACHE[id(pg)] = (pg, rc)
+    return rc
+
+
+def _rccl_call(fn, *args):
+    """A native RCCL enqueue; its failures surface as the torch.distributed error class the
+    training driver's recovery recognises (train._is_comm_failure)."""
+    try:
+        return fn(*args)
+    except RuntimeError as e:
+        if str(e).startswith("rccl"):
+            raise dist.DistBackendError(str(e)) from e
+        raise
+
+
+_REDOPS = {dist.ReduceOp.SUM: 0, dist.ReduceOp.MAX: 1, dist.ReduceOp.MIN: 2}
+
+
 # handles of dedicated streams whose owner is gone, by (device index, priority): reused, never
 # destroyed -- the caching allocator may still record events on a stream a freed tensor was
 # record_stream()-ed to, so destroying one can crash a later free
@@ -129,6 +195,7 @@ class Comm:
     def refresh(self):
         """Re-read rank / world / backend after the default process group was re-created (in-place
         rollback, minips_amd.train): every table keeps this same Comm object."""
+        self.drop_native("the process group was re-formed")
         self._sb = 0  # the new group's store starts its barrier counters afresh
         self.initialized = dist.is_available() and dist.is_initialized()
         self.rank = dist.get_rank(self.group) if self.initialized else 0
@@ -150,6 +217,27 @@ class Comm:
 
     def state(self) -> str:
         return "comm" if self._waiting > 0 else "run"
+
+    def _rc(self):
+        """The native RCCL communicator of this Comm's group (created at the first collective, shared
+        by every Comm over the group), or None: not RCCL, staged gloo tests, NATIVE_RCCL off."""
+        rc = self.__dict__.get("_rcc", False)
+        if rc is False:
+            rc = None
+            if self.backend == "nccl" and _NATIVE_RCCL and self.device.type == "cuda" and self.initialized:
+                rc = _native_rccl(self)
+            self._rcc = rc
+        return rc
+
+    def drop_native(self, why: str = "dropped"):
+        """Abort and forget the native communicator (rollback / rescale: its peers may be gone, and
+        a re-formed group needs a new one)."""
+        rc = self.__dict__.pop("_rcc", None)
+        if rc:
+            rc.abort(why)
+            for k, v in list(_RCCL_CACHE.items()):
+                if v[1] is rc:
+                    del _RCCL_CACHE[k]
 
     def _bare(self, fn, *args, **kw):
         """A collective enqueued bare (_plain): no generator context managers, but still counted as
@@ -276,6 +364,16 @@ class Comm:
             return out
         nbytes = inp[: sum(send_splits)].numel() * inp.element_size()
         self.stats.bytes_a2a += nbytes
+        rc = self._rc()
+        if rc is not None:  # one grouped send / recv launch from C++ (both the a2a-v and the p2p form)
+            o = out[: sum(recv_splits)]
+            i = inp[: sum(send_splits)]
+            if self._plain():
+                self._bare(_rccl_call, rc.all_to_all_v, o, i, recv_splits, send_splits)
+                return out
+            with self.waiting(), self._timed("p2p_send_recv" if p2p else "all_to_all_v", nbytes):
+                _rccl_call(rc.all_to_all_v, o, i, recv_splits, send_splits)
+            return out
         if not p2p:
             o = out[: sum(recv_splits)]
             i = inp[: sum(send_splits)]
@@ -313,7 +411,10 @@ class Comm:
             recv.copy_(counts)
             return recv
         self._record("a2a_counts", counts, counts.numel())
-        if self._staged(recv, counts):
+        rc = None if self._staged(recv, counts) else self._rc()
+        if rc is not None:
+            self._bare(_rccl_call, rc.all_to_all, recv, counts)
+        elif self._staged(recv, counts):
             r = torch.empty(recv.shape, dtype=recv.dtype)
             with self.waiting():
                 dist.all_to_all_single(r, counts.cpu(), group=self.group)
@@ -348,11 +449,18 @@ class Comm:
             out_shard.copy_(inp)
             return out_shard
         self.stats.bytes_rs += inp.numel() * inp.element_size()
+        rc = self._rc()
         if self._plain():
-            self._bare(dist.reduce_scatter_tensor, out_shard, inp, group=self.group)
+            if rc is not None:
+                self._bare(_rccl_call, rc.reduce_scatter, out_shard, inp)
+            else:
+                self._bare(dist.reduce_scatter_tensor, out_shard, inp, group=self.group)
             return out_shard
         with self.waiting(), self._timed("reduce_scatter", inp.numel() * inp.element_size()):
-            dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
+            if rc is not None:
+                _rccl_call(rc.reduce_scatter, out_shard, inp)
+            else:
+                dist.reduce_scatter_tensor(out_shard, inp, group=self.group)
         return out_shard
 
     def all_gather(self, out_full: torch.Tensor, shard: torch.Tensor):
@@ -372,11 +480,18 @@ class Comm:
         if self.backend == "gloo" and shard.data_ptr() >= out_full.data_ptr() and \
                 shard.data_ptr() < out_full.data_ptr() + out_full.numel() * out_full.element_size():
             shard = shard.clone()  # gloo does not support the in-place (aliased) form
+        rc = self._rc()
         if self._plain():
-            self._bare(dist.all_gather_into_tensor, out_full, shard, group=self.group)
+            if rc is not None:
+                self._bare(_rccl_call, rc.all_gather, out_full, shard)
+            else:
+                self._bare(dist.all_gather_into_tensor, out_full, shard, group=self.group)
             return out_full
         with self.waiting(), self._timed("all_gather", out_full.numel() * out_full.element_size()):
-            dist.all_gather_into_tensor(out_full, shard, group=self.group)
+            if rc is not None:
+                _rccl_call(rc.all_gather, out_full, shard)
+            else:
+                dist.all_gather_into_tensor(out_full, shard, group=self.group)
         return out_full
 
     def all_reduce_(self, t: torch.Tensor, op=None):
@@ -389,8 +504,12 @@ class Comm:
                 dist.all_reduce(h, op=op or dist.ReduceOp.SUM, group=self.group)
             t.copy_(h)
             return t
+        rc = self._rc()
         with self.waiting(), self._timed("all_reduce", t.numel() * t.element_size()):
-            dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
+            if rc is not None and (op or dist.ReduceOp.SUM) in _REDOPS:
+                _rccl_call(rc.all_reduce, t, _REDOPS[op or dist.ReduceOp.SUM])
+            else:
+                dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
         return t
 
     def store_barrier(self, tag: str, timeout_s: float | None = None):
@@ -444,22 +563,59 @@ class LoopbackComm(Comm):
       all-gather           every slot of out = this rank's shard (writes N x shard)
       barrier / all-reduce no-ops
 
-    Wire time is therefore excluded by construction: ``bench.py --emulate-world N`` times the
-    per-rank GPU and host program of an N-rank step on one GPU, so the step's kernels, host syncs
-    and launch count can be profiled (rocprofv3) before an N-GPU node is available."""
+    Wire time is excluded by default: ``bench.py --emulate-world N`` times the per-rank GPU and host
+    program of an N-rank step on one GPU, so the step's kernels, host syncs and launch count can be
+    profiled (rocprofv3) before an N-GPU node is available.
+
+    ``wire`` (bench.py --emu-wire, MINIPS_EMU_WIRE) adds a modelled link time to each collective: a
+    device spin on the collective's stream, on ``channels`` workgroups (the CUs an RCCL collective's
+    channels hold), of latency + bytes / bandwidth per SURVEY §5.8 for 7 point-to-point xGMI links
+    of ``link_gbps`` each:
+      all-to-all(-v)          every peer segment on its own link: S_sent / ((P - 1) * link)
+      RS / AG "ring"          one link per hop: (P - 1) / P * S / link
+      RS / AG "direct"        all 7 links at once: (P - 1) / P * S / ((P - 1) * link)
+    (S: the bytes this rank's collective moves; a fixed per-collective latency on top)."""
 
     emulated = True
 
-    def __init__(self, world: int, rank: int = 0, device: torch.device | None = None):
+    def __init__(self, world: int, rank: int = 0, device: torch.device | None = None, wire: str | None = None,
+                 link_gbps: float | None = None, latency_us: float | None = None, channels: int | None = None):
         if world < 2 or not 0 <= rank < world:
             raise ValueError(f"LoopbackComm: rank {rank} of world {world}")
         super().__init__(device=device)
         self.world, self.rank = int(world), int(rank)
         self.backend = "loopback"
         self.initialized = False
+        self.wire = (wire if wire is not None else os.environ.get("MINIPS_EMU_WIRE", "none")) or "none"
+        if self.wire not in ("none", "ring", "direct"):
+            raise ValueError(f"LoopbackComm wire model {self.wire!r}: none | ring | direct")
+        self.link_gbps = float(link_gbps if link_gbps is not None else os.environ.get("MINIPS_EMU_LINK_GBPS", "153"))
+        self.latency_us = float(latency_us if latency_us is not None else os.environ.get("MINIPS_EMU_LAT_US", "8"))
+        self.channels = int(channels if channels is not None else os.environ.get("MINIPS_EMU_CHANNELS", "16"))
+        self.wire_us = 0.0  # modelled link time issued so far (bench.py diag)
+
+    def _wire(self, kind: str, nbytes: int):
+        """The modelled link time of one collective, spun on the current stream (GPU only)."""
+        if self.wire == "none" or self.device.type != "cuda":
+            return
+        P, bw = self.world, self.link_gbps * 1e3  # bytes per us
+        if kind == "a2a":
+            us = nbytes * (P - 1) / P / ((P - 1) * bw)
+        elif self.wire == "ring":
+            us = (P - 1) / P * nbytes / bw
+        else:
+            us = (P - 1) / P * nbytes / ((P - 1) * bw)
+        us += self.latency_us
+        self.wire_us += us
+        from .._native import kernels
+
+        kernels().wire_spin(max(1, min(1_000_000, int(us * 100))), self.channels, 0)
 
     def refresh(self):
         self._sb = 0
+
+    def _rc(self):
+        return None
 
     def _plain(self) -> bool:  # (the loopback copies stand in for RCCL's bare enqueue)
         return self.timing is None and not (_ROCTX_ON or _HOST_ON)
@@ -472,6 +628,7 @@ class LoopbackComm(Comm):
         n = int(sum(send_splits))
         nbytes = n * inp[:1].numel() * inp.element_size()
         self.stats.bytes_a2a += nbytes
+        self._wire("a2a", nbytes)
         if self._plain():
             if n and out.data_ptr() != inp.data_ptr():
                 out[:n].copy_(inp[:n])
@@ -483,6 +640,7 @@ class LoopbackComm(Comm):
 
     def all_to_all_counts(self, recv, counts):
         self._record("a2a_counts", counts, counts.numel())
+        self._wire("a2a", counts.numel() * counts.element_size())
         recv.copy_(counts)
         return recv
 
@@ -494,6 +652,7 @@ class LoopbackComm(Comm):
         self.stats.calls += 1
         self._record("reduce_scatter", inp, inp.numel())
         self.stats.bytes_rs += inp.numel() * inp.element_size()
+        self._wire("rs", inp.numel() * inp.element_size())
         if self._plain():
             torch.sum(inp.view(self.world, -1), 0, out=out_shard.view(-1))
             return out_shard
@@ -505,6 +664,7 @@ class LoopbackComm(Comm):
         self.stats.calls += 1
         self._record("all_gather", out_full, out_full.numel())
         self.stats.bytes_ag += out_full.numel() * out_full.element_size()
+        self._wire("ag", out_full.numel() * out_full.element_size())
         with contextlib.nullcontext() if self._plain() else self._timed(
                 "all_gather", out_full.numel() * out_full.element_size()):
             lo, hi = out_full.data_ptr(), out_full.data_ptr() + out_full.numel() * out_full.element_size()

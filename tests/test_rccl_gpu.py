@@ -35,6 +35,7 @@ def nccl_comm():
 def test_rccl_table_collectives(nccl_comm):
     comm = nccl_comm
     dev = comm.device
+    assert comm._rc() is not None  # the native data plane (csrc/comm/rccl_comm.h) carries every call
     # sparse Get / Add: rows of width 33 (32 emb + 1 wide) in bf16, and fp32 gradient rows
     for dt in (torch.bfloat16, torch.float32):
         inp = torch.randn(1000, 33, device=dev).to(dt)
@@ -150,3 +151,73 @@ def test_rccl_destroy_reinit_restore(tmp_path, monkeypatch):
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def test_native_rccl_matches_c10d(nccl_comm, monkeypatch):
+    """The native RCCL data plane and torch's ProcessGroupNCCL give identical results for every
+    collective the tables issue (uneven bf16 row all-to-all-v, int64 keys, fp32 / fp64
+    reduce-scatter, bf16 all-gather, MAX all-reduce)."""
+    from minips_amd.ps import comm as cm
+
+    dev = nccl_comm.device
+    g = torch.Generator(device=dev).manual_seed(7)
+    rows = torch.randn(777, 36, device=dev, generator=g).to(torch.bfloat16)
+    keys = torch.randint(0, 1 << 40, (777,), device=dev, generator=g)
+    grad = torch.randn(1 << 15, device=dev, generator=g)
+    gd = grad.double()
+    par = torch.randn(1 << 14, device=dev, generator=g).to(torch.bfloat16)
+    outs = {}
+    for native in (True, False):
+        monkeypatch.setattr(cm, "_NATIVE_RCCL", native)
+        c = cm.Comm(device=dev, force_collectives=True)
+        assert (c._rc() is not None) == native
+        r = torch.zeros(800, 36, dtype=torch.bfloat16, device=dev)
+        c.all_to_all_v(r, rows, [777], [777])
+        k = torch.zeros(800, dtype=torch.int64, device=dev)
+        c.all_to_all_v(k, keys, [777], [777], p2p=True)
+        rs, rsd = torch.empty_like(grad), torch.empty_like(gd)
+        c.reduce_scatter(rs, grad)
+        c.reduce_scatter(rsd, gd)
+        ag = torch.empty_like(par)
+        c.all_gather(ag, par)
+        m = torch.tensor([2.5, -1.0], device=dev)
+        c.all_reduce_(m, op=dist.ReduceOp.MAX)
+        torch.cuda.synchronize(dev)
+        outs[native] = [r, k, rs, rsd, ag, m]
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
+
+
+def test_native_rccl_watchdog_aborts_a_stuck_collective(nccl_comm):
+    """A stream that stops completing (a collective waiting for a dead peer, here: 1.5 s of device
+    spins queued behind one) is detected by the native communicator's watchdog within its
+    timeout: the communicator is aborted and the next call raises the torch.distributed error the
+    training driver's recovery handles (train._is_comm_failure) -- no hang."""
+    import time
+
+    from minips_amd._native import kernels
+    from minips_amd.ps.comm import _rccl_call, _rccl_lib
+    from minips_amd.train import _is_comm_failure
+
+    dev = nccl_comm.device
+    k = kernels()
+    lib = _rccl_lib()
+    rc = k.Rccl(lib, k.rccl_unique_id(lib), 1, 0, dev.index or 0, timeout_s=0.4, teardown=False)
+    s = torch.cuda.Stream(device=dev)
+    x = torch.ones(1024, device=dev)
+    y = torch.empty_like(x)
+    buf = torch.zeros(2, dtype=torch.int64, device=dev)
+    with torch.cuda.stream(s):
+        rc.all_gather(y, x)  # the stream is now watched
+        for _ in range(150):  # 150 x 10 ms of spins: the stream makes no progress for ~1.5 s
+            k.clock_probe(buf, 1_000_000, s.cuda_stream)
+    t0 = time.monotonic()
+    while not rc.aborted and time.monotonic() - t0 < 5.0:
+        time.sleep(0.02)
+    assert rc.aborted, "the watchdog did not abort the stuck communicator"
+    assert "did not complete" in rc.async_error()
+    with pytest.raises(dist.DistBackendError) as ei:
+        with torch.cuda.stream(s):
+            _rccl_call(rc.all_gather, y, x)
+    assert _is_comm_failure(ei.value)
+    torch.cuda.synchronize(dev)  # the spins drain; nothing is left running

@@ -426,7 +426,22 @@ def cmd_issue(a):
     fev = streams.FastEvent()
     cur = torch.cuda.current_stream(dev)
     pin = torch.zeros(8, dtype=torch.int64, pin_memory=True)
+    # the native RCCL data plane (csrc/comm/rccl_comm.h) behind minips_amd.ps.comm.Comm: the binding
+    # alone and the whole Comm method a table calls
+    from minips_amd.ps.comm import Comm
+
+    comm = Comm(device=dev, force_collectives=True)
+    rc = comm._rc()
+    cnt, cnt_o = torch.ones(1, dtype=torch.int64, device=dev), torch.empty(1, dtype=torch.int64, device=dev)
+    rows2 = torch.empty(4096, 36, dtype=torch.bfloat16, device=dev)
     cases = {
+        "native rccl all_to_all_v (binding)": lambda: rc.all_to_all_v(bo, bfv, [n], [n]),
+        "native rccl all_to_all (counts)": lambda: rc.all_to_all(cnt_o, cnt),
+        "native rccl reduce_scatter": lambda: rc.reduce_scatter(o, f),
+        "native rccl all_gather": lambda: rc.all_gather(bo, bfv),
+        "Comm.all_to_all_v (rows, native)": lambda: comm.all_to_all_v(rows2, rows, [4096], [4096]),
+        "Comm.reduce_scatter (native)": lambda: comm.reduce_scatter(o, f),
+        "Comm.all_gather (native)": lambda: comm.all_gather(bo, bfv),
         "c10d all_to_all_single (equal)": lambda: dist.all_to_all_single(bo, bfv),
         "c10d all_to_all_single (splits)": lambda: dist.all_to_all_single(bo, bfv, [n], [n]),
         "c10d reduce_scatter_tensor": lambda: dist.reduce_scatter_tensor(o, f),
