@@ -790,6 +790,46 @@ void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g
                        nullptr, sl.n ? &sl : nullptr);
 }
 
+// several ranks: the dense clock's reduce-scatter input = g + its split-K slab planes, g cleared
+void slab_pack(at::Tensor& g, at::Tensor& out, const std::vector<std::tuple<at::Tensor, int64_t, int64_t, int64_t>>& slabs) {
+  check_gpu(g, "g");
+  check_gpu(out, "out");
+  check_dtype(g, at::kFloat, "g");
+  check_dtype(out, at::kFloat, "out");
+  TORCH_CHECK(out.numel() == g.numel(), "slab_pack: out and g sizes differ");
+  minips_k::AdamSlabs sl;
+  TORCH_CHECK(slabs.size() <= 4, "slab_pack: at most 4 slab regions");
+  for (const auto& t : slabs) {
+    const at::Tensor& p = std::get<0>(t);
+    const int64_t ns = std::get<1>(t), plane = std::get<2>(t), off = std::get<3>(t);
+    check_gpu(p, "slab");
+    check_dtype(p, at::kFloat, "slab");
+    TORCH_CHECK(ns >= 1 && p.numel() >= ns * plane && off >= 0 && off + plane <= g.numel(), "slab_pack slab bounds");
+    sl.p[sl.n] = ptr<float>(p);
+    sl.nsplit[sl.n] = (int)ns;
+    sl.plane[sl.n] = plane;
+    sl.len[sl.n] = plane;
+    sl.off[sl.n] = off;
+    ++sl.n;
+  }
+  minips_k::slab_pack(ptr<float>(g), ptr<float>(out), g.numel(), sl.n ? &sl : nullptr, stream_of(g));
+}
+
+void emu_sum_slices(const at::Tensor& in, at::Tensor& out, int64_t P) {
+  check_gpu(in, "in");
+  check_gpu(out, "out");
+  check_dtype(in, at::kFloat, "in");
+  check_dtype(out, at::kFloat, "out");
+  TORCH_CHECK(in.numel() == out.numel() * P, "emu_sum_slices: in = P x out");
+  minips_k::emu_sum_slices(ptr<float>(in), ptr<float>(out), out.numel(), (int)P, stream_of(in));
+}
+
+void emu_rebase(at::Tensor& keys, int64_t step, int64_t P, int64_t base) {
+  check_gpu(keys, "keys");
+  check_dtype(keys, at::kLong, "keys");
+  minips_k::emu_rebase(ptr<int64_t>(keys), keys.numel(), step, (int)P, base, stream_of(keys));
+}
+
 // split-K GEMM into slab planes without their reduction (the Adam kernel folds them): returns nsplit
 int64_t gemm_slab(const at::Tensor& A, const at::Tensor& B, at::Tensor& slab, int64_t M, int64_t N, int64_t K,
                   bool a_km, bool b_kn, int64_t split_k) {
@@ -1935,6 +1975,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("kmeans_argmin", &kmeans_argmin);
   m.def("criteo_synth", &criteo_synth);
   m.def("multi_copy", &multi_copy);
+  m.def("slab_pack", &slab_pack);
+  m.def("emu_sum_slices", &emu_sum_slices);
+  m.def("emu_rebase", &emu_rebase);
   m.def("wire_spin", [](int64_t ticks, int64_t blocks, int64_t stream) {
     minips_k::wire_spin((int)ticks, (int)blocks,
                        stream ? reinterpret_cast<hipStream_t>(stream)

@@ -162,6 +162,44 @@ void wire_spin(int spin_ticks, int blocks, hipStream_t s) {
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
+// ---- loopback stand-ins of an emulated N-rank job (ps/comm.py LoopbackComm, ps/tables.py): the
+// reduce-scatter's sum of the N equal slices (in slice order), and the re-base of this rank's own
+// requests to owner s into its own range (key - s * step with s = min(key / step, P - 1), + base)
+__global__ __launch_bounds__(256) void emu_sum_slices_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                             int64_t n4, int P) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 a = reinterpret_cast<const float4*>(in)[i];
+    for (int r = 1; r < P; ++r) {
+      const float4 b = reinterpret_cast<const float4*>(in)[r * n4 + i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = a;
+  }
+}
+
+__global__ void emu_rebase_kernel(int64_t* __restrict__ keys, int64_t n, int64_t step, int P, int64_t base) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = keys[i];
+    const int64_t s = min(k / step, (int64_t)(P - 1));
+    keys[i] = k - s * step + base;
+  }
+}
+
+void emu_sum_slices(const float* in, float* out, int64_t n, int P, hipStream_t s) {
+  if (n % 4 || (reinterpret_cast<uintptr_t>(in) & 15) || (reinterpret_cast<uintptr_t>(out) & 15) || P < 1)
+    throw std::runtime_error("emu_sum_slices: 16-byte aligned slices of a multiple of 4 floats");
+  if (n == 0) return;
+  hipLaunchKernelGGL(emu_sum_slices_kernel, grid_for(n / 4, 256, 4096), 256, 0, s, in, out, n / 4, P);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void emu_rebase(int64_t* keys, int64_t n, int64_t step, int P, int64_t base, hipStream_t s) {
+  if (n <= 0) return;
+  if (step <= 0) throw std::runtime_error("emu_rebase: step > 0");
+  hipLaunchKernelGGL(emu_rebase_kernel, grid_for(n, 256, 4096), 256, 0, s, keys, n, step, P, base);
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
 void clock_probe(int64_t* out, int spin_ticks, hipStream_t s) {
   if (spin_ticks < 1 || spin_ticks > 1000000) throw std::runtime_error("clock_probe: 1 <= spin_ticks <= 1e6");
   hipLaunchKernelGGL(clock_probe_kernel, 1, 64, 0, s, out, spin_ticks);

@@ -205,6 +205,8 @@ struct AdamSlabs {
   int64_t off[4] = {0, 0, 0, 0}, len[4] = {0, 0, 0, 0}, plane[4] = {0, 0, 0, 0};
   int nsplit[4] = {0, 0, 0, 0};
 };
+// several ranks: out = g + the split-K planes of its regions, g cleared (the reduce-scatter input)
+void slab_pack(float* g, float* out, int64_t n, const AdamSlabs* slabs, hipStream_t s);
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2,
                 float eps, float weight_decay, int step, float grad_scale, bf16_t* w_bf16, hipStream_t s,
                 const int* step_dev = nullptr, bool zero_g = false, const int64_t* active = nullptr,
@@ -286,6 +288,8 @@ void uniform_synth(uint64_t seed, uint64_t step, int64_t B, int F, uint64_t rows
 // out[0] = shader-clock cycles, out[1] = 100 MHz real-time ticks over ~spin_ticks (one wave; diagnostics)
 void clock_probe(int64_t* out, int spin_ticks, hipStream_t s);
 void wire_spin(int spin_ticks, int blocks, hipStream_t s);
+void emu_sum_slices(const float* in, float* out, int64_t n, int P, hipStream_t s);
+void emu_rebase(int64_t* keys, int64_t n, int64_t step, int P, int64_t base, hipStream_t s);
 // up to 16 device-to-device copies in one launch: pair t copies n16[t] 16-byte vectors then tail[t]
 // bytes (src / dst 16-byte aligned when n16 > 0); start[] = exclusive prefix of n16 + tail
 constexpr int kMultiCopyMax = 16;

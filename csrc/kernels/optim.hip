@@ -81,8 +81,47 @@ __global__ void adam_kernel(float* __restrict__ w, float* __restrict__ m, float*
   }
 }
 
+// Several ranks: the reduce-scatter input of a dense clock. out = g + the split-K weight-gradient
+// planes of its regions (the same fold as adam_kernel's), g cleared for the next clock -- one pass
+// instead of a split-K reduce per weight gradient plus a clearing pass over the gradient.
+__global__ void slab_pack_kernel(float* __restrict__ g, float* __restrict__ out, int64_t n4, AdamSlabs sl) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 G = reinterpret_cast<const float4*>(g)[i];
+    for (int k = 0; k < sl.n; ++k) {
+      const int64_t e = 4 * i - sl.off[k];
+      if (e < 0 || e >= sl.len[k]) continue;
+      const float* p = sl.p[k] + e;
+      for (int z = 0; z < sl.nsplit[k]; ++z) {
+        const float4 a = *reinterpret_cast<const float4*>(p + z * sl.plane[k]);
+        G.x += a.x;
+        G.y += a.y;
+        G.z += a.z;
+        G.w += a.w;
+      }
+    }
+    reinterpret_cast<float4*>(out)[i] = G;
+    reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 static void check_align(const void* p, const char* what) {
   if (reinterpret_cast<uintptr_t>(p) & 15) throw std::runtime_error(std::string(what) + " must be 16-byte aligned");
+}
+
+void slab_pack(float* g, float* out, int64_t n, const AdamSlabs* slabs, hipStream_t s) {
+  AdamSlabs sl{};
+  if (slabs) {
+    sl = *slabs;
+    for (int k = 0; k < sl.n; ++k)
+      if ((sl.off[k] & 3) || (sl.len[k] & 3) || (sl.plane[k] & 3) || sl.off[k] < 0 || sl.off[k] + sl.len[k] > n ||
+          (reinterpret_cast<uintptr_t>(sl.p[k]) & 15))
+        throw std::runtime_error("slab_pack: 16-byte aligned planes and ranges inside the gradient");
+  }
+  if (n % 4 || (reinterpret_cast<uintptr_t>(g) & 15) || (reinterpret_cast<uintptr_t>(out) & 15))
+    throw std::runtime_error("slab_pack: 16-byte aligned gradient of a multiple of 4 floats");
+  if (n == 0) return;
+  hipLaunchKernelGGL(slab_pack_kernel, grid_for(n / 4, 256, 4096), 256, 0, s, g, out, n / 4, sl);
+  MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 void adam_apply(float* w, float* m, float* v, const float* g, int64_t n, float lr, float beta1, float beta2, float eps,

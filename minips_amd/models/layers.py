@@ -10,6 +10,7 @@ from __future__ import annotations
 
 
 import math
+import os
 
 import torch
 
@@ -182,9 +183,18 @@ class SideStream:
     all forked work. Disabled (or on CPU) it is a no-op and the block runs inline. Stream changes
     go through utils/streams (no per-call device resolution: this is the step's hottest host path)."""
 
-    def __init__(self, device, enabled: bool = True):
-        self.stream = torch.cuda.Stream(device=device, priority=compute_priority()) \
-            if enabled and torch.device(device).type == "cuda" else None
+    def __init__(self, device, enabled: bool = True, priority: int | None = None):
+        """``priority`` (HIP: -1 high, 0 normal, 1 low; default compute_priority()): a low-priority
+        side stream lets the dispatcher favour the compute stream's workgroups when both wait."""
+        cuda = enabled and torch.device(device).type == "cuda"
+        if priority is None:
+            priority = int(os.environ.get("MINIPS_SIDE_PRIO", str(compute_priority())))
+        if cuda and priority > 0:
+            from ..ps.comm import dedicated_stream
+
+            self.stream = dedicated_stream(device, priority)
+        else:
+            self.stream = torch.cuda.Stream(device=device, priority=priority) if cuda else None
         # fork / join events are re-recorded every step (a wait binds to the record issued before
         # it): no event objects created and destroyed per fork. Same-device ordering only, so
         # fence-free native events (ops_py FastEvent; MINIPS_STREAM_DEBUG sysfence=side: torch events)

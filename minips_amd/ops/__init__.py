@@ -666,6 +666,19 @@ def adam_apply(w, m, v, g, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.
         g_in.zero_()
 
 
+def slab_pack(g, out, slabs=()):
+    """out = g + the split-K planes ``slabs`` ((slab, nsplit, plane, offset), as adam_apply) folded
+    into their regions; g cleared -- a several-rank dense clock's reduce-scatter input in one pass."""
+    if _gpu(g):
+        kernels().slab_pack(g, out, [(s, int(n), int(p), int(o)) for s, n, p, o in slabs])
+        return out
+    out.copy_(g)
+    for s, n, p, o in slabs:
+        out[o: o + p] += s[: n * p].view(n, p).sum(0)
+    g.zero_()
+    return out
+
+
 def sgd_apply(w, g, lr, grad_scale=1.0, w_bf16=None):
     if _gpu(w):
         kernels().sgd_apply(w, g, float(lr), float(grad_scale), w_bf16)

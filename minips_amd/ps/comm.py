@@ -653,11 +653,14 @@ class LoopbackComm(Comm):
         self._record("reduce_scatter", inp, inp.numel())
         self.stats.bytes_rs += inp.numel() * inp.element_size()
         self._wire("rs", inp.numel() * inp.element_size())
-        if self._plain():
-            torch.sum(inp.view(self.world, -1), 0, out=out_shard.view(-1))
-            return out_shard
-        with self._timed("reduce_scatter", inp.numel() * inp.element_size()):
-            torch.sum(inp.view(self.world, -1), 0, out=out_shard.view(-1))
+        with contextlib.nullcontext() if self._plain() else self._timed(
+                "reduce_scatter", inp.numel() * inp.element_size()):
+            if inp.is_cuda and inp.dtype == torch.float32 and out_shard.numel() % 4 == 0:
+                from .._native import kernels
+
+                kernels().emu_sum_slices(inp, out_shard, self.world)  # (slice order, one kernel)
+            else:
+                torch.sum(inp.view(self.world, -1), 0, out=out_shard.view(-1))
         return out_shard
 
     def all_gather(self, out_full, shard):
@@ -668,9 +671,16 @@ class LoopbackComm(Comm):
         with contextlib.nullcontext() if self._plain() else self._timed(
                 "all_gather", out_full.numel() * out_full.element_size()):
             lo, hi = out_full.data_ptr(), out_full.data_ptr() + out_full.numel() * out_full.element_size()
-            if lo <= shard.data_ptr() < hi:
-                shard = shard.clone()  # (the in-place form: this rank's slot of out_full)
-            out_full.view(self.world, -1).copy_(shard.reshape(1, -1).expand(self.world, -1))
+            slots = list(out_full.view(self.world, -1))
+            if lo <= shard.data_ptr() < hi:  # the in-place form: this rank's slot of out_full is the shard
+                slots = [t for t in slots if t.data_ptr() != shard.data_ptr()]
+            if out_full.is_cuda and len(slots) <= 16:
+                from .._native import kernels
+
+                kernels().multi_copy(slots, [shard.reshape(-1)] * len(slots))  # (one kernel)
+            else:
+                for t in slots:
+                    t.copy_(shard.reshape(-1))
         return out_full
 
     def all_reduce_(self, t, op=None):

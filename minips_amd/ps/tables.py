@@ -533,9 +533,20 @@ class DenseTable:
                     # Adam clears it in the same pass (one fewer full-size kernel per clock)
                     cleared = self._apply(grad, step, zero_g=grad.numel() == self.shard, step_dev=sd)
                 else:
-                    comm.reduce_scatter(self.grad_shard, grad)
+                    sink = getattr(self, "_sink", None)
+                    if sink is not None:
+                        # the split-K weight-gradient planes folded into the reduce-scatter input and
+                        # the gradient cleared, in one pass (no split-K reduce kernels, no fill)
+                        send = self.__dict__.get("_rs_send")
+                        if send is None:
+                            send = self._rs_send = torch.empty_like(grad)
+                        ops.slab_pack(grad, send, sink.take(grad))
+                        comm.reduce_scatter(self.grad_shard, send)
+                        cleared = True
+                    else:
+                        comm.reduce_scatter(self.grad_shard, grad)
+                        cleared = False
                     self._apply(self.grad_shard, step, step_dev=sd)
-                    cleared = False
                 comm.all_gather(self.params, self.params[self.base: self.base + self.shard])
             else:
                 cleared = False
@@ -549,11 +560,14 @@ class DenseTable:
             self.pipe.wait_clock(step - len(self._ring))
 
     def slab_sink(self):
-        """A sink for split-K weight gradients whose K slices this table's next Adam folds in
+        """A sink for split-K weight gradients whose K slices this table's next clock folds in
         (ops.linear_wgrad(defer=...): no reduce kernel, no pass of the sum through the gradient
-        buffer); None where the clock does not apply the whole gradient in one Adam kernel (several
-        ranks, buckets, other optimizers)."""
-        if (not _WGRAD_DEFER or self.comm.world != 1 or self.optimizer != "adam" or self.comm.device.type != "cuda"
+        buffer): one rank's Adam, or several ranks' reduce-scatter pack (ops.slab_pack); None with
+        buckets (a bucket's collectives start mid-backward) and for other optimizers at one rank."""
+        # several ranks (unbucketed): the planes are folded by the reduce-scatter's pack (clock)
+        if (not _WGRAD_DEFER or self.comm.device.type != "cuda" or self.buckets is not None
+                or (self.comm.world == 1 and self.optimizer != "adam")
+                or (self.comm.world > 1 and self.value_dtype != torch.float32)
                 or (self.pipe.async_ and len(self._ring) < 2)):
             # (an asynchronous clock applies after the next step's GEMMs ran: those write the next
             # buffer of the gradient ring -- and its own planes -- which the ring's clock wait protects)
@@ -1028,8 +1042,13 @@ class SparseTable:
             # of one requester segment stay distinct (the direct owner apply has one writer per
             # (row, requester) entry) -- the shard has the last range's spare rows (_rows_alloc)
             step = self.bounds_list[1]
-            q = torch.div(recv_keys, step, rounding_mode="floor").clamp_(max=comm.world - 1)
-            recv_keys.sub_(q.mul_(step)).add_(self.base)
+            if recv_keys.is_cuda:
+                from .._native import kernels
+
+                kernels().emu_rebase(recv_keys, step, comm.world, self.base)
+            else:
+                q = torch.div(recv_keys, step, rounding_mode="floor").clamp_(max=comm.world - 1)
+                recv_keys.sub_(q.mul_(step)).add_(self.base)
         p = SparsePlan(n, pp.inv, pp.uniq, U, send, recv, recv_keys, csr=pp.csr, _U=U)
         if M > 0 and self._owner_direct_ok():
             p.extra["direct"] = True  # the push applies by direct addressing: no owner-side plan
