@@ -48,9 +48,22 @@ __global__ void criteo_synth_kernel(uint64_t seed, uint64_t step, const int64_t*
       const uint64_t sb = splitmix(base ^ (uint64_t)b * 0xd1342543de82ef95ULL);
       const int64_t card = cards[f];
       const int64_t raw = raw_id(sb, f, card);
-      const uint64_t h = card < (1LL << 32)
-                             ? ((uint64_t)raw * 2654435761ULL) % (uint64_t)card
-                             : (uint64_t)(((unsigned __int128)raw * 2654435761ULL) % (unsigned __int128)card);
+      uint64_t h;
+      if (card < (1LL << 16)) {
+        // raw < card < 2^16: (raw * (A mod card)) < 2^32 -- a 32-bit remainder, same value
+        h = ((uint32_t)raw * (2654435761u % (uint32_t)card)) % (uint32_t)card;
+      } else if (card < (1LL << 32)) {
+        // product < 2^56: a double-precision quotient is off by at most one for card >= 2^16
+        // (the 64-bit integer remainder is a long software routine); exact after the correction
+        const uint64_t prod = (uint64_t)raw * 2654435761ULL;
+        const int64_t q = (int64_t)((double)prod / (double)card);
+        int64_t r = (int64_t)prod - q * card;
+        if (r < 0) r += card;
+        if (r >= card) r -= card;
+        h = (uint64_t)r;
+      } else {
+        h = (uint64_t)(((unsigned __int128)raw * 2654435761ULL) % (unsigned __int128)card);
+      }
       keys[e] = (int64_t)h + offsets[f];
     } else {
       const int64_t b = e - nk;

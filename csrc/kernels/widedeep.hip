@@ -8,6 +8,8 @@
 #include <utility>
 #include <vector>
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -1066,10 +1068,20 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
 
 constexpr int kSegG = 16, kSegBatch = 8, kSegVW = 4;
 
-constexpr int seg_per_piece(int D) { return (64 / (D / kSegVW)) * kSegG; }
+constexpr int seg_per_piece(int D, int vw = kSegVW) { return (64 / (D / vw)) * kSegG; }
+
+// MINIPS_EMB_VW (A/B knob, read once): 4 (default) or 8 gradient values per lane of a lookup row --
+// 8 moves a bf16 row's 64 bytes with 16-byte loads over 4 lanes (16 rows per wave instruction)
+static int emb_seg_vw() {
+  static const int v = [] {
+    const char* e = std::getenv("MINIPS_EMB_VW");
+    return e && std::atoi(e) == 8 ? 8 : 4;
+  }();
+  return v;
+}
 
 int64_t emb_seg_part_floats(int64_t total, int D) {
-  const int64_t pw = seg_per_piece(D);
+  const int64_t pw = std::min(seg_per_piece(D, 4), seg_per_piece(D, 8));  // (sized for either width)
   return 2 * ((total + pw - 1) / pw) * seg_part_stride(D);
 }
 
@@ -1077,20 +1089,27 @@ template <typename TX, typename TO>
 static void emb_seg_det(const TX* dX, int ldx, const float* dwide, int64_t B, int F, int D, const int* members,
                         const int* memrow, TO* out, int row_stride, float* part, hipStream_t s, bool sorted_rows) {
   const int total = (int)(B * F);
-  const int64_t pw = seg_per_piece(D);
+  const int vw = std::is_same<TX, bf16_t>::value && sorted_rows ? emb_seg_vw() : kSegVW;
+  const int64_t pw = seg_per_piece(D, vw);
   const int64_t pieces = (total + pw - 1) / pw;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((pieces + 3) / 4, 65535));
   const int fix_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((pieces + 3) / 4, 4096));  // a wave per piece
-#define MINIPS_SEG_DET(DD)                                                                                         \
+#define MINIPS_SEG_DET_VW(DD, VV)                                                                                  \
   if (sorted_rows)                                                                                                \
-    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, true, kSegVW>), blocks, 256, 0, s, dX,    \
-                       ldx, dwide, F, members, memrow, total, out, row_stride, part);                             \
+    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, true, VV>), blocks, 256, 0, s, dX, ldx,   \
+                       dwide, F, members, memrow, total, out, row_stride, part);                                  \
   else                                                                                                            \
-    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, false, kSegVW>), blocks, 256, 0, s, dX,   \
-                       ldx, dwide, F, members, memrow, total, out, row_stride, part);                             \
+    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, false, VV>), blocks, 256, 0, s, dX, ldx,  \
+                       dwide, F, members, memrow, total, out, row_stride, part);                                  \
   if (pieces > 1)                                                                                                 \
-    hipLaunchKernelGGL((emb_seg_fix_kernel<TO, DD, kSegVW, seg_per_piece(DD)>), fix_blocks, 256, 0, s, memrow,     \
+    hipLaunchKernelGGL((emb_seg_fix_kernel<TO, DD, VV, seg_per_piece(DD, VV)>), fix_blocks, 256, 0, s, memrow,     \
                        total, part, out, row_stride, dwide != nullptr);
+#define MINIPS_SEG_DET(DD)          \
+  if (vw == 8 && DD >= 32) {        \
+    MINIPS_SEG_DET_VW(DD, 8)        \
+  } else {                          \
+    MINIPS_SEG_DET_VW(DD, kSegVW)   \
+  }
   switch (D) {
     case 16:
       MINIPS_SEG_DET(16)
@@ -1105,6 +1124,7 @@ static void emb_seg_det(const TX* dX, int ldx, const float* dwide, int64_t B, in
       throw std::runtime_error("emb_backward_seg: D must be 16, 32 or 64");
   }
 #undef MINIPS_SEG_DET
+#undef MINIPS_SEG_DET_VW
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

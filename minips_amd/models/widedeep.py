@@ -56,7 +56,9 @@ class WideDeepConfig:
     # layers' weight gradients exist -- beside the remaining backward (0: one clock at the end).
     # The 6.3 MB of W&D gradients: one reduce-scatter + all-gather after the backward measured
     # 6 % faster than two buckets at 8 emulated ranks (0.475-0.503 vs 0.517-0.530 ms/step: half
-    # the collective calls and clock issue on the host-bound step; profiles/r5/ab_dense_buckets.txt)
+    # the collective calls and clock issue on the host-bound step; profiles/r5/ab_dense_buckets.txt),
+    # and no worse with modelled xGMI wire time either (ring RS/AG 0.498 vs 0.505, direct 0.487 vs
+    # 0.517 ms/step, 8 emulated ranks; profiles/r6/ab_buckets_wire.txt)
     bucket_mb: float = 0.0
 
     def __post_init__(self):

@@ -386,10 +386,21 @@ class DenseTable:
         self._issued.add(k)
         g_b, gs_own, w, m, v, p_own, p_b = self._bucket_views(k, grad)
         local = comm.world == 1 and not comm.force  # one rank owns the whole bucket: no copy
+        packed = False
         if local:
             gs = g_b
         else:
-            comm.reduce_scatter(gs_own, g_b)
+            sink = getattr(self, "_sink", None)
+            if sink is not None and comm.world > 1:  # the bucket's split-K planes folded into its RS input
+                send = self.__dict__.get("_rs_send")
+                if send is None:
+                    send = self._rs_send = torch.empty_like(self.grad)
+                lo, hi = self.buckets[k]
+                ops.slab_pack(g_b, send[lo:hi], sink.take(g_b))
+                comm.reduce_scatter(gs_own, send[lo:hi])
+                packed = True
+            else:
+                comm.reduce_scatter(gs_own, g_b)
             gs = gs_own
         out = p_own if self.pull_dtype == torch.bfloat16 else None
         zeroed = False
@@ -398,7 +409,7 @@ class DenseTable:
             slabs = sink.take(gs) if sink is not None and local else ()
             ops.adam_apply(w, m, v, gs, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, step, 1.0,
                            out, step_dev=sd, zero_g=local, slabs=slabs)
-            zeroed = local  # the kernel cleared the gradient it read
+            zeroed = local or packed  # the kernel (or the pack) cleared the gradient
         elif self.optimizer == "adagrad":
             ops.adagrad_apply(w, m, gs, self.lr, self.eps, 1.0, out)
         elif self.optimizer == "sgd":
@@ -412,7 +423,7 @@ class DenseTable:
         if out is None:
             p_own.copy_(w)
         comm.all_gather(p_b, p_own)
-        if not zeroed:
+        if not (zeroed or packed):
             g_b.zero_()
         key, nb = self._bstat[k]
         bb = comm.stats.bucket_bytes
@@ -562,10 +573,10 @@ class DenseTable:
     def slab_sink(self):
         """A sink for split-K weight gradients whose K slices this table's next clock folds in
         (ops.linear_wgrad(defer=...): no reduce kernel, no pass of the sum through the gradient
-        buffer): one rank's Adam, or several ranks' reduce-scatter pack (ops.slab_pack); None with
-        buckets (a bucket's collectives start mid-backward) and for other optimizers at one rank."""
-        # several ranks (unbucketed): the planes are folded by the reduce-scatter's pack (clock)
-        if (not _WGRAD_DEFER or self.comm.device.type != "cuda" or self.buckets is not None
+        buffer): one rank's Adam, or several ranks' reduce-scatter pack of the clock or of each
+        bucket (ops.slab_pack); None for other optimizers at one rank."""
+        # several ranks: the planes are folded by the reduce-scatter's pack (clock / bucket)
+        if (not _WGRAD_DEFER or self.comm.device.type != "cuda"
                 or (self.comm.world == 1 and self.optimizer != "adam")
                 or (self.comm.world > 1 and self.value_dtype != torch.float32)
                 or (self.pipe.async_ and len(self._ring) < 2)):
