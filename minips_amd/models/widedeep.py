@@ -124,6 +124,9 @@ _ROWIDX = True
 # 0.368-0.370 either way) and at 8 emulated ranks (0.491-0.499 vs 0.488-0.502 ms), where the step
 # waits on the planning's count exchange instead (profiles/r5/host_issue.txt). False: op by op.
 _REPLAY = True
+# the head writes each lookup's wide gradient at its member-order row (plan positions), so the
+# embedding backward reads it contiguously instead of gathering dwide[members[m] / F] (DWIDE_MEMBER off)
+_DWIDE_MEMBER = os.environ.get("MINIPS_WD_DWIDE_MEMBER", "1") == "1"
 
 
 def _wgrad(dH, H, Gw, sink=None):
@@ -241,6 +244,7 @@ class WideDeep(LookaheadPlans):
                 dX=torch.empty(B, cfg.F * cfg.emb_dim, **bf),  # bf16: half the bytes of the emb backward
                 wide=torch.empty(B, dtype=torch.float32, device=dev),
                 dwide=torch.empty(B, dtype=torch.float32, device=dev),
+                dwide_m=torch.empty(B * cfg.F, dtype=torch.float32, device=dev),  # member order (_DWIDE_MEMBER)
                 loss=torch.zeros(1, dtype=torch.float32, device=dev),
             )
         return self._bufs[B]
@@ -327,8 +331,11 @@ class WideDeep(LookaheadPlans):
         else:
             self._forward(b, P)
         # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
+        sorted_rows = plan.csr is not None and len(plan.csr) >= 3 and plan.csr[2] is not None
+        dw_member = sorted_rows and _DWIDE_MEMBER and dense.is_cuda
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
-                    b["dwide"], b["loss"], self.view(G, "b3"), scale)
+                    b["dwide"], b["loss"], self.view(G, "b3"), scale,
+                    pos=plan.csr[2] if dw_member else None, dws=b["dwide_m"] if dw_member else None)
         ph.__exit__(None, None, None)
         ph = phase("wd.bwd_dense")
         ph.__enter__()
@@ -348,7 +355,6 @@ class WideDeep(LookaheadPlans):
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
         # (members, memrow, positions or None[, rowstart]): positions -> the dgrad writes the rows sorted
-        sorted_rows = plan.csr is not None and len(plan.csr) >= 3 and plan.csr[2] is not None
         if sorted_rows:
             ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"].view(B * F, D),
                              perm=plan.csr[2], seg=D)
@@ -373,7 +379,8 @@ class WideDeep(LookaheadPlans):
         ph = phase("wd.emb_push")
         ph.__enter__()
         dXe = b["dX"].view(B * F, D) if sorted_rows else b["dX"]
-        self.emb.add_lookup_grads(plan, dXe, b["dwide"], F, D, sorted_rows=sorted_rows)  # the table reduces
+        self.emb.add_lookup_grads(plan, dXe, b["dwide_m"] if dw_member else b["dwide"], F, D,  # the table reduces
+                                  sorted_rows=sorted_rows, dw_member=dw_member)
         self.emb.clock()
         issue_next("push")
         ph.__exit__(None, None, None)

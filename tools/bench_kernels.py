@@ -153,6 +153,28 @@ def cmd_kscan(a):
               f"{2.0 * M * N * K / t / 1e6:7.1f} TF/s", flush=True)
 
 
+def cmd_wgrad(a):
+    """The W&D weight-gradient GEMMs in their step form (split-K into fp32 slab planes, ops.linear_wgrad
+    defer path -> gemm_slab) over split counts; MINIPS_GEMM_TILE forces the tile (128 / 200 / 256).
+    Also the plane bytes the Adam then folds (nsplit x N x K x 4)."""
+    from minips_amd._native import kernels
+
+    B = a.batch
+    for name, N, K in (("W3", 256, 512), ("W2", 512, 1024), ("W1", 1024, 896)):
+        dy = torch.randn(B, N, device=dev()).to(torch.bfloat16)
+        x = torch.randn(B, K, device=dev()).to(torch.bfloat16)
+        for split in [int(v) for v in a.splits.split(",")]:
+            slab = torch.empty(split * N * K, device=dev())
+            ns = [0]
+
+            def f():
+                ns[0] = kernels().gemm_slab(dy, x, slab, N, K, B, True, True, split)
+
+            t = median_rounds({"k": f}, rounds=15)["k"]
+            print(f"{name} N={N:5d} K={K:5d} M={B} split={split:3d} (ran {ns[0]:3d}) {t:7.1f} us "
+                  f"{2.0 * B * N * K / t / 1e6:7.1f} TF/s  planes {ns[0] * N * K * 4 / 1e6:6.1f} MB", flush=True)
+
+
 def cmd_pmc(a):
     def bf(*s):
         return torch.randn(*s, device=dev()).to(torch.bfloat16)
@@ -269,6 +291,10 @@ def cmd_embstep(a):
     wide = torch.empty(B, device=dev())
     n = B * F
     t_emb = timed(lambda: ops.wd_emb_backward(dX, dw, inv, F, D, g, csr=(members, memrow)))
+    # the step's form: the dX dgrad wrote the lookups' rows in member order (positions), one row per
+    # lookup read contiguously
+    dXs = dX.view(n, D)[members.long()].contiguous()
+    t_embs = timed(lambda: ops.wd_emb_backward(dXs, dw, inv, F, D, g, csr=(members, memrow), sorted_rows=True))
     t_ada = timed(lambda: ops.sparse_rowwise_adagrad(table, state, uniq, 0, g, 0.01, 1e-8, state2=state2, split=D,
                                                      n_dev=U_dev))
     t_asm = timed(lambda: ops.wd_assemble_tab(dense, table, uniq, 0, inv, F, D, X, wide, ones_col=F * D + 13,
@@ -277,7 +303,8 @@ def cmd_embstep(a):
     mb_ada = (U * W * 4 * 3 + U * 16) / 1e6
     mb_asm = (n * 4 + n * 128 + B * 896 * 2) / 1e6
     print(f"U={U} lookups={n}")
-    for name, t, mb in (("emb backward", t_emb, mb_emb), ("rowwise adagrad", t_ada, mb_ada),
+    for name, t, mb in (("emb backward", t_emb, mb_emb), ("emb backward (sorted)", t_embs, mb_emb),
+                        ("rowwise adagrad", t_ada, mb_ada),
                         ("assemble (in place)", t_asm, mb_asm)):
         print(f"{name:22s} {t:8.1f} us  {mb:7.1f} MB  {mb / t:6.2f} TB/s")
 
@@ -510,6 +537,9 @@ def main(argv=None):
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--ops", default="reduce_scatter,all_gather,all_to_all,all_to_all_v")
     sub.add_parser("issue").add_argument("--iters", type=int, default=200)
+    p = sub.add_parser("wgrad")
+    p.add_argument("--batch", type=int, default=16384)
+    p.add_argument("--splits", default="2,4,6,8,10,12,16,24,32")
     a = ap.parse_args(argv)
     from minips_amd import _native
 
