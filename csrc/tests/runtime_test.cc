@@ -1246,6 +1246,57 @@ TEST(AsyncServer, AppliesArrivedClocksInOrderAndPauses) {
   req0.Unlink();
 }
 
+namespace {
+struct ClockApplier : minips::Applier {
+  std::vector<std::array<int64_t, 3>> seen;  // (table, requester or -1 = whole clock, clock)
+  void Apply(int t, int r, int64_t c) override { seen.push_back({t, r, c}); }
+  void ApplyClock(int t, int64_t c, int /*world*/) override { seen.push_back({t, -1, c}); }
+  void Flush() override {}
+};
+}  // namespace
+
+TEST(AsyncServer, CoalescedTableAppliesWholeClocksOnly) {
+  // An SSP table served clock-coalesced (AsyncServer::SetCoalesce): clock c is applied once, as
+  // one ApplyClock, only after EVERY requester sent it, and published for all requesters together;
+  // a plain table of the same server keeps applying push by push.
+  using namespace minips;
+  const std::string name = "minips_srv_coal_" + std::to_string(::getpid());
+  PSBoard req0(name, 2, 0, 2), req1(name, 2, 1, 2);
+  ClockApplier ap;
+  AsyncServer srv(name, 2, 0, 2, &ap);
+  srv.SetCoalesce(0, true);
+  srv.Enable(0);
+  srv.Enable(1);
+  srv.Start();
+  req1.PublishAppliedRow(0, 1000);  // owner 1 (no server here) has applied everything
+  req1.PublishAppliedRow(1, 1000);
+  req0.PublishSent(0, 3);  // requester 0 ran ahead: clocks 0..2
+  req0.PublishSent(1, 3);
+  EXPECT_TRUE(req0.WaitAppliedFrom(1, 0, 3, 5.0) >= 0);  // the plain table applied them at once
+  std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  EXPECT_EQ(req0.Applied(0, 0, 0), 0);  // coalesced: nothing until requester 1 sent clock 0
+  req1.PublishSent(0, 2);               // requester 1: clocks 0..1
+  EXPECT_TRUE(req0.WaitAppliedFrom(0, 0, 2, 5.0) >= 0);
+  std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  EXPECT_EQ(req0.Applied(0, 0, 0), 2);  // clock 2 waits for requester 1 although requester 0 sent it
+  EXPECT_EQ(req0.Applied(0, 0, 1), 2);  // published for both requesters together
+  req1.PublishSent(0, 3);
+  EXPECT_TRUE(req0.WaitAppliedFrom(0, 1, 3, 5.0) >= 0);
+  srv.Stop();
+  EXPECT_EQ(srv.Error(), "");
+  std::vector<int64_t> want_clocks;
+  for (const auto& e : ap.seen)
+    if (e[0] == 0) {
+      EXPECT_EQ(e[1], -1);  // table 0 only ever sees whole-clock applies
+      want_clocks.push_back(e[2]);
+    } else {
+      EXPECT_TRUE(e[1] == 0);  // table 1: requester 0's pushes, one by one
+    }
+  EXPECT_EQ(want_clocks.size(), 3u);
+  for (size_t i = 0; i < want_clocks.size(); ++i) EXPECT_EQ(want_clocks[i], (int64_t)i);
+  req0.Unlink();
+}
+
 TEST(ShardIO, ReadsVersion1Files) {
   // Round-1 shard files (v1: each array's bytes right after its descriptor, no offsets) still
   // restore through the v2 reader (header parse + offset ranged reads).

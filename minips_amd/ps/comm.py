@@ -7,6 +7,13 @@ The PS message patterns map onto collectives:
   C6    Barrier         -> 1-element all-reduce on the group
 With one rank every collective degenerates to a local copy (no RCCL launch at all).
 
+On RCCL the collectives run on the rank's native data plane (csrc/comm/rccl_comm.h, the Rccl
+binding): our own communicator over the RCCL torch loaded, each collective ONE enqueue from C++
+onto the issuing stream (the all-to-all-v as grouped ncclSend / ncclRecv), a watchdog that aborts
+the communicator when a collective stops completing; c10d (ProcessGroupNCCL) stays for the
+rendezvous, the unique-id exchange (store) and anything outside the step (MINIPS_NATIVE_RCCL=0:
+every collective through c10d).
+
 Ordering contract (why the data plane cannot deadlock, whatever the HW-queue count)
 -----------------------------------------------------------------------------------
 The reference keeps one FIFO sender per process (comm/sender.cpp:7-30 feeding
