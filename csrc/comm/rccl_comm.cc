@@ -178,6 +178,9 @@ void RcclComm::Watch() {
     for (Probe& p : streams_) {
       if (!p.ev) continue;
       if (!p.pending) {  // a probe behind whatever the stream holds now
+        // (never into a stream being captured into a HIP graph: the record would become a node)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(p.stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) continue;
         if (hipEventRecord(p.ev, p.stream) == hipSuccess) {
           p.pending = true;
           p.t_rec = t;
