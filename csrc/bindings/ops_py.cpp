@@ -572,8 +572,7 @@ void wd_assemble_tab(const at::Tensor& dense, const at::Tensor& tab, const at::T
 
 void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& wide_logit,
              const at::Tensor& labels, at::Tensor& dH, at::Tensor& dw, at::Tensor& db, at::Tensor& dwide,
-             at::Tensor& loss_sum, const c10::optional<at::Tensor>& dH_colsum, double grad_scale,
-             const c10::optional<at::Tensor>& pos, const c10::optional<at::Tensor>& dws) {
+             at::Tensor& loss_sum, const c10::optional<at::Tensor>& dH_colsum, double grad_scale) {
   for (auto* t : {&H, &w, &b0, &wide_logit, &labels}) check_gpu(*t, "wd_head input");
   check_dtype(H, at::kBFloat16, "H");
   check_dtype(w, at::kBFloat16, "w");
@@ -582,17 +581,10 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
   TORCH_CHECK(dH.sizes() == H.sizes(), "dH shape");
   TORCH_CHECK(w.numel() == H.size(1) && dw.numel() == H.size(1), "w/dw length");
   float* cs = opt_ptr<float>(dH_colsum, at::kFloat, "dH_colsum");
-  const int* pp = opt_ptr<int>(pos, at::kInt, "pos");
-  float* dp = opt_ptr<float>(dws, at::kFloat, "dws");
-  int F = 0;
-  if (pp) {
-    TORCH_CHECK(dp && pos->numel() % H.size(0) == 0 && dws->numel() == pos->numel(), "pos / dws: [B*F]");
-    F = (int)(pos->numel() / H.size(0));
-  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(H.device());
   minips_k::wd_head(ptr<bf16_t>(H), H.size(0), (int)H.size(1), ptr<bf16_t>(w), ptr<bf16_t>(b0),
                     ptr<float>(wide_logit), ptr<float>(labels), ptr<bf16_t>(dH), ptr<float>(dw), ptr<float>(db),
-                    ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H), pp, dp, F);
+                    ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H));
 }
 
 // Lookup CSR grouped by unique row (members/memrow int32 [B*F]) for U (upper-bound) rows.
@@ -619,11 +611,9 @@ std::vector<at::Tensor> emb_build_csr(const at::Tensor& inv, int64_t F, int64_t 
 
 void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwide, const at::Tensor& inv, int64_t F,
                      int64_t D, at::Tensor& grad_rows, int64_t x_off, const c10::optional<at::Tensor>& members,
-                     const c10::optional<at::Tensor>& memrow, bool sorted_rows, bool dw_member) {
+                     const c10::optional<at::Tensor>& memrow, bool sorted_rows) {
   check_gpu(dX, "dX");
   const float* dw = opt_ptr<float>(dwide, at::kFloat, "dwide");
-  TORCH_CHECK(!dw_member || (sorted_rows && dw && dwide->numel() == inv.numel()),
-              "member-order dwide: sorted rows and dwide [B*F]");
   check_gpu(inv, "inv");
   check_gpu(grad_rows, "grad_rows");
   TORCH_CHECK(dX.scalar_type() == at::kFloat || dX.scalar_type() == at::kBFloat16, "dX must be fp32 or bf16");
@@ -652,7 +642,7 @@ void wd_emb_backward(const at::Tensor& dX, const c10::optional<at::Tensor>& dwid
                   "members/memrow: int32 [B*F]");
       minips_k::emb_backward_csr(base0, bf0, (int)dX.stride(0), dw, B, (int)F, (int)D, members->data_ptr<int>(),
                                  memrow->data_ptr<int>(), grad_rows.data_ptr(), out_bf, (int)grad_rows.stride(0),
-                                 part.data_ptr<float>(), stream_of(dX), sorted_rows, dw_member);
+                                 part.data_ptr<float>(), stream_of(dX), sorted_rows);
       return;
     }
     at::Tensor ws = at::empty({3 * U + 1 + 2 * B * F + U / 1024 + 1}, inv.options().dtype(at::kInt));
@@ -801,7 +791,8 @@ void adam_apply(at::Tensor& w, at::Tensor& m, at::Tensor& v, const at::Tensor& g
 }
 
 // several ranks: the dense clock's reduce-scatter input = g + its split-K slab planes, g cleared
-void slab_pack(at::Tensor& g, at::Tensor& out, const std::vector<std::tuple<at::Tensor, int64_t, int64_t, int64_t>>& slabs) {
+void slab_pack(at::Tensor& g, at::Tensor& out,
+               const std::vector<std::tuple<at::Tensor, int64_t, int64_t, int64_t>>& slabs) {
   check_gpu(g, "g");
   check_gpu(out, "out");
   check_dtype(g, at::kFloat, "g");
@@ -1953,9 +1944,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1, py::arg("zero") = py::none());
-  m.def("wd_head", &wd_head, py::arg("H"), py::arg("w"), py::arg("b0"), py::arg("wide_logit"), py::arg("labels"),
-        py::arg("dH"), py::arg("dw"), py::arg("db"), py::arg("dwide"), py::arg("loss_sum"), py::arg("dH_colsum"),
-        py::arg("grad_scale"), py::arg("pos") = py::none(), py::arg("dws") = py::none());
+  m.def("wd_head", &wd_head);
   m.def("wd_assemble_tab", &wd_assemble_tab);
   m.def("owner_slots", &owner_slots, py::arg("own_inv"), py::arg("splits"), py::arg("cap"));
   m.def("owner_rows_adagrad", &owner_rows_adagrad, py::arg("table"), py::arg("state"), py::arg("state2"),
@@ -1966,7 +1955,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("stamp"), py::arg("lr"), py::arg("eps"));
   m.def("wd_emb_backward", &wd_emb_backward, py::arg("dX"), py::arg("dwide"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("grad_rows"), py::arg("x_off") = 0, py::arg("members") = py::none(),
-        py::arg("memrow") = py::none(), py::arg("sorted_rows") = false, py::arg("dw_member") = false);
+        py::arg("memrow") = py::none(), py::arg("sorted_rows") = false);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("plan_sorted", &plan_sorted, py::arg("keys"), py::arg("col_base"), py::arg("col_bits"),
         py::arg("col_bits_host"), py::arg("route_mult"), py::arg("route_n"), py::arg("bounds"),

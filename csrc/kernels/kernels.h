@@ -144,9 +144,7 @@ void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t 
                      const int32_t* rowidx = nullptr);  // rowidx: lookup j's row + base (plan_sorted)
 void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
-             float grad_scale, hipStream_t s, const int* pos = nullptr, float* dws = nullptr, int F = 0);
-// (pos != null: also dws[pos[b*F + f]] = dwide[b] for f < F -- the wide gradient of every lookup at
-// its member-order row, for the embedding backward's dw_member form)
+             float grad_scale, hipStream_t s);
 // Embedding backward: grad_rows[inv[b*F+f], 0:D] += dX[b, f*D : (f+1)*D] (fp32 dX, ld ldx),
 // grad_rows[inv[b*F+f], D] += dwide[b] when dwide != null (grad_rows fp32 [U, row_stride],
 // pre-zeroed).
@@ -172,8 +170,7 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
 // it as one contiguous stream instead of gathering 2*D-byte pieces of [B, F*D] rows.
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, void* out, bool out_bf16, int row_stride, float* part,
-                      hipStream_t s, bool sorted_rows = false, bool dw_member = false);
-// (dw_member, sorted rows only: dwide is [B*F] in member order -- wd_head's dws -- read as dwide[m])
+                      hipStream_t s, bool sorted_rows = false);
 // pos[members[m]] = m (n entries): where each lookup's gradient row goes in member order.
 void emb_csr_positions(const int* members, int64_t n, int* pos, hipStream_t s);
 void wd_emb_backward_bf16(const bf16_t* dX, int ldx, const float* dwide, const int64_t* inv, int64_t B, int F, int D,

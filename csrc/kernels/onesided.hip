@@ -856,9 +856,9 @@ void HipApplier::ApplyClock(int t, int64_t c, int world) {
                        reinterpret_cast<int2*>(p.rs), stamp);
     dim3 ga((unsigned)std::max<int64_t>(1, std::min<int64_t>((p.cap * 8 + 255) / 256, 8192 / world)), (unsigned)world);
     if (p.bf16)
-      hipLaunchKernelGGL(ps_clock_adagrad_kernel<true>, ga, 256, 0, stream_, (void*)p.table, p.ld, p.state, p.state2, D1,
-                         p.inbox, stride, off, p.cap, p.base, p.W, world, reinterpret_cast<const int2*>(p.rs), stamp,
-                         p.lr, p.eps, step, p.seed);
+      hipLaunchKernelGGL(ps_clock_adagrad_kernel<true>, ga, 256, 0, stream_, (void*)p.table, p.ld, p.state, p.state2,
+                         D1, p.inbox, stride, off, p.cap, p.base, p.W, world, reinterpret_cast<const int2*>(p.rs),
+                         stamp, p.lr, p.eps, step, p.seed);
     else
       hipLaunchKernelGGL(ps_clock_adagrad_kernel<false>, ga, 256, 0, stream_, (void*)p.table, p.ld, p.state, p.state2,
                          D1, p.inbox, stride, off, p.cap, p.base, p.W, world, reinterpret_cast<const int2*>(p.rs),

@@ -8,8 +8,6 @@
 #include <utility>
 #include <vector>
 
-#include <type_traits>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -225,8 +223,7 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
                                                       const float* __restrict__ wide, const float* __restrict__ y,
                                                       bf16_t* __restrict__ dH, float* dw, float* db, float* dwide,
                                                       float* loss_sum, float* colsum, float scale,
-                                                      float* __restrict__ slab, unsigned* ticket,
-                                                      const int* __restrict__ pos, float* __restrict__ dws, int F) {
+                                                      float* __restrict__ slab, unsigned* ticket) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -271,9 +268,6 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
         dbl += dz;
         lossl += fmaxf(zz, 0.f) - zz * label + log1pf(__expf(-fabsf(zz)));
       }
-      // the wide gradient of each of the sample's F lookups, at the lookup's member-order row (the
-      // embedding backward then reads it contiguously instead of gathering dwide[members[m] / F])
-      if (pos && lane < F) dws[pos[b * F + lane]] = dz;
       float gv[PER_LANE];
 #pragma unroll
       for (int j = 0; j < PER_LANE; ++j) {
@@ -386,8 +380,7 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
 
 void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
-             float grad_scale, hipStream_t s, const int* pos, float* dws, int F) {
-  if (pos && (F < 1 || F > 64 || !dws)) throw std::runtime_error("wd_head: member-order dwide needs 1 <= F <= 64");
+             float grad_scale, hipStream_t s) {
   if (B <= 0) return;
   const int block = 64 * kHeadWaves;
   // per-block LDS reduction, partial rows, the last block folds them (one block per CU at most)
@@ -413,13 +406,13 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
   if (grid > 256) throw std::runtime_error("wd_head: at most 256 blocks");
   switch (Hd) {
     case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, pos, dws, F); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
     case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, pos, dws, F); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
     case 64 * 4: hipLaunchKernelGGL(wd_head_kernel<4>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, pos, dws, F); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
     case 64 * 8: hipLaunchKernelGGL(wd_head_kernel<8>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, pos, dws, F); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
     default: throw std::runtime_error("wd_head: Hd must be 64, 128, 256 or 512, got " + std::to_string(Hd));
   }
   MINIPS_HIP_CHECK(hipGetLastError());
@@ -847,7 +840,7 @@ __global__ __launch_bounds__(256) void emb_seg_det_kernel(const TX* __restrict__
                                                           const int* __restrict__ members,
                                                           const int* __restrict__ memrow, int total,
                                                           TO* __restrict__ out, int row_stride,
-                                                          float* __restrict__ part, bool dw_member) {
+                                                          float* __restrict__ part) {
   constexpr int L = D / VW, PER = 64 / L, PW = PER * G;
   const int lane = threadIdx.x & 63, sub = lane / L, l = lane % L;
   const bool wide = dwide != nullptr;
@@ -877,8 +870,7 @@ __global__ __launch_bounds__(256) void emb_seg_det_kernel(const TX* __restrict__
         const TX* src;
         if (SORTED) {
           src = dX + (int64_t)(m < b ? m : a) * D + VW * l;
-          // dw_member: dwide is already in member order (wd_head wrote it through the positions)
-          bb[q] = (wide && l == 0 && m < b) ? (dw_member ? m : members[m] / F) : 0;
+          bb[q] = (wide && l == 0 && m < b) ? members[m] / F : 0;
         } else {
           const int j = m < b ? members[m] : members[a];
           bb[q] = j / F;
@@ -1074,62 +1066,31 @@ void emb_build_csr(const int64_t* inv, int64_t B, int F, int U, int* ws, int* me
 
 constexpr int kSegG = 16, kSegBatch = 8, kSegVW = 4;
 
-constexpr int seg_per_piece(int D, int vw = kSegVW) { return (64 / (D / vw)) * kSegG; }
-
-// MINIPS_EMB_VW (A/B knob, read once): 4 (default) or 8 gradient values per lane of a lookup row --
-// 8 moves a bf16 row's 64 bytes with 16-byte loads over 4 lanes (16 rows per wave instruction)
-static int emb_seg_vw() {
-  static const int v = [] {
-    const char* e = std::getenv("MINIPS_EMB_VW");
-    return e && std::atoi(e) == 8 ? 8 : 4;
-  }();
-  return v;
-}
-// MINIPS_EMB_BATCH (A/B knob, read once): lookups whose loads a lane group keeps in flight at once
-// (8 default; 16 = a group's whole G-lookup run in one round trip)
-static int emb_seg_batch() {
-  static const int v = [] {
-    const char* e = std::getenv("MINIPS_EMB_BATCH");
-    return e && std::atoi(e) == 16 ? 16 : kSegBatch;
-  }();
-  return v;
-}
+constexpr int seg_per_piece(int D) { return (64 / (D / kSegVW)) * kSegG; }
 
 int64_t emb_seg_part_floats(int64_t total, int D) {
-  const int64_t pw = std::min(seg_per_piece(D, 4), seg_per_piece(D, 8));  // (sized for either width)
+  const int64_t pw = seg_per_piece(D);
   return 2 * ((total + pw - 1) / pw) * seg_part_stride(D);
 }
 
 template <typename TX, typename TO>
 static void emb_seg_det(const TX* dX, int ldx, const float* dwide, int64_t B, int F, int D, const int* members,
-                        const int* memrow, TO* out, int row_stride, float* part, hipStream_t s, bool sorted_rows,
-                        bool dw_member) {
-  if (dw_member && !sorted_rows) throw std::runtime_error("emb backward: member-order dwide needs sorted rows");
+                        const int* memrow, TO* out, int row_stride, float* part, hipStream_t s, bool sorted_rows) {
   const int total = (int)(B * F);
-  const int vw = std::is_same<TX, bf16_t>::value && sorted_rows ? emb_seg_vw() : kSegVW;
-  const int64_t pw = seg_per_piece(D, vw);
+  const int64_t pw = seg_per_piece(D);
   const int64_t pieces = (total + pw - 1) / pw;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((pieces + 3) / 4, 65535));
   const int fix_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((pieces + 3) / 4, 4096));  // a wave per piece
-#define MINIPS_SEG_DET_VW(DD, VV)                                                                                  \
-  if (sorted_rows && emb_seg_batch() == 16)                                                                      \
-    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, 16, true, VV>), blocks, 256, 0, s, dX, ldx,          \
-                       dwide, F, members, memrow, total, out, row_stride, part, dw_member);                                  \
-  else if (sorted_rows)                                                                                           \
-    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, true, VV>), blocks, 256, 0, s, dX, ldx,   \
-                       dwide, F, members, memrow, total, out, row_stride, part, dw_member);                                  \
+#define MINIPS_SEG_DET(DD)                                                                                         \
+  if (sorted_rows)                                                                                                \
+    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, true, kSegVW>), blocks, 256, 0, s, dX,    \
+                       ldx, dwide, F, members, memrow, total, out, row_stride, part);                             \
   else                                                                                                            \
-    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, false, VV>), blocks, 256, 0, s, dX, ldx,  \
-                       dwide, F, members, memrow, total, out, row_stride, part, dw_member);                                  \
+    hipLaunchKernelGGL((emb_seg_det_kernel<TX, TO, DD, kSegG, kSegBatch, false, kSegVW>), blocks, 256, 0, s, dX,   \
+                       ldx, dwide, F, members, memrow, total, out, row_stride, part);                             \
   if (pieces > 1)                                                                                                 \
-    hipLaunchKernelGGL((emb_seg_fix_kernel<TO, DD, VV, seg_per_piece(DD, VV)>), fix_blocks, 256, 0, s, memrow,     \
+    hipLaunchKernelGGL((emb_seg_fix_kernel<TO, DD, kSegVW, seg_per_piece(DD)>), fix_blocks, 256, 0, s, memrow,     \
                        total, part, out, row_stride, dwide != nullptr);
-#define MINIPS_SEG_DET(DD)          \
-  if (vw == 8 && DD >= 32) {        \
-    MINIPS_SEG_DET_VW(DD, 8)        \
-  } else {                          \
-    MINIPS_SEG_DET_VW(DD, kSegVW)   \
-  }
   switch (D) {
     case 16:
       MINIPS_SEG_DET(16)
@@ -1144,27 +1105,26 @@ static void emb_seg_det(const TX* dX, int ldx, const float* dwide, int64_t B, in
       throw std::runtime_error("emb_backward_seg: D must be 16, 32 or 64");
   }
 #undef MINIPS_SEG_DET
-#undef MINIPS_SEG_DET_VW
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
 void emb_backward_csr(const void* dX, bool bf16, int ldx, const float* dwide, int64_t B, int F, int D,
                       const int* members, const int* memrow, void* out, bool out_bf16, int row_stride, float* part,
-                      hipStream_t s, bool sorted_rows, bool dw_member) {
+                      hipStream_t s, bool sorted_rows) {
   if (B <= 0) return;
   if (row_stride < D + (dwide ? 1 : 0)) throw std::runtime_error("emb_backward_csr: row_stride too small");
   if (bf16 && out_bf16)
     emb_seg_det(static_cast<const bf16_t*>(dX), ldx, dwide, B, F, D, members, memrow, static_cast<bf16_t*>(out),
-                row_stride, part, s, sorted_rows, dw_member);
+                row_stride, part, s, sorted_rows);
   else if (bf16)
     emb_seg_det(static_cast<const bf16_t*>(dX), ldx, dwide, B, F, D, members, memrow, static_cast<float*>(out),
-                row_stride, part, s, sorted_rows, dw_member);
+                row_stride, part, s, sorted_rows);
   else if (out_bf16)
     emb_seg_det(static_cast<const float*>(dX), ldx, dwide, B, F, D, members, memrow, static_cast<bf16_t*>(out),
-                row_stride, part, s, sorted_rows, dw_member);
+                row_stride, part, s, sorted_rows);
   else
     emb_seg_det(static_cast<const float*>(dX), ldx, dwide, B, F, D, members, memrow, static_cast<float*>(out),
-                row_stride, part, s, sorted_rows, dw_member);
+                row_stride, part, s, sorted_rows);
 }
 
 __global__ void emb_csr_positions_kernel(const int* __restrict__ members, int64_t n, int* __restrict__ pos) {
@@ -1185,7 +1145,7 @@ void emb_backward_segment(const void* dX, bool bf16, int ldx, const float* dwide
   int* members = ws + 3 * U + 1 + (U / 1024 + 1);
   int* memrow = members + B * F;
   emb_build_csr(inv, B, F, U, ws, members, memrow, s);
-  emb_backward_csr(dX, bf16, ldx, dwide, B, F, D, members, memrow, out, out_bf16, row_stride, part, s, false, false);
+  emb_backward_csr(dX, bf16, ldx, dwide, B, F, D, members, memrow, out, out_bf16, row_stride, part, s, false);
 }
 
 }  // namespace minips_k

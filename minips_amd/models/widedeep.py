@@ -17,7 +17,6 @@ Step (every kernel is a gfx950 HIP kernel; comm is RCCL):
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import torch
@@ -112,10 +111,12 @@ _DENSE_ON_SIDE = True
 # WD_W1_LATE on: fork the layer-1 weight gradient after the embedding dgrad (beside the
 # embedding backward rather than beside the dgrad: two big GEMMs at once only share the CUs);
 # round 3 measured it 5 % slower (profiles/r3/ab_wd_r3.txt)
-_W1_LATE = os.environ.get("MINIPS_WD_W1_LATE", "0") == "1"
+# (round 6, the planning mid-step: 0.363 vs 0.342-0.344 ms/step, profiles/r6/ab_wd_r6.txt)
+_W1_LATE = False
 # the one-rank side-stream Adam waits for the compute stream only up to the embedding dgrad (the
-# last reader of W), not up to the end of the step's issue (ADAM_EDGE=end: the round-5 fork)
-_ADAM_AFTER_DGRAD = os.environ.get("MINIPS_WD_ADAM_EDGE", "dgrad") == "dgrad"
+# last reader of W), not up to the end of the step's issue (off: the round-5 fork at the end):
+# 0.3514-0.3553 vs 0.3564-0.3568 ms/step (profiles/r6/ab_wd_r6.txt)
+_ADAM_AFTER_DGRAD = True
 # ROWIDX off: the input assembly follows inv -> uniq instead of the planner's per-lookup rows
 _ROWIDX = True
 # the dense forward and the backward GEMM chain up to the embedding dgrad, recorded once per set of
@@ -124,9 +125,6 @@ _ROWIDX = True
 # 0.368-0.370 either way) and at 8 emulated ranks (0.491-0.499 vs 0.488-0.502 ms), where the step
 # waits on the planning's count exchange instead (profiles/r5/host_issue.txt). False: op by op.
 _REPLAY = True
-# the head writes each lookup's wide gradient at its member-order row (plan positions), so the
-# embedding backward reads it contiguously instead of gathering dwide[members[m] / F] (DWIDE_MEMBER off)
-_DWIDE_MEMBER = os.environ.get("MINIPS_WD_DWIDE_MEMBER", "1") == "1"
 
 
 def _wgrad(dH, H, Gw, sink=None):
@@ -244,7 +242,6 @@ class WideDeep(LookaheadPlans):
                 dX=torch.empty(B, cfg.F * cfg.emb_dim, **bf),  # bf16: half the bytes of the emb backward
                 wide=torch.empty(B, dtype=torch.float32, device=dev),
                 dwide=torch.empty(B, dtype=torch.float32, device=dev),
-                dwide_m=torch.empty(B * cfg.F, dtype=torch.float32, device=dev),  # member order (_DWIDE_MEMBER)
                 loss=torch.zeros(1, dtype=torch.float32, device=dev),
             )
         return self._bufs[B]
@@ -331,11 +328,8 @@ class WideDeep(LookaheadPlans):
         else:
             self._forward(b, P)
         # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
-        sorted_rows = plan.csr is not None and len(plan.csr) >= 3 and plan.csr[2] is not None
-        dw_member = sorted_rows and _DWIDE_MEMBER and dense.is_cuda
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
-                    b["dwide"], b["loss"], self.view(G, "b3"), scale,
-                    pos=plan.csr[2] if dw_member else None, dws=b["dwide_m"] if dw_member else None)
+                    b["dwide"], b["loss"], self.view(G, "b3"), scale)
         ph.__exit__(None, None, None)
         ph = phase("wd.bwd_dense")
         ph.__enter__()
@@ -355,6 +349,7 @@ class WideDeep(LookaheadPlans):
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
         # (members, memrow, positions or None[, rowstart]): positions -> the dgrad writes the rows sorted
+        sorted_rows = plan.csr is not None and len(plan.csr) >= 3 and plan.csr[2] is not None
         if sorted_rows:
             ops.linear_dgrad(b["dH1"], self.view(P, "W1"), n_cols=F * D, out=b["dX"].view(B * F, D),
                              perm=plan.csr[2], seg=D)
@@ -379,8 +374,7 @@ class WideDeep(LookaheadPlans):
         ph = phase("wd.emb_push")
         ph.__enter__()
         dXe = b["dX"].view(B * F, D) if sorted_rows else b["dX"]
-        self.emb.add_lookup_grads(plan, dXe, b["dwide_m"] if dw_member else b["dwide"], F, D,  # the table reduces
-                                  sorted_rows=sorted_rows, dw_member=dw_member)
+        self.emb.add_lookup_grads(plan, dXe, b["dwide"], F, D, sorted_rows=sorted_rows)  # the table reduces
         self.emb.clock()
         issue_next("push")
         ph.__exit__(None, None, None)

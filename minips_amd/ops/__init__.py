@@ -569,13 +569,9 @@ def wd_assemble_tab(dense, table, index, base, inv, F, D, X, wide_logit, ones_co
     return wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col, zero)
 
 
-def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum=None, grad_scale=1.0, pos=None,
-            dws=None):
-    """... ``pos`` (int32 [B*F], the member-order row of each lookup) with ``dws`` (fp32 [B*F]): also
-    dws[pos[b*F + f]] = dwide[b] -- the wide gradient in the embedding backward's member order."""
+def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum=None, grad_scale=1.0):
     if _gpu(H):
-        kernels().wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, float(grad_scale),
-                          pos, dws)
+        kernels().wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, float(grad_scale))
         return
     h = H.float()
     z = h @ w.float() + b0.float() + wide_logit
@@ -590,8 +586,6 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
     dw += (dz.unsqueeze(1) * h).sum(0)
     if dH_colsum is not None:
         dH_colsum += g.float().sum(0)
-    if pos is not None:
-        dws[pos.long()] = dz.repeat_interleave(pos.numel() // dz.numel())
 
 
 def emb_csr_positions(members):
@@ -614,24 +608,19 @@ def emb_build_csr(inv, F, U, zeroed=None, counts_ready=False):
     return order.to(torch.int32), inv[order].to(torch.int32)
 
 
-def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, csr=None, sorted_rows=False, dw_member=False):
+def wd_emb_backward(dX, dwide, inv, F, D, grad_rows, x_off=0, csr=None, sorted_rows=False):
     """grad_rows[u, :D] = sum of dX[b, x_off + f*D : ...] over the lookups (b, f) with
     inv[b*F+f] == u; column D likewise sums dwide[b] when given, columns D+1.. are 0. On the GPU
     (D 16 / 32 / 64) every row that has lookups (every unique row of a plan) is written exactly
     once, in a fixed summation order -- the same bits on every run; rows without lookups are left
     untouched -- and ``grad_rows`` may be fp32 or bf16 (the multi-rank push payload);
     the CPU reference adds into grad_rows, so callers pass a zeroed buffer. ``sorted_rows``: dX is
-    [B*F, D] in the CSR's member order (row m = lookup csr[0][m]; linear_dgrad(perm=csr[2]) writes it).
-    ``dw_member`` (sorted_rows): dwide is [B*F] in member order (wd_head's dws), not [B]."""
+    [B*F, D] in the CSR's member order (row m = lookup csr[0][m]; linear_dgrad(perm=csr[2]) writes it)."""
     if _gpu(dX):
         members, memrow = (csr[0], csr[1]) if csr is not None else (None, None)
         kernels().wd_emb_backward(dX, dwide, inv, int(F), int(D), grad_rows, int(x_off), members, memrow,
-                                  bool(sorted_rows), bool(dw_member))
+                                  bool(sorted_rows))
         return grad_rows
-    if dw_member:  # back to one value per sample
-        dl = torch.empty_like(dwide)
-        dl[csr[0].long()] = dwide
-        dwide = dl.view(-1, F)[:, 0].contiguous()
     if sorted_rows:  # back to lookup order
         un = torch.empty_like(dX)
         un[csr[0].long()] = dX

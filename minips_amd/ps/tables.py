@@ -1215,7 +1215,7 @@ class SparseTable:
 
     @traced("sparse.add_lookup_grads")
     def add_lookup_grads(self, plan: SparsePlan, dX: torch.Tensor, dwide, F: int, D: int, x_off: int = 0,
-                         sorted_rows: bool = False, dw_member: bool = False):
+                         sorted_rows: bool = False):
         """Push the gradient of every lookup of ``plan``'s batch: dX[b, x_off + f*D : +D] for
         lookup (b, f) (+ dwide[b] into column D of the row). The table reduces them per unique
         row -- the Add of the reference's worker, which sends one summed row per key -- with the
@@ -1225,8 +1225,7 @@ class SparseTable:
         gdt = self.push_dtype if self.comm.world > 1 else getattr(self, "grad_dtype", torch.float32)
         grad_rows = (torch.empty if dev.type == "cuda" else torch.zeros)(max(plan.cap, 1), self.width, dtype=gdt,
                                                                          device=dev)
-        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, grad_rows, x_off=x_off, csr=plan.csr, sorted_rows=sorted_rows,
-                            dw_member=dw_member)
+        ops.wd_emb_backward(dX, dwide, plan.inv, F, D, grad_rows, x_off=x_off, csr=plan.csr, sorted_rows=sorted_rows)
         self.add(plan, grad_rows)
 
     def add_keys(self, keys: torch.Tensor, vals: torch.Tensor):
