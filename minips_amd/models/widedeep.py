@@ -127,9 +127,17 @@ _ROWIDX = True
 _REPLAY = True
 
 
-def _wgrad(dH, H, Gw, sink=None):
+# per-layer split-K of the weight gradients (W1, W2, W3), A/B knob MINIPS_WD_WGRAD_SPLITS="8,16,16":
+# isolated the 320-workgroup target's 6 / 10 / 16 splits run 50.6 / 33.9 / 17.7 us against 42.0 / 26.8 /
+# 17.7 at 8 / 16 / 16 (profiles/r6/wgrad_split_sweep.txt); None: the workgroup target
+_WGRAD_SPLITS = tuple(int(v) for v in __import__("os").environ["MINIPS_WD_WGRAD_SPLITS"].split(",")) \
+    if __import__("os").environ.get("MINIPS_WD_WGRAD_SPLITS") else None
+
+
+def _wgrad(dH, H, Gw, sink=None, layer=None):
     # (round 4: the hipBLASLt alternative, WD_WGRAD=lib, measured slower and removed)
-    return ops.linear_wgrad(dH, H, Gw, blocks=_WGRAD_BLOCKS, defer=sink)
+    split = _WGRAD_SPLITS[layer - 1] if _WGRAD_SPLITS is not None and layer is not None else None
+    return ops.linear_wgrad(dH, H, Gw, split_k=split, blocks=_WGRAD_BLOCKS, defer=sink)
 
 
 def _align(n, a=8):
@@ -359,7 +367,7 @@ class WideDeep(LookaheadPlans):
         w_read = side.point() if _ADAM_AFTER_DGRAD and self.comm.world == 1 else None
         if _W1_LATE:  # the layer-1 weight gradient beside the memory-bound embedding backward instead
             with side.fork():
-                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
+                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink, 1)
         # an async dense clock (its own stream) needs only the weight gradients: issued from the
         # side stream it starts as soon as the last wgrad ends, beside the embedding backward and
         # the sparse push, instead of behind them
@@ -420,16 +428,16 @@ class WideDeep(LookaheadPlans):
         forked beside it: GEMM-family ops and forks only (replayable, see layers.Replayer)."""
         k3 = self.k_in[2]
         with side.fork():
-            _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink)
+            _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink, 3)
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"])
         with side.fork():
             ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
-            _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink)
+            _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink, 2)
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         self._bucket_done(1, side)  # (layers 2, 3 and the head: their weight gradients are issued)
         if not _W1_LATE:
             with side.fork():
-                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
+                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink, 1)
 
     def _bucket_done(self, layer: int, side):
         """Every layer >= ``layer`` has its weight gradient issued (on the side stream): the buckets
