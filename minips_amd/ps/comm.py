@@ -601,18 +601,23 @@ class LoopbackComm(Comm):
         self.channels = int(channels if channels is not None else os.environ.get("MINIPS_EMU_CHANNELS", "16"))
         self.wire_us = 0.0  # modelled link time issued so far (bench.py diag)
 
+    def wire_time_us(self, kind: str, nbytes: int) -> float:
+        """Modelled link time (us) of one collective moving ``nbytes`` on this rank: "a2a" (every peer
+        segment on its own link) or "rs" / "ag" (ring: one link per hop; direct: all P - 1 links)."""
+        if self.wire == "none":
+            return 0.0
+        P, bw = self.world, self.link_gbps * 1e3  # bytes per us
+        if kind == "a2a" or self.wire == "direct":
+            us = nbytes * (P - 1) / P / ((P - 1) * bw)
+        else:
+            us = (P - 1) / P * nbytes / bw
+        return us + self.latency_us
+
     def _wire(self, kind: str, nbytes: int):
         """The modelled link time of one collective, spun on the current stream (GPU only)."""
         if self.wire == "none" or self.device.type != "cuda":
             return
-        P, bw = self.world, self.link_gbps * 1e3  # bytes per us
-        if kind == "a2a":
-            us = nbytes * (P - 1) / P / ((P - 1) * bw)
-        elif self.wire == "ring":
-            us = (P - 1) / P * nbytes / bw
-        else:
-            us = (P - 1) / P * nbytes / ((P - 1) * bw)
-        us += self.latency_us
+        us = self.wire_time_us(kind, nbytes)
         self.wire_us += us
         from .._native import kernels
 

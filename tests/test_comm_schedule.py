@@ -148,3 +148,25 @@ def test_emulated_rank_issues_the_real_rank_program(fn, cons):
     assert emu == real
     assert all(l == l and abs(l) < 1e6 for l in losses)
     assert model.emb.rows_local == model.emb.bounds_list[1] and model.dense.shard * 4 == model.dense.n_pad
+
+
+def test_loopback_wire_model_matches_survey_formulas():
+    """LoopbackComm's modelled link times (SURVEY §5.8, 7 xGMI links of 153 GB/s at 8 ranks): an
+    all-to-all puts every peer segment on its own link, a ring RS/AG is per-link bound, a direct
+    one uses all 7 links; plus the per-collective latency."""
+    import pytest
+
+    from minips_amd.ps.comm import LoopbackComm
+
+    S = 8 << 20
+    ring = LoopbackComm(8, wire="ring", link_gbps=153, latency_us=8, device=torch.device("cpu"))
+    direct = LoopbackComm(8, wire="direct", link_gbps=153, latency_us=8, device=torch.device("cpu"))
+    none = LoopbackComm(8, device=torch.device("cpu"))
+    bw = 153e3  # bytes per us
+    assert ring.wire_time_us("rs", S) == pytest.approx(7 / 8 * S / bw + 8)
+    assert direct.wire_time_us("ag", S) == pytest.approx(S / (8 * bw) + 8)
+    assert ring.wire_time_us("a2a", S) == pytest.approx(S / (8 * bw) + 8)
+    assert direct.wire_time_us("a2a", S) == ring.wire_time_us("a2a", S)
+    assert none.wire_time_us("rs", S) == 0.0
+    with pytest.raises(ValueError):
+        LoopbackComm(8, wire="mesh", device=torch.device("cpu"))
