@@ -572,7 +572,7 @@ void wd_assemble_tab(const at::Tensor& dense, const at::Tensor& tab, const at::T
 
 void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& wide_logit,
              const at::Tensor& labels, at::Tensor& dH, at::Tensor& dw, at::Tensor& db, at::Tensor& dwide,
-             at::Tensor& loss_sum, const c10::optional<at::Tensor>& dH_colsum, double grad_scale) {
+             at::Tensor& loss_sum, const c10::optional<at::Tensor>& dH_colsum, double grad_scale, bool defer_fold) {
   for (auto* t : {&H, &w, &b0, &wide_logit, &labels}) check_gpu(*t, "wd_head input");
   check_dtype(H, at::kBFloat16, "H");
   check_dtype(w, at::kBFloat16, "w");
@@ -584,7 +584,33 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
   c10::hip::HIPGuardMasqueradingAsCUDA g(H.device());
   minips_k::wd_head(ptr<bf16_t>(H), H.size(0), (int)H.size(1), ptr<bf16_t>(w), ptr<bf16_t>(b0),
                     ptr<float>(wide_logit), ptr<float>(labels), ptr<bf16_t>(dH), ptr<float>(dw), ptr<float>(db),
-                    ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H));
+                    ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H), defer_fold);
+}
+
+struct HeadFoldLaunch {
+  int64_t B;
+  int Hd;
+  float *dw, *db, *loss, *colsum;
+  void launch(hipStream_t s) const { minips_k::wd_head_fold(B, Hd, dw, db, loss, colsum, s); }
+};
+
+HeadFoldLaunch prepare_head_fold(int64_t B, int64_t Hd, at::Tensor& dw, at::Tensor& db, at::Tensor& loss_sum,
+                                 const c10::optional<at::Tensor>& dH_colsum) {
+  for (auto* t : {&dw, &db, &loss_sum}) {
+    check_gpu(*t, "wd_head_fold output");
+    check_dtype(*t, at::kFloat, "wd_head_fold output");
+  }
+  TORCH_CHECK(dw.numel() == Hd && db.numel() >= 1 && loss_sum.numel() >= 1, "wd_head_fold: dw [Hd], db, loss");
+  float* cs = opt_ptr<float>(dH_colsum, at::kFloat, "dH_colsum");
+  TORCH_CHECK(!cs || dH_colsum->numel() >= Hd, "wd_head_fold: dH_colsum >= Hd floats");
+  return HeadFoldLaunch{B, (int)Hd, ptr<float>(dw), ptr<float>(db), ptr<float>(loss_sum), cs};
+}
+
+// the totals of the last wd_head(defer_fold=True) of this device (same B, Hd), on dw's stream
+void wd_head_fold(int64_t B, int64_t Hd, at::Tensor& dw, at::Tensor& db, at::Tensor& loss_sum,
+                  const c10::optional<at::Tensor>& dH_colsum) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dw.device());
+  prepare_head_fold(B, Hd, dw, db, loss_sum, dH_colsum).launch(stream_of(dw));
 }
 
 // Lookup CSR grouped by unique row (members/memrow int32 [B*F]) for U (upper-bound) rows.
@@ -1545,6 +1571,17 @@ class LaunchList {
     ops_.push_back([c, k](const hipStream_t* s) { c.launch(s[k]); });
   }
 
+  void wd_head_fold(int64_t B, int64_t Hd, at::Tensor& dw, at::Tensor& db, at::Tensor& loss_sum,
+                    const c10::optional<at::Tensor>& dH_colsum) {
+    c10::hip::HIPGuardMasqueradingAsCUDA gd(dw.device());
+    const HeadFoldLaunch f = prepare_head_fold(B, Hd, dw, db, loss_sum, dH_colsum);
+    const int k = slot(dw);
+    f.launch(rec_[k]);
+    hold({dw, db, loss_sum});
+    if (dH_colsum.has_value()) hold({*dH_colsum});
+    ops_.push_back([f, k](const hipStream_t* s) { f.launch(s[k]); });
+  }
+
   // stream ``dst`` waits for the work issued so far on stream ``src`` (raw stream handles of the
   // recording: the list's two streams)
   void fork(int64_t src, int64_t dst) {
@@ -1759,7 +1796,8 @@ class GpuAsyncServer {
     d.rs = reinterpret_cast<void*>(rs);
     TORCH_CHECK(!coalesce || opt != minips_k::kPsRowwiseAdagrad || hash_cap != 0 || rs != 0,
                 "clock-coalesced row-wise Adagrad needs its (stamp, index) table");
-    TORCH_CHECK(W % 4 == 0 && W <= 64 && cap < (int64_t)INT32_MAX, "sparse rows: W % 4 == 0, W <= 64");
+    TORCH_CHECK(cap < (int64_t)INT32_MAX, "sparse inbox capacity");
+    TORCH_CHECK(rs == 0 || (W % 4 == 0 && W <= 64), "clock-coalesced sparse rows: W % 4 == 0, W <= 64");
     applier_.SetSparse((int)t, d);
     server_.SetCoalesce((int)t, coalesce);
     server_.Enable((int)t);
@@ -1944,7 +1982,10 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("wd_assemble", &wd_assemble, py::arg("dense"), py::arg("rows"), py::arg("inv"), py::arg("F"),
         py::arg("D"), py::arg("X"), py::arg("wide_logit"), py::arg("ones_col") = -1, py::arg("zero") = py::none());
-  m.def("wd_head", &wd_head);
+  m.def("wd_head", &wd_head, py::arg("H"), py::arg("w"), py::arg("b0"), py::arg("wide_logit"), py::arg("labels"),
+        py::arg("dH"), py::arg("dw"), py::arg("db"), py::arg("dwide"), py::arg("loss_sum"), py::arg("dH_colsum"),
+        py::arg("grad_scale"), py::arg("defer_fold") = false);
+  m.def("wd_head_fold", &wd_head_fold);
   m.def("wd_assemble_tab", &wd_assemble_tab);
   m.def("owner_slots", &owner_slots, py::arg("own_inv"), py::arg("splits"), py::arg("cap"));
   m.def("owner_rows_adagrad", &owner_rows_adagrad, py::arg("table"), py::arg("state"), py::arg("state2"),
@@ -2027,6 +2068,7 @@ PYBIND11_MODULE(_kernels, m) {
       .def("gemm", &LaunchList::gemm)
       .def("gemm_slab", &LaunchList::gemm_slab)
       .def("colsum_bf16", &LaunchList::colsum_bf16)
+      .def("wd_head_fold", &LaunchList::wd_head_fold)
       .def("fork", &LaunchList::fork)
       .def("run", &LaunchList::run)
       .def("size", &LaunchList::size);

@@ -144,7 +144,11 @@ void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t 
                      const int32_t* rowidx = nullptr);  // rowidx: lookup j's row + base (plan_sorted)
 void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
-             float grad_scale, hipStream_t s);
+             float grad_scale, hipStream_t s, bool defer_fold = false);
+// defer_fold: the head leaves its per-block partial rows in a per-device slab and wd_head_fold
+// (same B / Hd, a later kernel on any stream ordered after it, before the next head of the
+// device) adds their totals into dw / db / loss_sum / dH_colsum.
+void wd_head_fold(int64_t B, int Hd, float* dw, float* db, float* loss_sum, float* dH_colsum, hipStream_t s);
 // Embedding backward: grad_rows[inv[b*F+f], 0:D] += dX[b, f*D : (f+1)*D] (fp32 dX, ld ldx),
 // grad_rows[inv[b*F+f], D] += dwide[b] when dwide != null (grad_rows fp32 [U, row_stride],
 // pre-zeroed).

@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
                                                       const float* __restrict__ wide, const float* __restrict__ y,
                                                       bf16_t* __restrict__ dH, float* dw, float* db, float* dwide,
                                                       float* loss_sum, float* colsum, float scale,
-                                                      float* __restrict__ slab, unsigned* ticket) {
+                                                      float* __restrict__ slab, unsigned* ticket, int defer) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -307,6 +307,29 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
   const int grp = blockIdx.x / kHeadGroup;
   const int g0 = grp * kHeadGroup, gn = min(kHeadGroup, nb - g0);
   float* row = slab + (int64_t)blockIdx.x * NP;
+  if (defer) {  // wd_head_fold (a later kernel, off the dgrad chain) folds the partial rows
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < kHeadWaves; ++w) {
+        a += red[0][w][c];
+        b += red[1][w][c];
+      }
+      row[c] = a;
+      row[NC + c] = b;
+    }
+    if (threadIdx.x == 0) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < kHeadWaves; ++w) {
+        a += red_s[0][w];
+        b += red_s[1][w];
+      }
+      row[2 * NC] = a;
+      row[2 * NC + 1] = b;
+    }
+    return;
+  }
   for (int c = threadIdx.x; c < NC; c += blockDim.x) {
     float a = 0.f, b = 0.f;
 #pragma unroll
@@ -378,17 +401,52 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
   }
 }
 
-void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
-             const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
-             float grad_scale, hipStream_t s) {
-  if (B <= 0) return;
-  const int block = 64 * kHeadWaves;
-  // per-block LDS reduction, partial rows, the last block folds them (one block per CU at most)
-  // 256 blocks (every CU, one sample iteration per wave): W&D 0.3632-0.3637 vs 0.3672-0.3678 ms at
-  // 128 (profiles/r4/ab_wd_knobs.txt); the two-level fold takes at most 256
-  constexpr int max_blocks = 256;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(max_blocks, (B + 63) / 64));
-  // the partial slab + ticket of this device: allocated once (zero ticket), before any capture
+// The deferred fold of wd_head's per-block partial rows (slab [nb][2*NC + 2]) into dw / colsum /
+// db / loss: a block owns 32 columns, its 16 row chunks each sum their rows in order, then chunk
+// order in LDS -- one fixed summation order (deterministic). Issued on the weight-gradient stream
+// right behind the head, it takes the two ticketed fold levels (~8 us of the head's ~17, the last
+// blocks waiting on each other's write-through round trips) off the dgrad chain.
+constexpr int kFoldCols = 32, kFoldChunks = 16;
+__global__ __launch_bounds__(kFoldCols * kFoldChunks) void wd_head_fold_kernel(const float* __restrict__ slab,
+                                                                               int nb, int NC, float* dw,
+                                                                               float* colsum, float* db,
+                                                                               float* loss_sum) {
+  __shared__ float red[kFoldChunks][kFoldCols + 1];
+  const int NP = 2 * NC + 2;
+  const int cl = threadIdx.x % kFoldCols, ch = threadIdx.x / kFoldCols;
+  const int c = blockIdx.x * kFoldCols + cl;
+  const int per = (nb + kFoldChunks - 1) / kFoldChunks;
+  const int r0 = ch * per, r1 = min(nb, r0 + per);
+  float acc = 0.f;
+  if (c < NP) {
+    for (int r = r0; r < r1; r += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = r + k < r1 ? slab[(int64_t)(r + k) * NP + c] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += v[k];
+    }
+  }
+  red[ch][cl] = acc;
+  __syncthreads();
+  if (ch != 0 || c >= NP) return;
+  float tot = 0.f;
+#pragma unroll
+  for (int k = 0; k < kFoldChunks; ++k) tot += red[k][cl];
+  if (c < NC) dw[c] += tot;
+  else if (c < 2 * NC) {
+    if (colsum) colsum[c - NC] += tot;
+  } else if (c == 2 * NC) *db += tot;
+  else *loss_sum += tot;
+}
+
+namespace {
+// 256 blocks (every CU, one sample iteration per wave): W&D 0.3632-0.3637 vs 0.3672-0.3678 ms at
+// 128 (profiles/r4/ab_wd_knobs.txt); the two-level fold takes at most 256
+int head_grid(int64_t B) { return (int)std::max<int64_t>(1, std::min<int64_t>(256, (B + 63) / 64)); }
+
+// the partial slab + ticket of this device: allocated once (zero ticket), before any capture
+void head_ws(float** slab, unsigned** ticket) {
   static thread_local std::vector<std::pair<int, void*>> ws_cache;
   int dev = 0;
   MINIPS_HIP_CHECK(hipGetDevice(&dev));
@@ -401,20 +459,46 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
     MINIPS_HIP_CHECK(hipMemset(ws, 0, slab_bytes + 256));
     ws_cache.push_back({dev, ws});
   }
-  float* slab = static_cast<float*>(ws);
-  unsigned* ticket = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + slab_bytes);
-  if (grid > 256) throw std::runtime_error("wd_head: at most 256 blocks");
+  *slab = static_cast<float*>(ws);
+  *ticket = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + slab_bytes);
+}
+}  // namespace
+
+void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
+             const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
+             float grad_scale, hipStream_t s, bool defer_fold) {
+  if (B <= 0) return;
+  const int block = 64 * kHeadWaves;
+  // per-block LDS reduction, partial rows; the last block folds them (one block per CU at most),
+  // or wd_head_fold does (defer_fold)
+  const int grid = head_grid(B), defer = defer_fold ? 1 : 0;
+  float* slab = nullptr;
+  unsigned* ticket = nullptr;
+  head_ws(&slab, &ticket);
   switch (Hd) {
     case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer); break;
     case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer); break;
     case 64 * 4: hipLaunchKernelGGL(wd_head_kernel<4>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer); break;
     case 64 * 8: hipLaunchKernelGGL(wd_head_kernel<8>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer); break;
     default: throw std::runtime_error("wd_head: Hd must be 64, 128, 256 or 512, got " + std::to_string(Hd));
   }
+  MINIPS_HIP_CHECK(hipGetLastError());
+}
+
+void wd_head_fold(int64_t B, int Hd, float* dw, float* db, float* loss_sum, float* dH_colsum, hipStream_t s) {
+  if (B <= 0) return;
+  if (Hd != 64 && Hd != 128 && Hd != 256 && Hd != 512)
+    throw std::runtime_error("wd_head_fold: Hd must be 64, 128, 256 or 512, got " + std::to_string(Hd));
+  float* slab = nullptr;
+  unsigned* ticket = nullptr;
+  head_ws(&slab, &ticket);
+  const int NP = 2 * Hd + 2;
+  hipLaunchKernelGGL(wd_head_fold_kernel, (NP + kFoldCols - 1) / kFoldCols, kFoldCols * kFoldChunks, 0, s, slab,
+                     head_grid(B), Hd, dw, dH_colsum, db, loss_sum);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 

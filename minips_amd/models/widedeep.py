@@ -44,8 +44,9 @@ class WideDeepConfig:
     # "collective": SparseTable / DenseTable over RCCL; "onesided": SSP / ASP with no collective on
     # the data path -- rows pulled one-sidedly from the owners' HBM, gradients pushed into the
     # owners' inboxes, row-wise Adagrad / Adam applied by each owner's server thread (ps/onesided.py);
-    # "auto" (default): one-sided for SSP / ASP (the reference's asynchronous servers, and faster on
-    # one MI355X: 0.402 vs 0.411 ms/step, profiles/r4/ssp_onesided_vs_collective.txt), collective for BSP
+    # "auto" (default): one-sided for SSP / ASP (the reference's asynchronous servers; on one MI355X
+    # 0.404 vs 0.400 ms/step, profiles/r6/ssp_onesided_vs_collective.txt -- no collective rendezvous
+    # at N > 1), collective for BSP
     transport: str = "auto"
     dense_transport: str | None = None  # (None: ``transport``) the dense table's, when it differs
     max_batch: int = 16384       # onesided: inbox slots hold max_batch * F gradient rows
@@ -125,19 +126,21 @@ _ROWIDX = True
 # 0.368-0.370 either way) and at 8 emulated ranks (0.491-0.499 vs 0.488-0.502 ms), where the step
 # waits on the planning's count exchange instead (profiles/r5/host_issue.txt). False: op by op.
 _REPLAY = True
+# the head's batch sums (last-layer weight/bias gradient, layer-3 bias gradient, loss) folded by a
+# separate kernel on the weight-gradient stream instead of by the head's last blocks: the two ticketed
+# fold levels leave the dgrad chain (head 17 -> 11 us in-step): 0.335-0.339 vs 0.344-0.345 ms/step
+# (profiles/r6/ab_wd_r6.txt). False: the round-5 in-kernel fold.
+_HEAD_DEFER = True
 
 
-# per-layer split-K of the weight gradients (W1, W2, W3), A/B knob MINIPS_WD_WGRAD_SPLITS="8,16,16":
-# isolated the 320-workgroup target's 6 / 10 / 16 splits run 50.6 / 33.9 / 17.7 us against 42.0 / 26.8 /
-# 17.7 at 8 / 16 / 16 (profiles/r6/wgrad_split_sweep.txt); None: the workgroup target
-_WGRAD_SPLITS = tuple(int(v) for v in __import__("os").environ["MINIPS_WD_WGRAD_SPLITS"].split(",")) \
-    if __import__("os").environ.get("MINIPS_WD_WGRAD_SPLITS") else None
-
-
-def _wgrad(dH, H, Gw, sink=None, layer=None):
+# (round 6: per-layer split-K of the weight gradients instead of the workgroup target -- isolated,
+# the target's 6 / 10 / 16 splits of W1 / W2 / W3 run 50.6 / 33.9 / 17.7 us against 42.0 / 26.8 /
+# 17.7 at 8 / 16 / 16 (profiles/r6/wgrad_split_sweep.txt) -- but in the step the faster, wider
+# splits crowd the dgrad chain: 0.363-0.366 ms at 8,16,16 vs 0.354-0.355 at the target, 6,16,16
+# 0.352-0.355 (profiles/r6/ab_wd_r6.txt); the knob was removed)
+def _wgrad(dH, H, Gw, sink=None):
     # (round 4: the hipBLASLt alternative, WD_WGRAD=lib, measured slower and removed)
-    split = _WGRAD_SPLITS[layer - 1] if _WGRAD_SPLITS is not None and layer is not None else None
-    return ops.linear_wgrad(dH, H, Gw, split_k=split, blocks=_WGRAD_BLOCKS, defer=sink)
+    return ops.linear_wgrad(dH, H, Gw, blocks=_WGRAD_BLOCKS, defer=sink)
 
 
 def _align(n, a=8):
@@ -304,8 +307,8 @@ class WideDeep(LookaheadPlans):
         with phase("wd.plan_next"):
             issue_next("start")
         pend_side = self.__dict__.pop("_side_pending", None)
-        if pend_side is not None:  # the previous step's weight gradients read X: done before it is rewritten
-            streams.current(self.comm.device).wait_event(pend_side[0])
+        if pend_side is not None and pend_side[0] is not None:  # the previous step's weight gradients
+            streams.current(self.comm.device).wait_event(pend_side[0])  # read X: done before it is rewritten
         ph = phase("wd.get_assemble")
         ph.__enter__()
         src = self.emb.get_source(keys, plan=plan)  # one rank: the rows are read in place
@@ -328,31 +331,33 @@ class WideDeep(LookaheadPlans):
         scale = 1.0 / (B * self.comm.world)
         w4, gw4 = self.view(P, "w4"), self.view(G, "w4")
         sink = self.dense.slab_sink() if hasattr(self.dense, "slab_sink") else None
+        side = self._side
+        defer = _HEAD_DEFER and side.stream is not None
         rp = self._replay if (self._replay is not None and _REPLAY and self._wbucket is None
                               and streams.DELAY_US <= 0 and not torch.cuda.is_current_stream_capturing()) else None
-        key = (B, P.data_ptr(), G.data_ptr(), sink is not None)
+        key = (B, P.data_ptr(), G.data_ptr(), sink is not None, defer)
         if rp is not None:
             rp(("fwd",) + key, lambda: self._forward(b, P))
         else:
             self._forward(b, P)
         # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
         ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
-                    b["dwide"], b["loss"], self.view(G, "b3"), scale)
+                    b["dwide"], b["loss"], self.view(G, "b3"), scale, defer_fold=defer)
         ph.__exit__(None, None, None)
         ph = phase("wd.bwd_dense")
         ph.__enter__()
         issue_next("head")
-        side = self._side
         # weight gradients fork onto a second stream as soon as their inputs exist, beside the
         # dgrad chain (their split-K tails and reduces fill the gaps of the dependent chain).
         # Each fork records an event on the compute stream (~2-4 us queue bubble on MI355X), but
         # fewer, later forks lose more overlap than they save: W3+W2 forked together 0.431-0.438,
         # all three after dgrad1 0.446 vs 0.418-0.421 ms/step (profiles/r3/ab_wd_forks.txt)
         # one rank: the weight gradients' split-K slices are folded by the dense table's Adam (sink)
+        fold = (B, h, gw4[:h], gw4[h:h + 1], b["loss"], self.view(G, "b3")) if defer else None
         if rp is not None:
-            rp(("bwd",) + key, lambda: self._backward_chain(b, P, G, sink, side))
+            rp(("bwd",) + key, lambda: self._backward_chain(b, P, G, sink, side, fold))
         else:
-            self._backward_chain(b, P, G, sink, side)
+            self._backward_chain(b, P, G, sink, side, fold)
         # the embedding gradient leaves the dgrad GEMM already in the planner's row-sorted order
         # (one 64-byte row per lookup, grouped by unique key), so the embedding backward reads one
         # contiguous stream instead of gathering 64-byte pieces of [B, F*D] rows
@@ -367,7 +372,7 @@ class WideDeep(LookaheadPlans):
         w_read = side.point() if _ADAM_AFTER_DGRAD and self.comm.world == 1 else None
         if _W1_LATE:  # the layer-1 weight gradient beside the memory-bound embedding backward instead
             with side.fork():
-                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink, 1)
+                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
         # an async dense clock (its own stream) needs only the weight gradients: issued from the
         # side stream it starts as soon as the last wgrad ends, beside the embedding backward and
         # the sparse push, instead of behind them
@@ -407,10 +412,12 @@ class WideDeep(LookaheadPlans):
             # compute stream (side.fork) -- a missing edge by construction. With the edge, repeated
             # op-by-op runs stopped varying at the 4th decimal (profiles/r5/race_dgrad_adam.txt)
             ev_x = side.mark()
+            if defer:  # the returned loss is folded on the side stream: final on the compute stream
+                side.wait(ev_x)  # (the next step's assembly waited for this point anyway)
             with side.fork(after=w_read):
                 self.dense.add()
                 self.dense.clock()
-            self._side_pending = (ev_x, side.mark())
+            self._side_pending = (None if defer else ev_x, side.mark())
             if hasattr(self.dense, "hold"):  # a checkpoint (drain) waits for this Adam too
                 self.dense.hold(self._side_pending[1])
         else:
@@ -423,21 +430,25 @@ class WideDeep(LookaheadPlans):
             self._advance_next_plan()
         return b["loss"]
 
-    def _backward_chain(self, b, P, G, sink, side):
+    def _backward_chain(self, b, P, G, sink, side, fold=None):
         """dgrad chain down to dH1 with the three weight gradients (and the layer-2 bias gradient)
-        forked beside it: GEMM-family ops and forks only (replayable, see layers.Replayer)."""
+        forked beside it: GEMM-family ops and forks only (replayable, see layers.Replayer).
+        ``fold``: wd_head_fold's arguments (the head deferred its batch sums), run first on the
+        side stream."""
         k3 = self.k_in[2]
         with side.fork():
-            _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink, 3)
+            if fold is not None:
+                ops.wd_head_fold(*fold)
+            _wgrad(b["dH3"], b["H2"], self.view(G, "W3"), sink)
         ops.linear_dgrad(b["dH3"], self.view(P, "W3"), mask=b["H2"], n_cols=k3, out=b["dH2"])
         with side.fork():
             ops.colsum_add(b["dH2"], self.view(G, "b2"))  # the layer-2 bias gradient
-            _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink, 2)
+            _wgrad(b["dH2"], b["H1"], self.view(G, "W2"), sink)
         ops.linear_dgrad(b["dH2"], self.view(P, "W2"), mask=b["H1"], n_cols=self.k_in[1], out=b["dH1"])
         self._bucket_done(1, side)  # (layers 2, 3 and the head: their weight gradients are issued)
         if not _W1_LATE:
             with side.fork():
-                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink, 1)
+                _wgrad(b["dH1"], b["X"], self.view(G, "W1"), sink)
 
     def _bucket_done(self, layer: int, side):
         """Every layer >= ``layer`` has its weight gradient issued (on the side stream): the buckets

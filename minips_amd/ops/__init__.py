@@ -569,9 +569,15 @@ def wd_assemble_tab(dense, table, index, base, inv, F, D, X, wide_logit, ones_co
     return wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col, zero)
 
 
-def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum=None, grad_scale=1.0):
+def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum=None, grad_scale=1.0,
+            defer_fold=False):
+    """Last layer + BCE forward/backward. ``defer_fold`` (GPU): the batch sums into dw / db /
+    loss_sum / dH_colsum are left as per-block partials for wd_head_fold (a later kernel, e.g. on
+    the weight-gradient stream, off the dgrad chain); on the CPU they are added here and the fold
+    is a no-op."""
     if _gpu(H):
-        kernels().wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, float(grad_scale))
+        kernels().wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, float(grad_scale),
+                          bool(defer_fold))
         return
     h = H.float()
     z = h @ w.float() + b0.float() + wide_logit
@@ -586,6 +592,13 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
     dw += (dz.unsqueeze(1) * h).sum(0)
     if dH_colsum is not None:
         dH_colsum += g.float().sum(0)
+
+
+def wd_head_fold(B, Hd, dw, db, loss_sum, dH_colsum=None):
+    """The totals of the device's last wd_head(defer_fold=True) (same B, Hd), on the current
+    stream (recordable into a LaunchList). No-op on the CPU (wd_head added them)."""
+    if _gpu(dw):
+        (kernels() if _REC is None else _REC.lst).wd_head_fold(int(B), int(Hd), dw, db, loss_sum, dH_colsum)
 
 
 def emb_csr_positions(members):

@@ -20,7 +20,7 @@ wait for a peer's pushes. These tables do the same with no collective on the dat
   optimizer and the OWNER's state (row-wise Adagrad, Adam, Adagrad, SGD or the reference's plain
   add; csrc/kernels/onesided.hip HipApplier) on its own high-priority stream, and publishes
   ``applied``;
-* SSP tables with a stateful optimizer (row-wise Adagrad, Adam, Adagrad) are served
+* SSP tables with a stateful optimizer (row-wise Adagrad, Adam, Adagrad) on several ranks are served
   clock-coalesced (AsyncServer::SetCoalesce): the owner applies clock c once every requester
   sent it, as ONE optimizer step over the P pushes summed per key in requester order -- the BSP
   update of that clock. The reference's SSP server applies each Add on arrival as ``+=``
@@ -476,8 +476,10 @@ class AsyncSparseTable(_AsyncTable, SparseTable):
         self.state2 = torch.zeros_like(self.state) if (self.state is not None and split is not None) else None
         # SSP + row-wise Adagrad: one Adagrad step per row per clock over every requester's push
         # (module docstring); the owner's direct-addressed (stamp, index) table of that apply
-        self.coalesced = (consistency == "ssp" and optimizer == "rowwise_adagrad"
-                          and 8 * P * self.rows_local <= _COALESCE_MAX_BYTES)
+        # (the clock kernel moves rows in float4 pieces: W % 4 == 0, W <= 64)
+        # (one rank: a clock holds one push -- the per-push apply is the same update, one kernel)
+        self.coalesced = (consistency == "ssp" and P > 1 and optimizer == "rowwise_adagrad" and width % 4 == 0
+                          and width <= 64 and 8 * P * self.rows_local <= _COALESCE_MAX_BYTES)
         self._rs = torch.zeros(2 * P * self.rows_local, dtype=torch.int32, device=dev) \
             if self.coalesced and self.cuda else None
         self._inbox = self._share([P * self.depth * self.slot_bytes] * P, "inbox", kind=_INBOX_MEM)
@@ -950,7 +952,7 @@ class AsyncDenseTable(_AsyncTable):
         P, me, dev = comm.world, comm.rank, comm.device
         self.table_id, self.n_params = table_id, n_params
         self.optimizer, self.lr = optimizer, lr
-        self.coalesced = consistency == "ssp" and optimizer in ("adam", "adagrad")
+        self.coalesced = consistency == "ssp" and P > 1 and optimizer in ("adam", "adagrad")
         self.push_lr = lr / P if optimizer in ("adam", "adagrad") and not self.coalesced else lr
         self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
         self.pull_dtype = pull_dtype

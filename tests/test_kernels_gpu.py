@@ -243,17 +243,27 @@ def test_wd_assemble_tab_and_head_full_batch(dev):
     wide = torch.randn(Bh, generator=g)
     y = (torch.rand(Bh, generator=g) > 0.5).float()
 
-    def run(dv):
+    def run(dv, defer=False):
         o = dict(dH=torch.empty(Bh, Hd, dtype=torch.bfloat16, device=dv), dw=torch.full((Hd,), 0.5, device=dv),
                  db=torch.full((1,), 0.25, device=dv), dwide=torch.empty(Bh, device=dv),
                  loss=torch.zeros(1, device=dv), cs=torch.zeros(Hd, device=dv))
         ops.wd_head(H.to(dv), w.to(dv), b0.to(dv), wide.to(dv), y.to(dv), o["dH"], o["dw"], o["db"], o["dwide"],
-                    o["loss"], o["cs"], 1.0 / Bh)
+                    o["loss"], o["cs"], 1.0 / Bh, defer_fold=defer)
+        if defer:  # the batch sums folded by the separate kernel, on another stream
+            side = torch.cuda.Stream(device=dv)
+            side.wait_stream(torch.cuda.current_stream(dv))
+            with torch.cuda.stream(side):
+                ops.wd_head_fold(Bh, Hd, o["dw"], o["db"], o["loss"], o["cs"])
+            torch.cuda.current_stream(dv).wait_stream(side)
         return {k: v.cpu() for k, v in o.items()}
 
     r, o = run("cpu"), run(dev)
     for k in r:
         torch.testing.assert_close(o[k].float(), r[k].float(), rtol=2e-2, atol=1e-4)
+    # the deferred fold sums the 256 block rows in the in-kernel fold's order: bit-identical
+    od = run(dev, defer=True)
+    for k in o:
+        assert torch.equal(od[k], o[k]), k
 
 
 def test_lr_and_kmeans(dev):

@@ -4,6 +4,7 @@
 #     all          smoke + GPU tests + short bench + rocprofv3 kernel stats of the bench
 #     trace        kernel trace of the W&D bench (BENCH_ARGS), with the steady-state step breakdown and
 #                  one step's timeline (tools/prof_summary.py trace; ANCHOR: the kernel a step starts at)
+#     lag          host launch return vs GPU start of every kernel of a steady step (tools/prof_summary.py lag)
 #     audit        host issue time + host syncs per step at world 1 (the real path) and 4 / 8 (gloo, one card)
 #     micro        isolated GPT-2 kernels: every GEMM shape vs hipBLASLt, memory-bound kernels, attention
 #     models       bench lines of the other BASELINE configs (MODELS, default "mlp dlrm dlrm-10b gpt2")
@@ -60,6 +61,17 @@ if [[ $STAGE == trace ]]; then
     echo "=== trace ($f)"
     python tools/prof_summary.py trace "$f" --anchor ${ANCHOR:-wd_head_kernel} --skip 8 --top ${TOP:-30} --timeline | tee $d.summary.txt
   done
+fi
+if [[ $STAGE == lag ]]; then
+  # host launch time vs GPU start per kernel (runtime tracing adds host cost per HIP call: an upper
+  # bound on how host-bound the step is)
+  prof_env
+  d=gpurun_out/lag
+  rm -rf $d
+  timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $d -o run -- python bench.py --steps 40 --warmup 5 ${BENCH_ARGS} > $d.log 2>&1 || { tail -30 $d.log; exit 1; }
+  python tools/prof_summary.py lag "$(find $d -name "*kernel_trace.csv" | head -1)" "$(find $d -name "*hip_api_trace.csv" | head -1)" --anchor ${ANCHOR:-wd_head_kernel} > $d.summary.txt
+  head -40 $d.summary.txt
+  rm -rf $d
 fi
 if [[ $STAGE == audit ]]; then
   timeout -k 10 200 python bench.py --steps 200 --warmup 10 --sync-audit 50 > gpurun_out/audit_w1.txt 2>&1

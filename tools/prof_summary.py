@@ -11,6 +11,12 @@
         all queues (GPU busy), per-queue busy time and the kernels by device time per step -- the
         numbers that tell an overlap problem (busy << wall) from a kernel problem (busy ~ wall)
 
+    python tools/prof_summary.py lag run_kernel_trace.csv run_hip_api_trace.csv [--anchor K] [--skip 8]
+        (rocprofv3 --kernel-trace --hip-runtime-trace) one steady step kernel by kernel with the HOST
+        time its launch call returned next to the GPU start: ``slack`` = GPU start - launch return.
+        A kernel with ~0 slack started as soon as the host issued it -- the host path, not a GPU
+        dependency, set its start (the steady-step median slack per kernel is printed too)
+
     python tools/prof_summary.py markers run_marker_api_trace.csv [--steps N]
         roctx ranges (MINIPS_ROCTX=1 under ``rocprofv3 --marker-trace``): count and host time per
         range name (Get / Add / Clock / collectives / the owner's apply batches)
@@ -142,6 +148,32 @@ def trace(a):
             print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {gap:7.1f}  q{q}  {_short(n)[:90]}")
 
 
+def lag(a):
+    kr = list(csv.DictReader(open(a.trace)))
+    launch = {}
+    for r in csv.DictReader(open(a.api)):
+        if "Launch" in r.get("Function", r.get("Operation", "")):
+            launch[r["Correlation_Id"]] = int(r["End_Timestamp"])
+    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Queue_Id", "0"),
+                 launch.get(r.get("Correlation_Id"))) for r in kr)
+    anchors = [s for s, e, n, q, h in ks if a.anchor in n]
+    if len(anchors) < a.skip + 3:
+        raise SystemExit(f"only {len(anchors)} '{a.anchor}' kernels in the trace")
+    slack = collections.defaultdict(list)
+    for s, e, n, q, h in ks:
+        if anchors[a.skip] <= s < anchors[-1] and h is not None:
+            slack[_short(n)].append((s - h) / 1e3)
+    print(f"median slack (GPU start - host launch return, us) over steps {a.skip}..{len(anchors) - 1}:")
+    for n, v in sorted(slack.items(), key=lambda kv: sorted(kv[1])[len(kv[1]) // 2]):
+        print(f"  {sorted(v)[len(v) // 2]:9.1f}  (min {min(v):8.1f}, n {len(v):5d})  {n[:80]}")
+    t0, t1 = anchors[a.skip + 1], anchors[a.skip + 2]
+    print(f"\none step ({(t1 - t0) / 1e3:.1f} us), anchor {a.anchor}: start_us dur_us host_us slack_us queue kernel")
+    for s, e, n, q, h in ks:
+        if t0 <= s < t1:
+            hs = f"{(h - t0) / 1e3:8.1f} {(s - h) / 1e3:8.1f}" if h is not None else f"{'-':>8} {'-':>8}"
+            print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {hs}  q{q}  {_short(n)[:80]}")
+
+
 def markers(a):
     """roctx ranges of a ``--marker-trace`` run (MINIPS_ROCTX=1): per range name its count, total
     and mean host time, per thread; ``--steps`` divides the totals into per-step figures."""
@@ -201,7 +233,7 @@ def early(a):
 
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    if argv and argv[0] not in ("stats", "pmc", "pmctable", "trace", "markers", "early", "-h", "--help"):
+    if argv and argv[0] not in ("stats", "pmc", "pmctable", "trace", "lag", "markers", "early", "-h", "--help"):
         argv.insert(0, "stats")
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -219,6 +251,11 @@ def main(argv=None):
     p.add_argument("--skip", type=int, default=3)
     p.add_argument("--top", type=int, default=30)
     p.add_argument("--timeline", action="store_true", help="also list one steady step kernel by kernel")
+    p = sub.add_parser("lag")
+    p.add_argument("trace")
+    p.add_argument("api")
+    p.add_argument("--anchor", default="wd_head_kernel")
+    p.add_argument("--skip", type=int, default=8)
     p = sub.add_parser("early")
     p.add_argument("trace")
     p.add_argument("--anchor", default="adam_kernel")
@@ -236,6 +273,8 @@ def main(argv=None):
         pmc(a.paths)
     elif a.cmd == "pmctable":
         pmc_table(a.paths, a.match)
+    elif a.cmd == "lag":
+        lag(a)
     elif a.cmd == "early":
         early(a)
     else:
