@@ -93,12 +93,19 @@ struct GemmLaunch {
   float* slab;
   const int* perm;
   int seg, colsum_ld;
+  int tile = 0;
   void launch(hipStream_t s) const {
     minips_k::gemm_bf16_batched(A, B, C, M, N, K, lda, ldb, ldc, a_km, b_kn, epi, bias, mask, ldmask, colsum, alpha,
                                 split_k, batch, inner, st[0], st[1], st[2], st[3], st[4], st[5], s, slab, perm, seg,
-                                colsum_ld);
+                                colsum_ld, tile);
   }
 };
+
+// a GEMM tile hint: 0 (the launcher's choice), 128 (128x128), 200 (256x128) or 256 (256x256)
+int check_tile(int64_t tile) {
+  TORCH_CHECK(tile == 0 || tile == 128 || tile == 200 || tile == 256, "gemm tile hint: 0, 128, 200 or 256");
+  return (int)tile;
+}
 
 // Validates a gemm() call and returns its launch; ``slab`` receives the split-K planes it needs
 // (a caching-allocator block), if any.
@@ -201,12 +208,13 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
           bool b_kn, int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& mask,
           const c10::optional<at::Tensor>& colsum, double alpha, int64_t split_k, int64_t batch, int64_t inner,
           int64_t lda_, int64_t ldb_, int64_t ldc_, std::vector<int64_t> strides,
-          const c10::optional<at::Tensor>& perm, int64_t seg) {
+          const c10::optional<at::Tensor>& perm, int64_t seg, int64_t tile) {
   c10::hip::HIPGuardMasqueradingAsCUDA gd(A.device());
   at::Tensor slab;
-  prepare_gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, alpha, split_k, batch, inner, lda_, ldb_, ldc_,
-               strides, perm, seg, slab)
-      .launch(stream_of(A));
+  GemmLaunch g = prepare_gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, alpha, split_k, batch, inner,
+                              lda_, ldb_, ldc_, strides, perm, seg, slab);
+  g.tile = check_tile(tile);
+  g.launch(stream_of(A));
 }
 
 // Bitmap planner of a bounded key space (keys, after the optional routing k * mult mod rn, in
@@ -1526,11 +1534,12 @@ class LaunchList {
   void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K, bool a_km,
             bool b_kn, int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& mask,
             const c10::optional<at::Tensor>& colsum, double alpha, int64_t split_k,
-            const c10::optional<at::Tensor>& perm, int64_t seg) {
+            const c10::optional<at::Tensor>& perm, int64_t seg, int64_t tile) {
     c10::hip::HIPGuardMasqueradingAsCUDA gd(A.device());
     at::Tensor slab;
-    const GemmLaunch g = prepare_gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, alpha, split_k, 1, 1, 0,
-                                      0, 0, {}, perm, seg, slab);
+    GemmLaunch g = prepare_gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, alpha, split_k, 1, 1, 0, 0, 0,
+                                {}, perm, seg, slab);
+    g.tile = check_tile(tile);
     const int k = slot(A);
     g.launch(rec_[k]);
     for (const auto* t : {&bias, &mask, &colsum, &perm})
@@ -1948,7 +1957,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("a_km"), py::arg("b_kn"), py::arg("epi"), py::arg("bias"), py::arg("mask"), py::arg("colsum"),
         py::arg("alpha") = 1.0, py::arg("split_k") = 1, py::arg("batch") = 1, py::arg("inner") = 1,
         py::arg("lda") = 0, py::arg("ldb") = 0, py::arg("ldc") = 0, py::arg("strides") = std::vector<int64_t>(),
-        py::arg("perm") = py::none(), py::arg("seg") = 0);
+        py::arg("perm") = py::none(), py::arg("seg") = 0, py::arg("tile") = 0);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("softmax_xent", &softmax_xent);

@@ -83,7 +83,7 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
                        bool a_km, bool b_kn, int epi, const bf16_t* bias, const bf16_t* mask, int ldmask,
                        float* colsum, float alpha, int split_k, int batch, int inner, int64_t sa_o, int64_t sa_i,
                        int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s, float* slab,
-                       const int* perm, int seg, int colsum_ld) {
+                       const int* perm, int seg, int colsum_ld, int tile) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return;
   if (epi == kEpiPermRowsBf16 && (!perm || seg <= 0 || seg % 8 || N % seg || batch != 1 || split_k > 1))
     throw std::runtime_error("gemm: the permuted-rows epilogue needs perm, seg % 8 == 0, N % seg == 0, no batch");
@@ -98,6 +98,7 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
     // split-K without atomics: every K slice stores its partial tile into its own slab plane,
     // one streaming kernel adds the planes into C (measured faster than fp32 atomics)
     EpiArgs sp{slab, N, nullptr, nullptr, 0, nullptr, alpha, 1, 0, 0, 0, 0, 0, 0, (int64_t)M * N, nullptr, 0};
+    sp.tile = tile;
     nsplit = dispatch_layout(a_km, b_kn, kEpiStoreF32, A, B, M, N, K, lda, ldb, split_k, sp, batch, s);
     MINIPS_HIP_CHECK(hipGetLastError());
     if (bf16_out)
@@ -111,6 +112,7 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
   }
   EpiArgs ep{C, ldc, bias, mask, ldmask, colsum, alpha, inner, sa_o, sa_i, sb_o, sb_i, sc_o, sc_i, 0, perm, seg};
   ep.colsum_ld = colsum_ld > 0 ? colsum_ld : 1;
+  ep.tile = tile;
   // an accumulating GEMM with one K slice has one writer per output element: read-add-write
   // instead of memory-side fp32 atomics
   if (epi == kEpiAtomicF32 && split_k == 1) epi = kEpiAccumF32;

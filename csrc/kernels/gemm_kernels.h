@@ -125,6 +125,9 @@ struct EpiArgs {
   // its L2 (the plain tile remap gives each XCD whole tile rows over every slice: each XCD then
   // streams the full other operand)
   int zmap = 0;
+  // host-side tile hint (128, 256 or 200 = 256x128; 0: the wave-quantisation choice) -- a GEMM
+  // that runs beside another stream's workgroups may want the smaller tile (see launch)
+  int tile = 0;
 };
 
 // Destination of an output row segment (kEpiPermRowsBf16: the permuted row of its segment).
@@ -703,7 +706,7 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int N, int K, int lda, int l
     const int64_t t128 = work * (int64_t)tiles;
     const double eff256 = (double)t256 / (double)(((t256 + 255) / 256) * 256);
     const double eff128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
-    const int pick = force ? force : (eff256 >= eff128 ? 256 : 128);
+    const int pick = force ? force : ep.tile ? ep.tile : (eff256 >= eff128 ? 256 : 128);
     // (round 4's 8-wave 256x256 variants -- phase-split v3, quarter-staged v4, ping-pong v5 -- and
     // round 5's 4-wave 128x128-per-wave v6 and 4-deep ring of 32-deep K-steps v7 measured slower
     // than v2 on the model shapes and are gone: profiles/r4/gemm_*_v5.txt, profiles/r5/gemm_v7_ring.txt)

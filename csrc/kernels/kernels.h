@@ -44,7 +44,8 @@ void gemm_bf16_batched(const bf16_t* A, const bf16_t* B, void* C, int M, int N, 
                        int64_t sb_o, int64_t sb_i, int64_t sc_o, int64_t sc_i, hipStream_t s,
                        float* slab = nullptr,  // split-K workspace [split_k][M][N] (atomic epilogue only)
                        const int* perm = nullptr, int seg = 0,  // kEpiPermRowsBf16
-                       int colsum_ld = 1);                      // colsum[col * colsum_ld]
+                       int colsum_ld = 1,  // colsum[col * colsum_ld]
+                       int tile = 0);      // EpiArgs::tile
 
 // ------------------------------------------------------------------ sparse keys (sparse.hip)
 // Hash-based dedupe + owner bucketing of int64 keys in 3 launches (no sort):

@@ -131,6 +131,9 @@ _REPLAY = True
 # fold levels leave the dgrad chain (head 17 -> 11 us in-step): 0.335-0.339 vs 0.344-0.345 ms/step
 # (profiles/r6/ab_wd_r6.txt). False: the round-5 in-kernel fold.
 _HEAD_DEFER = True
+# (the dgrads beside the weight-gradient stream keep the launcher's 256x256 tile: forcing 128x128 on
+# the dH1 / dX dgrad, which shares CUs with the wgrads' 128x128 workgroups, measured 0.336-0.339 /
+# 0.344-0.345, both 0.347-0.353, 256x128 0.376-0.379 vs 0.336-0.339 ms; profiles/r6/ab_wd_r6.txt)
 
 
 # (round 6: per-layer split-K of the weight gradients instead of the workgroup target -- isolated,

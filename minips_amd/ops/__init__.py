@@ -66,17 +66,18 @@ class recording:
 
 
 def gemm(A, B, C, M, N, K, a_km=False, b_kn=False, epi=EPI_STORE_F32, bias=None, mask=None, colsum=None,
-         alpha=1.0, split_k=1, perm=None, seg=0):
+         alpha=1.0, split_k=1, perm=None, seg=0, tile=0):
     """C[M,N] (op)= A.B.  A is [M][K] (a_km=False) or [K][M]; B is [N][K] (b_kn=False) or [K][N].
-    EPI_PERM_ROWS_BF16: C is [M*N/seg, seg] and output (row, col) goes to row perm[row*N/seg + col//seg]."""
+    EPI_PERM_ROWS_BF16: C is [M*N/seg, seg] and output (row, col) goes to row perm[row*N/seg + col//seg].
+    ``tile`` (GPU): 128 / 200 (256x128) / 256 forces the workgroup tile, 0 lets the launcher pick."""
     if _gpu(A):
         if _REC is not None:
             _REC.lst.gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k), perm,
-                          int(seg))
+                          int(seg), int(tile))
             return C
         # (all positional: pybind's keyword / default-argument path costs ~1 us per call)
         kernels().gemm(A, B, C, M, N, K, a_km, b_kn, epi, bias, mask, colsum, float(alpha), int(split_k), 1, 1, 0, 0,
-                       0, _NO_STRIDES, perm, int(seg))
+                       0, _NO_STRIDES, perm, int(seg), int(tile))
         return C
     a = (A[:K, :M].t() if a_km else A[:M, :K]).float()
     b = (B[:K, :N] if b_kn else B[:N, :K].t()).float()
@@ -165,20 +166,20 @@ def colsum_add(x, out):
     return out
 
 
-def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=None, perm=None, seg=0):
+def linear_dgrad(dy, w, mask=None, colsum=None, out_f32=False, n_cols=None, out=None, perm=None, seg=0, tile=0):
     """dx = dy w (dy [M,N], w [N,K]) -> bf16 masked by (mask > 0) (+colsum), or fp32. ``perm`` /
     ``seg``: dx's row segments of ``seg`` columns go to rows perm[...] of out [M*K/seg, seg] (the
-    embedding gradient written straight into the key planner's row-sorted order)."""
+    embedding gradient written straight into the key planner's row-sorted order). ``tile``: gemm's."""
     M, N = dy.shape
     K = w.shape[1] if n_cols is None else n_cols
     if perm is not None:
         if out is None:
             out = torch.empty(M * K // seg, seg, dtype=torch.bfloat16, device=dy.device)
-        return gemm(dy, w, out, M, K, N, False, True, EPI_PERM_ROWS_BF16, perm=perm, seg=seg)
+        return gemm(dy, w, out, M, K, N, False, True, EPI_PERM_ROWS_BF16, perm=perm, seg=seg, tile=tile)
     if out is None:
         out = torch.empty(M, K, dtype=torch.float32 if out_f32 else torch.bfloat16, device=dy.device)
     epi = EPI_STORE_F32 if out_f32 else (EPI_RELU_MASK_BF16 if mask is not None else EPI_STORE_BF16)
-    return gemm(dy, w, out, M, K, N, False, True, epi, mask=mask, colsum=colsum)
+    return gemm(dy, w, out, M, K, N, False, True, epi, mask=mask, colsum=colsum, tile=tile)
 
 
 # Split-K weight gradients: about one 128x128 workgroup per CU pair (512 blocks), but a minimum number
