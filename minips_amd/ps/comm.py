@@ -41,6 +41,7 @@ import datetime
 import os
 import threading
 import time
+import warnings
 from dataclasses import dataclass, field
 
 import torch
@@ -72,8 +73,8 @@ def _native_rccl(comm: "Comm"):
 
     pg = comm.group if comm.group is not None else dist.group.WORLD
     hit = _RCCL_CACHE.get(id(pg))
-    if hit is not None and hit[0] is pg and not hit[1].aborted:
-        return hit[1]
+    if hit is not None and hit[0] is pg and (hit[1] is None or not hit[1].aborted):
+        return hit[1]  # (None: the self-test failed on some rank -- the group runs on c10d)
     k = kernels()
     lib = _rccl_lib()
     store = dist.distributed_c10d._get_default_store()
@@ -95,10 +96,52 @@ def _native_rccl(comm: "Comm"):
             store.delete_key(tag + "/ack")
         # the watchdog's timeout and failure mode follow the process group's: TORCH_NCCL_ASYNC_ERROR_
         # HANDLING 1 / 3 end the process on a stuck collective, 2 (in-place rollback) raises instead
-        rc = k.Rccl(lib, uid, comm.world, comm.rank, comm.device.index or 0,
-                    timeout_s=float(os.environ.get("MINIPS_PG_TIMEOUT", "60")), teardown=mode in ("1", "3"))
+        rc, ok = None, 1
+        try:
+            rc = k.Rccl(lib, uid, comm.world, comm.rank, comm.device.index or 0,
+                        timeout_s=float(os.environ.get("MINIPS_PG_TIMEOUT", "60")), teardown=mode in ("1", "3"))
+            ok = int(_rccl_selftest(rc, comm))
+        except RuntimeError as e:
+            ok, why = 0, str(e)
+        else:
+            why = "wrong self-test result"
+        # every rank takes the same path: if the communicator failed anywhere, the whole group falls
+        # back to ProcessGroupNCCL (a rank on its own communicator while a peer waits in c10d hangs)
+        if comm.world > 1:
+            fdev = comm.device if dist.get_backend(pg) == "nccl" else torch.device("cpu")
+            flag = torch.tensor([ok], dtype=torch.int32, device=fdev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=pg)
+            ok = int(flag.item())
+        if not ok:
+            if rc is not None:
+                rc.abort("native RCCL self-test failed on a rank")
+            rc = None
+            if comm.rank == 0:
+                warnings.warn(f"native RCCL data plane disabled for {tag} ({why}); collectives run on c10d")
     _RCCL_CACHE[id(pg)] = (pg, rc)
     return rc
+
+
+def _rccl_selftest(rc, comm: "Comm") -> bool:
+    """One all-to-all-v (rank r sends r * P + p to peer p, two values to the next rank) and one
+    all-reduce on the new communicator, checked on the host: a broken data plane is caught before
+    a table's first exchange, while the group can still fall back together."""
+    P, r, dev = comm.world, comm.rank, comm.device
+    send = [2 if p == (r + 1) % P else 1 for p in range(P)]
+    recv = [2 if p == (r - 1) % P else 1 for p in range(P)]
+    vals = []
+    for p in range(P):
+        vals += [r * P + p] * send[p]
+    inp = torch.tensor(vals, dtype=torch.int64, device=dev)
+    out = torch.full((sum(recv),), -1, dtype=torch.int64, device=dev)
+    want = []
+    for p in range(P):
+        want += [p * P + r] * recv[p]
+    ones = torch.ones(4, dtype=torch.float32, device=dev)
+    rc.all_to_all_v(out, inp, recv, send)
+    rc.all_reduce(ones, 0)
+    torch.cuda.current_stream(dev).synchronize()
+    return out.tolist() == want and ones.tolist() == [float(P)] * 4
 
 
 def _rccl_call(fn, *args):

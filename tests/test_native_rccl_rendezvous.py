@@ -2,8 +2,9 @@
 CPU ranks: the RCCL calls are replaced by a fake, the protocol over the real c10d store is the
 production one -- rank 0 publishes ONE unique id, every rank builds its communicator from that
 same id, the keys are gone afterwards (a re-formed group starts clean), a second Comm over the
-group reuses the communicator, and refresh() drops it so the next collective makes a new one.
-(The RCCL calls themselves run on the GPU box at world 1: tests/test_rccl_gpu.py.)"""
+group reuses the communicator, and refresh() drops it so the next collective makes a new one; a
+communicator whose self-test fails on ONE rank is dropped on every rank (the group falls back to
+c10d together). (The RCCL calls themselves run on the GPU box at world 1: tests/test_rccl_gpu.py.)"""
 import torch
 
 from test_ps_gloo import run_world
@@ -39,6 +40,7 @@ def _rendezvous(rank, world):
 
     fake = _FakeKernels()
     _native.kernels = lambda: fake  # the fake RCCL behind the production rendezvous
+    cm._rccl_selftest = lambda rc, comm: True  # (the data-plane self-test needs a GPU)
     c = cm.Comm()
     c.backend, c.device = "nccl", torch.device("cuda", 0)  # (as on a GPU rank; nothing touches a GPU)
     rc = c._rc()
@@ -69,3 +71,32 @@ def test_native_rccl_rendezvous_four_ranks():
         assert not o["left"], o     # the id / ack keys were deleted after the rendezvous
         assert o["aborted"] and "re-formed" in o["why"], o
         assert o["new"] and o["new_uid_differs"], o
+
+
+def _selftest_fails_on_one_rank(rank, world):
+    import warnings
+
+    from minips_amd import _native
+    from minips_amd.ps import comm as cm
+
+    fake = _FakeKernels()
+    _native.kernels = lambda: fake
+    cm._rccl_selftest = lambda rc, comm: comm.rank != 2  # a broken data plane on rank 2 only
+    c = cm.Comm()
+    c.backend, c.device = "nccl", torch.device("cuda", 0)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        rc = c._rc()
+    made = [v for v in cm._RCCL_CACHE.values()]
+    c2 = cm.Comm()
+    c2.backend, c2.device = "nccl", torch.device("cuda", 0)
+    return dict(rc=rc, again=c2._rc(), made=fake.made, warned=any("disabled" in str(x.message) for x in w),
+                cached=[m[1] for m in made])
+
+
+def test_native_rccl_selftest_failure_disables_it_on_every_rank():
+    out = run_world(_selftest_fails_on_one_rank, world=4)
+    for r, o in out.items():
+        assert o["rc"] is None and o["again"] is None, o  # every rank on c10d, not only rank 2
+        assert o["made"] == 1, o                          # no second attempt by a later Comm
+        assert o["warned"] == (r == 0), o

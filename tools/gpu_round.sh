@@ -70,7 +70,7 @@ if [[ $STAGE == lag ]]; then
   rm -rf $d
   timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $d -o run -- python bench.py --steps 40 --warmup 5 ${BENCH_ARGS} > $d.log 2>&1 || { tail -30 $d.log; exit 1; }
   python tools/prof_summary.py lag "$(find $d -name "*kernel_trace.csv" | head -1)" "$(find $d -name "*hip_api_trace.csv" | head -1)" --anchor ${ANCHOR:-wd_head_kernel} > $d.summary.txt
-  head -40 $d.summary.txt
+  head -60 $d.summary.txt
   rm -rf $d
 fi
 if [[ $STAGE == audit ]]; then

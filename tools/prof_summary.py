@@ -151,9 +151,17 @@ def trace(a):
 def lag(a):
     kr = list(csv.DictReader(open(a.trace)))
     launch = {}
+    dur = collections.defaultdict(list)
     for r in csv.DictReader(open(a.api)):
-        if "Launch" in r.get("Function", r.get("Operation", "")):
+        fn = r.get("Function", r.get("Operation", ""))
+        dur[fn].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        if "Launch" in fn:
             launch[r["Correlation_Id"]] = int(r["End_Timestamp"])
+    print("host time per HIP API call (us): calls, median, p90, max, total ms -- a call that blocks the host")
+    print("(e.g. a stream wait that waits for its event) shows a large p90 / max")
+    for fn, v in sorted(dur.items(), key=lambda kv: -sum(kv[1]))[:16]:
+        v.sort()
+        print(f"  {len(v):7d} {v[len(v) // 2]:8.1f} {v[int(len(v) * 0.9)]:8.1f} {v[-1]:9.1f} {sum(v) / 1e3:9.2f}  {fn}")
     ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Queue_Id", "0"),
                  launch.get(r.get("Correlation_Id"))) for r in kr)
     anchors = [s for s, e, n, q, h in ks if a.anchor in n]
