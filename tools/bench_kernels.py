@@ -422,6 +422,53 @@ def cmd_rccl(a):
     dist.destroy_process_group()
 
 
+def cmd_bubble(a):
+    """GPU-side cost of a cross-stream fork on the stream forked FROM: N x (a 256-workgroup spin
+    kernel of ~3 us on the compute stream [+ an event record there] [+ the side stream's wait on
+    it] [+ a tiny kernel on the side stream]), per-iteration time from events around the loop.
+    The difference to the bare loop is the bubble a fork puts on the compute stream."""
+    from minips_amd._native import kernels
+    k = kernels()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    raw, sraw = s.cuda_stream, side.cuda_stream
+    fev = [k.FastEvent() for _ in range(8)]
+    tev = [torch.cuda.Event() for _ in range(8)]
+    n, ticks = 300, int(a.ticks)
+
+    def run(kind):
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t0.record(s)
+        for i in range(n):
+            k.wire_spin(ticks, 256, raw)
+            if kind == "spin":
+                continue
+            if kind.startswith("torch"):
+                e = tev[i % 8]
+                e.record(s)
+                if kind == "torch+wait":
+                    side.wait_event(e)
+                continue
+            e = fev[i % 8]
+            e.record(raw)
+            if kind in ("fast+wait", "fast+wait+side"):
+                e.wait(sraw)
+            if kind == "fast+wait+side":
+                k.wire_spin(10, 1, sraw)
+        t1.record(s)
+        torch.cuda.synchronize()
+        return t0.elapsed_time(t1) * 1e3 / n
+
+    for rep in range(2):
+        base = run("spin")
+        print(f"rep {rep}: spin only {base:7.2f} us/iter (spin {ticks} ticks = {ticks / 100:.1f} us)")
+        for kind in ("fast", "fast+wait", "fast+wait+side", "torch", "torch+wait"):
+            t = run(kind)
+            print(f"       + {kind:16s} {t:7.2f} us/iter  (+{t - base:5.2f})")
+
+
 def cmd_issue(a):
     """HOST issue cost per call (no sync between calls) of the step's building blocks on one GPU:
     c10d collectives over a one-rank RCCL group (the Python + ProcessGroupNCCL + RCCL enqueue path
@@ -537,6 +584,7 @@ def main(argv=None):
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--ops", default="reduce_scatter,all_gather,all_to_all,all_to_all_v")
     sub.add_parser("issue").add_argument("--iters", type=int, default=200)
+    sub.add_parser("bubble").add_argument("--ticks", type=int, default=2000)
     p = sub.add_parser("wgrad")
     p.add_argument("--batch", type=int, default=16384)
     p.add_argument("--splits", default="2,4,6,8,10,12,16,24,32")
