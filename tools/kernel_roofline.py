@@ -59,10 +59,13 @@ def spec(U):
         (r"splitk_reduce_kernel", 2, f"split-K reduce W1 ({s1} planes)", 0, s1 * H1 * K1 * 4 + 2 * H1 * K1 * 4),
         (r"wd_assemble_tab_kernel", 0, "Get + assemble X (rows read from the fp32 shard + dense + wide sum)", 0,
          B * K1 * 2 + n * (D * 4 + 4 + 8 + 8) + B * ND * 4 + B * 4),
-        (r"wd_head_kernel", 0, "head Linear 256->1 + BCE fwd/bwd (+ dH3 column sums)", 0, B * H3 * 2 * 2 + B * 12),
+        (r"wd_head_kernel", 0, "head Linear 256->1 + BCE fwd/bwd (+ per-block dH3 column sums)", 0,
+         B * H3 * 2 * 2 + B * 12),
+        (r"wd_head_fold_kernel", 0, "head batch sums folded (weight-gradient stream)", 0, 256 * (2 * H3 + 2) * 4),
         (r"colsum_bf16_kernel", 0, "layer-2 bias gradient (dH2 column sums)", 0, B * H2 * 2),
+        (r"colsum_fold_kernel", 0, "layer-2 bias gradient: fold of the column-sum partials", 0, 0),
         (r"zero_rows_dev_kernel", 0, "zero grad rows", 0, U * W * 4),
-        (r"emb_seg_det_kernel", 0, "embedding backward: deterministic segment sums (member-order dX rows)", 0,
+        (r"emb_seg_det_kernel", 0, "embedding backward: deterministic segment sums (dX rows gathered by the CSR)", 0,
          n * (D * 2 + 8 + 4) + U * W * 4),
         (r"emb_seg_fix_kernel", 0, "embedding backward: rows cut by piece boundaries (partials)", 0,
          (n // 128) * 2 * (D + 4) * 4 * 2),
