@@ -65,6 +65,11 @@ _WGRAD_DEFER_GPT2 = False
 # profiles/r5/ab_gpt2_lm_split.txt).
 # All three LM-head GEMMs (logits, dgrad, wte wgrad) run on gemm.hip (round 5: the hipBLASLt path is gone)
 _LM_DGRAD_SPLIT = 8
+# the wte weight gradient (50304 x 768 outputs, K = 8192 tokens) on 256x256 tiles: 746 vs 835 us
+# isolated at the launcher's 128x128 choice (its wave quantisation, 591 vs 2358 tiles, favours 128;
+# the 256 tile moves half the L2->LDS bytes per MFMA), hipBLASLt 635; in the step 12.89-12.91 vs
+# 13.19-13.22 ms (635 vs 620 K tokens/s; profiles/r6/lm_head_tiles.txt)
+_LM_WGRAD_TILE = 256
 # MLP: the fc forward saves gelu'(u) (its tanh is computed there anyway) and the fc2 dgrad multiplies
 # by it; GPT2_GELU_D off saves u and re-evaluates tanh in the dgrad epilogue
 _GELU_D = True
@@ -194,7 +199,7 @@ class GPT2:
         side = self._side
         dh = b["dh"]
         with side.fork():
-            ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"))
+            ops.linear_wgrad(logits, hf[:, :d], v(G, "wte"), tile=_LM_WGRAD_TILE)
         # long K (the vocabulary), few outputs: split-K into fp32 slabs + one bf16 reduce
         ops.gemm(logits, wte, dh, M, d, c.vocab_pad, False, True, ops.EPI_STORE_BF16, split_k=_LM_DGRAD_SPLIT)
         dx = b["dx"]

@@ -203,12 +203,12 @@ def overlap_mode(on: bool) -> bool:
     return prev
 
 
-def linear_wgrad(dy, x, dw, split_k=None, blocks=None, defer=None):
+def linear_wgrad(dy, x, dw, split_k=None, blocks=None, defer=None, tile=0):
     """dw[N,K] += dy^T x (dy [M,N], x [M,K]); fp32 accumulate. ``blocks``: the workgroup target of
     the split-K choice (default _WGRAD_BLOCKS; a model may tune its own). ``defer``: a
     DenseTable slab sink (DenseTable.slab_sink()): the K slices stay in fp32 slab planes that the
     table's next Adam folds in (no reduce kernel); dw must be a contiguous [N, K] region of the
-    table's gradient, which the sum then never passes through."""
+    table's gradient, which the sum then never passes through. ``tile``: gemm's tile hint."""
     M, N = dy.shape
     K = x.shape[1]
     if split_k is None:
@@ -225,7 +225,7 @@ def linear_wgrad(dy, x, dw, split_k=None, blocks=None, defer=None):
         if _REC is not None:
             _REC.sink_adds.append((defer, dw, slab, nsplit))
         return dw
-    return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k)
+    return gemm(dy, x, dw, N, K, M, True, True, EPI_ATOMIC_F32, split_k=split_k, tile=tile)
 
 
 # ----------------------------------------------------------------------------- sparse keys
