@@ -241,10 +241,13 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
   constexpr int S = 4;
   for (int64_t b0s = wave * S; b0s < B; b0s += nwaves * S) {
     float h[S][PER_LANE];
-    float z[S];
+    float z[S], wv[S], yv[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int64_t b = b0s + s;
+      // the wide logit and label load with the row (not after the wave reduction: one round trip)
+      wv[s] = b < B ? wide[b] : 0.f;
+      yv[s] = b < B ? y[b] : 0.f;
 #pragma unroll
       for (int j = 0; j < PER_LANE; ++j) h[s][j] = 0.f;
       if (b < B) head_load<PER_LANE>(H + b * Hd + lane * PER_LANE, h[s]);
@@ -259,8 +262,8 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
     for (int s = 0; s < S; ++s) {
       const int64_t b = b0s + s;
       if (b >= B) break;
-      const float zz = z[s] + bias + wide[b];
-      const float label = y[b] > 0.5f ? 1.f : 0.f;
+      const float zz = z[s] + bias + wv[s];
+      const float label = yv[s] > 0.5f ? 1.f : 0.f;
       const float p = sigmoidf_(zz);
       const float dz = (p - label) * scale;
       if (lane == 0) {
