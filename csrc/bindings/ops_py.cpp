@@ -565,10 +565,6 @@ void wd_assemble_tab(const at::Tensor& dense, const at::Tensor& tab, const at::T
   TORCH_CHECK(inv.numel() == B * F, "inv must be [B*F]");
   TORCH_CHECK(dense.size(0) == B, "dense rows");
   TORCH_CHECK(tab.size(1) > D, "tab rows must hold D deep values + the wide weight");
-  check_dtype(wide_logit, at::kFloat, "wide_logit");
-  // [B] wide sums, or [B * F] per-lookup wide weights that wd_head sums (wide_parts)
-  const bool parts = wide_logit.numel() == B * F && F > 1;
-  TORCH_CHECK(parts || wide_logit.numel() == B, "wide_logit: [B] sums or [B, F] parts");
   const int32_t* ri = nullptr;
   if (rowidx && rowidx->defined()) {
     check_gpu(*rowidx, "rowidx");
@@ -579,7 +575,7 @@ void wd_assemble_tab(const at::Tensor& dense, const at::Tensor& tab, const at::T
   c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
   minips_k::wd_assemble_tab(ptr<float>(dense), (int)dense.size(1), ptr<float>(tab), tab.stride(0),
                             ptr<int64_t>(uniq), base, ptr<int64_t>(inv), B, (int)F, (int)D, ptr<bf16_t>(X),
-                            (int)X.size(1), ptr<float>(wide_logit), (int)ones_col, stream_of(X), z, ri, parts);
+                            (int)X.size(1), ptr<float>(wide_logit), (int)ones_col, stream_of(X), z, ri);
 }
 
 void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& wide_logit,
@@ -593,16 +589,10 @@ void wd_head(const at::Tensor& H, const at::Tensor& w, const at::Tensor& b0, con
   TORCH_CHECK(dH.sizes() == H.sizes(), "dH shape");
   TORCH_CHECK(w.numel() == H.size(1) && dw.numel() == H.size(1), "w/dw length");
   float* cs = opt_ptr<float>(dH_colsum, at::kFloat, "dH_colsum");
-  check_dtype(wide_logit, at::kFloat, "wide_logit");
-  // [B] wide logits or [B, F] per-lookup wide weights (wd_assemble_tab wide parts), summed here
-  const int64_t nb = H.size(0), nw = wide_logit.numel();
-  TORCH_CHECK(nb > 0 && nw % nb == 0 && nw / nb <= 64, "wide_logit: [B] or [B, F <= 64]");
-  const int wide_F = nw == nb ? 0 : (int)(nw / nb);
   c10::hip::HIPGuardMasqueradingAsCUDA g(H.device());
   minips_k::wd_head(ptr<bf16_t>(H), H.size(0), (int)H.size(1), ptr<bf16_t>(w), ptr<bf16_t>(b0),
                     ptr<float>(wide_logit), ptr<float>(labels), ptr<bf16_t>(dH), ptr<float>(dw), ptr<float>(db),
-                    ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H), defer_fold,
-                    wide_F);
+                    ptr<float>(dwide), ptr<float>(loss_sum), cs, (float)grad_scale, stream_of(H), defer_fold);
 }
 
 struct HeadFoldLaunch {

@@ -142,12 +142,10 @@ void wd_assemble(const float* dense, int n_dense, const bf16_t* rows, int row_st
 void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t tab_ld, const int64_t* uniq,
                      int64_t base, const int64_t* inv, int64_t B, int F, int D, bf16_t* X, int ldx,
                      float* wide_logit, int ones_col, hipStream_t s, float* zero_out,
-                     const int32_t* rowidx = nullptr,
-                     bool wide_parts = false);  // wide_logit [B, F]: per-lookup wide weights, not sums  // rowidx: lookup j's row + base (plan_sorted)
+                     const int32_t* rowidx = nullptr);  // rowidx: lookup j's row + base (plan_sorted)
 void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
-             float grad_scale, hipStream_t s, bool defer_fold = false,
-             int wide_F = 0);  // > 0: wide_logit is [B, wide_F] parts, summed here
+             float grad_scale, hipStream_t s, bool defer_fold = false);
 // defer_fold: the head leaves its per-block partial rows in a per-device slab and wd_head_fold
 // (same B / Hd, a later kernel on any stream ordered after it, before the next head of the
 // device) adds their totals into dw / db / loss_sum / dH_colsum.

@@ -99,23 +99,18 @@ __global__ void wd_assemble_tab_kernel(const float* __restrict__ dense, int n_de
                                        int64_t tab_ld, const int64_t* __restrict__ uniq, int64_t base,
                                        const int64_t* __restrict__ inv, int64_t B, int F, int D,
                                        bf16_t* __restrict__ X, int ldx, float* __restrict__ wide_logit, int ones_col,
-                                       float* __restrict__ zero_out, const int32_t* __restrict__ rowidx,
-                                       int wide_parts) {
+                                       float* __restrict__ zero_out, const int32_t* __restrict__ rowidx) {
   if (zero_out && blockIdx.x == 0 && threadIdx.x == 0) *zero_out = 0.f;
   const int chunks = ldx >> 3;
   const int emb_cols = F * D;
   const int64_t total = B * chunks;
   const int64_t total_r = (total + 63) & ~63ll;
-  // wide_parts: wide_logit is [B, F] -- the thread of each embedding's last chunk also stores the
-  // lookup's wide weight (the row's next float, in the line it just read) and the head sums the F
-  // parts; no separate pass of wide-weight loads (else: the [B] sums, 32 lanes per sample below)
-  const int64_t n_items = total_r + (wide_parts ? 0 : 32 * B);
   // the planner's per-lookup row (one coalesced index load) or the inv -> uniq chain
   auto row_of = [&](int64_t b, int f) {
     const int64_t r = rowidx ? (int64_t)rowidx[b * F + f] : uniq[inv[b * F + f]];
     return tab + (r - base) * tab_ld;
   };
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n_items;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total_r + 32 * B;
        c += (int64_t)gridDim.x * blockDim.x) {
     if (c >= total_r) {
       const int64_t k = c - total_r, b = k >> 5;
@@ -136,8 +131,6 @@ __global__ void wd_assemble_tab_kernel(const float* __restrict__ dense, int n_de
       const float* src = row_of(b, f) + d;
       const float4 lo = *reinterpret_cast<const float4*>(src);
       const float4 hi = *reinterpret_cast<const float4*>(src + 4);
-      if (wide_parts && d == D - 8)  // (bf16-rounded as in the gathered path)
-        wide_logit[b * F + f] = __uint_as_float(pack_bf2(src[8], 0.f) << 16);
       packed[0] = pack_bf2(lo.x, lo.y);
       packed[1] = pack_bf2(lo.z, lo.w);
       packed[2] = pack_bf2(hi.x, hi.y);
@@ -165,8 +158,7 @@ __global__ void wd_assemble_tab_kernel(const float* __restrict__ dense, int n_de
 
 void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t tab_ld, const int64_t* uniq,
                      int64_t base, const int64_t* inv, int64_t B, int F, int D, bf16_t* X, int ldx,
-                     float* wide_logit, int ones_col, hipStream_t s, float* zero_out, const int32_t* rowidx,
-                     bool wide_parts) {
+                     float* wide_logit, int ones_col, hipStream_t s, float* zero_out, const int32_t* rowidx) {
   if (ldx % 8) throw std::runtime_error("wd_assemble_tab: ldx must be a multiple of 8");
   if (F * D + n_dense > ldx) throw std::runtime_error("wd_assemble_tab: ldx too small");
   if (ones_col >= ldx) throw std::runtime_error("wd_assemble_tab: ones_col out of range");
@@ -176,10 +168,9 @@ void wd_assemble_tab(const float* dense, int n_dense, const float* tab, int64_t 
   const int block = 256;
   // (measured: a lane-per-lookup form -- 9 x 16-byte loads of one 144-byte row per lane, a half-wave
   // per sample -- ran the W&D step 15 us slower: 26 rows per wave-instruction vs 8 here)
-  const int64_t items = ((B * (ldx / 8) + 63) & ~63ll) + (wide_parts ? 0 : 32 * B);
+  const int64_t items = ((B * (ldx / 8) + 63) & ~63ll) + 32 * B;
   hipLaunchKernelGGL(wd_assemble_tab_kernel, (int)((items + block - 1) / block), block, 0, s, dense, n_dense, tab,
-                     tab_ld, uniq, base, inv, B, F, D, X, ldx, wide_logit, ones_col, zero_out, rowidx,
-                     wide_parts ? 1 : 0);
+                     tab_ld, uniq, base, inv, B, F, D, X, ldx, wide_logit, ones_col, zero_out, rowidx);
   MINIPS_HIP_CHECK(hipGetLastError());
 }
 
@@ -232,8 +223,7 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
                                                       const float* __restrict__ wide, const float* __restrict__ y,
                                                       bf16_t* __restrict__ dH, float* dw, float* db, float* dwide,
                                                       float* loss_sum, float* colsum, float scale,
-                                                      float* __restrict__ slab, unsigned* ticket, int defer,
-                                                      int wideF) {
+                                                      float* __restrict__ slab, unsigned* ticket, int defer) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -255,9 +245,8 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int64_t b = b0s + s;
-      // the wide logit and label load with the row (not after the wave reduction: one round trip);
-      // wideF > 0: lanes < wideF each hold one feature's wide weight, summed by the reduction below
-      wv[s] = b >= B ? 0.f : wideF == 0 ? wide[b] : lane < wideF ? wide[b * wideF + lane] : 0.f;
+      // the wide logit and label load with the row (not after the wave reduction: one round trip)
+      wv[s] = b < B ? wide[b] : 0.f;
       yv[s] = b < B ? y[b] : 0.f;
 #pragma unroll
       for (int j = 0; j < PER_LANE; ++j) h[s][j] = 0.f;
@@ -265,7 +254,7 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
       float acc = 0.f;
 #pragma unroll
       for (int j = 0; j < PER_LANE; ++j) acc += h[s][j] * wl[j];
-      z[s] = wideF > 0 ? acc + wv[s] : acc;
+      z[s] = acc;
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) z[s] = warp_sum(z[s]);
@@ -273,7 +262,7 @@ __global__ __launch_bounds__(64 * kHeadWaves) void wd_head_kernel(const bf16_t* 
     for (int s = 0; s < S; ++s) {
       const int64_t b = b0s + s;
       if (b >= B) break;
-      const float zz = z[s] + bias + (wideF > 0 ? 0.f : wv[s]);
+      const float zz = z[s] + bias + wv[s];
       const float label = yv[s] > 0.5f ? 1.f : 0.f;
       const float p = sigmoidf_(zz);
       const float dz = (p - label) * scale;
@@ -480,9 +469,8 @@ void head_ws(float** slab, unsigned** ticket) {
 
 void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* b0, const float* wide_logit,
              const float* labels, bf16_t* dH, float* dw, float* db, float* dwide, float* loss_sum, float* dH_colsum,
-             float grad_scale, hipStream_t s, bool defer_fold, int wide_F) {
+             float grad_scale, hipStream_t s, bool defer_fold) {
   if (B <= 0) return;
-  if (wide_F < 0 || wide_F > 64) throw std::runtime_error("wd_head: 0..64 wide parts per sample");
   const int block = 64 * kHeadWaves;
   // per-block LDS reduction, partial rows; the last block folds them (one block per CU at most),
   // or wd_head_fold does (defer_fold)
@@ -492,17 +480,13 @@ void wd_head(const bf16_t* H, int64_t B, int Hd, const bf16_t* w, const bf16_t* 
   head_ws(&slab, &ticket);
   switch (Hd) {
     case 64 * 1: hipLaunchKernelGGL(wd_head_kernel<1>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer,
-                                    wide_F); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer); break;
     case 64 * 2: hipLaunchKernelGGL(wd_head_kernel<2>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer,
-                                    wide_F); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer); break;
     case 64 * 4: hipLaunchKernelGGL(wd_head_kernel<4>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer,
-                                    wide_F); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer); break;
     case 64 * 8: hipLaunchKernelGGL(wd_head_kernel<8>, grid, block, 0, s, H, B, Hd, w, b0, wide_logit, labels,
-                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer,
-                                    wide_F); break;
+                                    dH, dw, db, dwide, loss_sum, dH_colsum, grad_scale, slab, ticket, defer); break;
     default: throw std::runtime_error("wd_head: Hd must be 64, 128, 256 or 512, got " + std::to_string(Hd));
   }
   MINIPS_HIP_CHECK(hipGetLastError());

@@ -131,11 +131,6 @@ _REPLAY = True
 # fold levels leave the dgrad chain (head 17 -> 11 us in-step): 0.335-0.339 vs 0.344-0.345 ms/step
 # (profiles/r6/ab_wd_r6.txt). False: the round-5 in-kernel fold.
 _HEAD_DEFER = True
-# one rank (input assembled from the shard in place): each lookup's wide weight is stored by the
-# thread that reads the embedding's last chunk (same row, same line) and the head sums the F parts
-# inside its logit reduction, instead of a second pass of per-lookup wide-weight loads in the
-# assembly. A/B knob MINIPS_WD_WIDE_PARTS=1 (temporary; off until measured)
-_WIDE_PARTS = __import__("os").environ.get("MINIPS_WD_WIDE_PARTS", "0") == "1"
 # (the dgrads beside the weight-gradient stream keep the launcher's 256x256 tile: forcing 128x128 on
 # the dH1 / dX dgrad, which shares CUs with the wgrads' 128x128 workgroups, measured 0.336-0.339 /
 # 0.344-0.345, both 0.347-0.353, 256x128 0.376-0.379 vs 0.336-0.339 ms; profiles/r6/ab_wd_r6.txt)
@@ -260,7 +255,6 @@ class WideDeep(LookaheadPlans):
                 dH1=torch.empty(B, h1, **bf),
                 dX=torch.empty(B, cfg.F * cfg.emb_dim, **bf),  # bf16: half the bytes of the emb backward
                 wide=torch.empty(B, dtype=torch.float32, device=dev),
-                wide_parts=torch.empty(B * self.cfg.F, dtype=torch.float32, device=dev),
                 dwide=torch.empty(B, dtype=torch.float32, device=dev),
                 loss=torch.zeros(1, dtype=torch.float32, device=dev),
             )
@@ -325,13 +319,10 @@ class WideDeep(LookaheadPlans):
             plan, table, index, base = src
             # (members, memrow, positions, rowstart, rowidx): the planner's per-lookup rows
             rowidx = plan.csr[4] if plan.csr is not None and len(plan.csr) >= 5 and _ROWIDX else None
-            # (the lookups' wide weights land per lookup, read with their rows; the head sums them)
-            wide = b["wide_parts"] if _WIDE_PARTS else b["wide"]
-            ops.wd_assemble_tab(dense, table, index, base, plan.inv, F, D, b["X"], wide, ones_col=self.k_in[0],
+            ops.wd_assemble_tab(dense, table, index, base, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0],
                                 zero=b["loss"], rowidx=rowidx)
         else:
             rows, plan = self.emb.get(keys, plan=plan)
-            wide = b["wide"]
             ops.wd_assemble(dense, rows, plan.inv, F, D, b["X"], b["wide"], ones_col=self.k_in[0], zero=b["loss"])
         if pend_side is not None:  # ... and its dense Adam ran (side stream) before the forward reads W
             streams.current(self.comm.device).wait_event(pend_side[1])
@@ -353,7 +344,7 @@ class WideDeep(LookaheadPlans):
         else:
             self._forward(b, P)
         # the head also sums dH3 over the batch (per-block partials): the layer-3 bias gradient
-        ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], wide, labels, b["dH3"], gw4[:h], gw4[h:h + 1],
+        ops.wd_head(b["H3"], w4[:h], w4[h:h + 1], b["wide"], labels, b["dH3"], gw4[:h], gw4[h:h + 1],
                     b["dwide"], b["loss"], self.view(G, "b3"), scale, defer_fold=defer)
         ph.__exit__(None, None, None)
         ph = phase("wd.bwd_dense")

@@ -553,19 +553,14 @@ def wd_assemble(dense, rows, inv, F, D, X, wide_logit, ones_col=-1, zero=None):
     X[:, F * D: F * D + dense.shape[1]] = dense.to(torch.bfloat16)
     if ones_col >= 0:
         X[:, ones_col] = 1.0
-    if wide_logit.numel() == B * F and F > 1:  # per-lookup wide weights (the head sums them)
-        wide_logit.view(B, F).copy_(r[:, :, D])
-    else:
-        wide_logit.copy_(r[:, :, D].sum(1))
+    wide_logit.copy_(r[:, :, D].sum(1))
     return X, wide_logit
 
 
 def wd_assemble_tab(dense, table, index, base, inv, F, D, X, wide_logit, ones_col=-1, zero=None, rowidx=None):
     """wd_assemble with the rows read in place: the row of unique u is table[index[u] - base]
     (fp32), rounded to bf16 exactly as gather_rows(out bf16) does. ``rowidx`` (plan_sorted, one
-    owner): lookup j's row + base directly (the same rows, one index load per lookup).
-    ``wide_logit`` [B] receives the wide sums, or, sized [B * F], each lookup's wide weight
-    (read with the embedding's last chunk; wd_head sums them)."""
+    owner): lookup j's row + base directly (the same rows, one index load per lookup)."""
     if _gpu(X):
         kernels().wd_assemble_tab(dense, table, index, int(base), inv, int(F), int(D), X, wide_logit, int(ones_col),
                                   zero, rowidx)
@@ -577,8 +572,7 @@ def wd_assemble_tab(dense, table, index, base, inv, F, D, X, wide_logit, ones_co
 
 def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum=None, grad_scale=1.0,
             defer_fold=False):
-    """Last layer + BCE forward/backward. ``wide_logit``: [B], or [B, F] per-lookup wide weights
-    (wd_assemble_tab's parts) summed here. ``defer_fold`` (GPU): the batch sums into dw / db /
+    """Last layer + BCE forward/backward. ``defer_fold`` (GPU): the batch sums into dw / db /
     loss_sum / dH_colsum are left as per-block partials for wd_head_fold (a later kernel, e.g. on
     the weight-gradient stream, off the dgrad chain); on the CPU they are added here and the fold
     is a no-op."""
@@ -586,8 +580,6 @@ def wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum
         kernels().wd_head(H, w, b0, wide_logit, labels, dH, dw, db, dwide, loss_sum, dH_colsum, float(grad_scale),
                           bool(defer_fold))
         return
-    if wide_logit.numel() != H.shape[0]:  # [B, F] per-lookup wide weights
-        wide_logit = wide_logit.view(H.shape[0], -1).sum(1)
     h = H.float()
     z = h @ w.float() + b0.float() + wide_logit
     y = (labels > 0.5).float()

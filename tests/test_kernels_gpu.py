@@ -231,15 +231,6 @@ def test_wd_assemble_tab_and_head_full_batch(dev):
     assert torch.equal(X1, X2)
     torch.testing.assert_close(w2, w1, rtol=1e-6, atol=1e-6)
     assert float(z2) == 0.0
-    # per-lookup wide weights (the head sums them): same X, parts summing to the wide logits
-    X4, p4 = torch.empty_like(X1), torch.empty(B * F, device=dev)
-    ops.wd_assemble_tab(d(dense), d(shard), d(uniq), base, d(inv), F, D, X4, p4, ones_col=F * D + nd)
-    assert torch.equal(X4, X1)
-    torch.testing.assert_close(p4.view(B, F).sum(1), w1, rtol=1e-5, atol=1e-5)
-    p4_ref = torch.empty(B * F)
-    ops.wd_assemble_tab(dense, shard, uniq, base, inv, F, D, torch.empty(B, ldx, dtype=torch.bfloat16), p4_ref,
-                        ones_col=F * D + nd)
-    assert torch.equal(p4.cpu(), p4_ref)
     # CPU reference of the in-place form
     X3, w3 = torch.empty(B, ldx, dtype=torch.bfloat16), torch.empty(B)
     ops.wd_assemble_tab(dense, shard, uniq, base, inv, F, D, X3, w3, ones_col=F * D + nd)
@@ -273,22 +264,6 @@ def test_wd_assemble_tab_and_head_full_batch(dev):
     od = run(dev, defer=True)
     for k in o:
         assert torch.equal(od[k], o[k]), k
-    # the wide logit as F per-lookup parts, summed inside the head's logit reduction
-    Fp = 26
-    parts = torch.randn(Bh, Fp, generator=g) * 0.05
-    wide_sum = parts.sum(1)
-
-    def run_parts(dv, wd):
-        o2 = dict(dH=torch.empty(Bh, Hd, dtype=torch.bfloat16, device=dv), dw=torch.zeros(Hd, device=dv),
-                  db=torch.zeros(1, device=dv), dwide=torch.empty(Bh, device=dv),
-                  loss=torch.zeros(1, device=dv), cs=torch.zeros(Hd, device=dv))
-        ops.wd_head(H.to(dv), w.to(dv), b0.to(dv), wd.to(dv), y.to(dv), o2["dH"], o2["dw"], o2["db"], o2["dwide"],
-                    o2["loss"], o2["cs"], 1.0 / Bh)
-        return {k: v.cpu() for k, v in o2.items()}
-
-    rp, op_ = run_parts("cpu", wide_sum), run_parts(dev, parts.reshape(-1))
-    for k in rp:
-        torch.testing.assert_close(op_[k].float(), rp[k].float(), rtol=2e-2, atol=1e-4)
 
 
 def test_lr_and_kmeans(dev):
