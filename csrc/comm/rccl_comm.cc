@@ -123,12 +123,23 @@ double now_s() {
 // aborted communicator (see the abort protocol in the header).
 struct RcclComm::Call {
   RcclComm* c;
-  Call(RcclComm* comm, hipStream_t s) : c(comm) {
+  hipStream_t s;
+  std::unique_lock<std::mutex> order;
+  bool captured = false;  // (a stream under graph capture: no event chain into or out of the graph)
+  Call(RcclComm* comm, hipStream_t stream) : c(comm), s(stream), order(comm->order_mu_) {
     c->in_call_.fetch_add(1);
     if (c->abort_req_.load()) {
       c->in_call_.fetch_sub(1);
       std::lock_guard<std::mutex> lk(c->mu_);
       throw std::runtime_error("rccl: communicator aborted (" + c->error_ + ")");
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    captured = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+    // after the previous collective, whichever stream it went to (issue order = GPU order)
+    const bool chain = !captured && c->order_stream_ && c->order_stream_ != s;
+    if (chain && hipStreamWaitEvent(s, c->order_ev_, 0) != hipSuccess) {
+      c->in_call_.fetch_sub(1);
+      throw std::runtime_error("rccl: stream wait on the previous collective failed");
     }
     std::lock_guard<std::mutex> lk(c->mu_);
     for (const Probe& p : c->streams_)
@@ -138,7 +149,11 @@ struct RcclComm::Call {
     if (hipEventCreateWithFlags(&p.ev, hipEventDisableTiming) != hipSuccess) p.ev = nullptr;
     c->streams_.push_back(p);
   }
-  ~Call() { c->in_call_.fetch_sub(1); }
+  ~Call() {
+    if (captured) c->order_stream_ = nullptr;
+    else if (c->order_ev_ && hipEventRecord(c->order_ev_, s) == hipSuccess) c->order_stream_ = s;
+    c->in_call_.fetch_sub(1);
+  }
 };
 
 RcclComm::RcclComm(const std::string& lib_path, const std::string& unique_id, int world, int rank, int device,
@@ -151,6 +166,8 @@ RcclComm::RcclComm(const std::string& lib_path, const std::string& unique_id, in
   std::memcpy(id.internal, unique_id.data(), sizeof(id.internal));
   if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("rccl: hipSetDevice");
   Check(lib_->ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  if (hipEventCreateWithFlags(&order_ev_, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+    throw std::runtime_error("rccl: hipEventCreateWithFlags");
   if (timeout_s_ > 0) wd_ = std::thread([this] { Watch(); });
 }
 
@@ -164,6 +181,7 @@ RcclComm::~RcclComm() {
   if (!aborted_.load() && comm_) (void)lib_->ncclCommDestroy(comm_);
   for (Probe& p : streams_)
     if (p.ev) (void)hipEventDestroy(p.ev);
+  if (order_ev_) (void)hipEventDestroy(order_ev_);
 }
 
 void RcclComm::Watch() {

@@ -101,6 +101,14 @@ class RcclComm {
     double t_rec = 0;
   };
   std::vector<Probe> streams_;
+  // issue order across streams: RCCL itself lets a collective enqueued on another stream run ahead
+  // of an earlier one (measured: tests/test_rccl_gpu.py), so each collective's stream first waits
+  // for the previous collective's completion event -- one GPU order, the issue order, as
+  // ProcessGroupNCCL's single internal stream gives (the data plane's deadlock-freedom argument,
+  // minips_amd/ps/comm.py). order_mu_ is held across a whole call (one issuing thread at a time).
+  std::mutex order_mu_;
+  hipEvent_t order_ev_ = nullptr;
+  hipStream_t order_stream_ = nullptr;
   std::thread wd_;
   std::condition_variable wcv_;
   bool wstop_ = false;

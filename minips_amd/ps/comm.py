@@ -21,9 +21,14 @@ comm/mailbox.cpp:231-308), so a worker's messages leave in program order. The GP
 keeps the same contract with ONE communicator per rank:
 
 1. Every collective of a rank goes through this Comm's single process group, whichever HIP
-   stream issues it (compute, planning, a table's clock stream). RCCL runs a communicator's
-   ops on one internal stream in issue order, so the n-th collective of every rank is the
-   same op (same kind, dtype and row width; all-to-all-v splits agree pairwise).
+   stream issues it (compute, planning, a table's clock stream), and runs on the GPU in issue
+   order: ProcessGroupNCCL enqueues on its one internal stream; the native plane makes each
+   collective's stream wait for the previous collective's completion event (RcclComm::Call) --
+   RCCL alone lets a collective enqueued on another stream overtake an earlier one
+   (tests/test_rccl_gpu.py::test_native_rccl_keeps_issue_order_across_streams failed without the
+   chain: the later one finished at 0.28 ms, the earlier one behind a 2 ms kernel). So the n-th
+   collective of every rank is the same op (same kind, dtype and row width; all-to-all-v splits
+   agree pairwise), executed after collectives < n.
 2. Every rank issues the same program: the tables' issue points (plan, get, clock, advance)
    are identical on all ranks and never depend on timing or on a non-blocking query.
 3. A host wait (an event of the count exchange) and a stream wait (wait_event) only target

@@ -221,3 +221,32 @@ def test_native_rccl_watchdog_aborts_a_stuck_collective(nccl_comm):
             _rccl_call(rc.all_gather, y, x)
     assert _is_comm_failure(ei.value)
     torch.cuda.synchronize(dev)  # the spins drain; nothing is left running
+
+
+def test_native_rccl_keeps_issue_order_across_streams(nccl_comm):
+    """The data plane's deadlock-freedom argument (ps/comm.py, ordering contract 1) needs one
+    communicator's collectives to run in issue order even when they are enqueued on different
+    HIP streams: collective B on stream 2 must not finish before collective A, issued first on
+    stream 1 behind a ~2 ms kernel. RCCL alone lets B overtake A (this test failed, B done at
+    0.28 ms); RcclComm chains each collective after the previous one's completion event."""
+    from minips_amd._native import kernels
+
+    comm = nccl_comm
+    dev = comm.device
+    rc = comm._rc()
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    a, b = torch.ones(1 << 18, device=dev), torch.ones(1 << 18, device=dev)
+    torch.cuda.synchronize()
+    t0 = torch.cuda.Event(enable_timing=True)
+    e_spin, e_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record(s1)
+    s2.wait_event(t0)
+    kernels().wire_spin(200000, 1, s1.cuda_stream)  # ~2 ms
+    e_spin.record(s1)
+    with torch.cuda.stream(s1):
+        rc.all_reduce(a, 0)
+    with torch.cuda.stream(s2):
+        rc.all_reduce(b, 0)
+    e_b.record(s2)
+    torch.cuda.synchronize()
+    assert t0.elapsed_time(e_b) >= t0.elapsed_time(e_spin), "RCCL ran a later collective ahead of an earlier one"
