@@ -104,7 +104,10 @@ _K1_ALIGN = 64
 # split-K workgroup target of the three weight gradients (ops.linear_wgrad blocks): W&D 0.402 ms at
 # 320 vs 0.409-0.412 at the default 512 (GPT-2 keeps 512: 12.90 vs 13.18 ms at 256), ab_wd_r3.txt;
 # round 5 (planning mid-step): 0.349-0.351 vs 0.357-0.359 at 192, 0.360-0.361 at 512 (ab_wd_r5.txt)
-_WGRAD_BLOCKS = 320
+# round 6 (head fold off the chain, side-stream Adam after the embedding dgrad): 256 -- W1 / W2 / W3 in
+# 5 / 8 / 16 slices instead of 6 / 10 / 16, fewer planes for the Adam to fold -- 0.3384-0.3407 vs
+# 0.3395-0.3454 at 320, 0.346-0.351 at 192 / 224, 0.351-0.353 at 384 / 448 (ab_wd_r6.txt)
+_WGRAD_BLOCKS = 256
 
 
 # DENSE_ON_SIDE off: one rank's dense Adam on the main stream at the step end (joined)
