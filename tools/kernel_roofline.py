@@ -28,8 +28,8 @@ def gemm(M, N, K, out_bytes, split=1):
     return flops, byts
 
 
-def _split(n_out, k_in, blocks=320, min_rows=1024):
-    """ops.linear_wgrad's split-K choice for W&D's overlapped weight gradients (blocks=320)."""
+def _split(n_out, k_in, blocks=256, min_rows=1024):
+    """ops.linear_wgrad's split-K choice for W&D's overlapped weight gradients (blocks=256)."""
     tiles = ((n_out + 127) // 128) * ((k_in + 127) // 128)
     return max(1, min(B // min_rows, (blocks + tiles - 1) // tiles))
 
